@@ -1,0 +1,495 @@
+// Varlen causal GQA flash-attention forward/backward for gfx950.
+//
+// Layout: the packed QKV GEMM output qkv[M, (nq + 2*nkv) * 128] (bf16, token-major, no
+// transposes anywhere); sequences are [cu[b], cu[b+1]). Output o[M, nq*128], lse[nq, M] (fp32,
+// natural log). Backward returns dqkv in the same packed layout, ready for the fused QKV
+// linear's backward.
+//
+// CDNA4 mapping:
+// * MFMA v_mfma_f32_16x16x32_bf16 throughout (wave64; lane maps below), fp32 accumulate;
+// * "swapped" products (S^T = K Q^T, dP^T = V dO^T, ...) put the reduction index of the next
+//   product in the accumulator registers, so P / dS feed the next MFMA straight from
+//   registers (cvt to bf16, no LDS round trip, no cross-lane shuffles);
+// * K/V/Q/dO tiles are staged in LDS as [rows][128] bf16 images with an XOR swizzle that is
+//   conflict-free for both 16-byte row reads (MFMA operands along head_dim) and the gfx950
+//   transposed read ds_read_b64_tr_b16 (MFMA operands along the key/query axis);
+// * online softmax in the exp2 domain with fp32 running max/sum per query row; the four lanes
+//   that share a query column combine with two xor-shuffles.
+//
+// mfma_f32_16x16x32_bf16 lane maps (g = lane >> 4, r = lane & 15, j = 0..7, i = 0..3):
+//   A[row r][k 8g+j], B[k 8g+j][col r], C[row 4g+i][col r].
+// Accumulator-as-operand: two 16-row C tiles (t0, t1) give lane (g, r) the k values
+//   {4g+i} from t0 and {16+4g+i} from t1; we use that order as the k permutation
+//   p(8g+j) = j<4 ? 4g+j : 16+4g+(j-4) on BOTH operands of the next MFMA.
+#include "common.h"
+
+namespace sftamd {
+
+namespace attn {
+
+constexpr int D = 128;       // head_dim (SmolLM3-3B, Llama-3-8B)
+constexpr int ROWB = D * 2;  // bytes per LDS image row
+constexpr float LOG2E = 1.4426950408889634f;
+constexpr float LN2 = 0.6931471805599453f;
+
+__device__ __forceinline__ int swz(int row, int ch) { return ch ^ (((row & 3) << 2) | ((row >> 2) & 3)); }
+__device__ __forceinline__ int img_off(int row, int ch) { return row * ROWB + 16 * swz(row, ch); }
+
+__device__ __forceinline__ f32x4 mfma(const bf16x8& a, const bf16x8& b, const f32x4& c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
+
+// Stage rows [0, R) of a row-major global matrix (row stride ld elements) into an LDS image.
+// Rows >= nvalid are zero-filled (never read from HBM).
+template <int R, int NT>
+__device__ __forceinline__ void stage(char* lds, const u16* __restrict__ g, long ld, int nvalid, int tid) {
+#pragma unroll
+  for (int it = 0; it < (R * 16) / NT; ++it) {
+    const int idx = tid + it * NT;
+    const int r = idx >> 4, ch = idx & 15;
+    uint4 v = make_uint4(0, 0, 0, 0);
+    if (r < nvalid) v = *(const uint4*)(g + (long)r * ld + ch * 8);
+    *(uint4*)(lds + img_off(r, ch)) = v;
+  }
+}
+
+// Operand along head_dim: rows rbase + (lane & 15), k-step s covers d = 32s .. 32s+31.
+__device__ __forceinline__ bf16x8 frag_row(const char* lds, int rbase, int s, int lane) {
+  return *(const bf16x8*)(lds + img_off(rbase + (lane & 15), 4 * s + (lane >> 4)));
+}
+
+// Operand along the row axis (transposed): lane gets column 16*cb + (lane & 15) of rows
+// rb + p(8g + j) (the accumulator permutation above). Two ds_read_b64_tr_b16.
+template <bool TR>
+__device__ __forceinline__ bf16x8 frag_tr(const char* lds, int rb, int cb, int lane) {
+  const int g = lane >> 4, i = lane & 15;
+  if constexpr (TR) {
+    const int q = i >> 2, p = i & 3;
+    const int ch = 2 * cb + (p >> 1);
+    const int r0 = rb + 4 * g + q;
+    const int o0 = img_off(r0, ch) + 8 * (p & 1);
+    const int o1 = img_off(r0 + 16, ch) + 8 * (p & 1);
+    typedef __attribute__((address_space(3))) s16x4 lds_s4;
+    s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4*)(lds + o0));
+    s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4*)(lds + o1));
+    typedef __attribute__((ext_vector_type(8))) short s16x8;
+    s16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+    return __builtin_bit_cast(bf16x8, v);
+  } else {
+    const int col = 16 * cb + i;
+    const int ch = col >> 3, e = col & 7;
+    typedef __attribute__((ext_vector_type(8))) short s16x8;
+    s16x8 v;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int row = rb + (j < 4 ? 4 * g + j : 16 + 4 * g + (j - 4));
+      v[j] = *(const short*)(lds + img_off(row, ch) + 2 * e);
+    }
+    return __builtin_bit_cast(bf16x8, v);
+  }
+}
+
+__device__ __forceinline__ bf16x8 pack_acc(const f32x4& t0, const f32x4& t1) {
+  bf16x8 r;
+  r[0] = (__bf16)t0[0];
+  r[1] = (__bf16)t0[1];
+  r[2] = (__bf16)t0[2];
+  r[3] = (__bf16)t0[3];
+  r[4] = (__bf16)t1[0];
+  r[5] = (__bf16)t1[1];
+  r[6] = (__bf16)t1[2];
+  r[7] = (__bf16)t1[3];
+  return r;
+}
+
+__device__ __forceinline__ bf16x8 load_frag_global(const u16* p, bool ok) {
+  if (!ok) return bf16x8{};
+  return __builtin_bit_cast(bf16x8, *(const uint4*)p);
+}
+
+__device__ __forceinline__ void store4(u16* p, const f32x4& v, float s) {
+  uint2 w;
+  w.x = (unsigned)f2bf(v[0] * s) | ((unsigned)f2bf(v[1] * s) << 16);
+  w.y = (unsigned)f2bf(v[2] * s) | ((unsigned)f2bf(v[3] * s) << 16);
+  *(uint2*)p = w;
+}
+
+// ------------------------------------------------------------------------------ forward
+// grid (q-blocks of 64, nq, nseq); 4 waves x 16 query rows. Per 64-key tile: S^T (16 MFMA),
+// online softmax in registers, O^T += V^T P^T (16 MFMA).
+template <bool TR>
+__global__ __launch_bounds__(256) void fwd_kernel(const u16* __restrict__ qkv, u16* __restrict__ out,
+                                                  float* __restrict__ lse, const int* __restrict__ cu, int nq, int nkv,
+                                                  int total, float sl2, int causal) {
+  __shared__ __attribute__((aligned(16))) char smem[2 * 64 * ROWB];
+  char* Ks = smem;
+  char* Vs = smem + 64 * ROWB;
+  const int qb = blockIdx.x, h = blockIdx.y, b = blockIdx.z;
+  const int start = cu[b], len = cu[b + 1] - start;
+  const int q0 = qb * 64;
+  if (q0 >= len) return;
+  const int kvh = h / (nq / nkv);
+  const long ld = (long)(nq + 2 * nkv) * D;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, g = lane >> 4;
+  const int qrow = q0 + wave * 16 + (lane & 15);
+  const bool qok = qrow < len;
+  const u16* qp = qkv + (long)(start + qrow) * ld + h * D + 8 * g;
+  bf16x8 qf[4];
+#pragma unroll
+  for (int s = 0; s < 4; ++s) qf[s] = load_frag_global(qp + 32 * s, qok);
+
+  f32x4 o[8];
+#pragma unroll
+  for (int dt = 0; dt < 8; ++dt) o[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
+  float m = -1e30f, l = 0.f;
+  const int nkb = (len + 63) / 64;
+  const int nkt = causal ? min(qb + 1, nkb) : nkb;
+  for (int kt = 0; kt < nkt; ++kt) {
+    const int k0 = kt * 64;
+    const int kvalid = min(64, len - k0);
+    __syncthreads();
+    stage<64, 256>(Ks, qkv + (long)(start + k0) * ld + (nq + kvh) * D, ld, kvalid, tid);
+    stage<64, 256>(Vs, qkv + (long)(start + k0) * ld + (nq + nkv + kvh) * D, ld, kvalid, tid);
+    __syncthreads();
+    f32x4 sc[4];
+#pragma unroll
+    for (int nt = 0; nt < 4; ++nt) {
+      sc[nt] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int s = 0; s < 4; ++s) sc[nt] = mfma(frag_row(Ks, 16 * nt, s, lane), qf[s], sc[nt]);
+    }
+    float tmax = -INFINITY;
+#pragma unroll
+    for (int nt = 0; nt < 4; ++nt)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int key = k0 + 16 * nt + 4 * g + i;
+        float v = sc[nt][i] * sl2;
+        if (key >= len || (causal && key > qrow)) v = -INFINITY;
+        sc[nt][i] = v;
+        tmax = fmaxf(tmax, v);
+      }
+    tmax = fmaxf(tmax, __shfl_xor(tmax, 16, 64));
+    tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64));
+    const float mnew = fmaxf(m, tmax);
+    const float alpha = exp2f(m - mnew);
+    float rs = 0.f;
+#pragma unroll
+    for (int nt = 0; nt < 4; ++nt)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const float p = exp2f(sc[nt][i] - mnew);
+        sc[nt][i] = p;
+        rs += p;
+      }
+    rs += __shfl_xor(rs, 16, 64);
+    rs += __shfl_xor(rs, 32, 64);
+    l = l * alpha + rs;
+    m = mnew;
+#pragma unroll
+    for (int dt = 0; dt < 8; ++dt) o[dt] *= alpha;
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      const bf16x8 pb = pack_acc(sc[2 * ks], sc[2 * ks + 1]);
+#pragma unroll
+      for (int dt = 0; dt < 8; ++dt) o[dt] = mfma(frag_tr<TR>(Vs, 32 * ks, dt, lane), pb, o[dt]);
+    }
+  }
+  if (qok) {
+    const float inv = 1.f / l;
+    u16* op = out + (long)(start + qrow) * nq * D + h * D + 4 * g;
+#pragma unroll
+    for (int dt = 0; dt < 8; ++dt) store4(op + 16 * dt, o[dt], inv);
+    if (g == 0) lse[(long)h * total + start + qrow] = (m + log2f(l)) * LN2;
+  }
+}
+
+// ------------------------------------------------------------------------------ backward
+// delta[h][m] = sum_d dO[m, h*D + d] * O[m, h*D + d]   (16 lanes per row)
+__global__ __launch_bounds__(256) void delta_kernel(const u16* __restrict__ dout, const u16* __restrict__ out,
+                                                    float* __restrict__ delta, int total, int nq) {
+  const long rowid = blockIdx.x * 16L + (threadIdx.x >> 4);  // (m, h) flattened as m*nq + h
+  const int sub = threadIdx.x & 15;
+  float s = 0.f;
+  const bool ok = rowid < (long)total * nq;
+  if (ok) {
+    const long base = rowid * D + sub * 8;
+    float a[8], c[8];
+    unpack8(*(const uint4*)(dout + base), a);
+    unpack8(*(const uint4*)(out + base), c);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) s += a[i] * c[i];
+  }
+#pragma unroll
+  for (int o = 8; o > 0; o >>= 1) s += __shfl_xor(s, o, 16);
+  if (ok && sub == 0) {
+    const long m = rowid / nq;
+    const int h = (int)(rowid - m * nq);
+    delta[(long)h * total + m] = s;
+  }
+}
+
+// dK/dV: grid (key blocks of 64, nkv, nseq); wave owns 16 keys (K, V fragments in registers,
+// dK^T/dV^T accumulators in registers); loops over the GQA group's query heads and 64-row
+// query tiles: S, dP (32 MFMA) -> P, dS -> dV^T += dO^T P, dK^T += Q^T dS (32 MFMA).
+template <bool TR>
+__global__ __launch_bounds__(256) void bwd_dkdv_kernel(const u16* __restrict__ qkv, const u16* __restrict__ dout,
+                                                       const float* __restrict__ lse, const float* __restrict__ delta,
+                                                       const int* __restrict__ cu, u16* __restrict__ dqkv, int nq,
+                                                       int nkv, int total, float sl2, float scale, int causal) {
+  __shared__ __attribute__((aligned(16))) char smem[2 * 64 * ROWB + 2 * 64 * 4];
+  char* Qs = smem;
+  char* Os = smem + 64 * ROWB;
+  float* Ls = (float*)(smem + 2 * 64 * ROWB);
+  float* Dl = Ls + 64;
+  const int kb = blockIdx.x, kvh = blockIdx.y, b = blockIdx.z;
+  const int start = cu[b], len = cu[b + 1] - start;
+  const int k0 = kb * 64;
+  if (k0 >= len) return;
+  const int rep = nq / nkv;
+  const long ld = (long)(nq + 2 * nkv) * D;
+  const long ldo = (long)nq * D;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, g = lane >> 4;
+  const int key = k0 + wave * 16 + (lane & 15);
+  const bool kok = key < len;
+  bf16x8 kf[4], vf[4];
+  {
+    const u16* kp = qkv + (long)(start + key) * ld + (nq + kvh) * D + 8 * g;
+    const u16* vp = qkv + (long)(start + key) * ld + (nq + nkv + kvh) * D + 8 * g;
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      kf[s] = load_frag_global(kp + 32 * s, kok);
+      vf[s] = load_frag_global(vp + 32 * s, kok);
+    }
+  }
+  f32x4 dk[8], dv[8];
+#pragma unroll
+  for (int dt = 0; dt < 8; ++dt) {
+    dk[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
+    dv[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
+  }
+  const int qt0 = causal ? kb : 0;
+  const int nqt = (len + 63) / 64;
+  for (int r = 0; r < rep; ++r) {
+    const int h = kvh * rep + r;
+    for (int qt = qt0; qt < nqt; ++qt) {
+      const int q0 = qt * 64;
+      const int qvalid = min(64, len - q0);
+      __syncthreads();
+      stage<64, 256>(Qs, qkv + (long)(start + q0) * ld + h * D, ld, qvalid, tid);
+      stage<64, 256>(Os, dout + (long)(start + q0) * ldo + h * D, ldo, qvalid, tid);
+      if (tid < 64) {
+        const bool ok = tid < qvalid;
+        Ls[tid] = ok ? lse[(long)h * total + start + q0 + tid] * LOG2E : 0.f;
+        Dl[tid] = ok ? delta[(long)h * total + start + q0 + tid] : 0.f;
+      }
+      __syncthreads();
+      f32x4 sc[4], dp[4];
+#pragma unroll
+      for (int mt = 0; mt < 4; ++mt) {
+        sc[mt] = f32x4{0.f, 0.f, 0.f, 0.f};
+        dp[mt] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+          sc[mt] = mfma(frag_row(Qs, 16 * mt, s, lane), kf[s], sc[mt]);
+          dp[mt] = mfma(frag_row(Os, 16 * mt, s, lane), vf[s], dp[mt]);
+        }
+      }
+      // lane: key column, query rows q0 + 16mt + 4g + i
+#pragma unroll
+      for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int qi = 16 * mt + 4 * g + i;
+          const int q = q0 + qi;
+          float p = exp2f(sc[mt][i] * sl2 - Ls[qi]);
+          if (q >= len || (causal && key > q)) p = 0.f;
+          sc[mt][i] = p;
+          dp[mt][i] = p * (dp[mt][i] - Dl[qi]);
+        }
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        const bf16x8 pb = pack_acc(sc[2 * ks], sc[2 * ks + 1]);
+        const bf16x8 db = pack_acc(dp[2 * ks], dp[2 * ks + 1]);
+#pragma unroll
+        for (int dt = 0; dt < 8; ++dt) {
+          dv[dt] = mfma(frag_tr<TR>(Os, 32 * ks, dt, lane), pb, dv[dt]);
+          dk[dt] = mfma(frag_tr<TR>(Qs, 32 * ks, dt, lane), db, dk[dt]);
+        }
+      }
+    }
+  }
+  if (kok) {
+    u16* kp = dqkv + (long)(start + key) * ld + (nq + kvh) * D + 4 * g;
+    u16* vp = dqkv + (long)(start + key) * ld + (nq + nkv + kvh) * D + 4 * g;
+#pragma unroll
+    for (int dt = 0; dt < 8; ++dt) {
+      store4(kp + 16 * dt, dk[dt], scale);
+      store4(vp + 16 * dt, dv[dt], 1.f);
+    }
+  }
+}
+
+// dQ: grid (q blocks of 64, nq, nseq); wave owns 16 query rows (Q, dO fragments in registers);
+// per 64-key tile: S^T, dP^T (32 MFMA) -> dS^T -> dQ^T += K^T dS^T (16 MFMA).
+template <bool TR>
+__global__ __launch_bounds__(256) void bwd_dq_kernel(const u16* __restrict__ qkv, const u16* __restrict__ dout,
+                                                     const float* __restrict__ lse, const float* __restrict__ delta,
+                                                     const int* __restrict__ cu, u16* __restrict__ dqkv, int nq,
+                                                     int nkv, int total, float sl2, float scale, int causal) {
+  __shared__ __attribute__((aligned(16))) char smem[2 * 64 * ROWB];
+  char* Ks = smem;
+  char* Vs = smem + 64 * ROWB;
+  const int qb = blockIdx.x, h = blockIdx.y, b = blockIdx.z;
+  const int start = cu[b], len = cu[b + 1] - start;
+  const int q0 = qb * 64;
+  if (q0 >= len) return;
+  const int kvh = h / (nq / nkv);
+  const long ld = (long)(nq + 2 * nkv) * D;
+  const long ldo = (long)nq * D;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, g = lane >> 4;
+  const int qrow = q0 + wave * 16 + (lane & 15);
+  const bool qok = qrow < len;
+  bf16x8 qf[4], df[4];
+  {
+    const u16* qp = qkv + (long)(start + qrow) * ld + h * D + 8 * g;
+    const u16* dp = dout + (long)(start + qrow) * ldo + h * D + 8 * g;
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      qf[s] = load_frag_global(qp + 32 * s, qok);
+      df[s] = load_frag_global(dp + 32 * s, qok);
+    }
+  }
+  const float lse2 = qok ? lse[(long)h * total + start + qrow] * LOG2E : 0.f;
+  const float dl = qok ? delta[(long)h * total + start + qrow] : 0.f;
+  f32x4 dq[8];
+#pragma unroll
+  for (int dt = 0; dt < 8; ++dt) dq[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const int nkb = (len + 63) / 64;
+  const int nkt = causal ? min(qb + 1, nkb) : nkb;
+  for (int kt = 0; kt < nkt; ++kt) {
+    const int k0 = kt * 64;
+    const int kvalid = min(64, len - k0);
+    __syncthreads();
+    stage<64, 256>(Ks, qkv + (long)(start + k0) * ld + (nq + kvh) * D, ld, kvalid, tid);
+    stage<64, 256>(Vs, qkv + (long)(start + k0) * ld + (nq + nkv + kvh) * D, ld, kvalid, tid);
+    __syncthreads();
+    f32x4 sc[4], dp[4];
+#pragma unroll
+    for (int nt = 0; nt < 4; ++nt) {
+      sc[nt] = f32x4{0.f, 0.f, 0.f, 0.f};
+      dp[nt] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {
+        sc[nt] = mfma(frag_row(Ks, 16 * nt, s, lane), qf[s], sc[nt]);
+        dp[nt] = mfma(frag_row(Vs, 16 * nt, s, lane), df[s], dp[nt]);
+      }
+    }
+#pragma unroll
+    for (int nt = 0; nt < 4; ++nt)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int key = k0 + 16 * nt + 4 * g + i;
+        float p = exp2f(sc[nt][i] * sl2 - lse2);
+        if (key >= len || (causal && key > qrow) || !qok) p = 0.f;
+        dp[nt][i] = p * (dp[nt][i] - dl);
+      }
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      const bf16x8 db = pack_acc(dp[2 * ks], dp[2 * ks + 1]);
+#pragma unroll
+      for (int dt = 0; dt < 8; ++dt) dq[dt] = mfma(frag_tr<TR>(Ks, 32 * ks, dt, lane), db, dq[dt]);
+    }
+  }
+  if (qok) {
+    u16* qp = dqkv + (long)(start + qrow) * ld + h * D + 4 * g;
+#pragma unroll
+    for (int dt = 0; dt < 8; ++dt) store4(qp + 16 * dt, dq[dt], scale);
+  }
+}
+
+}  // namespace attn
+
+static void check_attn_args(const at::Tensor& qkv, const at::Tensor& cu, int64_t nq, int64_t nkv, int64_t hd) {
+  SFT_CHECK_CUDA(qkv);
+  SFT_CHECK_BF16(qkv);
+  SFT_CHECK_CONTIG(qkv);
+  SFT_CHECK(hd == attn::D, "flash attention kernel is built for head_dim 128, got ", hd);
+  SFT_CHECK(nq % nkv == 0, "nq must be a multiple of nkv");
+  SFT_CHECK(qkv.dim() == 2 && qkv.size(1) == (nq + 2 * nkv) * hd, "qkv must be [M, (nq+2nkv)*hd]");
+  SFT_CHECK(cu.scalar_type() == at::kInt && cu.is_cuda() && cu.dim() == 1 && cu.numel() >= 2, "cu_seqlens int32");
+}
+
+// variant: 1 = ds_read_b64_tr_b16 transposed operand reads (default), 0 = scalar LDS gathers
+static int attn_variant() {
+  const char* e = std::getenv("SFTAMD_ATTN_TR");
+  return (e && e[0] == '0') ? 0 : 1;
+}
+
+std::tuple<at::Tensor, at::Tensor> flash_fwd(const at::Tensor& qkv, const at::Tensor& cu, int64_t max_seqlen,
+                                             int64_t nq, int64_t nkv, int64_t hd, double scale, bool causal) {
+  check_attn_args(qkv, cu, nq, nkv, hd);
+  const int total = qkv.size(0);
+  const int nseq = cu.numel() - 1;
+  auto out = at::empty({total, nq * hd}, qkv.options());
+  auto lse = at::empty({nq, total}, qkv.options().dtype(at::kFloat));
+  if (total == 0 || max_seqlen == 0) return {out, lse};
+  dim3 grid((max_seqlen + 63) / 64, nq, nseq);
+  const float sl2 = (float)scale * attn::LOG2E;
+  auto cu_c = cu.contiguous();
+  if (attn_variant())
+    attn::fwd_kernel<true><<<grid, 256, 0, cur_stream()>>>((const u16*)qkv.data_ptr(), (u16*)out.data_ptr(),
+                                                           lse.data_ptr<float>(), cu_c.data_ptr<int>(), nq, nkv, total,
+                                                           sl2, causal ? 1 : 0);
+  else
+    attn::fwd_kernel<false><<<grid, 256, 0, cur_stream()>>>((const u16*)qkv.data_ptr(), (u16*)out.data_ptr(),
+                                                            lse.data_ptr<float>(), cu_c.data_ptr<int>(), nq, nkv, total,
+                                                            sl2, causal ? 1 : 0);
+  SFT_LAUNCH_CHECK();
+  return {out, lse};
+}
+
+at::Tensor flash_bwd(const at::Tensor& dout, const at::Tensor& qkv, const at::Tensor& out, const at::Tensor& lse,
+                     const at::Tensor& cu, int64_t max_seqlen, int64_t nq, int64_t nkv, int64_t hd, double scale,
+                     bool causal) {
+  check_attn_args(qkv, cu, nq, nkv, hd);
+  SFT_CHECK_CONTIG(dout);
+  SFT_CHECK_CONTIG(out);
+  SFT_CHECK(dout.sizes() == out.sizes() && out.size(1) == nq * hd, "dout/out shape");
+  const int total = qkv.size(0);
+  const int nseq = cu.numel() - 1;
+  auto dqkv = at::empty_like(qkv);
+  if (total == 0 || max_seqlen == 0) return dqkv;
+  auto delta = at::empty({nq, total}, qkv.options().dtype(at::kFloat));
+  const long rows = (long)total * nq;
+  attn::delta_kernel<<<(rows + 15) / 16, 256, 0, cur_stream()>>>((const u16*)dout.data_ptr(), (const u16*)out.data_ptr(),
+                                                                  delta.data_ptr<float>(), total, nq);
+  SFT_LAUNCH_CHECK();
+  const float sl2 = (float)scale * attn::LOG2E;
+  auto cu_c = cu.contiguous();
+  dim3 gk((max_seqlen + 63) / 64, nkv, nseq);
+  dim3 gq((max_seqlen + 63) / 64, nq, nseq);
+  auto run = [&](auto tr) {
+    constexpr bool TR = decltype(tr)::value;
+    attn::bwd_dkdv_kernel<TR><<<gk, 256, 0, cur_stream()>>>(
+        (const u16*)qkv.data_ptr(), (const u16*)dout.data_ptr(), lse.data_ptr<float>(), delta.data_ptr<float>(),
+        cu_c.data_ptr<int>(), (u16*)dqkv.data_ptr(), nq, nkv, total, sl2, (float)scale, causal ? 1 : 0);
+    SFT_LAUNCH_CHECK();
+    attn::bwd_dq_kernel<TR><<<gq, 256, 0, cur_stream()>>>(
+        (const u16*)qkv.data_ptr(), (const u16*)dout.data_ptr(), lse.data_ptr<float>(), delta.data_ptr<float>(),
+        cu_c.data_ptr<int>(), (u16*)dqkv.data_ptr(), nq, nkv, total, sl2, (float)scale, causal ? 1 : 0);
+    SFT_LAUNCH_CHECK();
+  };
+  if (attn_variant())
+    run(std::true_type());
+  else
+    run(std::false_type());
+  return dqkv;
+}
+
+TORCH_LIBRARY_IMPL(sftamd, CUDA, m) {
+  m.impl("flash_fwd", &flash_fwd);
+  m.impl("flash_bwd", &flash_bwd);
+}
+
+}  // namespace sftamd

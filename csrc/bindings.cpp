@@ -1,0 +1,27 @@
+// Schema definitions of the sftamd custom-op library. Implementations live next to their
+// kernels (TORCH_LIBRARY_IMPL(sftamd, CUDA, ...) in each .hip file); the CPU path of every
+// op is the PyTorch reference in llm_fine_tune_distributed_amd/ops/reference.py, except the
+// native data-pipeline ops below which are CPU kernels.
+#include <torch/library.h>
+
+TORCH_LIBRARY(sftamd, m) {
+  // norms / elementwise
+  m.def("rmsnorm_fwd(Tensor x, Tensor? residual, Tensor weight, float eps) -> (Tensor, Tensor, Tensor)");
+  m.def("rmsnorm_bwd(Tensor dy, Tensor h, Tensor weight, Tensor rstd, Tensor? dres) -> (Tensor, Tensor)");
+  m.def("swiglu_fwd(Tensor gate_up) -> Tensor");
+  m.def("swiglu_bwd(Tensor dy, Tensor gate_up) -> Tensor");
+  m.def("rope_(Tensor(a!) qkv, Tensor cos, Tensor sin, int n_q, int n_kv, int head_dim, bool inverse) -> ()");
+  m.def("embedding_fwd(Tensor ids, Tensor weight) -> Tensor");
+  m.def("embedding_bwd(Tensor dy, Tensor sorted_ids, Tensor perm, Tensor(a!) grad_weight) -> ()");
+  // loss
+  m.def("ce_fwd(Tensor(a!) logits, Tensor labels, Tensor inv_count, bool write_grad) -> Tensor");
+  // attention
+  m.def("flash_fwd(Tensor qkv, Tensor cu_seqlens, int max_seqlen, int n_q, int n_kv, int head_dim, float scale, bool causal) -> (Tensor, Tensor)");
+  m.def("flash_bwd(Tensor dout, Tensor qkv, Tensor out, Tensor lse, Tensor cu_seqlens, int max_seqlen, int n_q, int n_kv, int head_dim, float scale, bool causal) -> Tensor");
+  // optimizer
+  m.def("sumsq(Tensor x) -> Tensor");
+  m.def("adamw_flat(Tensor(a!) param, Tensor grad, Tensor(b!)? master, Tensor(c!) exp_avg, Tensor(d!) exp_avg_sq, Tensor clip_coef, float lr, float beta1, float beta2, float eps, float weight_decay, float bc1, float bc2) -> ()");
+  // native data pipeline (CPU)
+  m.def("pack_sequences(Tensor tokens, Tensor offsets, Tensor order, int max_tokens, int pad_id, int pad_multiple) -> (Tensor, Tensor, Tensor, Tensor, Tensor)");
+  m.def("pad_batch(Tensor tokens, Tensor offsets, Tensor order, int pad_id, int pad_multiple, int max_length) -> (Tensor, Tensor, Tensor)");
+}

@@ -1,0 +1,65 @@
+// Shared helpers for the gfx950 (MI355X / CDNA4) kernels of the sftamd extension.
+// Wave64 everywhere: lane = threadIdx.x & 63; bf16 is handled as raw u16 storage with
+// fp32 math; 16-byte vector accesses (8 x bf16) for every streaming kernel (CDNA guide G13).
+#pragma once
+
+#include <ATen/ATen.h>
+#include <c10/hip/HIPException.h>
+#include <c10/hip/HIPStream.h>
+#include <hip/hip_runtime.h>
+#include <torch/library.h>
+
+#include <cstdint>
+
+namespace sftamd {
+
+typedef unsigned short u16;
+typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
+typedef __attribute__((ext_vector_type(4))) short s16x4;
+typedef __attribute__((ext_vector_type(4))) float f32x4;
+
+constexpr int WAVE = 64;
+
+__device__ __forceinline__ float bf2f(u16 u) { return __uint_as_float(((unsigned)u) << 16); }
+__device__ __forceinline__ u16 f2bf(float f) { return __builtin_bit_cast(u16, (__bf16)f); }
+
+// 8 x bf16 in a uint4 <-> 8 floats
+__device__ __forceinline__ void unpack8(const uint4& v, float* f) {
+  const unsigned w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    f[2 * i] = __uint_as_float(w[i] << 16);
+    f[2 * i + 1] = __uint_as_float(w[i] & 0xffff0000u);
+  }
+}
+__device__ __forceinline__ uint4 pack8(const float* f) {
+  uint4 v;
+  v.x = (unsigned)f2bf(f[0]) | ((unsigned)f2bf(f[1]) << 16);
+  v.y = (unsigned)f2bf(f[2]) | ((unsigned)f2bf(f[3]) << 16);
+  v.z = (unsigned)f2bf(f[4]) | ((unsigned)f2bf(f[5]) << 16);
+  v.w = (unsigned)f2bf(f[6]) | ((unsigned)f2bf(f[7]) << 16);
+  return v;
+}
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+inline hipStream_t cur_stream() { return c10::hip::getCurrentHIPStream().stream(); }
+
+inline int num_cus() { return 256; }  // MI355X: 8 XCDs x 32 CUs
+
+#define SFT_CHECK(cond, ...) TORCH_CHECK(cond, "sftamd: ", __VA_ARGS__)
+#define SFT_CHECK_CUDA(t) SFT_CHECK((t).is_cuda(), #t " must be a GPU tensor")
+#define SFT_CHECK_BF16(t) SFT_CHECK((t).scalar_type() == at::kBFloat16, #t " must be bfloat16")
+#define SFT_CHECK_CONTIG(t) SFT_CHECK((t).is_contiguous(), #t " must be contiguous")
+#define SFT_LAUNCH_CHECK() C10_HIP_KERNEL_LAUNCH_CHECK()
+
+}  // namespace sftamd

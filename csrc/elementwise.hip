@@ -1,0 +1,239 @@
+// Memory-bound elementwise kernels for gfx950: SwiGLU (K6), in-place RoPE on the packed
+// qkv GEMM output (K4), embedding gather (K1) and deterministic embedding backward (K1b).
+// All accesses are 16-byte vectors (8 x bf16); grids are capped at ~8 blocks/CU and
+// grid-stride the rest (CDNA guide G11).
+#include "common.h"
+
+namespace sftamd {
+
+static inline int ew_grid(long nvec) {
+  long g = (nvec + 255) / 256;
+  return (int)std::max<long>(1, std::min<long>(g, 256L * 8));
+}
+
+// ------------------------------------------------------------------------------ SwiGLU
+__global__ __launch_bounds__(256) void swiglu_fwd_kernel(const u16* __restrict__ gu, u16* __restrict__ out, long M,
+                                                         int I) {
+  const int vpr = I / 8;  // vectors per row
+  const long n = M * vpr;
+  for (long v = blockIdx.x * 256L + threadIdx.x; v < n; v += (long)gridDim.x * 256) {
+    const long m = v / vpr;
+    const int c = (int)(v - m * vpr) * 8;
+    float g[8], u[8], o[8];
+    unpack8(*(const uint4*)(gu + m * 2 * I + c), g);
+    unpack8(*(const uint4*)(gu + m * 2 * I + I + c), u);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) o[i] = g[i] / (1.f + __expf(-g[i])) * u[i];
+    *(uint4*)(out + m * I + c) = pack8(o);
+  }
+}
+
+__global__ __launch_bounds__(256) void swiglu_bwd_kernel(const u16* __restrict__ dy, const u16* __restrict__ gu,
+                                                         u16* __restrict__ dgu, long M, int I) {
+  const int vpr = I / 8;
+  const long n = M * vpr;
+  for (long v = blockIdx.x * 256L + threadIdx.x; v < n; v += (long)gridDim.x * 256) {
+    const long m = v / vpr;
+    const int c = (int)(v - m * vpr) * 8;
+    float g[8], u[8], d[8], dg[8], du[8];
+    unpack8(*(const uint4*)(gu + m * 2 * I + c), g);
+    unpack8(*(const uint4*)(gu + m * 2 * I + I + c), u);
+    unpack8(*(const uint4*)(dy + m * I + c), d);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const float s = 1.f / (1.f + __expf(-g[i]));
+      du[i] = d[i] * g[i] * s;
+      dg[i] = d[i] * u[i] * s * (1.f + g[i] * (1.f - s));
+    }
+    *(uint4*)(dgu + m * 2 * I + c) = pack8(dg);
+    *(uint4*)(dgu + m * 2 * I + I + c) = pack8(du);
+  }
+}
+
+at::Tensor swiglu_fwd(const at::Tensor& gu) {
+  SFT_CHECK_BF16(gu);
+  SFT_CHECK_CONTIG(gu);
+  const int I = gu.size(-1) / 2;
+  SFT_CHECK(I % 8 == 0, "intermediate size must be a multiple of 8");
+  const long M = gu.numel() / (2 * I);
+  auto sizes = gu.sizes().vec();
+  sizes.back() = I;
+  auto out = at::empty(sizes, gu.options());
+  if (M == 0) return out;
+  swiglu_fwd_kernel<<<ew_grid(M * I / 8), 256, 0, cur_stream()>>>((const u16*)gu.data_ptr(), (u16*)out.data_ptr(), M, I);
+  SFT_LAUNCH_CHECK();
+  return out;
+}
+
+at::Tensor swiglu_bwd(const at::Tensor& dy, const at::Tensor& gu) {
+  SFT_CHECK_CONTIG(dy);
+  SFT_CHECK_CONTIG(gu);
+  const int I = gu.size(-1) / 2;
+  const long M = gu.numel() / (2 * I);
+  auto dgu = at::empty_like(gu);
+  if (M == 0) return dgu;
+  swiglu_bwd_kernel<<<ew_grid(M * I / 8), 256, 0, cur_stream()>>>((const u16*)dy.data_ptr(), (const u16*)gu.data_ptr(),
+                                                                   (u16*)dgu.data_ptr(), M, I);
+  SFT_LAUNCH_CHECK();
+  return dgu;
+}
+
+// ------------------------------------------------------------------------------ RoPE
+// qkv: [M, ld] with heads [0, nh) rotated (q heads then k heads), rotate_half convention:
+// (x1, x2) = (x[i], x[i + D/2]) -> (x1 c - x2 s, x2 c + x1 s); inverse uses -s.
+__global__ __launch_bounds__(256) void rope_kernel(u16* __restrict__ qkv, const float* __restrict__ cosb,
+                                                   const float* __restrict__ sinb, long M, int ld, int nh, int D,
+                                                   float sign) {
+  const int half = D / 2;
+  const int np = half / 8;  // 8-pair chunks per head
+  const long n = M * nh * np;
+  for (long t = blockIdx.x * 256L + threadIdx.x; t < n; t += (long)gridDim.x * 256) {
+    const long m = t / (nh * np);
+    const int rem = (int)(t - m * nh * np);
+    const int hh = rem / np, p = (rem - hh * np) * 8;
+    u16* base = qkv + m * ld + hh * D;
+    float a[8], b[8], c[8], s[8], o1[8], o2[8];
+    unpack8(*(const uint4*)(base + p), a);
+    unpack8(*(const uint4*)(base + half + p), b);
+    const float4* cp = (const float4*)(cosb + m * half + p);
+    const float4* sp = (const float4*)(sinb + m * half + p);
+    *(float4*)&c[0] = cp[0];
+    *(float4*)&c[4] = cp[1];
+    *(float4*)&s[0] = sp[0];
+    *(float4*)&s[4] = sp[1];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const float si = sign * s[i];
+      o1[i] = a[i] * c[i] - b[i] * si;
+      o2[i] = b[i] * c[i] + a[i] * si;
+    }
+    *(uint4*)(base + p) = pack8(o1);
+    *(uint4*)(base + half + p) = pack8(o2);
+  }
+}
+
+void rope_(at::Tensor qkv, const at::Tensor& cos, const at::Tensor& sin, int64_t n_q, int64_t n_kv, int64_t head_dim,
+           bool inverse) {
+  SFT_CHECK_BF16(qkv);
+  SFT_CHECK_CONTIG(qkv);
+  SFT_CHECK(cos.scalar_type() == at::kFloat && sin.scalar_type() == at::kFloat, "cos/sin must be fp32");
+  SFT_CHECK(cos.is_contiguous() && sin.is_contiguous(), "cos/sin contiguous");
+  SFT_CHECK(head_dim % 16 == 0, "head_dim must be a multiple of 16");
+  const int ld = qkv.size(-1);
+  const long M = qkv.numel() / ld;
+  SFT_CHECK(cos.numel() == M * head_dim / 2, "cos table shape");
+  const int nh = n_q + n_kv;
+  if (M == 0) return;
+  const long n = M * nh * (head_dim / 16);
+  rope_kernel<<<ew_grid(n), 256, 0, cur_stream()>>>((u16*)qkv.data_ptr(), cos.data_ptr<float>(), sin.data_ptr<float>(), M,
+                                                    ld, nh, (int)head_dim, inverse ? -1.f : 1.f);
+  SFT_LAUNCH_CHECK();
+}
+
+// ------------------------------------------------------------------------------ embedding
+__global__ __launch_bounds__(256) void embedding_fwd_kernel(const int64_t* __restrict__ ids, const u16* __restrict__ w,
+                                                            u16* __restrict__ out, long M, int H, long V) {
+  const int vpr = H / 8;
+  const long n = M * vpr;
+  for (long t = blockIdx.x * 256L + threadIdx.x; t < n; t += (long)gridDim.x * 256) {
+    const long m = t / vpr;
+    const int c = (int)(t - m * vpr) * 8;
+    long id = ids[m];
+    id = id < 0 ? 0 : (id >= V ? V - 1 : id);
+    *(uint4*)(out + m * H + c) = *(const uint4*)(w + id * H + c);
+  }
+}
+
+// One wave per sorted position; the first position of each run of equal ids sums all rows of
+// the run in fp32 (fixed order) and adds the result into the bf16 gradient row: one writer per
+// row, no atomics, bitwise reproducible.
+template <int NV>
+__global__ __launch_bounds__(256) void embedding_bwd_kernel(const u16* __restrict__ dy, const int* __restrict__ sorted,
+                                                            const int* __restrict__ perm, u16* __restrict__ gw, int M,
+                                                            int H) {
+  const int i = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (i >= M) return;
+  const int id = sorted[i];
+  if (i > 0 && sorted[i - 1] == id) return;
+  float acc[NV][8];
+#pragma unroll
+  for (int j = 0; j < NV; ++j)
+#pragma unroll
+    for (int e = 0; e < 8; ++e) acc[j][e] = 0.f;
+  for (int k = i; k < M && sorted[k] == id; ++k) {
+    const long row = perm[k];
+#pragma unroll
+    for (int j = 0; j < NV; ++j) {
+      const int c = (lane + 64 * j) * 8;
+      if (c < H) {
+        float f[8];
+        unpack8(*(const uint4*)(dy + row * H + c), f);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) acc[j][e] += f[e];
+      }
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < NV; ++j) {
+    const int c = (lane + 64 * j) * 8;
+    if (c < H) {
+      float f[8];
+      u16* p = gw + (long)id * H + c;
+      unpack8(*(const uint4*)p, f);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) f[e] += acc[j][e];
+      *(uint4*)p = pack8(f);
+    }
+  }
+}
+
+at::Tensor embedding_fwd(const at::Tensor& ids, const at::Tensor& w) {
+  SFT_CHECK_BF16(w);
+  SFT_CHECK_CONTIG(w);
+  SFT_CHECK(ids.scalar_type() == at::kLong, "ids must be int64");
+  auto idc = ids.contiguous();
+  const int H = w.size(1);
+  SFT_CHECK(H % 8 == 0, "hidden % 8");
+  const long M = idc.numel();
+  auto sizes = idc.sizes().vec();
+  sizes.push_back(H);
+  auto out = at::empty(sizes, w.options());
+  if (M == 0) return out;
+  embedding_fwd_kernel<<<ew_grid(M * H / 8), 256, 0, cur_stream()>>>(idc.data_ptr<int64_t>(), (const u16*)w.data_ptr(),
+                                                                      (u16*)out.data_ptr(), M, H, w.size(0));
+  SFT_LAUNCH_CHECK();
+  return out;
+}
+
+void embedding_bwd(const at::Tensor& dy, const at::Tensor& sorted_ids, const at::Tensor& perm, at::Tensor gw) {
+  SFT_CHECK_CONTIG(dy);
+  SFT_CHECK_BF16(gw);
+  SFT_CHECK_CONTIG(gw);
+  SFT_CHECK(sorted_ids.scalar_type() == at::kInt && perm.scalar_type() == at::kInt, "int32 index tensors");
+  const int H = gw.size(1);
+  const int M = sorted_ids.numel();
+  SFT_CHECK(H % 8 == 0 && H <= 4096, "hidden");
+  if (M == 0) return;
+  dim3 grid((M + 3) / 4);
+  auto launch = [&](auto nv) {
+    constexpr int NV = decltype(nv)::value;
+    embedding_bwd_kernel<NV><<<grid, 256, 0, cur_stream()>>>((const u16*)dy.data_ptr(), sorted_ids.data_ptr<int>(),
+                                                             perm.data_ptr<int>(), (u16*)gw.data_ptr(), M, H);
+  };
+  if (H <= 512) launch(std::integral_constant<int, 1>());
+  else if (H <= 1024) launch(std::integral_constant<int, 2>());
+  else if (H <= 2048) launch(std::integral_constant<int, 4>());
+  else launch(std::integral_constant<int, 8>());
+  SFT_LAUNCH_CHECK();
+}
+
+TORCH_LIBRARY_IMPL(sftamd, CUDA, m) {
+  m.impl("swiglu_fwd", &swiglu_fwd);
+  m.impl("swiglu_bwd", &swiglu_bwd);
+  m.impl("rope_", &rope_);
+  m.impl("embedding_fwd", &embedding_fwd);
+  m.impl("embedding_bwd", &embedding_bwd);
+}
+
+}  // namespace sftamd

@@ -1,0 +1,126 @@
+// Flat-buffer optimizer kernels for gfx950: global sum-of-squares for
+// grad clipping and a fused AdamW that reads the clip coefficient from device memory (no host
+// sync), updates the fp32 master + fp32 moments and writes the bf16 working copy, 8 elements
+// per thread per iteration with 16/32-byte vector accesses.
+#include "common.h"
+
+namespace sftamd {
+
+__global__ __launch_bounds__(256) void sumsq_kernel(const u16* __restrict__ x, long n, float* __restrict__ part) {
+  float s = 0.f;
+  const long nv = n / 8;
+  for (long v = blockIdx.x * 256L + threadIdx.x; v < nv; v += (long)gridDim.x * 256) {
+    float f[8];
+    unpack8(*(const uint4*)(x + v * 8), f);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) s += f[i] * f[i];
+  }
+  for (long i = nv * 8 + blockIdx.x * 256L + threadIdx.x; i < n; i += (long)gridDim.x * 256) {
+    const float f = bf2f(x[i]);
+    s += f * f;
+  }
+  s = wave_sum(s);
+  __shared__ float red[4];
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) part[blockIdx.x] = red[0] + red[1] + red[2] + red[3];
+}
+
+at::Tensor sumsq(const at::Tensor& x) {
+  SFT_CHECK_BF16(x);
+  SFT_CHECK_CONTIG(x);
+  const long n = x.numel();
+  int grid = (int)std::min<long>(std::max<long>(1, (n / 8 + 255) / 256), 1024);
+  auto part = at::empty({grid}, x.options().dtype(at::kFloat));
+  sumsq_kernel<<<grid, 256, 0, cur_stream()>>>((const u16*)x.data_ptr(), n, part.data_ptr<float>());
+  SFT_LAUNCH_CHECK();
+  return part;
+}
+
+__device__ __forceinline__ void adam_elem(float& w, float g, float& m, float& v, float lr, float b1, float b2, float eps,
+                                          float wd, float rbc1, float rsbc2) {
+  m = b1 * m + (1.f - b1) * g;
+  v = b2 * v + (1.f - b2) * g * g;
+  const float denom = sqrtf(v) * rsbc2 + eps;
+  w = w * (1.f - lr * wd) - lr * rbc1 * m / denom;
+}
+
+template <bool MASTER>
+__global__ __launch_bounds__(256) void adamw_kernel(u16* __restrict__ p, const u16* __restrict__ g,
+                                                    float* __restrict__ master, float* __restrict__ mom,
+                                                    float* __restrict__ var, const float* __restrict__ coef, long n,
+                                                    float lr, float b1, float b2, float eps, float wd, float rbc1,
+                                                    float rsbc2) {
+  const float c = coef[0];
+  const long nv = n / 8;
+  for (long v = blockIdx.x * 256L + threadIdx.x; v < nv; v += (long)gridDim.x * 256) {
+    const long o = v * 8;
+    float gf[8], w[8], mm[8], vv[8];
+    unpack8(*(const uint4*)(g + o), gf);
+    if (MASTER) {
+      *(float4*)&w[0] = *(const float4*)(master + o);
+      *(float4*)&w[4] = *(const float4*)(master + o + 4);
+    } else {
+      unpack8(*(const uint4*)(p + o), w);
+    }
+    *(float4*)&mm[0] = *(const float4*)(mom + o);
+    *(float4*)&mm[4] = *(const float4*)(mom + o + 4);
+    *(float4*)&vv[0] = *(const float4*)(var + o);
+    *(float4*)&vv[4] = *(const float4*)(var + o + 4);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) adam_elem(w[i], gf[i] * c, mm[i], vv[i], lr, b1, b2, eps, wd, rbc1, rsbc2);
+    if (MASTER) {
+      *(float4*)(master + o) = *(float4*)&w[0];
+      *(float4*)(master + o + 4) = *(float4*)&w[4];
+    }
+    *(float4*)(mom + o) = *(float4*)&mm[0];
+    *(float4*)(mom + o + 4) = *(float4*)&mm[4];
+    *(float4*)(var + o) = *(float4*)&vv[0];
+    *(float4*)(var + o + 4) = *(float4*)&vv[4];
+    *(uint4*)(p + o) = pack8(w);
+  }
+  for (long i = nv * 8 + blockIdx.x * 256L + threadIdx.x; i < n; i += (long)gridDim.x * 256) {
+    float w = MASTER ? master[i] : bf2f(p[i]);
+    float m = mom[i], vr = var[i];
+    adam_elem(w, bf2f(g[i]) * c, m, vr, lr, b1, b2, eps, wd, rbc1, rsbc2);
+    if (MASTER) master[i] = w;
+    mom[i] = m;
+    var[i] = vr;
+    p[i] = f2bf(w);
+  }
+}
+
+void adamw_flat(at::Tensor param, const at::Tensor& grad, const c10::optional<at::Tensor>& master, at::Tensor exp_avg,
+                at::Tensor exp_avg_sq, const at::Tensor& clip_coef, double lr, double beta1, double beta2, double eps,
+                double weight_decay, double bc1, double bc2) {
+  SFT_CHECK_BF16(param);
+  SFT_CHECK_BF16(grad);
+  SFT_CHECK(param.is_contiguous() && grad.is_contiguous() && exp_avg.is_contiguous() && exp_avg_sq.is_contiguous(),
+            "contiguous");
+  SFT_CHECK(exp_avg.scalar_type() == at::kFloat && exp_avg_sq.scalar_type() == at::kFloat, "fp32 moments");
+  const long n = param.numel();
+  SFT_CHECK(grad.numel() == n && exp_avg.numel() == n && exp_avg_sq.numel() == n, "sizes");
+  if (n == 0) return;
+  int grid = (int)std::min<long>(std::max<long>(1, (n / 8 + 255) / 256), 2048);
+  const float rbc1 = (float)(1.0 / bc1), rsbc2 = (float)(1.0 / std::sqrt(bc2));
+  if (master.has_value() && master->defined()) {
+    SFT_CHECK(master->scalar_type() == at::kFloat && master->numel() == n && master->is_contiguous(), "master");
+    adamw_kernel<true><<<grid, 256, 0, cur_stream()>>>(
+        (u16*)param.data_ptr(), (const u16*)grad.data_ptr(), master->data_ptr<float>(), exp_avg.data_ptr<float>(),
+        exp_avg_sq.data_ptr<float>(), clip_coef.data_ptr<float>(), n, (float)lr, (float)beta1, (float)beta2,
+        (float)eps, (float)weight_decay, rbc1, rsbc2);
+  } else {
+    adamw_kernel<false><<<grid, 256, 0, cur_stream()>>>(
+        (u16*)param.data_ptr(), (const u16*)grad.data_ptr(), nullptr, exp_avg.data_ptr<float>(),
+        exp_avg_sq.data_ptr<float>(), clip_coef.data_ptr<float>(), n, (float)lr, (float)beta1, (float)beta2,
+        (float)eps, (float)weight_decay, rbc1, rsbc2);
+  }
+  SFT_LAUNCH_CHECK();
+}
+
+TORCH_LIBRARY_IMPL(sftamd, CUDA, m) {
+  m.impl("sumsq", &sumsq);
+  m.impl("adamw_flat", &adamw_flat);
+}
+
+}  // namespace sftamd

@@ -1,0 +1,202 @@
+// Fused residual-add + RMSNorm forward/backward for gfx950.
+//
+// One wave64 per row: each lane owns NV 16-byte vectors (8 bf16) of the row, the sum of
+// squares is a pure in-wave shuffle reduction (no LDS, no block barrier), and the
+// residual add is fused so the residual stream is read once and written once.
+// Backward keeps the weight gradient in registers across a grid-stride loop over rows,
+// reduces the 4 waves of a block in LDS, and a second kernel sums the per-block
+// partials in a fixed order (deterministic dW, no float atomics in HBM).
+#include "common.h"
+
+namespace sftamd {
+
+template <int NV>
+__global__ __launch_bounds__(256) void rmsnorm_fwd_kernel(const u16* __restrict__ x, const u16* __restrict__ res,
+                                                          const u16* __restrict__ w, u16* __restrict__ y,
+                                                          u16* __restrict__ res_out, float* __restrict__ rstd_out,
+                                                          int M, int H, float eps) {
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (row >= M) return;
+  const long base = (long)row * H;
+  float v[NV][8];
+  float ss = 0.f;
+#pragma unroll
+  for (int j = 0; j < NV; ++j) {
+    const int c = (lane + 64 * j) * 8;
+    if (c < H) {
+      uint4 a = *(const uint4*)(x + base + c);
+      unpack8(a, v[j]);
+      if (res) {
+        float r[8];
+        unpack8(*(const uint4*)(res + base + c), r);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) v[j][i] = bf2f(f2bf(v[j][i] + r[i]));
+        *(uint4*)(res_out + base + c) = pack8(v[j]);
+      }
+#pragma unroll
+      for (int i = 0; i < 8; ++i) ss += v[j][i] * v[j][i];
+    }
+  }
+  ss = wave_sum(ss);
+  const float rstd = rsqrtf(ss / (float)H + eps);
+#pragma unroll
+  for (int j = 0; j < NV; ++j) {
+    const int c = (lane + 64 * j) * 8;
+    if (c < H) {
+      float wf[8], o[8];
+      unpack8(*(const uint4*)(w + c), wf);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) o[i] = bf2f(f2bf(v[j][i] * rstd)) * wf[i];
+      *(uint4*)(y + base + c) = pack8(o);
+    }
+  }
+  if (lane == 0) rstd_out[row] = rstd;
+}
+
+template <int NV>
+__global__ __launch_bounds__(256) void rmsnorm_bwd_kernel(const u16* __restrict__ dy, const u16* __restrict__ h,
+                                                          const u16* __restrict__ w, const float* __restrict__ rstd,
+                                                          const u16* __restrict__ dres, u16* __restrict__ dx,
+                                                          float* __restrict__ dw_part, int M, int H) {
+  __shared__ float red[4096];
+  const int lane = threadIdx.x & 63;
+  const int nwaves = gridDim.x * 4;
+  float wv[NV][8], dw[NV][8];
+#pragma unroll
+  for (int j = 0; j < NV; ++j) {
+    const int c = (lane + 64 * j) * 8;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) dw[j][i] = 0.f;
+    if (c < H) unpack8(*(const uint4*)(w + c), wv[j]);
+  }
+  for (int row = blockIdx.x * 4 + (threadIdx.x >> 6); row < M; row += nwaves) {
+    const long base = (long)row * H;
+    const float r = rstd[row];
+    float n[NV][8], g[NV][8];
+    float dot = 0.f;
+#pragma unroll
+    for (int j = 0; j < NV; ++j) {
+      const int c = (lane + 64 * j) * 8;
+      if (c < H) {
+        unpack8(*(const uint4*)(h + base + c), n[j]);
+        unpack8(*(const uint4*)(dy + base + c), g[j]);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          n[j][i] *= r;
+          dw[j][i] += g[j][i] * n[j][i];
+          g[j][i] *= wv[j][i];
+          dot += g[j][i] * n[j][i];
+        }
+      }
+    }
+    dot = wave_sum(dot) / (float)H;
+#pragma unroll
+    for (int j = 0; j < NV; ++j) {
+      const int c = (lane + 64 * j) * 8;
+      if (c < H) {
+        float o[8], d[8];
+        if (dres) unpack8(*(const uint4*)(dres + base + c), d);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) o[i] = r * (g[j][i] - n[j][i] * dot) + (dres ? d[i] : 0.f);
+        *(uint4*)(dx + base + c) = pack8(o);
+      }
+    }
+  }
+  for (int c = threadIdx.x; c < H; c += 256) red[c] = 0.f;
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < NV; ++j) {
+    const int c = (lane + 64 * j) * 8;
+    if (c < H) {
+#pragma unroll
+      for (int i = 0; i < 8; ++i) atomicAdd(&red[c + i], dw[j][i]);
+    }
+  }
+  __syncthreads();
+  for (int c = threadIdx.x; c < H; c += 256) dw_part[(long)blockIdx.x * H + c] = red[c];
+}
+
+// out[c] = sum_b part[b][c] in fixed order (deterministic)
+__global__ void col_sum_kernel(const float* __restrict__ part, float* __restrict__ out, int P, int H) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= H) return;
+  float s = 0.f;
+  for (int b = 0; b < P; ++b) s += part[(long)b * H + c];
+  out[c] = s;
+}
+
+#define NV_DISPATCH(H, ...)                      \
+  if ((H) <= 512) {                              \
+    constexpr int NV = 1;                        \
+    __VA_ARGS__;                                 \
+  } else if ((H) <= 1024) {                      \
+    constexpr int NV = 2;                        \
+    __VA_ARGS__;                                 \
+  } else if ((H) <= 2048) {                      \
+    constexpr int NV = 4;                        \
+    __VA_ARGS__;                                 \
+  } else {                                       \
+    constexpr int NV = 8;                        \
+    __VA_ARGS__;                                 \
+  }
+
+std::tuple<at::Tensor, at::Tensor, at::Tensor> rmsnorm_fwd(const at::Tensor& x, const c10::optional<at::Tensor>& residual,
+                                                           const at::Tensor& weight, double eps) {
+  SFT_CHECK_CUDA(x);
+  SFT_CHECK_BF16(x);
+  SFT_CHECK_CONTIG(x);
+  SFT_CHECK_BF16(weight);
+  const int H = x.size(-1);
+  const int M = x.numel() / H;
+  SFT_CHECK(H % 8 == 0 && H <= 4096, "hidden size must be a multiple of 8 and <= 4096");
+  auto y = at::empty_like(x);
+  auto rstd = at::empty({M}, x.options().dtype(at::kFloat));
+  at::Tensor res_out = x;
+  const u16* rp = nullptr;
+  if (residual.has_value() && residual->defined()) {
+    SFT_CHECK(residual->sizes() == x.sizes() && residual->is_contiguous(), "residual shape");
+    res_out = at::empty_like(x);
+    rp = (const u16*)residual->data_ptr();
+  }
+  if (M == 0) return {y, res_out, rstd};
+  dim3 grid((M + 3) / 4);
+  NV_DISPATCH(H, rmsnorm_fwd_kernel<NV><<<grid, 256, 0, cur_stream()>>>(
+                     (const u16*)x.data_ptr(), rp, (const u16*)weight.data_ptr(), (u16*)y.data_ptr(),
+                     (u16*)res_out.data_ptr(), rstd.data_ptr<float>(), M, H, (float)eps));
+  SFT_LAUNCH_CHECK();
+  return {y, res_out, rstd};
+}
+
+std::tuple<at::Tensor, at::Tensor> rmsnorm_bwd(const at::Tensor& dy, const at::Tensor& h, const at::Tensor& weight,
+                                               const at::Tensor& rstd, const c10::optional<at::Tensor>& dres) {
+  SFT_CHECK_BF16(dy);
+  SFT_CHECK_CONTIG(dy);
+  SFT_CHECK_CONTIG(h);
+  const int H = h.size(-1);
+  const int M = h.numel() / H;
+  auto dx = at::empty_like(h);
+  const u16* dr = nullptr;
+  if (dres.has_value() && dres->defined()) {
+    SFT_CHECK(dres->is_contiguous() && dres->scalar_type() == at::kBFloat16, "dres");
+    dr = (const u16*)dres->data_ptr();
+  }
+  int nblk = std::min((M + 3) / 4, 512);
+  nblk = std::max(nblk, 1);
+  auto part = at::empty({nblk, H}, h.options().dtype(at::kFloat));
+  auto dw = at::empty({H}, h.options().dtype(at::kFloat));
+  NV_DISPATCH(H, rmsnorm_bwd_kernel<NV><<<nblk, 256, 0, cur_stream()>>>(
+                     (const u16*)dy.data_ptr(), (const u16*)h.data_ptr(), (const u16*)weight.data_ptr(),
+                     rstd.data_ptr<float>(), dr, (u16*)dx.data_ptr(), part.data_ptr<float>(), M, H));
+  SFT_LAUNCH_CHECK();
+  col_sum_kernel<<<(H + 255) / 256, 256, 0, cur_stream()>>>(part.data_ptr<float>(), dw.data_ptr<float>(), nblk, H);
+  SFT_LAUNCH_CHECK();
+  return {dx, dw};
+}
+
+TORCH_LIBRARY_IMPL(sftamd, CUDA, m) {
+  m.impl("rmsnorm_fwd", &rmsnorm_fwd);
+  m.impl("rmsnorm_bwd", &rmsnorm_bwd);
+}
+
+}  // namespace sftamd

@@ -1,0 +1,21 @@
+"""Fused ops: HIP/CDNA4 kernels (GPU) with PyTorch reference implementations (CPU/oracle)."""
+from . import reference
+from ._ext import load as load_extension, use_hip, hip_disabled
+from .fused import (
+    IGNORE_INDEX,
+    add_rms_norm,
+    embedding,
+    flash_attention,
+    linear,
+    lm_head_cross_entropy,
+    rms_norm,
+    rope_,
+    swiglu,
+)
+from .optim_kernels import adamw_flat_, grad_norm_flat
+
+__all__ = [
+    "reference", "load_extension", "use_hip", "hip_disabled", "IGNORE_INDEX", "add_rms_norm",
+    "embedding", "flash_attention", "linear", "lm_head_cross_entropy", "rms_norm", "rope_", "swiglu",
+    "adamw_flat_", "grad_norm_flat",
+]

@@ -1,0 +1,320 @@
+"""Autograd Functions for the SmolLM3/Llama hot path.
+
+Every Function is device-agnostic: on GPU tensors it calls the CDNA4 HIP kernels in
+``torch.ops.sftamd`` (csrc/*.hip); on CPU tensors it runs ``ops.reference``. The same
+gradient plumbing runs in both cases, so CPU tests exercise it.
+
+Gradient plumbing (replaces the c10d Reducer's copy-into-bucket):
+trainable parameters may carry ``param.main_grad`` — a view into the DDP engine's flat,
+bucketed gradient buffer. Weight gradients are accumulated *directly* into it (GEMM with
+beta=1 for linears, fused reductions for norms, a deterministic segment-sum for the
+embedding), and autograd never materialises ``param.grad``. Each parameter declares how
+many times it is used per forward (``_sftamd_uses``; 2 for a tied embedding); when all
+uses have been back-propagated the parameter's ready-hook fires, which is what lets the
+DDP engine launch bucket all-reduces while backward is still running.
+"""
+from __future__ import annotations
+
+import math
+from typing import Optional, Tuple
+
+import torch
+from torch.autograd import Function
+
+from . import _ext
+from . import reference as ref
+
+IGNORE_INDEX = -100
+
+
+# ----------------------------------------------------------------------------- grad plumbing
+def _weight_grad_done(param: torch.Tensor) -> None:
+    rem = getattr(param, "_sftamd_remaining", None)
+    if rem is None:
+        return
+    rem -= 1
+    param._sftamd_remaining = rem
+    if rem <= 0:
+        hook = getattr(param, "_sftamd_ready_hook", None)
+        if hook is not None:
+            hook(param)
+
+
+def _accumulate_weight_grad(param: torch.Tensor, dy2d: torch.Tensor, x2d: torch.Tensor,
+                            scale: Optional[torch.Tensor] = None):
+    """dW = dy^T @ x (optionally * scale). Accumulates into main_grad if present."""
+    mg = getattr(param, "main_grad", None)
+    if scale is not None:
+        x2d = x2d * scale.to(x2d.dtype)
+    if mg is not None:
+        if mg.dtype == dy2d.dtype:
+            mg.addmm_(dy2d.t(), x2d)
+        else:
+            mg.add_(torch.mm(dy2d.t(), x2d).to(mg.dtype))
+        _weight_grad_done(param)
+        return None
+    return torch.mm(dy2d.t(), x2d).to(param.dtype)
+
+
+def _accumulate_small_grad(param: torch.Tensor, g: torch.Tensor):
+    mg = getattr(param, "main_grad", None)
+    if mg is not None:
+        mg.add_(g.to(mg.dtype))
+        _weight_grad_done(param)
+        return None
+    return g.to(param.dtype)
+
+
+# ----------------------------------------------------------------------------- linear
+class LinearFn(Function):
+    @staticmethod
+    def forward(ctx, x, weight):
+        ctx.save_for_backward(x)
+        ctx.weight = weight
+        return torch.nn.functional.linear(x, weight)
+
+    @staticmethod
+    def backward(ctx, dy):
+        (x,) = ctx.saved_tensors
+        w = ctx.weight
+        dy2d = dy.reshape(-1, dy.shape[-1])
+        dx = dw = None
+        if ctx.needs_input_grad[0]:
+            dx = torch.mm(dy2d, w).view(*dy.shape[:-1], w.shape[1])
+        if ctx.needs_input_grad[1]:
+            dw = _accumulate_weight_grad(w, dy2d, x.reshape(-1, x.shape[-1]))
+        return dx, dw
+
+
+def linear(x: torch.Tensor, weight: torch.Tensor) -> torch.Tensor:
+    return LinearFn.apply(x, weight)
+
+
+# ----------------------------------------------------------------------------- embedding
+class EmbeddingFn(Function):
+    @staticmethod
+    def forward(ctx, ids, weight):
+        ctx.save_for_backward(ids)
+        ctx.weight = weight
+        if _ext.use_hip(weight):
+            return _ext.ops().embedding_fwd(ids, weight)
+        return torch.nn.functional.embedding(ids, weight)
+
+    @staticmethod
+    def backward(ctx, dy):
+        (ids,) = ctx.saved_tensors
+        w = ctx.weight
+        if not ctx.needs_input_grad[1]:
+            return None, None
+        mg = getattr(w, "main_grad", None)
+        flat_ids = ids.reshape(-1)
+        dy2d = dy.reshape(-1, dy.shape[-1]).contiguous()
+        if _ext.use_hip(dy):
+            sorted_ids, perm = torch.sort(flat_ids.to(torch.int32))
+            target = mg if mg is not None else torch.zeros_like(w)
+            _ext.ops().embedding_bwd(dy2d, sorted_ids, perm.to(torch.int32), target)
+            if mg is not None:
+                _weight_grad_done(w)
+                return None, None
+            return None, target
+        g = torch.zeros(w.shape, dtype=torch.float32, device=w.device)
+        g.index_add_(0, flat_ids, dy2d.float())
+        return None, _accumulate_small_grad(w, g)
+
+
+def embedding(ids: torch.Tensor, weight: torch.Tensor) -> torch.Tensor:
+    return EmbeddingFn.apply(ids, weight)
+
+
+# ----------------------------------------------------------------------------- RMSNorm (+residual)
+class AddRMSNormFn(Function):
+    """res_out = x (+ residual); y = rmsnorm(res_out) * w. Returns (y, res_out)."""
+
+    @staticmethod
+    def forward(ctx, x, residual, weight, eps):
+        if _ext.use_hip(x):
+            y, res_out, rstd = _ext.ops().rmsnorm_fwd(x, residual, weight, eps)
+        else:
+            res_out = x if residual is None else (x.float() + residual.float()).to(x.dtype)
+            y, rstd = ref.rms_norm(res_out, weight, eps)
+        ctx.save_for_backward(res_out, rstd)
+        ctx.weight = weight
+        ctx.has_residual = residual is not None
+        return y, res_out
+
+    @staticmethod
+    def backward(ctx, dy, dres):
+        h, rstd = ctx.saved_tensors
+        w = ctx.weight
+        if _ext.use_hip(h):
+            dx, dw = _ext.ops().rmsnorm_bwd(dy.contiguous(), h, w, rstd,
+                                           dres.contiguous() if dres is not None else None)
+        else:
+            hf = h.float()
+            n = hf * rstd[..., None]
+            dyf = dy.float()
+            dyw = dyf * w.float()
+            dx = rstd[..., None] * (dyw - n * (dyw * n).mean(-1, keepdim=True))
+            if dres is not None:
+                dx = dx + dres.float()
+            dx = dx.to(h.dtype)
+            dw = (dyf * n).reshape(-1, h.shape[-1]).sum(0)
+        dweight = None
+        if ctx.needs_input_grad[2]:
+            dweight = _accumulate_small_grad(w, dw)
+        dresid = dx if ctx.has_residual else None
+        return dx, dresid, dweight, None
+
+
+def add_rms_norm(x, residual, weight, eps) -> Tuple[torch.Tensor, torch.Tensor]:
+    return AddRMSNormFn.apply(x, residual, weight, eps)
+
+
+def rms_norm(x, weight, eps) -> torch.Tensor:
+    return AddRMSNormFn.apply(x, None, weight, eps)[0]
+
+
+# ----------------------------------------------------------------------------- SwiGLU
+class SwiGLUFn(Function):
+    @staticmethod
+    def forward(ctx, gate_up):
+        ctx.save_for_backward(gate_up)
+        if _ext.use_hip(gate_up):
+            return _ext.ops().swiglu_fwd(gate_up)
+        return ref.swiglu(gate_up)
+
+    @staticmethod
+    def backward(ctx, dy):
+        (gu,) = ctx.saved_tensors
+        if _ext.use_hip(gu):
+            return _ext.ops().swiglu_bwd(dy.contiguous(), gu)
+        g, u = gu.float().chunk(2, dim=-1)
+        sg = torch.sigmoid(g)
+        silu = g * sg
+        dyf = dy.float()
+        dg = dyf * u * (sg * (1 + g * (1 - sg)))
+        du = dyf * silu
+        return torch.cat([dg, du], dim=-1).to(gu.dtype)
+
+
+def swiglu(gate_up: torch.Tensor) -> torch.Tensor:
+    return SwiGLUFn.apply(gate_up)
+
+
+# ----------------------------------------------------------------------------- RoPE (in place on packed qkv)
+class RoPEFn(Function):
+    @staticmethod
+    def forward(ctx, qkv, cos, sin, n_q, n_kv, head_dim):
+        ctx.save_for_backward(cos, sin)
+        ctx.dims = (n_q, n_kv, head_dim)
+        _rope_inplace(qkv, cos, sin, n_q, n_kv, head_dim, inverse=False)
+        ctx.mark_dirty(qkv)
+        return qkv
+
+    @staticmethod
+    def backward(ctx, dqkv):
+        cos, sin = ctx.saved_tensors
+        n_q, n_kv, hd = ctx.dims
+        dqkv = dqkv.contiguous()
+        _rope_inplace(dqkv, cos, sin, n_q, n_kv, hd, inverse=True)
+        return dqkv, None, None, None, None, None
+
+
+def _rope_inplace(qkv, cos, sin, n_q, n_kv, hd, inverse):
+    if _ext.use_hip(qkv):
+        _ext.ops().rope_(qkv, cos, sin, n_q, n_kv, hd, inverse)
+        return
+    M = qkv.shape[0]
+    qk = qkv[:, : (n_q + n_kv) * hd].view(M, n_q + n_kv, hd)
+    qk.copy_(ref.apply_rope(qk, cos, sin, inverse=inverse))
+
+
+def rope_(qkv, cos, sin, n_q, n_kv, head_dim):
+    return RoPEFn.apply(qkv, cos, sin, n_q, n_kv, head_dim)
+
+
+# ----------------------------------------------------------------------------- attention
+class FlashAttnFn(Function):
+    @staticmethod
+    def forward(ctx, qkv, cu_seqlens, max_seqlen, n_q, n_kv, head_dim, scale, causal):
+        ctx.dims = (max_seqlen, n_q, n_kv, head_dim, scale, causal)
+        if _ext.use_hip(qkv):
+            out, lse = _ext.ops().flash_fwd(qkv, cu_seqlens, max_seqlen, n_q, n_kv, head_dim, scale, causal)
+            ctx.save_for_backward(qkv, cu_seqlens, out, lse)
+            ctx.hip = True
+        else:
+            out = ref.attention(qkv, n_q, n_kv, head_dim, cu_seqlens, scale, causal)
+            ctx.save_for_backward(qkv, cu_seqlens)
+            ctx.hip = False
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        max_seqlen, n_q, n_kv, hd, scale, causal = ctx.dims
+        if ctx.hip:
+            qkv, cu, out, lse = ctx.saved_tensors
+            dqkv = _ext.ops().flash_bwd(dout.contiguous(), qkv, out, lse, cu, max_seqlen, n_q, n_kv, hd, scale, causal)
+        else:
+            qkv, cu = ctx.saved_tensors
+            with torch.enable_grad():
+                q = qkv.detach().float().requires_grad_(True)
+                o = ref.attention(q, n_q, n_kv, hd, cu, scale, causal)
+                (dq,) = torch.autograd.grad(o, q, dout.float())
+            dqkv = dq.to(qkv.dtype)
+        return dqkv, None, None, None, None, None, None, None
+
+
+def flash_attention(qkv, cu_seqlens, max_seqlen, n_q, n_kv, head_dim, scale=None, causal=True):
+    scale = scale if scale is not None else 1.0 / math.sqrt(head_dim)
+    return FlashAttnFn.apply(qkv, cu_seqlens, int(max_seqlen), n_q, n_kv, head_dim, float(scale), bool(causal))
+
+
+# ----------------------------------------------------------------------------- LM head + CE
+def _ce_rows(logits: torch.Tensor, labels: torch.Tensor, inv_count: torch.Tensor, write_grad: bool):
+    """Per-row CE over the vocab. Returns stats [4, M] fp32 = (loss, lse, entropy, correct).
+    If write_grad, logits is overwritten in place by d(sum(loss)*inv_count)/dlogits."""
+    if _ext.use_hip(logits):
+        return _ext.ops().ce_fwd(logits, labels, inv_count, write_grad)
+    loss, lse, correct, ent = ref.cross_entropy(logits, labels)
+    if write_grad:
+        valid = (labels != IGNORE_INDEX)
+        p = torch.softmax(logits.float(), -1)
+        p[torch.arange(p.shape[0], device=p.device), labels.clamp(min=0)] -= 1.0
+        p *= (valid.float() * inv_count.float())[:, None]
+        logits.copy_(p)
+    return torch.stack([loss, lse, ent, correct.float()])
+
+
+class LMHeadCEFn(Function):
+    """loss = sum_t CE(h_t W^T, y_t) * inv_count, with dlogits computed in the forward pass
+    (written over the logits buffer), so the fp32 logits are never materialised."""
+
+    @staticmethod
+    def forward(ctx, h, weight, labels, inv_count):
+        h2d = h.reshape(-1, h.shape[-1])
+        logits = torch.nn.functional.linear(h2d, weight)
+        need_grad = ctx.needs_input_grad[0] or ctx.needs_input_grad[1]
+        stats = _ce_rows(logits, labels.reshape(-1), inv_count, need_grad)
+        loss = (stats[0].sum() * inv_count.float()).reshape(())
+        if need_grad:
+            ctx.save_for_backward(h2d, logits)
+        ctx.weight = weight
+        ctx.h_shape = h.shape
+        ctx.mark_non_differentiable(stats)
+        return loss, stats
+
+    @staticmethod
+    def backward(ctx, dloss, _dstats):
+        h2d, dlogits = ctx.saved_tensors
+        w = ctx.weight
+        g = dloss.float()
+        dh = dw = None
+        if ctx.needs_input_grad[0]:
+            dh = (torch.mm(dlogits, w) * g.to(dlogits.dtype)).view(ctx.h_shape)
+        if ctx.needs_input_grad[1]:
+            dw = _accumulate_weight_grad(w, dlogits, h2d, scale=g)
+        return dh, dw, None, None
+
+
+def lm_head_cross_entropy(h, weight, labels, inv_count) -> Tuple[torch.Tensor, torch.Tensor]:
+    return LMHeadCEFn.apply(h, weight, labels, inv_count)

@@ -1,0 +1,129 @@
+"""Pure-PyTorch reference implementations of every fused op.
+
+These run on CPU (tests, the gloo plumbing config of BASELINE.json) and serve as the fp32
+numerics oracle for the HIP kernels. Semantics follow the HF modules the reference runs
+(transformers ``modeling_smollm3.py``: RMSNorm, rotate_half RoPE, SwiGLU, causal GQA SDPA,
+``loss_utils.py`` ForCausalLMLoss with ignore_index=-100 and sum/num_items normalisation).
+"""
+from __future__ import annotations
+
+import math
+from typing import Optional, Tuple
+
+import torch
+import torch.nn.functional as F
+
+IGNORE_INDEX = -100
+
+
+def rms_norm(x: torch.Tensor, weight: torch.Tensor, eps: float) -> Tuple[torch.Tensor, torch.Tensor]:
+    """Returns (y, rstd). y = weight * x / sqrt(mean(x^2) + eps), computed in fp32."""
+    xf = x.float()
+    rstd = torch.rsqrt(xf.pow(2).mean(-1, keepdim=True) + eps)
+    y = (xf * rstd).to(x.dtype) * weight
+    return y, rstd.squeeze(-1)
+
+
+def swiglu(gate_up: torch.Tensor) -> torch.Tensor:
+    g, u = gate_up.chunk(2, dim=-1)
+    return (F.silu(g.float()) * u.float()).to(gate_up.dtype)
+
+
+def rope_cos_sin(positions: torch.Tensor, head_dim: int, theta: float,
+                 scaling: Optional[dict] = None) -> Tuple[torch.Tensor, torch.Tensor]:
+    """cos/sin tables [n, head_dim/2] in fp32 for the given integer positions."""
+    inv_freq = rope_inv_freq(head_dim, theta, scaling, positions.device)
+    freqs = positions.float()[:, None] * inv_freq[None, :]
+    return freqs.cos(), freqs.sin()
+
+
+def rope_inv_freq(head_dim: int, theta: float, scaling: Optional[dict], device=None) -> torch.Tensor:
+    inv = 1.0 / (theta ** (torch.arange(0, head_dim, 2, dtype=torch.float64, device=device) / head_dim))
+    if scaling and scaling.get("rope_type", scaling.get("type")) == "llama3":
+        factor = scaling["factor"]
+        lo, hi = scaling.get("low_freq_factor", 1.0), scaling.get("high_freq_factor", 4.0)
+        old = scaling.get("original_max_position_embeddings", 8192)
+        lo_wl, hi_wl = old / lo, old / hi
+        wl = 2 * math.pi / inv
+        scaled = torch.where(wl > lo_wl, inv / factor, inv)
+        smooth = (old / wl - lo) / (hi - lo)
+        mid = (1 - smooth) * scaled / factor + smooth * scaled
+        is_mid = (wl <= lo_wl) & (wl >= hi_wl)
+        inv = torch.where(is_mid, mid, scaled)
+    return inv.float()
+
+
+def apply_rope(x: torch.Tensor, cos: torch.Tensor, sin: torch.Tensor, inverse: bool = False) -> torch.Tensor:
+    """x [M, H, D]; cos/sin [M, D/2]. rotate_half convention (HF Llama/SmolLM3)."""
+    d2 = x.shape[-1] // 2
+    xf = x.float()
+    x1, x2 = xf[..., :d2], xf[..., d2:]
+    c, s = cos[:, None, :], sin[:, None, :]
+    if inverse:
+        s = -s
+    o1 = x1 * c - x2 * s
+    o2 = x2 * c + x1 * s
+    return torch.cat([o1, o2], dim=-1).to(x.dtype)
+
+
+def attention(qkv: torch.Tensor, n_q: int, n_kv: int, head_dim: int, cu_seqlens: torch.Tensor,
+              scale: Optional[float] = None, causal: bool = True) -> torch.Tensor:
+    """Varlen causal GQA attention on the packed qkv layout [M, (n_q+2n_kv)*D] -> [M, n_q*D]."""
+    scale = scale if scale is not None else 1.0 / math.sqrt(head_dim)
+    M = qkv.shape[0]
+    q = qkv[:, : n_q * head_dim].view(M, n_q, head_dim)
+    k = qkv[:, n_q * head_dim: (n_q + n_kv) * head_dim].view(M, n_kv, head_dim)
+    v = qkv[:, (n_q + n_kv) * head_dim:].view(M, n_kv, head_dim)
+    out = torch.empty(M, n_q, head_dim, dtype=qkv.dtype, device=qkv.device)
+    rep = n_q // n_kv
+    cu = cu_seqlens.tolist()
+    for i in range(len(cu) - 1):
+        s, e = cu[i], cu[i + 1]
+        if e <= s:
+            continue
+        qi = q[s:e].float().transpose(0, 1)  # [H, T, D]
+        ki = k[s:e].float().transpose(0, 1).repeat_interleave(rep, 0)
+        vi = v[s:e].float().transpose(0, 1).repeat_interleave(rep, 0)
+        att = (qi @ ki.transpose(-1, -2)) * scale
+        if causal:
+            T = e - s
+            mask = torch.ones(T, T, dtype=torch.bool, device=qkv.device).tril()
+            att = att.masked_fill(~mask, float("-inf"))
+        p = att.softmax(-1)
+        out[s:e] = (p @ vi).transpose(0, 1).to(qkv.dtype)
+    if cu[-1] < M:  # tokens outside any sequence (should not happen) -> zeros
+        out[cu[-1]:] = 0
+    return out.view(M, n_q * head_dim)
+
+
+def cross_entropy(logits: torch.Tensor, labels: torch.Tensor):
+    """Per-token CE in fp32 (ignore_index=-100). Returns (loss_per_token, lse, argmax_correct, entropy)."""
+    lf = logits.float()
+    lse = torch.logsumexp(lf, dim=-1)
+    valid = labels != IGNORE_INDEX
+    safe = labels.clamp(min=0)
+    tgt = lf.gather(-1, safe[:, None]).squeeze(-1)
+    loss = torch.where(valid, lse - tgt, torch.zeros_like(lse))
+    p = torch.softmax(lf, -1)
+    entropy = lse - (p * lf).sum(-1)
+    correct = (lf.argmax(-1) == labels) & valid
+    return loss, lse, correct, entropy
+
+
+def adamw_(param: torch.Tensor, grad: torch.Tensor, exp_avg: torch.Tensor, exp_avg_sq: torch.Tensor,
+           master: Optional[torch.Tensor], lr: float, beta1: float, beta2: float, eps: float,
+           weight_decay: float, step: int, grad_scale: float = 1.0) -> None:
+    """Decoupled-weight-decay Adam (torch.optim.AdamW semantics) on flat tensors, in place."""
+    w = master if master is not None else param.float()
+    g = grad.float() * grad_scale
+    exp_avg.mul_(beta1).add_(g.to(exp_avg.dtype), alpha=1 - beta1)
+    exp_avg_sq.mul_(beta2).addcmul_(g.to(exp_avg_sq.dtype), g.to(exp_avg_sq.dtype), value=1 - beta2)
+    bc1 = 1 - beta1 ** step
+    bc2 = 1 - beta2 ** step
+    denom = (exp_avg_sq.float() / bc2).sqrt().add_(eps)
+    w.mul_(1 - lr * weight_decay)
+    w.addcdiv_(exp_avg.float(), denom, value=-lr / bc1)
+    if master is not None:
+        param.copy_(master)
+    else:
+        param.copy_(w)

@@ -1,0 +1,166 @@
+"""Numerics of every HIP kernel vs a plain PyTorch fp32 reference of the same op (GPU only)."""
+import math
+import os
+
+import pytest
+import torch
+
+from llm_fine_tune_distributed_amd.ops import _ext
+from llm_fine_tune_distributed_amd.ops import reference as ref
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _ext_loaded():
+    assert _ext.load(), _ext.load_error()
+    yield
+
+
+def rel_err(a, b):
+    a, b = a.float(), b.float()
+    return ((a - b).norm() / (b.norm() + 1e-12)).item()
+
+
+@pytest.mark.parametrize("H", [2048, 4096, 640])
+@pytest.mark.parametrize("with_res", [False, True])
+def test_rmsnorm(H, with_res):
+    torch.manual_seed(0)
+    M = 1000
+    x = torch.randn(M, H, device=DEV, dtype=torch.bfloat16)
+    r = torch.randn(M, H, device=DEV, dtype=torch.bfloat16) if with_res else None
+    w = (1 + 0.1 * torch.randn(H, device=DEV)).to(torch.bfloat16)
+    y, ro, rstd = _ext.ops().rmsnorm_fwd(x, r, w, 1e-6)
+    h = x if r is None else (x.float() + r.float()).to(torch.bfloat16)
+    y_ref, rstd_ref = ref.rms_norm(h, w, 1e-6)
+    assert torch.equal(ro, h)
+    assert rel_err(y, y_ref) < 1e-2
+    assert torch.allclose(rstd, rstd_ref, rtol=1e-4)
+    # backward vs autograd on fp32
+    dy = torch.randn_like(x)
+    dres = torch.randn_like(x) if with_res else None
+    dx, dw = _ext.ops().rmsnorm_bwd(dy, h, w, rstd, dres)
+    hf = h.float().requires_grad_(True)
+    wf = w.float().requires_grad_(True)
+    yf = hf * torch.rsqrt(hf.pow(2).mean(-1, keepdim=True) + 1e-6) * wf
+    gx, gw = torch.autograd.grad(yf, (hf, wf), dy.float())
+    if dres is not None:
+        gx = gx + dres.float()
+    assert rel_err(dx, gx) < 1e-2
+    assert rel_err(dw, gw) < 1e-3
+
+
+def test_swiglu():
+    torch.manual_seed(0)
+    gu = torch.randn(777, 2 * 1376, device=DEV, dtype=torch.bfloat16)
+    out = _ext.ops().swiglu_fwd(gu)
+    assert rel_err(out, ref.swiglu(gu.float())) < 1e-2
+    dy = torch.randn_like(out)
+    g = gu.float().requires_grad_(True)
+    o = ref.swiglu(g)
+    (gref,) = torch.autograd.grad(o, g, dy.float())
+    assert rel_err(_ext.ops().swiglu_bwd(dy, gu), gref) < 1e-2
+
+
+@pytest.mark.parametrize("inverse", [False, True])
+def test_rope(inverse):
+    torch.manual_seed(0)
+    M, nq, nkv, D = 300, 16, 4, 128
+    qkv = torch.randn(M, (nq + 2 * nkv) * D, device=DEV, dtype=torch.bfloat16)
+    pos = torch.randint(0, 4000, (M,), device=DEV)
+    cos, sin = ref.rope_cos_sin(pos, D, 2e6)
+    exp = qkv.clone()
+    qk = exp[:, : (nq + nkv) * D].view(M, nq + nkv, D)
+    qk.copy_(ref.apply_rope(qk.float(), cos, sin, inverse=inverse))
+    got = qkv.clone()
+    _ext.ops().rope_(got, cos.contiguous(), sin.contiguous(), nq, nkv, D, inverse)
+    assert rel_err(got, exp) < 1e-2
+    assert torch.equal(got[:, (nq + nkv) * D:], qkv[:, (nq + nkv) * D:])  # V untouched
+
+
+def test_embedding():
+    torch.manual_seed(0)
+    V, H, M = 5000, 2048, 3000
+    w = torch.randn(V, H, device=DEV, dtype=torch.bfloat16)
+    ids = torch.randint(0, 300, (M,), device=DEV)  # many repeats
+    assert torch.equal(_ext.ops().embedding_fwd(ids, w), w[ids])
+    dy = torch.randn(M, H, device=DEV, dtype=torch.bfloat16)
+    g = torch.zeros(V, H, device=DEV, dtype=torch.bfloat16)
+    s, perm = torch.sort(ids.to(torch.int32))
+    _ext.ops().embedding_bwd(dy, s, perm.to(torch.int32), g)
+    gr = torch.zeros(V, H, device=DEV).index_add_(0, ids, dy.float())
+    assert rel_err(g, gr) < 1e-2
+    g2 = torch.zeros_like(g)
+    _ext.ops().embedding_bwd(dy, s, perm.to(torch.int32), g2)
+    assert torch.equal(g, g2)  # deterministic
+
+
+@pytest.mark.parametrize("V", [128256, 512])
+def test_cross_entropy(V):
+    torch.manual_seed(0)
+    M = 257
+    logits = (3 * torch.randn(M, V, device=DEV)).to(torch.bfloat16)
+    labels = torch.randint(0, V, (M,), device=DEV)
+    labels[::7] = -100
+    inv = torch.tensor([1.0 / 100.0], device=DEV)
+    lg = logits.clone()
+    stats = _ext.ops().ce_fwd(lg, labels, inv, True)
+    loss, lse, correct, ent = ref.cross_entropy(logits, labels)
+    assert torch.allclose(stats[0], loss, atol=2e-3, rtol=1e-3)
+    assert torch.allclose(stats[1], lse, atol=2e-3, rtol=1e-3)
+    assert torch.allclose(stats[2], ent, atol=2e-2, rtol=1e-2)
+    assert torch.equal(stats[3].bool(), correct)
+    lf = logits.float().requires_grad_(True)
+    l = torch.nn.functional.cross_entropy(lf, labels, ignore_index=-100, reduction="sum") * inv[0]
+    (gref,) = torch.autograd.grad(l, lf)
+    assert rel_err(lg, gref) < 2e-2
+
+
+def _attn_case(lens, nq, nkv, causal, variant):
+    os.environ["SFTAMD_ATTN_TR"] = variant
+    torch.manual_seed(0)
+    D = 128
+    cu = torch.tensor([0] + list(torch.tensor(lens).cumsum(0)), dtype=torch.int32, device=DEV)
+    M = int(cu[-1])
+    qkv = torch.randn(M, (nq + 2 * nkv) * D, device=DEV, dtype=torch.bfloat16)
+    scale = 1 / math.sqrt(D)
+    out, lse = _ext.ops().flash_fwd(qkv, cu, max(lens), nq, nkv, D, scale, causal)
+    q32 = qkv.float().requires_grad_(True)
+    o_ref = ref.attention(q32, nq, nkv, D, cu, scale, causal)
+    assert rel_err(out, o_ref) < 2e-2, rel_err(out, o_ref)
+    dout = torch.randn_like(out)
+    (g_ref,) = torch.autograd.grad(o_ref, q32, dout.float())
+    dqkv = _ext.ops().flash_bwd(dout, qkv, out, lse, cu, max(lens), nq, nkv, D, scale, causal)
+    for name, sl in (("dq", slice(0, nq * D)), ("dk", slice(nq * D, (nq + nkv) * D)), ("dv", slice((nq + nkv) * D, None))):
+        e = rel_err(dqkv[:, sl], g_ref[:, sl])
+        assert e < 3e-2, (name, e)
+
+
+@pytest.mark.parametrize("variant", ["1", "0"])
+@pytest.mark.parametrize("causal", [True, False])
+def test_flash_attention_varlen_gqa(variant, causal):
+    _attn_case([100, 255, 64, 1], 8, 2, causal, variant)
+
+
+def test_flash_attention_smollm3_shape():
+    _attn_case([512] * 4, 16, 4, True, "1")
+
+
+def test_adamw_and_norm():
+    torch.manual_seed(0)
+    n = 100003
+    p = torch.randn(n, device=DEV).to(torch.bfloat16)
+    g = torch.randn(n, device=DEV).to(torch.bfloat16)
+    master = p.float()
+    m = torch.randn(n, device=DEV).abs() * 0.01
+    v = torch.randn(n, device=DEV).abs() * 0.001
+    coef = torch.tensor([0.5], device=DEV)
+    p2, master2, m2, v2 = p.clone(), master.clone(), m.clone(), v.clone()
+    _ext.ops().adamw_flat(p, g, master, m, v, coef, 1e-3, 0.9, 0.999, 1e-8, 0.01, 1 - 0.9 ** 3, 1 - 0.999 ** 3)
+    ref.adamw_(p2, g.float() * 0.5, m2, v2, master2, 1e-3, 0.9, 0.999, 1e-8, 0.01, 3)
+    assert torch.allclose(master, master2, atol=1e-6, rtol=1e-5)
+    assert torch.allclose(m, m2, atol=1e-6) and torch.allclose(v, v2, atol=1e-7)
+    assert torch.equal(p, master.to(torch.bfloat16))
+    part = _ext.ops().sumsq(g)
+    assert abs(part.sum().item() - g.float().pow(2).sum().item()) / g.float().pow(2).sum().item() < 1e-5
