@@ -1,0 +1,126 @@
+#!/usr/bin/env python3
+"""Headline benchmark: SmolLM3-3B full-parameter SFT, bf16, samples/s on N MI355X GPUs.
+
+Metric and config follow BASELINE.json: "samples/sec SmolLM3-3B full SFT bf16 at 1/2/4/8
+MI355X; DDP scaling efficiency", reference 4-GPU config = per-device batch 8 x GA 2
+(README.md:69). Every timed step is a complete optimizer step of the real training path
+(``SFTTrainer.optimizer_step``): GA micro-batches of fwd+bwd through the HIP kernels, RCCL
+bucket all-reduce overlapped with backward, grad-norm clip and fused AdamW (fp32 master).
+Data: synthetic token sequences of ``--seq`` tokens (the reference's samples are ~420-525
+tokens), random-init weights of the SmolLM3-3B architecture (no network).
+
+Weak scaling: per-GPU work is fixed (micro-batch x GA), global batch = 16 x N.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+    python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--model", default="smollm3-3b")
+    ap.add_argument("--micro-batch", type=int, default=8)
+    ap.add_argument("--ga", type=int, default=2)
+    ap.add_argument("--seq", type=int, default=512)
+    ap.add_argument("--bucket-mb", type=float, default=float(os.environ.get("SFTAMD_BUCKET_MB", "64")))
+    ap.add_argument("--packing", action="store_true")
+    ap.add_argument("--tunableop", default=os.environ.get("SFTAMD_TUNABLEOP", "auto"),
+                    help="auto: use the committed hipBLASLt selection file if present")
+    ap.add_argument("--profile-steps", type=int, default=0)
+    a = ap.parse_args()
+
+    root = os.path.dirname(os.path.abspath(__file__))
+    tfile = os.path.join(root, "tuning", "tunableop_results_mi355x.csv")
+    if a.tunableop != "off" and os.path.exists(tfile) and "PYTORCH_TUNABLEOP_ENABLED" not in os.environ:
+        os.environ["PYTORCH_TUNABLEOP_ENABLED"] = "1"
+        os.environ["PYTORCH_TUNABLEOP_TUNING"] = "0"
+        os.environ["PYTORCH_TUNABLEOP_FILENAME"] = tfile
+
+    import torch
+    import torch.distributed as dist
+
+    from llm_fine_tune_distributed_amd.data.dataset import TokenizedDataset
+    from llm_fine_tune_distributed_amd.models import build_model, get_config
+    from llm_fine_tune_distributed_amd.parallel.process_group import barrier, setup_distributed
+    from llm_fine_tune_distributed_amd.train import SFTConfig, SFTTrainer
+
+    st = setup_distributed(verbose=False)
+    if st.world_size != a.gpus:
+        raise SystemExit(f"--gpus {a.gpus} but WORLD_SIZE={st.world_size}")
+    cfg = get_config(a.model)
+    model = build_model(cfg, device=st.device, dtype=torch.bfloat16, seed=0)
+    per_rank_samples = a.micro_batch * a.ga * (a.steps + a.warmup + 2)
+    ds = TokenizedDataset.synthetic(per_rank_samples * st.world_size, cfg.vocab_size, a.seq, a.seq, seed=1)
+    args = SFTConfig(output_dir="/tmp/sftamd_bench", per_device_train_batch_size=a.micro_batch,
+                     gradient_accumulation_steps=a.ga, learning_rate=5e-5 * st.world_size, max_grad_norm=1.0,
+                     bf16=True, gradient_checkpointing=False, max_length=a.seq, packing=a.packing,
+                     ddp_bucket_cap_mb=a.bucket_mb, dataloader_drop_last=True, jsonl_log=False, logging_steps=0)
+    trainer = SFTTrainer(model=model, args=args, train_dataset=ds)
+    loader = trainer.get_train_dataloader()
+    it = iter(loader)
+
+    def next_micro():
+        return [next(it) for _ in range(a.ga)]
+
+    def step():
+        return trainer.optimizer_step(next_micro(), lr=args.learning_rate)
+
+    for _ in range(a.warmup):
+        r = step()
+    torch.cuda.synchronize()
+    barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        r = step()
+    torch.cuda.synchronize()
+    barrier()
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    t = torch.tensor([dt], device=st.device, dtype=torch.float64)
+    if st.world_size > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    dt = t.item()
+    loss = r["acc"][0].item()
+    ms = dt / a.steps * 1e3
+    samples = a.micro_batch * a.ga * st.world_size * a.steps
+    value = samples / dt
+    tok_s = value * a.seq
+    mfu = tok_s * cfg.flops_per_token(a.seq) / (2.5e15 * st.world_size)
+    if st.is_main:
+        rec = {
+            "metric": "samples/sec SmolLM3-3B full SFT bf16 (DDP)",
+            "value": round(value, 3), "unit": "samples/s", "n_gpus": st.world_size, "steps": a.steps,
+            "warmup": a.warmup, "ms_per_step": round(ms, 3), "higher_is_better": True, "scaling": "weak",
+            "vs_baseline": None, "dtype": "bf16", "data": "synthetic (random tokens, random-init weights)",
+            "config": {"model": "SmolLM3-3B", "global_batch": a.micro_batch * a.ga * st.world_size,
+                       "per_device_batch": a.micro_batch, "gradient_accumulation_steps": a.ga, "seq_len": a.seq,
+                       "parallelism": f"dp{st.world_size}", "optimizer": "AdamW fp32-master (fused HIP)",
+                       "gradient_checkpointing": False, "packing": a.packing},
+            "tokens_per_sec": round(tok_s, 1), "mfu": round(mfu, 4), "final_loss": round(loss, 4),
+            "peak_mem_gb": round(torch.cuda.max_memory_allocated() / 1e9, 2),
+        }
+        print(json.dumps(rec), flush=True)
+    if a.profile_steps:
+        torch.cuda.synchronize()
+        for _ in range(a.profile_steps):
+            step()
+        torch.cuda.synchronize()
+    if st.world_size > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -117,13 +117,27 @@ __global__ __launch_bounds__(256) void rmsnorm_bwd_kernel(const u16* __restrict_
   for (int c = threadIdx.x; c < H; c += 256) dw_part[(long)blockIdx.x * H + c] = red[c];
 }
 
-// out[c] = sum_b part[b][c] in fixed order (deterministic)
-__global__ void col_sum_kernel(const float* __restrict__ part, float* __restrict__ out, int P, int H) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= H) return;
-  float s = 0.f;
-  for (int b = 0; b < P; ++b) s += part[(long)b * H + c];
-  out[c] = s;
+// out[c] = sum_b part[b][c] in a fixed order (deterministic). Block = 64 columns x 4 row
+// groups; each thread keeps 4 independent accumulators so the loads pipeline.
+__global__ __launch_bounds__(256) void col_sum_kernel(const float* __restrict__ part, float* __restrict__ out, int P,
+                                                      int H) {
+  __shared__ float red[4][64];
+  const int c = blockIdx.x * 64 + (threadIdx.x & 63);
+  const int rg = threadIdx.x >> 6;
+  float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
+  if (c < H) {
+    int b = rg;
+    for (; b + 12 < P; b += 16) {
+      a0 += part[(long)b * H + c];
+      a1 += part[(long)(b + 4) * H + c];
+      a2 += part[(long)(b + 8) * H + c];
+      a3 += part[(long)(b + 12) * H + c];
+    }
+    for (; b < P; b += 4) a0 += part[(long)b * H + c];
+  }
+  red[rg][threadIdx.x & 63] = (a0 + a1) + (a2 + a3);
+  __syncthreads();
+  if (rg == 0 && c < H) out[c] = (red[0][threadIdx.x] + red[1][threadIdx.x]) + (red[2][threadIdx.x] + red[3][threadIdx.x]);
 }
 
 #define NV_DISPATCH(H, ...)                      \
@@ -181,7 +195,7 @@ std::tuple<at::Tensor, at::Tensor> rmsnorm_bwd(const at::Tensor& dy, const at::T
     SFT_CHECK(dres->is_contiguous() && dres->scalar_type() == at::kBFloat16, "dres");
     dr = (const u16*)dres->data_ptr();
   }
-  int nblk = std::min((M + 3) / 4, 512);
+  int nblk = std::min((M + 3) / 4, 256);
   nblk = std::max(nblk, 1);
   auto part = at::empty({nblk, H}, h.options().dtype(at::kFloat));
   auto dw = at::empty({H}, h.options().dtype(at::kFloat));
@@ -189,7 +203,7 @@ std::tuple<at::Tensor, at::Tensor> rmsnorm_bwd(const at::Tensor& dy, const at::T
                      (const u16*)dy.data_ptr(), (const u16*)h.data_ptr(), (const u16*)weight.data_ptr(),
                      rstd.data_ptr<float>(), dr, (u16*)dx.data_ptr(), part.data_ptr<float>(), M, H));
   SFT_LAUNCH_CHECK();
-  col_sum_kernel<<<(H + 255) / 256, 256, 0, cur_stream()>>>(part.data_ptr<float>(), dw.data_ptr<float>(), nblk, H);
+  col_sum_kernel<<<(H + 63) / 64, 256, 0, cur_stream()>>>(part.data_ptr<float>(), dw.data_ptr<float>(), nblk, H);
   SFT_LAUNCH_CHECK();
   return {dx, dw};
 }

@@ -34,6 +34,7 @@ class CausalLMOutput:
     logits: Optional[torch.Tensor] = None
     stats: Optional[torch.Tensor] = None  # [4, M]: loss, lse, entropy, correct (per token)
     num_tokens: Optional[torch.Tensor] = None
+    metrics: Optional[torch.Tensor] = None
 
 
 class RMSNorm(nn.Module):
@@ -238,7 +239,10 @@ class CausalLM(nn.Module):
                 cnt = torch.tensor(float(num_items_in_batch))
             inv = (1.0 / cnt.to(device=dev, dtype=torch.float32)).reshape(1)
             out.loss, out.stats = ops.lm_head_cross_entropy(h, self.lm_head_weight, labels, inv)
-            out.num_tokens = valid.sum()
+            vf = valid.float()
+            out.num_tokens = vf.sum()
+            # TRL-style training metrics from the same fused CE pass: [correct, entropy_sum, valid]
+            out.metrics = torch.stack([out.stats[3].sum(), (out.stats[2] * vf).sum(), out.num_tokens])
         if return_logits or labels is None:
             out.logits = torch.nn.functional.linear(h, self.lm_head_weight)
         return out

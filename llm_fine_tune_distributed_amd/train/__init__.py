@@ -1,0 +1,8 @@
+from .config import SFTConfig, config_from_env
+from .callbacks import (TrainerCallback, TrainerControl, TrainerState, TrainingHistoryCallback, PerplexityCallback,
+                        AimCallback, JSONLLoggerCallback)
+from .trainer import SFTTrainer, TrainOutput, set_seed
+
+__all__ = ["SFTConfig", "config_from_env", "TrainerCallback", "TrainerControl", "TrainerState",
+           "TrainingHistoryCallback", "PerplexityCallback", "AimCallback", "JSONLLoggerCallback", "SFTTrainer",
+           "TrainOutput", "set_seed"]

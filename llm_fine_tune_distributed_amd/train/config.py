@@ -1,0 +1,170 @@
+"""``SFTConfig``: TRL/HF-compatible training configuration (reference T1, ``training.py:258-287``).
+
+Accepts the same keyword names the reference passes (including the legacy ``max_seq_length``
+alias of ``max_length`` and the ``ddp_*`` / ``dataloader_*`` knobs). Unknown HF fields are
+accepted and ignored with a warning so existing scripts keep working. Defaults follow the
+libraries the reference runs with (HF TrainingArguments / TRL SFTConfig), e.g. AdamW
+betas (0.9, 0.999), eps 1e-8, weight_decay 0, linear LR decay without warmup.
+
+MI355X-specific extras (all optional): ``freeze_policy``, ``lora_*``, ``master_weights``,
+``ddp_first_bucket_mb``, ``pad_to_multiple_of``, ``max_steps_per_epoch``...
+"""
+from __future__ import annotations
+
+import dataclasses
+import json
+import os
+import warnings
+from dataclasses import dataclass, field
+from typing import Any, Dict, List, Optional
+
+
+@dataclass
+class SFTConfig:
+    # ---- reference kwargs (training.py:258-287)
+    output_dir: str = "outputs/checkpoints"
+    per_device_train_batch_size: int = 8
+    per_device_eval_batch_size: int = 8
+    gradient_accumulation_steps: int = 1
+    learning_rate: float = 2e-5
+    max_grad_norm: float = 1.0
+    num_train_epochs: float = 3.0
+    max_steps: int = -1
+    logging_steps: float = 500
+    logging_first_step: bool = False
+    save_steps: float = 500
+    bf16: bool = True
+    fp16: bool = False
+    eval_strategy: str = "no"
+    eval_steps: Optional[float] = None
+    save_strategy: str = "steps"
+    load_best_model_at_end: bool = False
+    metric_for_best_model: Optional[str] = None
+    greater_is_better: Optional[bool] = None
+    save_total_limit: Optional[int] = None
+    dataloader_pin_memory: bool = True
+    dataloader_num_workers: int = 0
+    remove_unused_columns: bool = True
+    gradient_checkpointing: bool = False
+    dataloader_drop_last: bool = False
+    max_length: Optional[int] = 1024
+    packing: bool = False
+    ddp_backend: Optional[str] = None
+    ddp_find_unused_parameters: Optional[bool] = None
+    ddp_bucket_cap_mb: Optional[float] = None
+    ddp_timeout: int = 1800
+    local_rank: int = -1
+    # ---- optimizer / schedule (HF defaults)
+    optim: str = "adamw_torch_fused"
+    adam_beta1: float = 0.9
+    adam_beta2: float = 0.999
+    adam_epsilon: float = 1e-8
+    weight_decay: float = 0.0
+    lr_scheduler_type: str = "linear"
+    lr_scheduler_kwargs: Dict[str, Any] = field(default_factory=dict)
+    warmup_steps: int = 0
+    warmup_ratio: float = 0.0
+    seed: int = 42
+    data_seed: Optional[int] = None
+    report_to: Any = "none"
+    run_name: Optional[str] = None
+    resume_from_checkpoint: Optional[str] = None
+    # ---- TRL SFT
+    dataset_text_field: str = "text"
+    completion_only_loss: Optional[bool] = None
+    assistant_only_loss: bool = False
+    average_tokens_across_devices: bool = True
+    # ---- MI355X-native extras
+    freeze_policy: str = "full"             # full | last_n_layers | lora
+    freeze_last_n_layers: int = 2
+    lora_r: int = 16
+    lora_alpha: float = 8.0
+    lora_dropout: float = 0.05
+    lora_target_modules: Optional[List[str]] = None
+    master_weights: bool = True             # fp32 master copy + fp32 Adam moments
+    ddp_first_bucket_mb: float = 4.0
+    ddp_broadcast_params: bool = False      # weights are identical by construction (seeded / loaded)
+    ddp_check_sync_every: int = 0           # cross-rank param checksum every N steps (0 = off)
+    pad_to_multiple_of: Optional[int] = None
+    max_train_samples: Optional[int] = None
+    max_eval_samples: Optional[int] = None
+    eval_accumulation: bool = True
+    jsonl_log: bool = True
+    prefetch_batches: int = 2
+
+    def __post_init__(self):
+        pass
+
+    # legacy alias used by the reference (training.py:282)
+    @property
+    def max_seq_length(self) -> Optional[int]:
+        return self.max_length
+
+    @classmethod
+    def create(cls, **kw) -> "SFTConfig":
+        names = {f.name for f in dataclasses.fields(cls)}
+        known, unknown = {}, {}
+        for k, v in kw.items():
+            if k == "max_seq_length":
+                known["max_length"] = v
+            elif k == "evaluation_strategy":
+                known["eval_strategy"] = v
+            elif k in names:
+                known[k] = v
+            else:
+                unknown[k] = v
+        if unknown:
+            warnings.warn(f"SFTConfig: ignoring unsupported fields {sorted(unknown)}")
+        return cls(**known)
+
+    def resolved_eval_steps(self) -> Optional[int]:
+        if self.eval_strategy in ("no", None):
+            return None
+        if self.eval_strategy == "epoch":
+            return -1
+        v = self.eval_steps if self.eval_steps is not None else self.logging_steps
+        return int(v) if v else None
+
+    def to_dict(self) -> Dict[str, Any]:
+        return dataclasses.asdict(self)
+
+    def to_json(self, path: str):
+        with open(path, "w") as f:
+            json.dump(self.to_dict(), f, indent=2, default=str)
+
+
+# SFTConfig(**kwargs) must accept legacy/unknown names like TRL does
+_orig_init = SFTConfig.__init__
+
+
+def _init(self, *args, **kw):
+    names = {f.name for f in dataclasses.fields(SFTConfig)}
+    if "max_seq_length" in kw:
+        kw["max_length"] = kw.pop("max_seq_length")
+    if "evaluation_strategy" in kw:
+        kw["eval_strategy"] = kw.pop("evaluation_strategy")
+    unknown = {k: kw.pop(k) for k in list(kw) if k not in names}
+    if unknown:
+        warnings.warn(f"SFTConfig: ignoring unsupported fields {sorted(unknown)}")
+    _orig_init(self, *args, **kw)
+
+
+SFTConfig.__init__ = _init
+
+
+def config_from_env(base: Optional[SFTConfig] = None, world_size: int = 1) -> Dict[str, Any]:
+    """The reference's env contract (training.py:56-60,240): EPOCHS, BATCH_SIZE, LEARNING_RATE,
+    DATA_DIR, OUTPUT_DIR, AIM_REPO. Returns the resolved values (LR scaled by world size like
+    training.py:263)."""
+    epochs = int(os.getenv("EPOCHS", "4"))
+    batch = int(os.getenv("BATCH_SIZE", "8"))
+    lr = float(os.getenv("LEARNING_RATE", "5e-5"))
+    return {
+        "epochs": epochs,
+        "batch_size": batch,
+        "learning_rate": lr,
+        "scaled_learning_rate": lr * world_size if world_size > 1 else lr,
+        "data_dir": os.getenv("DATA_DIR", "/tmp/data"),
+        "output_dir": os.getenv("OUTPUT_DIR", "/tmp/models"),
+        "aim_repo": os.getenv("AIM_REPO", "/aim"),
+    }

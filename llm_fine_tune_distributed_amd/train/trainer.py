@@ -1,0 +1,397 @@
+"""``SFTTrainer``: the TRL/HF-style supervised fine-tuning loop on the MI355X-native engine.
+
+Reference surface (``training.py:289-312``): ``SFTTrainer(model, args, train_dataset,
+eval_dataset, callbacks).train()`` -> ``TrainOutput``; ``.save_model(dir)``. The loop
+reproduces the HF ``Trainer._inner_training_loop`` semantics the reference depends on
+(SURVEY.md §3.2, T6):
+
+* gradient accumulation over ``gradient_accumulation_steps`` micro-batches, gradient
+  synchronisation only on the last one (``DDPEngine.no_sync``);
+* loss normalisation by the GLOBAL number of non-ignored label tokens of the optimizer step
+  (``num_items_in_batch`` summed over GA micro-batches and ranks): every micro-batch's loss is
+  ``sum_token_CE / N_global`` and bucket all-reduces SUM, which equals HF's
+  ``loss * world_size`` + averaging DDP;
+* clip to ``max_grad_norm`` then AdamW then LR schedule step; logs ``loss, grad_norm,
+  learning_rate, epoch`` (+ TRL's ``mean_token_accuracy, entropy, num_tokens``) every
+  ``logging_steps``; eval every ``eval_steps`` with best-``eval_loss`` tracking; checkpoints
+  every ``save_steps`` with rotation and ``resume_from_checkpoint``;
+* end-of-train metrics ``train_runtime, train_samples_per_second, train_steps_per_second,
+  total_flos, train_loss`` (HF definitions: wall time includes eval) plus pure-training
+  samples/s, tokens/s and MFU.
+"""
+from __future__ import annotations
+
+import contextlib
+import math
+import os
+import random
+import time
+from typing import Any, Dict, List, NamedTuple, Optional, Sequence
+
+import numpy as np
+import torch
+
+from ..data.collator import DataLoader, DistributedBatchSampler, SFTCollator
+from ..data.dataset import TokenizedDataset, tokenize_rows
+from ..models import CausalLM, apply_freeze_policy, build_model, get_config
+from ..models.lora import LoRAConfig
+from ..parallel.ddp import DDPEngine
+from ..parallel.process_group import all_reduce_sum_, barrier, setup_distributed
+from . import checkpoint as ckpt
+from .callbacks import (AimCallback, CallbackHandler, JSONLLoggerCallback, PrinterCallback, TrainerCallback,
+                        TrainerControl, TrainerState)
+from .config import SFTConfig
+from .optim import FlatAdamW, LRScheduler, get_schedule
+
+PEAK_BF16_FLOPS = 2.5e15  # MI355X dense bf16 (vendor figure; AMD's 5 PF headline includes 2:1 sparsity)
+
+
+class TrainOutput(NamedTuple):
+    global_step: int
+    training_loss: float
+    metrics: Dict[str, float]
+
+
+def set_seed(seed: int):
+    random.seed(seed)
+    np.random.seed(seed)
+    torch.manual_seed(seed)
+    if torch.cuda.is_available():
+        torch.cuda.manual_seed_all(seed)
+
+
+class SFTTrainer:
+    def __init__(self, model=None, args: Optional[SFTConfig] = None, train_dataset=None, eval_dataset=None,
+                 processing_class=None, tokenizer=None, callbacks: Optional[Sequence[TrainerCallback]] = None,
+                 data_collator: Optional[SFTCollator] = None, peft_config: Optional[LoRAConfig] = None,
+                 model_init_seed: int = 0):
+        self.args = args = args or SFTConfig()
+        self.dist = setup_distributed(timeout_s=args.ddp_timeout, verbose=False)
+        set_seed(args.seed)
+        dev = self.dist.device
+        # ------------------------------------------------------------ model
+        if isinstance(model, str):
+            if os.path.isdir(model) and any(f.endswith(".safetensors") for f in os.listdir(model)):
+                model = ckpt.from_pretrained(model, device=dev, dtype=torch.bfloat16)
+            else:
+                model = build_model(get_config(model), device=dev, dtype=torch.bfloat16, seed=model_init_seed)
+        assert isinstance(model, CausalLM), "SFTTrainer expects a CausalLM (or a preset name / HF dir)"
+        if next(model.parameters()).device != dev:
+            model.to(dev)
+            model.inv_freq = model.inv_freq.to(dev)
+        self.model = model
+        if peft_config is not None or args.freeze_policy != "full":
+            lc = peft_config or LoRAConfig(r=args.lora_r, lora_alpha=args.lora_alpha, lora_dropout=args.lora_dropout,
+                                           **({"target_modules": args.lora_target_modules} if args.lora_target_modules else {}))
+            policy = "lora" if peft_config is not None else args.freeze_policy
+            apply_freeze_policy(model, policy, n_last=args.freeze_last_n_layers, lora_config=lc)
+        if args.gradient_checkpointing:
+            model.gradient_checkpointing_enable()
+        self.trainable_params = model.num_parameters(trainable_only=True)
+        self.total_params = model.num_parameters()
+        # ------------------------------------------------------------ data
+        self.tokenizer = processing_class or tokenizer
+        if self.tokenizer is None and (self._needs_tokenizer(train_dataset) or self._needs_tokenizer(eval_dataset)):
+            from ..data.tokenizer import load_tokenizer
+            self.tokenizer = load_tokenizer()
+        self.train_dataset = self._prepare(train_dataset, args.max_train_samples)
+        self.eval_dataset = self._prepare(eval_dataset, args.max_eval_samples)
+        pad_id = self.tokenizer.pad_token_id if self.tokenizer is not None else (model.config.pad_token_id or 0)
+        self.collator = data_collator or SFTCollator(pad_id, args.pad_to_multiple_of, args.max_length, args.packing,
+                                                     args.per_device_train_batch_size * (args.max_length or 1024)
+                                                     if args.packing else None)
+        # ------------------------------------------------------------ engine + optimizer
+        self.engine = DDPEngine(model, self.dist.world_size, self.dist.rank,
+                                bucket_cap_mb=args.ddp_bucket_cap_mb or 25.0,
+                                first_bucket_mb=args.ddp_first_bucket_mb,
+                                broadcast_params=args.ddp_broadcast_params)
+        self.optimizer = FlatAdamW(self.engine, lr=args.learning_rate, betas=(args.adam_beta1, args.adam_beta2),
+                                   eps=args.adam_epsilon, weight_decay=args.weight_decay,
+                                   master_weights=args.master_weights)
+        self.scheduler: Optional[LRScheduler] = None
+        # ------------------------------------------------------------ callbacks / state
+        self.state = TrainerState(is_world_process_zero=self.dist.is_main)
+        self.control = TrainerControl()
+        cbs = list(callbacks or [])
+        if args.jsonl_log and self.dist.is_main:
+            cbs.append(JSONLLoggerCallback(os.path.join(args.output_dir, "metrics.jsonl")))
+        cbs.append(PrinterCallback())
+        self.callback_handler = CallbackHandler(cbs)
+        self._timers: Dict[str, float] = {"eval": 0.0}
+
+    # ------------------------------------------------------------------ data helpers
+    @staticmethod
+    def _needs_tokenizer(ds) -> bool:
+        return ds is not None and not isinstance(ds, TokenizedDataset)
+
+    def _prepare(self, ds, limit):
+        if ds is None:
+            return None
+        if isinstance(ds, TokenizedDataset):
+            return ds
+        rows = list(ds) if not isinstance(ds, list) else ds
+        if limit:
+            rows = rows[:limit]
+        return tokenize_rows(rows, self.tokenizer, self.args.max_length, self.args.assistant_only_loss,
+                             self.args.dataset_text_field)
+
+    def get_train_dataloader(self) -> DataLoader:
+        a = self.args
+        s = DistributedBatchSampler(len(self.train_dataset), a.per_device_train_batch_size, self.dist.world_size,
+                                    self.dist.rank, shuffle=True, seed=a.data_seed or a.seed,
+                                    drop_last=a.dataloader_drop_last)
+        return DataLoader(self.train_dataset, self.collator, s, self.dist.device, a.dataloader_pin_memory,
+                          a.prefetch_batches)
+
+    def get_eval_dataloader(self) -> DataLoader:
+        a = self.args
+        s = DistributedBatchSampler(len(self.eval_dataset), a.per_device_eval_batch_size, self.dist.world_size,
+                                    self.dist.rank, shuffle=False, drop_last=a.dataloader_drop_last)
+        return DataLoader(self.eval_dataset, self.collator, s, self.dist.device, a.dataloader_pin_memory,
+                          a.prefetch_batches)
+
+    # ------------------------------------------------------------------ core step
+    @staticmethod
+    def _model_inputs(b: Dict) -> Dict:
+        kw = {"input_ids": b["input_ids"], "labels": b["labels"]}
+        if "cu_seqlens" in b:
+            kw.update(cu_seqlens=b["cu_seqlens"], position_ids=b["position_ids"], max_seqlen=b["max_seqlen"],
+                      shift_labels=not b.get("shifted", False))
+        return kw
+
+    def global_num_items(self, micro: List[Dict]) -> torch.Tensor:
+        n = torch.tensor([float(sum(b["num_items"] for b in micro))], device=self.dist.device)
+        if self.args.average_tokens_across_devices:
+            all_reduce_sum_(n)
+        return n.clamp(min=1.0)
+
+    def optimizer_step(self, micro: List[Dict], lr: float) -> Dict[str, torch.Tensor]:
+        """One optimizer step over ``micro`` (GA micro-batches). Returns device-side sums:
+        loss (this rank's share of the global mean), correct, entropy_sum, valid tokens."""
+        model, eng = self.model, self.engine
+        model.train()
+        n_items = self.global_num_items(micro)
+        acc = torch.zeros(4, device=self.dist.device)  # loss, correct, entropy_sum, valid
+        for i, b in enumerate(micro):
+            sync = i == len(micro) - 1
+            ctx = contextlib.nullcontext() if sync else eng.no_sync()
+            with ctx:
+                eng.prepare_backward()
+                out = model(**self._model_inputs(b), num_items_in_batch=n_items)
+                out.loss.backward()
+            acc[0] += out.loss.detach()
+            acc[1:] += out.metrics
+        eng.finish_backward()
+        norm = self.optimizer.step(lr=lr, max_grad_norm=self.args.max_grad_norm)
+        eng.zero_grad()
+        return {"acc": acc, "grad_norm": norm}
+
+    # ------------------------------------------------------------------ evaluation
+    @torch.no_grad()
+    def evaluate(self, eval_dataset=None, metric_key_prefix: str = "eval") -> Dict[str, float]:
+        if eval_dataset is not None:
+            self.eval_dataset = self._prepare(eval_dataset, self.args.max_eval_samples)
+        if self.eval_dataset is None:
+            return {}
+        t0 = time.time()
+        self.model.eval()
+        acc = torch.zeros(5, device=self.dist.device)  # loss_sum, correct, entropy_sum, valid, samples
+        loader = self.get_eval_dataloader()
+        for b in loader:
+            out = self.model(**self._model_inputs(b), num_items_in_batch=1.0)
+            acc[0] += out.loss
+            acc[1:4] += out.metrics
+            acc[4] += b["num_samples"]
+        all_reduce_sum_(acc)
+        vals = acc.tolist()
+        self.model.train()
+        rt = time.time() - t0
+        valid = max(vals[3], 1.0)
+        nb = len(loader) * self.dist.world_size
+        m = {f"{metric_key_prefix}_loss": vals[0] / valid, f"{metric_key_prefix}_runtime": rt,
+             f"{metric_key_prefix}_samples_per_second": vals[4] / max(rt, 1e-9),
+             f"{metric_key_prefix}_steps_per_second": nb / max(rt, 1e-9),
+             f"{metric_key_prefix}_mean_token_accuracy": vals[1] / valid,
+             f"{metric_key_prefix}_entropy": vals[2] / valid, f"{metric_key_prefix}_num_tokens": vals[3],
+             "epoch": self.state.epoch}
+        self._timers["eval"] += rt
+        self.callback_handler.call("on_evaluate", self.args, self.state, self.control, metrics=m)
+        self.log(m)
+        return m
+
+    # ------------------------------------------------------------------ logging / saving
+    def log(self, logs: Dict[str, Any]):
+        logs = dict(logs)
+        logs.setdefault("step", self.state.global_step)
+        self.state.log_history.append(dict(logs))
+        self.control = self.callback_handler.call("on_log", self.args, self.state, self.control, logs=logs)
+
+    def _save_checkpoint(self):
+        a = self.args
+        path = os.path.join(a.output_dir, f"checkpoint-{self.state.global_step}")
+        barrier()
+        ckpt.save_rng(path, self.dist.rank)
+        ckpt.save_checkpoint(path, self.model, self.optimizer, self.scheduler, self.state, a, self.dist.rank,
+                             tokenizer=self.tokenizer)
+        barrier()
+        if self.dist.is_main:
+            ckpt.rotate_checkpoints(a.output_dir, a.save_total_limit, self.state.best_model_checkpoint)
+        barrier()
+        self.callback_handler.call("on_save", a, self.state, self.control)
+        return path
+
+    def save_model(self, output_dir: Optional[str] = None):
+        output_dir = output_dir or self.args.output_dir
+        if self.dist.is_main:
+            ckpt.save_pretrained(self.model, output_dir, tokenizer=self.tokenizer)
+        barrier()
+
+    def _update_best(self, metrics: Dict[str, float], ckpt_path: Optional[str]):
+        key = self.args.metric_for_best_model or "eval_loss"
+        if not key.startswith("eval_"):
+            key = "eval_" + key
+        if key not in metrics:
+            return
+        v = metrics[key]
+        gib = self.args.greater_is_better
+        if gib is None:
+            gib = not key.endswith("loss")
+        b = self.state.best_metric
+        if b is None or (v > b if gib else v < b):
+            self.state.best_metric = v
+            if ckpt_path:
+                self.state.best_model_checkpoint = ckpt_path
+
+    # ------------------------------------------------------------------ train
+    def train(self, resume_from_checkpoint: Optional[str] = None) -> TrainOutput:
+        a = self.args
+        loader = self.get_train_dataloader()
+        ga = max(1, a.gradient_accumulation_steps)
+        nb = len(loader)
+        steps_per_epoch = max(1, nb // ga + int(nb % ga > 0))
+        max_steps = a.max_steps if a.max_steps and a.max_steps > 0 else math.ceil(a.num_train_epochs * steps_per_epoch)
+        warm = a.warmup_steps or int(math.ceil(a.warmup_ratio * max_steps))
+        self.scheduler = LRScheduler(self.optimizer, get_schedule(a.lr_scheduler_type, max_steps, warm,
+                                                                  **a.lr_scheduler_kwargs))
+        self.state.max_steps = max_steps
+        self.state.num_train_epochs = math.ceil(max_steps / steps_per_epoch)
+        self.state.train_batch_size = a.per_device_train_batch_size
+        start_epoch, skip_batches = 0, 0
+        resume = resume_from_checkpoint or a.resume_from_checkpoint
+        if resume:
+            if resume is True or resume == "auto":
+                resume = ckpt.latest_checkpoint(a.output_dir)
+            if resume:
+                st, _ = ckpt.load_checkpoint(resume, self.model, self.optimizer, self.scheduler, self.dist.rank)
+                st.is_world_process_zero = self.dist.is_main
+                self.state = st
+                start_epoch = self.state.global_step // steps_per_epoch
+                skip_batches = (self.state.global_step % steps_per_epoch) * ga
+                if self.dist.is_main:
+                    print(f"[trainer] resumed from {resume} at step {self.state.global_step}", flush=True)
+        if self.dist.is_main:
+            print(f"[trainer] world={self.dist.world_size} device={self.dist.device} trainable="
+                  f"{self.trainable_params:,}/{self.total_params:,} "
+                  f"({100.0 * self.trainable_params / max(1, self.total_params):.2f}%) steps={max_steps} "
+                  f"ga={ga} micro={a.per_device_train_batch_size}", flush=True)
+        self.control = self.callback_handler.call("on_train_begin", a, self.state, self.control)
+        eval_every = a.resolved_eval_steps()
+        log_every = max(1, int(a.logging_steps)) if a.logging_steps else 0
+        save_every = int(a.save_steps) if a.save_strategy == "steps" and a.save_steps else 0
+        cfg = self.model.config
+        run_acc = torch.zeros(4, device=self.dist.device)
+        steps_since_log = 0
+        total_loss = torch.zeros(1, device=self.dist.device)
+        samples = tokens = 0
+        flops = 0.0
+        t_start = time.time()
+        self._timers["eval"] = 0.0
+        last_norm = None
+        done = self.state.global_step >= max_steps
+        for epoch in range(start_epoch, self.state.num_train_epochs):
+            if done:
+                break
+            loader.set_epoch(epoch)
+            self.control = self.callback_handler.call("on_epoch_begin", a, self.state, self.control)
+            it = loader.iter(skip=skip_batches if epoch == start_epoch else 0)
+            step_in_epoch = (skip_batches // ga) if epoch == start_epoch else 0
+            while True:
+                micro = []
+                for _ in range(ga):
+                    try:
+                        micro.append(next(it))
+                    except StopIteration:
+                        break
+                if not micro:
+                    break
+                self.control = self.callback_handler.call("on_step_begin", a, self.state, self.control)
+                lr = self.scheduler.get_lr()
+                r = self.optimizer_step(micro, lr)
+                self.scheduler.step()
+                run_acc += r["acc"]
+                total_loss += r["acc"][0]
+                last_norm = r["grad_norm"]
+                steps_since_log += 1
+                n_s = sum(b["num_samples"] for b in micro)
+                n_t = sum(b["num_tokens"] for b in micro)
+                samples += n_s * self.dist.world_size
+                tokens += n_t * self.dist.world_size
+                T = max(b["input_ids"].shape[-1] for b in micro)
+                flops += cfg.flops_per_token(T, training=True, recompute=a.gradient_checkpointing) * n_t * \
+                    self.dist.world_size
+                self.state.global_step += 1
+                step_in_epoch += 1
+                self.state.epoch = epoch + step_in_epoch / steps_per_epoch
+                self.state.samples_seen += n_s * self.dist.world_size
+                self.state.tokens_seen += n_t * self.dist.world_size
+                self.state.total_flos += 6.0 * self.trainable_params * n_t * self.dist.world_size
+                self.control = self.callback_handler.call("on_step_end", a, self.state, self.control)
+                gs = self.state.global_step
+                if log_every and (gs % log_every == 0 or (gs == 1 and a.logging_first_step)):
+                    red = run_acc.clone()
+                    all_reduce_sum_(red)
+                    v = red.tolist()
+                    valid = max(v[3], 1.0)
+                    self.log({"loss": v[0] / steps_since_log, "grad_norm": float(last_norm),
+                              "learning_rate": self.scheduler.get_lr(), "epoch": round(self.state.epoch, 4),
+                              "mean_token_accuracy": v[1] / valid, "entropy": v[2] / valid,
+                              "num_tokens": float(self.state.tokens_seen)})
+                    run_acc.zero_()
+                    steps_since_log = 0
+                if a.ddp_check_sync_every and gs % a.ddp_check_sync_every == 0:
+                    self.engine.assert_in_sync()
+                metrics = None
+                if eval_every and eval_every > 0 and gs % eval_every == 0 and self.eval_dataset is not None:
+                    metrics = self.evaluate()
+                ck = None
+                if save_every and gs % save_every == 0:
+                    ck = self._save_checkpoint()
+                if metrics:
+                    self._update_best(metrics, ck)
+                if gs >= max_steps or self.control.should_training_stop:
+                    done = True
+                    break
+            if eval_every == -1 and self.eval_dataset is not None:
+                m = self.evaluate()
+                self._update_best(m, None)
+            self.control = self.callback_handler.call("on_epoch_end", a, self.state, self.control)
+        if torch.cuda.is_available():
+            torch.cuda.synchronize()
+        runtime = time.time() - t_start
+        tl = total_loss.clone()
+        all_reduce_sum_(tl)
+        train_loss = tl.item() / max(1, self.state.global_step - (0 if not resume else 0))
+        pure = max(runtime - self._timers["eval"], 1e-9)
+        metrics = {"train_runtime": runtime, "train_samples_per_second": samples / max(runtime, 1e-9),
+                   "train_steps_per_second": self.state.global_step / max(runtime, 1e-9),
+                   "total_flos": self.state.total_flos, "train_loss": train_loss, "epoch": self.state.epoch,
+                   "train_pure_samples_per_second": samples / pure, "train_tokens_per_second": tokens / pure,
+                   "train_mfu": flops / pure / (PEAK_BF16_FLOPS * self.dist.world_size)
+                   if self.dist.device.type == "cuda" else 0.0}
+        if a.load_best_model_at_end and self.state.best_model_checkpoint:
+            sd = ckpt.load_state_dict(self.state.best_model_checkpoint, device="cpu")
+            with torch.no_grad():
+                self.model.load_hf_state_dict({k: v.to(torch.bfloat16) for k, v in sd.items()}, strict=False)
+        self.log(metrics)
+        self.control = self.callback_handler.call("on_train_end", a, self.state, self.control)
+        return TrainOutput(self.state.global_step, train_loss, metrics)

@@ -1,0 +1,97 @@
+"""Data pipeline: split parity with HF datasets, native collator vs Python, sampler sharding."""
+import torch
+
+from llm_fine_tune_distributed_amd.data import collator as C
+from llm_fine_tune_distributed_amd.data.dataset import TokenizedDataset, train_test_split, tokenize_rows
+from llm_fine_tune_distributed_amd.data.prompts import format_prompt, WILDERNESS_EXPERT_SYSTEM_PROMPT
+from llm_fine_tune_distributed_amd.data.synthetic import generate_qa, write_parquet
+from llm_fine_tune_distributed_amd.data.tokenizer import load_tokenizer
+from llm_fine_tune_distributed_amd.ops import _ext
+
+
+def test_split_matches_hf_datasets():
+    import datasets
+    rows = [{"full-question": f"q{i}", "answer": f"a{i}"} for i in range(2845)]
+    tr, te = train_test_split(rows, test_size=0.1, seed=42)
+    assert (len(tr), len(te)) == (2560, 285)  # reference sizes (README.md:125)
+    hf = datasets.Dataset.from_list(rows).train_test_split(test_size=0.1, seed=42)
+    assert [r["full-question"] for r in tr] == hf["train"]["full-question"]
+    assert [r["full-question"] for r in te] == hf["test"]["full-question"]
+
+
+def test_format_prompt_schema():
+    m = format_prompt({"full-question": "For X, why?", "answer": "because"})["messages"]
+    assert [x["role"] for x in m] == ["system", "user", "assistant"]
+    assert m[0]["content"] == WILDERNESS_EXPERT_SYSTEM_PROMPT
+
+
+def test_synthetic_qa_schema(tmp_path):
+    rows = generate_qa(300, seed=1)
+    assert all(r["full-question"].startswith("For ") for r in rows)
+    assert max(len(r["answer"]) for r in rows) <= 406
+    p = tmp_path / "qa.parquet"
+    write_parquet(rows, str(p))
+    from llm_fine_tune_distributed_amd.data.dataset import load_qa_parquet
+    back = load_qa_parquet(str(p))
+    assert back[0] == {"full-question": rows[0]["full-question"], "answer": rows[0]["answer"]}
+
+
+def test_tokenizer_roundtrip_and_chat():
+    tk = load_tokenizer()
+    msgs = format_prompt({"full-question": "For Essential Knots and Uses, how do I tie a bowline?",
+                          "answer": "Form a loop."})["messages"]
+    txt = tk.apply_chat_template(msgs, tokenize=False)
+    assert "<|im_start|>assistant" in txt and txt.endswith("<|im_end|>\n")
+    ids = tk.apply_chat_template(msgs)
+    assert tk.decode(ids) == txt
+    assert tk.pad_token_id == tk.eos_token_id  # reference: pad = eos
+
+
+def _ds():
+    return TokenizedDataset.synthetic(20, 1000, 3, 17, seed=0)
+
+
+def test_native_collator_matches_python():
+    assert _ext.load()
+    ds = _ds()
+    idx = torch.tensor([3, 1, 7, 19])
+    a = _ext.ops().pad_batch(ds.tokens, ds.offsets, idx, 5, 8, 0)
+    b = C._pad_py(ds, idx, 5, 8, 0)
+    for x, y in zip(a, b):
+        assert torch.equal(x, y)
+    a = _ext.ops().pack_sequences(ds.tokens, ds.offsets, idx, 30, 5, 8)
+    b = C._pack_py(ds, idx, 30, 5, 8)
+    for x, y in zip(a, b):
+        assert torch.equal(x, y)
+
+
+def test_collator_num_items():
+    ds = _ds()
+    col = C.SFTCollator(pad_token_id=0)
+    b = col(ds, torch.tensor([0, 1]))
+    lens = ds.lengths()[:2]
+    assert b["num_items"] == int((lens - 1).sum())  # HF: shifted labels != -100
+    col = C.SFTCollator(pad_token_id=0, packing=True)
+    p = col(ds, torch.tensor([0, 1]))
+    assert p["num_items"] == b["num_items"]
+
+
+def test_sampler_shards_like_accelerate():
+    s = [C.DistributedBatchSampler(40, 4, 2, r, shuffle=True, seed=42) for r in range(2)]
+    one = C.DistributedBatchSampler(40, 4, 1, 0, shuffle=True, seed=42)
+    base = list(one)
+    r0, r1 = list(s[0]), list(s[1])
+    assert len(r0) == len(r1) == 5
+    for i in range(5):
+        assert torch.equal(r0[i], base[2 * i]) and torch.equal(r1[i], base[2 * i + 1])
+    s[0].set_epoch(1)
+    assert not torch.equal(list(s[0])[0], r0[0])
+
+
+def test_assistant_only_loss_masks_prompt():
+    tk = load_tokenizer()
+    rows = generate_qa(4, seed=3)
+    ds = tokenize_rows(rows, tk, 1024, assistant_only_loss=True)
+    b = C.SFTCollator(tk.pad_token_id)(ds, torch.tensor([0]))
+    st = int(ds.loss_start[0])
+    assert (b["labels"][0, :st] == -100).all() and (b["labels"][0, st:int(ds.lengths()[0])] != -100).all()

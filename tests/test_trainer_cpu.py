@@ -1,0 +1,128 @@
+"""Trainer semantics on CPU: BASELINE config #1 (8 synthetic Q&A pairs, 1 optimizer step),
+artifacts, checkpoint/resume, LoRA, LR schedules, callbacks."""
+import json
+import math
+import os
+
+import pytest
+import torch
+
+from llm_fine_tune_distributed_amd.data.synthetic import generate_qa
+from llm_fine_tune_distributed_amd.data.tokenizer import load_tokenizer
+from llm_fine_tune_distributed_amd.models import build_model, tiny
+from llm_fine_tune_distributed_amd.train import (PerplexityCallback, SFTConfig, SFTTrainer, TrainingHistoryCallback)
+from llm_fine_tune_distributed_amd.train import checkpoint as ckpt
+from llm_fine_tune_distributed_amd.train.optim import get_schedule
+
+
+@pytest.fixture(scope="module")
+def tk():
+    return load_tokenizer()
+
+
+def _model(seed=0):
+    return build_model(tiny(vocab_size=1024), dtype=torch.float32, seed=seed)
+
+
+def test_baseline_config1_one_step(tmp_path, tk):
+    """8 synthetic Q&A pairs, 1 optimizer step, reference SFTConfig kwargs verbatim (training.py:258-287)."""
+    rows = generate_qa(8, seed=0)
+    args = SFTConfig(output_dir=str(tmp_path / "checkpoints"), per_device_train_batch_size=8,
+                     per_device_eval_batch_size=8, gradient_accumulation_steps=1, learning_rate=5e-5,
+                     max_grad_norm=1.0, num_train_epochs=1, logging_steps=2, logging_first_step=True, save_steps=500,
+                     bf16=True, eval_strategy="steps", eval_steps=10, save_strategy="steps",
+                     load_best_model_at_end=True, metric_for_best_model="eval_loss", greater_is_better=False,
+                     save_total_limit=3, dataloader_pin_memory=True, dataloader_num_workers=0,
+                     remove_unused_columns=False, gradient_checkpointing=True, dataloader_drop_last=True,
+                     max_seq_length=1024, packing=False, ddp_backend=None)
+    h = TrainingHistoryCallback()
+    t = SFTTrainer(model=_model(), args=args, train_dataset=rows, eval_dataset=rows[:4], processing_class=tk,
+                   callbacks=[h, PerplexityCallback()])
+    before = t.engine.param_flat.clone()
+    out = t.train()
+    assert out.global_step == 1
+    assert not torch.equal(before, t.engine.param_flat)
+    first = h.history[0]
+    assert {"loss", "grad_norm", "learning_rate", "epoch", "perplexity"} <= set(first)
+    assert math.isclose(first["perplexity"], math.exp(first["loss"]), rel_tol=1e-6)
+    assert {"train_runtime", "train_samples_per_second", "train_loss"} <= set(h.history[-1])
+
+
+def test_save_model_hf_layout_roundtrip(tmp_path, tk):
+    m = _model()
+    t = SFTTrainer(model=m, args=SFTConfig(output_dir=str(tmp_path), jsonl_log=False), train_dataset=generate_qa(4),
+                   processing_class=tk)
+    t.save_model(str(tmp_path / "best_model"))
+    files = set(os.listdir(tmp_path / "best_model"))
+    assert {"model.safetensors", "config.json", "generation_config.json", "tokenizer.json"} <= files
+    from safetensors.torch import load_file
+    sd = load_file(str(tmp_path / "best_model" / "model.safetensors"))
+    assert "lm_head.weight" not in sd and "model.layers.0.self_attn.q_proj.weight" in sd  # tied, HF names
+    m2 = ckpt.from_pretrained(str(tmp_path / "best_model"), dtype=torch.float32)
+    for (n, a), (_, b) in zip(m.named_parameters(), m2.named_parameters()):
+        assert torch.equal(a, b), n
+
+
+def test_sharded_save(tmp_path):
+    m = _model()
+    ckpt.save_state_dict_sharded(m.hf_state_dict(), str(tmp_path), max_shard_size=200_000)
+    assert os.path.exists(tmp_path / "model.safetensors.index.json")
+    sd = ckpt.load_state_dict(str(tmp_path))
+    assert set(sd) == set(m.hf_state_dict())
+
+
+def test_checkpoint_resume_continuity(tmp_path, tk):
+    """Train 4 steps straight vs 2 steps + resume 2 steps: identical weights."""
+    rows = generate_qa(32, seed=5)
+
+    def mk(out, max_steps, save_steps):
+        a = SFTConfig(output_dir=str(out), per_device_train_batch_size=4, gradient_accumulation_steps=1,
+                      learning_rate=1e-3, max_steps=max_steps, logging_steps=1, save_steps=save_steps,
+                      dataloader_drop_last=True, jsonl_log=False, lr_scheduler_type="cosine", warmup_steps=1)
+        return SFTTrainer(model=_model(1), args=a, train_dataset=rows, processing_class=tk)
+
+    t_full = mk(tmp_path / "a", 4, 0)
+    t_full.train()
+    t1 = mk(tmp_path / "b", 4, 2)
+    t1.args.max_steps = 2
+    t1.train()
+    assert os.path.exists(tmp_path / "b" / "checkpoint-2" / "optimizer.pt")
+    t2 = mk(tmp_path / "b", 4, 0)
+    out = t2.train(resume_from_checkpoint="auto")
+    assert out.global_step == 4
+    assert torch.allclose(t2.engine.param_flat, t_full.engine.param_flat, atol=1e-6)
+
+
+def test_lora_trains_only_adapters(tmp_path, tk):
+    a = SFTConfig(output_dir=str(tmp_path), per_device_train_batch_size=4, max_steps=2, learning_rate=1e-2,
+                  freeze_policy="lora", lora_r=4, jsonl_log=False)
+    m = _model()
+    base = m.model.layers[0].self_attn.qkv_proj.detach().clone()
+    t = SFTTrainer(model=m, args=a, train_dataset=generate_qa(16), processing_class=tk)
+    assert t.trainable_params < t.total_params
+    t.train()
+    assert torch.equal(base, m.model.layers[0].self_attn.qkv_proj)
+    B = m.model.layers[0].self_attn.lora["qkv"].B[0]
+    assert B.abs().sum() > 0  # adapters moved
+    t.save_model(str(tmp_path / "lora_model"))
+    assert os.path.exists(tmp_path / "lora_model" / "adapter_model.safetensors")
+
+
+def test_schedules():
+    lin = get_schedule("linear", 10, 0)
+    assert lin(0) == 1.0 and lin(5) == 0.5 and lin(10) == 0.0
+    cos = get_schedule("cosine", 10, 2)
+    assert cos(1) == 0.5 and abs(cos(2) - 1.0) < 1e-9 and abs(cos(10)) < 1e-9
+    assert get_schedule("constant", 10)(7) == 1.0
+
+
+def test_reference_freeze_policy_counts(tmp_path, tk):
+    a = SFTConfig(output_dir=str(tmp_path), freeze_policy="last_n_layers", max_steps=1, jsonl_log=False,
+                  per_device_train_batch_size=2)
+    m = _model()
+    t = SFTTrainer(model=m, args=a, train_dataset=generate_qa(4), processing_class=tk)
+    per_layer = sum(p.numel() for p in m.model.layers[0].parameters())
+    assert t.trainable_params == 2 * per_layer + m.config.vocab_size * m.config.hidden_size
+    frozen0 = m.model.layers[0].self_attn.qkv_proj.detach().clone()
+    t.train()
+    assert torch.equal(frozen0, m.model.layers[0].self_attn.qkv_proj)

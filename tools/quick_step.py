@@ -1,5 +1,8 @@
 """Quick single-GPU fwd/bwd timing of SmolLM3-3B (random init) for early bring-up."""
 import argparse
+import os
+import sys
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import time
 
 import torch
