@@ -1,0 +1,121 @@
+"""Single-node multi-GPU launcher (replaces the reference's Kubeflow PyTorchJob).
+
+    python -m llm_fine_tune_distributed_amd.launch --nproc-per-node 8 train_script.py [args...]
+    python -m llm_fine_tune_distributed_amd.launch --nproc-per-node 8 -m llm_fine_tune_distributed_amd.cli.train
+
+One process per GPU; each child gets the torchrun env contract (``WORLD_SIZE, RANK, LOCAL_RANK,
+LOCAL_WORLD_SIZE, MASTER_ADDR, MASTER_PORT``) plus ``HSA_ENABLE_IPC_MODE_LEGACY=0`` (dmabuf IPC for
+RCCL over xGMI). The launcher never touches the GPU itself.
+
+Failure detection: the launcher polls its children; when one exits non-zero the others are
+terminated (SIGTERM, then SIGKILL after ``--grace``) instead of blocking in a collective until
+the watchdog timeout (the reference's "workers hang until NCCL timeout"). With
+``--max-restarts K`` the whole group is restarted (``SFTAMD_RESTART_COUNT`` is exported) and the
+training script resumes from its latest checkpoint (``--resume auto``).
+"""
+from __future__ import annotations
+
+import argparse
+import os
+import signal
+import socket
+import subprocess
+import sys
+import time
+from typing import List
+
+
+def _free_port(addr: str) -> int:
+    s = socket.socket()
+    s.bind((addr, 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _spawn(n: int, cmd: List[str], addr: str, port: int, restart: int, node_rank: int, nnodes: int) -> List[subprocess.Popen]:
+    procs = []
+    for lr in range(n):
+        env = dict(os.environ)
+        env.update(WORLD_SIZE=str(n * nnodes), RANK=str(node_rank * n + lr), LOCAL_RANK=str(lr),
+                   LOCAL_WORLD_SIZE=str(n), GROUP_RANK=str(node_rank), MASTER_ADDR=addr, MASTER_PORT=str(port),
+                   SFTAMD_RESTART_COUNT=str(restart), HSA_ENABLE_IPC_MODE_LEGACY="0")
+        env.setdefault("OMP_NUM_THREADS", "1")
+        procs.append(subprocess.Popen(cmd, env=env, start_new_session=True))
+    return procs
+
+
+def _terminate(procs: List[subprocess.Popen], grace: float):
+    for p in procs:
+        if p.poll() is None:
+            try:
+                os.killpg(p.pid, signal.SIGTERM)
+            except ProcessLookupError:
+                pass
+    t0 = time.time()
+    while time.time() - t0 < grace and any(p.poll() is None for p in procs):
+        time.sleep(0.1)
+    for p in procs:
+        if p.poll() is None:
+            try:
+                os.killpg(p.pid, signal.SIGKILL)
+            except ProcessLookupError:
+                pass
+    for p in procs:
+        p.wait()
+
+
+def run(argv=None) -> int:
+    ap = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
+    ap.add_argument("--nproc-per-node", "--nproc_per_node", type=int, default=1)
+    ap.add_argument("--nnodes", type=int, default=1)
+    ap.add_argument("--node-rank", type=int, default=0)
+    ap.add_argument("--master-addr", "--master_addr", default=os.environ.get("MASTER_ADDR", "127.0.0.1"))
+    ap.add_argument("--master-port", "--master_port", type=int, default=int(os.environ.get("MASTER_PORT", "0")))
+    ap.add_argument("--max-restarts", type=int, default=0)
+    ap.add_argument("--grace", type=float, default=10.0)
+    ap.add_argument("--monitor-interval", type=float, default=0.5)
+    ap.add_argument("-m", dest="module", default=None, help="run a module (like python -m)")
+    ap.add_argument("script", nargs="?")
+    ap.add_argument("args", nargs=argparse.REMAINDER)
+    a = ap.parse_args(argv)
+    if a.module:
+        cmd = [sys.executable, "-u", "-m", a.module] + ([a.script] if a.script else []) + a.args
+    elif a.script:
+        cmd = [sys.executable, "-u", a.script] + a.args
+    else:
+        ap.error("need a script or -m module")
+    restart = 0
+    while True:
+        port = a.master_port or _free_port(a.master_addr)
+        procs = _spawn(a.nproc_per_node, cmd, a.master_addr, port, restart, a.node_rank, a.nnodes)
+        failed = None
+        try:
+            while True:
+                codes = [p.poll() for p in procs]
+                bad = [(i, c) for i, c in enumerate(codes) if c not in (None, 0)]
+                if bad:
+                    failed = bad[0]
+                    break
+                if all(c == 0 for c in codes):
+                    return 0
+                time.sleep(a.monitor_interval)
+        except KeyboardInterrupt:
+            _terminate(procs, a.grace)
+            return 130
+        rank, code = failed
+        print(f"[launch] local rank {rank} exited with code {code}; terminating the other ranks", file=sys.stderr,
+              flush=True)
+        _terminate(procs, a.grace)
+        if restart >= a.max_restarts:
+            return code if code > 0 else 1
+        restart += 1
+        print(f"[launch] restarting group (attempt {restart}/{a.max_restarts})", file=sys.stderr, flush=True)
+
+
+def main():
+    sys.exit(run())
+
+
+if __name__ == "__main__":
+    main()

@@ -172,7 +172,7 @@ def llama3_8b() -> ModelConfig:
 def tiny(model_type: str = "smollm3", **kw) -> ModelConfig:
     """Small config with the same structure (GQA, NoPE interval, tied head) for tests."""
     base = dict(
-        model_type=model_type, vocab_size=512, hidden_size=128, intermediate_size=256,
+        model_type=model_type, vocab_size=1024, hidden_size=128, intermediate_size=256,
         num_hidden_layers=4, num_attention_heads=4, num_key_value_heads=2, head_dim=32,
         rope_theta=10000.0, max_position_embeddings=1024, tie_word_embeddings=(model_type == "smollm3"),
         bos_token_id=1, eos_token_id=2, pad_token_id=2,
