@@ -37,16 +37,9 @@ def main():
     ap.add_argument("--bucket-mb", type=float, default=float(os.environ.get("SFTAMD_BUCKET_MB", "64")))
     ap.add_argument("--packing", action="store_true")
     ap.add_argument("--tunableop", default=os.environ.get("SFTAMD_TUNABLEOP", "auto"),
-                    help="auto: use the committed hipBLASLt selection file if present")
+                    help="auto: load the committed GEMM selections; tune: tune missing shapes into it; off")
     ap.add_argument("--profile-steps", type=int, default=0)
     a = ap.parse_args()
-
-    root = os.path.dirname(os.path.abspath(__file__))
-    tfile = os.path.join(root, "tuning", "tunableop_results_mi355x.csv")
-    if a.tunableop != "off" and os.path.exists(tfile) and "PYTORCH_TUNABLEOP_ENABLED" not in os.environ:
-        os.environ["PYTORCH_TUNABLEOP_ENABLED"] = "1"
-        os.environ["PYTORCH_TUNABLEOP_TUNING"] = "0"
-        os.environ["PYTORCH_TUNABLEOP_FILENAME"] = tfile
 
     import torch
     import torch.distributed as dist
@@ -57,6 +50,9 @@ def main():
     from llm_fine_tune_distributed_amd.train import SFTConfig, SFTTrainer
 
     st = setup_distributed(verbose=False)
+    if a.tunableop != "off" and "PYTORCH_TUNABLEOP_ENABLED" not in os.environ:
+        from llm_fine_tune_distributed_amd.utils.gemm_tuning import enable_tuned_gemms
+        enable_tuned_gemms(tune=(a.tunableop == "tune"), verbose=st.is_main)
     if st.world_size != a.gpus:
         raise SystemExit(f"--gpus {a.gpus} but WORLD_SIZE={st.world_size}")
     cfg = get_config(a.model)

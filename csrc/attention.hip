@@ -408,6 +408,424 @@ __global__ __launch_bounds__(256) void bwd_dq_kernel(const u16* __restrict__ qkv
   }
 }
 
+
+// ============================================================================== v2 kernels
+// Same math and lane maps as v1, restructured for latency hiding on CDNA4:
+// * K/V (fwd, dQ) and Q/dO (dK/dV) tiles are double-buffered in LDS; the next tile is issued
+//   global->registers BEFORE the current tile's MFMAs and written to the other LDS buffer after
+//   them (T14 async-STAGE split), so HBM/L2 latency hides under compute; one barrier per tile;
+// * fwd/dQ use 8-wave (512-thread) workgroups over 128 query rows, halving K/V staging per row
+//   and giving two waves per SIMD; waves whose 16 rows are entirely below a causal key tile skip
+//   its MFMAs (wave-uniform branch);
+// * dK/dV is split over the query heads of a GQA group (4x the workgroups, no causal tail of
+//   32 sequential tiles): each workgroup writes an fp32 partial slab, and a vectorised reduce
+//   kernel sums the rep partials in a fixed order (deterministic) straight into packed dqkv.
+
+template <int R, int NT>
+struct TileRegs {
+  static constexpr int N = (R * 16) / NT;
+  uint4 v[N];
+  __device__ __forceinline__ void load(const u16* __restrict__ g, long ld, int nvalid, int tid) {
+#pragma unroll
+    for (int it = 0; it < N; ++it) {
+      const int idx = tid + it * NT;
+      const int r = idx >> 4, ch = idx & 15;
+      v[it] = make_uint4(0, 0, 0, 0);
+      if (r < nvalid) v[it] = *(const uint4*)(g + (long)r * ld + ch * 8);
+    }
+  }
+  __device__ __forceinline__ void store(char* lds, int tid) const {
+#pragma unroll
+    for (int it = 0; it < N; ++it) {
+      const int idx = tid + it * NT;
+      *(uint4*)(lds + img_off(idx >> 4, idx & 15)) = v[it];
+    }
+  }
+};
+
+template <bool TR, int NW>
+__global__ __launch_bounds__(NW * 64) void fwd2_kernel(const u16* __restrict__ qkv, u16* __restrict__ out,
+                                                       float* __restrict__ lse, const int* __restrict__ cu, int nq,
+                                                       int nkv, int total, float sl2, int causal) {
+  constexpr int NT = NW * 64, BM = NW * 16, TB = 64 * ROWB;
+  __shared__ __attribute__((aligned(16))) char smem[4 * TB];  // K0 V0 K1 V1
+  const int qb = blockIdx.x, h = blockIdx.y, b = blockIdx.z;
+  const int start = cu[b], len = cu[b + 1] - start;
+  const int q0 = qb * BM;
+  if (q0 >= len) return;
+  const int kvh = h / (nq / nkv);
+  const long ld = (long)(nq + 2 * nkv) * D;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, g = lane >> 4;
+  const int qrow = q0 + wave * 16 + (lane & 15);
+  const int wlast = q0 + wave * 16 + 15;  // last query row of this wave
+  const bool qok = qrow < len;
+  const u16* kbase = qkv + (long)start * ld + (nq + kvh) * D;
+  const u16* vbase = qkv + (long)start * ld + (nq + nkv + kvh) * D;
+  const int nkb = (len + 63) / 64;
+  const int nkt = causal ? min((q0 + BM + 63) / 64, nkb) : nkb;
+  {
+    TileRegs<64, NT> tk, tv;
+    tk.load(kbase, ld, min(64, len), tid);
+    tv.load(vbase, ld, min(64, len), tid);
+    tk.store(smem, tid);
+    tv.store(smem + TB, tid);
+  }
+  bf16x8 qf[4];
+  {
+    const u16* qp = qkv + (long)(start + qrow) * ld + h * D + 8 * g;
+#pragma unroll
+    for (int s = 0; s < 4; ++s) qf[s] = load_frag_global(qp + 32 * s, qok);
+  }
+  f32x4 o[8];
+#pragma unroll
+  for (int dt = 0; dt < 8; ++dt) o[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
+  float m = -1e30f, l = 0.f;
+  __syncthreads();
+  for (int kt = 0; kt < nkt; ++kt) {
+    const int k0 = kt * 64;
+    char* Ks = smem + (kt & 1) * 2 * TB;
+    char* Vs = Ks + TB;
+    const bool pre = kt + 1 < nkt;
+    TileRegs<64, NT> tk, tv;
+    if (pre) {
+      const int kv = min(64, len - k0 - 64);
+      tk.load(kbase + (long)(k0 + 64) * ld, ld, kv, tid);
+      tv.load(vbase + (long)(k0 + 64) * ld, ld, kv, tid);
+    }
+    if (!causal || k0 <= wlast) {
+      f32x4 sc[4];
+#pragma unroll
+      for (int nt = 0; nt < 4; ++nt) {
+        sc[nt] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int s = 0; s < 4; ++s) sc[nt] = mfma(frag_row(Ks, 16 * nt, s, lane), qf[s], sc[nt]);
+      }
+      float tmax = -INFINITY;
+#pragma unroll
+      for (int nt = 0; nt < 4; ++nt)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int key = k0 + 16 * nt + 4 * g + i;
+          float v = sc[nt][i] * sl2;
+          if (key >= len || (causal && key > qrow)) v = -INFINITY;
+          sc[nt][i] = v;
+          tmax = fmaxf(tmax, v);
+        }
+      tmax = fmaxf(tmax, __shfl_xor(tmax, 16, 64));
+      tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64));
+      const float mnew = fmaxf(m, tmax);
+      const float alpha = exp2f(m - mnew);
+      float rs = 0.f;
+#pragma unroll
+      for (int nt = 0; nt < 4; ++nt)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const float p = exp2f(sc[nt][i] - mnew);
+          sc[nt][i] = p;
+          rs += p;
+        }
+      rs += __shfl_xor(rs, 16, 64);
+      rs += __shfl_xor(rs, 32, 64);
+      l = l * alpha + rs;
+      m = mnew;
+#pragma unroll
+      for (int dt = 0; dt < 8; ++dt) o[dt] *= alpha;
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        const bf16x8 pb = pack_acc(sc[2 * ks], sc[2 * ks + 1]);
+#pragma unroll
+        for (int dt = 0; dt < 8; ++dt) o[dt] = mfma(frag_tr<TR>(Vs, 32 * ks, dt, lane), pb, o[dt]);
+      }
+    }
+    if (pre) {
+      char* Kn = smem + ((kt + 1) & 1) * 2 * TB;
+      tk.store(Kn, tid);
+      tv.store(Kn + TB, tid);
+    }
+    __syncthreads();
+  }
+  if (qok) {
+    const float inv = 1.f / l;
+    u16* op = out + (long)(start + qrow) * nq * D + h * D + 4 * g;
+#pragma unroll
+    for (int dt = 0; dt < 8; ++dt) store4(op + 16 * dt, o[dt], inv);
+    if (g == 0) lse[(long)h * total + start + qrow] = (m + log2f(l)) * LN2;
+  }
+}
+
+template <bool TR, int NW>
+__global__ __launch_bounds__(NW * 64) void bwd_dq2_kernel(const u16* __restrict__ qkv, const u16* __restrict__ dout,
+                                                          const float* __restrict__ lse,
+                                                          const float* __restrict__ delta, const int* __restrict__ cu,
+                                                          u16* __restrict__ dqkv, int nq, int nkv, int total,
+                                                          float sl2, float scale, int causal) {
+  constexpr int NT = NW * 64, BM = NW * 16, TB = 64 * ROWB;
+  __shared__ __attribute__((aligned(16))) char smem[4 * TB];
+  const int qb = blockIdx.x, h = blockIdx.y, b = blockIdx.z;
+  const int start = cu[b], len = cu[b + 1] - start;
+  const int q0 = qb * BM;
+  if (q0 >= len) return;
+  const int kvh = h / (nq / nkv);
+  const long ld = (long)(nq + 2 * nkv) * D;
+  const long ldo = (long)nq * D;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, g = lane >> 4;
+  const int qrow = q0 + wave * 16 + (lane & 15);
+  const int wlast = q0 + wave * 16 + 15;
+  const bool qok = qrow < len;
+  const u16* kbase = qkv + (long)start * ld + (nq + kvh) * D;
+  const u16* vbase = qkv + (long)start * ld + (nq + nkv + kvh) * D;
+  const int nkb = (len + 63) / 64;
+  const int nkt = causal ? min((q0 + BM + 63) / 64, nkb) : nkb;
+  {
+    TileRegs<64, NT> tk, tv;
+    tk.load(kbase, ld, min(64, len), tid);
+    tv.load(vbase, ld, min(64, len), tid);
+    tk.store(smem, tid);
+    tv.store(smem + TB, tid);
+  }
+  bf16x8 qf[4], df[4];
+  {
+    const u16* qp = qkv + (long)(start + qrow) * ld + h * D + 8 * g;
+    const u16* dp = dout + (long)(start + qrow) * ldo + h * D + 8 * g;
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      qf[s] = load_frag_global(qp + 32 * s, qok);
+      df[s] = load_frag_global(dp + 32 * s, qok);
+    }
+  }
+  const float lse2 = qok ? lse[(long)h * total + start + qrow] * LOG2E : 0.f;
+  const float dl = qok ? delta[(long)h * total + start + qrow] : 0.f;
+  f32x4 dq[8];
+#pragma unroll
+  for (int dt = 0; dt < 8; ++dt) dq[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
+  __syncthreads();
+  for (int kt = 0; kt < nkt; ++kt) {
+    const int k0 = kt * 64;
+    char* Ks = smem + (kt & 1) * 2 * TB;
+    char* Vs = Ks + TB;
+    const bool pre = kt + 1 < nkt;
+    TileRegs<64, NT> tk, tv;
+    if (pre) {
+      const int kv = min(64, len - k0 - 64);
+      tk.load(kbase + (long)(k0 + 64) * ld, ld, kv, tid);
+      tv.load(vbase + (long)(k0 + 64) * ld, ld, kv, tid);
+    }
+    if (!causal || k0 <= wlast) {
+      f32x4 sc[4], dp[4];
+#pragma unroll
+      for (int nt = 0; nt < 4; ++nt) {
+        sc[nt] = f32x4{0.f, 0.f, 0.f, 0.f};
+        dp[nt] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+          sc[nt] = mfma(frag_row(Ks, 16 * nt, s, lane), qf[s], sc[nt]);
+          dp[nt] = mfma(frag_row(Vs, 16 * nt, s, lane), df[s], dp[nt]);
+        }
+      }
+#pragma unroll
+      for (int nt = 0; nt < 4; ++nt)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int key = k0 + 16 * nt + 4 * g + i;
+          float p = exp2f(sc[nt][i] * sl2 - lse2);
+          if (key >= len || (causal && key > qrow) || !qok) p = 0.f;
+          dp[nt][i] = p * (dp[nt][i] - dl);
+        }
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        const bf16x8 db = pack_acc(dp[2 * ks], dp[2 * ks + 1]);
+#pragma unroll
+        for (int dt = 0; dt < 8; ++dt) dq[dt] = mfma(frag_tr<TR>(Ks, 32 * ks, dt, lane), db, dq[dt]);
+      }
+    }
+    if (pre) {
+      char* Kn = smem + ((kt + 1) & 1) * 2 * TB;
+      tk.store(Kn, tid);
+      tv.store(Kn + TB, tid);
+    }
+    __syncthreads();
+  }
+  if (qok) {
+    u16* qp = dqkv + (long)(start + qrow) * ld + h * D + 4 * g;
+#pragma unroll
+    for (int dt = 0; dt < 8; ++dt) store4(qp + 16 * dt, dq[dt], scale);
+  }
+}
+
+// dK/dV partials for ONE query head h (grid (key blocks, nq, nseq)); writes fp32 slab
+// part[r][token][2*nkv*D] (r = h % rep; dK at kvh*D, dV at (nkv+kvh)*D). When rep == 1 the
+// result goes straight to dqkv (bf16, dK scaled).
+template <bool TR>
+__global__ __launch_bounds__(256, 2) void bwd_dkdv2_kernel(const u16* __restrict__ qkv, const u16* __restrict__ dout,
+                                                           const float* __restrict__ lse,
+                                                           const float* __restrict__ delta,
+                                                           const int* __restrict__ cu, float* __restrict__ part,
+                                                           u16* __restrict__ dqkv, int nq, int nkv, int total,
+                                                           float sl2, float scale, int causal) {
+  constexpr int NT = 256, TB = 64 * ROWB;
+  __shared__ __attribute__((aligned(16))) char smem[4 * TB + 2 * 2 * 64 * 4];
+  float* LDs = (float*)(smem + 4 * TB);  // [buf][lse2 64 | delta 64]
+  const int kb = blockIdx.x, h = blockIdx.y, b = blockIdx.z;
+  const int start = cu[b], len = cu[b + 1] - start;
+  const int k0 = kb * 64;
+  if (k0 >= len) return;
+  const int rep = nq / nkv;
+  const int kvh = h / rep, r = h - kvh * rep;
+  const long ld = (long)(nq + 2 * nkv) * D;
+  const long ldo = (long)nq * D;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, g = lane >> 4;
+  const int key = k0 + wave * 16 + (lane & 15);
+  const int wfirst = k0 + wave * 16;
+  const bool kok = key < len;
+  const u16* qbase = qkv + (long)start * ld + h * D;
+  const u16* obase = dout + (long)start * ldo + h * D;
+  const float* lbase = lse + (long)h * total + start;
+  const float* dbase = delta + (long)h * total + start;
+  const int qt0 = causal ? kb : 0;
+  const int nqt = (len + 63) / 64;
+  {
+    const int q0 = qt0 * 64, qv = min(64, len - q0);
+    TileRegs<64, NT> tq, to;
+    tq.load(qbase + (long)q0 * ld, ld, qv, tid);
+    to.load(obase + (long)q0 * ldo, ldo, qv, tid);
+    tq.store(smem, tid);
+    to.store(smem + TB, tid);
+    if (tid < 64) {
+      LDs[tid] = tid < qv ? lbase[q0 + tid] * LOG2E : 0.f;
+      LDs[64 + tid] = tid < qv ? dbase[q0 + tid] : 0.f;
+    }
+  }
+  bf16x8 kf[4], vf[4];
+  {
+    const u16* kp = qkv + (long)(start + key) * ld + (nq + kvh) * D + 8 * g;
+    const u16* vp = qkv + (long)(start + key) * ld + (nq + nkv + kvh) * D + 8 * g;
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      kf[s] = load_frag_global(kp + 32 * s, kok);
+      vf[s] = load_frag_global(vp + 32 * s, kok);
+    }
+  }
+  f32x4 dk[8], dv[8];
+#pragma unroll
+  for (int dt = 0; dt < 8; ++dt) {
+    dk[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
+    dv[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
+  }
+  __syncthreads();
+  for (int qt = qt0; qt < nqt; ++qt) {
+    const int q0 = qt * 64;
+    const int buf = (qt - qt0) & 1;
+    char* Qs = smem + buf * 2 * TB;
+    char* Os = Qs + TB;
+    const float* Ls = LDs + buf * 128;
+    const float* Dl = Ls + 64;
+    const bool pre = qt + 1 < nqt;
+    TileRegs<64, NT> tq, to;
+    float pl = 0.f, pd = 0.f;
+    if (pre) {
+      const int qn = q0 + 64, qv = min(64, len - qn);
+      tq.load(qbase + (long)qn * ld, ld, qv, tid);
+      to.load(obase + (long)qn * ldo, ldo, qv, tid);
+      if (tid < 64 && tid < qv) {
+        pl = lbase[qn + tid] * LOG2E;
+        pd = dbase[qn + tid];
+      }
+    }
+    // a wave whose 16 keys are all later than every query of the tile contributes nothing
+    if (!causal || wfirst <= q0 + 63) {
+      f32x4 sc[4], dp[4];
+#pragma unroll
+      for (int mt = 0; mt < 4; ++mt) {
+        sc[mt] = f32x4{0.f, 0.f, 0.f, 0.f};
+        dp[mt] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+          sc[mt] = mfma(frag_row(Qs, 16 * mt, s, lane), kf[s], sc[mt]);
+          dp[mt] = mfma(frag_row(Os, 16 * mt, s, lane), vf[s], dp[mt]);
+        }
+      }
+#pragma unroll
+      for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int qi = 16 * mt + 4 * g + i;
+          const int q = q0 + qi;
+          float p = exp2f(sc[mt][i] * sl2 - Ls[qi]);
+          if (q >= len || (causal && key > q)) p = 0.f;
+          sc[mt][i] = p;
+          dp[mt][i] = p * (dp[mt][i] - Dl[qi]);
+        }
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        const bf16x8 pb = pack_acc(sc[2 * ks], sc[2 * ks + 1]);
+        const bf16x8 db = pack_acc(dp[2 * ks], dp[2 * ks + 1]);
+#pragma unroll
+        for (int dt = 0; dt < 8; ++dt) {
+          dv[dt] = mfma(frag_tr<TR>(Os, 32 * ks, dt, lane), pb, dv[dt]);
+          dk[dt] = mfma(frag_tr<TR>(Qs, 32 * ks, dt, lane), db, dk[dt]);
+        }
+      }
+    }
+    if (pre) {
+      char* Qn = smem + (buf ^ 1) * 2 * TB;
+      tq.store(Qn, tid);
+      to.store(Qn + TB, tid);
+      if (tid < 64) {
+        float* Ln = LDs + (buf ^ 1) * 128;
+        Ln[tid] = pl;
+        Ln[64 + tid] = pd;
+      }
+    }
+    __syncthreads();
+  }
+  if (!kok) return;
+  if (rep == 1) {
+    u16* kp = dqkv + (long)(start + key) * ld + (nq + kvh) * D + 4 * g;
+    u16* vp = dqkv + (long)(start + key) * ld + (nq + nkv + kvh) * D + 4 * g;
+#pragma unroll
+    for (int dt = 0; dt < 8; ++dt) {
+      store4(kp + 16 * dt, dk[dt], scale);
+      store4(vp + 16 * dt, dv[dt], 1.f);
+    }
+    return;
+  }
+  const long pld = 2L * nkv * D;
+  float* pk = part + ((long)r * total + start + key) * pld + kvh * D + 4 * g;
+  float* pv = pk + (long)nkv * D;
+#pragma unroll
+  for (int dt = 0; dt < 8; ++dt) {
+    *(float4*)(pk + 16 * dt) = make_float4(dk[dt][0], dk[dt][1], dk[dt][2], dk[dt][3]);
+    *(float4*)(pv + 16 * dt) = make_float4(dv[dt][0], dv[dt][1], dv[dt][2], dv[dt][3]);
+  }
+}
+
+// dqkv[m, nq*D + c] = bf16(sum_r part[r][m][c] * (c < nkv*D ? scale : 1)), fixed summation order.
+__global__ __launch_bounds__(256) void dkdv_reduce_kernel(const float* __restrict__ part, u16* __restrict__ dqkv,
+                                                          int total, int nq, int nkv, int rep, float scale) {
+  const int C = 2 * nkv * D;
+  const long nvec = (long)total * C / 8;
+  const long ld = (long)(nq + 2 * nkv) * D;
+  const long stride = (long)total * C;
+  for (long v = blockIdx.x * 256L + threadIdx.x; v < nvec; v += (long)gridDim.x * 256) {
+    const long e = v * 8;
+    const long m = e / C;
+    const int c = (int)(e - m * C);
+    float acc[8];
+    *(float4*)&acc[0] = *(const float4*)(part + e);
+    *(float4*)&acc[4] = *(const float4*)(part + e + 4);
+    for (int r = 1; r < rep; ++r) {
+      const float4 a = *(const float4*)(part + r * stride + e);
+      const float4 b2 = *(const float4*)(part + r * stride + e + 4);
+      acc[0] += a.x; acc[1] += a.y; acc[2] += a.z; acc[3] += a.w;
+      acc[4] += b2.x; acc[5] += b2.y; acc[6] += b2.z; acc[7] += b2.w;
+    }
+    const float sc = c < nkv * D ? scale : 1.f;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) acc[i] *= sc;
+    *(uint4*)(dqkv + m * ld + (long)nq * D + c) = pack8(acc);
+  }
+}
+
 }  // namespace attn
 
 static void check_attn_args(const at::Tensor& qkv, const at::Tensor& cu, int64_t nq, int64_t nkv, int64_t hd) {
@@ -421,6 +839,12 @@ static void check_attn_args(const at::Tensor& qkv, const at::Tensor& cu, int64_t
 }
 
 // variant: 1 = ds_read_b64_tr_b16 transposed operand reads (default), 0 = scalar LDS gathers
+// implementation: 2 = double-buffered v2 kernels (default), 1 = v1 (single-buffered)
+static int attn_impl() {
+  const char* e = std::getenv("SFTAMD_ATTN_IMPL");
+  return (e && e[0] == '1') ? 1 : 2;
+}
+
 static int attn_variant() {
   const char* e = std::getenv("SFTAMD_ATTN_TR");
   return (e && e[0] == '0') ? 0 : 1;
@@ -437,6 +861,18 @@ std::tuple<at::Tensor, at::Tensor> flash_fwd(const at::Tensor& qkv, const at::Te
   dim3 grid((max_seqlen + 63) / 64, nq, nseq);
   const float sl2 = (float)scale * attn::LOG2E;
   auto cu_c = cu.contiguous();
+  if (attn_impl() == 2) {
+    dim3 g2((max_seqlen + 127) / 128, nq, nseq);
+    auto go = [&](auto tr) {
+      constexpr bool TR = decltype(tr)::value;
+      attn::fwd2_kernel<TR, 8><<<g2, 512, 0, cur_stream()>>>((const u16*)qkv.data_ptr(), (u16*)out.data_ptr(),
+                                                            lse.data_ptr<float>(), cu_c.data_ptr<int>(), nq, nkv,
+                                                            total, sl2, causal ? 1 : 0);
+    };
+    if (attn_variant()) go(std::true_type()); else go(std::false_type());
+    SFT_LAUNCH_CHECK();
+    return {out, lse};
+  }
   if (attn_variant())
     attn::fwd_kernel<true><<<grid, 256, 0, cur_stream()>>>((const u16*)qkv.data_ptr(), (u16*)out.data_ptr(),
                                                            lse.data_ptr<float>(), cu_c.data_ptr<int>(), nq, nkv, total,
@@ -480,10 +916,37 @@ at::Tensor flash_bwd(const at::Tensor& dout, const at::Tensor& qkv, const at::Te
         cu_c.data_ptr<int>(), (u16*)dqkv.data_ptr(), nq, nkv, total, sl2, (float)scale, causal ? 1 : 0);
     SFT_LAUNCH_CHECK();
   };
-  if (attn_variant())
+  auto run2 = [&](auto tr) {
+    constexpr bool TR = decltype(tr)::value;
+    const int rep = nq / nkv;
+    at::Tensor part;
+    if (rep > 1) part = at::empty({(long)rep * total * 2 * nkv * hd}, qkv.options().dtype(at::kFloat));
+    dim3 gk2((max_seqlen + 63) / 64, nq, nseq);
+    attn::bwd_dkdv2_kernel<TR><<<gk2, 256, 0, cur_stream()>>>(
+        (const u16*)qkv.data_ptr(), (const u16*)dout.data_ptr(), lse.data_ptr<float>(), delta.data_ptr<float>(),
+        cu_c.data_ptr<int>(), rep > 1 ? part.data_ptr<float>() : nullptr, (u16*)dqkv.data_ptr(), nq, nkv, total, sl2,
+        (float)scale, causal ? 1 : 0);
+    SFT_LAUNCH_CHECK();
+    if (rep > 1) {
+      const long nvec = (long)total * 2 * nkv * hd / 8;
+      const int grid = (int)std::min<long>((nvec + 255) / 256, 2048);
+      attn::dkdv_reduce_kernel<<<grid, 256, 0, cur_stream()>>>(part.data_ptr<float>(), (u16*)dqkv.data_ptr(), total,
+                                                               nq, nkv, rep, (float)scale);
+      SFT_LAUNCH_CHECK();
+    }
+    dim3 gq2((max_seqlen + 127) / 128, nq, nseq);
+    attn::bwd_dq2_kernel<TR, 8><<<gq2, 512, 0, cur_stream()>>>(
+        (const u16*)qkv.data_ptr(), (const u16*)dout.data_ptr(), lse.data_ptr<float>(), delta.data_ptr<float>(),
+        cu_c.data_ptr<int>(), (u16*)dqkv.data_ptr(), nq, nkv, total, sl2, (float)scale, causal ? 1 : 0);
+    SFT_LAUNCH_CHECK();
+  };
+  if (attn_impl() == 2) {
+    if (attn_variant()) run2(std::true_type()); else run2(std::false_type());
+  } else if (attn_variant()) {
     run(std::true_type());
-  else
+  } else {
     run(std::false_type());
+  }
   return dqkv;
 }
 

@@ -171,10 +171,14 @@ class DDPEngine:
 
     # ------------------------------------------------------------------ hooks
     def _post_accumulate(self, p):
-        # plain-autograd parameters (e.g. LoRA adapters): fold .grad into the flat buffer
-        if p.grad is not None:
-            p.main_grad.add_(p.grad.to(p.main_grad.dtype))
-            p.grad = None
+        # Plain-autograd parameters (e.g. LoRA adapters): fold .grad into the flat buffer.
+        # The hook also fires for parameters whose fused op returned no gradient (they already
+        # accumulated into main_grad and signalled readiness themselves): ignore those, or the
+        # bucket would be counted twice and launched before its gradients are complete.
+        if p.grad is None:
+            return
+        p.main_grad.add_(p.grad.to(p.main_grad.dtype))
+        p.grad = None
         self._on_param_ready(p)
 
     def _on_param_ready(self, p):
@@ -184,6 +188,8 @@ class DDPEngine:
         if b is None:
             return
         b.pending -= 1
+        if b.pending < 0:
+            raise RuntimeError(f"DDP bucket {b.index}: parameter {self.param_names.get(id(p))} signalled ready twice")
         if b.pending == 0:
             b.ready = True
             self._launch_ready()

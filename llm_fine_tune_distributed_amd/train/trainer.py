@@ -42,6 +42,7 @@ from .callbacks import (AimCallback, CallbackHandler, JSONLLoggerCallback, Print
                         TrainerControl, TrainerState)
 from .config import SFTConfig
 from .optim import FlatAdamW, LRScheduler, get_schedule
+from ..utils.faults import maybe_inject
 
 PEAK_BF16_FLOPS = 2.5e15  # MI355X dense bf16 (vendor figure; AMD's 5 PF headline includes 2:1 sparsity)
 
@@ -69,6 +70,9 @@ class SFTTrainer:
         self.dist = setup_distributed(timeout_s=args.ddp_timeout, verbose=False)
         set_seed(args.seed)
         dev = self.dist.device
+        if args.gemm_tuning and dev.type == "cuda" and "PYTORCH_TUNABLEOP_ENABLED" not in os.environ:
+            from ..utils.gemm_tuning import enable_tuned_gemms
+            enable_tuned_gemms()
         # ------------------------------------------------------------ model
         if isinstance(model, str):
             if os.path.isdir(model) and any(f.endswith(".safetensors") for f in os.listdir(model)):
@@ -347,6 +351,7 @@ class SFTTrainer:
                 self.state.total_flos += 6.0 * self.trainable_params * n_t * self.dist.world_size
                 self.control = self.callback_handler.call("on_step_end", a, self.state, self.control)
                 gs = self.state.global_step
+                maybe_inject(self.dist.rank, gs)
                 if log_every and (gs % log_every == 0 or (gs == 1 and a.logging_first_step)):
                     red = run_acc.clone()
                     all_reduce_sum_(red)

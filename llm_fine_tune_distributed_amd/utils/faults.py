@@ -1,0 +1,23 @@
+"""Fault injection for failure-detection / resume tests.
+
+``SFTAMD_FAULT_INJECT="rank:step[:code]"`` makes that rank exit abruptly (``os._exit``) when it
+reaches that optimizer step — the launcher must then tear the group down and, with
+``--max-restarts``, restart it so the trainer resumes from the latest checkpoint. Only the first
+attempt injects (``SFTAMD_RESTART_COUNT == 0``).
+"""
+from __future__ import annotations
+
+import os
+import sys
+
+
+def maybe_inject(rank: int, step: int) -> None:
+    spec = os.environ.get("SFTAMD_FAULT_INJECT")
+    if not spec or os.environ.get("SFTAMD_RESTART_COUNT", "0") != "0":
+        return
+    parts = spec.split(":")
+    r, s = int(parts[0]), int(parts[1])
+    code = int(parts[2]) if len(parts) > 2 else 17
+    if rank == r and step == s:
+        print(f"[fault] injecting failure on rank {rank} at step {step}", file=sys.stderr, flush=True)
+        os._exit(code)

@@ -1,0 +1,34 @@
+"""hipBLASLt/rocBLAS kernel selection for the plain projection GEMMs (PyTorch TunableOp).
+
+The fused/hot non-GEMM ops are hand-written HIP; the plain library GEMMs (q/k/v, o, gate/up, down,
+lm_head: fwd, dgrad, wgrad) go to hipBLASLt/rocBLAS. TunableOp benchmarks every candidate solution
+of both libraries per GEMM shape on the actual MI355X and records the fastest. We ship the selections
+for the SmolLM3-3B training shapes in ``tuning/tunableop_results_mi355x.csv`` (produced on MI355X with
+``tools/tune_gemms.sh``) and load them read-only at start-up, so no tuning happens in timed runs.
+Shapes missing from the file fall back to the library default heuristics.
+"""
+from __future__ import annotations
+
+import os
+from typing import Optional
+
+_DEFAULT = os.path.join(os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))), "tuning",
+                        "tunableop_results_mi355x.csv")
+
+
+def enable_tuned_gemms(path: Optional[str] = None, tune: bool = False, verbose: bool = False) -> bool:
+    import torch
+    if not torch.cuda.is_available():
+        return False
+    path = path or os.environ.get("SFTAMD_GEMM_TUNING_FILE", _DEFAULT)
+    tun = torch.cuda.tunable
+    tun.enable(True)
+    tun.tuning_enable(bool(tune))
+    if tune:
+        tun.set_filename(path, insert_device_ordinal=False)
+    ok = False
+    if os.path.exists(path):
+        ok = bool(tun.read_file(path))
+    if verbose:
+        print(f"[gemm] TunableOp enabled (tuning={tune}) selections={path if ok else 'none'}", flush=True)
+    return ok

@@ -117,8 +117,9 @@ def test_cross_entropy(V):
     assert rel_err(lg, gref) < 2e-2
 
 
-def _attn_case(lens, nq, nkv, causal, variant):
+def _attn_case(lens, nq, nkv, causal, variant, impl="2"):
     os.environ["SFTAMD_ATTN_TR"] = variant
+    os.environ["SFTAMD_ATTN_IMPL"] = impl
     torch.manual_seed(0)
     D = 128
     cu = torch.tensor([0] + list(torch.tensor(lens).cumsum(0)), dtype=torch.int32, device=DEV)
@@ -137,14 +138,20 @@ def _attn_case(lens, nq, nkv, causal, variant):
         assert e < 3e-2, (name, e)
 
 
+@pytest.mark.parametrize("impl", ["2", "1"])
 @pytest.mark.parametrize("variant", ["1", "0"])
 @pytest.mark.parametrize("causal", [True, False])
-def test_flash_attention_varlen_gqa(variant, causal):
-    _attn_case([100, 255, 64, 1], 8, 2, causal, variant)
+def test_flash_attention_varlen_gqa(variant, causal, impl):
+    _attn_case([100, 255, 64, 1, 300], 8, 2, causal, variant, impl)
 
 
-def test_flash_attention_smollm3_shape():
-    _attn_case([512] * 4, 16, 4, True, "1")
+def test_flash_attention_mha_and_long():
+    _attn_case([1000, 37], 4, 4, True, "1")
+
+
+@pytest.mark.parametrize("impl", ["2", "1"])
+def test_flash_attention_smollm3_shape(impl):
+    _attn_case([512] * 4, 16, 4, True, "1", impl)
 
 
 def test_adamw_and_norm():
