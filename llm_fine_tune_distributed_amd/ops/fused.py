@@ -47,10 +47,17 @@ def _accumulate_weight_grad(param: torch.Tensor, dy2d: torch.Tensor, x2d: torch.
     if scale is not None:
         x2d = x2d * scale.to(x2d.dtype)
     if mg is not None:
+        fresh = getattr(param, "_sftamd_fresh", False)
         if mg.dtype == dy2d.dtype:
-            mg.addmm_(dy2d.t(), x2d)
+            if fresh:  # first contribution of the step: beta=0 GEMM, no zero-fill pass needed
+                torch.mm(dy2d.t(), x2d, out=mg)
+            else:
+                mg.addmm_(dy2d.t(), x2d)
+        elif fresh:
+            mg.copy_(torch.mm(dy2d.t(), x2d))
         else:
             mg.add_(torch.mm(dy2d.t(), x2d).to(mg.dtype))
+        param._sftamd_fresh = False
         _weight_grad_done(param)
         return None
     return torch.mm(dy2d.t(), x2d).to(param.dtype)
@@ -59,7 +66,11 @@ def _accumulate_weight_grad(param: torch.Tensor, dy2d: torch.Tensor, x2d: torch.
 def _accumulate_small_grad(param: torch.Tensor, g: torch.Tensor):
     mg = getattr(param, "main_grad", None)
     if mg is not None:
-        mg.add_(g.to(mg.dtype))
+        if getattr(param, "_sftamd_fresh", False):
+            mg.copy_(g)
+            param._sftamd_fresh = False
+        else:
+            mg.add_(g.to(mg.dtype))
         _weight_grad_done(param)
         return None
     return g.to(param.dtype)
@@ -112,6 +123,9 @@ class EmbeddingFn(Function):
         if _ext.use_hip(dy):
             sorted_ids, perm = torch.sort(flat_ids.to(torch.int32))
             target = mg if mg is not None else torch.zeros_like(w)
+            if mg is not None and getattr(w, "_sftamd_fresh", False):
+                mg.zero_()  # untied embedding: the sparse row update needs a zeroed buffer
+                w._sftamd_fresh = False
             _ext.ops().embedding_bwd(dy2d, sorted_ids, perm.to(torch.int32), target)
             if mg is not None:
                 _weight_grad_done(w)

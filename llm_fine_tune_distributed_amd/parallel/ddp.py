@@ -154,8 +154,15 @@ class DDPEngine:
         finally:
             self.sync_grads = prev
 
-    def zero_grad(self):
-        self.grad_flat.zero_()
+    def zero_grad(self, set_fresh: bool = True):
+        """Start a new accumulation window. With ``set_fresh`` (default) no memset is issued: each
+        parameter's FIRST gradient contribution overwrites its slice (beta=0 GEMM / copy) and
+        ``finish_backward`` zero-fills slices that received nothing (unused parameters)."""
+        if not set_fresh:
+            self.grad_flat.zero_()
+            return
+        for p, _, _, _ in self.layout:
+            p._sftamd_fresh = True
 
     def prepare_backward(self):
         """Call before every backward: resets per-parameter use counters and bucket state."""
@@ -170,6 +177,12 @@ class DDPEngine:
         self._next = 0
 
     # ------------------------------------------------------------------ hooks
+    def _zero_untouched(self):
+        for p, _, _, _ in self.layout:
+            if getattr(p, "_sftamd_fresh", False):
+                p.main_grad.zero_()
+                p._sftamd_fresh = False
+
     def _post_accumulate(self, p):
         # Plain-autograd parameters (e.g. LoRA adapters): fold .grad into the flat buffer.
         # The hook also fires for parameters whose fused op returned no gradient (they already
@@ -177,7 +190,11 @@ class DDPEngine:
         # bucket would be counted twice and launched before its gradients are complete.
         if p.grad is None:
             return
-        p.main_grad.add_(p.grad.to(p.main_grad.dtype))
+        if getattr(p, "_sftamd_fresh", False):
+            p.main_grad.copy_(p.grad)
+            p._sftamd_fresh = False
+        else:
+            p.main_grad.add_(p.grad.to(p.main_grad.dtype))
         p.grad = None
         self._on_param_ready(p)
 
@@ -206,7 +223,10 @@ class DDPEngine:
 
     def finish_backward(self):
         """Wait for all bucket all-reduces (launching any bucket whose params had no grad)."""
-        if not self.sync_grads or self.world_size == 1:
+        if not self.sync_grads:
+            return
+        self._zero_untouched()
+        if self.world_size == 1:
             return
         for b in self.buckets[self._next:]:
             self._launch(b)
