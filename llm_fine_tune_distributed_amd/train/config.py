@@ -91,6 +91,7 @@ class SFTConfig:
     eval_accumulation: bool = True
     jsonl_log: bool = True
     prefetch_batches: int = 2
+    optimizer_overlap: bool = True          # pipeline AdamW under the next forward (side HIP stream)
     gemm_tuning: bool = True                # load shipped hipBLASLt/rocBLAS selections (utils/gemm_tuning.py)
 
     def __post_init__(self):

@@ -34,22 +34,117 @@ class FlatAdamW:
         self.exp_avg = torch.zeros(n, dtype=torch.float32, device=dev)
         self.exp_avg_sq = torch.zeros(n, dtype=torch.float32, device=dev)
         self.last_grad_norm: Optional[torch.Tensor] = None
+        self.overlap = False
+
+    # ------------------------------------------------------------------ overlap with next forward
+    def enable_overlap(self, model) -> bool:
+        """Pipeline the update under the NEXT step's forward (MI355X: AdamW is HBM-bound, the
+        forward GEMMs are MFMA-bound, so they co-run well). Updates are issued on a side stream in
+        forward order (embedding, layer 0, ..., layer L-1, final norm/head), one event per group;
+        forward pre-hooks make the compute stream wait only for the group it is about to read."""
+        if not self.engine.param_flat.is_cuda:
+            return False
+        e = self.engine
+        region_of = {}
+        for s, t, decay in e.regions:
+            region_of[(s, t)] = decay
+        offs = {id(p): (o, n) for p, o, n, _ in e.layout}
+
+        def ranges(params):
+            rs = []
+            for p in params:
+                if id(p) not in offs:
+                    continue
+                o, n = offs[id(p)]
+                n = (n + 63) // 64 * 64
+                decay = next(d for (s, t), d in region_of.items() if s <= o < t)
+                rs.append([o, o + n, decay])
+            rs.sort()
+            merged = []
+            for r in rs:
+                if merged and merged[-1][1] == r[0] and merged[-1][2] == r[2]:
+                    merged[-1][1] = r[1]
+                else:
+                    merged.append(r)
+            return merged
+
+        inner = model.model
+        seen = set()
+        groups = []
+
+        def add(mods_params):
+            ps = [p for p in mods_params if id(p) not in seen]
+            for p in ps:
+                seen.add(id(p))
+            groups.append(ranges(ps))
+
+        add([inner.embed_tokens])
+        for layer in inner.layers:
+            add(list(layer.parameters()))
+        add(list(inner.norm.parameters()) + ([model.lm_head] if model.lm_head is not None else []))
+        rest = [p for p, _, _, _ in e.layout if id(p) not in seen]
+        if rest:
+            groups[-1] += ranges(rest)
+        self._groups = groups
+        self._events = [torch.cuda.Event() for _ in groups]
+        self._stream = torch.cuda.Stream(device=e.device)
+        self._pending = False
+        self._hooks = []
+
+        def waiter(i):
+            def hook(*_a, **_k):
+                if self._pending:
+                    torch.cuda.current_stream().wait_event(self._events[i])
+            return hook
+
+        self._hooks.append(model.register_forward_pre_hook(waiter(0)))
+        for i, layer in enumerate(inner.layers):
+            self._hooks.append(layer.register_forward_pre_hook(waiter(i + 1)))
+        self._hooks.append(inner.layers[-1].register_forward_hook(waiter(len(groups) - 1)))
+        self.overlap = True
+        return True
+
+    def synchronize(self):
+        """Make the current stream wait for every pending update (before eval / save / logging)."""
+        if getattr(self, "_pending", False):
+            cs = torch.cuda.current_stream()
+            for ev in self._events:
+                cs.wait_event(ev)
+            self._pending = False
 
     @torch.no_grad()
     def step(self, lr: Optional[float] = None, max_grad_norm: Optional[float] = None):
         lr = self.lr if lr is None else lr
         self.step_count += 1
         e = self.engine
+        self.synchronize()
         norm, coef = ops.grad_norm_flat([e.grad_flat], max_grad_norm if max_grad_norm else 0.0)
         self.last_grad_norm = norm
         b1, b2 = self.betas
-        for s, t, decay in e.regions:
+
+        def upd(s, t, decay):
             ops.adamw_flat_(e.param_flat[s:t], e.grad_flat[s:t], None if self.master is None else self.master[s:t],
                             self.exp_avg[s:t], self.exp_avg_sq[s:t], coef, lr, b1, b2, self.eps,
                             self.weight_decay if decay else 0.0, self.step_count)
+
+        if getattr(self, "overlap", False):
+            st = self._stream
+            st.wait_stream(torch.cuda.current_stream())
+            coef.record_stream(st)
+            self._coef = coef
+            with torch.cuda.stream(st):
+                for rs, ev in zip(self._groups, self._events):
+                    for s, t, decay in rs:
+                        upd(s, t, decay)
+                    ev.record(st)
+            self._pending = True
+            return norm
+        for s, t, decay in e.regions:
+            upd(s, t, decay)
         return norm
 
     def state_dict(self) -> Dict:
+        self.synchronize()
         return {"step": self.step_count, "exp_avg": self.exp_avg, "exp_avg_sq": self.exp_avg_sq,
                 "master": self.master, "lr": self.lr, "betas": self.betas, "eps": self.eps,
                 "weight_decay": self.weight_decay}

@@ -112,6 +112,8 @@ class SFTTrainer:
         self.optimizer = FlatAdamW(self.engine, lr=args.learning_rate, betas=(args.adam_beta1, args.adam_beta2),
                                    eps=args.adam_epsilon, weight_decay=args.weight_decay,
                                    master_weights=args.master_weights)
+        if args.optimizer_overlap and dev.type == "cuda":
+            self.optimizer.enable_overlap(model)
         self.scheduler: Optional[LRScheduler] = None
         # ------------------------------------------------------------ callbacks / state
         self.state = TrainerState(is_world_process_zero=self.dist.is_main)
@@ -198,6 +200,7 @@ class SFTTrainer:
         if self.eval_dataset is None:
             return {}
         t0 = time.time()
+        self.optimizer.synchronize()
         self.model.eval()
         acc = torch.zeros(5, device=self.dist.device)  # loss_sum, correct, entropy_sum, valid, samples
         loader = self.get_eval_dataloader()
@@ -231,6 +234,7 @@ class SFTTrainer:
         self.control = self.callback_handler.call("on_log", self.args, self.state, self.control, logs=logs)
 
     def _save_checkpoint(self):
+        self.optimizer.synchronize()
         a = self.args
         path = os.path.join(a.output_dir, f"checkpoint-{self.state.global_step}")
         barrier()
@@ -246,6 +250,7 @@ class SFTTrainer:
 
     def save_model(self, output_dir: Optional[str] = None):
         output_dir = output_dir or self.args.output_dir
+        self.optimizer.synchronize()
         if self.dist.is_main:
             ckpt.save_pretrained(self.model, output_dir, tokenizer=self.tokenizer)
         barrier()
@@ -380,6 +385,7 @@ class SFTTrainer:
                 m = self.evaluate()
                 self._update_best(m, None)
             self.control = self.callback_handler.call("on_epoch_end", a, self.state, self.control)
+        self.optimizer.synchronize()
         if torch.cuda.is_available():
             torch.cuda.synchronize()
         runtime = time.time() - t_start

@@ -1,0 +1,50 @@
+"""Micro-benchmark of the flash-attention kernels (SmolLM3 shape: 8 x 512 tokens, 16q/4kv, d128).
+Interleaves implementations in one process (CDNA guide rule 24) and reports median TFLOP/s."""
+import math
+import os
+import statistics
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import torch  # noqa: E402
+
+from llm_fine_tune_distributed_amd.ops import _ext  # noqa: E402
+
+assert _ext.load(), _ext.load_error()
+B, T, NQ, NKV, D = int(os.environ.get("B", 8)), int(os.environ.get("T", 512)), 16, 4, 128
+M = B * T
+cu = torch.arange(0, (B + 1) * T, T, dtype=torch.int32, device="cuda")
+qkv = torch.randn(M, (NQ + 2 * NKV) * D, device="cuda", dtype=torch.bfloat16)
+dout = torch.randn(M, NQ * D, device="cuda", dtype=torch.bfloat16)
+sc = 1 / math.sqrt(D)
+flops_f = 4.0 * B * NQ * T * T * D / 2  # causal
+ops = _ext.ops()
+
+
+def timeit(fn, n=20):
+    for _ in range(3):
+        fn()
+    ts = []
+    for _ in range(n):
+        s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        s.record()
+        fn()
+        e.record()
+        torch.cuda.synchronize()
+        ts.append(s.elapsed_time(e))
+    return statistics.median(ts)
+
+
+res = {}
+for rnd in range(3):
+    for impl in ("1", "2"):
+        os.environ["SFTAMD_ATTN_IMPL"] = impl
+        out, lse = ops.flash_fwd(qkv, cu, T, NQ, NKV, D, sc, True)
+        tf = timeit(lambda: ops.flash_fwd(qkv, cu, T, NQ, NKV, D, sc, True))
+        tb = timeit(lambda: ops.flash_bwd(dout, qkv, out, lse, cu, T, NQ, NKV, D, sc, True))
+        res.setdefault(impl, []).append((tf, tb))
+for impl, v in res.items():
+    tf = statistics.median(x[0] for x in v)
+    tb = statistics.median(x[1] for x in v)
+    print(f"impl {impl}: fwd {tf*1e3:.1f} us ({flops_f/tf/1e9:.0f} TFLOP/s)  bwd {tb*1e3:.1f} us "
+          f"({2.5*flops_f/tb/1e9:.0f} TFLOP/s)")
