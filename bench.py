@@ -41,6 +41,8 @@ def main():
     ap.add_argument("--seq", type=int, default=512)
     ap.add_argument("--bucket-mb", type=float, default=float(os.environ.get("SFTAMD_BUCKET_MB", "64")))
     ap.add_argument("--packing", action="store_true")
+    ap.add_argument("--freeze-policy", default="full", choices=["full", "last_n_layers", "lora"])
+    ap.add_argument("--no-master-weights", action="store_true")
     ap.add_argument("--tunableop", default=os.environ.get("SFTAMD_TUNABLEOP", "auto"),
                     help="auto: load the committed GEMM selections; tune: tune missing shapes into it; off")
     ap.add_argument("--profile-steps", type=int, default=0)
@@ -68,7 +70,8 @@ def main():
                      gradient_accumulation_steps=a.ga, learning_rate=5e-5 * st.world_size, max_grad_norm=1.0,
                      bf16=True, gradient_checkpointing=False, max_length=a.seq, packing=a.packing,
                      ddp_bucket_cap_mb=a.bucket_mb, dataloader_drop_last=True, jsonl_log=False, logging_steps=0,
-                     optimizer_overlap=not a.no_overlap)
+                     optimizer_overlap=not a.no_overlap, freeze_policy=a.freeze_policy,
+                     master_weights=not a.no_master_weights)
     trainer = SFTTrainer(model=model, args=args, train_dataset=ds)
     loader = trainer.get_train_dataloader()
     it = iter(loader)
@@ -101,16 +104,18 @@ def main():
     samples = a.micro_batch * a.ga * st.world_size * a.steps
     value = samples / dt
     tok_s = value * a.seq
-    mfu = tok_s * cfg.flops_per_token(a.seq) / (2.5e15 * st.world_size)
+    mfu = tok_s * cfg.flops_per_token(a.seq) / (2.5e15 * st.world_size) if a.freeze_policy == "full" else None
     if st.is_main:
         rec = {
-            "metric": "samples/sec SmolLM3-3B full SFT bf16 (DDP)",
+            "metric": ("samples/sec SmolLM3-3B full SFT bf16 (DDP)" if a.model == "smollm3-3b" and a.freeze_policy == "full"
+                       else f"samples/sec {a.model} {a.freeze_policy} SFT bf16 (DDP)"),
             "value": round(value, 3), "unit": "samples/s", "n_gpus": st.world_size, "steps": a.steps,
             "warmup": a.warmup, "ms_per_step": round(ms, 3), "higher_is_better": True, "scaling": "weak",
             "vs_baseline": None, "dtype": "bf16", "data": "synthetic (random tokens, random-init weights)",
-            "config": {"model": "SmolLM3-3B", "global_batch": a.micro_batch * a.ga * st.world_size,
+            "config": {"model": {"smollm3-3b": "SmolLM3-3B", "llama3-8b": "Llama-3-8B"}.get(a.model, a.model),
+                       "freeze_policy": a.freeze_policy, "global_batch": a.micro_batch * a.ga * st.world_size,
                        "per_device_batch": a.micro_batch, "gradient_accumulation_steps": a.ga, "seq_len": a.seq,
-                       "parallelism": f"dp{st.world_size}", "optimizer": "AdamW fp32-master (fused HIP)",
+                       "parallelism": f"dp{st.world_size}", "optimizer": "AdamW fp32-master (fused HIP)" if not a.no_master_weights else "AdamW bf16-params fp32-moments (fused HIP)",
                        "samples_per_device_per_step": a.micro_batch * a.ga,
                        "gradient_checkpointing": False, "packing": a.packing},
             "tokens_per_sec": round(tok_s, 1), "mfu": round(mfu, 4), "final_loss": round(loss, 4),

@@ -45,12 +45,32 @@ __device__ __forceinline__ void adam_elem(float& w, float g, float& m, float& v,
   w = w * (1.f - lr * wd) - lr * rbc1 * m / denom;
 }
 
-template <bool MASTER>
+// Stateless per-element hash (Wang/PCG-style mix) for stochastic rounding.
+__device__ __forceinline__ unsigned sr_hash(unsigned long long i, unsigned seed) {
+  unsigned x = (unsigned)i * 0x9E3779B9u ^ (unsigned)(i >> 32) * 0x85EBCA6Bu ^ seed * 0xC2B2AE35u;
+  x ^= x >> 16;
+  x *= 0x7FEB352Du;
+  x ^= x >> 15;
+  x *= 0x846CA68Bu;
+  x ^= x >> 16;
+  return x;
+}
+
+// fp32 -> bf16 with stochastic rounding: add uniform noise below the bf16 ulp, then truncate.
+// E[bf16(w)] = w, so pure-bf16 weights do not lose small Adam updates to round-to-nearest.
+__device__ __forceinline__ u16 f2bf_sr(float f, unsigned r) {
+  unsigned u = __float_as_uint(f);
+  if ((u & 0x7f800000u) == 0x7f800000u) return f2bf(f);  // inf / nan
+  u += (r & 0xffffu);
+  return (u16)(u >> 16);
+}
+
+template <bool MASTER, bool SR>
 __global__ __launch_bounds__(256) void adamw_kernel(u16* __restrict__ p, const u16* __restrict__ g,
                                                     float* __restrict__ master, float* __restrict__ mom,
                                                     float* __restrict__ var, const float* __restrict__ coef, long n,
                                                     float lr, float b1, float b2, float eps, float wd, float rbc1,
-                                                    float rsbc2) {
+                                                    float rsbc2, unsigned seed) {
   const float c = coef[0];
   const long nv = n / 8;
   for (long v = blockIdx.x * 256L + threadIdx.x; v < nv; v += (long)gridDim.x * 256) {
@@ -77,7 +97,14 @@ __global__ __launch_bounds__(256) void adamw_kernel(u16* __restrict__ p, const u
     *(float4*)(mom + o + 4) = *(float4*)&mm[4];
     *(float4*)(var + o) = *(float4*)&vv[0];
     *(float4*)(var + o + 4) = *(float4*)&vv[4];
-    *(uint4*)(p + o) = pack8(w);
+    if (SR) {
+      u16 b[8];
+#pragma unroll
+      for (int i = 0; i < 8; ++i) b[i] = f2bf_sr(w[i], sr_hash(o + i, seed));
+      *(uint4*)(p + o) = make_uint4(b[0] | (b[1] << 16), b[2] | (b[3] << 16), b[4] | (b[5] << 16), b[6] | (b[7] << 16));
+    } else {
+      *(uint4*)(p + o) = pack8(w);
+    }
   }
   for (long i = nv * 8 + blockIdx.x * 256L + threadIdx.x; i < n; i += (long)gridDim.x * 256) {
     float w = MASTER ? master[i] : bf2f(p[i]);
@@ -86,13 +113,13 @@ __global__ __launch_bounds__(256) void adamw_kernel(u16* __restrict__ p, const u
     if (MASTER) master[i] = w;
     mom[i] = m;
     var[i] = vr;
-    p[i] = f2bf(w);
+    p[i] = SR ? f2bf_sr(w, sr_hash(i, seed)) : f2bf(w);
   }
 }
 
 void adamw_flat(at::Tensor param, const at::Tensor& grad, const c10::optional<at::Tensor>& master, at::Tensor exp_avg,
                 at::Tensor exp_avg_sq, const at::Tensor& clip_coef, double lr, double beta1, double beta2, double eps,
-                double weight_decay, double bc1, double bc2) {
+                double weight_decay, double bc1, double bc2, int64_t sr_seed) {
   SFT_CHECK_BF16(param);
   SFT_CHECK_BF16(grad);
   SFT_CHECK(param.is_contiguous() && grad.is_contiguous() && exp_avg.is_contiguous() && exp_avg_sq.is_contiguous(),
@@ -103,18 +130,21 @@ void adamw_flat(at::Tensor param, const at::Tensor& grad, const c10::optional<at
   if (n == 0) return;
   int grid = (int)std::min<long>(std::max<long>(1, (n / 8 + 255) / 256), 2048);
   const float rbc1 = (float)(1.0 / bc1), rsbc2 = (float)(1.0 / std::sqrt(bc2));
-  if (master.has_value() && master->defined()) {
+  const bool has_master = master.has_value() && master->defined();
+  if (has_master)
     SFT_CHECK(master->scalar_type() == at::kFloat && master->numel() == n && master->is_contiguous(), "master");
-    adamw_kernel<true><<<grid, 256, 0, cur_stream()>>>(
-        (u16*)param.data_ptr(), (const u16*)grad.data_ptr(), master->data_ptr<float>(), exp_avg.data_ptr<float>(),
+  float* mp = has_master ? master->data_ptr<float>() : nullptr;
+  const unsigned seed = (unsigned)sr_seed;
+  auto go = [&](auto ms, auto sr) {
+    constexpr bool M = decltype(ms)::value, S = decltype(sr)::value;
+    adamw_kernel<M, S><<<grid, 256, 0, cur_stream()>>>(
+        (u16*)param.data_ptr(), (const u16*)grad.data_ptr(), mp, exp_avg.data_ptr<float>(),
         exp_avg_sq.data_ptr<float>(), clip_coef.data_ptr<float>(), n, (float)lr, (float)beta1, (float)beta2,
-        (float)eps, (float)weight_decay, rbc1, rsbc2);
-  } else {
-    adamw_kernel<false><<<grid, 256, 0, cur_stream()>>>(
-        (u16*)param.data_ptr(), (const u16*)grad.data_ptr(), nullptr, exp_avg.data_ptr<float>(),
-        exp_avg_sq.data_ptr<float>(), clip_coef.data_ptr<float>(), n, (float)lr, (float)beta1, (float)beta2,
-        (float)eps, (float)weight_decay, rbc1, rsbc2);
-  }
+        (float)eps, (float)weight_decay, rbc1, rsbc2, seed);
+  };
+  if (has_master) go(std::true_type(), std::false_type());
+  else if (sr_seed != 0) go(std::false_type(), std::true_type());
+  else go(std::false_type(), std::false_type());
   SFT_LAUNCH_CHECK();
 }
 

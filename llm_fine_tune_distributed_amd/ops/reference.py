@@ -112,7 +112,7 @@ def cross_entropy(logits: torch.Tensor, labels: torch.Tensor):
 
 def adamw_(param: torch.Tensor, grad: torch.Tensor, exp_avg: torch.Tensor, exp_avg_sq: torch.Tensor,
            master: Optional[torch.Tensor], lr: float, beta1: float, beta2: float, eps: float,
-           weight_decay: float, step: int, grad_scale: float = 1.0) -> None:
+           weight_decay: float, step: int, grad_scale: float = 1.0, sr_seed: int = 0) -> None:
     """Decoupled-weight-decay Adam (torch.optim.AdamW semantics) on flat tensors, in place."""
     w = master if master is not None else param.float()
     g = grad.float() * grad_scale
@@ -125,5 +125,10 @@ def adamw_(param: torch.Tensor, grad: torch.Tensor, exp_avg: torch.Tensor, exp_a
     w.addcdiv_(exp_avg.float(), denom, value=-lr / bc1)
     if master is not None:
         param.copy_(master)
+    elif sr_seed and param.dtype == torch.bfloat16:
+        gen = torch.Generator(device=w.device).manual_seed(int(sr_seed))
+        noise = torch.randint(0, 1 << 16, w.shape, generator=gen, device=w.device, dtype=torch.int32)
+        bits = w.contiguous().view(torch.int32) + noise
+        param.copy_((bits & ~0xFFFF).view(torch.float32))
     else:
         param.copy_(w)

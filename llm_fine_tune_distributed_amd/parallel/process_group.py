@@ -60,7 +60,7 @@ def setup_distributed(backend: Optional[str] = None, timeout_s: float = 1800.0, 
         dev = torch.device("cuda", local_rank % n)
     else:
         dev = torch.device("cpu")
-    be = backend or ("nccl" if use_gpu else "gloo")
+    be = backend or os.environ.get("SFTAMD_DIST_BACKEND") or ("nccl" if use_gpu else "gloo")
     if ws > 1 and not dist.is_initialized():
         # RCCL: keep peer-to-peer (xGMI) on; async error handling = watchdog aborts on hangs.
         os.environ.setdefault("TORCH_NCCL_ASYNC_ERROR_HANDLING", "1")
@@ -86,7 +86,7 @@ def get_state() -> DistState:
 def barrier():
     if dist.is_available() and dist.is_initialized():
         st = get_state()
-        if st.backend == "nccl":
+        if st.backend == "nccl" and st.device.type == "cuda":
             dist.barrier(device_ids=[st.device.index])
         else:
             dist.barrier()

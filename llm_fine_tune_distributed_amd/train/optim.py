@@ -20,13 +20,14 @@ from .. import ops
 
 class FlatAdamW:
     def __init__(self, engine, lr: float, betas=(0.9, 0.999), eps: float = 1e-8, weight_decay: float = 0.0,
-                 master_weights: bool = True):
+                 master_weights: bool = True, stochastic_rounding: bool = True):
         self.engine = engine
         self.lr = lr
         self.betas = betas
         self.eps = eps
         self.weight_decay = weight_decay
         self.master_weights = master_weights
+        self.stochastic_rounding = stochastic_rounding and not master_weights
         self.step_count = 0
         n = engine.numel
         dev = engine.device
@@ -125,7 +126,8 @@ class FlatAdamW:
         def upd(s, t, decay):
             ops.adamw_flat_(e.param_flat[s:t], e.grad_flat[s:t], None if self.master is None else self.master[s:t],
                             self.exp_avg[s:t], self.exp_avg_sq[s:t], coef, lr, b1, b2, self.eps,
-                            self.weight_decay if decay else 0.0, self.step_count)
+                            self.weight_decay if decay else 0.0, self.step_count,
+                            sr_seed=(0x5EED + 7919 * self.step_count + s) & 0x7FFFFFFF if self.stochastic_rounding else 0)
 
         if getattr(self, "overlap", False):
             st = self._stream

@@ -1,0 +1,61 @@
+"""DDP engine on GPU tensors: 2 ranks sharing one MI355X (gloo transport, the engine's streams,
+hooks, bucket views and the HIP kernels are the same as with RCCL) == 1 rank on the same global batch.
+The RCCL/xGMI path itself runs in the driver's 8-GPU scaling bench."""
+import os
+import socket
+import tempfile
+
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+pytestmark = pytest.mark.gpu
+
+
+def _port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _run(rank, world, port, out, per_dev):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), WORLD_SIZE=str(world), RANK=str(rank),
+                      LOCAL_RANK=str(rank), SFTAMD_DIST_BACKEND="gloo")
+    import llm_fine_tune_distributed_amd.parallel.process_group as pgm
+    pgm._STATE = None
+    from llm_fine_tune_distributed_amd.data.dataset import TokenizedDataset
+    from llm_fine_tune_distributed_amd.models import build_model, tiny
+    from llm_fine_tune_distributed_amd.train import SFTConfig, SFTTrainer
+    cfg = tiny(hidden_size=256, num_attention_heads=2, num_key_value_heads=1, head_dim=128, intermediate_size=512,
+               vocab_size=1024, num_hidden_layers=3)
+    m = build_model(cfg, device="cuda", dtype=torch.bfloat16, seed=0)
+    ds = TokenizedDataset.synthetic(64, cfg.vocab_size, 20, 60, seed=3)
+    a = SFTConfig(output_dir=out, per_device_train_batch_size=per_dev, max_steps=3, learning_rate=1e-3,
+                  logging_steps=1, jsonl_log=False, save_strategy="no", dataloader_drop_last=True,
+                  ddp_bucket_cap_mb=0.5, ddp_first_bucket_mb=0.1, ddp_check_sync_every=1)
+    t = SFTTrainer(model=m, args=a, train_dataset=ds)
+    t.train()
+    t.optimizer.synchronize()
+    torch.save({"p": t.engine.param_flat.float().cpu(), "log": [h["loss"] for h in t.state.log_history if "loss" in h]},
+               os.path.join(out, f"w{world}_r{rank}.pt"))
+    pgm.cleanup_distributed()
+
+
+def test_ddp2_on_gpu_matches_single():
+    d = tempfile.mkdtemp()
+    ctx = mp.get_context("spawn")
+    for world, per_dev in ((1, 4), (2, 2)):
+        port = _port()
+        ps = [ctx.Process(target=_run, args=(r, world, port, d, per_dev)) for r in range(world)]
+        [p.start() for p in ps]
+        [p.join(timeout=300) for p in ps]
+        assert all(p.exitcode == 0 for p in ps)
+    s = torch.load(os.path.join(d, "w1_r0.pt"))
+    a = torch.load(os.path.join(d, "w2_r0.pt"))
+    b = torch.load(os.path.join(d, "w2_r1.pt"))
+    assert torch.equal(a["p"], b["p"])
+    assert a["log"] == pytest.approx(s["log"], rel=2e-2)
+    rel = (a["p"] - s["p"]).norm() / s["p"].norm()
+    assert rel < 1e-2

@@ -171,3 +171,23 @@ def test_adamw_and_norm():
     assert torch.equal(p, master.to(torch.bfloat16))
     part = _ext.ops().sumsq(g)
     assert abs(part.sum().item() - g.float().pow(2).sum().item()) / g.float().pow(2).sum().item() < 1e-5
+
+
+def test_adamw_stochastic_rounding_unbiased():
+    torch.manual_seed(0)
+    n = 1 << 20
+    p = torch.full((n,), 1.0, device=DEV).to(torch.bfloat16)
+    g = torch.ones(n, device=DEV).to(torch.bfloat16)
+    m = torch.zeros(n, device=DEV)
+    v = torch.zeros(n, device=DEV)
+    coef = torch.ones(1, device=DEV)
+    # one Adam step moves every weight by -lr (first step: m/sqrt(v) = 1); lr far below bf16 ulp(1)=2^-7
+    lr = 1e-4
+    _ext.ops().adamw_flat(p, g, None, m, v, coef, lr, 0.9, 0.999, 1e-12, 0.0, 1 - 0.9, 1 - 0.999, 1234)
+    pf = p.float()
+    assert ((pf - (1 - lr)).abs() <= 2 ** -7).all()  # within one ulp
+    assert abs(pf.mean().item() - (1 - lr)) < 2e-5  # unbiased: RNE would leave every weight at 1.0
+    p2 = torch.full((n,), 1.0, device=DEV).to(torch.bfloat16)
+    m.zero_(), v.zero_()
+    _ext.ops().adamw_flat(p2, g, None, m, v, coef, lr, 0.9, 0.999, 1e-12, 0.0, 1 - 0.9, 1 - 0.999, 0)
+    assert (p2.float() == 1.0).all()  # round-to-nearest loses the update
