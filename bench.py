@@ -118,7 +118,7 @@ def main():
                        "parallelism": f"dp{st.world_size}", "optimizer": "AdamW fp32-master (fused HIP)" if not a.no_master_weights else "AdamW bf16-params fp32-moments (fused HIP)",
                        "samples_per_device_per_step": a.micro_batch * a.ga,
                        "gradient_checkpointing": False, "packing": a.packing},
-            "tokens_per_sec": round(tok_s, 1), "mfu": round(mfu, 4), "final_loss": round(loss, 4),
+            "tokens_per_sec": round(tok_s, 1), "mfu": None if mfu is None else round(mfu, 4), "final_loss": round(loss, 4),
             "peak_mem_gb": round(torch.cuda.max_memory_allocated() / 1e9, 2),
         }
         print(json.dumps(rec), flush=True)

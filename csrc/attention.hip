@@ -23,6 +23,8 @@
 //   p(8g+j) = j<4 ? 4g+j : 16+4g+(j-4) on BOTH operands of the next MFMA.
 #include "common.h"
 
+#include <cstring>
+
 namespace sftamd {
 
 namespace attn {
@@ -443,12 +445,12 @@ struct TileRegs {
   }
 };
 
-template <bool TR, int NW>
+template <bool TR, int NW, int NBUF>
 __global__ __launch_bounds__(NW * 64) void fwd2_kernel(const u16* __restrict__ qkv, u16* __restrict__ out,
                                                        float* __restrict__ lse, const int* __restrict__ cu, int nq,
                                                        int nkv, int total, float sl2, int causal) {
   constexpr int NT = NW * 64, BM = NW * 16, TB = 64 * ROWB;
-  __shared__ __attribute__((aligned(16))) char smem[4 * TB];  // K0 V0 K1 V1
+  __shared__ __attribute__((aligned(16))) char smem[2 * NBUF * TB];  // K0 V0 (K1 V1)
   const int qb = blockIdx.x, h = blockIdx.y, b = blockIdx.z;
   const int start = cu[b], len = cu[b + 1] - start;
   const int q0 = qb * BM;
@@ -483,7 +485,7 @@ __global__ __launch_bounds__(NW * 64) void fwd2_kernel(const u16* __restrict__ q
   __syncthreads();
   for (int kt = 0; kt < nkt; ++kt) {
     const int k0 = kt * 64;
-    char* Ks = smem + (kt & 1) * 2 * TB;
+    char* Ks = smem + (NBUF == 2 ? (kt & 1) : 0) * 2 * TB;
     char* Vs = Ks + TB;
     const bool pre = kt + 1 < nkt;
     TileRegs<64, NT> tk, tv;
@@ -538,7 +540,8 @@ __global__ __launch_bounds__(NW * 64) void fwd2_kernel(const u16* __restrict__ q
       }
     }
     if (pre) {
-      char* Kn = smem + ((kt + 1) & 1) * 2 * TB;
+      if (NBUF == 1) __syncthreads();  // every wave is done reading the single buffer
+      char* Kn = smem + (NBUF == 2 ? ((kt + 1) & 1) : 0) * 2 * TB;
       tk.store(Kn, tid);
       tv.store(Kn + TB, tid);
     }
@@ -553,14 +556,14 @@ __global__ __launch_bounds__(NW * 64) void fwd2_kernel(const u16* __restrict__ q
   }
 }
 
-template <bool TR, int NW>
+template <bool TR, int NW, int NBUF>
 __global__ __launch_bounds__(NW * 64) void bwd_dq2_kernel(const u16* __restrict__ qkv, const u16* __restrict__ dout,
                                                           const float* __restrict__ lse,
                                                           const float* __restrict__ delta, const int* __restrict__ cu,
                                                           u16* __restrict__ dqkv, int nq, int nkv, int total,
                                                           float sl2, float scale, int causal) {
   constexpr int NT = NW * 64, BM = NW * 16, TB = 64 * ROWB;
-  __shared__ __attribute__((aligned(16))) char smem[4 * TB];
+  __shared__ __attribute__((aligned(16))) char smem[2 * NBUF * TB];
   const int qb = blockIdx.x, h = blockIdx.y, b = blockIdx.z;
   const int start = cu[b], len = cu[b + 1] - start;
   const int q0 = qb * BM;
@@ -601,7 +604,7 @@ __global__ __launch_bounds__(NW * 64) void bwd_dq2_kernel(const u16* __restrict_
   __syncthreads();
   for (int kt = 0; kt < nkt; ++kt) {
     const int k0 = kt * 64;
-    char* Ks = smem + (kt & 1) * 2 * TB;
+    char* Ks = smem + (NBUF == 2 ? (kt & 1) : 0) * 2 * TB;
     char* Vs = Ks + TB;
     const bool pre = kt + 1 < nkt;
     TileRegs<64, NT> tk, tv;
@@ -639,7 +642,8 @@ __global__ __launch_bounds__(NW * 64) void bwd_dq2_kernel(const u16* __restrict_
       }
     }
     if (pre) {
-      char* Kn = smem + ((kt + 1) & 1) * 2 * TB;
+      if (NBUF == 1) __syncthreads();  // every wave is done reading the single buffer
+      char* Kn = smem + (NBUF == 2 ? ((kt + 1) & 1) : 0) * 2 * TB;
       tk.store(Kn, tid);
       tv.store(Kn + TB, tid);
     }
@@ -655,7 +659,7 @@ __global__ __launch_bounds__(NW * 64) void bwd_dq2_kernel(const u16* __restrict_
 // dK/dV partials for ONE query head h (grid (key blocks, nq, nseq)); writes fp32 slab
 // part[r][token][2*nkv*D] (r = h % rep; dK at kvh*D, dV at (nkv+kvh)*D). When rep == 1 the
 // result goes straight to dqkv (bf16, dK scaled).
-template <bool TR>
+template <bool TR, int NBUF>
 __global__ __launch_bounds__(256, 2) void bwd_dkdv2_kernel(const u16* __restrict__ qkv, const u16* __restrict__ dout,
                                                            const float* __restrict__ lse,
                                                            const float* __restrict__ delta,
@@ -663,8 +667,8 @@ __global__ __launch_bounds__(256, 2) void bwd_dkdv2_kernel(const u16* __restrict
                                                            u16* __restrict__ dqkv, int nq, int nkv, int total,
                                                            float sl2, float scale, int causal) {
   constexpr int NT = 256, TB = 64 * ROWB;
-  __shared__ __attribute__((aligned(16))) char smem[4 * TB + 2 * 2 * 64 * 4];
-  float* LDs = (float*)(smem + 4 * TB);  // [buf][lse2 64 | delta 64]
+  __shared__ __attribute__((aligned(16))) char smem[2 * NBUF * TB + NBUF * 2 * 64 * 4];
+  float* LDs = (float*)(smem + 2 * NBUF * TB);  // [buf][lse2 64 | delta 64]
   const int kb = blockIdx.x, h = blockIdx.y, b = blockIdx.z;
   const int start = cu[b], len = cu[b + 1] - start;
   const int k0 = kb * 64;
@@ -714,7 +718,7 @@ __global__ __launch_bounds__(256, 2) void bwd_dkdv2_kernel(const u16* __restrict
   __syncthreads();
   for (int qt = qt0; qt < nqt; ++qt) {
     const int q0 = qt * 64;
-    const int buf = (qt - qt0) & 1;
+    const int buf = NBUF == 2 ? ((qt - qt0) & 1) : 0;
     char* Qs = smem + buf * 2 * TB;
     char* Os = Qs + TB;
     const float* Ls = LDs + buf * 128;
@@ -767,11 +771,13 @@ __global__ __launch_bounds__(256, 2) void bwd_dkdv2_kernel(const u16* __restrict
       }
     }
     if (pre) {
-      char* Qn = smem + (buf ^ 1) * 2 * TB;
+      if (NBUF == 1) __syncthreads();
+      const int nb = NBUF == 2 ? (buf ^ 1) : 0;
+      char* Qn = smem + nb * 2 * TB;
       tq.store(Qn, tid);
       to.store(Qn + TB, tid);
       if (tid < 64) {
-        float* Ln = LDs + (buf ^ 1) * 128;
+        float* Ln = LDs + nb * 128;
         Ln[tid] = pl;
         Ln[64 + tid] = pd;
       }
@@ -845,6 +851,18 @@ static int attn_impl() {
   return (e && e[0] == '1') ? 1 : 2;
 }
 
+// launch geometry for the v2 kernels: SFTAMD_ATTN_CFG="<waves fwd/dq: 4|8>,<LDS buffers: 1|2>"
+static void attn_cfg(int& nw, int& nbuf) {
+  nw = 8;
+  nbuf = 2;
+  const char* e = std::getenv("SFTAMD_ATTN_CFG");
+  if (e && e[0]) {
+    nw = (e[0] == '4') ? 4 : 8;
+    const char* c = std::strchr(e, ',');
+    if (c && c[1] == '1') nbuf = 1;
+  }
+}
+
 static int attn_variant() {
   const char* e = std::getenv("SFTAMD_ATTN_TR");
   return (e && e[0] == '0') ? 0 : 1;
@@ -862,14 +880,25 @@ std::tuple<at::Tensor, at::Tensor> flash_fwd(const at::Tensor& qkv, const at::Te
   const float sl2 = (float)scale * attn::LOG2E;
   auto cu_c = cu.contiguous();
   if (attn_impl() == 2) {
-    dim3 g2((max_seqlen + 127) / 128, nq, nseq);
-    auto go = [&](auto tr) {
+    int nw, nbuf;
+    attn_cfg(nw, nbuf);
+    auto go = [&](auto tr, auto w, auto b) {
       constexpr bool TR = decltype(tr)::value;
-      attn::fwd2_kernel<TR, 8><<<g2, 512, 0, cur_stream()>>>((const u16*)qkv.data_ptr(), (u16*)out.data_ptr(),
-                                                            lse.data_ptr<float>(), cu_c.data_ptr<int>(), nq, nkv,
-                                                            total, sl2, causal ? 1 : 0);
+      constexpr int NW = decltype(w)::value, NB = decltype(b)::value;
+      dim3 g2((max_seqlen + NW * 16 - 1) / (NW * 16), nq, nseq);
+      attn::fwd2_kernel<TR, NW, NB><<<g2, NW * 64, 0, cur_stream()>>>(
+          (const u16*)qkv.data_ptr(), (u16*)out.data_ptr(), lse.data_ptr<float>(), cu_c.data_ptr<int>(), nq, nkv,
+          total, sl2, causal ? 1 : 0);
     };
-    if (attn_variant()) go(std::true_type()); else go(std::false_type());
+    using I4 = std::integral_constant<int, 4>;
+    using I8 = std::integral_constant<int, 8>;
+    using B1 = std::integral_constant<int, 1>;
+    using B2 = std::integral_constant<int, 2>;
+    if (!attn_variant()) go(std::false_type(), I8(), B2());
+    else if (nw == 8 && nbuf == 2) go(std::true_type(), I8(), B2());
+    else if (nw == 8) go(std::true_type(), I8(), B1());
+    else if (nbuf == 2) go(std::true_type(), I4(), B2());
+    else go(std::true_type(), I4(), B1());
     SFT_LAUNCH_CHECK();
     return {out, lse};
   }
@@ -916,13 +945,16 @@ at::Tensor flash_bwd(const at::Tensor& dout, const at::Tensor& qkv, const at::Te
         cu_c.data_ptr<int>(), (u16*)dqkv.data_ptr(), nq, nkv, total, sl2, (float)scale, causal ? 1 : 0);
     SFT_LAUNCH_CHECK();
   };
-  auto run2 = [&](auto tr) {
+  int nw, nbuf;
+  attn_cfg(nw, nbuf);
+  auto run2 = [&](auto tr, auto w, auto bb) {
     constexpr bool TR = decltype(tr)::value;
+    constexpr int NW = decltype(w)::value, NB = decltype(bb)::value;
     const int rep = nq / nkv;
     at::Tensor part;
     if (rep > 1) part = at::empty({(long)rep * total * 2 * nkv * hd}, qkv.options().dtype(at::kFloat));
     dim3 gk2((max_seqlen + 63) / 64, nq, nseq);
-    attn::bwd_dkdv2_kernel<TR><<<gk2, 256, 0, cur_stream()>>>(
+    attn::bwd_dkdv2_kernel<TR, NB><<<gk2, 256, 0, cur_stream()>>>(
         (const u16*)qkv.data_ptr(), (const u16*)dout.data_ptr(), lse.data_ptr<float>(), delta.data_ptr<float>(),
         cu_c.data_ptr<int>(), rep > 1 ? part.data_ptr<float>() : nullptr, (u16*)dqkv.data_ptr(), nq, nkv, total, sl2,
         (float)scale, causal ? 1 : 0);
@@ -934,14 +966,22 @@ at::Tensor flash_bwd(const at::Tensor& dout, const at::Tensor& qkv, const at::Te
                                                                nq, nkv, rep, (float)scale);
       SFT_LAUNCH_CHECK();
     }
-    dim3 gq2((max_seqlen + 127) / 128, nq, nseq);
-    attn::bwd_dq2_kernel<TR, 8><<<gq2, 512, 0, cur_stream()>>>(
+    dim3 gq2((max_seqlen + NW * 16 - 1) / (NW * 16), nq, nseq);
+    attn::bwd_dq2_kernel<TR, NW, NB><<<gq2, NW * 64, 0, cur_stream()>>>(
         (const u16*)qkv.data_ptr(), (const u16*)dout.data_ptr(), lse.data_ptr<float>(), delta.data_ptr<float>(),
         cu_c.data_ptr<int>(), (u16*)dqkv.data_ptr(), nq, nkv, total, sl2, (float)scale, causal ? 1 : 0);
     SFT_LAUNCH_CHECK();
   };
+  using I4 = std::integral_constant<int, 4>;
+  using I8 = std::integral_constant<int, 8>;
+  using B1 = std::integral_constant<int, 1>;
+  using B2 = std::integral_constant<int, 2>;
   if (attn_impl() == 2) {
-    if (attn_variant()) run2(std::true_type()); else run2(std::false_type());
+    if (!attn_variant()) run2(std::false_type(), I8(), B2());
+    else if (nw == 8 && nbuf == 2) run2(std::true_type(), I8(), B2());
+    else if (nw == 8) run2(std::true_type(), I8(), B1());
+    else if (nbuf == 2) run2(std::true_type(), I4(), B2());
+    else run2(std::true_type(), I4(), B1());
   } else if (attn_variant()) {
     run(std::true_type());
   } else {

@@ -117,9 +117,10 @@ def test_cross_entropy(V):
     assert rel_err(lg, gref) < 2e-2
 
 
-def _attn_case(lens, nq, nkv, causal, variant, impl="2"):
+def _attn_case(lens, nq, nkv, causal, variant, impl="2", cfg=""):
     os.environ["SFTAMD_ATTN_TR"] = variant
     os.environ["SFTAMD_ATTN_IMPL"] = impl
+    os.environ["SFTAMD_ATTN_CFG"] = cfg
     torch.manual_seed(0)
     D = 128
     cu = torch.tensor([0] + list(torch.tensor(lens).cumsum(0)), dtype=torch.int32, device=DEV)
@@ -147,6 +148,11 @@ def test_flash_attention_varlen_gqa(variant, causal, impl):
 
 def test_flash_attention_mha_and_long():
     _attn_case([1000, 37], 4, 4, True, "1")
+
+
+@pytest.mark.parametrize("cfg", ["8,1", "4,2", "4,1"])
+def test_flash_attention_launch_configs(cfg):
+    _attn_case([100, 255, 64, 1, 300], 8, 2, True, "1", "2", cfg)
 
 
 @pytest.mark.parametrize("impl", ["2", "1"])

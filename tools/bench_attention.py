@@ -35,14 +35,24 @@ def timeit(fn, n=20):
     return statistics.median(ts)
 
 
+CFGS = [("1", ""), ("2", "8,2"), ("2", "8,1"), ("2", "4,2"), ("2", "4,1")]
 res = {}
+ref = None
 for rnd in range(3):
-    for impl in ("1", "2"):
+    for impl, cfg in CFGS:
         os.environ["SFTAMD_ATTN_IMPL"] = impl
+        os.environ["SFTAMD_ATTN_CFG"] = cfg
         out, lse = ops.flash_fwd(qkv, cu, T, NQ, NKV, D, sc, True)
+        dq = ops.flash_bwd(dout, qkv, out, lse, cu, T, NQ, NKV, D, sc, True)
+        if ref is None:
+            ref = (out.float(), dq.float())
+        else:
+            eo = ((out.float() - ref[0]).norm() / ref[0].norm()).item()
+            ed = ((dq.float() - ref[1]).norm() / ref[1].norm()).item()
+            assert eo < 1e-2 and ed < 1e-2, (impl, cfg, eo, ed)
         tf = timeit(lambda: ops.flash_fwd(qkv, cu, T, NQ, NKV, D, sc, True))
         tb = timeit(lambda: ops.flash_bwd(dout, qkv, out, lse, cu, T, NQ, NKV, D, sc, True))
-        res.setdefault(impl, []).append((tf, tb))
+        res.setdefault(impl + ":" + cfg, []).append((tf, tb))
 for impl, v in res.items():
     tf = statistics.median(x[0] for x in v)
     tb = statistics.median(x[1] for x in v)
