@@ -20,7 +20,7 @@ TORCH_LIBRARY(sftamd, m) {
   m.def("flash_bwd(Tensor dout, Tensor qkv, Tensor out, Tensor lse, Tensor cu_seqlens, int max_seqlen, int n_q, int n_kv, int head_dim, float scale, bool causal) -> Tensor");
   // optimizer
   m.def("sumsq(Tensor x) -> Tensor");
-  m.def("adamw_flat(Tensor(a!) param, Tensor grad, Tensor(b!)? master, Tensor(c!) exp_avg, Tensor(d!) exp_avg_sq, Tensor clip_coef, float lr, float beta1, float beta2, float eps, float weight_decay, float bc1, float bc2, int sr_seed=0) -> ()");
+  m.def("adamw_flat(Tensor(a!) param, Tensor grad, Tensor(b!)? master, Tensor(c!) exp_avg, Tensor(d!) exp_avg_sq, Tensor clip_coef, float lr, float beta1, float beta2, float eps, float weight_decay, float bc1, float bc2, int sr_seed=0, int sr_offset=0) -> ()");
   // native data pipeline (CPU)
   m.def("pack_sequences(Tensor tokens, Tensor offsets, Tensor order, int max_tokens, int pad_id, int pad_multiple) -> (Tensor, Tensor, Tensor, Tensor, Tensor)");
   m.def("pad_batch(Tensor tokens, Tensor offsets, Tensor order, int pad_id, int pad_multiple, int max_length) -> (Tensor, Tensor, Tensor)");

@@ -70,7 +70,7 @@ __global__ __launch_bounds__(256) void adamw_kernel(u16* __restrict__ p, const u
                                                     float* __restrict__ master, float* __restrict__ mom,
                                                     float* __restrict__ var, const float* __restrict__ coef, long n,
                                                     float lr, float b1, float b2, float eps, float wd, float rbc1,
-                                                    float rsbc2, unsigned seed) {
+                                                    float rsbc2, unsigned seed, long idx0) {
   const float c = coef[0];
   const long nv = n / 8;
   for (long v = blockIdx.x * 256L + threadIdx.x; v < nv; v += (long)gridDim.x * 256) {
@@ -100,7 +100,7 @@ __global__ __launch_bounds__(256) void adamw_kernel(u16* __restrict__ p, const u
     if (SR) {
       u16 b[8];
 #pragma unroll
-      for (int i = 0; i < 8; ++i) b[i] = f2bf_sr(w[i], sr_hash(o + i, seed));
+      for (int i = 0; i < 8; ++i) b[i] = f2bf_sr(w[i], sr_hash(idx0 + o + i, seed));
       *(uint4*)(p + o) = make_uint4(b[0] | (b[1] << 16), b[2] | (b[3] << 16), b[4] | (b[5] << 16), b[6] | (b[7] << 16));
     } else {
       *(uint4*)(p + o) = pack8(w);
@@ -113,13 +113,13 @@ __global__ __launch_bounds__(256) void adamw_kernel(u16* __restrict__ p, const u
     if (MASTER) master[i] = w;
     mom[i] = m;
     var[i] = vr;
-    p[i] = SR ? f2bf_sr(w, sr_hash(i, seed)) : f2bf(w);
+    p[i] = SR ? f2bf_sr(w, sr_hash(idx0 + i, seed)) : f2bf(w);
   }
 }
 
 void adamw_flat(at::Tensor param, const at::Tensor& grad, const c10::optional<at::Tensor>& master, at::Tensor exp_avg,
                 at::Tensor exp_avg_sq, const at::Tensor& clip_coef, double lr, double beta1, double beta2, double eps,
-                double weight_decay, double bc1, double bc2, int64_t sr_seed) {
+                double weight_decay, double bc1, double bc2, int64_t sr_seed, int64_t sr_offset) {
   SFT_CHECK_BF16(param);
   SFT_CHECK_BF16(grad);
   SFT_CHECK(param.is_contiguous() && grad.is_contiguous() && exp_avg.is_contiguous() && exp_avg_sq.is_contiguous(),
@@ -140,7 +140,7 @@ void adamw_flat(at::Tensor param, const at::Tensor& grad, const c10::optional<at
     adamw_kernel<M, S><<<grid, 256, 0, cur_stream()>>>(
         (u16*)param.data_ptr(), (const u16*)grad.data_ptr(), mp, exp_avg.data_ptr<float>(),
         exp_avg_sq.data_ptr<float>(), clip_coef.data_ptr<float>(), n, (float)lr, (float)beta1, (float)beta2,
-        (float)eps, (float)weight_decay, rbc1, rsbc2, seed);
+        (float)eps, (float)weight_decay, rbc1, rsbc2, seed, (long)sr_offset);
   };
   if (has_master) go(std::true_type(), std::false_type());
   else if (sr_seed != 0) go(std::false_type(), std::true_type());

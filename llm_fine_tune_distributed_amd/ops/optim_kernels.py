@@ -36,7 +36,7 @@ def grad_norm_flat(grads: Iterable[torch.Tensor], max_norm: float):
 def adamw_flat_(param: torch.Tensor, grad: torch.Tensor, master: Optional[torch.Tensor],
                 exp_avg: torch.Tensor, exp_avg_sq: torch.Tensor, clip_coef: torch.Tensor,
                 lr: float, beta1: float, beta2: float, eps: float, weight_decay: float, step: int,
-                sr_seed: int = 0) -> None:
+                sr_seed: int = 0, sr_offset: int = 0) -> None:
     """In-place AdamW on flat buffers. grad is multiplied by clip_coef (device scalar).
     Without a master copy, ``sr_seed != 0`` writes the bf16 parameters with stochastic rounding."""
     if param.numel() == 0:
@@ -46,7 +46,7 @@ def adamw_flat_(param: torch.Tensor, grad: torch.Tensor, master: Optional[torch.
     if _ext.use_hip(param):
         _ext.ops().adamw_flat(param, grad, master, exp_avg, exp_avg_sq, clip_coef,
                               float(lr), float(beta1), float(beta2), float(eps), float(weight_decay),
-                              float(bc1), float(bc2), int(sr_seed))
+                              float(bc1), float(bc2), int(sr_seed), int(sr_offset))
         return
     g = grad.float() * clip_coef.float()
     ref.adamw_(param, g, exp_avg, exp_avg_sq, master, lr, beta1, beta2, eps, weight_decay, step,

@@ -81,7 +81,11 @@ class SFTConfig:
     lora_alpha: float = 8.0
     lora_dropout: float = 0.05
     lora_target_modules: Optional[List[str]] = None
-    master_weights: bool = True             # fp32 master copy + fp32 Adam moments
+    # Reference parity: the reference updates bf16 parameters directly (no master copy,
+    # training.py:99). We do the same but with fp32 Adam moments and stochastic rounding of the
+    # bf16 write-back (unbiased); master_weights=True keeps an fp32 master copy instead.
+    master_weights: bool = False
+    stochastic_rounding: bool = True
     ddp_first_bucket_mb: float = 4.0
     ddp_broadcast_params: bool = False      # weights are identical by construction (seeded / loaded)
     ddp_check_sync_every: int = 0           # cross-rank param checksum every N steps (0 = off)

@@ -127,7 +127,8 @@ class FlatAdamW:
             ops.adamw_flat_(e.param_flat[s:t], e.grad_flat[s:t], None if self.master is None else self.master[s:t],
                             self.exp_avg[s:t], self.exp_avg_sq[s:t], coef, lr, b1, b2, self.eps,
                             self.weight_decay if decay else 0.0, self.step_count,
-                            sr_seed=(0x5EED + 7919 * self.step_count + s) & 0x7FFFFFFF if self.stochastic_rounding else 0)
+                            sr_seed=(0x5EED + 7919 * self.step_count) & 0x7FFFFFFF if self.stochastic_rounding else 0,
+                            sr_offset=s)
 
         if getattr(self, "overlap", False):
             st = self._stream

@@ -111,7 +111,8 @@ class SFTTrainer:
                                 broadcast_params=args.ddp_broadcast_params)
         self.optimizer = FlatAdamW(self.engine, lr=args.learning_rate, betas=(args.adam_beta1, args.adam_beta2),
                                    eps=args.adam_epsilon, weight_decay=args.weight_decay,
-                                   master_weights=args.master_weights)
+                                   master_weights=args.master_weights,
+                                   stochastic_rounding=args.stochastic_rounding)
         if args.optimizer_overlap and dev.type == "cuda":
             self.optimizer.enable_overlap(model)
         self.scheduler: Optional[LRScheduler] = None
