@@ -832,6 +832,434 @@ __global__ __launch_bounds__(256) void dkdv_reduce_kernel(const float* __restric
   }
 }
 
+// ============================================================================== v3 kernels
+// VALU diet for the v2 structure (the v2 main loops issued ~7 VALU per MFMA: rocprofv3 showed
+// SQ_INSTS_VALU ~ 10x the MFMA count). Changes, all wave-uniform:
+// * LDS operand addresses are per-lane constants computed once: 4 row-read bases (one per
+//   k-step) and 8 transposed-read bases (one per 16-column block); tile / k-step / half-tile
+//   displacements are compile-time immediates of the ds_read instructions;
+// * causal/length masks are applied only on tiles that straddle the diagonal or the sequence end;
+// * the softmax scale is folded into the exponent (one FMA per score), the running max is taken
+//   on raw scores (v_max3), and O/l are rescaled only when the row max grows by more than
+//   THR = 8 (log2 domain; T13 deferred rescale: P stays <= 2^8, exact in bf16 exponent range);
+// * full tiles are staged without per-row bounds checks; one LDS buffer (register prefetch).
+constexpr float THR = 8.f;
+
+struct Offs {
+  int row[4];  // frag_row bases, k-step s
+  int tr[8];   // frag_tr bases, column block dt
+  __device__ __forceinline__ void init(int lane) {
+    const int g = lane >> 4, r = lane & 15;
+#pragma unroll
+    for (int s = 0; s < 4; ++s) row[s] = img_off(r, 4 * s + g);
+    const int q = r >> 2, p = r & 3, r0 = 4 * g + q;
+#pragma unroll
+    for (int dt = 0; dt < 8; ++dt) tr[dt] = img_off(r0, 2 * dt + (p >> 1)) + 8 * (p & 1);
+  }
+};
+
+__device__ __forceinline__ bf16x8 lds_row(const char* base, int off) { return *(const bf16x8*)(base + off); }
+
+__device__ __forceinline__ bf16x8 lds_tr(const char* base, int off) {
+  typedef __attribute__((address_space(3))) s16x4 lds_s4;
+  s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4*)(base + off));
+  s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4*)(base + off + 16 * ROWB));
+  typedef __attribute__((ext_vector_type(8))) short s16x8;
+  s16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+  return __builtin_bit_cast(bf16x8, v);
+}
+
+template <int R, int NT>
+struct Stage {
+  static constexpr int N = (R * 16) / NT;
+  uint4 v[N];
+  __device__ __forceinline__ void load(const u16* __restrict__ g, long ld, int nvalid, int tid) {
+    const int r = tid >> 4, ch = tid & 15;
+    const u16* p = g + (long)r * ld + ch * 8;
+    if (nvalid >= R) {
+#pragma unroll
+      for (int it = 0; it < N; ++it) v[it] = *(const uint4*)(p + (long)it * (NT / 16) * ld);
+    } else {
+#pragma unroll
+      for (int it = 0; it < N; ++it)
+        v[it] = (r + it * (NT / 16) < nvalid) ? *(const uint4*)(p + (long)it * (NT / 16) * ld) : make_uint4(0, 0, 0, 0);
+    }
+  }
+  __device__ __forceinline__ void store(char* lds, int tid) const {
+    const int off = img_off(tid >> 4, tid & 15);  // rows advance by NT/16 (multiple of 16): same swizzle
+#pragma unroll
+    for (int it = 0; it < N; ++it) *(uint4*)(lds + off + it * (NT / 16) * ROWB) = v[it];
+  }
+};
+
+template <int NW>
+__global__ __launch_bounds__(NW * 64) void fwd3_kernel(const u16* __restrict__ qkv, u16* __restrict__ out,
+                                                       float* __restrict__ lse, const int* __restrict__ cu, int nq,
+                                                       int nkv, int total, float sl2, int causal) {
+  constexpr int NT = NW * 64, BM = NW * 16, TB = 64 * ROWB;
+  __shared__ __attribute__((aligned(16))) char smem[2 * TB];
+  char* Ks = smem;
+  char* Vs = smem + TB;
+  const int qb = blockIdx.x, h = blockIdx.y, b = blockIdx.z;
+  const int start = cu[b], len = cu[b + 1] - start;
+  const int q0 = qb * BM;
+  if (q0 >= len) return;
+  const int kvh = h / (nq / nkv);
+  const long ld = (long)(nq + 2 * nkv) * D;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, g = lane >> 4;
+  const int wfirst = q0 + wave * 16;
+  const int qrow = wfirst + (lane & 15);
+  const bool qok = qrow < len;
+  const u16* kbase = qkv + (long)start * ld + (nq + kvh) * D;
+  const u16* vbase = qkv + (long)start * ld + (nq + nkv + kvh) * D;
+  const int nkb = (len + 63) / 64;
+  const int nkt = causal ? min((q0 + BM + 63) / 64, nkb) : nkb;
+  Offs off;
+  off.init(lane);
+  {
+    Stage<64, NT> tk, tv;
+    tk.load(kbase, ld, len, tid);
+    tv.load(vbase, ld, len, tid);
+    tk.store(Ks, tid);
+    tv.store(Vs, tid);
+  }
+  bf16x8 qf[4];
+  {
+    const u16* qp = qkv + (long)(start + qrow) * ld + h * D + 8 * g;
+#pragma unroll
+    for (int s = 0; s < 4; ++s) qf[s] = load_frag_global(qp + 32 * s, qok);
+  }
+  f32x4 o[8];
+#pragma unroll
+  for (int dt = 0; dt < 8; ++dt) o[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
+  float m = -1e30f, l = 0.f;
+  __syncthreads();
+  for (int kt = 0; kt < nkt; ++kt) {
+    const int k0 = kt * 64;
+    const bool pre = kt + 1 < nkt;
+    Stage<64, NT> tk, tv;
+    if (pre) {
+      tk.load(kbase + (long)(k0 + 64) * ld, ld, len - k0 - 64, tid);
+      tv.load(vbase + (long)(k0 + 64) * ld, ld, len - k0 - 64, tid);
+    }
+    if (!causal || k0 <= wfirst + 15) {
+      f32x4 sc[4];
+#pragma unroll
+      for (int nt = 0; nt < 4; ++nt) {
+        sc[nt] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int s = 0; s < 4; ++s) sc[nt] = mfma(lds_row(Ks, off.row[s] + nt * 16 * ROWB), qf[s], sc[nt]);
+      }
+      const bool need_mask = (k0 + 64 > len) || (causal && k0 + 63 > wfirst);
+      if (need_mask) {
+#pragma unroll
+        for (int nt = 0; nt < 4; ++nt)
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const int key = k0 + 16 * nt + 4 * g + i;
+            if (key >= len || (causal && key > qrow)) sc[nt][i] = -INFINITY;
+          }
+      }
+      float tmax = fmaxf(fmaxf(fmaxf(sc[0][0], sc[0][1]), fmaxf(sc[0][2], sc[0][3])),
+                         fmaxf(fmaxf(sc[1][0], sc[1][1]), fmaxf(sc[1][2], sc[1][3])));
+      tmax = fmaxf(tmax, fmaxf(fmaxf(fmaxf(sc[2][0], sc[2][1]), fmaxf(sc[2][2], sc[2][3])),
+                               fmaxf(fmaxf(sc[3][0], sc[3][1]), fmaxf(sc[3][2], sc[3][3]))));
+      tmax = fmaxf(tmax, __shfl_xor(tmax, 16, 64));
+      tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64));
+      tmax *= sl2;
+      if (__any(tmax > m + THR)) {  // deferred rescale (rare after the first tiles)
+        const float mnew = fmaxf(m, tmax);
+        const float alpha = exp2f(m - mnew);
+        l *= alpha;
+#pragma unroll
+        for (int dt = 0; dt < 8; ++dt) o[dt] *= alpha;
+        m = mnew;
+      }
+      float rs = 0.f;
+#pragma unroll
+      for (int nt = 0; nt < 4; ++nt)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const float p = exp2f(fmaf(sc[nt][i], sl2, -m));
+          sc[nt][i] = p;
+          rs += p;
+        }
+      rs += __shfl_xor(rs, 16, 64);
+      rs += __shfl_xor(rs, 32, 64);
+      l += rs;
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        const bf16x8 pb = pack_acc(sc[2 * ks], sc[2 * ks + 1]);
+#pragma unroll
+        for (int dt = 0; dt < 8; ++dt) o[dt] = mfma(lds_tr(Vs, off.tr[dt] + ks * 32 * ROWB), pb, o[dt]);
+      }
+    }
+    if (pre) {
+      __syncthreads();
+      tk.store(Ks, tid);
+      tv.store(Vs, tid);
+    }
+    __syncthreads();
+  }
+  if (qok) {
+    const float inv = 1.f / l;
+    u16* op = out + (long)(start + qrow) * nq * D + h * D + 4 * g;
+#pragma unroll
+    for (int dt = 0; dt < 8; ++dt) store4(op + 16 * dt, o[dt], inv);
+    if (g == 0) lse[(long)h * total + start + qrow] = (m + log2f(l)) * LN2;
+  }
+}
+
+template <int NW>
+__global__ __launch_bounds__(NW * 64) void bwd_dq3_kernel(const u16* __restrict__ qkv, const u16* __restrict__ dout,
+                                                          const float* __restrict__ lse,
+                                                          const float* __restrict__ delta, const int* __restrict__ cu,
+                                                          u16* __restrict__ dqkv, int nq, int nkv, int total,
+                                                          float sl2, float scale, int causal) {
+  constexpr int NT = NW * 64, BM = NW * 16, TB = 64 * ROWB;
+  __shared__ __attribute__((aligned(16))) char smem[2 * TB];
+  char* Ks = smem;
+  char* Vs = smem + TB;
+  const int qb = blockIdx.x, h = blockIdx.y, b = blockIdx.z;
+  const int start = cu[b], len = cu[b + 1] - start;
+  const int q0 = qb * BM;
+  if (q0 >= len) return;
+  const int kvh = h / (nq / nkv);
+  const long ld = (long)(nq + 2 * nkv) * D;
+  const long ldo = (long)nq * D;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, g = lane >> 4;
+  const int wfirst = q0 + wave * 16;
+  const int qrow = wfirst + (lane & 15);
+  const bool qok = qrow < len;
+  const u16* kbase = qkv + (long)start * ld + (nq + kvh) * D;
+  const u16* vbase = qkv + (long)start * ld + (nq + nkv + kvh) * D;
+  const int nkb = (len + 63) / 64;
+  const int nkt = causal ? min((q0 + BM + 63) / 64, nkb) : nkb;
+  Offs off;
+  off.init(lane);
+  {
+    Stage<64, NT> tk, tv;
+    tk.load(kbase, ld, len, tid);
+    tv.load(vbase, ld, len, tid);
+    tk.store(Ks, tid);
+    tv.store(Vs, tid);
+  }
+  bf16x8 qf[4], df[4];
+  {
+    const u16* qp = qkv + (long)(start + qrow) * ld + h * D + 8 * g;
+    const u16* dp = dout + (long)(start + qrow) * ldo + h * D + 8 * g;
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      qf[s] = load_frag_global(qp + 32 * s, qok);
+      df[s] = load_frag_global(dp + 32 * s, qok);
+    }
+  }
+  const float lse2 = qok ? lse[(long)h * total + start + qrow] * LOG2E : 0.f;
+  const float dl = qok ? delta[(long)h * total + start + qrow] : 0.f;
+  f32x4 dq[8];
+#pragma unroll
+  for (int dt = 0; dt < 8; ++dt) dq[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
+  __syncthreads();
+  for (int kt = 0; kt < nkt; ++kt) {
+    const int k0 = kt * 64;
+    const bool pre = kt + 1 < nkt;
+    Stage<64, NT> tk, tv;
+    if (pre) {
+      tk.load(kbase + (long)(k0 + 64) * ld, ld, len - k0 - 64, tid);
+      tv.load(vbase + (long)(k0 + 64) * ld, ld, len - k0 - 64, tid);
+    }
+    if (!causal || k0 <= wfirst + 15) {
+      f32x4 sc[4], dp[4];
+#pragma unroll
+      for (int nt = 0; nt < 4; ++nt) {
+        sc[nt] = f32x4{0.f, 0.f, 0.f, 0.f};
+        dp[nt] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+          sc[nt] = mfma(lds_row(Ks, off.row[s] + nt * 16 * ROWB), qf[s], sc[nt]);
+          dp[nt] = mfma(lds_row(Vs, off.row[s] + nt * 16 * ROWB), df[s], dp[nt]);
+        }
+      }
+      const bool need_mask = (k0 + 64 > len) || (causal && k0 + 63 > wfirst) || (q0 + BM > len);
+#pragma unroll
+      for (int nt = 0; nt < 4; ++nt)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          float p = exp2f(fmaf(sc[nt][i], sl2, -lse2));
+          if (need_mask) {
+            const int key = k0 + 16 * nt + 4 * g + i;
+            if (key >= len || (causal && key > qrow) || !qok) p = 0.f;
+          }
+          dp[nt][i] = p * (dp[nt][i] - dl);
+        }
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        const bf16x8 db = pack_acc(dp[2 * ks], dp[2 * ks + 1]);
+#pragma unroll
+        for (int dt = 0; dt < 8; ++dt) dq[dt] = mfma(lds_tr(Ks, off.tr[dt] + ks * 32 * ROWB), db, dq[dt]);
+      }
+    }
+    if (pre) {
+      __syncthreads();
+      tk.store(Ks, tid);
+      tv.store(Vs, tid);
+    }
+    __syncthreads();
+  }
+  if (qok) {
+    u16* qp = dqkv + (long)(start + qrow) * ld + h * D + 4 * g;
+#pragma unroll
+    for (int dt = 0; dt < 8; ++dt) store4(qp + 16 * dt, dq[dt], scale);
+  }
+}
+
+__global__ __launch_bounds__(256, 2) void bwd_dkdv3_kernel(const u16* __restrict__ qkv, const u16* __restrict__ dout,
+                                                           const float* __restrict__ lse,
+                                                           const float* __restrict__ delta,
+                                                           const int* __restrict__ cu, float* __restrict__ part,
+                                                           u16* __restrict__ dqkv, int nq, int nkv, int total,
+                                                           float sl2, float scale, int causal) {
+  constexpr int NT = 256, TB = 64 * ROWB;
+  __shared__ __attribute__((aligned(16))) char smem[2 * TB + 2 * 64 * 4];
+  char* Qs = smem;
+  char* Os = smem + TB;
+  float* Ls = (float*)(smem + 2 * TB);
+  float* Dl = Ls + 64;
+  const int kb = blockIdx.x, h = blockIdx.y, b = blockIdx.z;
+  const int start = cu[b], len = cu[b + 1] - start;
+  const int k0 = kb * 64;
+  if (k0 >= len) return;
+  const int rep = nq / nkv;
+  const int kvh = h / rep, r = h - kvh * rep;
+  const long ld = (long)(nq + 2 * nkv) * D;
+  const long ldo = (long)nq * D;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, g = lane >> 4;
+  const int wfirst = k0 + wave * 16;
+  const int key = wfirst + (lane & 15);
+  const bool kok = key < len;
+  const u16* qbase = qkv + (long)start * ld + h * D;
+  const u16* obase = dout + (long)start * ldo + h * D;
+  const float* lbase = lse + (long)h * total + start;
+  const float* dbase = delta + (long)h * total + start;
+  const int qt0 = causal ? kb : 0;
+  const int nqt = (len + 63) / 64;
+  Offs off;
+  off.init(lane);
+  {
+    const int q0 = qt0 * 64, qv = len - q0;
+    Stage<64, NT> tq, to;
+    tq.load(qbase + (long)q0 * ld, ld, qv, tid);
+    to.load(obase + (long)q0 * ldo, ldo, qv, tid);
+    tq.store(Qs, tid);
+    to.store(Os, tid);
+    if (tid < 64) {
+      Ls[tid] = tid < qv ? lbase[q0 + tid] * LOG2E : 0.f;
+      Dl[tid] = tid < qv ? dbase[q0 + tid] : 0.f;
+    }
+  }
+  bf16x8 kf[4], vf[4];
+  {
+    const u16* kp = qkv + (long)(start + key) * ld + (nq + kvh) * D + 8 * g;
+    const u16* vp = qkv + (long)(start + key) * ld + (nq + nkv + kvh) * D + 8 * g;
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      kf[s] = load_frag_global(kp + 32 * s, kok);
+      vf[s] = load_frag_global(vp + 32 * s, kok);
+    }
+  }
+  f32x4 dk[8], dv[8];
+#pragma unroll
+  for (int dt = 0; dt < 8; ++dt) {
+    dk[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
+    dv[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
+  }
+  __syncthreads();
+  for (int qt = qt0; qt < nqt; ++qt) {
+    const int q0 = qt * 64;
+    const bool pre = qt + 1 < nqt;
+    Stage<64, NT> tq, to;
+    float pl = 0.f, pd = 0.f;
+    if (pre) {
+      const int qn = q0 + 64, qv = len - qn;
+      tq.load(qbase + (long)qn * ld, ld, qv, tid);
+      to.load(obase + (long)qn * ldo, ldo, qv, tid);
+      if (tid < 64 && tid < qv) {
+        pl = lbase[qn + tid] * LOG2E;
+        pd = dbase[qn + tid];
+      }
+    }
+    if (!causal || wfirst <= q0 + 63) {
+      f32x4 sc[4], dp[4];
+#pragma unroll
+      for (int mt = 0; mt < 4; ++mt) {
+        sc[mt] = f32x4{0.f, 0.f, 0.f, 0.f};
+        dp[mt] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+          sc[mt] = mfma(lds_row(Qs, off.row[s] + mt * 16 * ROWB), kf[s], sc[mt]);
+          dp[mt] = mfma(lds_row(Os, off.row[s] + mt * 16 * ROWB), vf[s], dp[mt]);
+        }
+      }
+      const bool need_mask = (q0 + 64 > len) || (causal && wfirst + 15 > q0);
+#pragma unroll
+      for (int mt = 0; mt < 4; ++mt) {
+        const float4 L4 = *(const float4*)(Ls + 16 * mt + 4 * g);
+        const float4 D4 = *(const float4*)(Dl + 16 * mt + 4 * g);
+        const float Lv[4] = {L4.x, L4.y, L4.z, L4.w}, Dv[4] = {D4.x, D4.y, D4.z, D4.w};
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          float p = exp2f(fmaf(sc[mt][i], sl2, -Lv[i]));
+          if (need_mask) {
+            const int q = q0 + 16 * mt + 4 * g + i;
+            if (q >= len || (causal && key > q)) p = 0.f;
+          }
+          sc[mt][i] = p;
+          dp[mt][i] = p * (dp[mt][i] - Dv[i]);
+        }
+      }
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        const bf16x8 pb = pack_acc(sc[2 * ks], sc[2 * ks + 1]);
+        const bf16x8 db = pack_acc(dp[2 * ks], dp[2 * ks + 1]);
+#pragma unroll
+        for (int dt = 0; dt < 8; ++dt) {
+          dv[dt] = mfma(lds_tr(Os, off.tr[dt] + ks * 32 * ROWB), pb, dv[dt]);
+          dk[dt] = mfma(lds_tr(Qs, off.tr[dt] + ks * 32 * ROWB), db, dk[dt]);
+        }
+      }
+    }
+    if (pre) {
+      __syncthreads();
+      tq.store(Qs, tid);
+      to.store(Os, tid);
+      if (tid < 64) {
+        Ls[tid] = pl;
+        Dl[tid] = pd;
+      }
+    }
+    __syncthreads();
+  }
+  if (!kok) return;
+  if (rep == 1) {
+    u16* kp = dqkv + (long)(start + key) * ld + (nq + kvh) * D + 4 * g;
+    u16* vp = dqkv + (long)(start + key) * ld + (nq + nkv + kvh) * D + 4 * g;
+#pragma unroll
+    for (int dt = 0; dt < 8; ++dt) {
+      store4(kp + 16 * dt, dk[dt], scale);
+      store4(vp + 16 * dt, dv[dt], 1.f);
+    }
+    return;
+  }
+  const long pld = 2L * nkv * D;
+  float* pk = part + ((long)r * total + start + key) * pld + kvh * D + 4 * g;
+  float* pv = pk + (long)nkv * D;
+#pragma unroll
+  for (int dt = 0; dt < 8; ++dt) {
+    *(float4*)(pk + 16 * dt) = make_float4(dk[dt][0], dk[dt][1], dk[dt][2], dk[dt][3]);
+    *(float4*)(pv + 16 * dt) = make_float4(dv[dt][0], dv[dt][1], dv[dt][2], dv[dt][3]);
+  }
+}
+
 }  // namespace attn
 
 static void check_attn_args(const at::Tensor& qkv, const at::Tensor& cu, int64_t nq, int64_t nkv, int64_t hd) {
@@ -848,7 +1276,9 @@ static void check_attn_args(const at::Tensor& qkv, const at::Tensor& cu, int64_t
 // implementation: 2 = double-buffered v2 kernels (default), 1 = v1 (single-buffered)
 static int attn_impl() {
   const char* e = std::getenv("SFTAMD_ATTN_IMPL");
-  return (e && e[0] == '1') ? 1 : 2;
+  if (e && e[0] == '1') return 1;
+  if (e && e[0] == '2') return 2;
+  return 3;
 }
 
 // launch geometry for the v2 kernels: SFTAMD_ATTN_CFG="<waves fwd/dq: 4|8>,<LDS buffers: 1|2>"
@@ -879,6 +1309,20 @@ std::tuple<at::Tensor, at::Tensor> flash_fwd(const at::Tensor& qkv, const at::Te
   dim3 grid((max_seqlen + 63) / 64, nq, nseq);
   const float sl2 = (float)scale * attn::LOG2E;
   auto cu_c = cu.contiguous();
+  if (attn_impl() == 3) {
+    int nw, nbuf;
+    attn_cfg(nw, nbuf);
+    auto go3 = [&](auto w) {
+      constexpr int NW = decltype(w)::value;
+      dim3 g3((max_seqlen + NW * 16 - 1) / (NW * 16), nq, nseq);
+      attn::fwd3_kernel<NW><<<g3, NW * 64, 0, cur_stream()>>>((const u16*)qkv.data_ptr(), (u16*)out.data_ptr(),
+                                                             lse.data_ptr<float>(), cu_c.data_ptr<int>(), nq, nkv,
+                                                             total, sl2, causal ? 1 : 0);
+    };
+    if (nw == 4) go3(std::integral_constant<int, 4>()); else go3(std::integral_constant<int, 8>());
+    SFT_LAUNCH_CHECK();
+    return {out, lse};
+  }
   if (attn_impl() == 2) {
     int nw, nbuf;
     attn_cfg(nw, nbuf);
@@ -976,7 +1420,33 @@ at::Tensor flash_bwd(const at::Tensor& dout, const at::Tensor& qkv, const at::Te
   using I8 = std::integral_constant<int, 8>;
   using B1 = std::integral_constant<int, 1>;
   using B2 = std::integral_constant<int, 2>;
-  if (attn_impl() == 2) {
+  auto run3 = [&](auto w) {
+    constexpr int NW = decltype(w)::value;
+    const int rep = nq / nkv;
+    at::Tensor part;
+    if (rep > 1) part = at::empty({(long)rep * total * 2 * nkv * hd}, qkv.options().dtype(at::kFloat));
+    dim3 gk3((max_seqlen + 63) / 64, nq, nseq);
+    attn::bwd_dkdv3_kernel<<<gk3, 256, 0, cur_stream()>>>(
+        (const u16*)qkv.data_ptr(), (const u16*)dout.data_ptr(), lse.data_ptr<float>(), delta.data_ptr<float>(),
+        cu_c.data_ptr<int>(), rep > 1 ? part.data_ptr<float>() : nullptr, (u16*)dqkv.data_ptr(), nq, nkv, total, sl2,
+        (float)scale, causal ? 1 : 0);
+    SFT_LAUNCH_CHECK();
+    if (rep > 1) {
+      const long nvec = (long)total * 2 * nkv * hd / 8;
+      const int grid = (int)std::min<long>((nvec + 255) / 256, 2048);
+      attn::dkdv_reduce_kernel<<<grid, 256, 0, cur_stream()>>>(part.data_ptr<float>(), (u16*)dqkv.data_ptr(), total,
+                                                               nq, nkv, rep, (float)scale);
+      SFT_LAUNCH_CHECK();
+    }
+    dim3 gq3((max_seqlen + NW * 16 - 1) / (NW * 16), nq, nseq);
+    attn::bwd_dq3_kernel<NW><<<gq3, NW * 64, 0, cur_stream()>>>(
+        (const u16*)qkv.data_ptr(), (const u16*)dout.data_ptr(), lse.data_ptr<float>(), delta.data_ptr<float>(),
+        cu_c.data_ptr<int>(), (u16*)dqkv.data_ptr(), nq, nkv, total, sl2, (float)scale, causal ? 1 : 0);
+    SFT_LAUNCH_CHECK();
+  };
+  if (attn_impl() == 3) {
+    if (nw == 4) run3(I4()); else run3(I8());
+  } else if (attn_impl() == 2) {
     if (!attn_variant()) run2(std::false_type(), I8(), B2());
     else if (nw == 8 && nbuf == 2) run2(std::true_type(), I8(), B2());
     else if (nw == 8) run2(std::true_type(), I8(), B1());

@@ -139,7 +139,7 @@ def _attn_case(lens, nq, nkv, causal, variant, impl="2", cfg=""):
         assert e < 3e-2, (name, e)
 
 
-@pytest.mark.parametrize("impl", ["2", "1"])
+@pytest.mark.parametrize("impl", ["3", "2", "1"])
 @pytest.mark.parametrize("variant", ["1", "0"])
 @pytest.mark.parametrize("causal", [True, False])
 def test_flash_attention_varlen_gqa(variant, causal, impl):
@@ -150,9 +150,28 @@ def test_flash_attention_mha_and_long():
     _attn_case([1000, 37], 4, 4, True, "1")
 
 
-@pytest.mark.parametrize("cfg", ["8,1", "4,2", "4,1"])
-def test_flash_attention_launch_configs(cfg):
-    _attn_case([100, 255, 64, 1, 300], 8, 2, True, "1", "2", cfg)
+@pytest.mark.parametrize("impl,cfg", [("2", "8,1"), ("2", "4,2"), ("2", "4,1"), ("3", "4,1"), ("3", "8,1")])
+def test_flash_attention_launch_configs(impl, cfg):
+    _attn_case([100, 255, 64, 1, 300], 8, 2, True, "1", impl, cfg)
+    _attn_case([100, 255, 64, 1, 300], 8, 2, False, "1", impl, cfg)
+
+
+def test_flash_attention_deferred_rescale_branch():
+    """Force the online-softmax max to jump past THR mid-sequence (CDNA guide rule 26)."""
+    os.environ["SFTAMD_ATTN_IMPL"] = "3"
+    os.environ["SFTAMD_ATTN_CFG"] = ""
+    torch.manual_seed(1)
+    D, nq, nkv = 128, 4, 2
+    T = 384
+    cu = torch.tensor([0, T], dtype=torch.int32, device=DEV)
+    qkv = (0.3 * torch.randn(T, (nq + 2 * nkv) * D, device=DEV)).to(torch.bfloat16)
+    k = qkv[:, nq * D:(nq + nkv) * D].view(T, nkv, D)
+    q = qkv[:, :nq * D].view(T, nq, D)
+    k[200] = 4.0 * q[300, 0].repeat(1, 1).to(k.dtype)  # key 200 spikes for query 300 (tile 3 of 6)
+    scale = 1 / math.sqrt(D)
+    out, lse = _ext.ops().flash_fwd(qkv, cu, T, nq, nkv, D, scale, True)
+    o_ref = ref.attention(qkv.float(), nq, nkv, D, cu, scale, True)
+    assert rel_err(out, o_ref) < 2e-2
 
 
 @pytest.mark.parametrize("impl", ["2", "1"])
