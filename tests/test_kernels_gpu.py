@@ -167,7 +167,7 @@ def test_flash_attention_deferred_rescale_branch():
     qkv = (0.3 * torch.randn(T, (nq + 2 * nkv) * D, device=DEV)).to(torch.bfloat16)
     k = qkv[:, nq * D:(nq + nkv) * D].view(T, nkv, D)
     q = qkv[:, :nq * D].view(T, nq, D)
-    k[200] = 4.0 * q[300, 0].repeat(1, 1).to(k.dtype)  # key 200 spikes for query 300 (tile 3 of 6)
+    k[200] = (20.0 * q[300, 0].float()).to(k.dtype)  # key 200 spikes for query 300: max jumps ~27 (log2) at tile 3
     scale = 1 / math.sqrt(D)
     out, lse = _ext.ops().flash_fwd(qkv, cu, T, nq, nkv, D, scale, True)
     o_ref = ref.attention(qkv.float(), nq, nkv, D, cu, scale, True)
