@@ -195,7 +195,7 @@ std::tuple<at::Tensor, at::Tensor> rmsnorm_bwd(const at::Tensor& dy, const at::T
     SFT_CHECK(dres->is_contiguous() && dres->scalar_type() == at::kBFloat16, "dres");
     dr = (const u16*)dres->data_ptr();
   }
-  int nblk = std::min((M + 3) / 4, 256);
+  int nblk = std::min((M + 3) / 4, 1024);  // >=4 waves/SIMD in flight; partial dW rows reduced below
   nblk = std::max(nblk, 1);
   auto part = at::empty({nblk, H}, h.options().dtype(at::kFloat));
   auto dw = at::empty({H}, h.options().dtype(at::kFloat));

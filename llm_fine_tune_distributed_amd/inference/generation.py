@@ -32,9 +32,7 @@ def _layer(model, li, x, residual, cache: KVCache, pos: torch.Tensor, prefill: b
     at = layer.self_attn
     nq, nkv, D = cfg.num_attention_heads, cfg.num_key_value_heads, cfg.head_dim
     h, residual = ops.add_rms_norm(x, residual, layer.input_layernorm.weight, cfg.rms_norm_eps)
-    qkv = ops.linear(h, at.qkv_proj)
-    if at.lora is not None:
-        qkv = qkv + at.lora["qkv"](h)
+    qkv = ops.linear(h, at.qkv_proj) if at.lora is None else ops.lora_linear(h, at.qkv_proj, at.lora["qkv"])
     if at.use_rope:
         cos, sin = model.rope_tables(pos)
         ops.rope_(qkv, cos, sin, nq, nkv, D)
@@ -56,9 +54,7 @@ def _layer(model, li, x, residual, cache: KVCache, pos: torch.Tensor, prefill: b
         att = torch.einsum("grd,sgd->grs", qg, K) / math.sqrt(D)
         p = att.softmax(-1)
         a = torch.einsum("grs,sgd->grd", p, V).reshape(1, nq * D).to(x.dtype)
-    o = ops.linear(a, at.o_proj)
-    if at.lora is not None:
-        o = o + at.lora["o"](a)
+    o = ops.linear(a, at.o_proj) if at.lora is None else ops.lora_linear(a, at.o_proj, at.lora["o"])
     h, residual = ops.add_rms_norm(o, residual, layer.post_attention_layernorm.weight, cfg.rms_norm_eps)
     return layer.mlp(h), residual
 

@@ -56,16 +56,11 @@ class Attention(nn.Module):
 
     def forward(self, h, rope_cs, cu_seqlens, max_seqlen):
         c = self.cfg
-        qkv = ops.linear(h, self.qkv_proj)
-        if self.lora is not None:
-            qkv = qkv + self.lora["qkv"](h)
+        qkv = ops.linear(h, self.qkv_proj) if self.lora is None else ops.lora_linear(h, self.qkv_proj, self.lora["qkv"])
         if self.use_rope:
             qkv = ops.rope_(qkv, rope_cs[0], rope_cs[1], c.num_attention_heads, c.num_key_value_heads, c.head_dim)
         a = ops.flash_attention(qkv, cu_seqlens, max_seqlen, c.num_attention_heads, c.num_key_value_heads, c.head_dim)
-        o = ops.linear(a, self.o_proj)
-        if self.lora is not None:
-            o = o + self.lora["o"](a)
-        return o
+        return ops.linear(a, self.o_proj) if self.lora is None else ops.lora_linear(a, self.o_proj, self.lora["o"])
 
 
 class MLP(nn.Module):
@@ -76,14 +71,10 @@ class MLP(nn.Module):
         self.lora = None
 
     def forward(self, h):
-        gu = ops.linear(h, self.gate_up_proj)
-        if self.lora is not None:
-            gu = gu + self.lora["gate_up"](h)
+        L = self.lora
+        gu = ops.linear(h, self.gate_up_proj) if L is None else ops.lora_linear(h, self.gate_up_proj, L["gate_up"])
         a = ops.swiglu(gu)
-        o = ops.linear(a, self.down_proj)
-        if self.lora is not None:
-            o = o + self.lora["down"](a)
-        return o
+        return ops.linear(a, self.down_proj) if L is None else ops.lora_linear(a, self.down_proj, L["down"])
 
 
 class DecoderLayer(nn.Module):

@@ -8,6 +8,7 @@ from .fused import (
     flash_attention,
     linear,
     lm_head_cross_entropy,
+    lora_linear,
     rms_norm,
     rope_,
     swiglu,
@@ -16,6 +17,6 @@ from .optim_kernels import adamw_flat_, grad_norm_flat
 
 __all__ = [
     "reference", "load_extension", "use_hip", "hip_disabled", "IGNORE_INDEX", "add_rms_norm",
-    "embedding", "flash_attention", "linear", "lm_head_cross_entropy", "rms_norm", "rope_", "swiglu",
+    "embedding", "flash_attention", "linear", "lora_linear", "lm_head_cross_entropy", "rms_norm", "rope_", "swiglu",
     "adamw_flat_", "grad_norm_flat",
 ]

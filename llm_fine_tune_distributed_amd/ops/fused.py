@@ -332,3 +332,84 @@ class LMHeadCEFn(Function):
 
 def lm_head_cross_entropy(h, weight, labels, inv_count) -> Tuple[torch.Tensor, torch.Tensor]:
     return LMHeadCEFn.apply(h, weight, labels, inv_count)
+
+
+# ----------------------------------------------------------------------------- LoRA linear
+class LoRALinearFn(Function):
+    """y = x W^T + scaling * concat_i(dropout(x) A_i^T B_i^T) over the sub-projections of a fused
+    weight, without materialising dropout(x) twice, the per-adapter outputs, or a concatenation:
+    the rank-r products are added in place into column slices of the base GEMM output."""
+
+    @staticmethod
+    def forward(ctx, x, weight, scaling, p, splits, *ab):
+        n = len(ab) // 2
+        As, Bs = ab[:n], ab[n:]
+        x2d = x.reshape(-1, x.shape[-1])
+        y = torch.nn.functional.linear(x2d, weight)
+        mask = None
+        xd = x2d
+        if p > 0 and torch.is_grad_enabled():
+            mask = torch.rand_like(x2d, dtype=torch.float32) >= p
+            xd = x2d * mask.to(x2d.dtype) * (1.0 / (1.0 - p))
+        xas = []
+        col = 0
+        for A, B, w in zip(As, Bs, splits):
+            if A.numel():
+                xa = torch.mm(xd, A.t())
+                y[:, col:col + w].addmm_(xa, B.t(), alpha=scaling)
+                xas.append(xa)
+            else:
+                xas.append(None)
+            col += w
+        ctx.save_for_backward(x2d, *(t for t in xas if t is not None), *As, *Bs)
+        ctx.mask = mask
+        ctx.meta = (scaling, p, tuple(splits), n, tuple(xa is not None for xa in xas), x.shape)
+        ctx.weight = weight
+        if x.dim() == 2:
+            return y
+        return y.view(*x.shape[:-1], weight.shape[0]).clone()
+
+    @staticmethod
+    def backward(ctx, dy):
+        scaling, p, splits, n, has, xshape = ctx.meta
+        saved = ctx.saved_tensors
+        x2d = saved[0]
+        k = 1 + sum(has)
+        xas_it = iter(saved[1:k])
+        As, Bs = saved[k:k + n], saved[k + n:k + 2 * n]
+        w = ctx.weight
+        dy2d = dy.reshape(-1, dy.shape[-1])
+        dx = torch.mm(dy2d, w) if ctx.needs_input_grad[0] else None
+        dW = None
+        if ctx.needs_input_grad[1]:
+            dW = _accumulate_weight_grad(w, dy2d, x2d)
+        xd = x2d if ctx.mask is None else x2d * ctx.mask.to(x2d.dtype) * (1.0 / (1.0 - p))
+        dAs, dBs, dxd = [], [], None
+        col = 0
+        for A, B, wd, h in zip(As, Bs, splits, has):
+            if not h:
+                dAs.append(None)
+                dBs.append(None)
+                col += wd
+                continue
+            xa = next(xas_it)
+            dyi = dy2d[:, col:col + wd]
+            dBs.append(torch.mm(dyi.t(), xa).mul_(scaling).to(B.dtype))
+            t = torch.mm(dyi, B)
+            dAs.append(torch.mm(t.t(), xd).mul_(scaling).to(A.dtype))
+            c = torch.mm(t, A).mul_(scaling)
+            dxd = c if dxd is None else dxd.add_(c)
+            col += wd
+        if dx is not None and dxd is not None:
+            if ctx.mask is not None:
+                dxd = dxd * ctx.mask.to(dxd.dtype) * (1.0 / (1.0 - p))
+            dx = dx + dxd
+        if dx is not None:
+            dx = dx.view(xshape)
+        return (dx, dW, None, None, None, *dAs, *dBs)
+
+
+def lora_linear(x, weight, lora) -> torch.Tensor:
+    """``lora``: a models.lora.FusedLoRA module (adapters per sub-projection)."""
+    p = lora.dropout.p if isinstance(lora.dropout, torch.nn.Dropout) and lora.training else 0.0
+    return LoRALinearFn.apply(x, weight, float(lora.scaling), float(p), tuple(lora.out_splits), *lora.A, *lora.B)
