@@ -2,9 +2,12 @@
 
 Prefill runs the training kernels (fused RMSNorm, packed QKV GEMM, in-place RoPE, the varlen
 flash-attention forward) over the prompt and stores K/V in a preallocated cache sized for the
-whole generation (288 GB of HBM: no paging needed at this scale). Decode appends one token per
-step; single-query GQA attention over the cache is a memory-bound GEMV (batched matmul on the
-cache slice). Sampling matches HF's logits-processor order: repetition penalty -> temperature ->
+whole generation (288 GB of HBM: no paging needed at this scale). On the GPU the decode step is
+shape-static — the token, its position and the live cache length sit in device tensors, the KV
+append is an ``index_copy_`` and attention is the HIP split-K decode kernel that reads the
+length from device memory — so ONE decode step is captured into a hipGraph and replayed per
+token (no per-layer launch overhead, no host sync inside the step). On CPU the same step runs
+eagerly. Sampling matches HF's logits-processor order: repetition penalty -> temperature ->
 top-k -> top-p -> multinomial.
 """
 from __future__ import annotations
@@ -98,16 +101,77 @@ def sample_next(logits: torch.Tensor, history: torch.Tensor, temperature: float 
     return int(torch.multinomial(p, 1, generator=generator))
 
 
+class GraphDecoder:
+    """Static-shape decode step over a KVCache, captured once into a hipGraph (GPU)."""
+
+    def __init__(self, model, cache: KVCache):
+        self.model, self.cache = model, cache
+        dev = model.model.embed_tokens.device
+        self.tok = torch.zeros(1, dtype=torch.long, device=dev)
+        self.pos = torch.zeros(1, dtype=torch.long, device=dev)
+        self.len = torch.ones(1, dtype=torch.int32, device=dev)
+        self.graph = None
+        self.logits = None
+
+    @torch.no_grad()
+    def _step(self) -> torch.Tensor:
+        m, cfg = self.model, self.model.config
+        nq, nkv, D = cfg.num_attention_heads, cfg.num_key_value_heads, cfg.head_dim
+        x = ops.embedding(self.tok, m.model.embed_tokens)
+        residual = None
+        cos = sin = None
+        for li, layer in enumerate(m.model.layers):
+            at = layer.self_attn
+            h, residual = ops.add_rms_norm(x, residual, layer.input_layernorm.weight, cfg.rms_norm_eps)
+            qkv = ops.linear(h, at.qkv_proj) if at.lora is None else ops.lora_linear(h, at.qkv_proj, at.lora["qkv"])
+            if at.use_rope:
+                if cos is None:
+                    cos, sin = m.rope_tables(self.pos)
+                ops.rope_(qkv, cos, sin, nq, nkv, D)
+            self.cache.k[li].index_copy_(0, self.pos, qkv[:, nq * D:(nq + nkv) * D].view(1, nkv, D))
+            self.cache.v[li].index_copy_(0, self.pos, qkv[:, (nq + nkv) * D:].view(1, nkv, D))
+            a = ops.decode_attention(qkv[0, :nq * D].contiguous(), self.cache.k[li], self.cache.v[li], self.len,
+                                     nq, nkv).view(1, nq * D)
+            o = ops.linear(a, at.o_proj) if at.lora is None else ops.lora_linear(a, at.o_proj, at.lora["o"])
+            h, residual = ops.add_rms_norm(o, residual, layer.post_attention_layernorm.weight, cfg.rms_norm_eps)
+            x = layer.mlp(h)
+        n = m.model.norm
+        h, _ = ops.add_rms_norm(x, residual, n.weight, cfg.rms_norm_eps)
+        return torch.nn.functional.linear(h, m.lm_head_weight).float()[0]
+
+    def step(self, token: int, position: int, use_graph: bool = True) -> torch.Tensor:
+        self.tok.fill_(token)
+        self.pos.fill_(position)
+        self.len.fill_(position + 1)
+        if not use_graph:
+            return self._step()
+        if self.graph is None:
+            s = torch.cuda.Stream()
+            s.wait_stream(torch.cuda.current_stream())
+            with torch.cuda.stream(s):
+                for _ in range(2):  # warm up allocator / kernels outside capture
+                    self._step()
+            torch.cuda.current_stream().wait_stream(s)
+            self.graph = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(self.graph):
+                self.logits = self._step()
+        self.graph.replay()
+        return self.logits
+
+
 @torch.no_grad()
 def generate(model, prompt_ids: List[int], max_new_tokens: int = 256, eos_token_id: Optional[int] = None,
              temperature: float = 0.6, top_k: int = 40, top_p: float = 0.95, repetition_penalty: float = 1.1,
-             do_sample: bool = True, seed: Optional[int] = None) -> List[int]:
+             do_sample: bool = True, seed: Optional[int] = None, use_graph: Optional[bool] = None) -> List[int]:
     model.eval()
     dev = model.model.embed_tokens.device
     cache = KVCache(model.config, len(prompt_ids) + max_new_tokens + 1, dev, model.model.embed_tokens.dtype)
     g = torch.Generator(device=dev).manual_seed(seed) if seed is not None else None
     ids = torch.tensor(prompt_ids, device=dev)
     logits = forward_cached(model, ids, cache, prefill=True)
+    gpu_path = dev.type == "cuda" and model.config.head_dim == 128 and ops.use_hip(ids)
+    dec = GraphDecoder(model, cache) if gpu_path else None
+    graph = gpu_path if use_graph is None else (use_graph and gpu_path)
     hist = ids.clone()
     out: List[int] = []
     for _ in range(max_new_tokens):
@@ -117,5 +181,9 @@ def generate(model, prompt_ids: List[int], max_new_tokens: int = 256, eos_token_
             break
         nt = torch.tensor([t], device=dev)
         hist = torch.cat([hist, nt])
-        logits = forward_cached(model, nt, cache, prefill=False)
+        if dec is not None:
+            logits = dec.step(t, cache.len, use_graph=graph).clone()
+            cache.len += 1
+        else:
+            logits = forward_cached(model, nt, cache, prefill=False)
     return out

@@ -4,6 +4,7 @@ from ._ext import load as load_extension, use_hip, hip_disabled
 from .fused import (
     IGNORE_INDEX,
     add_rms_norm,
+    decode_attention,
     embedding,
     flash_attention,
     linear,
@@ -16,7 +17,7 @@ from .fused import (
 from .optim_kernels import adamw_flat_, grad_norm_flat
 
 __all__ = [
-    "reference", "load_extension", "use_hip", "hip_disabled", "IGNORE_INDEX", "add_rms_norm",
+    "reference", "load_extension", "use_hip", "hip_disabled", "IGNORE_INDEX", "add_rms_norm", "decode_attention",
     "embedding", "flash_attention", "linear", "lora_linear", "lm_head_cross_entropy", "rms_norm", "rope_", "swiglu",
     "adamw_flat_", "grad_norm_flat",
 ]

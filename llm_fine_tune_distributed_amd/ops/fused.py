@@ -413,3 +413,15 @@ def lora_linear(x, weight, lora) -> torch.Tensor:
     """``lora``: a models.lora.FusedLoRA module (adapters per sub-projection)."""
     p = lora.dropout.p if isinstance(lora.dropout, torch.nn.Dropout) and lora.training else 0.0
     return LoRALinearFn.apply(x, weight, float(lora.scaling), float(p), tuple(lora.out_splits), *lora.A, *lora.B)
+
+
+def decode_attention(q, kcache, vcache, cache_len, n_q, n_kv, scale=None):
+    """Single-token GQA attention over cache[:cache_len] (cache_len: int32 device tensor)."""
+    scale = scale if scale is not None else 1.0 / math.sqrt(q.numel() // n_q)
+    if _ext.use_hip(q):
+        return _ext.ops().decode_attention(q, kcache, vcache, cache_len, n_q, n_kv, float(scale))
+    L = int(cache_len.item())
+    D = q.numel() // n_q
+    qg = q.float().view(n_kv, n_q // n_kv, D)
+    att = torch.einsum("grd,sgd->grs", qg, kcache[:L].float()) * scale
+    return torch.einsum("grs,sgd->grd", att.softmax(-1), vcache[:L].float()).reshape(-1).to(q.dtype)

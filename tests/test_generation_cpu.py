@@ -26,3 +26,20 @@ def test_sampling_processors():
     g = torch.Generator().manual_seed(0)
     picks = {sample_next(lg, torch.tensor([], dtype=torch.long), top_k=2, generator=g) for _ in range(50)}
     assert picks <= {1, 3}
+
+
+def test_static_decoder_matches_cached_forward_cpu():
+    from llm_fine_tune_distributed_amd.inference.generation import GraphDecoder, KVCache, forward_cached
+    torch.manual_seed(0)
+    m = build_model(tiny(), dtype=torch.float32, seed=2)
+    prompt = torch.randint(0, 512, (7,))
+    c1 = KVCache(m.config, 16, "cpu", torch.float32)
+    c2 = KVCache(m.config, 16, "cpu", torch.float32)
+    forward_cached(m, prompt, c1, prefill=True)
+    forward_cached(m, prompt, c2, prefill=True)
+    dec = GraphDecoder(m, c2)
+    for t in (5, 9, 11):
+        a = forward_cached(m, torch.tensor([t]), c1, prefill=False)
+        b = dec.step(t, c2.len, use_graph=False)
+        c2.len += 1
+        assert torch.allclose(a, b, atol=1e-4)

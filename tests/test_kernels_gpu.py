@@ -216,3 +216,18 @@ def test_adamw_stochastic_rounding_unbiased():
     m.zero_(), v.zero_()
     _ext.ops().adamw_flat(p2, g, None, m, v, coef, lr, 0.9, 0.999, 1e-12, 0.0, 1 - 0.9, 1 - 0.999, 0)
     assert (p2.float() == 1.0).all()  # round-to-nearest loses the update
+
+
+@pytest.mark.parametrize("L", [1, 200, 777])
+def test_decode_attention(L):
+    torch.manual_seed(0)
+    D, nq, nkv, S = 128, 16, 4, 1024
+    q = torch.randn(nq * D, device=DEV, dtype=torch.bfloat16)
+    kc = torch.randn(S, nkv, D, device=DEV, dtype=torch.bfloat16)
+    vc = torch.randn(S, nkv, D, device=DEV, dtype=torch.bfloat16)
+    ln = torch.tensor([L], dtype=torch.int32, device=DEV)
+    out = _ext.ops().decode_attention(q, kc, vc, ln, nq, nkv, 1 / math.sqrt(D))
+    qf = q.float().view(nkv, nq // nkv, D)
+    att = torch.einsum("grd,sgd->grs", qf, kc[:L].float()) / math.sqrt(D)
+    ref_o = torch.einsum("grs,sgd->grd", att.softmax(-1), vc[:L].float()).reshape(-1)
+    assert rel_err(out, ref_o) < 1e-2
