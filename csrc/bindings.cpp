@@ -19,6 +19,8 @@ TORCH_LIBRARY(sftamd, m) {
   m.def("flash_fwd(Tensor qkv, Tensor cu_seqlens, int max_seqlen, int n_q, int n_kv, int head_dim, float scale, bool causal) -> (Tensor, Tensor)");
   m.def("flash_bwd(Tensor dout, Tensor qkv, Tensor out, Tensor lse, Tensor cu_seqlens, int max_seqlen, int n_q, int n_kv, int head_dim, float scale, bool causal) -> Tensor");
   m.def("decode_attention(Tensor q, Tensor kcache, Tensor vcache, Tensor cache_len, int n_q, int n_kv, float scale) -> Tensor");
+  // weight-gradient GEMM: out[N,K] (+)= dy[T,N]^T x[T,K]
+  m.def("wgrad_gemm(Tensor(a!) out, Tensor dy, Tensor x, bool accumulate, int cfg=0) -> ()");
   // optimizer
   m.def("sumsq(Tensor x) -> Tensor");
   m.def("adamw_flat(Tensor(a!) param, Tensor grad, Tensor(b!)? master, Tensor(c!) exp_avg, Tensor(d!) exp_avg_sq, Tensor clip_coef, float lr, float beta1, float beta2, float eps, float weight_decay, float bc1, float bc2, int sr_seed=0, int sr_offset=0) -> ()");

@@ -1,0 +1,527 @@
+// Weight-gradient GEMM for gfx950: dW[N, K] (+)= dy[T, N]^T @ x[T, K], bf16 in, fp32 accumulate,
+// written (or accumulated, beta = 1) straight into the bf16 flat gradient buffer.
+//
+// Why a hand-written kernel: both operands of a weight gradient are stored "reduction-major"
+// (the token index T is the ROW index of dy and of x), the layout that hipBLASLt/rocBLAS run at
+// ~1.0 PF/s on MI355X for the SmolLM3 shapes (NT in BLAS terms, profiles/), against ~1.4 PF/s
+// for the forward (TN) GEMMs. On CDNA4 that layout costs nothing extra: the tiles are staged
+// row-major into LDS exactly as they sit in HBM (global_load_lds, 16 B per lane, no register
+// round trip) and BOTH MFMA operands are read with the gfx950 transposed LDS read
+// ds_read_b64_tr_b16, which delivers 4 rows x 16 columns column-major per 16-lane group.
+//
+// Kernel structure (CDNA guide §5 "glds vs register staging"):
+//   * BM x BN output tile per 512-thread workgroup (8 waves, WM x WN wave grid), BK = 64 tokens
+//     per K-step, two LDS stages: glds of step k+1 in flight while step k is computed;
+//   * LDS images are [64 tokens][128 columns] bf16 (256-byte rows) with the chunk XOR swizzle
+//     ch ^ ((row&3)<<2 | (row>>2)&3), applied on the GLOBAL source address (glds writes
+//     lane-linear), which keeps the transposed reads bank-conflict free;
+//   * v_mfma_f32_16x16x32_bf16; lane (g = lane>>4, i = lane&15) gets the reduction indices
+//     {4g..4g+3, 16+4g..16+4g+3} of the 32-token chunk on both operands (the order is irrelevant
+//     to a reduction as long as it is the same on both sides);
+//   * XCD-aware workgroup remap: consecutive tiles along K (which share the dy column slab) land
+//     on the same XCD / L2;
+//   * epilogue through LDS (fp32, padded rows) so the beta-accumulate read-modify-write of the
+//     bf16 gradient is 16-byte vectorised.
+#include "common.h"
+
+#include <type_traits>
+
+namespace sftamd {
+namespace wgrad {
+
+constexpr int BK = 64;
+constexpr int ROWB = 256;             // bytes per LDS image row (128 bf16)
+constexpr int IMG = BK * ROWB;        // 16 KB per [64][128] image
+constexpr int NT = 512;
+
+__device__ __forceinline__ int swz(int row, int ch) { return ch ^ (((row & 3) << 2) | ((row >> 2) & 3)); }
+__device__ __forceinline__ int img_off(int row, int ch) { return row * ROWB + 16 * swz(row, ch); }
+
+typedef __attribute__((address_space(3))) s16x4 lds_s4;
+
+__device__ __forceinline__ bf16x8 lds_tr(const char* base, int off) {
+  s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4*)(base + off));
+  s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4*)(base + off + 16 * ROWB));
+  typedef __attribute__((ext_vector_type(8))) short s16x8;
+  s16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+  return __builtin_bit_cast(bf16x8, v);
+}
+
+__device__ __forceinline__ void glds16(const u16* src, char* dst) {
+  __builtin_amdgcn_global_load_lds((const void __attribute__((address_space(1)))*)src,
+                                   (void __attribute__((address_space(3)))*)dst, 16, 0, 0);
+}
+
+template <int BM, int BN, int WM, int WN>
+struct Cfg {
+  static constexpr int TM = BM / WM, TN = BN / WN;  // wave tile
+  static constexpr int FM = TM / 16, FN = TN / 16;  // 16x16 fragments per wave
+  static constexpr int IA = BM / 128, IB = BN / 128;
+  static constexpr int STAGE = (IA + IB) * IMG;
+  static constexpr int PIECES = (IA + IB) * 16;     // 1 KB glds pieces per stage
+  static constexpr int PPW = PIECES / 8;            // per wave
+  static constexpr int EPI_ROWS = 64;               // rows per epilogue pass per wave
+  static constexpr int EPI_LD = TN + 4;             // padded fp32 row (bank-conflict free)
+  static constexpr int EPI = 8 * EPI_ROWS * EPI_LD * 4;
+  static constexpr int LDS = (2 * STAGE > EPI) ? 2 * STAGE : EPI;
+  static_assert(WM * WN == 8, "8 waves");
+  static_assert(PIECES % 8 == 0, "pieces per wave");
+  static_assert(TM % EPI_ROWS == 0 || TM < EPI_ROWS, "epilogue passes");
+};
+
+// LDS-DMA staging of one K-tile. Piece j (1 KB = 4 image rows) of wave w is image j>>1, rows
+// 32*(j&1) + 4w .. +3, so the image (hence the matrix) of every piece is a compile-time constant
+// and the per-lane part of the address (row 4w + lane/16, swizzled chunk) is shared by all pieces:
+// two 64-bit lane pointers plus scalar offsets instead of one pointer per piece.
+template <class G>
+struct Stager {
+  const u16* pa;
+  const u16* pb;
+  long lda, ldb;
+  int w;
+  __device__ __forceinline__ void init(const u16* A, const u16* B, int N, int K, int n0, int k0, int wave, int lane) {
+    w = wave;
+    lda = N;
+    ldb = K;
+    const int r = 4 * wave + (lane >> 4), c = lane & 15;
+    pa = A + (long)r * N + n0 + 8 * swz(r, c);
+    pb = B + (long)r * K + k0 + 8 * swz(r, c);
+  }
+  __device__ __forceinline__ void issue(char* buf) {
+#pragma unroll
+    for (int j = 0; j < G::PPW; ++j) {
+      const int img = j >> 1, half = j & 1;
+      const u16* p = img < G::IA ? pa + 32 * half * lda + img * 128 : pb + 32 * half * ldb + (img - G::IA) * 128;
+      glds16(p, buf + img * IMG + (half * 8 + w) * 1024);
+    }
+    pa += BK * lda;
+    pb += BK * ldb;
+  }
+};
+
+// One K-step: wait for the current stage, start the global_load_lds of the next one, MFMA over the
+// current one. ``cur`` and ``nxt`` are __restrict__ so that, once inlined, the ds_reads of ``cur``
+// carry alias scopes disjoint from the LDS-DMA writes into ``nxt``: without that the compiler's
+// waitcnt pass drains vmcnt(0) before the first ds_read and the prefetch overlaps nothing.
+template <class G>
+__device__ __forceinline__ void kstep(const char* __restrict__ cur, char* __restrict__ nxt, int kt, int nk, Stager<G>& st,
+                                      const int (&offA)[G::FM], const int (&offB)[G::FN], f32x4 (&acc)[G::FM][G::FN]) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (kt + 1 < nk) st.issue(nxt);
+#pragma unroll
+  for (int ks = 0; ks < 2; ++ks) {
+    bf16x8 af[G::FM], bfr[G::FN];
+#pragma unroll
+    for (int j = 0; j < G::FN; ++j) bfr[j] = lds_tr(cur, offB[j] + ks * 32 * ROWB);
+#pragma unroll
+    for (int i = 0; i < G::FM; ++i) af[i] = lds_tr(cur, offA[i] + ks * 32 * ROWB);
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int i = 0; i < G::FM; ++i)
+#pragma unroll
+      for (int j = 0; j < G::FN; ++j)
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+  }
+}
+
+template <class G>
+__device__ __forceinline__ void read_frags(const char* base, int ks, const int (&offA)[G::FM], const int (&offB)[G::FN],
+                                           bf16x8 (&af)[G::FM], bf16x8 (&bf)[G::FN]) {
+#pragma unroll
+  for (int j = 0; j < G::FN; ++j) bf[j] = lds_tr(base, offB[j] + ks * 32 * ROWB);
+#pragma unroll
+  for (int i = 0; i < G::FM; ++i) af[i] = lds_tr(base, offA[i] + ks * 32 * ROWB);
+}
+
+template <class G>
+__device__ __forceinline__ void mfma_block(const bf16x8 (&af)[G::FM], const bf16x8 (&bf)[G::FN], f32x4 (&acc)[G::FM][G::FN]) {
+  __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+  for (int i = 0; i < G::FM; ++i)
+#pragma unroll
+    for (int j = 0; j < G::FN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bf[j], acc[i][j], 0, 0, 0);
+  __builtin_amdgcn_s_setprio(0);
+}
+
+// One K-step of the register-pipelined loop on stage ``cur`` (``oth`` = the other stage).
+template <class G, int DIAG>
+__device__ __forceinline__ void pipe_step(char* __restrict__ cur, char* __restrict__ oth, int kt, int nk, Stager<G>& st,
+                                          const int (&offA)[G::FM], const int (&offB)[G::FN], bf16x8 (&a0)[G::FM],
+                                          bf16x8 (&c0)[G::FN], bf16x8 (&a1)[G::FM], bf16x8 (&c1)[G::FN],
+                                          f32x4 (&acc)[G::FM][G::FN]) {
+  constexpr unsigned LGKM0 = 0xC07F, VM0_LGKM0 = 0x0070;
+  __builtin_amdgcn_s_waitcnt(LGKM0);  // F0 landed (read during the previous MFMA block)
+  read_frags<G>(cur, 1, offA, offB, a1, c1);
+  mfma_block<G>(a0, c0, acc);
+  __builtin_amdgcn_s_waitcnt(VM0_LGKM0);  // K-tile kt+1 landed; this wave's reads of cur done
+  if (DIAG != 2) __builtin_amdgcn_s_barrier();
+  if (DIAG != 1 && kt + 2 < nk) st.issue(cur);
+  if (kt + 1 < nk) read_frags<G>(oth, 0, offA, offB, a0, c0);
+  mfma_block<G>(a1, c1, acc);
+}
+
+// Register-pipelined main loop (PIPE = 1). Every MFMA block finds its operands already in registers:
+//   K-step kt on stage S:  [read F1 = (kt, tokens 32..63) from S | MFMA F0]
+//                          wait vmcnt(0) (K-tile kt+1 landed), lgkmcnt(0) (S fully read); barrier
+//                          [glds K-tile kt+2 -> S; read F0 = (kt+1, tokens 0..31) from S^1 | MFMA F1]
+// so the barrier is the only bubble, and each K-tile's loads have one full K-step to land. The
+// whole loop lives in one function whose two stage pointers are __restrict__: every ds_read then
+// carries an alias scope disjoint from the LDS-DMA writes into the other stage, and the compiler's
+// waitcnt pass does not drain vmcnt before it.
+template <class G, int DIAG>
+__device__ __forceinline__ void mainloop_pipe(char* __restrict__ b0, char* __restrict__ b1, int nk, Stager<G>& st,
+                                              const int (&offA)[G::FM], const int (&offB)[G::FN],
+                                              f32x4 (&acc)[G::FM][G::FN]) {
+  bf16x8 a0[G::FM], c0[G::FN], a1[G::FM], c1[G::FN];
+  auto issue = [&](char* buf) { st.issue(buf); };
+  // s_waitcnt through the builtin (not inline asm) so that the compiler's waitcnt pass sees the drain:
+  // gfx9 encoding vmcnt[3:0] | expcnt[6:4] | lgkmcnt[11:8] | vmcnt[5:4] << 14.
+  constexpr unsigned VM0_LGKM0 = 0x0070;
+  constexpr unsigned VM_PPW = (G::PPW & 15) | ((G::PPW >> 4) << 14) | 0x70 | 0xF00;
+  issue(b0);
+  if (nk > 1) {
+    issue(b1);
+    __builtin_amdgcn_s_waitcnt(VM_PPW);
+  } else {
+    __builtin_amdgcn_s_waitcnt(VM0_LGKM0);
+  }
+  __builtin_amdgcn_s_barrier();
+  read_frags<G>(b0, 0, offA, offB, a0, c0);
+  for (int kt = 0; kt < nk; kt += 2) {
+    pipe_step<G, DIAG>(b0, b1, kt, nk, st, offA, offB, a0, c0, a1, c1, acc);
+    if (kt + 1 < nk) pipe_step<G, DIAG>(b1, b0, kt + 1, nk, st, offA, offB, a0, c0, a1, c1, acc);
+  }
+}
+
+// Epilogue: fp32 wave tile -> LDS (rows padded to TN + 4 floats: conflict-free) -> 16-byte
+// read-modify-write of the bf16 gradient (beta = 1 when accumulating, else plain store).
+template <class G>
+__device__ __forceinline__ void epilogue(char* smem, f32x4 (&acc)[G::FM][G::FN], u16* __restrict__ C, int K, int n0,
+                                         int k0, int wm, int wk, int w, int lane, int accumulate) {
+  const int g = lane >> 4, ii = lane & 15;
+  float* ep = reinterpret_cast<float*>(smem) + w * G::EPI_ROWS * G::EPI_LD;
+  constexpr int FPP = G::EPI_ROWS / 16 < G::FM ? G::EPI_ROWS / 16 : G::FM;  // fragments per pass
+  constexpr int ROWS = FPP * 16;
+#pragma unroll
+  for (int pass = 0; pass < G::FM / FPP; ++pass) {
+#pragma unroll
+    for (int i = 0; i < FPP; ++i)
+#pragma unroll
+      for (int j = 0; j < G::FN; ++j)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) ep[(16 * i + 4 * g + e) * G::EPI_LD + 16 * j + ii] = acc[pass * FPP + i][j][e];
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // wave-private region: writes before reads
+    constexpr int SEGS = G::TN / 8;                      // 16-byte output segments per row
+#pragma unroll
+    for (int it = 0; it < ROWS * SEGS / 64; ++it) {
+      const int seg = it * 64 + lane, row = seg / SEGS, cs = seg - row * SEGS;
+      const float* pr = ep + row * G::EPI_LD + cs * 8;
+      float v[8];
+      *(float4*)&v[0] = *(const float4*)pr;
+      *(float4*)&v[4] = *(const float4*)(pr + 4);
+      u16* out = C + (long)(n0 + wm * G::TM + pass * ROWS + row) * K + k0 + wk * G::TN + cs * 8;
+      if (accumulate) {
+        float o[8];
+        unpack8(*(const uint4*)out, o);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[e] += o[e];
+      }
+      *(uint4*)out = pack8(v);
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  }
+}
+
+template <int BM, int BN, int WM, int WN, int PIPE>
+__global__ void __launch_bounds__(NT) wgrad_kernel(const u16* __restrict__ A, const u16* __restrict__ B,
+                                                   u16* __restrict__ C, int T, int N, int K, int nbk, int accumulate) {
+  using G = Cfg<BM, BN, WM, WN>;
+  __shared__ __attribute__((aligned(16))) char smem[G::LDS];
+
+  // XCD-aware bijective remap (CDNA guide §5: consecutive remapped ids share an XCD)
+  const int nwg = gridDim.x, orig = blockIdx.x;
+  const int xcd = orig & 7, q8 = nwg >> 3, r8 = nwg & 7;
+  const int wgid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (orig >> 3);
+  const int bn = wgid / nbk, bk = wgid - bn * nbk;
+  const int n0 = bn * BM, k0 = bk * BN;
+
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int wm = w / WN, wk = w - wm * WN;
+
+  Stager<G> st;
+  st.init(A, B, N, K, n0, k0, w, lane);
+
+  // ---- fragment read offsets (transposed reads, see attention.hip Offs::tr)
+  // 16-lane group g reads token rows 4b..4b+3 and 16+4b..16+4b+3 with b = ((g&1)<<1)|(g>>1): the two
+  // groups of each 32-lane half then read blocks 8 rows apart, which is bank-conflict free for
+  // ds_read_b64_tr_b16 on this swizzle (b = g, i.e. stacked blocks, is 2-way).
+  const int g = lane >> 4, ii = lane & 15, qq = ii >> 2, pp = ii & 3;
+  const int r0 = 4 * (((g & 1) << 1) | (g >> 1)) + qq;
+  int offA[G::FM], offB[G::FN];
+#pragma unroll
+  for (int i = 0; i < G::FM; ++i) {
+    const int nl = wm * G::TM + 16 * i;
+    offA[i] = (nl >> 7) * IMG + img_off(r0, 2 * ((nl & 127) >> 4) + (pp >> 1)) + 8 * (pp & 1);
+  }
+#pragma unroll
+  for (int j = 0; j < G::FN; ++j) {
+    const int kl = wk * G::TN + 16 * j;
+    offB[j] = (G::IA + (kl >> 7)) * IMG + img_off(r0, 2 * ((kl & 127) >> 4) + (pp >> 1)) + 8 * (pp & 1);
+  }
+
+  f32x4 acc[G::FM][G::FN];
+#pragma unroll
+  for (int i = 0; i < G::FM; ++i)
+#pragma unroll
+    for (int j = 0; j < G::FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int nk = T / BK;
+  if constexpr (PIPE) {
+    mainloop_pipe<G, PIPE - 1>(smem, smem + G::STAGE, nk, st, offA, offB, acc);
+  } else {
+    st.issue(smem);
+    for (int kt = 0; kt < nk; kt += 2) {
+      kstep<G>(smem, smem + G::STAGE, kt, nk, st, offA, offB, acc);
+      if (kt + 1 < nk) kstep<G>(smem + G::STAGE, smem, kt + 1, nk, st, offA, offB, acc);
+    }
+  }
+  __syncthreads();
+
+  epilogue<G>(smem, acc, C, K, n0, k0, wm, wk, w, lane, accumulate);
+}
+
+// ============================================================================================
+// Ring-pipelined variant: BK = 32 tokens per stage, NS stages (up to all 160 KB of LDS), the
+// global_load_lds of a stage issued NS-1 steps before it is read. The 64-token, two-stage loop
+// above keeps only one 64 KB K-tile in flight per CU and measures load-latency bound (removing
+// its loads makes it 1.46x faster); the ring keeps up to NS x 32 KB in flight. Per 32-token step:
+//   wait vmcnt((NS-2) x pieces) -> step t+1 landed; lgkmcnt(0) -> this wave's reads of slot t done
+//   barrier; glds step t+NS -> slot t % NS; ds_read fragments of step t+1; MFMA on step t (regs).
+// ============================================================================================
+constexpr int BKR = 32;
+constexpr int IMGR = BKR * ROWB;  // 8 KB per [32][128] image
+
+template <int BM, int BN, int WM, int WN, int NS_>
+struct RCfg {
+  static constexpr int NS = NS_;
+  static constexpr int TM = BM / WM, TN = BN / WN;
+  static constexpr int FM = TM / 16, FN = TN / 16;
+  static constexpr int IA = BM / 128, IB = BN / 128, NIMG = IA + IB;
+  static constexpr int STAGE = NIMG * IMGR;
+  static constexpr int PPW = NIMG;  // one 1 KB piece (rows 4w..4w+3) per image per wave
+  static constexpr int EPI_ROWS = 64, EPI_LD = TN + 4;
+  static constexpr int EPI = 8 * EPI_ROWS * EPI_LD * 4;
+  static constexpr int LDS = (NS * STAGE > EPI) ? NS * STAGE : EPI;
+  static_assert(WM * WN == 8 && NS >= 3 && NS <= 6, "ring config");
+  static_assert(LDS <= 160 * 1024, "LDS budget");
+};
+
+template <class G>
+struct RStager {
+  const u16* pa;
+  const u16* pb;
+  long lda, ldb;
+  int w, left;
+  __device__ __forceinline__ void init(const u16* A, const u16* B, int N, int K, int n0, int k0, int wave, int lane,
+                                       int nsteps) {
+    w = wave;
+    lda = N;
+    ldb = K;
+    left = nsteps;
+    const int r = 4 * wave + (lane >> 4), c = lane & 15;
+    pa = A + (long)r * N + n0 + 8 * swz(r, c);
+    pb = B + (long)r * K + k0 + 8 * swz(r, c);
+  }
+  // Past the last step the same (valid) rows are fetched again into a slot nobody reads: every
+  // step then issues exactly PPW DMAs, so the counted waits are compile-time constants with no
+  // tail branches (a branch around a wait makes the compiler's own waitcnt pass assume the
+  // no-wait path and drain lgkmcnt before the next MFMA block).
+  __device__ __forceinline__ void issue(char* buf) {
+#pragma unroll
+    for (int j = 0; j < G::NIMG; ++j) {
+      const u16* p = j < G::IA ? pa + j * 128 : pb + (j - G::IA) * 128;
+      glds16(p, buf + j * IMGR + w * 1024);
+    }
+    if (--left > 0) {
+      pa += BKR * lda;
+      pb += BKR * ldb;
+    }
+  }
+};
+
+template <class G>
+__device__ __forceinline__ void rread(const char* base, const int (&offA)[G::FM], const int (&offB)[G::FN],
+                                      bf16x8 (&af)[G::FM], bf16x8 (&bf)[G::FN]) {
+#pragma unroll
+  for (int j = 0; j < G::FN; ++j) bf[j] = lds_tr(base, offB[j]);
+#pragma unroll
+  for (int i = 0; i < G::FM; ++i) af[i] = lds_tr(base, offA[i]);
+}
+
+__device__ __forceinline__ char* pick(int i, char* b0, char* b1, char* b2, char* b3, char* b4, char* b5) {
+  switch (i) {
+    case 0: return b0;
+    case 1: return b1;
+    case 2: return b2;
+    case 3: return b3;
+    case 4: return b4;
+    default: return b5;
+  }
+}
+
+constexpr unsigned waitcnt_imm(int vm, int lgkm) {  // gfx9: vmcnt[3:0] expcnt[6:4] lgkmcnt[11:8] vmcnt[5:4]<<14
+  return (unsigned)((vm & 15) | (7 << 4) | ((lgkm & 15) << 8) | ((vm >> 4) << 14));
+}
+
+// The stage pointers are separate __restrict__ parameters: once inlined, every ds_read and every
+// LDS-DMA write carries the alias scope of its stage, so the compiler's waitcnt pass only waits for
+// DMA into the slot being read (which the explicit counted wait already retired).
+//
+// Registers: the B fragments of the next step are double-buffered (read at the start of a step),
+// the A fragments are refilled in place — fragment row i of step t+1 is read right after the four
+// MFMAs of row i of step t, so it still has a whole step of MFMAs to land — which keeps the kernel
+// at ~216 VGPRs (2 waves per SIMD) with every MFMA operand already resident.
+template <class G>
+__device__ __forceinline__ void ring_loop(char* __restrict__ b0, char* __restrict__ b1, char* __restrict__ b2,
+                                          char* __restrict__ b3, char* __restrict__ b4, char* __restrict__ b5,
+                                          int nsteps, RStager<G>& st, const int (&offA)[G::FM],
+                                          const int (&offB)[G::FN], f32x4 (&acc)[G::FM][G::FN]) {
+  constexpr int NS = G::NS, PPW = G::PPW;
+  constexpr int U = (NS % 2) ? 2 * NS : NS;  // unroll: stage slot and B register set both compile-time
+  bf16x8 fa[G::FM], fb[2][G::FN];
+#pragma unroll
+  for (int i = 0; i < NS; ++i) st.issue(pick(i, b0, b1, b2, b3, b4, b5));
+  __builtin_amdgcn_s_waitcnt(waitcnt_imm((NS - 1) * PPW, 0));
+  __builtin_amdgcn_s_barrier();
+  rread<G>(b0, offA, offB, fa, fb[0]);
+  for (int t0 = 0; t0 < nsteps; t0 += U) {
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      if (t0 + u < nsteps) {
+        __builtin_amdgcn_s_waitcnt(waitcnt_imm((NS - 2) * PPW, 0));
+        __builtin_amdgcn_s_barrier();
+        st.issue(pick(u % NS, b0, b1, b2, b3, b4, b5));
+        const char* nxt = pick((u + 1) % NS, b0, b1, b2, b3, b4, b5);
+        const int cb = u & 1;
+#pragma unroll
+        for (int j = 0; j < G::FN; ++j) fb[cb ^ 1][j] = lds_tr(nxt, offB[j]);
+        __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+        for (int i = 0; i < G::FM; ++i) {
+#pragma unroll
+          for (int j = 0; j < G::FN; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[cb][j], acc[i][j], 0, 0, 0);
+          fa[i] = lds_tr(nxt, offA[i]);
+        }
+        __builtin_amdgcn_s_setprio(0);
+      }
+    }
+  }
+  __builtin_amdgcn_s_waitcnt(waitcnt_imm(0, 0));  // drain the tail DMAs before LDS is reused
+}
+
+template <int BM, int BN, int WM, int WN, int NS>
+__global__ void __launch_bounds__(NT) ring_kernel(const u16* __restrict__ A, const u16* __restrict__ B,
+                                                  u16* __restrict__ C, int T, int N, int K, int nbk, int accumulate) {
+  using G = RCfg<BM, BN, WM, WN, NS>;
+  __shared__ __attribute__((aligned(16))) char smem[G::LDS];
+  const int nwg = gridDim.x, orig = blockIdx.x;
+  const int xcd = orig & 7, q8 = nwg >> 3, r8 = nwg & 7;
+  const int wgid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (orig >> 3);
+  const int bn = wgid / nbk, bk = wgid - bn * nbk;
+  const int n0 = bn * BM, k0 = bk * BN;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int wm = w / WN, wk = w - wm * WN;
+
+  RStager<G> st;
+  st.init(A, B, N, K, n0, k0, w, lane, T / BKR);
+  const int g = lane >> 4, ii = lane & 15, qq = ii >> 2, pp = ii & 3;
+  const int r0 = 4 * (((g & 1) << 1) | (g >> 1)) + qq;  // conflict-free block order (see wgrad_kernel)
+  int offA[G::FM], offB[G::FN];
+#pragma unroll
+  for (int i = 0; i < G::FM; ++i) {
+    const int nl = wm * G::TM + 16 * i;
+    offA[i] = (nl >> 7) * IMGR + img_off(r0, 2 * ((nl & 127) >> 4) + (pp >> 1)) + 8 * (pp & 1);
+  }
+#pragma unroll
+  for (int j = 0; j < G::FN; ++j) {
+    const int kl = wk * G::TN + 16 * j;
+    offB[j] = (G::IA + (kl >> 7)) * IMGR + img_off(r0, 2 * ((kl & 127) >> 4) + (pp >> 1)) + 8 * (pp & 1);
+  }
+  f32x4 acc[G::FM][G::FN];
+#pragma unroll
+  for (int i = 0; i < G::FM; ++i)
+#pragma unroll
+    for (int j = 0; j < G::FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  char* b[6];
+#pragma unroll
+  for (int i = 0; i < 6; ++i) b[i] = smem + (i < NS ? i : 0) * G::STAGE;
+  ring_loop<G>(b[0], b[1], b[2], b[3], b[4], b[5], T / BKR, st, offA, offB, acc);
+  __syncthreads();
+  epilogue<G>(smem, acc, C, K, n0, k0, wm, wk, w, lane, accumulate);
+}
+
+template <int BM, int BN, int WM, int WN, int NS>
+void launch_ring(const at::Tensor& dy, const at::Tensor& x, at::Tensor& out, bool accumulate) {
+  const int T = dy.size(0), N = dy.size(1), K = x.size(1);
+  const int nbn = N / BM, nbk = K / BN;
+  ring_kernel<BM, BN, WM, WN, NS><<<nbn * nbk, NT, 0, cur_stream()>>>(
+      (const u16*)dy.data_ptr(), (const u16*)x.data_ptr(), (u16*)out.data_ptr(), T, N, K, nbk, accumulate ? 1 : 0);
+  SFT_LAUNCH_CHECK();
+}
+
+template <int BM, int BN, int WM, int WN, int PIPE>
+void launch(const at::Tensor& dy, const at::Tensor& x, at::Tensor& out, bool accumulate) {
+  const int T = dy.size(0), N = dy.size(1), K = x.size(1);
+  const int nbn = N / BM, nbk = K / BN;
+  wgrad_kernel<BM, BN, WM, WN, PIPE><<<nbn * nbk, NT, 0, cur_stream()>>>(
+      (const u16*)dy.data_ptr(), (const u16*)x.data_ptr(), (u16*)out.data_ptr(), T, N, K, nbk, accumulate ? 1 : 0);
+  SFT_LAUNCH_CHECK();
+}
+
+}  // namespace wgrad
+
+// cfg: 0 = auto, 1 = 256x256 (8 waves 2x4), 2 = 256x128 (8 waves 4x2); +2 = register-pipelined loop
+void wgrad_gemm(at::Tensor out, at::Tensor dy, at::Tensor x, bool accumulate, int64_t cfg) {
+  SFT_CHECK_CUDA(dy);
+  SFT_CHECK_BF16(dy);
+  SFT_CHECK_BF16(x);
+  SFT_CHECK_BF16(out);
+  SFT_CHECK_CONTIG(dy);
+  SFT_CHECK_CONTIG(x);
+  SFT_CHECK_CONTIG(out);
+  SFT_CHECK(dy.dim() == 2 && x.dim() == 2 && out.dim() == 2, "wgrad_gemm: 2-D operands");
+  const int64_t T = dy.size(0), N = dy.size(1), K = x.size(1);
+  SFT_CHECK(x.size(0) == T && out.size(0) == N && out.size(1) == K, "wgrad_gemm: shape mismatch");
+  SFT_CHECK(T % 32 == 0 && T > 0, "wgrad_gemm: T must be a positive multiple of 32");
+  SFT_CHECK(cfg >= 7 || cfg == 0 || T % wgrad::BK == 0, "wgrad_gemm: cfg 1-6 need T % 64 == 0");
+  if (cfg == 0) cfg = (N % 256 == 0 && K % 256 == 0 && (N / 256) * (K / 256) >= 512) ? 1 : 2;
+  if (cfg == 1 || cfg == 3) {
+    SFT_CHECK(N % 256 == 0 && K % 256 == 0, "wgrad_gemm 256x256: N, K multiples of 256");
+    if (cfg == 1) wgrad::launch<256, 256, 2, 4, 0>(dy, x, out, accumulate);
+    else wgrad::launch<256, 256, 2, 4, 1>(dy, x, out, accumulate);
+  } else if (cfg == 7) {
+    SFT_CHECK(N % 256 == 0 && K % 256 == 0 && T % 32 == 0, "wgrad_gemm ring 256x256: N, K multiples of 256");
+    wgrad::launch_ring<256, 256, 2, 4, 5>(dy, x, out, accumulate);
+  } else if (cfg == 8) {
+    SFT_CHECK(N % 256 == 0 && K % 256 == 0 && T % 32 == 0, "wgrad_gemm ring 256x256: N, K multiples of 256");
+    wgrad::launch_ring<256, 256, 2, 4, 4>(dy, x, out, accumulate);
+  } else if (cfg == 9) {
+    SFT_CHECK(N % 256 == 0 && K % 128 == 0 && T % 32 == 0, "wgrad_gemm ring 256x128: N multiple of 256, K of 128");
+    wgrad::launch_ring<256, 128, 4, 2, 6>(dy, x, out, accumulate);
+  } else if (cfg == 5 || cfg == 6) {  // diagnostics (wrong results): 5 = no loads in loop, 6 = no barrier
+    if (cfg == 5) wgrad::launch<256, 256, 2, 4, 2>(dy, x, out, accumulate);
+    else wgrad::launch<256, 256, 2, 4, 3>(dy, x, out, accumulate);
+  } else {
+    SFT_CHECK(N % 256 == 0 && K % 128 == 0, "wgrad_gemm 256x128: N multiple of 256, K of 128");
+    if (cfg == 2) wgrad::launch<256, 128, 4, 2, 0>(dy, x, out, accumulate);
+    else wgrad::launch<256, 128, 4, 2, 1>(dy, x, out, accumulate);
+  }
+}
+
+TORCH_LIBRARY_IMPL(sftamd, CUDA, m) { m.impl("wgrad_gemm", &wgrad_gemm); }
+
+}  // namespace sftamd

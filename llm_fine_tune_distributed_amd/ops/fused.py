@@ -16,6 +16,7 @@ DDP engine launch bucket all-reduces while backward is still running.
 from __future__ import annotations
 
 import math
+import os
 from typing import Optional, Tuple
 
 import torch
@@ -40,6 +41,39 @@ def _weight_grad_done(param: torch.Tensor) -> None:
             hook(param)
 
 
+_WGRAD_MODE = os.environ.get("SFTAMD_WGRAD", "auto")  # auto | blas | <cfg int> (kernel variant)
+
+
+def _wgrad_cfg(T: int, N: int, K: int) -> int:
+    """Which wgrad GEMM runs dW[N,K] = dy[T,N]^T x[T,K]: 0 = hipBLASLt/rocBLAS, else a variant of the
+    hand-written gfx950 kernel (csrc/gemm_wgrad.hip). Chosen from tools/bench_wgrad.py on MI355X
+    (profiles/r1_wgrad_microbench.md): the 256x256 ring kernel wherever it fills >= 2 waves of the
+    256 CUs (gate_up 0.62 vs 0.77 ms, lm_head 3.5 vs 4.0 ms at T=8192), the 256x128 ring kernel on
+    mid-size grids (qkv 0.113 vs 0.142 ms); BLAS elsewhere (o_proj, down_proj: BLAS equal/faster)."""
+    if _WGRAD_MODE == "blas" or T % 32 or T < 1024:
+        return 0
+    if _WGRAD_MODE not in ("auto", ""):
+        return int(_WGRAD_MODE)
+    if N % 256 == 0 and K % 256 == 0 and (N // 256) * (K // 256) >= 512:
+        return 7
+    if N % 256 == 0 and K % 128 == 0 and 160 <= (N // 256) * (K // 128) < 512:
+        return 9
+    return 0
+
+
+def _wgrad_mm(out: torch.Tensor, dy2d: torch.Tensor, x2d: torch.Tensor, accumulate: bool) -> None:
+    """out (+)= dy2d^T @ x2d, all bf16 (out is the flat-buffer gradient view)."""
+    cfg = 0
+    if _ext.use_hip(dy2d) and dy2d.dtype == torch.bfloat16 and out.is_contiguous():
+        cfg = _wgrad_cfg(dy2d.shape[0], dy2d.shape[1], x2d.shape[1])
+    if cfg:
+        _ext.ops().wgrad_gemm(out, dy2d.contiguous(), x2d.contiguous(), accumulate, cfg)
+    elif accumulate:
+        out.addmm_(dy2d.t(), x2d)
+    else:
+        torch.mm(dy2d.t(), x2d, out=out)
+
+
 def _accumulate_weight_grad(param: torch.Tensor, dy2d: torch.Tensor, x2d: torch.Tensor,
                             scale: Optional[torch.Tensor] = None):
     """dW = dy^T @ x (optionally * scale). Accumulates into main_grad if present."""
@@ -49,10 +83,8 @@ def _accumulate_weight_grad(param: torch.Tensor, dy2d: torch.Tensor, x2d: torch.
     if mg is not None:
         fresh = getattr(param, "_sftamd_fresh", False)
         if mg.dtype == dy2d.dtype:
-            if fresh:  # first contribution of the step: beta=0 GEMM, no zero-fill pass needed
-                torch.mm(dy2d.t(), x2d, out=mg)
-            else:
-                mg.addmm_(dy2d.t(), x2d)
+            # first contribution of the step: beta=0 GEMM, no zero-fill pass needed
+            _wgrad_mm(mg, dy2d, x2d, accumulate=not fresh)
         elif fresh:
             mg.copy_(torch.mm(dy2d.t(), x2d))
         else:

@@ -231,3 +231,19 @@ def test_decode_attention(L):
     att = torch.einsum("grd,sgd->grs", qf, kc[:L].float()) / math.sqrt(D)
     ref_o = torch.einsum("grs,sgd->grd", att.softmax(-1), vc[:L].float()).reshape(-1)
     assert rel_err(out, ref_o) < 1e-2
+
+
+@pytest.mark.parametrize("cfg,T,N,K", [(1, 256, 512, 512), (2, 192, 512, 256), (0, 128, 256, 384), (1, 64, 256, 256),
+                                       (3, 256, 512, 512), (4, 192, 512, 256), (7, 352, 512, 512), (7, 96, 256, 256),
+                                       (8, 256, 512, 768), (9, 416, 512, 384), (9, 32, 256, 128)])
+@pytest.mark.parametrize("accumulate", [False, True])
+def test_wgrad_gemm(cfg, T, N, K, accumulate):
+    torch.manual_seed(0)
+    dy = torch.randn(T, N, device="cuda", dtype=torch.bfloat16)
+    x = torch.randn(T, K, device="cuda", dtype=torch.bfloat16)
+    out = torch.randn(N, K, device="cuda", dtype=torch.bfloat16)
+    base = out.float().clone()
+    _ext.ops().wgrad_gemm(out, dy, x, accumulate, cfg)
+    want = dy.float().t() @ x.float() + (base if accumulate else 0)
+    err = (out.float() - want).abs().max().item()
+    assert err <= 0.02 * want.abs().max().item(), err
