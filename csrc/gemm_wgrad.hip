@@ -338,16 +338,20 @@ struct RStager {
   // step then issues exactly PPW DMAs, so the counted waits are compile-time constants with no
   // tail branches (a branch around a wait makes the compiler's own waitcnt pass assume the
   // no-wait path and drain lgkmcnt before the next MFMA block).
-  __device__ __forceinline__ void issue(char* buf) {
-#pragma unroll
-    for (int j = 0; j < G::NIMG; ++j) {
-      const u16* p = j < G::IA ? pa + j * 128 : pb + (j - G::IA) * 128;
-      glds16(p, buf + j * IMGR + w * 1024);
-    }
+  __device__ __forceinline__ void piece(char* buf, int j) {
+    const u16* p = j < G::IA ? pa + j * 128 : pb + (j - G::IA) * 128;
+    glds16(p, buf + j * IMGR + w * 1024);
+  }
+  __device__ __forceinline__ void advance() {
     if (--left > 0) {
       pa += BKR * lda;
       pb += BKR * ldb;
     }
+  }
+  __device__ __forceinline__ void issue(char* buf) {
+#pragma unroll
+    for (int j = 0; j < G::NIMG; ++j) piece(buf, j);
+    advance();
   }
 };
 
@@ -383,7 +387,7 @@ constexpr unsigned waitcnt_imm(int vm, int lgkm) {  // gfx9: vmcnt[3:0] expcnt[6
 // the A fragments are refilled in place — fragment row i of step t+1 is read right after the four
 // MFMAs of row i of step t, so it still has a whole step of MFMAs to land — which keeps the kernel
 // at ~216 VGPRs (2 waves per SIMD) with every MFMA operand already resident.
-template <class G>
+template <class G, bool SCHED>
 __device__ __forceinline__ void ring_loop(char* __restrict__ b0, char* __restrict__ b1, char* __restrict__ b2,
                                           char* __restrict__ b3, char* __restrict__ b4, char* __restrict__ b5,
                                           int nsteps, RStager<G>& st, const int (&offA)[G::FM],
@@ -402,19 +406,28 @@ __device__ __forceinline__ void ring_loop(char* __restrict__ b0, char* __restric
       if (t0 + u < nsteps) {
         __builtin_amdgcn_s_waitcnt(waitcnt_imm((NS - 2) * PPW, 0));
         __builtin_amdgcn_s_barrier();
-        st.issue(pick(u % NS, b0, b1, b2, b3, b4, b5));
+        char* dst = pick(u % NS, b0, b1, b2, b3, b4, b5);
         const char* nxt = pick((u + 1) % NS, b0, b1, b2, b3, b4, b5);
         const int cb = u & 1;
 #pragma unroll
         for (int j = 0; j < G::FN; ++j) fb[cb ^ 1][j] = lds_tr(nxt, offB[j]);
         __builtin_amdgcn_s_setprio(1);
+        // one LDS-DMA piece after each of the first NIMG fragment rows: the DMA issue cost is
+        // spread between MFMA groups instead of stalling every wave right after the barrier
 #pragma unroll
         for (int i = 0; i < G::FM; ++i) {
 #pragma unroll
           for (int j = 0; j < G::FN; ++j)
             acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[cb][j], acc[i][j], 0, 0, 0);
           fa[i] = lds_tr(nxt, offA[i]);
+          if (i < G::NIMG) st.piece(dst, i);
+          if (SCHED) {
+            __builtin_amdgcn_sched_group_barrier(0x008, G::FN, 0);  // MFMA
+            __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);      // DS read (one fragment)
+            if (i < G::NIMG) __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);  // VMEM read (the DMA)
+          }
         }
+        st.advance();
         __builtin_amdgcn_s_setprio(0);
       }
     }
@@ -422,7 +435,7 @@ __device__ __forceinline__ void ring_loop(char* __restrict__ b0, char* __restric
   __builtin_amdgcn_s_waitcnt(waitcnt_imm(0, 0));  // drain the tail DMAs before LDS is reused
 }
 
-template <int BM, int BN, int WM, int WN, int NS>
+template <int BM, int BN, int WM, int WN, int NS, bool SCHED>
 __global__ void __launch_bounds__(NT) ring_kernel(const u16* __restrict__ A, const u16* __restrict__ B,
                                                   u16* __restrict__ C, int T, int N, int K, int nbk, int accumulate) {
   using G = RCfg<BM, BN, WM, WN, NS>;
@@ -459,16 +472,16 @@ __global__ void __launch_bounds__(NT) ring_kernel(const u16* __restrict__ A, con
   char* b[6];
 #pragma unroll
   for (int i = 0; i < 6; ++i) b[i] = smem + (i < NS ? i : 0) * G::STAGE;
-  ring_loop<G>(b[0], b[1], b[2], b[3], b[4], b[5], T / BKR, st, offA, offB, acc);
+  ring_loop<G, SCHED>(b[0], b[1], b[2], b[3], b[4], b[5], T / BKR, st, offA, offB, acc);
   __syncthreads();
   epilogue<G>(smem, acc, C, K, n0, k0, wm, wk, w, lane, accumulate);
 }
 
-template <int BM, int BN, int WM, int WN, int NS>
+template <int BM, int BN, int WM, int WN, int NS, bool SCHED = false>
 void launch_ring(const at::Tensor& dy, const at::Tensor& x, at::Tensor& out, bool accumulate) {
   const int T = dy.size(0), N = dy.size(1), K = x.size(1);
   const int nbn = N / BM, nbk = K / BN;
-  ring_kernel<BM, BN, WM, WN, NS><<<nbn * nbk, NT, 0, cur_stream()>>>(
+  ring_kernel<BM, BN, WM, WN, NS, SCHED><<<nbn * nbk, NT, 0, cur_stream()>>>(
       (const u16*)dy.data_ptr(), (const u16*)x.data_ptr(), (u16*)out.data_ptr(), T, N, K, nbk, accumulate ? 1 : 0);
   SFT_LAUNCH_CHECK();
 }
@@ -512,6 +525,12 @@ void wgrad_gemm(at::Tensor out, at::Tensor dy, at::Tensor x, bool accumulate, in
   } else if (cfg == 9) {
     SFT_CHECK(N % 256 == 0 && K % 128 == 0 && T % 32 == 0, "wgrad_gemm ring 256x128: N multiple of 256, K of 128");
     wgrad::launch_ring<256, 128, 4, 2, 6>(dy, x, out, accumulate);
+  } else if (cfg == 10) {
+    SFT_CHECK(N % 256 == 0 && K % 256 == 0 && T % 32 == 0, "wgrad_gemm ring 256x256: N, K multiples of 256");
+    wgrad::launch_ring<256, 256, 2, 4, 5, true>(dy, x, out, accumulate);
+  } else if (cfg == 11) {
+    SFT_CHECK(N % 256 == 0 && K % 128 == 0 && T % 32 == 0, "wgrad_gemm ring 256x128: N multiple of 256, K of 128");
+    wgrad::launch_ring<256, 128, 4, 2, 6, true>(dy, x, out, accumulate);
   } else if (cfg == 5 || cfg == 6) {  // diagnostics (wrong results): 5 = no loads in loop, 6 = no barrier
     if (cfg == 5) wgrad::launch<256, 256, 2, 4, 2>(dy, x, out, accumulate);
     else wgrad::launch<256, 256, 2, 4, 3>(dy, x, out, accumulate);

@@ -3,9 +3,9 @@
 // One wave64 per row: each lane owns NV 16-byte vectors (8 bf16) of the row, the sum of
 // squares is a pure in-wave shuffle reduction (no LDS, no block barrier), and the
 // residual add is fused so the residual stream is read once and written once.
-// Backward keeps the weight gradient in registers across a grid-stride loop over rows,
-// reduces the 4 waves of a block in LDS, and a second kernel sums the per-block
-// partials in a fixed order (deterministic dW, no float atomics in HBM).
+// Backward keeps the weight gradient in registers across a grid-stride loop over rows (two rows
+// in flight per wave), reduces the 8 waves of a block in LDS, and a second kernel sums the
+// per-block partials in a fixed order (deterministic dW, no float atomics in HBM).
 #include "common.h"
 
 namespace sftamd {
@@ -54,57 +54,101 @@ __global__ __launch_bounds__(256) void rmsnorm_fwd_kernel(const u16* __restrict_
   if (lane == 0) rstd_out[row] = rstd;
 }
 
+// Backward: 8 waves per block, each wave handles two rows per iteration (both rows' h/dy loads
+// are in flight together: 16 KB per wave, 128 KB per CU at one block per CU), dW accumulated in
+// registers across the grid-stride loop and reduced over the block's waves in LDS.
 template <int NV>
-__global__ __launch_bounds__(256) void rmsnorm_bwd_kernel(const u16* __restrict__ dy, const u16* __restrict__ h,
+constexpr int bwd_threads() { return NV <= 4 ? 512 : 256; }  // H = 4096 rows need > 256 VGPRs: 1 wave/SIMD
+
+template <int NV>
+__global__ __launch_bounds__(bwd_threads<NV>()) void rmsnorm_bwd_kernel(const u16* __restrict__ dy, const u16* __restrict__ h,
                                                           const u16* __restrict__ w, const float* __restrict__ rstd,
                                                           const u16* __restrict__ dres, u16* __restrict__ dx,
                                                           float* __restrict__ dw_part, int M, int H) {
+  constexpr int RPI = NV <= 4 ? 2 : 1;  // rows in flight per wave (register budget: 2 waves/SIMD)
   __shared__ float red[4096];
+  __shared__ float wl[4096];
   const int lane = threadIdx.x & 63;
-  const int nwaves = gridDim.x * 4;
-  float wv[NV][8], dw[NV][8];
+  constexpr int NT = bwd_threads<NV>(), WPB = NT / 64;
+  const int nwaves = gridDim.x * WPB;
+  float dw[NV][8];
 #pragma unroll
-  for (int j = 0; j < NV; ++j) {
-    const int c = (lane + 64 * j) * 8;
+  for (int j = 0; j < NV; ++j)
 #pragma unroll
     for (int i = 0; i < 8; ++i) dw[j][i] = 0.f;
-    if (c < H) unpack8(*(const uint4*)(w + c), wv[j]);
+  for (int c = threadIdx.x; c < H; c += NT) {
+    red[c] = 0.f;
+    wl[c] = bf2f(w[c]);
   }
-  for (int row = blockIdx.x * 4 + (threadIdx.x >> 6); row < M; row += nwaves) {
-    const long base = (long)row * H;
-    const float r = rstd[row];
-    float n[NV][8], g[NV][8];
-    float dot = 0.f;
+  __syncthreads();
+  for (int row0 = blockIdx.x * WPB + (threadIdx.x >> 6); row0 < M; row0 += RPI * nwaves) {
+    uint4 hv[RPI][NV], gv[RPI][NV];
 #pragma unroll
-    for (int j = 0; j < NV; ++j) {
-      const int c = (lane + 64 * j) * 8;
-      if (c < H) {
-        unpack8(*(const uint4*)(h + base + c), n[j]);
-        unpack8(*(const uint4*)(dy + base + c), g[j]);
+    for (int q = 0; q < RPI; ++q) {
+      const int row = row0 + q * nwaves;
+      const long base = (long)row * H;
 #pragma unroll
-        for (int i = 0; i < 8; ++i) {
-          n[j][i] *= r;
-          dw[j][i] += g[j][i] * n[j][i];
-          g[j][i] *= wv[j][i];
-          dot += g[j][i] * n[j][i];
+      for (int j = 0; j < NV; ++j) {
+        const int c = (lane + 64 * j) * 8;
+        if (c < H && row < M) {
+          hv[q][j] = *(const uint4*)(h + base + c);
+          gv[q][j] = *(const uint4*)(dy + base + c);
+        } else {
+          hv[q][j] = make_uint4(0, 0, 0, 0);
+          gv[q][j] = make_uint4(0, 0, 0, 0);
         }
       }
     }
-    dot = wave_sum(dot) / (float)H;
 #pragma unroll
-    for (int j = 0; j < NV; ++j) {
-      const int c = (lane + 64 * j) * 8;
-      if (c < H) {
-        float o[8], d[8];
-        if (dres) unpack8(*(const uint4*)(dres + base + c), d);
+    for (int q = 0; q < RPI; ++q) {
+      const int row = row0 + q * nwaves;
+      if (row >= M) break;
+      const long base = (long)row * H;
+      const float r = rstd[row];
+      // rows stay packed (bf16) in registers and are unpacked again in the second pass: keeps
+      // the kernel at 2 waves/SIMD without spills up to H = 4096
+      float dot = 0.f;
 #pragma unroll
-        for (int i = 0; i < 8; ++i) o[i] = r * (g[j][i] - n[j][i] * dot) + (dres ? d[i] : 0.f);
-        *(uint4*)(dx + base + c) = pack8(o);
+      for (int j = 0; j < NV; ++j) {
+        const int c = (lane + 64 * j) * 8;
+        float wv[8], n[8], g[8];
+        *(float4*)&wv[0] = *(const float4*)&wl[c < H ? c : 0];
+        *(float4*)&wv[4] = *(const float4*)&wl[(c < H ? c : 0) + 4];
+        unpack8(hv[q][j], n);
+        unpack8(gv[q][j], g);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          const float nn = n[i] * r;
+          dw[j][i] += g[i] * nn;
+          dot += g[i] * wv[i] * nn;
+        }
+      }
+      uint4 dv[NV];
+      if (dres) {
+#pragma unroll
+        for (int j = 0; j < NV; ++j) {
+          const int c = (lane + 64 * j) * 8;
+          dv[j] = c < H ? *(const uint4*)(dres + base + c) : make_uint4(0, 0, 0, 0);
+        }
+      }
+      dot = wave_sum(dot) / (float)H;
+#pragma unroll
+      for (int j = 0; j < NV; ++j) {
+        const int c = (lane + 64 * j) * 8;
+        if (c < H) {
+          float wv[8], n[8], g[8], o[8], d[8];
+          *(float4*)&wv[0] = *(const float4*)&wl[c];
+          *(float4*)&wv[4] = *(const float4*)&wl[c + 4];
+          unpack8(hv[q][j], n);
+          unpack8(gv[q][j], g);
+          if (dres) unpack8(dv[j], d);
+#pragma unroll
+          for (int i = 0; i < 8; ++i) o[i] = r * (g[i] * wv[i] - n[i] * r * dot) + (dres ? d[i] : 0.f);
+          *(uint4*)(dx + base + c) = pack8(o);
+        }
       }
     }
   }
-  for (int c = threadIdx.x; c < H; c += 256) red[c] = 0.f;
-  __syncthreads();
 #pragma unroll
   for (int j = 0; j < NV; ++j) {
     const int c = (lane + 64 * j) * 8;
@@ -114,7 +158,7 @@ __global__ __launch_bounds__(256) void rmsnorm_bwd_kernel(const u16* __restrict_
     }
   }
   __syncthreads();
-  for (int c = threadIdx.x; c < H; c += 256) dw_part[(long)blockIdx.x * H + c] = red[c];
+  for (int c = threadIdx.x; c < H; c += NT) dw_part[(long)blockIdx.x * H + c] = red[c];
 }
 
 // out[c] = sum_b part[b][c] in a fixed order (deterministic). Block = 64 columns x 4 row
@@ -195,11 +239,11 @@ std::tuple<at::Tensor, at::Tensor> rmsnorm_bwd(const at::Tensor& dy, const at::T
     SFT_CHECK(dres->is_contiguous() && dres->scalar_type() == at::kBFloat16, "dres");
     dr = (const u16*)dres->data_ptr();
   }
-  int nblk = std::min((M + 3) / 4, 1024);  // >=4 waves/SIMD in flight; partial dW rows reduced below
+  int nblk = std::min((M + 15) / 16, 256);  // one 8-wave block per CU, >= 2 rows per wave
   nblk = std::max(nblk, 1);
   auto part = at::empty({nblk, H}, h.options().dtype(at::kFloat));
   auto dw = at::empty({H}, h.options().dtype(at::kFloat));
-  NV_DISPATCH(H, rmsnorm_bwd_kernel<NV><<<nblk, 256, 0, cur_stream()>>>(
+  NV_DISPATCH(H, rmsnorm_bwd_kernel<NV><<<nblk, bwd_threads<NV>(), 0, cur_stream()>>>(
                      (const u16*)dy.data_ptr(), (const u16*)h.data_ptr(), (const u16*)weight.data_ptr(),
                      rstd.data_ptr<float>(), dr, (u16*)dx.data_ptr(), part.data_ptr<float>(), M, H));
   SFT_LAUNCH_CHECK();

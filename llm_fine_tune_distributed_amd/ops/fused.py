@@ -48,15 +48,15 @@ def _wgrad_cfg(T: int, N: int, K: int) -> int:
     """Which wgrad GEMM runs dW[N,K] = dy[T,N]^T x[T,K]: 0 = hipBLASLt/rocBLAS, else a variant of the
     hand-written gfx950 kernel (csrc/gemm_wgrad.hip). Chosen from tools/bench_wgrad.py on MI355X
     (profiles/r1_wgrad_microbench.md): the 256x256 ring kernel wherever it fills >= 2 waves of the
-    256 CUs (gate_up 0.62 vs 0.77 ms, lm_head 3.5 vs 4.0 ms at T=8192), the 256x128 ring kernel on
-    mid-size grids (qkv 0.113 vs 0.142 ms); BLAS elsewhere (o_proj, down_proj: BLAS equal/faster)."""
+    256 CUs (gate_up 0.58 vs 0.74 ms, lm_head 3.2 vs 3.9 ms at T=8192), the 256x128 ring kernel on
+    mid-size grids (qkv 0.113 vs 0.139 ms, down 0.337 vs 0.349 ms); BLAS for small grids (o_proj)."""
     if _WGRAD_MODE == "blas" or T % 32 or T < 1024:
         return 0
     if _WGRAD_MODE not in ("auto", ""):
         return int(_WGRAD_MODE)
     if N % 256 == 0 and K % 256 == 0 and (N // 256) * (K // 256) >= 512:
-        return 7
-    if N % 256 == 0 and K % 128 == 0 and 160 <= (N // 256) * (K // 128) < 512:
+        return 10
+    if N % 256 == 0 and K % 128 == 0 and (N // 256) * (K // 128) >= 160:
         return 9
     return 0
 
