@@ -12,6 +12,10 @@ TORCH_LIBRARY(sftamd, m) {
   m.def("swiglu_bwd(Tensor dy, Tensor gate_up) -> Tensor");
   m.def("rope_(Tensor(a!) qkv, Tensor cos, Tensor sin, int n_q, int n_kv, int head_dim, bool inverse) -> ()");
   m.def("embedding_fwd(Tensor ids, Tensor weight) -> Tensor");
+  m.def("dropout_add(Tensor? a, Tensor b, float p, int seed) -> Tensor");
+  m.def("lora_widen(Tensor x, int R, float p, int seed) -> (Tensor, Tensor)");
+  m.def("lora_fwd(Tensor x, Tensor A, float s, float p, int seed) -> (Tensor, Tensor)");
+  m.def("lora_bwd_dx(Tensor base, Tensor dxa, Tensor A, float p, int seed) -> Tensor");
   m.def("embedding_bwd(Tensor dy, Tensor sorted_ids, Tensor perm, Tensor(a!) grad_weight) -> ()");
   // loss
   m.def("ce_fwd(Tensor(a!) logits, Tensor labels, Tensor inv_count, bool write_grad) -> Tensor");

@@ -52,6 +52,18 @@ __device__ __forceinline__ float wave_max(float v) {
   return v;
 }
 
+// Counter-based 32-bit hash (murmur3-style finaliser) of a 64-bit element index and a seed: the
+// random stream of stochastic rounding and LoRA dropout. Regenerable anywhere (no RNG state).
+__device__ __forceinline__ unsigned hash_u32(unsigned long long i, unsigned seed) {
+  unsigned x = (unsigned)i * 0x9E3779B9u ^ (unsigned)(i >> 32) * 0x85EBCA6Bu ^ seed * 0xC2B2AE35u;
+  x ^= x >> 16;
+  x *= 0x7FEB352Du;
+  x ^= x >> 15;
+  x *= 0x846CA68Bu;
+  x ^= x >> 16;
+  return x;
+}
+
 inline hipStream_t cur_stream() { return c10::hip::getCurrentHIPStream().stream(); }
 
 inline int num_cus() { return 256; }  // MI355X: 8 XCDs x 32 CUs

@@ -228,7 +228,107 @@ void embedding_bwd(const at::Tensor& dy, const at::Tensor& sorted_ids, const at:
   SFT_LAUNCH_CHECK();
 }
 
+// ---------------------------------------------------------------------------------------------
+// LoRA dropout: out[t,k] = a[t,k] + keep(t*K+k) * b[t,k] / (1-p), keep = hash(index, seed) >= p*2^32.
+// The mask is a pure function of (seed, element index), so backward regenerates it instead of
+// storing it; a and b may be column slices of wider buffers (row strides lda, ldb).
+// grid: (column blocks of 256 x 8 elements, rows); no integer division in the index math
+__global__ __launch_bounds__(256) void dropout_add_kernel(const u16* __restrict__ a, long lda, const u16* __restrict__ b,
+                                                          long ldb, u16* __restrict__ out, long ldo, long T, int K,
+                                                          unsigned thresh, float scale, unsigned seed) {
+  const int k = (blockIdx.x * 256 + threadIdx.x) * 8;
+  if (k >= K) return;
+  for (long t = blockIdx.y; t < T; t += gridDim.y) {
+  float bv[8], o[8];
+  unpack8(*(const uint4*)(b + t * ldb + k), bv);
+  if (a) {
+    unpack8(*(const uint4*)(a + t * lda + k), o);
+  } else {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) o[i] = 0.f;
+  }
+  const unsigned long long idx = (unsigned long long)t * K + k;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) o[i] += hash_u32(idx + i, seed) >= thresh ? bv[i] * scale : 0.f;
+  *(uint4*)(out + t * ldo + k) = pack8(o);
+  }
+}
+
+// LoRA input widening: X[:, :K] = x and (p > 0) xd = dropout(x), one read of x.
+__global__ __launch_bounds__(256) void lora_widen_kernel(const u16* __restrict__ x, u16* __restrict__ X, long ldX,
+                                                         u16* __restrict__ xd, long T, int K, unsigned thresh,
+                                                         float scale, unsigned seed) {
+  const int k = (blockIdx.x * 256 + threadIdx.x) * 8;
+  if (k >= K) return;
+  for (long t = blockIdx.y; t < T; t += gridDim.y) {
+  const uint4 v = *(const uint4*)(x + t * K + k);
+  *(uint4*)(X + t * ldX + k) = v;
+  if (xd) {
+    float f[8];
+    unpack8(v, f);
+    const unsigned long long idx = (unsigned long long)t * K + k;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) f[i] = hash_u32(idx + i, seed) >= thresh ? f[i] * scale : 0.f;
+    *(uint4*)(xd + t * (long)K + k) = pack8(f);
+  }
+  }
+}
+
+static unsigned drop_thresh(double p, float* scale) {
+  const double pc = p < 0 ? 0 : (p > 0.999 ? 0.999 : p);
+  *scale = (float)(1.0 / (1.0 - pc));
+  return (unsigned)(pc * 4294967296.0);
+}
+
+at::Tensor dropout_add(const c10::optional<at::Tensor>& a, const at::Tensor& b, double p, int64_t seed) {
+  SFT_CHECK_CUDA(b);
+  SFT_CHECK_BF16(b);
+  SFT_CHECK(b.dim() == 2 && b.stride(1) == 1 && b.stride(0) % 8 == 0 && b.size(1) % 8 == 0, "dropout_add: b layout");
+  const long T = b.size(0);
+  const int K = b.size(1);
+  const u16* ap = nullptr;
+  long lda = 0;
+  if (a.has_value() && a->defined()) {
+    SFT_CHECK(a->sizes() == b.sizes() && a->stride(1) == 1 && a->stride(0) % 8 == 0 && a->scalar_type() == at::kBFloat16,
+              "dropout_add: a layout");
+    ap = (const u16*)a->data_ptr();
+    lda = a->stride(0);
+  }
+  auto out = at::empty({T, K}, b.options());
+  if (T == 0) return out;
+  float scale;
+  const unsigned thresh = drop_thresh(p, &scale);
+  dim3 grid((K / 8 + 255) / 256, (unsigned)std::min<long>(T, 65535));
+  dropout_add_kernel<<<grid, 256, 0, cur_stream()>>>(ap, lda, (const u16*)b.data_ptr(), b.stride(0), (u16*)out.data_ptr(),
+                                                     K, T, K, thresh, scale, (unsigned)seed);
+  SFT_LAUNCH_CHECK();
+  return out;
+}
+
+// Returns (X [T, K+R] with X[:, :K] = x (X[:, K:] uninitialised), xd = dropout(x) or an empty tensor if p == 0).
+std::tuple<at::Tensor, at::Tensor> lora_widen(const at::Tensor& x, int64_t R, double p, int64_t seed) {
+  SFT_CHECK_CUDA(x);
+  SFT_CHECK_BF16(x);
+  SFT_CHECK_CONTIG(x);
+  SFT_CHECK(x.dim() == 2 && x.size(1) % 8 == 0 && R % 8 == 0, "lora_widen: x [T, K], K and R multiples of 8");
+  const long T = x.size(0);
+  const int K = x.size(1);
+  auto X = at::empty({T, K + R}, x.options());
+  at::Tensor xd = p > 0 ? at::empty_like(x) : at::empty({0}, x.options());
+  if (T == 0) return {X, xd};
+  float scale;
+  const unsigned thresh = drop_thresh(p, &scale);
+  dim3 grid((K / 8 + 255) / 256, (unsigned)std::min<long>(T, 65535));
+  lora_widen_kernel<<<grid, 256, 0, cur_stream()>>>((const u16*)x.data_ptr(), (u16*)X.data_ptr(), K + R,
+                                                    p > 0 ? (u16*)xd.data_ptr() : nullptr, T, K, thresh, scale,
+                                                    (unsigned)seed);
+  SFT_LAUNCH_CHECK();
+  return {X, xd};
+}
+
 TORCH_LIBRARY_IMPL(sftamd, CUDA, m) {
+  m.impl("dropout_add", &dropout_add);
+  m.impl("lora_widen", &lora_widen);
   m.impl("swiglu_fwd", &swiglu_fwd);
   m.impl("swiglu_bwd", &swiglu_bwd);
   m.impl("rope_", &rope_);

@@ -46,15 +46,7 @@ __device__ __forceinline__ void adam_elem(float& w, float g, float& m, float& v,
 }
 
 // Stateless per-element hash (Wang/PCG-style mix) for stochastic rounding.
-__device__ __forceinline__ unsigned sr_hash(unsigned long long i, unsigned seed) {
-  unsigned x = (unsigned)i * 0x9E3779B9u ^ (unsigned)(i >> 32) * 0x85EBCA6Bu ^ seed * 0xC2B2AE35u;
-  x ^= x >> 16;
-  x *= 0x7FEB352Du;
-  x ^= x >> 15;
-  x *= 0x846CA68Bu;
-  x ^= x >> 16;
-  return x;
-}
+__device__ __forceinline__ unsigned sr_hash(unsigned long long i, unsigned seed) { return hash_u32(i, seed); }
 
 // fp32 -> bf16 with stochastic rounding: add uniform noise below the bf16 ulp, then truncate.
 // E[bf16(w)] = w, so pure-bf16 weights do not lose small Adam updates to round-to-nearest.

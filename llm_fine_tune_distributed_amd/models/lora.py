@@ -92,8 +92,31 @@ def apply_lora(model, cfg: LoRAConfig = None):
     for n, p in model.named_parameters():
         if ".lora." in n and p.numel() > 0:
             p.requires_grad_(True)
+    for layer in model.model.layers:
+        for owner, wname, key in ((layer.self_attn, "qkv_proj", "qkv"), (layer.self_attn, "o_proj", "o"),
+                                  (layer.mlp, "gate_up_proj", "gate_up"), (layer.mlp, "down_proj", "down")):
+            _widen(owner, wname, owner.lora[key])
     model._lora_config = cfg
     return model
+
+
+@torch.no_grad()
+def _widen(owner: nn.Module, wname: str, fl: FusedLoRA) -> None:
+    """Re-home the frozen base weight W [n, K] as the left block of W' = [W | B_blockdiag] [n, K+R]
+    (ops.LoRAWideFn): the base Parameter becomes a column-slice view of W', so checkpoint I/O,
+    merge_lora and plain inference keep working on it unchanged."""
+    w = getattr(owner, wname)
+    act = [i for i, a in enumerate(fl.active) if a]
+    if not act:
+        return
+    n, K = w.shape
+    R = fl.r * len(act)
+    wide = torch.zeros(n, K + R, device=w.device, dtype=w.dtype)
+    wide[:, :K].copy_(w)
+    setattr(owner, wname, nn.Parameter(wide[:, :K], requires_grad=False))
+    offs = [sum(fl.out_splits[:i]) for i in range(len(fl.out_splits))]
+    fl.wide = wide
+    fl.wide_meta = [(offs[i], fl.out_splits[i], j * fl.r) for j, i in enumerate(act)]
 
 
 def lora_state_dict(model) -> Dict[str, torch.Tensor]:

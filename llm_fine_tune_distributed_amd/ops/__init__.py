@@ -5,6 +5,7 @@ from .fused import (
     IGNORE_INDEX,
     add_rms_norm,
     decode_attention,
+    dropout_add,
     embedding,
     flash_attention,
     linear,
@@ -17,7 +18,7 @@ from .fused import (
 from .optim_kernels import adamw_flat_, grad_norm_flat
 
 __all__ = [
-    "reference", "load_extension", "use_hip", "hip_disabled", "IGNORE_INDEX", "add_rms_norm", "decode_attention",
+    "reference", "load_extension", "use_hip", "hip_disabled", "IGNORE_INDEX", "add_rms_norm", "decode_attention", "dropout_add",
     "embedding", "flash_attention", "linear", "lora_linear", "lm_head_cross_entropy", "rms_norm", "rope_", "swiglu",
     "adamw_flat_", "grad_norm_flat",
 ]

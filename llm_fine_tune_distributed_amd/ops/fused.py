@@ -441,9 +441,99 @@ class LoRALinearFn(Function):
         return (dx, dW, None, None, None, *dAs, *dBs)
 
 
+def dropout_add(a: Optional[torch.Tensor], b: torch.Tensor, p: float, seed: int) -> torch.Tensor:
+    """(a or 0) + dropout(b) with a counter-hash mask (regenerable from seed; see csrc/elementwise.hip)."""
+    if _ext.use_hip(b):
+        return _ext.ops().dropout_add(a, b, float(p), int(seed))
+    return ref.dropout_add(a, b, p, seed)
+
+
+def _lora_fwd(x2d, acat, s, p, seed):
+    if _ext.use_hip(x2d) and x2d.shape[1] % 256 == 0 and acat.shape[0] % 16 == 0 and acat.shape[0] <= 64:
+        X, xd = _ext.ops().lora_fwd(x2d, acat, float(s), float(p), int(seed))
+        return X, (xd if p > 0 else None)
+    return ref.lora_fwd(x2d, acat, s, p, seed)
+
+
+def _lora_bwd_dx(base, dxa, acat, p, seed):
+    if _ext.use_hip(base) and acat.shape[0] % 16 == 0 and acat.shape[0] <= 64:
+        return _ext.ops().lora_bwd_dx(base, dxa, acat, float(p), int(seed))
+    return ref.lora_bwd_dx(base, dxa, acat, p, seed)
+
+
+class LoRAWideFn(Function):
+    """LoRA folded into the base GEMM (models.lora.FusedLoRA.wide).
+
+    The frozen base weight W [n, K] lives in the left columns of W' = [W | B_blockdiag] [n, K+R]
+    (R = r x active sub-projections); the activation is widened the same way, X' = [x | s * xa] with
+    xa = dropout(x) A_cat^T (csrc/lora.hip lora_fwd: one pass over x). Then
+        forward:  y = X' W'^T                      (one GEMM, K+R deep: no rank-r pass over y)
+        backward: dX' = dy W'  (or dy W and dy B_blockdiag separately when n is large: the N = K+R
+                               dgrad tiles badly, profiles/r1_lora_microbench.md)
+                  dB = dy^T X'[:, K:]              (block-diagonal slices)
+                  dA = (s dX'[:, K:])^T dropout(x)
+                  dx = dX'[:, :K] + dropout((s dX'[:, K:]) A_cat)   (csrc/lora.hip lora_bwd_dx: one pass)"""
+
+    SPLIT_DGRAD_MIN_N = 8192
+
+    @staticmethod
+    def forward(ctx, x, wide, K, scaling, p, seed, meta, *ab):
+        n = len(ab) // 2
+        As, Bs = ab[:n], ab[n:]
+        r = As[0].shape[0]
+        R = r * n
+        x2d = x.reshape(-1, K)
+        if not x2d.is_contiguous():
+            x2d = x2d.contiguous()
+        with torch.no_grad():
+            for (o, rows, c), B in zip(meta, Bs):
+                wide[o:o + rows, K + c:K + c + r].copy_(B)
+        acat = As[0].contiguous() if n == 1 else torch.cat(As, 0)
+        X, xd = _lora_fwd(x2d, acat, scaling, p, seed)
+        y = torch.mm(X, wide.t())
+        ctx.save_for_backward(X, acat, xd if xd is not None else X.new_empty(0))
+        ctx.wide = wide
+        ctx.meta = (K, R, r, n, float(scaling), float(p), int(seed), tuple(meta), x.shape)
+        if x.dim() == 2:
+            return y
+        return y.view(*x.shape[:-1], wide.shape[0])
+
+    @staticmethod
+    def backward(ctx, dy):
+        X, acat, xd = ctx.saved_tensors
+        K, R, r, n, scaling, p, seed, meta, xshape = ctx.meta
+        wide = ctx.wide
+        dy2d = dy.reshape(-1, dy.shape[-1])
+        if not dy2d.is_contiguous():
+            dy2d = dy2d.contiguous()
+        if wide.shape[0] >= LoRAWideFn.SPLIT_DGRAD_MIN_N:
+            base = torch.mm(dy2d, wide[:, :K])
+            dxa = torch.mm(dy2d, wide[:, K:]).mul_(scaling)
+        else:
+            dX = torch.mm(dy2d, wide)                   # [T, K+R]
+            base = dX[:, :K]
+            dxa = dX[:, K:].mul(scaling)                # contiguous [T, R]
+        dBf = torch.mm(dy2d.t(), X[:, K:])              # [n_out, R]
+        dBs = [dBf[o:o + rows, c:c + r].contiguous() for (o, rows, c) in meta]
+        dAf = torch.mm(dxa.t(), xd if p > 0 else X[:, :K])  # [R, K]
+        dAs = [dAf[i * r:(i + 1) * r] for i in range(n)]
+        dx = None
+        if ctx.needs_input_grad[0]:
+            dx = _lora_bwd_dx(base, dxa, acat, p, seed).view(xshape)
+        return (dx, None, None, None, None, None, None, *dAs, *dBs)
+
+
 def lora_linear(x, weight, lora) -> torch.Tensor:
     """``lora``: a models.lora.FusedLoRA module (adapters per sub-projection)."""
     p = lora.dropout.p if isinstance(lora.dropout, torch.nn.Dropout) and lora.training else 0.0
+    wide = getattr(lora, "wide", None)
+    if wide is not None and weight.data_ptr() == wide.data_ptr() and weight.shape[1] == lora.in_features:
+        As = [a for a, act in zip(lora.A, lora.active) if act]
+        Bs = [b for b, act in zip(lora.B, lora.active) if act]
+        if As:
+            seed = int(torch.randint(1, 2 ** 31 - 1, (1,)).item()) if p > 0 else 0
+            return LoRAWideFn.apply(x, wide, lora.in_features, float(lora.scaling), float(p), seed,
+                                    tuple(lora.wide_meta), *As, *Bs)
     return LoRALinearFn.apply(x, weight, float(lora.scaling), float(p), tuple(lora.out_splits), *lora.A, *lora.B)
 
 

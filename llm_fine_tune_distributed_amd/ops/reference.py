@@ -132,3 +132,45 @@ def adamw_(param: torch.Tensor, grad: torch.Tensor, exp_avg: torch.Tensor, exp_a
         param.copy_((bits & ~0xFFFF).view(torch.float32))
     else:
         param.copy_(w)
+
+
+_M32 = 0xFFFFFFFF
+
+
+def hash_u32(idx: torch.Tensor, seed: int) -> torch.Tensor:
+    """Bit-exact torch twin of csrc/common.h hash_u32 (int64 tensors holding uint32 values)."""
+    lo, hi = idx & _M32, (idx >> 32) & _M32
+    x = ((lo * 0x9E3779B9) & _M32) ^ ((hi * 0x85EBCA6B) & _M32) ^ ((int(seed) * 0xC2B2AE35) & _M32)
+    x = x ^ (x >> 16)
+    x = (x * 0x7FEB352D) & _M32
+    x = x ^ (x >> 15)
+    x = (x * 0x846CA68B) & _M32
+    return x ^ (x >> 16)
+
+
+def dropout_add(a: Optional[torch.Tensor], b: torch.Tensor, p: float, seed: int) -> torch.Tensor:
+    """(a or 0) + b * keep / (1-p), keep = hash(t*K + k, seed) >= p * 2^32 (same mask as the HIP kernel)."""
+    T, K = b.shape
+    p = min(max(float(p), 0.0), 0.999)
+    idx = torch.arange(T * K, device=b.device, dtype=torch.int64).view(T, K)
+    keep = hash_u32(idx, seed) >= int(p * 4294967296.0)
+    out = torch.where(keep, b.float() * (1.0 / (1.0 - p)), torch.zeros((), device=b.device))
+    if a is not None:
+        out = out + a.float()
+    return out.to(b.dtype)
+
+
+def lora_fwd(x: torch.Tensor, A: torch.Tensor, s: float, p: float, seed: int):
+    """(X' = [x | s * dropout(x) A^T], xd = dropout(x) or None) — twin of csrc/lora.hip lora_fwd."""
+    xd = dropout_add(None, x, p, seed) if p > 0 else None
+    xa = (xd if xd is not None else x).float() @ A.float().t()
+    X = torch.cat([x, (xa * s).to(x.dtype)], dim=1)
+    return X, xd
+
+
+def lora_bwd_dx(base: torch.Tensor, dxa: torch.Tensor, A: torch.Tensor, p: float, seed: int) -> torch.Tensor:
+    """dx = base + dropout(dxa @ A) (same mask as the forward) — twin of csrc/lora.hip lora_bwd_dx."""
+    dxd = (dxa.float() @ A.float()).to(base.dtype)
+    if p > 0:
+        return dropout_add(base, dxd, p, seed)
+    return (base.float() + dxd.float()).to(base.dtype)

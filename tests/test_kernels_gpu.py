@@ -247,3 +247,35 @@ def test_wgrad_gemm(cfg, T, N, K, accumulate):
     want = dy.float().t() @ x.float() + (base if accumulate else 0)
     err = (out.float() - want).abs().max().item()
     assert err <= 0.02 * want.abs().max().item(), err
+
+
+def test_dropout_add_matches_reference_mask():
+    torch.manual_seed(0)
+    wide = torch.randn(300, 528, device="cuda", dtype=torch.bfloat16)
+    a, b = wide[:, 16:272], wide[:, 272:528]  # strided column slices (row stride 528)
+    for p, seed in ((0.05, 11), (0.5, 12345)):
+        got = _ext.ops().dropout_add(a, b, p, seed)
+        want = ref.dropout_add(a.cpu(), b.cpu(), p, seed)
+        assert (got.float().cpu() - want.float()).abs().max().item() < 0.02
+        got0 = _ext.ops().dropout_add(None, b, p, seed)
+        assert torch.equal(got0 != 0, ref.dropout_add(None, b.cpu(), p, seed).cuda() != 0)
+
+
+@pytest.mark.parametrize("K,R,p", [(2048, 48, 0.05), (2048, 16, 0.0), (1024, 32, 0.3), (11008, 16, 0.05)])
+def test_lora_fwd_bwd_kernels(K, R, p):
+    torch.manual_seed(0)
+    T = 200
+    x = torch.randn(T, K, device="cuda", dtype=torch.bfloat16)
+    A = (torch.randn(R, K, device="cuda") * 0.05).to(torch.bfloat16)
+    X, xd = _ext.ops().lora_fwd(x, A, 0.5, p, 99)
+    Xr, xdr = ref.lora_fwd(x, A, 0.5, p, 99)
+    assert torch.equal(X[:, :K], x)
+    assert (X[:, K:].float() - Xr[:, K:].float()).abs().max().item() < 2e-2 * (Xr[:, K:].float().abs().max().item() + 1)
+    if p > 0:
+        assert torch.equal(xd, xdr)
+    wideb = torch.randn(T, K + 64, device="cuda", dtype=torch.bfloat16)
+    base = wideb[:, :K]
+    dxa = (torch.randn(T, R, device="cuda") * 0.1).to(torch.bfloat16)
+    dx = _ext.ops().lora_bwd_dx(base, dxa, A, p, 99)
+    dxr = ref.lora_bwd_dx(base, dxa, A, p, 99)
+    assert (dx.float() - dxr.float()).abs().max().item() < 3e-2

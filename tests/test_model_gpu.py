@@ -38,3 +38,50 @@ def test_model_hip_vs_reference(mt):
     for n in g_ref:
         e = (g_hip[n] - g_ref[n]).norm() / (g_ref[n].norm() + 1e-12)
         assert e < 5e-2, (n, e.item())
+
+
+def test_lora_wide_gpu_matches_unfused():
+    from llm_fine_tune_distributed_amd.models.lora import LoRAConfig, apply_lora
+    import llm_fine_tune_distributed_amd.models.transformer as T
+    import llm_fine_tune_distributed_amd.ops as ops
+    torch.manual_seed(0)
+    cfg = tiny(hidden_size=512, num_attention_heads=4, num_key_value_heads=2, head_dim=128, intermediate_size=1024,
+               vocab_size=1024, num_hidden_layers=2)
+    m = build_model(cfg, device="cuda", dtype=torch.bfloat16, seed=1)
+    apply_lora(m, LoRAConfig(r=16, lora_alpha=8, lora_dropout=0.1))
+    for l in m.model.layers:
+        for fl in (l.self_attn.lora["qkv"], l.self_attn.lora["o"], l.mlp.lora["gate_up"], l.mlp.lora["down"]):
+            for bb in fl.B:
+                torch.nn.init.normal_(bb, std=0.05)
+    m.train()
+    ids = torch.randint(0, 1024, (4, 128), device="cuda")
+
+    def unfused(x, w, lora):
+        p = lora.dropout.p if lora.training else 0.0
+        seed = int(torch.randint(1, 2 ** 31 - 1, (1,)).item()) if p > 0 else 0
+        x2d = x.reshape(-1, x.shape[-1])
+        keep = ops.dropout_add(None, torch.ones_like(x2d), p, seed) != 0
+        xd = x2d * keep / (1 - p)
+        outs = [(xd.float() @ a.float().t() @ b.float().t()) for a, b in zip(lora.A, lora.B)]
+        y = x2d.float() @ w.float().t() + torch.cat(outs, -1) * lora.scaling
+        return y.to(x.dtype).view(*x.shape[:-1], -1)
+
+    torch.manual_seed(7)
+    out = m(ids, labels=ids)
+    out.loss.backward()
+    g1 = {n: p.grad.float().clone() for n, p in m.named_parameters() if p.grad is not None}
+    orig = T.ops.lora_linear
+    T.ops.lora_linear = unfused
+    try:
+        for p in m.parameters():
+            p.grad = None
+        torch.manual_seed(7)
+        out2 = m(ids, labels=ids)
+        out2.loss.backward()
+    finally:
+        T.ops.lora_linear = orig
+    assert abs(out.loss.item() - out2.loss.item()) < 2e-2
+    for n, p in m.named_parameters():
+        if p.grad is not None:
+            rel = (g1[n] - p.grad.float()).norm() / (p.grad.float().norm() + 1e-6)
+            assert rel < 5e-2, (n, rel.item())
