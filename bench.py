@@ -43,6 +43,8 @@ def main():
     ap.add_argument("--packing", action="store_true")
     ap.add_argument("--freeze-policy", default="full", choices=["full", "last_n_layers", "lora"])
     ap.add_argument("--master-weights", action="store_true", help="fp32 master copy (default: bf16 params + SR)")
+    ap.add_argument("--optim-state", default=os.environ.get("SFTAMD_OPTIM_STATE", "fp32"), choices=["fp32", "bf16"],
+                    help="Adam moment dtype (bf16 = torch AdamW's state dtype for the reference's bf16 params)")
     ap.add_argument("--tunableop", default=os.environ.get("SFTAMD_TUNABLEOP", "auto"),
                     help="auto: load the committed GEMM selections; tune: tune missing shapes into it; off")
     ap.add_argument("--profile-steps", type=int, default=0)
@@ -71,7 +73,7 @@ def main():
                      bf16=True, gradient_checkpointing=False, max_length=a.seq, packing=a.packing,
                      ddp_bucket_cap_mb=a.bucket_mb, dataloader_drop_last=True, jsonl_log=False, logging_steps=0,
                      optimizer_overlap=not a.no_overlap, freeze_policy=a.freeze_policy,
-                     master_weights=a.master_weights)
+                     master_weights=a.master_weights, optim_state_dtype=a.optim_state)
     trainer = SFTTrainer(model=model, args=args, train_dataset=ds)
     loader = trainer.get_train_dataloader()
     it = iter(loader)
@@ -116,7 +118,7 @@ def main():
                        "freeze_policy": a.freeze_policy, "global_batch": a.micro_batch * a.ga * st.world_size,
                        "per_device_batch": a.micro_batch, "gradient_accumulation_steps": a.ga, "seq_len": a.seq,
                        "parallelism": f"dp{st.world_size}", "optimizer": ("AdamW fp32-master (fused HIP)" if a.master_weights else
-                                     "AdamW bf16 params + stochastic rounding, fp32 moments (fused HIP)"),
+                                     f"AdamW bf16 params + stochastic rounding, {a.optim_state} moments (fused HIP)"),
                        "samples_per_device_per_step": a.micro_batch * a.ga,
                        "gradient_checkpointing": False, "packing": a.packing},
             "tokens_per_sec": round(tok_s, 1), "mfu": None if mfu is None else round(mfu, 4), "final_loss": round(loss, 4),

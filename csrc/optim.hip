@@ -37,10 +37,12 @@ at::Tensor sumsq(const at::Tensor& x) {
   return part;
 }
 
+// omb1 = 1 - beta1, omb2 = 1 - beta2 computed in double on the host (torch AdamW's constants:
+// 1.f - 0.999f would be 1.0000467e-3, not fp32(1e-3)).
 __device__ __forceinline__ void adam_elem(float& w, float g, float& m, float& v, float lr, float b1, float b2, float eps,
-                                          float wd, float rbc1, float rsbc2) {
-  m = b1 * m + (1.f - b1) * g;
-  v = b2 * v + (1.f - b2) * g * g;
+                                          float wd, float rbc1, float rsbc2, float omb1, float omb2) {
+  m = b1 * m + omb1 * g;
+  v = b2 * v + omb2 * g * g;
   const float denom = sqrtf(v) * rsbc2 + eps;
   w = w * (1.f - lr * wd) - lr * rbc1 * m / denom;
 }
@@ -57,12 +59,56 @@ __device__ __forceinline__ u16 f2bf_sr(float f, unsigned r) {
   return (u16)(u >> 16);
 }
 
-template <bool MASTER, bool SR>
+__device__ __forceinline__ uint4 pack8_sr(const float* f, unsigned long long idx, unsigned seed) {
+  u16 b[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) b[i] = f2bf_sr(f[i], sr_hash(idx + i, seed));
+  return make_uint4(b[0] | (b[1] << 16), b[2] | (b[3] << 16), b[4] | (b[5] << 16), b[6] | (b[7] << 16));
+}
+
+// Moment storage: fp32 (default) or bf16 (BF16M: the reference's own state dtype — torch AdamW keeps
+// exp_avg/exp_avg_sq in the bf16 parameter dtype — 14 instead of 22 HBM bytes per parameter). bf16
+// moments are written with stochastic rounding on streams independent of the parameter's when SR is
+// on, round-to-nearest otherwise.
+template <bool BF16M>
+struct Moments {
+  static __device__ __forceinline__ void load(const void* base, long o, float* f) {
+    if constexpr (BF16M) {
+      unpack8(*(const uint4*)((const u16*)base + o), f);
+    } else {
+      *(float4*)&f[0] = *(const float4*)((const float*)base + o);
+      *(float4*)&f[4] = *(const float4*)((const float*)base + o + 4);
+    }
+  }
+  static __device__ __forceinline__ void store(void* base, long o, const float* f, bool sr, unsigned long long idx,
+                                               unsigned seed) {
+    if constexpr (BF16M) {
+      *(uint4*)((u16*)base + o) = sr ? pack8_sr(f, idx, seed) : pack8(f);
+    } else {
+      *(float4*)((float*)base + o) = *(const float4*)&f[0];
+      *(float4*)((float*)base + o + 4) = *(const float4*)&f[4];
+    }
+  }
+  static __device__ __forceinline__ float load1(const void* base, long i) {
+    if constexpr (BF16M) return bf2f(((const u16*)base)[i]);
+    else return ((const float*)base)[i];
+  }
+  static __device__ __forceinline__ void store1(void* base, long i, float f, bool sr, unsigned long long idx,
+                                                unsigned seed) {
+    if constexpr (BF16M) ((u16*)base)[i] = sr ? f2bf_sr(f, sr_hash(idx, seed)) : f2bf(f);
+    else ((float*)base)[i] = f;
+  }
+};
+
+constexpr unsigned SEED_M = 0x68E31DA4u, SEED_V = 0xB5297A4Du;
+
+template <bool MASTER, bool SR, bool BF16M>
 __global__ __launch_bounds__(256) void adamw_kernel(u16* __restrict__ p, const u16* __restrict__ g,
-                                                    float* __restrict__ master, float* __restrict__ mom,
-                                                    float* __restrict__ var, const float* __restrict__ coef, long n,
+                                                    float* __restrict__ master, void* __restrict__ mom,
+                                                    void* __restrict__ var, const float* __restrict__ coef, long n,
                                                     float lr, float b1, float b2, float eps, float wd, float rbc1,
-                                                    float rsbc2, unsigned seed, long idx0) {
+                                                    float rsbc2, float omb1, float omb2, unsigned seed, long idx0) {
+  using Mo = Moments<BF16M>;
   const float c = coef[0];
   const long nv = n / 8;
   for (long v = blockIdx.x * 256L + threadIdx.x; v < nv; v += (long)gridDim.x * 256) {
@@ -75,36 +121,25 @@ __global__ __launch_bounds__(256) void adamw_kernel(u16* __restrict__ p, const u
     } else {
       unpack8(*(const uint4*)(p + o), w);
     }
-    *(float4*)&mm[0] = *(const float4*)(mom + o);
-    *(float4*)&mm[4] = *(const float4*)(mom + o + 4);
-    *(float4*)&vv[0] = *(const float4*)(var + o);
-    *(float4*)&vv[4] = *(const float4*)(var + o + 4);
+    Mo::load(mom, o, mm);
+    Mo::load(var, o, vv);
 #pragma unroll
-    for (int i = 0; i < 8; ++i) adam_elem(w[i], gf[i] * c, mm[i], vv[i], lr, b1, b2, eps, wd, rbc1, rsbc2);
+    for (int i = 0; i < 8; ++i) adam_elem(w[i], gf[i] * c, mm[i], vv[i], lr, b1, b2, eps, wd, rbc1, rsbc2, omb1, omb2);
     if (MASTER) {
       *(float4*)(master + o) = *(float4*)&w[0];
       *(float4*)(master + o + 4) = *(float4*)&w[4];
     }
-    *(float4*)(mom + o) = *(float4*)&mm[0];
-    *(float4*)(mom + o + 4) = *(float4*)&mm[4];
-    *(float4*)(var + o) = *(float4*)&vv[0];
-    *(float4*)(var + o + 4) = *(float4*)&vv[4];
-    if (SR) {
-      u16 b[8];
-#pragma unroll
-      for (int i = 0; i < 8; ++i) b[i] = f2bf_sr(w[i], sr_hash(idx0 + o + i, seed));
-      *(uint4*)(p + o) = make_uint4(b[0] | (b[1] << 16), b[2] | (b[3] << 16), b[4] | (b[5] << 16), b[6] | (b[7] << 16));
-    } else {
-      *(uint4*)(p + o) = pack8(w);
-    }
+    Mo::store(mom, o, mm, SR, idx0 + o, seed ^ SEED_M);
+    Mo::store(var, o, vv, SR, idx0 + o, seed ^ SEED_V);
+    *(uint4*)(p + o) = SR ? pack8_sr(w, idx0 + o, seed) : pack8(w);
   }
   for (long i = nv * 8 + blockIdx.x * 256L + threadIdx.x; i < n; i += (long)gridDim.x * 256) {
     float w = MASTER ? master[i] : bf2f(p[i]);
-    float m = mom[i], vr = var[i];
-    adam_elem(w, bf2f(g[i]) * c, m, vr, lr, b1, b2, eps, wd, rbc1, rsbc2);
+    float m = Mo::load1(mom, i), vr = Mo::load1(var, i);
+    adam_elem(w, bf2f(g[i]) * c, m, vr, lr, b1, b2, eps, wd, rbc1, rsbc2, omb1, omb2);
     if (MASTER) master[i] = w;
-    mom[i] = m;
-    var[i] = vr;
+    Mo::store1(mom, i, m, SR, idx0 + i, seed ^ SEED_M);
+    Mo::store1(var, i, vr, SR, idx0 + i, seed ^ SEED_V);
     p[i] = SR ? f2bf_sr(w, sr_hash(idx0 + i, seed)) : f2bf(w);
   }
 }
@@ -116,7 +151,10 @@ void adamw_flat(at::Tensor param, const at::Tensor& grad, const c10::optional<at
   SFT_CHECK_BF16(grad);
   SFT_CHECK(param.is_contiguous() && grad.is_contiguous() && exp_avg.is_contiguous() && exp_avg_sq.is_contiguous(),
             "contiguous");
-  SFT_CHECK(exp_avg.scalar_type() == at::kFloat && exp_avg_sq.scalar_type() == at::kFloat, "fp32 moments");
+  SFT_CHECK(exp_avg.scalar_type() == exp_avg_sq.scalar_type() &&
+                (exp_avg.scalar_type() == at::kFloat || exp_avg.scalar_type() == at::kBFloat16),
+            "moments must both be fp32 or both bf16");
+  const bool bf16m = exp_avg.scalar_type() == at::kBFloat16;
   const long n = param.numel();
   SFT_CHECK(grad.numel() == n && exp_avg.numel() == n && exp_avg_sq.numel() == n, "sizes");
   if (n == 0) return;
@@ -127,16 +165,21 @@ void adamw_flat(at::Tensor param, const at::Tensor& grad, const c10::optional<at
     SFT_CHECK(master->scalar_type() == at::kFloat && master->numel() == n && master->is_contiguous(), "master");
   float* mp = has_master ? master->data_ptr<float>() : nullptr;
   const unsigned seed = (unsigned)sr_seed;
-  auto go = [&](auto ms, auto sr) {
-    constexpr bool M = decltype(ms)::value, S = decltype(sr)::value;
-    adamw_kernel<M, S><<<grid, 256, 0, cur_stream()>>>(
-        (u16*)param.data_ptr(), (const u16*)grad.data_ptr(), mp, exp_avg.data_ptr<float>(),
-        exp_avg_sq.data_ptr<float>(), clip_coef.data_ptr<float>(), n, (float)lr, (float)beta1, (float)beta2,
-        (float)eps, (float)weight_decay, rbc1, rsbc2, seed, (long)sr_offset);
+  SFT_CHECK(clip_coef.scalar_type() == at::kFloat && clip_coef.numel() >= 1 && clip_coef.is_cuda(), "clip_coef");
+  auto go = [&](auto ms, auto sr, auto bm) {
+    constexpr bool M = decltype(ms)::value, S = decltype(sr)::value, B = decltype(bm)::value;
+    adamw_kernel<M, S, B><<<grid, 256, 0, cur_stream()>>>(
+        (u16*)param.data_ptr(), (const u16*)grad.data_ptr(), mp, exp_avg.data_ptr(), exp_avg_sq.data_ptr(),
+        clip_coef.data_ptr<float>(), n, (float)lr, (float)beta1, (float)beta2, (float)eps, (float)weight_decay, rbc1,
+        rsbc2, (float)(1.0 - beta1), (float)(1.0 - beta2), seed, (long)sr_offset);
   };
-  if (has_master) go(std::true_type(), std::false_type());
-  else if (sr_seed != 0) go(std::false_type(), std::true_type());
-  else go(std::false_type(), std::false_type());
+  auto go2 = [&](auto ms, auto sr) {
+    if (bf16m) go(ms, sr, std::true_type());
+    else go(ms, sr, std::false_type());
+  };
+  if (has_master) go2(std::true_type(), std::false_type());
+  else if (sr_seed != 0) go2(std::false_type(), std::true_type());
+  else go2(std::false_type(), std::false_type());
   SFT_LAUNCH_CHECK();
 }
 

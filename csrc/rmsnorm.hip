@@ -161,6 +161,122 @@ __global__ __launch_bounds__(bwd_threads<NV>()) void rmsnorm_bwd_kernel(const u1
   for (int c = threadIdx.x; c < H; c += NT) dw_part[(long)blockIdx.x * H + c] = red[c];
 }
 
+// Backward v2 (default): 4-wave blocks, ONE row per wave per iteration with every load of the row
+// (h, dy, dres, rstd) issued together — v1 issues dres only after the dot-product reduction, so
+// each of its iterations pays two serialised HBM latencies. ~120 VGPRs -> 4 waves/SIMD, 16 rows
+// (192 KB) in flight per CU. The weight stays packed bf16 in registers; dW accumulates in fp32
+// registers across the wave's rows and the 4 waves' partials are summed in LDS in a FIXED order
+// (v1's LDS float atomics made dW run-to-run nondeterministic).
+template <int NV>
+__global__ __launch_bounds__(256) void rmsnorm_bwd2_kernel(const u16* __restrict__ dy, const u16* __restrict__ h,
+                                                           const u16* __restrict__ w, const float* __restrict__ rstd,
+                                                           const u16* __restrict__ dres, u16* __restrict__ dx,
+                                                           float* __restrict__ dw_part, int M, int H) {
+  __shared__ __attribute__((aligned(16))) float red[4][NV * 512];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int nwaves = gridDim.x * 4;
+  float dw[NV][8];
+  uint4 wp[NV];
+#pragma unroll
+  for (int j = 0; j < NV; ++j) {
+    const int c = (lane + 64 * j) * 8;
+    wp[j] = c < H ? *(const uint4*)(w + c) : make_uint4(0, 0, 0, 0);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) dw[j][i] = 0.f;
+  }
+  const float invH = 1.f / (float)H;
+  for (int row = blockIdx.x * 4 + wave; row < M; row += nwaves) {
+    const long base = (long)row * H;
+    uint4 hv[NV], gv[NV], dv[NV];
+#pragma unroll
+    for (int j = 0; j < NV; ++j) {
+      const int c = (lane + 64 * j) * 8;
+      const bool ok = c < H;
+      hv[j] = ok ? *(const uint4*)(h + base + c) : make_uint4(0, 0, 0, 0);
+      gv[j] = ok ? *(const uint4*)(dy + base + c) : make_uint4(0, 0, 0, 0);
+      dv[j] = (ok && dres) ? *(const uint4*)(dres + base + c) : make_uint4(0, 0, 0, 0);
+    }
+    const float r = rstd[row];
+    float dot = 0.f;
+#pragma unroll
+    for (int j = 0; j < NV; ++j) {
+      float n[8], g[8], wf[8];
+      unpack8(hv[j], n);
+      unpack8(gv[j], g);
+      unpack8(wp[j], wf);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const float nn = n[i] * r;
+        dw[j][i] = fmaf(g[i], nn, dw[j][i]);
+        dot = fmaf(g[i] * wf[i], nn, dot);
+      }
+    }
+    dot = wave_sum(dot) * invH;
+    const float rr = r * dot;
+#pragma unroll
+    for (int j = 0; j < NV; ++j) {
+      const int c = (lane + 64 * j) * 8;
+      if (c < H) {
+        float n[8], g[8], wf[8], d[8], o[8];
+        unpack8(hv[j], n);
+        unpack8(gv[j], g);
+        unpack8(wp[j], wf);
+        unpack8(dv[j], d);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) o[i] = fmaf(r, fmaf(g[i], wf[i], -n[i] * rr), d[i]);
+        *(uint4*)(dx + base + c) = pack8(o);
+      }
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < NV; ++j) {
+    const int c = (lane + 64 * j) * 8;
+    if (c < H) {
+      *(float4*)&red[wave][c] = make_float4(dw[j][0], dw[j][1], dw[j][2], dw[j][3]);
+      *(float4*)&red[wave][c + 4] = make_float4(dw[j][4], dw[j][5], dw[j][6], dw[j][7]);
+    }
+  }
+  __syncthreads();
+  for (int c = threadIdx.x; c < H; c += 256)
+    dw_part[(long)blockIdx.x * H + c] = (red[0][c] + red[1][c]) + (red[2][c] + red[3][c]);
+}
+
+// out[c] = sum_p part[p][c], fixed order (deterministic). Block = 64 columns (16 float4 lanes) x
+// 64 row groups; each thread sums its rows with two independent accumulators, then a fixed
+// LDS tree over the row groups. All P rows of a 64-column slab are in flight at once.
+__global__ __launch_bounds__(1024) void col_sum2_kernel(const float* __restrict__ part, float* __restrict__ out, int P,
+                                                        int H) {
+  __shared__ float4 red[64][16];
+  const int c4 = threadIdx.x & 15, rg = threadIdx.x >> 4;
+  const int c = blockIdx.x * 64 + c4 * 4;
+  float4 a = make_float4(0.f, 0.f, 0.f, 0.f), b = a;
+  if (c < H) {
+    int p = rg;
+    for (; p + 64 < P; p += 128) {
+      const float4 x = *(const float4*)(part + (long)p * H + c);
+      const float4 y = *(const float4*)(part + (long)(p + 64) * H + c);
+      a.x += x.x; a.y += x.y; a.z += x.z; a.w += x.w;
+      b.x += y.x; b.y += y.y; b.z += y.z; b.w += y.w;
+    }
+    if (p < P) {
+      const float4 x = *(const float4*)(part + (long)p * H + c);
+      a.x += x.x; a.y += x.y; a.z += x.z; a.w += x.w;
+    }
+  }
+  red[rg][c4] = make_float4(a.x + b.x, a.y + b.y, a.z + b.z, a.w + b.w);
+  __syncthreads();
+#pragma unroll
+  for (int s = 32; s > 0; s >>= 1) {
+    if (rg < s) {
+      const float4 u = red[rg + s][c4];
+      float4& v = red[rg][c4];
+      v.x += u.x; v.y += u.y; v.z += u.z; v.w += u.w;
+    }
+    __syncthreads();
+  }
+  if (rg == 0 && c < H) *(float4*)(out + c) = red[0][c4];
+}
+
 // out[c] = sum_b part[b][c] in a fixed order (deterministic). Block = 64 columns x 4 row
 // groups; each thread keeps 4 independent accumulators so the loads pipeline.
 __global__ __launch_bounds__(256) void col_sum_kernel(const float* __restrict__ part, float* __restrict__ out, int P,
@@ -239,10 +355,28 @@ std::tuple<at::Tensor, at::Tensor> rmsnorm_bwd(const at::Tensor& dy, const at::T
     SFT_CHECK(dres->is_contiguous() && dres->scalar_type() == at::kBFloat16, "dres");
     dr = (const u16*)dres->data_ptr();
   }
+  SFT_CHECK(rstd.numel() == M && weight.numel() == H && dy.numel() == h.numel(), "rmsnorm_bwd: shape mismatch");
+  auto dw = at::empty({H}, h.options().dtype(at::kFloat));
+  static const bool v1 = [] {
+    const char* e = std::getenv("SFTAMD_RMSNORM_BWD");
+    return e && e[0] == '1';
+  }();
+  if (M == 0) return {dx, dw.zero_()};
+  if (!v1) {
+    // 4 rows per wave at M = 8192 (512 blocks = 2 per CU): partials stay small (4 MB fp32)
+    const int nblk = std::max(1, std::min((M + 15) / 16, 512));
+    auto part = at::empty({nblk, H}, h.options().dtype(at::kFloat));
+    NV_DISPATCH(H, rmsnorm_bwd2_kernel<NV><<<nblk, 256, 0, cur_stream()>>>(
+                       (const u16*)dy.data_ptr(), (const u16*)h.data_ptr(), (const u16*)weight.data_ptr(),
+                       rstd.data_ptr<float>(), dr, (u16*)dx.data_ptr(), part.data_ptr<float>(), M, H));
+    SFT_LAUNCH_CHECK();
+    col_sum2_kernel<<<(H + 63) / 64, 1024, 0, cur_stream()>>>(part.data_ptr<float>(), dw.data_ptr<float>(), nblk, H);
+    SFT_LAUNCH_CHECK();
+    return {dx, dw};
+  }
   int nblk = std::min((M + 15) / 16, 256);  // one 8-wave block per CU, >= 2 rows per wave
   nblk = std::max(nblk, 1);
   auto part = at::empty({nblk, H}, h.options().dtype(at::kFloat));
-  auto dw = at::empty({H}, h.options().dtype(at::kFloat));
   NV_DISPATCH(H, rmsnorm_bwd_kernel<NV><<<nblk, bwd_threads<NV>(), 0, cur_stream()>>>(
                      (const u16*)dy.data_ptr(), (const u16*)h.data_ptr(), (const u16*)weight.data_ptr(),
                      rstd.data_ptr<float>(), dr, (u16*)dx.data_ptr(), part.data_ptr<float>(), M, H));

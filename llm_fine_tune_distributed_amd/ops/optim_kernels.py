@@ -38,7 +38,8 @@ def adamw_flat_(param: torch.Tensor, grad: torch.Tensor, master: Optional[torch.
                 lr: float, beta1: float, beta2: float, eps: float, weight_decay: float, step: int,
                 sr_seed: int = 0, sr_offset: int = 0) -> None:
     """In-place AdamW on flat buffers. grad is multiplied by clip_coef (device scalar).
-    Without a master copy, ``sr_seed != 0`` writes the bf16 parameters with stochastic rounding."""
+    Moments are fp32 or bf16 (both the same). Without a master copy, ``sr_seed != 0`` writes the
+    bf16 parameters (and bf16 moments) with stochastic rounding."""
     if param.numel() == 0:
         return
     bc1 = 1.0 - beta1 ** step
@@ -50,4 +51,4 @@ def adamw_flat_(param: torch.Tensor, grad: torch.Tensor, master: Optional[torch.
         return
     g = grad.float() * clip_coef.float()
     ref.adamw_(param, g, exp_avg, exp_avg_sq, master, lr, beta1, beta2, eps, weight_decay, step,
-               sr_seed=sr_seed)
+               sr_seed=sr_seed, sr_offset=sr_offset)

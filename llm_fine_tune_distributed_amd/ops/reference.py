@@ -112,29 +112,38 @@ def cross_entropy(logits: torch.Tensor, labels: torch.Tensor):
 
 def adamw_(param: torch.Tensor, grad: torch.Tensor, exp_avg: torch.Tensor, exp_avg_sq: torch.Tensor,
            master: Optional[torch.Tensor], lr: float, beta1: float, beta2: float, eps: float,
-           weight_decay: float, step: int, grad_scale: float = 1.0, sr_seed: int = 0) -> None:
-    """Decoupled-weight-decay Adam (torch.optim.AdamW semantics) on flat tensors, in place."""
+           weight_decay: float, step: int, grad_scale: float = 1.0, sr_seed: int = 0, sr_offset: int = 0) -> None:
+    """Decoupled-weight-decay Adam (torch.optim.AdamW semantics) on flat tensors, in place.
+
+    Math in fp32 whatever the storage dtypes (twin of csrc/optim.hip adamw_kernel). bf16 storage
+    (parameters without a master copy, and bf16 moments) is written with stochastic rounding when
+    ``sr_seed`` is set — the same hash streams as the kernel, so CPU and GPU agree bit for bit on
+    the rounding — and round-to-nearest otherwise."""
     w = master if master is not None else param.float()
     g = grad.float() * grad_scale
-    exp_avg.mul_(beta1).add_(g.to(exp_avg.dtype), alpha=1 - beta1)
-    exp_avg_sq.mul_(beta2).addcmul_(g.to(exp_avg_sq.dtype), g.to(exp_avg_sq.dtype), value=1 - beta2)
+    m = exp_avg.float().mul_(beta1).add_(g, alpha=1 - beta1)
+    v = exp_avg_sq.float().mul_(beta2).addcmul_(g, g, value=1 - beta2)
     bc1 = 1 - beta1 ** step
     bc2 = 1 - beta2 ** step
-    denom = (exp_avg_sq.float() / bc2).sqrt().add_(eps)
+    denom = (v / bc2).sqrt().add_(eps)
     w.mul_(1 - lr * weight_decay)
-    w.addcdiv_(exp_avg.float(), denom, value=-lr / bc1)
+    w.addcdiv_(m, denom, value=-lr / bc1)
+    sr = bool(sr_seed) and master is None
+    for dst, src, s in ((exp_avg, m, _SEED_M), (exp_avg_sq, v, _SEED_V)):
+        if dst.dtype == torch.bfloat16 and sr:
+            dst.copy_(bf16_stochastic_round(src, (int(sr_seed) ^ s) & _M32, sr_offset))
+        else:
+            dst.copy_(src)
     if master is not None:
         param.copy_(master)
-    elif sr_seed and param.dtype == torch.bfloat16:
-        gen = torch.Generator(device=w.device).manual_seed(int(sr_seed))
-        noise = torch.randint(0, 1 << 16, w.shape, generator=gen, device=w.device, dtype=torch.int32)
-        bits = w.contiguous().view(torch.int32) + noise
-        param.copy_((bits & ~0xFFFF).view(torch.float32))
+    elif sr and param.dtype == torch.bfloat16:
+        param.copy_(bf16_stochastic_round(w, int(sr_seed), sr_offset))
     else:
         param.copy_(w)
 
 
 _M32 = 0xFFFFFFFF
+_SEED_M, _SEED_V = 0x68E31DA4, 0xB5297A4D  # csrc/optim.hip SEED_M / SEED_V
 
 
 def hash_u32(idx: torch.Tensor, seed: int) -> torch.Tensor:
@@ -146,6 +155,20 @@ def hash_u32(idx: torch.Tensor, seed: int) -> torch.Tensor:
     x = x ^ (x >> 15)
     x = (x * 0x846CA68B) & _M32
     return x ^ (x >> 16)
+
+
+def bf16_stochastic_round(x: torch.Tensor, seed: int, offset: int = 0) -> torch.Tensor:
+    """fp32 -> bf16 with stochastic rounding: bits + (hash(offset + i, seed) & 0xffff), truncated.
+    Twin of csrc/optim.hip f2bf_sr over a flat tensor (E[result] = x)."""
+    xf = x.float().contiguous().reshape(-1)
+    idx = torch.arange(xf.numel(), dtype=torch.int64, device=xf.device) + int(offset)
+    bits = xf.view(torch.int32).to(torch.int64) & _M32
+    finite = (bits & 0x7F800000) != 0x7F800000
+    rounded = ((bits + (hash_u32(idx, seed) & 0xFFFF)) >> 16) << 16
+    out = torch.where(finite, rounded, bits)
+    out = torch.where(out >= 1 << 31, out - (1 << 32), out).to(torch.int32).view(torch.float32)
+    res = out.to(torch.bfloat16)  # exact: low 16 bits are zero (non-finite: round-to-nearest, as f2bf)
+    return torch.where(finite, res, xf.to(torch.bfloat16)).view(x.shape)
 
 
 def dropout_add(a: Optional[torch.Tensor], b: torch.Tensor, p: float, seed: int) -> torch.Tensor:

@@ -86,6 +86,9 @@ class SFTConfig:
     # bf16 write-back (unbiased); master_weights=True keeps an fp32 master copy instead.
     master_weights: bool = False
     stochastic_rounding: bool = True
+    # Adam moment storage: "fp32" (default) or "bf16" (torch AdamW's state dtype for the
+    # reference's bf16 params; stochastic-rounded, 14 instead of 22 HBM bytes/param per step)
+    optim_state_dtype: str = "fp32"
     ddp_first_bucket_mb: float = 4.0
     ddp_broadcast_params: bool = False      # weights are identical by construction (seeded / loaded)
     ddp_check_sync_every: int = 0           # cross-rank param checksum every N steps (0 = off)

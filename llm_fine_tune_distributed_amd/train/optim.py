@@ -20,7 +20,10 @@ from .. import ops
 
 class FlatAdamW:
     def __init__(self, engine, lr: float, betas=(0.9, 0.999), eps: float = 1e-8, weight_decay: float = 0.0,
-                 master_weights: bool = True, stochastic_rounding: bool = True):
+                 master_weights: bool = True, stochastic_rounding: bool = True, state_dtype=torch.float32):
+        """``state_dtype`` = dtype of exp_avg / exp_avg_sq: fp32 (default) or bf16 — what torch's
+        AdamW keeps for the reference's bf16 parameters (training.py:99) — stored with stochastic
+        rounding (unbiased) when ``stochastic_rounding`` is on; 8 fewer HBM bytes per parameter."""
         self.engine = engine
         self.lr = lr
         self.betas = betas
@@ -31,9 +34,15 @@ class FlatAdamW:
         self.step_count = 0
         n = engine.numel
         dev = engine.device
+        if isinstance(state_dtype, str):
+            state_dtype = {"fp32": torch.float32, "float32": torch.float32, "bf16": torch.bfloat16,
+                           "bfloat16": torch.bfloat16}[state_dtype]
+        if state_dtype not in (torch.float32, torch.bfloat16):
+            raise ValueError(f"optimizer state dtype must be fp32 or bf16, got {state_dtype}")
+        self.state_dtype = state_dtype
         self.master = engine.param_flat.float() if master_weights else None
-        self.exp_avg = torch.zeros(n, dtype=torch.float32, device=dev)
-        self.exp_avg_sq = torch.zeros(n, dtype=torch.float32, device=dev)
+        self.exp_avg = torch.zeros(n, dtype=state_dtype, device=dev)
+        self.exp_avg_sq = torch.zeros(n, dtype=state_dtype, device=dev)
         self.last_grad_norm: Optional[torch.Tensor] = None
         self.overlap = False
 
@@ -154,7 +163,7 @@ class FlatAdamW:
 
     def load_state_dict(self, sd: Dict):
         self.step_count = int(sd["step"])
-        self.exp_avg.copy_(sd["exp_avg"])
+        self.exp_avg.copy_(sd["exp_avg"])  # copy_ converts between fp32 / bf16 state checkpoints
         self.exp_avg_sq.copy_(sd["exp_avg_sq"])
         if self.master is not None:
             if sd.get("master") is not None:

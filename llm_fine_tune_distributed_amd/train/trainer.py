@@ -112,7 +112,8 @@ class SFTTrainer:
         self.optimizer = FlatAdamW(self.engine, lr=args.learning_rate, betas=(args.adam_beta1, args.adam_beta2),
                                    eps=args.adam_epsilon, weight_decay=args.weight_decay,
                                    master_weights=args.master_weights,
-                                   stochastic_rounding=args.stochastic_rounding)
+                                   stochastic_rounding=args.stochastic_rounding,
+                                   state_dtype=args.optim_state_dtype)
         if args.optimizer_overlap and dev.type == "cuda":
             self.optimizer.enable_overlap(model)
         self.scheduler: Optional[LRScheduler] = None

@@ -51,6 +51,26 @@ def test_rmsnorm(H, with_res):
     assert rel_err(dw, gw) < 1e-3
 
 
+def test_rmsnorm_bwd_training_shape_deterministic():
+    """M = 8192 tokens x H = 2048 (the bench micro-batch): many rows per wave, two-level dW reduce."""
+    torch.manual_seed(1)
+    M, H = 8192, 2048
+    h = torch.randn(M, H, device=DEV, dtype=torch.bfloat16)
+    w = (1 + 0.1 * torch.randn(H, device=DEV)).to(torch.bfloat16)
+    _, _, rstd = _ext.ops().rmsnorm_fwd(h, None, w, 1e-6)
+    dy = torch.randn_like(h)
+    dres = torch.randn_like(h)
+    dx, dw = _ext.ops().rmsnorm_bwd(dy, h, w, rstd, dres)
+    dx2, dw2 = _ext.ops().rmsnorm_bwd(dy, h, w, rstd, dres)
+    assert torch.equal(dx, dx2) and torch.equal(dw, dw2)  # fixed-order reductions
+    hf = h.float().requires_grad_(True)
+    wf = w.float().requires_grad_(True)
+    yf = hf * torch.rsqrt(hf.pow(2).mean(-1, keepdim=True) + 1e-6) * wf
+    gx, gw = torch.autograd.grad(yf, (hf, wf), dy.float())
+    assert rel_err(dx, gx + dres.float()) < 1e-2
+    assert rel_err(dw, gw) < 1e-3
+
+
 def test_swiglu():
     torch.manual_seed(0)
     gu = torch.randn(777, 2 * 1376, device=DEV, dtype=torch.bfloat16)
@@ -216,6 +236,36 @@ def test_adamw_stochastic_rounding_unbiased():
     m.zero_(), v.zero_()
     _ext.ops().adamw_flat(p2, g, None, m, v, coef, lr, 0.9, 0.999, 1e-12, 0.0, 1 - 0.9, 1 - 0.999, 0)
     assert (p2.float() == 1.0).all()  # round-to-nearest loses the update
+
+
+@pytest.mark.parametrize("state", [torch.float32, torch.bfloat16])
+def test_adamw_sr_matches_reference_twin(state):
+    """bf16 params (+ optionally bf16 moments) with stochastic rounding: the kernel and the PyTorch
+    twin use the same hash streams, so they agree except where fp32 op ordering moves a value
+    across a rounding threshold (rare, and then by one bf16 ulp)."""
+    torch.manual_seed(0)
+    n, off, seed = 200003, 4096, 777
+    p = torch.randn(n, device=DEV).to(torch.bfloat16)
+    g = torch.randn(n, device=DEV).to(torch.bfloat16)
+    m = (torch.randn(n, device=DEV) * 0.01).to(state)
+    v = (torch.randn(n, device=DEV).abs() * 0.001).to(state)
+    coef = torch.tensor([0.7], device=DEV)
+    p2, m2, v2 = p.clone(), m.clone(), v.clone()
+    _ext.ops().adamw_flat(p, g, None, m, v, coef, 1e-3, 0.9, 0.999, 1e-8, 0.01, 1 - 0.9 ** 5, 1 - 0.999 ** 5,
+                          seed, off)
+    ref.adamw_(p2, g.float() * 0.7, m2, v2, None, 1e-3, 0.9, 0.999, 1e-8, 0.01, 5, sr_seed=seed, sr_offset=off)
+    for a, b in ((p, p2), (m, m2), (v, v2)):
+        assert a.dtype == b.dtype
+        diff = (a.float() - b.float()).abs()
+        bf = b.float().abs()
+        # fp32: the kernel's (1.f - b2) is 1 - fp32(0.999) = 1.0000467e-3, torch's is fp32(1e-3): 5e-5
+        # relative on the g^2 term; values near zero come out of cancellations (m = 0.9 m + 0.1 g)
+        # bf16: an SR decision flipped by fp32 op ordering costs one ulp (two when it crosses a binade)
+        tol = (bf * 2 ** -6 if a.dtype == torch.bfloat16 else bf * 2e-4) + 1e-6 * bf.max()
+        bad = diff > tol
+        assert not bad.any(), (a.dtype, int(bad.sum()), a.float()[bad][:4].tolist(), b.float()[bad][:4].tolist())
+        if a.dtype == torch.bfloat16:
+            assert (diff > 0).float().mean().item() < 1e-3
 
 
 @pytest.mark.parametrize("L", [1, 200, 777])

@@ -116,6 +116,36 @@ def test_schedules():
     assert get_schedule("constant", 10)(7) == 1.0
 
 
+def test_stochastic_rounding_twin_unbiased():
+    from llm_fine_tune_distributed_amd.ops import reference as ref
+    x = torch.full((1 << 16,), 1.0 + 2 ** -9)  # 1/4 of the way from bf16 1.0 to the next value 1 + 2^-7
+    r = ref.bf16_stochastic_round(x, seed=3, offset=11)
+    assert set(r.float().unique().tolist()) == {1.0, 1.0 + 2 ** -7}
+    assert abs(r.float().mean().item() - (1.0 + 2 ** -9)) < 2e-4
+    assert torch.equal(r, ref.bf16_stochastic_round(x, seed=3, offset=11))  # counter-based: reproducible
+    assert not torch.equal(r, ref.bf16_stochastic_round(x, seed=4, offset=11))
+    y = torch.tensor([float("inf"), -float("inf"), -3.5])
+    assert torch.equal(ref.bf16_stochastic_round(y, 1).float(), y)
+
+
+def test_bf16_optimizer_state_trains(tmp_path, tk):
+    """optim_state_dtype="bf16": bf16 params + bf16 moments (stochastic rounding) — torch AdamW's state
+    dtype for the reference's bf16 model — trains and tracks the fp32-state run closely."""
+    rows = generate_qa(16, seed=2)
+    res = {}
+    for st in ("fp32", "bf16"):
+        a = SFTConfig(output_dir=str(tmp_path / st), per_device_train_batch_size=4, max_steps=3, learning_rate=1e-3,
+                      jsonl_log=False, optim_state_dtype=st, logging_steps=1)
+        m = build_model(tiny(vocab_size=1024), dtype=torch.bfloat16, seed=0)
+        t = SFTTrainer(model=m, args=a, train_dataset=rows, processing_class=tk)
+        assert t.optimizer.exp_avg.dtype == (torch.bfloat16 if st == "bf16" else torch.float32)
+        out = t.train()
+        res[st] = (out.training_loss, t.engine.param_flat.float().clone())
+    assert abs(res["fp32"][0] - res["bf16"][0]) < 0.05 * abs(res["fp32"][0])
+    d = (res["fp32"][1] - res["bf16"][1]).norm() / res["fp32"][1].norm()
+    assert d < 1e-2
+
+
 def test_reference_freeze_policy_counts(tmp_path, tk):
     a = SFTConfig(output_dir=str(tmp_path), freeze_policy="last_n_layers", max_steps=1, jsonl_log=False,
                   per_device_train_batch_size=2)
