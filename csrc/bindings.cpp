@@ -25,6 +25,10 @@ TORCH_LIBRARY(sftamd, m) {
   m.def("decode_attention(Tensor q, Tensor kcache, Tensor vcache, Tensor cache_len, int n_q, int n_kv, float scale) -> Tensor");
   // weight-gradient GEMM: out[N,K] (+)= dy[T,N]^T x[T,K]
   m.def("wgrad_gemm(Tensor(a!) out, Tensor dy, Tensor x, bool accumulate, int cfg=0) -> ()");
+  // forward-layout GEMM C = a w^T with fused epilogues (csrc/gemm_tn.hip)
+  m.def("gemm_tn(Tensor a, Tensor w, int cfg=0) -> Tensor");
+  m.def("gemm_tn_swiglu(Tensor x, Tensor w_gate_up) -> (Tensor, Tensor)");
+  m.def("gemm_tn_rope(Tensor x, Tensor w, Tensor cos, Tensor sin, int rope_cols, int cfg=0) -> Tensor");
   // optimizer
   m.def("sumsq(Tensor x) -> Tensor");
   m.def("adamw_flat(Tensor(a!) param, Tensor grad, Tensor(b!)? master, Tensor(c!) exp_avg, Tensor(d!) exp_avg_sq, Tensor clip_coef, float lr, float beta1, float beta2, float eps, float weight_decay, float bc1, float bc2, int sr_seed=0, int sr_offset=0) -> ()");

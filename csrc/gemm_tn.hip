@@ -1,0 +1,683 @@
+// Forward-layout GEMM for gfx950 with fused epilogues: C[M, N] = A[M, K] . B[N, K]^T, bf16 in, fp32
+// accumulate (the projection forward y = x W^T: both operands K-contiguous, "TN" in BLAS terms).
+//
+// Why a hand-written kernel next to hipBLASLt: the elementwise op that follows each projection can
+// ride in the epilogue instead of re-reading the GEMM output from HBM:
+//   EPI_SWIGLU  gate_up projection: writes gu = [gate | up] (saved for backward) AND act = silu(gate)*up
+//               (the down projection's input) — the separate SwiGLU kernel's 540 MB/layer re-read is gone;
+//   EPI_ROPE    qkv projection: rotary embedding of the q and k heads applied before the store.
+// The pairing trick: the B tile's LDS image is filled from permuted WEIGHT ROWS (no weight copy —
+// the stager just points its pieces at other rows) so that MFMA fragments j = 2q and 2q + 1 of a
+// wave hold the two columns the epilogue must combine: (gate c, up c) for SwiGLU, (d, d + 64) of a
+// head for RoPE (rotate_half). Weights keep their HF layout ([gate; up], [q; k; v]).
+//
+// Main loop = the ring structure of gemm_wgrad.hip (measured there): 256 x 256 (or 256 x 128) tile
+// per 512-thread workgroup (8 waves, 2x4 / 4x2), BK = 32 per stage, NS stages of global_load_lds
+// in flight (up to all 160 KB of LDS), counted vmcnt + raw s_barrier (one per stage), next-stage
+// fragments read during the current stage's MFMAs, LDS-DMA pieces interleaved with MFMA rows.
+// Operands are K-contiguous, so fragments are plain 16-byte ds_read_b128 rows (no transposed read):
+// LDS image rows are 64 B (32 bf16 of k) with a chunk swizzle (swz below) applied on the GLOBAL
+// source address (glds writes lane-linear) that makes every ds_read_b128 lane group conflict-free.
+// Tile order: XCD-aware bijective remap, then GROUP_M-blocked (8 M-tiles per group) so the ~32
+// tiles an XCD runs at once share A and B slabs in its L2.
+#include "common.h"
+
+namespace sftamd {
+namespace tn {
+
+constexpr int NT = 512;
+constexpr int BK = 32;     // k per stage
+constexpr int ROWB = 64;   // bytes per LDS image row
+static int group_m() {
+  static const int v = [] {
+    const char* e = std::getenv("SFTAMD_TN_GROUP");
+    return e && e[0] ? std::max(1, atoi(e)) : 8;
+  }();
+  return v;
+}
+
+enum { EPI_PLAIN = 0, EPI_SWIGLU = 1, EPI_ROPE = 2 };
+
+// ds_read_b128 is serviced in four NON-contiguous 16-lane groups (MI355X_MICROARCH.md §LDS:
+// {0-3,12-15,20-27}, {4-11,16-19,28-31}, ...). A fragment read has lane (g = lane>>4, ii = lane&15) at
+// image row R + ii, chunk g: its 16-B slot in the 256-B bank row is 4 (ii & 3) + (g ^ S(ii >> 2)).
+// S = {0, 2, 3, 1} makes the 16 slots of every group distinct (the plain S(q) = q is 2-way).
+__device__ __forceinline__ int swz_sel(int q) { return (0x78 >> (2 * q)) & 3; }
+__device__ __forceinline__ int swz(int row, int ch) { return ch ^ swz_sel((row >> 2) & 3); }
+
+__device__ __forceinline__ void glds16(const u16* src, char* dst) {
+  __builtin_amdgcn_global_load_lds((const void __attribute__((address_space(1)))*)src,
+                                   (void __attribute__((address_space(3)))*)dst, 16, 0, 0);
+}
+
+__device__ __forceinline__ bf16x8 lds_row(const char* base, int off) { return *(const bf16x8*)(base + off); }
+
+constexpr unsigned waitcnt_imm(int vm, int lgkm) {  // gfx9: vmcnt[3:0] expcnt[6:4] lgkmcnt[11:8] vmcnt[5:4]<<14
+  return (unsigned)((vm & 15) | (7 << 4) | ((lgkm & 15) << 8) | ((vm >> 4) << 14));
+}
+
+template <int BM, int BN, int WM, int WN, int NS_>
+struct Cfg {
+  static constexpr int NS = NS_;
+  static constexpr int TM = BM / WM, TN = BN / WN;
+  static constexpr int FM = TM / 16, FN = TN / 16;
+  static constexpr int APIECES = BM / 16, PIECES = (BM + BN) / 16;  // 1 KB = 16 image rows per piece
+  static constexpr int PPW = PIECES / 8;
+  static constexpr int STAGE = (BM + BN) * ROWB;
+  static constexpr int EPI_ROWS = 64, EPI_LD = TN + 4;
+  static constexpr int EPI = 8 * EPI_ROWS * EPI_LD * 4;
+  static constexpr int LDS = (NS * STAGE > EPI) ? NS * STAGE : EPI;
+  static_assert(WM * WN == 8 && PIECES % 8 == 0 && FM >= PPW, "config");
+  static_assert(TN == 64, "epilogue pairing assumes 64-column wave tiles");
+  static_assert(LDS <= 160 * 1024, "LDS budget");
+};
+
+// Global row of the B operand that lands in LDS image rows [16 pb, 16 pb + 16) of a tile.
+template <int EPI, int BN>
+__device__ __forceinline__ int b_piece_row(int pb, int n0, int I) {
+  if constexpr (EPI == EPI_SWIGLU) {
+    // image rows 32q + 16h + r <- gate (h=0) / up (h=1) row c0 + 16q + r; c0 = n0 / 2 (act columns)
+    return (pb & 1) * I + (n0 >> 1) + 16 * (pb >> 1);
+  } else if constexpr (EPI == EPI_ROPE) {
+    // per 128-row head: image rows 32q + 16h + r <- head dim d = 16q + 64h + r
+    const int head = pb >> 3, u = pb & 7;
+    return n0 + 128 * head + 16 * (u >> 1) + 64 * (u & 1);
+  } else {
+    return n0 + 16 * pb;
+  }
+}
+
+// Piece j of wave w is global piece P = w + 8 j (A pieces first). Every piece of a wave is a fixed
+// number of rows away from the wave's first A / first B piece (also for the permuted B rows of the
+// SWIGLU / ROPE tiles), so the stager keeps two lane pointers and compile-time row strides.
+template <int EPI>
+constexpr int b_piece_stride() { return EPI == EPI_SWIGLU ? 64 : 128; }  // rows between B pieces w + 8k
+
+template <class G, int EPI>
+struct Stager {
+  static constexpr int JA = G::APIECES / 8;  // pieces j < JA are A pieces
+  const u16* pa;
+  const u16* pb;
+  long lda, ldb;
+  int left;
+  __device__ __forceinline__ void piece(char* buf, int w, int j) {
+    const u16* src = j < JA ? pa + (long)(128 * j) * lda : pb + (long)(b_piece_stride<EPI>() * (j - JA)) * ldb;
+    glds16(src, buf + (w + 8 * j) * 1024);  // image = A rows then B rows, 1 KB (16 rows) per piece
+  }
+  __device__ __forceinline__ void advance() {
+    if (--left > 0) {
+      pa += BK;
+      pb += BK;
+    }
+  }
+  __device__ __forceinline__ void issue(char* buf, int w) {
+#pragma unroll
+    for (int j = 0; j < G::PPW; ++j) piece(buf, w, j);
+    advance();
+  }
+};
+
+__device__ __forceinline__ char* pick(int i, char* b0, char* b1, char* b2, char* b3, char* b4, char* b5) {
+  switch (i) {
+    case 0: return b0;
+    case 1: return b1;
+    case 2: return b2;
+    case 3: return b3;
+    case 4: return b4;
+    default: return b5;
+  }
+}
+
+template <class G, int EPI>
+__device__ __forceinline__ void ring_loop(char* __restrict__ b0, char* __restrict__ b1, char* __restrict__ b2,
+                                          char* __restrict__ b3, char* __restrict__ b4, char* __restrict__ b5,
+                                          int nsteps, Stager<G, EPI>& st, int w, int offA, int offB,
+                                          f32x4 (&acc)[G::FM][G::FN]) {
+  constexpr int NS = G::NS, PPW = G::PPW;
+  constexpr int U = (NS % 2) ? 2 * NS : NS;  // stage slot and B register set both compile-time
+  bf16x8 fa[G::FM], fb[2][G::FN];
+#pragma unroll
+  for (int i = 0; i < NS; ++i) st.issue(pick(i, b0, b1, b2, b3, b4, b5), w);
+  __builtin_amdgcn_s_waitcnt(waitcnt_imm((NS - 1) * PPW, 0));
+  __builtin_amdgcn_s_barrier();
+#pragma unroll
+  for (int j = 0; j < G::FN; ++j) fb[0][j] = lds_row(b0, offB + 1024 * j);
+#pragma unroll
+  for (int i = 0; i < G::FM; ++i) fa[i] = lds_row(b0, offA + 1024 * i);
+  for (int t0 = 0; t0 < nsteps; t0 += U) {
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      if (t0 + u < nsteps) {
+        __builtin_amdgcn_s_waitcnt(waitcnt_imm((NS - 2) * PPW, 0));
+        __builtin_amdgcn_s_barrier();
+        char* dst = pick(u % NS, b0, b1, b2, b3, b4, b5);
+        const char* nxt = pick((u + 1) % NS, b0, b1, b2, b3, b4, b5);
+        const int cb = u & 1;
+#pragma unroll
+        for (int j = 0; j < G::FN; ++j) fb[cb ^ 1][j] = lds_row(nxt, offB + 1024 * j);
+        __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+        for (int i = 0; i < G::FM; ++i) {
+#pragma unroll
+          for (int j = 0; j < G::FN; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[cb][j], acc[i][j], 0, 0, 0);
+          fa[i] = lds_row(nxt, offA + 1024 * i);
+          if (i < PPW) st.piece(dst, w, i);
+          __builtin_amdgcn_sched_group_barrier(0x008, G::FN, 0);  // MFMA
+          __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);      // DS read (one fragment)
+          if (i < PPW) __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);  // VMEM (the DMA)
+        }
+        st.advance();
+        __builtin_amdgcn_s_setprio(0);
+      }
+    }
+  }
+  __builtin_amdgcn_s_waitcnt(waitcnt_imm(0, 0));  // drain the tail DMAs before LDS is reused
+}
+
+struct EpiArgs {
+  u16* C;        // PLAIN / ROPE: C[M, ldc];  SWIGLU: gu[M, 2I]
+  u16* act;      // SWIGLU: act[M, I]
+  const float* cosb;  // ROPE: [M, 64] fp32
+  const float* sinb;
+  long ldc;
+  int I;          // SWIGLU: intermediate size
+  int rope_cols;  // ROPE: columns [0, rope_cols) are rotated (q and k heads)
+};
+
+__device__ __forceinline__ float silu(float g) { return g / (1.f + __expf(-g)); }
+__device__ __forceinline__ float rbf(float x) { return bf2f(f2bf(x)); }
+
+// fp32 wave tile -> wave-private LDS rows (TN + 4 floats, conflict-free) -> 16-byte stores.
+template <class G, int EPI>
+__device__ __forceinline__ void epilogue(char* smem, f32x4 (&acc)[G::FM][G::FN], const EpiArgs& ea, int m0, int n0,
+                                         int wm, int wn, int w, int lane) {
+  const int g = lane >> 4, ii = lane & 15;
+  float* ep = reinterpret_cast<float*>(smem) + w * G::EPI_ROWS * G::EPI_LD;
+  constexpr int FPP = G::EPI_ROWS / 16 < G::FM ? G::EPI_ROWS / 16 : G::FM;  // fragment rows per pass
+  constexpr int ROWS = FPP * 16;
+#pragma unroll
+  for (int pass = 0; pass < G::FM / FPP; ++pass) {
+#pragma unroll
+    for (int i = 0; i < FPP; ++i)
+#pragma unroll
+      for (int j = 0; j < G::FN; ++j)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) ep[(16 * i + 4 * g + e) * G::EPI_LD + 16 * j + ii] = acc[pass * FPP + i][j][e];
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // wave-private region: writes before reads
+    const int rbase = m0 + wm * G::TM + pass * ROWS;
+    if constexpr (EPI == EPI_PLAIN) {
+      constexpr int SEGS = G::TN / 8;
+#pragma unroll
+      for (int it = 0; it < ROWS * SEGS / 64; ++it) {
+        const int seg = it * 64 + lane, row = seg / SEGS, cs = seg - row * SEGS;
+        const float* pr = ep + row * G::EPI_LD + cs * 8;
+        float v[8];
+        *(float4*)&v[0] = *(const float4*)pr;
+        *(float4*)&v[4] = *(const float4*)(pr + 4);
+        *(uint4*)(ea.C + (long)(rbase + row) * ea.ldc + n0 + wn * G::TN + cs * 8) = pack8(v);
+      }
+    } else {
+      // unit = (row, pair p, half): segment a = cols 32p + 8h (fragment 2p), b = cols 32p + 16 + 8h (2p + 1)
+      constexpr int UPR = G::TN / 16;  // units per row
+#pragma unroll
+      for (int it = 0; it < ROWS * UPR / 64; ++it) {
+        const int un = it * 64 + lane, row = un / UPR, r = un - row * UPR, p = r >> 1, hh = r & 1;
+        const float* pa = ep + row * G::EPI_LD + 32 * p + 8 * hh;
+        float a[8], b[8];
+        *(float4*)&a[0] = *(const float4*)pa;
+        *(float4*)&a[4] = *(const float4*)(pa + 4);
+        *(float4*)&b[0] = *(const float4*)(pa + 16);
+        *(float4*)&b[4] = *(const float4*)(pa + 20);
+        const long grow = rbase + row;
+        const int t = wn * G::TN + 32 * p + 8 * hh;  // image column of segment a
+        if constexpr (EPI == EPI_SWIGLU) {
+          const int c = (n0 >> 1) + 16 * (t >> 5) + 8 * hh;  // act column
+          float o[8];
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            a[e] = rbf(a[e]);  // act from the bf16 gate/up the backward will see
+            b[e] = rbf(b[e]);
+            o[e] = silu(a[e]) * b[e];
+          }
+          u16* gp = ea.C + grow * ea.ldc + c;
+          *(uint4*)gp = pack8(a);
+          *(uint4*)(gp + ea.I) = pack8(b);
+          *(uint4*)(ea.act + grow * ea.I + c) = pack8(o);
+        } else {  // ROPE
+          const int head = t >> 7, u = t & 127, d = 16 * (u >> 5) + 8 * hh;
+          const int col = n0 + 128 * head + d;
+          u16* op = ea.C + grow * ea.ldc + col;
+          if (col < ea.rope_cols) {
+            float cs[8], sn[8], lo[8], hi[8];
+            const float* cp = ea.cosb + grow * 64 + d;
+            const float* sp = ea.sinb + grow * 64 + d;
+            *(float4*)&cs[0] = *(const float4*)cp;
+            *(float4*)&cs[4] = *(const float4*)(cp + 4);
+            *(float4*)&sn[0] = *(const float4*)sp;
+            *(float4*)&sn[4] = *(const float4*)(sp + 4);
+#pragma unroll
+            for (int e = 0; e < 8; ++e) {
+              const float x1 = rbf(a[e]), x2 = rbf(b[e]);  // rope of the bf16 projection (unfused twin)
+              lo[e] = x1 * cs[e] - x2 * sn[e];
+              hi[e] = x2 * cs[e] + x1 * sn[e];
+            }
+            *(uint4*)op = pack8(lo);
+            *(uint4*)(op + 64) = pack8(hi);
+          } else {
+            *(uint4*)op = pack8(a);
+            *(uint4*)(op + 64) = pack8(b);
+          }
+        }
+      }
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  }
+}
+
+template <int BM, int BN, int WM, int WN, int NS, int EPI>
+__global__ void __launch_bounds__(NT) tn_kernel(const u16* __restrict__ A, const u16* __restrict__ B, int K, long lda,
+                                                long ldb, int nbm, int nbn, int group, EpiArgs ea) {
+  using G = Cfg<BM, BN, WM, WN, NS>;
+  __shared__ __attribute__((aligned(16))) char smem[G::LDS];
+  // XCD-aware bijective remap (consecutive ids share an XCD), then GROUP_M-blocked tile order
+  const int nwg = gridDim.x, orig = blockIdx.x;
+  const int xcd = orig & 7, q8 = nwg >> 3, r8 = nwg & 7;
+  const int wgid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (orig >> 3);
+  const int per_group = group * nbn;
+  const int grp = wgid / per_group, first = grp * group;
+  const int gsz = min(nbm - first, group);
+  const int in = wgid - grp * per_group;
+  const int bm = first + in % gsz, bn = in / gsz;
+  const int m0 = bm * BM, n0 = bn * BN;
+
+  const int tid = threadIdx.x, lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = w / WN, wn = w - wm * WN;
+
+  Stager<G, EPI> st;
+  st.lda = lda;
+  st.ldb = ldb;
+  st.left = K / BK;
+  {
+    const int lr = lane >> 2, ch = swz(lr, lane & 3);  // row in piece, pre-swizzled chunk
+    st.pa = A + (long)(m0 + 16 * w + lr) * lda + 8 * ch;
+    st.pb = B + (long)(b_piece_row<EPI, BN>(w, n0, ea.I) + lr) * ldb + 8 * ch;
+  }
+  // fragment rows 16 i + ii all share the swizzle of ii (bits 2-3 of the row): fragment i of a wave
+  // is 1 KB after fragment i - 1, an immediate offset of the ds_read
+  const int g = lane >> 4, ii = lane & 15;
+  const int offA = (wm * G::TM + ii) * ROWB + 16 * swz(ii, g);
+  const int offB = (BM + wn * G::TN + ii) * ROWB + 16 * swz(ii, g);
+  f32x4 acc[G::FM][G::FN];
+#pragma unroll
+  for (int i = 0; i < G::FM; ++i)
+#pragma unroll
+    for (int j = 0; j < G::FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  char* b[6];
+#pragma unroll
+  for (int i = 0; i < 6; ++i) b[i] = smem + (i < NS ? i : 0) * G::STAGE;
+  ring_loop<G, EPI>(b[0], b[1], b[2], b[3], b[4], b[5], K / BK, st, w, offA, offB, acc);
+  __syncthreads();
+  epilogue<G, EPI>(smem, acc, ea, m0, n0, wm, wn, w, lane);
+}
+
+// ============================================================================================
+// BK = 64 variant: 128-byte LDS image rows = whole cache lines per glds row (the BK = 32 ring above
+// fetches every line in two 64-byte halves, one per stage, which costs L2 request bandwidth).
+// Stage = (BM + BN) x 128 B (64 KB at 256 x 256), NS = 2 stages; each stage is consumed in two
+// 32-deep MFMA sub-steps; the only barrier is before the first read of the next stage, after which
+// the DMA of stage t + NS goes into the slot just drained.
+// Swizzle for 128-B rows: chunk ^ ((row >> 1) & 7) — conflict-free for the ds_read_b128 lane groups.
+// ============================================================================================
+constexpr int BK2 = 64, ROWB2 = 128;
+__device__ __forceinline__ int swz2(int row, int ch) { return ch ^ ((row >> 1) & 7); }
+
+template <int BM, int BN, int WM, int WN, int NS_>
+struct Cfg2 {
+  static constexpr int NS = NS_;
+  static constexpr int TM = BM / WM, TN = BN / WN;
+  static constexpr int FM = TM / 16, FN = TN / 16;
+  static constexpr int APIECES = BM / 8, PIECES = (BM + BN) / 8;  // 1 KB = 8 image rows per piece
+  static constexpr int PPW = PIECES / 8;
+  static constexpr int STAGE = (BM + BN) * ROWB2;
+  static constexpr int EPI_ROWS = 64, EPI_LD = TN + 4;
+  static constexpr int EPI = 8 * EPI_ROWS * EPI_LD * 4;
+  static constexpr int LDS = (NS * STAGE > EPI) ? NS * STAGE : EPI;
+  static_assert(WM * WN == 8 && PIECES % 8 == 0 && FM * 2 >= PPW, "config");
+  static_assert(TN == 64, "epilogue pairing assumes 64-column wave tiles");
+  static_assert(LDS <= 160 * 1024, "LDS budget");
+};
+
+// Row offset (in B rows) of B piece pb = w + 8 k relative to piece w, and the base row of piece w.
+// 8-row pieces of the permuted images: SWIGLU image row 32q + 16h + r, ROPE (per 128-row head) 32q + 16h + r.
+template <int EPI>
+__device__ __forceinline__ int b2_row(int pb, int n0, int I) {
+  if constexpr (EPI == EPI_SWIGLU) {
+    return ((pb >> 1) & 1) * I + (n0 >> 1) + 16 * (pb >> 2) + 8 * (pb & 1);
+  } else if constexpr (EPI == EPI_ROPE) {
+    const int head = pb >> 4, v = pb & 15;
+    return n0 + 128 * head + 16 * (v >> 2) + 64 * ((v >> 1) & 1) + 8 * (v & 1);
+  } else {
+    return n0 + 8 * pb;
+  }
+}
+template <int EPI>
+constexpr int b2_koff(int k) {  // b2_row(w + 8k) - b2_row(w), independent of w < 8
+  return EPI == EPI_SWIGLU ? 32 * k : (EPI == EPI_ROPE ? 32 * (k & 1) + 128 * (k >> 1) : 64 * k);
+}
+
+template <class G, int EPI>
+struct Stager2 {
+  static constexpr int JA = G::APIECES / 8;
+  const u16* pa;
+  const u16* pb;
+  long lda, ldb;
+  int left;
+  __device__ __forceinline__ void piece(char* buf, int w, int j) {
+    const u16* src = j < JA ? pa + (long)(64 * j) * lda : pb + (long)b2_koff<EPI>(j - JA) * ldb;
+    glds16(src, buf + (w + 8 * j) * 1024);
+  }
+  __device__ __forceinline__ void advance() {
+    if (--left > 0) {
+      pa += BK2;
+      pb += BK2;
+    }
+  }
+};
+
+template <class G, int EPI, bool SCHED = true>
+__device__ __forceinline__ void ring2_loop(char* __restrict__ b0, char* __restrict__ b1, char* __restrict__ b2,
+                                           int nsteps, Stager2<G, EPI>& st, int w, int offA0, int offA1, int offB0,
+                                           int offB1, f32x4 (&acc)[G::FM][G::FN]) {
+  constexpr int NS = G::NS, PPW = G::PPW;
+  bf16x8 fa[G::FM], fb[2][G::FN];
+#pragma unroll
+  for (int i = 0; i < NS; ++i) {
+    char* d = i == 0 ? b0 : (i == 1 ? b1 : b2);
+#pragma unroll
+    for (int j = 0; j < PPW; ++j) st.piece(d, w, j);
+    st.advance();
+  }
+  __builtin_amdgcn_s_waitcnt(waitcnt_imm((NS - 1) * PPW, 0));
+  __builtin_amdgcn_s_barrier();
+#pragma unroll
+  for (int j = 0; j < G::FN; ++j) fb[0][j] = lds_row(b0, offB0 + 2048 * j);
+#pragma unroll
+  for (int i = 0; i < G::FM; ++i) fa[i] = lds_row(b0, offA0 + 2048 * i);
+  for (int t0 = 0; t0 < nsteps; t0 += NS) {
+#pragma unroll
+    for (int u = 0; u < NS; ++u) {
+      if (t0 + u < nsteps) {
+        char* cur = u == 0 ? b0 : (u == 1 ? b1 : b2);
+        const int un = (u + 1) % NS;
+        char* nxt = un == 0 ? b0 : (un == 1 ? b1 : b2);
+        // sub-step 0: MFMA on (t, k 0..31) while reading (t, k 32..63) from the same slot
+#pragma unroll
+        for (int j = 0; j < G::FN; ++j) fb[1][j] = lds_row(cur, offB1 + 2048 * j);
+        __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+        for (int i = 0; i < G::FM; ++i) {
+#pragma unroll
+          for (int j = 0; j < G::FN; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[0][j], acc[i][j], 0, 0, 0);
+          fa[i] = lds_row(cur, offA1 + 2048 * i);
+          if (SCHED) {
+            __builtin_amdgcn_sched_group_barrier(0x008, G::FN, 0);
+            __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+          }
+        }
+        __builtin_amdgcn_s_setprio(0);
+        // sub-step 1: stage t+1 landed (own DMAs) and every wave is done reading slot t -> barrier,
+        // then refill slot t with stage t + NS while MFMA-ing (t, k 32..63) and reading (t+1, k 0..31)
+        __builtin_amdgcn_s_waitcnt(waitcnt_imm((NS - 2) * PPW, 0));
+        __builtin_amdgcn_s_barrier();
+        // (after the last stage these read a slot nobody uses: harmless, and branch-free)
+#pragma unroll
+        for (int j = 0; j < G::FN; ++j) fb[0][j] = lds_row(nxt, offB0 + 2048 * j);
+        __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+        for (int i = 0; i < G::FM; ++i) {
+#pragma unroll
+          for (int j = 0; j < G::FN; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[1][j], acc[i][j], 0, 0, 0);
+          fa[i] = lds_row(nxt, offA0 + 2048 * i);
+          // DMA pieces of stage t + NS spread over the fragment rows (PPW <= 2 FM)
+          if (2 * i < PPW) st.piece(cur, w, 2 * i);
+          if (2 * i + 1 < PPW) st.piece(cur, w, 2 * i + 1);
+          if (SCHED) {
+            __builtin_amdgcn_sched_group_barrier(0x008, G::FN, 0);
+            __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+            if (2 * i + 1 < PPW) __builtin_amdgcn_sched_group_barrier(0x020, 2, 0);
+            else if (2 * i < PPW) __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
+          }
+        }
+        st.advance();
+        __builtin_amdgcn_s_setprio(0);
+      }
+    }
+  }
+  __builtin_amdgcn_s_waitcnt(waitcnt_imm(0, 0));
+}
+
+// Early-release variant of ring2_loop (NS = 2): all fragments of a stage's second k-half are read
+// at the start of the stage (32 more VGPRs), so the slot is released — and the DMA of stage t + 2
+// issued into it — half a stage earlier: ~1.5 stages of lead time per DMA instead of 1.
+template <class G, int EPI>
+__device__ __forceinline__ void ring2e_loop(char* __restrict__ b0, char* __restrict__ b1, int nsteps,
+                                            Stager2<G, EPI>& st, int w, int offA0, int offA1, int offB0, int offB1,
+                                            f32x4 (&acc)[G::FM][G::FN]) {
+  constexpr int PPW = G::PPW, H = G::FM / 2;
+  static_assert(G::NS == 2 && PPW <= 2 * H, "early-release ring: 2 stages");
+  bf16x8 fa[G::FM], fa2[G::FM], fb0[G::FN], fb1[G::FN];
+#pragma unroll
+  for (int j = 0; j < PPW; ++j) st.piece(b0, w, j);
+  st.advance();
+#pragma unroll
+  for (int j = 0; j < PPW; ++j) st.piece(b1, w, j);
+  st.advance();
+  __builtin_amdgcn_s_waitcnt(waitcnt_imm(PPW, 0));
+  __builtin_amdgcn_s_barrier();
+#pragma unroll
+  for (int j = 0; j < G::FN; ++j) fb0[j] = lds_row(b0, offB0 + 2048 * j);
+#pragma unroll
+  for (int i = 0; i < G::FM; ++i) fa[i] = lds_row(b0, offA0 + 2048 * i);
+  for (int t0 = 0; t0 < nsteps; t0 += 2) {
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      if (t0 + u < nsteps) {
+        char* cur = u == 0 ? b0 : b1;
+        char* nxt = u == 0 ? b1 : b0;
+        // A: read (t, k 32..63); MFMA the first half of (t, k 0..31) while they land
+#pragma unroll
+        for (int j = 0; j < G::FN; ++j) fb1[j] = lds_row(cur, offB1 + 2048 * j);
+#pragma unroll
+        for (int i = 0; i < G::FM; ++i) fa2[i] = lds_row(cur, offA1 + 2048 * i);
+        __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+        for (int i = 0; i < H; ++i)
+#pragma unroll
+          for (int j = 0; j < G::FN; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb0[j], acc[i][j], 0, 0, 0);
+        __builtin_amdgcn_s_setprio(0);
+        __builtin_amdgcn_s_waitcnt(waitcnt_imm(PPW, 0));  // own reads of slot cur done (stage t+1 may fly)
+        __builtin_amdgcn_s_barrier();                     // every wave's reads of slot cur done
+        __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+        for (int i = H; i < G::FM; ++i) {
+#pragma unroll
+          for (int j = 0; j < G::FN; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb0[j], acc[i][j], 0, 0, 0);
+          const int q = i - H;
+          if (2 * q < PPW) st.piece(cur, w, 2 * q);
+          if (2 * q + 1 < PPW) st.piece(cur, w, 2 * q + 1);
+          __builtin_amdgcn_sched_group_barrier(0x008, G::FN, 0);
+          if (2 * q + 1 < PPW) __builtin_amdgcn_sched_group_barrier(0x020, 2, 0);
+          else if (2 * q < PPW) __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
+        }
+        st.advance();
+        __builtin_amdgcn_s_setprio(0);
+        // B: stage t+1 landed (leave stage t+2 in flight); read (t+1, k 0..31) under (t, k 32..63)
+        __builtin_amdgcn_s_waitcnt(waitcnt_imm(PPW, 0));
+        __builtin_amdgcn_s_barrier();
+#pragma unroll
+        for (int j = 0; j < G::FN; ++j) fb0[j] = lds_row(nxt, offB0 + 2048 * j);
+        __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+        for (int i = 0; i < G::FM; ++i) {
+#pragma unroll
+          for (int j = 0; j < G::FN; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa2[i], fb1[j], acc[i][j], 0, 0, 0);
+          fa[i] = lds_row(nxt, offA0 + 2048 * i);
+          __builtin_amdgcn_sched_group_barrier(0x008, G::FN, 0);
+          __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+        }
+        __builtin_amdgcn_s_setprio(0);
+      }
+    }
+  }
+  __builtin_amdgcn_s_waitcnt(waitcnt_imm(0, 0));
+}
+
+template <int BM, int BN, int WM, int WN, int NS, int EPI, int VAR = 0>
+__global__ void __launch_bounds__(NT) tn2_kernel(const u16* __restrict__ A, const u16* __restrict__ B, int K, long lda,
+                                                 long ldb, int nbm, int nbn, int group, EpiArgs ea) {
+  using G = Cfg2<BM, BN, WM, WN, NS>;
+  __shared__ __attribute__((aligned(16))) char smem[G::LDS];
+  const int nwg = gridDim.x, orig = blockIdx.x;
+  const int xcd = orig & 7, q8 = nwg >> 3, r8 = nwg & 7;
+  const int wgid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (orig >> 3);
+  const int per_group = group * nbn;
+  const int grp = wgid / per_group, first = grp * group;
+  const int gsz = min(nbm - first, group);
+  const int in = wgid - grp * per_group;
+  const int bm = first + in % gsz, bn = in / gsz;
+  const int m0 = bm * BM, n0 = bn * BN;
+  const int tid = threadIdx.x, lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = w / WN, wn = w - wm * WN;
+
+  Stager2<G, EPI> st;
+  st.lda = lda;
+  st.ldb = ldb;
+  st.left = K / BK2;
+  {
+    // piece P = w + 8 j holds image rows 8P + lr (lr = lane >> 3), slot lane & 7; (row >> 1) & 7 =
+    // 4 (P & 1) + (lr >> 1) and P & 1 = w & 1 for every piece of the wave
+    const int lr = lane >> 3, ch = (lane & 7) ^ (4 * (w & 1) + (lr >> 1));
+    st.pa = A + (long)(m0 + 8 * w + lr) * lda + 8 * ch;
+    st.pb = B + (long)(b2_row<EPI>(w, n0, ea.I) + lr) * ldb + 8 * ch;
+  }
+  const int g = lane >> 4, ii = lane & 15;
+  const int ra = wm * G::TM + ii, rb = BM + wn * G::TN + ii;
+  const int offA0 = ra * ROWB2 + 16 * swz2(ra, g), offA1 = ra * ROWB2 + 16 * swz2(ra, 4 + g);
+  const int offB0 = rb * ROWB2 + 16 * swz2(rb, g), offB1 = rb * ROWB2 + 16 * swz2(rb, 4 + g);
+  f32x4 acc[G::FM][G::FN];
+#pragma unroll
+  for (int i = 0; i < G::FM; ++i)
+#pragma unroll
+    for (int j = 0; j < G::FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  if constexpr (VAR == 1)
+    ring2e_loop<G, EPI>(smem, smem + G::STAGE, K / BK2, st, w, offA0, offA1, offB0, offB1, acc);
+  else
+    ring2_loop<G, EPI, VAR == 2>(smem, smem + G::STAGE, smem + (NS > 2 ? 2 : 0) * G::STAGE, K / BK2, st, w, offA0,
+                                 offA1, offB0, offB1, acc);
+  __syncthreads();
+  epilogue<G, EPI>(smem, acc, ea, m0, n0, wm, wn, w, lane);
+}
+
+template <int BM, int BN, int WM, int WN, int NS, int EPI, int VAR = 0>
+void launch2(const at::Tensor& a, const at::Tensor& w, int N, const EpiArgs& ea) {
+  const int M = a.size(0), K = a.size(1);
+  const int nbm = M / BM, nbn = N / BN;
+  tn2_kernel<BM, BN, WM, WN, NS, EPI, VAR><<<nbm * nbn, NT, 0, cur_stream()>>>(
+      (const u16*)a.data_ptr(), (const u16*)w.data_ptr(), K, a.stride(0), w.stride(0), nbm, nbn,
+      std::min(group_m(), nbm), ea);
+  SFT_LAUNCH_CHECK();
+}
+
+template <int BM, int BN, int WM, int WN, int NS, int EPI>
+void launch(const at::Tensor& a, const at::Tensor& w, int N, const EpiArgs& ea) {
+  const int M = a.size(0), K = a.size(1);
+  const int nbm = M / BM, nbn = N / BN;
+  tn_kernel<BM, BN, WM, WN, NS, EPI><<<nbm * nbn, NT, 0, cur_stream()>>>(
+      (const u16*)a.data_ptr(), (const u16*)w.data_ptr(), K, a.stride(0), w.stride(0), nbm, nbn,
+      std::min(group_m(), nbm), ea);
+  SFT_LAUNCH_CHECK();
+}
+
+}  // namespace tn
+
+static void check_tn(const at::Tensor& a, const at::Tensor& w) {
+  SFT_CHECK_CUDA(a);
+  SFT_CHECK_BF16(a);
+  SFT_CHECK_BF16(w);
+  SFT_CHECK(a.dim() == 2 && w.dim() == 2 && a.size(1) == w.size(1), "gemm_tn: a [M, K], w [N, K]");
+  SFT_CHECK(a.stride(1) == 1 && w.stride(1) == 1, "gemm_tn: K-contiguous operands");
+  SFT_CHECK(a.stride(0) % 8 == 0 && w.stride(0) % 8 == 0, "gemm_tn: 16-byte aligned rows");
+  SFT_CHECK(a.size(0) % 256 == 0 && a.size(1) % tn::BK == 0 && a.size(1) > 0, "gemm_tn: M % 256, K % 32");
+}
+
+// cfg: 0 = 256x256 BK32 ring (NS 5), 1 = 256x128 BK32 ring (NS 6), 2 = 256x256 BK64 (NS 2; the fastest on the
+// SmolLM3 shapes, tools/bench_gemm_tn.py), 3 = BK64 early-release ring, 4 = BK64 with a pinned MFMA/DS/DMA
+// interleave (3 and 4 measured slower; kept for the microbench)
+at::Tensor gemm_tn(const at::Tensor& a, const at::Tensor& w, int64_t cfg) {
+  check_tn(a, w);
+  const int M = a.size(0), N = w.size(0);
+  auto c = at::empty({M, N}, a.options());
+  tn::EpiArgs ea{(u16*)c.data_ptr(), nullptr, nullptr, nullptr, (long)N, 0, 0};
+  if (cfg == 1) {
+    SFT_CHECK(N % 128 == 0, "gemm_tn 256x128: N % 128");
+    tn::launch<256, 128, 4, 2, 6, tn::EPI_PLAIN>(a, w, N, ea);
+  } else if (cfg == 2 || cfg == 3) {
+    SFT_CHECK(N % 256 == 0 && a.size(1) % 64 == 0, "gemm_tn BK64: N % 256, K % 64");
+    if (cfg == 2) tn::launch2<256, 256, 2, 4, 2, tn::EPI_PLAIN>(a, w, N, ea);
+    else tn::launch2<256, 256, 2, 4, 2, tn::EPI_PLAIN, 1>(a, w, N, ea);
+  } else if (cfg == 4) {  // BK64 with sched_group_barrier interleave pinned (measured slower: diagnostics)
+    SFT_CHECK(N % 256 == 0 && a.size(1) % 64 == 0, "gemm_tn BK64: N % 256, K % 64");
+    tn::launch2<256, 256, 2, 4, 2, tn::EPI_PLAIN, 2>(a, w, N, ea);
+  } else {
+    SFT_CHECK(N % 256 == 0, "gemm_tn 256x256: N % 256");
+    tn::launch<256, 256, 2, 4, 5, tn::EPI_PLAIN>(a, w, N, ea);
+  }
+  return c;
+}
+
+// x [M, K], w_gu [2I, K] = [gate; up]  ->  (gu [M, 2I], act [M, I] = silu(gate) * up)
+std::tuple<at::Tensor, at::Tensor> gemm_tn_swiglu(const at::Tensor& x, const at::Tensor& w_gu) {
+  check_tn(x, w_gu);
+  const int M = x.size(0), N = w_gu.size(0), I = N / 2;
+  SFT_CHECK(N % 2 == 0 && I % 128 == 0, "gemm_tn_swiglu: intermediate size % 128");
+  auto gu = at::empty({M, N}, x.options());
+  auto act = at::empty({M, I}, x.options());
+  tn::EpiArgs ea{(u16*)gu.data_ptr(), (u16*)act.data_ptr(), nullptr, nullptr, (long)N, I, 0};
+  if (x.size(1) % 64 == 0) tn::launch2<256, 256, 2, 4, 2, tn::EPI_SWIGLU>(x, w_gu, N, ea);
+  else tn::launch<256, 256, 2, 4, 5, tn::EPI_SWIGLU>(x, w_gu, N, ea);
+  return {gu, act};
+}
+
+// x [M, K], w [N, K] (N = (nq + 2 nkv) * 128), cos/sin [M, 64] fp32: C = x w^T with rotate_half RoPE
+// applied to columns [0, rope_cols).
+at::Tensor gemm_tn_rope(const at::Tensor& x, const at::Tensor& w, const at::Tensor& cosb, const at::Tensor& sinb,
+                        int64_t rope_cols, int64_t cfg) {
+  check_tn(x, w);
+  const int M = x.size(0), N = w.size(0);
+  SFT_CHECK(N % 256 == 0 && rope_cols % 128 == 0, "gemm_tn_rope: N % 256, head_dim 128");
+  SFT_CHECK(cosb.scalar_type() == at::kFloat && sinb.scalar_type() == at::kFloat && cosb.is_contiguous() &&
+                sinb.is_contiguous() && cosb.numel() == (long)M * 64 && sinb.numel() == (long)M * 64,
+            "gemm_tn_rope: cos/sin [M, 64] fp32");
+  auto c = at::empty({M, N}, x.options());
+  tn::EpiArgs ea{(u16*)c.data_ptr(), nullptr, cosb.data_ptr<float>(), sinb.data_ptr<float>(), (long)N, 0,
+                 (int)rope_cols};
+  if (cfg == 1) tn::launch<256, 128, 4, 2, 6, tn::EPI_ROPE>(x, w, N, ea);
+  else if (cfg == 2 && x.size(1) % 64 == 0) tn::launch2<256, 256, 2, 4, 2, tn::EPI_ROPE>(x, w, N, ea);
+  else tn::launch<256, 256, 2, 4, 5, tn::EPI_ROPE>(x, w, N, ea);
+  return c;
+}
+
+TORCH_LIBRARY_IMPL(sftamd, CUDA, m) {
+  m.impl("gemm_tn", &gemm_tn);
+  m.impl("gemm_tn_swiglu", &gemm_tn_swiglu);
+  m.impl("gemm_tn_rope", &gemm_tn_rope);
+}
+
+}  // namespace sftamd

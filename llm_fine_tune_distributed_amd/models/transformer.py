@@ -56,9 +56,14 @@ class Attention(nn.Module):
 
     def forward(self, h, rope_cs, cu_seqlens, max_seqlen):
         c = self.cfg
-        qkv = ops.linear(h, self.qkv_proj) if self.lora is None else ops.lora_linear(h, self.qkv_proj, self.lora["qkv"])
-        if self.use_rope:
-            qkv = ops.rope_(qkv, rope_cs[0], rope_cs[1], c.num_attention_heads, c.num_key_value_heads, c.head_dim)
+        if self.lora is None and self.use_rope:
+            # projection + RoPE in one HIP GEMM (epilogue rotation) where the shapes allow
+            qkv = ops.linear_rope(h, self.qkv_proj, rope_cs[0], rope_cs[1], c.num_attention_heads,
+                                  c.num_key_value_heads, c.head_dim)
+        else:
+            qkv = ops.linear(h, self.qkv_proj) if self.lora is None else ops.lora_linear(h, self.qkv_proj, self.lora["qkv"])
+            if self.use_rope:
+                qkv = ops.rope_(qkv, rope_cs[0], rope_cs[1], c.num_attention_heads, c.num_key_value_heads, c.head_dim)
         a = ops.flash_attention(qkv, cu_seqlens, max_seqlen, c.num_attention_heads, c.num_key_value_heads, c.head_dim)
         return ops.linear(a, self.o_proj) if self.lora is None else ops.lora_linear(a, self.o_proj, self.lora["o"])
 
@@ -72,8 +77,10 @@ class MLP(nn.Module):
 
     def forward(self, h):
         L = self.lora
-        gu = ops.linear(h, self.gate_up_proj) if L is None else ops.lora_linear(h, self.gate_up_proj, L["gate_up"])
-        a = ops.swiglu(gu)
+        if L is None:
+            a = ops.linear_swiglu(h, self.gate_up_proj)  # GEMM + SwiGLU epilogue where the shapes allow
+        else:
+            a = ops.swiglu(ops.lora_linear(h, self.gate_up_proj, L["gate_up"]))
         return ops.linear(a, self.down_proj) if L is None else ops.lora_linear(a, self.down_proj, L["down"])
 
 

@@ -9,6 +9,8 @@ from .fused import (
     embedding,
     flash_attention,
     linear,
+    linear_rope,
+    linear_swiglu,
     lm_head_cross_entropy,
     lora_linear,
     rms_norm,
@@ -19,6 +21,6 @@ from .optim_kernels import adamw_flat_, grad_norm_flat
 
 __all__ = [
     "reference", "load_extension", "use_hip", "hip_disabled", "IGNORE_INDEX", "add_rms_norm", "decode_attention", "dropout_add",
-    "embedding", "flash_attention", "linear", "lora_linear", "lm_head_cross_entropy", "rms_norm", "rope_", "swiglu",
+    "embedding", "flash_attention", "linear", "linear_rope", "linear_swiglu", "lora_linear", "lm_head_cross_entropy", "rms_norm", "rope_", "swiglu",
     "adamw_flat_", "grad_norm_flat",
 ]

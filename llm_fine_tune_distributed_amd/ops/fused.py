@@ -247,6 +247,94 @@ def swiglu(gate_up: torch.Tensor) -> torch.Tensor:
     return SwiGLUFn.apply(gate_up)
 
 
+# ----------------------------------------------------------------------------- projection + fused epilogue
+_TN_MODE = os.environ.get("SFTAMD_TN", "rope")  # rope | swiglu | 1 (both) | 0 (hipBLASLt + separate kernels)
+
+
+def _tn_ok(x2d: torch.Tensor, w: torch.Tensor) -> bool:
+    """Shapes the forward-layout HIP GEMM (csrc/gemm_tn.hip, BK64 tiles of 256 x 256) handles.
+
+    Default (measured end to end on MI355X, profiles/r1_gemm_tn.md): the qkv projection runs with the
+    RoPE epilogue (beats hipBLASLt + the rope kernel); gate_up + SwiGLU stays on hipBLASLt + the SwiGLU
+    kernel, because the fused kernel's GEMM core is ~5-10 % slower than hipBLASLt's on [8192, 22016] and
+    that cancels the saved pass (SFTAMD_TN=1 / swiglu turns it on)."""
+    return (_TN_MODE != "0" and _ext.use_hip(x2d) and x2d.dtype == torch.bfloat16 and w.dtype == torch.bfloat16
+            and x2d.dim() == 2 and x2d.shape[0] % 256 == 0 and x2d.shape[0] > 0 and x2d.shape[1] % 64 == 0
+            and x2d.stride(1) == 1 and x2d.stride(0) % 8 == 0 and w.is_contiguous() and w.shape[0] % 256 == 0)
+
+
+class GateUpSwiGLUFn(Function):
+    """act = silu(x Wg^T) * (x Wu^T) with W = [Wg; Wu]: ONE HIP GEMM whose epilogue writes both gu (saved
+    for backward) and act — the separate SwiGLU pass over the [M, 2I] output disappears."""
+
+    @staticmethod
+    def forward(ctx, x, weight):
+        x2d = x.reshape(-1, x.shape[-1])
+        gu, act = _ext.ops().gemm_tn_swiglu(x2d, weight)
+        ctx.save_for_backward(x2d, gu)
+        ctx.weight = weight
+        ctx.x_shape = x.shape
+        return act.view(*x.shape[:-1], act.shape[-1])
+
+    @staticmethod
+    def backward(ctx, dact):
+        x2d, gu = ctx.saved_tensors
+        w = ctx.weight
+        dgu = _ext.ops().swiglu_bwd(dact.reshape(-1, dact.shape[-1]).contiguous(), gu)
+        dx = dw = None
+        if ctx.needs_input_grad[0]:
+            dx = torch.mm(dgu, w).view(ctx.x_shape)
+        if ctx.needs_input_grad[1]:
+            dw = _accumulate_weight_grad(w, dgu, x2d)
+        return dx, dw
+
+
+def linear_swiglu(x: torch.Tensor, weight: torch.Tensor) -> torch.Tensor:
+    """SwiGLU MLP input projection: swiglu(linear(x, [Wg; Wu]))."""
+    x2d = x.reshape(-1, x.shape[-1])
+    if _TN_MODE in ("1", "swiglu") and _tn_ok(x2d, weight) and (weight.shape[0] // 2) % 128 == 0:
+        return GateUpSwiGLUFn.apply(x, weight)
+    return swiglu(linear(x, weight))
+
+
+class QKVRopeFn(Function):
+    """qkv = x W^T with rotate_half RoPE applied to the q and k heads in the GEMM epilogue."""
+
+    @staticmethod
+    def forward(ctx, x, weight, cos, sin, n_q, n_kv, head_dim):
+        x2d = x.reshape(-1, x.shape[-1])
+        qkv = _ext.ops().gemm_tn_rope(x2d, weight, cos, sin, (n_q + n_kv) * head_dim, 2)
+        ctx.save_for_backward(x2d, cos, sin)
+        ctx.weight = weight
+        ctx.dims = (n_q, n_kv, head_dim)
+        ctx.x_shape = x.shape
+        return qkv
+
+    @staticmethod
+    def backward(ctx, dqkv):
+        x2d, cos, sin = ctx.saved_tensors
+        w = ctx.weight
+        n_q, n_kv, hd = ctx.dims
+        dqkv = dqkv.contiguous()
+        _rope_inplace(dqkv, cos, sin, n_q, n_kv, hd, inverse=True)
+        dx = dw = None
+        if ctx.needs_input_grad[0]:
+            dx = torch.mm(dqkv, w).view(ctx.x_shape)
+        if ctx.needs_input_grad[1]:
+            dw = _accumulate_weight_grad(w, dqkv, x2d)
+        return dx, dw, None, None, None, None, None
+
+
+def linear_rope(x, weight, cos, sin, n_q, n_kv, head_dim):
+    """rope_(linear(x, W_qkv)) on the packed [M, (n_q + 2 n_kv) * head_dim] layout."""
+    x2d = x.reshape(-1, x.shape[-1])
+    if (_TN_MODE in ("1", "rope") and head_dim == 128 and _tn_ok(x2d, weight) and cos.dtype == torch.float32
+            and cos.is_contiguous()
+            and sin.is_contiguous() and cos.shape == (x2d.shape[0], 64)):
+        return QKVRopeFn.apply(x, weight, cos, sin, n_q, n_kv, head_dim)
+    return rope_(linear(x, weight), cos, sin, n_q, n_kv, head_dim)
+
+
 # ----------------------------------------------------------------------------- RoPE (in place on packed qkv)
 class RoPEFn(Function):
     @staticmethod

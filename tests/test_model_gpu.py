@@ -40,6 +40,47 @@ def test_model_hip_vs_reference(mt):
         assert e < 5e-2, (n, e.item())
 
 
+@pytest.mark.parametrize("mt", ["smollm3", "llama"])
+def test_model_fused_gemm_epilogues(mt, monkeypatch):
+    """M = 1024 tokens (multiple of 256): qkv+RoPE and gate_up+SwiGLU run as single HIP GEMMs with fused
+    epilogues (csrc/gemm_tn.hip); loss and every gradient match the unfused HIP path (hipBLASLt + kernels)
+    and the PyTorch reference."""
+    import llm_fine_tune_distributed_amd.ops.fused as F
+    torch.manual_seed(0)
+    cfg = tiny(mt, hidden_size=512, num_attention_heads=4, num_key_value_heads=2, head_dim=128,
+               intermediate_size=1024, vocab_size=1024, num_hidden_layers=4)
+    m = build_model(cfg, device="cuda", dtype=torch.bfloat16, seed=1)
+    ids = torch.randint(0, 1024, (4, 256), device="cuda")
+    labels = ids.clone()
+    labels[:, 200:] = -100
+    calls = {"swiglu": 0, "rope": 0}
+    orig_sw, orig_rope = F.GateUpSwiGLUFn.apply, F.QKVRopeFn.apply
+
+    def sw(*a):
+        calls["swiglu"] += 1
+        return orig_sw(*a)
+
+    def rp(*a):
+        calls["rope"] += 1
+        return orig_rope(*a)
+
+    monkeypatch.setattr(F.GateUpSwiGLUFn, "apply", sw)
+    monkeypatch.setattr(F.QKVRopeFn, "apply", rp)
+    monkeypatch.setattr(F, "_TN_MODE", "1")
+    l_f, g_f = _run(m, ids, labels, True)
+    assert calls["swiglu"] == 4 and calls["rope"] == (3 if mt == "smollm3" else 4)  # NoPE layer 3
+    monkeypatch.setattr(F, "_TN_MODE", "0")
+    l_u, g_u = _run(m, ids, labels, True)
+    l_r, g_r = _run(m, ids, labels, False)
+    assert abs(l_f.item() - l_u.item()) < 5e-3 * abs(l_u.item())
+    assert abs(l_f.item() - l_r.item()) < 2e-2 * abs(l_r.item())
+    for n in g_u:
+        e = (g_f[n] - g_u[n]).norm() / (g_u[n].norm() + 1e-12)
+        assert e < 2e-2, (n, e.item())
+        e = (g_f[n] - g_r[n]).norm() / (g_r[n].norm() + 1e-12)
+        assert e < 5e-2, (n, e.item())
+
+
 def test_lora_wide_gpu_matches_unfused():
     from llm_fine_tune_distributed_amd.models.lora import LoRAConfig, apply_lora
     import llm_fine_tune_distributed_amd.models.transformer as T

@@ -1,0 +1,104 @@
+"""Micro-benchmark of the forward-layout HIP GEMM (csrc/gemm_tn.hip) against hipBLASLt/rocBLAS
+(torch linear through TunableOp with the shipped MI355X selections), at the SmolLM3-3B training
+shapes (M = 16 x 512 tokens). Fused variants are timed against their unfused twins
+(BLAS GEMM + the separate SwiGLU / RoPE kernel). Interleaved in one process (CDNA guide rule 24).
+
+    python tools/bench_gemm_tn.py [--m 8192]
+"""
+import argparse
+import os
+import statistics
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import torch  # noqa: E402
+
+from llm_fine_tune_distributed_amd.ops import _ext  # noqa: E402
+from llm_fine_tune_distributed_amd.utils.gemm_tuning import enable_tuned_gemms  # noqa: E402
+
+ap = argparse.ArgumentParser()
+ap.add_argument("--m", type=int, default=8192)
+ap.add_argument("--iters", type=int, default=20)
+a = ap.parse_args()
+assert _ext.load(), _ext.load_error()
+enable_tuned_gemms()
+ops = _ext.ops()
+M = a.m
+torch.manual_seed(0)
+
+
+def timeit(fn, n=a.iters):
+    for _ in range(3):
+        fn()
+    ts = []
+    for _ in range(n):
+        s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        s.record()
+        fn()
+        e.record()
+        torch.cuda.synchronize()
+        ts.append(s.elapsed_time(e))
+    return statistics.median(ts)
+
+
+def rel(a_, b_):
+    return ((a_.float() - b_.float()).norm() / b_.float().norm()).item()
+
+
+print(f"M = {M}")
+print("| shape | N | K | blas ms (TF/s) | tn 256x256 BK32 | tn 256x128 BK32 | tn 256x256 BK64 | BK64 early | max rel err |")
+print("|---|---:|---:|---:|---:|---:|---:|---:|---:|")
+for name, N, K in [("qkv", 3072, 2048), ("o", 2048, 2048), ("gate_up", 22016, 2048), ("down", 2048, 11008),
+                   ("lm_head", 128256, 2048)]:
+    x = torch.randn(M, K, device="cuda", dtype=torch.bfloat16)
+    w = torch.randn(N, K, device="cuda", dtype=torch.bfloat16) * 0.02
+    fl = 2.0 * M * N * K
+    ref = torch.nn.functional.linear(x, w)
+    row = [name, str(N), str(K)]
+    t = timeit(lambda: torch.nn.functional.linear(x, w))
+    row.append(f"{t:.3f} ({fl / t / 1e9:.0f})")
+    err = 0.0
+    for cfg in (0, 1, 2, 3):
+        c = ops.gemm_tn(x, w, cfg)
+        err = max(err, rel(c, ref))
+        t = timeit(lambda: ops.gemm_tn(x, w, cfg))
+        row.append(f"{t:.3f} ({fl / t / 1e9:.0f})")
+    row.append(f"{err:.4f}")
+    print("| " + " | ".join(row) + " |", flush=True)
+    del x, w, ref
+
+# fused epilogues vs unfused twins
+K, I = 2048, 11008
+x = torch.randn(M, K, device="cuda", dtype=torch.bfloat16)
+wgu = torch.randn(2 * I, K, device="cuda", dtype=torch.bfloat16) * 0.02
+gu_ref = torch.nn.functional.linear(x, wgu)
+act_ref = ops.swiglu_fwd(gu_ref)
+gu, act = ops.gemm_tn_swiglu(x, wgu)
+print(f"\nswiglu fused: gu rel err {rel(gu, gu_ref):.4f}, act rel err {rel(act, act_ref):.4f}")
+t0 = timeit(lambda: ops.swiglu_fwd(torch.nn.functional.linear(x, wgu)))
+t1 = timeit(lambda: ops.gemm_tn_swiglu(x, wgu))
+print(f"gate_up + SwiGLU: blas + kernel {t0:.3f} ms, fused {t1:.3f} ms ({(t0 - t1) * 1e3:.0f} us saved per layer)")
+
+nq, nkv, D = 16, 4, 128
+wq = torch.randn((nq + 2 * nkv) * D, K, device="cuda", dtype=torch.bfloat16) * 0.02
+pos = torch.arange(512, device="cuda").repeat(M // 512).float()
+inv = 1.0 / (2e6 ** (torch.arange(0, D, 2, device="cuda").float() / D))
+fr = pos[:, None] * inv[None, :]
+cs, sn = fr.cos().contiguous(), fr.sin().contiguous()
+
+
+def unfused():
+    q = torch.nn.functional.linear(x, wq)
+    ops.rope_(q, cs, sn, nq, nkv, D, False)
+    return q
+
+
+qr = unfused()
+for cfg in (0, 1, 2):
+    qf = ops.gemm_tn_rope(x, wq, cs, sn, (nq + nkv) * D, cfg)
+    print(f"rope fused cfg{cfg}: rel err {rel(qf, qr):.4f}")
+t0 = timeit(unfused)
+t1 = timeit(lambda: ops.gemm_tn_rope(x, wq, cs, sn, (nq + nkv) * D, 0))
+t2 = timeit(lambda: ops.gemm_tn_rope(x, wq, cs, sn, (nq + nkv) * D, 1))
+t3 = timeit(lambda: ops.gemm_tn_rope(x, wq, cs, sn, (nq + nkv) * D, 2))
+print(f"qkv + RoPE: blas + kernel {t0:.3f} ms, fused 256x256 {t1:.3f} ms, fused 256x128 {t2:.3f} ms, fused BK64 {t3:.3f} ms")
