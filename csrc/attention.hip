@@ -34,7 +34,14 @@ constexpr int ROWB = D * 2;  // bytes per LDS image row
 constexpr float LOG2E = 1.4426950408889634f;
 constexpr float LN2 = 0.6931471805599453f;
 
-__device__ __forceinline__ int swz(int row, int ch) { return ch ^ (((row & 3) << 2) | ((row >> 2) & 3)); }
+// 16-byte chunk swizzle of the [rows][128] bf16 images (256-B rows = one LDS bank row):
+// ch ^ ((row & 3) << 2 | S((row >> 2) & 3)), S = {0, 2, 3, 1}. Checked exhaustively (tools/lds_swizzle_check.py)
+// against the MI355X lane groups: conflict-free for the 16-B row reads (ds_read_b128 groups
+// {0-3,12-15,20-27}, {4-11,16-19,28-31}, ...) AND for the transposed ds_read_b64_tr_b16 reads (2 x 32 lanes);
+// the previous S(q) = q was 2-way on both.
+__device__ __forceinline__ int swz(int row, int ch) {
+  return ch ^ (((row & 3) << 2) | ((0x78 >> (2 * ((row >> 2) & 3))) & 3));
+}
 __device__ __forceinline__ int img_off(int row, int ch) { return row * ROWB + 16 * swz(row, ch); }
 
 __device__ __forceinline__ f32x4 mfma(const bf16x8& a, const bf16x8& b, const f32x4& c) {

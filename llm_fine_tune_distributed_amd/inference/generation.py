@@ -101,6 +101,39 @@ def sample_next(logits: torch.Tensor, history: torch.Tensor, temperature: float 
     return int(torch.multinomial(p, 1, generator=generator))
 
 
+class DeviceSampler:
+    """GPU-resident sampling state of one sequence for the fused HIP sampler (csrc/sampler.hip): the
+    history as a presence bitmask (repetition penalty is a set operation), a step counter that keys the
+    counter-based RNG, the running position / KV length, and a device log of the generated tokens."""
+
+    def __init__(self, vocab_size: int, device, history_ids, max_new_tokens: int, seed: Optional[int],
+                 temperature: float, top_k: int, top_p: Optional[float], repetition_penalty: float, do_sample: bool):
+        import numpy as np
+        words = np.zeros((vocab_size + 31) // 32, dtype=np.uint32)
+        ids = np.asarray(list(history_ids), dtype=np.int64)
+        np.bitwise_or.at(words, ids >> 5, (np.uint32(1) << (ids & 31).astype(np.uint32)))
+        self.presence = torch.from_numpy(words.view(np.int32).copy()).to(device)
+        self.state = torch.zeros(4, dtype=torch.long, device=device)
+        self.log = torch.full((max(1, max_new_tokens),), -1, dtype=torch.long, device=device)
+        self.params = (float(temperature), int(top_k) if do_sample else 1, float(top_p if top_p is not None else 1.0),
+                       float(repetition_penalty or 1.0), bool(do_sample),
+                       int(seed if seed is not None else torch.randint(0, 2 ** 31 - 1, (1,)).item()))
+
+    @staticmethod
+    def supported(top_k: int, do_sample: bool) -> bool:
+        return (not do_sample) or (top_k is not None and 1 <= top_k <= 64)
+
+    def sample(self, logits: torch.Tensor, tok_out=None, pos_out=None, len_out=None) -> None:
+        t, k, p, rp, ds, seed = self.params
+        ops_ext().sample_token(logits.contiguous(), self.presence, self.state, tok_out, pos_out, len_out, self.log,
+                               t, k, p, rp, ds, seed)
+
+
+def ops_ext():
+    from ..ops import _ext
+    return _ext.ops()
+
+
 class GraphDecoder:
     """Static-shape decode step over a KVCache, captured once into a hipGraph (GPU)."""
 
@@ -139,6 +172,34 @@ class GraphDecoder:
         h, _ = ops.add_rms_norm(x, residual, n.weight, cfg.rms_norm_eps)
         return torch.nn.functional.linear(h, m.lm_head_weight).float()[0]
 
+    def run_sampled(self, sampler: DeviceSampler, n: int, use_graph: bool = True) -> None:
+        """n decode steps entirely on the device: each step runs the model on self.tok at self.pos and the
+        fused sampler writes the next token / position / KV length back into the step's inputs (one
+        hipGraph holds both, so consecutive replays need no host involvement)."""
+        def body():
+            logits = self._step()
+            sampler.sample(logits, self.tok, self.pos, self.len)
+        if not use_graph:
+            for _ in range(n):
+                body()
+            return
+        if self.graph is None:
+            # warm up on copies of the counters so the real sequence state is untouched
+            saved = [t.clone() for t in (self.tok, self.pos, self.len, sampler.state, sampler.presence, sampler.log)]
+            s = torch.cuda.Stream()
+            s.wait_stream(torch.cuda.current_stream())
+            with torch.cuda.stream(s):
+                for _ in range(2):
+                    body()
+            torch.cuda.current_stream().wait_stream(s)
+            for t, v in zip((self.tok, self.pos, self.len, sampler.state, sampler.presence, sampler.log), saved):
+                t.copy_(v)
+            self.graph = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(self.graph):
+                body()
+        for _ in range(n):
+            self.graph.replay()
+
     def step(self, token: int, position: int, use_graph: bool = True) -> torch.Tensor:
         self.tok.fill_(token)
         self.pos.fill_(position)
@@ -162,7 +223,8 @@ class GraphDecoder:
 @torch.no_grad()
 def generate(model, prompt_ids: List[int], max_new_tokens: int = 256, eos_token_id: Optional[int] = None,
              temperature: float = 0.6, top_k: int = 40, top_p: float = 0.95, repetition_penalty: float = 1.1,
-             do_sample: bool = True, seed: Optional[int] = None, use_graph: Optional[bool] = None) -> List[int]:
+             do_sample: bool = True, seed: Optional[int] = None, use_graph: Optional[bool] = None,
+             device_sampling: Optional[bool] = None) -> List[int]:
     model.eval()
     dev = model.model.embed_tokens.device
     cache = KVCache(model.config, len(prompt_ids) + max_new_tokens + 1, dev, model.model.embed_tokens.dtype)
@@ -172,6 +234,11 @@ def generate(model, prompt_ids: List[int], max_new_tokens: int = 256, eos_token_
     gpu_path = dev.type == "cuda" and model.config.head_dim == 128 and ops.use_hip(ids)
     dec = GraphDecoder(model, cache) if gpu_path else None
     graph = gpu_path if use_graph is None else (use_graph and gpu_path)
+    if device_sampling is None:
+        device_sampling = DeviceSampler.supported(top_k, do_sample)
+    if gpu_path and max_new_tokens > 0 and device_sampling:
+        return _generate_device(model, dec, cache, prompt_ids, logits, max_new_tokens, eos_token_id, temperature, top_k,
+                                top_p, repetition_penalty, do_sample, seed, graph)
     hist = ids.clone()
     out: List[int] = []
     for _ in range(max_new_tokens):
@@ -186,4 +253,31 @@ def generate(model, prompt_ids: List[int], max_new_tokens: int = 256, eos_token_
             cache.len += 1
         else:
             logits = forward_cached(model, nt, cache, prefill=False)
+    return out
+
+
+def _generate_device(model, dec: GraphDecoder, cache: KVCache, prompt_ids, logits, max_new_tokens, eos_token_id,
+                     temperature, top_k, top_p, repetition_penalty, do_sample, seed, use_graph, check_every: int = 16):
+    """Decode loop with sampling on the device (fused HIP sampler inside the decode hipGraph). The host
+    only reads the token log every ``check_every`` steps to stop at EOS."""
+    dev = model.model.embed_tokens.device
+    sm = DeviceSampler(model.config.vocab_size, dev, prompt_ids, max_new_tokens, seed, temperature, top_k, top_p,
+                       repetition_penalty, do_sample)
+    sm.state[2] = cache.len - 1  # the first sampled token gets position len(prompt)
+    sm.sample(logits, dec.tok, dec.pos, dec.len)  # token 1 from the prefill logits
+    done = 1
+    out: List[int] = []
+    while True:
+        if eos_token_id is not None or done >= max_new_tokens:
+            toks = sm.log[:done].tolist()
+            if eos_token_id is not None and eos_token_id in toks:
+                out = toks[:toks.index(eos_token_id) + 1]
+                break
+            if done >= max_new_tokens:
+                out = toks
+                break
+        n = min(check_every, max_new_tokens - done)
+        dec.run_sampled(sm, n, use_graph=use_graph)
+        done += n
+    cache.len = len(prompt_ids) + len(out)
     return out
