@@ -9,7 +9,8 @@ bucket all-reduce overlapped with backward, grad-norm clip and fused AdamW (fp32
 Data: synthetic token sequences of ``--seq`` tokens (the reference's samples are ~420-525
 tokens), random-init weights of the SmolLM3-3B architecture (no network).
 
-Weak scaling: per-GPU work is fixed (micro-batch x GA), global batch = 16 x N.
+Weak scaling: per-GPU work is fixed (micro-batch x GA), global batch = 16 x N. With N > 1 the optimizer
+state is sharded ZeRO-1 style by default (``--zero 0`` = replicated all-reduce DDP).
 
     python bench.py [--gpus N] [--steps K] [--warmup W]
     python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N
@@ -45,6 +46,9 @@ def main():
     ap.add_argument("--master-weights", action="store_true", help="fp32 master copy (default: bf16 params + SR)")
     ap.add_argument("--optim-state", default=os.environ.get("SFTAMD_OPTIM_STATE", "fp32"), choices=["fp32", "bf16"],
                     help="Adam moment dtype (bf16 = torch AdamW's state dtype for the reference's bf16 params)")
+    ap.add_argument("--zero", type=int, default=int(os.environ.get("SFTAMD_ZERO", "1")), choices=[0, 1],
+                    help="1 (default): ZeRO-1 over the DDP buckets when N > 1 (reduce-scatter grads, 1/N of AdamW "
+                         "per rank, all-gather params under the next forward); 0: replicated all-reduce DDP")
     ap.add_argument("--tunableop", default=os.environ.get("SFTAMD_TUNABLEOP", "auto"),
                     help="auto: load the committed GEMM selections; tune: tune missing shapes into it; off")
     ap.add_argument("--profile-steps", type=int, default=0)
@@ -73,7 +77,8 @@ def main():
                      bf16=True, gradient_checkpointing=False, max_length=a.seq, packing=a.packing,
                      ddp_bucket_cap_mb=a.bucket_mb, dataloader_drop_last=True, jsonl_log=False, logging_steps=0,
                      optimizer_overlap=not a.no_overlap, freeze_policy=a.freeze_policy,
-                     master_weights=a.master_weights, optim_state_dtype=a.optim_state)
+                     master_weights=a.master_weights, optim_state_dtype=a.optim_state,
+                     shard_optimizer_state=bool(a.zero))
     trainer = SFTTrainer(model=model, args=args, train_dataset=ds)
     loader = trainer.get_train_dataloader()
     it = iter(loader)
@@ -120,6 +125,7 @@ def main():
                        "parallelism": f"dp{st.world_size}", "optimizer": ("AdamW fp32-master (fused HIP)" if a.master_weights else
                                      f"AdamW bf16 params + stochastic rounding, {a.optim_state} moments (fused HIP)"),
                        "samples_per_device_per_step": a.micro_batch * a.ga,
+                       "optimizer_sharding": "zero1" if (a.zero and st.world_size > 1) else "none",
                        "gradient_checkpointing": False, "packing": a.packing},
             "tokens_per_sec": round(tok_s, 1), "mfu": None if mfu is None else round(mfu, 4), "final_loss": round(loss, 4),
             "peak_mem_gb": round(torch.cuda.max_memory_allocated() / 1e9, 2),

@@ -15,6 +15,17 @@ from . import _ext
 from . import reference as ref
 
 
+def sumsq_list(tensors) -> torch.Tensor:
+    """fp32 sum of squares over a list of (bf16) tensors: one HIP partial-sum kernel per tensor, one
+    concatenated reduction (ZeRO-1 grad norm over the owned gradient slices)."""
+    tensors = [t for t in tensors if t.numel() > 0]
+    if not tensors:
+        return torch.zeros((), dtype=torch.float32)
+    if _ext.use_hip(tensors[0]):
+        return torch.cat([_ext.ops().sumsq(t) for t in tensors]).sum()
+    return sum(t.float().pow(2).sum() for t in tensors)
+
+
 def grad_norm_flat(grads: Iterable[torch.Tensor], max_norm: float):
     """Returns (total_norm, clip_coef) as fp32 [1] tensors on the grads' device."""
     grads = [g for g in grads if g.numel() > 0]

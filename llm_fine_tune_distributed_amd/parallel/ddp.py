@@ -18,7 +18,12 @@ that maps to MI355X + RCCL over xGMI:
 * gradient accumulation = ``no_sync`` on all but the last micro-batch: no communication at all
   (one all-reduce round per optimizer step, the reference's GA semantics, lib trainer.py:1749);
 * all ranks build identical weights from the same seed / checkpoint, so the 6 GB rank-0
-  broadcast of the reference's DDP constructor (C3) is skipped unless asked for.
+  broadcast of the reference's DDP constructor (C3) is skipped unless asked for;
+* ``shard=True`` (ZeRO-1, train/optim.py ``ShardedAdamW``): a completed bucket is REDUCE-SCATTERED
+  in place (each rank receives the summed slice it owns — half the bytes of an all-reduce on the
+  backward critical path), each rank updates only its slice, and the updated parameter slices are
+  ALL-GATHERED back bucket by bucket under the next forward. The bucket padding below makes every
+  slice an equal, 128-byte-aligned 1/world_size of its bucket.
 
 Bucket sizing for xGMI: each GPU has 7 point-to-point links; RCCL rings stripe a message over
 its channels, so per-call latency (tens of microseconds) dominates small buckets while very
@@ -55,11 +60,12 @@ class DDPEngine:
     def __init__(self, model: torch.nn.Module, world_size: int = 1, rank: int = 0,
                  bucket_cap_mb: float = 50.0, first_bucket_mb: float = 4.0, grad_dtype: Optional[torch.dtype] = None,
                  broadcast_params: bool = False, align: int = 64, process_group=None,
-                 no_decay_fn: Callable[[str, torch.Tensor], bool] = _no_decay):
+                 no_decay_fn: Callable[[str, torch.Tensor], bool] = _no_decay, shard: bool = False):
         self.model = model
         self.world_size = world_size
         self.rank = rank
         self.pg = process_group
+        self.shard = shard
         self.sync_grads = True
         named = []
         seen = set()
@@ -218,8 +224,33 @@ class DDPEngine:
 
     def _launch(self, b: Bucket):
         view = self.grad_flat[b.start:b.end]
-        b.work = dist.all_reduce(view, op=dist.ReduceOp.SUM, group=self.pg, async_op=True)
+        if self.shard:
+            s, e = self.shard_range(b)
+            # in place: this rank's slice of the bucket receives the sum of every rank's slice
+            b.work = dist.reduce_scatter_tensor(self.grad_flat[s:e], view, op=dist.ReduceOp.SUM, group=self.pg,
+                                                async_op=True)
+        else:
+            b.work = dist.all_reduce(view, op=dist.ReduceOp.SUM, group=self.pg, async_op=True)
         b.launched = True
+
+    # ------------------------------------------------------------------ ZeRO-1 slices
+    def shard_range(self, b: Bucket):
+        """[start, end) of the slice of bucket ``b`` this rank owns (the whole bucket unless sharded)."""
+        if not self.shard or self.world_size == 1:
+            return b.start, b.end
+        n = (b.end - b.start) // self.world_size
+        return b.start + self.rank * n, b.start + (self.rank + 1) * n
+
+    def owned_ranges(self):
+        return [self.shard_range(b) for b in self.buckets]
+
+    def gather_params(self, b: Bucket, async_op: bool = True):
+        """All-gather the updated parameter slices of bucket ``b`` (in place) — ZeRO-1 only."""
+        if not self.shard or self.world_size == 1:
+            return None
+        s, e = self.shard_range(b)
+        return dist.all_gather_into_tensor(self.param_flat[b.start:b.end], self.param_flat[s:e], group=self.pg,
+                                           async_op=async_op)
 
     def finish_backward(self):
         """Wait for all bucket all-reduces (launching any bucket whose params had no grad)."""

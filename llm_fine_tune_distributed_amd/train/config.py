@@ -89,6 +89,9 @@ class SFTConfig:
     # Adam moment storage: "fp32" (default) or "bf16" (torch AdamW's state dtype for the
     # reference's bf16 params; stochastic-rounded, 14 instead of 22 HBM bytes/param per step)
     optim_state_dtype: str = "fp32"
+    # ZeRO-1 over the DDP buckets (world_size > 1): reduce-scatter gradients, update 1/world_size of the
+    # parameters per rank, all-gather them back under the next forward (train/optim.py ShardedAdamW)
+    shard_optimizer_state: bool = False
     ddp_first_bucket_mb: float = 4.0
     ddp_broadcast_params: bool = False      # weights are identical by construction (seeded / loaded)
     ddp_check_sync_every: int = 0           # cross-rank param checksum every N steps (0 = off)

@@ -172,6 +172,166 @@ class FlatAdamW:
                 self.master.copy_(self.engine.param_flat.float())
 
 
+class ShardedAdamW(FlatAdamW):
+    """ZeRO-1 AdamW over the DDP engine's flat buffers (engine built with ``shard=True``).
+
+    Each rank owns 1/world_size of every gradient bucket: the engine reduce-scatters a bucket the moment
+    it completes in backward (half the bytes of the all-reduce on the backward critical path), this
+    optimizer updates only the owned slices — moments and master copy exist for those slices only, so
+    optimizer HBM traffic and memory shrink by world_size — and the updated parameter slices are
+    all-gathered back, bucket by bucket in FORWARD order (embedding first), on the collective stream
+    while the next forward runs: a layer's forward pre-hook waits only for its own buckets.
+    The update itself is the same fused HIP kernel, with the stochastic-rounding stream keyed by the
+    GLOBAL element index, so a sharded run rounds exactly like the replicated one.
+    Checkpoints hold the full (gathered) state, interchangeable with ``FlatAdamW``'s."""
+
+    def __init__(self, engine, lr: float, betas=(0.9, 0.999), eps: float = 1e-8, weight_decay: float = 0.0,
+                 master_weights: bool = True, stochastic_rounding: bool = True, state_dtype=torch.float32):
+        if not engine.shard:
+            raise ValueError("ShardedAdamW needs a DDPEngine built with shard=True")
+        self.engine = engine
+        self.lr = lr
+        self.betas = betas
+        self.eps = eps
+        self.weight_decay = weight_decay
+        self.master_weights = master_weights
+        self.stochastic_rounding = stochastic_rounding and not master_weights
+        self.step_count = 0
+        if isinstance(state_dtype, str):
+            state_dtype = {"fp32": torch.float32, "float32": torch.float32, "bf16": torch.bfloat16,
+                           "bfloat16": torch.bfloat16}[state_dtype]
+        self.state_dtype = state_dtype
+        e = engine
+        # owned slice of every bucket -> offset in the local (sharded) state buffers
+        self.slices = []  # (bucket, start, end, local_offset, decay)
+        off = 0
+        for b in e.buckets:
+            s, t = e.shard_range(b)
+            decay = next(d for rs, rt, d in e.regions if rs <= b.start < rt)
+            self.slices.append((b, s, t, off, decay))
+            off += t - s
+        self.local_numel = off
+        dev = e.device
+        self.exp_avg = torch.zeros(off, dtype=state_dtype, device=dev)
+        self.exp_avg_sq = torch.zeros(off, dtype=state_dtype, device=dev)
+        self.master = None
+        if master_weights:
+            self.master = torch.empty(off, dtype=torch.float32, device=dev)
+            for _, s, t, lo, _ in self.slices:
+                self.master[lo:lo + t - s].copy_(e.param_flat[s:t].float())
+        self.last_grad_norm = None
+        self.overlap = False
+        self._ag = {}
+        self._pending = False
+
+    # ------------------------------------------------------------------ gather under the next forward
+    def enable_overlap(self, model) -> bool:
+        """Forward pre-hooks wait for the all-gathers of the buckets holding each module's parameters."""
+        e = self.engine
+        inner = model.model
+
+        def buckets_of(params):
+            out = []
+            for p in params:
+                b = e.param_bucket.get(id(p))
+                if b is not None and b.index not in out:
+                    out.append(b.index)
+            return out
+
+        groups = [buckets_of([inner.embed_tokens])]
+        for layer in inner.layers:
+            groups.append(buckets_of(list(layer.parameters())))
+        head = list(inner.norm.parameters()) + ([model.lm_head] if model.lm_head is not None else [])
+        groups.append(buckets_of(head))
+        self._wait_groups = groups
+
+        def waiter(i):
+            def hook(*_a, **_k):
+                if self._pending:
+                    for bi in self._wait_groups[i]:
+                        w = self._ag.pop(bi, None)
+                        if w is not None:
+                            w.wait()
+            return hook
+
+        self._hooks = [model.register_forward_pre_hook(waiter(0))]
+        for i, layer in enumerate(inner.layers):
+            self._hooks.append(layer.register_forward_pre_hook(waiter(i + 1)))
+        self._hooks.append(inner.layers[-1].register_forward_hook(waiter(len(groups) - 1)))
+        self.overlap = True
+        return True
+
+    def synchronize(self):
+        if self._ag:
+            for w in self._ag.values():
+                if w is not None:
+                    w.wait()
+            self._ag = {}
+        self._pending = False
+
+    @torch.no_grad()
+    def step(self, lr: Optional[float] = None, max_grad_norm: Optional[float] = None):
+        import torch.distributed as dist
+        lr = self.lr if lr is None else lr
+        self.step_count += 1
+        e = self.engine
+        self.synchronize()
+        # global grad norm: sum of squares of the owned (reduced) slices, all-reduced (one float)
+        owned = [e.grad_flat[s:t] for _, s, t, _, _ in self.slices if t > s]
+        norm2 = ops.sumsq_list(owned).reshape(1)
+        if e.world_size > 1:
+            dist.all_reduce(norm2, op=dist.ReduceOp.SUM, group=e.pg)
+        norm = norm2.sqrt()
+        coef = (max_grad_norm / (norm + 1e-6)).clamp(max=1.0) if max_grad_norm else torch.ones_like(norm)
+        self.last_grad_norm = norm
+        b1, b2 = self.betas
+        seed = (0x5EED + 7919 * self.step_count) & 0x7FFFFFFF if self.stochastic_rounding else 0
+        # forward order (the embedding's bucket is the LAST one in backward-ready layout): each bucket's
+        # gather is issued right after its update, so the first layers' parameters come back first
+        for b, s, t, lo, decay in reversed(self.slices):
+            n = t - s
+            if n:
+                ops.adamw_flat_(e.param_flat[s:t], e.grad_flat[s:t], None if self.master is None else self.master[lo:lo + n],
+                                self.exp_avg[lo:lo + n], self.exp_avg_sq[lo:lo + n], coef, lr, b1, b2, self.eps,
+                                self.weight_decay if decay else 0.0, self.step_count, sr_seed=seed, sr_offset=s)
+            w = e.gather_params(b, async_op=True)
+            if w is not None:
+                self._ag[b.index] = w
+        self._pending = bool(self._ag)
+        if not self.overlap:
+            self.synchronize()
+        return norm
+
+    # ------------------------------------------------------------------ checkpoints: full (gathered) state
+    def _gather_full(self, local: torch.Tensor, dtype) -> torch.Tensor:
+        import torch.distributed as dist
+        e = self.engine
+        full = torch.zeros(e.numel, dtype=dtype, device=e.device)
+        for b, s, t, lo, _ in self.slices:
+            full[s:t].copy_(local[lo:lo + t - s])
+            if e.world_size > 1:
+                dist.all_gather_into_tensor(full[b.start:b.end], full[s:t], group=e.pg)
+        return full
+
+    def state_dict(self) -> Dict:
+        self.synchronize()
+        return {"step": self.step_count, "exp_avg": self._gather_full(self.exp_avg, self.state_dtype),
+                "exp_avg_sq": self._gather_full(self.exp_avg_sq, self.state_dtype),
+                "master": None if self.master is None else self._gather_full(self.master, torch.float32),
+                "lr": self.lr, "betas": self.betas, "eps": self.eps, "weight_decay": self.weight_decay}
+
+    def load_state_dict(self, sd: Dict):
+        e = self.engine
+        self.step_count = int(sd["step"])
+        for _, s, t, lo, _ in self.slices:
+            n = t - s
+            self.exp_avg[lo:lo + n].copy_(sd["exp_avg"][s:t])
+            self.exp_avg_sq[lo:lo + n].copy_(sd["exp_avg_sq"][s:t])
+            if self.master is not None:
+                src = sd.get("master")
+                self.master[lo:lo + n].copy_(src[s:t] if src is not None else e.param_flat[s:t].float())
+
+
 def get_schedule(name: str, num_training_steps: int, num_warmup_steps: int = 0, **kw) -> Callable[[int], float]:
     """LR multiplier as a function of the optimizer step (HF transformers semantics)."""
     name = (name or "linear").lower()

@@ -41,7 +41,7 @@ from . import checkpoint as ckpt
 from .callbacks import (AimCallback, CallbackHandler, JSONLLoggerCallback, PrinterCallback, TrainerCallback,
                         TrainerControl, TrainerState)
 from .config import SFTConfig
-from .optim import FlatAdamW, LRScheduler, get_schedule
+from .optim import FlatAdamW, LRScheduler, ShardedAdamW, get_schedule
 from ..utils.faults import maybe_inject
 
 PEAK_BF16_FLOPS = 2.5e15  # MI355X dense bf16 (vendor figure; AMD's 5 PF headline includes 2:1 sparsity)
@@ -105,11 +105,13 @@ class SFTTrainer:
                                                      args.per_device_train_batch_size * (args.max_length or 1024)
                                                      if args.packing else None)
         # ------------------------------------------------------------ engine + optimizer
+        shard = bool(args.shard_optimizer_state) and self.dist.world_size > 1
         self.engine = DDPEngine(model, self.dist.world_size, self.dist.rank,
                                 bucket_cap_mb=args.ddp_bucket_cap_mb or 25.0,
                                 first_bucket_mb=args.ddp_first_bucket_mb,
-                                broadcast_params=args.ddp_broadcast_params)
-        self.optimizer = FlatAdamW(self.engine, lr=args.learning_rate, betas=(args.adam_beta1, args.adam_beta2),
+                                broadcast_params=args.ddp_broadcast_params, shard=shard)
+        opt_cls = ShardedAdamW if shard else FlatAdamW
+        self.optimizer = opt_cls(self.engine, lr=args.learning_rate, betas=(args.adam_beta1, args.adam_beta2),
                                    eps=args.adam_epsilon, weight_decay=args.weight_decay,
                                    master_weights=args.master_weights,
                                    stochastic_rounding=args.stochastic_rounding,
@@ -371,6 +373,7 @@ class SFTTrainer:
                     run_acc.zero_()
                     steps_since_log = 0
                 if a.ddp_check_sync_every and gs % a.ddp_check_sync_every == 0:
+                    self.optimizer.synchronize()  # pending (overlapped) updates / gathers land first
                     self.engine.assert_in_sync()
                 metrics = None
                 if eval_every and eval_every > 0 and gs % eval_every == 0 and self.eval_dataset is not None:

@@ -17,7 +17,7 @@ def _free_port():
     return p
 
 
-def _run(rank, world, port, out_dir, per_dev, ga, steps):
+def _run(rank, world, port, out_dir, per_dev, ga, steps, shard=False, tag=""):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), WORLD_SIZE=str(world), RANK=str(rank),
                       LOCAL_RANK=str(rank))
     import llm_fine_tune_distributed_amd.parallel.process_group as pgm
@@ -32,21 +32,23 @@ def _run(rank, world, port, out_dir, per_dev, ga, steps):
     args = SFTConfig(output_dir=out_dir, per_device_train_batch_size=per_dev, gradient_accumulation_steps=ga,
                      learning_rate=1e-3, max_steps=steps, logging_steps=1, dataloader_drop_last=True,
                      jsonl_log=False, ddp_check_sync_every=1, ddp_bucket_cap_mb=0.05, ddp_first_bucket_mb=0.01,
-                     save_strategy="no")
+                     save_strategy="no", shard_optimizer_state=shard)
     t = SFTTrainer(model=m, args=args, train_dataset=ds)
     out = t.train()
+    osd = t.optimizer.state_dict()  # collective in ZeRO-1 mode: every rank takes part
     torch.save({"params": t.engine.param_flat.clone(), "loss": out.training_loss,
-                "log": [h for h in t.state.log_history if "loss" in h]},
-               os.path.join(out_dir, f"r{world}_{rank}.pt"))
+                "log": [h for h in t.state.log_history if "loss" in h], "exp_avg": osd["exp_avg"].clone(),
+                "exp_avg_sq": osd["exp_avg_sq"].clone(), "sharded": type(t.optimizer).__name__},
+               os.path.join(out_dir, f"r{world}_{rank}{tag}.pt"))
     pgm.cleanup_distributed()
 
 
-def _launch(world, per_dev, ga, steps, d):
+def _launch(world, per_dev, ga, steps, d, shard=False, tag=""):
     port = _free_port()
     if world == 1:
-        _run(0, 1, port, d, per_dev, ga, steps)
+        _run(0, 1, port, d, per_dev, ga, steps, shard, tag)
     else:
-        mp.spawn(_run, args=(world, port, d, per_dev, ga, steps), nprocs=world, join=True)
+        mp.spawn(_run, args=(world, port, d, per_dev, ga, steps, shard, tag), nprocs=world, join=True)
 
 
 def test_ddp2_matches_single_process():
@@ -74,3 +76,21 @@ def test_grad_accumulation_equals_big_batch():
     assert torch.allclose(ga["params"], big["params"], atol=1e-5, rtol=1e-4)
     for a, b in zip(big["log"], ga["log"]):
         assert abs(a["loss"] - b["loss"]) < 1e-5
+
+
+def test_zero1_sharded_optimizer_matches_replicated():
+    """ZeRO-1 (reduce-scatter grads, update 1/world of the params per rank, all-gather them back) gives
+    the same parameters, losses, grad norms and (gathered) Adam state as replicated DDP."""
+    d = tempfile.mkdtemp()
+    _launch(2, 2, 2, 3, d)
+    _launch(2, 2, 2, 3, d, shard=True, tag="_z")
+    rep = [torch.load(os.path.join(d, f"r2_{r}.pt")) for r in range(2)]
+    z = [torch.load(os.path.join(d, f"r2_{r}_z.pt")) for r in range(2)]
+    assert z[0]["sharded"] == "ShardedAdamW" and rep[0]["sharded"] == "FlatAdamW"
+    assert torch.equal(z[0]["params"], z[1]["params"])  # all-gathered: ranks identical
+    assert torch.allclose(z[0]["params"], rep[0]["params"], atol=1e-6, rtol=1e-5)
+    for k in ("exp_avg", "exp_avg_sq"):
+        assert torch.allclose(z[0][k], rep[0][k], atol=1e-7, rtol=1e-4)
+    for a, b in zip(rep[0]["log"], z[0]["log"]):
+        assert abs(a["loss"] - b["loss"]) < 1e-5
+        assert abs(a["grad_norm"] - b["grad_norm"]) < 1e-4 * max(1.0, a["grad_norm"])
