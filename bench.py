@@ -5,7 +5,9 @@ Metric and config follow BASELINE.json: "samples/sec SmolLM3-3B full SFT bf16 at
 MI355X; DDP scaling efficiency", reference 4-GPU config = per-device batch 8 x GA 2
 (README.md:69). Every timed step is a complete optimizer step of the real training path
 (``SFTTrainer.optimizer_step``): GA micro-batches of fwd+bwd through the HIP kernels, RCCL
-bucket all-reduce overlapped with backward, grad-norm clip and fused AdamW (fp32 master).
+bucket reduce-scatter (ZeRO-1, default for N > 1) or all-reduce overlapped with backward, grad-norm
+clip, fused AdamW (bf16 params + stochastic rounding, fp32 moments) and, with ZeRO-1, the parameter
+all-gather (finished inside the timed region).
 Data: synthetic token sequences of ``--seq`` tokens (the reference's samples are ~420-525
 tokens), random-init weights of the SmolLM3-3B architecture (no network).
 
