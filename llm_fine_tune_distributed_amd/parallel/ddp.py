@@ -131,6 +131,7 @@ class DDPEngine:
                 p.main_grad = self.grad_flat[o:o + n].view(p.shape)
                 p.grad = None
         self._next = 0
+        self._comm_events = []
         for p, _, _, _ in self.layout:
             p._sftamd_ready_hook = self._on_param_ready
             p.register_post_accumulate_grad_hook(self._post_accumulate)
@@ -262,10 +263,31 @@ class DDPEngine:
         for b in self.buckets[self._next:]:
             self._launch(b)
         self._next = len(self.buckets)
+        timing = self.grad_flat.is_cuda
+        if timing:  # exposed communication = what the compute stream waits for after its last kernel
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
         for b in self.buckets:
             if b.work is not None:
                 b.work.wait()
                 b.work = None
+        if timing:
+            e1.record()
+            self._comm_events.append((e0, e1))
+            if len(self._comm_events) > 64:  # bounded when nobody reads them (e.g. logging off)
+                del self._comm_events[0]
+
+    def comm_exposed_ms(self, reset: bool = True) -> float:
+        """Mean exposed (non-overlapped) gradient-communication time per synchronised backward, in ms,
+        since the last call (reads CUDA events: call at log time, not per step)."""
+        ev = self._comm_events
+        if not ev:
+            return 0.0
+        ev[-1][1].synchronize()
+        v = sum(a.elapsed_time(b) for a, b in ev) / len(ev)
+        if reset:
+            self._comm_events = []
+        return v
 
     # ------------------------------------------------------------------ debug / safety
     @torch.no_grad()

@@ -366,10 +366,15 @@ class SFTTrainer:
                     all_reduce_sum_(red)
                     v = red.tolist()
                     valid = max(v[3], 1.0)
-                    self.log({"loss": v[0] / steps_since_log, "grad_norm": float(last_norm),
-                              "learning_rate": self.scheduler.get_lr(), "epoch": round(self.state.epoch, 4),
-                              "mean_token_accuracy": v[1] / valid, "entropy": v[2] / valid,
-                              "num_tokens": float(self.state.tokens_seen)})
+                    logs = {"loss": v[0] / steps_since_log, "grad_norm": float(last_norm),
+                            "learning_rate": self.scheduler.get_lr(), "epoch": round(self.state.epoch, 4),
+                            "mean_token_accuracy": v[1] / valid, "entropy": v[2] / valid,
+                            "num_tokens": float(self.state.tokens_seen)}
+                    if self.dist.device.type == "cuda":
+                        logs["hbm_peak_gb"] = round(torch.cuda.max_memory_allocated(self.dist.device) / 1e9, 3)
+                        if self.dist.world_size > 1:
+                            logs["comm_exposed_ms"] = round(self.engine.comm_exposed_ms(), 3)
+                    self.log(logs)
                     run_acc.zero_()
                     steps_since_log = 0
                 if a.ddp_check_sync_every and gs % a.ddp_check_sync_every == 0:
