@@ -74,6 +74,38 @@ def _wgrad_mm(out: torch.Tensor, dy2d: torch.Tensor, x2d: torch.Tensor, accumula
         torch.mm(dy2d.t(), x2d, out=out)
 
 
+# Optional (SFTAMD_WGRAD_STREAM=1): weight-gradient GEMMs off the critical path. Backward's dgrad
+# chain (dX of layer L feeds layer L-1) is serial, the weight gradients are not — they can go to a
+# side HIP stream to fill CUs the dgrad GEMMs / attention / norm kernels leave idle. Consumers of
+# main_grad wait for the side stream: the DDP bucket collectives (issued FROM the side stream, so the
+# compute stream never stalls), the end of backward and the tied-embedding backward, which
+# accumulates into the buffer the lm_head wgrad wrote. Measured on MI355X (profiles/r1_gemm_tn.md):
+# 3.5 % SLOWER end to end — two 256x256-tile GEMMs at one workgroup per CU thrash each other's L2
+# and LDS-DMA bandwidth — so it is off by default; the plumbing stays tested (bitwise-equal grads).
+_WGRAD_STREAM_MODE = os.environ.get("SFTAMD_WGRAD_STREAM", "0")
+_wgrad_streams = {}
+
+
+def _wgrad_stream(dev: torch.device):
+    if _WGRAD_STREAM_MODE == "0" or dev.type != "cuda":
+        return None
+    idx = dev.index if dev.index is not None else torch.cuda.current_device()
+    s = _wgrad_streams.get(idx)
+    if s is None:
+        s = _wgrad_streams[idx] = torch.cuda.Stream(device=idx)
+    return s
+
+
+def wgrad_sync(dev: Optional[torch.device] = None) -> None:
+    """Make the current stream wait for every weight-gradient GEMM issued on the side stream."""
+    if not _wgrad_streams:
+        return
+    idx = torch.cuda.current_device() if dev is None or dev.index is None else dev.index
+    s = _wgrad_streams.get(idx)
+    if s is not None:
+        torch.cuda.current_stream(idx).wait_stream(s)
+
+
 def _accumulate_weight_grad(param: torch.Tensor, dy2d: torch.Tensor, x2d: torch.Tensor,
                             scale: Optional[torch.Tensor] = None):
     """dW = dy^T @ x (optionally * scale). Accumulates into main_grad if present."""
@@ -84,7 +116,15 @@ def _accumulate_weight_grad(param: torch.Tensor, dy2d: torch.Tensor, x2d: torch.
         fresh = getattr(param, "_sftamd_fresh", False)
         if mg.dtype == dy2d.dtype:
             # first contribution of the step: beta=0 GEMM, no zero-fill pass needed
-            _wgrad_mm(mg, dy2d, x2d, accumulate=not fresh)
+            ws = _wgrad_stream(dy2d.device)
+            if ws is not None:
+                ws.wait_stream(torch.cuda.current_stream(dy2d.device))
+                with torch.cuda.stream(ws):
+                    _wgrad_mm(mg, dy2d, x2d, accumulate=not fresh)
+                dy2d.record_stream(ws)  # keep the operands alive until the side stream is done
+                x2d.record_stream(ws)
+            else:
+                _wgrad_mm(mg, dy2d, x2d, accumulate=not fresh)
         elif fresh:
             mg.copy_(torch.mm(dy2d.t(), x2d))
         else:
@@ -158,6 +198,7 @@ class EmbeddingFn(Function):
             if mg is not None and getattr(w, "_sftamd_fresh", False):
                 mg.zero_()  # untied embedding: the sparse row update needs a zeroed buffer
                 w._sftamd_fresh = False
+            wgrad_sync(dy2d.device)  # tied weight: the lm_head wgrad (side stream) wrote this buffer first
             _ext.ops().embedding_bwd(dy2d, sorted_ids, perm.to(torch.int32), target)
             if mg is not None:
                 _weight_grad_done(w)

@@ -225,6 +225,22 @@ class DDPEngine:
 
     def _launch(self, b: Bucket):
         view = self.grad_flat[b.start:b.end]
+        ws = None
+        if view.is_cuda:
+            from ..ops.fused import _wgrad_stream
+            ws = _wgrad_stream(view.device)
+        if ws is not None:
+            # the bucket's weight gradients may still be in flight on the side stream: issue the
+            # collective from that stream (after it has also caught up with the compute stream), so
+            # RCCL waits for them without ever stalling the compute stream's dgrad chain
+            ws.wait_stream(torch.cuda.current_stream(view.device))
+            with torch.cuda.stream(ws):
+                self._collective(b, view)
+        else:
+            self._collective(b, view)
+        b.launched = True
+
+    def _collective(self, b: Bucket, view: torch.Tensor):
         if self.shard:
             s, e = self.shard_range(b)
             # in place: this rank's slice of the bucket receives the sum of every rank's slice
@@ -232,7 +248,6 @@ class DDPEngine:
                                                 async_op=True)
         else:
             b.work = dist.all_reduce(view, op=dist.ReduceOp.SUM, group=self.pg, async_op=True)
-        b.launched = True
 
     # ------------------------------------------------------------------ ZeRO-1 slices
     def shard_range(self, b: Bucket):
@@ -255,6 +270,9 @@ class DDPEngine:
 
     def finish_backward(self):
         """Wait for all bucket all-reduces (launching any bucket whose params had no grad)."""
+        if self.grad_flat.is_cuda:
+            from ..ops.fused import wgrad_sync
+            wgrad_sync(self.grad_flat.device)
         if not self.sync_grads:
             return
         self._zero_untouched()
