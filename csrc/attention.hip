@@ -899,7 +899,9 @@ struct Stage {
   }
 };
 
-template <int NW>
+// DIAG (timing-only ablations, wrong results): bit0 no next-tile loads/stores, bit1 no softmax math,
+// bit2 no PV MFMAs, bit3 no QK MFMAs
+template <int NW, int DIAG = 0>
 __global__ __launch_bounds__(NW * 64) void fwd3_kernel(const u16* __restrict__ qkv, u16* __restrict__ out,
                                                        float* __restrict__ lse, const int* __restrict__ cu, int nq,
                                                        int nkv, int total, float sl2, int causal) {
@@ -943,7 +945,7 @@ __global__ __launch_bounds__(NW * 64) void fwd3_kernel(const u16* __restrict__ q
   __syncthreads();
   for (int kt = 0; kt < nkt; ++kt) {
     const int k0 = kt * 64;
-    const bool pre = kt + 1 < nkt;
+    const bool pre = !(DIAG & 1) && kt + 1 < nkt;
     Stage<64, NT> tk, tv;
     if (pre) {
       tk.load(kbase + (long)(k0 + 64) * ld, ld, len - k0 - 64, tid);
@@ -955,8 +957,10 @@ __global__ __launch_bounds__(NW * 64) void fwd3_kernel(const u16* __restrict__ q
       for (int nt = 0; nt < 4; ++nt) {
         sc[nt] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-        for (int s = 0; s < 4; ++s) sc[nt] = mfma(lds_row(Ks, off.row[s] + nt * 16 * ROWB), qf[s], sc[nt]);
+        for (int s = 0; s < 4; ++s)
+          if (!(DIAG & 8)) sc[nt] = mfma(lds_row(Ks, off.row[s] + nt * 16 * ROWB), qf[s], sc[nt]);
       }
+      if constexpr (!(DIAG & 2)) {
       const bool need_mask = (k0 + 64 > len) || (causal && k0 + 63 > wfirst);
       if (need_mask) {
 #pragma unroll
@@ -994,11 +998,13 @@ __global__ __launch_bounds__(NW * 64) void fwd3_kernel(const u16* __restrict__ q
       rs += __shfl_xor(rs, 16, 64);
       rs += __shfl_xor(rs, 32, 64);
       l += rs;
+      }
 #pragma unroll
       for (int ks = 0; ks < 2; ++ks) {
         const bf16x8 pb = pack_acc(sc[2 * ks], sc[2 * ks + 1]);
 #pragma unroll
-        for (int dt = 0; dt < 8; ++dt) o[dt] = mfma(lds_tr(Vs, off.tr[dt] + ks * 32 * ROWB), pb, o[dt]);
+        for (int dt = 0; dt < 8; ++dt)
+          if (!(DIAG & 4)) o[dt] = mfma(lds_tr(Vs, off.tr[dt] + ks * 32 * ROWB), pb, o[dt]);
       }
     }
     if (pre) {
@@ -1014,6 +1020,154 @@ __global__ __launch_bounds__(NW * 64) void fwd3_kernel(const u16* __restrict__ q
 #pragma unroll
     for (int dt = 0; dt < 8; ++dt) store4(op + 16 * dt, o[dt], inv);
     if (g == 0) lse[(long)h * total + start + qrow] = (m + log2f(l)) * LN2;
+  }
+}
+
+// v4 forward: every wave owns RG = 2 row groups of 16 queries, so each K fragment (row read) and V
+// fragment (transposed read) fetched from LDS feeds RG MFMAs — v3 reads 1 KB of LDS per MFMA, twice
+// what the LDS can deliver at the MFMA rate (256 B/clk/CU vs 4 SIMDs x 16x16x32 per 16 clk); v4 reads
+// 0.5 KB. Otherwise v3's structure: one LDS K/V buffer with register prefetch, masks only on
+// diagonal / tail tiles, exp2 with the scale folded in, deferred rescale (THR).
+template <int NW, int RG>
+__global__ __launch_bounds__(NW * 64) void fwd4_kernel(const u16* __restrict__ qkv, u16* __restrict__ out,
+                                                       float* __restrict__ lse, const int* __restrict__ cu, int nq,
+                                                       int nkv, int total, float sl2, int causal) {
+  constexpr int NT = NW * 64, BM = NW * 16 * RG, TB = 64 * ROWB;
+  __shared__ __attribute__((aligned(16))) char smem[2 * TB];
+  char* Ks = smem;
+  char* Vs = smem + TB;
+  const int qb = blockIdx.x, h = blockIdx.y, b = blockIdx.z;
+  const int start = cu[b], len = cu[b + 1] - start;
+  const int q0 = qb * BM;
+  if (q0 >= len) return;
+  const int kvh = h / (nq / nkv);
+  const long ld = (long)(nq + 2 * nkv) * D;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, g = lane >> 4;
+  const int wfirst = q0 + wave * 16 * RG;  // first query row of the wave
+  const u16* kbase = qkv + (long)start * ld + (nq + kvh) * D;
+  const u16* vbase = qkv + (long)start * ld + (nq + nkv + kvh) * D;
+  const int nkb = (len + 63) / 64;
+  const int nkt = causal ? min((q0 + BM + 63) / 64, nkb) : nkb;
+  Offs off;
+  off.init(lane);
+  {
+    Stage<64, NT> tk, tv;
+    tk.load(kbase, ld, len, tid);
+    tv.load(vbase, ld, len, tid);
+    tk.store(Ks, tid);
+    tv.store(Vs, tid);
+  }
+  bf16x8 qf[RG][4];
+#pragma unroll
+  for (int r = 0; r < RG; ++r) {
+    const int qrow = wfirst + 16 * r + (lane & 15);
+    const u16* qp = qkv + (long)(start + qrow) * ld + h * D + 8 * g;
+#pragma unroll
+    for (int s2 = 0; s2 < 4; ++s2) qf[r][s2] = load_frag_global(qp + 32 * s2, qrow < len);
+  }
+  f32x4 o[RG][8];
+  float m[RG], l[RG];
+#pragma unroll
+  for (int r = 0; r < RG; ++r) {
+#pragma unroll
+    for (int dt = 0; dt < 8; ++dt) o[r][dt] = f32x4{0.f, 0.f, 0.f, 0.f};
+    m[r] = -1e30f;
+    l[r] = 0.f;
+  }
+  __syncthreads();
+  for (int kt = 0; kt < nkt; ++kt) {
+    const int k0 = kt * 64;
+    const bool pre = kt + 1 < nkt;
+    Stage<64, NT> tk, tv;
+    if (pre) {
+      tk.load(kbase + (long)(k0 + 64) * ld, ld, len - k0 - 64, tid);
+      tv.load(vbase + (long)(k0 + 64) * ld, ld, len - k0 - 64, tid);
+    }
+    if (!causal || k0 <= wfirst + 16 * RG - 1) {
+      f32x4 sc[RG][4];
+#pragma unroll
+      for (int r = 0; r < RG; ++r)
+#pragma unroll
+        for (int nt = 0; nt < 4; ++nt) sc[r][nt] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int nt = 0; nt < 4; ++nt)
+#pragma unroll
+        for (int s2 = 0; s2 < 4; ++s2) {
+          const bf16x8 kf = lds_row(Ks, off.row[s2] + nt * 16 * ROWB);
+#pragma unroll
+          for (int r = 0; r < RG; ++r) sc[r][nt] = mfma(kf, qf[r][s2], sc[r][nt]);
+        }
+      bf16x8 pb[RG][2];
+#pragma unroll
+      for (int r = 0; r < RG; ++r) {
+        const int rfirst = wfirst + 16 * r;
+        const int qrow = rfirst + (lane & 15);
+        const bool need_mask = (k0 + 64 > len) || (causal && k0 + 63 > rfirst);
+        if (need_mask) {
+#pragma unroll
+          for (int nt = 0; nt < 4; ++nt)
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+              const int key = k0 + 16 * nt + 4 * g + i;
+              if (key >= len || (causal && key > qrow)) sc[r][nt][i] = -INFINITY;
+            }
+        }
+        float tmax = fmaxf(fmaxf(fmaxf(sc[r][0][0], sc[r][0][1]), fmaxf(sc[r][0][2], sc[r][0][3])),
+                           fmaxf(fmaxf(sc[r][1][0], sc[r][1][1]), fmaxf(sc[r][1][2], sc[r][1][3])));
+        tmax = fmaxf(tmax, fmaxf(fmaxf(fmaxf(sc[r][2][0], sc[r][2][1]), fmaxf(sc[r][2][2], sc[r][2][3])),
+                                 fmaxf(fmaxf(sc[r][3][0], sc[r][3][1]), fmaxf(sc[r][3][2], sc[r][3][3]))));
+        tmax = fmaxf(tmax, __shfl_xor(tmax, 16, 64));
+        tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64));
+        tmax *= sl2;
+        if (__any(tmax > m[r] + THR)) {
+          const float mnew = fmaxf(m[r], tmax);
+          const float alpha = exp2f(m[r] - mnew);
+          l[r] *= alpha;
+#pragma unroll
+          for (int dt = 0; dt < 8; ++dt) o[r][dt] *= alpha;
+          m[r] = mnew;
+        }
+        float rs = 0.f;
+#pragma unroll
+        for (int nt = 0; nt < 4; ++nt)
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const float p = exp2f(fmaf(sc[r][nt][i], sl2, -m[r]));
+            sc[r][nt][i] = p;
+            rs += p;
+          }
+        rs += __shfl_xor(rs, 16, 64);
+        rs += __shfl_xor(rs, 32, 64);
+        l[r] += rs;
+        pb[r][0] = pack_acc(sc[r][0], sc[r][1]);
+        pb[r][1] = pack_acc(sc[r][2], sc[r][3]);
+      }
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+        for (int dt = 0; dt < 8; ++dt) {
+          const bf16x8 vf = lds_tr(Vs, off.tr[dt] + ks * 32 * ROWB);
+#pragma unroll
+          for (int r = 0; r < RG; ++r) o[r][dt] = mfma(vf, pb[r][ks], o[r][dt]);
+        }
+    }
+    if (pre) {
+      __syncthreads();
+      tk.store(Ks, tid);
+      tv.store(Vs, tid);
+    }
+    __syncthreads();
+  }
+#pragma unroll
+  for (int r = 0; r < RG; ++r) {
+    const int qrow = wfirst + 16 * r + (lane & 15);
+    if (qrow < len) {
+      const float inv = 1.f / l[r];
+      u16* op = out + (long)(start + qrow) * nq * D + h * D + 4 * g;
+#pragma unroll
+      for (int dt = 0; dt < 8; ++dt) store4(op + 16 * dt, o[r][dt], inv);
+      if (g == 0) lse[(long)h * total + start + qrow] = (m[r] + log2f(l[r])) * LN2;
+    }
   }
 }
 
@@ -1285,6 +1439,7 @@ static int attn_impl() {
   const char* e = std::getenv("SFTAMD_ATTN_IMPL");
   if (e && e[0] == '1') return 1;
   if (e && e[0] == '2') return 2;
+  if (e && e[0] == '4') return 4;  // forward v4 (measured slower, kept selectable: profiles/r1_attention_microbench.txt)
   return 3;
 }
 
@@ -1316,6 +1471,35 @@ std::tuple<at::Tensor, at::Tensor> flash_fwd(const at::Tensor& qkv, const at::Te
   dim3 grid((max_seqlen + 63) / 64, nq, nseq);
   const float sl2 = (float)scale * attn::LOG2E;
   auto cu_c = cu.contiguous();
+  if (attn_impl() == 4) {  // forward v4 (2 row groups per wave); backward stays on v3
+    constexpr int NW = 4, RG = 2;
+    dim3 g4((max_seqlen + NW * 16 * RG - 1) / (NW * 16 * RG), nq, nseq);
+    attn::fwd4_kernel<NW, RG><<<g4, NW * 64, 0, cur_stream()>>>((const u16*)qkv.data_ptr(), (u16*)out.data_ptr(),
+                                                               lse.data_ptr<float>(), cu_c.data_ptr<int>(), nq, nkv,
+                                                               total, sl2, causal ? 1 : 0);
+    SFT_LAUNCH_CHECK();
+    return {out, lse};
+  }
+  if (attn_impl() == 3 && std::getenv("SFTAMD_ATTN_DIAG")) {  // timing-only ablations of fwd v3 (8 waves)
+    const int diag = atoi(std::getenv("SFTAMD_ATTN_DIAG"));
+    dim3 g3((max_seqlen + 127) / 128, nq, nseq);
+    auto gd = [&](auto dg) {
+      attn::fwd3_kernel<8, decltype(dg)::value><<<g3, 512, 0, cur_stream()>>>(
+          (const u16*)qkv.data_ptr(), (u16*)out.data_ptr(), lse.data_ptr<float>(), cu_c.data_ptr<int>(), nq, nkv, total,
+          sl2, causal ? 1 : 0);
+    };
+    switch (diag) {
+      case 1: gd(std::integral_constant<int, 1>()); break;
+      case 2: gd(std::integral_constant<int, 2>()); break;
+      case 4: gd(std::integral_constant<int, 4>()); break;
+      case 8: gd(std::integral_constant<int, 8>()); break;
+      case 12: gd(std::integral_constant<int, 12>()); break;
+      case 15: gd(std::integral_constant<int, 15>()); break;
+      default: gd(std::integral_constant<int, 0>()); break;
+    }
+    SFT_LAUNCH_CHECK();
+    return {out, lse};
+  }
   if (attn_impl() == 3) {
     int nw, nbuf;
     attn_cfg(nw, nbuf);
@@ -1451,7 +1635,7 @@ at::Tensor flash_bwd(const at::Tensor& dout, const at::Tensor& qkv, const at::Te
         cu_c.data_ptr<int>(), (u16*)dqkv.data_ptr(), nq, nkv, total, sl2, (float)scale, causal ? 1 : 0);
     SFT_LAUNCH_CHECK();
   };
-  if (attn_impl() == 3) {
+  if (attn_impl() >= 3) {
     if (nw == 4) run3(I4()); else run3(I8());
   } else if (attn_impl() == 2) {
     if (!attn_variant()) run2(std::false_type(), I8(), B2());

@@ -159,7 +159,7 @@ def _attn_case(lens, nq, nkv, causal, variant, impl="2", cfg=""):
         assert e < 3e-2, (name, e)
 
 
-@pytest.mark.parametrize("impl", ["3", "2", "1"])
+@pytest.mark.parametrize("impl", ["4", "3", "2", "1"])
 @pytest.mark.parametrize("variant", ["1", "0"])
 @pytest.mark.parametrize("causal", [True, False])
 def test_flash_attention_varlen_gqa(variant, causal, impl):
@@ -170,15 +170,16 @@ def test_flash_attention_mha_and_long():
     _attn_case([1000, 37], 4, 4, True, "1")
 
 
-@pytest.mark.parametrize("impl,cfg", [("2", "8,1"), ("2", "4,2"), ("2", "4,1"), ("3", "4,1"), ("3", "8,1")])
+@pytest.mark.parametrize("impl,cfg", [("2", "8,1"), ("2", "4,2"), ("2", "4,1"), ("3", "4,1"), ("3", "8,1"), ("4", "")])
 def test_flash_attention_launch_configs(impl, cfg):
     _attn_case([100, 255, 64, 1, 300], 8, 2, True, "1", impl, cfg)
     _attn_case([100, 255, 64, 1, 300], 8, 2, False, "1", impl, cfg)
 
 
-def test_flash_attention_deferred_rescale_branch():
+@pytest.mark.parametrize("impl", ["3", "4"])
+def test_flash_attention_deferred_rescale_branch(impl):
     """Force the online-softmax max to jump past THR mid-sequence (CDNA guide rule 26)."""
-    os.environ["SFTAMD_ATTN_IMPL"] = "3"
+    os.environ["SFTAMD_ATTN_IMPL"] = impl
     os.environ["SFTAMD_ATTN_CFG"] = ""
     torch.manual_seed(1)
     D, nq, nkv = 128, 4, 2

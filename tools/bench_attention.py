@@ -35,7 +35,7 @@ def timeit(fn, n=20):
     return statistics.median(ts)
 
 
-CFGS = [("1", ""), ("2", "8,1"), ("3", "8,1"), ("3", "4,1")]
+CFGS = [("1", ""), ("2", "8,1"), ("3", "8,1"), ("3", "4,1"), ("4", "")]
 res = {}
 ref = None
 for rnd in range(3):
