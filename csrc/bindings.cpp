@@ -7,7 +7,7 @@
 TORCH_LIBRARY(sftamd, m) {
   // norms / elementwise
   m.def("rmsnorm_fwd(Tensor x, Tensor? residual, Tensor weight, float eps) -> (Tensor, Tensor, Tensor)");
-  m.def("rmsnorm_bwd(Tensor dy, Tensor h, Tensor weight, Tensor rstd, Tensor? dres) -> (Tensor, Tensor)");
+  m.def("rmsnorm_bwd(Tensor dy, Tensor h, Tensor weight, Tensor rstd, Tensor? dres, Tensor(a!)? dw_out=None, bool accumulate=False) -> (Tensor, Tensor)");
   m.def("swiglu_fwd(Tensor gate_up) -> Tensor");
   m.def("swiglu_bwd(Tensor dy, Tensor gate_up) -> Tensor");
   m.def("rope_(Tensor(a!) qkv, Tensor cos, Tensor sin, int n_q, int n_kv, int head_dim, bool inverse) -> ()");

@@ -244,8 +244,11 @@ __global__ __launch_bounds__(256) void rmsnorm_bwd2_kernel(const u16* __restrict
 // out[c] = sum_p part[p][c], fixed order (deterministic). Block = 64 columns (16 float4 lanes) x
 // 64 row groups; each thread sums its rows with two independent accumulators, then a fixed
 // LDS tree over the row groups. All P rows of a 64-column slab are in flight at once.
-__global__ __launch_bounds__(1024) void col_sum2_kernel(const float* __restrict__ part, float* __restrict__ out, int P,
-                                                        int H) {
+// out_bf (optional): the bf16 weight-gradient buffer itself (the DDP engine's flat gradient slice),
+// written (accumulate = 0: first contribution of the step) or accumulated (beta = 1) in place — the
+// fp32 dW never goes back to PyTorch for a separate copy/add kernel.
+__global__ __launch_bounds__(1024) void col_sum2_kernel(const float* __restrict__ part, float* __restrict__ out,
+                                                        u16* __restrict__ out_bf, int accumulate, int P, int H) {
   __shared__ float4 red[64][16];
   const int c4 = threadIdx.x & 15, rg = threadIdx.x >> 4;
   const int c = blockIdx.x * 64 + c4 * 4;
@@ -274,7 +277,22 @@ __global__ __launch_bounds__(1024) void col_sum2_kernel(const float* __restrict_
     }
     __syncthreads();
   }
-  if (rg == 0 && c < H) *(float4*)(out + c) = red[0][c4];
+  if (rg == 0 && c < H) {
+    float4 r = red[0][c4];
+    if (out_bf) {
+      if (accumulate) {
+        const uint2 o = *(const uint2*)(out_bf + c);
+        r.x += __uint_as_float(o.x << 16);
+        r.y += __uint_as_float(o.x & 0xffff0000u);
+        r.z += __uint_as_float(o.y << 16);
+        r.w += __uint_as_float(o.y & 0xffff0000u);
+      }
+      *(uint2*)(out_bf + c) = make_uint2((unsigned)f2bf(r.x) | ((unsigned)f2bf(r.y) << 16),
+                                         (unsigned)f2bf(r.z) | ((unsigned)f2bf(r.w) << 16));
+    } else {
+      *(float4*)(out + c) = r;
+    }
+  }
 }
 
 // out[c] = sum_b part[b][c] in a fixed order (deterministic). Block = 64 columns x 4 row
@@ -342,8 +360,11 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor> rmsnorm_fwd(const at::Tensor& x, 
   return {y, res_out, rstd};
 }
 
+// dw_out (optional, bf16 [H]): receive the weight gradient directly (overwritten, or accumulated when
+// ``accumulate``); the returned dW is then an empty tensor.
 std::tuple<at::Tensor, at::Tensor> rmsnorm_bwd(const at::Tensor& dy, const at::Tensor& h, const at::Tensor& weight,
-                                               const at::Tensor& rstd, const c10::optional<at::Tensor>& dres) {
+                                               const at::Tensor& rstd, const c10::optional<at::Tensor>& dres,
+                                               const c10::optional<at::Tensor>& dw_out, bool accumulate) {
   SFT_CHECK_BF16(dy);
   SFT_CHECK_CONTIG(dy);
   SFT_CHECK_CONTIG(h);
@@ -356,6 +377,7 @@ std::tuple<at::Tensor, at::Tensor> rmsnorm_bwd(const at::Tensor& dy, const at::T
     dr = (const u16*)dres->data_ptr();
   }
   SFT_CHECK(rstd.numel() == M && weight.numel() == H && dy.numel() == h.numel(), "rmsnorm_bwd: shape mismatch");
+  SFT_CHECK(H % 8 == 0 && H <= 4096, "rmsnorm_bwd: hidden size must be a multiple of 8 and <= 4096");
   auto dw = at::empty({H}, h.options().dtype(at::kFloat));
   static const bool v1 = [] {
     const char* e = std::getenv("SFTAMD_RMSNORM_BWD");
@@ -370,9 +392,17 @@ std::tuple<at::Tensor, at::Tensor> rmsnorm_bwd(const at::Tensor& dy, const at::T
                        (const u16*)dy.data_ptr(), (const u16*)h.data_ptr(), (const u16*)weight.data_ptr(),
                        rstd.data_ptr<float>(), dr, (u16*)dx.data_ptr(), part.data_ptr<float>(), M, H));
     SFT_LAUNCH_CHECK();
-    col_sum2_kernel<<<(H + 63) / 64, 1024, 0, cur_stream()>>>(part.data_ptr<float>(), dw.data_ptr<float>(), nblk, H);
+    u16* obf = nullptr;
+    if (dw_out.has_value() && dw_out->defined()) {
+      SFT_CHECK(dw_out->scalar_type() == at::kBFloat16 && dw_out->is_contiguous() && dw_out->numel() == H &&
+                    (reinterpret_cast<uintptr_t>(dw_out->data_ptr()) % 8) == 0,
+                "rmsnorm_bwd: dw_out must be a contiguous, 8-byte aligned bf16 [H]");
+      obf = (u16*)dw_out->data_ptr();
+    }
+    col_sum2_kernel<<<(H + 63) / 64, 1024, 0, cur_stream()>>>(part.data_ptr<float>(), dw.data_ptr<float>(), obf,
+                                                              accumulate ? 1 : 0, nblk, H);
     SFT_LAUNCH_CHECK();
-    return {dx, dw};
+    return {dx, obf ? at::empty({0}, dw.options()) : dw};
   }
   int nblk = std::min((M + 15) / 16, 256);  // one 8-wave block per CU, >= 2 rows per wave
   nblk = std::max(nblk, 1);
@@ -383,6 +413,11 @@ std::tuple<at::Tensor, at::Tensor> rmsnorm_bwd(const at::Tensor& dy, const at::T
   SFT_LAUNCH_CHECK();
   col_sum_kernel<<<(H + 63) / 64, 256, 0, cur_stream()>>>(part.data_ptr<float>(), dw.data_ptr<float>(), nblk, H);
   SFT_LAUNCH_CHECK();
+  if (dw_out.has_value() && dw_out->defined()) {
+    at::Tensor o = *dw_out;
+    if (accumulate) o.add_(dw.to(o.scalar_type())); else o.copy_(dw);
+    return {dx, at::empty({0}, dw.options())};
+  }
   return {dx, dw};
 }
 

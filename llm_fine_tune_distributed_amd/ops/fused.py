@@ -233,9 +233,19 @@ class AddRMSNormFn(Function):
     def backward(ctx, dy, dres):
         h, rstd = ctx.saved_tensors
         w = ctx.weight
+        mg = getattr(w, "main_grad", None)
         if _ext.use_hip(h):
+            direct = (ctx.needs_input_grad[2] and mg is not None and mg.dtype == torch.bfloat16
+                      and mg.is_contiguous() and mg.data_ptr() % 8 == 0)
+            # the column-sum kernel writes / accumulates dW straight into the flat gradient buffer
             dx, dw = _ext.ops().rmsnorm_bwd(dy.contiguous(), h, w, rstd,
-                                           dres.contiguous() if dres is not None else None)
+                                           dres.contiguous() if dres is not None else None,
+                                           mg if direct else None,
+                                           direct and not getattr(w, "_sftamd_fresh", False))
+            if direct:
+                w._sftamd_fresh = False
+                _weight_grad_done(w)
+                return dx, (dx if ctx.has_residual else None), None, None
         else:
             hf = h.float()
             n = hf * rstd[..., None]

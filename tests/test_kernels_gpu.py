@@ -71,6 +71,24 @@ def test_rmsnorm_bwd_training_shape_deterministic():
     assert rel_err(dw, gw) < 1e-3
 
 
+def test_rmsnorm_bwd_direct_dw_out():
+    """dW written / accumulated straight into a bf16 gradient buffer (the flat DDP slice)."""
+    torch.manual_seed(2)
+    M, H = 1024, 2048
+    h = torch.randn(M, H, device=DEV, dtype=torch.bfloat16)
+    w = (1 + 0.1 * torch.randn(H, device=DEV)).to(torch.bfloat16)
+    _, _, rstd = _ext.ops().rmsnorm_fwd(h, None, w, 1e-6)
+    dy = torch.randn_like(h)
+    dx_ref, dw_ref = _ext.ops().rmsnorm_bwd(dy, h, w, rstd, None)
+    buf = torch.full((H + 64,), 7.0, device=DEV, dtype=torch.bfloat16)
+    out = buf[64:]
+    dx, dw = _ext.ops().rmsnorm_bwd(dy, h, w, rstd, None, out, False)
+    assert dw.numel() == 0 and torch.equal(dx, dx_ref)
+    assert torch.equal(out, dw_ref.to(torch.bfloat16)) and (buf[:64] == 7.0).all()
+    _ext.ops().rmsnorm_bwd(dy, h, w, rstd, None, out, True)
+    assert rel_err(out, 2 * dw_ref) < 1e-2
+
+
 def test_swiglu():
     torch.manual_seed(0)
     gu = torch.randn(777, 2 * 1376, device=DEV, dtype=torch.bfloat16)
