@@ -386,7 +386,7 @@ struct Stager2 {
   }
 };
 
-template <class G, int EPI, bool SCHED = true>
+template <class G, int EPI, bool SCHED = true, bool TRC = false>
 __device__ __forceinline__ void ring2_loop(char* __restrict__ b0, char* __restrict__ b1, char* __restrict__ b2,
                                            int nsteps, Stager2<G, EPI>& st, int w, int offA0, int offA1, int offB0,
                                            int offB1, f32x4 (&acc)[G::FM][G::FN]) {
@@ -420,7 +420,8 @@ __device__ __forceinline__ void ring2_loop(char* __restrict__ b0, char* __restri
         for (int i = 0; i < G::FM; ++i) {
 #pragma unroll
           for (int j = 0; j < G::FN; ++j)
-            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[0][j], acc[i][j], 0, 0, 0);
+            acc[i][j] = TRC ? __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[0][j], fa[i], acc[i][j], 0, 0, 0)
+                            : __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[0][j], acc[i][j], 0, 0, 0);
           fa[i] = lds_row(cur, offA1 + 2048 * i);
           if (SCHED) {
             __builtin_amdgcn_sched_group_barrier(0x008, G::FN, 0);
@@ -440,7 +441,8 @@ __device__ __forceinline__ void ring2_loop(char* __restrict__ b0, char* __restri
         for (int i = 0; i < G::FM; ++i) {
 #pragma unroll
           for (int j = 0; j < G::FN; ++j)
-            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[1][j], acc[i][j], 0, 0, 0);
+            acc[i][j] = TRC ? __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[1][j], fa[i], acc[i][j], 0, 0, 0)
+                            : __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[1][j], acc[i][j], 0, 0, 0);
           fa[i] = lds_row(nxt, offA0 + 2048 * i);
           // DMA pieces of stage t + NS spread over the fragment rows (PPW <= 2 FM)
           if (2 * i < PPW) st.piece(cur, w, 2 * i);
@@ -539,6 +541,104 @@ __device__ __forceinline__ void ring2e_loop(char* __restrict__ b0, char* __restr
   __builtin_amdgcn_s_waitcnt(waitcnt_imm(0, 0));
 }
 
+// Epilogue of the TRC (transposed-C) build: with the B fragment as the MFMA's first operand, lane
+// (g, ii) of fragment (i, j) holds output row 16 i + ii, columns 16 j + 4 g .. + 3 — four consecutive
+// columns, so the tile goes to LDS as packed bf16x4 (one ds_write_b64 per fragment instead of four
+// ds_write_b32 of fp32) and back as 16-byte rows for the global stores; the paired fragments (2q,
+// 2q + 1) of SWIGLU / ROPE meet in one lane and are combined in registers before staging.
+__device__ __forceinline__ uint2 pack4(const float* f) {
+  return make_uint2((unsigned)f2bf(f[0]) | ((unsigned)f2bf(f[1]) << 16), (unsigned)f2bf(f[2]) | ((unsigned)f2bf(f[3]) << 16));
+}
+
+template <class G, int EPI>
+__device__ __forceinline__ void epilogue_t(char* smem, f32x4 (&acc)[G::FM][G::FN], const EpiArgs& ea, int m0, int n0,
+                                           int wm, int wn, int w, int lane) {
+  // per-wave LDS region: EROWS rows x LDW bf16 (rows 16-byte multiples, +16 B pad against write conflicts)
+  constexpr int NCOL = EPI == EPI_SWIGLU ? G::TN + G::TN / 2 : G::TN;  // SWIGLU stages gate | up | act
+  constexpr int LDW = NCOL + 8;
+  constexpr int EROWS = (G::TM * LDW * 2 * 8 <= G::LDS) ? G::TM : G::TM / 2;  // within the kernel's LDS
+  constexpr int PASSES = G::TM / EROWS, FPP = EROWS / 16;
+  static_assert(EROWS * LDW * 2 * 8 <= G::LDS, "epilogue LDS");
+  const int g = lane >> 4, ii = lane & 15;
+  u16* ep = reinterpret_cast<u16*>(smem) + w * EROWS * LDW;
+#pragma unroll
+  for (int pass = 0; pass < PASSES; ++pass) {
+    const int rbase = m0 + wm * G::TM + pass * EROWS;
+#pragma unroll
+    for (int fi = 0; fi < FPP; ++fi) {
+      const int i = pass * FPP + fi;
+      u16* er = ep + (16 * fi + ii) * LDW;
+      if constexpr (EPI == EPI_PLAIN) {
+#pragma unroll
+        for (int j = 0; j < G::FN; ++j) {
+          const float v[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
+          *(uint2*)(er + 16 * j + 4 * g) = pack4(v);
+        }
+      } else {
+#pragma unroll
+        for (int q = 0; q < G::FN / 2; ++q) {
+          float a[4], b[4];
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            a[e] = rbf(acc[i][2 * q][e]);  // the bf16 projection values the unfused path would see
+            b[e] = rbf(acc[i][2 * q + 1][e]);
+          }
+          if constexpr (EPI == EPI_SWIGLU) {
+            float o[4];
+#pragma unroll
+            for (int e = 0; e < 4; ++e) o[e] = silu(a[e]) * b[e];
+            *(uint2*)(er + 16 * q + 4 * g) = pack4(a);                       // gate  [0, TN/2)
+            *(uint2*)(er + G::TN / 2 + 16 * q + 4 * g) = pack4(b);           // up    [TN/2, TN)
+            *(uint2*)(er + G::TN + 16 * q + 4 * g) = pack4(o);               // act   [TN, 3TN/2)
+          } else {  // ROPE: lo = head dim d, hi = d + 64
+            const int t = wn * G::TN + 32 * q + 4 * g;
+            const int head = t >> 7, u = t & 127, d = 16 * (u >> 5) + (u & 15);
+            if (n0 + 128 * head + d < ea.rope_cols) {
+              const long row = rbase + 16 * fi + ii;
+              const float4 c4 = *(const float4*)(ea.cosb + row * 64 + d);
+              const float4 s4 = *(const float4*)(ea.sinb + row * 64 + d);
+              const float cs[4] = {c4.x, c4.y, c4.z, c4.w}, sn[4] = {s4.x, s4.y, s4.z, s4.w};
+              float lo[4], hi[4];
+#pragma unroll
+              for (int e = 0; e < 4; ++e) {
+                lo[e] = a[e] * cs[e] - b[e] * sn[e];
+                hi[e] = b[e] * cs[e] + a[e] * sn[e];
+              }
+              *(uint2*)(er + 16 * q + 4 * g) = pack4(lo);
+              *(uint2*)(er + G::TN / 2 + 16 * q + 4 * g) = pack4(hi);
+            } else {
+              *(uint2*)(er + 16 * q + 4 * g) = pack4(a);
+              *(uint2*)(er + G::TN / 2 + 16 * q + 4 * g) = pack4(b);
+            }
+          }
+        }
+      }
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // wave-private region: writes before reads
+    constexpr int SEGS = NCOL / 8;                       // 16-byte segments per staged row
+#pragma unroll
+    for (int it = 0; it < EROWS * SEGS / 64; ++it) {
+      const int sg = it * 64 + lane, row = sg / SEGS, cs = sg - row * SEGS;
+      const uint4 v = *(const uint4*)(ep + row * LDW + cs * 8);
+      const long grow = rbase + row;
+      if constexpr (EPI == EPI_PLAIN) {
+        *(uint4*)(ea.C + grow * ea.ldc + n0 + wn * G::TN + cs * 8) = v;
+      } else if constexpr (EPI == EPI_SWIGLU) {
+        const int part = cs / (G::TN / 16), k = cs - part * (G::TN / 16);  // 0 gate, 1 up, 2 act
+        const int c = (n0 >> 1) + (G::TN / 2) * wn + 8 * k;
+        if (part == 0) *(uint4*)(ea.C + grow * ea.ldc + c) = v;
+        else if (part == 1) *(uint4*)(ea.C + grow * ea.ldc + ea.I + c) = v;
+        else *(uint4*)(ea.act + grow * ea.I + c) = v;
+      } else {  // ROPE: staged [lo 32 | hi 32]
+        const int part = cs / (G::TN / 16), k = cs - part * (G::TN / 16);
+        const int head = wn >> 1, dbase = 32 * (wn & 1);
+        *(uint4*)(ea.C + grow * ea.ldc + n0 + 128 * head + dbase + 64 * part + 8 * k) = v;
+      }
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  }
+}
+
 template <int BM, int BN, int WM, int WN, int NS, int EPI, int VAR = 0>
 __global__ void __launch_bounds__(NT) tn2_kernel(const u16* __restrict__ A, const u16* __restrict__ B, int K, long lda,
                                                  long ldb, int nbm, int nbn, int group, EpiArgs ea) {
@@ -579,10 +679,13 @@ __global__ void __launch_bounds__(NT) tn2_kernel(const u16* __restrict__ A, cons
   if constexpr (VAR == 1)
     ring2e_loop<G, EPI>(smem, smem + G::STAGE, K / BK2, st, w, offA0, offA1, offB0, offB1, acc);
   else
-    ring2_loop<G, EPI, VAR == 2>(smem, smem + G::STAGE, smem + (NS > 2 ? 2 : 0) * G::STAGE, K / BK2, st, w, offA0,
-                                 offA1, offB0, offB1, acc);
+    ring2_loop<G, EPI, VAR == 2, VAR == 3>(smem, smem + G::STAGE, smem + (NS > 2 ? 2 : 0) * G::STAGE, K / BK2, st,
+                                           w, offA0, offA1, offB0, offB1, acc);
   __syncthreads();
-  epilogue<G, EPI>(smem, acc, ea, m0, n0, wm, wn, w, lane);
+  if constexpr (VAR == 3)
+    epilogue_t<G, EPI>(smem, acc, ea, m0, n0, wm, wn, w, lane);
+  else
+    epilogue<G, EPI>(smem, acc, ea, m0, n0, wm, wn, w, lane);
 }
 
 template <int BM, int BN, int WM, int WN, int NS, int EPI, int VAR = 0>
@@ -632,6 +735,9 @@ at::Tensor gemm_tn(const at::Tensor& a, const at::Tensor& w, int64_t cfg) {
     SFT_CHECK(N % 256 == 0 && a.size(1) % 64 == 0, "gemm_tn BK64: N % 256, K % 64");
     if (cfg == 2) tn::launch2<256, 256, 2, 4, 2, tn::EPI_PLAIN>(a, w, N, ea);
     else tn::launch2<256, 256, 2, 4, 2, tn::EPI_PLAIN, 1>(a, w, N, ea);
+  } else if (cfg == 5) {  // BK64, transposed-C fragments, packed-bf16 LDS epilogue
+    SFT_CHECK(N % 256 == 0 && a.size(1) % 64 == 0, "gemm_tn BK64: N % 256, K % 64");
+    tn::launch2<256, 256, 2, 4, 2, tn::EPI_PLAIN, 3>(a, w, N, ea);
   } else if (cfg == 4) {  // BK64 with sched_group_barrier interleave pinned (measured slower: diagnostics)
     SFT_CHECK(N % 256 == 0 && a.size(1) % 64 == 0, "gemm_tn BK64: N % 256, K % 64");
     tn::launch2<256, 256, 2, 4, 2, tn::EPI_PLAIN, 2>(a, w, N, ea);
@@ -650,7 +756,12 @@ std::tuple<at::Tensor, at::Tensor> gemm_tn_swiglu(const at::Tensor& x, const at:
   auto gu = at::empty({M, N}, x.options());
   auto act = at::empty({M, I}, x.options());
   tn::EpiArgs ea{(u16*)gu.data_ptr(), (u16*)act.data_ptr(), nullptr, nullptr, (long)N, I, 0};
-  if (x.size(1) % 64 == 0) tn::launch2<256, 256, 2, 4, 2, tn::EPI_SWIGLU>(x, w_gu, N, ea);
+  static const bool trc = [] {
+    const char* e = std::getenv("SFTAMD_TN_TRC");
+    return !(e && e[0] == '0');
+  }();
+  if (x.size(1) % 64 == 0 && trc) tn::launch2<256, 256, 2, 4, 2, tn::EPI_SWIGLU, 3>(x, w_gu, N, ea);
+  else if (x.size(1) % 64 == 0) tn::launch2<256, 256, 2, 4, 2, tn::EPI_SWIGLU>(x, w_gu, N, ea);
   else tn::launch<256, 256, 2, 4, 5, tn::EPI_SWIGLU>(x, w_gu, N, ea);
   return {gu, act};
 }
@@ -670,6 +781,7 @@ at::Tensor gemm_tn_rope(const at::Tensor& x, const at::Tensor& w, const at::Tens
                  (int)rope_cols};
   if (cfg == 1) tn::launch<256, 128, 4, 2, 6, tn::EPI_ROPE>(x, w, N, ea);
   else if (cfg == 2 && x.size(1) % 64 == 0) tn::launch2<256, 256, 2, 4, 2, tn::EPI_ROPE>(x, w, N, ea);
+  else if (cfg == 5 && x.size(1) % 64 == 0) tn::launch2<256, 256, 2, 4, 2, tn::EPI_ROPE, 3>(x, w, N, ea);
   else tn::launch<256, 256, 2, 4, 5, tn::EPI_ROPE>(x, w, N, ea);
   return c;
 }
