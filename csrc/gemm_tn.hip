@@ -336,16 +336,17 @@ __device__ __forceinline__ int swz2(int row, int ch) { return ch ^ ((row >> 1) &
 template <int BM, int BN, int WM, int WN, int NS_>
 struct Cfg2 {
   static constexpr int NS = NS_;
+  static constexpr int NW = WM * WN;  // 8 waves (2x4: 128x64 wave tiles) or 4 waves (2x2: 128x128, acc in AGPRs)
   static constexpr int TM = BM / WM, TN = BN / WN;
   static constexpr int FM = TM / 16, FN = TN / 16;
   static constexpr int APIECES = BM / 8, PIECES = (BM + BN) / 8;  // 1 KB = 8 image rows per piece
-  static constexpr int PPW = PIECES / 8;
+  static constexpr int PPW = PIECES / NW;
   static constexpr int STAGE = (BM + BN) * ROWB2;
   static constexpr int EPI_ROWS = 64, EPI_LD = TN + 4;
-  static constexpr int EPI = 8 * EPI_ROWS * EPI_LD * 4;
+  static constexpr int EPI = NW * EPI_ROWS * EPI_LD * 4;
   static constexpr int LDS = (NS * STAGE > EPI) ? NS * STAGE : EPI;
-  static_assert(WM * WN == 8 && PIECES % 8 == 0 && FM * 2 >= PPW, "config");
-  static_assert(TN == 64, "epilogue pairing assumes 64-column wave tiles");
+  static_assert((NW == 8 || NW == 4) && PIECES % NW == 0 && APIECES % NW == 0 && FM * 2 >= PPW, "config");
+  static_assert(TN % 32 == 0, "epilogue pairing needs 32-column multiples per wave");
   static_assert(LDS <= 160 * 1024, "LDS budget");
 };
 
@@ -362,21 +363,22 @@ __device__ __forceinline__ int b2_row(int pb, int n0, int I) {
     return n0 + 8 * pb;
   }
 }
-template <int EPI>
-constexpr int b2_koff(int k) {  // b2_row(w + 8k) - b2_row(w), independent of w < 8
-  return EPI == EPI_SWIGLU ? 32 * k : (EPI == EPI_ROPE ? 32 * (k & 1) + 128 * (k >> 1) : 64 * k);
+template <int EPI, int NW>
+constexpr int b2_koff(int k) {  // b2_row(w + NW k) - b2_row(w), independent of w < NW (NW = 4 or 8)
+  return EPI == EPI_SWIGLU ? 4 * NW * k
+                           : (EPI == EPI_ROPE ? 128 * ((NW * k) >> 4) + 16 * (((NW * k) & 15) >> 2) : 8 * NW * k);
 }
 
 template <class G, int EPI>
 struct Stager2 {
-  static constexpr int JA = G::APIECES / 8;
+  static constexpr int JA = G::APIECES / G::NW;
   const u16* pa;
   const u16* pb;
   long lda, ldb;
   int left;
   __device__ __forceinline__ void piece(char* buf, int w, int j) {
-    const u16* src = j < JA ? pa + (long)(64 * j) * lda : pb + (long)b2_koff<EPI>(j - JA) * ldb;
-    glds16(src, buf + (w + 8 * j) * 1024);
+    const u16* src = j < JA ? pa + (long)(8 * G::NW * j) * lda : pb + (long)b2_koff<EPI, G::NW>(j - JA) * ldb;
+    glds16(src, buf + (w + G::NW * j) * 1024);
   }
   __device__ __forceinline__ void advance() {
     if (--left > 0) {
@@ -554,6 +556,7 @@ template <class G, int EPI>
 __device__ __forceinline__ void epilogue_t(char* smem, f32x4 (&acc)[G::FM][G::FN], const EpiArgs& ea, int m0, int n0,
                                            int wm, int wn, int w, int lane) {
   // per-wave LDS region: EROWS rows x LDW bf16 (rows 16-byte multiples, +16 B pad against write conflicts)
+  static_assert(G::NW == 8 && G::TN == 64, "transposed-C epilogue: 8 waves of 128x64");
   constexpr int NCOL = EPI == EPI_SWIGLU ? G::TN + G::TN / 2 : G::TN;  // SWIGLU stages gate | up | act
   constexpr int LDW = NCOL + 8;
   constexpr int EROWS = (G::TM * LDW * 2 * 8 <= G::LDS) ? G::TM : G::TM / 2;  // within the kernel's LDS
@@ -640,7 +643,7 @@ __device__ __forceinline__ void epilogue_t(char* smem, f32x4 (&acc)[G::FM][G::FN
 }
 
 template <int BM, int BN, int WM, int WN, int NS, int EPI, int VAR = 0>
-__global__ void __launch_bounds__(NT) tn2_kernel(const u16* __restrict__ A, const u16* __restrict__ B, int K, long lda,
+__global__ void __launch_bounds__(WM * WN * 64) tn2_kernel(const u16* __restrict__ A, const u16* __restrict__ B, int K, long lda,
                                                  long ldb, int nbm, int nbn, int group, EpiArgs ea) {
   using G = Cfg2<BM, BN, WM, WN, NS>;
   __shared__ __attribute__((aligned(16))) char smem[G::LDS];
@@ -661,8 +664,8 @@ __global__ void __launch_bounds__(NT) tn2_kernel(const u16* __restrict__ A, cons
   st.ldb = ldb;
   st.left = K / BK2;
   {
-    // piece P = w + 8 j holds image rows 8P + lr (lr = lane >> 3), slot lane & 7; (row >> 1) & 7 =
-    // 4 (P & 1) + (lr >> 1) and P & 1 = w & 1 for every piece of the wave
+    // piece P = w + NW j holds image rows 8P + lr (lr = lane >> 3), slot lane & 7; (row >> 1) & 7 =
+    // 4 (P & 1) + (lr >> 1) and P & 1 = w & 1 for every piece of the wave (NW even)
     const int lr = lane >> 3, ch = (lane & 7) ^ (4 * (w & 1) + (lr >> 1));
     st.pa = A + (long)(m0 + 8 * w + lr) * lda + 8 * ch;
     st.pb = B + (long)(b2_row<EPI>(w, n0, ea.I) + lr) * ldb + 8 * ch;
@@ -692,7 +695,7 @@ template <int BM, int BN, int WM, int WN, int NS, int EPI, int VAR = 0>
 void launch2(const at::Tensor& a, const at::Tensor& w, int N, const EpiArgs& ea) {
   const int M = a.size(0), K = a.size(1);
   const int nbm = M / BM, nbn = N / BN;
-  tn2_kernel<BM, BN, WM, WN, NS, EPI, VAR><<<nbm * nbn, NT, 0, cur_stream()>>>(
+  tn2_kernel<BM, BN, WM, WN, NS, EPI, VAR><<<nbm * nbn, WM * WN * 64, 0, cur_stream()>>>(
       (const u16*)a.data_ptr(), (const u16*)w.data_ptr(), K, a.stride(0), w.stride(0), nbm, nbn,
       std::min(group_m(), nbm), ea);
   SFT_LAUNCH_CHECK();
