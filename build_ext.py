@@ -7,6 +7,9 @@ against libtorch. No hipify, no JIT cache: the .so lives in the source tree so i
 the GPU box with the snapshot. Incremental: objects newer than their sources/headers are reused.
 
     python build_ext.py [--jobs N] [--force] [--debug]
+
+``--debug`` builds a separate ``_C_debug.so`` (-O1 -g, device asserts ``SFT_DASSERT`` compiled in, objects
+under build/obj_debug); the loader picks it when ``SFTAMD_DEBUG=1`` (SURVEY §5.2 triage mode).
 """
 from __future__ import annotations
 
@@ -20,8 +23,10 @@ from concurrent.futures import ThreadPoolExecutor
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(ROOT, "csrc")
-OBJ = os.path.join(ROOT, "build", "obj")
-OUT = os.path.join(ROOT, "llm_fine_tune_distributed_amd", "_C.so")
+OBJ_RELEASE = os.path.join(ROOT, "build", "obj")
+OBJ_DEBUG = os.path.join(ROOT, "build", "obj_debug")
+OUT_RELEASE = os.path.join(ROOT, "llm_fine_tune_distributed_amd", "_C.so")
+OUT_DEBUG = os.path.join(ROOT, "llm_fine_tune_distributed_amd", "_C_debug.so")
 ARCH = os.environ.get("PYTORCH_ROCM_ARCH", "gfx950")
 ROCM = os.environ.get("ROCM_PATH", "/opt/rocm")
 
@@ -45,16 +50,17 @@ def main(argv=None) -> str:
     ap = argparse.ArgumentParser()
     ap.add_argument("--jobs", type=int, default=min(8, os.cpu_count() or 4))
     ap.add_argument("--force", action="store_true")
-    ap.add_argument("--debug", action="store_true", help="-O1 -g, device asserts on")
+    ap.add_argument("--debug", action="store_true", help="_C_debug.so: -O1 -g, device asserts on")
     ap.add_argument("--save-temps", action="store_true", help="keep .s for inspection (build/obj)")
     args = ap.parse_args(argv)
 
     inc, libdir, abi = torch_paths()
+    OBJ, OUT = (OBJ_DEBUG, OUT_DEBUG) if args.debug else (OBJ_RELEASE, OUT_RELEASE)
     os.makedirs(OBJ, exist_ok=True)
     headers = glob.glob(os.path.join(CSRC, "*.h"))
     common = [f"-D_GLIBCXX_USE_CXX11_ABI={abi}", "-DUSE_ROCM=1", "-fPIC", "-std=c++17",
               "-DTORCH_EXTENSION_NAME=sftamd", "-Wno-unused-result"] + [f"-I{p}" for p in inc] + [f"-I{CSRC}"]
-    opt = ["-O1", "-g"] if args.debug else ["-O3", "-DNDEBUG"]
+    opt = ["-O1", "-g", "-DSFTAMD_DEBUG"] if args.debug else ["-O3", "-DNDEBUG"]
     hip_flags = [f"--offload-arch={ARCH}", "-munsafe-fp-atomics", "-fgpu-flush-denormals-to-zero"] + opt + common
     if args.save_temps:
         hip_flags.append("-save-temps=obj")

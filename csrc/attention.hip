@@ -460,6 +460,7 @@ __global__ __launch_bounds__(NW * 64) void fwd2_kernel(const u16* __restrict__ q
   __shared__ __attribute__((aligned(16))) char smem[2 * NBUF * TB];  // K0 V0 (K1 V1)
   const int qb = blockIdx.x, h = blockIdx.y, b = blockIdx.z;
   const int start = cu[b], len = cu[b + 1] - start;
+  SFT_DASSERT(start >= 0 && len >= 0 && start + len <= total);
   const int q0 = qb * BM;
   if (q0 >= len) return;
   const int kvh = h / (nq / nkv);
@@ -573,6 +574,7 @@ __global__ __launch_bounds__(NW * 64) void bwd_dq2_kernel(const u16* __restrict_
   __shared__ __attribute__((aligned(16))) char smem[2 * NBUF * TB];
   const int qb = blockIdx.x, h = blockIdx.y, b = blockIdx.z;
   const int start = cu[b], len = cu[b + 1] - start;
+  SFT_DASSERT(start >= 0 && len >= 0 && start + len <= total);
   const int q0 = qb * BM;
   if (q0 >= len) return;
   const int kvh = h / (nq / nkv);
@@ -911,6 +913,7 @@ __global__ __launch_bounds__(NW * 64) void fwd3_kernel(const u16* __restrict__ q
   char* Vs = smem + TB;
   const int qb = blockIdx.x, h = blockIdx.y, b = blockIdx.z;
   const int start = cu[b], len = cu[b + 1] - start;
+  SFT_DASSERT(start >= 0 && len >= 0 && start + len <= total);
   const int q0 = qb * BM;
   if (q0 >= len) return;
   const int kvh = h / (nq / nkv);
@@ -1038,6 +1041,7 @@ __global__ __launch_bounds__(NW * 64) void fwd4_kernel(const u16* __restrict__ q
   char* Vs = smem + TB;
   const int qb = blockIdx.x, h = blockIdx.y, b = blockIdx.z;
   const int start = cu[b], len = cu[b + 1] - start;
+  SFT_DASSERT(start >= 0 && len >= 0 && start + len <= total);
   const int q0 = qb * BM;
   if (q0 >= len) return;
   const int kvh = h / (nq / nkv);
@@ -1183,6 +1187,7 @@ __global__ __launch_bounds__(NW * 64) void bwd_dq3_kernel(const u16* __restrict_
   char* Vs = smem + TB;
   const int qb = blockIdx.x, h = blockIdx.y, b = blockIdx.z;
   const int start = cu[b], len = cu[b + 1] - start;
+  SFT_DASSERT(start >= 0 && len >= 0 && start + len <= total);
   const int q0 = qb * BM;
   if (q0 >= len) return;
   const int kvh = h / (nq / nkv);

@@ -74,4 +74,23 @@ inline int num_cus() { return 256; }  // MI355X: 8 XCDs x 32 CUs
 #define SFT_CHECK_CONTIG(t) SFT_CHECK((t).is_contiguous(), #t " must be contiguous")
 #define SFT_LAUNCH_CHECK() C10_HIP_KERNEL_LAUNCH_CHECK()
 
+// Device-side invariant checks, compiled in only by `python build_ext.py --debug` (-DSFTAMD_DEBUG,
+// separate _C_debug.so loaded when SFTAMD_DEBUG=1). The release kernels clamp or skip bad inputs
+// instead; the debug build names the kernel, block and thread of the first violation and aborts.
+// Triage recipe: SFTAMD_DEBUG=1 AMD_SERIALIZE_KERNEL=3 HIP_LAUNCH_BLOCKING=1 python ...
+#ifdef SFTAMD_DEBUG
+#define SFT_DASSERT(cond)                                                                                   \
+  do {                                                                                                      \
+    if (!(cond)) {                                                                                          \
+      printf("sftamd device assert failed: %s at %s:%d (block %d,%d,%d thread %d)\n", #cond, __FILE__,      \
+             __LINE__, (int)blockIdx.x, (int)blockIdx.y, (int)blockIdx.z, (int)threadIdx.x);                \
+      __builtin_trap();                                                                                     \
+    }                                                                                                       \
+  } while (0)
+#else
+#define SFT_DASSERT(cond) \
+  do {                    \
+  } while (0)
+#endif
+
 }  // namespace sftamd

@@ -38,6 +38,7 @@ __global__ __launch_bounds__(256) void ce_fwd_kernel(u16* __restrict__ logits, c
   const int tid = threadIdx.x;
   u16* lr = logits + (long)row * V;
   const long label = labels[row];
+  SFT_DASSERT(label == -100 || (label >= 0 && label < V));
   const bool valid = label >= 0 && label < V;
   const int nvec = V / 8;
 

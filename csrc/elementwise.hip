@@ -139,6 +139,7 @@ __global__ __launch_bounds__(256) void embedding_fwd_kernel(const int64_t* __res
     const long m = t / vpr;
     const int c = (int)(t - m * vpr) * 8;
     long id = ids[m];
+    SFT_DASSERT(id >= 0 && id < V);
     id = id < 0 ? 0 : (id >= V ? V - 1 : id);
     *(uint4*)(out + m * H + c) = *(const uint4*)(w + id * H + c);
   }
@@ -155,6 +156,7 @@ __global__ __launch_bounds__(256) void embedding_bwd_kernel(const u16* __restric
   const int lane = threadIdx.x & 63;
   if (i >= M) return;
   const int id = sorted[i];
+  SFT_DASSERT(i == 0 || sorted[i - 1] <= id);
   if (i > 0 && sorted[i - 1] == id) return;
   float acc[NV][8];
 #pragma unroll

@@ -25,6 +25,7 @@ def main(argv=None):
     from ..parallel.process_group import cleanup_distributed, setup_distributed
     from ..train import (AimCallback, PerplexityCallback, SFTConfig, SFTTrainer, TrainingHistoryCallback,
                          config_from_env)
+    from ..train.config import apply_overrides
 
     ap = argparse.ArgumentParser()
     ap.add_argument("--model", default=os.getenv("MODEL_NAME", "HuggingFaceTB/SmolLM3-3B"),
@@ -41,6 +42,10 @@ def main(argv=None):
     ap.add_argument("--no-gradient-checkpointing", action="store_true")
     ap.add_argument("--resume", default=None, help="checkpoint dir or 'auto'")
     ap.add_argument("--max-train-samples", type=int, default=None)
+    ap.add_argument("--config", default=os.getenv("SFT_CONFIG"),
+                    help="YAML/JSON file of SFTConfig field overrides (applied over the reference defaults)")
+    ap.add_argument("--set", dest="sets", action="append", default=[], metavar="FIELD=VALUE",
+                    help="override one SFTConfig field (repeatable; highest precedence)")
     a = ap.parse_args(argv)
 
     st = setup_distributed()
@@ -84,6 +89,9 @@ def main(argv=None):
         max_seq_length=a.max_length, packing=a.packing, ddp_backend="nccl" if st.device.type == "cuda" else "gloo",
         freeze_policy=a.freeze_policy, lr_scheduler_type=a.lr_scheduler, max_train_samples=a.max_train_samples,
         **dist_args)
+    args = apply_overrides(args, a.config, a.sets)
+    if st.is_main:  # the resolved configuration of this run, next to its artifacts
+        args.to_json(f"{out}/sft_config.json")
     trainer = SFTTrainer(model=a.model, args=args, train_dataset=train_rows, eval_dataset=val_rows,
                          processing_class=tokenizer, callbacks=[history, ppl, aim])
     if st.device.type == "cuda" and st.is_main:

@@ -6,7 +6,8 @@ The extension registers its kernels as torch custom ops in the ``sftamd`` namesp
 Policy: on a GPU process the HIP path is *mandatory* — if the .so is missing or fails to
 load and a CUDA(HIP) tensor reaches an op, we raise instead of silently running the
 PyTorch reference (set ``SFTAMD_ALLOW_FALLBACK=1`` to opt in to the fallback, or
-``SFTAMD_DISABLE_HIP=1`` to force the reference path for A/B numerics).
+``SFTAMD_DISABLE_HIP=1`` to force the reference path for A/B numerics). ``SFTAMD_DEBUG=1`` loads
+``_C_debug.so`` instead (``build_ext.py --debug``: -O1 -g, device asserts on).
 """
 from __future__ import annotations
 
@@ -15,7 +16,14 @@ import threading
 
 import torch
 
-_LIB_PATH = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "_C.so")
+_PKG = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _select_lib() -> str:
+    return os.path.join(_PKG, "_C_debug.so" if os.environ.get("SFTAMD_DEBUG", "0") == "1" else "_C.so")
+
+
+_LIB_PATH = _select_lib()
 _lock = threading.Lock()
 _loaded = None  # None = not tried, True/False afterwards
 _error = None
@@ -33,7 +41,8 @@ def load() -> bool:
         if _loaded is not None:
             return _loaded
         if not os.path.exists(_LIB_PATH):
-            _loaded, _error = False, f"extension not built: {_LIB_PATH} (run python build_ext.py)"
+            flag = " --debug" if _LIB_PATH.endswith("_debug.so") else ""
+            _loaded, _error = False, f"extension not built: {_LIB_PATH} (run python build_ext.py{flag})"
             return False
         try:
             torch.ops.load_library(_LIB_PATH)

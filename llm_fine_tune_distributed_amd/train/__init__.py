@@ -1,4 +1,4 @@
-from .config import SFTConfig, config_from_env
+from .config import SFTConfig, apply_overrides, config_from_env, load_config_file
 from .callbacks import (TrainerCallback, TrainerControl, TrainerState, TrainingHistoryCallback, PerplexityCallback,
                         AimCallback, JSONLLoggerCallback)
 from .trainer import SFTTrainer, TrainOutput, set_seed

@@ -144,6 +144,72 @@ class SFTConfig:
         with open(path, "w") as f:
             json.dump(self.to_dict(), f, indent=2, default=str)
 
+    def replace(self, **overrides) -> "SFTConfig":
+        """Copy with ``overrides`` applied (same alias / unknown-field handling as the constructor)."""
+        kw = self.to_dict()
+        kw.update(overrides)
+        return SFTConfig(**kw)
+
+
+def _coerce(field_type, raw: str):
+    """Parse a ``--set key=value`` string into the dataclass field's type."""
+    t = str(field_type)
+    low = raw.strip().lower()
+    if low in ("none", "null"):
+        return None
+    if "bool" in t:
+        if low in ("1", "true", "yes", "on"):
+            return True
+        if low in ("0", "false", "no", "off"):
+            return False
+        raise ValueError(f"not a boolean: {raw!r}")
+    if "List" in t or "Dict" in t:
+        return json.loads(raw)
+    if "float" in t:
+        return float(raw)
+    if "int" in t:
+        return int(float(raw))
+    return raw
+
+
+def load_config_file(path: str) -> Dict[str, Any]:
+    """Read SFTConfig overrides from a YAML (``yaml.safe_load``) or JSON file: a flat mapping of field
+    names, optionally nested under a top-level ``sft_config:`` key."""
+    with open(path) as f:
+        text = f.read()
+    if path.endswith((".yaml", ".yml")):
+        import yaml
+        data = yaml.safe_load(text) or {}
+    else:
+        data = json.loads(text)
+    if not isinstance(data, dict):
+        raise ValueError(f"{path}: expected a mapping of SFTConfig fields")
+    return dict(data.get("sft_config", data))
+
+
+def apply_overrides(cfg: SFTConfig, config_file: Optional[str] = None,
+                    sets: Optional[List[str]] = None) -> SFTConfig:
+    """Layering (lowest to highest): ``cfg`` (code defaults + env contract) < config file < ``--set k=v``.
+    Unknown keys raise here (a typo in a config file must not be silently ignored)."""
+    fields = {f.name: f.type for f in dataclasses.fields(SFTConfig)}
+    aliases = {"max_seq_length": "max_length", "evaluation_strategy": "eval_strategy"}
+    over: Dict[str, Any] = {}
+    if config_file:
+        over.update(load_config_file(config_file))
+    for item in sets or []:
+        if "=" not in item:
+            raise ValueError(f"--set expects key=value, got {item!r}")
+        k, v = item.split("=", 1)
+        k = aliases.get(k.strip(), k.strip())
+        if k not in fields:
+            raise KeyError(f"--set: unknown SFTConfig field {k!r}")
+        over[k] = _coerce(fields[k], v)
+    over = {aliases.get(k, k): v for k, v in over.items()}
+    bad = sorted(k for k in over if k not in fields)
+    if bad:
+        raise KeyError(f"unknown SFTConfig fields in overrides: {bad}")
+    return cfg.replace(**over) if over else cfg
+
 
 # SFTConfig(**kwargs) must accept legacy/unknown names like TRL does
 _orig_init = SFTConfig.__init__

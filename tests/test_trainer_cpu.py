@@ -156,3 +156,25 @@ def test_reference_freeze_policy_counts(tmp_path, tk):
     frozen0 = m.model.layers[0].self_attn.qkv_proj.detach().clone()
     t.train()
     assert torch.equal(frozen0, m.model.layers[0].self_attn.qkv_proj)
+
+
+def test_config_file_and_set_overrides(tmp_path):
+    from llm_fine_tune_distributed_amd.train import SFTConfig, apply_overrides
+    y = tmp_path / "run.yaml"
+    y.write_text("sft_config:\n  learning_rate: 3.0e-5\n  max_seq_length: 2048\n  lora_target_modules: [q_proj, v_proj]\n"
+                 "  shard_optimizer_state: true\n")
+    base = SFTConfig(learning_rate=1e-4, gradient_accumulation_steps=4)
+    cfg = apply_overrides(base, str(y), ["gradient_accumulation_steps=2", "bf16=false", "warmup_ratio=0.1",
+                                         "eval_steps=none"])
+    assert cfg.learning_rate == 3e-5 and cfg.max_length == 2048 and cfg.lora_target_modules == ["q_proj", "v_proj"]
+    assert cfg.gradient_accumulation_steps == 2 and cfg.bf16 is False and cfg.warmup_ratio == 0.1
+    assert cfg.shard_optimizer_state is True and cfg.eval_steps is None
+    assert base.gradient_accumulation_steps == 4  # the base config is not mutated
+    j = tmp_path / "run.json"
+    j.write_text('{"optim_state_dtype": "bf16"}')
+    assert apply_overrides(base, str(j)).optim_state_dtype == "bf16"
+    with pytest.raises(KeyError):
+        apply_overrides(base, None, ["learning_rat=1"])
+    (tmp_path / "bad.yaml").write_text("not_a_field: 1\n")
+    with pytest.raises(KeyError):
+        apply_overrides(base, str(tmp_path / "bad.yaml"))
