@@ -154,6 +154,9 @@ class LinearFn(Function):
     def forward(ctx, x, weight):
         ctx.save_for_backward(x)
         ctx.weight = weight
+        x2d = x.reshape(-1, x.shape[-1])
+        if _tn_plain_ok(x2d, weight):
+            return _ext.ops().gemm_tn(x2d, weight, 2).view(*x.shape[:-1], weight.shape[0])
         return torch.nn.functional.linear(x, weight)
 
     @staticmethod
@@ -312,6 +315,16 @@ def _tn_ok(x2d: torch.Tensor, w: torch.Tensor) -> bool:
     return (_TN_MODE != "0" and _ext.use_hip(x2d) and x2d.dtype == torch.bfloat16 and w.dtype == torch.bfloat16
             and x2d.dim() == 2 and x2d.shape[0] % 256 == 0 and x2d.shape[0] > 0 and x2d.shape[1] % 64 == 0
             and x2d.stride(1) == 1 and x2d.stride(0) % 8 == 0 and w.is_contiguous() and w.shape[0] % 256 == 0)
+
+
+_TN_PLAIN = os.environ.get("SFTAMD_TN_PLAIN", "1") == "1"
+
+
+def _tn_plain_ok(x2d: torch.Tensor, w: torch.Tensor) -> bool:
+    """Plain projections where the BK64 HIP GEMM beats hipBLASLt (profiles/r1_gemm_tn.md: o_proj
+    [8192 x 2048 x 2048] 0.059 vs 0.063 ms, NoPE-layer qkv [8192 x 3072 x 2048] 0.101 vs 0.119 ms): N and K
+    up to 4096. The large-N/K shapes (gate_up, down, lm_head) stay on hipBLASLt."""
+    return _TN_PLAIN and w.shape[0] <= 4096 and w.shape[1] <= 4096 and _tn_ok(x2d, w)
 
 
 class GateUpSwiGLUFn(Function):

@@ -94,3 +94,22 @@ def test_zero1_sharded_optimizer_matches_replicated():
     for a, b in zip(rep[0]["log"], z[0]["log"]):
         assert abs(a["loss"] - b["loss"]) < 1e-5
         assert abs(a["grad_norm"] - b["grad_norm"]) < 1e-4 * max(1.0, a["grad_norm"])
+
+
+def test_zero1_world4_matches_replicated():
+    """ZeRO-1 at world_size 4 (bucket shards of uneven sizes, first-bucket split, 4-way reduce-scatter /
+    all-gather) against replicated DDP at the same world size: the code path bench.py takes at N = 4 / 8."""
+    d = tempfile.mkdtemp()
+    _launch(4, 1, 2, 2, d)
+    _launch(4, 1, 2, 2, d, shard=True, tag="_z")
+    rep = [torch.load(os.path.join(d, f"r4_{r}.pt")) for r in range(4)]
+    z = [torch.load(os.path.join(d, f"r4_{r}_z.pt")) for r in range(4)]
+    assert z[0]["sharded"] == "ShardedAdamW"
+    for r in range(1, 4):
+        assert torch.equal(z[0]["params"], z[r]["params"])
+        assert torch.equal(rep[0]["params"], rep[r]["params"])
+    assert torch.allclose(z[0]["params"], rep[0]["params"], atol=1e-6, rtol=1e-5)
+    for k in ("exp_avg", "exp_avg_sq"):
+        assert torch.allclose(z[0][k], rep[0][k], atol=1e-7, rtol=1e-4)
+    for a, b in zip(rep[0]["log"], z[0]["log"]):
+        assert abs(a["loss"] - b["loss"]) < 1e-5

@@ -64,13 +64,26 @@ def test_model_fused_gemm_epilogues(mt, monkeypatch):
         calls["rope"] += 1
         return orig_rope(*a)
 
+    orig_plain = F._tn_plain_ok
+    calls["plain"] = 0
+
+    def plain(*a):
+        ok = orig_plain(*a)
+        calls["plain"] += int(ok)
+        return ok
+
     monkeypatch.setattr(F.GateUpSwiGLUFn, "apply", sw)
     monkeypatch.setattr(F.QKVRopeFn, "apply", rp)
+    monkeypatch.setattr(F, "_tn_plain_ok", plain)
     monkeypatch.setattr(F, "_TN_MODE", "1")
     l_f, g_f = _run(m, ids, labels, True)
     assert calls["swiglu"] == 4 and calls["rope"] == (3 if mt == "smollm3" else 4)  # NoPE layer 3
+    # plain BK64 GEMM: o_proj and down_proj of every layer (+ the NoPE layer's qkv)
+    assert calls["plain"] == 8 + (1 if mt == "smollm3" else 0), calls
     monkeypatch.setattr(F, "_TN_MODE", "0")
+    calls["plain"] = 0
     l_u, g_u = _run(m, ids, labels, True)
+    assert calls["plain"] == 0
     l_r, g_r = _run(m, ids, labels, False)
     assert abs(l_f.item() - l_u.item()) < 5e-3 * abs(l_u.item())
     assert abs(l_f.item() - l_r.item()) < 2e-2 * abs(l_r.item())
