@@ -1440,6 +1440,14 @@ static void check_attn_args(const at::Tensor& qkv, const at::Tensor& cu, int64_t
 
 // variant: 1 = ds_read_b64_tr_b16 transposed operand reads (default), 0 = scalar LDS gathers
 // implementation: 2 = double-buffered v2 kernels (default), 1 = v1 (single-buffered)
+// SFTAMD_ATTN_CONC=1: dq and dK/dV backward kernels concurrently on two HIP streams (they write disjoint
+// column ranges of dqkv). Measured neutral at the SmolLM3 shape (bwd 266.5 vs 262.5 us serial, end to end
+// within noise: profiles/r1_attention_microbench.txt), so serial is the default.
+static bool attn_concurrent_bwd() {
+  const char* e = std::getenv("SFTAMD_ATTN_CONC");
+  return e && e[0] == '1';
+}
+
 static int attn_impl() {
   const char* e = std::getenv("SFTAMD_ATTN_IMPL");
   if (e && e[0] == '1') return 1;
@@ -1616,9 +1624,29 @@ at::Tensor flash_bwd(const at::Tensor& dout, const at::Tensor& qkv, const at::Te
   using I8 = std::integral_constant<int, 8>;
   using B1 = std::integral_constant<int, 1>;
   using B2 = std::integral_constant<int, 2>;
+  // side stream for the dq kernel: forked after the delta kernel, joined before returning
+  hipStream_t dq_stream = cur_stream();
+  static thread_local hipEvent_t ev_fork = nullptr, ev_join = nullptr;
+  c10::optional<c10::hip::HIPStream> side;
+  if (attn_impl() >= 3 && attn_concurrent_bwd()) {
+    if (!ev_fork) {
+      C10_HIP_CHECK(hipEventCreateWithFlags(&ev_fork, hipEventDisableTiming));
+      C10_HIP_CHECK(hipEventCreateWithFlags(&ev_join, hipEventDisableTiming));
+    }
+    side = c10::hip::getStreamFromPool(false, qkv.device().index());
+    dq_stream = side->stream();
+    C10_HIP_CHECK(hipEventRecord(ev_fork, cur_stream()));
+    C10_HIP_CHECK(hipStreamWaitEvent(dq_stream, ev_fork, 0));
+  }
   auto run3 = [&](auto w) {
     constexpr int NW = decltype(w)::value;
     const int rep = nq / nkv;
+    // dq first: on the side stream it starts filling the GPU while dK/dV is enqueued
+    dim3 gq3((max_seqlen + NW * 16 - 1) / (NW * 16), nq, nseq);
+    attn::bwd_dq3_kernel<NW><<<gq3, NW * 64, 0, dq_stream>>>(
+        (const u16*)qkv.data_ptr(), (const u16*)dout.data_ptr(), lse.data_ptr<float>(), delta.data_ptr<float>(),
+        cu_c.data_ptr<int>(), (u16*)dqkv.data_ptr(), nq, nkv, total, sl2, (float)scale, causal ? 1 : 0);
+    SFT_LAUNCH_CHECK();
     at::Tensor part;
     if (rep > 1) part = at::empty({(long)rep * total * 2 * nkv * hd}, qkv.options().dtype(at::kFloat));
     dim3 gk3((max_seqlen + 63) / 64, nq, nseq);
@@ -1634,14 +1662,13 @@ at::Tensor flash_bwd(const at::Tensor& dout, const at::Tensor& qkv, const at::Te
                                                                nq, nkv, rep, (float)scale);
       SFT_LAUNCH_CHECK();
     }
-    dim3 gq3((max_seqlen + NW * 16 - 1) / (NW * 16), nq, nseq);
-    attn::bwd_dq3_kernel<NW><<<gq3, NW * 64, 0, cur_stream()>>>(
-        (const u16*)qkv.data_ptr(), (const u16*)dout.data_ptr(), lse.data_ptr<float>(), delta.data_ptr<float>(),
-        cu_c.data_ptr<int>(), (u16*)dqkv.data_ptr(), nq, nkv, total, sl2, (float)scale, causal ? 1 : 0);
-    SFT_LAUNCH_CHECK();
   };
   if (attn_impl() >= 3) {
     if (nw == 4) run3(I4()); else run3(I8());
+    if (side) {  // join: everything after this op on the current stream sees dq
+      C10_HIP_CHECK(hipEventRecord(ev_join, dq_stream));
+      C10_HIP_CHECK(hipStreamWaitEvent(cur_stream(), ev_join, 0));
+    }
   } else if (attn_impl() == 2) {
     if (!attn_variant()) run2(std::false_type(), I8(), B2());
     else if (nw == 8 && nbuf == 2) run2(std::true_type(), I8(), B2());

@@ -213,6 +213,28 @@ def test_flash_attention_deferred_rescale_branch(impl):
     assert rel_err(out, o_ref) < 2e-2
 
 
+def test_flash_attention_concurrent_bwd_bitwise(monkeypatch):
+    """dq on a side stream concurrently with dK/dV (default) == the serial launch order, bit for bit, and the
+    result is complete when the op returns on the caller's stream (no extra sync)."""
+    monkeypatch.setenv("SFTAMD_ATTN_IMPL", "3")
+    monkeypatch.setenv("SFTAMD_ATTN_CFG", "")
+    torch.manual_seed(3)
+    D, nq, nkv = 128, 16, 4
+    lens = [512, 300, 17, 512]
+    cu = torch.tensor([0] + list(torch.tensor(lens).cumsum(0)), dtype=torch.int32, device=DEV)
+    M = int(cu[-1])
+    qkv = torch.randn(M, (nq + 2 * nkv) * D, device=DEV, dtype=torch.bfloat16)
+    scale = 1 / math.sqrt(D)
+    out, lse = _ext.ops().flash_fwd(qkv, cu, max(lens), nq, nkv, D, scale, True)
+    dout = torch.randn_like(out)
+    res = {}
+    for conc in ("0", "1"):
+        monkeypatch.setenv("SFTAMD_ATTN_CONC", conc)
+        d = _ext.ops().flash_bwd(dout, qkv, out, lse, cu, max(lens), nq, nkv, D, scale, True)
+        res[conc] = (d * 1).clone()  # consumed on the current stream right away
+    assert torch.equal(res["0"], res["1"])
+
+
 @pytest.mark.parametrize("impl", ["2", "1"])
 def test_flash_attention_smollm3_shape(impl):
     _attn_case([512] * 4, 16, 4, True, "1", impl)

@@ -35,13 +35,16 @@ def timeit(fn, n=20):
     return statistics.median(ts)
 
 
-CFGS = [("1", ""), ("2", "8,1"), ("3", "8,1"), ("3", "4,1"), ("4", "")]
+CFGS = [("1", ""), ("2", "8,1"), ("3", "8,1"), ("3", "4,1"), ("4", ""), ("3", "8,1,serial")]
+if os.environ.get("ATTN_QUICK"):
+    CFGS = [("3", "8,1"), ("3", "8,1,serial")]
 res = {}
 ref = None
 for rnd in range(3):
     for impl, cfg in CFGS:
         os.environ["SFTAMD_ATTN_IMPL"] = impl
-        os.environ["SFTAMD_ATTN_CFG"] = cfg
+        os.environ["SFTAMD_ATTN_CFG"] = cfg.replace(",serial", "")
+        os.environ["SFTAMD_ATTN_CONC"] = "0" if cfg.endswith("serial") else "1"
         out, lse = ops.flash_fwd(qkv, cu, T, NQ, NKV, D, sc, True)
         dq = ops.flash_bwd(dout, qkv, out, lse, cu, T, NQ, NKV, D, sc, True)
         if ref is None:
