@@ -12,42 +12,91 @@ static inline int ew_grid(long nvec) {
 }
 
 // ------------------------------------------------------------------------------ SwiGLU
-__global__ __launch_bounds__(256) void swiglu_fwd_kernel(const u16* __restrict__ gu, u16* __restrict__ out, long M,
-                                                         int I) {
-  const int vpr = I / 8;  // vectors per row
-  const long n = M * vpr;
-  for (long v = blockIdx.x * 256L + threadIdx.x; v < n; v += (long)gridDim.x * 256) {
-    const long m = v / vpr;
-    const int c = (int)(v - m * vpr) * 8;
-    float g[8], u[8], o[8];
-    unpack8(*(const uint4*)(gu + m * 2 * I + c), g);
-    unpack8(*(const uint4*)(gu + m * 2 * I + I + c), u);
+// Streaming at HBM rate needs many 16-byte loads in flight per wave: each thread handles UNR vectors per
+// grid-stride step and issues all their loads before any math or store. Index math stays 32-bit (host
+// checks M * I / 8 < 2^31): a 64-bit division per vector is a long software sequence on the VALU.
+constexpr int SW_UNR = 4;  // max unroll (grid sizing / index bound)
+
+template <int SW_UNR>
+__global__ __launch_bounds__(256) void swiglu_fwd_kernel(const u16* __restrict__ gu, u16* __restrict__ out, int n,
+                                                         int vpr) {
+  const int I = vpr * 8;
+  const int stride = gridDim.x * 256 * SW_UNR;
+  for (int v0 = blockIdx.x * 256 * SW_UNR + threadIdx.x; v0 < n; v0 += stride) {
+    uint4 ga[SW_UNR], ua[SW_UNR];
+    long orow[SW_UNR];
 #pragma unroll
-    for (int i = 0; i < 8; ++i) o[i] = g[i] / (1.f + __expf(-g[i])) * u[i];
-    *(uint4*)(out + m * I + c) = pack8(o);
+    for (int k = 0; k < SW_UNR; ++k) {
+      const int v = v0 + k * 256;
+      const int m = v / vpr, c = (v - m * vpr) * 8;
+      orow[k] = (long)m * I + c;
+      if (v < n) {
+        const u16* src = gu + (long)m * 2 * I + c;
+        ga[k] = *(const uint4*)src;
+        ua[k] = *(const uint4*)(src + I);
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < SW_UNR; ++k) {
+      if (v0 + k * 256 < n) {
+        float g[8], u[8], o[8];
+        unpack8(ga[k], g);
+        unpack8(ua[k], u);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) o[i] = g[i] / (1.f + __expf(-g[i])) * u[i];
+        *(uint4*)(out + orow[k]) = pack8(o);
+      }
+    }
   }
 }
 
+template <int SW_UNR>
 __global__ __launch_bounds__(256) void swiglu_bwd_kernel(const u16* __restrict__ dy, const u16* __restrict__ gu,
-                                                         u16* __restrict__ dgu, long M, int I) {
-  const int vpr = I / 8;
-  const long n = M * vpr;
-  for (long v = blockIdx.x * 256L + threadIdx.x; v < n; v += (long)gridDim.x * 256) {
-    const long m = v / vpr;
-    const int c = (int)(v - m * vpr) * 8;
-    float g[8], u[8], d[8], dg[8], du[8];
-    unpack8(*(const uint4*)(gu + m * 2 * I + c), g);
-    unpack8(*(const uint4*)(gu + m * 2 * I + I + c), u);
-    unpack8(*(const uint4*)(dy + m * I + c), d);
+                                                         u16* __restrict__ dgu, int n, int vpr) {
+  const int I = vpr * 8;
+  const int stride = gridDim.x * 256 * SW_UNR;
+  for (int v0 = blockIdx.x * 256 * SW_UNR + threadIdx.x; v0 < n; v0 += stride) {
+    uint4 ga[SW_UNR], ua[SW_UNR], da[SW_UNR];
+    long grow[SW_UNR];
 #pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      const float s = 1.f / (1.f + __expf(-g[i]));
-      du[i] = d[i] * g[i] * s;
-      dg[i] = d[i] * u[i] * s * (1.f + g[i] * (1.f - s));
+    for (int k = 0; k < SW_UNR; ++k) {
+      const int v = v0 + k * 256;
+      const int m = v / vpr, c = (v - m * vpr) * 8;
+      grow[k] = (long)m * 2 * I + c;
+      if (v < n) {
+        ga[k] = *(const uint4*)(gu + grow[k]);
+        ua[k] = *(const uint4*)(gu + grow[k] + I);
+        da[k] = *(const uint4*)(dy + (long)m * I + c);
+      }
     }
-    *(uint4*)(dgu + m * 2 * I + c) = pack8(dg);
-    *(uint4*)(dgu + m * 2 * I + I + c) = pack8(du);
+#pragma unroll
+    for (int k = 0; k < SW_UNR; ++k) {
+      if (v0 + k * 256 < n) {
+        float g[8], u[8], d[8], dg[8], du[8];
+        unpack8(ga[k], g);
+        unpack8(ua[k], u);
+        unpack8(da[k], d);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          const float sg = 1.f / (1.f + __expf(-g[i]));
+          du[i] = d[i] * g[i] * sg;
+          dg[i] = d[i] * u[i] * sg * (1.f + g[i] * (1.f - sg));
+        }
+        *(uint4*)(dgu + grow[k]) = pack8(dg);
+        *(uint4*)(dgu + grow[k] + I) = pack8(du);
+      }
+    }
   }
+}
+
+static inline int sw_unroll() {  // SFTAMD_SWIGLU_UNR = 1 | 2 | 4 (A/B knob)
+  const char* e = std::getenv("SFTAMD_SWIGLU_UNR");
+  return e && e[0] == '1' ? 1 : (e && e[0] == '2' ? 2 : 4);
+}
+
+static inline int sw_grid(long nvec, int unr) {
+  long g = (nvec + 256L * unr - 1) / (256L * unr);
+  return (int)std::max<long>(1, std::min<long>(g, 256L * 8));
 }
 
 at::Tensor swiglu_fwd(const at::Tensor& gu) {
@@ -60,7 +109,22 @@ at::Tensor swiglu_fwd(const at::Tensor& gu) {
   sizes.back() = I;
   auto out = at::empty(sizes, gu.options());
   if (M == 0) return out;
-  swiglu_fwd_kernel<<<ew_grid(M * I / 8), 256, 0, cur_stream()>>>((const u16*)gu.data_ptr(), (u16*)out.data_ptr(), M, I);
+  const long nvec = M * I / 8;
+  SFT_CHECK(nvec < (1L << 31) - 256L * 8 * 256 * SW_UNR, "swiglu: tensor too large for 32-bit indexing");
+  const int unr = sw_unroll();
+  switch (unr) {
+    case 1:
+      swiglu_fwd_kernel<1><<<sw_grid(nvec, 1), 256, 0, cur_stream()>>>((const u16*)gu.data_ptr(), (u16*)out.data_ptr(),
+                                                                       (int)nvec, I / 8);
+      break;
+    case 2:
+      swiglu_fwd_kernel<2><<<sw_grid(nvec, 2), 256, 0, cur_stream()>>>((const u16*)gu.data_ptr(), (u16*)out.data_ptr(),
+                                                                       (int)nvec, I / 8);
+      break;
+    default:
+      swiglu_fwd_kernel<4><<<sw_grid(nvec, 4), 256, 0, cur_stream()>>>((const u16*)gu.data_ptr(), (u16*)out.data_ptr(),
+                                                                       (int)nvec, I / 8);
+  }
   SFT_LAUNCH_CHECK();
   return out;
 }
@@ -70,10 +134,18 @@ at::Tensor swiglu_bwd(const at::Tensor& dy, const at::Tensor& gu) {
   SFT_CHECK_CONTIG(gu);
   const int I = gu.size(-1) / 2;
   const long M = gu.numel() / (2 * I);
+  SFT_CHECK(I % 8 == 0 && dy.numel() == M * I, "swiglu_bwd: shapes");
   auto dgu = at::empty_like(gu);
   if (M == 0) return dgu;
-  swiglu_bwd_kernel<<<ew_grid(M * I / 8), 256, 0, cur_stream()>>>((const u16*)dy.data_ptr(), (const u16*)gu.data_ptr(),
-                                                                   (u16*)dgu.data_ptr(), M, I);
+  const long nvec = M * I / 8;
+  SFT_CHECK(nvec < (1L << 31) - 256L * 8 * 256 * SW_UNR, "swiglu: tensor too large for 32-bit indexing");
+  const u16 *dp = (const u16*)dy.data_ptr(), *gp = (const u16*)gu.data_ptr();
+  u16* op = (u16*)dgu.data_ptr();
+  switch (sw_unroll()) {
+    case 1: swiglu_bwd_kernel<1><<<sw_grid(nvec, 1), 256, 0, cur_stream()>>>(dp, gp, op, (int)nvec, I / 8); break;
+    case 2: swiglu_bwd_kernel<2><<<sw_grid(nvec, 2), 256, 0, cur_stream()>>>(dp, gp, op, (int)nvec, I / 8); break;
+    default: swiglu_bwd_kernel<4><<<sw_grid(nvec, 4), 256, 0, cur_stream()>>>(dp, gp, op, (int)nvec, I / 8);
+  }
   SFT_LAUNCH_CHECK();
   return dgu;
 }

@@ -89,9 +89,10 @@ def test_rmsnorm_bwd_direct_dw_out():
     assert rel_err(out, 2 * dw_ref) < 1e-2
 
 
-def test_swiglu():
+@pytest.mark.parametrize("M,I", [(777, 1376), (1, 8), (3, 24), (2048, 11008)])
+def test_swiglu(M, I):
     torch.manual_seed(0)
-    gu = torch.randn(777, 2 * 1376, device=DEV, dtype=torch.bfloat16)
+    gu = torch.randn(M, 2 * I, device=DEV, dtype=torch.bfloat16)
     out = _ext.ops().swiglu_fwd(gu)
     assert rel_err(out, ref.swiglu(gu.float())) < 1e-2
     dy = torch.randn_like(out)
