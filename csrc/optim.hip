@@ -102,7 +102,9 @@ struct Moments {
 
 constexpr unsigned SEED_M = 0x68E31DA4u, SEED_V = 0xB5297A4Du;
 
-template <bool MASTER, bool SR, bool BF16M>
+// UNR vectors of 8 elements per thread per grid-stride step, all loads issued before any math: the update
+// streams 22 (fp32 moments) or 14 (bf16) bytes per parameter, so bytes in flight per wave set its speed.
+template <bool MASTER, bool SR, bool BF16M, int UNR>
 __global__ __launch_bounds__(256) void adamw_kernel(u16* __restrict__ p, const u16* __restrict__ g,
                                                     float* __restrict__ master, void* __restrict__ mom,
                                                     void* __restrict__ var, const float* __restrict__ coef, long n,
@@ -111,27 +113,42 @@ __global__ __launch_bounds__(256) void adamw_kernel(u16* __restrict__ p, const u
   using Mo = Moments<BF16M>;
   const float c = coef[0];
   const long nv = n / 8;
-  for (long v = blockIdx.x * 256L + threadIdx.x; v < nv; v += (long)gridDim.x * 256) {
-    const long o = v * 8;
-    float gf[8], w[8], mm[8], vv[8];
-    unpack8(*(const uint4*)(g + o), gf);
-    if (MASTER) {
-      *(float4*)&w[0] = *(const float4*)(master + o);
-      *(float4*)&w[4] = *(const float4*)(master + o + 4);
-    } else {
-      unpack8(*(const uint4*)(p + o), w);
-    }
-    Mo::load(mom, o, mm);
-    Mo::load(var, o, vv);
+  const long step = (long)gridDim.x * 256 * UNR;
+  for (long v0 = blockIdx.x * 256L * UNR + threadIdx.x; v0 < nv; v0 += step) {
+    float gf[UNR][8], w[UNR][8], mm[UNR][8], vv[UNR][8];
 #pragma unroll
-    for (int i = 0; i < 8; ++i) adam_elem(w[i], gf[i] * c, mm[i], vv[i], lr, b1, b2, eps, wd, rbc1, rsbc2, omb1, omb2);
-    if (MASTER) {
-      *(float4*)(master + o) = *(float4*)&w[0];
-      *(float4*)(master + o + 4) = *(float4*)&w[4];
+    for (int k = 0; k < UNR; ++k) {
+      const long v = v0 + k * 256;
+      if (v < nv) {
+        const long o = v * 8;
+        unpack8(*(const uint4*)(g + o), gf[k]);
+        if (MASTER) {
+          *(float4*)&w[k][0] = *(const float4*)(master + o);
+          *(float4*)&w[k][4] = *(const float4*)(master + o + 4);
+        } else {
+          unpack8(*(const uint4*)(p + o), w[k]);
+        }
+        Mo::load(mom, o, mm[k]);
+        Mo::load(var, o, vv[k]);
+      }
     }
-    Mo::store(mom, o, mm, SR, idx0 + o, seed ^ SEED_M);
-    Mo::store(var, o, vv, SR, idx0 + o, seed ^ SEED_V);
-    *(uint4*)(p + o) = SR ? pack8_sr(w, idx0 + o, seed) : pack8(w);
+#pragma unroll
+    for (int k = 0; k < UNR; ++k) {
+      const long v = v0 + k * 256;
+      if (v < nv) {
+        const long o = v * 8;
+#pragma unroll
+        for (int i = 0; i < 8; ++i)
+          adam_elem(w[k][i], gf[k][i] * c, mm[k][i], vv[k][i], lr, b1, b2, eps, wd, rbc1, rsbc2, omb1, omb2);
+        if (MASTER) {
+          *(float4*)(master + o) = *(float4*)&w[k][0];
+          *(float4*)(master + o + 4) = *(float4*)&w[k][4];
+        }
+        Mo::store(mom, o, mm[k], SR, idx0 + o, seed ^ SEED_M);
+        Mo::store(var, o, vv[k], SR, idx0 + o, seed ^ SEED_V);
+        *(uint4*)(p + o) = SR ? pack8_sr(w[k], idx0 + o, seed) : pack8(w[k]);
+      }
+    }
   }
   for (long i = nv * 8 + blockIdx.x * 256L + threadIdx.x; i < n; i += (long)gridDim.x * 256) {
     float w = MASTER ? master[i] : bf2f(p[i]);
@@ -142,6 +159,11 @@ __global__ __launch_bounds__(256) void adamw_kernel(u16* __restrict__ p, const u
     Mo::store1(var, i, vr, SR, idx0 + i, seed ^ SEED_V);
     p[i] = SR ? f2bf_sr(w, sr_hash(idx0 + i, seed)) : f2bf(w);
   }
+}
+
+static long env_long(const char* name, long dflt) {
+  const char* e = std::getenv(name);
+  return e && e[0] ? atol(e) : dflt;
 }
 
 void adamw_flat(at::Tensor param, const at::Tensor& grad, const c10::optional<at::Tensor>& master, at::Tensor exp_avg,
@@ -158,7 +180,11 @@ void adamw_flat(at::Tensor param, const at::Tensor& grad, const c10::optional<at
   const long n = param.numel();
   SFT_CHECK(grad.numel() == n && exp_avg.numel() == n && exp_avg_sq.numel() == n, "sizes");
   if (n == 0) return;
-  int grid = (int)std::min<long>(std::max<long>(1, (n / 8 + 255) / 256), 2048);
+  // launch shape (A/B knobs, read per call): SFTAMD_ADAM_UNR vectors per thread step (1 | 2),
+  // SFTAMD_ADAM_BLOCKS block cap (fewer blocks measured slower under the overlapped forward: gpu_run49)
+  const int unr = env_long("SFTAMD_ADAM_UNR", 2) == 1 ? 1 : 2;
+  const long cap = std::max(1L, env_long("SFTAMD_ADAM_BLOCKS", 2048));
+  int grid = (int)std::min<long>(std::max<long>(1, (n / 8 + 256L * unr - 1) / (256L * unr)), cap);
   const float rbc1 = (float)(1.0 / bc1), rsbc2 = (float)(1.0 / std::sqrt(bc2));
   const bool has_master = master.has_value() && master->defined();
   if (has_master)
@@ -168,10 +194,15 @@ void adamw_flat(at::Tensor param, const at::Tensor& grad, const c10::optional<at
   SFT_CHECK(clip_coef.scalar_type() == at::kFloat && clip_coef.numel() >= 1 && clip_coef.is_cuda(), "clip_coef");
   auto go = [&](auto ms, auto sr, auto bm) {
     constexpr bool M = decltype(ms)::value, S = decltype(sr)::value, B = decltype(bm)::value;
-    adamw_kernel<M, S, B><<<grid, 256, 0, cur_stream()>>>(
-        (u16*)param.data_ptr(), (const u16*)grad.data_ptr(), mp, exp_avg.data_ptr(), exp_avg_sq.data_ptr(),
-        clip_coef.data_ptr<float>(), n, (float)lr, (float)beta1, (float)beta2, (float)eps, (float)weight_decay, rbc1,
-        rsbc2, (float)(1.0 - beta1), (float)(1.0 - beta2), seed, (long)sr_offset);
+    auto launch = [&](auto u) {
+      constexpr int U = decltype(u)::value;
+      adamw_kernel<M, S, B, U><<<grid, 256, 0, cur_stream()>>>(
+          (u16*)param.data_ptr(), (const u16*)grad.data_ptr(), mp, exp_avg.data_ptr(), exp_avg_sq.data_ptr(),
+          clip_coef.data_ptr<float>(), n, (float)lr, (float)beta1, (float)beta2, (float)eps, (float)weight_decay,
+          rbc1, rsbc2, (float)(1.0 - beta1), (float)(1.0 - beta2), seed, (long)sr_offset);
+    };
+    if (unr == 1) launch(std::integral_constant<int, 1>());
+    else launch(std::integral_constant<int, 2>());
   };
   auto go2 = [&](auto ms, auto sr) {
     if (bf16m) go(ms, sr, std::true_type());

@@ -165,6 +165,9 @@ class DataLoader:
             if k < skip:
                 continue
             b = self.collator(self.ds, idx)
+            # the token count travels with the batch (pinned, non-blocking H2D): building it on the device
+            # later from a Python number is a pageable copy that stalls the host at every step
+            b["num_items_t"] = torch.tensor([float(b["num_items"])], dtype=torch.float32)
             if self.pin:
                 b = {k2: (v.pin_memory() if torch.is_tensor(v) else v) for k2, v in b.items()}
             yield b

@@ -175,6 +175,17 @@ class CausalLM(nn.Module):
         return n
 
     # ------------------------------------------------------------------ forward
+    def _padded_meta(self, B: int, T: int, dev):
+        cache = self.__dict__.setdefault("_meta_cache", {})
+        key = (B, T, str(dev), self.inv_freq.data_ptr())
+        hit = cache.get(key)
+        if hit is None:
+            if len(cache) >= 8:
+                cache.clear()
+            cu = torch.arange(0, (B + 1) * T, T, dtype=torch.int32, device=dev)
+            hit = cache[key] = (cu, T, self.rope_tables(torch.arange(T, device=dev).expand(B, T)))
+        return hit
+
     def rope_tables(self, position_ids: torch.Tensor):
         freqs = position_ids.reshape(-1).float()[:, None] * self.inv_freq[None, :].to(position_ids.device)
         return freqs.cos().contiguous(), freqs.sin().contiguous()
@@ -191,6 +202,10 @@ class CausalLM(nn.Module):
         """
         cfg = self.config
         dev = input_ids.device
+        rope_cs = None
+        if input_ids.dim() == 2 and cu_seqlens is None and position_ids is None:
+            # padded batches of one shape repeat every step: cu_seqlens / RoPE tables are built once
+            cu_seqlens, max_seqlen, rope_cs = self._padded_meta(input_ids.shape[0], input_ids.shape[1], dev)
         if input_ids.dim() == 2:
             B, T = input_ids.shape
             if cu_seqlens is None:
@@ -214,7 +229,8 @@ class CausalLM(nn.Module):
             labels = labels.reshape(-1)
             if shift_labels:
                 labels = _shift_packed(labels, cu_seqlens)
-        rope_cs = self.rope_tables(position_ids)
+        if rope_cs is None:
+            rope_cs = self.rope_tables(position_ids)
 
         x = ops.embedding(ids, self.model.embed_tokens)
         residual = None

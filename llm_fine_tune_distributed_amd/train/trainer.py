@@ -170,7 +170,12 @@ class SFTTrainer:
         return kw
 
     def global_num_items(self, micro: List[Dict]) -> torch.Tensor:
-        n = torch.tensor([float(sum(b["num_items"] for b in micro))], device=self.dist.device)
+        if all(torch.is_tensor(b.get("num_items_t")) for b in micro):
+            n = micro[0]["num_items_t"].to(self.dist.device, non_blocking=True).clone()
+            for b in micro[1:]:
+                n += b["num_items_t"].to(self.dist.device, non_blocking=True)
+        else:
+            n = torch.tensor([float(sum(b["num_items"] for b in micro))], device=self.dist.device)
         if self.args.average_tokens_across_devices:
             all_reduce_sum_(n)
         return n.clamp(min=1.0)
