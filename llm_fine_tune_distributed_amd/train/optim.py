@@ -128,7 +128,13 @@ class FlatAdamW:
         self.step_count += 1
         e = self.engine
         self.synchronize()
-        norm, coef = ops.grad_norm_flat([e.grad_flat], max_grad_norm if max_grad_norm else 0.0)
+        norm2 = e.grad_norm_sq()  # computed bucket by bucket during backward (replicated buckets)
+        if norm2 is not None:
+            norm = norm2.sqrt()
+            coef = ((max_grad_norm / (norm + 1e-6)).clamp(max=1.0) if max_grad_norm and max_grad_norm > 0
+                    else torch.ones_like(norm))
+        else:
+            norm, coef = ops.grad_norm_flat([e.grad_flat], max_grad_norm if max_grad_norm else 0.0)
         self.last_grad_norm = norm
         b1, b2 = self.betas
 
@@ -277,8 +283,10 @@ class ShardedAdamW(FlatAdamW):
         e = self.engine
         self.synchronize()
         # global grad norm: sum of squares of the owned (reduced) slices, all-reduced (one float)
-        owned = [e.grad_flat[s:t] for _, s, t, _, _ in self.slices if t > s]
-        norm2 = ops.sumsq_list(owned).reshape(1)
+        norm2 = e.grad_norm_sq()  # owned slices, summed bucket by bucket during backward
+        if norm2 is None:
+            owned = [e.grad_flat[s:t] for _, s, t, _, _ in self.slices if t > s]
+            norm2 = ops.sumsq_list(owned).reshape(1)
         if e.world_size > 1:
             dist.all_reduce(norm2, op=dist.ReduceOp.SUM, group=e.pg)
         norm = norm2.sqrt()

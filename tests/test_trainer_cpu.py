@@ -178,3 +178,27 @@ def test_config_file_and_set_overrides(tmp_path):
     (tmp_path / "bad.yaml").write_text("not_a_field: 1\n")
     with pytest.raises(KeyError):
         apply_overrides(base, str(tmp_path / "bad.yaml"))
+
+
+@pytest.mark.parametrize("policy,ckpt", [("full", False), ("full", True), ("lora", False), ("last_n_layers", True)])
+def test_grad_norm_from_backward_partials(tmp_path, tk, monkeypatch, policy, ckpt):
+    """The gradient norm summed bucket by bucket during backward (default) equals the post-backward full
+    pass (SFTAMD_NORM_IN_BWD=0), with GA 2, gradient checkpointing and every freeze policy; updates match."""
+    rows = generate_qa(16, seed=1)
+    res = {}
+    for flag in ("1", "0"):
+        monkeypatch.setenv("SFTAMD_NORM_IN_BWD", flag)
+        args = SFTConfig(output_dir=str(tmp_path / flag), per_device_train_batch_size=4, gradient_accumulation_steps=2,
+                         learning_rate=1e-3, max_grad_norm=0.5, max_steps=2, logging_steps=1, save_strategy="no",
+                         jsonl_log=False, gradient_checkpointing=ckpt, freeze_policy=policy, lora_r=4,
+                         ddp_bucket_cap_mb=0.05, ddp_first_bucket_mb=0.01, seed=3)
+        h = TrainingHistoryCallback()
+        t = SFTTrainer(model=_model(seed=2), args=args, train_dataset=rows, processing_class=tk, callbacks=[h])
+        assert t.engine.track_norm == (flag == "1")
+        t.train()
+        res[flag] = ([x["grad_norm"] for x in h.history if "grad_norm" in x], t.engine.param_flat.clone())
+    (n1, p1), (n0, p0) = res["1"], res["0"]
+    assert len(n1) == 2 and all(a > 0 for a in n1)
+    for a, b in zip(n1, n0):
+        assert abs(a - b) <= 1e-5 * max(1.0, b), (a, b)
+    assert torch.allclose(p1, p0, atol=1e-6, rtol=1e-5)
