@@ -725,7 +725,8 @@ static void check_tn(const at::Tensor& a, const at::Tensor& w) {
 
 // cfg: 0 = 256x256 BK32 ring (NS 5), 1 = 256x128 BK32 ring (NS 6), 2 = 256x256 BK64 (NS 2; the fastest on the
 // SmolLM3 shapes, tools/bench_gemm_tn.py), 3 = BK64 early-release ring, 4 = BK64 with a pinned MFMA/DS/DMA
-// interleave (3 and 4 measured slower; kept for the microbench)
+// interleave (3 and 4 measured slower; kept for the microbench), 5 = BK64 transposed-C epilogue, 6 / 7 = BK64
+// 256x128 tiles with 3 / 2 LDS stages (twice the workgroups: 3 full waves on qkv's 384-tile grid)
 at::Tensor gemm_tn(const at::Tensor& a, const at::Tensor& w, int64_t cfg) {
   check_tn(a, w);
   const int M = a.size(0), N = w.size(0);
@@ -741,6 +742,10 @@ at::Tensor gemm_tn(const at::Tensor& a, const at::Tensor& w, int64_t cfg) {
   } else if (cfg == 5) {  // BK64, transposed-C fragments, packed-bf16 LDS epilogue
     SFT_CHECK(N % 256 == 0 && a.size(1) % 64 == 0, "gemm_tn BK64: N % 256, K % 64");
     tn::launch2<256, 256, 2, 4, 2, tn::EPI_PLAIN, 3>(a, w, N, ea);
+  } else if (cfg == 6 || cfg == 7) {  // BK64 256x128 tiles (64x64 per wave): 3 (cfg 6) or 2 LDS stages
+    SFT_CHECK(N % 128 == 0 && a.size(1) % 64 == 0, "gemm_tn BK64 256x128: N % 128, K % 64");
+    if (cfg == 6) tn::launch2<256, 128, 4, 2, 3, tn::EPI_PLAIN>(a, w, N, ea);
+    else tn::launch2<256, 128, 4, 2, 2, tn::EPI_PLAIN>(a, w, N, ea);
   } else if (cfg == 4) {  // BK64 with sched_group_barrier interleave pinned (measured slower: diagnostics)
     SFT_CHECK(N % 256 == 0 && a.size(1) % 64 == 0, "gemm_tn BK64: N % 256, K % 64");
     tn::launch2<256, 256, 2, 4, 2, tn::EPI_PLAIN, 2>(a, w, N, ea);
@@ -785,6 +790,8 @@ at::Tensor gemm_tn_rope(const at::Tensor& x, const at::Tensor& w, const at::Tens
   if (cfg == 1) tn::launch<256, 128, 4, 2, 6, tn::EPI_ROPE>(x, w, N, ea);
   else if (cfg == 2 && x.size(1) % 64 == 0) tn::launch2<256, 256, 2, 4, 2, tn::EPI_ROPE>(x, w, N, ea);
   else if (cfg == 5 && x.size(1) % 64 == 0) tn::launch2<256, 256, 2, 4, 2, tn::EPI_ROPE, 3>(x, w, N, ea);
+  else if (cfg == 6 && x.size(1) % 64 == 0) tn::launch2<256, 128, 4, 2, 3, tn::EPI_ROPE>(x, w, N, ea);
+  else if (cfg == 7 && x.size(1) % 64 == 0) tn::launch2<256, 128, 4, 2, 2, tn::EPI_ROPE>(x, w, N, ea);
   else tn::launch<256, 256, 2, 4, 5, tn::EPI_ROPE>(x, w, N, ea);
   return c;
 }

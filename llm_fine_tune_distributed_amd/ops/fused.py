@@ -156,7 +156,8 @@ class LinearFn(Function):
         ctx.weight = weight
         x2d = x.reshape(-1, x.shape[-1])
         if _tn_plain_ok(x2d, weight):
-            return _ext.ops().gemm_tn(x2d, weight, 2).view(*x.shape[:-1], weight.shape[0])
+            return _ext.ops().gemm_tn(x2d, weight, _tn_cfg(x2d.shape[0], weight.shape[0])).view(
+                *x.shape[:-1], weight.shape[0])
         return torch.nn.functional.linear(x, weight)
 
     @staticmethod
@@ -320,6 +321,14 @@ def _tn_ok(x2d: torch.Tensor, w: torch.Tensor) -> bool:
 _TN_PLAIN = os.environ.get("SFTAMD_TN_PLAIN", "1") == "1"
 
 
+def _tn_cfg(M: int, N: int) -> int:
+    """BK64 tile for a forward GEMM: 256x256 (cfg 2) when its grid fills whole waves of the 256 CUs,
+    else 256x128 with 3 LDS stages (cfg 6): qkv [8192 x 3072] is 384 big tiles = 1.5 waves but 768 small
+    ones = 3 (0.095 vs 0.102 ms; o_proj's 256 tiles stay on 256x256: 0.058 vs 0.065 ms, r1_gemm_tn.md)."""
+    tiles = (M // 256) * (N // 256)
+    return 2 if (N % 256 == 0 and tiles % 256 == 0) or N % 128 != 0 else 6
+
+
 def _tn_plain_ok(x2d: torch.Tensor, w: torch.Tensor) -> bool:
     """Plain projections where the BK64 HIP GEMM beats hipBLASLt (profiles/r1_gemm_tn.md: o_proj
     [8192 x 2048 x 2048] 0.059 vs 0.063 ms, NoPE-layer qkv [8192 x 3072 x 2048] 0.101 vs 0.119 ms): N and K
@@ -367,7 +376,7 @@ class QKVRopeFn(Function):
     @staticmethod
     def forward(ctx, x, weight, cos, sin, n_q, n_kv, head_dim):
         x2d = x.reshape(-1, x.shape[-1])
-        qkv = _ext.ops().gemm_tn_rope(x2d, weight, cos, sin, (n_q + n_kv) * head_dim, 2)
+        qkv = _ext.ops().gemm_tn_rope(x2d, weight, cos, sin, (n_q + n_kv) * head_dim, _tn_cfg(x2d.shape[0], weight.shape[0]))
         ctx.save_for_backward(x2d, cos, sin)
         ctx.weight = weight
         ctx.dims = (n_q, n_kv, head_dim)

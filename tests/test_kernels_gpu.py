@@ -373,7 +373,7 @@ def test_lora_fwd_bwd_kernels(K, R, p):
     assert (dx.float() - dxr.float()).abs().max().item() < 3e-2
 
 
-@pytest.mark.parametrize("cfg", [0, 1, 2, 3, 5])
+@pytest.mark.parametrize("cfg", [0, 1, 2, 3, 5, 6, 7])
 @pytest.mark.parametrize("M,N,K", [(256, 256, 64), (512, 768, 256), (768, 512, 2112)])
 def test_gemm_tn_plain(cfg, M, N, K):
     torch.manual_seed(0)
@@ -406,7 +406,7 @@ def test_gemm_tn_swiglu(I, K):
     assert rel_err(act, _ext.ops().swiglu_fwd(gu)) < 2e-3
 
 
-@pytest.mark.parametrize("cfg", [0, 1, 2, 5])
+@pytest.mark.parametrize("cfg", [0, 1, 2, 5, 6, 7])
 def test_gemm_tn_rope(cfg):
     torch.manual_seed(0)
     M, K, nq, nkv, D = 512, 256, 2, 1, 128

@@ -46,8 +46,9 @@ def rel(a_, b_):
 
 
 print(f"M = {M}")
-print("| shape | N | K | blas ms (TF/s) | tn 256x256 BK32 | tn 256x128 BK32 | tn 256x256 BK64 | BK64 early | BK64 TRC-epi | max rel err |")
-print("|---|---:|---:|---:|---:|---:|---:|---:|---:|---:|")
+print("| shape | N | K | blas ms (TF/s) | tn 256x256 BK32 | tn 256x128 BK32 | tn 256x256 BK64 | BK64 TRC-epi | "
+      "BK64 256x128 NS3 | BK64 256x128 NS2 | max rel err |")
+print("|---|---:|---:|---:|---:|---:|---:|---:|---:|---:|---:|")
 for name, N, K in [("qkv", 3072, 2048), ("o", 2048, 2048), ("gate_up", 22016, 2048), ("down", 2048, 11008),
                    ("lm_head", 128256, 2048)]:
     x = torch.randn(M, K, device="cuda", dtype=torch.bfloat16)
@@ -58,7 +59,7 @@ for name, N, K in [("qkv", 3072, 2048), ("o", 2048, 2048), ("gate_up", 22016, 20
     t = timeit(lambda: torch.nn.functional.linear(x, w))
     row.append(f"{t:.3f} ({fl / t / 1e9:.0f})")
     err = 0.0
-    for cfg in (0, 1, 2, 3, 5):
+    for cfg in (0, 1, 2, 5, 6, 7):
         c = ops.gemm_tn(x, w, cfg)
         err = max(err, rel(c, ref))
         t = timeit(lambda: ops.gemm_tn(x, w, cfg))
@@ -94,7 +95,7 @@ def unfused():
 
 
 qr = unfused()
-for cfg in (0, 1, 2, 5):
+for cfg in (0, 1, 2, 5, 6, 7):
     qf = ops.gemm_tn_rope(x, wq, cs, sn, (nq + nkv) * D, cfg)
     print(f"rope fused cfg{cfg}: rel err {rel(qf, qr):.4f}")
 t0 = timeit(unfused)
@@ -102,5 +103,7 @@ t1 = timeit(lambda: ops.gemm_tn_rope(x, wq, cs, sn, (nq + nkv) * D, 0))
 t2 = timeit(lambda: ops.gemm_tn_rope(x, wq, cs, sn, (nq + nkv) * D, 1))
 t3 = timeit(lambda: ops.gemm_tn_rope(x, wq, cs, sn, (nq + nkv) * D, 2))
 t4 = timeit(lambda: ops.gemm_tn_rope(x, wq, cs, sn, (nq + nkv) * D, 5))
+t5 = timeit(lambda: ops.gemm_tn_rope(x, wq, cs, sn, (nq + nkv) * D, 6))
+t6 = timeit(lambda: ops.gemm_tn_rope(x, wq, cs, sn, (nq + nkv) * D, 7))
 print(f"qkv + RoPE: blas + kernel {t0:.3f} ms, fused 256x256 {t1:.3f} ms, fused 256x128 {t2:.3f} ms, fused BK64 {t3:.3f} ms, "
-      f"fused BK64 TRC {t4:.3f} ms")
+      f"fused BK64 TRC {t4:.3f} ms, fused BK64 256x128 NS3 {t5:.3f} ms, NS2 {t6:.3f} ms")
