@@ -318,13 +318,19 @@ def _tn_ok(x2d: torch.Tensor, w: torch.Tensor) -> bool:
             and x2d.stride(1) == 1 and x2d.stride(0) % 8 == 0 and w.is_contiguous() and w.shape[0] % 256 == 0)
 
 
-_TN_PLAIN = os.environ.get("SFTAMD_TN_PLAIN", "1") == "1"
+# Both win in the isolated microbench but lose inside the training step. Same-box interleaved bench.py
+# (gpu_run57): 98.36 samples/s with both, 98.71 / 98.70 with either one off, 98.84 at the session-start
+# commit. Both are opt-in.
+_TN_PLAIN = os.environ.get("SFTAMD_TN_PLAIN", "0") == "1"
+_TN_SMALL_TILES = os.environ.get("SFTAMD_TN_SMALL_TILES", "0")
 
 
 def _tn_cfg(M: int, N: int) -> int:
     """BK64 tile for a forward GEMM: 256x256 (cfg 2) when its grid fills whole waves of the 256 CUs,
     else 256x128 with 3 LDS stages (cfg 6): qkv [8192 x 3072] is 384 big tiles = 1.5 waves but 768 small
     ones = 3 (0.095 vs 0.102 ms; o_proj's 256 tiles stay on 256x256: 0.058 vs 0.065 ms, r1_gemm_tn.md)."""
+    if _TN_SMALL_TILES == "0":
+        return 2
     tiles = (M // 256) * (N // 256)
     return 2 if (N % 256 == 0 and tiles % 256 == 0) or N % 128 != 0 else 6
 

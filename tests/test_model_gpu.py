@@ -75,6 +75,8 @@ def test_model_fused_gemm_epilogues(mt, monkeypatch):
     monkeypatch.setattr(F.GateUpSwiGLUFn, "apply", sw)
     monkeypatch.setattr(F.QKVRopeFn, "apply", rp)
     monkeypatch.setattr(F, "_tn_plain_ok", plain)
+    monkeypatch.setattr(F, "_TN_PLAIN", True)  # opt-in paths, exercised here
+    monkeypatch.setattr(F, "_TN_SMALL_TILES", "1")
     monkeypatch.setattr(F, "_TN_MODE", "1")
     l_f, g_f = _run(m, ids, labels, True)
     assert calls["swiglu"] == 4 and calls["rope"] == (3 if mt == "smollm3" else 4)  # NoPE layer 3
