@@ -46,6 +46,8 @@ def main(argv=None):
                     help="YAML/JSON file of SFTConfig field overrides (applied over the reference defaults)")
     ap.add_argument("--set", dest="sets", action="append", default=[], metavar="FIELD=VALUE",
                     help="override one SFTConfig field (repeatable; highest precedence)")
+    ap.add_argument("--merge-lora", action="store_true",
+                    help="LoRA runs: write best_model/ with the adapters merged into the weights")
     a = ap.parse_args(argv)
 
     st = setup_distributed()
@@ -98,7 +100,7 @@ def main(argv=None):
         print(f"VRAM after model load: {torch.cuda.memory_allocated() / 2**30:.2f} GB allocated")
     result = trainer.train(resume_from_checkpoint=a.resume)
 
-    trainer.save_model(f"{out}/best_model")  # rank 0 writes, all ranks barrier
+    trainer.save_model(f"{out}/best_model", merge_lora=a.merge_lora)  # rank 0 writes, all ranks barrier
     if st.is_main:
         with open(f"{out}/training_history.json", "w") as f:
             json.dump(history.history, f, indent=2)

@@ -86,12 +86,39 @@ def load_state_dict(path: str, device="cpu") -> Dict[str, torch.Tensor]:
     return load_file(os.path.join(path, "model.safetensors"), device=str(device))
 
 
+@torch.no_grad()
+def _merged_lora_state_dict(model, sd: Dict[str, torch.Tensor]) -> Dict[str, torch.Tensor]:
+    cfg = model.config
+    sd = dict(sd)
+    for i, l in enumerate(model.model.layers):
+        p = f"model.layers.{i}."
+        a, m = l.self_attn, l.mlp
+        if getattr(a, "lora", None) is not None:
+            w = a.qkv_proj.detach() + a.lora["qkv"].delta_weight().to(a.qkv_proj.dtype)
+            q, k, v = w.split([cfg.q_size, cfg.kv_size, cfg.kv_size], 0)
+            sd[p + "self_attn.q_proj.weight"], sd[p + "self_attn.k_proj.weight"] = q, k
+            sd[p + "self_attn.v_proj.weight"] = v
+            sd[p + "self_attn.o_proj.weight"] = a.o_proj.detach() + a.lora["o"].delta_weight().to(a.o_proj.dtype)
+        if getattr(m, "lora", None) is not None:
+            w = m.gate_up_proj.detach() + m.lora["gate_up"].delta_weight().to(m.gate_up_proj.dtype)
+            g, u = w.split([cfg.intermediate_size] * 2, 0)
+            sd[p + "mlp.gate_proj.weight"], sd[p + "mlp.up_proj.weight"] = g, u
+            sd[p + "mlp.down_proj.weight"] = m.down_proj.detach() + m.lora["down"].delta_weight().to(m.down_proj.dtype)
+    return sd
+
+
 def save_pretrained(model, path: str, tokenizer=None, max_shard_size: int = 5 * 1024 ** 3, merge_lora: bool = False):
-    """HF layout: safetensors + config.json + generation_config.json (+ tokenizer files)."""
+    """HF layout: safetensors + config.json + generation_config.json (+ tokenizer files). LoRA models write
+    the base weights plus ``adapter_model.safetensors``; ``merge_lora=True`` writes merged weights instead."""
     from ..models.lora import lora_state_dict
     tmp = _atomic_dir(path)
-    lora = any(getattr(l.self_attn, "lora", None) is not None for l in model.model.layers)
-    save_state_dict_sharded(model.hf_state_dict(), tmp, max_shard_size)
+    lora = any(getattr(l.self_attn, "lora", None) is not None or getattr(l.mlp, "lora", None) is not None
+               for l in model.model.layers)
+    sd = model.hf_state_dict()
+    if lora and merge_lora:  # export: adapters folded into copies of the base weights (the model keeps them)
+        sd = _merged_lora_state_dict(model, sd)
+        lora = False
+    save_state_dict_sharded(sd, tmp, max_shard_size)
     if lora:
         from safetensors.torch import save_file
         save_file({k: v.contiguous().cpu() for k, v in lora_state_dict(model).items()},

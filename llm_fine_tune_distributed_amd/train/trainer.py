@@ -257,11 +257,13 @@ class SFTTrainer:
         self.callback_handler.call("on_save", a, self.state, self.control)
         return path
 
-    def save_model(self, output_dir: Optional[str] = None):
+    def save_model(self, output_dir: Optional[str] = None, merge_lora: bool = False):
+        """Rank 0 writes the HF directory; every rank waits. ``merge_lora`` folds LoRA adapters into the
+        saved weights (export for plain HF / llama.cpp consumers) instead of writing them separately."""
         output_dir = output_dir or self.args.output_dir
         self.optimizer.synchronize()
         if self.dist.is_main:
-            ckpt.save_pretrained(self.model, output_dir, tokenizer=self.tokenizer)
+            ckpt.save_pretrained(self.model, output_dir, tokenizer=self.tokenizer, merge_lora=merge_lora)
         barrier()
 
     def _update_best(self, metrics: Dict[str, float], ckpt_path: Optional[str]):

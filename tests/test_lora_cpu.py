@@ -92,3 +92,36 @@ def test_hash_dropout_statistics():
     y2 = ref.dropout_add(b, b, 0.25, 7)
     assert torch.allclose(y2, y + 1)
     assert not torch.equal(ref.dropout_add(None, b, 0.25, 8), y)
+
+
+def test_save_merged_lora_loads_in_transformers(tmp_path):
+    """save_pretrained(merge_lora=True): adapters folded into copies of the base weights (the live model
+    keeps its adapters); transformers loads the directory and reproduces the adapted model's logits."""
+    import os
+    from transformers import AutoModelForCausalLM
+    from llm_fine_tune_distributed_amd.train.checkpoint import save_pretrained
+    torch.manual_seed(0)
+    m = build_model(tiny("smollm3"), dtype=torch.float32, seed=5)
+    apply_lora(m, LoRAConfig(r=4, lora_alpha=8, lora_dropout=0.0, target_modules=["q_proj", "v_proj", "o_proj",
+                                                                                   "up_proj", "down_proj"]))
+    with torch.no_grad():
+        for n, p in m.named_parameters():
+            if ".lora." in n and p.numel() > 0:
+                p.normal_(0.0, 0.05)
+    m.eval()
+    ids = torch.randint(0, m.config.vocab_size, (2, 16))
+    with torch.no_grad():
+        mo = m(ids, return_logits=True).logits
+    save_pretrained(m, str(tmp_path / "merged"), merge_lora=True)
+    save_pretrained(m, str(tmp_path / "adapters"))
+    assert not os.path.exists(tmp_path / "merged" / "adapter_model.safetensors")
+    assert os.path.exists(tmp_path / "adapters" / "adapter_model.safetensors")
+    assert m.model.layers[0].self_attn.lora is not None  # live model untouched
+    hm = AutoModelForCausalLM.from_pretrained(str(tmp_path / "merged"), torch_dtype=torch.float32).eval()
+    with torch.no_grad():
+        ho = hm(input_ids=ids).logits
+    assert (ho.reshape(mo.shape) - mo).abs().max() < 1e-4
+    base = AutoModelForCausalLM.from_pretrained(str(tmp_path / "adapters"), torch_dtype=torch.float32).eval()
+    with torch.no_grad():
+        bo = base(input_ids=ids).logits
+    assert (bo.reshape(mo.shape) - mo).abs().max() > 1e-3  # base weights alone differ: the merge did something

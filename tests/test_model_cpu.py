@@ -90,3 +90,23 @@ def test_param_counts_and_freeze_policy():
 def test_smollm3_nope_layers():
     c = smollm3_3b()
     assert [i for i in range(36) if not c.uses_rope(i)] == list(range(3, 36, 4))
+
+
+@pytest.mark.parametrize("mt", ["smollm3", "llama"])
+def test_saved_model_loads_in_transformers(tmp_path, mt):
+    """save_pretrained() output is a plain HF directory: transformers' AutoModelForCausalLM loads it
+    (config.json, safetensors names, tied lm_head dedup) and produces the same logits — the layout that
+    downstream tools such as llama.cpp's convert_hf_to_gguf.py read (reference README.md:87-118)."""
+    from transformers import AutoModelForCausalLM
+    from llm_fine_tune_distributed_amd.train.checkpoint import save_pretrained
+    torch.manual_seed(0)
+    cfg = tiny(mt)
+    m = build_model(cfg, dtype=torch.float32, seed=4)
+    save_pretrained(m, str(tmp_path / "out"))
+    hm = AutoModelForCausalLM.from_pretrained(str(tmp_path / "out"), torch_dtype=torch.float32)
+    hm.eval()
+    ids = torch.randint(0, cfg.vocab_size, (2, 16))
+    with torch.no_grad():
+        ho = hm(input_ids=ids).logits
+        mo = m(ids, return_logits=True).logits
+    assert (ho.reshape(-1, cfg.vocab_size) - mo).abs().max() < 1e-4
