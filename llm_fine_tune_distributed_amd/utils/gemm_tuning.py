@@ -26,6 +26,11 @@ def enable_tuned_gemms(path: Optional[str] = None, tune: bool = False, verbose: 
     tun.tuning_enable(bool(tune))
     if tune:
         tun.set_filename(path, insert_device_ordinal=False)
+    else:  # read-only: no per-rank tunableop_results<N>.csv dumped into the working directory at exit
+        try:
+            tun.write_file_on_exit(False)
+        except AttributeError:  # older torch
+            pass
     ok = False
     if os.path.exists(path):
         ok = bool(tun.read_file(path))
