@@ -53,6 +53,7 @@ class Attention(nn.Module):
         self.qkv_proj = nn.Parameter(torch.empty(cfg.qkv_size, cfg.hidden_size))
         self.o_proj = nn.Parameter(torch.empty(cfg.hidden_size, cfg.q_size))
         self.lora = None  # set by apply_lora
+        self.cp_group = None  # context-parallel process group (CausalLM.enable_context_parallel)
 
     def forward(self, h, rope_cs, cu_seqlens, max_seqlen):
         c = self.cfg
@@ -64,7 +65,13 @@ class Attention(nn.Module):
             qkv = ops.linear(h, self.qkv_proj) if self.lora is None else ops.lora_linear(h, self.qkv_proj, self.lora["qkv"])
             if self.use_rope:
                 qkv = ops.rope_(qkv, rope_cs[0], rope_cs[1], c.num_attention_heads, c.num_key_value_heads, c.head_dim)
-        a = ops.flash_attention(qkv, cu_seqlens, max_seqlen, c.num_attention_heads, c.num_key_value_heads, c.head_dim)
+        if self.cp_group is not None:
+            from ..parallel.context_parallel import ring_attention
+            a = ring_attention(qkv, cu_seqlens, max_seqlen, c.num_attention_heads, c.num_key_value_heads, c.head_dim,
+                               self.cp_group)
+        else:
+            a = ops.flash_attention(qkv, cu_seqlens, max_seqlen, c.num_attention_heads, c.num_key_value_heads,
+                                    c.head_dim)
         return ops.linear(a, self.o_proj) if self.lora is None else ops.lora_linear(a, self.o_proj, self.lora["o"])
 
 
@@ -148,6 +155,13 @@ class CausalLM(nn.Module):
 
     def gradient_checkpointing_disable(self):
         self.gradient_checkpointing = False
+
+    def enable_context_parallel(self, group) -> None:
+        """Attention over sequence chunks spread across ``group`` (ring attention, parallel/context_parallel.py).
+        Inputs must then be this rank's chunk with explicit global ``position_ids`` and pre-shifted labels
+        (``context_parallel.shard_batch``)."""
+        for layer in self.model.layers:
+            layer.self_attn.cp_group = group
 
     @torch.no_grad()
     def init_weights(self, seed: int = 0):

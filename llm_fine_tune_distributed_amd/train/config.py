@@ -92,6 +92,9 @@ class SFTConfig:
     # ZeRO-1 over the DDP buckets (world_size > 1): reduce-scatter gradients, update 1/world_size of the
     # parameters per rank, all-gather them back under the next forward (train/optim.py ShardedAdamW)
     shard_optimizer_state: bool = False
+    # context parallelism (ring attention, parallel/context_parallel.py): consecutive groups of this many ranks
+    # share each batch with the sequence split across them; data parallelism runs across the groups
+    context_parallel_size: int = 1
     ddp_first_bucket_mb: float = 4.0
     ddp_broadcast_params: bool = False      # weights are identical by construction (seeded / loaded)
     ddp_check_sync_every: int = 0           # cross-rank param checksum every N steps (0 = off)

@@ -68,6 +68,16 @@ class SFTTrainer:
                  model_init_seed: int = 0):
         self.args = args = args or SFTConfig()
         self.dist = setup_distributed(timeout_s=args.ddp_timeout, verbose=False)
+        # context parallelism: consecutive ranks form CP groups that share each batch, sequence-sharded
+        # (ring attention); data parallelism runs across the groups
+        self.cp_size = int(getattr(args, "context_parallel_size", 1) or 1)
+        self.cp_group, self.cp_rank, self.dp_rank, self.dp_size = None, 0, self.dist.rank, self.dist.world_size
+        if self.cp_size > 1:
+            from ..parallel.context_parallel import new_groups
+            if args.packing:
+                raise ValueError("context_parallel_size > 1 needs padded batches (packing=False)")
+            self.cp_group, self.cp_rank, self.dp_rank, self.dp_size = new_groups(
+                self.dist.world_size, self.dist.rank, self.cp_size)
         set_seed(args.seed)
         dev = self.dist.device
         if args.gemm_tuning and dev.type == "cuda" and "PYTORCH_TUNABLEOP_ENABLED" not in os.environ:
@@ -91,6 +101,8 @@ class SFTTrainer:
             apply_freeze_policy(model, policy, n_last=args.freeze_last_n_layers, lora_config=lc)
         if args.gradient_checkpointing:
             model.gradient_checkpointing_enable()
+        if self.cp_size > 1:
+            model.enable_context_parallel(self.cp_group)
         self.trainable_params = model.num_parameters(trainable_only=True)
         self.total_params = model.num_parameters()
         # ------------------------------------------------------------ data
@@ -101,6 +113,7 @@ class SFTTrainer:
         self.train_dataset = self._prepare(train_dataset, args.max_train_samples)
         self.eval_dataset = self._prepare(eval_dataset, args.max_eval_samples)
         pad_id = self.tokenizer.pad_token_id if self.tokenizer is not None else (model.config.pad_token_id or 0)
+        self._pad_id = pad_id
         self.collator = data_collator or SFTCollator(pad_id, args.pad_to_multiple_of, args.max_length, args.packing,
                                                      args.per_device_train_batch_size * (args.max_length or 1024)
                                                      if args.packing else None)
@@ -147,16 +160,16 @@ class SFTTrainer:
 
     def get_train_dataloader(self) -> DataLoader:
         a = self.args
-        s = DistributedBatchSampler(len(self.train_dataset), a.per_device_train_batch_size, self.dist.world_size,
-                                    self.dist.rank, shuffle=True, seed=a.data_seed or a.seed,
+        s = DistributedBatchSampler(len(self.train_dataset), a.per_device_train_batch_size, self.dp_size,
+                                    self.dp_rank, shuffle=True, seed=a.data_seed or a.seed,
                                     drop_last=a.dataloader_drop_last)
         return DataLoader(self.train_dataset, self.collator, s, self.dist.device, a.dataloader_pin_memory,
                           a.prefetch_batches)
 
     def get_eval_dataloader(self) -> DataLoader:
         a = self.args
-        s = DistributedBatchSampler(len(self.eval_dataset), a.per_device_eval_batch_size, self.dist.world_size,
-                                    self.dist.rank, shuffle=False, drop_last=a.dataloader_drop_last)
+        s = DistributedBatchSampler(len(self.eval_dataset), a.per_device_eval_batch_size, self.dp_size,
+                                    self.dp_rank, shuffle=False, drop_last=a.dataloader_drop_last)
         return DataLoader(self.eval_dataset, self.collator, s, self.dist.device, a.dataloader_pin_memory,
                           a.prefetch_batches)
 
@@ -167,7 +180,15 @@ class SFTTrainer:
         if "cu_seqlens" in b:
             kw.update(cu_seqlens=b["cu_seqlens"], position_ids=b["position_ids"], max_seqlen=b["max_seqlen"],
                       shift_labels=not b.get("shifted", False))
+        elif "position_ids" in b:  # context-parallel chunk: global positions, labels shifted before sharding
+            kw.update(position_ids=b["position_ids"], shift_labels=not b.get("shifted", False))
         return kw
+
+    def _cp_shard(self, b: Dict) -> Dict:
+        if self.cp_size == 1:
+            return b
+        from ..parallel.context_parallel import shard_batch
+        return shard_batch(b, self.cp_rank, self.cp_size, self._pad_id)
 
     def global_num_items(self, micro: List[Dict]) -> torch.Tensor:
         if all(torch.is_tensor(b.get("num_items_t")) for b in micro):
@@ -185,6 +206,7 @@ class SFTTrainer:
         loss (this rank's share of the global mean), correct, entropy_sum, valid tokens."""
         model, eng = self.model, self.engine
         model.train()
+        micro = [self._cp_shard(b) for b in micro]
         n_items = self.global_num_items(micro)
         acc = torch.zeros(4, device=self.dist.device)  # loss, correct, entropy_sum, valid
         for i, b in enumerate(micro):
@@ -214,16 +236,17 @@ class SFTTrainer:
         acc = torch.zeros(5, device=self.dist.device)  # loss_sum, correct, entropy_sum, valid, samples
         loader = self.get_eval_dataloader()
         for b in loader:
+            b = self._cp_shard(b)
             out = self.model(**self._model_inputs(b), num_items_in_batch=1.0)
             acc[0] += out.loss
             acc[1:4] += out.metrics
-            acc[4] += b["num_samples"]
+            acc[4] += b["num_samples"] if self.cp_rank == 0 else 0  # a CP group shares its samples
         all_reduce_sum_(acc)
         vals = acc.tolist()
         self.model.train()
         rt = time.time() - t0
         valid = max(vals[3], 1.0)
-        nb = len(loader) * self.dist.world_size
+        nb = len(loader) * self.dp_size
         m = {f"{metric_key_prefix}_loss": vals[0] / valid, f"{metric_key_prefix}_runtime": rt,
              f"{metric_key_prefix}_samples_per_second": vals[4] / max(rt, 1e-9),
              f"{metric_key_prefix}_steps_per_second": nb / max(rt, 1e-9),
@@ -354,17 +377,17 @@ class SFTTrainer:
                 steps_since_log += 1
                 n_s = sum(b["num_samples"] for b in micro)
                 n_t = sum(b["num_tokens"] for b in micro)
-                samples += n_s * self.dist.world_size
-                tokens += n_t * self.dist.world_size
+                samples += n_s * self.dp_size  # a context-parallel group shares its samples
+                tokens += n_t * self.dp_size
                 T = max(b["input_ids"].shape[-1] for b in micro)
                 flops += cfg.flops_per_token(T, training=True, recompute=a.gradient_checkpointing) * n_t * \
-                    self.dist.world_size
+                    self.dp_size
                 self.state.global_step += 1
                 step_in_epoch += 1
                 self.state.epoch = epoch + step_in_epoch / steps_per_epoch
-                self.state.samples_seen += n_s * self.dist.world_size
-                self.state.tokens_seen += n_t * self.dist.world_size
-                self.state.total_flos += 6.0 * self.trainable_params * n_t * self.dist.world_size
+                self.state.samples_seen += n_s * self.dp_size
+                self.state.tokens_seen += n_t * self.dp_size
+                self.state.total_flos += 6.0 * self.trainable_params * n_t * self.dp_size
                 self.control = self.callback_handler.call("on_step_end", a, self.state, self.control)
                 gs = self.state.global_step
                 maybe_inject(self.dist.rank, gs)
