@@ -80,7 +80,8 @@ class SFTTrainer:
                 self.dist.world_size, self.dist.rank, self.cp_size)
         set_seed(args.seed)
         dev = self.dist.device
-        if args.gemm_tuning and dev.type == "cuda" and "PYTORCH_TUNABLEOP_ENABLED" not in os.environ:
+        if (args.gemm_tuning and dev.type == "cuda" and "PYTORCH_TUNABLEOP_ENABLED" not in os.environ
+                and not torch.cuda.tunable.is_enabled()):  # a caller's own TunableOp setup (e.g. tuning) wins
             from ..utils.gemm_tuning import enable_tuned_gemms
             enable_tuned_gemms()
         # ------------------------------------------------------------ model
