@@ -259,6 +259,8 @@ class CausalLM(nn.Module):
         out = CausalLMOutput()
         if labels is not None:
             valid = labels != -100
+            if hasattr(num_items_in_batch, "resolve"):  # trainer's in-flight global count (PendingCount)
+                num_items_in_batch = num_items_in_batch.resolve()
             if num_items_in_batch is None:
                 cnt = valid.sum().clamp(min=1)
             elif torch.is_tensor(num_items_in_batch):

@@ -109,6 +109,30 @@ def all_reduce_sum_(t: torch.Tensor) -> torch.Tensor:
     return t
 
 
+class PendingCount:
+    """A count whose all-reduce is in flight; ``resolve()`` makes the current stream wait for it (once)
+    and returns it clamped to >= 1."""
+
+    def __init__(self, t: torch.Tensor, work=None):
+        self._t, self._work, self._done = t, work, None
+
+    def resolve(self) -> torch.Tensor:
+        if self._done is None:
+            if self._work is not None:
+                self._work.wait()
+            self._done = self._t.clamp(min=1.0)
+        return self._done
+
+
+def all_reduce_sum_async(t: torch.Tensor) -> PendingCount:
+    """In-place SUM all-reduce of ``t`` issued without blocking the compute stream (world size 1:
+    nothing in flight)."""
+    work = None
+    if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
+        work = dist.all_reduce(t, op=dist.ReduceOp.SUM, async_op=True)
+    return PendingCount(t, work)
+
+
 def broadcast_object(obj, src: int = 0):
     if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
         lst = [obj]

@@ -36,7 +36,7 @@ from ..data.dataset import TokenizedDataset, tokenize_rows
 from ..models import CausalLM, apply_freeze_policy, build_model, get_config
 from ..models.lora import LoRAConfig
 from ..parallel.ddp import DDPEngine
-from ..parallel.process_group import all_reduce_sum_, barrier, setup_distributed
+from ..parallel.process_group import all_reduce_sum_, all_reduce_sum_async, barrier, setup_distributed
 from . import checkpoint as ckpt
 from .callbacks import (AimCallback, CallbackHandler, JSONLLoggerCallback, PrinterCallback, TrainerCallback,
                         TrainerControl, TrainerState)
@@ -191,7 +191,15 @@ class SFTTrainer:
         from ..parallel.context_parallel import shard_batch
         return shard_batch(b, self.cp_rank, self.cp_size, self._pad_id)
 
-    def global_num_items(self, micro: List[Dict]) -> torch.Tensor:
+    def global_num_items(self, micro: List[Dict]):
+        """Global count of loss tokens of this optimizer step (TRL ``num_items_in_batch``).
+
+        With more than one rank the 1-float all-reduce is issued asynchronously and handed to the model
+        as a ``PendingCount``, resolved only where the loss needs it (after the last decoder layer).
+        Under ZeRO-1 the previous step's parameter all-gathers are still queued on the same RCCL
+        communicator: a blocking all-reduce here would make the compute stream wait for ALL of them
+        before the first layer, serialising the gather that is meant to run under the forward.
+        """
         if all(torch.is_tensor(b.get("num_items_t")) for b in micro):
             n = micro[0]["num_items_t"].to(self.dist.device, non_blocking=True).clone()
             for b in micro[1:]:
@@ -199,7 +207,7 @@ class SFTTrainer:
         else:
             n = torch.tensor([float(sum(b["num_items"] for b in micro))], device=self.dist.device)
         if self.args.average_tokens_across_devices:
-            all_reduce_sum_(n)
+            return all_reduce_sum_async(n)
         return n.clamp(min=1.0)
 
     def optimizer_step(self, micro: List[Dict], lr: float) -> Dict[str, torch.Tensor]:
