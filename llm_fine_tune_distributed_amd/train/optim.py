@@ -10,12 +10,25 @@ the clip coefficient never leaves the GPU.
 """
 from __future__ import annotations
 
+import contextlib
 import math
 from typing import Callable, Dict, Optional
 
 import torch
 
 from .. import ops
+
+
+class _StreamPoint:
+    """Work-like handle for an update with no collective behind it: ``wait()`` makes the current
+    stream wait for the side stream up to the point where the handle was created."""
+
+    def __init__(self, stream):
+        self._ev = torch.cuda.Event()
+        self._ev.record(stream)
+
+    def wait(self):
+        torch.cuda.current_stream().wait_event(self._ev)
 
 
 class FlatAdamW:
@@ -251,6 +264,8 @@ class ShardedAdamW(FlatAdamW):
         groups.append(buckets_of(head))
         self._wait_groups = groups
 
+        last = len(groups) - 1
+
         def waiter(i):
             def hook(*_a, **_k):
                 if self._pending:
@@ -258,12 +273,15 @@ class ShardedAdamW(FlatAdamW):
                         w = self._ag.pop(bi, None)
                         if w is not None:
                             w.wait()
+                    if i == last:  # buckets outside every group: done before the next backward writes grads
+                        self.synchronize()
             return hook
 
         self._hooks = [model.register_forward_pre_hook(waiter(0))]
         for i, layer in enumerate(inner.layers):
             self._hooks.append(layer.register_forward_pre_hook(waiter(i + 1)))
-        self._hooks.append(inner.layers[-1].register_forward_hook(waiter(len(groups) - 1)))
+        self._hooks.append(inner.layers[-1].register_forward_hook(waiter(last)))
+        self._stream = torch.cuda.Stream(device=e.device) if e.device.type == "cuda" else None
         self.overlap = True
         return True
 
@@ -294,17 +312,29 @@ class ShardedAdamW(FlatAdamW):
         self.last_grad_norm = norm
         b1, b2 = self.betas
         seed = (0x5EED + 7919 * self.step_count) & 0x7FFFFFFF if self.stochastic_rounding else 0
-        # forward order (the embedding's bucket is the LAST one in backward-ready layout): each bucket's
-        # gather is issued right after its update, so the first layers' parameters come back first
-        for b, s, t, lo, decay in reversed(self.slices):
-            n = t - s
-            if n:
-                ops.adamw_flat_(e.param_flat[s:t], e.grad_flat[s:t], None if self.master is None else self.master[lo:lo + n],
-                                self.exp_avg[lo:lo + n], self.exp_avg_sq[lo:lo + n], coef, lr, b1, b2, self.eps,
-                                self.weight_decay if decay else 0.0, self.step_count, sr_seed=seed, sr_offset=s)
-            w = e.gather_params(b, async_op=True)
-            if w is not None:
-                self._ag[b.index] = w
+        # Overlapped: updates AND gathers are issued from a side stream, so the next forward only waits
+        # for the buckets each layer reads (update -> gather chain per bucket), not for the whole update.
+        st = self._stream if (self.overlap and getattr(self, "_stream", None) is not None) else None
+        ctx = contextlib.nullcontext()
+        if st is not None:
+            st.wait_stream(torch.cuda.current_stream(e.device))
+            coef.record_stream(st)
+            ctx = torch.cuda.stream(st)
+        with ctx:
+            # forward order (the embedding's bucket is the LAST one in backward-ready layout): each bucket's
+            # gather is issued right after its update, so the first layers' parameters come back first
+            for b, s, t, lo, decay in reversed(self.slices):
+                n = t - s
+                if n:
+                    ops.adamw_flat_(e.param_flat[s:t], e.grad_flat[s:t],
+                                    None if self.master is None else self.master[lo:lo + n],
+                                    self.exp_avg[lo:lo + n], self.exp_avg_sq[lo:lo + n], coef, lr, b1, b2, self.eps,
+                                    self.weight_decay if decay else 0.0, self.step_count, sr_seed=seed, sr_offset=s)
+                w = e.gather_params(b, async_op=True)
+                if w is None and st is not None:
+                    w = _StreamPoint(st)
+                if w is not None:
+                    self._ag[b.index] = w
         self._pending = bool(self._ag)
         if not self.overlap:
             self.synchronize()
