@@ -62,6 +62,45 @@ def test_ddp2_on_gpu_matches_single():
     assert rel < 1e-2
 
 
+def _rccl_world1(port, out):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import torch.distributed as dist
+    from llm_fine_tune_distributed_amd.parallel.process_group import all_reduce_sum_async, nccl_options
+    torch.cuda.set_device(0)
+    dev = torch.device("cuda", 0)
+    opts = nccl_options()
+    kw = {"pg_options": opts} if opts is not None else {}
+    dist.init_process_group("nccl", init_method="env://", world_size=1, rank=0, device_id=dev, **kw)
+    x = torch.arange(4096, device=dev, dtype=torch.float32).to(torch.bfloat16)
+    ref = x.clone()
+    dist.all_reduce(x)
+    pc = all_reduce_sum_async(torch.tensor([3.0], device=dev))
+    side = torch.cuda.Stream()
+    side.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(side):  # the ZeRO-1 pattern: in-place RS / AG issued from a side stream
+        w1 = dist.reduce_scatter_tensor(x[:4096], x, async_op=True)
+        w2 = dist.all_gather_into_tensor(x, x[:4096], async_op=True)
+    w1.wait()
+    w2.wait()
+    cnt = pc.resolve()
+    torch.cuda.synchronize()
+    torch.save({"ok": bool(torch.equal(x, ref)), "cnt": float(cnt.item()),
+                "hp": bool(getattr(opts, "is_high_priority_stream", False))}, os.path.join(out, "rccl.pt"))
+    dist.destroy_process_group()
+
+
+def test_rccl_process_group_options_and_side_stream_collectives():
+    """The RCCL (nccl backend) path itself on one MI355X: high-priority collective streams, in-place
+    reduce-scatter / all-gather issued from a side stream, and the async token-count all-reduce."""
+    d = tempfile.mkdtemp()
+    p = mp.get_context("spawn").Process(target=_rccl_world1, args=(_port(), d))
+    p.start()
+    p.join(timeout=180)
+    assert p.exitcode == 0
+    r = torch.load(os.path.join(d, "rccl.pt"))
+    assert r["ok"] and r["cnt"] == 3.0 and r["hp"]
+
+
 def test_zero1_on_gpu_matches_replicated():
     """ZeRO-1 on GPU tensors (2 ranks on one MI355X): the reduce-scatter / sharded HIP AdamW /
     overlapped all-gather path gives the replicated run's parameters."""
