@@ -14,8 +14,22 @@ tokens), random-init weights of the SmolLM3-3B architecture (no
 Weak scaling: per-GPU work is fixed (micro-batch x GA), global batch = 16 x N. With N > 1 the optimizer
 state is sharded ZeRO-1 style by default (``--zero 0`` = replicated all-reduce DDP).
 
-    python bench.py [--gpus N] [--steps K] [--warmup W]
+Launching (the reference's ``training.py:16-42`` env contract):
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]          # N > 1: spawns N ranks itself
     python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N
+    python bench.py --gpus 4 --device cpu --model tiny             # gloo rehearsal of the N-rank path
+
+When ``WORLD_SIZE`` is unset and ``--gpus N > 1`` this process becomes a launcher: it never imports
+torch (so it never touches a GPU), starts N fresh ``bench.py`` children with the torchrun env contract
+(``RANK/LOCAL_RANK/WORLD_SIZE/MASTER_ADDR=127.0.0.1/MASTER_PORT``) through ``launch.py``, lets rank 0
+print the JSON line, and exits with the first failing rank's code after tearing the others down.
+
+Besides the driver contract fields the JSON line carries the multi-GPU diagnostics a scaling run needs:
+``dist`` (backend and world size as every rank saw them), ``bucket_plan`` (count / sizes of the
+gradient buckets), ``comm_exposed_ms`` (non-overlapped gradient-collective wait per step, max over
+ranks), per-rank ``peak_mem_gb`` / ``ms_per_step`` and, given ``--baseline-1gpu V``,
+``scaling_efficiency = value / (N * V)``.
 """
 from __future__ import annotations
 
@@ -25,15 +39,18 @@ import os
 import sys
 import time
 
-sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, HERE)
 
 
-def main():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--model", default="smollm3-3b")
+    ap.add_argument("--device", default="auto", choices=["auto", "cuda", "cpu"],
+                    help="cpu: gloo + the PyTorch fallbacks (a CPU rehearsal of the N-rank path; use --model tiny)")
     # Reference 4-GPU config: 8 samples/device x GA 2 = 16 samples per device per optimizer step
     # (README.md:69). MI355X's 288 GB holds all 16 at once, so the default runs them as ONE
     # micro-batch (identical optimizer-step math: the loss is normalised by the step's global
@@ -42,7 +59,8 @@ def main():
     ap.add_argument("--ga", type=int, default=1)
     ap.add_argument("--no-overlap", action="store_true", help="disable AdamW/forward overlap")
     ap.add_argument("--seq", type=int, default=512)
-    ap.add_argument("--bucket-mb", type=float, default=float(os.environ.get("SFTAMD_BUCKET_MB", "64")))
+    ap.add_argument("--bucket-mb", type=float, default=float(os.environ.get("SFTAMD_BUCKET_MB", "0")),
+                    help="gradient bucket cap in MB; 0 (default) = the xGMI plan of parallel.ddp.plan_bucket_mb")
     ap.add_argument("--packing", action="store_true")
     ap.add_argument("--freeze-policy", default="full", choices=["full", "last_n_layers", "lora"])
     ap.add_argument("--master-weights", action="store_true", help="fp32 master copy (default: bf16 params + SR)")
@@ -53,9 +71,35 @@ def main():
                          "per rank, all-gather params under the next forward); 0: replicated all-reduce DDP")
     ap.add_argument("--tunableop", default=os.environ.get("SFTAMD_TUNABLEOP", "auto"),
                     help="auto: load the committed GEMM selections; tune: tune missing shapes into it; off")
+    ap.add_argument("--baseline-1gpu", type=float, default=float(os.environ.get("SFTAMD_BENCH_1GPU", "0")),
+                    help="1-GPU samples/s of the same config: adds scaling_efficiency = value / (N * this)")
     ap.add_argument("--profile-steps", type=int, default=0)
-    a = ap.parse_args()
+    return ap.parse_args(argv)
 
+
+def launch_ranks(a, argv) -> int:
+    """Parent side of a standalone ``--gpus N`` run: spawn N ranks, never touch the GPU.
+
+    ``launch.py`` is loaded by file path so the package ``__init__`` (which imports torch) does not run
+    here; its children stay in this process group and die with this process (PR_SET_PDEATHSIG)."""
+    import importlib.util
+    spec = importlib.util.spec_from_file_location(
+        "_sftamd_launch", os.path.join(HERE, "llm_fine_tune_distributed_amd", "launch.py"))
+    launch = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(launch)
+    return launch.run(["--nproc-per-node", str(a.gpus), "--master-addr", "127.0.0.1", "--same-session",
+                       "--grace", "15", os.path.abspath(__file__)] + list(argv))
+
+
+def bucket_plan(engine) -> dict:
+    mb = [(b.end - b.start) * engine.grad_flat.element_size() / 2 ** 20 for b in engine.buckets]
+    srt = sorted(mb)
+    return {"count": len(mb), "cap_mb": round(engine.bucket_cap_mb, 3), "first_mb": round(mb[0], 3),
+            "min_mb": round(srt[0], 3), "median_mb": round(srt[len(srt) // 2], 3), "max_mb": round(srt[-1], 3),
+            "total_mb": round(sum(mb), 1), "split_params": engine.num_split_params}
+
+
+def run(a):
     import torch
     import torch.distributed as dist
 
@@ -64,82 +108,127 @@ def main():
     from llm_fine_tune_distributed_amd.parallel.process_group import barrier, setup_distributed
     from llm_fine_tune_distributed_amd.train import SFTConfig, SFTTrainer
 
-    st = setup_distributed(verbose=False)
-    if a.tunableop != "off" and "PYTORCH_TUNABLEOP_ENABLED" not in os.environ:
+    st = setup_distributed(verbose=False, device="cpu" if a.device == "cpu" else None)
+    on_gpu = st.device.type == "cuda"
+    if a.device == "cuda" and not on_gpu:
+        raise SystemExit("--device cuda but no GPU is visible")
+    if on_gpu and a.tunableop != "off" and "PYTORCH_TUNABLEOP_ENABLED" not in os.environ:
         from llm_fine_tune_distributed_amd.utils.gemm_tuning import enable_tuned_gemms
         enable_tuned_gemms(tune=(a.tunableop == "tune"), verbose=st.is_main)
     if st.world_size != a.gpus:
         raise SystemExit(f"--gpus {a.gpus} but WORLD_SIZE={st.world_size}")
+
+    def sync():
+        if on_gpu:
+            torch.cuda.synchronize()
+
     cfg = get_config(a.model)
     model = build_model(cfg, device=st.device, dtype=torch.bfloat16, seed=0)
-    per_rank_samples = a.micro_batch * a.ga * (a.steps + a.warmup + 2)
+    per_rank_samples = a.micro_batch * a.ga * (a.steps + a.warmup + a.profile_steps + 2)
     ds = TokenizedDataset.synthetic(per_rank_samples * st.world_size, cfg.vocab_size, a.seq, a.seq, seed=1)
     args = SFTConfig(output_dir="/tmp/sftamd_bench", per_device_train_batch_size=a.micro_batch,
                      gradient_accumulation_steps=a.ga, learning_rate=5e-5 * st.world_size, max_grad_norm=1.0,
                      bf16=True, gradient_checkpointing=False, max_length=a.seq, packing=a.packing,
-                     ddp_bucket_cap_mb=a.bucket_mb, dataloader_drop_last=True, jsonl_log=False, logging_steps=0,
-                     optimizer_overlap=not a.no_overlap, freeze_policy=a.freeze_policy,
+                     ddp_bucket_cap_mb=a.bucket_mb or None, dataloader_drop_last=True, jsonl_log=False,
+                     logging_steps=0, optimizer_overlap=not a.no_overlap, freeze_policy=a.freeze_policy,
                      master_weights=a.master_weights, optim_state_dtype=a.optim_state,
-                     shard_optimizer_state=bool(a.zero))
+                     shard_optimizer_state=bool(a.zero), gemm_tuning=False)
     trainer = SFTTrainer(model=model, args=args, train_dataset=ds)
     loader = trainer.get_train_dataloader()
     it = iter(loader)
 
-    def next_micro():
-        return [next(it) for _ in range(a.ga)]
+    from llm_fine_tune_distributed_amd.utils.faults import maybe_inject
+    n_step = [0]
 
     def step():
-        return trainer.optimizer_step(next_micro(), lr=args.learning_rate)
+        n_step[0] += 1
+        maybe_inject(st.rank, n_step[0])  # SFTAMD_FAULT_INJECT=rank:step (launcher teardown test)
+        return trainer.optimizer_step([next(it) for _ in range(a.ga)], lr=args.learning_rate)
 
     for _ in range(a.warmup):
         r = step()
-    torch.cuda.synchronize()
+    trainer.optimizer.synchronize()
+    sync()
     barrier()
-    torch.cuda.synchronize()
+    sync()
+    trainer.engine.comm_exposed_ms(reset=True)  # drop the warmup's samples
     t0 = time.perf_counter()
     for _ in range(a.steps):
         r = step()
-    torch.cuda.synchronize()
+    trainer.optimizer.synchronize()  # ZeRO-1: the last step's parameter all-gathers land inside the timing
+    sync()
     barrier()
-    torch.cuda.synchronize()
+    sync()
     dt = time.perf_counter() - t0
-    t = torch.tensor([dt], device=st.device, dtype=torch.float64)
+    comm_ms = trainer.engine.comm_exposed_ms(reset=True)
+    peak = torch.cuda.max_memory_allocated() / 1e9 if on_gpu else 0.0
+    mine = {"rank": st.rank, "world_size": dist.get_world_size() if dist.is_initialized() else 1,
+            "backend": dist.get_backend() if dist.is_initialized() else None,
+            "device": str(st.device), "ms_per_step": round(dt / a.steps * 1e3, 3), "peak_mem_gb": round(peak, 2),
+            "comm_exposed_ms": round(comm_ms, 3)}
+    ranks = [mine]
     if st.world_size > 1:
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    dt = t.item()
-    trainer.optimizer.synchronize()
+        ranks = [None] * st.world_size
+        dist.all_gather_object(ranks, mine)
+    dt = max(r_["ms_per_step"] for r_ in ranks) * a.steps / 1e3  # the MAX over ranks
     loss = r["acc"][0].item()
     ms = dt / a.steps * 1e3
     samples = a.micro_batch * a.ga * st.world_size * a.steps
     value = samples / dt
     tok_s = value * a.seq
-    mfu = tok_s * cfg.flops_per_token(a.seq) / (2.5e15 * st.world_size) if a.freeze_policy == "full" else None
+    full = a.freeze_policy == "full"
+    mfu = tok_s * cfg.flops_per_token(a.seq) / (2.5e15 * st.world_size) if (full and on_gpu) else None
+    shard = trainer.engine.shard
     if st.is_main:
         rec = {
-            "metric": ("samples/sec SmolLM3-3B full SFT bf16 (DDP)" if a.model == "smollm3-3b" and a.freeze_policy == "full"
+            "metric": ("samples/sec SmolLM3-3B full SFT bf16 (DDP)" if a.model == "smollm3-3b" and full
                        else f"samples/sec {a.model} {a.freeze_policy} SFT bf16 (DDP)"),
             "value": round(value, 3), "unit": "samples/s", "n_gpus": st.world_size, "steps": a.steps,
             "warmup": a.warmup, "ms_per_step": round(ms, 3), "higher_is_better": True, "scaling": "weak",
-            "vs_baseline": None, "dtype": "bf16", "data": "synthetic (random tokens, random-init weights)",
+            "vs_baseline": None, "dtype": "bf16",
+            "data": "synthetic (random tokens, random-init weights)" + ("" if on_gpu else "; CPU/gloo rehearsal"),
             "config": {"model": {"smollm3-3b": "SmolLM3-3B", "llama3-8b": "Llama-3-8B"}.get(a.model, a.model),
                        "freeze_policy": a.freeze_policy, "global_batch": a.micro_batch * a.ga * st.world_size,
                        "per_device_batch": a.micro_batch, "gradient_accumulation_steps": a.ga, "seq_len": a.seq,
-                       "parallelism": f"dp{st.world_size}", "optimizer": ("AdamW fp32-master (fused HIP)" if a.master_weights else
-                                     f"AdamW bf16 params + stochastic rounding, {a.optim_state} moments (fused HIP)"),
+                       "parallelism": f"dp{st.world_size}",
+                       "optimizer": ("AdamW fp32-master" if a.master_weights else
+                                     f"AdamW bf16 params + stochastic rounding, {a.optim_state} moments")
+                       + (" (fused HIP)" if on_gpu else " (torch fallback)"),
                        "samples_per_device_per_step": a.micro_batch * a.ga,
-                       "optimizer_sharding": "zero1" if (a.zero and st.world_size > 1) else "none",
+                       "optimizer_sharding": "zero1" if shard else "none",
                        "gradient_checkpointing": False, "packing": a.packing},
-            "tokens_per_sec": round(tok_s, 1), "mfu": None if mfu is None else round(mfu, 4), "final_loss": round(loss, 4),
-            "peak_mem_gb": round(torch.cuda.max_memory_allocated() / 1e9, 2),
+            "tokens_per_sec": round(tok_s, 1), "mfu": None if mfu is None else round(mfu, 4),
+            "final_loss": round(loss, 4), "peak_mem_gb": max(r_["peak_mem_gb"] for r_ in ranks),
+            "dist": {"backend": mine["backend"], "world_size": mine["world_size"],
+                     "consistent": all(r_["world_size"] == st.world_size and r_["backend"] == mine["backend"]
+                                       for r_ in ranks),
+                     "launcher": os.environ.get("SFTAMD_LAUNCHER", "external" if st.world_size > 1 else "none")},
+            "optimizer_sharding": "zero1" if shard else "none",
+            "bucket_plan": bucket_plan(trainer.engine),
+            "comm_exposed_ms": max(r_["comm_exposed_ms"] for r_ in ranks),
+            "per_rank": [{k: r_[k] for k in ("rank", "device", "ms_per_step", "peak_mem_gb", "comm_exposed_ms")}
+                         for r_ in ranks],
         }
+        if a.baseline_1gpu > 0:
+            rec["scaling_efficiency"] = round(value / (st.world_size * a.baseline_1gpu), 4)
         print(json.dumps(rec), flush=True)
     if a.profile_steps:
-        torch.cuda.synchronize()
+        sync()
         for _ in range(a.profile_steps):
             step()
-        torch.cuda.synchronize()
+        trainer.optimizer.synchronize()
+        sync()
     if st.world_size > 1:
+        barrier()
         dist.destroy_process_group()
+
+
+def main(argv=None):
+    argv = sys.argv[1:] if argv is None else argv
+    a = parse(argv)
+    if a.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch_ranks(a, argv))
+    run(a)
 
 
 if __name__ == "__main__":

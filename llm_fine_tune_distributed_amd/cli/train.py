@@ -78,7 +78,10 @@ def main(argv=None):
     aim = AimCallback(repo=env["aim_repo"], experiment="smollm3-wilderness-finetuning-distributed")
     dist_args = {}
     if st.world_size > 1:
-        dist_args = dict(ddp_find_unused_parameters=False, ddp_bucket_cap_mb=50, local_rank=st.local_rank)
+        # the reference's ddp_bucket_cap_mb=50 (training.py:253) was sized for one TCP ring; on the xGMI
+        # full mesh the cap grows with N (parallel/ddp.py plan_bucket_mb). DDP_BUCKET_CAP_MB pins it.
+        cap = float(os.environ["DDP_BUCKET_CAP_MB"]) if os.environ.get("DDP_BUCKET_CAP_MB") else None
+        dist_args = dict(ddp_find_unused_parameters=False, ddp_bucket_cap_mb=cap, local_rank=st.local_rank)
     args = SFTConfig(
         output_dir=f"{out}/checkpoints", per_device_train_batch_size=env["batch_size"],
         per_device_eval_batch_size=env["batch_size"], gradient_accumulation_steps=a.grad_accum,

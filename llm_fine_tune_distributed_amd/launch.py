@@ -33,34 +33,49 @@ def _free_port(addr: str) -> int:
     return p
 
 
-def _spawn(n: int, cmd: List[str], addr: str, port: int, restart: int, node_rank: int, nnodes: int) -> List[subprocess.Popen]:
+def _die_with_parent():
+    """Child pre-exec: SIGTERM this rank when the launcher dies (PR_SET_PDEATHSIG), so a launcher killed by
+    a time limit never leaves ranks holding GPUs."""
+    try:
+        import ctypes
+        ctypes.CDLL("libc.so.6", use_errno=True).prctl(1, signal.SIGTERM)  # 1 = PR_SET_PDEATHSIG
+    except Exception:
+        pass
+
+
+def _spawn(n: int, cmd: List[str], addr: str, port: int, restart: int, node_rank: int, nnodes: int,
+           new_session: bool = True) -> List[subprocess.Popen]:
     procs = []
     for lr in range(n):
         env = dict(os.environ)
         env.update(WORLD_SIZE=str(n * nnodes), RANK=str(node_rank * n + lr), LOCAL_RANK=str(lr),
                    LOCAL_WORLD_SIZE=str(n), GROUP_RANK=str(node_rank), MASTER_ADDR=addr, MASTER_PORT=str(port),
-                   SFTAMD_RESTART_COUNT=str(restart), HSA_ENABLE_IPC_MODE_LEGACY="0")
+                   SFTAMD_RESTART_COUNT=str(restart), HSA_ENABLE_IPC_MODE_LEGACY="0", SFTAMD_LAUNCHER="sftamd")
         env.setdefault("OMP_NUM_THREADS", "1")
-        procs.append(subprocess.Popen(cmd, env=env, start_new_session=True))
+        procs.append(subprocess.Popen(cmd, env=env, start_new_session=new_session, preexec_fn=_die_with_parent))
     return procs
 
 
-def _terminate(procs: List[subprocess.Popen], grace: float):
+def _signal(p: subprocess.Popen, sig, group: bool):
+    try:
+        if group:
+            os.killpg(p.pid, sig)
+        else:
+            p.send_signal(sig)
+    except ProcessLookupError:
+        pass
+
+
+def _terminate(procs: List[subprocess.Popen], grace: float, group: bool = True):
     for p in procs:
         if p.poll() is None:
-            try:
-                os.killpg(p.pid, signal.SIGTERM)
-            except ProcessLookupError:
-                pass
+            _signal(p, signal.SIGTERM, group)
     t0 = time.time()
     while time.time() - t0 < grace and any(p.poll() is None for p in procs):
         time.sleep(0.1)
     for p in procs:
         if p.poll() is None:
-            try:
-                os.killpg(p.pid, signal.SIGKILL)
-            except ProcessLookupError:
-                pass
+            _signal(p, signal.SIGKILL, group)
     for p in procs:
         p.wait()
 
@@ -75,6 +90,8 @@ def run(argv=None) -> int:
     ap.add_argument("--max-restarts", type=int, default=0)
     ap.add_argument("--grace", type=float, default=10.0)
     ap.add_argument("--monitor-interval", type=float, default=0.5)
+    ap.add_argument("--same-session", action="store_true",
+                    help="keep the ranks in the launcher's process group (a signal to the group reaches them)")
     ap.add_argument("-m", dest="module", default=None, help="run a module (like python -m)")
     ap.add_argument("script", nargs="?")
     ap.add_argument("args", nargs=argparse.REMAINDER)
@@ -88,7 +105,9 @@ def run(argv=None) -> int:
     restart = 0
     while True:
         port = a.master_port or _free_port(a.master_addr)
-        procs = _spawn(a.nproc_per_node, cmd, a.master_addr, port, restart, a.node_rank, a.nnodes)
+        procs = _spawn(a.nproc_per_node, cmd, a.master_addr, port, restart, a.node_rank, a.nnodes,
+                       new_session=not a.same_session)
+        grp = not a.same_session
         failed = None
         try:
             while True:
@@ -101,12 +120,12 @@ def run(argv=None) -> int:
                     return 0
                 time.sleep(a.monitor_interval)
         except KeyboardInterrupt:
-            _terminate(procs, a.grace)
+            _terminate(procs, a.grace, grp)
             return 130
         rank, code = failed
         print(f"[launch] local rank {rank} exited with code {code}; terminating the other ranks", file=sys.stderr,
               flush=True)
-        _terminate(procs, a.grace)
+        _terminate(procs, a.grace, grp)
         if restart >= a.max_restarts:
             return code if code > 0 else 1
         restart += 1

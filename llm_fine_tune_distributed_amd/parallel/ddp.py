@@ -25,10 +25,21 @@ that maps to MI355X + RCCL over xGMI:
   ALL-GATHERED back bucket by bucket under the next forward. The bucket padding below makes every
   slice an equal, 128-byte-aligned 1/world_size of its bucket.
 
-Bucket sizing for xGMI: each GPU has 7 point-to-point links; RCCL rings stripe a message over
-its channels, so per-call latency (tens of microseconds) dominates small buckets while very
-large ones delay the start of communication. Buckets are padded to a multiple of
-``world_size * 64`` elements so every shard is 128-byte aligned.
+Bucket sizing for xGMI (``plan_bucket_mb``): each MI355X has 7 point-to-point xGMI links, one per
+peer, and RCCL stripes a collective over channels that use all N-1 of them, so a reduce-scatter of S
+bytes costs about ``alpha + S / (N * L)`` (``alpha`` = per-call latency, ``L`` = effective per-link
+bandwidth). The cap is the smallest S whose latency share is <= ~15% (``S >= 5.7 * alpha * N * L``),
+clamped to [16, 256] MB and to >= 8 buckets over the model, then rounded so every one of the N shards is a
+whole number of 4 KiB pages. With the default ``alpha`` = 30 us and ``L`` = 100 GB/s (env
+``SFTAMD_XGMI_ALPHA_US`` / ``SFTAMD_XGMI_LINK_GBPS``) this gives 33 / 65 / 130 MB at N = 2 / 4 / 8 — grown
+with N because each rank moves only 1/N of a bucket per link (the reference's 50 MB cap,
+``training.py:253``, was sized for a single TCP ring). The first bucket stays small (4 MB) so
+communication starts early in backward.
+
+Oversized parameters (larger than twice the cap, e.g. Llama-3-8B's 1 GB untied lm_head or the 525 MB
+tied SmolLM3 embedding) are SPLIT across consecutive buckets at shard-aligned cut points: every bucket
+that holds a slice of the parameter counts it, and the parameter's ready signal completes all of them,
+so no collective is larger than ~2 caps and ZeRO-1 state / gathers stay evenly spread.
 """
 from __future__ import annotations
 
@@ -56,12 +67,30 @@ def _no_decay(name: str, p: torch.Tensor) -> bool:
     return p.dim() < 2 or "norm" in name or name.endswith(".bias")
 
 
+SHARD_PAGE_BYTES = 4096  # every reduce-scatter / all-gather shard is a whole number of 4 KiB pages
+
+
+def plan_bucket_mb(world_size: int, total_bytes: int = 0, alpha_us: Optional[float] = None,
+                   link_gbps: Optional[float] = None) -> float:
+    """Gradient-bucket cap (MB) for a reduce-scatter / all-reduce over N ranks on the xGMI full mesh
+    (see the module docstring): latency share <= ~15%, clamped to [16, 256] MB and to >= 8 buckets."""
+    import os
+    alpha = (alpha_us if alpha_us is not None else float(os.environ.get("SFTAMD_XGMI_ALPHA_US", "30"))) * 1e-6
+    link = (link_gbps if link_gbps is not None else float(os.environ.get("SFTAMD_XGMI_LINK_GBPS", "100"))) * 1e9
+    n = max(1, world_size)
+    mb = 5.7 * alpha * n * link / 2 ** 20
+    if total_bytes > 0:
+        mb = min(mb, max(16.0, total_bytes / 8 / 2 ** 20))
+    return float(min(256.0, max(16.0, mb)))
+
+
 class DDPEngine:
     def __init__(self, model: torch.nn.Module, world_size: int = 1, rank: int = 0,
-                 bucket_cap_mb: float = 50.0, first_bucket_mb: float = 4.0, grad_dtype: Optional[torch.dtype] = None,
+                 bucket_cap_mb: Optional[float] = None, first_bucket_mb: float = 4.0,
+                 grad_dtype: Optional[torch.dtype] = None,
                  broadcast_params: bool = False, align: int = 64, process_group=None,
                  no_decay_fn: Callable[[str, torch.Tensor], bool] = _no_decay, shard: bool = False,
-                 track_norm: Optional[bool] = None):
+                 track_norm: Optional[bool] = None, split_oversized: bool = True):
         self.model = model
         self.world_size = world_size
         self.rank = rank
@@ -86,19 +115,24 @@ class DDPEngine:
         self.dtype = dtype
         self.device = dev
         self.grad_dtype = grad_dtype or dtype
-        pad_unit = align * max(1, world_size)
+        esz = torch.empty((), dtype=self.grad_dtype).element_size()
+        # bucket boundaries: multiples of world_size * (4 KiB of elements) -> equal, page-aligned shards
+        pad_unit = max(align, SHARD_PAGE_BYTES // esz) * max(1, world_size)
 
         def rup(x, m):
             return (x + m - 1) // m * m
 
-        # layout + buckets in one pass: buckets are contiguous slices whose boundaries are
-        # multiples of world_size*align elements (equal, aligned shards for reduce-scatter)
-        cap = int(bucket_cap_mb * 1024 * 1024 / torch.empty((), dtype=self.grad_dtype).element_size())
-        first_cap = int(first_bucket_mb * 1024 * 1024 / torch.empty((), dtype=self.grad_dtype).element_size())
+        if not bucket_cap_mb:
+            bucket_cap_mb = plan_bucket_mb(world_size, sum(p.numel() for _, p in named) * esz)
+        self.bucket_cap_mb = float(bucket_cap_mb)
+        cap = max(pad_unit, int(bucket_cap_mb * 1024 * 1024 / esz))
+        first_cap = max(pad_unit, int(first_bucket_mb * 1024 * 1024 / esz))
+        split_at = 2 * cap if split_oversized else None
         self.layout: List[tuple] = []  # (param, offset, numel, region)
         self.regions = []  # (start, end, weight_decay_enabled)
         self.buckets: List[Bucket] = []
-        self.param_bucket: Dict[int, Bucket] = {}
+        self.param_bucket: Dict[int, List[Bucket]] = {}
+        self.num_split_params = 0
         off = 0
         for region, plist in (("decay", decay), ("no_decay", nodecay)):
             if not plist:
@@ -116,9 +150,21 @@ class DDPEngine:
                     cur = Bucket(index=len(self.buckets), start=off, end=off)
                     self.buckets.append(cur)
                 self.layout.append((p, off, p.numel(), region))
+                owners = [cur]
                 cur.params.append(p)
-                self.param_bucket[id(p)] = cur
-                off += sz
+                end = off + sz
+                if split_at is not None and sz > split_at:
+                    # oversized: cut into ~cap-sized buckets at shard-aligned points inside the parameter
+                    self.num_split_params += 1
+                    while end - cur.start > split_at:
+                        cut = (cur.start + cap) // pad_unit * pad_unit
+                        cur.end = cut
+                        cur = Bucket(index=len(self.buckets), start=cut, end=cut)
+                        self.buckets.append(cur)
+                        cur.params.append(p)
+                        owners.append(cur)
+                self.param_bucket[id(p)] = owners
+                off = end
             off = rup(off, pad_unit)
             cur.end = off
             self.regions.append((rs, off, region == "decay"))
@@ -224,15 +270,17 @@ class DDPEngine:
     def _on_param_ready(self, p):
         if not self.sync_grads or (self.world_size == 1 and not self.track_norm):
             return
-        b = self.param_bucket.get(id(p))
-        if b is None:
+        owners = self.param_bucket.get(id(p))
+        if owners is None:
             return
-        b.pending -= 1
-        if b.pending < 0:
-            raise RuntimeError(f"DDP bucket {b.index}: parameter {self.param_names.get(id(p))} signalled ready twice")
-        if b.pending == 0:
-            b.ready = True
-            self._launch_ready()
+        for b in owners:
+            b.pending -= 1
+            if b.pending < 0:
+                raise RuntimeError(f"DDP bucket {b.index}: parameter {self.param_names.get(id(p))} signalled ready "
+                                   "twice")
+            if b.pending == 0:
+                b.ready = True
+        self._launch_ready()
 
     def _launch_ready(self):
         while self._next < len(self.buckets) and self.buckets[self._next].ready:

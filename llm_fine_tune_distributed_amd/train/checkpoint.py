@@ -4,7 +4,8 @@
   at most ``max_shard_size`` + ``model.safetensors.index.json``), HF key names, the tied lm_head
   deduplicated, ``config.json`` and ``generation_config.json``. Written to a temp dir and renamed
   (atomic), rank 0 only.
-* ``save_checkpoint`` adds ``optimizer.pt`` (flat fp32 master / moments), ``scheduler.pt``,
+* ``save_checkpoint`` adds ``optimizer.pt`` (Adam moments / fp32 master keyed by parameter name, so it
+  resumes at any world size; gathered from the ZeRO-1 shards by every rank), ``scheduler.pt``,
   per-rank ``rng_state_{rank}.pth``, ``trainer_state.json`` and ``training_args.json`` under
   ``checkpoint-{step}/``; ``rotate_checkpoints`` keeps ``save_total_limit`` (never the best one).
 * ``load_checkpoint`` restores everything for ``resume_from_checkpoint`` (``"auto"`` = latest).
@@ -169,12 +170,19 @@ def set_rng_state(st: Dict):
 
 
 def save_checkpoint(path: str, model, optimizer, scheduler, state, args, rank: int, tokenizer=None,
-                    extra: Optional[Dict] = None):
+                    extra: Optional[Dict] = None, optimizer_state: Optional[Dict] = None):
     """Rank 0 writes model/optimizer/scheduler/state; every rank writes its RNG state.
-    Caller must barrier before and after."""
+    Caller must barrier before and after. ``optimizer_state`` must be gathered by EVERY rank beforehand
+    (``optimizer.state_dict()`` is a collective under ZeRO-1); it is only computed here when missing,
+    which is safe for replicated optimizers only."""
+    if optimizer_state is None and rank == 0:
+        if type(optimizer).__name__ == "ShardedAdamW" and optimizer.engine.world_size > 1:
+            raise RuntimeError("ShardedAdamW.state_dict() is collective: gather it on every rank and pass "
+                               "optimizer_state=")
+        optimizer_state = optimizer.state_dict()
     if rank == 0:
         save_pretrained(model, path, tokenizer=tokenizer)
-        torch.save(optimizer.state_dict(), os.path.join(path, "optimizer.pt"))
+        torch.save(optimizer_state, os.path.join(path, "optimizer.pt"))
         torch.save({**scheduler.state_dict(), **(extra or {})}, os.path.join(path, "scheduler.pt"))
         state.to_json(os.path.join(path, "trainer_state.json"))
         args.to_json(os.path.join(path, "training_args.json"))
@@ -221,7 +229,7 @@ def load_checkpoint(path: str, model, optimizer, scheduler, rank: int):
         ad = os.path.join(path, "adapter_model.safetensors")
         if os.path.exists(ad):
             _load_lora(model, ad)
-    osd = torch.load(os.path.join(path, "optimizer.pt"), map_location=optimizer.engine.device, weights_only=True)
+    osd = torch.load(os.path.join(path, "optimizer.pt"), map_location="cpu", weights_only=True)
     optimizer.load_state_dict(osd)
     ssd = torch.load(os.path.join(path, "scheduler.pt"), weights_only=True)
     scheduler.load_state_dict(ssd)

@@ -174,21 +174,67 @@ class FlatAdamW:
             upd(s, t, decay)
         return norm
 
+    # ------------------------------------------------------------------ checkpoints (per parameter)
+    def _full_state(self, key: str) -> Optional[torch.Tensor]:
+        """The whole-model flat tensor of ``key`` in this engine's layout (collective under ZeRO-1)."""
+        return {"exp_avg": self.exp_avg, "exp_avg_sq": self.exp_avg_sq, "master": self.master}[key]
+
+    def _state_ranges(self):
+        """(global_start, global_end, local_offset) of the flat state this rank holds."""
+        return [(0, self.engine.numel, 0)]
+
     def state_dict(self) -> Dict:
+        """Adam state keyed by PARAMETER NAME (``param_state[name] = {exp_avg, exp_avg_sq, master}`` with the
+        parameter's shape), so a checkpoint resumes at any world size / bucket plan: the flat layout pads
+        buckets to multiples of world_size pages and is therefore world-size dependent. Every rank must
+        call this (ZeRO-1 gathers the sharded state); tensors are host copies."""
         self.synchronize()
-        return {"step": self.step_count, "exp_avg": self.exp_avg, "exp_avg_sq": self.exp_avg_sq,
-                "master": self.master, "lr": self.lr, "betas": self.betas, "eps": self.eps,
-                "weight_decay": self.weight_decay}
+        e = self.engine
+        full = {}
+        for k in ("exp_avg", "exp_avg_sq", "master"):
+            t = self._full_state(k)
+            full[k] = None if t is None else t.detach().cpu()
+        ps = {}
+        for p, o, n, _ in e.layout:
+            ps[e.param_names[id(p)]] = {k: (None if v is None else v[o:o + n].view(p.shape)) for k, v in full.items()}
+        return {"format": "sftamd-adamw-v2", "step": self.step_count, "param_state": ps,
+                "state_dtype": str(self.state_dtype).replace("torch.", ""), "lr": self.lr, "betas": self.betas,
+                "eps": self.eps, "weight_decay": self.weight_decay, "saved_world_size": e.world_size}
 
     def load_state_dict(self, sd: Dict):
+        e = self.engine
         self.step_count = int(sd["step"])
-        self.exp_avg.copy_(sd["exp_avg"])  # copy_ converts between fp32 / bf16 state checkpoints
-        self.exp_avg_sq.copy_(sd["exp_avg_sq"])
-        if self.master is not None:
-            if sd.get("master") is not None:
-                self.master.copy_(sd["master"])
-            else:
-                self.master.copy_(self.engine.param_flat.float())
+        ranges = self._state_ranges()
+        dsts = {"exp_avg": self.exp_avg, "exp_avg_sq": self.exp_avg_sq, "master": self.master}
+        if "param_state" not in sd:  # round-1 flat format: only valid for the same layout
+            if sd["exp_avg"].numel() != e.numel:
+                raise ValueError(f"flat optimizer state of {sd['exp_avg'].numel()} elements does not match this "
+                                 f"layout ({e.numel}); re-save with the per-parameter format")
+            for s, t, lo in ranges:
+                for k in ("exp_avg", "exp_avg_sq"):
+                    dsts[k][lo:lo + t - s].copy_(sd[k][s:t])
+                if self.master is not None:
+                    src = sd.get("master")
+                    self.master[lo:lo + t - s].copy_(src[s:t] if src is not None else e.param_flat[s:t].float())
+            return
+        ps = sd["param_state"]
+        missing = [e.param_names[id(p)] for p, _, _, _ in e.layout if e.param_names[id(p)] not in ps]
+        if missing:
+            raise KeyError(f"optimizer checkpoint has no state for {missing[:4]}{'...' if len(missing) > 4 else ''}")
+        for p, o, n, _ in e.layout:
+            st = ps[e.param_names[id(p)]]
+            for s, t, lo in ranges:
+                a, b = max(s, o), min(t, o + n)
+                if a >= b:
+                    continue
+                for k in ("exp_avg", "exp_avg_sq", "master"):
+                    dst = dsts[k]
+                    if dst is None:
+                        continue
+                    src = st.get(k)
+                    if src is None:  # no saved master: start it from the current (bf16) parameters
+                        src = e.param_flat[o:o + n].float()
+                    dst[lo + a - s:lo + b - s].copy_(src.reshape(-1)[a - o:b - o].to(dst.device, dst.dtype))
 
 
 class ShardedAdamW(FlatAdamW):
@@ -202,7 +248,8 @@ class ShardedAdamW(FlatAdamW):
     while the next forward runs: a layer's forward pre-hook waits only for its own buckets.
     The update itself is the same fused HIP kernel, with the stochastic-rounding stream keyed by the
     GLOBAL element index, so a sharded run rounds exactly like the replicated one.
-    Checkpoints hold the full (gathered) state, interchangeable with ``FlatAdamW``'s."""
+    Checkpoints hold the full (gathered) per-parameter state, interchangeable with ``FlatAdamW``'s and
+    loadable at any world size."""
 
     def __init__(self, engine, lr: float, betas=(0.9, 0.999), eps: float = 1e-8, weight_decay: float = 0.0,
                  master_weights: bool = True, stochastic_rounding: bool = True, state_dtype=torch.float32):
@@ -252,9 +299,9 @@ class ShardedAdamW(FlatAdamW):
         def buckets_of(params):
             out = []
             for p in params:
-                b = e.param_bucket.get(id(p))
-                if b is not None and b.index not in out:
-                    out.append(b.index)
+                for b in e.param_bucket.get(id(p), ()):
+                    if b.index not in out:
+                        out.append(b.index)
             return out
 
         groups = [buckets_of([inner.embed_tokens])]
@@ -341,33 +388,21 @@ class ShardedAdamW(FlatAdamW):
         return norm
 
     # ------------------------------------------------------------------ checkpoints: full (gathered) state
-    def _gather_full(self, local: torch.Tensor, dtype) -> torch.Tensor:
+    def _full_state(self, key: str) -> Optional[torch.Tensor]:
         import torch.distributed as dist
+        local = {"exp_avg": self.exp_avg, "exp_avg_sq": self.exp_avg_sq, "master": self.master}[key]
+        if local is None:
+            return None
         e = self.engine
-        full = torch.zeros(e.numel, dtype=dtype, device=e.device)
+        full = torch.zeros(e.numel, dtype=local.dtype, device=e.device)
         for b, s, t, lo, _ in self.slices:
             full[s:t].copy_(local[lo:lo + t - s])
             if e.world_size > 1:
                 dist.all_gather_into_tensor(full[b.start:b.end], full[s:t], group=e.pg)
         return full
 
-    def state_dict(self) -> Dict:
-        self.synchronize()
-        return {"step": self.step_count, "exp_avg": self._gather_full(self.exp_avg, self.state_dtype),
-                "exp_avg_sq": self._gather_full(self.exp_avg_sq, self.state_dtype),
-                "master": None if self.master is None else self._gather_full(self.master, torch.float32),
-                "lr": self.lr, "betas": self.betas, "eps": self.eps, "weight_decay": self.weight_decay}
-
-    def load_state_dict(self, sd: Dict):
-        e = self.engine
-        self.step_count = int(sd["step"])
-        for _, s, t, lo, _ in self.slices:
-            n = t - s
-            self.exp_avg[lo:lo + n].copy_(sd["exp_avg"][s:t])
-            self.exp_avg_sq[lo:lo + n].copy_(sd["exp_avg_sq"][s:t])
-            if self.master is not None:
-                src = sd.get("master")
-                self.master[lo:lo + n].copy_(src[s:t] if src is not None else e.param_flat[s:t].float())
+    def _state_ranges(self):
+        return [(s, t, lo) for _, s, t, lo, _ in self.slices]
 
 
 def get_schedule(name: str, num_training_steps: int, num_warmup_steps: int = 0, **kw) -> Callable[[int], float]:

@@ -121,7 +121,7 @@ class SFTTrainer:
         # ------------------------------------------------------------ engine + optimizer
         shard = bool(args.shard_optimizer_state) and self.dist.world_size > 1
         self.engine = DDPEngine(model, self.dist.world_size, self.dist.rank,
-                                bucket_cap_mb=args.ddp_bucket_cap_mb or 25.0,
+                                bucket_cap_mb=args.ddp_bucket_cap_mb,  # None: xGMI plan (plan_bucket_mb)
                                 first_bucket_mb=args.ddp_first_bucket_mb,
                                 broadcast_params=args.ddp_broadcast_params, shard=shard)
         opt_cls = ShardedAdamW if shard else FlatAdamW
@@ -208,7 +208,9 @@ class SFTTrainer:
             n = torch.tensor([float(sum(b["num_items"] for b in micro))], device=self.dist.device)
         if self.args.average_tokens_across_devices:
             return all_reduce_sum_async(n)
-        return n.clamp(min=1.0)
+        # per-rank normalisation (HF: local mean per rank, DDP then AVERAGES the gradients): the buckets are
+        # SUM-reduced here, so each rank's local count is scaled by the world size
+        return n.clamp(min=1.0) * self.dist.world_size
 
     def optimizer_step(self, micro: List[Dict], lr: float) -> Dict[str, torch.Tensor]:
         """One optimizer step over ``micro`` (GA micro-batches). Returns device-side sums:
@@ -278,10 +280,14 @@ class SFTTrainer:
         self.optimizer.synchronize()
         a = self.args
         path = os.path.join(a.output_dir, f"checkpoint-{self.state.global_step}")
+        # EVERY rank takes part: under ZeRO-1 the state is all-gathered from the shards (a collective that
+        # would deadlock if only rank 0 entered it while the others wait in the barrier)
+        osd = self.optimizer.state_dict()
         barrier()
         ckpt.save_rng(path, self.dist.rank)
         ckpt.save_checkpoint(path, self.model, self.optimizer, self.scheduler, self.state, a, self.dist.rank,
-                             tokenizer=self.tokenizer)
+                             tokenizer=self.tokenizer, optimizer_state=osd if self.dist.is_main else {})
+        del osd
         barrier()
         if self.dist.is_main:
             ckpt.rotate_checkpoints(a.output_dir, a.save_total_limit, self.state.best_model_checkpoint)
@@ -360,6 +366,7 @@ class SFTTrainer:
         self._timers["eval"] = 0.0
         last_norm = None
         done = self.state.global_step >= max_steps
+        start_step = self.state.global_step  # train_loss averages the steps run by THIS call
         for epoch in range(start_epoch, self.state.num_train_epochs):
             if done:
                 break
@@ -440,7 +447,8 @@ class SFTTrainer:
         runtime = time.time() - t_start
         tl = total_loss.clone()
         all_reduce_sum_(tl)
-        train_loss = tl.item() / max(1, self.state.global_step - (0 if not resume else 0))
+        steps_run = self.state.global_step - start_step
+        train_loss = tl.item() / max(1, steps_run)  # (HF divides by global_step, under-reporting after a resume)
         pure = max(runtime - self._timers["eval"], 1e-9)
         metrics = {"train_runtime": runtime, "train_samples_per_second": samples / max(runtime, 1e-9),
                    "train_steps_per_second": self.state.global_step / max(runtime, 1e-9),

@@ -16,12 +16,16 @@ out = sys.argv[1]
 cfg = tiny()
 m = build_model(cfg, dtype=torch.float32, seed=0)
 ds = TokenizedDataset.synthetic(64, cfg.vocab_size, 5, 20, seed=1)
+shard = os.environ.get("SFTAMD_TEST_SHARD", "0") == "1"
 args = SFTConfig(output_dir=out, per_device_train_batch_size=2, max_steps=6, save_steps=2, logging_steps=1,
-                 learning_rate=1e-3, dataloader_drop_last=True, jsonl_log=False, ddp_timeout=60)
+                 learning_rate=1e-3, dataloader_drop_last=True, jsonl_log=False, ddp_timeout=60,
+                 shard_optimizer_state=shard, ddp_bucket_cap_mb=0.05, ddp_first_bucket_mb=0.01)
 t = SFTTrainer(model=m, args=args, train_dataset=ds)
 r = t.train(resume_from_checkpoint="auto")
 if t.dist.is_main:
     with open(os.path.join(out, "result.json"), "w") as f:
         json.dump({"step": r.global_step, "restart": os.environ.get("SFTAMD_RESTART_COUNT"), "log": [h.get("loss") for h in t.state.log_history if "loss" in h],
-                   "checksum": float(t.engine.param_flat.double().sum())}, f)
+                   "checksum": float(t.engine.param_flat.double().sum()), "train_loss": r.training_loss,
+                   "optimizer": type(t.optimizer).__name__}, f)
+    torch.save(t.engine.param_flat.clone(), os.path.join(out, "params.pt"))
 cleanup_distributed()

@@ -1,0 +1,76 @@
+"""xGMI bucket plan and oversized-parameter splitting of the DDP engine."""
+import pytest
+import torch
+
+from llm_fine_tune_distributed_amd.models import build_model, tiny
+from llm_fine_tune_distributed_amd.parallel.ddp import DDPEngine, plan_bucket_mb
+
+
+def test_plan_grows_with_world_size_and_is_clamped():
+    caps = [plan_bucket_mb(n) for n in (1, 2, 4, 8)]
+    assert caps == sorted(caps) and caps[0] < 20 and 100 < caps[3] <= 256
+    assert plan_bucket_mb(8, total_bytes=64 * 2 ** 20) == 16.0  # tiny models still get >= 8 buckets (floor 16)
+    assert plan_bucket_mb(8, alpha_us=1000, link_gbps=1000) == 256.0
+
+
+@pytest.mark.parametrize("world", [1, 2, 8])
+def test_oversized_param_split_layout_and_ready_signalling(world):
+    m = build_model(tiny(), dtype=torch.float32, seed=0)
+    eng = DDPEngine(m, world_size=world, rank=0, bucket_cap_mb=0.05, first_bucket_mb=0.01)
+    launched = []
+    eng._collective = lambda b, view: launched.append(b.index)  # no process group needed
+    emb = m.model.embed_tokens
+    owners = eng.param_bucket[id(emb)]
+    assert eng.num_split_params >= 1 and len(owners) >= 3
+    unit = 1024 * world  # fp32: 4 KiB pages per shard
+    prev_end = None
+    for b in eng.buckets:
+        assert b.start % unit == 0 and b.end % unit == 0 and b.end > b.start
+        if prev_end is not None and b.start != prev_end:
+            assert b.start > prev_end  # only region padding between buckets
+        prev_end = b.end
+    cap = int(0.05 * 2 ** 20 / 4)
+    assert max(b.end - b.start for b in eng.buckets) <= 2 * cap + unit
+    # the split parameter's slices are contiguous consecutive buckets covering it exactly
+    o = eng.param_offset(emb)
+    assert owners[0].start <= o and owners[-1].end >= o + emb.numel()
+    assert [b.index for b in owners] == list(range(owners[0].index, owners[-1].index + 1))
+    # ready signalling: every bucket launches exactly once, in index order, after its last parameter
+    eng.prepare_backward()
+    for p in eng.params():
+        eng._on_param_ready(p)
+    if world > 1:  # (a single rank has nothing to communicate: no signalling)
+        assert launched == list(range(len(eng.buckets)))
+        assert all(b.pending == 0 and b.ready for b in eng.buckets)
+        with pytest.raises(RuntimeError, match="twice"):
+            eng._on_param_ready(emb)
+
+
+def test_full_smollm3_plan_at_8_ranks_on_meta():
+    """SmolLM3-3B full-param shapes at N=8 (meta tensors, registration order of the real model): the 525 MB
+    tied embedding is split, no bucket exceeds two caps."""
+    from llm_fine_tune_distributed_amd.models import smollm3_3b
+    c = smollm3_3b()
+
+    def P(*shape):
+        return torch.nn.Parameter(torch.empty(*shape, device="meta", dtype=torch.bfloat16))
+
+    m = torch.nn.Module()
+    m.embed_tokens = P(c.vocab_size, c.hidden_size)
+    m.layers = torch.nn.ModuleList()
+    for _ in range(c.num_hidden_layers):
+        layer = torch.nn.Module()
+        layer.input_layernorm = P(c.hidden_size)
+        layer.qkv_proj = P(c.qkv_size, c.hidden_size)
+        layer.o_proj = P(c.hidden_size, c.q_size)
+        layer.post_attention_layernorm = P(c.hidden_size)
+        layer.gate_up_proj = P(2 * c.intermediate_size, c.hidden_size)
+        layer.down_proj = P(c.hidden_size, c.intermediate_size)
+        m.layers.append(layer)
+    m.norm = P(c.hidden_size)
+    eng = DDPEngine(m, world_size=8, rank=0)
+    sizes = [(b.end - b.start) * 2 / 2 ** 20 for b in eng.buckets]
+    assert 100 < eng.bucket_cap_mb <= 256
+    assert eng.num_split_params == 1 and len(eng.param_bucket[id(m.embed_tokens)]) >= 2
+    assert max(sizes) <= 2 * eng.bucket_cap_mb + 1
+    assert sizes[0] < 50  # the last layer's down_proj alone (a parameter is never split below 2 caps)

@@ -17,7 +17,12 @@ def _free_port():
     return p
 
 
-def _run(rank, world, port, out_dir, per_dev, ga, steps, shard=False, tag=""):
+def _flat_state(osd, k):
+    """Per-parameter optimizer state (checkpoint format v2) flattened in name order."""
+    return torch.cat([v[k].reshape(-1).float() for _, v in sorted(osd["param_state"].items())])
+
+
+def _run(rank, world, port, out_dir, per_dev, ga, steps, shard=False, tag="", avg_tokens=True, fixed_len=False):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), WORLD_SIZE=str(world), RANK=str(rank),
                       LOCAL_RANK=str(rank))
     import llm_fine_tune_distributed_amd.parallel.process_group as pgm
@@ -28,27 +33,28 @@ def _run(rank, world, port, out_dir, per_dev, ga, steps, shard=False, tag=""):
     torch.manual_seed(0)
     cfg = tiny()
     m = build_model(cfg, dtype=torch.float32, seed=3)
-    ds = TokenizedDataset.synthetic(64, cfg.vocab_size, 5, 20, seed=7)
+    ds = TokenizedDataset.synthetic(64, cfg.vocab_size, 12 if fixed_len else 5, 12 if fixed_len else 20, seed=7)
     args = SFTConfig(output_dir=out_dir, per_device_train_batch_size=per_dev, gradient_accumulation_steps=ga,
                      learning_rate=1e-3, max_steps=steps, logging_steps=1, dataloader_drop_last=True,
                      jsonl_log=False, ddp_check_sync_every=1, ddp_bucket_cap_mb=0.05, ddp_first_bucket_mb=0.01,
-                     save_strategy="no", shard_optimizer_state=shard)
+                     save_strategy="no", shard_optimizer_state=shard, average_tokens_across_devices=avg_tokens)
     t = SFTTrainer(model=m, args=args, train_dataset=ds)
     out = t.train()
     osd = t.optimizer.state_dict()  # collective in ZeRO-1 mode: every rank takes part
     torch.save({"params": t.engine.param_flat.clone(), "loss": out.training_loss,
-                "log": [h for h in t.state.log_history if "loss" in h], "exp_avg": osd["exp_avg"].clone(),
-                "exp_avg_sq": osd["exp_avg_sq"].clone(), "sharded": type(t.optimizer).__name__},
+                "log": [h for h in t.state.log_history if "loss" in h], "exp_avg": _flat_state(osd, "exp_avg"),
+                "exp_avg_sq": _flat_state(osd, "exp_avg_sq"), "sharded": type(t.optimizer).__name__},
                os.path.join(out_dir, f"r{world}_{rank}{tag}.pt"))
     pgm.cleanup_distributed()
 
 
-def _launch(world, per_dev, ga, steps, d, shard=False, tag=""):
+def _launch(world, per_dev, ga, steps, d, shard=False, tag="", avg_tokens=True, fixed_len=False):
     port = _free_port()
     if world == 1:
-        _run(0, 1, port, d, per_dev, ga, steps, shard, tag)
+        _run(0, 1, port, d, per_dev, ga, steps, shard, tag, avg_tokens, fixed_len)
     else:
-        mp.spawn(_run, args=(world, port, d, per_dev, ga, steps, shard, tag), nprocs=world, join=True)
+        mp.spawn(_run, args=(world, port, d, per_dev, ga, steps, shard, tag, avg_tokens, fixed_len), nprocs=world,
+                 join=True)
 
 
 def test_ddp2_matches_single_process():
@@ -113,3 +119,67 @@ def test_zero1_world4_matches_replicated():
         assert torch.allclose(z[0][k], rep[0][k], atol=1e-7, rtol=1e-4)
     for a, b in zip(rep[0]["log"], z[0]["log"]):
         assert abs(a["loss"] - b["loss"]) < 1e-5
+
+
+def test_local_token_normalisation_matches_single_process():
+    """average_tokens_across_devices=False (HF: each rank's loss is its LOCAL mean, DDP averages the
+    gradients): with equal token counts per rank, world 2 == world 1 on the same global batch — the
+    SUM-reduced buckets must not make the gradients world_size times larger."""
+    d = tempfile.mkdtemp()
+    _launch(1, 4, 1, 2, d, tag="_l", avg_tokens=False, fixed_len=True)
+    _launch(2, 2, 1, 2, d, tag="_l", avg_tokens=False, fixed_len=True)
+    single = torch.load(os.path.join(d, "r1_0_l.pt"))
+    r0 = torch.load(os.path.join(d, "r2_0_l.pt"))
+    assert torch.allclose(r0["params"], single["params"], atol=1e-5, rtol=1e-4)
+    for a, b in zip(single["log"], r0["log"]):
+        assert abs(a["loss"] - b["loss"]) < 1e-4
+        assert abs(a["grad_norm"] - b["grad_norm"]) < 1e-3 * max(1.0, a["grad_norm"])
+
+
+def _save_zero_ckpt(rank, world, port, out_dir):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), WORLD_SIZE=str(world), RANK=str(rank),
+                      LOCAL_RANK=str(rank))
+    import llm_fine_tune_distributed_amd.parallel.process_group as pgm
+    pgm._STATE = None
+    from llm_fine_tune_distributed_amd.data.dataset import TokenizedDataset
+    from llm_fine_tune_distributed_amd.models import build_model, tiny
+    from llm_fine_tune_distributed_amd.train import SFTConfig, SFTTrainer
+    cfg = tiny()
+    m = build_model(cfg, dtype=torch.float32, seed=3)
+    ds = TokenizedDataset.synthetic(64, cfg.vocab_size, 5, 20, seed=7)
+    args = SFTConfig(output_dir=out_dir, per_device_train_batch_size=2, learning_rate=1e-3, max_steps=2,
+                     logging_steps=0, jsonl_log=False, save_strategy="steps", save_steps=2,
+                     shard_optimizer_state=True, ddp_bucket_cap_mb=0.05, ddp_first_bucket_mb=0.01,
+                     master_weights=True)
+    SFTTrainer(model=m, args=args, train_dataset=ds).train()
+    pgm.cleanup_distributed()
+
+
+def test_zero1_checkpoint_resumes_at_another_world_size():
+    """The optimizer checkpoint is keyed by parameter name, not by the world-size-dependent flat layout:
+    a ZeRO-1 checkpoint written at world 4 loads into a replicated optimizer at world 1 exactly."""
+    d = tempfile.mkdtemp()
+    mp.spawn(_save_zero_ckpt, args=(4, _free_port(), d), nprocs=4, join=True)
+    path = os.path.join(d, "checkpoint-2")
+    saved = torch.load(os.path.join(path, "optimizer.pt"), weights_only=True)
+    assert saved["format"] == "sftamd-adamw-v2" and saved["saved_world_size"] == 4
+    from llm_fine_tune_distributed_amd.data.dataset import TokenizedDataset
+    from llm_fine_tune_distributed_amd.models import build_model, tiny
+    from llm_fine_tune_distributed_amd.train import SFTConfig, SFTTrainer
+    from llm_fine_tune_distributed_amd.train import checkpoint as ck
+    import llm_fine_tune_distributed_amd.parallel.process_group as pgm
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK"):
+        os.environ.pop(k, None)
+    pgm._STATE = None
+    cfg = tiny()
+    t = SFTTrainer(model=build_model(cfg, dtype=torch.float32, seed=5),
+                   args=SFTConfig(output_dir=tempfile.mkdtemp(), jsonl_log=False, max_steps=1, master_weights=True),
+                   train_dataset=TokenizedDataset.synthetic(8, cfg.vocab_size, 5, 20, seed=7))
+    from llm_fine_tune_distributed_amd.train.optim import LRScheduler, get_schedule
+    t.scheduler = LRScheduler(t.optimizer, get_schedule("linear", 10))
+    ck.load_checkpoint(path, t.model, t.optimizer, t.scheduler, 0)
+    got = t.optimizer.state_dict()
+    assert got["step"] == saved["step"] == 2
+    for name, st in saved["param_state"].items():
+        for k in ("exp_avg", "exp_avg_sq", "master"):
+            assert torch.equal(got["param_state"][name][k], st[k]), (name, k)
