@@ -42,6 +42,10 @@ def main(argv=None):
     ap.add_argument("--no-gradient-checkpointing", action="store_true")
     ap.add_argument("--resume", default=None, help="checkpoint dir or 'auto'")
     ap.add_argument("--max-train-samples", type=int, default=None)
+    ap.add_argument("--log-step-phases", action="store_true",
+                    help="log data/fwd/bwd/comm_wait/optim *_ms per step (roctx ranges around each phase)")
+    ap.add_argument("--log-system-metrics-every", type=int, default=int(os.getenv("LOG_SYSTEM_METRICS_EVERY", "0")),
+                    help="GPU telemetry (amdsmi) into the trackers every N log steps (0 = off)")
     ap.add_argument("--config", default=os.getenv("SFT_CONFIG"),
                     help="YAML/JSON file of SFTConfig field overrides (applied over the reference defaults)")
     ap.add_argument("--set", dest="sets", action="append", default=[], metavar="FIELD=VALUE",
@@ -93,6 +97,7 @@ def main(argv=None):
         gradient_checkpointing=not a.no_gradient_checkpointing, dataloader_drop_last=True,
         max_seq_length=a.max_length, packing=a.packing, ddp_backend="nccl" if st.device.type == "cuda" else "gloo",
         freeze_policy=a.freeze_policy, lr_scheduler_type=a.lr_scheduler, max_train_samples=a.max_train_samples,
+        log_step_phases=a.log_step_phases, log_system_metrics_every=a.log_system_metrics_every,
         **dist_args)
     args = apply_overrides(args, a.config, a.sets)
     if st.is_main:  # the resolved configuration of this run, next to its artifacts

@@ -112,3 +112,50 @@ def tokenize_rows(rows: Sequence[Dict], tokenizer, max_length: Optional[int] = N
     if max_length:
         ids = [s[:max_length] for s in ids]  # TRL truncation at max_length (training.py:282)
     return TokenizedDataset.from_token_lists(ids, starts if assistant_only_loss else None)
+
+
+def _fingerprint(rows: Sequence[Dict], tokenizer, **kw) -> str:
+    import hashlib
+    import json
+    h = hashlib.sha256()
+    h.update(json.dumps(kw, sort_keys=True, default=str).encode())
+    tk = getattr(tokenizer, "_tk", None)
+    h.update((tk.to_str() if tk is not None else repr(type(tokenizer))).encode())
+    h.update(str(getattr(tokenizer, "chat_template", None)).encode())
+    for r in rows:
+        h.update(json.dumps(r, sort_keys=True, default=str).encode())
+    return h.hexdigest()[:24]
+
+
+def cached_tokenize(rows: Sequence[Dict], tokenizer, cache_dir: Optional[str], is_main: bool = True,
+                    barrier: Optional[Callable[[], None]] = None, max_length: Optional[int] = None,
+                    assistant_only_loss: bool = False, text_field: str = "text") -> TokenizedDataset:
+    """TRL's ``main_process_first`` tokenisation: rank 0 renders + tokenises and writes the
+    CSR arrays to ``cache_dir/tokenized-<fingerprint>.pt``; the other ranks wait at ``barrier`` and load
+    them. The fingerprint covers the rows, the tokenizer (vocabulary + template) and the options, so a
+    rerun with the same inputs loads instead of re-tokenising. Without ``cache_dir`` every rank tokenises."""
+    import os
+    kw = dict(max_length=max_length, assistant_only_loss=assistant_only_loss, text_field=text_field)
+    if not cache_dir:
+        return tokenize_rows(rows, tokenizer, **kw)
+    path = os.path.join(cache_dir, f"tokenized-{_fingerprint(rows, tokenizer, **kw)}.pt")
+
+    def load():
+        d = torch.load(path, weights_only=True)
+        return TokenizedDataset(d["tokens"], d["offsets"], d.get("loss_start"))
+
+    ds = None
+    if is_main:
+        if os.path.exists(path):
+            ds = load()
+        else:
+            ds = tokenize_rows(rows, tokenizer, **kw)
+            os.makedirs(cache_dir, exist_ok=True)
+            tmp = f"{path}.tmp{os.getpid()}"
+            torch.save({"tokens": ds.tokens, "offsets": ds.offsets, "loss_start": ds.loss_start}, tmp)
+            os.replace(tmp, path)
+    if barrier is not None:
+        barrier()
+    if ds is None:
+        ds = load() if os.path.exists(path) else tokenize_rows(rows, tokenizer, **kw)  # no shared filesystem
+    return ds

@@ -15,7 +15,7 @@ import json
 import os
 from typing import Dict, Iterable, List, Optional
 
-from . import chat_template
+from . import chat_template as chat_template_mod
 
 SPECIAL_TOKENS = ["<|begin_of_text|>", "<|end_of_text|>", "<|im_start|>", "<|im_end|>",
                   "<|finetune_right_pad_id|>", "<think>", "</think>"]
@@ -23,8 +23,10 @@ SPECIAL_TOKENS = ["<|begin_of_text|>", "<|end_of_text|>", "<|im_start|>", "<|im_
 
 class SFTTokenizer:
     def __init__(self, tk, eos_token: str = "<|im_end|>", bos_token: Optional[str] = None,
-                 pad_token: Optional[str] = None, chat_kwargs: Optional[dict] = None):
+                 pad_token: Optional[str] = None, chat_kwargs: Optional[dict] = None,
+                 chat_template: Optional[str] = None):
         self._tk = tk
+        self.chat_template = chat_template  # the tokenizer's own Jinja template (None: built-in renderer)
         self.eos_token = eos_token
         self.bos_token = bos_token
         self.pad_token = pad_token or eos_token  # reference: pad = eos
@@ -68,9 +70,21 @@ class SFTTokenizer:
         return {"input_ids": self.encode(text)}
 
     def apply_chat_template(self, messages: List[Dict[str, str]], tokenize: bool = True,
-                            add_generation_prompt: bool = False, enable_thinking: bool = False, **_):
-        text = chat_template.render(messages, add_generation_prompt=add_generation_prompt,
-                                    enable_thinking=enable_thinking, **self.chat_kwargs)
+                            add_generation_prompt: bool = False, enable_thinking: Optional[bool] = None,
+                            chat_template: Optional[str] = None, **kwargs):
+        """HF semantics: the tokenizer's Jinja template when it has one (extra kwargs such as
+        ``enable_thinking`` reach the template), else the built-in SmolLM3-style ChatML renderer."""
+        tpl = chat_template or self.chat_template
+        if tpl:
+            if enable_thinking is not None:
+                kwargs["enable_thinking"] = enable_thinking
+            text = chat_template_mod.render_jinja(
+                tpl, messages, add_generation_prompt=add_generation_prompt,
+                special_tokens={"bos_token": self.bos_token, "eos_token": self.eos_token,
+                                "pad_token": self.pad_token}, **kwargs)
+        else:
+            text = chat_template_mod.render(messages, add_generation_prompt=add_generation_prompt,
+                                            enable_thinking=bool(enable_thinking), **self.chat_kwargs)
         return self.encode(text) if tokenize else text
 
     # ------------------------------------------------------------------ io
@@ -78,9 +92,13 @@ class SFTTokenizer:
         os.makedirs(path, exist_ok=True)
         self._tk.save(os.path.join(path, "tokenizer.json"))
         with open(os.path.join(path, "tokenizer_config.json"), "w") as f:
-            json.dump({"eos_token": self.eos_token, "bos_token": self.bos_token, "pad_token": self.pad_token,
-                       "padding_side": self.padding_side, "chat_template_style": "smollm3-chatml",
-                       "tokenizer_class": "PreTrainedTokenizerFast"}, f, indent=2)
+            cfg = {"eos_token": self.eos_token, "bos_token": self.bos_token, "pad_token": self.pad_token,
+                   "padding_side": self.padding_side, "tokenizer_class": "PreTrainedTokenizerFast"}
+            if self.chat_template:
+                cfg["chat_template"] = self.chat_template
+            else:
+                cfg["chat_template_style"] = "smollm3-chatml"
+            json.dump(cfg, f, indent=2)
 
     @classmethod
     def from_pretrained(cls, path: str) -> "SFTTokenizer":
@@ -96,7 +114,13 @@ class SFTTokenizer:
             return v.get("content") if isinstance(v, dict) else v
 
         eos = tok(cfg.get("eos_token")) or "<|im_end|>"
-        return cls(tk, eos_token=eos, bos_token=tok(cfg.get("bos_token")), pad_token=tok(cfg.get("pad_token")))
+        tpl = chat_template_mod.select_template(cfg.get("chat_template"))
+        jp = os.path.join(path, "chat_template.jinja")  # newer transformers save the template as its own file
+        if tpl is None and os.path.exists(jp):
+            with open(jp) as f:
+                tpl = f.read()
+        return cls(tk, eos_token=eos, bos_token=tok(cfg.get("bos_token")), pad_token=tok(cfg.get("pad_token")),
+                   chat_template=tpl)
 
 
 def train_synthetic_tokenizer(texts: Iterable[str], vocab_size: int = 16384) -> SFTTokenizer:

@@ -188,6 +188,9 @@ PRESETS = {
     "meta-llama/Meta-Llama-3-8B": llama3_8b,
     "tiny": tiny,
     "tiny-llama": lambda: tiny("llama"),
+    # tiny depth/width with the real head_dim (128) the HIP attention kernels are built for (GPU tests)
+    "tiny-gpu": lambda: tiny(hidden_size=256, num_attention_heads=2, num_key_value_heads=1, head_dim=128,
+                             intermediate_size=512, vocab_size=1024, num_hidden_layers=3),
 }
 
 

@@ -164,8 +164,12 @@ class AimCallback(TrainerCallback):
         for k, v in logs.items():
             if not isinstance(v, (int, float)):
                 continue
-            subset = "eval" if k.startswith("eval_") else "train"
-            name = k[5:] if k.startswith("eval_") else k
+            if k.startswith("sys_"):  # GPU telemetry (Aim's system metrics; amdsmi instead of NVML)
+                subset, name = "system", k[4:]
+            elif k.startswith("eval_"):
+                subset, name = "eval", k[5:]
+            else:
+                subset, name = "train", k
             if self._run is not None:
                 self._run.track(v, name=name, step=state.global_step, epoch=state.epoch, context={"subset": subset})
             elif self._fallback:

@@ -16,7 +16,7 @@ import json
 import os
 import warnings
 from dataclasses import dataclass, field
-from typing import Any, Dict, List, Optional
+from typing import Any, Dict, List, Optional, Union
 
 
 @dataclass
@@ -106,6 +106,14 @@ class SFTConfig:
     prefetch_batches: int = 2
     optimizer_overlap: bool = True          # pipeline AdamW under the next forward (side HIP stream)
     gemm_tuning: bool = True                # load shipped hipBLASLt/rocBLAS selections (utils/gemm_tuning.py)
+    # tokenisation cache (TRL main_process_first): rank 0 tokenises, the others load; True = output_dir/.sftamd_cache,
+    # a str = that directory, False = every rank tokenises
+    dataset_cache: Union[bool, str] = True
+    # observability: per-step phase breakdown (data / fwd / bwd / comm_wait / optim, with
+    # roctx ranges, logged as *_ms keys; adds a device sync per phase, so off by default) and GPU telemetry
+    # (utilisation / power / temperature / HBM via amdsmi or rocm-smi) every N log steps into the trackers
+    log_step_phases: bool = False
+    log_system_metrics_every: int = 0
 
     def __post_init__(self):
         pass

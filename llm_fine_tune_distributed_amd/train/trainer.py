@@ -32,7 +32,7 @@ import numpy as np
 import torch
 
 from ..data.collator import DataLoader, DistributedBatchSampler, SFTCollator
-from ..data.dataset import TokenizedDataset, tokenize_rows
+from ..data.dataset import TokenizedDataset, cached_tokenize
 from ..models import CausalLM, apply_freeze_policy, build_model, get_config
 from ..models.lora import LoRAConfig
 from ..parallel.ddp import DDPEngine
@@ -109,8 +109,7 @@ class SFTTrainer:
         # ------------------------------------------------------------ data
         self.tokenizer = processing_class or tokenizer
         if self.tokenizer is None and (self._needs_tokenizer(train_dataset) or self._needs_tokenizer(eval_dataset)):
-            from ..data.tokenizer import load_tokenizer
-            self.tokenizer = load_tokenizer()
+            self.tokenizer = self._main_first_tokenizer()
         self.train_dataset = self._prepare(train_dataset, args.max_train_samples)
         self.eval_dataset = self._prepare(eval_dataset, args.max_eval_samples)
         pad_id = self.tokenizer.pad_token_id if self.tokenizer is not None else (model.config.pad_token_id or 0)
@@ -142,11 +141,38 @@ class SFTTrainer:
         cbs.append(PrinterCallback())
         self.callback_handler = CallbackHandler(cbs)
         self._timers: Dict[str, float] = {"eval": 0.0}
+        from ..utils.profiling import StepTimer
+        self.phase_timer = StepTimer(enabled=dev.type == "cuda") if args.log_step_phases else None
+        self._log_count = 0
 
     # ------------------------------------------------------------------ data helpers
     @staticmethod
     def _needs_tokenizer(ds) -> bool:
         return ds is not None and not isinstance(ds, TokenizedDataset)
+
+    def _cache_dir(self) -> Optional[str]:
+        a = self.args
+        if not a.dataset_cache:
+            return None
+        return a.dataset_cache if isinstance(a.dataset_cache, str) else os.path.join(a.output_dir, ".sftamd_cache")
+
+    def _main_first_tokenizer(self):
+        """Offline synthetic tokenizer, trained ONCE: rank 0 trains and saves it, the others load it."""
+        from ..data.tokenizer import load_tokenizer
+        cache = self._cache_dir()
+        if cache is None or self.dist.world_size == 1:
+            return load_tokenizer()
+        tdir = os.path.join(cache, "tokenizer")
+        if self.dist.is_main:
+            tk = load_tokenizer()
+            tmp = f"{tdir}.tmp{os.getpid()}"
+            tk.save_pretrained(tmp)
+            if os.path.isdir(tdir):
+                import shutil
+                shutil.rmtree(tdir, ignore_errors=True)
+            os.replace(tmp, tdir)
+        barrier()
+        return tk if self.dist.is_main else load_tokenizer(tdir)
 
     def _prepare(self, ds, limit):
         if ds is None:
@@ -156,8 +182,10 @@ class SFTTrainer:
         rows = list(ds) if not isinstance(ds, list) else ds
         if limit:
             rows = rows[:limit]
-        return tokenize_rows(rows, self.tokenizer, self.args.max_length, self.args.assistant_only_loss,
-                             self.args.dataset_text_field)
+        return cached_tokenize(rows, self.tokenizer, self._cache_dir(), is_main=self.dist.is_main,
+                               barrier=barrier if self.dist.world_size > 1 else None, max_length=self.args.max_length,
+                               assistant_only_loss=self.args.assistant_only_loss,
+                               text_field=self.args.dataset_text_field)
 
     def get_train_dataloader(self) -> DataLoader:
         a = self.args
@@ -212,6 +240,11 @@ class SFTTrainer:
         # SUM-reduced here, so each rank's local count is scaled by the world size
         return n.clamp(min=1.0) * self.dist.world_size
 
+    def _phase(self, name: str, host: bool = False):
+        """Step-phase timing + roctx range (``log_step_phases``); a no-op otherwise."""
+        t = self.phase_timer
+        return t.phase(name, host=host) if t is not None else contextlib.nullcontext()
+
     def optimizer_step(self, micro: List[Dict], lr: float) -> Dict[str, torch.Tensor]:
         """One optimizer step over ``micro`` (GA micro-batches). Returns device-side sums:
         loss (this rank's share of the global mean), correct, entropy_sum, valid tokens."""
@@ -225,12 +258,16 @@ class SFTTrainer:
             ctx = contextlib.nullcontext() if sync else eng.no_sync()
             with ctx:
                 eng.prepare_backward()
-                out = model(**self._model_inputs(b), num_items_in_batch=n_items)
-                out.loss.backward()
+                with self._phase("fwd"):
+                    out = model(**self._model_inputs(b), num_items_in_batch=n_items)
+                with self._phase("bwd"):
+                    out.loss.backward()
             acc[0] += out.loss.detach()
             acc[1:] += out.metrics
-        eng.finish_backward()
-        norm = self.optimizer.step(lr=lr, max_grad_norm=self.args.max_grad_norm)
+        with self._phase("comm_wait"):
+            eng.finish_backward()
+        with self._phase("optim"):
+            norm = self.optimizer.step(lr=lr, max_grad_norm=self.args.max_grad_norm)
         eng.zero_grad()
         return {"acc": acc, "grad_norm": norm}
 
@@ -376,11 +413,12 @@ class SFTTrainer:
             step_in_epoch = (skip_batches // ga) if epoch == start_epoch else 0
             while True:
                 micro = []
-                for _ in range(ga):
-                    try:
-                        micro.append(next(it))
-                    except StopIteration:
-                        break
+                with self._phase("data", host=True):
+                    for _ in range(ga):
+                        try:
+                            micro.append(next(it))
+                        except StopIteration:
+                            break
                 if not micro:
                     break
                 self.control = self.callback_handler.call("on_step_begin", a, self.state, self.control)
@@ -420,6 +458,14 @@ class SFTTrainer:
                         logs["hbm_peak_gb"] = round(torch.cuda.max_memory_allocated(self.dist.device) / 1e9, 3)
                         if self.dist.world_size > 1:
                             logs["comm_exposed_ms"] = round(self.engine.comm_exposed_ms(), 3)
+                    if self.phase_timer is not None:  # mean per optimizer step since the last log
+                        for k, v in self.phase_timer.summary().items():
+                            logs[f"{k}_ms"] = round(v / steps_since_log, 3)
+                    self._log_count += 1
+                    if a.log_system_metrics_every and self._log_count % a.log_system_metrics_every == 0 \
+                            and self.dist.is_main:
+                        from ..utils.telemetry import system_log_entries
+                        logs.update(system_log_entries())
                     self.log(logs)
                     run_acc.zero_()
                     steps_since_log = 0

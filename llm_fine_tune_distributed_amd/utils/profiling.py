@@ -39,10 +39,13 @@ class StepTimer:
         self._cpu = defaultdict(float)
 
     @contextlib.contextmanager
-    def phase(self, name: str):
-        if not self.enabled:
+    def phase(self, name: str, host: bool = False):
+        """Time ``name``: device time between two events on the current stream (no sync), or host wall time
+        when the timer is disabled / ``host=True`` (e.g. data loading, which runs on the CPU)."""
+        if not self.enabled or host:
             t = time.perf_counter()
-            yield
+            with range(name):
+                yield
             self._cpu[name] += time.perf_counter() - t
             return
         s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)

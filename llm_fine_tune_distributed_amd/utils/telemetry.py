@@ -29,6 +29,11 @@ def gpu_stats() -> List[Dict[str, float]]:
                 except Exception:
                     pass
                 try:
+                    rec["temp_c"] = float(amdsmi.amdsmi_get_temp_metric(
+                        h, amdsmi.AmdSmiTemperatureType.HOTSPOT, amdsmi.AmdSmiTemperatureMetric.CURRENT))
+                except Exception:
+                    pass
+                try:
                     pw = amdsmi.amdsmi_get_power_info(h)
                     rec["power_w"] = float(pw.get("current_socket_power", pw.get("average_socket_power", 0)) or 0)
                 except Exception:
@@ -52,3 +57,15 @@ def memory_report(device=None) -> Dict[str, float]:
     return {"hbm_allocated_gb": torch.cuda.memory_allocated(device) / 1e9,
             "hbm_reserved_gb": torch.cuda.memory_reserved(device) / 1e9,
             "hbm_peak_gb": torch.cuda.max_memory_allocated(device) / 1e9}
+
+
+def system_log_entries(stats: List[Dict[str, float]] = None) -> Dict[str, float]:
+    """Flatten ``gpu_stats()`` into tracker keys ``sys_gpu{i}_{metric}`` (logged with context subset=system)."""
+    stats = gpu_stats() if stats is None else stats
+    out = {}
+    for rec in stats:
+        i = int(rec.get("index", 0))
+        for k, v in rec.items():
+            if k != "index" and isinstance(v, (int, float)):
+                out[f"sys_gpu{i}_{k}"] = float(v)
+    return out

@@ -95,3 +95,63 @@ def test_assistant_only_loss_masks_prompt():
     b = C.SFTCollator(tk.pad_token_id)(ds, torch.tensor([0]))
     st = int(ds.loss_start[0])
     assert (b["labels"][0, :st] == -100).all() and (b["labels"][0, st:int(ds.lengths()[0])] != -100).all()
+
+
+def _main_first_worker(rank, world, port, out_dir, forbid):
+    import os
+    import torch
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), WORLD_SIZE=str(world), RANK=str(rank),
+                      LOCAL_RANK=str(rank))
+    import llm_fine_tune_distributed_amd.parallel.process_group as pgm
+    pgm._STATE = None
+    from llm_fine_tune_distributed_amd.data import dataset as dsm
+    from llm_fine_tune_distributed_amd.data.synthetic import generate_qa
+    from llm_fine_tune_distributed_amd.models import build_model, tiny
+    from llm_fine_tune_distributed_amd.train import SFTConfig, SFTTrainer
+    calls = []
+    orig = dsm.tokenize_rows
+
+    def spy(*a, **k):
+        calls.append(rank)
+        if forbid:
+            raise AssertionError("tokenised although the cache holds this dataset")
+        return orig(*a, **k)
+
+    dsm.tokenize_rows = spy
+    rows = [{"full-question": r["full-question"], "answer": r["answer"]} for r in generate_qa(24, seed=5)]
+    args = SFTConfig(output_dir=out_dir, jsonl_log=False, max_steps=1, save_strategy="no",
+                     dataset_cache=os.path.join(out_dir, "cache"))
+    t = SFTTrainer(model=build_model(tiny(vocab_size=16384), dtype=torch.float32, seed=0), args=args,
+                   train_dataset=rows)
+    torch.save({"tokens": t.train_dataset.tokens, "offsets": t.train_dataset.offsets, "calls": calls,
+                "vocab": t.tokenizer.vocab_size}, os.path.join(out_dir, f"tok{int(forbid)}_{rank}.pt"))
+    pgm.cleanup_distributed()
+
+
+def test_tokenisation_on_main_process_first_with_cache():
+    """TRL main_process_first: rank 0 trains the tokenizer and tokenises, the other rank loads
+    both behind a barrier; a second run with the same inputs loads the cached CSR arrays."""
+    import os
+    import socket
+    import tempfile
+
+    import torch
+    import torch.multiprocessing as mp
+
+    def port():
+        s = socket.socket()
+        s.bind(("127.0.0.1", 0))
+        p = s.getsockname()[1]
+        s.close()
+        return p
+
+    d = tempfile.mkdtemp()
+    mp.spawn(_main_first_worker, args=(2, port(), d, False), nprocs=2, join=True)
+    r0, r1 = (torch.load(os.path.join(d, f"tok0_{r}.pt")) for r in range(2))
+    assert r0["calls"] == [0] and r1["calls"] == []  # only rank 0 tokenised
+    assert torch.equal(r0["tokens"], r1["tokens"]) and torch.equal(r0["offsets"], r1["offsets"])
+    assert r0["vocab"] == r1["vocab"]
+    assert any(f.startswith("tokenized-") for f in os.listdir(os.path.join(d, "cache")))
+    mp.spawn(_main_first_worker, args=(2, port(), d, True), nprocs=2, join=True)  # cache hit on every rank
+    c0 = torch.load(os.path.join(d, "tok1_0.pt"))
+    assert torch.equal(c0["tokens"], r0["tokens"])
