@@ -210,6 +210,12 @@ class DDPEngine:
     def named_params(self):
         return [(self.param_names[id(p)], p) for p, _, _, _ in self.layout]
 
+    @torch.no_grad()
+    def params_by_name(self) -> torch.Tensor:
+        """All trainable parameters concatenated in name order: a world-size-independent view of
+        ``param_flat`` (whose bucket padding depends on the world size) for cross-run comparisons."""
+        return torch.cat([p.detach().reshape(-1) for _, p in sorted(self.named_params(), key=lambda t: t[0])])
+
     # ------------------------------------------------------------------ GA / sync control
     @contextlib.contextmanager
     def no_sync(self):

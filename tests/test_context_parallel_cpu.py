@@ -134,7 +134,7 @@ def _trainer_worker(rank, world, port, out_dir, cp):
                      save_strategy="no", context_parallel_size=cp, ddp_bucket_cap_mb=0.05, ddp_first_bucket_mb=0.01)
     t = SFTTrainer(model=m, args=args, train_dataset=ds)
     t.train()
-    torch.save({"params": t.engine.param_flat.clone(), "log": [h for h in t.state.log_history if "loss" in h]},
+    torch.save({"params": t.engine.params_by_name().clone(), "log": [h for h in t.state.log_history if "loss" in h]},
                os.path.join(out_dir, f"t{world}_{cp}_{rank}.pt"))
     pgm.cleanup_distributed()
 

@@ -39,7 +39,7 @@ def _run(rank, world, port, out, per_dev, shard=False):
     t = SFTTrainer(model=m, args=a, train_dataset=ds)
     t.train()
     t.optimizer.synchronize()
-    torch.save({"p": t.engine.param_flat.float().cpu(), "log": [h["loss"] for h in t.state.log_history if "loss" in h]},
+    torch.save({"p": t.engine.params_by_name().float().cpu(), "log": [h["loss"] for h in t.state.log_history if "loss" in h]},
                os.path.join(out, f"w{world}_r{rank}{'_z' if shard else ''}.pt"))
     pgm.cleanup_distributed()
 

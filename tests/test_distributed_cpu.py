@@ -41,7 +41,7 @@ def _run(rank, world, port, out_dir, per_dev, ga, steps, shard=False, tag="", av
     t = SFTTrainer(model=m, args=args, train_dataset=ds)
     out = t.train()
     osd = t.optimizer.state_dict()  # collective in ZeRO-1 mode: every rank takes part
-    torch.save({"params": t.engine.param_flat.clone(), "loss": out.training_loss,
+    torch.save({"params": t.engine.params_by_name().clone(), "loss": out.training_loss,
                 "log": [h for h in t.state.log_history if "loss" in h], "exp_avg": _flat_state(osd, "exp_avg"),
                 "exp_avg_sq": _flat_state(osd, "exp_avg_sq"), "sharded": type(t.optimizer).__name__},
                os.path.join(out_dir, f"r{world}_{rank}{tag}.pt"))
