@@ -6,7 +6,8 @@ MI355X; DDP scaling efficiency", reference 4-GPU config = per-device batch 8 x G
 (README.md:69). Every timed step is a complete optimizer step of the real training path
 (``SFTTrainer.optimizer_step``): GA micro-batches of fwd+bwd through the HIP kernels, RCCL
 bucket reduce-scatter (ZeRO-1, default for N > 1) or all-reduce overlapped with backward, grad-norm
-clip, fused AdamW (bf16 params + stochastic rounding, fp32 moments) and, with ZeRO-1, the parameter
+clip, fused AdamW (bf16 params and bf16 moments like the reference's torch AdamW over its bf16 model, both
+stochastically rounded) and, with ZeRO-1, the parameter
 all-gather (finished inside the timed region).
 Data: synthetic token sequences of ``--seq`` tokens (the reference's samples are ~420-525
 tokens), random-init weights of the SmolLM3-3B architecture (no network).
@@ -58,14 +59,19 @@ def parse(argv=None):
     ap.add_argument("--micro-batch", type=int, default=16)
     ap.add_argument("--ga", type=int, default=1)
     ap.add_argument("--no-overlap", action="store_true", help="disable AdamW/forward overlap")
+    ap.add_argument("--ga-merge-max-tokens", type=int, default=None,
+                    help="run the GA micro-batches of a step as one pass up to this many tokens (SFTConfig default "
+                         "32768); 0 = one fwd/bwd pass per micro-batch")
     ap.add_argument("--seq", type=int, default=512)
     ap.add_argument("--bucket-mb", type=float, default=float(os.environ.get("SFTAMD_BUCKET_MB", "0")),
                     help="gradient bucket cap in MB; 0 (default) = the xGMI plan of parallel.ddp.plan_bucket_mb")
     ap.add_argument("--packing", action="store_true")
     ap.add_argument("--freeze-policy", default="full", choices=["full", "last_n_layers", "lora"])
     ap.add_argument("--master-weights", action="store_true", help="fp32 master copy (default: bf16 params + SR)")
-    ap.add_argument("--optim-state", default=os.environ.get("SFTAMD_OPTIM_STATE", "fp32"), choices=["fp32", "bf16"],
-                    help="Adam moment dtype (bf16 = torch AdamW's state dtype for the reference's bf16 params)")
+    ap.add_argument("--optim-state", default=os.environ.get("SFTAMD_OPTIM_STATE", "bf16"), choices=["fp32", "bf16"],
+                    help="Adam moment dtype. bf16 (default) = the reference's: torch AdamW keeps exp_avg / exp_avg_sq "
+                         "in the parameter dtype, bf16 for its bf16 model (training.py:99); here stored with "
+                         "stochastic rounding (unbiased), so not less precise than the reference")
     ap.add_argument("--zero", type=int, default=int(os.environ.get("SFTAMD_ZERO", "1")), choices=[0, 1],
                     help="1 (default): ZeRO-1 over the DDP buckets when N > 1 (reduce-scatter grads, 1/N of AdamW "
                          "per rank, all-gather params under the next forward); 0: replicated all-reduce DDP")
@@ -132,7 +138,8 @@ def run(a):
                      ddp_bucket_cap_mb=a.bucket_mb or None, dataloader_drop_last=True, jsonl_log=False,
                      logging_steps=0, optimizer_overlap=not a.no_overlap, freeze_policy=a.freeze_policy,
                      master_weights=a.master_weights, optim_state_dtype=a.optim_state,
-                     shard_optimizer_state=bool(a.zero), gemm_tuning=False)
+                     shard_optimizer_state=bool(a.zero), gemm_tuning=False,
+                     **({} if a.ga_merge_max_tokens is None else {"ga_merge_max_tokens": a.ga_merge_max_tokens}))
     trainer = SFTTrainer(model=model, args=args, train_dataset=ds)
     loader = trainer.get_train_dataloader()
     it = iter(loader)
@@ -195,6 +202,8 @@ def run(a):
                                      f"AdamW bf16 params + stochastic rounding, {a.optim_state} moments")
                        + (" (fused HIP)" if on_gpu else " (torch fallback)"),
                        "samples_per_device_per_step": a.micro_batch * a.ga,
+                       "ga_passes_per_step": 1 if (a.ga > 1 and a.micro_batch * a.ga * a.seq <= args.ga_merge_max_tokens)
+                       else a.ga,
                        "optimizer_sharding": "zero1" if shard else "none",
                        "gradient_checkpointing": False, "packing": a.packing},
             "tokens_per_sec": round(tok_s, 1), "mfu": None if mfu is None else round(mfu, 4),

@@ -49,7 +49,9 @@ def _wgrad_cfg(T: int, N: int, K: int) -> int:
     hand-written gfx950 kernel (csrc/gemm_wgrad.hip). Chosen from tools/bench_wgrad.py on MI355X
     (profiles/r1_wgrad_microbench.md): the 256x256 ring kernel wherever it fills >= 2 waves of the
     256 CUs (gate_up 0.58 vs 0.74 ms, lm_head 3.2 vs 3.9 ms at T=8192), the 256x128 ring kernel on
-    mid-size grids (qkv 0.113 vs 0.139 ms, down 0.337 vs 0.349 ms); BLAS for small grids (o_proj)."""
+    mid-size grids (qkv 0.113 vs 0.139 ms, down 0.337 vs 0.349 ms); on small grids (o_proj 2048 x 2048 = 128
+    tiles of 256 x 128) the same kernel split 2 ways over the tokens (cfg 209, fp32 slabs + ordered reduce):
+    0.071 vs 0.090 ms for hipBLASLt (profiles/r2_wgrad_splitk.md)."""
     if _WGRAD_MODE == "blas" or T % 32 or T < 1024:
         return 0
     if _WGRAD_MODE not in ("auto", ""):
@@ -58,6 +60,8 @@ def _wgrad_cfg(T: int, N: int, K: int) -> int:
         return 10
     if N % 256 == 0 and K % 128 == 0 and (N // 256) * (K // 128) >= 160:
         return 9
+    if N % 256 == 0 and K % 128 == 0 and (T // 32) % 2 == 0 and (N // 256) * (K // 128) >= 32:
+        return 209
     return 0
 
 

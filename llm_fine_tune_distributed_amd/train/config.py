@@ -106,6 +106,12 @@ class SFTConfig:
     prefetch_batches: int = 2
     optimizer_overlap: bool = True          # pipeline AdamW under the next forward (side HIP stream)
     gemm_tuning: bool = True                # load shipped hipBLASLt/rocBLAS selections (utils/gemm_tuning.py)
+    # GA micro-batch merging (MI355X-first): gradient accumulation exists to fit a per-device batch into
+    # memory; when the step's GA micro-batches together hold at most this many tokens (288 GB of HBM holds
+    # far more than the reference's 48 GB L40S), they run as ONE fwd/bwd pass. Same gradient, loss
+    # normalisation (global token count) and metrics; only the fp32-vs-bf16 summation order of the weight
+    # gradient changes (one fp32-accumulated GEMM instead of bf16 += per micro-batch). 0 = always run GA passes.
+    ga_merge_max_tokens: int = 32768
     # tokenisation cache (TRL main_process_first): rank 0 tokenises, the others load; True = output_dir/.sftamd_cache,
     # a str = that directory, False = every rank tokenises
     dataset_cache: Union[bool, str] = True

@@ -245,12 +245,46 @@ class SFTTrainer:
         t = self.phase_timer
         return t.phase(name, host=host) if t is not None else contextlib.nullcontext()
 
+    def _merge_micro(self, micro: List[Dict]) -> List[Dict]:
+        """Run the step's GA micro-batches as one pass when they fit ``ga_merge_max_tokens`` (see SFTConfig):
+        padded batches are re-padded to the longest and stacked, packed (varlen) batches are concatenated with
+        shifted ``cu_seqlens``. The per-batch scalars (token / sample / label counts) are summed."""
+        cap = int(getattr(self.args, "ga_merge_max_tokens", 0) or 0)
+        if len(micro) < 2 or cap <= 0 or self.cp_size > 1:
+            return micro
+        packed = "cu_seqlens" in micro[0]
+        if any(("cu_seqlens" in b) != packed for b in micro):
+            return micro
+        total = sum(b["input_ids"].numel() for b in micro) if packed else \
+            sum(b["input_ids"].shape[0] for b in micro) * max(b["input_ids"].shape[1] for b in micro)
+        if total > cap:
+            return micro
+        out = {k: sum(b[k] for b in micro) for k in ("num_items", "num_samples", "num_tokens")}
+        if all(torch.is_tensor(b.get("num_items_t")) for b in micro):
+            out["num_items_t"] = torch.stack([b["num_items_t"] for b in micro]).sum(0)
+        if packed:
+            cus, off = [micro[0]["cu_seqlens"]], micro[0]["cu_seqlens"][-1:]
+            for b in micro[1:]:
+                cus.append(b["cu_seqlens"][1:] + off)
+                off = off + b["cu_seqlens"][-1:]
+            out.update(input_ids=torch.cat([b["input_ids"] for b in micro]),
+                       labels=torch.cat([b["labels"] for b in micro]), cu_seqlens=torch.cat(cus),
+                       position_ids=torch.cat([b["position_ids"] for b in micro]),
+                       max_seqlen=max(b["max_seqlen"] for b in micro), shifted=micro[0].get("shifted", False))
+        else:
+            T = max(b["input_ids"].shape[1] for b in micro)
+            F = torch.nn.functional
+            out.update(input_ids=torch.cat([F.pad(b["input_ids"], (0, T - b["input_ids"].shape[1]), value=self._pad_id)
+                                            for b in micro]),
+                       labels=torch.cat([F.pad(b["labels"], (0, T - b["labels"].shape[1]), value=-100) for b in micro]))
+        return [out]
+
     def optimizer_step(self, micro: List[Dict], lr: float) -> Dict[str, torch.Tensor]:
         """One optimizer step over ``micro`` (GA micro-batches). Returns device-side sums:
         loss (this rank's share of the global mean), correct, entropy_sum, valid tokens."""
         model, eng = self.model, self.engine
         model.train()
-        micro = [self._cp_shard(b) for b in micro]
+        micro = self._merge_micro([self._cp_shard(b) for b in micro])
         n_items = self.global_num_items(micro)
         acc = torch.zeros(4, device=self.dist.device)  # loss, correct, entropy_sum, valid
         for i, b in enumerate(micro):

@@ -22,7 +22,8 @@ def _flat_state(osd, k):
     return torch.cat([v[k].reshape(-1).float() for _, v in sorted(osd["param_state"].items())])
 
 
-def _run(rank, world, port, out_dir, per_dev, ga, steps, shard=False, tag="", avg_tokens=True, fixed_len=False):
+def _run(rank, world, port, out_dir, per_dev, ga, steps, shard=False, tag="", avg_tokens=True, fixed_len=False,
+         merge=0):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), WORLD_SIZE=str(world), RANK=str(rank),
                       LOCAL_RANK=str(rank))
     import llm_fine_tune_distributed_amd.parallel.process_group as pgm
@@ -37,7 +38,8 @@ def _run(rank, world, port, out_dir, per_dev, ga, steps, shard=False, tag="", av
     args = SFTConfig(output_dir=out_dir, per_device_train_batch_size=per_dev, gradient_accumulation_steps=ga,
                      learning_rate=1e-3, max_steps=steps, logging_steps=1, dataloader_drop_last=True,
                      jsonl_log=False, ddp_check_sync_every=1, ddp_bucket_cap_mb=0.05, ddp_first_bucket_mb=0.01,
-                     save_strategy="no", shard_optimizer_state=shard, average_tokens_across_devices=avg_tokens)
+                     save_strategy="no", shard_optimizer_state=shard, average_tokens_across_devices=avg_tokens,
+                     ga_merge_max_tokens=merge)
     t = SFTTrainer(model=m, args=args, train_dataset=ds)
     out = t.train()
     osd = t.optimizer.state_dict()  # collective in ZeRO-1 mode: every rank takes part
@@ -48,13 +50,13 @@ def _run(rank, world, port, out_dir, per_dev, ga, steps, shard=False, tag="", av
     pgm.cleanup_distributed()
 
 
-def _launch(world, per_dev, ga, steps, d, shard=False, tag="", avg_tokens=True, fixed_len=False):
+def _launch(world, per_dev, ga, steps, d, shard=False, tag="", avg_tokens=True, fixed_len=False, merge=0):
     port = _free_port()
     if world == 1:
-        _run(0, 1, port, d, per_dev, ga, steps, shard, tag, avg_tokens, fixed_len)
+        _run(0, 1, port, d, per_dev, ga, steps, shard, tag, avg_tokens, fixed_len, merge)
     else:
-        mp.spawn(_run, args=(world, port, d, per_dev, ga, steps, shard, tag, avg_tokens, fixed_len), nprocs=world,
-                 join=True)
+        mp.spawn(_run, args=(world, port, d, per_dev, ga, steps, shard, tag, avg_tokens, fixed_len, merge),
+                 nprocs=world, join=True)
 
 
 def test_ddp2_matches_single_process():
@@ -77,11 +79,18 @@ def test_grad_accumulation_equals_big_batch():
     _launch(1, 4, 1, 2, d)
     big = torch.load(os.path.join(d, "r1_0.pt"))
     d2 = tempfile.mkdtemp()
-    _launch(1, 2, 2, 2, d2)
+    _launch(1, 2, 2, 2, d2)  # GA run as two passes (ga_merge_max_tokens=0)
     ga = torch.load(os.path.join(d2, "r1_0.pt"))
     assert torch.allclose(ga["params"], big["params"], atol=1e-5, rtol=1e-4)
     for a, b in zip(big["log"], ga["log"]):
         assert abs(a["loss"] - b["loss"]) < 1e-5
+    d3 = tempfile.mkdtemp()
+    _launch(1, 2, 2, 2, d3, merge=4096)  # GA micro-batches merged into one pass (the MI355X default)
+    mg = torch.load(os.path.join(d3, "r1_0.pt"))
+    assert torch.allclose(mg["params"], big["params"], atol=1e-5, rtol=1e-4)
+    for a, b in zip(big["log"], mg["log"]):
+        assert abs(a["loss"] - b["loss"]) < 1e-5
+        assert abs(a["grad_norm"] - b["grad_norm"]) < 1e-4 * max(1.0, a["grad_norm"])
 
 
 def test_zero1_sharded_optimizer_matches_replicated():

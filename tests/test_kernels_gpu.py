@@ -327,7 +327,10 @@ def test_decode_attention(L):
 
 @pytest.mark.parametrize("cfg,T,N,K", [(1, 256, 512, 512), (2, 192, 512, 256), (0, 128, 256, 384), (1, 64, 256, 256),
                                        (3, 256, 512, 512), (4, 192, 512, 256), (7, 352, 512, 512), (7, 96, 256, 256),
-                                       (8, 256, 512, 768), (9, 416, 512, 384), (9, 32, 256, 128), (10, 352, 512, 512), (11, 96, 256, 384)])
+                                       (8, 256, 512, 768), (9, 416, 512, 384), (9, 32, 256, 128), (10, 352, 512, 512), (11, 96, 256, 384),
+                                       # split-K ring (cfg = 100 * splits + variant): fp32 slabs + ordered reduce
+                                       (210, 512, 512, 512), (410, 1024, 256, 256), (309, 384, 512, 384),
+                                       (209, 64, 256, 128)])
 @pytest.mark.parametrize("accumulate", [False, True])
 def test_wgrad_gemm(cfg, T, N, K, accumulate):
     torch.manual_seed(0)

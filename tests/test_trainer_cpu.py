@@ -202,3 +202,25 @@ def test_grad_norm_from_backward_partials(tmp_path, tk, monkeypatch, policy, ckp
     for a, b in zip(n1, n0):
         assert abs(a - b) <= 1e-5 * max(1.0, b), (a, b)
     assert torch.allclose(p1, p0, atol=1e-6, rtol=1e-5)
+
+
+@pytest.mark.parametrize("packing", [False, True])
+def test_ga_merge_matches_separate_passes(tmp_path, tk, packing):
+    """ga_merge_max_tokens: the GA micro-batches of a step run as ONE pass (re-padded / varlen-concatenated)
+    with the same loss, grad norm, metrics and update as running them one by one."""
+    rows = generate_qa(16, seed=4)
+    res = {}
+    for merge in (0, 1 << 16):
+        args = SFTConfig(output_dir=str(tmp_path / str(merge)), per_device_train_batch_size=4,
+                         gradient_accumulation_steps=2, learning_rate=1e-3, max_steps=2, logging_steps=1,
+                         save_strategy="no", jsonl_log=False, packing=packing, ga_merge_max_tokens=merge, seed=1)
+        h = TrainingHistoryCallback()
+        t = SFTTrainer(model=_model(seed=7), args=args, train_dataset=rows, processing_class=tk, callbacks=[h])
+        out = t.train()
+        logs = [x for x in h.history if "loss" in x]
+        res[merge] = (logs, t.engine.param_flat.clone(), out.metrics["train_samples_per_second"] > 0)
+    (l0, p0, _), (l1, p1, _) = res[0], res[1 << 16]
+    assert torch.allclose(p0, p1, atol=1e-5, rtol=1e-4)
+    for a, b in zip(l0, l1):
+        for k in ("loss", "grad_norm", "mean_token_accuracy", "entropy", "num_tokens"):
+            assert abs(a[k] - b[k]) <= 1e-5 * max(1.0, abs(a[k])), (k, a[k], b[k])

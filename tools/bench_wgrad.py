@@ -53,11 +53,15 @@ def main():
         rec["blas_ms"] = round(ms, 4)
         rec["blas_tflops"] = round(flop / ms / 1e9, 1)
         for cfg in [int(c) for c in a.cfgs.split(",")]:
-            if cfg in (1, 3) and (N % 256 or K % 256):
+            if cfg % 100 in (1, 3, 7, 8, 10) and (N % 256 or K % 256):
                 continue
             if N % 256 or K % 128:
                 continue
-            ms = timeit(lambda: _ext.ops().wgrad_gemm(out, dy, x, False, cfg))
+            try:
+                ms = timeit(lambda: _ext.ops().wgrad_gemm(out, dy, x, False, cfg))
+            except RuntimeError as e:  # shape not supported by this variant
+                rec[f"cfg{cfg}"] = str(e).split(":")[-1].strip()[:60]
+                continue
             err = ((out.float() - ref).abs().max() / ref.abs().max()).item()
             rec[f"cfg{cfg}_ms"] = round(ms, 4)
             rec[f"cfg{cfg}_tflops"] = round(flop / ms / 1e9, 1)
