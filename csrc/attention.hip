@@ -1175,6 +1175,80 @@ __global__ __launch_bounds__(NW * 64) void fwd4_kernel(const u16* __restrict__ q
   }
 }
 
+// dQ from the materialised dS (v4 backward): bwd_dkdv3_kernel already computes dS = P o (dP - delta) for
+// every (query, key) pair of a head; it stores it transposed, dS^T[b][h][key][query] (bf16, lp x lp per head),
+// so dQ^T = K^T dS^T is ONE MFMA product per 64-key tile here — 16 MFMA per wave per tile instead of the 48 of
+// dq3 (which recomputes S and dP), no exp2 / softmax VALU, no lse / delta reads. The dS^T tile [64 keys][128
+// queries] is staged exactly like a K/V image and read with the same transposed reads (query column block =
+// the wave's 16 rows), so both MFMA operands come from LDS. Rows past the sequence end are zero-filled by the
+// stager; entries never written by dkdv (queries past the last 64-query tile, key tiles above a wave's causal
+// diagonal) are never used: a wave skips tiles above its diagonal and each query column is independent.
+template <int NW>
+__global__ __launch_bounds__(NW * 64) void bwd_dq4_kernel(const u16* __restrict__ qkv, const u16* __restrict__ dst,
+                                                          const int* __restrict__ cu, u16* __restrict__ dqkv, int nq,
+                                                          int nkv, int lp, float scale, int causal) {
+  static_assert(NW == 8, "the dS^T image is 128 queries wide: 8 waves x 16 rows");
+  constexpr int NT = NW * 64, BM = NW * 16, TB = 64 * ROWB;
+  __shared__ __attribute__((aligned(16))) char smem[2 * TB];
+  char* Ks = smem;
+  char* Ss = smem + TB;
+  const int qb = blockIdx.x, h = blockIdx.y, b = blockIdx.z;
+  const int start = cu[b], len = cu[b + 1] - start;
+  const int q0 = qb * BM;
+  if (q0 >= len) return;
+  SFT_DASSERT(q0 + BM <= lp);
+  const int kvh = h / (nq / nkv);
+  const long ld = (long)(nq + 2 * nkv) * D;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, g = lane >> 4;
+  const int wfirst = q0 + wave * 16;
+  const int qrow = wfirst + (lane & 15);
+  const u16* kbase = qkv + (long)start * ld + (nq + kvh) * D;
+  const u16* sbase = dst + (long)(b * nq + h) * lp * lp + q0;
+  const int nkb = (len + 63) / 64;
+  const int nkt = causal ? min((q0 + BM + 63) / 64, nkb) : nkb;
+  Offs off;
+  off.init(lane);
+  {
+    Stage<64, NT> tk, ts;
+    tk.load(kbase, ld, len, tid);
+    ts.load(sbase, lp, len, tid);
+    tk.store(Ks, tid);
+    ts.store(Ss, tid);
+  }
+  f32x4 dq[8];
+#pragma unroll
+  for (int dt = 0; dt < 8; ++dt) dq[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
+  __syncthreads();
+  for (int kt = 0; kt < nkt; ++kt) {
+    const int k0 = kt * 64;
+    const bool pre = kt + 1 < nkt;
+    Stage<64, NT> tk, ts;
+    if (pre) {
+      tk.load(kbase + (long)(k0 + 64) * ld, ld, len - k0 - 64, tid);
+      ts.load(sbase + (long)(k0 + 64) * lp, lp, len - k0 - 64, tid);
+    }
+    if (!causal || k0 <= wfirst + 15) {
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        const bf16x8 db = lds_tr(Ss, off.tr[wave] + ks * 32 * ROWB);
+#pragma unroll
+        for (int dt = 0; dt < 8; ++dt) dq[dt] = mfma(lds_tr(Ks, off.tr[dt] + ks * 32 * ROWB), db, dq[dt]);
+      }
+    }
+    if (pre) {
+      __syncthreads();
+      tk.store(Ks, tid);
+      ts.store(Ss, tid);
+    }
+    __syncthreads();
+  }
+  if (qrow < len) {
+    u16* qp = dqkv + (long)(start + qrow) * ld + h * D + 4 * g;
+#pragma unroll
+    for (int dt = 0; dt < 8; ++dt) store4(qp + 16 * dt, dq[dt], scale);
+  }
+}
+
 template <int NW>
 __global__ __launch_bounds__(NW * 64) void bwd_dq3_kernel(const u16* __restrict__ qkv, const u16* __restrict__ dout,
                                                           const float* __restrict__ lse,
@@ -1284,7 +1358,8 @@ __global__ __launch_bounds__(256, 2) void bwd_dkdv3_kernel(const u16* __restrict
                                                            const float* __restrict__ delta,
                                                            const int* __restrict__ cu, float* __restrict__ part,
                                                            u16* __restrict__ dqkv, int nq, int nkv, int total,
-                                                           float sl2, float scale, int causal) {
+                                                           float sl2, float scale, int causal,
+                                                           u16* __restrict__ dst = nullptr, int lp = 0) {
   constexpr int NT = 256, TB = 64 * ROWB;
   __shared__ __attribute__((aligned(16))) char smem[2 * TB + 2 * 64 * 4];
   char* Qs = smem;
@@ -1383,6 +1458,11 @@ __global__ __launch_bounds__(256, 2) void bwd_dkdv3_kernel(const u16* __restrict
           dp[mt][i] = p * (dp[mt][i] - Dv[i]);
         }
       }
+      if (dst != nullptr && kok) {  // dS^T row of this lane's key: 4 consecutive queries per fragment (bf16)
+        u16* drow = dst + ((long)(b * nq + h) * lp + key) * lp + q0 + 4 * g;
+#pragma unroll
+        for (int mt = 0; mt < 4; ++mt) store4(drow + 16 * mt, dp[mt], 1.f);
+      }
 #pragma unroll
       for (int ks = 0; ks < 2; ++ks) {
         const bf16x8 pb = pack_acc(sc[2 * ks], sc[2 * ks + 1]);
@@ -1446,6 +1526,11 @@ static void check_attn_args(const at::Tensor& qkv, const at::Tensor& cu, int64_t
 static bool attn_concurrent_bwd() {
   const char* e = std::getenv("SFTAMD_ATTN_CONC");
   return e && e[0] == '1';
+}
+
+static long attn_ds_budget() {  // read per call (cheap next to the kernels): tests switch paths in-process
+  const char* e = std::getenv("SFTAMD_ATTN_DS_MB");
+  return (e && e[0] ? atol(e) : 2048L) * 1024L * 1024L;
 }
 
 static int attn_impl() {
@@ -1637,6 +1722,36 @@ at::Tensor flash_bwd(const at::Tensor& dout, const at::Tensor& qkv, const at::Te
     dq_stream = side->stream();
     C10_HIP_CHECK(hipEventRecord(ev_fork, cur_stream()));
     C10_HIP_CHECK(hipStreamWaitEvent(dq_stream, ev_fork, 0));
+  }
+  // v4 backward: dkdv3 stores dS^T, dQ = one product per tile (bwd_dq4_kernel). Needs the lp x lp bf16 dS^T
+  // blocks of every (sequence, head) — 134 MB for 16 x 512 tokens, 16 heads — so it is used when they fit
+  // SFTAMD_ATTN_DS_MB (default 2048); otherwise dq3 recomputes S / dP.
+  const long lp = (max_seqlen + 127) / 128 * 128;
+  const long ds_bytes = (long)nseq * nq * lp * lp * 2;
+  if (attn_impl() >= 3 && !side && ds_bytes <= attn_ds_budget() && hd == 128) {
+    const int rep = nq / nkv;
+    auto dst = at::empty({ds_bytes / 2}, qkv.options());
+    at::Tensor part;
+    if (rep > 1) part = at::empty({(long)rep * total * 2 * nkv * hd}, qkv.options().dtype(at::kFloat));
+    dim3 gk3((max_seqlen + 63) / 64, nq, nseq);
+    attn::bwd_dkdv3_kernel<<<gk3, 256, 0, cur_stream()>>>(
+        (const u16*)qkv.data_ptr(), (const u16*)dout.data_ptr(), lse.data_ptr<float>(), delta.data_ptr<float>(),
+        cu_c.data_ptr<int>(), rep > 1 ? part.data_ptr<float>() : nullptr, (u16*)dqkv.data_ptr(), nq, nkv, total, sl2,
+        (float)scale, causal ? 1 : 0, (u16*)dst.data_ptr(), (int)lp);
+    SFT_LAUNCH_CHECK();
+    if (rep > 1) {
+      const long nvec = (long)total * 2 * nkv * hd / 8;
+      const int grid = (int)std::min<long>((nvec + 255) / 256, 2048);
+      attn::dkdv_reduce_kernel<<<grid, 256, 0, cur_stream()>>>(part.data_ptr<float>(), (u16*)dqkv.data_ptr(), total,
+                                                               nq, nkv, rep, (float)scale);
+      SFT_LAUNCH_CHECK();
+    }
+    dim3 gq4((max_seqlen + 127) / 128, nq, nseq);
+    attn::bwd_dq4_kernel<8><<<gq4, 512, 0, cur_stream()>>>((const u16*)qkv.data_ptr(), (const u16*)dst.data_ptr(),
+                                                           cu_c.data_ptr<int>(), (u16*)dqkv.data_ptr(), nq, nkv,
+                                                           (int)lp, (float)scale, causal ? 1 : 0);
+    SFT_LAUNCH_CHECK();
+    return dqkv;
   }
   auto run3 = [&](auto w) {
     constexpr int NW = decltype(w)::value;

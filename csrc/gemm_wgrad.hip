@@ -435,11 +435,11 @@ __device__ __forceinline__ void ring_loop(char* __restrict__ b0, char* __restric
   __builtin_amdgcn_s_waitcnt(waitcnt_imm(0, 0));  // drain the tail DMAs before LDS is reused
 }
 
-// Split-K epilogue: the fp32 wave tile goes straight to this split's slab P[s][N][K] (no bf16 rounding, no
-// read of C); splitk_reduce_kernel sums the slabs in a fixed order (deterministic) into the bf16 gradient.
-template <class G>
-__device__ __forceinline__ void epilogue_partial(f32x4 (&acc)[G::FM][G::FN], float* __restrict__ P, int K, int n0,
-                                                 int k0, int wm, int wk, int lane) {
+// Split-K epilogue: the fp32 wave tile goes straight to this piece's tile-local slab P[BM][BN] (no bf16
+// rounding, no read of C); splitk_fixup_kernel sums a tile's slabs in a fixed order (deterministic).
+template <class G, int BN>
+__device__ __forceinline__ void epilogue_partial(f32x4 (&acc)[G::FM][G::FN], float* __restrict__ P, int wm, int wk,
+                                                 int lane) {
   const int g = lane >> 4, ii = lane & 15;
 #pragma unroll
   for (int i = 0; i < G::FM; ++i)
@@ -447,51 +447,68 @@ __device__ __forceinline__ void epilogue_partial(f32x4 (&acc)[G::FM][G::FN], flo
     for (int j = 0; j < G::FN; ++j)
 #pragma unroll
       for (int e = 0; e < 4; ++e)
-        P[(long)(n0 + wm * G::TM + 16 * i + 4 * g + e) * K + k0 + wk * G::TN + 16 * j + ii] = acc[i][j][e];
+        P[(wm * G::TM + 16 * i + 4 * g + e) * BN + wk * G::TN + 16 * j + ii] = acc[i][j][e];
 }
 
-// C[i] = bf16(sum_s P[s][i] (+ C[i] when accumulating)), 8 elements per thread, slabs summed in order s = 0..S-1.
-__global__ void __launch_bounds__(256) splitk_reduce_kernel(const float* __restrict__ P, u16* __restrict__ C, long nk,
-                                                            int splits, int accumulate) {
-  const long i = ((long)blockIdx.x * 256 + threadIdx.x) * 8;
-  if (i >= nk) return;
+// Split tiles t = tile0 .. tile0 + ntiles - 1: C[tile] = bf16(sum_s P[t][s] (+ C when accumulating)),
+// 8 elements per thread, slabs summed in order s = 0..S-1.
+template <int BM, int BN>
+__global__ void __launch_bounds__(256) splitk_fixup_kernel(const float* __restrict__ P, u16* __restrict__ C, int tile0,
+                                                           int ntiles, int splits, int nbk, int K, int accumulate) {
+  constexpr int E8 = BM * BN / 8;
+  const long idx = (long)blockIdx.x * 256 + threadIdx.x;
+  if (idx >= (long)ntiles * E8) return;
+  const int t = (int)(idx / E8), e = (int)(idx - (long)t * E8) * 8;
+  const int row = e / BN, col = e - row * BN;
+  const float* q = P + (long)t * splits * BM * BN + e;
   float v[8];
-  *(float4*)&v[0] = *(const float4*)(P + i);
-  *(float4*)&v[4] = *(const float4*)(P + i + 4);
+  *(float4*)&v[0] = *(const float4*)q;
+  *(float4*)&v[4] = *(const float4*)(q + 4);
   for (int s = 1; s < splits; ++s) {
-    const float* q = P + (long)s * nk + i;
-    const float4 a = *(const float4*)q, b = *(const float4*)(q + 4);
+    const float4 a = *(const float4*)(q + (long)s * BM * BN), b = *(const float4*)(q + (long)s * BM * BN + 4);
     v[0] += a.x; v[1] += a.y; v[2] += a.z; v[3] += a.w;
     v[4] += b.x; v[5] += b.y; v[6] += b.z; v[7] += b.w;
   }
+  const int tile = tile0 + t, bn = tile / nbk, bk = tile - bn * nbk;
+  u16* out = C + (long)(bn * BM + row) * K + bk * BN + col;
   if (accumulate) {
     float o[8];
-    unpack8(*(const uint4*)(C + i), o);
+    unpack8(*(const uint4*)out, o);
 #pragma unroll
-    for (int e = 0; e < 8; ++e) v[e] += o[e];
+    for (int i = 0; i < 8; ++i) v[i] += o[i];
   }
-  *(uint4*)(C + i) = pack8(v);
+  *(uint4*)out = pack8(v);
 }
 
 template <int BM, int BN, int WM, int WN, int NS, bool SCHED>
 __global__ void __launch_bounds__(NT) ring_kernel(const u16* __restrict__ A, const u16* __restrict__ B,
                                                   u16* __restrict__ C, int T, int N, int K, int nbk, int accumulate,
-                                                  float* __restrict__ P, int splits) {
+                                                  float* __restrict__ P, int ndp, int splits) {
   using G = RCfg<BM, BN, WM, WN, NS>;
   __shared__ __attribute__((aligned(16))) char smem[G::LDS];
   const int nwg = gridDim.x, orig = blockIdx.x;
   const int xcd = orig & 7, q8 = nwg >> 3, r8 = nwg & 7;
   const int wgid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (orig >> 3);
-  // split-K (P != nullptr): the splits of one output tile are consecutive workgroups (same XCD / L2)
-  const int sk = wgid % splits, tile = wgid / splits;
+  // Hybrid data-parallel + split-K: workgroups [0, ndp) own whole tiles (direct epilogue); the remaining
+  // tiles (the partial last wave) are each split `splits` ways over the token axis — consecutive workgroups,
+  // uneven step ranges allowed — into fp32 slabs reduced by splitk_fixup_kernel.
+  const int nall = T / BKR;
+  int tile = wgid, sk = 0, s0 = 0, s1 = nall;
+  if (wgid >= ndp) {
+    const int j = wgid - ndp;
+    sk = j % splits;
+    tile = ndp + j / splits;
+    s0 = (int)((long)sk * nall / splits);
+    s1 = (int)((long)(sk + 1) * nall / splits);
+  }
   const int bn = tile / nbk, bk = tile - bn * nbk;
   const int n0 = bn * BM, k0 = bk * BN;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int wm = w / WN, wk = w - wm * WN;
-  const int nsteps = T / BKR / splits;
+  const int nsteps = s1 - s0;
 
   RStager<G> st;
-  st.init(A, B, N, K, n0, k0, w, lane, nsteps, sk * nsteps * BKR);
+  st.init(A, B, N, K, n0, k0, w, lane, nsteps, s0 * BKR);
   const int g = lane >> 4, ii = lane & 15, qq = ii >> 2, pp = ii & 3;
   const int r0 = 4 * (((g & 1) << 1) | (g >> 1)) + qq;  // conflict-free block order (see wgrad_kernel)
   int offA[G::FM], offB[G::FN];
@@ -515,29 +532,34 @@ __global__ void __launch_bounds__(NT) ring_kernel(const u16* __restrict__ A, con
 #pragma unroll
   for (int i = 0; i < 6; ++i) b[i] = smem + (i < NS ? i : 0) * G::STAGE;
   ring_loop<G, SCHED>(b[0], b[1], b[2], b[3], b[4], b[5], nsteps, st, offA, offB, acc);
-  if (P != nullptr) {
-    epilogue_partial<G>(acc, P + (long)sk * N * K, K, n0, k0, wm, wk, lane);
+  if (wgid >= ndp) {
+    epilogue_partial<G, BN>(acc, P + ((long)(tile - ndp) * splits + sk) * BM * BN, wm, wk, lane);
     return;
   }
   __syncthreads();
   epilogue<G>(smem, acc, C, K, n0, k0, wm, wk, w, lane, accumulate);
 }
 
+// splits > 1: tiles beyond the first `full_waves` x 256 (or all of them when full_waves == 0) are split over the
+// token axis; full_waves < 0 = split every tile.
 template <int BM, int BN, int WM, int WN, int NS, bool SCHED = false>
-void launch_ring(const at::Tensor& dy, const at::Tensor& x, at::Tensor& out, bool accumulate, int splits = 1) {
+void launch_ring(const at::Tensor& dy, const at::Tensor& x, at::Tensor& out, bool accumulate, int splits = 1,
+                 bool hybrid = false) {
   const int T = dy.size(0), N = dy.size(1), K = x.size(1);
-  const int nbn = N / BM, nbk = K / BN;
+  const int nbn = N / BM, nbk = K / BN, tiles = nbn * nbk;
+  const int ndp = splits <= 1 ? tiles : (hybrid ? tiles / 256 * 256 : 0);
+  const int nsk = tiles - ndp;
   at::Tensor part;
-  if (splits > 1)  // fp32 slabs, one per split (stream-ordered caching allocation)
-    part = at::empty({(long)splits * N * K}, dy.options().dtype(at::kFloat));
-  ring_kernel<BM, BN, WM, WN, NS, SCHED><<<nbn * nbk * splits, NT, 0, cur_stream()>>>(
+  if (nsk > 0)  // tile-local fp32 slabs, one per split piece (stream-ordered caching allocation)
+    part = at::empty({(long)nsk * splits * BM * BN}, dy.options().dtype(at::kFloat));
+  ring_kernel<BM, BN, WM, WN, NS, SCHED><<<ndp + nsk * splits, NT, 0, cur_stream()>>>(
       (const u16*)dy.data_ptr(), (const u16*)x.data_ptr(), (u16*)out.data_ptr(), T, N, K, nbk, accumulate ? 1 : 0,
-      splits > 1 ? part.data_ptr<float>() : nullptr, splits);
+      nsk > 0 ? part.data_ptr<float>() : nullptr, ndp, splits);
   SFT_LAUNCH_CHECK();
-  if (splits > 1) {
-    const long nk = (long)N * K;
-    splitk_reduce_kernel<<<(unsigned)((nk / 8 + 255) / 256), 256, 0, cur_stream()>>>(
-        part.data_ptr<float>(), (u16*)out.data_ptr(), nk, splits, accumulate ? 1 : 0);
+  if (nsk > 0) {
+    const long n8 = (long)nsk * BM * BN / 8;
+    splitk_fixup_kernel<BM, BN><<<(unsigned)((n8 + 255) / 256), 256, 0, cur_stream()>>>(
+        part.data_ptr<float>(), (u16*)out.data_ptr(), ndp, nsk, splits, nbk, K, accumulate ? 1 : 0);
     SFT_LAUNCH_CHECK();
   }
 }
@@ -568,19 +590,22 @@ void wgrad_gemm(at::Tensor out, at::Tensor dy, at::Tensor x, bool accumulate, in
   SFT_CHECK(T % 32 == 0 && T > 0, "wgrad_gemm: T must be a positive multiple of 32");
   SFT_CHECK(cfg >= 7 || cfg == 0 || T % wgrad::BK == 0, "wgrad_gemm: cfg 1-6 need T % 64 == 0");
   if (cfg == 0) cfg = (N % 256 == 0 && K % 256 == 0 && (N / 256) * (K / 256) >= 512) ? 1 : 2;
-  // cfg = 100 * S + c: ring variant c (9 / 10) split S ways over the token (reduction) axis — fills the chip
-  // for small outputs (o_proj 2048 x 2048 = 64 tiles of 256 x 256); fp32 slabs + deterministic reduce
-  const int splits = cfg >= 100 ? (int)(cfg / 100) : 1;
+  // cfg = 1000 * H + 100 * S + c: ring variant c (9 / 10) with tiles split S ways over the token (reduction)
+  // axis — all tiles (H = 0: fills the chip for small outputs, o_proj 2048 x 2048 = 64 tiles of 256 x 256) or
+  // only those past the last full wave of 256 workgroups (H = 1, hybrid data-parallel + split-K: the partial
+  // last wave of e.g. down_proj's 344 tiles becomes ~1 wave of thinner pieces); fp32 slabs + ordered fixup
+  const bool hybrid = cfg >= 1000;
+  const int splits = (int)((cfg % 1000) / 100);
   cfg %= 100;
-  SFT_CHECK(splits == 1 || ((cfg == 9 || cfg == 10) && (T / 32) % splits == 0 && (N * K) % 8 == 0),
-            "wgrad_gemm split-K: ring cfg 9/10 with T/32 divisible by the split count");
+  SFT_CHECK(splits <= 1 || ((cfg == 9 || cfg == 10) && T / 32 >= splits),
+            "wgrad_gemm split-K: ring cfg 9/10 with at least one 32-token step per split");
   if (splits > 1) {
     if (cfg == 10) {
       SFT_CHECK(N % 256 == 0 && K % 256 == 0, "wgrad_gemm ring 256x256: N, K multiples of 256");
-      wgrad::launch_ring<256, 256, 2, 4, 5, true>(dy, x, out, accumulate, splits);
+      wgrad::launch_ring<256, 256, 2, 4, 5, true>(dy, x, out, accumulate, splits, hybrid);
     } else {
       SFT_CHECK(N % 256 == 0 && K % 128 == 0, "wgrad_gemm ring 256x128: N multiple of 256, K of 128");
-      wgrad::launch_ring<256, 128, 4, 2, 6, true>(dy, x, out, accumulate, splits);
+      wgrad::launch_ring<256, 128, 4, 2, 6, true>(dy, x, out, accumulate, splits, hybrid);
     }
     return;
   }

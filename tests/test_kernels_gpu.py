@@ -156,10 +156,11 @@ def test_cross_entropy(V):
     assert rel_err(lg, gref) < 2e-2
 
 
-def _attn_case(lens, nq, nkv, causal, variant, impl="2", cfg=""):
+def _attn_case(lens, nq, nkv, causal, variant, impl="2", cfg="", ds_mb=""):
     os.environ["SFTAMD_ATTN_TR"] = variant
     os.environ["SFTAMD_ATTN_IMPL"] = impl
     os.environ["SFTAMD_ATTN_CFG"] = cfg
+    os.environ["SFTAMD_ATTN_DS_MB"] = ds_mb  # "" = default budget (materialised dS^T + dq4), "0" = dq3 path
     torch.manual_seed(0)
     D = 128
     cu = torch.tensor([0] + list(torch.tensor(lens).cumsum(0)), dtype=torch.int32, device=DEV)
@@ -183,6 +184,15 @@ def _attn_case(lens, nq, nkv, causal, variant, impl="2", cfg=""):
 @pytest.mark.parametrize("causal", [True, False])
 def test_flash_attention_varlen_gqa(variant, causal, impl):
     _attn_case([100, 255, 64, 1, 300], 8, 2, causal, variant, impl)
+
+
+@pytest.mark.parametrize("causal", [True, False])
+@pytest.mark.parametrize("ds_mb", ["", "0"])
+def test_flash_attention_bwd_materialised_ds_vs_recompute(causal, ds_mb):
+    """v4 backward (dkdv stores dS^T, dq4 = one product per tile) and the dq3 recompute path (budget 0) both
+    match the fp32 reference on ragged GQA batches (lengths off the 64 / 128 tile grid)."""
+    _attn_case([100, 255, 64, 1, 300, 129], 8, 2, causal, "1", "3", "", ds_mb)
+    _attn_case([512, 511, 7], 16, 4, causal, "1", "3", "", ds_mb)
 
 
 def test_flash_attention_mha_and_long():
@@ -219,6 +229,7 @@ def test_flash_attention_concurrent_bwd_bitwise(monkeypatch):
     result is complete when the op returns on the caller's stream (no extra sync)."""
     monkeypatch.setenv("SFTAMD_ATTN_IMPL", "3")
     monkeypatch.setenv("SFTAMD_ATTN_CFG", "")
+    monkeypatch.setenv("SFTAMD_ATTN_DS_MB", "0")  # the dq3 (recompute) path, which has the concurrent option
     torch.manual_seed(3)
     D, nq, nkv = 128, 16, 4
     lens = [512, 300, 17, 512]
@@ -236,7 +247,7 @@ def test_flash_attention_concurrent_bwd_bitwise(monkeypatch):
     assert torch.equal(res["0"], res["1"])
 
 
-@pytest.mark.parametrize("impl", ["2", "1"])
+@pytest.mark.parametrize("impl", ["3", "2", "1"])
 def test_flash_attention_smollm3_shape(impl):
     _attn_case([512] * 4, 16, 4, True, "1", impl)
 
@@ -330,7 +341,9 @@ def test_decode_attention(L):
                                        (8, 256, 512, 768), (9, 416, 512, 384), (9, 32, 256, 128), (10, 352, 512, 512), (11, 96, 256, 384),
                                        # split-K ring (cfg = 100 * splits + variant): fp32 slabs + ordered reduce
                                        (210, 512, 512, 512), (410, 1024, 256, 256), (309, 384, 512, 384),
-                                       (209, 64, 256, 128)])
+                                       (209, 64, 256, 128), (310, 320, 256, 256),
+                                       # hybrid (1000 + ...): 256 whole tiles + the rest split (uneven pieces)
+                                       (1310, 96, 4096, 4352), (1309, 128, 4096, 2304), (1210, 160, 4352, 4096)])
 @pytest.mark.parametrize("accumulate", [False, True])
 def test_wgrad_gemm(cfg, T, N, K, accumulate):
     torch.manual_seed(0)

@@ -35,16 +35,18 @@ def timeit(fn, n=20):
     return statistics.median(ts)
 
 
-CFGS = [("1", ""), ("2", "8,1"), ("3", "8,1"), ("3", "4,1"), ("4", ""), ("3", "8,1,serial")]
+# suffix ",serial": dq3 after dK/dV on one stream; ",ds": v4 backward (materialised dS^T + dq4, the default)
+CFGS = [("1", ""), ("2", "8,1"), ("3", "8,1"), ("3", "4,1"), ("4", ""), ("3", "8,1,serial"), ("3", "8,1,ds")]
 if os.environ.get("ATTN_QUICK"):
-    CFGS = [("3", "8,1"), ("3", "8,1,serial")]
+    CFGS = [("3", "8,1,serial"), ("3", "8,1,ds")]
 res = {}
 ref = None
 for rnd in range(3):
     for impl, cfg in CFGS:
         os.environ["SFTAMD_ATTN_IMPL"] = impl
-        os.environ["SFTAMD_ATTN_CFG"] = cfg.replace(",serial", "")
-        os.environ["SFTAMD_ATTN_CONC"] = "0" if cfg.endswith("serial") else "1"
+        os.environ["SFTAMD_ATTN_CFG"] = cfg.replace(",serial", "").replace(",ds", "")
+        os.environ["SFTAMD_ATTN_CONC"] = "0" if cfg.endswith("serial") or cfg.endswith("ds") else "1"
+        os.environ["SFTAMD_ATTN_DS_MB"] = "" if cfg.endswith("ds") else "0"
         out, lse = ops.flash_fwd(qkv, cu, T, NQ, NKV, D, sc, True)
         dq = ops.flash_bwd(dout, qkv, out, lse, cu, T, NQ, NKV, D, sc, True)
         if ref is None:
