@@ -1,0 +1,343 @@
+// Input-gradient ("dgrad") GEMM for gfx950: dX[M, N] = dY[M, K] . W[K, N], bf16 in, fp32 accumulate — the
+// backward of y = x W^T for a weight stored [K = out features][N = in features] (NN in BLAS terms), with an
+// optional fused SwiGLU-backward epilogue for the MLP down projection:
+//
+//   EPI_PLAIN       dX[m][n] = bf16(acc)
+//   EPI_SWIGLU_BWD  with gu = [gate | up] saved by the forward ([M, 2N]) and dact = acc (fp32, never stored):
+//                   dgu[m][n]     = dact * up * s * (1 + gate * (1 - s)),   s = sigmoid(gate)
+//                   dgu[m][N + n] = dact * gate * s
+//                   — the [M, N] bf16 dact round trip (write + re-read, 360 MB per SmolLM3 layer at 16 x 512
+//                   tokens) and the separate swiglu_bwd launch disappear.
+//
+// Layout: computed transposed, C'[n][m] = sum_k W[k][n] dY[m][k], so the W tile (reduction-major, rows k) is
+// the MFMA A operand read with the gfx950 transposed LDS read ds_read_b64_tr_b16 exactly as the weight-gradient
+// kernel reads its operands (gemm_wgrad.hip: [32 k][128 n] images, 256-B rows, chunk XOR swizzle applied on the
+// global source address because global_load_lds writes lane-linear), and the dY tile (K-contiguous rows m) is
+// the B operand read along its rows like the forward kernel's weight tile (gemm_tn.hip: [m][32 k] images,
+// 64-B rows). The transposed read hands lane group g the reduction indices
+//   phi(g, j) = 4 perm(g) + j (j < 4),  16 + 4 perm(g) + (j - 4) (j >= 4),  perm = {0, 2, 1, 3}
+// of each 32-deep step, so the B fragment is fetched in the same k order with two 8-byte reads per lane
+// (ds_read_b64 at bytes 8 perm(g) and 32 + 8 perm(g) of the row) instead of one 16-byte read.
+//
+// Main loop = the ring of gemm_wgrad.hip: 256 x 256 tile (n x m) per 512-thread workgroup (8 waves 2 x 4),
+// BK = 32 per stage, NS stages of global_load_lds in flight, counted vmcnt + raw s_barrier once per stage,
+// the next stage's fragments read while the current stage's MFMAs run, the DMA pieces spread between MFMA
+// rows. Tile order: XCD-aware bijective remap, then GROUP-blocked along n.
+// Epilogue: per 16-row slice of m, the fp32 wave tile is transposed through wave-private LDS ([m][n] rows of
+// TM + 4 floats) so every output / gate / up access is a 16-byte vector along n.
+#include "common.h"
+
+namespace sftamd {
+namespace dgrad {
+
+constexpr int NT = 512;
+constexpr int BK = 32;
+constexpr int AROWB = 256;          // A image row: 128 n x bf16
+constexpr int AIMG = BK * AROWB;    // [32 k][128 n] = 8 KB
+constexpr int BROWB = 64;           // B image row: 32 k x bf16
+
+enum { EPI_PLAIN = 0, EPI_SWIGLU_BWD = 1 };
+
+__device__ __forceinline__ int swz_a(int row, int ch) { return ch ^ (((row & 3) << 2) | ((row >> 2) & 3)); }
+__device__ __forceinline__ int img_a(int row, int ch) { return row * AROWB + 16 * swz_a(row, ch); }
+__device__ __forceinline__ int swz_b(int row, int ch) { return ch ^ ((0x78 >> (2 * ((row >> 2) & 3))) & 3); }
+
+__device__ __forceinline__ void glds16(const u16* src, char* dst) {
+  __builtin_amdgcn_global_load_lds((const void __attribute__((address_space(1)))*)src,
+                                   (void __attribute__((address_space(3)))*)dst, 16, 0, 0);
+}
+
+typedef __attribute__((address_space(3))) s16x4 lds_s4;
+
+__device__ __forceinline__ bf16x8 lds_tr(const char* base, int off) {
+  s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4*)(base + off));
+  s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4*)(base + off + 16 * AROWB));
+  typedef __attribute__((ext_vector_type(8))) short s16x8;
+  s16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+  return __builtin_bit_cast(bf16x8, v);
+}
+
+__device__ __forceinline__ bf16x8 lds_b2(const char* base, int off1, int off2) {
+  const uint2 a = *(const uint2*)(base + off1), b = *(const uint2*)(base + off2);
+  const uint4 v = make_uint4(a.x, a.y, b.x, b.y);
+  return __builtin_bit_cast(bf16x8, v);
+}
+
+constexpr unsigned waitcnt_imm(int vm, int lgkm) {  // gfx9: vmcnt[3:0] expcnt[6:4] lgkmcnt[11:8] vmcnt[5:4]<<14
+  return (unsigned)((vm & 15) | (7 << 4) | ((lgkm & 15) << 8) | ((vm >> 4) << 14));
+}
+
+template <int BM, int BN, int WM, int WN, int NS_>
+struct Cfg {
+  static constexpr int NS = NS_;
+  static constexpr int TM = BM / WM, TN = BN / WN;  // wave tile: TM n x TN m
+  static constexpr int FM = TM / 16, FN = TN / 16;
+  static constexpr int IA = BM / 128;               // A images per stage
+  static constexpr int STAGE_A = IA * AIMG, STAGE = STAGE_A + BN * BROWB;
+  static constexpr int PB = BN / 128;               // B pieces (16 rows x 64 B) per wave per stage
+  static constexpr int PPW = IA + PB;               // DMA pieces per wave per stage
+  static constexpr int EPI_LD = TM + 4;
+  static constexpr int EPI = 8 * 16 * EPI_LD * 4;
+  static constexpr int LDS = (NS * STAGE > EPI) ? NS * STAGE : EPI;
+  static_assert(WM * WN == 8 && BM % 128 == 0 && BN % 128 == 0 && FM >= PPW, "config");
+  static_assert(LDS <= 160 * 1024, "LDS budget");
+};
+
+template <class G>
+struct Stager {
+  const u16* pa;
+  const u16* pb;
+  long lda, ldb;
+  int w, left;
+  __device__ __forceinline__ void init(const u16* W, const u16* dY, long ldw, long ldd, int n0, int m0, int wave,
+                                       int lane, int nsteps) {
+    w = wave;
+    lda = ldw;
+    ldb = ldd;
+    left = nsteps;
+    const int ra = 4 * wave + (lane >> 4), ca = lane & 15;  // A: rows k 4w..4w+3, 16 lanes per 256-B row
+    pa = W + (long)ra * ldw + n0 + 8 * swz_a(ra, ca);
+    const int rb = lane >> 2;                                // B: 16 rows m per piece, 4 lanes per 64-B row
+    pb = dY + (long)(m0 + 16 * wave + rb) * ldd + 8 * swz_b(rb, lane & 3);
+  }
+  // Past the last step the same rows are fetched again into a slot nobody reads, so every step issues
+  // exactly PPW DMAs and the counted waits stay compile-time constants (see gemm_wgrad.hip).
+  __device__ __forceinline__ void piece(char* buf, int j) {
+    if (j < G::IA) {
+      glds16(pa + j * 128, buf + j * AIMG + w * 1024);
+    } else {
+      const int jj = j - G::IA;  // B piece w + 8 jj: rows 16 (w + 8 jj) ..
+      glds16(pb + (long)(128 * jj) * ldb, buf + G::STAGE_A + (w + 8 * jj) * 1024);
+    }
+  }
+  __device__ __forceinline__ void advance() {
+    if (--left > 0) {
+      pa += BK * lda;
+      pb += BK;
+    }
+  }
+  __device__ __forceinline__ void issue(char* buf) {
+#pragma unroll
+    for (int j = 0; j < G::PPW; ++j) piece(buf, j);
+    advance();
+  }
+};
+
+__device__ __forceinline__ char* pick(int i, char* b0, char* b1, char* b2, char* b3, char* b4) {
+  switch (i) {
+    case 0: return b0;
+    case 1: return b1;
+    case 2: return b2;
+    case 3: return b3;
+    default: return b4;
+  }
+}
+
+template <class G>
+__device__ __forceinline__ void ring_loop(char* __restrict__ b0, char* __restrict__ b1, char* __restrict__ b2,
+                                          char* __restrict__ b3, char* __restrict__ b4, int nsteps, Stager<G>& st,
+                                          const int (&offA)[G::FM], int offB1, int offB2, f32x4 (&acc)[G::FM][G::FN]) {
+  constexpr int NS = G::NS, PPW = G::PPW;
+  constexpr int U = (NS % 2) ? 2 * NS : NS;  // unroll: stage slot and B register set both compile-time
+  bf16x8 fa[G::FM], fb[2][G::FN];
+#pragma unroll
+  for (int i = 0; i < NS; ++i) st.issue(pick(i, b0, b1, b2, b3, b4));
+  __builtin_amdgcn_s_waitcnt(waitcnt_imm((NS - 1) * PPW, 0));
+  __builtin_amdgcn_s_barrier();
+#pragma unroll
+  for (int j = 0; j < G::FN; ++j) fb[0][j] = lds_b2(b0, offB1 + 1024 * j, offB2 + 1024 * j);
+#pragma unroll
+  for (int i = 0; i < G::FM; ++i) fa[i] = lds_tr(b0, offA[i]);
+  for (int t0 = 0; t0 < nsteps; t0 += U) {
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      if (t0 + u < nsteps) {
+        __builtin_amdgcn_s_waitcnt(waitcnt_imm((NS - 2) * PPW, 0));
+        __builtin_amdgcn_s_barrier();
+        char* dst = pick(u % NS, b0, b1, b2, b3, b4);
+        const char* nxt = pick((u + 1) % NS, b0, b1, b2, b3, b4);
+        const int cb = u & 1;
+#pragma unroll
+        for (int j = 0; j < G::FN; ++j) fb[cb ^ 1][j] = lds_b2(nxt, offB1 + 1024 * j, offB2 + 1024 * j);
+        __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+        for (int i = 0; i < G::FM; ++i) {
+#pragma unroll
+          for (int j = 0; j < G::FN; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[cb][j], acc[i][j], 0, 0, 0);
+          fa[i] = lds_tr(nxt, offA[i]);
+          if (i < PPW) st.piece(dst, i);
+          __builtin_amdgcn_sched_group_barrier(0x008, G::FN, 0);  // MFMA
+          __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);      // DS read (one fragment)
+          if (i < PPW) __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);  // VMEM (the DMA)
+        }
+        st.advance();
+        __builtin_amdgcn_s_setprio(0);
+      }
+    }
+  }
+  __builtin_amdgcn_s_waitcnt(waitcnt_imm(0, 0));  // drain the tail DMAs before LDS is reused
+}
+
+struct EpiArgs {
+  u16* out;        // PLAIN: dX [M, ldo];  SWIGLU_BWD: dgu [M, 2N]
+  const u16* gu;   // SWIGLU_BWD: gate | up [M, 2N]
+  long ldo;
+  int N;
+};
+
+template <class G, int EPI>
+__device__ __forceinline__ void epilogue(char* smem, f32x4 (&acc)[G::FM][G::FN], const EpiArgs& ea, int n0, int m0,
+                                         int wm, int wn, int w, int lane) {
+  const int g = lane >> 4, c = lane & 15;
+  float* ep = reinterpret_cast<float*>(smem) + w * 16 * G::EPI_LD;
+  constexpr int SEGS = G::TM / 8;  // 16-byte output segments per m row
+#pragma unroll
+  for (int jf = 0; jf < G::FN; ++jf) {
+#pragma unroll
+    for (int i = 0; i < G::FM; ++i) *(f32x4*)(ep + c * G::EPI_LD + 16 * i + 4 * g) = acc[i][jf];
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // wave-private region: writes before reads
+#pragma unroll
+    for (int it = 0; it < 16 * SEGS / 64; ++it) {
+      const int seg = it * 64 + lane, row = seg / SEGS, cs = seg - row * SEGS;
+      const float* pr = ep + row * G::EPI_LD + cs * 8;
+      float v[8];
+      *(float4*)&v[0] = *(const float4*)pr;
+      *(float4*)&v[4] = *(const float4*)(pr + 4);
+      const long m = m0 + wn * G::TN + 16 * jf + row;
+      const int n = n0 + wm * G::TM + cs * 8;
+      if constexpr (EPI == EPI_PLAIN) {
+        *(uint4*)(ea.out + m * ea.ldo + n) = pack8(v);
+      } else {
+        const long base = m * 2L * ea.N + n;
+        float gt[8], up[8], dg[8], du[8];
+        unpack8(*(const uint4*)(ea.gu + base), gt);
+        unpack8(*(const uint4*)(ea.gu + base + ea.N), up);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const float s = 1.f / (1.f + __expf(-gt[e]));
+          du[e] = v[e] * gt[e] * s;
+          dg[e] = v[e] * up[e] * s * (1.f + gt[e] * (1.f - s));
+        }
+        *(uint4*)(ea.out + base) = pack8(dg);
+        *(uint4*)(ea.out + base + ea.N) = pack8(du);
+      }
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // reads done before the next slice overwrites
+  }
+}
+
+template <int BM, int BN, int WM, int WN, int NS, int EPI>
+__global__ void __launch_bounds__(NT) dgrad_kernel(const u16* __restrict__ dY, const u16* __restrict__ W, int K,
+                                                   long ldd, long ldw, int nbn, int nbm, int group, EpiArgs ea) {
+  using G = Cfg<BM, BN, WM, WN, NS>;
+  __shared__ __attribute__((aligned(16))) char smem[G::LDS];
+  const int nwg = gridDim.x, orig = blockIdx.x;
+  const int xcd = orig & 7, q8 = nwg >> 3, r8 = nwg & 7;
+  const int wgid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (orig >> 3);
+  const int per_group = group * nbm;
+  const int grp = wgid / per_group, first = grp * group;
+  const int gsz = min(nbn - first, group);
+  const int in = wgid - grp * per_group;
+  const int bn = first + in % gsz, bm = in / gsz;
+  const int n0 = bn * BM, m0 = bm * BN;
+  SFT_DASSERT(bn < nbn && bm < nbm);
+
+  const int tid = threadIdx.x, lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = w / WN, wn = w - wm * WN;
+
+  Stager<G> st;
+  st.init(W, dY, ldw, ldd, n0, m0, w, lane, K / BK);
+  const int g = lane >> 4, ii = lane & 15, qq = ii >> 2, pp = ii & 3;
+  const int pg = ((g & 1) << 1) | (g >> 1);  // the block order of the transposed A reads (gemm_wgrad.hip)
+  const int r0 = 4 * pg + qq;
+  int offA[G::FM];
+#pragma unroll
+  for (int i = 0; i < G::FM; ++i) {
+    const int nl = wm * G::TM + 16 * i;
+    offA[i] = (nl >> 7) * AIMG + img_a(r0, 2 * ((nl & 127) >> 4) + (pp >> 1)) + 8 * (pp & 1);
+  }
+  // B fragment rows wn*TN + 16 j + ii all share the swizzle of ii: fragment j is 1 KB after j - 1
+  const int rowb = wn * G::TN + ii;
+  const int offB1 = G::STAGE_A + rowb * BROWB + 16 * swz_b(ii, pg >> 1) + 8 * (pg & 1);
+  const int offB2 = G::STAGE_A + rowb * BROWB + 16 * swz_b(ii, 2 + (pg >> 1)) + 8 * (pg & 1);
+  f32x4 acc[G::FM][G::FN];
+#pragma unroll
+  for (int i = 0; i < G::FM; ++i)
+#pragma unroll
+    for (int j = 0; j < G::FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  char* b[5];
+#pragma unroll
+  for (int i = 0; i < 5; ++i) b[i] = smem + (i < NS ? i : 0) * G::STAGE;
+  ring_loop<G>(b[0], b[1], b[2], b[3], b[4], K / BK, st, offA, offB1, offB2, acc);
+  __syncthreads();
+  epilogue<G, EPI>(smem, acc, ea, n0, m0, wm, wn, w, lane);
+}
+
+static int group_n() {
+  static const int v = [] {
+    const char* e = std::getenv("SFTAMD_DGRAD_GROUP");
+    return e && e[0] ? std::max(1, atoi(e)) : 8;
+  }();
+  return v;
+}
+
+template <int BM, int BN, int WM, int WN, int NS, int EPI>
+void launch(const at::Tensor& dy, const at::Tensor& w, const EpiArgs& ea) {
+  const int M = dy.size(0), K = dy.size(1), N = w.size(1);
+  const int nbn = N / BM, nbm = M / BN;
+  dgrad_kernel<BM, BN, WM, WN, NS, EPI><<<nbn * nbm, NT, 0, cur_stream()>>>(
+      (const u16*)dy.data_ptr(), (const u16*)w.data_ptr(), K, dy.stride(0), w.stride(0), nbn, nbm,
+      std::min(group_n(), nbn), ea);
+  SFT_LAUNCH_CHECK();
+}
+
+}  // namespace dgrad
+
+// dX = dy @ w (w [K, N]); with gate_up ([M, 2N], the SwiGLU input saved by the forward) the SwiGLU backward
+// is fused: returns dgu [M, 2N] instead of dX. cfg: 0 = default (256 x 256, 4 stages), 1 = 3 stages.
+at::Tensor dgrad_gemm(const at::Tensor& dy, const at::Tensor& w, const c10::optional<at::Tensor>& gate_up,
+                      int64_t cfg) {
+  SFT_CHECK_CUDA(dy);
+  SFT_CHECK_BF16(dy);
+  SFT_CHECK_BF16(w);
+  SFT_CHECK(dy.dim() == 2 && w.dim() == 2, "dgrad_gemm: 2-D operands");
+  SFT_CHECK(dy.stride(1) == 1 && w.stride(1) == 1, "dgrad_gemm: rows must be contiguous");
+  const int64_t M = dy.size(0), K = dy.size(1), N = w.size(1);
+  SFT_CHECK(w.size(0) == K, "dgrad_gemm: dy [M, K] . w [K, N]");
+  SFT_CHECK(M % 256 == 0 && N % 256 == 0 && K % 32 == 0 && K >= 32, "dgrad_gemm: M, N multiples of 256, K of 32");
+  SFT_CHECK(dy.stride(0) % 8 == 0 && w.stride(0) % 8 == 0 && (uintptr_t)dy.data_ptr() % 16 == 0 &&
+                (uintptr_t)w.data_ptr() % 16 == 0,
+            "dgrad_gemm: 16-byte aligned rows");
+  dgrad::EpiArgs ea{};
+  ea.N = (int)N;
+  at::Tensor out;
+  const bool swiglu = gate_up.has_value() && gate_up->defined();
+  if (swiglu) {
+    const at::Tensor& gu = *gate_up;
+    SFT_CHECK_BF16(gu);
+    SFT_CHECK_CONTIG(gu);
+    SFT_CHECK(gu.dim() == 2 && gu.size(0) == M && gu.size(1) == 2 * N, "dgrad_gemm: gate_up must be [M, 2N]");
+    out = at::empty({M, 2 * N}, dy.options());
+    ea.gu = (const u16*)gu.data_ptr();
+    ea.ldo = 2 * N;
+  } else {
+    out = at::empty({M, N}, dy.options());
+    ea.ldo = N;
+  }
+  ea.out = (u16*)out.data_ptr();
+  if (M == 0 || N == 0) return out;
+  if (swiglu) {
+    if (cfg == 1) dgrad::launch<256, 256, 2, 4, 3, dgrad::EPI_SWIGLU_BWD>(dy, w, ea);
+    else dgrad::launch<256, 256, 2, 4, 4, dgrad::EPI_SWIGLU_BWD>(dy, w, ea);
+  } else {
+    if (cfg == 1) dgrad::launch<256, 256, 2, 4, 3, dgrad::EPI_PLAIN>(dy, w, ea);
+    else dgrad::launch<256, 256, 2, 4, 4, dgrad::EPI_PLAIN>(dy, w, ea);
+  }
+  return out;
+}
+
+TORCH_LIBRARY_IMPL(sftamd, CUDA, m) { m.impl("dgrad_gemm", &dgrad_gemm); }
+
+}  // namespace sftamd

@@ -84,6 +84,8 @@ class MLP(nn.Module):
 
     def forward(self, h):
         L = self.lora
+        if L is None and ops.fuse_swiglu_down():  # SwiGLU backward fused into the down projection's dgrad GEMM
+            return ops.swiglu_linear(ops.linear(h, self.gate_up_proj), self.down_proj)
         if L is None:
             a = ops.linear_swiglu(h, self.gate_up_proj)  # GEMM + SwiGLU epilogue where the shapes allow
         else:

@@ -171,7 +171,7 @@ class LinearFn(Function):
         dy2d = dy.reshape(-1, dy.shape[-1])
         dx = dw = None
         if ctx.needs_input_grad[0]:
-            dx = torch.mm(dy2d, w).view(*dy.shape[:-1], w.shape[1])
+            dx = dgrad_mm(dy2d, w).view(*dy.shape[:-1], w.shape[1])
         if ctx.needs_input_grad[1]:
             dw = _accumulate_weight_grad(w, dy2d, x.reshape(-1, x.shape[-1]))
         return dx, dw
@@ -179,6 +179,76 @@ class LinearFn(Function):
 
 def linear(x: torch.Tensor, weight: torch.Tensor) -> torch.Tensor:
     return LinearFn.apply(x, weight)
+
+
+# ----------------------------------------------------------------------------- input-gradient GEMM
+_DGRAD_MODE = os.environ.get("SFTAMD_DGRAD", "auto")  # auto | blas | hip
+
+
+def _dgrad_ok(dy2d: torch.Tensor, w: torch.Tensor) -> bool:
+    """Shapes the hand-written NN dgrad (csrc/gemm_dgrad.hip, 256 x 256 tiles) handles."""
+    M, K = dy2d.shape
+    N = w.shape[1]
+    return (_DGRAD_MODE != "blas" and _ext.use_hip(dy2d) and dy2d.dtype == torch.bfloat16 and w.dtype == torch.bfloat16
+            and M % 256 == 0 and M > 0 and N % 256 == 0 and K % 32 == 0 and dy2d.stride(1) == 1 and w.stride(1) == 1
+            and dy2d.stride(0) % 8 == 0 and w.stride(0) % 8 == 0 and dy2d.data_ptr() % 16 == 0
+            and w.data_ptr() % 16 == 0)
+
+
+def dgrad_mm(dy2d: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
+    """dX = dy @ W (W = the projection's [out, in] weight). The HIP kernel where it beats hipBLASLt
+    (profiles/r2_dgrad.md, M = 8192: o_proj 0.063 vs 0.078 ms, qkv 0.088 vs 0.097 ms): reductions of at most
+    4096 output features into at most 4096 inputs; gate_up (K = 22016) and lm_head stay on hipBLASLt."""
+    if _dgrad_ok(dy2d, w) and (_DGRAD_MODE == "hip" or (dy2d.shape[1] <= 4096 and w.shape[1] <= 4096)):
+        return _ext.ops().dgrad_gemm(dy2d, w, None, 1)
+    return torch.mm(dy2d, w)
+
+
+class SwiGLULinearFn(Function):
+    """y = swiglu(gu) @ W^T — the MLP down projection with its SwiGLU input. Backward: ONE
+    HIP GEMM dgu = swiglu_bwd(dy @ W, gu) with the SwiGLU backward in the epilogue (the [M, I] dact is never
+    written), plus the weight gradient from the saved activation."""
+
+    @staticmethod
+    def forward(ctx, gu, weight):
+        act = _ext.ops().swiglu_fwd(gu)
+        ctx.save_for_backward(gu, act)
+        ctx.weight = weight
+        a2d = act.reshape(-1, act.shape[-1])
+        return torch.nn.functional.linear(a2d, weight).view(*gu.shape[:-1], weight.shape[0])
+
+    @staticmethod
+    def backward(ctx, dy):
+        gu, act = ctx.saved_tensors
+        w = ctx.weight
+        dy2d = dy.reshape(-1, dy.shape[-1]).contiguous()
+        gu2d = gu.reshape(-1, gu.shape[-1])
+        dgu = dw = None
+        if ctx.needs_input_grad[0]:
+            if _dgrad_ok(dy2d, w) and gu2d.is_contiguous():
+                dgu = _ext.ops().dgrad_gemm(dy2d, w, gu2d, 1)
+            else:
+                dgu = _ext.ops().swiglu_bwd(torch.mm(dy2d, w), gu2d)
+            dgu = dgu.view(gu.shape)
+        if ctx.needs_input_grad[1]:
+            dw = _accumulate_weight_grad(w, dy2d, act.reshape(-1, act.shape[-1]))
+        return dgu, dw
+
+
+_SWIGLU_DOWN = os.environ.get("SFTAMD_SWIGLU_DOWN", "1") == "1"
+
+
+def fuse_swiglu_down() -> bool:
+    """MLP split (default): gate_up GEMM | down GEMM with the SwiGLU backward fused into its dgrad. Off when the
+    forward-fused gate_up + SwiGLU epilogue is requested instead (SFTAMD_TN=swiglu / 1) or SFTAMD_SWIGLU_DOWN=0."""
+    return _SWIGLU_DOWN and _TN_MODE not in ("1", "swiglu")
+
+
+def swiglu_linear(gu: torch.Tensor, weight: torch.Tensor) -> torch.Tensor:
+    """linear(swiglu(gu), weight) with the fused backward where the HIP kernels apply."""
+    if _SWIGLU_DOWN and _ext.use_hip(gu) and gu.dtype == torch.bfloat16 and gu.is_contiguous():
+        return SwiGLULinearFn.apply(gu, weight)
+    return linear(swiglu(gu), weight)
 
 
 # ----------------------------------------------------------------------------- embedding

@@ -438,3 +438,39 @@ def test_gemm_tn_rope(cfg):
     exp = torch.cat([ref.apply_rope(qk, cs, sn).reshape(M, -1), y[:, (nq + nkv) * D:]], dim=1)
     assert rel_err(out, exp) < 1e-2
     assert torch.equal(out[:, (nq + nkv) * D:], y[:, (nq + nkv) * D:]) or rel_err(out[:, (nq + nkv) * D:], y[:, (nq + nkv) * D:]) < 5e-3
+
+
+@pytest.mark.parametrize("M,K,N,wpad", [(256, 64, 256, 0), (512, 2048, 768, 0), (256, 96, 512, 64), (768, 1024, 256, 0)])
+def test_dgrad_gemm_plain(M, K, N, wpad):
+    """dX = dy @ w (w [K, N], optionally a column-sliced view): the hand-written NN dgrad vs fp32."""
+    torch.manual_seed(0)
+    dy = torch.randn(M, K, device="cuda", dtype=torch.bfloat16)
+    wfull = torch.randn(K, N + wpad, device="cuda", dtype=torch.bfloat16)
+    w = wfull[:, :N]
+    for cfg in (0, 1):
+        out = _ext.ops().dgrad_gemm(dy, w, None, cfg)
+        want = dy.float() @ w.float()
+        assert out.shape == (M, N)
+        assert rel_err(out, want) < 1e-2, rel_err(out, want)
+    # asymmetric structure: a row-shifted identity catches any transposed / permuted k mapping
+    eye = torch.zeros(K, N, device="cuda")
+    eye[torch.arange(min(K, N)), (torch.arange(min(K, N)) + 5) % N] = 1.0
+    ramp = (torch.arange(M * K, device="cuda") % 251).float().view(M, K).to(torch.bfloat16)
+    got = _ext.ops().dgrad_gemm(ramp, eye.to(torch.bfloat16), None, 0).float()
+    assert torch.equal(got, ramp.float() @ eye)
+
+
+@pytest.mark.parametrize("M,K,N", [(256, 256, 256), (512, 2048, 512), (256, 64, 768)])
+def test_dgrad_gemm_swiglu_bwd(M, K, N):
+    """Down-projection dgrad with the SwiGLU backward fused into the epilogue == swiglu_bwd(dy @ w, gu) in fp32."""
+    torch.manual_seed(1)
+    dy = torch.randn(M, K, device="cuda", dtype=torch.bfloat16)
+    w = (0.05 * torch.randn(K, N, device="cuda")).to(torch.bfloat16)
+    gu = torch.randn(M, 2 * N, device="cuda", dtype=torch.bfloat16)
+    dgu = _ext.ops().dgrad_gemm(dy, w, gu, 0)
+    dact = dy.float() @ w.float()
+    g, u = gu.float().chunk(2, dim=-1)
+    s = torch.sigmoid(g)
+    want = torch.cat([dact * u * s * (1 + g * (1 - s)), dact * g * s], dim=-1)
+    assert dgu.shape == (M, 2 * N)
+    assert rel_err(dgu, want) < 1e-2, rel_err(dgu, want)
