@@ -472,7 +472,7 @@ class QKVRopeFn(Function):
         _rope_inplace(dqkv, cos, sin, n_q, n_kv, hd, inverse=True)
         dx = dw = None
         if ctx.needs_input_grad[0]:
-            dx = torch.mm(dqkv, w).view(ctx.x_shape)
+            dx = dgrad_mm(dqkv, w).view(ctx.x_shape)
         if ctx.needs_input_grad[1]:
             dw = _accumulate_weight_grad(w, dqkv, x2d)
         return dx, dw, None, None, None, None, None

@@ -98,6 +98,9 @@ class SFTConfig:
     ddp_first_bucket_mb: float = 4.0
     ddp_broadcast_params: bool = False      # weights are identical by construction (seeded / loaded)
     ddp_check_sync_every: int = 0           # cross-rank param checksum every N steps (0 = off)
+    # None = auto: on the GPU, padded batches are padded to a multiple of 64 tokens (and packed batches to 256)
+    # so every micro-batch GEMM has M % 256 == 0 and runs on the MFMA-tiled HIP paths; pads are label -100, so
+    # the loss and gradients are unchanged. 1 = pad to the longest sample exactly (TRL's behaviour).
     pad_to_multiple_of: Optional[int] = None
     max_train_samples: Optional[int] = None
     max_eval_samples: Optional[int] = None

@@ -114,7 +114,10 @@ class SFTTrainer:
         self.eval_dataset = self._prepare(eval_dataset, args.max_eval_samples)
         pad_id = self.tokenizer.pad_token_id if self.tokenizer is not None else (model.config.pad_token_id or 0)
         self._pad_id = pad_id
-        self.collator = data_collator or SFTCollator(pad_id, args.pad_to_multiple_of, args.max_length, args.packing,
+        pad_mult = args.pad_to_multiple_of
+        if pad_mult is None and dev.type == "cuda":
+            pad_mult = 256 if args.packing else 64
+        self.collator = data_collator or SFTCollator(pad_id, pad_mult, args.max_length, args.packing,
                                                      args.per_device_train_batch_size * (args.max_length or 1024)
                                                      if args.packing else None)
         # ------------------------------------------------------------ engine + optimizer

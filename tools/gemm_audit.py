@@ -51,6 +51,9 @@ def flops(name, shapes):
         if name.startswith("sftamd::gemm_tn"):
             (m, k), (n, _) = shapes[0], shapes[1]
             return 2 * m * n * k
+        if name == "sftamd::dgrad_gemm":  # dy [M, K], w [K, N]
+            (m, k), (_, n) = shapes[0], shapes[1]
+            return 2 * m * n * k
         if name == "sftamd::wgrad_gemm":  # out [N, K], dy [T, N], x [T, K]
             (n, k), (t, _) = shapes[0], shapes[1]
             return 2 * t * n * k
@@ -62,7 +65,7 @@ def flops(name, shapes):
 rows = []
 for e in prof.key_averages(group_by_input_shape=True):
     if not (e.key in ("aten::mm", "aten::addmm") or e.key.startswith("sftamd::gemm_tn")
-            or e.key == "sftamd::wgrad_gemm"):
+            or e.key in ("sftamd::wgrad_gemm", "sftamd::dgrad_gemm")):
         continue
     dev = getattr(e, "device_time_total", None)
     if dev is None:
