@@ -135,6 +135,22 @@ def test_embedding():
     assert torch.equal(g, g2)  # deterministic
 
 
+def test_embedding_bwd_skewed_runs():
+    """Real chat data: a few ids repeat hundreds of times (system prompt in every sample). Runs of 1, 7, 8, 9,
+    17 and 700 rows (the batched-load tails) against the fp32 sum; bf16 rows accumulate into an existing grad."""
+    torch.manual_seed(2)
+    H = 2048
+    ids = torch.cat([torch.full((n,), i, dtype=torch.long) for i, n in enumerate([1, 7, 8, 9, 17, 700, 3])])
+    ids = ids[torch.randperm(ids.numel())].to(DEV)
+    M, V = ids.numel(), 16
+    dy = torch.randn(M, H, device=DEV, dtype=torch.bfloat16)
+    g = torch.randn(V, H, device=DEV, dtype=torch.bfloat16)
+    want = g.float().index_add_(0, ids, dy.float())
+    s, perm = torch.sort(ids.to(torch.int32), stable=True)
+    _ext.ops().embedding_bwd(dy, s, perm.to(torch.int32), g)
+    assert rel_err(g, want) < 1e-2
+
+
 @pytest.mark.parametrize("V", [128256, 512])
 def test_cross_entropy(V):
     torch.manual_seed(0)
