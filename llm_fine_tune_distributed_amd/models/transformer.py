@@ -54,6 +54,7 @@ class Attention(nn.Module):
         self.o_proj = nn.Parameter(torch.empty(cfg.hidden_size, cfg.q_size))
         self.lora = None  # set by apply_lora
         self.cp_group = None  # context-parallel process group (CausalLM.enable_context_parallel)
+        self.cp_layout = "zigzag"
 
     def forward(self, h, rope_cs, cu_seqlens, max_seqlen):
         c = self.cfg
@@ -68,7 +69,7 @@ class Attention(nn.Module):
         if self.cp_group is not None:
             from ..parallel.context_parallel import ring_attention
             a = ring_attention(qkv, cu_seqlens, max_seqlen, c.num_attention_heads, c.num_key_value_heads, c.head_dim,
-                               self.cp_group)
+                               self.cp_group, layout=self.cp_layout)
         else:
             a = ops.flash_attention(qkv, cu_seqlens, max_seqlen, c.num_attention_heads, c.num_key_value_heads,
                                     c.head_dim)
@@ -158,12 +159,13 @@ class CausalLM(nn.Module):
     def gradient_checkpointing_disable(self):
         self.gradient_checkpointing = False
 
-    def enable_context_parallel(self, group) -> None:
+    def enable_context_parallel(self, group, layout: str = "zigzag") -> None:
         """Attention over sequence chunks spread across ``group`` (ring attention, parallel/context_parallel.py).
         Inputs must then be this rank's chunk with explicit global ``position_ids`` and pre-shifted labels
-        (``context_parallel.shard_batch``)."""
+        (``context_parallel.shard_batch`` with the same ``layout``)."""
         for layer in self.model.layers:
             layer.self_attn.cp_group = group
+            layer.self_attn.cp_layout = layout
 
     @torch.no_grad()
     def init_weights(self, seed: int = 0):

@@ -31,8 +31,13 @@ sums gradients over the whole world, and the loss is normalised by the global to
 tested in ``tests/test_context_parallel_cpu.py``. CPU tensors (gloo) take an fp32 PyTorch block
 path with the same interface, which is what the CPU tests exercise.
 
-Layout choice: plain contiguous chunks. Causal work is therefore unbalanced (rank cp-1 computes
-cp blocks, rank 0 one). A zig-zag assignment would balance it and is future work.
+Layouts (``layout=``):
+* ``"zigzag"`` (default): every sequence is cut into 2 cp half-chunks and rank r holds half-chunks r and
+  2 cp - 1 - r, concatenated. With causal attention every ring step then costs every rank exactly two
+  (L/2)^2 blocks — (q_r, kv_src) and (q_{2cp-1-r}, kv_src) below the diagonal, or the two causal diagonal
+  halves plus (q_{2cp-1-r}, kv_r) at step 0 — so no rank waits for another (the causal work of rank r is
+  balanced; with contiguous chunks rank cp - 1 computes cp blocks and rank 0 one).
+* ``"contiguous"``: rank r holds positions ``[r L, (r + 1) L)`` (simplest; unbalanced).
 """
 from __future__ import annotations
 
@@ -156,6 +161,8 @@ def _exchange(tensors, nxt, prv, group):
 
 
 class RingAttnFn(Function):
+    """Contiguous layout: one causal / full block per ring step (see module docstring)."""
+
     @staticmethod
     def forward(ctx, qkv, cu, max_seqlen, n_q, n_kv, D, scale, group):
         r, n, nxt, prv = _ring_peers(group)
@@ -212,40 +219,147 @@ class RingAttnFn(Function):
         return dqkv, None, None, None, None, None, None, None
 
 
-def ring_attention(qkv, cu_seqlens, max_seqlen, n_q, n_kv, head_dim, group, scale: Optional[float] = None):
+def _zz_pairs(r: int, src: int, n: int):
+    """(q half, kv half, causal) blocks of a zig-zag ring step: local half 0 / 1 of rank x is global
+    half-chunk x / 2n - 1 - x; a key half-chunk below the query's is a full block, the same one causal."""
+    qc = (r, 2 * n - 1 - r)
+    kc = (src, 2 * n - 1 - src)
+    out = []
+    for x in range(2):
+        for y in range(2):
+            if kc[y] < qc[x]:
+                out.append((x, y, False))
+            elif kc[y] == qc[x]:
+                out.append((x, y, True))
+    return out
+
+
+def _halves(t: torch.Tensor, B: int, h: int):
+    """[B * 2h, F] -> the two [B * h, F] half-chunk row sets (copies)."""
+    v = t.view(B, 2, h, t.shape[-1])
+    return [v[:, 0].reshape(B * h, -1), v[:, 1].reshape(B * h, -1)]
+
+
+def _join(a: torch.Tensor, b: torch.Tensor, B: int, h: int) -> torch.Tensor:
+    return torch.stack([a.view(B, h, -1), b.view(B, h, -1)], 1).reshape(B * 2 * h, -1)
+
+
+class ZigzagRingAttnFn(Function):
+    """Zig-zag layout (module docstring): local rows are [half r | half 2n-1-r] per sequence of 2h tokens."""
+
+    @staticmethod
+    def forward(ctx, qkv, B, h, n_q, n_kv, D, scale, group):
+        r, n, nxt, prv = _ring_peers(group)
+        qh = _halves(qkv[:, : n_q * D], B, h)
+        cur = qkv[:, n_q * D:].contiguous()
+        cu = torch.arange(0, (B + 1) * h, h, dtype=torch.int32, device=qkv.device)
+        o = [None, None]
+        lse = [None, None]
+        for s in range(n):
+            src = (r - s) % n
+            pending = None
+            if s < n - 1:
+                (nxt_buf,), pending = _exchange([cur], nxt, prv, group)
+            kvh = _halves(cur, B, h)
+            for x, y, causal in _zz_pairs(r, src, n):
+                o_s, lse_s = _block_fwd(qh[x], kvh[y], cu, h, n_q, n_kv, D, scale, causal=causal)
+                o[x], lse[x] = _merge(o[x], lse[x], o_s, lse_s, n_q, D)
+            if pending is not None:
+                for w in pending:
+                    w.wait()
+                cur = nxt_buf
+        out = _join(o[0], o[1], B, h).to(qkv.dtype)
+        ctx.save_for_backward(qkv, out, lse[0], lse[1])
+        ctx.dims = (B, h, n_q, n_kv, D, scale)
+        ctx.group = group
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        qkv, out, lse0, lse1 = ctx.saved_tensors
+        B, h, n_q, n_kv, D, scale = ctx.dims
+        group = ctx.group
+        r, n, nxt, prv = _ring_peers(group)
+        qh = _halves(qkv[:, : n_q * D], B, h)
+        oh = _halves(out, B, h)
+        dh = _halves(dout.contiguous(), B, h)
+        lse = (lse0, lse1)
+        cu = torch.arange(0, (B + 1) * h, h, dtype=torch.int32, device=qkv.device)
+        cur = qkv[:, n_q * D:].contiguous()
+        dq = [torch.zeros(B * h, n_q * D, dtype=torch.float32, device=qkv.device) for _ in range(2)]
+        dkv = torch.zeros(cur.shape, dtype=torch.float32, device=qkv.device)
+        for s in range(n):
+            src = (r - s) % n
+            pending_kv = None
+            if s < n - 1:
+                (nxt_kv,), pending_kv = _exchange([cur], nxt, prv, group)
+            kvh = _halves(cur, B, h)
+            dkvh = [torch.zeros(B * h, cur.shape[1], dtype=torch.float32, device=qkv.device) for _ in range(2)]
+            for x, y, causal in _zz_pairs(r, src, n):
+                dq_s, dkv_s = _block_bwd(dh[x], qh[x], kvh[y], oh[x], lse[x], cu, h, n_q, n_kv, D, scale,
+                                         causal=causal)
+                dq[x] += dq_s
+                dkvh[y] += dkv_s
+            dkv = dkv + _join(dkvh[0], dkvh[1], B, h)
+            (nxt_dkv,), pending = _exchange([dkv], nxt, prv, group)
+            for w in pending + (pending_kv or []):
+                w.wait()
+            dkv = nxt_dkv
+            if pending_kv is not None:
+                cur = nxt_kv
+        dqkv = torch.cat([_join(dq[0], dq[1], B, h), dkv], 1).to(qkv.dtype)
+        return dqkv, None, None, None, None, None, None, None
+
+
+def ring_attention(qkv, cu_seqlens, max_seqlen, n_q, n_kv, head_dim, group, scale: Optional[float] = None,
+                   layout: str = "zigzag"):
     """Causal GQA attention for a sequence-sharded batch (see module docstring); ``qkv`` is this rank's
-    packed chunk [B * L, (n_q + 2 n_kv) * D], ``cu_seqlens`` its local sequence boundaries."""
+    packed chunk [B * L, (n_q + 2 n_kv) * D], ``cu_seqlens`` its local sequence boundaries (equal lengths L;
+    zig-zag: L even, rows [half r | half 2 cp - 1 - r] per sequence)."""
     scale = scale if scale is not None else 1.0 / math.sqrt(head_dim)
     if group is None or dist.get_world_size(group) == 1:
         from ..ops import flash_attention
         return flash_attention(qkv, cu_seqlens, max_seqlen, n_q, n_kv, head_dim, scale, True)
+    if layout == "zigzag":
+        L = int(max_seqlen)
+        B = qkv.shape[0] // L
+        if L % 2 or B * L != qkv.shape[0]:
+            raise ValueError("zig-zag context parallelism needs equal, even local sequence lengths")
+        return ZigzagRingAttnFn.apply(qkv, B, L // 2, n_q, n_kv, head_dim, scale, group)
     return RingAttnFn.apply(qkv, cu_seqlens, max_seqlen, n_q, n_kv, head_dim, scale, group)
 
 
 # ----------------------------------------------------------------------------------------- data
-def shard_batch(b: Dict, cp_rank: int, cp_size: int, pad_id: int = 0) -> Dict:
+def shard_batch(b: Dict, cp_rank: int, cp_size: int, pad_id: int = 0, layout: str = "zigzag") -> Dict:
     """Cut a padded micro-batch ([B, T] input_ids / labels, unshifted HF labels) into this CP rank's chunk.
 
     Labels are shifted over the FULL sequence first (the last token of chunk r is scored against the
-    first token of chunk r + 1), T is padded to a multiple of ``cp_size`` (pads: ``pad_id`` / -100), and the
-    chunk carries its global ``position_ids`` so RoPE sees the true positions. ``num_items`` becomes the local
-    count of scored tokens: summed over every rank it is the global count the loss is normalised by."""
+    first token of chunk r + 1), T is padded to a multiple of ``cp_size`` (zig-zag: ``2 cp_size``; pads:
+    ``pad_id`` / -100), and the chunk carries its global ``position_ids`` so RoPE sees the true positions.
+    ``num_items`` becomes the local count of scored tokens: summed over every rank it is the global count the
+    loss is normalised by. Zig-zag: the chunk is half-chunks cp_rank and 2 cp_size - 1 - cp_rank."""
     ids, labels = b["input_ids"], b["labels"]
     if ids.dim() != 2 or "cu_seqlens" in b:
         raise ValueError("context parallelism expects padded [B, T] batches (packing=False)")
     B, T = ids.shape
     shifted = torch.cat([labels[:, 1:], torch.full_like(labels[:, :1], -100)], dim=1)
-    Tp = -(-T // cp_size) * cp_size
+    unit = 2 * cp_size if layout == "zigzag" else cp_size
+    Tp = -(-T // unit) * unit
     if Tp != T:
         ids = torch.cat([ids, torch.full((B, Tp - T), pad_id, dtype=ids.dtype, device=ids.device)], 1)
         shifted = torch.cat([shifted, torch.full((B, Tp - T), -100, dtype=shifted.dtype, device=shifted.device)], 1)
-    L = Tp // cp_size
-    sl = slice(cp_rank * L, (cp_rank + 1) * L)
+    if layout == "zigzag":
+        h = Tp // (2 * cp_size)
+        pos = torch.cat([torch.arange(cp_rank * h, (cp_rank + 1) * h),
+                         torch.arange((2 * cp_size - 1 - cp_rank) * h, (2 * cp_size - cp_rank) * h)]).to(ids.device)
+    else:
+        L = Tp // cp_size
+        pos = torch.arange(cp_rank * L, (cp_rank + 1) * L, device=ids.device)
     out = dict(b)
-    out["input_ids"] = ids[:, sl].contiguous()
-    out["labels"] = shifted[:, sl].contiguous()
+    out["input_ids"] = ids[:, pos].contiguous()
+    out["labels"] = shifted[:, pos].contiguous()
     out["shifted"] = True
-    out["position_ids"] = torch.arange(cp_rank * L, (cp_rank + 1) * L, device=ids.device).expand(B, L)
+    out["position_ids"] = pos.expand(B, pos.numel())
     n = int((out["labels"] != -100).sum())
     out["num_items"] = n
     out["num_items_t"] = torch.tensor([float(n)], device=ids.device)

@@ -95,6 +95,7 @@ class SFTConfig:
     # context parallelism (ring attention, parallel/context_parallel.py): consecutive groups of this many ranks
     # share each batch with the sequence split across them; data parallelism runs across the groups
     context_parallel_size: int = 1
+    context_parallel_layout: str = "zigzag"   # zigzag (causal work balanced across the group) | contiguous
     ddp_first_bucket_mb: float = 4.0
     ddp_broadcast_params: bool = False      # weights are identical by construction (seeded / loaded)
     ddp_check_sync_every: int = 0           # cross-rank param checksum every N steps (0 = off)

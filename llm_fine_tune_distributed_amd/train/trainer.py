@@ -103,7 +103,7 @@ class SFTTrainer:
         if args.gradient_checkpointing:
             model.gradient_checkpointing_enable()
         if self.cp_size > 1:
-            model.enable_context_parallel(self.cp_group)
+            model.enable_context_parallel(self.cp_group, args.context_parallel_layout)
         self.trainable_params = model.num_parameters(trainable_only=True)
         self.total_params = model.num_parameters()
         # ------------------------------------------------------------ data
@@ -220,7 +220,7 @@ class SFTTrainer:
         if self.cp_size == 1:
             return b
         from ..parallel.context_parallel import shard_batch
-        return shard_batch(b, self.cp_rank, self.cp_size, self._pad_id)
+        return shard_batch(b, self.cp_rank, self.cp_size, self._pad_id, self.args.context_parallel_layout)
 
     def global_num_items(self, micro: List[Dict]):
         """Global count of loss tokens of this optimizer step (TRL ``num_items_in_batch``).

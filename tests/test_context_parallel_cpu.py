@@ -24,11 +24,16 @@ def _init(rank, world, port):
     return dist
 
 
-def _chunk_rows(B, T, L, r):
+def _chunk_rows(B, T, L, r, layout="contiguous", world=1):
+    if layout == "zigzag":
+        h = L // 2
+        return torch.cat([torch.cat([torch.arange(b * T + r * h, b * T + (r + 1) * h),
+                                     torch.arange(b * T + (2 * world - 1 - r) * h, b * T + (2 * world - r) * h)])
+                          for b in range(B)])
     return torch.cat([torch.arange(b * T + r * L, b * T + (r + 1) * L) for b in range(B)])
 
 
-def _op_worker(rank, world, port, out_dir):
+def _op_worker(rank, world, port, out_dir, layout):
     dist = _init(rank, world, port)
     from llm_fine_tune_distributed_amd.ops import reference as ref
     from llm_fine_tune_distributed_amd.parallel.context_parallel import ring_attention
@@ -41,27 +46,28 @@ def _op_worker(rank, world, port, out_dir):
     full = qkv.clone().requires_grad_(True)
     o_ref = ref.attention(full, nq, nkv, D, cu, None, True)
     (g_ref,) = torch.autograd.grad(o_ref, full, dout)
-    rows = _chunk_rows(B, T, L, rank)
+    rows = _chunk_rows(B, T, L, rank, layout, world)
     loc = qkv[rows].clone().requires_grad_(True)
     cu_l = torch.arange(0, (B + 1) * L, L, dtype=torch.int32)
-    o = ring_attention(loc, cu_l, L, nq, nkv, D, dist.group.WORLD)
+    o = ring_attention(loc, cu_l, L, nq, nkv, D, dist.group.WORLD, layout=layout)
     (g,) = torch.autograd.grad(o, loc, dout[rows])
     torch.save({"eo": (o - o_ref[rows]).abs().max().item(), "eg": (g - g_ref[rows]).abs().max().item(),
                 "gn": g_ref[rows].abs().max().item()}, os.path.join(out_dir, f"op{rank}.pt"))
     dist.destroy_process_group()
 
 
+@pytest.mark.parametrize("layout", ["zigzag", "contiguous"])
 @pytest.mark.parametrize("world", [2, 4])
-def test_ring_attention_matches_full_attention(world):
+def test_ring_attention_matches_full_attention(world, layout):
     d = tempfile.mkdtemp()
-    mp.spawn(_op_worker, args=(world, _free_port(), d), nprocs=world, join=True)
+    mp.spawn(_op_worker, args=(world, _free_port(), d, layout), nprocs=world, join=True)
     for r in range(world):
         res = torch.load(os.path.join(d, f"op{r}.pt"))
         assert res["eo"] < 1e-5, res
         assert res["eg"] < 1e-5 * max(1.0, res["gn"]), res
 
 
-def _model_worker(rank, world, port, out_dir):
+def _model_worker(rank, world, port, out_dir, layout):
     dist = _init(rank, world, port)
     from llm_fine_tune_distributed_amd.models import build_model, tiny
     from llm_fine_tune_distributed_amd.parallel.context_parallel import shard_batch
@@ -72,8 +78,8 @@ def _model_worker(rank, world, port, out_dir):
     labels = ids.clone()
     labels[1, 15:] = -100
     m = build_model(cfg, dtype=torch.float32, seed=7)
-    m.enable_context_parallel(dist.group.WORLD)
-    b = shard_batch({"input_ids": ids, "labels": labels}, rank, world)
+    m.enable_context_parallel(dist.group.WORLD, layout)
+    b = shard_batch({"input_ids": ids, "labels": labels}, rank, world, layout=layout)
     n = torch.tensor([float(b["num_items"])])
     dist.all_reduce(n)
     m.reset_grad_use_counters()
@@ -92,11 +98,12 @@ def _model_worker(rank, world, port, out_dir):
     dist.destroy_process_group()
 
 
+@pytest.mark.parametrize("layout", ["zigzag", "contiguous"])
 @pytest.mark.parametrize("world", [2, 4])
-def test_context_parallel_model_matches_single_process(world):
+def test_context_parallel_model_matches_single_process(world, layout):
     from llm_fine_tune_distributed_amd.models import build_model, tiny
     d = tempfile.mkdtemp()
-    mp.spawn(_model_worker, args=(world, _free_port(), d), nprocs=world, join=True)
+    mp.spawn(_model_worker, args=(world, _free_port(), d, layout), nprocs=world, join=True)
     torch.manual_seed(0)
     cfg = tiny("smollm3", num_hidden_layers=4)
     B, T = 2, 21
@@ -156,3 +163,12 @@ def test_trainer_context_parallel_equals_single_process():
     for a, b in zip(single["log"], cp[0]["log"]):
         assert abs(a["loss"] - b["loss"]) < 1e-4 * max(1.0, abs(a["loss"])), (a, b)
         assert abs(a["grad_norm"] - b["grad_norm"]) < 1e-4 * max(1.0, a["grad_norm"]), (a, b)
+
+
+def test_zigzag_balances_causal_work():
+    """Every rank computes the same number of half-chunk blocks at every ring step (contiguous: 0 .. 1)."""
+    from llm_fine_tune_distributed_amd.parallel.context_parallel import _zz_pairs
+    for n in (2, 4, 8):
+        for s in range(n):
+            work = [sum(0.5 if c else 1.0 for _, _, c in _zz_pairs(r, (r - s) % n, n)) for r in range(n)]
+            assert work == [2.0] * n, (n, s, work)  # two (L/2)^2 blocks per rank per step
