@@ -27,6 +27,8 @@
 // TM + 4 floats) so every output / gate / up access is a 16-byte vector along n.
 #include "common.h"
 
+#include <type_traits>
+
 namespace sftamd {
 namespace dgrad {
 
@@ -227,9 +229,9 @@ __device__ __forceinline__ void epilogue(char* smem, f32x4 (&acc)[G::FM][G::FN],
   }
 }
 
-template <int BM, int BN, int WM, int WN, int NS, int EPI>
-__global__ void __launch_bounds__(NT) dgrad_kernel(const u16* __restrict__ dY, const u16* __restrict__ W, int K,
-                                                   long ldd, long ldw, int nbn, int nbm, int group, EpiArgs ea) {
+template <int BM, int BN, int WM, int WN, int NS, int EPI, int OCC = 1>
+__global__ void __launch_bounds__(NT, OCC) dgrad_kernel(const u16* __restrict__ dY, const u16* __restrict__ W, int K,
+                                                        long ldd, long ldw, int nbn, int nbm, int group, EpiArgs ea) {
   using G = Cfg<BM, BN, WM, WN, NS>;
   __shared__ __attribute__((aligned(16))) char smem[G::LDS];
   const int nwg = gridDim.x, orig = blockIdx.x;
@@ -283,11 +285,11 @@ static int group_n() {
   return v;
 }
 
-template <int BM, int BN, int WM, int WN, int NS, int EPI>
+template <int BM, int BN, int WM, int WN, int NS, int EPI, int OCC = 1>
 void launch(const at::Tensor& dy, const at::Tensor& w, const EpiArgs& ea) {
   const int M = dy.size(0), K = dy.size(1), N = w.size(1);
   const int nbn = N / BM, nbm = M / BN;
-  dgrad_kernel<BM, BN, WM, WN, NS, EPI><<<nbn * nbm, NT, 0, cur_stream()>>>(
+  dgrad_kernel<BM, BN, WM, WN, NS, EPI, OCC><<<nbn * nbm, NT, 0, cur_stream()>>>(
       (const u16*)dy.data_ptr(), (const u16*)w.data_ptr(), K, dy.stride(0), w.stride(0), nbn, nbm,
       std::min(group_n(), nbn), ea);
   SFT_LAUNCH_CHECK();
@@ -296,7 +298,9 @@ void launch(const at::Tensor& dy, const at::Tensor& w, const EpiArgs& ea) {
 }  // namespace dgrad
 
 // dX = dy @ w (w [K, N]); with gate_up ([M, 2N], the SwiGLU input saved by the forward) the SwiGLU backward
-// is fused: returns dgu [M, 2N] instead of dX. cfg: 0 = default (256 x 256, 4 stages), 1 = 3 stages.
+// is fused: returns dgu [M, 2N] instead of dX. cfg (tile n x m, LDS stages): 0 = 256 x 256 / 4, 1 = 256 x 256 / 3,
+// 2 = 256 x 128 / 3, 3 = 256 x 128 / 4 (156 VGPRs: three waves per SIMD; capping at 128 for two workgroups
+// per CU spills).
 at::Tensor dgrad_gemm(const at::Tensor& dy, const at::Tensor& w, const c10::optional<at::Tensor>& gate_up,
                       int64_t cfg) {
   SFT_CHECK_CUDA(dy);
@@ -306,7 +310,8 @@ at::Tensor dgrad_gemm(const at::Tensor& dy, const at::Tensor& w, const c10::opti
   SFT_CHECK(dy.stride(1) == 1 && w.stride(1) == 1, "dgrad_gemm: rows must be contiguous");
   const int64_t M = dy.size(0), K = dy.size(1), N = w.size(1);
   SFT_CHECK(w.size(0) == K, "dgrad_gemm: dy [M, K] . w [K, N]");
-  SFT_CHECK(M % 256 == 0 && N % 256 == 0 && K % 32 == 0 && K >= 32, "dgrad_gemm: M, N multiples of 256, K of 32");
+  SFT_CHECK(M % 128 == 0 && N % 256 == 0 && K % 32 == 0 && K >= 32, "dgrad_gemm: M multiple of 128 (256 for cfg 0/1), N of 256, K of 32");
+  SFT_CHECK(cfg >= 2 || M % 256 == 0, "dgrad_gemm: cfg 0/1 need M % 256 == 0");
   SFT_CHECK(dy.stride(0) % 8 == 0 && w.stride(0) % 8 == 0 && (uintptr_t)dy.data_ptr() % 16 == 0 &&
                 (uintptr_t)w.data_ptr() % 16 == 0,
             "dgrad_gemm: 16-byte aligned rows");
@@ -328,13 +333,18 @@ at::Tensor dgrad_gemm(const at::Tensor& dy, const at::Tensor& w, const c10::opti
   }
   ea.out = (u16*)out.data_ptr();
   if (M == 0 || N == 0) return out;
-  if (swiglu) {
-    if (cfg == 1) dgrad::launch<256, 256, 2, 4, 3, dgrad::EPI_SWIGLU_BWD>(dy, w, ea);
-    else dgrad::launch<256, 256, 2, 4, 4, dgrad::EPI_SWIGLU_BWD>(dy, w, ea);
-  } else {
-    if (cfg == 1) dgrad::launch<256, 256, 2, 4, 3, dgrad::EPI_PLAIN>(dy, w, ea);
-    else dgrad::launch<256, 256, 2, 4, 4, dgrad::EPI_PLAIN>(dy, w, ea);
-  }
+  auto run = [&](auto epi) {
+    constexpr int E = decltype(epi)::value;
+    switch (cfg) {
+      case 1: dgrad::launch<256, 256, 2, 4, 3, E>(dy, w, ea); break;
+      case 2: dgrad::launch<256, 128, 4, 2, 3, E>(dy, w, ea); break;
+      case 3: dgrad::launch<256, 128, 4, 2, 4, E>(dy, w, ea); break;
+      default: dgrad::launch<256, 256, 2, 4, 4, E>(dy, w, ea);
+    }
+  };
+  if (cfg >= 2) SFT_CHECK(M % 128 == 0, "dgrad_gemm: M multiple of 128");
+  if (swiglu) run(std::integral_constant<int, dgrad::EPI_SWIGLU_BWD>());
+  else run(std::integral_constant<int, dgrad::EPI_PLAIN>());
   return out;
 }
 

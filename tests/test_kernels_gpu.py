@@ -463,7 +463,7 @@ def test_dgrad_gemm_plain(M, K, N, wpad):
     dy = torch.randn(M, K, device="cuda", dtype=torch.bfloat16)
     wfull = torch.randn(K, N + wpad, device="cuda", dtype=torch.bfloat16)
     w = wfull[:, :N]
-    for cfg in (0, 1):
+    for cfg in (0, 1, 2, 3):
         out = _ext.ops().dgrad_gemm(dy, w, None, cfg)
         want = dy.float() @ w.float()
         assert out.shape == (M, N)
@@ -484,6 +484,7 @@ def test_dgrad_gemm_swiglu_bwd(M, K, N):
     w = (0.05 * torch.randn(K, N, device="cuda")).to(torch.bfloat16)
     gu = torch.randn(M, 2 * N, device="cuda", dtype=torch.bfloat16)
     dgu = _ext.ops().dgrad_gemm(dy, w, gu, 0)
+    assert torch.equal(_ext.ops().dgrad_gemm(dy, w, gu, 2), dgu)  # 256 x 128 tiles: same fp32 sums per element
     dact = dy.float() @ w.float()
     g, u = gu.float().chunk(2, dim=-1)
     s = torch.sigmoid(g)

@@ -16,6 +16,9 @@ from llm_fine_tune_distributed_amd.ops import _ext  # noqa: E402
 from llm_fine_tune_distributed_amd.utils.gemm_tuning import enable_tuned_gemms  # noqa: E402
 
 
+CFGS = [int(c) for c in os.environ.get("DGRAD_CFGS", "0,1").split(",")]
+
+
 def timeit(fn, iters=20):
     for _ in range(3):
         fn()
@@ -51,21 +54,21 @@ def main():
         for name, (K, N) in shapes.items():
             dy, w = data[name]
             flop = 2.0 * M * K * N
-            r = res.setdefault(name, {"blas": [], "hip0": [], "hip1": []})
+            r = res.setdefault(name, {"blas": [], **{f"hip{c}": [] for c in CFGS}})
             r["blas"].append(timeit(lambda: torch.mm(dy, w)))
-            for cfg in (0, 1):
+            for cfg in CFGS:
                 r[f"hip{cfg}"].append(timeit(lambda: ops.dgrad_gemm(dy, w, None, cfg)))
             r["flop"] = flop
         dy, w = data["down"]
-        r = res.setdefault("down+swiglu_bwd", {"blas+kernel": [], "fused0": [], "fused1": []})
+        r = res.setdefault("down+swiglu_bwd", {"blas+kernel": [], **{f"fused{c}": [] for c in CFGS}})
         r["blas+kernel"].append(timeit(lambda: ops.swiglu_bwd(torch.mm(dy, w), gu)))
-        for cfg in (0, 1):
+        for cfg in CFGS:
             r[f"fused{cfg}"].append(timeit(lambda: ops.dgrad_gemm(dy, w, gu, cfg)))
         r["flop"] = 2.0 * M * 2048 * 11008
     for name, (K, N) in shapes.items():
         dy, w = data[name]
         ref = torch.mm(dy.float(), w.float())
-        for cfg in (0, 1):
+        for cfg in CFGS:
             e = ((ops.dgrad_gemm(dy, w, None, cfg).float() - ref).norm() / ref.norm()).item()
             res[name][f"relerr{cfg}"] = e
     for name, r in res.items():
