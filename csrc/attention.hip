@@ -904,14 +904,15 @@ struct Stage {
 // DIAG (timing-only ablations, wrong results): bit0 no next-tile loads/stores, bit1 no softmax math,
 // bit2 no PV MFMAs, bit3 no QK MFMAs
 template <int NW, int DIAG = 0>
-__global__ __launch_bounds__(NW * 64) void fwd3_kernel(const u16* __restrict__ qkv, u16* __restrict__ out,
+__global__ __launch_bounds__(NW * 64, NW == 8 ? 4 : 2) void fwd3_kernel(const u16* __restrict__ qkv, u16* __restrict__ out,
                                                        float* __restrict__ lse, const int* __restrict__ cu, int nq,
                                                        int nkv, int total, float sl2, int causal) {
   constexpr int NT = NW * 64, BM = NW * 16, TB = 64 * ROWB;
   __shared__ __attribute__((aligned(16))) char smem[2 * TB];
   char* Ks = smem;
   char* Vs = smem + TB;
-  const int qb = blockIdx.x, h = blockIdx.y, b = blockIdx.z;
+  // grid (heads, sequences, q-blocks) with the last (causally heaviest) q-block dispatched first: LPT order
+  const int h = blockIdx.x, b = blockIdx.y, qb = gridDim.z - 1 - blockIdx.z;
   const int start = cu[b], len = cu[b + 1] - start;
   SFT_DASSERT(start >= 0 && len >= 0 && start + len <= total);
   const int q0 = qb * BM;
@@ -1192,7 +1193,8 @@ __global__ __launch_bounds__(NW * 64) void bwd_dq4_kernel(const u16* __restrict_
   __shared__ __attribute__((aligned(16))) char smem[2 * TB];
   char* Ks = smem;
   char* Ss = smem + TB;
-  const int qb = blockIdx.x, h = blockIdx.y, b = blockIdx.z;
+  // grid (heads, sequences, q-blocks) with the last (causally heaviest) q-block dispatched first: LPT order
+  const int h = blockIdx.x, b = blockIdx.y, qb = gridDim.z - 1 - blockIdx.z;
   const int start = cu[b], len = cu[b + 1] - start;
   const int q0 = qb * BM;
   if (q0 >= len) return;
@@ -1259,7 +1261,8 @@ __global__ __launch_bounds__(NW * 64) void bwd_dq3_kernel(const u16* __restrict_
   __shared__ __attribute__((aligned(16))) char smem[2 * TB];
   char* Ks = smem;
   char* Vs = smem + TB;
-  const int qb = blockIdx.x, h = blockIdx.y, b = blockIdx.z;
+  // grid (heads, sequences, q-blocks) with the last (causally heaviest) q-block dispatched first: LPT order
+  const int h = blockIdx.x, b = blockIdx.y, qb = gridDim.z - 1 - blockIdx.z;
   const int start = cu[b], len = cu[b + 1] - start;
   SFT_DASSERT(start >= 0 && len >= 0 && start + len <= total);
   const int q0 = qb * BM;
@@ -1366,7 +1369,8 @@ __global__ __launch_bounds__(256, 2) void bwd_dkdv3_kernel(const u16* __restrict
   char* Os = smem + TB;
   float* Ls = (float*)(smem + 2 * TB);
   float* Dl = Ls + 64;
-  const int kb = blockIdx.x, h = blockIdx.y, b = blockIdx.z;
+  // grid (heads, sequences, key blocks): key block 0 (causally heaviest: every query tile) dispatched first
+  const int h = blockIdx.x, b = blockIdx.y, kb = blockIdx.z;
   const int start = cu[b], len = cu[b + 1] - start;
   const int k0 = kb * 64;
   if (k0 >= len) return;
@@ -1580,7 +1584,7 @@ std::tuple<at::Tensor, at::Tensor> flash_fwd(const at::Tensor& qkv, const at::Te
   }
   if (attn_impl() == 3 && std::getenv("SFTAMD_ATTN_DIAG")) {  // timing-only ablations of fwd v3 (8 waves)
     const int diag = atoi(std::getenv("SFTAMD_ATTN_DIAG"));
-    dim3 g3((max_seqlen + 127) / 128, nq, nseq);
+    dim3 g3(nq, nseq, (max_seqlen + 127) / 128);
     auto gd = [&](auto dg) {
       attn::fwd3_kernel<8, decltype(dg)::value><<<g3, 512, 0, cur_stream()>>>(
           (const u16*)qkv.data_ptr(), (u16*)out.data_ptr(), lse.data_ptr<float>(), cu_c.data_ptr<int>(), nq, nkv, total,
@@ -1603,7 +1607,7 @@ std::tuple<at::Tensor, at::Tensor> flash_fwd(const at::Tensor& qkv, const at::Te
     attn_cfg(nw, nbuf);
     auto go3 = [&](auto w) {
       constexpr int NW = decltype(w)::value;
-      dim3 g3((max_seqlen + NW * 16 - 1) / (NW * 16), nq, nseq);
+      dim3 g3(nq, nseq, (max_seqlen + NW * 16 - 1) / (NW * 16));
       attn::fwd3_kernel<NW><<<g3, NW * 64, 0, cur_stream()>>>((const u16*)qkv.data_ptr(), (u16*)out.data_ptr(),
                                                              lse.data_ptr<float>(), cu_c.data_ptr<int>(), nq, nkv,
                                                              total, sl2, causal ? 1 : 0);
@@ -1733,7 +1737,7 @@ at::Tensor flash_bwd(const at::Tensor& dout, const at::Tensor& qkv, const at::Te
     auto dst = at::empty({ds_bytes / 2}, qkv.options());
     at::Tensor part;
     if (rep > 1) part = at::empty({(long)rep * total * 2 * nkv * hd}, qkv.options().dtype(at::kFloat));
-    dim3 gk3((max_seqlen + 63) / 64, nq, nseq);
+    dim3 gk3(nq, nseq, (max_seqlen + 63) / 64);
     attn::bwd_dkdv3_kernel<<<gk3, 256, 0, cur_stream()>>>(
         (const u16*)qkv.data_ptr(), (const u16*)dout.data_ptr(), lse.data_ptr<float>(), delta.data_ptr<float>(),
         cu_c.data_ptr<int>(), rep > 1 ? part.data_ptr<float>() : nullptr, (u16*)dqkv.data_ptr(), nq, nkv, total, sl2,
@@ -1746,7 +1750,7 @@ at::Tensor flash_bwd(const at::Tensor& dout, const at::Tensor& qkv, const at::Te
                                                                nq, nkv, rep, (float)scale);
       SFT_LAUNCH_CHECK();
     }
-    dim3 gq4((max_seqlen + 127) / 128, nq, nseq);
+    dim3 gq4(nq, nseq, (max_seqlen + 127) / 128);
     attn::bwd_dq4_kernel<8><<<gq4, 512, 0, cur_stream()>>>((const u16*)qkv.data_ptr(), (const u16*)dst.data_ptr(),
                                                            cu_c.data_ptr<int>(), (u16*)dqkv.data_ptr(), nq, nkv,
                                                            (int)lp, (float)scale, causal ? 1 : 0);
@@ -1757,14 +1761,14 @@ at::Tensor flash_bwd(const at::Tensor& dout, const at::Tensor& qkv, const at::Te
     constexpr int NW = decltype(w)::value;
     const int rep = nq / nkv;
     // dq first: on the side stream it starts filling the GPU while dK/dV is enqueued
-    dim3 gq3((max_seqlen + NW * 16 - 1) / (NW * 16), nq, nseq);
+    dim3 gq3(nq, nseq, (max_seqlen + NW * 16 - 1) / (NW * 16));
     attn::bwd_dq3_kernel<NW><<<gq3, NW * 64, 0, dq_stream>>>(
         (const u16*)qkv.data_ptr(), (const u16*)dout.data_ptr(), lse.data_ptr<float>(), delta.data_ptr<float>(),
         cu_c.data_ptr<int>(), (u16*)dqkv.data_ptr(), nq, nkv, total, sl2, (float)scale, causal ? 1 : 0);
     SFT_LAUNCH_CHECK();
     at::Tensor part;
     if (rep > 1) part = at::empty({(long)rep * total * 2 * nkv * hd}, qkv.options().dtype(at::kFloat));
-    dim3 gk3((max_seqlen + 63) / 64, nq, nseq);
+    dim3 gk3(nq, nseq, (max_seqlen + 63) / 64);
     attn::bwd_dkdv3_kernel<<<gk3, 256, 0, cur_stream()>>>(
         (const u16*)qkv.data_ptr(), (const u16*)dout.data_ptr(), lse.data_ptr<float>(), delta.data_ptr<float>(),
         cu_c.data_ptr<int>(), rep > 1 ? part.data_ptr<float>() : nullptr, (u16*)dqkv.data_ptr(), nq, nkv, total, sl2,

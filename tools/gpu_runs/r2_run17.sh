@@ -1,0 +1,11 @@
+#!/bin/bash
+# Round 2: full GPU suite on the current tree + default bench x2.
+cd $GRAFT_REPO_ROOT
+mkdir -p gpurun_out
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/r2_17_tests.log 2>&1 || { tail -40 gpurun_out/r2_17_tests.log; exit 1; }
+tail -1 gpurun_out/r2_17_tests.log
+for r in 1 2; do
+  timeout -k 10 300 python bench.py --steps 20 --warmup 5 > gpurun_out/r2_17_b$r.log 2>&1 || { tail -20 gpurun_out/r2_17_b$r.log; exit 1; }
+  grep -o '"value": [0-9.]*' gpurun_out/r2_17_b$r.log
+done
+python -c "import __graft_entry__ as g; g.smoke()" 2>&1 | tail -1
