@@ -135,7 +135,7 @@ __device__ __forceinline__ char* pick(int i, char* b0, char* b1, char* b2, char*
   }
 }
 
-template <class G>
+template <class G, bool SCHED>
 __device__ __forceinline__ void ring_loop(char* __restrict__ b0, char* __restrict__ b1, char* __restrict__ b2,
                                           char* __restrict__ b3, char* __restrict__ b4, int nsteps, Stager<G>& st,
                                           const int (&offA)[G::FM], int offB1, int offB2, f32x4 (&acc)[G::FM][G::FN]) {
@@ -169,9 +169,11 @@ __device__ __forceinline__ void ring_loop(char* __restrict__ b0, char* __restric
             acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[cb][j], acc[i][j], 0, 0, 0);
           fa[i] = lds_tr(nxt, offA[i]);
           if (i < PPW) st.piece(dst, i);
-          __builtin_amdgcn_sched_group_barrier(0x008, G::FN, 0);  // MFMA
-          __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);      // DS read (one fragment)
-          if (i < PPW) __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);  // VMEM (the DMA)
+          if (SCHED) {
+            __builtin_amdgcn_sched_group_barrier(0x008, G::FN, 0);  // MFMA
+            __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);      // DS read (one fragment)
+            if (i < PPW) __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);  // VMEM (the DMA)
+          }
         }
         st.advance();
         __builtin_amdgcn_s_setprio(0);
@@ -229,7 +231,7 @@ __device__ __forceinline__ void epilogue(char* smem, f32x4 (&acc)[G::FM][G::FN],
   }
 }
 
-template <int BM, int BN, int WM, int WN, int NS, int EPI, int OCC = 1>
+template <int BM, int BN, int WM, int WN, int NS, int EPI, int OCC = 1, bool SCHED = true>
 __global__ void __launch_bounds__(NT, OCC) dgrad_kernel(const u16* __restrict__ dY, const u16* __restrict__ W, int K,
                                                         long ldd, long ldw, int nbn, int nbm, int group, EpiArgs ea) {
   using G = Cfg<BM, BN, WM, WN, NS>;
@@ -272,10 +274,177 @@ __global__ void __launch_bounds__(NT, OCC) dgrad_kernel(const u16* __restrict__ 
   char* b[5];
 #pragma unroll
   for (int i = 0; i < 5; ++i) b[i] = smem + (i < NS ? i : 0) * G::STAGE;
-  ring_loop<G>(b[0], b[1], b[2], b[3], b[4], K / BK, st, offA, offB1, offB2, acc);
+  ring_loop<G, SCHED>(b[0], b[1], b[2], b[3], b[4], K / BK, st, offA, offB1, offB2, acc);
   __syncthreads();
   epilogue<G, EPI>(smem, acc, ea, n0, m0, wm, wn, w, lane);
 }
+
+// ============================================================================================
+// BK = 64 variant (cfg 7): a stage holds 64 k — A' images [64 k][128 n] (16 KB), B' rows of 128 B (whole
+// cache lines: the BK = 32 ring fetches every dY line in two halves) — in NS = 2 slots (128 KB). Each stage is
+// consumed in two 32-deep sub-steps (the pipeline of gemm_tn.hip ring2_loop): sub-step 0 computes k 0..31 from
+// registers while reading k 32..63 of the same slot; then one barrier (stage t+1 landed, slot t drained), and
+// sub-step 1 computes k 32..63 while reading stage t+1's k 0..31 and refilling slot t with stage t+2.
+// B' swizzle for 128-B rows: chunk ^ ((row >> 1) & 7).
+constexpr int BK2 = 64;
+constexpr int AIMG2 = BK2 * AROWB;  // [64 k][128 n] = 16 KB
+constexpr int BROWB2 = 128;
+__device__ __forceinline__ int swz_b2(int row, int ch) { return ch ^ ((row >> 1) & 7); }
+
+template <int BM, int BN, int WM, int WN>
+struct Cfg2 {
+  static constexpr int NS = 2;
+  static constexpr int TM = BM / WM, TN = BN / WN;
+  static constexpr int FM = TM / 16, FN = TN / 16;
+  static constexpr int IA = BM / 128;
+  static constexpr int STAGE_A = IA * AIMG2, STAGE = STAGE_A + BN * BROWB2;
+  static constexpr int PA = IA * 2;                 // A pieces per wave: 2 row groups (of 32 k) per image
+  static constexpr int PB = BN / 64;                // B pieces (8 rows x 128 B) per wave
+  static constexpr int PPW = PA + PB;
+  static constexpr int EPI_LD = TM + 4;
+  static constexpr int EPI = 8 * 16 * EPI_LD * 4;
+  static constexpr int LDS = (NS * STAGE > EPI) ? NS * STAGE : EPI;
+  static_assert(WM * WN == 8 && BM % 128 == 0 && BN % 64 == 0 && 2 * FM >= PPW, "config");
+  static_assert(LDS <= 160 * 1024, "LDS budget");
+};
+
+template <class G>
+struct Stager2 {
+  const u16* pa;
+  const u16* pb;
+  long lda, ldb;
+  int w, left;
+  __device__ __forceinline__ void init(const u16* W, const u16* dY, long ldw, long ldd, int n0, int m0, int wave,
+                                       int lane, int nsteps) {
+    w = wave;
+    lda = ldw;
+    ldb = ldd;
+    left = nsteps;
+    const int ra = 4 * wave + (lane >> 4);  // + 32 jj: the swizzle depends on row & 15 only through wave / lane
+    pa = W + (long)ra * ldw + n0 + 8 * swz_a(ra, lane & 15);
+    const int rb = 8 * wave + (lane >> 3);  // B piece w + 8 j: rows 8 (w + 8 j) + lane / 8
+    pb = dY + (long)(m0 + rb) * ldd + 8 * swz_b2(rb, lane & 7);
+  }
+  __device__ __forceinline__ void piece(char* buf, int j) {
+    if (j < G::PA) {  // image j >> 1, row group j & 1
+      glds16(pa + (long)(32 * (j & 1)) * lda + 128 * (j >> 1), buf + (j >> 1) * AIMG2 + (w + 8 * (j & 1)) * 1024);
+    } else {
+      const int jb = j - G::PA;
+      glds16(pb + (long)(64 * jb) * ldb, buf + G::STAGE_A + (w + 8 * jb) * 1024);
+    }
+  }
+  __device__ __forceinline__ void advance() {
+    if (--left > 0) {
+      pa += BK2 * lda;
+      pb += BK2;
+    }
+  }
+};
+
+template <class G>
+__device__ __forceinline__ void ring2_loop(char* __restrict__ b0, char* __restrict__ b1, int nsteps, Stager2<G>& st,
+                                           const int (&offA)[G::FM], int ob00, int ob01, int ob10, int ob11,
+                                           f32x4 (&acc)[G::FM][G::FN]) {
+  constexpr int PPW = G::PPW;
+  bf16x8 fa[G::FM], fb[2][G::FN];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+#pragma unroll
+    for (int j = 0; j < PPW; ++j) st.piece(i == 0 ? b0 : b1, j);
+    st.advance();
+  }
+  __builtin_amdgcn_s_waitcnt(waitcnt_imm(PPW, 0));
+  __builtin_amdgcn_s_barrier();
+#pragma unroll
+  for (int j = 0; j < G::FN; ++j) fb[0][j] = lds_b2(b0, ob00 + 2048 * j, ob01 + 2048 * j);
+#pragma unroll
+  for (int i = 0; i < G::FM; ++i) fa[i] = lds_tr(b0, offA[i]);
+  for (int t0 = 0; t0 < nsteps; t0 += 2) {
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      if (t0 + u < nsteps) {
+        char* cur = u == 0 ? b0 : b1;
+        char* nxt = u == 0 ? b1 : b0;
+        // sub-step 0: k 0..31 of stage t from registers; read k 32..63 of the same slot
+#pragma unroll
+        for (int j = 0; j < G::FN; ++j) fb[1][j] = lds_b2(cur, ob10 + 2048 * j, ob11 + 2048 * j);
+        __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+        for (int i = 0; i < G::FM; ++i) {
+#pragma unroll
+          for (int j = 0; j < G::FN; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[0][j], acc[i][j], 0, 0, 0);
+          fa[i] = lds_tr(cur, offA[i] + 32 * AROWB);
+        }
+        __builtin_amdgcn_s_setprio(0);
+        // stage t + 1 landed (this wave's DMAs) and every wave is done reading slot t
+        __builtin_amdgcn_s_waitcnt(waitcnt_imm(0, 0));
+        __builtin_amdgcn_s_barrier();
+#pragma unroll
+        for (int j = 0; j < G::FN; ++j) fb[0][j] = lds_b2(nxt, ob00 + 2048 * j, ob01 + 2048 * j);
+        __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+        for (int i = 0; i < G::FM; ++i) {
+#pragma unroll
+          for (int j = 0; j < G::FN; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[1][j], acc[i][j], 0, 0, 0);
+          fa[i] = lds_tr(nxt, offA[i]);
+          if (2 * i < PPW) st.piece(cur, 2 * i);          // refill slot t with stage t + 2
+          if (2 * i + 1 < PPW) st.piece(cur, 2 * i + 1);
+        }
+        st.advance();
+        __builtin_amdgcn_s_setprio(0);
+      }
+    }
+  }
+  __builtin_amdgcn_s_waitcnt(waitcnt_imm(0, 0));
+}
+
+template <int BM, int BN, int WM, int WN, int EPI>
+__global__ void __launch_bounds__(NT) dgrad2_kernel(const u16* __restrict__ dY, const u16* __restrict__ W, int K,
+                                                    long ldd, long ldw, int nbn, int nbm, int group, EpiArgs ea) {
+  using G = Cfg2<BM, BN, WM, WN>;
+  __shared__ __attribute__((aligned(16))) char smem[G::LDS];
+  const int nwg = gridDim.x, orig = blockIdx.x;
+  const int xcd = orig & 7, q8 = nwg >> 3, r8 = nwg & 7;
+  const int wgid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (orig >> 3);
+  const int per_group = group * nbm;
+  const int grp = wgid / per_group, first = grp * group;
+  const int gsz = min(nbn - first, group);
+  const int in = wgid - grp * per_group;
+  const int bn = first + in % gsz, bm = in / gsz;
+  const int n0 = bn * BM, m0 = bm * BN;
+
+  const int tid = threadIdx.x, lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = w / WN, wn = w - wm * WN;
+  Stager2<G> st;
+  st.init(W, dY, ldw, ldd, n0, m0, w, lane, K / BK2);
+  const int g = lane >> 4, ii = lane & 15, qq = ii >> 2, pp = ii & 3;
+  const int pg = ((g & 1) << 1) | (g >> 1);
+  const int r0 = 4 * pg + qq;
+  int offA[G::FM];
+#pragma unroll
+  for (int i = 0; i < G::FM; ++i) {
+    const int nl = wm * G::TM + 16 * i;
+    offA[i] = (nl >> 7) * AIMG2 + img_a(r0, 2 * ((nl & 127) >> 4) + (pp >> 1)) + 8 * (pp & 1);
+  }
+  // B fragment of sub-step s: bytes 64 s + 8 pg and 64 s + 32 + 8 pg of row wn*TN + 16 j + ii (swizzle of ii)
+  const int rowb = wn * G::TN + ii;
+  const int bbase = G::STAGE_A + rowb * BROWB2 + 8 * (pg & 1);
+  const int ob00 = bbase + 16 * swz_b2(ii, (pg >> 1)), ob01 = bbase + 16 * swz_b2(ii, 2 + (pg >> 1));
+  const int ob10 = bbase + 16 * swz_b2(ii, 4 + (pg >> 1)), ob11 = bbase + 16 * swz_b2(ii, 6 + (pg >> 1));
+  f32x4 acc[G::FM][G::FN];
+#pragma unroll
+  for (int i = 0; i < G::FM; ++i)
+#pragma unroll
+    for (int j = 0; j < G::FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  ring2_loop<G>(smem, smem + G::STAGE, K / BK2, st, offA, ob00, ob01, ob10, ob11, acc);
+  __syncthreads();
+  epilogue<Cfg<BM, BN, WM, WN, 2>, EPI>(smem, acc, ea, n0, m0, wm, wn, w, lane);
+}
+
+template <int BM, int BN, int WM, int WN, int EPI>
+void launch2(const at::Tensor& dy, const at::Tensor& w, const EpiArgs& ea);
 
 static int group_n() {
   static const int v = [] {
@@ -285,11 +454,21 @@ static int group_n() {
   return v;
 }
 
-template <int BM, int BN, int WM, int WN, int NS, int EPI, int OCC = 1>
+template <int BM, int BN, int WM, int WN, int NS, int EPI, int OCC = 1, bool SCHED = true>
 void launch(const at::Tensor& dy, const at::Tensor& w, const EpiArgs& ea) {
   const int M = dy.size(0), K = dy.size(1), N = w.size(1);
   const int nbn = N / BM, nbm = M / BN;
-  dgrad_kernel<BM, BN, WM, WN, NS, EPI, OCC><<<nbn * nbm, NT, 0, cur_stream()>>>(
+  dgrad_kernel<BM, BN, WM, WN, NS, EPI, OCC, SCHED><<<nbn * nbm, NT, 0, cur_stream()>>>(
+      (const u16*)dy.data_ptr(), (const u16*)w.data_ptr(), K, dy.stride(0), w.stride(0), nbn, nbm,
+      std::min(group_n(), nbn), ea);
+  SFT_LAUNCH_CHECK();
+}
+
+template <int BM, int BN, int WM, int WN, int EPI>
+void launch2(const at::Tensor& dy, const at::Tensor& w, const EpiArgs& ea) {
+  const int M = dy.size(0), K = dy.size(1), N = w.size(1);
+  const int nbn = N / BM, nbm = M / BN;
+  dgrad2_kernel<BM, BN, WM, WN, EPI><<<nbn * nbm, NT, 0, cur_stream()>>>(
       (const u16*)dy.data_ptr(), (const u16*)w.data_ptr(), K, dy.stride(0), w.stride(0), nbn, nbm,
       std::min(group_n(), nbn), ea);
   SFT_LAUNCH_CHECK();
@@ -310,8 +489,9 @@ at::Tensor dgrad_gemm(const at::Tensor& dy, const at::Tensor& w, const c10::opti
   SFT_CHECK(dy.stride(1) == 1 && w.stride(1) == 1, "dgrad_gemm: rows must be contiguous");
   const int64_t M = dy.size(0), K = dy.size(1), N = w.size(1);
   SFT_CHECK(w.size(0) == K, "dgrad_gemm: dy [M, K] . w [K, N]");
+  SFT_CHECK(cfg != 7 || K % 64 == 0, "dgrad_gemm cfg 7 (BK 64): K multiple of 64");
   SFT_CHECK(M % 128 == 0 && N % 256 == 0 && K % 32 == 0 && K >= 32, "dgrad_gemm: M multiple of 128 (256 for cfg 0/1), N of 256, K of 32");
-  SFT_CHECK(cfg >= 2 || M % 256 == 0, "dgrad_gemm: cfg 0/1 need M % 256 == 0");
+  SFT_CHECK(cfg == 2 || cfg == 3 || M % 256 == 0, "dgrad_gemm: 256 x 256 tiles need M % 256 == 0");
   SFT_CHECK(dy.stride(0) % 8 == 0 && w.stride(0) % 8 == 0 && (uintptr_t)dy.data_ptr() % 16 == 0 &&
                 (uintptr_t)w.data_ptr() % 16 == 0,
             "dgrad_gemm: 16-byte aligned rows");
@@ -339,10 +519,13 @@ at::Tensor dgrad_gemm(const at::Tensor& dy, const at::Tensor& w, const c10::opti
       case 1: dgrad::launch<256, 256, 2, 4, 3, E>(dy, w, ea); break;
       case 2: dgrad::launch<256, 128, 4, 2, 3, E>(dy, w, ea); break;
       case 3: dgrad::launch<256, 128, 4, 2, 4, E>(dy, w, ea); break;
+      case 5: dgrad::launch<256, 256, 2, 4, 3, E, 1, false>(dy, w, ea); break;  // no sched_group_barrier pinning
+      case 6: dgrad::launch<256, 256, 2, 4, 4, E, 1, false>(dy, w, ea); break;
+      case 7: dgrad::launch2<256, 256, 2, 4, E>(dy, w, ea); break;
       default: dgrad::launch<256, 256, 2, 4, 4, E>(dy, w, ea);
     }
   };
-  if (cfg >= 2) SFT_CHECK(M % 128 == 0, "dgrad_gemm: M multiple of 128");
+  if (cfg == 2 || cfg == 3) SFT_CHECK(M % 128 == 0, "dgrad_gemm: M multiple of 128");
   if (swiglu) run(std::integral_constant<int, dgrad::EPI_SWIGLU_BWD>());
   else run(std::integral_constant<int, dgrad::EPI_PLAIN>());
   return out;

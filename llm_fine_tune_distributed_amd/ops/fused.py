@@ -195,12 +195,18 @@ def _dgrad_ok(dy2d: torch.Tensor, w: torch.Tensor) -> bool:
             and w.data_ptr() % 16 == 0)
 
 
+def _dgrad_cfg(dy2d: torch.Tensor) -> int:
+    """Kernel configuration: 7 = 256 x 256 tiles, 64-deep K stages (two 32-deep MFMA sub-steps per barrier);
+    5 = the 32-deep three-stage ring for reductions that are not a multiple of 64 (profiles/r2_dgrad.md)."""
+    return 7 if dy2d.shape[1] % 64 == 0 else 5
+
+
 def dgrad_mm(dy2d: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
     """dX = dy @ W (W = the projection's [out, in] weight). The HIP kernel where it beats hipBLASLt
     (profiles/r2_dgrad.md, M = 8192: o_proj 0.063 vs 0.078 ms, qkv 0.088 vs 0.097 ms): reductions of at most
     4096 output features into at most 4096 inputs; gate_up (K = 22016) and lm_head stay on hipBLASLt."""
     if _dgrad_ok(dy2d, w) and (_DGRAD_MODE == "hip" or (dy2d.shape[1] <= 4096 and w.shape[1] <= 4096)):
-        return _ext.ops().dgrad_gemm(dy2d, w, None, 1)
+        return _ext.ops().dgrad_gemm(dy2d, w, None, _dgrad_cfg(dy2d))
     return torch.mm(dy2d, w)
 
 
@@ -226,7 +232,7 @@ class SwiGLULinearFn(Function):
         dgu = dw = None
         if ctx.needs_input_grad[0]:
             if _dgrad_ok(dy2d, w) and gu2d.is_contiguous():
-                dgu = _ext.ops().dgrad_gemm(dy2d, w, gu2d, 1)
+                dgu = _ext.ops().dgrad_gemm(dy2d, w, gu2d, _dgrad_cfg(dy2d))
             else:
                 dgu = _ext.ops().swiglu_bwd(torch.mm(dy2d, w), gu2d)
             dgu = dgu.view(gu.shape)

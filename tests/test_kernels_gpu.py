@@ -463,7 +463,7 @@ def test_dgrad_gemm_plain(M, K, N, wpad):
     dy = torch.randn(M, K, device="cuda", dtype=torch.bfloat16)
     wfull = torch.randn(K, N + wpad, device="cuda", dtype=torch.bfloat16)
     w = wfull[:, :N]
-    for cfg in (0, 1, 2, 3):
+    for cfg in (0, 1, 2, 3, 5, 7) if K % 64 == 0 else (0, 1, 2, 3, 5):
         out = _ext.ops().dgrad_gemm(dy, w, None, cfg)
         want = dy.float() @ w.float()
         assert out.shape == (M, N)
@@ -472,8 +472,9 @@ def test_dgrad_gemm_plain(M, K, N, wpad):
     eye = torch.zeros(K, N, device="cuda")
     eye[torch.arange(min(K, N)), (torch.arange(min(K, N)) + 5) % N] = 1.0
     ramp = (torch.arange(M * K, device="cuda") % 251).float().view(M, K).to(torch.bfloat16)
-    got = _ext.ops().dgrad_gemm(ramp, eye.to(torch.bfloat16), None, 0).float()
-    assert torch.equal(got, ramp.float() @ eye)
+    for cfg in (0, 7) if K % 64 == 0 else (0,):
+        got = _ext.ops().dgrad_gemm(ramp, eye.to(torch.bfloat16), None, cfg).float()
+        assert torch.equal(got, ramp.float() @ eye), cfg
 
 
 @pytest.mark.parametrize("M,K,N", [(256, 256, 256), (512, 2048, 512), (256, 64, 768)])
@@ -485,6 +486,7 @@ def test_dgrad_gemm_swiglu_bwd(M, K, N):
     gu = torch.randn(M, 2 * N, device="cuda", dtype=torch.bfloat16)
     dgu = _ext.ops().dgrad_gemm(dy, w, gu, 0)
     assert torch.equal(_ext.ops().dgrad_gemm(dy, w, gu, 2), dgu)  # 256 x 128 tiles: same fp32 sums per element
+    assert torch.equal(_ext.ops().dgrad_gemm(dy, w, gu, 7), dgu)  # BK 64: same k order within each 32-deep MFMA
     dact = dy.float() @ w.float()
     g, u = gu.float().chunk(2, dim=-1)
     s = torch.sigmoid(g)
