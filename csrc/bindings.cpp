@@ -31,7 +31,7 @@ TORCH_LIBRARY(sftamd, m) {
   m.def("dgrad_gemm(Tensor dy, Tensor w, Tensor? gate_up=None, int cfg=0) -> Tensor");
   // forward-layout GEMM C = a w^T with fused epilogues (csrc/gemm_tn.hip)
   m.def("gemm_tn(Tensor a, Tensor w, int cfg=0) -> Tensor");
-  m.def("gemm_tn_swiglu(Tensor x, Tensor w_gate_up) -> (Tensor, Tensor)");
+  m.def("gemm_tn_swiglu(Tensor x, Tensor w_gate_up, int cfg=5) -> (Tensor, Tensor)");
   m.def("gemm_tn_rope(Tensor x, Tensor w, Tensor cos, Tensor sin, int rope_cols, int cfg=0) -> Tensor");
   // optimizer
   m.def("sumsq(Tensor x) -> Tensor");

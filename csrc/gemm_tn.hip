@@ -691,6 +691,259 @@ __global__ void __launch_bounds__(WM * WN * 64) tn2_kernel(const u16* __restrict
     epilogue<G, EPI>(smem, acc, ea, m0, n0, wm, wn, w, lane);
 }
 
+// ============================================================================================
+// Ping-pong 8-phase schedule (cfg 8 / 9), cdna_hip_programming.md §5 "The 256² 8-phase template".
+// Same tile (256 x 256, BK = 64, 8 waves of 128 x 64) and the same two 64 KB LDS stages as the BK = 64
+// ring above, but each K-tile runs as FOUR phases, one output quadrant (64 x 32 per wave, 16 MFMAs)
+// each, and the two wave rows run ONE BARRIER APART: while wave row 0 is in a phase's MFMA segment,
+// wave row 1 (its partner on the same SIMD) issues the next phase's LDS reads and DMA, and vice versa
+// — matrix beside memory on every SIMD (MI355X_MICROARCH.md §Two waves per SIMD). Every phase is
+//   [L: ds_reads of this phase's fragments | DMA of one class of tile t + 2 | counted vmcnt]
+//   lgkmcnt(0); s_barrier; setprio 1; 16 MFMA; setprio 0; s_barrier
+// The stage is laid out in four 16 KB CLASS images, one per group of fragments read together:
+//   A_lo: tile rows {0..63, 128..191} (fragments i = 0..3 of both wave rows), A_hi: rows +64 (i = 4..7),
+//   B_lo: tile columns 64 q + {0..31} (j = 0, 1 of every wave column), B_hi: columns +32 (j = 2, 3),
+// so each class is released right after the phase that reads it and refilled with tile t + 2 at once:
+//   ph1 reads A_lo + B_lo -> quadrant (A_lo, B_lo);  ph2 reads B_hi, DMA A_lo + B_lo -> (A_lo, B_hi)
+//   ph3 reads A_hi, DMA B_hi -> (A_hi, B_hi);        ph4 DMA A_hi                   -> (A_hi, B_lo)
+// A DMA therefore has ~6-7 phases to land. The class images are separate __restrict__ pointers, so the
+// compiler's waitcnt pass does not drain the DMA of one class before reading another. Each wave issues
+// 2 DMAs per class in a fixed order, so the vmcnt that retires a class is a compile-time count:
+//   ph1 waits for B_hi(t) (10 younger DMAs), ph2 for A_hi(t) (8), ph4 for A_lo/B_lo(t + 1) (10),
+// always one barrier pair before the read (LDS-DMA data is ordered for other waves only by the
+// issuer's vmcnt followed by a barrier the reader has passed); lgkmcnt(0) BEFORE each phase's first
+// barrier retires the phase's reads, which is what lets the next phase refill that class.
+// ============================================================================================
+constexpr int CLS = 16 * 1024;  // class image: 128 rows x 128 B
+__device__ __forceinline__ void wait_vm(int n) {
+  switch (n) {  // immediates must be literal; n is wave-uniform and even
+    case 0: __builtin_amdgcn_s_waitcnt(waitcnt_imm(0, 15)); break;
+    case 2: __builtin_amdgcn_s_waitcnt(waitcnt_imm(2, 15)); break;
+    case 4: __builtin_amdgcn_s_waitcnt(waitcnt_imm(4, 15)); break;
+    case 6: __builtin_amdgcn_s_waitcnt(waitcnt_imm(6, 15)); break;
+    case 8: __builtin_amdgcn_s_waitcnt(waitcnt_imm(8, 15)); break;
+    case 10: __builtin_amdgcn_s_waitcnt(waitcnt_imm(10, 15)); break;
+    case 12: __builtin_amdgcn_s_waitcnt(waitcnt_imm(12, 15)); break;
+    default: __builtin_amdgcn_s_waitcnt(waitcnt_imm(0, 15)); break;
+  }
+}
+__device__ __forceinline__ void bar() {
+  __builtin_amdgcn_sched_barrier(0);
+  __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_sched_barrier(0);
+}
+__device__ __forceinline__ void lgkm0() { __builtin_amdgcn_s_waitcnt(waitcnt_imm(63, 0)); }
+
+struct Stager3 {
+  const u16* pa;  // this lane's source in the wave's first A_lo piece (tile row 8 w + lr)
+  const u16* pb;  // ... first B_lo piece
+  long a64, a128, a192, b1, b2, b3;  // element offsets of the wave's other pieces
+  // the wave's two 8-row pieces of class C (0 A_lo, 1 A_hi, 2 B_lo, 3 B_hi) into class image ``img``;
+  // KOFF = K-tile offset from the stager's current tile
+  template <int C, int KOFF = 0>
+  __device__ __forceinline__ void cls(char* img, int w) {
+    const u16* a = pa + KOFF * BK2;
+    const u16* b = pb + KOFF * BK2;
+    const u16* s0 = C == 0 ? a : (C == 1 ? a + a64 : (C == 2 ? b : b + b2));
+    const u16* s1 = C == 0 ? a + a128 : (C == 1 ? a + a192 : (C == 2 ? b + b1 : b + b3));
+    glds16(s0, img + w * 1024);
+    glds16(s1, img + (8 + w) * 1024);
+  }
+  __device__ __forceinline__ void advance() {
+    pa += BK2;
+    pb += BK2;
+  }
+};
+
+template <bool TRC, int I0, int J0>
+__device__ __forceinline__ void pp_mma(f32x4 (&acc)[8][4], const bf16x8 (&fa)[4][2], const bf16x8 (&fb)[2][2]) {
+  __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+  for (int s = 0; s < 2; ++s)
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+        acc[I0 + i][J0 + j] = TRC ? __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[j][s], fa[i][s], acc[I0 + i][J0 + j], 0, 0, 0)
+                                  : __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i][s], fb[j][s], acc[I0 + i][J0 + j], 0, 0, 0);
+  __builtin_amdgcn_s_setprio(0);
+}
+
+// fragment reads: offA / offB = this lane's (row, k-chunk g) byte offset in a class image; +2048 per
+// 16-row fragment, k-sub-step 1 = chunk 4 + g (offX1)
+__device__ __forceinline__ void pp_read_a(const char* img, int offA0, int offA1, bf16x8 (&fa)[4][2]) {
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    fa[i][0] = lds_row(img, offA0 + 2048 * i);
+    fa[i][1] = lds_row(img, offA1 + 2048 * i);
+  }
+}
+__device__ __forceinline__ void pp_read_b(const char* img, int offB0, int offB1, bf16x8 (&fb)[2][2]) {
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    fb[j][0] = lds_row(img, offB0 + 2048 * j);
+    fb[j][1] = lds_row(img, offB1 + 2048 * j);
+  }
+}
+
+// End of a phase's load segment, then its MFMA segment. D = 1: lgkmcnt(0) before the first barrier
+// (a class may be refilled ONE phase after it is read); D = 2: lgkmcnt(0) after it (refilled two
+// phases after: cdna_hip_programming.md §5, "Read a staged buffer ... WAR").
+template <int D, bool TRC, int I0, int J0>
+__device__ __forceinline__ void pp_phase(f32x4 (&acc)[8][4], const bf16x8 (&fa)[4][2], const bf16x8 (&fb)[2][2]) {
+  if (D == 1) lgkm0();
+  bar();
+  if (D == 2) lgkm0();  // also retires phase 4's read of the NEXT tile's B_lo, used only by its phase 1
+  pp_mma<TRC, I0, J0>(acc, fa, fb);
+  bar();
+}
+
+// One K-tile t on stage X (class images xAl, xAh, xBl, xBh); Y = the other stage (tile t + 1).
+// Reads: A_lo(t) in phase 1, B_hi(t) in 2, A_hi(t) in 3, B_lo(t + 1) in 4 (into the other B_lo register
+// set), 8 / 4 / 8 / 4 ds_read_b128 per phase. Each wait retires the class read in the NEXT phase.
+// D = 1 DMA slots: ph1 B_lo(t+2), ph2 A_lo(t+2), ph3 B_hi(t+2), ph4 A_hi(t+2) -> X.
+// D = 2 DMA slots: ph1 A_hi(t+1) -> Y, ph2 B_lo(t+2), ph3 A_lo(t+2), ph4 B_hi(t+2) -> X.
+// e1 = tile t+1 exists (so tile t-1 issued its slots for t+1), e0 = tile t+2 exists; a wait's count
+// is 2 x the number of this wave's DMA slots issued after the awaited one.
+template <bool TRC, int D>
+__device__ __forceinline__ void pp_tile(char* __restrict__ xAl, char* __restrict__ xAh, char* __restrict__ xBl,
+                                        char* __restrict__ xBh, char* __restrict__ yAh, const char* __restrict__ yBl,
+                                        int t, int nk, Stager3& st, int w, int offA0, int offA1, int offB0,
+                                        int offB1, f32x4 (&acc)[8][4], bf16x8 (&blc)[2][2], bf16x8 (&bln)[2][2]) {
+  const int e1 = t + 1 < nk, e0 = t + 2 < nk;
+  bf16x8 fa[4][2], fbh[2][2];
+  // phase 1: retire B_hi(t); read A_lo(t)
+  wait_vm(D == 1 ? 2 + 8 * e1 : 2 + 6 * e1);
+  pp_read_a(xAl, offA0, offA1, fa);
+  if (D == 1) {
+    if (e0) st.cls<2>(xBl, w);
+  } else {
+    if (e1) st.cls<1, -1>(yAh, w);
+  }
+  pp_phase<D, TRC, 0, 0>(acc, fa, blc);
+  // phase 2: retire A_hi(t); read B_hi(t)
+  wait_vm(D == 1 ? 8 * e1 + 2 * e0 : 8 * e1);
+  pp_read_b(xBh, offB0, offB1, fbh);
+  if (e0) {
+    if (D == 1) st.cls<0>(xAl, w);
+    else st.cls<2>(xBl, w);
+  }
+  pp_phase<D, TRC, 0, 2>(acc, fa, fbh);
+  // phase 3: retire B_lo(t+1); read A_hi(t)
+  if (e1) wait_vm(D == 1 ? 6 + 4 * e0 : 6 + 2 * e0);
+  pp_read_a(xAh, offA0, offA1, fa);
+  if (e0) {
+    if (D == 1) st.cls<3>(xBh, w);
+    else st.cls<0>(xAl, w);
+  }
+  pp_phase<D, TRC, 4, 2>(acc, fa, fbh);
+  // phase 4: retire A_lo(t+1); read B_lo(t+1)
+  if (e1) {
+    wait_vm(D == 1 ? 4 + 6 * e0 : 4 + 4 * e0);
+    pp_read_b(yBl, offB0, offB1, bln);
+  }
+  if (e0) {
+    if (D == 1) st.cls<1>(xAh, w);
+    else st.cls<3>(xBh, w);
+    st.advance();
+  }
+  pp_phase<D, TRC, 4, 0>(acc, fa, blc);
+}
+
+template <int EPI, bool TRC, int D>
+__global__ void __launch_bounds__(512) tn3_kernel(const u16* __restrict__ A, const u16* __restrict__ B, int K, long lda,
+                                                  long ldb, int nbm, int nbn, int group, EpiArgs ea) {
+  using G = Cfg2<256, 256, 2, 4, 2>;
+  __shared__ __attribute__((aligned(16))) char smem[G::LDS];
+  const int nwg = gridDim.x, orig = blockIdx.x;
+  const int xcd = orig & 7, q8 = nwg >> 3, r8 = nwg & 7;
+  const int wgid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (orig >> 3);
+  const int per_group = group * nbn;
+  const int grp = wgid / per_group, first = grp * group;
+  const int gsz = min(nbm - first, group);
+  const int in = wgid - grp * per_group;
+  const int bm = first + in % gsz, bn = in / gsz;
+  const int m0 = bm * 256, n0 = bn * 256;
+  const int tid = threadIdx.x, lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = w >> 2, wn = w & 3;
+  const int nk = K / BK2;
+
+  Stager3 st;
+  {
+    // class piece c (8 image rows 8c + lr) of wave w: c = w and c = w + 8 -> (row >> 1) & 7 = 4 (w & 1) + (lr >> 1)
+    const int lr = lane >> 3, ch = (lane & 7) ^ (4 * (w & 1) + (lr >> 1));
+    st.pa = A + (long)(m0 + 8 * w + lr) * lda + 8 * ch;
+    st.a64 = 64 * lda;
+    st.a128 = 128 * lda;
+    st.a192 = 192 * lda;
+    // B_lo piece c covers tile columns 64 (c >> 2) + 8 (c & 3) + lr = 8-column piece P = 8 (c >> 2) + (c & 3);
+    // B_hi adds 32 columns (4 pieces); the EPI permutation maps pieces to weight rows (b2_row)
+    const int P0 = 8 * (w >> 2) + (w & 3);
+    const int r0 = b2_row<EPI>(P0, n0, ea.I);
+    st.pb = B + (long)(r0 + lr) * ldb + 8 * ch;
+    st.b1 = (long)(b2_row<EPI>(P0 + 16, n0, ea.I) - r0) * ldb;
+    st.b2 = (long)(b2_row<EPI>(P0 + 4, n0, ea.I) - r0) * ldb;
+    st.b3 = (long)(b2_row<EPI>(P0 + 20, n0, ea.I) - r0) * ldb;
+  }
+  const int g = lane >> 4, ii = lane & 15;
+  const int ra = wm * 64 + ii, rb = wn * 32 + ii;  // class-image rows of this lane's first A / B fragment
+  const int offA0 = ra * ROWB2 + 16 * swz2(ra, g), offA1 = ra * ROWB2 + 16 * swz2(ra, 4 + g);
+  const int offB0 = rb * ROWB2 + 16 * swz2(rb, g), offB1 = rb * ROWB2 + 16 * swz2(rb, 4 + g);
+  f32x4 acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  char* x0 = smem;
+  char* y0 = smem + 4 * CLS;
+  // prologue: the DMA slots tiles -2 and -1 would have issued (class order B_lo, A_lo, B_hi, A_hi; with
+  // D = 2, A_hi(1) is left to phase 1 of tile 0), then B_lo(0) into the first B_lo register set
+  st.cls<2>(x0 + 2 * CLS, w);
+  st.cls<0>(x0, w);
+  st.cls<3>(x0 + 3 * CLS, w);
+  st.cls<1>(x0 + CLS, w);
+  st.advance();
+  if (nk > 1) {
+    st.cls<2>(y0 + 2 * CLS, w);
+    st.cls<0>(y0, w);
+    st.cls<3>(y0 + 3 * CLS, w);
+    if (D == 1) st.cls<1>(y0 + CLS, w);
+  }
+  st.advance();
+  wait_vm(nk > 1 ? (D == 1 ? 12 : 10) : 4);  // B_lo(0), A_lo(0)
+  bar();
+  bf16x8 bl0[2][2], bl1[2][2];
+  pp_read_b(x0 + 2 * CLS, offB0, offB1, bl0);
+  lgkm0();
+  if (D == 1) bar();   // phase 1 of tile 0 refills B_lo (D = 1): every wave's read of B_lo(0) retired first
+  if (wm == 1) bar();  // wave row 1 runs one barrier behind wave row 0
+  for (int t = 0; t < nk; t += 2) {
+    pp_tile<TRC, D>(x0, x0 + CLS, x0 + 2 * CLS, x0 + 3 * CLS, y0 + CLS, y0 + 2 * CLS, t, nk, st, w, offA0, offA1,
+                    offB0, offB1, acc, bl0, bl1);
+    if (t + 1 < nk)
+      pp_tile<TRC, D>(y0, y0 + CLS, y0 + 2 * CLS, y0 + 3 * CLS, x0 + CLS, x0 + 2 * CLS, t + 1, nk, st, w, offA0,
+                      offA1, offB0, offB1, acc, bl1, bl0);
+  }
+  if (wm == 0) bar();
+  __builtin_amdgcn_s_waitcnt(waitcnt_imm(0, 0));
+  __syncthreads();
+  if constexpr (TRC)
+    epilogue_t<G, EPI>(smem, acc, ea, m0, n0, wm, wn, w, lane);
+  else
+    epilogue<G, EPI>(smem, acc, ea, m0, n0, wm, wn, w, lane);
+}
+
+template <int EPI, bool TRC, int D = 1>
+void launch3(const at::Tensor& a, const at::Tensor& w, int N, const EpiArgs& ea) {
+  const int M = a.size(0), K = a.size(1);
+  const int nbm = M / 256, nbn = N / 256;
+  tn3_kernel<EPI, TRC, D><<<nbm * nbn, 512, 0, cur_stream()>>>((const u16*)a.data_ptr(), (const u16*)w.data_ptr(), K,
+                                                            a.stride(0), w.stride(0), nbm, nbn,
+                                                            std::min(group_m(), nbm), ea);
+  SFT_LAUNCH_CHECK();
+}
+
 template <int BM, int BN, int WM, int WN, int NS, int EPI, int VAR = 0>
 void launch2(const at::Tensor& a, const at::Tensor& w, int N, const EpiArgs& ea) {
   const int M = a.size(0), K = a.size(1);
@@ -746,6 +999,12 @@ at::Tensor gemm_tn(const at::Tensor& a, const at::Tensor& w, int64_t cfg) {
     SFT_CHECK(N % 128 == 0 && a.size(1) % 64 == 0, "gemm_tn BK64 256x128: N % 128, K % 64");
     if (cfg == 6) tn::launch2<256, 128, 4, 2, 3, tn::EPI_PLAIN>(a, w, N, ea);
     else tn::launch2<256, 128, 4, 2, 2, tn::EPI_PLAIN>(a, w, N, ea);
+  } else if (cfg >= 8 && cfg <= 11) {  // ping-pong 8-phase schedule (9, 11: transposed-C epilogue; 10, 11: D = 2)
+    SFT_CHECK(N % 256 == 0 && a.size(1) % 64 == 0, "gemm_tn ping-pong: N % 256, K % 64");
+    if (cfg == 8) tn::launch3<tn::EPI_PLAIN, false, 1>(a, w, N, ea);
+    else if (cfg == 9) tn::launch3<tn::EPI_PLAIN, true, 1>(a, w, N, ea);
+    else if (cfg == 10) tn::launch3<tn::EPI_PLAIN, false, 2>(a, w, N, ea);
+    else tn::launch3<tn::EPI_PLAIN, true, 2>(a, w, N, ea);
   } else if (cfg == 4) {  // BK64 with sched_group_barrier interleave pinned (measured slower: diagnostics)
     SFT_CHECK(N % 256 == 0 && a.size(1) % 64 == 0, "gemm_tn BK64: N % 256, K % 64");
     tn::launch2<256, 256, 2, 4, 2, tn::EPI_PLAIN, 2>(a, w, N, ea);
@@ -757,7 +1016,7 @@ at::Tensor gemm_tn(const at::Tensor& a, const at::Tensor& w, int64_t cfg) {
 }
 
 // x [M, K], w_gu [2I, K] = [gate; up]  ->  (gu [M, 2I], act [M, I] = silu(gate) * up)
-std::tuple<at::Tensor, at::Tensor> gemm_tn_swiglu(const at::Tensor& x, const at::Tensor& w_gu) {
+std::tuple<at::Tensor, at::Tensor> gemm_tn_swiglu(const at::Tensor& x, const at::Tensor& w_gu, int64_t cfg) {
   check_tn(x, w_gu);
   const int M = x.size(0), N = w_gu.size(0), I = N / 2;
   SFT_CHECK(N % 2 == 0 && I % 128 == 0, "gemm_tn_swiglu: intermediate size % 128");
@@ -768,7 +1027,8 @@ std::tuple<at::Tensor, at::Tensor> gemm_tn_swiglu(const at::Tensor& x, const at:
     const char* e = std::getenv("SFTAMD_TN_TRC");
     return !(e && e[0] == '0');
   }();
-  if (x.size(1) % 64 == 0 && trc) tn::launch2<256, 256, 2, 4, 2, tn::EPI_SWIGLU, 3>(x, w_gu, N, ea);
+  if (x.size(1) % 64 == 0 && N % 256 == 0 && cfg == 11) tn::launch3<tn::EPI_SWIGLU, true, 2>(x, w_gu, N, ea);
+  else if (x.size(1) % 64 == 0 && trc) tn::launch2<256, 256, 2, 4, 2, tn::EPI_SWIGLU, 3>(x, w_gu, N, ea);
   else if (x.size(1) % 64 == 0) tn::launch2<256, 256, 2, 4, 2, tn::EPI_SWIGLU>(x, w_gu, N, ea);
   else tn::launch<256, 256, 2, 4, 5, tn::EPI_SWIGLU>(x, w_gu, N, ea);
   return {gu, act};
@@ -792,6 +1052,7 @@ at::Tensor gemm_tn_rope(const at::Tensor& x, const at::Tensor& w, const at::Tens
   else if (cfg == 5 && x.size(1) % 64 == 0) tn::launch2<256, 256, 2, 4, 2, tn::EPI_ROPE, 3>(x, w, N, ea);
   else if (cfg == 6 && x.size(1) % 64 == 0) tn::launch2<256, 128, 4, 2, 3, tn::EPI_ROPE>(x, w, N, ea);
   else if (cfg == 7 && x.size(1) % 64 == 0) tn::launch2<256, 128, 4, 2, 2, tn::EPI_ROPE>(x, w, N, ea);
+  else if (cfg == 11 && x.size(1) % 64 == 0) tn::launch3<tn::EPI_ROPE, true, 2>(x, w, N, ea);
   else tn::launch<256, 256, 2, 4, 5, tn::EPI_ROPE>(x, w, N, ea);
   return c;
 }

@@ -85,13 +85,10 @@ class MLP(nn.Module):
 
     def forward(self, h):
         L = self.lora
-        if L is None and ops.fuse_swiglu_down():  # SwiGLU backward fused into the down projection's dgrad GEMM
-            return ops.swiglu_linear(ops.linear(h, self.gate_up_proj), self.down_proj)
-        if L is None:
-            a = ops.linear_swiglu(h, self.gate_up_proj)  # GEMM + SwiGLU epilogue where the shapes allow
-        else:
-            a = ops.swiglu(ops.lora_linear(h, self.gate_up_proj, L["gate_up"]))
-        return ops.linear(a, self.down_proj) if L is None else ops.lora_linear(a, self.down_proj, L["down"])
+        if L is None:  # SwiGLU fused into the GEMM epilogues where the kernels apply (ops.swiglu_mlp)
+            return ops.swiglu_mlp(h, self.gate_up_proj, self.down_proj)
+        a = ops.swiglu(ops.lora_linear(h, self.gate_up_proj, L["gate_up"]))
+        return ops.lora_linear(a, self.down_proj, L["down"])
 
 
 class DecoderLayer(nn.Module):

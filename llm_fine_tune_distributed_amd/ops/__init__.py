@@ -19,11 +19,12 @@ from .fused import (
     rope_,
     swiglu,
     swiglu_linear,
+    swiglu_mlp,
 )
 from .optim_kernels import adamw_flat_, grad_norm_flat, sumsq_list
 
 __all__ = [
     "reference", "load_extension", "use_hip", "hip_disabled", "IGNORE_INDEX", "add_rms_norm", "decode_attention", "dropout_add",
     "embedding", "flash_attention", "linear", "linear_rope", "linear_swiglu", "lora_linear", "lm_head_cross_entropy", "rms_norm", "rope_", "swiglu",
-    "swiglu_linear", "dgrad_mm", "fuse_swiglu_down", "adamw_flat_", "grad_norm_flat", "sumsq_list",
+    "swiglu_linear", "swiglu_mlp", "dgrad_mm", "fuse_swiglu_down", "adamw_flat_", "grad_norm_flat", "sumsq_list",
 ]

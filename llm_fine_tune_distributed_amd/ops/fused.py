@@ -405,10 +405,16 @@ _TN_PLAIN = os.environ.get("SFTAMD_TN_PLAIN", "0") == "1"
 _TN_SMALL_TILES = os.environ.get("SFTAMD_TN_SMALL_TILES", "0")
 
 
+_TN_PINGPONG = os.environ.get("SFTAMD_TN_PINGPONG", "1") == "1"
+
+
 def _tn_cfg(M: int, N: int) -> int:
-    """BK64 tile for a forward GEMM: 256x256 (cfg 2) when its grid fills whole waves of the 256 CUs,
-    else 256x128 with 3 LDS stages (cfg 6): qkv [8192 x 3072] is 384 big tiles = 1.5 waves but 768 small
-    ones = 3 (0.095 vs 0.102 ms; o_proj's 256 tiles stay on 256x256: 0.058 vs 0.065 ms, r1_gemm_tn.md)."""
+    """Forward GEMM configuration. Default: the ping-pong 8-phase schedule (cfg 11, csrc/gemm_tn.hip: the two
+    wave rows one barrier apart, transposed-C epilogue) wherever N % 256 == 0 — 2-6 % faster than the BK64 ring
+    (cfg 2) on every SmolLM3 shape (profiles/r2_gemm_pingpong.md). SFTAMD_TN_SMALL_TILES=1: 256x128 tiles
+    (cfg 6) when the 256x256 grid does not fill whole waves of the 256 CUs."""
+    if _TN_PINGPONG and N % 256 == 0:
+        return 11
     if _TN_SMALL_TILES == "0":
         return 2
     tiles = (M // 256) * (N // 256)
@@ -429,7 +435,7 @@ class GateUpSwiGLUFn(Function):
     @staticmethod
     def forward(ctx, x, weight):
         x2d = x.reshape(-1, x.shape[-1])
-        gu, act = _ext.ops().gemm_tn_swiglu(x2d, weight)
+        gu, act = _ext.ops().gemm_tn_swiglu(x2d, weight, _tn_swiglu_cfg(weight))
         ctx.save_for_backward(x2d, gu)
         ctx.weight = weight
         ctx.x_shape = x.shape
@@ -448,12 +454,87 @@ class GateUpSwiGLUFn(Function):
         return dx, dw
 
 
+def _tn_swiglu_cfg(weight: torch.Tensor) -> int:
+    return 11 if _TN_PINGPONG and weight.shape[0] % 256 == 0 else 5
+
+
 def linear_swiglu(x: torch.Tensor, weight: torch.Tensor) -> torch.Tensor:
     """SwiGLU MLP input projection: swiglu(linear(x, [Wg; Wu]))."""
     x2d = x.reshape(-1, x.shape[-1])
     if _TN_MODE in ("1", "swiglu") and _tn_ok(x2d, weight) and (weight.shape[0] // 2) % 128 == 0:
         return GateUpSwiGLUFn.apply(x, weight)
     return swiglu(linear(x, weight))
+
+
+class GateUpActFn(Function):
+    """(gu, act) = (x [Wg; Wu]^T, silu(gate) * up) from ONE HIP GEMM with the SwiGLU epilogue; act is
+    non-differentiable here because the consumer (SwiGLUDownFn) returns the gradient of gu directly."""
+
+    @staticmethod
+    def forward(ctx, x, weight):
+        x2d = x.reshape(-1, x.shape[-1])
+        gu, act = _ext.ops().gemm_tn_swiglu(x2d, weight, _tn_swiglu_cfg(weight))
+        ctx.save_for_backward(x2d)
+        ctx.weight = weight
+        ctx.x_shape = x.shape
+        ctx.mark_non_differentiable(act)
+        return gu.view(*x.shape[:-1], gu.shape[-1]), act.view(*x.shape[:-1], act.shape[-1])
+
+    @staticmethod
+    def backward(ctx, dgu, _dact):
+        (x2d,) = ctx.saved_tensors
+        w = ctx.weight
+        dgu2d = dgu.reshape(-1, dgu.shape[-1])
+        dx = dw = None
+        if ctx.needs_input_grad[0]:
+            dx = dgrad_mm(dgu2d, w).view(ctx.x_shape)
+        if ctx.needs_input_grad[1]:
+            dw = _accumulate_weight_grad(w, dgu2d, x2d)
+        return dx, dw
+
+
+class SwiGLUDownFn(Function):
+    """y = act @ W^T for an act produced together with gu (GateUpActFn); backward = the fused
+    dgu = swiglu_bwd(dy @ W, gu) GEMM of SwiGLULinearFn — neither SwiGLU pass runs as a separate kernel."""
+
+    @staticmethod
+    def forward(ctx, gu, act, weight):
+        ctx.save_for_backward(gu, act)
+        ctx.weight = weight
+        a2d = act.reshape(-1, act.shape[-1])
+        return torch.nn.functional.linear(a2d, weight).view(*gu.shape[:-1], weight.shape[0])
+
+    @staticmethod
+    def backward(ctx, dy):
+        gu, act = ctx.saved_tensors
+        w = ctx.weight
+        dy2d = dy.reshape(-1, dy.shape[-1]).contiguous()
+        gu2d = gu.reshape(-1, gu.shape[-1])
+        dgu = dw = None
+        if ctx.needs_input_grad[0]:
+            if _dgrad_ok(dy2d, w):
+                dgu = _ext.ops().dgrad_gemm(dy2d, w, gu2d, _dgrad_cfg(dy2d))
+            else:
+                dgu = _ext.ops().swiglu_bwd(torch.mm(dy2d, w), gu2d)
+            dgu = dgu.view(gu.shape)
+        if ctx.needs_input_grad[2]:
+            dw = _accumulate_weight_grad(w, dy2d, act.reshape(-1, act.shape[-1]))
+        return dgu, None, dw
+
+
+def swiglu_mlp(h: torch.Tensor, w_gate_up: torch.Tensor, w_down: torch.Tensor) -> torch.Tensor:
+    """down(swiglu(gate_up(h))) — the SwiGLU MLP without LoRA, on the fastest available fusion:
+    SFTAMD_TN=1 / swiglu: gate_up GEMM with the SwiGLU epilogue + down GEMM with the SwiGLU backward in its dgrad
+    (no separate SwiGLU kernel in either direction); default: hipBLASLt gate_up + SwiGLU kernel + the fused down
+    dgrad (SFTAMD_SWIGLU_DOWN=1); otherwise the unfused chain."""
+    h2d = h.reshape(-1, h.shape[-1])
+    if (_TN_MODE in ("1", "swiglu") and _SWIGLU_DOWN and _tn_ok(h2d, w_gate_up) and w_gate_up.shape[0] % 256 == 0
+            and (w_gate_up.shape[0] // 2) % 128 == 0):
+        gu, act = GateUpActFn.apply(h, w_gate_up)
+        return SwiGLUDownFn.apply(gu, act, w_down)
+    if fuse_swiglu_down():
+        return swiglu_linear(linear(h, w_gate_up), w_down)
+    return linear(linear_swiglu(h, w_gate_up), w_down)
 
 
 class QKVRopeFn(Function):

@@ -405,8 +405,9 @@ def test_lora_fwd_bwd_kernels(K, R, p):
     assert (dx.float() - dxr.float()).abs().max().item() < 3e-2
 
 
-@pytest.mark.parametrize("cfg", [0, 1, 2, 3, 5, 6, 7])
-@pytest.mark.parametrize("M,N,K", [(256, 256, 64), (512, 768, 256), (768, 512, 2112)])
+@pytest.mark.parametrize("cfg", [0, 1, 2, 3, 5, 6, 7, 8, 9, 10, 11])
+@pytest.mark.parametrize("M,N,K", [(256, 256, 64), (512, 512, 128), (256, 512, 192), (512, 768, 256), (768, 512, 2112),
+                                   (2048, 3072, 320)])
 def test_gemm_tn_plain(cfg, M, N, K):
     torch.manual_seed(0)
     x = torch.randn(M, K, device=DEV, dtype=torch.bfloat16)
@@ -424,13 +425,14 @@ def test_gemm_tn_strided_rows():
     assert rel_err(_ext.ops().gemm_tn(x, w, 0), x.float() @ w.float().t()) < 5e-3
 
 
+@pytest.mark.parametrize("cfg", [5, 11])
 @pytest.mark.parametrize("I,K", [(128, 320), (384, 320), (128, 384), (384, 2048)])
-def test_gemm_tn_swiglu(I, K):
+def test_gemm_tn_swiglu(I, K, cfg):
     torch.manual_seed(0)
     M = 512
     x = torch.randn(M, K, device=DEV, dtype=torch.bfloat16)
     w = torch.randn(2 * I, K, device=DEV, dtype=torch.bfloat16) * 0.1
-    gu, act = _ext.ops().gemm_tn_swiglu(x, w)
+    gu, act = _ext.ops().gemm_tn_swiglu(x, w, cfg)
     gu_ref = x.float() @ w.float().t()
     assert rel_err(gu, gu_ref) < 5e-3
     assert rel_err(act, ref.swiglu(gu_ref)) < 1e-2
@@ -438,7 +440,7 @@ def test_gemm_tn_swiglu(I, K):
     assert rel_err(act, _ext.ops().swiglu_fwd(gu)) < 2e-3
 
 
-@pytest.mark.parametrize("cfg", [0, 1, 2, 5, 6, 7])
+@pytest.mark.parametrize("cfg", [0, 1, 2, 5, 6, 7, 11])
 def test_gemm_tn_rope(cfg):
     torch.manual_seed(0)
     M, K, nq, nkv, D = 512, 256, 2, 1, 128

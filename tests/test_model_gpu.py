@@ -40,8 +40,9 @@ def test_model_hip_vs_reference(mt):
         assert e < 5e-2, (n, e.item())
 
 
+@pytest.mark.parametrize("down_fused", [True, False])
 @pytest.mark.parametrize("mt", ["smollm3", "llama"])
-def test_model_fused_gemm_epilogues(mt, monkeypatch):
+def test_model_fused_gemm_epilogues(mt, down_fused, monkeypatch):
     """M = 1024 tokens (multiple of 256): qkv+RoPE and gate_up+SwiGLU run as single HIP GEMMs with fused
     epilogues (csrc/gemm_tn.hip); loss and every gradient match the unfused HIP path (hipBLASLt + kernels)
     and the PyTorch reference."""
@@ -54,7 +55,11 @@ def test_model_fused_gemm_epilogues(mt, monkeypatch):
     labels = ids.clone()
     labels[:, 200:] = -100
     calls = {"swiglu": 0, "rope": 0}
-    orig_sw, orig_rope = F.GateUpSwiGLUFn.apply, F.QKVRopeFn.apply
+    # down_fused: gate_up GEMM + SwiGLU epilogue feeding the down GEMM whose dgrad carries the SwiGLU backward
+    # (GateUpActFn + SwiGLUDownFn); else GateUpSwiGLUFn + a plain down projection
+    sw_fn = F.GateUpActFn if down_fused else F.GateUpSwiGLUFn
+    monkeypatch.setattr(F, "_SWIGLU_DOWN", down_fused)
+    orig_sw, orig_rope = sw_fn.apply, F.QKVRopeFn.apply
 
     def sw(*a):
         calls["swiglu"] += 1
@@ -72,7 +77,7 @@ def test_model_fused_gemm_epilogues(mt, monkeypatch):
         calls["plain"] += int(ok)
         return ok
 
-    monkeypatch.setattr(F.GateUpSwiGLUFn, "apply", sw)
+    monkeypatch.setattr(sw_fn, "apply", sw)
     monkeypatch.setattr(F.QKVRopeFn, "apply", rp)
     monkeypatch.setattr(F, "_tn_plain_ok", plain)
     monkeypatch.setattr(F, "_TN_PLAIN", True)  # opt-in paths, exercised here
@@ -80,8 +85,8 @@ def test_model_fused_gemm_epilogues(mt, monkeypatch):
     monkeypatch.setattr(F, "_TN_MODE", "1")
     l_f, g_f = _run(m, ids, labels, True)
     assert calls["swiglu"] == 4 and calls["rope"] == (3 if mt == "smollm3" else 4)  # NoPE layer 3
-    # plain BK64 GEMM: o_proj and down_proj of every layer (+ the NoPE layer's qkv)
-    assert calls["plain"] == 8 + (1 if mt == "smollm3" else 0), calls
+    # plain HIP GEMM: o_proj (and down_proj unless it is SwiGLUDownFn) of every layer (+ the NoPE layer's qkv)
+    assert calls["plain"] == (4 if down_fused else 8) + (1 if mt == "smollm3" else 0), calls
     monkeypatch.setattr(F, "_TN_MODE", "0")
     calls["plain"] = 0
     l_u, g_u = _run(m, ids, labels, True)

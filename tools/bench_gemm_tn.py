@@ -19,6 +19,9 @@ from llm_fine_tune_distributed_amd.utils.gemm_tuning import enable_tuned_gemms  
 ap = argparse.ArgumentParser()
 ap.add_argument("--m", type=int, default=8192)
 ap.add_argument("--iters", type=int, default=20)
+ap.add_argument("--cfgs", default="0,1,2,5,6,7", help="gemm_tn configurations to time (8/9 = ping-pong)")
+ap.add_argument("--shapes", default="", help="name:N:K,... instead of the SmolLM3 projection shapes")
+ap.add_argument("--plain-only", action="store_true", help="skip the fused-epilogue section")
 a = ap.parse_args()
 assert _ext.load(), _ext.load_error()
 enable_tuned_gemms()
@@ -46,11 +49,13 @@ def rel(a_, b_):
 
 
 print(f"M = {M}")
-print("| shape | N | K | blas ms (TF/s) | tn 256x256 BK32 | tn 256x128 BK32 | tn 256x256 BK64 | BK64 TRC-epi | "
-      "BK64 256x128 NS3 | BK64 256x128 NS2 | max rel err |")
-print("|---|---:|---:|---:|---:|---:|---:|---:|---:|---:|---:|")
-for name, N, K in [("qkv", 3072, 2048), ("o", 2048, 2048), ("gate_up", 22016, 2048), ("down", 2048, 11008),
-                   ("lm_head", 128256, 2048)]:
+CFGS = [int(c) for c in a.cfgs.split(",")]
+print("| shape | N | K | blas ms (TF/s) | " + " | ".join(f"cfg {c}" for c in CFGS) + " | max rel err |")
+print("|---|---:|---:|---:|" + "---:|" * len(CFGS) + "---:|")
+SHAPES = ([(f.split(":")[0], int(f.split(":")[1]), int(f.split(":")[2])) for f in a.shapes.split(",")] if a.shapes else
+          [("qkv", 3072, 2048), ("o", 2048, 2048), ("gate_up", 22016, 2048), ("down", 2048, 11008),
+           ("lm_head", 128256, 2048)])
+for name, N, K in SHAPES:
     x = torch.randn(M, K, device="cuda", dtype=torch.bfloat16)
     w = torch.randn(N, K, device="cuda", dtype=torch.bfloat16) * 0.02
     fl = 2.0 * M * N * K
@@ -59,7 +64,7 @@ for name, N, K in [("qkv", 3072, 2048), ("o", 2048, 2048), ("gate_up", 22016, 20
     t = timeit(lambda: torch.nn.functional.linear(x, w))
     row.append(f"{t:.3f} ({fl / t / 1e9:.0f})")
     err = 0.0
-    for cfg in (0, 1, 2, 5, 6, 7):
+    for cfg in CFGS:
         c = ops.gemm_tn(x, w, cfg)
         err = max(err, rel(c, ref))
         t = timeit(lambda: ops.gemm_tn(x, w, cfg))
@@ -68,6 +73,8 @@ for name, N, K in [("qkv", 3072, 2048), ("o", 2048, 2048), ("gate_up", 22016, 20
     print("| " + " | ".join(row) + " |", flush=True)
     del x, w, ref
 
+if a.plain_only:
+    sys.exit(0)
 # fused epilogues vs unfused twins
 K, I = 2048, 11008
 x = torch.randn(M, K, device="cuda", dtype=torch.bfloat16)
