@@ -26,7 +26,7 @@ TORCH_LIBRARY(sftamd, m) {
   // fused decode sampler: penalty -> temperature -> top-k -> top-p -> draw, device-resident state
   m.def("sample_token(Tensor logits, Tensor(a!) presence, Tensor(b!) state, Tensor(c!)? tok_out, Tensor(d!)? pos_out, Tensor(e!)? len_out, Tensor(f!)? log, float temperature, int top_k, float top_p, float repetition_penalty, bool do_sample, int seed) -> ()");
   // weight-gradient GEMM: out[N,K] (+)= dy[T,N]^T x[T,K]
-  m.def("wgrad_gemm(Tensor(a!) out, Tensor dy, Tensor x, bool accumulate, int cfg=0) -> ()");
+  m.def("wgrad_gemm(Tensor(a!) out, Tensor dy, Tensor x, bool accumulate, int cfg=0, Tensor(b!)? norm=None) -> ()");
   // input-gradient GEMM dX = dy w (w [K, N]), optional fused SwiGLU backward (csrc/gemm_dgrad.hip)
   m.def("dgrad_gemm(Tensor dy, Tensor w, Tensor? gate_up=None, int cfg=0) -> Tensor");
   // forward-layout GEMM C = a w^T with fused epilogues (csrc/gemm_tn.hip)
@@ -35,6 +35,7 @@ TORCH_LIBRARY(sftamd, m) {
   m.def("gemm_tn_rope(Tensor x, Tensor w, Tensor cos, Tensor sin, int rope_cols, int cfg=0) -> Tensor");
   // optimizer
   m.def("sumsq(Tensor x) -> Tensor");
+  m.def("sumsq_chunks(Tensor x, Tensor chunks) -> Tensor");
   m.def("adamw_flat(Tensor(a!) param, Tensor grad, Tensor(b!)? master, Tensor(c!) exp_avg, Tensor(d!) exp_avg_sq, Tensor clip_coef, float lr, float beta1, float beta2, float eps, float weight_decay, float bc1, float bc2, int sr_seed=0, int sr_offset=0) -> ()");
   // native data pipeline (CPU)
   m.def("pack_sequences(Tensor tokens, Tensor offsets, Tensor order, int max_tokens, int pad_id, int pad_multiple) -> (Tensor, Tensor, Tensor, Tensor, Tensor)");

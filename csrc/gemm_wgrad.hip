@@ -197,10 +197,15 @@ __device__ __forceinline__ void mainloop_pipe(char* __restrict__ b0, char* __res
 
 // Epilogue: fp32 wave tile -> LDS (rows padded to TN + 4 floats: conflict-free) -> 16-byte
 // read-modify-write of the bf16 gradient (beta = 1 when accumulating, else plain store).
+// ``nrm`` (optional): this wave's slot of the gradient-norm partials — the fp32 sum of squares of the values
+// it stores (before bf16 rounding; the FINAL gradient when this is the last contribution of the step), so the
+// clip norm needs no separate pass over the gradient.
 template <class G>
 __device__ __forceinline__ void epilogue(char* smem, f32x4 (&acc)[G::FM][G::FN], u16* __restrict__ C, int K, int n0,
-                                         int k0, int wm, int wk, int w, int lane, int accumulate) {
+                                         int k0, int wm, int wk, int w, int lane, int accumulate,
+                                         float* __restrict__ nrm = nullptr) {
   const int g = lane >> 4, ii = lane & 15;
+  float ss = 0.f;
   float* ep = reinterpret_cast<float*>(smem) + w * G::EPI_ROWS * G::EPI_LD;
   constexpr int FPP = G::EPI_ROWS / 16 < G::FM ? G::EPI_ROWS / 16 : G::FM;  // fragments per pass
   constexpr int ROWS = FPP * 16;
@@ -228,9 +233,17 @@ __device__ __forceinline__ void epilogue(char* smem, f32x4 (&acc)[G::FM][G::FN],
 #pragma unroll
         for (int e = 0; e < 8; ++e) v[e] += o[e];
       }
+      if (nrm != nullptr) {  // fp32 values before the bf16 store: no extra registers (the 256x256 ring kernel
+#pragma unroll             // sits at 256 VGPRs; unpacking the stored bf16 made it spill inside its main loop)
+        for (int e = 0; e < 8; ++e) ss += v[e] * v[e];
+      }
       *(uint4*)out = pack8(v);
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  }
+  if (nrm != nullptr) {
+    ss = wave_sum(ss);
+    if (lane == 0) *nrm = ss;
   }
 }
 
@@ -454,10 +467,16 @@ __device__ __forceinline__ void epilogue_partial(f32x4 (&acc)[G::FM][G::FN], flo
 // 8 elements per thread, slabs summed in order s = 0..S-1.
 template <int BM, int BN>
 __global__ void __launch_bounds__(256) splitk_fixup_kernel(const float* __restrict__ P, u16* __restrict__ C, int tile0,
-                                                           int ntiles, int splits, int nbk, int K, int accumulate) {
+                                                           int ntiles, int splits, int nbk, int K, int accumulate,
+                                                           float* __restrict__ nrm) {
   constexpr int E8 = BM * BN / 8;
+  if (nrm != nullptr && blockIdx.x == 0) {  // the whole tiles' partials, parked past the slabs by ring_kernel
+    const float* src = P + (long)ntiles * splits * BM * BN;
+    for (int i = threadIdx.x; i < tile0 * 8; i += 256) nrm[i] = src[i];
+  }
+  static_assert((BM * BN / 8) % 256 == 0, "fixup blocks cover whole tiles");
   const long idx = (long)blockIdx.x * 256 + threadIdx.x;
-  if (idx >= (long)ntiles * E8) return;
+  if (idx >= (long)ntiles * E8) return;  // never taken: the grid covers whole tiles
   const int t = (int)(idx / E8), e = (int)(idx - (long)t * E8) * 8;
   const int row = e / BN, col = e - row * BN;
   const float* q = P + (long)t * splits * BM * BN + e;
@@ -477,13 +496,28 @@ __global__ void __launch_bounds__(256) splitk_fixup_kernel(const float* __restri
 #pragma unroll
     for (int i = 0; i < 8; ++i) v[i] += o[i];
   }
-  *(uint4*)out = pack8(v);
+  const uint4 pk = pack8(v);
+  *(uint4*)out = pk;
+  if (nrm != nullptr) {  // per-block slot (blocks never straddle a tile: E8 % 256 == 0)
+    float r[8], ss = 0.f;
+    unpack8(pk, r);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) ss += r[i] * r[i];
+    ss = wave_sum(ss);
+    __shared__ float red[4];
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = ss;
+    __syncthreads();
+    if (threadIdx.x == 0) nrm[(long)tile0 * 8 + blockIdx.x] = red[0] + red[1] + red[2] + red[3];
+  }
 }
 
-template <int BM, int BN, int WM, int WN, int NS, bool SCHED>
+template <int BM, int BN, int WM, int WN, int NS, bool SCHED, bool NORM = false>
 __global__ void __launch_bounds__(NT) ring_kernel(const u16* __restrict__ A, const u16* __restrict__ B,
-                                                  u16* __restrict__ C, int T, int N, int K, int nbk, int accumulate,
+                                                  u16* __restrict__ C, int T, int N, int K, int nbk, int flags,
                                                   float* __restrict__ P, int ndp, int splits) {
+  // flags: bit 0 = accumulate into C, bit 1 = write gradient-norm partials of the whole tiles (8 per tile) to
+  // P (no split) or past the split slabs (no extra kernel argument: one more pointer costs this 256-VGPR kernel
+  // spills inside its main loop)
   using G = RCfg<BM, BN, WM, WN, NS>;
   __shared__ __attribute__((aligned(16))) char smem[G::LDS];
   const int nwg = gridDim.x, orig = blockIdx.x;
@@ -537,29 +571,44 @@ __global__ void __launch_bounds__(NT) ring_kernel(const u16* __restrict__ A, con
     return;
   }
   __syncthreads();
-  epilogue<G>(smem, acc, C, K, n0, k0, wm, wk, w, lane, accumulate);
+  float* nrm = nullptr;  // wave-uniform (scalar) pointer: no VGPRs
+  if (NORM && (flags & 2))
+    nrm = (splits <= 1 ? P : P + (long)(gridDim.x - ndp) * BM * BN) + tile * 8 + __builtin_amdgcn_readfirstlane(w);
+  epilogue<G>(smem, acc, C, K, n0, k0, wm, wk, w, lane, flags & 1, nrm);
 }
+
+// Gradient-norm slots a ring launch writes (norm partials): 8 per whole tile, one per fixup block of a split tile.
+static long ring_norm_slots(int tiles, int ndp, int BM, int BN) { return (long)ndp * 8 + (long)(tiles - ndp) * BM * BN / 2048; }
 
 // splits > 1: tiles beyond the first `full_waves` x 256 (or all of them when full_waves == 0) are split over the
 // token axis; full_waves < 0 = split every tile.
 template <int BM, int BN, int WM, int WN, int NS, bool SCHED = false>
 void launch_ring(const at::Tensor& dy, const at::Tensor& x, at::Tensor& out, bool accumulate, int splits = 1,
-                 bool hybrid = false) {
+                 bool hybrid = false, float* nrm = nullptr, long nrm_cap = 0) {
   const int T = dy.size(0), N = dy.size(1), K = x.size(1);
   const int nbn = N / BM, nbk = K / BN, tiles = nbn * nbk;
   const int ndp = splits <= 1 ? tiles : (hybrid ? tiles / 256 * 256 : 0);
   const int nsk = tiles - ndp;
+  SFT_CHECK(nrm == nullptr || ring_norm_slots(tiles, ndp, BM, BN) <= nrm_cap, "wgrad_gemm: norm slot buffer too small");
   at::Tensor part;
-  if (nsk > 0)  // tile-local fp32 slabs, one per split piece (stream-ordered caching allocation)
-    part = at::empty({(long)nsk * splits * BM * BN}, dy.options().dtype(at::kFloat));
-  ring_kernel<BM, BN, WM, WN, NS, SCHED><<<ndp + nsk * splits, NT, 0, cur_stream()>>>(
-      (const u16*)dy.data_ptr(), (const u16*)x.data_ptr(), (u16*)out.data_ptr(), T, N, K, nbk, accumulate ? 1 : 0,
-      nsk > 0 ? part.data_ptr<float>() : nullptr, ndp, splits);
+  if (nsk > 0)  // tile-local fp32 slabs, one per split piece (stream-ordered caching allocation) [+ whole-tile norms]
+    part = at::empty({(long)nsk * splits * BM * BN + (nrm != nullptr ? (long)ndp * 8 : 0)}, dy.options().dtype(at::kFloat));
+  float* P = nsk > 0 ? part.data_ptr<float>() : nrm;
+  const int flags = (accumulate ? 1 : 0) | (nrm != nullptr ? 2 : 0);
+  // NORM: separate instantiation, so the plain kernel keeps its register allocation; at 256 x 256 without the
+  // pinned MFMA / DMA interleave (with it the allocator spills inside the main loop: 14 reloads vs 1)
+  constexpr bool SCHED_N = BN == 256 ? false : SCHED;
+  if (nrm != nullptr)
+    ring_kernel<BM, BN, WM, WN, NS, SCHED_N, true><<<ndp + nsk * splits, NT, 0, cur_stream()>>>(
+        (const u16*)dy.data_ptr(), (const u16*)x.data_ptr(), (u16*)out.data_ptr(), T, N, K, nbk, flags, P, ndp, splits);
+  else
+    ring_kernel<BM, BN, WM, WN, NS, SCHED><<<ndp + nsk * splits, NT, 0, cur_stream()>>>(
+        (const u16*)dy.data_ptr(), (const u16*)x.data_ptr(), (u16*)out.data_ptr(), T, N, K, nbk, flags, P, ndp, splits);
   SFT_LAUNCH_CHECK();
   if (nsk > 0) {
     const long n8 = (long)nsk * BM * BN / 8;
     splitk_fixup_kernel<BM, BN><<<(unsigned)((n8 + 255) / 256), 256, 0, cur_stream()>>>(
-        part.data_ptr<float>(), (u16*)out.data_ptr(), ndp, nsk, splits, nbk, K, accumulate ? 1 : 0);
+        part.data_ptr<float>(), (u16*)out.data_ptr(), ndp, nsk, splits, nbk, K, accumulate ? 1 : 0, nrm);
     SFT_LAUNCH_CHECK();
   }
 }
@@ -576,7 +625,11 @@ void launch(const at::Tensor& dy, const at::Tensor& x, at::Tensor& out, bool acc
 }  // namespace wgrad
 
 // cfg: 0 = auto, 1 = 256x256 (8 waves 2x4), 2 = 256x128 (8 waves 4x2); +2 = register-pipelined loop
-void wgrad_gemm(at::Tensor out, at::Tensor dy, at::Tensor x, bool accumulate, int64_t cfg) {
+// norm (optional, fp32, contiguous): gradient-norm partial slots for the ring variants (cfg 9 / 10 and their split-K
+// forms): every slot the launch owns is written, the rest are left untouched (the caller zeroes the buffer once per
+// step); other variants reject it.
+void wgrad_gemm(at::Tensor out, at::Tensor dy, at::Tensor x, bool accumulate, int64_t cfg,
+                const c10::optional<at::Tensor>& norm) {
   SFT_CHECK_CUDA(dy);
   SFT_CHECK_BF16(dy);
   SFT_CHECK_BF16(x);
@@ -599,13 +652,21 @@ void wgrad_gemm(at::Tensor out, at::Tensor dy, at::Tensor x, bool accumulate, in
   cfg %= 100;
   SFT_CHECK(splits <= 1 || ((cfg == 9 || cfg == 10) && T / 32 >= splits),
             "wgrad_gemm split-K: ring cfg 9/10 with at least one 32-token step per split");
+  float* nrm = nullptr;
+  long nrm_cap = 0;
+  if (norm.has_value() && norm->defined()) {
+    SFT_CHECK(cfg == 9 || cfg == 10, "wgrad_gemm: norm partials need the ring variants (cfg 9 / 10)");
+    SFT_CHECK(norm->scalar_type() == at::kFloat && norm->is_contiguous() && norm->is_cuda(), "wgrad_gemm: fp32 norm slots");
+    nrm = norm->data_ptr<float>();
+    nrm_cap = norm->numel();
+  }
   if (splits > 1) {
     if (cfg == 10) {
       SFT_CHECK(N % 256 == 0 && K % 256 == 0, "wgrad_gemm ring 256x256: N, K multiples of 256");
-      wgrad::launch_ring<256, 256, 2, 4, 5, true>(dy, x, out, accumulate, splits, hybrid);
+      wgrad::launch_ring<256, 256, 2, 4, 5, true>(dy, x, out, accumulate, splits, hybrid, nrm, nrm_cap);
     } else {
       SFT_CHECK(N % 256 == 0 && K % 128 == 0, "wgrad_gemm ring 256x128: N multiple of 256, K of 128");
-      wgrad::launch_ring<256, 128, 4, 2, 6, true>(dy, x, out, accumulate, splits, hybrid);
+      wgrad::launch_ring<256, 128, 4, 2, 6, true>(dy, x, out, accumulate, splits, hybrid, nrm, nrm_cap);
     }
     return;
   }
@@ -621,10 +682,10 @@ void wgrad_gemm(at::Tensor out, at::Tensor dy, at::Tensor x, bool accumulate, in
     wgrad::launch_ring<256, 256, 2, 4, 4>(dy, x, out, accumulate);
   } else if (cfg == 9) {
     SFT_CHECK(N % 256 == 0 && K % 128 == 0 && T % 32 == 0, "wgrad_gemm ring 256x128: N multiple of 256, K of 128");
-    wgrad::launch_ring<256, 128, 4, 2, 6>(dy, x, out, accumulate);
+    wgrad::launch_ring<256, 128, 4, 2, 6>(dy, x, out, accumulate, 1, false, nrm, nrm_cap);
   } else if (cfg == 10) {
     SFT_CHECK(N % 256 == 0 && K % 256 == 0 && T % 32 == 0, "wgrad_gemm ring 256x256: N, K multiples of 256");
-    wgrad::launch_ring<256, 256, 2, 4, 5, true>(dy, x, out, accumulate);
+    wgrad::launch_ring<256, 256, 2, 4, 5, true>(dy, x, out, accumulate, 1, false, nrm, nrm_cap);
   } else if (cfg == 11) {
     SFT_CHECK(N % 256 == 0 && K % 128 == 0 && T % 32 == 0, "wgrad_gemm ring 256x128: N multiple of 256, K of 128");
     wgrad::launch_ring<256, 128, 4, 2, 6, true>(dy, x, out, accumulate);

@@ -37,6 +37,56 @@ at::Tensor sumsq(const at::Tensor& x) {
   return part;
 }
 
+// Sum of squares over a list of ranges of one flat bf16 buffer in ONE launch: block b covers chunk b =
+// (start, length) of ``chunks`` (int64 [C, 2] on the device; the caller splits long ranges into <= 256K-element
+// chunks so ~C blocks fill the chip). The gradient norm's leftovers after the wgrad epilogues took theirs
+// (tied embedding, norm weights, adapters).
+__global__ __launch_bounds__(256) void sumsq_chunks_kernel(const u16* __restrict__ x, const long* __restrict__ chunks,
+                                                           float* __restrict__ part) {
+  const long st = chunks[2 * blockIdx.x], n = chunks[2 * blockIdx.x + 1];
+  const u16* p = x + st;
+  float s = 0.f;
+  if ((st & 7) == 0) {
+    const long nv = n / 8;
+    for (long v = threadIdx.x; v < nv; v += 256) {
+      float f[8];
+      unpack8(*(const uint4*)(p + v * 8), f);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) s += f[i] * f[i];
+    }
+    for (long i = nv * 8 + threadIdx.x; i < n; i += 256) {
+      const float f = bf2f(p[i]);
+      s += f * f;
+    }
+  } else {
+    for (long i = threadIdx.x; i < n; i += 256) {
+      const float f = bf2f(p[i]);
+      s += f * f;
+    }
+  }
+  s = wave_sum(s);
+  __shared__ float red[4];
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) part[blockIdx.x] = red[0] + red[1] + red[2] + red[3];
+}
+
+at::Tensor sumsq_chunks(const at::Tensor& x, const at::Tensor& chunks) {
+  SFT_CHECK_BF16(x);
+  SFT_CHECK_CONTIG(x);
+  SFT_CHECK(chunks.scalar_type() == at::kLong && chunks.is_contiguous() && chunks.dim() == 2 && chunks.size(1) == 2 &&
+                chunks.device() == x.device(),
+            "sumsq_chunks: int64 [C, 2] (start, length) on the buffer's device");
+  const long C = chunks.size(0);
+  auto part = at::zeros({std::max<long>(C, 1)}, x.options().dtype(at::kFloat));
+  if (C > 0) {
+    sumsq_chunks_kernel<<<(unsigned)C, 256, 0, cur_stream()>>>((const u16*)x.data_ptr(), chunks.data_ptr<long>(),
+                                                               part.data_ptr<float>());
+    SFT_LAUNCH_CHECK();
+  }
+  return part;
+}
+
 // omb1 = 1 - beta1, omb2 = 1 - beta2 computed in double on the host (torch AdamW's constants:
 // 1.f - 0.999f would be 1.0000467e-3, not fp32(1e-3)).
 __device__ __forceinline__ void adam_elem(float& w, float g, float& m, float& v, float lr, float b1, float b2, float eps,
@@ -216,6 +266,7 @@ void adamw_flat(at::Tensor param, const at::Tensor& grad, const c10::optional<at
 
 TORCH_LIBRARY_IMPL(sftamd, CUDA, m) {
   m.impl("sumsq", &sumsq);
+  m.impl("sumsq_chunks", &sumsq_chunks);
   m.impl("adamw_flat", &adamw_flat);
 }
 

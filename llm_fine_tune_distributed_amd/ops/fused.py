@@ -65,17 +65,23 @@ def _wgrad_cfg(T: int, N: int, K: int) -> int:
     return 0
 
 
-def _wgrad_mm(out: torch.Tensor, dy2d: torch.Tensor, x2d: torch.Tensor, accumulate: bool) -> None:
-    """out (+)= dy2d^T @ x2d, all bf16 (out is the flat-buffer gradient view)."""
+def _wgrad_mm(out: torch.Tensor, dy2d: torch.Tensor, x2d: torch.Tensor, accumulate: bool,
+              norm: Optional[torch.Tensor] = None) -> bool:
+    """out (+)= dy2d^T @ x2d, all bf16 (out is the flat-buffer gradient view). ``norm``: gradient-norm partial
+    slots the ring kernels fill with the sum of squares of the values they store; returns whether they did
+    (other variants leave the norm to DDPEngine.grad_norm_sq's leftover pass)."""
     cfg = 0
     if _ext.use_hip(dy2d) and dy2d.dtype == torch.bfloat16 and out.is_contiguous():
         cfg = _wgrad_cfg(dy2d.shape[0], dy2d.shape[1], x2d.shape[1])
     if cfg:
-        _ext.ops().wgrad_gemm(out, dy2d.contiguous(), x2d.contiguous(), accumulate, cfg)
-    elif accumulate:
+        use_norm = norm is not None and cfg % 100 in (9, 10)
+        _ext.ops().wgrad_gemm(out, dy2d.contiguous(), x2d.contiguous(), accumulate, cfg, norm if use_norm else None)
+        return use_norm
+    if accumulate:
         out.addmm_(dy2d.t(), x2d)
     else:
         torch.mm(dy2d.t(), x2d, out=out)
+    return False
 
 
 # Optional (SFTAMD_WGRAD_STREAM=1): weight-gradient GEMMs off the critical path. Backward's dgrad
@@ -119,16 +125,22 @@ def _accumulate_weight_grad(param: torch.Tensor, dy2d: torch.Tensor, x2d: torch.
     if mg is not None:
         fresh = getattr(param, "_sftamd_fresh", False)
         if mg.dtype == dy2d.dtype:
-            # first contribution of the step: beta=0 GEMM, no zero-fill pass needed
+            # first contribution of the step: beta=0 GEMM, no zero-fill pass needed. Norm partials (DDPEngine
+            # fused norm, synchronising pass only) when this is the parameter's last contribution of the pass.
+            ns = getattr(param, "_sftamd_norm_slots", None)
+            if ns is not None and getattr(param, "_sftamd_remaining", 1) != 1:
+                ns = None
             ws = _wgrad_stream(dy2d.device)
             if ws is not None:
                 ws.wait_stream(torch.cuda.current_stream(dy2d.device))
                 with torch.cuda.stream(ws):
-                    _wgrad_mm(mg, dy2d, x2d, accumulate=not fresh)
+                    done = _wgrad_mm(mg, dy2d, x2d, accumulate=not fresh, norm=ns)
                 dy2d.record_stream(ws)  # keep the operands alive until the side stream is done
                 x2d.record_stream(ws)
             else:
-                _wgrad_mm(mg, dy2d, x2d, accumulate=not fresh)
+                done = _wgrad_mm(mg, dy2d, x2d, accumulate=not fresh, norm=ns)
+            if done:
+                param._sftamd_norm_done = True
         elif fresh:
             mg.copy_(torch.mm(dy2d.t(), x2d))
         else:

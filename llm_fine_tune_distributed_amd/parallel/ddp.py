@@ -44,6 +44,7 @@ so no collective is larger than ~2 caps and ZeRO-1 state / gathers stay evenly s
 from __future__ import annotations
 
 import contextlib
+import os
 from dataclasses import dataclass, field
 from typing import Callable, Dict, List, Optional
 
@@ -185,10 +186,28 @@ class DDPEngine:
         # vs 96.2-96.3 samples/s without — the concurrent HBM pass slows the backward GEMMs as much as it
         # saves, so it is off by default.
         if track_norm is None:
-            import os
             track_norm = os.environ.get("SFTAMD_NORM_IN_BWD", "0") == "1"
         self.track_norm = bool(track_norm)
         self.norm_partials = torch.zeros(len(self.buckets), dtype=torch.float32, device=dev)
+        # World size 1 on GPU (SFTAMD_NORM_FUSED, default on): the weight-gradient GEMMs of the synchronising pass
+        # write the sum of squares of the gradient they store into per-(tile, wave) slots (csrc/gemm_wgrad.hip), so
+        # the clip norm is one small reduction over the slots plus a pass over what no wgrad epilogue produced
+        # (tied embedding, norm weights, adapters): the 6 GB sum-of-squares pass of a 3B model disappears.
+        self.fused_norm = (world_size == 1 and dev.type == "cuda" and not self.track_norm
+                           and os.environ.get("SFTAMD_NORM_FUSED", "1") == "1")
+        self._norm_slot_views = {}
+        self._norm_chunk_cache = {}
+        if self.fused_norm:
+            total = 0
+            offs = []
+            for p, _, _, _ in self.layout:
+                if p.dim() == 2:
+                    cap = -(-p.shape[0] // 256) * -(-p.shape[1] // 128) * 32  # >= slots of any ring launch
+                    offs.append((p, total, cap))
+                    total += cap
+            self.norm_slots = torch.zeros(max(total, 1), dtype=torch.float32, device=dev)
+            for p, o, cap in offs:
+                self._norm_slot_views[id(p)] = self.norm_slots[o:o + cap]
         self._norm_stream = torch.cuda.Stream(device=dev) if (self.track_norm and dev.type == "cuda") else None
         self._norm_valid = False
         for p, _, _, _ in self.layout:
@@ -244,6 +263,12 @@ class DDPEngine:
         reset = getattr(self.model, "reset_grad_use_counters", None)
         if reset is not None:
             reset()
+        if self.fused_norm:
+            if self.sync_grads:
+                self.norm_slots.zero_()
+            for p, _, _, _ in self.layout:
+                p._sftamd_norm_slots = self._norm_slot_views.get(id(p)) if self.sync_grads else None
+                p._sftamd_norm_done = False
         for b in self.buckets:
             b.pending = len(b.params)
             b.ready = False
@@ -339,10 +364,37 @@ class DDPEngine:
         the last synchronised backward; None when that backward did not produce it."""
         if not self._norm_valid:
             return None
+        if self.fused_norm:
+            self._norm_valid = False
+            return (self.norm_slots.sum() + self._leftover_sumsq()).reshape(1)
         if self._norm_stream is not None:
             torch.cuda.current_stream(self.grad_flat.device).wait_stream(self._norm_stream)
         self._norm_valid = False
         return self.norm_partials.sum().reshape(1)
+
+    def _leftover_sumsq(self) -> torch.Tensor:
+        """Sum of squares of the gradients no wgrad epilogue covered this step, in one launch over
+        chunks of grad_flat (256K elements per block; the chunk table is cached per set of leftover ranges)."""
+        ranges = []
+        for p, o, n, _ in self.layout:
+            if not getattr(p, "_sftamd_norm_done", False):
+                if ranges and ranges[-1][0] + ranges[-1][1] == o:
+                    ranges[-1][1] += n
+                else:
+                    ranges.append([o, n])
+        if not ranges:
+            return torch.zeros((), dtype=torch.float32, device=self.grad_flat.device)
+        key = tuple((o, n) for o, n in ranges)
+        chunks = self._norm_chunk_cache.get(key)
+        if chunks is None:
+            CH = 1 << 18  # ~1000 blocks for a 262M-element tied embedding
+            tab = [(o + s, min(CH, n - s)) for o, n in ranges for s in range(0, n, CH)]
+            chunks = torch.tensor(tab, dtype=torch.int64).to(self.grad_flat.device)
+            if len(self._norm_chunk_cache) > 16:
+                self._norm_chunk_cache.clear()
+            self._norm_chunk_cache[key] = chunks
+        from ..ops import _ext
+        return _ext.ops().sumsq_chunks(self.grad_flat, chunks).sum()
 
     def _collective(self, b: Bucket, view: torch.Tensor):
         if self.shard:
@@ -380,6 +432,8 @@ class DDPEngine:
         if not self.sync_grads:
             return
         self._zero_untouched()
+        if self.fused_norm:
+            self._norm_valid = True
         if self.world_size == 1 and not self.track_norm:
             return
         for b in self.buckets[self._next:]:

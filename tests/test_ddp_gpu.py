@@ -1,6 +1,7 @@
 """DDP engine on GPU tensors: 2 ranks sharing one MI355X (gloo transport, the engine's streams,
 hooks, bucket views and the HIP kernels are the same as with RCCL) == 1 rank on the same global batch.
 The RCCL/xGMI path itself runs in the driver's 8-GPU scaling bench."""
+import contextlib
 import os
 import socket
 import tempfile
@@ -118,3 +119,30 @@ def test_zero1_on_gpu_matches_replicated():
     assert torch.equal(z0["p"], z1["p"])
     assert torch.equal(z0["p"], a["p"]) or ((z0["p"] - a["p"]).norm() / a["p"].norm()) < 1e-3
     assert z0["log"] == pytest.approx(a["log"], rel=1e-3)
+
+
+@pytest.mark.parametrize("ga", [1, 2])
+def test_fused_grad_norm_world1(ga, monkeypatch):
+    """World size 1: the clip norm from the wgrad epilogues' partial slots + the leftover pass (tied embedding,
+    norm weights) equals a plain sum of squares over the flat gradient, with and without gradient accumulation."""
+    from llm_fine_tune_distributed_amd.models import build_model, tiny
+    from llm_fine_tune_distributed_amd.parallel.ddp import DDPEngine
+    torch.manual_seed(0)
+    cfg = tiny(hidden_size=1024, num_attention_heads=8, num_key_value_heads=2, head_dim=128, intermediate_size=2048,
+               vocab_size=1024, num_hidden_layers=2)
+    m = build_model(cfg, device="cuda", dtype=torch.bfloat16, seed=0)
+    eng = DDPEngine(m, world_size=1, rank=0, process_group=None)
+    assert eng.fused_norm
+    ids = torch.randint(0, 1024, (ga, 2, 1024), device="cuda")
+    eng.zero_grad()
+    for i in range(ga):
+        ctx = eng.no_sync() if i < ga - 1 else contextlib.nullcontext()
+        with ctx:
+            eng.prepare_backward()
+            m(ids[i], labels=ids[i]).loss.backward()
+            eng.finish_backward()
+    covered = [n for n, p in m.named_parameters() if getattr(p, "_sftamd_norm_done", False)]
+    assert len(covered) == 4 * cfg.num_hidden_layers, covered  # qkv, o, gate_up, down of every layer
+    got = eng.grad_norm_sq().item()
+    want = eng.grad_flat.float().pow(2).sum().item()
+    assert abs(got - want) <= 1e-4 * want, (got, want)

@@ -373,6 +373,39 @@ def test_wgrad_gemm(cfg, T, N, K, accumulate):
     assert err <= 0.02 * want.abs().max().item(), err
 
 
+@pytest.mark.parametrize("cfg,T,N,K", [(9, 416, 512, 384), (10, 352, 512, 512), (210, 512, 512, 512), (309, 384, 512, 384),
+                                       (1310, 96, 4096, 4352), (1309, 128, 4096, 2304)])
+@pytest.mark.parametrize("accumulate", [False, True])
+def test_wgrad_gemm_norm_slots(cfg, T, N, K, accumulate):
+    """The ring wgrad kernels' norm partials (epilogue / split-K fixup) sum to the squared norm of the bf16
+    gradient they stored; the slots a launch does not own stay untouched."""
+    torch.manual_seed(0)
+    dy = torch.randn(T, N, device="cuda", dtype=torch.bfloat16)
+    x = torch.randn(T, K, device="cuda", dtype=torch.bfloat16)
+    out = torch.randn(N, K, device="cuda", dtype=torch.bfloat16)
+    cap = -(-N // 256) * -(-K // 128) * 32
+    slots = torch.zeros(cap + 64, device="cuda")
+    slots[cap:] = 7.0  # sentinel past the capacity handed to the kernel
+    _ext.ops().wgrad_gemm(out, dy, x, accumulate, cfg, slots[:cap])
+    want = out.float().pow(2).sum().item()
+    assert abs(slots[:cap].sum().item() - want) <= 1e-4 * want
+    assert torch.all(slots[cap:] == 7.0)
+    with pytest.raises(RuntimeError):  # the non-ring variants have no norm epilogue
+        _ext.ops().wgrad_gemm(out, dy, x, accumulate, 1, slots[:cap])
+
+
+def test_sumsq_chunks():
+    torch.manual_seed(0)
+    x = torch.randn(5_000_003, device="cuda").to(torch.bfloat16)
+    tab = [(0, 1 << 20), (1 << 20, 3), (1_500_001, 77_777), (4_000_000, 1_000_003), (17, 0)]
+    chunks = torch.tensor(tab, dtype=torch.int64, device="cuda")
+    part = _ext.ops().sumsq_chunks(x, chunks)
+    xf = x.float()
+    for i, (o, n) in enumerate(tab):
+        want = xf[o:o + n].pow(2).sum().item()
+        assert abs(part[i].item() - want) <= 1e-4 * max(want, 1.0)
+
+
 def test_dropout_add_matches_reference_mask():
     torch.manual_seed(0)
     wide = torch.randn(300, 528, device="cuda", dtype=torch.bfloat16)
