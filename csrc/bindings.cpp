@@ -4,7 +4,13 @@
 // native data-pipeline ops below which are CPU kernels.
 #include <torch/library.h>
 
+namespace sftamd {
+int64_t cu_masked_stream(int64_t n, int64_t stride, int64_t offset);  // csrc/optim.hip
+}
+
 TORCH_LIBRARY(sftamd, m) {
+  // runtime: CU-restricted HIP stream for the optimizer's side stream (no tensor arguments: catch-all kernel)
+  m.def("cu_masked_stream(int n, int stride=1, int offset=0) -> int", &sftamd::cu_masked_stream);
   // norms / elementwise
   m.def("rmsnorm_fwd(Tensor x, Tensor? residual, Tensor weight, float eps) -> (Tensor, Tensor, Tensor)");
   m.def("rmsnorm_bwd(Tensor dy, Tensor h, Tensor weight, Tensor rstd, Tensor? dres, Tensor(a!)? dw_out=None, bool accumulate=False) -> (Tensor, Tensor)");

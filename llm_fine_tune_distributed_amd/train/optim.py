@@ -12,11 +12,34 @@ from __future__ import annotations
 
 import contextlib
 import math
+import os
 from typing import Callable, Dict, Optional
 
 import torch
 
 from .. import ops
+
+
+_UPDATE_STREAMS = {}
+
+
+def _update_stream(device: torch.device):
+    """Side stream of the overlapped optimizer update. SFTAMD_ADAMW_CUS=n (> 0) restricts it to n CUs (CU
+    i * SFTAMD_ADAMW_CU_STRIDE, hipExtStreamCreateWithCUMask): the HBM-bound update then streams on a few CUs
+    instead of time-sharing every CU with the next forward's GEMM workgroups. Default: unrestricted."""
+    n = int(os.environ.get("SFTAMD_ADAMW_CUS", "0") or 0)
+    if n <= 0:
+        return torch.cuda.Stream(device=device)
+    idx = device.index if device.index is not None else torch.cuda.current_device()
+    key = (idx, n)
+    st = _UPDATE_STREAMS.get(key)
+    if st is None:
+        from ..ops import _ext
+        stride = int(os.environ.get("SFTAMD_ADAMW_CU_STRIDE", "1") or 1)
+        with torch.cuda.device(idx):
+            handle = _ext.ops().cu_masked_stream(n, stride, 0)
+        st = _UPDATE_STREAMS[key] = torch.cuda.ExternalStream(handle, device=torch.device("cuda", idx))
+    return st
 
 
 class _StreamPoint:
@@ -110,7 +133,7 @@ class FlatAdamW:
             groups[-1] += ranges(rest)
         self._groups = groups
         self._events = [torch.cuda.Event() for _ in groups]
-        self._stream = torch.cuda.Stream(device=e.device)
+        self._stream = _update_stream(e.device)
         self._pending = False
         self._hooks = []
 
@@ -328,7 +351,7 @@ class ShardedAdamW(FlatAdamW):
         for i, layer in enumerate(inner.layers):
             self._hooks.append(layer.register_forward_pre_hook(waiter(i + 1)))
         self._hooks.append(inner.layers[-1].register_forward_hook(waiter(last)))
-        self._stream = torch.cuda.Stream(device=e.device) if e.device.type == "cuda" else None
+        self._stream = _update_stream(e.device) if e.device.type == "cuda" else None
         self.overlap = True
         return True
 
