@@ -1510,7 +1510,167 @@ __global__ __launch_bounds__(256, 2) void bwd_dkdv3_kernel(const u16* __restrict
   }
 }
 
+// GQA-grouped dK/dV (v5): one workgroup per (kv head, sequence, 64-key block) walks the query tiles of ALL
+// rep = nq / nkv query heads that share the kv head, keeping K/V fragments and the dK/dV accumulators in
+// registers across heads. dK/dV are written once, in bf16, straight into dqkv: no rep x [total, 2*nkv*128] fp32
+// partial slabs (134 MB written + re-read at 16 x 512 tokens, 16q/4kv) and no dkdv_reduce pass. The per-tile
+// math (S^T, dP^T, dS^T store for dq4) is bwd_dkdv3_kernel's; the iteration space is flattened over
+// (head, query tile) so the register prefetch of the next tile crosses head boundaries. Causal imbalance
+// (key block 0 walks rep x nqt tiles) is absorbed by the dispatch order: blockIdx.z = key block, heaviest first.
+__global__ __launch_bounds__(256, 2) void bwd_dkdv5_kernel(const u16* __restrict__ qkv, const u16* __restrict__ dout,
+                                                           const float* __restrict__ lse,
+                                                           const float* __restrict__ delta,
+                                                           const int* __restrict__ cu, u16* __restrict__ dqkv,
+                                                           int nq, int nkv, int total, float sl2, float scale,
+                                                           int causal, u16* __restrict__ dst, int lp) {
+  constexpr int NT = 256, TB = 64 * ROWB;
+  __shared__ __attribute__((aligned(16))) char smem[2 * TB + 2 * 64 * 4];
+  char* Qs = smem;
+  char* Os = smem + TB;
+  float* Ls = (float*)(smem + 2 * TB);
+  float* Dl = Ls + 64;
+  const int kvh = blockIdx.x, b = blockIdx.y, kb = blockIdx.z;
+  const int start = cu[b], len = cu[b + 1] - start;
+  const int k0 = kb * 64;
+  if (k0 >= len) return;
+  const int rep = nq / nkv;
+  const long ld = (long)(nq + 2 * nkv) * D;
+  const long ldo = (long)nq * D;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, g = lane >> 4;
+  const int wfirst = k0 + wave * 16;
+  const int key = wfirst + (lane & 15);
+  const bool kok = key < len;
+  const int qt0 = causal ? kb : 0;
+  const int nqt = (len + 63) / 64;
+  const int nt = nqt - qt0;        // query tiles per head
+  const int niter = rep * nt;
+  Offs off;
+  off.init(lane);
+  // iteration it -> head h = kvh * rep + it / nt, query tile qt0 + it % nt (kept incrementally)
+  int h = kvh * rep, qt = qt0;
+  {
+    const int q0 = qt0 * 64, qv = len - q0;
+    Stage<64, NT> tq, to;
+    tq.load(qkv + (long)(start + q0) * ld + h * D, ld, qv, tid);
+    to.load(dout + (long)(start + q0) * ldo + h * D, ldo, qv, tid);
+    tq.store(Qs, tid);
+    to.store(Os, tid);
+    if (tid < 64) {
+      Ls[tid] = tid < qv ? lse[(long)h * total + start + q0 + tid] * LOG2E : 0.f;
+      Dl[tid] = tid < qv ? delta[(long)h * total + start + q0 + tid] : 0.f;
+    }
+  }
+  bf16x8 kf[4], vf[4];
+  {
+    const u16* kp = qkv + (long)(start + key) * ld + (nq + kvh) * D + 8 * g;
+    const u16* vp = qkv + (long)(start + key) * ld + (nq + nkv + kvh) * D + 8 * g;
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      kf[s] = load_frag_global(kp + 32 * s, kok);
+      vf[s] = load_frag_global(vp + 32 * s, kok);
+    }
+  }
+  f32x4 dk[8], dv[8];
+#pragma unroll
+  for (int dt = 0; dt < 8; ++dt) {
+    dk[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
+    dv[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
+  }
+  __syncthreads();
+  for (int it = 0; it < niter; ++it) {
+    const int q0 = qt * 64;
+    const bool pre = it + 1 < niter;
+    int hn = h, qtn = qt + 1;
+    if (qtn == nqt) {
+      qtn = qt0;
+      ++hn;
+    }
+    Stage<64, NT> tq, to;
+    float pl = 0.f, pd = 0.f;
+    if (pre) {
+      const int qn = qtn * 64, qv = len - qn;
+      tq.load(qkv + (long)(start + qn) * ld + hn * D, ld, qv, tid);
+      to.load(dout + (long)(start + qn) * ldo + hn * D, ldo, qv, tid);
+      if (tid < 64 && tid < qv) {
+        pl = lse[(long)hn * total + start + qn + tid] * LOG2E;
+        pd = delta[(long)hn * total + start + qn + tid];
+      }
+    }
+    if (!causal || wfirst <= q0 + 63) {
+      f32x4 sc[4], dp[4];
+#pragma unroll
+      for (int mt = 0; mt < 4; ++mt) {
+        sc[mt] = f32x4{0.f, 0.f, 0.f, 0.f};
+        dp[mt] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+          sc[mt] = mfma(lds_row(Qs, off.row[s] + mt * 16 * ROWB), kf[s], sc[mt]);
+          dp[mt] = mfma(lds_row(Os, off.row[s] + mt * 16 * ROWB), vf[s], dp[mt]);
+        }
+      }
+      const bool need_mask = (q0 + 64 > len) || (causal && wfirst + 15 > q0);
+#pragma unroll
+      for (int mt = 0; mt < 4; ++mt) {
+        const float4 L4 = *(const float4*)(Ls + 16 * mt + 4 * g);
+        const float4 D4 = *(const float4*)(Dl + 16 * mt + 4 * g);
+        const float Lv[4] = {L4.x, L4.y, L4.z, L4.w}, Dv[4] = {D4.x, D4.y, D4.z, D4.w};
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          float p = exp2f(fmaf(sc[mt][i], sl2, -Lv[i]));
+          if (need_mask) {
+            const int q = q0 + 16 * mt + 4 * g + i;
+            if (q >= len || (causal && key > q)) p = 0.f;
+          }
+          sc[mt][i] = p;
+          dp[mt][i] = p * (dp[mt][i] - Dv[i]);
+        }
+      }
+      if (dst != nullptr && kok) {
+        u16* drow = dst + ((long)(b * nq + h) * lp + key) * lp + q0 + 4 * g;
+#pragma unroll
+        for (int mt = 0; mt < 4; ++mt) store4(drow + 16 * mt, dp[mt], 1.f);
+      }
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        const bf16x8 pb = pack_acc(sc[2 * ks], sc[2 * ks + 1]);
+        const bf16x8 db = pack_acc(dp[2 * ks], dp[2 * ks + 1]);
+#pragma unroll
+        for (int dt = 0; dt < 8; ++dt) {
+          dv[dt] = mfma(lds_tr(Os, off.tr[dt] + ks * 32 * ROWB), pb, dv[dt]);
+          dk[dt] = mfma(lds_tr(Qs, off.tr[dt] + ks * 32 * ROWB), db, dk[dt]);
+        }
+      }
+    }
+    if (pre) {
+      __syncthreads();
+      tq.store(Qs, tid);
+      to.store(Os, tid);
+      if (tid < 64) {
+        Ls[tid] = pl;
+        Dl[tid] = pd;
+      }
+    }
+    __syncthreads();
+    h = hn;
+    qt = qtn;
+  }
+  if (!kok) return;
+  u16* kp = dqkv + (long)(start + key) * ld + (nq + kvh) * D + 4 * g;
+  u16* vp = dqkv + (long)(start + key) * ld + (nq + nkv + kvh) * D + 4 * g;
+#pragma unroll
+  for (int dt = 0; dt < 8; ++dt) {
+    store4(kp + 16 * dt, dk[dt], scale);
+    store4(vp + 16 * dt, dv[dt], 1.f);
+  }
+}
+
 }  // namespace attn
+
+// SFTAMD_ATTN_GQA=0: per-query-head dK/dV + fp32 partials + dkdv_reduce (v4) instead of the GQA-grouped v5 kernel
+static bool attn_gqa_grouped() {
+  const char* e = std::getenv("SFTAMD_ATTN_GQA");
+  return !(e && e[0] == '0');
+}
 
 static void check_attn_args(const at::Tensor& qkv, const at::Tensor& cu, int64_t nq, int64_t nkv, int64_t hd) {
   SFT_CHECK_CUDA(qkv);
@@ -1735,15 +1895,25 @@ at::Tensor flash_bwd(const at::Tensor& dout, const at::Tensor& qkv, const at::Te
   if (attn_impl() >= 3 && !side && ds_bytes <= attn_ds_budget() && hd == 128) {
     const int rep = nq / nkv;
     auto dst = at::empty({ds_bytes / 2}, qkv.options());
+    const bool grouped = rep > 1 && attn_gqa_grouped();
     at::Tensor part;
-    if (rep > 1) part = at::empty({(long)rep * total * 2 * nkv * hd}, qkv.options().dtype(at::kFloat));
-    dim3 gk3(nq, nseq, (max_seqlen + 63) / 64);
-    attn::bwd_dkdv3_kernel<<<gk3, 256, 0, cur_stream()>>>(
-        (const u16*)qkv.data_ptr(), (const u16*)dout.data_ptr(), lse.data_ptr<float>(), delta.data_ptr<float>(),
-        cu_c.data_ptr<int>(), rep > 1 ? part.data_ptr<float>() : nullptr, (u16*)dqkv.data_ptr(), nq, nkv, total, sl2,
-        (float)scale, causal ? 1 : 0, (u16*)dst.data_ptr(), (int)lp);
-    SFT_LAUNCH_CHECK();
-    if (rep > 1) {
+    if (grouped) {
+      dim3 gk5(nkv, nseq, (max_seqlen + 63) / 64);
+      attn::bwd_dkdv5_kernel<<<gk5, 256, 0, cur_stream()>>>(
+          (const u16*)qkv.data_ptr(), (const u16*)dout.data_ptr(), lse.data_ptr<float>(), delta.data_ptr<float>(),
+          cu_c.data_ptr<int>(), (u16*)dqkv.data_ptr(), nq, nkv, total, sl2, (float)scale, causal ? 1 : 0,
+          (u16*)dst.data_ptr(), (int)lp);
+      SFT_LAUNCH_CHECK();
+    } else {
+      if (rep > 1) part = at::empty({(long)rep * total * 2 * nkv * hd}, qkv.options().dtype(at::kFloat));
+      dim3 gk3(nq, nseq, (max_seqlen + 63) / 64);
+      attn::bwd_dkdv3_kernel<<<gk3, 256, 0, cur_stream()>>>(
+          (const u16*)qkv.data_ptr(), (const u16*)dout.data_ptr(), lse.data_ptr<float>(), delta.data_ptr<float>(),
+          cu_c.data_ptr<int>(), rep > 1 ? part.data_ptr<float>() : nullptr, (u16*)dqkv.data_ptr(), nq, nkv, total, sl2,
+          (float)scale, causal ? 1 : 0, (u16*)dst.data_ptr(), (int)lp);
+      SFT_LAUNCH_CHECK();
+    }
+    if (rep > 1 && !grouped) {
       const long nvec = (long)total * 2 * nkv * hd / 8;
       const int grid = (int)std::min<long>((nvec + 255) / 256, 2048);
       attn::dkdv_reduce_kernel<<<grid, 256, 0, cur_stream()>>>(part.data_ptr<float>(), (u16*)dqkv.data_ptr(), total,
@@ -1766,15 +1936,24 @@ at::Tensor flash_bwd(const at::Tensor& dout, const at::Tensor& qkv, const at::Te
         (const u16*)qkv.data_ptr(), (const u16*)dout.data_ptr(), lse.data_ptr<float>(), delta.data_ptr<float>(),
         cu_c.data_ptr<int>(), (u16*)dqkv.data_ptr(), nq, nkv, total, sl2, (float)scale, causal ? 1 : 0);
     SFT_LAUNCH_CHECK();
+    const bool grouped = rep > 1 && attn_gqa_grouped();
     at::Tensor part;
-    if (rep > 1) part = at::empty({(long)rep * total * 2 * nkv * hd}, qkv.options().dtype(at::kFloat));
-    dim3 gk3(nq, nseq, (max_seqlen + 63) / 64);
-    attn::bwd_dkdv3_kernel<<<gk3, 256, 0, cur_stream()>>>(
-        (const u16*)qkv.data_ptr(), (const u16*)dout.data_ptr(), lse.data_ptr<float>(), delta.data_ptr<float>(),
-        cu_c.data_ptr<int>(), rep > 1 ? part.data_ptr<float>() : nullptr, (u16*)dqkv.data_ptr(), nq, nkv, total, sl2,
-        (float)scale, causal ? 1 : 0);
-    SFT_LAUNCH_CHECK();
-    if (rep > 1) {
+    if (grouped) {
+      dim3 gk5(nkv, nseq, (max_seqlen + 63) / 64);
+      attn::bwd_dkdv5_kernel<<<gk5, 256, 0, cur_stream()>>>(
+          (const u16*)qkv.data_ptr(), (const u16*)dout.data_ptr(), lse.data_ptr<float>(), delta.data_ptr<float>(),
+          cu_c.data_ptr<int>(), (u16*)dqkv.data_ptr(), nq, nkv, total, sl2, (float)scale, causal ? 1 : 0, nullptr, 0);
+      SFT_LAUNCH_CHECK();
+    } else {
+      if (rep > 1) part = at::empty({(long)rep * total * 2 * nkv * hd}, qkv.options().dtype(at::kFloat));
+      dim3 gk3(nq, nseq, (max_seqlen + 63) / 64);
+      attn::bwd_dkdv3_kernel<<<gk3, 256, 0, cur_stream()>>>(
+          (const u16*)qkv.data_ptr(), (const u16*)dout.data_ptr(), lse.data_ptr<float>(), delta.data_ptr<float>(),
+          cu_c.data_ptr<int>(), rep > 1 ? part.data_ptr<float>() : nullptr, (u16*)dqkv.data_ptr(), nq, nkv, total, sl2,
+          (float)scale, causal ? 1 : 0);
+      SFT_LAUNCH_CHECK();
+    }
+    if (rep > 1 && !grouped) {
       const long nvec = (long)total * 2 * nkv * hd / 8;
       const int grid = (int)std::min<long>((nvec + 255) / 256, 2048);
       attn::dkdv_reduce_kernel<<<grid, 256, 0, cur_stream()>>>(part.data_ptr<float>(), (u16*)dqkv.data_ptr(), total,
