@@ -1515,49 +1515,53 @@ __global__ __launch_bounds__(256, 2) void bwd_dkdv3_kernel(const u16* __restrict
 // registers across heads. dK/dV are written once, in bf16, straight into dqkv: no rep x [total, 2*nkv*128] fp32
 // partial slabs (134 MB written + re-read at 16 x 512 tokens, 16q/4kv) and no dkdv_reduce pass. The per-tile
 // math (S^T, dP^T, dS^T store for dq4) is bwd_dkdv3_kernel's; the iteration space is flattened over
-// (head, query tile) so the register prefetch of the next tile crosses head boundaries. Causal imbalance
-// (key block 0 walks rep x nqt tiles) is absorbed by the dispatch order: blockIdx.z = key block, heaviest first.
-__global__ __launch_bounds__(256, 2) void bwd_dkdv5_kernel(const u16* __restrict__ qkv, const u16* __restrict__ dout,
-                                                           const float* __restrict__ lse,
-                                                           const float* __restrict__ delta,
-                                                           const int* __restrict__ cu, u16* __restrict__ dqkv,
-                                                           int nq, int nkv, int total, float sl2, float scale,
-                                                           int causal, u16* __restrict__ dst, int lp) {
-  constexpr int NT = 256, TB = 64 * ROWB;
-  __shared__ __attribute__((aligned(16))) char smem[2 * TB + 2 * 64 * 4];
-  char* Qs = smem;
-  char* Os = smem + TB;
-  float* Ls = (float*)(smem + 2 * TB);
+// (head, query tile) so the register prefetch of the next tile crosses head boundaries.
+// G = 2 (default when rep is even): the workgroup is two 4-wave groups over the SAME 64 keys, each walking half
+// of the heads with its own Q/dO LDS images; group 1 hands its fp32 dK/dV to group 0 through LDS at the end.
+// That halves the serial chain of the causally heaviest key block (block 0 walks rep x nqt tiles), which is what
+// bounds this kernel: at 16 x 512 tokens the MFMA work alone is ~18 us, one tile step ~3 us of latency.
+// blockIdx.z = key block, heaviest first.
+template <int G>
+__global__ __launch_bounds__(256 * G, G == 1 ? 2 : 1) void bwd_dkdv5_kernel(
+    const u16* __restrict__ qkv, const u16* __restrict__ dout, const float* __restrict__ lse,
+    const float* __restrict__ delta, const int* __restrict__ cu, u16* __restrict__ dqkv, int nq, int nkv, int total,
+    float sl2, float scale, int causal, u16* __restrict__ dst, int lp) {
+  constexpr int NT = 256, TB = 64 * ROWB, GB = 2 * TB + 2 * 64 * 4;  // per group: Q, dO images + lse, delta
+  __shared__ __attribute__((aligned(16))) char smem[G * GB];
+  const int tid = threadIdx.x, grp = tid >> 8, gtid = tid & 255;
+  char* Qs = smem + grp * GB;
+  char* Os = Qs + TB;
+  float* Ls = (float*)(Qs + 2 * TB);
   float* Dl = Ls + 64;
   const int kvh = blockIdx.x, b = blockIdx.y, kb = blockIdx.z;
   const int start = cu[b], len = cu[b + 1] - start;
   const int k0 = kb * 64;
   if (k0 >= len) return;
-  const int rep = nq / nkv;
+  const int rep = nq / nkv, hpg = rep / G;  // heads per group
   const long ld = (long)(nq + 2 * nkv) * D;
   const long ldo = (long)nq * D;
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, g = lane >> 4;
+  const int lane = tid & 63, wave = (tid >> 6) & 3, g = lane >> 4;
   const int wfirst = k0 + wave * 16;
   const int key = wfirst + (lane & 15);
   const bool kok = key < len;
   const int qt0 = causal ? kb : 0;
   const int nqt = (len + 63) / 64;
   const int nt = nqt - qt0;        // query tiles per head
-  const int niter = rep * nt;
+  const int niter = hpg * nt;      // the same in every group: the loop's barriers line up
   Offs off;
   off.init(lane);
-  // iteration it -> head h = kvh * rep + it / nt, query tile qt0 + it % nt (kept incrementally)
-  int h = kvh * rep, qt = qt0;
+  // iteration it -> head h = kvh * rep + grp * hpg + it / nt, query tile qt0 + it % nt (kept incrementally)
+  int h = kvh * rep + grp * hpg, qt = qt0;
   {
     const int q0 = qt0 * 64, qv = len - q0;
     Stage<64, NT> tq, to;
-    tq.load(qkv + (long)(start + q0) * ld + h * D, ld, qv, tid);
-    to.load(dout + (long)(start + q0) * ldo + h * D, ldo, qv, tid);
-    tq.store(Qs, tid);
-    to.store(Os, tid);
-    if (tid < 64) {
-      Ls[tid] = tid < qv ? lse[(long)h * total + start + q0 + tid] * LOG2E : 0.f;
-      Dl[tid] = tid < qv ? delta[(long)h * total + start + q0 + tid] : 0.f;
+    tq.load(qkv + (long)(start + q0) * ld + h * D, ld, qv, gtid);
+    to.load(dout + (long)(start + q0) * ldo + h * D, ldo, qv, gtid);
+    tq.store(Qs, gtid);
+    to.store(Os, gtid);
+    if (gtid < 64) {
+      Ls[gtid] = gtid < qv ? lse[(long)h * total + start + q0 + gtid] * LOG2E : 0.f;
+      Dl[gtid] = gtid < qv ? delta[(long)h * total + start + q0 + gtid] : 0.f;
     }
   }
   bf16x8 kf[4], vf[4];
@@ -1589,11 +1593,11 @@ __global__ __launch_bounds__(256, 2) void bwd_dkdv5_kernel(const u16* __restrict
     float pl = 0.f, pd = 0.f;
     if (pre) {
       const int qn = qtn * 64, qv = len - qn;
-      tq.load(qkv + (long)(start + qn) * ld + hn * D, ld, qv, tid);
-      to.load(dout + (long)(start + qn) * ldo + hn * D, ldo, qv, tid);
-      if (tid < 64 && tid < qv) {
-        pl = lse[(long)hn * total + start + qn + tid] * LOG2E;
-        pd = delta[(long)hn * total + start + qn + tid];
+      tq.load(qkv + (long)(start + qn) * ld + hn * D, ld, qv, gtid);
+      to.load(dout + (long)(start + qn) * ldo + hn * D, ldo, qv, gtid);
+      if (gtid < 64 && gtid < qv) {
+        pl = lse[(long)hn * total + start + qn + gtid] * LOG2E;
+        pd = delta[(long)hn * total + start + qn + gtid];
       }
     }
     if (!causal || wfirst <= q0 + 63) {
@@ -1643,16 +1647,37 @@ __global__ __launch_bounds__(256, 2) void bwd_dkdv5_kernel(const u16* __restrict
     }
     if (pre) {
       __syncthreads();
-      tq.store(Qs, tid);
-      to.store(Os, tid);
-      if (tid < 64) {
-        Ls[tid] = pl;
-        Dl[tid] = pd;
+      tq.store(Qs, gtid);
+      to.store(Os, gtid);
+      if (gtid < 64) {
+        Ls[gtid] = pl;
+        Dl[gtid] = pd;
       }
     }
     __syncthreads();
     h = hn;
     qt = qtn;
+  }
+  if constexpr (G == 2) {
+    // group 1 -> LDS (fp32, [wave][dt][lane] float4: consecutive lanes, conflict-free) -> group 0 adds.
+    // 2 x 4 waves x 8 x 64 x 16 B = 64 KB = both groups' Q/dO images, free after the loop's last barrier.
+    float4* xk = (float4*)smem;
+    float4* xv = xk + 4 * 8 * 64;
+    if (grp == 1) {
+#pragma unroll
+      for (int dt = 0; dt < 8; ++dt) {
+        xk[(wave * 8 + dt) * 64 + lane] = make_float4(dk[dt][0], dk[dt][1], dk[dt][2], dk[dt][3]);
+        xv[(wave * 8 + dt) * 64 + lane] = make_float4(dv[dt][0], dv[dt][1], dv[dt][2], dv[dt][3]);
+      }
+    }
+    __syncthreads();
+    if (grp == 1) return;
+#pragma unroll
+    for (int dt = 0; dt < 8; ++dt) {
+      const float4 a = xk[(wave * 8 + dt) * 64 + lane], c = xv[(wave * 8 + dt) * 64 + lane];
+      dk[dt] += f32x4{a.x, a.y, a.z, a.w};
+      dv[dt] += f32x4{c.x, c.y, c.z, c.w};
+    }
   }
   if (!kok) return;
   u16* kp = dqkv + (long)(start + key) * ld + (nq + kvh) * D + 4 * g;
@@ -1662,6 +1687,22 @@ __global__ __launch_bounds__(256, 2) void bwd_dkdv5_kernel(const u16* __restrict
     store4(kp + 16 * dt, dk[dt], scale);
     store4(vp + 16 * dt, dv[dt], 1.f);
   }
+}
+
+// host launcher: G = 2 head groups when rep is even (SFTAMD_ATTN_GQA_SPLIT=0 forces 1)
+static void launch_dkdv5(const u16* qkv, const u16* dout, const float* lse, const float* delta, const int* cu,
+                         u16* dqkv, int nq, int nkv, int total, int nseq, int max_seqlen, float sl2, float scale,
+                         int causal, u16* dst, int lp, hipStream_t st) {
+  const int rep = nq / nkv;
+  const char* e = std::getenv("SFTAMD_ATTN_GQA_SPLIT");
+  const bool split = rep % 2 == 0 && !(e && e[0] == '0');
+  dim3 grid(nkv, nseq, (max_seqlen + 63) / 64);
+  if (split)
+    bwd_dkdv5_kernel<2><<<grid, 512, 0, st>>>(qkv, dout, lse, delta, cu, dqkv, nq, nkv, total, sl2, scale, causal,
+                                              dst, lp);
+  else
+    bwd_dkdv5_kernel<1><<<grid, 256, 0, st>>>(qkv, dout, lse, delta, cu, dqkv, nq, nkv, total, sl2, scale, causal,
+                                              dst, lp);
 }
 
 }  // namespace attn
@@ -1898,11 +1939,9 @@ at::Tensor flash_bwd(const at::Tensor& dout, const at::Tensor& qkv, const at::Te
     const bool grouped = rep > 1 && attn_gqa_grouped();
     at::Tensor part;
     if (grouped) {
-      dim3 gk5(nkv, nseq, (max_seqlen + 63) / 64);
-      attn::bwd_dkdv5_kernel<<<gk5, 256, 0, cur_stream()>>>(
-          (const u16*)qkv.data_ptr(), (const u16*)dout.data_ptr(), lse.data_ptr<float>(), delta.data_ptr<float>(),
-          cu_c.data_ptr<int>(), (u16*)dqkv.data_ptr(), nq, nkv, total, sl2, (float)scale, causal ? 1 : 0,
-          (u16*)dst.data_ptr(), (int)lp);
+      attn::launch_dkdv5((const u16*)qkv.data_ptr(), (const u16*)dout.data_ptr(), lse.data_ptr<float>(),
+                         delta.data_ptr<float>(), cu_c.data_ptr<int>(), (u16*)dqkv.data_ptr(), nq, nkv, total, nseq,
+                         max_seqlen, sl2, (float)scale, causal ? 1 : 0, (u16*)dst.data_ptr(), (int)lp, cur_stream());
       SFT_LAUNCH_CHECK();
     } else {
       if (rep > 1) part = at::empty({(long)rep * total * 2 * nkv * hd}, qkv.options().dtype(at::kFloat));
@@ -1939,10 +1978,9 @@ at::Tensor flash_bwd(const at::Tensor& dout, const at::Tensor& qkv, const at::Te
     const bool grouped = rep > 1 && attn_gqa_grouped();
     at::Tensor part;
     if (grouped) {
-      dim3 gk5(nkv, nseq, (max_seqlen + 63) / 64);
-      attn::bwd_dkdv5_kernel<<<gk5, 256, 0, cur_stream()>>>(
-          (const u16*)qkv.data_ptr(), (const u16*)dout.data_ptr(), lse.data_ptr<float>(), delta.data_ptr<float>(),
-          cu_c.data_ptr<int>(), (u16*)dqkv.data_ptr(), nq, nkv, total, sl2, (float)scale, causal ? 1 : 0, nullptr, 0);
+      attn::launch_dkdv5((const u16*)qkv.data_ptr(), (const u16*)dout.data_ptr(), lse.data_ptr<float>(),
+                         delta.data_ptr<float>(), cu_c.data_ptr<int>(), (u16*)dqkv.data_ptr(), nq, nkv, total, nseq,
+                         max_seqlen, sl2, (float)scale, causal ? 1 : 0, nullptr, 0, cur_stream());
       SFT_LAUNCH_CHECK();
     } else {
       if (rep > 1) part = at::empty({(long)rep * total * 2 * nkv * hd}, qkv.options().dtype(at::kFloat));

@@ -213,14 +213,17 @@ def test_flash_attention_bwd_materialised_ds_vs_recompute(causal, ds_mb):
 
 @pytest.mark.parametrize("causal", [True, False])
 @pytest.mark.parametrize("ds_mb", ["", "0"])
-@pytest.mark.parametrize("gqa", ["1", "0"])
+@pytest.mark.parametrize("gqa", ["1", "split0", "0"])
 def test_flash_attention_bwd_gqa_grouped(causal, ds_mb, gqa, monkeypatch):
-    """dK/dV with the GQA-grouped kernel (one workgroup walks every query head of its kv head, default) and the
-    per-head kernel + fp32 partial reduction (SFTAMD_ATTN_GQA=0), on both dq paths, vs the fp32 reference."""
-    monkeypatch.setenv("SFTAMD_ATTN_GQA", gqa)
+    """dK/dV with the GQA-grouped kernel (one workgroup walks every query head of its kv head; default: two
+    4-wave head groups combined through LDS, "split0" = one group) and the per-head kernel + fp32 partial
+    reduction (SFTAMD_ATTN_GQA=0), on both dq paths, vs the fp32 reference (rep 4 and odd rep 3)."""
+    monkeypatch.setenv("SFTAMD_ATTN_GQA", "0" if gqa == "0" else "1")
+    monkeypatch.setenv("SFTAMD_ATTN_GQA_SPLIT", "0" if gqa == "split0" else "1")
     _attn_case([100, 255, 64, 1, 300, 129], 8, 2, causal, "1", "3", "", ds_mb)
     _attn_case([512, 511, 7], 16, 4, causal, "1", "3", "", ds_mb)
     _attn_case([200, 65], 12, 3, causal, "1", "3", "", ds_mb)
+    _attn_case([130, 64], 12, 2, causal, "1", "3", "", ds_mb)
 
 
 def test_flash_attention_mha_and_long():

@@ -40,14 +40,16 @@ def timeit(fn, n=20):
 CFGS = [("1", ""), ("2", "8,1"), ("3", "8,1"), ("3", "4,1"), ("4", ""), ("3", "8,1,serial"), ("3", "8,1,ds"),
         ("3", "8,1,ds,perhead")]
 if os.environ.get("ATTN_QUICK"):
-    CFGS = [("3", "8,1,serial"), ("3", "8,1,ds,perhead"), ("3", "8,1,ds")]
+    CFGS = [("3", "8,1,serial"), ("3", "8,1,ds,perhead"), ("3", "8,1,ds,nosplit"), ("3", "8,1,ds")]
 res = {}
 ref = None
 for rnd in range(3):
     for impl, cfg in CFGS:
         os.environ["SFTAMD_ATTN_IMPL"] = impl
         os.environ["SFTAMD_ATTN_GQA"] = "0" if cfg.endswith(",perhead") else "1"
-        cfg = cfg.replace(",perhead", "")
+        os.environ["SFTAMD_ATTN_GQA_SPLIT"] = "0" if cfg.endswith(",nosplit") else "1"
+        tag = cfg
+        cfg = cfg.replace(",perhead", "").replace(",nosplit", "")
         os.environ["SFTAMD_ATTN_CFG"] = cfg.replace(",serial", "").replace(",ds", "")
         os.environ["SFTAMD_ATTN_CONC"] = "0" if cfg.endswith("serial") or cfg.endswith("ds") else "1"
         os.environ["SFTAMD_ATTN_DS_MB"] = "" if cfg.endswith("ds") else "0"
@@ -61,7 +63,7 @@ for rnd in range(3):
             assert eo < 1e-2 and ed < 1e-2, (impl, cfg, eo, ed)
         tf = timeit(lambda: ops.flash_fwd(qkv, cu, T, NQ, NKV, D, sc, True))
         tb = timeit(lambda: ops.flash_bwd(dout, qkv, out, lse, cu, T, NQ, NKV, D, sc, True))
-        res.setdefault(impl + ":" + cfg + (",perhead" if os.environ["SFTAMD_ATTN_GQA"] == "0" else ""), []).append((tf, tb))
+        res.setdefault(impl + ":" + tag, []).append((tf, tb))
 for impl, v in res.items():
     tf = statistics.median(x[0] for x in v)
     tb = statistics.median(x[1] for x in v)
