@@ -2,16 +2,14 @@
 // longest sample (optionally to a multiple of 64 for MFMA-friendly M), HF label semantics
 // (pads -> -100), and padding-free packing into varlen streams with cu_seqlens/position_ids.
 // Token storage is one flat int32 array + int64 offsets (CSR), so a micro-batch is assembled
-// with memcpy-speed loops instead of per-sample Python tensors.
+// with memcpy-speed loops instead of per-sample Python tensors. The loops live in collate_core.h
+// (torch-free, also built under host ASan/UBSan by tests/test_sanitizers_cpu.py).
 #include <torch/library.h>
 #include <ATen/ATen.h>
 
-#include <algorithm>
-#include <vector>
+#include "collate_core.h"
 
 namespace sftamd {
-
-static inline int64_t round_up(int64_t x, int64_t m) { return m > 1 ? (x + m - 1) / m * m : x; }
 
 std::tuple<at::Tensor, at::Tensor, at::Tensor> pad_batch(const at::Tensor& tokens, const at::Tensor& offsets,
                                                          const at::Tensor& order, int64_t pad_id, int64_t pad_multiple,
@@ -21,34 +19,15 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor> pad_batch(const at::Tensor& token
   auto tok = tokens.contiguous();
   auto off = offsets.contiguous();
   auto ord = order.contiguous();
-  const int32_t* tp = tok.data_ptr<int32_t>();
-  const int64_t* op = off.data_ptr<int64_t>();
-  const int64_t* orp = ord.data_ptr<int64_t>();
   const int64_t B = ord.numel();
-  std::vector<int64_t> lens(B);
-  int64_t T = 1;
-  for (int64_t b = 0; b < B; ++b) {
-    const int64_t i = orp[b];
-    int64_t l = op[i + 1] - op[i];
-    if (max_length > 0) l = std::min(l, max_length);
-    lens[b] = l;
-    T = std::max(T, l);
-  }
-  T = round_up(T, pad_multiple);
+  std::vector<int64_t> lens;
+  const int64_t T = collate::pad_width(off.data_ptr<int64_t>(), ord.data_ptr<int64_t>(), B, max_length, pad_multiple,
+                                       lens);
   auto ids = at::full({B, T}, pad_id, at::kLong);
   auto labels = at::full({B, T}, -100, at::kLong);
   auto lengths = at::empty({B}, at::kInt);
-  int64_t* ip = ids.data_ptr<int64_t>();
-  int64_t* lp = labels.data_ptr<int64_t>();
-  int32_t* lenp = lengths.data_ptr<int32_t>();
-  for (int64_t b = 0; b < B; ++b) {
-    const int32_t* src = tp + op[orp[b]];
-    for (int64_t t = 0; t < lens[b]; ++t) {
-      ip[b * T + t] = src[t];
-      lp[b * T + t] = src[t];
-    }
-    lenp[b] = (int32_t)lens[b];
-  }
+  collate::pad_fill(tok.data_ptr<int32_t>(), off.data_ptr<int64_t>(), ord.data_ptr<int64_t>(), lens, T,
+                    ids.data_ptr<int64_t>(), labels.data_ptr<int64_t>(), lengths.data_ptr<int32_t>());
   return {ids, labels, lengths};
 }
 
@@ -63,45 +42,18 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor, at::Tensor> pack_sequ
   auto tok = tokens.contiguous();
   auto off = offsets.contiguous();
   auto ord = order.contiguous();
-  const int32_t* tp = tok.data_ptr<int32_t>();
-  const int64_t* op = off.data_ptr<int64_t>();
-  const int64_t* orp = ord.data_ptr<int64_t>();
-  const int64_t N = ord.numel();
-  std::vector<int64_t> cu{0};
-  int64_t used = 0, M = 0;
-  for (; used < N; ++used) {
-    const int64_t i = orp[used];
-    int64_t l = op[i + 1] - op[i];
-    if (max_tokens > 0) l = std::min(l, max_tokens);
-    if (max_tokens > 0 && M + l > max_tokens && used > 0) break;
-    M += l;
-    cu.push_back(M);
-  }
-  const int64_t Mp = round_up(std::max<int64_t>(M, 1), pad_multiple);
+  std::vector<int64_t> cu;
+  const int64_t used = collate::pack_plan(off.data_ptr<int64_t>(), ord.data_ptr<int64_t>(), ord.numel(), max_tokens, cu);
+  const int64_t M = cu.back();
+  const int64_t Mp = collate::round_up(std::max<int64_t>(M, 1), pad_multiple);
   auto ids = at::full({Mp}, pad_id, at::kLong);
   auto labels = at::full({Mp}, -100, at::kLong);
   auto pos = at::zeros({Mp}, at::kLong);
   const int64_t nseq = (int64_t)cu.size() - 1 + (Mp > M ? 1 : 0);
   auto cus = at::empty({nseq + 1}, at::kInt);
-  int64_t* ip = ids.data_ptr<int64_t>();
-  int64_t* lp = labels.data_ptr<int64_t>();
-  int64_t* pp = pos.data_ptr<int64_t>();
-  int32_t* cp = cus.data_ptr<int32_t>();
-  for (int64_t s = 0; s + 1 < (int64_t)cu.size(); ++s) {
-    const int32_t* src = tp + op[orp[s]];
-    const int64_t b = cu[s], l = cu[s + 1] - cu[s];
-    for (int64_t t = 0; t < l; ++t) {
-      ip[b + t] = src[t];
-      pp[b + t] = t;
-      lp[b + t] = (t + 1 < l) ? src[t + 1] : -100;
-    }
-    cp[s] = (int32_t)cu[s];
-  }
-  cp[cu.size() - 1] = (int32_t)M;
-  if (Mp > M) {  // tail padding is its own (fully ignored) sequence
-    for (int64_t t = M; t < Mp; ++t) pp[t] = t - M;
-    cp[nseq] = (int32_t)Mp;
-  }
+  collate::pack_fill(tok.data_ptr<int32_t>(), off.data_ptr<int64_t>(), ord.data_ptr<int64_t>(), cu, Mp,
+                     ids.data_ptr<int64_t>(), labels.data_ptr<int64_t>(), pos.data_ptr<int64_t>(),
+                     cus.data_ptr<int32_t>());
   auto n_used = at::full({1}, used, at::kLong);
   return {ids, labels, cus, pos, n_used};
 }
