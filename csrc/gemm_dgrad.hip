@@ -513,17 +513,46 @@ at::Tensor dgrad_gemm(const at::Tensor& dy, const at::Tensor& w, const c10::opti
   }
   ea.out = (u16*)out.data_ptr();
   if (M == 0 || N == 0) return out;
-  auto run = [&](auto epi) {
+  // Wave-quantisation tail (256 x 256 configs): with nbn x nbm tiles over 256 CUs the last round is partial —
+  // the SmolLM3 down projection has 43 x 32 = 1376 tiles = 5.375 rounds, run as 6. When the leftover n-tiles fit
+  // one round as 256 x 128 half tiles, the whole rounds run as one launch over the leading columns and the leftover
+  // columns as a second launch of half tiles (5 + 0.5 rounds). Column sub-ranges are plain pointer offsets: the
+  // W columns (stride stays N), the output / gate / up columns (ea.N keeps the full width for the up half).
+  // SFTAMD_DGRAD_TAIL: 0 = off, 2 / 3 = the half-tile config (default 2).
+  auto run1 = [&](auto epi, int c, const at::Tensor& wv, const dgrad::EpiArgs& e) {
     constexpr int E = decltype(epi)::value;
-    switch (cfg) {
-      case 1: dgrad::launch<256, 256, 2, 4, 3, E>(dy, w, ea); break;
-      case 2: dgrad::launch<256, 128, 4, 2, 3, E>(dy, w, ea); break;
-      case 3: dgrad::launch<256, 128, 4, 2, 4, E>(dy, w, ea); break;
-      case 5: dgrad::launch<256, 256, 2, 4, 3, E, 1, false>(dy, w, ea); break;  // no sched_group_barrier pinning
-      case 6: dgrad::launch<256, 256, 2, 4, 4, E, 1, false>(dy, w, ea); break;
-      case 7: dgrad::launch2<256, 256, 2, 4, E>(dy, w, ea); break;
-      default: dgrad::launch<256, 256, 2, 4, 4, E>(dy, w, ea);
+    switch (c) {
+      case 1: dgrad::launch<256, 256, 2, 4, 3, E>(dy, wv, e); break;
+      case 2: dgrad::launch<256, 128, 4, 2, 3, E>(dy, wv, e); break;
+      case 3: dgrad::launch<256, 128, 4, 2, 4, E>(dy, wv, e); break;
+      case 5: dgrad::launch<256, 256, 2, 4, 3, E, 1, false>(dy, wv, e); break;  // no sched_group_barrier pinning
+      case 6: dgrad::launch<256, 256, 2, 4, 4, E, 1, false>(dy, wv, e); break;
+      case 7: dgrad::launch2<256, 256, 2, 4, E>(dy, wv, e); break;
+      default: dgrad::launch<256, 256, 2, 4, 4, E>(dy, wv, e);
     }
+  };
+  const int tail_cfg = [] {
+    const char* e = std::getenv("SFTAMD_DGRAD_TAIL");
+    return e && e[0] ? atoi(e) : 2;
+  }();
+  auto run = [&](auto epi) {
+    const long nbn = N / 256, nbm = M / 256, tiles = nbn * nbm;
+    const bool full = cfg != 2 && cfg != 3;
+    long main_n = 0;
+    if (full && tail_cfg >= 2 && tail_cfg <= 3 && tiles % 256 != 0 && 256 % nbm == 0) {
+      main_n = tiles / 256 * (256 / nbm);                  // n-tiles of the whole rounds
+      if ((nbn - main_n) * (M / 128) > 256) main_n = 0;      // the half tiles must fit one round
+    }
+    if (main_n <= 0) {
+      run1(epi, (int)cfg, w, ea);
+      return;
+    }
+    const long n_split = main_n * 256;
+    run1(epi, (int)cfg, w.narrow(1, 0, n_split), ea);
+    dgrad::EpiArgs et = ea;
+    et.out = ea.out + n_split;
+    if (et.gu != nullptr) et.gu = ea.gu + n_split;
+    run1(epi, tail_cfg, w.narrow(1, n_split, N - n_split), et);
   };
   if (cfg == 2 || cfg == 3) SFT_CHECK(M % 128 == 0, "dgrad_gemm: M multiple of 128");
   if (swiglu) run(std::integral_constant<int, dgrad::EPI_SWIGLU_BWD>());

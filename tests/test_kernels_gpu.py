@@ -527,6 +527,31 @@ def test_dgrad_gemm_plain(M, K, N, wpad):
         assert torch.equal(got, ramp.float() @ eye), cfg
 
 
+@pytest.mark.parametrize("M,K,N,swiglu", [(8192, 64, 11008, True), (2048, 96, 9472, False), (4096, 64, 4352, True)])
+def test_dgrad_gemm_wave_tail_split(M, K, N, swiglu, monkeypatch):
+    """Grids with a partial last round of 256 workgroups (SmolLM3 down projection: 43 x 32 tiles) run the whole
+    rounds as one launch and the leftover columns as 256 x 128 half tiles (SFTAMD_DGRAD_TAIL): bit-identical to the
+    single launch (same per-element fp32 sums), and equal to the fp32 reference."""
+    torch.manual_seed(2)
+    dy = torch.randn(M, K, device="cuda", dtype=torch.bfloat16)
+    w = (0.05 * torch.randn(K, N, device="cuda")).to(torch.bfloat16)
+    gu = torch.randn(M, 2 * N, device="cuda", dtype=torch.bfloat16) if swiglu else None
+    res = {}
+    for cfg in (0, 7) if K % 64 == 0 else (0,):
+        for tail in ("0", "2", "3"):
+            monkeypatch.setenv("SFTAMD_DGRAD_TAIL", tail)
+            res[tail] = _ext.ops().dgrad_gemm(dy, w, gu, cfg)
+        assert torch.equal(res["0"], res["2"]) and torch.equal(res["0"], res["3"]), cfg
+    dact = dy.float() @ w.float()
+    if swiglu:
+        g, u = gu.float().chunk(2, dim=-1)
+        s = torch.sigmoid(g)
+        want = torch.cat([dact * u * s * (1 + g * (1 - s)), dact * g * s], dim=-1)
+    else:
+        want = dact
+    assert rel_err(res["2"], want) < 1e-2
+
+
 @pytest.mark.parametrize("M,K,N", [(256, 256, 256), (512, 2048, 512), (256, 64, 768)])
 def test_dgrad_gemm_swiglu_bwd(M, K, N):
     """Down-projection dgrad with the SwiGLU backward fused into the epilogue == swiglu_bwd(dy @ w, gu) in fp32."""
