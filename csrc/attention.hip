@@ -123,6 +123,28 @@ __device__ __forceinline__ void store4(u16* p, const f32x4& v, float s) {
   *(uint2*)p = w;
 }
 
+// Store a lane's 8 x 4 head-dim values (columns 16 dt + 4g + i, p = row + 4g) with the rotate_half RoPE inverted
+// first — the backward of the forward rotation (x1, x2) -> (x1 c - x2 s, x2 c + x1 s) is
+// (g1, g2) -> (g1 c + g2 s, g2 c - g1 s). Columns c and c + 64 of a pair sit in the same lane (dt and dt + 4), so
+// the rotation is in-register, on the fp32 accumulators before the single bf16 rounding. cs / sn: this row's
+// [64] fp32 cos / sin table + 4g.
+__device__ __forceinline__ void store4_rope_bwd(u16* p, const f32x4 (&v)[8], float s, const float* cs, const float* sn) {
+#pragma unroll
+  for (int dt = 0; dt < 4; ++dt) {
+    const float4 c4 = *(const float4*)(cs + 16 * dt), s4 = *(const float4*)(sn + 16 * dt);
+    const float c[4] = {c4.x, c4.y, c4.z, c4.w}, n[4] = {s4.x, s4.y, s4.z, s4.w};
+    f32x4 lo, hi;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const float a = v[dt][i] * s, b = v[dt + 4][i] * s;
+      lo[i] = a * c[i] + b * n[i];
+      hi[i] = b * c[i] - a * n[i];
+    }
+    store4(p + 16 * dt, lo, 1.f);
+    store4(p + 16 * dt + 64, hi, 1.f);
+  }
+}
+
 // ------------------------------------------------------------------------------ forward
 // grid (q-blocks of 64, nq, nseq); 4 waves x 16 query rows. Per 64-key tile: S^T (16 MFMA),
 // online softmax in registers, O^T += V^T P^T (16 MFMA).
@@ -1187,7 +1209,9 @@ __global__ __launch_bounds__(NW * 64) void fwd4_kernel(const u16* __restrict__ q
 template <int NW>
 __global__ __launch_bounds__(NW * 64) void bwd_dq4_kernel(const u16* __restrict__ qkv, const u16* __restrict__ dst,
                                                           const int* __restrict__ cu, u16* __restrict__ dqkv, int nq,
-                                                          int nkv, int lp, float scale, int causal) {
+                                                          int nkv, int lp, float scale, int causal,
+                                                          const float* __restrict__ rcos = nullptr,
+                                                          const float* __restrict__ rsin = nullptr) {
   static_assert(NW == 8, "the dS^T image is 128 queries wide: 8 waves x 16 rows");
   constexpr int NT = NW * 64, BM = NW * 16, TB = 64 * ROWB;
   __shared__ __attribute__((aligned(16))) char smem[2 * TB];
@@ -1246,8 +1270,13 @@ __global__ __launch_bounds__(NW * 64) void bwd_dq4_kernel(const u16* __restrict_
   }
   if (qrow < len) {
     u16* qp = dqkv + (long)(start + qrow) * ld + h * D + 4 * g;
+    if (rcos != nullptr) {
+      const long tr = (long)(start + qrow) * (D / 2) + 4 * g;
+      store4_rope_bwd(qp, dq, scale, rcos + tr, rsin + tr);
+    } else {
 #pragma unroll
-    for (int dt = 0; dt < 8; ++dt) store4(qp + 16 * dt, dq[dt], scale);
+      for (int dt = 0; dt < 8; ++dt) store4(qp + 16 * dt, dq[dt], scale);
+    }
   }
 }
 
@@ -1525,7 +1554,8 @@ template <int G>
 __global__ __launch_bounds__(256 * G, G == 1 ? 2 : 1) void bwd_dkdv5_kernel(
     const u16* __restrict__ qkv, const u16* __restrict__ dout, const float* __restrict__ lse,
     const float* __restrict__ delta, const int* __restrict__ cu, u16* __restrict__ dqkv, int nq, int nkv, int total,
-    float sl2, float scale, int causal, u16* __restrict__ dst, int lp) {
+    float sl2, float scale, int causal, u16* __restrict__ dst, int lp, const float* __restrict__ rcos,
+    const float* __restrict__ rsin) {
   constexpr int NT = 256, TB = 64 * ROWB, GB = 2 * TB + 2 * 64 * 4;  // per group: Q, dO images + lse, delta
   __shared__ __attribute__((aligned(16))) char smem[G * GB];
   const int tid = threadIdx.x, grp = tid >> 8, gtid = tid & 255;
@@ -1682,6 +1712,13 @@ __global__ __launch_bounds__(256 * G, G == 1 ? 2 : 1) void bwd_dkdv5_kernel(
   if (!kok) return;
   u16* kp = dqkv + (long)(start + key) * ld + (nq + kvh) * D + 4 * g;
   u16* vp = dqkv + (long)(start + key) * ld + (nq + nkv + kvh) * D + 4 * g;
+  if (rcos != nullptr) {
+    const long tr = (long)(start + key) * (D / 2) + 4 * g;
+    store4_rope_bwd(kp, dk, scale, rcos + tr, rsin + tr);
+#pragma unroll
+    for (int dt = 0; dt < 8; ++dt) store4(vp + 16 * dt, dv[dt], 1.f);
+    return;
+  }
 #pragma unroll
   for (int dt = 0; dt < 8; ++dt) {
     store4(kp + 16 * dt, dk[dt], scale);
@@ -1692,17 +1729,18 @@ __global__ __launch_bounds__(256 * G, G == 1 ? 2 : 1) void bwd_dkdv5_kernel(
 // host launcher: G = 2 head groups when rep is even (SFTAMD_ATTN_GQA_SPLIT=0 forces 1)
 static void launch_dkdv5(const u16* qkv, const u16* dout, const float* lse, const float* delta, const int* cu,
                          u16* dqkv, int nq, int nkv, int total, int nseq, int max_seqlen, float sl2, float scale,
-                         int causal, u16* dst, int lp, hipStream_t st) {
+                         int causal, u16* dst, int lp, hipStream_t st, const float* rcos = nullptr,
+                         const float* rsin = nullptr) {
   const int rep = nq / nkv;
   const char* e = std::getenv("SFTAMD_ATTN_GQA_SPLIT");
   const bool split = rep % 2 == 0 && !(e && e[0] == '0');
   dim3 grid(nkv, nseq, (max_seqlen + 63) / 64);
   if (split)
     bwd_dkdv5_kernel<2><<<grid, 512, 0, st>>>(qkv, dout, lse, delta, cu, dqkv, nq, nkv, total, sl2, scale, causal,
-                                              dst, lp);
+                                              dst, lp, rcos, rsin);
   else
     bwd_dkdv5_kernel<1><<<grid, 256, 0, st>>>(qkv, dout, lse, delta, cu, dqkv, nq, nkv, total, sl2, scale, causal,
-                                              dst, lp);
+                                              dst, lp, rcos, rsin);
 }
 
 }  // namespace attn
@@ -1852,9 +1890,13 @@ std::tuple<at::Tensor, at::Tensor> flash_fwd(const at::Tensor& qkv, const at::Te
   return {out, lse};
 }
 
-at::Tensor flash_bwd(const at::Tensor& dout, const at::Tensor& qkv, const at::Tensor& out, const at::Tensor& lse,
-                     const at::Tensor& cu, int64_t max_seqlen, int64_t nq, int64_t nkv, int64_t hd, double scale,
-                     bool causal) {
+// rcos / rsin (optional, [total, hd / 2] fp32): apply the inverse rotate_half RoPE to the dq and dk heads in the
+// epilogues (v4 dq path + GQA-grouped dK/dV); sets rope_done. Other paths leave it to the caller.
+static at::Tensor flash_bwd_impl(const at::Tensor& dout, const at::Tensor& qkv, const at::Tensor& out,
+                                 const at::Tensor& lse, const at::Tensor& cu, int64_t max_seqlen, int64_t nq,
+                                 int64_t nkv, int64_t hd, double scale, bool causal, const float* rcos,
+                                 const float* rsin, bool& rope_done) {
+  rope_done = false;
   check_attn_args(qkv, cu, nq, nkv, hd);
   SFT_CHECK_CONTIG(dout);
   SFT_CHECK_CONTIG(out);
@@ -1937,11 +1979,13 @@ at::Tensor flash_bwd(const at::Tensor& dout, const at::Tensor& qkv, const at::Te
     const int rep = nq / nkv;
     auto dst = at::empty({ds_bytes / 2}, qkv.options());
     const bool grouped = rep > 1 && attn_gqa_grouped();
+    const bool rope = grouped && rcos != nullptr;
     at::Tensor part;
     if (grouped) {
       attn::launch_dkdv5((const u16*)qkv.data_ptr(), (const u16*)dout.data_ptr(), lse.data_ptr<float>(),
                          delta.data_ptr<float>(), cu_c.data_ptr<int>(), (u16*)dqkv.data_ptr(), nq, nkv, total, nseq,
-                         max_seqlen, sl2, (float)scale, causal ? 1 : 0, (u16*)dst.data_ptr(), (int)lp, cur_stream());
+                         max_seqlen, sl2, (float)scale, causal ? 1 : 0, (u16*)dst.data_ptr(), (int)lp, cur_stream(),
+                         rope ? rcos : nullptr, rope ? rsin : nullptr);
       SFT_LAUNCH_CHECK();
     } else {
       if (rep > 1) part = at::empty({(long)rep * total * 2 * nkv * hd}, qkv.options().dtype(at::kFloat));
@@ -1962,8 +2006,10 @@ at::Tensor flash_bwd(const at::Tensor& dout, const at::Tensor& qkv, const at::Te
     dim3 gq4(nq, nseq, (max_seqlen + 127) / 128);
     attn::bwd_dq4_kernel<8><<<gq4, 512, 0, cur_stream()>>>((const u16*)qkv.data_ptr(), (const u16*)dst.data_ptr(),
                                                            cu_c.data_ptr<int>(), (u16*)dqkv.data_ptr(), nq, nkv,
-                                                           (int)lp, (float)scale, causal ? 1 : 0);
+                                                           (int)lp, (float)scale, causal ? 1 : 0,
+                                                           rope ? rcos : nullptr, rope ? rsin : nullptr);
     SFT_LAUNCH_CHECK();
+    rope_done = rope;
     return dqkv;
   }
   auto run3 = [&](auto w) {
@@ -2019,9 +2065,37 @@ at::Tensor flash_bwd(const at::Tensor& dout, const at::Tensor& qkv, const at::Te
   return dqkv;
 }
 
+at::Tensor flash_bwd(const at::Tensor& dout, const at::Tensor& qkv, const at::Tensor& out, const at::Tensor& lse,
+                     const at::Tensor& cu, int64_t max_seqlen, int64_t nq, int64_t nkv, int64_t hd, double scale,
+                     bool causal) {
+  bool rope_done;
+  return flash_bwd_impl(dout, qkv, out, lse, cu, max_seqlen, nq, nkv, hd, scale, causal, nullptr, nullptr, rope_done);
+}
+
+void rope_(at::Tensor qkv, const at::Tensor& cos, const at::Tensor& sin, int64_t n_q, int64_t n_kv, int64_t head_dim,
+           bool inverse);  // elementwise.hip
+
+// flash_bwd for a qkv whose q / k heads were rotated (RoPE) by the producing GEMM: returns the gradient w.r.t. the
+// UNROTATED qkv. The inverse rotation rides in the dq / dK epilogues on the default path; otherwise the rope kernel
+// runs after the backward.
+at::Tensor flash_bwd_rope(const at::Tensor& dout, const at::Tensor& qkv, const at::Tensor& out, const at::Tensor& lse,
+                          const at::Tensor& cu, int64_t max_seqlen, int64_t nq, int64_t nkv, int64_t hd, double scale,
+                          bool causal, const at::Tensor& cos, const at::Tensor& sin) {
+  SFT_CHECK(cos.scalar_type() == at::kFloat && sin.scalar_type() == at::kFloat && cos.is_contiguous() &&
+                sin.is_contiguous() && cos.is_cuda() && sin.is_cuda(),
+            "flash_bwd_rope: contiguous fp32 cos / sin");
+  SFT_CHECK(cos.numel() == qkv.size(0) * hd / 2 && sin.numel() == cos.numel(), "flash_bwd_rope: cos / sin [total, hd/2]");
+  bool rope_done;
+  auto dqkv = flash_bwd_impl(dout, qkv, out, lse, cu, max_seqlen, nq, nkv, hd, scale, causal, cos.data_ptr<float>(),
+                             sin.data_ptr<float>(), rope_done);
+  if (!rope_done) rope_(dqkv, cos, sin, nq, nkv, hd, true);
+  return dqkv;
+}
+
 TORCH_LIBRARY_IMPL(sftamd, CUDA, m) {
   m.impl("flash_fwd", &flash_fwd);
   m.impl("flash_bwd", &flash_bwd);
+  m.impl("flash_bwd_rope", &flash_bwd_rope);
 }
 
 }  // namespace sftamd

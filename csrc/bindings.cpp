@@ -28,6 +28,7 @@ TORCH_LIBRARY(sftamd, m) {
   // attention
   m.def("flash_fwd(Tensor qkv, Tensor cu_seqlens, int max_seqlen, int n_q, int n_kv, int head_dim, float scale, bool causal) -> (Tensor, Tensor)");
   m.def("flash_bwd(Tensor dout, Tensor qkv, Tensor out, Tensor lse, Tensor cu_seqlens, int max_seqlen, int n_q, int n_kv, int head_dim, float scale, bool causal) -> Tensor");
+  m.def("flash_bwd_rope(Tensor dout, Tensor qkv, Tensor out, Tensor lse, Tensor cu_seqlens, int max_seqlen, int n_q, int n_kv, int head_dim, float scale, bool causal, Tensor cos, Tensor sin) -> Tensor");
   m.def("decode_attention(Tensor q, Tensor kcache, Tensor vcache, Tensor cache_len, int n_q, int n_kv, float scale) -> Tensor");
   // fused decode sampler: penalty -> temperature -> top-k -> top-p -> draw, device-resident state
   m.def("sample_token(Tensor logits, Tensor(a!) presence, Tensor(b!) state, Tensor(c!)? tok_out, Tensor(d!)? pos_out, Tensor(e!)? len_out, Tensor(f!)? log, float temperature, int top_k, float top_p, float repetition_penalty, bool do_sample, int seed) -> ()");

@@ -58,6 +58,12 @@ class Attention(nn.Module):
 
     def forward(self, h, rope_cs, cu_seqlens, max_seqlen):
         c = self.cfg
+        if self.lora is None and self.use_rope and self.cp_group is None:
+            # projection + RoPE (GEMM epilogue) + attention as one autograd node: the backward applies the inverse
+            # rotation inside the attention kernels' dq / dK epilogues
+            a = ops.qkv_rope_attention(h, self.qkv_proj, rope_cs[0], rope_cs[1], cu_seqlens, max_seqlen,
+                                       c.num_attention_heads, c.num_key_value_heads, c.head_dim)
+            return ops.linear(a, self.o_proj)
         if self.lora is None and self.use_rope:
             # projection + RoPE in one HIP GEMM (epilogue rotation) where the shapes allow
             qkv = ops.linear_rope(h, self.qkv_proj, rope_cs[0], rope_cs[1], c.num_attention_heads,

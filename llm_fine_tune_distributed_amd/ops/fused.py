@@ -655,6 +655,57 @@ def flash_attention(qkv, cu_seqlens, max_seqlen, n_q, n_kv, head_dim, scale=None
     return FlashAttnFn.apply(qkv, cu_seqlens, int(max_seqlen), n_q, n_kv, head_dim, float(scale), bool(causal))
 
 
+class QKVRopeAttnFn(Function):
+    """attention(rope(x W_qkv^T)) as ONE autograd node: the forward is QKVRopeFn's GEMM (RoPE in the epilogue) +
+    the flash forward; the backward runs flash_bwd_rope, whose dq / dK epilogues apply the inverse rotation, so the
+    separate inverse-RoPE pass over dqkv (QKVRopeFn.backward) disappears. Gradients are those of
+    QKVRopeFn + FlashAttnFn (tests/test_model_gpu.py)."""
+
+    @staticmethod
+    def forward(ctx, x, weight, cos, sin, cu_seqlens, max_seqlen, n_q, n_kv, head_dim, scale, causal):
+        x2d = x.reshape(-1, x.shape[-1])
+        qkv = _ext.ops().gemm_tn_rope(x2d, weight, cos, sin, (n_q + n_kv) * head_dim,
+                                      _tn_cfg(x2d.shape[0], weight.shape[0]))
+        out, lse = _ext.ops().flash_fwd(qkv, cu_seqlens, max_seqlen, n_q, n_kv, head_dim, scale, causal)
+        ctx.save_for_backward(x2d, qkv, cu_seqlens, out, lse, cos, sin)
+        ctx.weight = weight
+        ctx.dims = (max_seqlen, n_q, n_kv, head_dim, scale, causal)
+        ctx.x_shape = x.shape
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        x2d, qkv, cu, out, lse, cos, sin = ctx.saved_tensors
+        max_seqlen, n_q, n_kv, hd, scale, causal = ctx.dims
+        w = ctx.weight
+        dqkv = _ext.ops().flash_bwd_rope(dout.contiguous(), qkv, out, lse, cu, max_seqlen, n_q, n_kv, hd, scale, causal,
+                                         cos, sin)
+        del qkv, out, lse
+        dx = dw = None
+        if ctx.needs_input_grad[0]:
+            dx = dgrad_mm(dqkv, w).view(ctx.x_shape)
+        if ctx.needs_input_grad[1]:
+            dw = _accumulate_weight_grad(w, dqkv, x2d)
+        return dx, dw, None, None, None, None, None, None, None, None, None
+
+
+_ROPE_ATTN_FUSED = os.environ.get("SFTAMD_ROPE_ATTN", "1") == "1"
+
+
+def qkv_rope_attention(x, weight, cos, sin, cu_seqlens, max_seqlen, n_q, n_kv, head_dim, scale=None, causal=True):
+    """flash_attention(linear_rope(x, W_qkv, cos, sin)) — one fused autograd node when the HIP paths apply
+    (SFTAMD_ROPE_ATTN=0: the two separate nodes)."""
+    scale = scale if scale is not None else 1.0 / math.sqrt(head_dim)
+    x2d = x.reshape(-1, x.shape[-1])
+    if (_ROPE_ATTN_FUSED and _TN_MODE in ("1", "rope") and head_dim == 128 and _tn_ok(x2d, weight)
+            and cos.dtype == torch.float32 and cos.is_contiguous() and sin.is_contiguous()
+            and cos.shape == (x2d.shape[0], 64)):
+        return QKVRopeAttnFn.apply(x, weight, cos, sin, cu_seqlens, int(max_seqlen), n_q, n_kv, head_dim,
+                                   float(scale), bool(causal))
+    qkv = linear_rope(x, weight, cos, sin, n_q, n_kv, head_dim)
+    return flash_attention(qkv, cu_seqlens, max_seqlen, n_q, n_kv, head_dim, scale, causal)
+
+
 # ----------------------------------------------------------------------------- LM head + CE
 def _ce_rows(logits: torch.Tensor, labels: torch.Tensor, inv_count: torch.Tensor, write_grad: bool):
     """Per-row CE over the vocab. Returns stats [4, M] fp32 = (loss, lse, entropy, correct).

@@ -226,6 +226,38 @@ def test_flash_attention_bwd_gqa_grouped(causal, ds_mb, gqa, monkeypatch):
     _attn_case([130, 64], 12, 2, causal, "1", "3", "", ds_mb)
 
 
+@pytest.mark.parametrize("path", ["default", "gqa0", "ds0", "mha"])
+def test_flash_bwd_rope(path, monkeypatch):
+    """flash_bwd_rope == inverse-RoPE(flash_bwd): fused into the dq / dK epilogues on the default path (one bf16
+    rounding instead of two: close), the rope kernel after the backward on the others (bitwise)."""
+    monkeypatch.setenv("SFTAMD_ATTN_IMPL", "3")
+    monkeypatch.setenv("SFTAMD_ATTN_CFG", "")
+    monkeypatch.setenv("SFTAMD_ATTN_GQA", "0" if path == "gqa0" else "1")
+    monkeypatch.setenv("SFTAMD_ATTN_DS_MB", "0" if path == "ds0" else "")
+    torch.manual_seed(5)
+    D = 128
+    nq, nkv = (4, 4) if path == "mha" else (8, 2)
+    lens = [300, 17, 512, 129]
+    cu = torch.tensor([0] + list(torch.tensor(lens).cumsum(0)), dtype=torch.int32, device=DEV)
+    M = int(cu[-1])
+    qkv = torch.randn(M, (nq + 2 * nkv) * D, device=DEV, dtype=torch.bfloat16)
+    pos = torch.cat([torch.arange(l) for l in lens]).to(DEV).float()
+    inv = 1.0 / (10000 ** (torch.arange(0, 64, device=DEV).float() / 64))
+    ang = pos[:, None] * inv[None]
+    cos, sin = ang.cos().contiguous(), ang.sin().contiguous()
+    scale = 1 / math.sqrt(D)
+    out, lse = _ext.ops().flash_fwd(qkv, cu, max(lens), nq, nkv, D, scale, True)
+    dout = torch.randn_like(out)
+    got = _ext.ops().flash_bwd_rope(dout, qkv, out, lse, cu, max(lens), nq, nkv, D, scale, True, cos, sin)
+    want = _ext.ops().flash_bwd(dout, qkv, out, lse, cu, max(lens), nq, nkv, D, scale, True)
+    _ext.ops().rope_(want, cos, sin, nq, nkv, D, True)
+    if path == "default":
+        assert rel_err(got, want) < 1e-2
+        assert torch.equal(got[:, (nq + nkv) * D:], want[:, (nq + nkv) * D:])  # dV untouched by the rotation
+    else:
+        assert torch.equal(got, want)
+
+
 def test_flash_attention_mha_and_long():
     _attn_case([1000, 37], 4, 4, True, "1")
 

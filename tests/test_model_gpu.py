@@ -59,7 +59,7 @@ def test_model_fused_gemm_epilogues(mt, down_fused, monkeypatch):
     # (GateUpActFn + SwiGLUDownFn); else GateUpSwiGLUFn + a plain down projection
     sw_fn = F.GateUpActFn if down_fused else F.GateUpSwiGLUFn
     monkeypatch.setattr(F, "_SWIGLU_DOWN", down_fused)
-    orig_sw, orig_rope = sw_fn.apply, F.QKVRopeFn.apply
+    orig_sw, orig_rope, orig_ra = sw_fn.apply, F.QKVRopeFn.apply, F.QKVRopeAttnFn.apply
 
     def sw(*a):
         calls["swiglu"] += 1
@@ -68,6 +68,10 @@ def test_model_fused_gemm_epilogues(mt, down_fused, monkeypatch):
     def rp(*a):
         calls["rope"] += 1
         return orig_rope(*a)
+
+    def ra(*a):  # qkv + RoPE GEMM fused with the attention node (default for RoPE layers)
+        calls["rope"] += 1
+        return orig_ra(*a)
 
     orig_plain = F._tn_plain_ok
     calls["plain"] = 0
@@ -79,6 +83,7 @@ def test_model_fused_gemm_epilogues(mt, down_fused, monkeypatch):
 
     monkeypatch.setattr(sw_fn, "apply", sw)
     monkeypatch.setattr(F.QKVRopeFn, "apply", rp)
+    monkeypatch.setattr(F.QKVRopeAttnFn, "apply", ra)
     monkeypatch.setattr(F, "_tn_plain_ok", plain)
     monkeypatch.setattr(F, "_TN_PLAIN", True)  # opt-in paths, exercised here
     monkeypatch.setattr(F, "_TN_SMALL_TILES", "1")
@@ -99,6 +104,41 @@ def test_model_fused_gemm_epilogues(mt, down_fused, monkeypatch):
         assert e < 2e-2, (n, e.item())
         e = (g_f[n] - g_r[n]).norm() / (g_r[n].norm() + 1e-12)
         assert e < 5e-2, (n, e.item())
+
+
+@pytest.mark.parametrize("mt", ["smollm3", "llama"])
+def test_model_rope_attention_node(mt, monkeypatch):
+    """qkv GEMM (+RoPE epilogue) + flash attention as ONE autograd node whose backward inverts the RoPE inside the
+    attention kernels' dq / dK epilogues == the two separate nodes (rope kernel on dqkv), and == the reference."""
+    import llm_fine_tune_distributed_amd.ops.fused as F
+    torch.manual_seed(0)
+    cfg = tiny(mt, hidden_size=512, num_attention_heads=8, num_key_value_heads=2, head_dim=128,
+               intermediate_size=1024, vocab_size=1024, num_hidden_layers=4)
+    m = build_model(cfg, device="cuda", dtype=torch.bfloat16, seed=1)
+    ids = torch.randint(0, 1024, (4, 256), device="cuda")
+    labels = ids.clone()
+    labels[:, 200:] = -100
+    n = {"fused": 0}
+    orig = F.QKVRopeAttnFn.apply
+
+    def ra(*a):
+        n["fused"] += 1
+        return orig(*a)
+
+    monkeypatch.setattr(F.QKVRopeAttnFn, "apply", ra)
+    monkeypatch.setattr(F, "_ROPE_ATTN_FUSED", True)
+    l_f, g_f = _run(m, ids, labels, True)
+    assert n["fused"] == (3 if mt == "smollm3" else 4)  # NoPE layer 3 keeps the plain projection
+    monkeypatch.setattr(F, "_ROPE_ATTN_FUSED", False)
+    l_s, g_s = _run(m, ids, labels, True)
+    assert n["fused"] == (3 if mt == "smollm3" else 4)
+    l_r, g_r = _run(m, ids, labels, False)
+    assert torch.equal(l_f, l_s)  # same forward kernels
+    for k in g_s:
+        e = (g_f[k] - g_s[k]).norm() / (g_s[k].norm() + 1e-12)
+        assert e < 1e-2, (k, e.item())
+        e = (g_f[k] - g_r[k]).norm() / (g_r[k].norm() + 1e-12)
+        assert e < 5e-2, (k, e.item())
 
 
 def test_lora_wide_gpu_matches_unfused():
