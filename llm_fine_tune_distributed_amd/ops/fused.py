@@ -288,6 +288,22 @@ class EmbeddingFn(Function):
         mg = getattr(w, "main_grad", None)
         flat_ids = ids.reshape(-1)
         dy2d = dy.reshape(-1, dy.shape[-1]).contiguous()
+        sink = getattr(w, "_sftamd_sparse_sink", None)
+        if sink is not None:
+            # sparse tied-embedding gradient (DDPEngine.tied_sparse): (unique ids, summed rows) go to the engine,
+            # which all-gathers them after backward; main_grad holds only the (early all-reduced) lm_head part
+            uniq, inv = torch.unique(flat_ids, sorted=True, return_inverse=True)
+            if _ext.use_hip(dy):
+                rows = torch.zeros(uniq.numel(), w.shape[-1], dtype=mg.dtype if mg is not None else w.dtype,
+                                   device=w.device)
+                sorted_inv, perm = torch.sort(inv.to(torch.int32))
+                _ext.ops().embedding_bwd(dy2d, sorted_inv, perm.to(torch.int32), rows)
+            else:
+                rows = torch.zeros(uniq.numel(), w.shape[-1], dtype=torch.float32, device=w.device)
+                rows.index_add_(0, inv, dy2d.float())
+                rows = rows.to(mg.dtype if mg is not None else w.dtype)
+            sink(uniq, rows)
+            return None, None
         if _ext.use_hip(dy):
             sorted_ids, perm = torch.sort(flat_ids.to(torch.int32))
             target = mg if mg is not None else torch.zeros_like(w)

@@ -62,6 +62,7 @@ class Bucket:
     ready: bool = False
     launched: bool = False
     work: Optional[object] = None
+    replicated: bool = False  # tied-embedding buckets in sparse mode: all-reduced and updated on every rank
 
 
 def _no_decay(name: str, p: torch.Tensor) -> bool:
@@ -91,7 +92,7 @@ class DDPEngine:
                  grad_dtype: Optional[torch.dtype] = None,
                  broadcast_params: bool = False, align: int = 64, process_group=None,
                  no_decay_fn: Callable[[str, torch.Tensor], bool] = _no_decay, shard: bool = False,
-                 track_norm: Optional[bool] = None, split_oversized: bool = True):
+                 track_norm: Optional[bool] = None, split_oversized: bool = True, tied_sparse: Optional[bool] = None):
         self.model = model
         self.world_size = world_size
         self.rank = rank
@@ -108,6 +109,26 @@ class DDPEngine:
             raise ValueError("no trainable parameters")
         # backward-ready order = reverse registration; decay params first, no-decay after
         rev = list(reversed(named))
+        if track_norm is None:
+            track_norm = os.environ.get("SFTAMD_NORM_IN_BWD", "0") == "1"
+        # Sparse tied-embedding gradient (world > 1, tied lm_head / embedding): the tied weight's gradient has a
+        # dense part (lm_head wgrad, the FIRST weight gradient of backward) and a sparse part (embedding backward,
+        # the LAST op of backward, only the rows of the step's tokens). Dense mode ships the sum as the last
+        # buckets, exposed after backward (and, under ZeRO-1, gathered again before the next forward's first op).
+        # Sparse mode: the tied weight leads the layout in buckets of its own, all-reduced as soon as the lm_head
+        # wgrad lands (overlapped with the whole backward); the embedding backward hands (unique ids, summed rows)
+        # to the engine instead, all ranks all-gather those (N x <= tokens x hidden) after backward and add them in
+        # rank order; the tied weight is then updated on every rank (replicated, no ZeRO all-gather).
+        tied_w = None
+        inner = getattr(model, "model", None)
+        if getattr(model, "lm_head", 0) is None and inner is not None and hasattr(inner, "embed_tokens"):
+            tied_w = inner.embed_tokens if inner.embed_tokens.requires_grad else None
+        if tied_sparse is None:
+            tied_sparse = os.environ.get("SFTAMD_TIED_SPARSE", "1") == "1"
+        self.tied_sparse = bool(tied_sparse and tied_w is not None and world_size > 1 and not track_norm)
+        self.tied_param = tied_w if self.tied_sparse else None
+        if self.tied_sparse:
+            rev = [(n, p) for n, p in rev if p is tied_w] + [(n, p) for n, p in rev if p is not tied_w]
         decay = [(n, p) for n, p in rev if not no_decay_fn(n, p)]
         nodecay = [(n, p) for n, p in rev if no_decay_fn(n, p)]
         self.param_names: Dict[int, str] = {id(p): n for n, p in named}
@@ -166,8 +187,17 @@ class DDPEngine:
                         owners.append(cur)
                 self.param_bucket[id(p)] = owners
                 off = end
+                if p is self.tied_param:  # buckets of its own: all-reduced early, updated on every rank
+                    for b in owners:
+                        b.replicated = True
+                    off = rup(off, pad_unit)
+                    cur.end = off
+                    cur = Bucket(index=len(self.buckets), start=off, end=off)
+                    self.buckets.append(cur)
             off = rup(off, pad_unit)
             cur.end = off
+            if not cur.params:  # the bucket opened after a tied weight that ended its region
+                self.buckets.pop()
             self.regions.append((rs, off, region == "decay"))
         self.numel = off
         self.param_flat = torch.zeros(self.numel, dtype=dtype, device=dev)
@@ -185,9 +215,9 @@ class DDPEngine:
         # a serial pass over every gradient after backward. Measured on MI355X (bench.py, interleaved): 96.0
         # vs 96.2-96.3 samples/s without — the concurrent HBM pass slows the backward GEMMs as much as it
         # saves, so it is off by default.
-        if track_norm is None:
-            track_norm = os.environ.get("SFTAMD_NORM_IN_BWD", "0") == "1"
         self.track_norm = bool(track_norm)
+        self._sparse = None
+        self.sparse_exchanges = 0  # synchronising passes whose tied-embedding rows went through the sparse path
         self.norm_partials = torch.zeros(len(self.buckets), dtype=torch.float32, device=dev)
         # World size 1 on GPU (SFTAMD_NORM_FUSED, default on): the weight-gradient GEMMs of the synchronising pass
         # write the sum of squares of the gradient they store into per-(tile, wave) slots (csrc/gemm_wgrad.hip), so
@@ -263,6 +293,14 @@ class DDPEngine:
         reset = getattr(self.model, "reset_grad_use_counters", None)
         if reset is not None:
             reset()
+        self._sparse = None
+        if self.tied_param is not None:
+            # synchronising pass: the tied weight is complete after its lm_head contribution; the embedding
+            # backward hands its sparse rows to _sparse_sink (no_sync passes keep the dense accumulation)
+            sparse = self.sync_grads
+            self.tied_param._sftamd_sparse_sink = self._sparse_sink if sparse else None
+            if sparse:
+                self.tied_param._sftamd_remaining = 1
         if self.fused_norm:
             if self.sync_grads:
                 self.norm_slots.zero_()
@@ -396,8 +434,41 @@ class DDPEngine:
         from ..ops import _ext
         return _ext.ops().sumsq_chunks(self.grad_flat, chunks).sum()
 
+    # ------------------------------------------------------------------ sparse tied-embedding gradient
+    def _sparse_sink(self, ids: torch.Tensor, rows: torch.Tensor):
+        """Embedding backward of the synchronising pass: unique token ids [U] (int64) and their summed gradient
+        rows [U, H] (the tied weight's dtype)."""
+        self._sparse = (ids, rows)
+
+    def _exchange_sparse(self):
+        """All ranks' sparse embedding rows into the (already all-reduced) tied gradient, in rank order: every
+        rank computes the same sum (each rank's ids are unique, so every row gets one add per rank)."""
+        p = self.tied_param
+        mg = p.main_grad
+        H = mg.shape[-1]
+        if self._sparse is None:
+            ids = torch.empty(0, dtype=torch.int64, device=mg.device)
+            rows = torch.empty(0, H, dtype=mg.dtype, device=mg.device)
+        else:
+            ids, rows = self._sparse
+            self.sparse_exchanges += 1
+        self._sparse = None
+        n = torch.tensor([ids.numel()], dtype=torch.int64, device=mg.device)
+        dist.all_reduce(n, op=dist.ReduceOp.MAX, group=self.pg)
+        cap = max(1, int(n.item()))
+        idp = torch.zeros(cap, dtype=torch.int64, device=mg.device)  # padding -> row 0, with zero rows (exact no-op)
+        rwp = torch.zeros(cap, H, dtype=mg.dtype, device=mg.device)
+        idp[:ids.numel()] = ids
+        rwp[:ids.numel()] = rows
+        gid = torch.empty(self.world_size * cap, dtype=torch.int64, device=mg.device)
+        grw = torch.empty(self.world_size * cap, H, dtype=mg.dtype, device=mg.device)
+        dist.all_gather_into_tensor(gid, idp, group=self.pg)
+        dist.all_gather_into_tensor(grw, rwp, group=self.pg)
+        for r in range(self.world_size):
+            mg.index_add_(0, gid[r * cap:(r + 1) * cap], grw[r * cap:(r + 1) * cap])
+
     def _collective(self, b: Bucket, view: torch.Tensor):
-        if self.shard:
+        if self.shard and not b.replicated:
             s, e = self.shard_range(b)
             # in place: this rank's slice of the bucket receives the sum of every rank's slice
             b.work = dist.reduce_scatter_tensor(self.grad_flat[s:e], view, op=dist.ReduceOp.SUM, group=self.pg,
@@ -408,7 +479,7 @@ class DDPEngine:
     # ------------------------------------------------------------------ ZeRO-1 slices
     def shard_range(self, b: Bucket):
         """[start, end) of the slice of bucket ``b`` this rank owns (the whole bucket unless sharded)."""
-        if not self.shard or self.world_size == 1:
+        if not self.shard or self.world_size == 1 or b.replicated:
             return b.start, b.end
         n = (b.end - b.start) // self.world_size
         return b.start + self.rank * n, b.start + (self.rank + 1) * n
@@ -418,7 +489,7 @@ class DDPEngine:
 
     def gather_params(self, b: Bucket, async_op: bool = True):
         """All-gather the updated parameter slices of bucket ``b`` (in place) — ZeRO-1 only."""
-        if not self.shard or self.world_size == 1:
+        if not self.shard or self.world_size == 1 or b.replicated:
             return None
         s, e = self.shard_range(b)
         return dist.all_gather_into_tensor(self.param_flat[b.start:b.end], self.param_flat[s:e], group=self.pg,
@@ -450,6 +521,8 @@ class DDPEngine:
             if b.work is not None:
                 b.work.wait()
                 b.work = None
+        if self.tied_param is not None:
+            self._exchange_sparse()
         if timing:
             e1.record()
             self._comm_events.append((e0, e1))

@@ -380,8 +380,9 @@ class ShardedAdamW(FlatAdamW):
         # global grad norm: sum of squares of the owned (reduced) slices, all-reduced (one float)
         norm2 = e.grad_norm_sq()  # owned slices, summed bucket by bucket during backward
         if norm2 is None:
-            owned = [e.grad_flat[s:t] for _, s, t, _, _ in self.slices if t > s]
-            norm2 = ops.sumsq_list(owned).reshape(1)
+            # replicated buckets (sparse tied embedding) are whole on every rank: counted once, on rank 0
+            owned = [e.grad_flat[s:t] for b, s, t, _, _ in self.slices if t > s and (not b.replicated or e.rank == 0)]
+            norm2 = ops.sumsq_list(owned).reshape(1) if owned else torch.zeros(1, device=e.device)
         if e.world_size > 1:
             dist.all_reduce(norm2, op=dist.ReduceOp.SUM, group=e.pg)
         norm = norm2.sqrt()
@@ -399,8 +400,12 @@ class ShardedAdamW(FlatAdamW):
             ctx = torch.cuda.stream(st)
         with ctx:
             # forward order (the embedding's bucket is the LAST one in backward-ready layout): each bucket's
-            # gather is issued right after its update, so the first layers' parameters come back first
-            for b, s, t, lo, decay in reversed(self.slices):
+            # gather is issued right after its update, so the first layers' parameters come back first; replicated
+            # buckets (the sparse-mode tied embedding: first in the layout, needed by the first forward op, no
+            # gather) are updated before everything else
+            order = [x for x in self.slices if x[0].replicated] + [x for x in reversed(self.slices)
+                                                                  if not x[0].replicated]
+            for b, s, t, lo, decay in order:
                 n = t - s
                 if n:
                     ops.adamw_flat_(e.param_flat[s:t], e.grad_flat[s:t],
@@ -427,7 +432,7 @@ class ShardedAdamW(FlatAdamW):
         full = torch.zeros(e.numel, dtype=local.dtype, device=e.device)
         for b, s, t, lo, _ in self.slices:
             full[s:t].copy_(local[lo:lo + t - s])
-            if e.world_size > 1:
+            if e.world_size > 1 and not b.replicated:
                 dist.all_gather_into_tensor(full[b.start:b.end], full[s:t], group=e.pg)
         return full
 

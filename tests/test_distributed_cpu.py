@@ -45,7 +45,9 @@ def _run(rank, world, port, out_dir, per_dev, ga, steps, shard=False, tag="", av
     osd = t.optimizer.state_dict()  # collective in ZeRO-1 mode: every rank takes part
     torch.save({"params": t.engine.params_by_name().clone(), "loss": out.training_loss,
                 "log": [h for h in t.state.log_history if "loss" in h], "exp_avg": _flat_state(osd, "exp_avg"),
-                "exp_avg_sq": _flat_state(osd, "exp_avg_sq"), "sharded": type(t.optimizer).__name__},
+                "exp_avg_sq": _flat_state(osd, "exp_avg_sq"), "sharded": type(t.optimizer).__name__,
+                "tied_sparse": t.engine.tied_sparse, "sparse_exchanges": t.engine.sparse_exchanges,
+                "replicated_buckets": sum(b.replicated for b in t.engine.buckets)},
                os.path.join(out_dir, f"r{world}_{rank}{tag}.pt"))
     pgm.cleanup_distributed()
 
@@ -192,3 +194,29 @@ def test_zero1_checkpoint_resumes_at_another_world_size():
     for name, st in saved["param_state"].items():
         for k in ("exp_avg", "exp_avg_sq", "master"):
             assert torch.equal(got["param_state"][name][k], st[k]), (name, k)
+
+
+@pytest.mark.parametrize("world,shard,ga,merge", [(2, True, 2, 0), (2, False, 1, 0), (4, True, 1, 0),
+                                                  (4, False, 2, 32768)])
+def test_tied_embedding_sparse_exchange(world, shard, ga, merge, monkeypatch):
+    """Sparse tied-embedding gradient (default for world > 1: the lm_head part all-reduced early in buckets of
+    its own, the embedding rows all-gathered after backward, the tied weight replicated under ZeRO-1) == the dense
+    bucket path, and both == one process on the same global batch; GA no_sync passes keep the dense accumulation."""
+    d = tempfile.mkdtemp()
+    per_dev = 4 // world if ga == 1 else 2 // (world // 2 if world > 2 else 1)
+    per_dev = max(1, per_dev)
+    monkeypatch.setenv("SFTAMD_TIED_SPARSE", "1")
+    _launch(world, per_dev, ga, 3, d, shard=shard, tag="_sp", merge=merge)
+    monkeypatch.setenv("SFTAMD_TIED_SPARSE", "0")
+    _launch(world, per_dev, ga, 3, d, shard=shard, tag="_dn", merge=merge)
+    sp = [torch.load(os.path.join(d, f"r{world}_{r}_sp.pt")) for r in range(world)]
+    dn = torch.load(os.path.join(d, f"r{world}_0_dn.pt"))
+    assert sp[0]["tied_sparse"] and sp[0]["sparse_exchanges"] == 3 and sp[0]["replicated_buckets"] >= 1
+    assert not dn["tied_sparse"] and dn["sparse_exchanges"] == 0 and dn["replicated_buckets"] == 0
+    for r in range(1, world):
+        assert torch.equal(sp[0]["params"], sp[r]["params"])  # replicated tied weight stays bit-identical
+    assert torch.allclose(sp[0]["params"], dn["params"], atol=1e-5, rtol=1e-4)
+    assert torch.allclose(sp[0]["exp_avg_sq"], dn["exp_avg_sq"], atol=1e-8, rtol=1e-3)
+    for a, b in zip(dn["log"], sp[0]["log"]):
+        assert abs(a["loss"] - b["loss"]) < 1e-4
+        assert abs(a["grad_norm"] - b["grad_norm"]) < 1e-3 * max(1.0, a["grad_norm"])
