@@ -102,7 +102,9 @@ def bucket_plan(engine) -> dict:
     srt = sorted(mb)
     return {"count": len(mb), "cap_mb": round(engine.bucket_cap_mb, 3), "first_mb": round(mb[0], 3),
             "min_mb": round(srt[0], 3), "median_mb": round(srt[len(srt) // 2], 3), "max_mb": round(srt[-1], 3),
-            "total_mb": round(sum(mb), 1), "split_params": engine.num_split_params}
+            "total_mb": round(sum(mb), 1), "split_params": engine.num_split_params,
+            "tied_sparse": bool(getattr(engine, "tied_sparse", False)),
+            "replicated_buckets": sum(bool(getattr(b, "replicated", False)) for b in engine.buckets)}
 
 
 def run(a):
