@@ -30,7 +30,8 @@ Besides the driver contract fields the JSON line carries the multi-GPU diagnosti
 ``dist`` (backend and world size as every rank saw them), ``bucket_plan`` (count / sizes of the
 gradient buckets), ``comm_exposed_ms`` (non-overlapped gradient-collective wait per step, max over
 ranks), per-rank ``peak_mem_gb`` / ``ms_per_step`` and, given ``--baseline-1gpu V``,
-``scaling_efficiency = value / (N * V)``.
+``scaling_efficiency = value / (N * V)``. ``comm_probe`` (N > 1, measured between warmup and the timed steps):
+reduce-scatter / all-gather / all-reduce bus bandwidth at the bucket size, i.e. what xGMI delivered on that node.
 """
 from __future__ import annotations
 
@@ -107,6 +108,35 @@ def bucket_plan(engine) -> dict:
             "replicated_buckets": sum(bool(getattr(b, "replicated", False)) for b in engine.buckets)}
 
 
+def comm_probe(dev, world: int, nbytes: int, iters: int = 5) -> dict:
+    """Bus bandwidth of the three collectives the step uses, at the gradient-bucket size, measured between the
+    warmup and the timed steps (not timed): reduce-scatter and all-gather (ZeRO-1) and all-reduce (DDP), bf16.
+    busbw = bytes / time x (N - 1) / N, the per-rank link traffic rate (nccl-tests convention)."""
+    import torch
+    import torch.distributed as dist
+    n = max(world * 64, (nbytes // 2) // (world * 64) * (world * 64))
+    buf = torch.ones(n, dtype=torch.bfloat16, device=dev)
+    part = buf[: n // world]
+    out = {"bytes": n * 2}
+    sync = (lambda: torch.cuda.synchronize()) if dev.type == "cuda" else (lambda: None)
+    for name, fn in (("reduce_scatter", lambda: dist.reduce_scatter_tensor(part, buf)),
+                     ("all_gather", lambda: dist.all_gather_into_tensor(buf, part)),
+                     ("all_reduce", lambda: dist.all_reduce(buf))):
+        for _ in range(2):
+            fn()
+        sync()
+        dist.barrier()
+        t0 = time.perf_counter()
+        for _ in range(iters):
+            fn()
+        sync()
+        dt = (time.perf_counter() - t0) / iters
+        bus = n * 2 / dt * (world - 1) / world * (2 if name == "all_reduce" else 1)
+        out[f"{name}_ms"] = round(dt * 1e3, 3)
+        out[f"{name}_busbw_gbps"] = round(bus / 1e9, 1)
+    return out
+
+
 def run(a):
     import torch
     import torch.distributed as dist
@@ -158,6 +188,9 @@ def run(a):
         r = step()
     trainer.optimizer.synchronize()
     sync()
+    probe = None
+    if st.world_size > 1 and os.environ.get("SFTAMD_BENCH_COMM_PROBE", "1") == "1":
+        probe = comm_probe(st.device, st.world_size, int(trainer.engine.bucket_cap_mb * 2 ** 20))
     barrier()
     sync()
     trainer.engine.comm_exposed_ms(reset=True)  # drop the warmup's samples
@@ -216,6 +249,7 @@ def run(a):
                      "launcher": os.environ.get("SFTAMD_LAUNCHER", "external" if st.world_size > 1 else "none")},
             "optimizer_sharding": "zero1" if shard else "none",
             "bucket_plan": bucket_plan(trainer.engine),
+            "comm_probe": probe,
             "comm_exposed_ms": max(r_["comm_exposed_ms"] for r_ in ranks),
             "per_rank": [{k: r_[k] for k in ("rank", "device", "ms_per_step", "peak_mem_gb", "comm_exposed_ms")}
                          for r_ in ranks],
