@@ -213,7 +213,10 @@ def run(a):
         ranks = [None] * st.world_size
         dist.all_gather_object(ranks, mine)
     dt = max(r_["ms_per_step"] for r_ in ranks) * a.steps / 1e3  # the MAX over ranks
-    loss = r["acc"][0].item()
+    loss_t = r["acc"][0].detach().clone().reshape(1)  # this rank's share of the global token-mean loss
+    if st.world_size > 1:
+        dist.all_reduce(loss_t)
+    loss = loss_t.item()
     ms = dt / a.steps * 1e3
     samples = a.micro_batch * a.ga * st.world_size * a.steps
     value = samples / dt
