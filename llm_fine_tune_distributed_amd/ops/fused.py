@@ -51,13 +51,19 @@ def _wgrad_cfg(T: int, N: int, K: int) -> int:
     256 CUs (gate_up 0.58 vs 0.74 ms, lm_head 3.2 vs 3.9 ms at T=8192), the 256x128 ring kernel on
     mid-size grids (qkv 0.113 vs 0.139 ms, down 0.337 vs 0.349 ms); on small grids (o_proj 2048 x 2048 = 128
     tiles of 256 x 128) the same kernel split 2 ways over the tokens (cfg 209, fp32 slabs + ordered reduce):
-    0.071 vs 0.090 ms for hipBLASLt (profiles/r2_wgrad_splitk.md)."""
+    0.071 vs 0.090 ms for hipBLASLt (profiles/r2_wgrad_splitk.md); mid grids of 64-128 256 x 256 tiles (qkv) split 2
+    ways (cfg 210)."""
     if _WGRAD_MODE == "blas" or T % 32 or T < 1024:
         return 0
     if _WGRAD_MODE not in ("auto", ""):
         return int(_WGRAD_MODE)
     if N % 256 == 0 and K % 256 == 0 and (N // 256) * (K // 256) >= 512:
         return 10
+    if (N % 256 == 0 and K % 256 == 0 and 64 < (N // 256) * (K // 256) <= 128 and (T // 32) % 2 == 0
+            and (N // 256) * (K // 128) < 256):
+        # e.g. qkv [3072 x 2048]: 96 tiles of 256 x 256 split 2 ways over the tokens fill 192 CUs with
+        # half-depth pieces, vs 192 tiles of 256 x 128 at 0.75 of a round: 0.113 vs 0.118 ms (r2_run48)
+        return 210
     if N % 256 == 0 and K % 128 == 0 and (N // 256) * (K // 128) >= 160:
         return 9
     if N % 256 == 0 and K % 128 == 0 and (T // 32) % 2 == 0 and (N // 256) * (K // 128) >= 32:
