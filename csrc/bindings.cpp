@@ -4,13 +4,28 @@
 // native data-pipeline ops below which are CPU kernels.
 #include <torch/library.h>
 
+#include <vector>
+
 namespace sftamd {
 int64_t cu_masked_stream(int64_t n, int64_t stride, int64_t offset);  // csrc/optim.hip
+// csrc/ipc_allreduce.hip: one-shot peer-memory all-reduce for small messages
+int64_t ipc_ar_create(int64_t cap, int64_t world, int64_t rank);
+std::vector<int64_t> ipc_ar_handle(int64_t id);
+void ipc_ar_open(int64_t id, std::vector<int64_t> handles);
+int64_t ipc_ar_check(int64_t id);
+void ipc_ar_destroy(int64_t id);
 }
 
 TORCH_LIBRARY(sftamd, m) {
   // runtime: CU-restricted HIP stream for the optimizer's side stream (no tensor arguments: catch-all kernel)
   m.def("cu_masked_stream(int n, int stride=1, int offset=0) -> int", &sftamd::cu_masked_stream);
+  // runtime: IPC peer-memory all-reduce contexts (no tensor arguments: catch-all kernels)
+  m.def("ipc_ar_create(int cap, int world, int rank) -> int", &sftamd::ipc_ar_create);
+  m.def("ipc_ar_handle(int ctx) -> int[]", &sftamd::ipc_ar_handle);
+  m.def("ipc_ar_open(int ctx, int[] handles) -> ()", &sftamd::ipc_ar_open);
+  m.def("ipc_ar_check(int ctx) -> int", &sftamd::ipc_ar_check);
+  m.def("ipc_ar_destroy(int ctx) -> ()", &sftamd::ipc_ar_destroy);
+  m.def("ipc_ar_allreduce(Tensor(a!) x, int ctx, int round, int blocks=16) -> ()");
   // norms / elementwise
   m.def("rmsnorm_fwd(Tensor x, Tensor? residual, Tensor weight, float eps) -> (Tensor, Tensor, Tensor)");
   m.def("rmsnorm_bwd(Tensor dy, Tensor h, Tensor weight, Tensor rstd, Tensor? dres, Tensor(a!)? dw_out=None, bool accumulate=False) -> (Tensor, Tensor)");

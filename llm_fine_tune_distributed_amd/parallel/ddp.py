@@ -434,6 +434,33 @@ class DDPEngine:
         from ..ops import _ext
         return _ext.ops().sumsq_chunks(self.grad_flat, chunks).sum()
 
+    # ------------------------------------------------------------------ small all-reduces
+    def all_reduce_small_(self, t: torch.Tensor) -> torch.Tensor:
+        """In-place SUM of a few values (the clip norm): through the peer-memory one-shot kernel
+        (parallel/ipc_allreduce.py, one ~10 us launch on the compute stream) when SFTAMD_IPC_ALLREDUCE=1 on GPUs,
+        else the process group's all_reduce."""
+        if self.world_size == 1:
+            return t
+        ar = self._small_ar()
+        if ar is not None and t.dtype == torch.float32 and t.is_contiguous() and t.numel() <= 1024:
+            n = t.numel()
+            buf = torch.zeros((n + 3) // 4 * 4, dtype=torch.float32, device=t.device)
+            buf[:n].copy_(t.reshape(-1))
+            ar.all_reduce_(buf)
+            t.copy_(buf[:n].view_as(t))
+            return t
+        dist.all_reduce(t, op=dist.ReduceOp.SUM, group=self.pg)
+        return t
+
+    def _small_ar(self):
+        if not hasattr(self, "_ipc_ar"):
+            self._ipc_ar = None
+            if (os.environ.get("SFTAMD_IPC_ALLREDUCE", "0") == "1" and self.device.type == "cuda"
+                    and self.world_size > 1):
+                from .ipc_allreduce import IPCAllReduce
+                self._ipc_ar = IPCAllReduce(max_bytes=1 << 16, group=self.pg)
+        return self._ipc_ar
+
     # ------------------------------------------------------------------ sparse tied-embedding gradient
     def _sparse_sink(self, ids: torch.Tensor, rows: torch.Tensor):
         """Embedding backward of the synchronising pass: unique token ids [U] (int64) and their summed gradient

@@ -372,7 +372,6 @@ class ShardedAdamW(FlatAdamW):
 
     @torch.no_grad()
     def step(self, lr: Optional[float] = None, max_grad_norm: Optional[float] = None):
-        import torch.distributed as dist
         lr = self.lr if lr is None else lr
         self.step_count += 1
         e = self.engine
@@ -384,7 +383,7 @@ class ShardedAdamW(FlatAdamW):
             owned = [e.grad_flat[s:t] for b, s, t, _, _ in self.slices if t > s and (not b.replicated or e.rank == 0)]
             norm2 = ops.sumsq_list(owned).reshape(1) if owned else torch.zeros(1, device=e.device)
         if e.world_size > 1:
-            dist.all_reduce(norm2, op=dist.ReduceOp.SUM, group=e.pg)
+            e.all_reduce_small_(norm2)
         norm = norm2.sqrt()
         coef = (max_grad_norm / (norm + 1e-6)).clamp(max=1.0) if max_grad_norm else torch.ones_like(norm)
         self.last_grad_norm = norm

@@ -102,9 +102,12 @@ def test_rccl_process_group_options_and_side_stream_collectives():
     assert r["ok"] and r["cnt"] == 3.0 and r["hp"]
 
 
-def test_zero1_on_gpu_matches_replicated():
+@pytest.mark.parametrize("ipc", ["0", "1"])
+def test_zero1_on_gpu_matches_replicated(ipc, monkeypatch):
     """ZeRO-1 on GPU tensors (2 ranks on one MI355X): the reduce-scatter / sharded HIP AdamW /
-    overlapped all-gather path gives the replicated run's parameters."""
+    overlapped all-gather path gives the replicated run's parameters; with SFTAMD_IPC_ALLREDUCE=1 the clip-norm
+    all-reduce runs through the peer-memory one-shot kernel (csrc/ipc_allreduce.hip)."""
+    monkeypatch.setenv("SFTAMD_IPC_ALLREDUCE", ipc)
     d = tempfile.mkdtemp()
     ctx = mp.get_context("spawn")
     for shard in (False, True):

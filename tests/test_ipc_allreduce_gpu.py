@@ -1,0 +1,72 @@
+"""Peer-memory one-shot all-reduce (csrc/ipc_allreduce.hip) with two ranks sharing one GPU (HIP IPC on the same
+device; gloo only exchanges the handles): sums match, are bitwise equal on both ranks, and a missing peer ends in the
+bounded-wait error instead of a hang."""
+import os
+import socket
+
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+pytestmark = pytest.mark.gpu
+
+
+def _port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), HSA_ENABLE_IPC_MODE_LEGACY="0")
+    import torch.distributed as dist
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from llm_fine_tune_distributed_amd.parallel.ipc_allreduce import IPCAllReduce
+    ar = IPCAllReduce(max_bytes=1 << 20)
+    res = {}
+    for dt, n in ((torch.float32, 4), (torch.float32, 1024), (torch.bfloat16, 8), (torch.bfloat16, 262144),
+                  (torch.float32, 65536)):
+        outs = []
+        for it in range(3):
+            g = torch.Generator().manual_seed(1000 * it + n)
+            parts = [torch.randn(n, generator=g) for _ in range(world)]
+            x = parts[rank].to(dt).cuda()
+            ar.all_reduce_(x)
+            want = sum(p.to(dt).float() for p in parts)
+            err = ((x.float().cpu() - want).abs().max() / (want.abs().max() + 1e-6)).item()
+            outs.append((err, x.float().cpu()))
+        res[(str(dt), n)] = outs
+    res["error_word"] = ar.check()
+    # a peer that never arrives: rank 1 skips one call -> rank 0's bounded wait expires and sets the error word
+    if rank == 0:
+        ar.all_reduce_(torch.ones(4, device="cuda"))
+        res["timeout_error"] = ar.check()
+    dist.barrier()
+    ar.close()
+    q.put((rank, res))
+    dist.destroy_process_group()
+
+
+def test_ipc_allreduce_two_ranks_one_gpu():
+    world, port = 2, _port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    out = dict(q.get(timeout=180) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for key, runs in out[0].items():
+        if not isinstance(key, tuple):
+            continue
+        for (e0, x0), (e1, x1) in zip(runs, out[1][key]):
+            tol = 1e-6 if "float32" in key[0] else 1e-2
+            assert e0 <= tol and e1 <= tol, (key, e0, e1)
+            assert torch.equal(x0, x1), key  # rank-order sum: identical on every rank
+    assert out[0]["error_word"] == 0 and out[1]["error_word"] == 0
+    assert out[0]["timeout_error"] == 1
