@@ -1052,8 +1052,31 @@ at::Tensor gemm_tn_rope(const at::Tensor& x, const at::Tensor& w, const at::Tens
   else if (cfg == 5 && x.size(1) % 64 == 0) tn::launch2<256, 256, 2, 4, 2, tn::EPI_ROPE, 3>(x, w, N, ea);
   else if (cfg == 6 && x.size(1) % 64 == 0) tn::launch2<256, 128, 4, 2, 3, tn::EPI_ROPE>(x, w, N, ea);
   else if (cfg == 7 && x.size(1) % 64 == 0) tn::launch2<256, 128, 4, 2, 2, tn::EPI_ROPE>(x, w, N, ea);
-  else if (cfg == 11 && x.size(1) % 64 == 0) tn::launch3<tn::EPI_ROPE, true, 2>(x, w, N, ea);
-  else tn::launch<256, 256, 2, 4, 5, tn::EPI_ROPE>(x, w, N, ea);
+  else if (cfg == 11 && x.size(1) % 64 == 0) {
+    // Wave-quantisation tail (gemm_dgrad.hip does the same): the SmolLM3 qkv grid is 32 x 12 = 384 tiles of
+    // 256 x 256 = 1.5 rounds of 256 CUs. The whole round runs as one launch over the leading columns and the
+    // leftover columns as 256 x 128 tiles (one round at about half a tile's time) in a second launch; heads never
+    // straddle the cut (a multiple of 256), the tail's rope boundary is shifted with its pointers.
+    // SFTAMD_TN_TAIL=0: one launch.
+    const char* e = std::getenv("SFTAMD_TN_TAIL");
+    const bool tail_on = !(e && e[0] == '0');
+    const int nbm = M / 256, nbn = N / 256, tiles = nbm * nbn;
+    int main_n = 0;
+    if (tail_on && tiles % 256 != 0 && 256 % nbm == 0) {
+      main_n = tiles / 256 * (256 / nbm);
+      if ((nbn - main_n) * 2 * nbm > 256) main_n = 0;  // the 256 x 128 tail must fit one round
+    }
+    if (main_n <= 0) {
+      tn::launch3<tn::EPI_ROPE, true, 2>(x, w, N, ea);
+    } else {
+      const int ncut = main_n * 256;
+      tn::launch3<tn::EPI_ROPE, true, 2>(x, w.narrow(0, 0, ncut), ncut, ea);
+      tn::EpiArgs et = ea;
+      et.C = ea.C + ncut;
+      et.rope_cols = std::max(0, ea.rope_cols - ncut);
+      tn::launch2<256, 128, 4, 2, 3, tn::EPI_ROPE>(x, w.narrow(0, ncut, N - ncut), N - ncut, et);
+    }
+  } else tn::launch<256, 256, 2, 4, 5, tn::EPI_ROPE>(x, w, N, ea);
   return c;
 }
 

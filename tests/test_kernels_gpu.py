@@ -538,6 +538,27 @@ def test_gemm_tn_rope(cfg):
     assert torch.equal(out[:, (nq + nkv) * D:], y[:, (nq + nkv) * D:]) or rel_err(out[:, (nq + nkv) * D:], y[:, (nq + nkv) * D:]) < 5e-3
 
 
+@pytest.mark.parametrize("tail", ["1", "0"])
+def test_gemm_tn_rope_wave_tail(tail, monkeypatch):
+    """SmolLM3 qkv grid (32 x 12 tiles = 1.5 rounds): the whole round + a 256 x 128 tail launch whose RoPE
+    boundary (k heads rotated, v heads not) is shifted with its pointers == the fp32 reference."""
+    monkeypatch.setenv("SFTAMD_TN_TAIL", tail)
+    torch.manual_seed(1)
+    M, K, nq, nkv, D = 8192, 128, 16, 4, 128
+    x = torch.randn(M, K, device=DEV, dtype=torch.bfloat16)
+    w = torch.randn((nq + 2 * nkv) * D, K, device=DEV, dtype=torch.bfloat16) * 0.1
+    pos = (torch.arange(M, device=DEV) % 512).float()
+    inv = 1.0 / (10000 ** (torch.arange(0, D, 2, device=DEV).float() / D))
+    fr = pos[:, None] * inv[None, :]
+    cs, sn = fr.cos().contiguous(), fr.sin().contiguous()
+    out = _ext.ops().gemm_tn_rope(x, w, cs, sn, (nq + nkv) * D, 11)
+    y = (x.float() @ w.float().t()).to(torch.bfloat16)
+    qk = y[:, :(nq + nkv) * D].view(M, nq + nkv, D)
+    exp = torch.cat([ref.apply_rope(qk, cs, sn).reshape(M, -1), y[:, (nq + nkv) * D:]], dim=1)
+    for lo, hi in ((0, 2048), (2048, (nq + nkv) * D), ((nq + nkv) * D, (nq + 2 * nkv) * D)):
+        assert rel_err(out[:, lo:hi], exp[:, lo:hi]) < 1e-2, (lo, hi)
+
+
 @pytest.mark.parametrize("M,K,N,wpad", [(256, 64, 256, 0), (512, 2048, 768, 0), (256, 96, 512, 64), (768, 1024, 256, 0)])
 def test_dgrad_gemm_plain(M, K, N, wpad):
     """dX = dy @ w (w [K, N], optionally a column-sliced view): the hand-written NN dgrad vs fp32."""
