@@ -514,7 +514,7 @@ __global__ void __launch_bounds__(256) splitk_fixup_kernel(const float* __restri
 template <int BM, int BN, int WM, int WN, int NS, bool SCHED, bool NORM = false>
 __global__ void __launch_bounds__(NT) ring_kernel(const u16* __restrict__ A, const u16* __restrict__ B,
                                                   u16* __restrict__ C, int T, int N, int K, int nbk, int flags,
-                                                  float* __restrict__ P, int ndp, int splits) {
+                                                  float* __restrict__ P, int ndp, int splits, int tile0 = 0) {
   // flags: bit 0 = accumulate into C, bit 1 = write gradient-norm partials of the whole tiles (8 per tile) to
   // P (no split) or past the split slabs (no extra kernel argument: one more pointer costs this 256-VGPR kernel
   // spills inside its main loop)
@@ -527,7 +527,7 @@ __global__ void __launch_bounds__(NT) ring_kernel(const u16* __restrict__ A, con
   // tiles (the partial last wave) are each split `splits` ways over the token axis — consecutive workgroups,
   // uneven step ranges allowed — into fp32 slabs reduced by splitk_fixup_kernel.
   const int nall = T / BKR;
-  int tile = wgid, sk = 0, s0 = 0, s1 = nall;
+  int tile = tile0 + wgid, sk = 0, s0 = 0, s1 = nall;  // tile0: a tail launch's first tile (DP only)
   if (wgid >= ndp) {
     const int j = wgid - ndp;
     sk = j % splits;
@@ -582,11 +582,35 @@ static long ring_norm_slots(int tiles, int ndp, int BM, int BN) { return (long)n
 
 // splits > 1: tiles beyond the first `full_waves` x 256 (or all of them when full_waves == 0) are split over the
 // token axis; full_waves < 0 = split every tile.
+// tail_stream (data-parallel launches only): when the grid ends in a partial round of 256 workgroups, the whole
+// rounds run on the current stream and the leftover tiles as a second launch on tail_stream (which the caller has
+// ordered after the operands and joins before the gradient is consumed), so the next kernels of backward fill the
+// CUs the partial round leaves idle.
 template <int BM, int BN, int WM, int WN, int NS, bool SCHED = false>
 void launch_ring(const at::Tensor& dy, const at::Tensor& x, at::Tensor& out, bool accumulate, int splits = 1,
-                 bool hybrid = false, float* nrm = nullptr, long nrm_cap = 0) {
+                 bool hybrid = false, float* nrm = nullptr, long nrm_cap = 0, hipStream_t tail_stream = nullptr) {
   const int T = dy.size(0), N = dy.size(1), K = x.size(1);
   const int nbn = N / BM, nbk = K / BN, tiles = nbn * nbk;
+  if (tail_stream != nullptr && splits <= 1 && tiles > 256 && tiles % 256 != 0) {
+    SFT_CHECK(nrm == nullptr || ring_norm_slots(tiles, tiles, BM, BN) <= nrm_cap, "wgrad_gemm: norm slot buffer too small");
+    const int main_tiles = tiles / 256 * 256;
+    const int flags = (accumulate ? 1 : 0) | (nrm != nullptr ? 2 : 0);
+    constexpr bool SCHED_N = BN == 256 ? false : SCHED;
+    auto go = [&](int grid, int tile0, hipStream_t st) {
+      if (nrm != nullptr)
+        ring_kernel<BM, BN, WM, WN, NS, SCHED_N, true><<<grid, NT, 0, st>>>(
+            (const u16*)dy.data_ptr(), (const u16*)x.data_ptr(), (u16*)out.data_ptr(), T, N, K, nbk, flags, nrm,
+            tiles, 1, tile0);
+      else
+        ring_kernel<BM, BN, WM, WN, NS, SCHED><<<grid, NT, 0, st>>>(
+            (const u16*)dy.data_ptr(), (const u16*)x.data_ptr(), (u16*)out.data_ptr(), T, N, K, nbk, flags, nullptr,
+            tiles, 1, tile0);
+      SFT_LAUNCH_CHECK();
+    };
+    go(main_tiles, 0, cur_stream());
+    go(tiles - main_tiles, main_tiles, tail_stream);
+    return;
+  }
   const int ndp = splits <= 1 ? tiles : (hybrid ? tiles / 256 * 256 : 0);
   const int nsk = tiles - ndp;
   SFT_CHECK(nrm == nullptr || ring_norm_slots(tiles, ndp, BM, BN) <= nrm_cap, "wgrad_gemm: norm slot buffer too small");
@@ -629,7 +653,8 @@ void launch(const at::Tensor& dy, const at::Tensor& x, at::Tensor& out, bool acc
 // forms): every slot the launch owns is written, the rest are left untouched (the caller zeroes the buffer once per
 // step); other variants reject it.
 void wgrad_gemm(at::Tensor out, at::Tensor dy, at::Tensor x, bool accumulate, int64_t cfg,
-                const c10::optional<at::Tensor>& norm) {
+                const c10::optional<at::Tensor>& norm, int64_t tail_stream) {
+  hipStream_t ts = (hipStream_t)(intptr_t)tail_stream;
   SFT_CHECK_CUDA(dy);
   SFT_CHECK_BF16(dy);
   SFT_CHECK_BF16(x);
@@ -682,10 +707,10 @@ void wgrad_gemm(at::Tensor out, at::Tensor dy, at::Tensor x, bool accumulate, in
     wgrad::launch_ring<256, 256, 2, 4, 4>(dy, x, out, accumulate);
   } else if (cfg == 9) {
     SFT_CHECK(N % 256 == 0 && K % 128 == 0 && T % 32 == 0, "wgrad_gemm ring 256x128: N multiple of 256, K of 128");
-    wgrad::launch_ring<256, 128, 4, 2, 6>(dy, x, out, accumulate, 1, false, nrm, nrm_cap);
+    wgrad::launch_ring<256, 128, 4, 2, 6>(dy, x, out, accumulate, 1, false, nrm, nrm_cap, ts);
   } else if (cfg == 10) {
     SFT_CHECK(N % 256 == 0 && K % 256 == 0 && T % 32 == 0, "wgrad_gemm ring 256x256: N, K multiples of 256");
-    wgrad::launch_ring<256, 256, 2, 4, 5, true>(dy, x, out, accumulate, 1, false, nrm, nrm_cap);
+    wgrad::launch_ring<256, 256, 2, 4, 5, true>(dy, x, out, accumulate, 1, false, nrm, nrm_cap, ts);
   } else if (cfg == 11) {
     SFT_CHECK(N % 256 == 0 && K % 128 == 0 && T % 32 == 0, "wgrad_gemm ring 256x128: N multiple of 256, K of 128");
     wgrad::launch_ring<256, 128, 4, 2, 6, true>(dy, x, out, accumulate);

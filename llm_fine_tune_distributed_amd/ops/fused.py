@@ -72,7 +72,7 @@ def _wgrad_cfg(T: int, N: int, K: int) -> int:
 
 
 def _wgrad_mm(out: torch.Tensor, dy2d: torch.Tensor, x2d: torch.Tensor, accumulate: bool,
-              norm: Optional[torch.Tensor] = None) -> bool:
+              norm: Optional[torch.Tensor] = None, tail_stream=None) -> bool:
     """out (+)= dy2d^T @ x2d, all bf16 (out is the flat-buffer gradient view). ``norm``: gradient-norm partial
     slots the ring kernels fill with the sum of squares of the values they store; returns whether they did
     (other variants leave the norm to DDPEngine.grad_norm_sq's leftover pass)."""
@@ -81,7 +81,8 @@ def _wgrad_mm(out: torch.Tensor, dy2d: torch.Tensor, x2d: torch.Tensor, accumula
         cfg = _wgrad_cfg(dy2d.shape[0], dy2d.shape[1], x2d.shape[1])
     if cfg:
         use_norm = norm is not None and cfg % 100 in (9, 10)
-        _ext.ops().wgrad_gemm(out, dy2d.contiguous(), x2d.contiguous(), accumulate, cfg, norm if use_norm else None)
+        _ext.ops().wgrad_gemm(out, dy2d.contiguous(), x2d.contiguous(), accumulate, cfg, norm if use_norm else None,
+                              0 if tail_stream is None else tail_stream.cuda_stream)
         return use_norm
     if accumulate:
         out.addmm_(dy2d.t(), x2d)
@@ -99,6 +100,9 @@ def _wgrad_mm(out: torch.Tensor, dy2d: torch.Tensor, x2d: torch.Tensor, accumula
 # 3.5 % SLOWER end to end — two 256x256-tile GEMMs at one workgroup per CU thrash each other's L2
 # and LDS-DMA bandwidth — so it is off by default; the plumbing stays tested (bitwise-equal grads).
 _WGRAD_STREAM_MODE = os.environ.get("SFTAMD_WGRAD_STREAM", "0")
+# SFTAMD_WGRAD_STREAM=tail: only the partial last round of a weight-gradient grid (gate_up / down: 688 tiles = 2.69
+# rounds of 256 CUs) goes to the side stream, so the next backward kernels fill the CUs it leaves idle; the whole
+# rounds stay on the compute stream (csrc/gemm_wgrad.hip launch_ring tail_stream).
 _wgrad_streams = {}
 
 
@@ -137,7 +141,12 @@ def _accumulate_weight_grad(param: torch.Tensor, dy2d: torch.Tensor, x2d: torch.
             if ns is not None and getattr(param, "_sftamd_remaining", 1) != 1:
                 ns = None
             ws = _wgrad_stream(dy2d.device)
-            if ws is not None:
+            if ws is not None and _WGRAD_STREAM_MODE == "tail":
+                ws.wait_stream(torch.cuda.current_stream(dy2d.device))  # the tail launch's operands are ready
+                done = _wgrad_mm(mg, dy2d, x2d, accumulate=not fresh, norm=ns, tail_stream=ws)
+                dy2d.record_stream(ws)
+                x2d.record_stream(ws)
+            elif ws is not None:
                 ws.wait_stream(torch.cuda.current_stream(dy2d.device))
                 with torch.cuda.stream(ws):
                     done = _wgrad_mm(mg, dy2d, x2d, accumulate=not fresh, norm=ns)

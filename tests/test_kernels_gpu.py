@@ -441,6 +441,28 @@ def test_wgrad_gemm_norm_slots(cfg, T, N, K, accumulate):
         _ext.ops().wgrad_gemm(out, dy, x, accumulate, 1, slots[:cap])
 
 
+@pytest.mark.parametrize("cfg,N,K", [(10, 4352, 4096), (9, 4352, 2048)])
+@pytest.mark.parametrize("accumulate", [False, True])
+def test_wgrad_gemm_tail_stream(cfg, N, K, accumulate):
+    """A grid with a partial last round (272 tiles) split into the whole round on the current stream and the
+    leftover tiles on a side stream == one launch, bit for bit, including the gradient-norm slots."""
+    torch.manual_seed(4)
+    T = 256
+    dy = torch.randn(T, N, device="cuda", dtype=torch.bfloat16)
+    x = torch.randn(T, K, device="cuda", dtype=torch.bfloat16)
+    base = torch.randn(N, K, device="cuda", dtype=torch.bfloat16)
+    cap = -(-N // 256) * -(-K // 128) * 32
+    o1, o2 = base.clone(), base.clone()
+    n1, n2 = torch.zeros(cap, device="cuda"), torch.zeros(cap, device="cuda")
+    _ext.ops().wgrad_gemm(o1, dy, x, accumulate, cfg, n1)
+    side = torch.cuda.Stream()
+    side.wait_stream(torch.cuda.current_stream())
+    _ext.ops().wgrad_gemm(o2, dy, x, accumulate, cfg, n2, side.cuda_stream)
+    torch.cuda.current_stream().wait_stream(side)
+    assert torch.equal(o1, o2)
+    assert torch.equal(n1, n2)
+
+
 def test_sumsq_chunks():
     torch.manual_seed(0)
     x = torch.randn(5_000_003, device="cuda").to(torch.bfloat16)

@@ -188,18 +188,20 @@ def test_lora_wide_gpu_matches_unfused():
             assert rel < 5e-2, (n, rel.item())
 
 
-def test_wgrad_side_stream_bitwise(monkeypatch):
-    """Weight-gradient GEMMs on the side stream produce exactly the gradients of the in-order run
-    (same kernels, same operands; only the scheduling differs), including the tied embedding that the
-    lm_head wgrad and the embedding backward both accumulate into."""
+@pytest.mark.parametrize("vocab", [1024, 66560])
+def test_wgrad_side_stream_bitwise(vocab, monkeypatch):
+    """Weight-gradient GEMMs on the side stream (whole: mode 1; only a partial last round: mode tail, which the
+    66560-token lm_head / tied embedding grid of 520 tiles exercises) produce exactly the gradients of the in-order
+    run (same kernels, same operands; only the scheduling differs), including the tied embedding that the lm_head
+    wgrad and the embedding backward both accumulate into."""
     import llm_fine_tune_distributed_amd.ops.fused as F
     torch.manual_seed(0)
     cfg = tiny(hidden_size=512, num_attention_heads=4, num_key_value_heads=2, head_dim=128, intermediate_size=1024,
-               vocab_size=1024, num_hidden_layers=3)
+               vocab_size=vocab, num_hidden_layers=3)
     m = build_model(cfg, device="cuda", dtype=torch.bfloat16, seed=2)
-    ids = torch.randint(0, 1024, (4, 256), device="cuda")
+    ids = torch.randint(0, vocab, (4, 256), device="cuda")
     res = {}
-    for mode in ("0", "1"):
+    for mode in ("0", "1", "tail"):
         monkeypatch.setattr(F, "_WGRAD_STREAM_MODE", mode)
         for p in m.parameters():
             p.main_grad = torch.zeros_like(p)
@@ -212,3 +214,4 @@ def test_wgrad_side_stream_bitwise(monkeypatch):
         res[mode] = {n: p.main_grad.clone() for n, p in m.named_parameters()}
     for n in res["0"]:
         assert torch.equal(res["0"][n], res["1"][n]), n
+        assert torch.equal(res["0"][n], res["tail"][n]), n
