@@ -116,7 +116,8 @@ def comm_probe(dev, world: int, nbytes: int, iters: int = 5) -> dict:
     import torch.distributed as dist
     n = max(world * 64, (nbytes // 2) // (world * 64) * (world * 64))
     buf = torch.ones(n, dtype=torch.bfloat16, device=dev)
-    part = buf[: n // world]
+    rank = dist.get_rank()
+    part = buf[rank * (n // world):(rank + 1) * (n // world)]  # in place, as the ZeRO-1 buckets do
     out = {"bytes": n * 2}
     sync = (lambda: torch.cuda.synchronize()) if dev.type == "cuda" else (lambda: None)
     for name, fn in (("reduce_scatter", lambda: dist.reduce_scatter_tensor(part, buf)),
