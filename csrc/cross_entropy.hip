@@ -9,6 +9,7 @@
 #include "common.h"
 
 #include <climits>
+#include <cstdlib>
 
 namespace sftamd {
 
@@ -31,6 +32,7 @@ __device__ __forceinline__ void ce_merge(CEAcc& a, const CEAcc& b) {
   }
 }
 
+template <int CE_U>  // row loads in flight per thread
 __global__ __launch_bounds__(256) void ce_fwd_kernel(u16* __restrict__ logits, const int64_t* __restrict__ labels,
                                                      const float* __restrict__ inv_count, float* __restrict__ stats,
                                                      int M, int V, int write_grad) {
@@ -43,9 +45,9 @@ __global__ __launch_bounds__(256) void ce_fwd_kernel(u16* __restrict__ logits, c
   const int nvec = V / 8;
 
   CEAcc acc{-INFINITY, 0.f, 0.f, -INFINITY, INT_MAX};
-  for (int v = tid; v < nvec; v += 256) {
+  auto accum = [&](const uint4& raw, int v) {
     float x[8];
-    unpack8(*(const uint4*)(lr + v * 8), x);
+    unpack8(raw, x);
     float mx = x[0];
 #pragma unroll
     for (int i = 1; i < 8; ++i) mx = fmaxf(mx, x[i]);
@@ -61,7 +63,19 @@ __global__ __launch_bounds__(256) void ce_fwd_kernel(u16* __restrict__ logits, c
       }
     }
     ce_merge(acc, b);
+  };
+  // U independent 16-byte loads in flight per thread before any of them is consumed: one load per iteration
+  // leaves the row stream latency-bound (~3.5 TB/s); ties in the argmax resolve by index in ce_merge, so the
+  // visiting order does not change the result
+  int v = tid;
+  for (; v + 256 * (CE_U - 1) < nvec; v += 256 * CE_U) {
+    uint4 r[CE_U];
+#pragma unroll
+    for (int u = 0; u < CE_U; ++u) r[u] = *(const uint4*)(lr + (long)(v + 256 * u) * 8);
+#pragma unroll
+    for (int u = 0; u < CE_U; ++u) accum(r[u], v + 256 * u);
   }
+  for (; v < nvec; v += 256) accum(*(const uint4*)(lr + (long)v * 8), v);
   // wave reduce
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) {
@@ -92,16 +106,25 @@ __global__ __launch_bounds__(256) void ce_fwd_kernel(u16* __restrict__ logits, c
   if (!write_grad) return;
   const float lse = sh_lse;
   const float scale = valid ? inv_count[0] : 0.f;
-  for (int v = tid; v < nvec; v += 256) {
+  auto grad = [&](const uint4& raw, int v) {
     float x[8];
-    unpack8(*(const uint4*)(lr + v * 8), x);
+    unpack8(raw, x);
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
       const float p = __expf(x[i] - lse);
       x[i] = (p - ((v * 8 + i) == label ? 1.f : 0.f)) * scale;
     }
-    *(uint4*)(lr + v * 8) = pack8(x);
+    *(uint4*)(lr + (long)v * 8) = pack8(x);
+  };
+  v = tid;
+  for (; v + 256 * (CE_U - 1) < nvec; v += 256 * CE_U) {
+    uint4 r[CE_U];
+#pragma unroll
+    for (int u = 0; u < CE_U; ++u) r[u] = *(const uint4*)(lr + (long)(v + 256 * u) * 8);
+#pragma unroll
+    for (int u = 0; u < CE_U; ++u) grad(r[u], v + 256 * u);
   }
+  for (; v < nvec; v += 256) grad(*(const uint4*)(lr + (long)v * 8), v);
 }
 
 at::Tensor ce_fwd(at::Tensor logits, const at::Tensor& labels, const at::Tensor& inv_count, bool write_grad) {
@@ -116,9 +139,17 @@ at::Tensor ce_fwd(at::Tensor logits, const at::Tensor& labels, const at::Tensor&
   auto lab = labels.contiguous();
   auto stats = at::empty({4, M}, logits.options().dtype(at::kFloat));
   if (M == 0) return stats;
-  ce_fwd_kernel<<<M, 256, 0, cur_stream()>>>((u16*)logits.data_ptr(), lab.data_ptr<int64_t>(),
-                                             inv_count.data_ptr<float>(), stats.data_ptr<float>(), M, V,
-                                             write_grad ? 1 : 0);
+  static const int unroll = [] {
+    const char* e = std::getenv("SFTAMD_CE_UNROLL");
+    return e && e[0] ? atoi(e) : 4;
+  }();
+  auto* lg = (u16*)logits.data_ptr();
+  if (unroll == 1)
+    ce_fwd_kernel<1><<<M, 256, 0, cur_stream()>>>(lg, lab.data_ptr<int64_t>(), inv_count.data_ptr<float>(),
+                                                  stats.data_ptr<float>(), M, V, write_grad ? 1 : 0);
+  else
+    ce_fwd_kernel<4><<<M, 256, 0, cur_stream()>>>(lg, lab.data_ptr<int64_t>(), inv_count.data_ptr<float>(),
+                                                  stats.data_ptr<float>(), M, V, write_grad ? 1 : 0);
   SFT_LAUNCH_CHECK();
   return stats;
 }

@@ -151,7 +151,7 @@ def test_embedding_bwd_skewed_runs():
     assert rel_err(g, want) < 1e-2
 
 
-@pytest.mark.parametrize("V", [128256, 512])
+@pytest.mark.parametrize("V", [128256, 8008, 512])
 def test_cross_entropy(V):
     torch.manual_seed(0)
     M = 257
