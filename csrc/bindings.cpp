@@ -14,6 +14,15 @@ std::vector<int64_t> ipc_ar_handle(int64_t id);
 void ipc_ar_open(int64_t id, std::vector<int64_t> handles);
 int64_t ipc_ar_check(int64_t id);
 void ipc_ar_destroy(int64_t id);
+// csrc/ddp_reducer.cpp: bucket planner + ready tracker of the DDP engine
+std::vector<int64_t> ddp_plan(std::vector<int64_t> sizes, std::vector<int64_t> region, int64_t tied, int64_t align,
+                              int64_t pad_unit, int64_t cap, int64_t first_cap, int64_t split_at);
+int64_t ddp_tracker_create(std::vector<int64_t> owner_ptr, std::vector<int64_t> owners, int64_t n_buckets);
+void ddp_tracker_reset(int64_t id);
+std::vector<int64_t> ddp_tracker_mark(int64_t id, int64_t param);
+std::vector<int64_t> ddp_tracker_drain(int64_t id);
+std::vector<int64_t> ddp_tracker_pending(int64_t id);
+void ddp_tracker_destroy(int64_t id);
 }
 
 TORCH_LIBRARY(sftamd, m) {
@@ -25,6 +34,15 @@ TORCH_LIBRARY(sftamd, m) {
   m.def("ipc_ar_open(int ctx, int[] handles) -> ()", &sftamd::ipc_ar_open);
   m.def("ipc_ar_check(int ctx) -> int", &sftamd::ipc_ar_check);
   m.def("ipc_ar_destroy(int ctx) -> ()", &sftamd::ipc_ar_destroy);
+  // runtime: DDP bucket planner / ready tracker (CPU, no tensor arguments)
+  m.def("ddp_plan(int[] sizes, int[] region, int tied, int align, int pad_unit, int cap, int first_cap, "
+        "int split_at) -> int[]", &sftamd::ddp_plan);
+  m.def("ddp_tracker_create(int[] owner_ptr, int[] owners, int n_buckets) -> int", &sftamd::ddp_tracker_create);
+  m.def("ddp_tracker_reset(int id) -> ()", &sftamd::ddp_tracker_reset);
+  m.def("ddp_tracker_mark(int id, int param) -> int[]", &sftamd::ddp_tracker_mark);
+  m.def("ddp_tracker_drain(int id) -> int[]", &sftamd::ddp_tracker_drain);
+  m.def("ddp_tracker_pending(int id) -> int[]", &sftamd::ddp_tracker_pending);
+  m.def("ddp_tracker_destroy(int id) -> ()", &sftamd::ddp_tracker_destroy);
   m.def("ipc_ar_allreduce(Tensor(a!) x, int ctx, int round, int blocks=16) -> ()");
   // norms / elementwise
   m.def("rmsnorm_fwd(Tensor x, Tensor? residual, Tensor weight, float eps) -> (Tensor, Tensor, Tensor)");

@@ -58,11 +58,157 @@ class Bucket:
     start: int
     end: int
     params: List[torch.nn.Parameter] = field(default_factory=list)
-    pending: int = 0
     ready: bool = False
     launched: bool = False
     work: Optional[object] = None
     replicated: bool = False  # tied-embedding buckets in sparse mode: all-reduced and updated on every rank
+
+
+def _plan_python(sizes, region, tied, align, pad_unit, cap, first_cap, split_at):
+    """Pure-Python twin of csrc/ddp_reducer.cpp ddp_plan (same packed result): used when the extension is not
+    built, and by the tests that pin the native planner to it."""
+    def rup(x, m):
+        return (x + m - 1) // m * m
+
+    np_ = len(sizes)
+    offset = [0] * np_
+    own = [[] for _ in range(np_)]
+    bstart, bend, brepl, regions = [], [], [], []
+    off = n_split = 0
+    i = 0
+    while i < np_:
+        reg = region[i]
+        j = i
+        while j < np_ and region[j] == reg:
+            j += 1
+        off = rup(off, pad_unit)
+        rs = off
+
+        def open_(at):
+            bstart.append(at)
+            bend.append(at)
+            brepl.append(0)
+            return len(bstart) - 1
+        cur, cur_params = open_(off), 0
+        for k in range(i, j):
+            sz = rup(sizes[k], align)
+            limit = first_cap if cur == 0 else cap
+            if cur_params and off + sz - bstart[cur] > limit:
+                off = rup(off, pad_unit)
+                bend[cur] = off
+                cur, cur_params = open_(off), 0
+            offset[k] = off
+            own[k].append(cur)
+            cur_params += 1
+            end = off + sz
+            if split_at > 0 and sz > split_at:
+                n_split += 1
+                while end - bstart[cur] > split_at:
+                    cut = (bstart[cur] + cap) // pad_unit * pad_unit
+                    bend[cur] = cut
+                    cur, cur_params = open_(cut), 1
+                    own[k].append(cur)
+            off = end
+            if k == tied:
+                for b in own[k]:
+                    brepl[b] = 1
+                off = rup(off, pad_unit)
+                bend[cur] = off
+                cur, cur_params = open_(off), 0
+        off = rup(off, pad_unit)
+        bend[cur] = off
+        if cur_params == 0:
+            bstart.pop(), bend.pop(), brepl.pop()
+        regions += [rs, off, 1 if reg == 0 else 0]
+        i = j
+    owner_ptr = [0]
+    for o in own:
+        owner_ptr.append(owner_ptr[-1] + len(o))
+    return ([off, len(bstart), np_, len(regions) // 3] + offset + bstart + bend + brepl + owner_ptr
+            + [b for o in own for b in o] + regions + [n_split])
+
+
+def _native():
+    from ..ops import _ext
+    return _ext.ops() if _ext.load() else None
+
+
+def ddp_plan(sizes, region, tied, align, pad_unit, cap, first_cap, split_at) -> List[int]:
+    """Bucket plan of the flat gradient buffer (csrc/ddp_reducer.cpp; Python twin when the extension is absent)."""
+    ops = _native()
+    if ops is not None:
+        return list(ops.ddp_plan(sizes, region, tied, align, pad_unit, cap, first_cap, split_at))
+    return _plan_python(sizes, region, tied, align, pad_unit, cap, first_cap, split_at)
+
+
+class ReadyTracker:
+    """Per-bucket pending counts and in-order launch (csrc/ddp_reducer.cpp ddp_tracker_*; the c10d Reducer's
+    bookkeeping), with a Python twin when the extension is absent (``native=False`` forces it)."""
+
+    def __init__(self, owner_ptr, owners, n_buckets: int, native: Optional[bool] = None):
+        self._ops = _native() if native is not False else None
+        if native and self._ops is None:
+            raise RuntimeError("native DDP tracker requested but the extension is not loaded")
+        self.n = n_buckets
+        if self._ops is not None:
+            self._id = self._ops.ddp_tracker_create(list(owner_ptr), list(owners), n_buckets)
+        else:
+            self._ptr, self._own = list(owner_ptr), list(owners)
+            self._init = [0] * n_buckets
+            for b in self._own:
+                self._init[b] += 1
+            self.reset()
+
+    @property
+    def native(self) -> bool:
+        return self._ops is not None
+
+    def reset(self):
+        if self._ops is not None:
+            self._ops.ddp_tracker_reset(self._id)
+            return
+        self._pending = list(self._init)
+        self._marked = [False] * (len(self._ptr) - 1)
+        self._ready = [False] * self.n
+        self._next = 0
+
+    def mark(self, param: int) -> List[int]:
+        if self._ops is not None:
+            return list(self._ops.ddp_tracker_mark(self._id, param))
+        if self._marked[param]:
+            raise RuntimeError(f"DDP parameter {param} signalled ready twice in one backward")
+        self._marked[param] = True
+        for b in self._own[self._ptr[param]:self._ptr[param + 1]]:
+            if self._pending[b] <= 0:
+                raise RuntimeError(f"DDP bucket {b}: more ready signals than parameters")
+            self._pending[b] -= 1
+            if self._pending[b] == 0:
+                self._ready[b] = True
+        out = []
+        while self._next < self.n and self._ready[self._next]:
+            out.append(self._next)
+            self._next += 1
+        return out
+
+    def drain(self) -> List[int]:
+        if self._ops is not None:
+            return list(self._ops.ddp_tracker_drain(self._id))
+        rest = list(range(self._next, self.n))
+        self._next = self.n
+        return rest
+
+    def pending(self) -> List[int]:
+        if self._ops is not None:
+            return list(self._ops.ddp_tracker_pending(self._id))
+        return list(self._pending)
+
+    def __del__(self):
+        ops = getattr(self, "_ops", None)
+        if ops is not None:
+            try:
+                ops.ddp_tracker_destroy(self._id)
+            except Exception:
+                pass
 
 
 def _no_decay(name: str, p: torch.Tensor) -> bool:
@@ -140,66 +286,43 @@ class DDPEngine:
         esz = torch.empty((), dtype=self.grad_dtype).element_size()
         # bucket boundaries: multiples of world_size * (4 KiB of elements) -> equal, page-aligned shards
         pad_unit = max(align, SHARD_PAGE_BYTES // esz) * max(1, world_size)
-
-        def rup(x, m):
-            return (x + m - 1) // m * m
-
         if not bucket_cap_mb:
             bucket_cap_mb = plan_bucket_mb(world_size, sum(p.numel() for _, p in named) * esz)
         self.bucket_cap_mb = float(bucket_cap_mb)
         cap = max(pad_unit, int(bucket_cap_mb * 1024 * 1024 / esz))
         first_cap = max(pad_unit, int(first_bucket_mb * 1024 * 1024 / esz))
         split_at = 2 * cap if split_oversized else None
+        ordered = decay + nodecay
+        tied_idx = next((i for i, (_, p) in enumerate(ordered) if p is self.tied_param), -1)
+        plan = ddp_plan([p.numel() for _, p in ordered], [0] * len(decay) + [1] * len(nodecay), tied_idx, align,
+                        pad_unit, cap, first_cap, split_at or 0)
+        numel, nb, np_, nr = plan[:4]
+        k = 4
+        offsets = plan[k:k + np_]
+        k += np_
+        bstart, bend, brepl = plan[k:k + nb], plan[k + nb:k + 2 * nb], plan[k + 2 * nb:k + 3 * nb]
+        k += 3 * nb
+        owner_ptr = plan[k:k + np_ + 1]
+        k += np_ + 1
+        owners = plan[k:k + owner_ptr[-1]]
+        k += owner_ptr[-1]
+        regs = plan[k:k + 3 * nr]
+        self.num_split_params = plan[k + 3 * nr]
+        self.buckets: List[Bucket] = [Bucket(index=i, start=bstart[i], end=bend[i], replicated=bool(brepl[i]))
+                                      for i in range(nb)]
         self.layout: List[tuple] = []  # (param, offset, numel, region)
-        self.regions = []  # (start, end, weight_decay_enabled)
-        self.buckets: List[Bucket] = []
         self.param_bucket: Dict[int, List[Bucket]] = {}
-        self.num_split_params = 0
-        off = 0
-        for region, plist in (("decay", decay), ("no_decay", nodecay)):
-            if not plist:
-                continue
-            off = rup(off, pad_unit)
-            rs = off
-            cur = Bucket(index=len(self.buckets), start=off, end=off)
-            self.buckets.append(cur)
-            for n, p in plist:
-                sz = rup(p.numel(), align)
-                limit = first_cap if cur.index == 0 else cap
-                if cur.params and (off + sz - cur.start) > limit:
-                    off = rup(off, pad_unit)
-                    cur.end = off
-                    cur = Bucket(index=len(self.buckets), start=off, end=off)
-                    self.buckets.append(cur)
-                self.layout.append((p, off, p.numel(), region))
-                owners = [cur]
-                cur.params.append(p)
-                end = off + sz
-                if split_at is not None and sz > split_at:
-                    # oversized: cut into ~cap-sized buckets at shard-aligned points inside the parameter
-                    self.num_split_params += 1
-                    while end - cur.start > split_at:
-                        cut = (cur.start + cap) // pad_unit * pad_unit
-                        cur.end = cut
-                        cur = Bucket(index=len(self.buckets), start=cut, end=cut)
-                        self.buckets.append(cur)
-                        cur.params.append(p)
-                        owners.append(cur)
-                self.param_bucket[id(p)] = owners
-                off = end
-                if p is self.tied_param:  # buckets of its own: all-reduced early, updated on every rank
-                    for b in owners:
-                        b.replicated = True
-                    off = rup(off, pad_unit)
-                    cur.end = off
-                    cur = Bucket(index=len(self.buckets), start=off, end=off)
-                    self.buckets.append(cur)
-            off = rup(off, pad_unit)
-            cur.end = off
-            if not cur.params:  # the bucket opened after a tied weight that ended its region
-                self.buckets.pop()
-            self.regions.append((rs, off, region == "decay"))
-        self.numel = off
+        self._param_index: Dict[int, int] = {}
+        for i, (_, p) in enumerate(ordered):
+            self.layout.append((p, offsets[i], p.numel(), "decay" if i < len(decay) else "no_decay"))
+            own = [self.buckets[b] for b in owners[owner_ptr[i]:owner_ptr[i + 1]]]
+            for b in own:
+                b.params.append(p)
+            self.param_bucket[id(p)] = own
+            self._param_index[id(p)] = i
+        self.regions = [(regs[3 * r], regs[3 * r + 1], bool(regs[3 * r + 2])) for r in range(nr)]
+        self._tracker = ReadyTracker(owner_ptr, owners, nb)
+        self.numel = numel
         self.param_flat = torch.zeros(self.numel, dtype=dtype, device=dev)
         self.grad_flat = torch.zeros(self.numel, dtype=self.grad_dtype, device=dev)
         with torch.no_grad():
@@ -208,7 +331,6 @@ class DDPEngine:
                 p.data = self.param_flat[o:o + n].view(p.shape)
                 p.main_grad = self.grad_flat[o:o + n].view(p.shape)
                 p.grad = None
-        self._next = 0
         self._comm_events = []
         # gradient-norm partials computed during backward (SFTAMD_NORM_IN_BWD=1): one sum of squares per
         # bucket (its reduced / owned slice), on a side stream as soon as the bucket is complete, instead of
@@ -308,11 +430,10 @@ class DDPEngine:
                 p._sftamd_norm_slots = self._norm_slot_views.get(id(p)) if self.sync_grads else None
                 p._sftamd_norm_done = False
         for b in self.buckets:
-            b.pending = len(b.params)
             b.ready = False
             b.launched = False
             b.work = None
-        self._next = 0
+        self._tracker.reset()
 
     # ------------------------------------------------------------------ hooks
     def _zero_untouched(self):
@@ -339,22 +460,20 @@ class DDPEngine:
     def _on_param_ready(self, p):
         if not self.sync_grads or (self.world_size == 1 and not self.track_norm):
             return
-        owners = self.param_bucket.get(id(p))
-        if owners is None:
+        i = self._param_index.get(id(p))
+        if i is None:
             return
-        for b in owners:
-            b.pending -= 1
-            if b.pending < 0:
-                raise RuntimeError(f"DDP bucket {b.index}: parameter {self.param_names.get(id(p))} signalled ready "
-                                   "twice")
-            if b.pending == 0:
-                b.ready = True
-        self._launch_ready()
+        try:
+            launch = self._tracker.mark(i)
+        except RuntimeError as e:
+            raise RuntimeError(f"{e} ({self.param_names.get(id(p))})") from None
+        for j in launch:
+            self.buckets[j].ready = True
+            self._launch(self.buckets[j])
 
-    def _launch_ready(self):
-        while self._next < len(self.buckets) and self.buckets[self._next].ready:
-            self._launch(self.buckets[self._next])
-            self._next += 1
+    def bucket_pending(self) -> List[int]:
+        """Parameters each bucket still waits for in the current backward (the ready tracker's counts)."""
+        return self._tracker.pending()
 
     def _launch(self, b: Bucket):
         view = self.grad_flat[b.start:b.end]
@@ -534,9 +653,8 @@ class DDPEngine:
             self._norm_valid = True
         if self.world_size == 1 and not self.track_norm:
             return
-        for b in self.buckets[self._next:]:
-            self._launch(b)
-        self._next = len(self.buckets)
+        for j in self._tracker.drain():
+            self._launch(self.buckets[j])
         self._norm_valid = self.track_norm
         if self.world_size == 1:
             return

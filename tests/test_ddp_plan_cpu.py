@@ -41,7 +41,7 @@ def test_oversized_param_split_layout_and_ready_signalling(world):
         eng._on_param_ready(p)
     if world > 1:  # (a single rank has nothing to communicate: no signalling)
         assert launched == list(range(len(eng.buckets)))
-        assert all(b.pending == 0 and b.ready for b in eng.buckets)
+        assert eng.bucket_pending() == [0] * len(eng.buckets) and all(b.ready for b in eng.buckets)
         with pytest.raises(RuntimeError, match="twice"):
             eng._on_param_ready(emb)
 
@@ -74,3 +74,67 @@ def test_full_smollm3_plan_at_8_ranks_on_meta():
     assert eng.num_split_params == 1 and len(eng.param_bucket[id(m.embed_tokens)]) >= 2
     assert max(sizes) <= 2 * eng.bucket_cap_mb + 1
     assert sizes[0] < 50  # the last layer's down_proj alone (a parameter is never split below 2 caps)
+
+
+def _random_plans():
+    import random
+    rnd = random.Random(0)
+    for case in range(60):
+        n = rnd.randint(1, 40)
+        sizes = [rnd.choice([1, 7, 64, 1000, 4096, 70000, 300000, 2_000_000]) for _ in range(n)]
+        nd = rnd.randint(0, n)
+        region = [0] * nd + [1] * (n - nd)
+        world = rnd.choice([1, 2, 4, 8])
+        pad_unit = 2048 * world
+        cap = rnd.choice([pad_unit, 50_000, 400_000])
+        first_cap = rnd.choice([pad_unit, 20_000])
+        split_at = rnd.choice([0, 2 * cap])
+        tied = rnd.choice([-1, rnd.randrange(n)])
+        yield sizes, region, tied, 64, pad_unit, cap, first_cap, split_at
+
+
+def test_native_bucket_planner_matches_python_twin():
+    """csrc/ddp_reducer.cpp ddp_plan == the Python twin on random parameter lists (regions, oversized splits, tied
+    weight in buckets of its own, world sizes 1-8)."""
+    from llm_fine_tune_distributed_amd.ops import _ext
+    from llm_fine_tune_distributed_amd.parallel.ddp import _plan_python
+    assert _ext.load(), _ext.load_error()
+    for args in _random_plans():
+        assert list(_ext.ops().ddp_plan(*args)) == _plan_python(*args), args
+
+
+def test_native_ready_tracker_matches_python_twin():
+    """Launch order, pending counts and the double-signal error of the native tracker vs the Python twin."""
+    import random
+    from llm_fine_tune_distributed_amd.parallel.ddp import ReadyTracker, _plan_python
+    rnd = random.Random(1)
+    for args in list(_random_plans())[:20]:
+        plan = _plan_python(*args)
+        nb, np_ = plan[1], plan[2]
+        k = 4 + np_ + 3 * nb
+        ptr = plan[k:k + np_ + 1]
+        own = plan[k + np_ + 1:k + np_ + 1 + ptr[-1]]
+        nat, py = ReadyTracker(ptr, own, nb, native=True), ReadyTracker(ptr, own, nb, native=False)
+        assert nat.native and not py.native
+        for _ in range(2):  # reset between backwards
+            nat.reset(), py.reset()
+            order = list(range(np_))
+            rnd.shuffle(order)
+            cut = rnd.randint(0, np_)
+            for i in order[:cut]:
+                assert nat.mark(i) == py.mark(i)
+                assert nat.pending() == py.pending()
+            assert nat.drain() == py.drain()
+        if np_:
+            nat.reset(), py.reset()
+            assert nat.mark(order[0]) == py.mark(order[0])
+            with pytest.raises(RuntimeError, match="twice"):
+                nat.mark(order[0])
+            with pytest.raises(RuntimeError, match="twice"):
+                py.mark(order[0])
+
+
+def test_engine_uses_native_reducer():
+    m = build_model(tiny(), dtype=torch.float32, seed=0)
+    eng = DDPEngine(m, world_size=2, rank=0, bucket_cap_mb=0.05, first_bucket_mb=0.01)
+    assert eng._tracker.native
