@@ -9,5 +9,9 @@ cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 OUT=${1:-gpurun_out/tune.csv}
 shift || true
 cp tuning/tunableop_results_mi355x.csv "$OUT"
+# tuning one shape can take minutes without output: a heartbeat line every 60 s keeps the run visibly alive
+( while sleep 60; do echo "[tune_gemms] still tuning $(date +%T)"; done ) &
+HB=$!
+trap 'kill $HB 2>/dev/null' EXIT
 PYTORCH_TUNABLEOP_ENABLED=1 PYTORCH_TUNABLEOP_TUNING=1 PYTORCH_TUNABLEOP_FILENAME="$OUT" \
     python bench.py --steps 2 --warmup 1 --tunableop off "$@"
