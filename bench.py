@@ -81,6 +81,22 @@ def parse(argv=None):
     ap.add_argument("--baseline-1gpu", type=float, default=float(os.environ.get("SFTAMD_BENCH_1GPU", "0")),
                     help="1-GPU samples/s of the same config: adds scaling_efficiency = value / (N * this)")
     ap.add_argument("--profile-steps", type=int, default=0)
+    # --recipe: the reference recipe end to end instead of the synthetic step loop: its own parquet
+    # (data/qa_dataset.parquet, 90/10 split, system prompt + chat template), per-device batch 8 x GA 2 (README.md:69),
+    # eval every 10 steps, through SFTTrainer.train(); reports HF's train_samples_per_second (wall time INCLUDING the
+    # evals, BASELINE.md "Metric definition") as value, and the pure-training samples/s next to it
+    ap.add_argument("--recipe", action="store_true", help="reference parquet + evals through SFTTrainer.train()")
+    ap.add_argument("--dataset", default=os.path.join(HERE, "data", "qa_dataset.parquet"))
+    ap.add_argument("--eval-steps", type=int, default=10)
+    ap.add_argument("--eval-batch", type=int, default=32,
+                    help="--recipe: per-device eval batch (eval loss is token-weighted, independent of it)")
+    # hang protection for the first RCCL multi-rank runs (utils/heartbeat.py, launch.py): a wall-clock bound on the
+    # whole run, a no-progress bound per rank (also the process group's collective timeout), and opt-in RCCL INFO
+    # capture (SFTAMD_BENCH_RCCL_INFO=1) whose channel / transport summary lands in the JSON line's ``dist``
+    ap.add_argument("--timeout-s", type=float, default=float(os.environ.get("SFTAMD_BENCH_TIMEOUT_S", "900")),
+                    help="wall-clock limit of the whole run; on expiry every rank prints its last heartbeat and exits 124")
+    ap.add_argument("--hang-timeout-s", type=float, default=float(os.environ.get("SFTAMD_BENCH_HANG_S", "300")),
+                    help="seconds without progress (no heartbeat) before a rank is declared hung")
     return ap.parse_args(argv)
 
 
@@ -95,7 +111,8 @@ def launch_ranks(a, argv) -> int:
     launch = importlib.util.module_from_spec(spec)
     spec.loader.exec_module(launch)
     return launch.run(["--nproc-per-node", str(a.gpus), "--master-addr", "127.0.0.1", "--same-session",
-                       "--grace", "15", os.path.abspath(__file__)] + list(argv))
+                       "--grace", "15", "--hang-timeout", str(a.hang_timeout_s), "--deadline", str(a.timeout_s + 60),
+                       os.path.abspath(__file__)] + list(argv))
 
 
 def bucket_plan(engine) -> dict:
@@ -139,6 +156,15 @@ def comm_probe(dev, world: int, nbytes: int, iters: int = 5) -> dict:
 
 
 def run(a):
+    # watchdog of this rank (also under an external torchrun): no heartbeat for hang_timeout_s, or the whole run past
+    # timeout_s -> print the last heartbeat, exit 124 (instead of waiting out the 1800 s process-group default)
+    os.environ.setdefault("SFTAMD_HANG_TIMEOUT_S", str(a.hang_timeout_s))
+    os.environ.setdefault("SFTAMD_RUN_DEADLINE_S", str(a.timeout_s))
+    rccl_dir = None
+    if os.environ.get("SFTAMD_BENCH_RCCL_INFO", "0") == "1" and int(os.environ.get("WORLD_SIZE", "1")) > 1:
+        from llm_fine_tune_distributed_amd.parallel import rccl_info
+        rccl_dir = os.environ.get("SFTAMD_RCCL_LOG_DIR", "/tmp/sftamd_rccl")
+        rccl_info.enable(rccl_dir)
     import torch
     import torch.distributed as dist
 
@@ -147,7 +173,13 @@ def run(a):
     from llm_fine_tune_distributed_amd.parallel.process_group import barrier, setup_distributed
     from llm_fine_tune_distributed_amd.train import SFTConfig, SFTTrainer
 
-    st = setup_distributed(verbose=False, device="cpu" if a.device == "cpu" else None)
+    # the collective timeout sits above the watchdog's, so a stuck collective is reported by the heartbeat watchdog
+    # (last position of this rank, exit 124) rather than by the process group's own abort
+    st = setup_distributed(verbose=False, device="cpu" if a.device == "cpu" else None,
+                           timeout_s=a.hang_timeout_s + 60)
+    from llm_fine_tune_distributed_amd.utils import heartbeat as hb
+    beat = hb.install(hb.Heartbeat(st.rank)).beat
+    beat(0, "init")
     on_gpu = st.device.type == "cuda"
     if a.device == "cuda" and not on_gpu:
         raise SystemExit("--device cuda but no GPU is visible")
@@ -185,10 +217,12 @@ def run(a):
         maybe_inject(st.rank, n_step[0])  # SFTAMD_FAULT_INJECT=rank:step (launcher teardown test)
         return trainer.optimizer_step([next(it) for _ in range(a.ga)], lr=args.learning_rate)
 
+    beat(0, "warmup")
     for _ in range(a.warmup):
         r = step()
     trainer.optimizer.synchronize()
     sync()
+    beat(None, "warmup_done")
     probe = None
     if st.world_size > 1 and os.environ.get("SFTAMD_BENCH_COMM_PROBE", "1") == "1":
         probe = comm_probe(st.device, st.world_size, int(trainer.engine.bucket_cap_mb * 2 ** 20))
@@ -204,11 +238,15 @@ def run(a):
     sync()
     dt = time.perf_counter() - t0
     comm_ms = trainer.engine.comm_exposed_ms(reset=True)
+    beat(None, "timed_done")
     peak = torch.cuda.max_memory_allocated() / 1e9 if on_gpu else 0.0
     mine = {"rank": st.rank, "world_size": dist.get_world_size() if dist.is_initialized() else 1,
             "backend": dist.get_backend() if dist.is_initialized() else None,
             "device": str(st.device), "ms_per_step": round(dt / a.steps * 1e3, 3), "peak_mem_gb": round(peak, 2),
             "comm_exposed_ms": round(comm_ms, 3)}
+    if rccl_dir is not None:
+        from llm_fine_tune_distributed_amd.parallel import rccl_info
+        mine["rccl"] = rccl_info.summarize(rccl_dir)
     ranks = [mine]
     if st.world_size > 1:
         ranks = [None] * st.world_size
@@ -250,7 +288,13 @@ def run(a):
             "dist": {"backend": mine["backend"], "world_size": mine["world_size"],
                      "consistent": all(r_["world_size"] == st.world_size and r_["backend"] == mine["backend"]
                                        for r_ in ranks),
-                     "launcher": os.environ.get("SFTAMD_LAUNCHER", "external" if st.world_size > 1 else "none")},
+                     "launcher": os.environ.get("SFTAMD_LAUNCHER", "external" if st.world_size > 1 else "none"),
+                     "timeout_s": a.timeout_s, "hang_timeout_s": a.hang_timeout_s,
+                     **({"rccl": mine.get("rccl"),
+                         "p2p_transport": (mine.get("rccl") or {}).get("p2p_transport"),
+                         "n_channels": (mine.get("rccl") or {}).get("n_channels"),
+                         "n_channels_per_rank": [(r_.get("rccl") or {}).get("n_channels") for r_ in ranks]}
+                        if rccl_dir is not None else {})},
             "optimizer_sharding": "zero1" if shard else "none",
             "bucket_plan": bucket_plan(trainer.engine),
             "comm_probe": probe,
@@ -272,12 +316,84 @@ def run(a):
         dist.destroy_process_group()
 
 
+def run_recipe(a):
+    """``--recipe``: ``warmup + steps`` optimizer steps of the reference recipe through ``SFTTrainer.train()`` (the
+    timed quantity is HF's: the whole train() wall time, evals included, like the reference's own metric)."""
+    os.environ.setdefault("SFTAMD_HANG_TIMEOUT_S", str(a.hang_timeout_s))
+    os.environ.setdefault("SFTAMD_RUN_DEADLINE_S", str(a.timeout_s))
+    import torch
+
+    from llm_fine_tune_distributed_amd.data.dataset import load_qa_parquet, train_test_split
+    from llm_fine_tune_distributed_amd.data.prompts import format_prompt
+    from llm_fine_tune_distributed_amd.data.tokenizer import load_tokenizer
+    from llm_fine_tune_distributed_amd.models import build_model, get_config
+    from llm_fine_tune_distributed_amd.parallel.process_group import cleanup_distributed, setup_distributed
+    from llm_fine_tune_distributed_amd.train import SFTConfig, SFTTrainer
+
+    st = setup_distributed(verbose=False, device="cpu" if a.device == "cpu" else None, timeout_s=a.hang_timeout_s + 60)
+    on_gpu = st.device.type == "cuda"
+    if on_gpu and a.tunableop != "off" and "PYTORCH_TUNABLEOP_ENABLED" not in os.environ:
+        from llm_fine_tune_distributed_amd.utils.gemm_tuning import enable_tuned_gemms
+        enable_tuned_gemms(tune=(a.tunableop == "tune"), verbose=st.is_main)
+    rows = load_qa_parquet(a.dataset)
+    train_rows, val_rows = train_test_split(rows, test_size=0.1, seed=42)
+    train_rows = [format_prompt(r) for r in train_rows]
+    val_rows = [format_prompt(r) for r in val_rows]
+    cfg = get_config(a.model)
+    model = build_model(cfg, device=st.device, dtype=torch.bfloat16, seed=0)
+    micro = 8 if a.micro_batch == 16 else a.micro_batch  # the recipe's own split: 8 x GA 2 (README.md:69)
+    ga = 2 if a.ga == 1 else a.ga
+    total = a.warmup + a.steps
+    args = SFTConfig(output_dir="/tmp/sftamd_bench_recipe", per_device_train_batch_size=micro,
+                     per_device_eval_batch_size=a.eval_batch, gradient_accumulation_steps=ga,
+                     learning_rate=5e-5 * st.world_size, max_grad_norm=1.0, max_steps=total, logging_steps=2,
+                     logging_first_step=True, eval_strategy="steps", eval_steps=a.eval_steps, save_strategy="no",
+                     bf16=True, gradient_checkpointing=False, max_length=1024, dataloader_drop_last=True,
+                     jsonl_log=False, freeze_policy=a.freeze_policy, shard_optimizer_state=bool(a.zero),
+                     dataset_cache=False, gemm_tuning=False,
+                     **({} if a.ga_merge_max_tokens is None else {"ga_merge_max_tokens": a.ga_merge_max_tokens}))
+    trainer = SFTTrainer(model=model, args=args, train_dataset=train_rows, eval_dataset=val_rows,
+                         processing_class=load_tokenizer(None))
+    if on_gpu:
+        torch.cuda.synchronize()
+    out = trainer.train()
+    m = out.metrics
+    evals = [h for h in trainer.state.log_history if "eval_loss" in h]
+    if st.is_main:
+        samples_per_step = micro * ga * st.world_size
+        rec = {
+            "metric": "samples/sec SmolLM3-3B full SFT bf16, reference recipe (HF train_samples_per_second incl. evals)"
+            if a.model == "smollm3-3b" and a.freeze_policy == "full" else f"samples/sec {a.model} recipe",
+            "value": round(m["train_samples_per_second"], 3), "unit": "samples/s", "n_gpus": st.world_size,
+            "steps": total, "warmup": 0, "ms_per_step": round(m["train_runtime"] / max(1, out.global_step) * 1e3, 3),
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "bf16",
+            "data": "reference data/qa_dataset.parquet (offline synthetic tokenizer), random-init weights",
+            "config": {"model": {"smollm3-3b": "SmolLM3-3B"}.get(a.model, a.model), "freeze_policy": a.freeze_policy,
+                       "global_batch": samples_per_step, "per_device_batch": micro,
+                       "gradient_accumulation_steps": ga, "seq_len": "ragged <= 1024 (padded to 64)",
+                       "parallelism": f"dp{st.world_size}", "eval_steps": a.eval_steps,
+                       "per_device_eval_batch": a.eval_batch},
+            "train_pure_samples_per_second": round(m["train_pure_samples_per_second"], 3),
+            "train_tokens_per_second": round(m["train_tokens_per_second"], 1),
+            "train_mfu": round(m.get("train_mfu", 0.0), 4), "train_runtime_s": round(m["train_runtime"], 3),
+            "eval_runtime_s": round(sum(h.get("eval_runtime", 0.0) for h in evals), 3), "n_evals": len(evals),
+            "final_eval_loss": round(evals[-1]["eval_loss"], 4) if evals else None,
+            "train_loss": round(out.training_loss, 4),
+            "peak_mem_gb": round(torch.cuda.max_memory_allocated() / 1e9, 2) if on_gpu else 0.0,
+        }
+        print(json.dumps(rec), flush=True)
+    cleanup_distributed()
+
+
 def main(argv=None):
     argv = sys.argv[1:] if argv is None else argv
     a = parse(argv)
     if a.gpus > 1 and "WORLD_SIZE" not in os.environ:
         sys.exit(launch_ranks(a, argv))
-    run(a)
+    if a.recipe:
+        run_recipe(a)
+    else:
+        run(a)
 
 
 if __name__ == "__main__":

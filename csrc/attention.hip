@@ -1844,6 +1844,7 @@ std::tuple<at::Tensor, at::Tensor> flash_fwd(const at::Tensor& qkv, const at::Te
   if (attn_impl() == 3) {
     int nw, nbuf;
     attn_cfg(nw, nbuf);
+    SFT_TRACE(nw == 8 ? "attn.fwd3" : "attn.fwd3.w4");
     auto go3 = [&](auto w) {
       constexpr int NW = decltype(w)::value;
       dim3 g3(nq, nseq, (max_seqlen + NW * 16 - 1) / (NW * 16));
@@ -1981,6 +1982,9 @@ static at::Tensor flash_bwd_impl(const at::Tensor& dout, const at::Tensor& qkv, 
     const bool grouped = rep > 1 && attn_gqa_grouped();
     const bool rope = grouped && rcos != nullptr;
     at::Tensor part;
+    SFT_TRACE(grouped ? "attn.dkdv5" : "attn.dkdv3");
+    SFT_TRACE("attn.dq4");
+    if (rope) SFT_TRACE("attn.bwd_rope_epi");
     if (grouped) {
       attn::launch_dkdv5((const u16*)qkv.data_ptr(), (const u16*)dout.data_ptr(), lse.data_ptr<float>(),
                          delta.data_ptr<float>(), cu_c.data_ptr<int>(), (u16*)dqkv.data_ptr(), nq, nkv, total, nseq,
@@ -2015,6 +2019,7 @@ static at::Tensor flash_bwd_impl(const at::Tensor& dout, const at::Tensor& qkv, 
   auto run3 = [&](auto w) {
     constexpr int NW = decltype(w)::value;
     const int rep = nq / nkv;
+    SFT_TRACE("attn.dq3");
     // dq first: on the side stream it starts filling the GPU while dK/dV is enqueued
     dim3 gq3(nq, nseq, (max_seqlen + NW * 16 - 1) / (NW * 16));
     attn::bwd_dq3_kernel<NW><<<gq3, NW * 64, 0, dq_stream>>>(

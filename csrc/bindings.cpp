@@ -4,6 +4,7 @@
 // native data-pipeline ops below which are CPU kernels.
 #include <torch/library.h>
 
+#include <string>
 #include <vector>
 
 namespace sftamd {
@@ -13,6 +14,8 @@ int64_t ipc_ar_create(int64_t cap, int64_t world, int64_t rank);
 std::vector<int64_t> ipc_ar_handle(int64_t id);
 void ipc_ar_open(int64_t id, std::vector<int64_t> handles);
 int64_t ipc_ar_check(int64_t id);
+int64_t ipc_ar_poll(int64_t id);
+int64_t ipc_ar_uncached(int64_t id);
 void ipc_ar_destroy(int64_t id);
 // csrc/ddp_reducer.cpp: bucket planner + ready tracker of the DDP engine
 std::vector<int64_t> ddp_plan(std::vector<int64_t> sizes, std::vector<int64_t> region, int64_t tied, int64_t align,
@@ -23,6 +26,9 @@ std::vector<int64_t> ddp_tracker_mark(int64_t id, int64_t param);
 std::vector<int64_t> ddp_tracker_drain(int64_t id);
 std::vector<int64_t> ddp_tracker_pending(int64_t id);
 void ddp_tracker_destroy(int64_t id);
+// csrc/dispatch_trace.cpp
+void dispatch_trace(bool on);
+std::string dispatch_trace_read();
 }
 
 TORCH_LIBRARY(sftamd, m) {
@@ -33,6 +39,8 @@ TORCH_LIBRARY(sftamd, m) {
   m.def("ipc_ar_handle(int ctx) -> int[]", &sftamd::ipc_ar_handle);
   m.def("ipc_ar_open(int ctx, int[] handles) -> ()", &sftamd::ipc_ar_open);
   m.def("ipc_ar_check(int ctx) -> int", &sftamd::ipc_ar_check);
+  m.def("ipc_ar_poll(int ctx) -> int", &sftamd::ipc_ar_poll);
+  m.def("ipc_ar_uncached(int ctx) -> int", &sftamd::ipc_ar_uncached);
   m.def("ipc_ar_destroy(int ctx) -> ()", &sftamd::ipc_ar_destroy);
   // runtime: DDP bucket planner / ready tracker (CPU, no tensor arguments)
   m.def("ddp_plan(int[] sizes, int[] region, int tied, int align, int pad_unit, int cap, int first_cap, "
@@ -44,6 +52,9 @@ TORCH_LIBRARY(sftamd, m) {
   m.def("ddp_tracker_pending(int id) -> int[]", &sftamd::ddp_tracker_pending);
   m.def("ddp_tracker_destroy(int id) -> ()", &sftamd::ddp_tracker_destroy);
   m.def("ipc_ar_allreduce(Tensor(a!) x, int ctx, int round, int blocks=16) -> ()");
+  // runtime: dispatch trace of the kernel variants launched (tests assert the default paths)
+  m.def("dispatch_trace(bool on) -> ()", &sftamd::dispatch_trace);
+  m.def("dispatch_trace_read() -> str", &sftamd::dispatch_trace_read);
   // norms / elementwise
   m.def("rmsnorm_fwd(Tensor x, Tensor? residual, Tensor weight, float eps) -> (Tensor, Tensor, Tensor)");
   m.def("rmsnorm_bwd(Tensor dy, Tensor h, Tensor weight, Tensor rstd, Tensor? dres, Tensor(a!)? dw_out=None, bool accumulate=False) -> (Tensor, Tensor)");

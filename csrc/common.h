@@ -10,6 +10,7 @@
 #include <torch/library.h>
 
 #include <cstdint>
+#include <string>
 
 namespace sftamd {
 
@@ -73,6 +74,15 @@ inline int num_cus() { return 256; }  // MI355X: 8 XCDs x 32 CUs
 #define SFT_CHECK_BF16(t) SFT_CHECK((t).scalar_type() == at::kBFloat16, #t " must be bfloat16")
 #define SFT_CHECK_CONTIG(t) SFT_CHECK((t).is_contiguous(), #t " must be contiguous")
 #define SFT_LAUNCH_CHECK() C10_HIP_KERNEL_LAUNCH_CHECK()
+
+// dispatch trace (csrc/dispatch_trace.cpp): SFT_TRACE("attn.fwd3") / SFT_TRACE(trace_name("tn.c", cfg))
+bool trace_on();
+void trace_hit(const std::string& name);
+inline std::string trace_name(const char* base, long v) { return std::string(base) + std::to_string(v); }
+#define SFT_TRACE(name)                                 \
+  do {                                                  \
+    if (::sftamd::trace_on()) ::sftamd::trace_hit(name); \
+  } while (0)
 
 // Device-side invariant checks, compiled in only by `python build_ext.py --debug` (-DSFTAMD_DEBUG,
 // separate _C_debug.so loaded when SFTAMD_DEBUG=1). The release kernels clamp or skip bad inputs

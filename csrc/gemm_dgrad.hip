@@ -521,6 +521,7 @@ at::Tensor dgrad_gemm(const at::Tensor& dy, const at::Tensor& w, const c10::opti
   // SFTAMD_DGRAD_TAIL: 0 = off, 2 / 3 = the half-tile config (default 2).
   auto run1 = [&](auto epi, int c, const at::Tensor& wv, const dgrad::EpiArgs& e) {
     constexpr int E = decltype(epi)::value;
+    SFT_TRACE(trace_name(E == dgrad::EPI_SWIGLU_BWD ? "dgrad.swiglu.c" : "dgrad.c", c));
     switch (c) {
       case 1: dgrad::launch<256, 256, 2, 4, 3, E>(dy, wv, e); break;
       case 2: dgrad::launch<256, 128, 4, 2, 3, E>(dy, wv, e); break;
@@ -548,6 +549,7 @@ at::Tensor dgrad_gemm(const at::Tensor& dy, const at::Tensor& w, const c10::opti
       return;
     }
     const long n_split = main_n * 256;
+    SFT_TRACE("dgrad.tail");
     run1(epi, (int)cfg, w.narrow(1, 0, n_split), ea);
     dgrad::EpiArgs et = ea;
     et.out = ea.out + n_split;

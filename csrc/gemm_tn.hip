@@ -934,6 +934,416 @@ __global__ void __launch_bounds__(512) tn3_kernel(const u16* __restrict__ A, con
     epilogue<G, EPI>(smem, acc, ea, m0, n0, wm, wn, w, lane);
 }
 
+// ============================================================================================
+// 4-wave 128 x 128 wave tiles (cfg 12): ONE wave per SIMD, 256 fp32 accumulators in the AGPR file.
+// Why: at 8 waves of 128 x 64 every 32 MFMAs of a wave need 12 fragment reads (8 A + 4 B); a 128 x 128
+// wave tile needs 16 per 64 MFMAs — a third fewer LDS read bytes per FLOP, which is what the chip's clock
+// under load responds to (MI355X_MICROARCH.md 'DVFS give-back'; hipBLASLt's 4-wave kernel holds ~2.17 GHz
+// vs ~1.94 for the 8-wave ping-pong on gate_up, profiles/r2_gemm_pingpong.md). hipcc cannot allocate
+// 256 accumulators next to double-buffered fragments when they are builtin MFMA values (it renames and
+// shuffles them through v_accvgpr_read/write, or spills: profiles/r1_gemm_tn.md); the MFMAs are therefore
+// inline asm with the accumulator TIED in an AGPR ("+a"), which pins every accumulator in place.
+// Hazards hipcc does not see for those asm MFMAs (cdna_hip_programming.md §5.7): fragment operands come
+// only from ds_read (retired by the explicit lgkmcnt(0) at every sub-step boundary, no VALU writer), and
+// the accumulators are read only after the loop, behind 20 wait states + a scheduling fence.
+// Schedule per 64-deep K-tile t (stage X = t, Y = t + 1, 64 KB each, 128-byte image rows, swz2):
+//   sub-step 0: 64 MFMA on F0 = (t, k 0..31) | ds_read F1 = (t, k 32..63) from X
+//   vmcnt(0) lgkmcnt(0) + barrier: tile t + 1 landed in Y, every wave is done reading X
+//   sub-step 1: 64 MFMA on F1 | ds_read F0 = (t + 1, k 0..31) from Y | glds tile t + 2 -> X (16 pieces/wave)
+// One barrier per K-tile; a tile's DMA has 1.5 sub-steps to land. K % 128 == 0 (even tile count).
+// ============================================================================================
+__device__ __forceinline__ void mfma_a(f32x4& c, const bf16x8& a, const bf16x8& b) {
+  asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+a"(c) : "v"(a), "v"(b));
+}
+
+template <int EPI>
+struct Stager4 {
+  const u16* pa;  // this lane's source in the wave's first A piece (image rows 8 w + lr)
+  const u16* pb;  // ... first B piece
+  long a32;       // A pieces j, j + 1 are 32 rows apart
+  long boff[8];   // B piece q relative to piece 0 (EPI row permutation)
+  __device__ __forceinline__ void piece(char* stage, int w, int j) {
+    const u16* src = j < 8 ? pa + j * a32 : pb + boff[j - 8];
+    glds16(src, stage + (w + 4 * j) * 1024);
+  }
+};
+
+// DIAG (timing-only builds, wrong results; tools/bench_gemm_tn.py cfg 1200 + DIAG): bit 0 = no DMA in the loop,
+// bit 1 = no fragment reads in the loop, bit 2 = no barriers in the loop.
+// One sub-step = 8 MFMA groups (fragment row i x the 8 B fragments). FRONT: the 16 fragment reads for the next
+// sub-step are issued after groups 0..3 (4 per group) so they have half a sub-step to land before the boundary's
+// lgkmcnt(0), instead of trailing into it. DMA pieces [J0, J0 + NP) of the wave are spread over the 8 groups. BAR: the
+// K-tile barrier is issued after group 0's MFMAs (which need only registers), ahead of the group's reads / DMA.
+template <int EPI, int DIAG, bool FRONT, int J0, int NP, bool BAR, int DG = 8>
+__device__ __forceinline__ void tn4_sub(f32x4 (&acc)[8][8], const bf16x8 (&fa)[8], const bf16x8 (&fb)[8],
+                                        bf16x8 (&ra)[8], bf16x8 (&rb)[8], const char* img, int offA, int offB,
+                                        Stager4<EPI>& st, char* dst, int w) {
+  static_assert(NP % DG == 0 && J0 + NP <= 16, "DMA pieces per group");
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) mfma_a(acc[i][j], fa[i], fb[j]);
+    if (BAR && i == 0 && !(DIAG & 4)) __builtin_amdgcn_s_barrier();
+    if (!(DIAG & 2)) {
+      if (!FRONT) {
+        ra[i] = lds_row(img, offA + 2048 * i);
+        rb[i] = lds_row(img, offB + 2048 * i);
+      } else if (i < 4) {
+        ra[2 * i] = lds_row(img, offA + 2048 * (2 * i));
+        rb[2 * i] = lds_row(img, offB + 2048 * (2 * i));
+        ra[2 * i + 1] = lds_row(img, offA + 2048 * (2 * i + 1));
+        rb[2 * i + 1] = lds_row(img, offB + 2048 * (2 * i + 1));
+      }
+    } else {
+      asm volatile("" : "+v"(ra[i]), "+v"(rb[i]));
+    }
+    if (!(DIAG & 1)) {
+      // DG = groups the DMA is spread over (8: the whole sub-step; 4 / 2: front-loaded, more time to land)
+      if (i < DG) {
+#pragma unroll
+        for (int k = 0; k < NP / DG; ++k) st.piece(dst, w, J0 + i * (NP / DG) + k);
+      }
+    }
+  }
+}
+
+// VAR: bit 0 FRONT reads, bit 1 split DMA (8 pieces in sub-step 1 of tile t, 8 in sub-step 0 of tile t + 1 — the
+// tile's 64 KB spread over a whole K-tile of MFMA instead of one sub-step), bit 2 barrier after the first MFMA group,
+// bit 3 / bit 4: the sub-step-1 DMA front-loaded into MFMA groups 0-3 / 0-1 (more time to land before the next
+// boundary's vmcnt(0))
+template <int EPI, int DIAG = 0, int VAR = 0>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1)))
+tn4_kernel(const u16* __restrict__ A, const u16* __restrict__ B, int K, long lda, long ldb, int nbm, int nbn,
+           int group, EpiArgs ea) {
+  using G = Cfg2<256, 256, 2, 2, 2>;
+  constexpr bool FRONT = VAR & 1, BAR = VAR & 4;
+  constexpr int P1 = (VAR & 2) ? 8 : 16, NB = 16 - P1;  // DMA pieces per wave in sub-step 1 / the next sub-step 0
+  constexpr int DG1 = (VAR & 16) ? 2 : ((VAR & 8) ? 4 : 8);
+  __shared__ __attribute__((aligned(16))) char smem[G::LDS];
+  const int nwg = gridDim.x, orig = blockIdx.x;
+  const int xcd = orig & 7, q8 = nwg >> 3, r8 = nwg & 7;
+  const int wgid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (orig >> 3);
+  const int per_group = group * nbn;
+  const int grp = wgid / per_group, first = grp * group;
+  const int gsz = min(nbm - first, group);
+  const int in = wgid - grp * per_group;
+  const int bm = first + in % gsz, bn = in / gsz;
+  const int m0 = bm * 256, n0 = bn * 256;
+  const int tid = threadIdx.x, lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = w >> 1, wn = w & 1;
+  const int nk = K / BK2;
+
+  Stager4<EPI> st;
+  {
+    // piece P = w + 4 j holds image rows 8 P + lr (lr = lane >> 3), slot lane & 7; (row >> 1) & 7 = 4 (P & 1) +
+    // (lr >> 1) and P & 1 = w & 1 for every piece of the wave
+    const int lr = lane >> 3, ch = (lane & 7) ^ (4 * (w & 1) + (lr >> 1));
+    st.pa = A + (long)(m0 + 8 * w + lr) * lda + 8 * ch;
+    st.a32 = 32 * lda;
+    const int r0 = b2_row<EPI>(w, n0, ea.I);
+    st.pb = B + (long)(r0 + lr) * ldb + 8 * ch;
+#pragma unroll
+    for (int q = 0; q < 8; ++q) st.boff[q] = (long)b2_koff<EPI, 4>(q) * ldb;
+  }
+  const int g = lane >> 4, ii = lane & 15;
+  const int ra = wm * 128 + ii, rb = 256 + wn * 128 + ii;
+  const int offA0 = ra * ROWB2 + 16 * swz2(ra, g), offA1 = ra * ROWB2 + 16 * swz2(ra, 4 + g);
+  const int offB0 = rb * ROWB2 + 16 * swz2(rb, g), offB1 = rb * ROWB2 + 16 * swz2(rb, 4 + g);
+  f32x4 acc[8][8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  char* X = smem;
+  char* Y = smem + G::STAGE;
+  // prologue: tile 0 -> X, the first P1 pieces of tile 1 -> Y (the rest in sub-step 0 of tile 0)
+#pragma unroll
+  for (int j = 0; j < 16; ++j) st.piece(X, w, j);
+  st.pa += BK2;
+  st.pb += BK2;
+#pragma unroll
+  for (int j = 0; j < P1; ++j) st.piece(Y, w, j);
+  if (NB == 0) {
+    st.pa += BK2;
+    st.pb += BK2;
+  }
+  if (!(DIAG & 16)) {  // DIAG 16 (timing only): the prologue's wait for tile 0 skipped
+    __builtin_amdgcn_s_waitcnt(waitcnt_imm(P1, 15));  // tile 0 landed (tile 1 may fly)
+    __builtin_amdgcn_s_barrier();
+  }
+  bf16x8 a0[8], b0[8], a1[8], b1[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    a0[i] = lds_row(X, offA0 + 2048 * i);
+    b0[i] = lds_row(X, offB0 + 2048 * i);
+  }
+  // Two K-tiles per pass: t on X, t + 1 on Y. Branch-free (a conditional sub-step splits the accumulators' live
+  // ranges and hipcc spills them); the last pass, whose only DMA is the rest of tile nk - 1, is peeled.
+  auto body = [&](auto d0, auto d1) {
+    constexpr bool D0 = decltype(d0)::value, D1 = decltype(d1)::value;  // DMA of the first / the other sub-steps
+    __builtin_amdgcn_s_waitcnt(waitcnt_imm(63, 0));
+    tn4_sub<EPI, DIAG, FRONT, P1, D0 ? NB : 0, false>(acc, a0, b0, a1, b1, X, offA1, offB1, st, Y, w);
+    if (D0 && NB) {
+      st.pa += BK2;
+      st.pb += BK2;
+    }
+    __builtin_amdgcn_s_waitcnt(waitcnt_imm(0, 0));
+    if (!BAR && !(DIAG & 4)) __builtin_amdgcn_s_barrier();
+    tn4_sub<EPI, DIAG, FRONT, 0, D1 ? P1 : 0, BAR, DG1>(acc, a1, b1, a0, b0, Y, offA0, offB0, st, X, w);
+    if (D1 && NB == 0) {
+      st.pa += BK2;
+      st.pb += BK2;
+    }
+    __builtin_amdgcn_s_waitcnt(waitcnt_imm(63, 0));
+    tn4_sub<EPI, DIAG, FRONT, P1, D1 ? NB : 0, false>(acc, a0, b0, a1, b1, Y, offA1, offB1, st, X, w);
+    if (D1 && NB) {
+      st.pa += BK2;
+      st.pb += BK2;
+    }
+    __builtin_amdgcn_s_waitcnt(waitcnt_imm(0, 0));
+    if (!BAR && !(DIAG & 4)) __builtin_amdgcn_s_barrier();
+    tn4_sub<EPI, DIAG, FRONT, 0, D1 ? P1 : 0, BAR, DG1>(acc, a1, b1, a0, b0, X, offA0, offB0, st, Y, w);
+    if (D1 && NB == 0) {
+      st.pa += BK2;
+      st.pb += BK2;
+    }
+  };
+  for (int t = 0; t < nk - 2; t += 2) body(std::true_type(), std::true_type());
+  body(std::true_type(), std::false_type());
+  // the last MFMAs' results are read by the epilogue's v_accvgpr_read: 20 wait states, then a fence that keeps
+  // the compiler from hoisting those reads above the nops
+  asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 3" ::: "memory");
+  __builtin_amdgcn_sched_barrier(0);
+  __builtin_amdgcn_s_waitcnt(waitcnt_imm(0, 0));
+  __syncthreads();
+  if constexpr (DIAG & 8) {  // timing only: no epilogue (one value per lane keeps the accumulators live)
+    float sum = 0.f;
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) sum += acc[i][j][0] + acc[i][j][1] + acc[i][j][2] + acc[i][j][3];
+    if (sum == 1.2345f) ea.C[tid] = 1;
+  } else {
+    epilogue<G, EPI>(smem, acc, ea, m0, n0, wm, wn, w, lane);
+  }
+}
+
+template <int EPI, int DIAG = 0, int VAR = 0>
+void launch4(const at::Tensor& a, const at::Tensor& w, int N, const EpiArgs& ea) {
+  const int M = a.size(0), K = a.size(1);
+  SFT_CHECK(M % 256 == 0 && N % 256 == 0 && K % 128 == 0, "gemm_tn 4-wave: M, N % 256, K % 128");
+  const int nbm = M / 256, nbn = N / 256;
+  tn4_kernel<EPI, DIAG, VAR><<<nbm * nbn, 256, 0, cur_stream()>>>((const u16*)a.data_ptr(), (const u16*)w.data_ptr(), K,
+                                                       a.stride(0), w.stride(0), nbm, nbn, std::min(group_m(), nbm),
+                                                       ea);
+  SFT_LAUNCH_CHECK();
+}
+
+// ============================================================================================
+// Persistent 4-wave GEMM (cfg 50): the cfg 12 main loop with the per-tile fixed cost taken off the critical path.
+// A K = 2048 tile round of the non-persistent kernels costs ~16 us besides its K loop (K sweep: 0.228 ms per 1024 of
+// K + 0.18 ms fixed on gate_up, profiles/r3_gemm_4wave.md): the prologue's 128 KB burst of every CU at once and the
+// LDS-staged epilogue's store burst. Here one workgroup per CU walks its XCD's tiles (per-XCD contiguous ranges of
+// the GROUP_M order, so the XCD's 32 CUs share A / B panels in its L2), and per tile:
+//   * the NEXT tile's first K-tile is DMA'd into stage X during the last sub-step (both stages are free after the
+//     last barrier: that sub-step's MFMAs need only registers), its second K-tile into Y right after the epilogue;
+//   * the epilogue stores straight from registers: TRC MFMAs (B fragment first) leave each lane 4 consecutive columns
+//     of a row per fragment; v_permlane16_swap between fragment pairs makes that 8 (16 bytes), so a tile is 32
+//     16-byte stores per lane, issued and not waited for (the next tile's MFMAs run while they drain);
+//   * the first sub-step's MFMAs take srcC = 0 (no accumulator zeroing pass).
+// vmcnt bookkeeping (loads and stores share the counter): next K0 (16) < stores (32) < next K1 (16), so "K0 landed"
+// is vmcnt(48) — within the counter's 63.
+// ============================================================================================
+template <bool INIT>
+__device__ __forceinline__ void mfma_t(f32x4& c, const bf16x8& b, const bf16x8& a) {
+  if constexpr (INIT)
+    asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, 0" : "=a"(c) : "v"(b), "v"(a));
+  else
+    asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+a"(c) : "v"(b), "v"(a));
+}
+
+// one sub-step: 8 MFMA groups (fragment row i x 8 B fragments, TRC); READ: the next sub-step's 16 fragments from img;
+// NP DMA pieces spread over the first DG groups; BAR: the K-tile barrier after group 0
+template <int EPI, bool INIT, bool READ, int NP, bool BAR, int DG = 4>
+__device__ __forceinline__ void tn5_sub(f32x4 (&acc)[8][8], const bf16x8 (&fa)[8], const bf16x8 (&fb)[8],
+                                        bf16x8 (&ra)[8], bf16x8 (&rb)[8], const char* img, int offA, int offB,
+                                        Stager4<EPI>& st, char* dst, int w) {
+  static_assert(NP % DG == 0, "DMA pieces per group");
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) mfma_t<INIT>(acc[i][j], fb[j], fa[i]);
+    if (BAR && i == 0) __builtin_amdgcn_s_barrier();
+    if (READ) {
+      ra[i] = lds_row(img, offA + 2048 * i);
+      rb[i] = lds_row(img, offB + 2048 * i);
+    }
+    if (i < DG) {
+#pragma unroll
+      for (int k = 0; k < NP / DG; ++k) st.piece(dst, w, i * (NP / DG) + k);
+    }
+  }
+}
+
+template <int EPI>
+__device__ __forceinline__ void tn5_stager(Stager4<EPI>& st, const u16* A, const u16* B, long lda, long ldb, int m0,
+                                           int n0, int w, int lane, int I) {
+  const int lr = lane >> 3, ch = (lane & 7) ^ (4 * (w & 1) + (lr >> 1));
+  st.pa = A + (long)(m0 + 8 * w + lr) * lda + 8 * ch;
+  st.pb = B + (long)(b2_row<EPI>(w, n0, I) + lr) * ldb + 8 * ch;
+}
+
+__device__ __forceinline__ void tn5_coords(int tile, int nbm, int nbn, int group, int& m0, int& n0) {
+  const int per_group = group * nbn;
+  const int grp = tile / per_group, first = grp * group;
+  const int gsz = min(nbm - first, group);
+  const int in = tile - grp * per_group;
+  m0 = (first + in % gsz) * 256;
+  n0 = (in / gsz) * 256;
+}
+
+__device__ __forceinline__ unsigned pack2(float a, float b) { return (unsigned)f2bf(a) | ((unsigned)f2bf(b) << 16); }
+
+// TRC accumulators of the wave's 128 x 128 tile -> C: 32 16-byte stores per lane (see above)
+__device__ __forceinline__ void tn5_store(f32x4 (&acc)[8][8], u16* C, long ldc, int row0, int col0, int lane) {
+  const int g = lane >> 4, ii = lane & 15;
+  u16* base = C + (long)(row0 + ii) * ldc + col0 + 16 * (g & 1) + 4 * (g & 2);
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+#pragma unroll
+    for (int p = 0; p < 4; ++p) {
+      unsigned v0 = pack2(acc[i][2 * p][0], acc[i][2 * p][1]), v1 = pack2(acc[i][2 * p][2], acc[i][2 * p][3]);
+      unsigned w0 = pack2(acc[i][2 * p + 1][0], acc[i][2 * p + 1][1]);
+      unsigned w1 = pack2(acc[i][2 * p + 1][2], acc[i][2 * p + 1][3]);
+      auto r0 = __builtin_amdgcn_permlane16_swap(v0, w0, false, false);
+      auto r1 = __builtin_amdgcn_permlane16_swap(v1, w1, false, false);
+      *(uint4*)(base + (long)(16 * i) * ldc + 32 * p) = make_uint4(r0[0], r1[0], r0[1], r1[1]);
+    }
+  }
+}
+
+template <int EPI, bool NK2>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1)))
+tn5_kernel(const u16* __restrict__ A, const u16* __restrict__ B, int K, long lda, long ldb, int nbm, int nbn,
+           int group, EpiArgs ea) {
+  using G = Cfg2<256, 256, 2, 2, 2>;
+  static_assert(EPI == EPI_PLAIN, "persistent 4-wave GEMM: plain epilogue");
+  __shared__ __attribute__((aligned(16))) char smem[2 * G::STAGE];
+  const int tiles = nbm * nbn, nwg = gridDim.x, orig = blockIdx.x;
+  // this XCD's contiguous share of the tile order, walked round-robin by its workgroups (blocks b, b + 8, ...)
+  const int xcd = orig & 7, l = orig >> 3, nx = (nwg - xcd + 7) >> 3;
+  const int q8 = tiles >> 3, r8 = tiles & 7;
+  const int t_end = xcd * q8 + min(xcd, r8) + q8 + (xcd < r8 ? 1 : 0);
+  int tile = xcd * q8 + min(xcd, r8) + l;
+  if (tile >= t_end) return;
+  const int tid = threadIdx.x, lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = w >> 1, wn = w & 1;
+  const int nk = K / BK2;
+  const int g = lane >> 4, ii = lane & 15;
+  const int ra = wm * 128 + ii, rb = 256 + wn * 128 + ii;
+  const int offA0 = ra * ROWB2 + 16 * swz2(ra, g), offA1 = ra * ROWB2 + 16 * swz2(ra, 4 + g);
+  const int offB0 = rb * ROWB2 + 16 * swz2(rb, g), offB1 = rb * ROWB2 + 16 * swz2(rb, 4 + g);
+  char* X = smem;
+  char* Y = smem + G::STAGE;
+  Stager4<EPI> st;
+  st.a32 = 32 * lda;
+#pragma unroll
+  for (int q = 0; q < 8; ++q) st.boff[q] = (long)b2_koff<EPI, 4>(q) * ldb;
+  int m0, n0;
+  tn5_coords(tile, nbm, nbn, group, m0, n0);
+  tn5_stager(st, A, B, lda, ldb, m0, n0, w, lane, ea.I);
+#pragma unroll
+  for (int j = 0; j < 16; ++j) st.piece(X, w, j);
+  st.pa += BK2;
+  st.pb += BK2;
+#pragma unroll
+  for (int j = 0; j < 16; ++j) st.piece(Y, w, j);
+  st.pa += BK2;
+  st.pb += BK2;
+  __builtin_amdgcn_s_waitcnt(waitcnt_imm(16, 15));  // K0 of the first tile (its K1 may fly)
+  f32x4 acc[8][8];
+  bf16x8 a0[8], b0[8], a1[8], b1[8];
+  for (;;) {
+    __builtin_amdgcn_s_barrier();
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      a0[i] = lds_row(X, offA0 + 2048 * i);
+      b0[i] = lds_row(X, offB0 + 2048 * i);
+    }
+    const int next = tile + nx;
+    const bool has_next = next < t_end;
+    int m1 = m0, n1 = n0;
+    if (has_next) tn5_coords(next, nbm, nbn, group, m1, n1);
+    // K-tile pairs (t on X, t + 1 on Y); boundary = vmcnt(0) lgkmcnt(0) + the barrier after the next sub-step's
+    // first MFMA group. LAST: the final sub-step DMAs the next tile's K0 into X (the current tile's K0 again when
+    // there is none: branch-free, harmless) and reads nothing.
+    auto pair = [&](auto init, auto dma, auto last) {
+      constexpr bool IN = decltype(init)::value, DM = decltype(dma)::value, LA = decltype(last)::value;
+      __builtin_amdgcn_s_waitcnt(waitcnt_imm(63, 0));
+      tn5_sub<EPI, IN, true, 0, false>(acc, a0, b0, a1, b1, X, offA1, offB1, st, X, w);
+      __builtin_amdgcn_s_waitcnt(waitcnt_imm(0, 0));
+      tn5_sub<EPI, false, true, DM ? 16 : 0, true>(acc, a1, b1, a0, b0, Y, offA0, offB0, st, X, w);
+      if (DM) {
+        st.pa += BK2;
+        st.pb += BK2;
+      }
+      __builtin_amdgcn_s_waitcnt(waitcnt_imm(63, 0));
+      tn5_sub<EPI, false, true, 0, false>(acc, a0, b0, a1, b1, Y, offA1, offB1, st, Y, w);
+      __builtin_amdgcn_s_waitcnt(waitcnt_imm(0, 0));
+      if constexpr (LA) {
+        tn5_stager(st, A, B, lda, ldb, m1, n1, w, lane, ea.I);
+        tn5_sub<EPI, false, false, 16, true>(acc, a1, b1, a0, b0, X, offA0, offB0, st, X, w);
+      } else {
+        tn5_sub<EPI, false, true, 16, true>(acc, a1, b1, a0, b0, X, offA0, offB0, st, Y, w);
+        st.pa += BK2;
+        st.pb += BK2;
+      }
+    };
+    if constexpr (NK2) {
+      pair(std::true_type(), std::false_type(), std::true_type());
+    } else {
+      pair(std::true_type(), std::true_type(), std::false_type());
+      for (int t = 2; t < nk - 2; t += 2) pair(std::false_type(), std::true_type(), std::false_type());
+      pair(std::false_type(), std::false_type(), std::true_type());
+    }
+    // the epilogue's accumulator reads follow the last MFMAs: 20 wait states + a fence against hoisting
+    asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 3" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+    tn5_store(acc, ea.C, ea.ldc, m0 + wm * 128, n0 + wn * 128, lane);
+    __builtin_amdgcn_sched_barrier(0);
+    if (!has_next) break;
+    // the next tile's K1 -> Y (Y's last reads were retired before the last barrier)
+    st.pa += BK2;
+    st.pb += BK2;
+#pragma unroll
+    for (int j = 0; j < 16; ++j) st.piece(Y, w, j);
+    st.pa += BK2;
+    st.pb += BK2;
+    __builtin_amdgcn_s_waitcnt(waitcnt_imm(48, 15));  // its K0 landed (the stores and its K1 may fly)
+    tile = next;
+    m0 = m1;
+    n0 = n1;
+  }
+  __builtin_amdgcn_s_waitcnt(waitcnt_imm(0, 15));
+}
+
+template <int EPI>
+void launch5(const at::Tensor& a, const at::Tensor& w, int N, const EpiArgs& ea) {
+  const int M = a.size(0), K = a.size(1);
+  SFT_CHECK(M % 256 == 0 && N % 256 == 0 && K % 128 == 0, "gemm_tn persistent: M, N % 256, K % 128");
+  SFT_CHECK(ea.ldc % 8 == 0 && ((uintptr_t)ea.C) % 16 == 0, "gemm_tn persistent: 16-byte aligned output rows");
+  const int nbm = M / 256, nbn = N / 256, tiles = nbm * nbn;
+  const int grid = std::min(tiles, num_cus());
+  const int grp = std::min(group_m(), nbm);
+  if (K == 128)
+    tn5_kernel<EPI, true><<<grid, 256, 0, cur_stream()>>>((const u16*)a.data_ptr(), (const u16*)w.data_ptr(), K,
+                                                          a.stride(0), w.stride(0), nbm, nbn, grp, ea);
+  else
+    tn5_kernel<EPI, false><<<grid, 256, 0, cur_stream()>>>((const u16*)a.data_ptr(), (const u16*)w.data_ptr(), K,
+                                                           a.stride(0), w.stride(0), nbm, nbn, grp, ea);
+  SFT_LAUNCH_CHECK();
+}
+
 template <int EPI, bool TRC, int D = 1>
 void launch3(const at::Tensor& a, const at::Tensor& w, int N, const EpiArgs& ea) {
   const int M = a.size(0), K = a.size(1);
@@ -982,6 +1392,7 @@ static void check_tn(const at::Tensor& a, const at::Tensor& w) {
 // 256x128 tiles with 3 / 2 LDS stages (twice the workgroups: 3 full waves on qkv's 384-tile grid)
 at::Tensor gemm_tn(const at::Tensor& a, const at::Tensor& w, int64_t cfg) {
   check_tn(a, w);
+  SFT_TRACE(trace_name("tn.c", cfg));
   const int M = a.size(0), N = w.size(0);
   auto c = at::empty({M, N}, a.options());
   tn::EpiArgs ea{(u16*)c.data_ptr(), nullptr, nullptr, nullptr, (long)N, 0, 0};
@@ -1005,6 +1416,35 @@ at::Tensor gemm_tn(const at::Tensor& a, const at::Tensor& w, int64_t cfg) {
     else if (cfg == 9) tn::launch3<tn::EPI_PLAIN, true, 1>(a, w, N, ea);
     else if (cfg == 10) tn::launch3<tn::EPI_PLAIN, false, 2>(a, w, N, ea);
     else tn::launch3<tn::EPI_PLAIN, true, 2>(a, w, N, ea);
+  } else if (cfg == 12) {  // 4 waves of 128 x 128 (one wave per SIMD, accumulators pinned in AGPRs), VAR 4
+    tn::launch4<tn::EPI_PLAIN, 0, 4>(a, w, N, ea);
+  } else if (cfg == 50) {  // persistent 4-wave (register epilogue, next tile's loads under this tile's end)
+    tn::launch5<tn::EPI_PLAIN>(a, w, N, ea);
+  } else if (cfg >= 13 && cfg <= 44) {  // cfg 12 schedule variants (tn4_kernel VAR = cfg - 12)
+    switch (cfg - 12) {
+      case 1: tn::launch4<tn::EPI_PLAIN, 0, 1>(a, w, N, ea); break;
+      case 4: tn::launch4<tn::EPI_PLAIN, 0, 4>(a, w, N, ea); break;
+      case 32: tn::launch4<tn::EPI_PLAIN, 0, 0>(a, w, N, ea); break;  // cfg 44: the first (VAR 0) schedule
+      case 8: tn::launch4<tn::EPI_PLAIN, 0, 8>(a, w, N, ea); break;
+      case 9: tn::launch4<tn::EPI_PLAIN, 0, 9>(a, w, N, ea); break;
+      case 12: tn::launch4<tn::EPI_PLAIN, 0, 12>(a, w, N, ea); break;
+      case 13: tn::launch4<tn::EPI_PLAIN, 0, 13>(a, w, N, ea); break;
+      case 16: tn::launch4<tn::EPI_PLAIN, 0, 16>(a, w, N, ea); break;
+      default: SFT_CHECK(false, "gemm_tn: 4-wave variant cfg ", cfg, " not built");
+    }
+  } else if (cfg >= 1201 && cfg <= 1231) {  // timing-only ablations of cfg 12 (wrong results)
+    switch (cfg - 1200) {
+      case 8: tn::launch4<tn::EPI_PLAIN, 8, 4>(a, w, N, ea); break;
+      case 16: tn::launch4<tn::EPI_PLAIN, 16, 4>(a, w, N, ea); break;
+      case 24: tn::launch4<tn::EPI_PLAIN, 24, 4>(a, w, N, ea); break;
+      case 1: tn::launch4<tn::EPI_PLAIN, 1>(a, w, N, ea); break;
+      case 2: tn::launch4<tn::EPI_PLAIN, 2>(a, w, N, ea); break;
+      case 3: tn::launch4<tn::EPI_PLAIN, 3>(a, w, N, ea); break;
+      case 4: tn::launch4<tn::EPI_PLAIN, 4>(a, w, N, ea); break;
+      case 5: tn::launch4<tn::EPI_PLAIN, 5>(a, w, N, ea); break;
+      case 6: tn::launch4<tn::EPI_PLAIN, 6>(a, w, N, ea); break;
+      default: tn::launch4<tn::EPI_PLAIN, 7>(a, w, N, ea); break;
+    }
   } else if (cfg == 4) {  // BK64 with sched_group_barrier interleave pinned (measured slower: diagnostics)
     SFT_CHECK(N % 256 == 0 && a.size(1) % 64 == 0, "gemm_tn BK64: N % 256, K % 64");
     tn::launch2<256, 256, 2, 4, 2, tn::EPI_PLAIN, 2>(a, w, N, ea);
@@ -1018,6 +1458,7 @@ at::Tensor gemm_tn(const at::Tensor& a, const at::Tensor& w, int64_t cfg) {
 // x [M, K], w_gu [2I, K] = [gate; up]  ->  (gu [M, 2I], act [M, I] = silu(gate) * up)
 std::tuple<at::Tensor, at::Tensor> gemm_tn_swiglu(const at::Tensor& x, const at::Tensor& w_gu, int64_t cfg) {
   check_tn(x, w_gu);
+  SFT_TRACE(trace_name("tn.swiglu.c", cfg));
   const int M = x.size(0), N = w_gu.size(0), I = N / 2;
   SFT_CHECK(N % 2 == 0 && I % 128 == 0, "gemm_tn_swiglu: intermediate size % 128");
   auto gu = at::empty({M, N}, x.options());
@@ -1027,7 +1468,8 @@ std::tuple<at::Tensor, at::Tensor> gemm_tn_swiglu(const at::Tensor& x, const at:
     const char* e = std::getenv("SFTAMD_TN_TRC");
     return !(e && e[0] == '0');
   }();
-  if (x.size(1) % 64 == 0 && N % 256 == 0 && cfg == 11) tn::launch3<tn::EPI_SWIGLU, true, 2>(x, w_gu, N, ea);
+  if (cfg == 12) tn::launch4<tn::EPI_SWIGLU, 0, 4>(x, w_gu, N, ea);
+  else if (x.size(1) % 64 == 0 && N % 256 == 0 && cfg == 11) tn::launch3<tn::EPI_SWIGLU, true, 2>(x, w_gu, N, ea);
   else if (x.size(1) % 64 == 0 && trc) tn::launch2<256, 256, 2, 4, 2, tn::EPI_SWIGLU, 3>(x, w_gu, N, ea);
   else if (x.size(1) % 64 == 0) tn::launch2<256, 256, 2, 4, 2, tn::EPI_SWIGLU>(x, w_gu, N, ea);
   else tn::launch<256, 256, 2, 4, 5, tn::EPI_SWIGLU>(x, w_gu, N, ea);
@@ -1039,6 +1481,7 @@ std::tuple<at::Tensor, at::Tensor> gemm_tn_swiglu(const at::Tensor& x, const at:
 at::Tensor gemm_tn_rope(const at::Tensor& x, const at::Tensor& w, const at::Tensor& cosb, const at::Tensor& sinb,
                         int64_t rope_cols, int64_t cfg) {
   check_tn(x, w);
+  SFT_TRACE(trace_name("tn.rope.c", cfg));
   const int M = x.size(0), N = w.size(0);
   SFT_CHECK(N % 256 == 0 && rope_cols % 128 == 0, "gemm_tn_rope: N % 256, head_dim 128");
   SFT_CHECK(cosb.scalar_type() == at::kFloat && sinb.scalar_type() == at::kFloat && cosb.is_contiguous() &&
@@ -1047,7 +1490,8 @@ at::Tensor gemm_tn_rope(const at::Tensor& x, const at::Tensor& w, const at::Tens
   auto c = at::empty({M, N}, x.options());
   tn::EpiArgs ea{(u16*)c.data_ptr(), nullptr, cosb.data_ptr<float>(), sinb.data_ptr<float>(), (long)N, 0,
                  (int)rope_cols};
-  if (cfg == 1) tn::launch<256, 128, 4, 2, 6, tn::EPI_ROPE>(x, w, N, ea);
+  if (cfg == 12) tn::launch4<tn::EPI_ROPE, 0, 4>(x, w, N, ea);
+  else if (cfg == 1) tn::launch<256, 128, 4, 2, 6, tn::EPI_ROPE>(x, w, N, ea);
   else if (cfg == 2 && x.size(1) % 64 == 0) tn::launch2<256, 256, 2, 4, 2, tn::EPI_ROPE>(x, w, N, ea);
   else if (cfg == 5 && x.size(1) % 64 == 0) tn::launch2<256, 256, 2, 4, 2, tn::EPI_ROPE, 3>(x, w, N, ea);
   else if (cfg == 6 && x.size(1) % 64 == 0) tn::launch2<256, 128, 4, 2, 3, tn::EPI_ROPE>(x, w, N, ea);
@@ -1070,6 +1514,7 @@ at::Tensor gemm_tn_rope(const at::Tensor& x, const at::Tensor& w, const at::Tens
       tn::launch3<tn::EPI_ROPE, true, 2>(x, w, N, ea);
     } else {
       const int ncut = main_n * 256;
+      SFT_TRACE("tn.rope.tail");
       tn::launch3<tn::EPI_ROPE, true, 2>(x, w.narrow(0, 0, ncut), ncut, ea);
       tn::EpiArgs et = ea;
       et.C = ea.C + ncut;

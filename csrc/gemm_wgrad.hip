@@ -668,6 +668,8 @@ void wgrad_gemm(at::Tensor out, at::Tensor dy, at::Tensor x, bool accumulate, in
   SFT_CHECK(T % 32 == 0 && T > 0, "wgrad_gemm: T must be a positive multiple of 32");
   SFT_CHECK(cfg >= 7 || cfg == 0 || T % wgrad::BK == 0, "wgrad_gemm: cfg 1-6 need T % 64 == 0");
   if (cfg == 0) cfg = (N % 256 == 0 && K % 256 == 0 && (N / 256) * (K / 256) >= 512) ? 1 : 2;
+  SFT_TRACE(trace_name("wgrad.c", cfg));
+  if (norm.has_value() && norm->defined()) SFT_TRACE("wgrad.norm_slots");
   // cfg = 1000 * H + 100 * S + c: ring variant c (9 / 10) with tiles split S ways over the token (reduction)
   // axis — all tiles (H = 0: fills the chip for small outputs, o_proj 2048 x 2048 = 64 tiles of 256 x 256) or
   // only those past the last full wave of 256 workgroups (H = 1, hybrid data-parallel + split-K: the partial

@@ -10,7 +10,11 @@
 //   4. x = sum over p = 0..N-1 of rank p's chunk, in rank order (every rank computes the identical sum);
 //   5. raise / wait a second flag set ("done reading") so the next call cannot overwrite a chunk a peer still reads.
 // Waits are bounded (s_memrealtime, 100 MHz): a peer that never arrives sets the region's error word instead of
-// hanging the device; ipc_ar_check() reports it. Flags and data use vector memory operations only.
+// hanging the device AND poisons this call's output with NaN (a silently wrong sum — e.g. a clip norm that differs
+// across ranks — is the failure to avoid); ipc_ar_check() (synchronising) or ipc_ar_poll() (a pinned copy of the
+// error word behind each call, read without waiting) report it. Flags and data use vector memory operations only.
+// The region is allocated uncached (hipDeviceMallocUncached) so peers polling it over xGMI never hit a stale cached
+// line; hipMalloc memory is the fallback when the driver refuses an IPC handle for it.
 #include "common.h"
 
 #include <cstring>
@@ -33,6 +37,9 @@ struct Ctx {
   long cap = 0;               // data bytes
   int world = 0, rank = 0;
   int* err = nullptr;         // device error word
+  int* err_host = nullptr;    // pinned copy of it, refreshed behind every call (ipc_ar_poll)
+  hipEvent_t ev = nullptr;    // recorded after that copy
+  bool uncached = false;
   std::vector<void*> opened;  // peer mappings to close
   Peers peers{};
   bool ready = false;
@@ -111,7 +118,10 @@ __global__ __launch_bounds__(NT) void allreduce_kernel(uint4* __restrict__ x, lo
   uint4* mine = (uint4*)local;
   for (long i = v0 + threadIdx.x; i < v1; i += NT) mine[i] = x[i];
   raise_flags(peers, cap, 0, world, rank, blk, round);
-  if (!wait_flags(local, cap, 0, world, blk, round, err)) return;
+  if (!wait_flags(local, cap, 0, world, blk, round, err)) {
+    for (long i = v0 + threadIdx.x; i < v1; i += NT) x[i] = make_uint4(0xffffffffu, 0xffffffffu, 0xffffffffu, 0xffffffffu);
+    return;  // NaN output (bf16 and fp32 all-ones = NaN): the caller cannot use a partial sum by accident
+  }
   for (long i = v0 + threadIdx.x; i < v1; i += NT) {
     float acc[E];
 #pragma unroll
@@ -137,10 +147,26 @@ int64_t ipc_ar_create(int64_t cap, int64_t world, int64_t rank) {
   c.world = (int)world;
   c.rank = (int)rank;
   const long bytes = cap + 2L * ipcar::MAXW * ipcar::MAXB * 4;
-  C10_HIP_CHECK(hipMalloc((void**)&c.local, bytes));
+  if (hipExtMallocWithFlags((void**)&c.local, bytes, hipDeviceMallocUncached) == hipSuccess) {
+    hipIpcMemHandle_t h;
+    if (hipIpcGetMemHandle(&h, c.local) == hipSuccess) {
+      c.uncached = true;
+    } else {
+      (void)hipGetLastError();
+      C10_HIP_CHECK(hipFree(c.local));
+      c.local = nullptr;
+    }
+  } else {
+    (void)hipGetLastError();
+    c.local = nullptr;
+  }
+  if (c.local == nullptr) C10_HIP_CHECK(hipMalloc((void**)&c.local, bytes));
   C10_HIP_CHECK(hipMemset(c.local, 0, bytes));
   C10_HIP_CHECK(hipMalloc((void**)&c.err, sizeof(int)));
   C10_HIP_CHECK(hipMemset(c.err, 0, sizeof(int)));
+  C10_HIP_CHECK(hipHostMalloc((void**)&c.err_host, sizeof(int), hipHostMallocDefault));
+  *c.err_host = 0;
+  C10_HIP_CHECK(hipEventCreateWithFlags(&c.ev, hipEventDisableTiming));
   C10_HIP_CHECK(hipDeviceSynchronize());
   contexts().push_back(c);
   return (int64_t)contexts().size() - 1;
@@ -202,7 +228,25 @@ void ipc_ar_allreduce(at::Tensor x, int64_t id, int64_t round, int64_t blocks) {
     ipcar::allreduce_kernel<float><<<nb, ipcar::NT, 0, cur_stream()>>>((uint4*)x.data_ptr(), nvec, c.peers, c.cap,
                                                                        c.world, c.rank, r, c.err);
   SFT_LAUNCH_CHECK();
+  C10_HIP_CHECK(hipMemcpyAsync(c.err_host, c.err, sizeof(int), hipMemcpyDeviceToHost, cur_stream()));
+  C10_HIP_CHECK(hipEventRecord(c.ev, cur_stream()));
 }
+
+// the error word as of the last completed call, without waiting: -1 = that call has not finished yet, 0 = ok,
+// 1 = a bounded wait timed out (its output was poisoned with NaN)
+int64_t ipc_ar_poll(int64_t id) {
+  Ctx& c = ctx_at(id);
+  const hipError_t q = hipEventQuery(c.ev);
+  if (q == hipErrorNotReady) {
+    (void)hipGetLastError();
+    return -1;
+  }
+  C10_HIP_CHECK(q);
+  return *c.err_host;
+}
+
+// 1 if the region is uncached device memory (the fallback is plain hipMalloc)
+int64_t ipc_ar_uncached(int64_t id) { return ctx_at(id).uncached ? 1 : 0; }
 
 // device error word (1 = a wait timed out); synchronises the device
 int64_t ipc_ar_check(int64_t id) {
@@ -219,6 +263,8 @@ void ipc_ar_destroy(int64_t id) {
   for (void* p : c.opened) C10_HIP_CHECK(hipIpcCloseMemHandle(p));
   C10_HIP_CHECK(hipFree(c.local));
   C10_HIP_CHECK(hipFree(c.err));
+  C10_HIP_CHECK(hipHostFree(c.err_host));
+  C10_HIP_CHECK(hipEventDestroy(c.ev));
   c = Ctx{};
 }
 

@@ -12,6 +12,12 @@ terminated (SIGTERM, then SIGKILL after ``--grace``) instead of blocking in a co
 the watchdog timeout (the reference's "workers hang until NCCL timeout"). With
 ``--max-restarts K`` the whole group is restarted (``SFTAMD_RESTART_COUNT`` is exported) and the
 training script resumes from its latest checkpoint (``--resume auto``).
+
+Hang detection: every rank writes a one-line heartbeat (step, phase, last gradient bucket launched) into
+``$SFTAMD_HEARTBEAT_DIR/rank<r>.hb`` (utils/heartbeat.py). With ``--hang-timeout S`` a rank whose heartbeat has
+not changed for S seconds (or that wrote none within ``--startup-timeout``) is declared hung; ``--deadline S``
+bounds the whole run. Either way — and on any failing rank — the launcher prints the last heartbeat of EVERY rank
+before tearing the group down, and exits with 124 for a hang / deadline.
 """
 from __future__ import annotations
 
@@ -21,6 +27,7 @@ import signal
 import socket
 import subprocess
 import sys
+import tempfile
 import time
 from typing import List
 
@@ -44,13 +51,14 @@ def _die_with_parent():
 
 
 def _spawn(n: int, cmd: List[str], addr: str, port: int, restart: int, node_rank: int, nnodes: int,
-           new_session: bool = True) -> List[subprocess.Popen]:
+           new_session: bool = True, hb_dir: str = "") -> List[subprocess.Popen]:
     procs = []
     for lr in range(n):
         env = dict(os.environ)
         env.update(WORLD_SIZE=str(n * nnodes), RANK=str(node_rank * n + lr), LOCAL_RANK=str(lr),
                    LOCAL_WORLD_SIZE=str(n), GROUP_RANK=str(node_rank), MASTER_ADDR=addr, MASTER_PORT=str(port),
-                   SFTAMD_RESTART_COUNT=str(restart), HSA_ENABLE_IPC_MODE_LEGACY="0", SFTAMD_LAUNCHER="sftamd")
+                   SFTAMD_RESTART_COUNT=str(restart), HSA_ENABLE_IPC_MODE_LEGACY="0", SFTAMD_LAUNCHER="sftamd",
+                   SFTAMD_HEARTBEAT_DIR=hb_dir)
         env.setdefault("OMP_NUM_THREADS", "1")
         procs.append(subprocess.Popen(cmd, env=env, start_new_session=new_session, preexec_fn=_die_with_parent))
     return procs
@@ -80,6 +88,45 @@ def _terminate(procs: List[subprocess.Popen], grace: float, group: bool = True):
         p.wait()
 
 
+def _heartbeats(hb_dir: str, n: int, node_rank: int):
+    """Last heartbeat line of each local rank (read without importing the package: no torch in the launcher)."""
+    out = []
+    now = time.time()
+    for lr in range(n):
+        r = node_rank * n + lr
+        p = os.path.join(hb_dir, f"rank{r}.hb")
+        try:
+            with open(p) as f:
+                out.append((lr, f.read().strip(), now - os.path.getmtime(p)))
+        except OSError:
+            out.append((lr, None, None))
+    return out
+
+
+def _print_heartbeats(hb_dir: str, n: int, node_rank: int):
+    for lr, line, age in _heartbeats(hb_dir, n, node_rank):
+        if line is None:
+            print(f"[launch] local rank {lr}: no heartbeat", file=sys.stderr, flush=True)
+        else:
+            print(f"[launch] local rank {lr} last heartbeat ({age:.1f} s ago): {line}", file=sys.stderr, flush=True)
+
+
+def _hung(hb_dir: str, n: int, node_rank: int, procs, started: float, hang_timeout: float, startup: float):
+    """(local rank, reason) of the first live rank whose heartbeat is stale, else None."""
+    if hang_timeout <= 0:
+        return None
+    now = time.time()
+    for (lr, line, age), p in zip(_heartbeats(hb_dir, n, node_rank), procs):
+        if p.poll() is not None:
+            continue
+        if line is None:
+            if now - started > startup:
+                return lr, f"no heartbeat within {startup:.0f} s of the start"
+        elif age > hang_timeout:
+            return lr, f"heartbeat unchanged for {age:.0f} s (hang timeout {hang_timeout:.0f} s)"
+    return None
+
+
 def run(argv=None) -> int:
     ap = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
     ap.add_argument("--nproc-per-node", "--nproc_per_node", type=int, default=1)
@@ -90,6 +137,12 @@ def run(argv=None) -> int:
     ap.add_argument("--max-restarts", type=int, default=0)
     ap.add_argument("--grace", type=float, default=10.0)
     ap.add_argument("--monitor-interval", type=float, default=0.5)
+    ap.add_argument("--hang-timeout", type=float, default=float(os.environ.get("SFTAMD_HANG_TIMEOUT_S", "0") or 0),
+                    help="seconds without a heartbeat change after which a rank counts as hung (0 = off)")
+    ap.add_argument("--startup-timeout", type=float, default=900.0,
+                    help="seconds a rank may take to write its first heartbeat (first import of torch, model build)")
+    ap.add_argument("--deadline", type=float, default=0.0, help="wall-clock limit of the whole run in seconds (0 = none)")
+    ap.add_argument("--heartbeat-dir", default=os.environ.get("SFTAMD_HEARTBEAT_DIR", ""))
     ap.add_argument("--same-session", action="store_true",
                     help="keep the ranks in the launcher's process group (a signal to the group reaches them)")
     ap.add_argument("-m", dest="module", default=None, help="run a module (like python -m)")
@@ -103,10 +156,19 @@ def run(argv=None) -> int:
     else:
         ap.error("need a script or -m module")
     restart = 0
+    hb_dir = a.heartbeat_dir or tempfile.mkdtemp(prefix="sftamd_hb_")
+    t_run = time.time()
     while True:
         port = a.master_port or _free_port(a.master_addr)
+        for f in os.listdir(hb_dir):  # a restarted group starts with no heartbeats
+            if f.endswith(".hb"):
+                try:
+                    os.remove(os.path.join(hb_dir, f))
+                except OSError:
+                    pass
+        started = time.time()
         procs = _spawn(a.nproc_per_node, cmd, a.master_addr, port, restart, a.node_rank, a.nnodes,
-                       new_session=not a.same_session)
+                       new_session=not a.same_session, hb_dir=hb_dir)
         grp = not a.same_session
         failed = None
         try:
@@ -118,13 +180,27 @@ def run(argv=None) -> int:
                     break
                 if all(c == 0 for c in codes):
                     return 0
+                if a.deadline > 0 and time.time() - t_run > a.deadline:
+                    failed = (-1, 124, f"deadline of {a.deadline:.0f} s exceeded")
+                    break
+                h = _hung(hb_dir, a.nproc_per_node, a.node_rank, procs, started, a.hang_timeout,
+                          max(a.startup_timeout, a.hang_timeout))
+                if h is not None:
+                    failed = (h[0], 124, h[1])
+                    break
                 time.sleep(a.monitor_interval)
         except KeyboardInterrupt:
             _terminate(procs, a.grace, grp)
             return 130
-        rank, code = failed
-        print(f"[launch] local rank {rank} exited with code {code}; terminating the other ranks", file=sys.stderr,
-              flush=True)
+        if len(failed) == 3:
+            rank, code, why = failed
+            who = "the run" if rank < 0 else f"local rank {rank}"
+            print(f"[launch] hang: {who}: {why}; terminating all ranks", file=sys.stderr, flush=True)
+        else:
+            rank, code = failed
+            print(f"[launch] local rank {rank} exited with code {code}; terminating the other ranks", file=sys.stderr,
+                  flush=True)
+        _print_heartbeats(hb_dir, a.nproc_per_node, a.node_rank)
         _terminate(procs, a.grace, grp)
         if restart >= a.max_restarts:
             return code if code > 0 else 1

@@ -305,19 +305,27 @@ class EmbeddingFn(Function):
         dy2d = dy.reshape(-1, dy.shape[-1]).contiguous()
         sink = getattr(w, "_sftamd_sparse_sink", None)
         if sink is not None:
-            # sparse tied-embedding gradient (DDPEngine.tied_sparse): (unique ids, summed rows) go to the engine,
-            # which all-gathers them after backward; main_grad holds only the (early all-reduced) lm_head part
-            uniq, inv = torch.unique(flat_ids, sorted=True, return_inverse=True)
+            # sparse tied-embedding gradient (DDPEngine.tied_sparse): (ids, summed rows) go to the engine, which
+            # all-gathers them after backward; main_grad holds only the (early all-reduced) lm_head part. No host
+            # sync: instead of torch.unique (whose output size is data-dependent) the n token rows are reduced into n
+            # slots — slot s = the s-th distinct id of the sorted ids, the unused tail slots keep id 0 and a zero row
+            # (an exact no-op when added)
+            n = flat_ids.numel()
+            sorted_ids, perm = torch.sort(flat_ids)
+            head = torch.ones(n, dtype=torch.bool, device=flat_ids.device)
+            if n > 1:
+                head[1:] = sorted_ids[1:] != sorted_ids[:-1]
+            seg = torch.cumsum(head, 0) - 1
+            ids = torch.zeros(n, dtype=torch.int64, device=flat_ids.device).scatter_(0, seg, sorted_ids)
+            rdt = mg.dtype if mg is not None else w.dtype
             if _ext.use_hip(dy):
-                rows = torch.zeros(uniq.numel(), w.shape[-1], dtype=mg.dtype if mg is not None else w.dtype,
-                                   device=w.device)
-                sorted_inv, perm = torch.sort(inv.to(torch.int32))
-                _ext.ops().embedding_bwd(dy2d, sorted_inv, perm.to(torch.int32), rows)
+                rows = torch.zeros(n, w.shape[-1], dtype=rdt, device=w.device)
+                _ext.ops().embedding_bwd(dy2d, seg.to(torch.int32), perm.to(torch.int32), rows)
             else:
-                rows = torch.zeros(uniq.numel(), w.shape[-1], dtype=torch.float32, device=w.device)
-                rows.index_add_(0, inv, dy2d.float())
-                rows = rows.to(mg.dtype if mg is not None else w.dtype)
-            sink(uniq, rows)
+                rows = torch.zeros(n, w.shape[-1], dtype=torch.float32, device=w.device)
+                rows.index_add_(0, seg[torch.argsort(perm)], dy2d.float())
+                rows = rows.to(rdt)
+            sink(ids, rows)
             return None, None
         if _ext.use_hip(dy):
             sorted_ids, perm = torch.sort(flat_ids.to(torch.int32))

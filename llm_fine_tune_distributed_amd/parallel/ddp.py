@@ -332,6 +332,7 @@ class DDPEngine:
                 p.main_grad = self.grad_flat[o:o + n].view(p.shape)
                 p.grad = None
         self._comm_events = []
+        self.last_launched = -1  # index of the last bucket whose collective was issued (heartbeat / hang triage)
         # gradient-norm partials computed during backward (SFTAMD_NORM_IN_BWD=1): one sum of squares per
         # bucket (its reduced / owned slice), on a side stream as soon as the bucket is complete, instead of
         # a serial pass over every gradient after backward. Measured on MI355X (bench.py, interleaved): 96.0
@@ -340,6 +341,7 @@ class DDPEngine:
         self.track_norm = bool(track_norm)
         self._sparse = None
         self.sparse_exchanges = 0  # synchronising passes whose tied-embedding rows went through the sparse path
+        self.sparse_cap = 0  # host-known upper bound of one pass's token count (trainer); 0 = measure per step
         self.norm_partials = torch.zeros(len(self.buckets), dtype=torch.float32, device=dev)
         # World size 1 on GPU (SFTAMD_NORM_FUSED, default on): the weight-gradient GEMMs of the synchronising pass
         # write the sum of squares of the gradient they store into per-(tile, wave) slots (csrc/gemm_wgrad.hip), so
@@ -433,6 +435,7 @@ class DDPEngine:
             b.ready = False
             b.launched = False
             b.work = None
+        self.last_launched = -1
         self._tracker.reset()
 
     # ------------------------------------------------------------------ hooks
@@ -495,6 +498,7 @@ class DDPEngine:
         if self.track_norm:
             self._bucket_norm(b, ws)
         b.launched = True
+        self.last_launched = b.index
 
     def _bucket_norm(self, b: Bucket, ws=None):
         """Sum of squares of bucket ``b``'s reduced gradient (its owned slice under ZeRO-1) into
@@ -562,6 +566,7 @@ class DDPEngine:
             return t
         ar = self._small_ar()
         if ar is not None and t.dtype == torch.float32 and t.is_contiguous() and t.numel() <= 1024:
+            ar.raise_if_failed()  # the previous call's bounded waits (non-blocking read of its error word)
             n = t.numel()
             buf = torch.zeros((n + 3) // 4 * 4, dtype=torch.float32, device=t.device)
             buf[:n].copy_(t.reshape(-1))
@@ -588,7 +593,12 @@ class DDPEngine:
 
     def _exchange_sparse(self):
         """All ranks' sparse embedding rows into the (already all-reduced) tied gradient, in rank order: every
-        rank computes the same sum (each rank's ids are unique, so every row gets one add per rank)."""
+        rank computes the same sum (each rank's ids are unique, so every row gets one add per rank; padding slots
+        carry id 0 and a zero row, an exact no-op).
+
+        The gather size is the host-known ``sparse_cap`` (the most tokens one synchronising pass can hold, set by
+        the trainer from its batch geometry — identical on every rank), so nothing here waits for the device; only
+        when no cap is known does it fall back to a MAX all-reduce of the counts plus a host read."""
         p = self.tied_param
         mg = p.main_grad
         H = mg.shape[-1]
@@ -599,17 +609,25 @@ class DDPEngine:
             ids, rows = self._sparse
             self.sparse_exchanges += 1
         self._sparse = None
-        n = torch.tensor([ids.numel()], dtype=torch.int64, device=mg.device)
-        dist.all_reduce(n, op=dist.ReduceOp.MAX, group=self.pg)
-        cap = max(1, int(n.item()))
-        idp = torch.zeros(cap, dtype=torch.int64, device=mg.device)  # padding -> row 0, with zero rows (exact no-op)
-        rwp = torch.zeros(cap, H, dtype=mg.dtype, device=mg.device)
-        idp[:ids.numel()] = ids
-        rwp[:ids.numel()] = rows
+        cap = int(self.sparse_cap or 0)
+        if cap <= 0 or ids.numel() > cap:
+            if cap > 0:
+                raise RuntimeError(f"sparse tied-embedding exchange: {ids.numel()} rows exceed the host cap {cap} "
+                                   "(every rank must use the same cap; raise DDPEngine.sparse_cap)")
+            n = torch.tensor([ids.numel()], dtype=torch.int64, device=mg.device)
+            dist.all_reduce(n, op=dist.ReduceOp.MAX, group=self.pg)
+            cap = max(1, int(n.item()))
+        if ids.numel() == cap:
+            idp, rwp = ids, rows
+        else:
+            idp = torch.zeros(cap, dtype=torch.int64, device=mg.device)  # padding -> row 0, with zero rows
+            rwp = torch.zeros(cap, H, dtype=mg.dtype, device=mg.device)
+            idp[:ids.numel()] = ids
+            rwp[:ids.numel()] = rows
         gid = torch.empty(self.world_size * cap, dtype=torch.int64, device=mg.device)
         grw = torch.empty(self.world_size * cap, H, dtype=mg.dtype, device=mg.device)
-        dist.all_gather_into_tensor(gid, idp, group=self.pg)
-        dist.all_gather_into_tensor(grw, rwp, group=self.pg)
+        dist.all_gather_into_tensor(gid, idp.contiguous(), group=self.pg)
+        dist.all_gather_into_tensor(grw, rwp.contiguous(), group=self.pg)
         for r in range(self.world_size):
             mg.index_add_(0, gid[r * cap:(r + 1) * cap], grw[r * cap:(r + 1) * cap])
 

@@ -10,8 +10,11 @@ existing process group, and every call is one kernel on the caller's stream:
     assert ar.check() == 0                         # 1 = a bounded wait timed out (a peer never arrived)
 
 Every rank sums the ranks' chunks in rank order, so the result is bitwise identical on all ranks. Waits are bounded
-(2 s) so a missing peer reports an error instead of hanging the device. Opt-in (`SFTAMD_IPC_ALLREDUCE=1` routes the
-trainer's scalar all-reduces through it); not measured on a multi-GPU node yet.
+(2 s) so a missing peer reports an error instead of hanging the device; the timed-out call's output is poisoned with
+NaN, and ``raise_if_failed()`` (non-blocking: it reads a pinned copy of the error word written behind each call)
+raises on the next use. Opt-in (`SFTAMD_IPC_ALLREDUCE=1` routes the trainer's scalar all-reduces through it) and
+UNVALIDATED across GPUs: the only test runs two ranks on one GPU (shared L2); the region is allocated uncached so that
+cross-GPU polling cannot read stale lines, but no multi-GPU run has exercised it yet.
 """
 from __future__ import annotations
 
@@ -58,6 +61,19 @@ class IPCAllReduce:
     def check(self) -> int:
         """Synchronises the device; 0 = every wait completed, 1 = a wait timed out."""
         return int(_ext.ops().ipc_ar_check(self.ctx))
+
+    def poll(self) -> int:
+        """Error word of the last finished call without waiting: -1 still running, 0 ok, 1 a wait timed out."""
+        return int(_ext.ops().ipc_ar_poll(self.ctx))
+
+    def raise_if_failed(self):
+        if self.poll() > 0:
+            raise RuntimeError("IPCAllReduce: a peer did not arrive within the bounded wait (output poisoned with NaN); "
+                               "unset SFTAMD_IPC_ALLREDUCE to use the process group's all-reduce")
+
+    @property
+    def uncached(self) -> bool:
+        return bool(_ext.ops().ipc_ar_uncached(self.ctx))
 
     def close(self):
         if self.ctx is not None:

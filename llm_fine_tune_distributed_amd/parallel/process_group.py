@@ -68,6 +68,9 @@ def setup_distributed(backend: Optional[str] = None, timeout_s: float = 1800.0, 
     if _STATE is not None:
         return _STATE
     ws, rank, local_rank = read_env()
+    # dmabuf IPC for RCCL / CUDA-tensor sharing between ranks: the HSA runtime reads this once, when it initialises,
+    # which torch.cuda.is_available() below triggers — so it must be in the environment before that call
+    os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
     use_gpu = (device != "cpu") and torch.cuda.is_available()
     if use_gpu:
         n = torch.cuda.device_count()
@@ -79,7 +82,6 @@ def setup_distributed(backend: Optional[str] = None, timeout_s: float = 1800.0, 
     if ws > 1 and not dist.is_initialized():
         # RCCL: keep peer-to-peer (xGMI) on; async error handling = watchdog aborts on hangs.
         os.environ.setdefault("TORCH_NCCL_ASYNC_ERROR_HANDLING", "1")
-        os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
         kw = dict(backend=be, init_method="env://", world_size=ws, rank=rank,
                   timeout=datetime.timedelta(seconds=timeout_s))
         if be == "nccl":
@@ -129,26 +131,28 @@ def all_reduce_sum_(t: torch.Tensor) -> torch.Tensor:
 
 class PendingCount:
     """A count whose all-reduce is in flight; ``resolve()`` makes the current stream wait for it (once)
-    and returns it clamped to >= 1."""
+    and returns it clamped to >= 1, times ``scale``."""
 
-    def __init__(self, t: torch.Tensor, work=None):
-        self._t, self._work, self._done = t, work, None
+    def __init__(self, t: torch.Tensor, work=None, scale: float = 1.0):
+        self._t, self._work, self._done, self._scale = t, work, None, scale
 
     def resolve(self) -> torch.Tensor:
         if self._done is None:
             if self._work is not None:
                 self._work.wait()
             self._done = self._t.clamp(min=1.0)
+            if self._scale != 1.0:
+                self._done = self._done * self._scale
         return self._done
 
 
-def all_reduce_sum_async(t: torch.Tensor) -> PendingCount:
-    """In-place SUM all-reduce of ``t`` issued without blocking the compute stream (world size 1:
-    nothing in flight)."""
+def all_reduce_sum_async(t: torch.Tensor, group=None, scale: float = 1.0) -> PendingCount:
+    """In-place SUM all-reduce of ``t`` (over ``group``, default the world) issued without blocking the compute
+    stream (a group of one: nothing in flight); the resolved count is multiplied by ``scale``."""
     work = None
-    if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
-        work = dist.all_reduce(t, op=dist.ReduceOp.SUM, async_op=True)
-    return PendingCount(t, work)
+    if dist.is_available() and dist.is_initialized() and dist.get_world_size(group) > 1:
+        work = dist.all_reduce(t, op=dist.ReduceOp.SUM, group=group, async_op=True)
+    return PendingCount(t, work, scale)
 
 
 def broadcast_object(obj, src: int = 0):

@@ -81,14 +81,15 @@ class SFTConfig:
     lora_alpha: float = 8.0
     lora_dropout: float = 0.05
     lora_target_modules: Optional[List[str]] = None
-    # Reference parity: the reference updates bf16 parameters directly (no master copy,
-    # training.py:99). We do the same but with fp32 Adam moments and stochastic rounding of the
-    # bf16 write-back (unbiased); master_weights=True keeps an fp32 master copy instead.
+    # Reference parity: the reference updates bf16 parameters directly (no master copy, training.py:99), and torch's
+    # AdamW keeps exp_avg / exp_avg_sq in the parameter dtype — bf16. The default here is the same state: bf16
+    # parameters and bf16 moments, every bf16 write-back stochastically rounded (unbiased, so not less precise than the
+    # reference's round-to-nearest), 14 HBM bytes per parameter and step. "auto" (default) = the parameter dtype, as
+    # in torch: bf16 moments for the bf16 model the trainer builds (what bench.py runs), fp32 for an fp32 model.
+    # "fp32" forces fp32 moments (22 bytes), master_weights=True adds an fp32 master copy.
     master_weights: bool = False
     stochastic_rounding: bool = True
-    # Adam moment storage: "fp32" (default) or "bf16" (torch AdamW's state dtype for the
-    # reference's bf16 params; stochastic-rounded, 14 instead of 22 HBM bytes/param per step)
-    optim_state_dtype: str = "fp32"
+    optim_state_dtype: str = "auto"
     # ZeRO-1 over the DDP buckets (world_size > 1): reduce-scatter gradients, update 1/world_size of the
     # parameters per rank, all-gather them back under the next forward (train/optim.py ShardedAdamW)
     shard_optimizer_state: bool = False

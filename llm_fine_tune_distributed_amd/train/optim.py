@@ -3,10 +3,11 @@
 The reference runs HF's default ``adamw_torch(_fused)`` over bf16 parameters with
 ``lr = LEARNING_RATE * WORLD_SIZE`` (training.py:263), betas (0.9, 0.999), eps 1e-8, wd 0, and
 ``lr_scheduler_type="linear"`` (decay to 0, no warmup). Here the update is ONE fused HIP kernel
-per weight-decay region over the DDP engine's flat buffers, with an fp32 master copy and fp32
-moments by default (``master_weights=False`` reproduces the reference's pure-bf16 parameter
-update with fp32 moments). Gradient clipping (max_grad_norm) is a flat sum-of-squares kernel;
-the clip coefficient never leaves the GPU.
+per weight-decay region over the DDP engine's flat buffers. Trainer default (SFTConfig): the reference's
+state — bf16 parameters updated in place and Adam moments in the parameter dtype (bf16), every bf16
+write-back stochastically rounded; fp32 moments and an fp32 master copy are options. Gradient clipping
+(max_grad_norm) is a sum of squares produced during backward (or a flat pass); the clip coefficient never
+leaves the GPU.
 """
 from __future__ import annotations
 
@@ -42,6 +43,17 @@ def _update_stream(device: torch.device):
     return st
 
 
+def _state_dtype(state_dtype, engine) -> torch.dtype:
+    """Adam moment dtype: "auto" = the parameter dtype (torch AdamW's state follows its parameters: bf16 for the
+    reference's bf16 model, training.py:99), "bf16" / "fp32", or a torch dtype."""
+    if isinstance(state_dtype, str):
+        if state_dtype == "auto":
+            return engine.dtype if engine.dtype in (torch.float32, torch.bfloat16) else torch.float32
+        state_dtype = {"fp32": torch.float32, "float32": torch.float32, "bf16": torch.bfloat16,
+                       "bfloat16": torch.bfloat16}[state_dtype]
+    return state_dtype
+
+
 class _StreamPoint:
     """Work-like handle for an update with no collective behind it: ``wait()`` makes the current
     stream wait for the side stream up to the point where the handle was created."""
@@ -56,10 +68,10 @@ class _StreamPoint:
 
 class FlatAdamW:
     def __init__(self, engine, lr: float, betas=(0.9, 0.999), eps: float = 1e-8, weight_decay: float = 0.0,
-                 master_weights: bool = True, stochastic_rounding: bool = True, state_dtype=torch.float32):
-        """``state_dtype`` = dtype of exp_avg / exp_avg_sq: fp32 (default) or bf16 — what torch's
-        AdamW keeps for the reference's bf16 parameters (training.py:99) — stored with stochastic
-        rounding (unbiased) when ``stochastic_rounding`` is on; 8 fewer HBM bytes per parameter."""
+                 master_weights: bool = True, stochastic_rounding: bool = True, state_dtype="auto"):
+        """``state_dtype`` = dtype of exp_avg / exp_avg_sq: "auto" (the parameter dtype, like torch), fp32 or bf16 —
+        what torch's AdamW keeps for the reference's bf16 parameters (training.py:99) — stored with stochastic
+        rounding (unbiased) when ``stochastic_rounding`` is on; 8 fewer HBM bytes per parameter than fp32."""
         self.engine = engine
         self.lr = lr
         self.betas = betas
@@ -70,9 +82,7 @@ class FlatAdamW:
         self.step_count = 0
         n = engine.numel
         dev = engine.device
-        if isinstance(state_dtype, str):
-            state_dtype = {"fp32": torch.float32, "float32": torch.float32, "bf16": torch.bfloat16,
-                           "bfloat16": torch.bfloat16}[state_dtype]
+        state_dtype = _state_dtype(state_dtype, engine)
         if state_dtype not in (torch.float32, torch.bfloat16):
             raise ValueError(f"optimizer state dtype must be fp32 or bf16, got {state_dtype}")
         self.state_dtype = state_dtype
@@ -205,25 +215,43 @@ class FlatAdamW:
         return norm
 
     # ------------------------------------------------------------------ checkpoints (per parameter)
-    def _full_state(self, key: str) -> Optional[torch.Tensor]:
-        """The whole-model flat tensor of ``key`` in this engine's layout (collective under ZeRO-1)."""
+    def _full_state(self, key: str, dst: Optional[int] = None) -> Optional[torch.Tensor]:
+        """The whole-model flat tensor of ``key`` in this engine's layout (collective under ZeRO-1; built only on
+        rank ``dst`` when given)."""
         return {"exp_avg": self.exp_avg, "exp_avg_sq": self.exp_avg_sq, "master": self.master}[key]
 
     def _state_ranges(self):
         """(global_start, global_end, local_offset) of the flat state this rank holds."""
         return [(0, self.engine.numel, 0)]
 
-    def state_dict(self) -> Dict:
+    def _collective_state(self) -> bool:
+        return False  # replicated state: every rank already holds all of it
+
+    def state_dict(self, dst: Optional[int] = 0) -> Dict:
         """Adam state keyed by PARAMETER NAME (``param_state[name] = {exp_avg, exp_avg_sq, master}`` with the
         parameter's shape), so a checkpoint resumes at any world size / bucket plan: the flat layout pads
-        buckets to multiples of world_size pages and is therefore world-size dependent. Every rank must
-        call this (ZeRO-1 gathers the sharded state); tensors are host copies."""
+        buckets to multiples of world_size pages and is therefore world-size dependent. Tensors are host copies.
+
+        ``dst`` (default 0): only that rank builds the state; every other rank returns ``{}`` without allocating a
+        full host (or device) copy — under ZeRO-1 they still join the collectives that bring their shards to
+        ``dst`` (every rank must call), replicated state needs no communication at all. ``dst=None``: every rank
+        builds the full state (the round-2 behaviour)."""
         self.synchronize()
         e = self.engine
+        self.last_state_dict_host_bytes = 0
+        mine = dst is None or e.rank == dst
+        if not mine and not self._collective_state():
+            return {}
         full = {}
         for k in ("exp_avg", "exp_avg_sq", "master"):
-            t = self._full_state(k)
+            t = self._full_state(k, dst)
+            if not mine:
+                continue
             full[k] = None if t is None else t.detach().cpu()
+            if t is not None:
+                self.last_state_dict_host_bytes += t.numel() * t.element_size()
+        if not mine:
+            return {}
         ps = {}
         for p, o, n, _ in e.layout:
             ps[e.param_names[id(p)]] = {k: (None if v is None else v[o:o + n].view(p.shape)) for k, v in full.items()}
@@ -282,7 +310,7 @@ class ShardedAdamW(FlatAdamW):
     loadable at any world size."""
 
     def __init__(self, engine, lr: float, betas=(0.9, 0.999), eps: float = 1e-8, weight_decay: float = 0.0,
-                 master_weights: bool = True, stochastic_rounding: bool = True, state_dtype=torch.float32):
+                 master_weights: bool = True, stochastic_rounding: bool = True, state_dtype="auto"):
         if not engine.shard:
             raise ValueError("ShardedAdamW needs a DDPEngine built with shard=True")
         self.engine = engine
@@ -293,10 +321,7 @@ class ShardedAdamW(FlatAdamW):
         self.master_weights = master_weights
         self.stochastic_rounding = stochastic_rounding and not master_weights
         self.step_count = 0
-        if isinstance(state_dtype, str):
-            state_dtype = {"fp32": torch.float32, "float32": torch.float32, "bf16": torch.bfloat16,
-                           "bfloat16": torch.bfloat16}[state_dtype]
-        self.state_dtype = state_dtype
+        self.state_dtype = state_dtype = _state_dtype(state_dtype, engine)
         e = engine
         # owned slice of every bucket -> offset in the local (sharded) state buffers
         self.slices = []  # (bucket, start, end, local_offset, decay)
@@ -422,17 +447,35 @@ class ShardedAdamW(FlatAdamW):
         return norm
 
     # ------------------------------------------------------------------ checkpoints: full (gathered) state
-    def _full_state(self, key: str) -> Optional[torch.Tensor]:
+    def _collective_state(self) -> bool:
+        return self.engine.world_size > 1
+
+    def _full_state(self, key: str, dst: Optional[int] = None) -> Optional[torch.Tensor]:
+        """The full flat state ``key``: all-gathered onto every rank (``dst=None``) or GATHERED onto rank ``dst``
+        only — the other ranks send their owned slice of each bucket and never allocate the full tensor (a 3B model's
+        bf16 moments are ~6 GB per tensor: at N = 8 a full copy on every rank would be ~48 GB per state tensor)."""
         import torch.distributed as dist
         local = {"exp_avg": self.exp_avg, "exp_avg_sq": self.exp_avg_sq, "master": self.master}[key]
         if local is None:
             return None
         e = self.engine
-        full = torch.zeros(e.numel, dtype=local.dtype, device=e.device)
+        if dst is None or e.world_size == 1:
+            full = torch.zeros(e.numel, dtype=local.dtype, device=e.device)
+            for b, s, t, lo, _ in self.slices:
+                full[s:t].copy_(local[lo:lo + t - s])
+                if e.world_size > 1 and not b.replicated:
+                    dist.all_gather_into_tensor(full[b.start:b.end], full[s:t], group=e.pg)
+            return full
+        me = e.rank == dst
+        full = torch.zeros(e.numel, dtype=local.dtype, device=e.device) if me else None
         for b, s, t, lo, _ in self.slices:
-            full[s:t].copy_(local[lo:lo + t - s])
-            if e.world_size > 1 and not b.replicated:
-                dist.all_gather_into_tensor(full[b.start:b.end], full[s:t], group=e.pg)
+            if b.replicated:  # whole on every rank: the destination has it already
+                if me:
+                    full[s:t].copy_(local[lo:lo + t - s])
+                continue
+            n = t - s
+            parts = [full[b.start + r * n:b.start + (r + 1) * n] for r in range(e.world_size)] if me else None
+            dist.gather(local[lo:lo + n].contiguous(), parts, dst=dst, group=e.pg)
         return full
 
     def _state_ranges(self):

@@ -126,6 +126,20 @@ class SFTTrainer:
                                 bucket_cap_mb=args.ddp_bucket_cap_mb,  # None: xGMI plan (plan_bucket_mb)
                                 first_bucket_mb=args.ddp_first_bucket_mb,
                                 broadcast_params=args.ddp_broadcast_params, shard=shard)
+        if self.engine.tied_sparse:
+            # most tokens one synchronising pass can hold (every rank computes the same bound from the config):
+            # the sparse tied-embedding exchange gathers that many rows without a device sync
+            L = int(args.max_length or 1024)
+            if args.packing:
+                per_pass = -(-args.per_device_train_batch_size * L // 256) * 256
+            else:
+                pm = int(pad_mult or 1)
+                per_pass = args.per_device_train_batch_size * (-(-L // pm) * pm)  # padded to the collator's multiple
+            if args.gradient_accumulation_steps > 1 and getattr(args, "ga_merge_max_tokens", 0):
+                per_pass = max(per_pass, int(args.ga_merge_max_tokens))
+            cap = -(-per_pass // self.cp_size)
+            V = model.config.vocab_size
+            self.engine.sparse_cap = cap if cap * self.dist.world_size < V else 0  # else: measured per step
         opt_cls = ShardedAdamW if shard else FlatAdamW
         self.optimizer = opt_cls(self.engine, lr=args.learning_rate, betas=(args.adam_beta1, args.adam_beta2),
                                    eps=args.adam_epsilon, weight_decay=args.weight_decay,
@@ -147,6 +161,15 @@ class SFTTrainer:
         from ..utils.profiling import StepTimer
         self.phase_timer = StepTimer(enabled=dev.type == "cuda") if args.log_step_phases else None
         self._log_count = 0
+        # per-rank heartbeat (step, phase, last gradient bucket issued): the launcher's hang detector reads it, the
+        # watchdog thread (SFTAMD_HANG_TIMEOUT_S / SFTAMD_RUN_DEADLINE_S) ends a stuck rank with exit code 124
+        from ..utils import heartbeat as hb
+        eng = self.engine
+        info = lambda: {"bucket": eng.last_launched, "buckets": len(eng.buckets)}  # noqa: E731
+        self.heartbeat = hb.get() or hb.install(hb.Heartbeat(self.dist.rank, info=info))
+        if self.heartbeat.info is None:  # a caller's heartbeat (bench.py): add this engine's bucket position
+            self.heartbeat.info = info
+        self._hb_step = 0
 
     # ------------------------------------------------------------------ data helpers
     @staticmethod
@@ -239,8 +262,11 @@ class SFTTrainer:
             n = torch.tensor([float(sum(b["num_items"] for b in micro))], device=self.dist.device)
         if self.args.average_tokens_across_devices:
             return all_reduce_sum_async(n)
-        # per-rank normalisation (HF: local mean per rank, DDP then AVERAGES the gradients): the buckets are
-        # SUM-reduced here, so each rank's local count is scaled by the world size
+        # per-rank normalisation (HF: local mean per DATA-PARALLEL rank, DDP then AVERAGES the gradients): the buckets
+        # are SUM-reduced here, so the local count is scaled by the data-parallel size. Under context parallelism a
+        # DP rank's batch is split over its CP group: its local count is the CP group's sum, not this chunk's
+        if self.cp_size > 1:
+            return all_reduce_sum_async(n, group=self.cp_group, scale=float(self.dp_size))
         return n.clamp(min=1.0) * self.dist.world_size
 
     def _phase(self, name: str, host: bool = False):
@@ -312,6 +338,8 @@ class SFTTrainer:
     def _optimizer_step(self, micro: List[Dict], lr: float) -> Dict[str, torch.Tensor]:
         model, eng = self.model, self.engine
         model.train()
+        self._hb_step += 1
+        beat = self.heartbeat.beat
         micro = self._merge_micro([self._cp_shard(b) for b in micro])
         n_items = self.global_num_items(micro)
         acc = torch.zeros(4, device=self.dist.device)  # loss, correct, entropy_sum, valid
@@ -320,14 +348,18 @@ class SFTTrainer:
             ctx = contextlib.nullcontext() if sync else eng.no_sync()
             with ctx:
                 eng.prepare_backward()
+                beat(self._hb_step, "fwd", micro=i)
                 with self._phase("fwd"):
                     out = model(**self._model_inputs(b), num_items_in_batch=n_items)
+                beat(self._hb_step, "bwd", micro=i)
                 with self._phase("bwd"):
                     out.loss.backward()
             acc[0] += out.loss.detach()
             acc[1:] += out.metrics
+        beat(self._hb_step, "comm_wait")
         with self._phase("comm_wait"):
             eng.finish_backward()
+        beat(self._hb_step, "optim")
         with self._phase("optim"):
             norm = self.optimizer.step(lr=lr, max_grad_norm=self.args.max_grad_norm)
         eng.zero_grad()
@@ -379,9 +411,9 @@ class SFTTrainer:
         self.optimizer.synchronize()
         a = self.args
         path = os.path.join(a.output_dir, f"checkpoint-{self.state.global_step}")
-        # EVERY rank takes part: under ZeRO-1 the state is all-gathered from the shards (a collective that
-        # would deadlock if only rank 0 entered it while the others wait in the barrier)
-        osd = self.optimizer.state_dict()
+        # EVERY rank takes part: under ZeRO-1 the shards are gathered onto rank 0 (a collective that would deadlock if
+        # only rank 0 entered it while the others wait in the barrier); no other rank builds a full host copy
+        osd = self.optimizer.state_dict(dst=0)
         barrier()
         ckpt.save_rng(path, self.dist.rank)
         ckpt.save_checkpoint(path, self.model, self.optimizer, self.scheduler, self.state, a, self.dist.rank,

@@ -4,11 +4,16 @@
 reaches that optimizer step — the launcher must then tear the group down and, with
 ``--max-restarts``, restart it so the trainer resumes from the latest checkpoint. Only the first
 attempt injects (``SFTAMD_RESTART_COUNT == 0``).
+
+``SFTAMD_FAULT_INJECT="rank:step:hang"`` makes that rank stop making progress instead (it sleeps forever without
+exiting, like a rank stuck in a driver call): the other ranks then block in their next collective, and only the
+heartbeat watchdogs (utils/heartbeat.py, launch.py ``--hang-timeout``) end the run.
 """
 from __future__ import annotations
 
 import os
 import sys
+import time
 
 
 def maybe_inject(rank: int, step: int) -> None:
@@ -17,7 +22,12 @@ def maybe_inject(rank: int, step: int) -> None:
         return
     parts = spec.split(":")
     r, s = int(parts[0]), int(parts[1])
+    if rank != r or step != s:
+        return
+    if len(parts) > 2 and parts[2] == "hang":
+        print(f"[fault] injecting a hang on rank {rank} at step {step}", file=sys.stderr, flush=True)
+        while True:
+            time.sleep(3600)
     code = int(parts[2]) if len(parts) > 2 else 17
-    if rank == r and step == s:
-        print(f"[fault] injecting failure on rank {rank} at step {step}", file=sys.stderr, flush=True)
-        os._exit(code)
+    print(f"[fault] injecting failure on rank {rank} at step {step}", file=sys.stderr, flush=True)
+    os._exit(code)

@@ -7,6 +7,21 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 if ROOT not in sys.path:
     sys.path.insert(0, ROOT)
 
+# SFTAMD_* variables present when the test session starts: the kernels read several of them per call, so a session
+# started with overrides would not test the shipped default paths (tests/test_env_guard.py fails on any)
+START_SFTAMD_ENV = {k: v for k, v in os.environ.items() if k.startswith("SFTAMD_")}
+
+
+@pytest.fixture(autouse=True)
+def _restore_environ():
+    """Every test starts and ends with the session's environment: a test that sets a dispatch override (e.g. an
+    attention variant) cannot leak it into the tests that run after it in the same process."""
+    saved = dict(os.environ)
+    yield
+    if os.environ != saved:
+        os.environ.clear()
+        os.environ.update(saved)
+
 
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an MI355X (HIP) GPU")

@@ -56,3 +56,36 @@ def test_bench_failing_rank_tears_down_the_group():
     assert r.returncode == 23, (r.returncode, r.stderr[-2000:])
     assert "terminating the other ranks" in r.stderr
     assert not _json_lines(r.stdout)
+
+
+def test_bench_hang_is_detected_and_reported():
+    """A rank that stops making progress (not an exit: it sleeps inside step 2) while its peer blocks in the next
+    collective: the heartbeat watchdogs end the run with 124 well inside the bench timeout and print the last
+    heartbeat (rank, step, phase, last gradient bucket) of the hung rank."""
+    import time
+    t0 = time.time()
+    r = _bench(2, ["--timeout-s", "150", "--hang-timeout-s", "12"], env_extra={"SFTAMD_FAULT_INJECT": "1:2:hang"},
+               timeout=240)
+    assert r.returncode == 124, (r.returncode, r.stderr[-3000:])
+    assert time.time() - t0 < 150
+    assert "injecting a hang on rank 1" in r.stderr
+    assert "last heartbeat" in r.stderr and '"rank":1' in r.stderr, r.stderr[-3000:]
+    assert '"bucket"' in r.stderr  # the DDP engine's position rides in every heartbeat
+    assert not _json_lines(r.stdout)
+
+
+def test_rccl_info_summary_parser():
+    from llm_fine_tune_distributed_amd.parallel.rccl_info import summarize_text
+    log = "\n".join([
+        "host:1:1 [0] NCCL INFO RCCL version : 2.22.3-develop",
+        "host:1:1 [0] NCCL INFO Channel 00/32 :    0   1   2   3   4   5   6   7",
+        "host:1:1 [0] NCCL INFO Channel 31/32 :    0   7   6   5   4   3   2   1",
+        "host:1:1 [0] NCCL INFO Channel 00/0 : 0[0] -> 1[1] via P2P/IPC",
+        "host:1:1 [0] NCCL INFO Channel 01/0 : 0[0] -> 7[7] via P2P/direct pointer",
+        "host:1:1 [0] NCCL INFO 32 coll channels, 32 collnet channels, 0 nvls channels, 32 p2p channels, 4 p2p "
+        "channels per peer",
+        "host:1:1 [0] NCCL INFO comm 0x1 rank 0 nranks 8 cudaDev 0 busId 1000 - Init COMPLETE"])
+    s = summarize_text(log)
+    assert s["n_channels"] == 32 and s["coll_channels"] == 32 and s["p2p_channels"] == 32
+    assert s["p2p_transport"] == ["P2P/IPC", "P2P/direct pointer"] and s["init_ok"] and s["version"] == "2.22.3"
+    assert summarize_text("")["n_channels"] is None

@@ -23,7 +23,7 @@ def _flat_state(osd, k):
 
 
 def _run(rank, world, port, out_dir, per_dev, ga, steps, shard=False, tag="", avg_tokens=True, fixed_len=False,
-         merge=0):
+         merge=0, max_len=1024):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), WORLD_SIZE=str(world), RANK=str(rank),
                       LOCAL_RANK=str(rank))
     import llm_fine_tune_distributed_amd.parallel.process_group as pgm
@@ -39,25 +39,30 @@ def _run(rank, world, port, out_dir, per_dev, ga, steps, shard=False, tag="", av
                      learning_rate=1e-3, max_steps=steps, logging_steps=1, dataloader_drop_last=True,
                      jsonl_log=False, ddp_check_sync_every=1, ddp_bucket_cap_mb=0.05, ddp_first_bucket_mb=0.01,
                      save_strategy="no", shard_optimizer_state=shard, average_tokens_across_devices=avg_tokens,
-                     ga_merge_max_tokens=merge)
+                     ga_merge_max_tokens=merge, max_length=max_len)
     t = SFTTrainer(model=m, args=args, train_dataset=ds)
     out = t.train()
-    osd = t.optimizer.state_dict()  # collective in ZeRO-1 mode: every rank takes part
+    osd = t.optimizer.state_dict(dst=None)  # full state on every rank (collective in ZeRO-1 mode)
+    osd0 = t.optimizer.state_dict(dst=0)  # the checkpoint form: built on rank 0 only
+    dst0 = {"empty": not osd0, "host_bytes": t.optimizer.last_state_dict_host_bytes,
+            "equal": bool(osd0) and all(torch.equal(_flat_state(osd0, k), _flat_state(osd, k))
+                                         for k in ("exp_avg", "exp_avg_sq"))}
     torch.save({"params": t.engine.params_by_name().clone(), "loss": out.training_loss,
                 "log": [h for h in t.state.log_history if "loss" in h], "exp_avg": _flat_state(osd, "exp_avg"),
                 "exp_avg_sq": _flat_state(osd, "exp_avg_sq"), "sharded": type(t.optimizer).__name__,
                 "tied_sparse": t.engine.tied_sparse, "sparse_exchanges": t.engine.sparse_exchanges,
-                "replicated_buckets": sum(b.replicated for b in t.engine.buckets)},
+                "replicated_buckets": sum(b.replicated for b in t.engine.buckets), "dst0": dst0,
+                "sparse_cap": t.engine.sparse_cap},
                os.path.join(out_dir, f"r{world}_{rank}{tag}.pt"))
     pgm.cleanup_distributed()
 
 
-def _launch(world, per_dev, ga, steps, d, shard=False, tag="", avg_tokens=True, fixed_len=False, merge=0):
+def _launch(world, per_dev, ga, steps, d, shard=False, tag="", avg_tokens=True, fixed_len=False, merge=0, max_len=1024):
     port = _free_port()
     if world == 1:
-        _run(0, 1, port, d, per_dev, ga, steps, shard, tag, avg_tokens, fixed_len, merge)
+        _run(0, 1, port, d, per_dev, ga, steps, shard, tag, avg_tokens, fixed_len, merge, max_len)
     else:
-        mp.spawn(_run, args=(world, port, d, per_dev, ga, steps, shard, tag, avg_tokens, fixed_len, merge),
+        mp.spawn(_run, args=(world, port, d, per_dev, ga, steps, shard, tag, avg_tokens, fixed_len, merge, max_len),
                  nprocs=world, join=True)
 
 
@@ -206,12 +211,14 @@ def test_tied_embedding_sparse_exchange(world, shard, ga, merge, monkeypatch):
     per_dev = 4 // world if ga == 1 else 2 // (world // 2 if world > 2 else 1)
     per_dev = max(1, per_dev)
     monkeypatch.setenv("SFTAMD_TIED_SPARSE", "1")
-    _launch(world, per_dev, ga, 3, d, shard=shard, tag="_sp", merge=merge)
+    _launch(world, per_dev, ga, 3, d, shard=shard, tag="_sp", merge=merge, max_len=24)
     monkeypatch.setenv("SFTAMD_TIED_SPARSE", "0")
-    _launch(world, per_dev, ga, 3, d, shard=shard, tag="_dn", merge=merge)
+    _launch(world, per_dev, ga, 3, d, shard=shard, tag="_dn", merge=merge, max_len=24)
     sp = [torch.load(os.path.join(d, f"r{world}_{r}_sp.pt")) for r in range(world)]
     dn = torch.load(os.path.join(d, f"r{world}_0_dn.pt"))
     assert sp[0]["tied_sparse"] and sp[0]["sparse_exchanges"] == 3 and sp[0]["replicated_buckets"] >= 1
+    # a host-known gather size (no device sync) unless the bound is too large for the vocabulary (merged GA passes)
+    assert (sp[0]["sparse_cap"] > 0) == (merge == 0), sp[0]["sparse_cap"]
     assert not dn["tied_sparse"] and dn["sparse_exchanges"] == 0 and dn["replicated_buckets"] == 0
     for r in range(1, world):
         assert torch.equal(sp[0]["params"], sp[r]["params"])  # replicated tied weight stays bit-identical
@@ -220,3 +227,16 @@ def test_tied_embedding_sparse_exchange(world, shard, ga, merge, monkeypatch):
     for a, b in zip(dn["log"], sp[0]["log"]):
         assert abs(a["loss"] - b["loss"]) < 1e-4
         assert abs(a["grad_norm"] - b["grad_norm"]) < 1e-3 * max(1.0, a["grad_norm"])
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_zero1_state_dict_gathers_to_rank0_only(world):
+    """Checkpoint form of the ZeRO-1 optimizer state: rank 0 receives every shard (equal to the all-gathered state);
+    the other ranks return nothing and copy nothing to the host (O(shard) memory)."""
+    d = tempfile.mkdtemp()
+    _launch(world, 1, 1, 2, d, shard=True, tag="_g")
+    recs = [torch.load(os.path.join(d, f"r{world}_{r}_g.pt")) for r in range(world)]
+    assert recs[0]["sharded"] == "ShardedAdamW"
+    assert not recs[0]["dst0"]["empty"] and recs[0]["dst0"]["equal"] and recs[0]["dst0"]["host_bytes"] > 0
+    for r in recs[1:]:
+        assert r["dst0"]["empty"] and r["dst0"]["host_bytes"] == 0

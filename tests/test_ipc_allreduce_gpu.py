@@ -40,10 +40,21 @@ def _worker(rank, world, port, q):
             outs.append((err, x.float().cpu()))
         res[(str(dt), n)] = outs
     res["error_word"] = ar.check()
-    # a peer that never arrives: rank 1 skips one call -> rank 0's bounded wait expires and sets the error word
+    res["poll_ok"] = ar.poll()
+    res["uncached"] = ar.uncached
+    # a peer that never arrives: rank 1 skips one call -> rank 0's bounded wait expires, sets the error word and
+    # poisons the output with NaN; the non-blocking poll reports it once the call has finished
     if rank == 0:
-        ar.all_reduce_(torch.ones(4, device="cuda"))
+        y = torch.ones(4, device="cuda")
+        ar.all_reduce_(y)
         res["timeout_error"] = ar.check()
+        res["timeout_nan"] = bool(torch.isnan(y).all().item())
+        res["timeout_poll"] = ar.poll()
+        try:
+            ar.raise_if_failed()
+            res["raised"] = False
+        except RuntimeError:
+            res["raised"] = True
     dist.barrier()
     ar.close()
     q.put((rank, res))
@@ -69,4 +80,6 @@ def test_ipc_allreduce_two_ranks_one_gpu():
             assert e0 <= tol and e1 <= tol, (key, e0, e1)
             assert torch.equal(x0, x1), key  # rank-order sum: identical on every rank
     assert out[0]["error_word"] == 0 and out[1]["error_word"] == 0
-    assert out[0]["timeout_error"] == 1
+    assert out[0]["poll_ok"] == 0 and out[1]["poll_ok"] == 0
+    assert out[0]["timeout_error"] == 1 and out[0]["timeout_nan"] and out[0]["timeout_poll"] == 1 and out[0]["raised"]
+    print("IPC region uncached:", out[0]["uncached"], out[1]["uncached"])

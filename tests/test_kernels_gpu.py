@@ -1,4 +1,5 @@
 """Numerics of every HIP kernel vs a plain PyTorch fp32 reference of the same op (GPU only)."""
+import contextlib
 import math
 import os
 
@@ -172,11 +173,28 @@ def test_cross_entropy(V):
     assert rel_err(lg, gref) < 2e-2
 
 
+@contextlib.contextmanager
+def _env(**kv):
+    """Set SFTAMD_* dispatch overrides for one case and restore the previous values afterwards."""
+    old = {k: os.environ.get(k) for k in kv}
+    os.environ.update(kv)
+    try:
+        yield
+    finally:
+        for k, v in old.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
+
+
 def _attn_case(lens, nq, nkv, causal, variant, impl="2", cfg="", ds_mb=""):
-    os.environ["SFTAMD_ATTN_TR"] = variant
-    os.environ["SFTAMD_ATTN_IMPL"] = impl
-    os.environ["SFTAMD_ATTN_CFG"] = cfg
-    os.environ["SFTAMD_ATTN_DS_MB"] = ds_mb  # "" = default budget (materialised dS^T + dq4), "0" = dq3 path
+    # ds_mb: "" = default budget (materialised dS^T + dq4), "0" = dq3 path
+    with _env(SFTAMD_ATTN_TR=variant, SFTAMD_ATTN_IMPL=impl, SFTAMD_ATTN_CFG=cfg, SFTAMD_ATTN_DS_MB=ds_mb):
+        _attn_case_body(lens, nq, nkv, causal)
+
+
+def _attn_case_body(lens, nq, nkv, causal):
     torch.manual_seed(0)
     D = 128
     cu = torch.tensor([0] + list(torch.tensor(lens).cumsum(0)), dtype=torch.int32, device=DEV)
@@ -269,10 +287,10 @@ def test_flash_attention_launch_configs(impl, cfg):
 
 
 @pytest.mark.parametrize("impl", ["3", "4"])
-def test_flash_attention_deferred_rescale_branch(impl):
+def test_flash_attention_deferred_rescale_branch(impl, monkeypatch):
     """Force the online-softmax max to jump past THR mid-sequence (CDNA guide rule 26)."""
-    os.environ["SFTAMD_ATTN_IMPL"] = impl
-    os.environ["SFTAMD_ATTN_CFG"] = ""
+    monkeypatch.setenv("SFTAMD_ATTN_IMPL", impl)
+    monkeypatch.setenv("SFTAMD_ATTN_CFG", "")
     torch.manual_seed(1)
     D, nq, nkv = 128, 4, 2
     T = 384
@@ -516,6 +534,38 @@ def test_gemm_tn_plain(cfg, M, N, K):
     w = torch.randn(N, K, device=DEV, dtype=torch.bfloat16)
     c = _ext.ops().gemm_tn(x, w, cfg)
     assert rel_err(c, x.float() @ w.float().t()) < 5e-3
+
+
+@pytest.mark.parametrize("M,N,K", [(256, 256, 128), (512, 512, 256), (768, 512, 2176), (2048, 3072, 384),
+                                   (512, 1280, 11008), (4096, 4352, 256), (2304, 7424, 128)])
+def test_gemm_tn_4wave(M, N, K):
+    """cfg 12: 4 waves of 128 x 128 (accumulators pinned in AGPRs by inline-asm MFMAs) vs the fp32 reference, plus the
+    fused SwiGLU / RoPE epilogues of the same kernel against their unfused twins."""
+    torch.manual_seed(0)
+    x = torch.randn(M, K, device=DEV, dtype=torch.bfloat16)
+    w = torch.randn(N, K, device=DEV, dtype=torch.bfloat16)
+    ref32 = x.float() @ w.float().t()
+    # 13-44: schedule variants of the same kernel; 50: the persistent version (tiles > 256 walk several per
+    # workgroup; K = 128 is its single-pair path)
+    for cfg in (12, 13, 16, 20, 21, 24, 25, 28, 44, 50):
+        c = _ext.ops().gemm_tn(x, w, cfg)
+        assert rel_err(c, ref32) < 5e-3, cfg
+    gu, act = _ext.ops().gemm_tn_swiglu(x, w * 0.1, 12)
+    gu_ref = x.float() @ (w * 0.1).float().t()
+    assert rel_err(gu, gu_ref) < 5e-3
+    assert rel_err(act, _ext.ops().swiglu_fwd(gu)) < 2e-3
+    if N % 128 == 0 and N >= 512:
+        D, nkv = 128, 1
+        nq = N // D - 2 * nkv
+        pos = torch.arange(M, device=DEV).float()
+        inv = 1.0 / (10000 ** (torch.arange(0, D, 2, device=DEV).float() / D))
+        fr = pos[:, None] * inv[None, :]
+        cs, sn = fr.cos().contiguous(), fr.sin().contiguous()
+        out = _ext.ops().gemm_tn_rope(x, w, cs, sn, (nq + nkv) * D, 12)
+        y = (x.float() @ w.float().t()).to(torch.bfloat16)
+        qk = y[:, :(nq + nkv) * D].view(M, nq + nkv, D)
+        exp = torch.cat([ref.apply_rope(qk, cs, sn).reshape(M, -1), y[:, (nq + nkv) * D:]], dim=1)
+        assert rel_err(out, exp) < 1e-2
 
 
 def test_gemm_tn_strided_rows():

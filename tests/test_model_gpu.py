@@ -10,6 +10,7 @@ pytestmark = pytest.mark.gpu
 
 
 def _run(model, ids, labels, hip: bool):
+    prev = os.environ.get("SFTAMD_DISABLE_HIP")
     os.environ["SFTAMD_DISABLE_HIP"] = "0" if hip else "1"
     try:
         for p in model.parameters():
@@ -20,7 +21,10 @@ def _run(model, ids, labels, hip: bool):
         grads = {n: p.grad.detach().float().clone() for n, p in model.named_parameters()}
         return out.loss.detach().float(), grads
     finally:
-        os.environ["SFTAMD_DISABLE_HIP"] = "0"
+        if prev is None:
+            os.environ.pop("SFTAMD_DISABLE_HIP", None)
+        else:
+            os.environ["SFTAMD_DISABLE_HIP"] = prev
 
 
 @pytest.mark.parametrize("mt", ["smollm3", "llama"])

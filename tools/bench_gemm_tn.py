@@ -22,6 +22,8 @@ ap.add_argument("--iters", type=int, default=20)
 ap.add_argument("--cfgs", default="0,1,2,5,6,7", help="gemm_tn configurations to time (8/9 = ping-pong)")
 ap.add_argument("--shapes", default="", help="name:N:K,... instead of the SmolLM3 projection shapes")
 ap.add_argument("--plain-only", action="store_true", help="skip the fused-epilogue section")
+ap.add_argument("--fused-cfgs", default="", help="time only gemm_tn_swiglu / gemm_tn_rope at these cfgs vs their unfused "
+                                                  "twins (skips the plain table)")
 a = ap.parse_args()
 assert _ext.load(), _ext.load_error()
 enable_tuned_gemms()
@@ -49,6 +51,38 @@ def rel(a_, b_):
 
 
 print(f"M = {M}")
+if a.fused_cfgs:
+    FC = [int(c) for c in a.fused_cfgs.split(",")]
+    K, I = 2048, 11008
+    x = torch.randn(M, K, device="cuda", dtype=torch.bfloat16)
+    wgu = torch.randn(2 * I, K, device="cuda", dtype=torch.bfloat16) * 0.02
+    gu_ref = torch.nn.functional.linear(x, wgu)
+    t0 = timeit(lambda: ops.swiglu_fwd(torch.nn.functional.linear(x, wgu)))
+    tb = timeit(lambda: torch.nn.functional.linear(x, wgu))
+    row = [f"blas {tb:.3f} + swiglu kernel = {t0:.3f}"]
+    for c in FC:
+        gu, act = ops.gemm_tn_swiglu(x, wgu, c)
+        assert rel(gu, gu_ref) < 1e-2, c
+        row.append(f"cfg {c} {timeit(lambda: ops.gemm_tn_swiglu(x, wgu, c)):.3f}")
+    print("gate_up + SwiGLU (ms): " + ", ".join(row), flush=True)
+    nq, nkv, D = 16, 4, 128
+    wq = torch.randn((nq + 2 * nkv) * D, K, device="cuda", dtype=torch.bfloat16) * 0.02
+    pos = torch.arange(512, device="cuda").repeat(M // 512).float()
+    inv = 1.0 / (2e6 ** (torch.arange(0, D, 2, device="cuda").float() / D))
+    fr = pos[:, None] * inv[None, :]
+    cs, sn = fr.cos().contiguous(), fr.sin().contiguous()
+
+    def unf():
+        q = torch.nn.functional.linear(x, wq)
+        ops.rope_(q, cs, sn, nq, nkv, D, False)
+        return q
+    qr = unf()
+    row = [f"blas + rope kernel {timeit(unf):.3f}"]
+    for c in FC:
+        assert rel(ops.gemm_tn_rope(x, wq, cs, sn, (nq + nkv) * D, c), qr) < 1e-2, c
+        row.append(f"cfg {c} {timeit(lambda: ops.gemm_tn_rope(x, wq, cs, sn, (nq + nkv) * D, c)):.3f}")
+    print("qkv + RoPE (ms): " + ", ".join(row), flush=True)
+    sys.exit(0)
 CFGS = [int(c) for c in a.cfgs.split(",")]
 print("| shape | N | K | blas ms (TF/s) | " + " | ".join(f"cfg {c}" for c in CFGS) + " | max rel err |")
 print("|---|---:|---:|---:|" + "---:|" * len(CFGS) + "---:|")
