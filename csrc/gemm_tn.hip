@@ -962,8 +962,8 @@ struct Stager4 {
   const u16* pb;  // ... first B piece
   long a32;       // A pieces j, j + 1 are 32 rows apart
   long boff[8];   // B piece q relative to piece 0 (EPI row permutation)
-  __device__ __forceinline__ void piece(char* stage, int w, int j) {
-    const u16* src = j < 8 ? pa + j * a32 : pb + boff[j - 8];
+  __device__ __forceinline__ void piece(char* stage, int w, int j, int koff = 0) {
+    const u16* src = (j < 8 ? pa + j * a32 : pb + boff[j - 8]) + koff;
     glds16(src, stage + (w + 4 * j) * 1024);
   }
 };
@@ -1167,8 +1167,8 @@ __device__ __forceinline__ void mfma_t(f32x4& c, const bf16x8& b, const bf16x8& 
 template <int EPI, bool INIT, bool READ, int NP, bool BAR, int DG = 4>
 __device__ __forceinline__ void tn5_sub(f32x4 (&acc)[8][8], const bf16x8 (&fa)[8], const bf16x8 (&fb)[8],
                                         bf16x8 (&ra)[8], bf16x8 (&rb)[8], const char* img, int offA, int offB,
-                                        Stager4<EPI>& st, char* dst, int w) {
-  static_assert(NP % DG == 0, "DMA pieces per group");
+                                        Stager4<EPI>& st, char* dst, int w, char* dst2 = nullptr) {
+  static_assert(NP % DG == 0 && NP <= 32, "DMA pieces per group");
 #pragma unroll
   for (int i = 0; i < 8; ++i) {
 #pragma unroll
@@ -1180,7 +1180,11 @@ __device__ __forceinline__ void tn5_sub(f32x4 (&acc)[8][8], const bf16x8 (&fa)[8
     }
     if (i < DG) {
 #pragma unroll
-      for (int k = 0; k < NP / DG; ++k) st.piece(dst, w, i * (NP / DG) + k);
+      for (int k = 0; k < NP / DG; ++k) {
+        const int pc = i * (NP / DG) + k;  // pieces 16..31: the following K-tile into dst2
+        if (pc < 16) st.piece(dst, w, pc);
+        else st.piece(dst2, w, pc - 16, BK2);
+      }
     }
   }
 }
@@ -1204,20 +1208,88 @@ __device__ __forceinline__ void tn5_coords(int tile, int nbm, int nbn, int group
 
 __device__ __forceinline__ unsigned pack2(float a, float b) { return (unsigned)f2bf(a) | ((unsigned)f2bf(b) << 16); }
 
-// TRC accumulators of the wave's 128 x 128 tile -> C: 32 16-byte stores per lane (see above)
-__device__ __forceinline__ void tn5_store(f32x4 (&acc)[8][8], u16* C, long ldc, int row0, int col0, int lane) {
+// TRC accumulators of the wave's 128 x 128 tile -> C, 16-byte stores straight from registers (see above).
+// PLAIN: 32 stores per lane. ROPE (the wave's 128 columns are one head, fragments 2q / 2q + 1 = head dims d / d + 64 of
+// one lane): rotate in registers (bf16 projection values, as the unfused path sees them), then pair lo / hi with
+// permlane16_swap — 32 stores. SWIGLU (fragments 2q / 2q + 1 = gate / up of the same act columns): gate / up paired
+// with each other, act (q) with act (q + 1) — 48 stores.
+template <int EPI>
+__device__ __forceinline__ void tn5_store(f32x4 (&acc)[8][8], const EpiArgs& ea, int row0, int m_col0, int wn,
+                                          int lane) {
   const int g = lane >> 4, ii = lane & 15;
-  u16* base = C + (long)(row0 + ii) * ldc + col0 + 16 * (g & 1) + 4 * (g & 2);
+  if constexpr (EPI == EPI_PLAIN) {
+    u16* base = ea.C + (long)(row0 + ii) * ea.ldc + m_col0 + 16 * (g & 1) + 4 * (g & 2);
 #pragma unroll
-  for (int i = 0; i < 8; ++i) {
+    for (int i = 0; i < 8; ++i) {
 #pragma unroll
-    for (int p = 0; p < 4; ++p) {
-      unsigned v0 = pack2(acc[i][2 * p][0], acc[i][2 * p][1]), v1 = pack2(acc[i][2 * p][2], acc[i][2 * p][3]);
-      unsigned w0 = pack2(acc[i][2 * p + 1][0], acc[i][2 * p + 1][1]);
-      unsigned w1 = pack2(acc[i][2 * p + 1][2], acc[i][2 * p + 1][3]);
-      auto r0 = __builtin_amdgcn_permlane16_swap(v0, w0, false, false);
-      auto r1 = __builtin_amdgcn_permlane16_swap(v1, w1, false, false);
-      *(uint4*)(base + (long)(16 * i) * ldc + 32 * p) = make_uint4(r0[0], r1[0], r0[1], r1[1]);
+      for (int p = 0; p < 4; ++p) {
+        unsigned v0 = pack2(acc[i][2 * p][0], acc[i][2 * p][1]), v1 = pack2(acc[i][2 * p][2], acc[i][2 * p][3]);
+        unsigned w0 = pack2(acc[i][2 * p + 1][0], acc[i][2 * p + 1][1]);
+        unsigned w1 = pack2(acc[i][2 * p + 1][2], acc[i][2 * p + 1][3]);
+        auto r0 = __builtin_amdgcn_permlane16_swap(v0, w0, false, false);
+        auto r1 = __builtin_amdgcn_permlane16_swap(v1, w1, false, false);
+        *(uint4*)(base + (long)(16 * i) * ea.ldc + 32 * p) = make_uint4(r0[0], r1[0], r0[1], r1[1]);
+      }
+    }
+  } else if constexpr (EPI == EPI_ROPE) {
+    const bool rot = m_col0 < ea.rope_cols;  // the wave's head is a q / k head (wave-uniform)
+    u16* base = ea.C + (long)(row0 + ii) * ea.ldc + m_col0 + 4 * (g & 2) + 64 * (g & 1);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const long row = row0 + 16 * i + ii;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        float lo[4], hi[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          lo[e] = acc[i][2 * q][e];
+          hi[e] = acc[i][2 * q + 1][e];
+        }
+        if (rot) {
+          const int d = 16 * q + 4 * g;
+          const float4 c4 = *(const float4*)(ea.cosb + row * 64 + d);
+          const float4 s4 = *(const float4*)(ea.sinb + row * 64 + d);
+          const float cs[4] = {c4.x, c4.y, c4.z, c4.w}, sn[4] = {s4.x, s4.y, s4.z, s4.w};
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const float x1 = rbf(lo[e]), x2 = rbf(hi[e]);
+            lo[e] = x1 * cs[e] - x2 * sn[e];
+            hi[e] = x2 * cs[e] + x1 * sn[e];
+          }
+        }
+        auto r0 = __builtin_amdgcn_permlane16_swap(pack2(lo[0], lo[1]), pack2(hi[0], hi[1]), false, false);
+        auto r1 = __builtin_amdgcn_permlane16_swap(pack2(lo[2], lo[3]), pack2(hi[2], hi[3]), false, false);
+        *(uint4*)(base + (long)(16 * i) * ea.ldc + 16 * q) = make_uint4(r0[0], r1[0], r0[1], r1[1]);
+      }
+    }
+  } else {  // SWIGLU: m_col0 = first act column of the wave
+    u16* gu = ea.C + (long)(row0 + ii) * ea.ldc + m_col0 + 4 * (g & 2) + (long)ea.I * (g & 1);
+    u16* ac = ea.act + (long)(row0 + ii) * ea.I + m_col0 + 4 * (g & 2) + 16 * (g & 1);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+#pragma unroll
+      for (int qq = 0; qq < 2; ++qq) {
+        unsigned a01[2], a23[2];
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          const int q = 2 * qq + h;
+          float ga[4], up[4], o[4];
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            ga[e] = rbf(acc[i][2 * q][e]);  // act from the bf16 gate / up the backward will see
+            up[e] = rbf(acc[i][2 * q + 1][e]);
+            o[e] = silu(ga[e]) * up[e];
+          }
+          auto r0 = __builtin_amdgcn_permlane16_swap(pack2(ga[0], ga[1]), pack2(up[0], up[1]), false, false);
+          auto r1 = __builtin_amdgcn_permlane16_swap(pack2(ga[2], ga[3]), pack2(up[2], up[3]), false, false);
+          *(uint4*)(gu + (long)(16 * i) * ea.ldc + 16 * q) = make_uint4(r0[0], r1[0], r0[1], r1[1]);
+          a01[h] = pack2(o[0], o[1]);
+          a23[h] = pack2(o[2], o[3]);
+        }
+        auto r0 = __builtin_amdgcn_permlane16_swap(a01[0], a01[1], false, false);
+        auto r1 = __builtin_amdgcn_permlane16_swap(a23[0], a23[1], false, false);
+        *(uint4*)(ac + (long)(16 * i) * ea.I + 32 * qq) = make_uint4(r0[0], r1[0], r0[1], r1[1]);
+      }
     }
   }
 }
@@ -1227,7 +1299,10 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))
 tn5_kernel(const u16* __restrict__ A, const u16* __restrict__ B, int K, long lda, long ldb, int nbm, int nbn,
            int group, EpiArgs ea) {
   using G = Cfg2<256, 256, 2, 2, 2>;
-  static_assert(EPI == EPI_PLAIN, "persistent 4-wave GEMM: plain epilogue");
+  // The next tile's K0 AND K1 go out in the last sub-step (both stages are free then), the epilogue's NST stores after
+  // them: the next tile waits vmcnt(NST + 16) (PLAIN / ROPE) or vmcnt(NST) (SWIGLU, 48 stores: the counter holds 63)
+  // for K0, and its first boundary only vmcnt(NST) for K1 — the stores drain under its first K-tile.
+  constexpr int NST = EPI == EPI_SWIGLU ? 48 : 32;
   __shared__ __attribute__((aligned(16))) char smem[2 * G::STAGE];
   const int tiles = nbm * nbn, nwg = gridDim.x, orig = blockIdx.x;
   // this XCD's contiguous share of the tile order, walked round-robin by its workgroups (blocks b, b + 8, ...)
@@ -1263,6 +1338,7 @@ tn5_kernel(const u16* __restrict__ A, const u16* __restrict__ B, int K, long lda
   __builtin_amdgcn_s_waitcnt(waitcnt_imm(16, 15));  // K0 of the first tile (its K1 may fly)
   f32x4 acc[8][8];
   bf16x8 a0[8], b0[8], a1[8], b1[8];
+  bool first = true;
   for (;;) {
     __builtin_amdgcn_s_barrier();
 #pragma unroll
@@ -1281,7 +1357,11 @@ tn5_kernel(const u16* __restrict__ A, const u16* __restrict__ B, int K, long lda
       constexpr bool IN = decltype(init)::value, DM = decltype(dma)::value, LA = decltype(last)::value;
       __builtin_amdgcn_s_waitcnt(waitcnt_imm(63, 0));
       tn5_sub<EPI, IN, true, 0, false>(acc, a0, b0, a1, b1, X, offA1, offB1, st, X, w);
-      __builtin_amdgcn_s_waitcnt(waitcnt_imm(0, 0));
+      if (IN && !first) {
+        __builtin_amdgcn_s_waitcnt(waitcnt_imm(NST, 0));  // K1 landed; the previous tile's stores may still drain
+      } else {
+        __builtin_amdgcn_s_waitcnt(waitcnt_imm(0, 0));
+      }
       tn5_sub<EPI, false, true, DM ? 16 : 0, true>(acc, a1, b1, a0, b0, Y, offA0, offB0, st, X, w);
       if (DM) {
         st.pa += BK2;
@@ -1292,7 +1372,7 @@ tn5_kernel(const u16* __restrict__ A, const u16* __restrict__ B, int K, long lda
       __builtin_amdgcn_s_waitcnt(waitcnt_imm(0, 0));
       if constexpr (LA) {
         tn5_stager(st, A, B, lda, ldb, m1, n1, w, lane, ea.I);
-        tn5_sub<EPI, false, false, 16, true>(acc, a1, b1, a0, b0, X, offA0, offB0, st, X, w);
+        tn5_sub<EPI, false, false, 32, true>(acc, a1, b1, a0, b0, X, offA0, offB0, st, X, w, Y);
       } else {
         tn5_sub<EPI, false, true, 16, true>(acc, a1, b1, a0, b0, X, offA0, offB0, st, Y, w);
         st.pa += BK2;
@@ -1309,17 +1389,16 @@ tn5_kernel(const u16* __restrict__ A, const u16* __restrict__ B, int K, long lda
     // the epilogue's accumulator reads follow the last MFMAs: 20 wait states + a fence against hoisting
     asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 3" ::: "memory");
     __builtin_amdgcn_sched_barrier(0);
-    tn5_store(acc, ea.C, ea.ldc, m0 + wm * 128, n0 + wn * 128, lane);
+    tn5_store<EPI>(acc, ea, m0 + wm * 128, EPI == EPI_SWIGLU ? (n0 >> 1) + 64 * wn : n0 + wn * 128, wn, lane);
     __builtin_amdgcn_sched_barrier(0);
     if (!has_next) break;
-    // the next tile's K1 -> Y (Y's last reads were retired before the last barrier)
-    st.pa += BK2;
-    st.pb += BK2;
-#pragma unroll
-    for (int j = 0; j < 16; ++j) st.piece(Y, w, j);
-    st.pa += BK2;
-    st.pb += BK2;
-    __builtin_amdgcn_s_waitcnt(waitcnt_imm(48, 15));  // its K0 landed (the stores and its K1 may fly)
+    st.pa += 2 * BK2;
+    st.pb += 2 * BK2;
+    if constexpr (EPI == EPI_SWIGLU)
+      __builtin_amdgcn_s_waitcnt(waitcnt_imm(NST, 15));  // K0 and K1 landed (the 48 stores may fly)
+    else
+      __builtin_amdgcn_s_waitcnt(waitcnt_imm(NST + 16, 15));  // K0 landed (K1 and the 32 stores may fly)
+    first = false;
     tile = next;
     m0 = m1;
     n0 = n1;
@@ -1468,7 +1547,8 @@ std::tuple<at::Tensor, at::Tensor> gemm_tn_swiglu(const at::Tensor& x, const at:
     const char* e = std::getenv("SFTAMD_TN_TRC");
     return !(e && e[0] == '0');
   }();
-  if (cfg == 12) tn::launch4<tn::EPI_SWIGLU, 0, 4>(x, w_gu, N, ea);
+  if (cfg == 50) tn::launch5<tn::EPI_SWIGLU>(x, w_gu, N, ea);
+  else if (cfg == 12) tn::launch4<tn::EPI_SWIGLU, 0, 4>(x, w_gu, N, ea);
   else if (x.size(1) % 64 == 0 && N % 256 == 0 && cfg == 11) tn::launch3<tn::EPI_SWIGLU, true, 2>(x, w_gu, N, ea);
   else if (x.size(1) % 64 == 0 && trc) tn::launch2<256, 256, 2, 4, 2, tn::EPI_SWIGLU, 3>(x, w_gu, N, ea);
   else if (x.size(1) % 64 == 0) tn::launch2<256, 256, 2, 4, 2, tn::EPI_SWIGLU>(x, w_gu, N, ea);
@@ -1490,7 +1570,8 @@ at::Tensor gemm_tn_rope(const at::Tensor& x, const at::Tensor& w, const at::Tens
   auto c = at::empty({M, N}, x.options());
   tn::EpiArgs ea{(u16*)c.data_ptr(), nullptr, cosb.data_ptr<float>(), sinb.data_ptr<float>(), (long)N, 0,
                  (int)rope_cols};
-  if (cfg == 12) tn::launch4<tn::EPI_ROPE, 0, 4>(x, w, N, ea);
+  if (cfg == 50) tn::launch5<tn::EPI_ROPE>(x, w, N, ea);
+  else if (cfg == 12) tn::launch4<tn::EPI_ROPE, 0, 4>(x, w, N, ea);
   else if (cfg == 1) tn::launch<256, 128, 4, 2, 6, tn::EPI_ROPE>(x, w, N, ea);
   else if (cfg == 2 && x.size(1) % 64 == 0) tn::launch2<256, 256, 2, 4, 2, tn::EPI_ROPE>(x, w, N, ea);
   else if (cfg == 5 && x.size(1) % 64 == 0) tn::launch2<256, 256, 2, 4, 2, tn::EPI_ROPE, 3>(x, w, N, ea);

@@ -179,6 +179,44 @@ def _accumulate_small_grad(param: torch.Tensor, g: torch.Tensor):
     return g.to(param.dtype)
 
 
+# ----------------------------------------------------------------------------- forward GEMMs
+# SFTAMD_FWD_GEMM: which kernel runs the plain projection forwards (o_proj, down_proj, lm_head, NoPE-layer qkv).
+# "persist" = the persistent 4-wave HIP GEMM (csrc/gemm_tn.hip cfg 50: 128 x 128 wave tiles, the next tile's loads and
+# this tile's register epilogue overlapped, profiles/r3_gemm_4wave.md); "blas" = hipBLASLt / rocBLAS through torch.
+# SFTAMD_GATE_UP: the gate_up projection — "blas" (+ the separate SwiGLU kernel) or the config (11 / 12 / 50) of the HIP
+# GEMM with the SwiGLU epilogue (gu and act written by the GEMM, the SwiGLU pass over [M, 2I] gone).
+_FWD_GEMM = os.environ.get("SFTAMD_FWD_GEMM", "blas")
+_GATE_UP = os.environ.get("SFTAMD_GATE_UP", "blas")
+_PERSIST_CFG = 50
+
+
+def _grid_fills(M: int, N: int) -> bool:
+    """256 x 256 tiles over 256 CUs: whole rounds, a last round at least 3/4 full, or enough rounds that a partial one
+    does not matter. Ragged shapes (e.g. down_proj at M = 10240: 1.25 rounds) stay on hipBLASLt, whose stream-K
+    kernels split the partial round (profiles/r3_gemm_4wave.md, M = 10240 table)."""
+    tiles = (M // 256) * (N // 256)
+    rest = tiles % 256
+    return rest == 0 or rest >= 192 or tiles >= 8 * 256
+
+
+def _persist_ok(x2d: torch.Tensor, w: torch.Tensor) -> bool:
+    """Shapes the persistent forward GEMM takes: M, N multiples of 256, K of 128, K-contiguous 16-byte rows."""
+    return (_ext.use_hip(x2d) and x2d.dtype == torch.bfloat16 and w.dtype == torch.bfloat16
+            and x2d.dim() == 2 and x2d.shape[0] % 256 == 0 and x2d.shape[0] > 0 and x2d.shape[1] % 128 == 0
+            and w.shape[0] % 256 == 0 and x2d.stride(1) == 1 and x2d.stride(0) % 8 == 0 and w.is_contiguous()
+            and x2d.data_ptr() % 16 == 0 and w.data_ptr() % 16 == 0 and _grid_fills(x2d.shape[0], w.shape[0]))
+
+
+def fwd_gemm(x2d: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
+    """y = x2d @ w^T for a projection forward: the persistent HIP GEMM where selected and it applies, else
+    hipBLASLt (or the opt-in plain ping-pong GEMM, SFTAMD_TN_PLAIN)."""
+    if _FWD_GEMM == "persist" and _persist_ok(x2d, w):
+        return _ext.ops().gemm_tn(x2d, w, _PERSIST_CFG)
+    if _tn_plain_ok(x2d, w):
+        return _ext.ops().gemm_tn(x2d, w, _tn_cfg(x2d.shape[0], w.shape[0]))
+    return torch.nn.functional.linear(x2d, w)
+
+
 # ----------------------------------------------------------------------------- linear
 class LinearFn(Function):
     @staticmethod
@@ -186,9 +224,8 @@ class LinearFn(Function):
         ctx.save_for_backward(x)
         ctx.weight = weight
         x2d = x.reshape(-1, x.shape[-1])
-        if _tn_plain_ok(x2d, weight):
-            return _ext.ops().gemm_tn(x2d, weight, _tn_cfg(x2d.shape[0], weight.shape[0])).view(
-                *x.shape[:-1], weight.shape[0])
+        if _ext.use_hip(x2d):
+            return fwd_gemm(x2d, weight).view(*x.shape[:-1], weight.shape[0])
         return torch.nn.functional.linear(x, weight)
 
     @staticmethod
@@ -248,7 +285,7 @@ class SwiGLULinearFn(Function):
         ctx.save_for_backward(gu, act)
         ctx.weight = weight
         a2d = act.reshape(-1, act.shape[-1])
-        return torch.nn.functional.linear(a2d, weight).view(*gu.shape[:-1], weight.shape[0])
+        return fwd_gemm(a2d, weight).view(*gu.shape[:-1], weight.shape[0])
 
     @staticmethod
     def backward(ctx, dy):
@@ -506,6 +543,8 @@ class GateUpSwiGLUFn(Function):
 
 
 def _tn_swiglu_cfg(weight: torch.Tensor) -> int:
+    if _GATE_UP not in ("blas", "") and weight.shape[0] % 256 == 0 and weight.shape[1] % 128 == 0:
+        return int(_GATE_UP)
     return 11 if _TN_PINGPONG and weight.shape[0] % 256 == 0 else 5
 
 
@@ -553,7 +592,7 @@ class SwiGLUDownFn(Function):
         ctx.save_for_backward(gu, act)
         ctx.weight = weight
         a2d = act.reshape(-1, act.shape[-1])
-        return torch.nn.functional.linear(a2d, weight).view(*gu.shape[:-1], weight.shape[0])
+        return fwd_gemm(a2d, weight).view(*gu.shape[:-1], weight.shape[0])
 
     @staticmethod
     def backward(ctx, dy):
@@ -579,7 +618,8 @@ def swiglu_mlp(h: torch.Tensor, w_gate_up: torch.Tensor, w_down: torch.Tensor) -
     (no separate SwiGLU kernel in either direction); default: hipBLASLt gate_up + SwiGLU kernel + the fused down
     dgrad (SFTAMD_SWIGLU_DOWN=1); otherwise the unfused chain."""
     h2d = h.reshape(-1, h.shape[-1])
-    if (_TN_MODE in ("1", "swiglu") and _SWIGLU_DOWN and _tn_ok(h2d, w_gate_up) and w_gate_up.shape[0] % 256 == 0
+    fused_gu = _TN_MODE in ("1", "swiglu") or (_GATE_UP not in ("blas", "") and _persist_ok(h2d, w_gate_up))
+    if (fused_gu and _SWIGLU_DOWN and _tn_ok(h2d, w_gate_up) and w_gate_up.shape[0] % 256 == 0
             and (w_gate_up.shape[0] // 2) % 128 == 0):
         gu, act = GateUpActFn.apply(h, w_gate_up)
         return SwiGLUDownFn.apply(gu, act, w_down)
@@ -768,7 +808,7 @@ class LMHeadCEFn(Function):
     @staticmethod
     def forward(ctx, h, weight, labels, inv_count):
         h2d = h.reshape(-1, h.shape[-1])
-        logits = torch.nn.functional.linear(h2d, weight)
+        logits = fwd_gemm(h2d, weight) if _ext.use_hip(h2d) else torch.nn.functional.linear(h2d, weight)
         need_grad = ctx.needs_input_grad[0] or ctx.needs_input_grad[1]
         stats = _ce_rows(logits, labels.reshape(-1), inv_count, need_grad)
         loss = (stats[0].sum() * inv_count.float()).reshape(())

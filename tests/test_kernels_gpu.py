@@ -550,10 +550,11 @@ def test_gemm_tn_4wave(M, N, K):
     for cfg in (12, 13, 16, 20, 21, 24, 25, 28, 44, 50):
         c = _ext.ops().gemm_tn(x, w, cfg)
         assert rel_err(c, ref32) < 5e-3, cfg
-    gu, act = _ext.ops().gemm_tn_swiglu(x, w * 0.1, 12)
     gu_ref = x.float() @ (w * 0.1).float().t()
-    assert rel_err(gu, gu_ref) < 5e-3
-    assert rel_err(act, _ext.ops().swiglu_fwd(gu)) < 2e-3
+    for cfg in (12, 50):
+        gu, act = _ext.ops().gemm_tn_swiglu(x, w * 0.1, cfg)
+        assert rel_err(gu, gu_ref) < 5e-3, cfg
+        assert rel_err(act, _ext.ops().swiglu_fwd(gu)) < 2e-3, cfg
     if N % 128 == 0 and N >= 512:
         D, nkv = 128, 1
         nq = N // D - 2 * nkv
@@ -561,11 +562,12 @@ def test_gemm_tn_4wave(M, N, K):
         inv = 1.0 / (10000 ** (torch.arange(0, D, 2, device=DEV).float() / D))
         fr = pos[:, None] * inv[None, :]
         cs, sn = fr.cos().contiguous(), fr.sin().contiguous()
-        out = _ext.ops().gemm_tn_rope(x, w, cs, sn, (nq + nkv) * D, 12)
         y = (x.float() @ w.float().t()).to(torch.bfloat16)
         qk = y[:, :(nq + nkv) * D].view(M, nq + nkv, D)
         exp = torch.cat([ref.apply_rope(qk, cs, sn).reshape(M, -1), y[:, (nq + nkv) * D:]], dim=1)
-        assert rel_err(out, exp) < 1e-2
+        for cfg in (12, 50):
+            out = _ext.ops().gemm_tn_rope(x, w, cs, sn, (nq + nkv) * D, cfg)
+            assert rel_err(out, exp) < 1e-2, cfg
 
 
 def test_gemm_tn_strided_rows():

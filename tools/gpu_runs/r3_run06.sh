@@ -11,6 +11,6 @@ timeout -k 10 300 python -u -m pytest -x -q --timeout 120 --timeout-method threa
   > gpurun_out/r3_06_k.log 2>&1 || { tail -40 gpurun_out/r3_06_k.log; exit 1; }
 tail -2 gpurun_out/r3_06_k.log
 for m in 8192 10240; do
-timeout -k 10 300 python -u tools/bench_gemm_tn.py --fused-cfgs 11,12 --m $m --iters 30 > gpurun_out/r3_06_$m.log 2>&1 || { tail -30 gpurun_out/r3_06_$m.log; exit 1; }
+timeout -k 10 300 python -u tools/bench_gemm_tn.py --fused-cfgs 11,12,50 --m $m --iters 30 > gpurun_out/r3_06_$m.log 2>&1 || { tail -30 gpurun_out/r3_06_$m.log; exit 1; }
 cat gpurun_out/r3_06_$m.log
 done
