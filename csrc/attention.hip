@@ -875,6 +875,7 @@ __global__ __launch_bounds__(256) void dkdv_reduce_kernel(const float* __restric
 //   THR = 8 (log2 domain; T13 deferred rescale: P stays <= 2^8, exact in bf16 exponent range);
 // * full tiles are staged without per-row bounds checks; one LDS buffer (register prefetch).
 constexpr float THR = 8.f;
+constexpr float THR_FAST = 40.f;  // v6 fast loop: P = exp2(s - m) <= 2^40, o <= 2^49 |V|: far from fp32 / bf16 limits
 
 struct Offs {
   int row[4];  // frag_row bases, k-step s
@@ -1194,6 +1195,221 @@ __global__ __launch_bounds__(NW * 64) void fwd4_kernel(const u16* __restrict__ q
 #pragma unroll
       for (int dt = 0; dt < 8; ++dt) store4(op + 16 * dt, o[r][dt], inv);
       if (g == 0) lse[(long)h * total + start + qrow] = (m[r] + log2f(l[r])) * LN2;
+    }
+  }
+}
+
+// v6 forward (GQA-stacked): one workgroup per (kv head, sequence, 64-query block), 4 waves; wave w owns query
+// positions q0 + 16 w .. + 15 for ALL REP query heads of the kv head. A K fragment (S^T = K Q^T) and a V^T fragment
+// (O^T += V^T P^T) are read from LDS once and feed REP MFMAs, one per head — REP x fewer LDS bytes per MFMA than v3,
+// whose 1 KB per MFMA is twice what the LDS delivers at the MFMA rate. The causal / length masks are shared by the REP
+// heads (same positions). K / V tiles (64 keys) go HBM -> LDS by global_load_lds (16 B per lane, lane-linear LDS
+// writes: the image swizzle is applied to the SOURCE chunk, rows past the sequence end clamped to its last row so
+// nothing outside the sequence is read) into two stages, the next tile's DMA in flight under the current tile's math.
+// The row sums stay per-lane partials until the end (the running max is the only per-tile cross-lane reduction).
+// REP x (32 o + 16 Q) registers per lane: one wave per SIMD, one workgroup per CU; grid (nkv, nseq, q-blocks) with the
+// causally heaviest q-blocks dispatched first (LPT: a CU that drew block 4 of 8 takes block 3 next).
+__device__ __forceinline__ void glds16(const u16* src, char* dst) {
+  __builtin_amdgcn_global_load_lds((const void __attribute__((address_space(1)))*)src,
+                                   (void __attribute__((address_space(3)))*)dst, 16, 0, 0);
+}
+
+// O^T += V^T P^T with the accumulator tied to an AGPR: REP x 8 accumulators stay put across the K loop (as builtins,
+// hipcc shuffled them between AGPRs and VGPRs every tile: ~1250 v_accvgpr moves per tile at REP 4). The compiler does
+// not see these as MFMAs: VALU reads of the accumulators (rescale, epilogue) sit behind nop_mfma() wait states.
+// The leading s_nop 1: P arrives from VALU packs (VALU write -> MFMA operand read: 2 wait states hipcc does not pad
+// inside asm, cdna_hip_programming.md §5.7 item 2).
+__device__ __forceinline__ void mfma_acc(f32x4& c, const bf16x8& a, const bf16x8& b) {
+  asm volatile("s_nop 1\n\tv_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+a"(c) : "v"(a), "v"(b));
+}
+// S^T = K Q^T into VGPRs (the softmax reads them): hipcc's builtin put them in AGPRs and copied them back every tile.
+// Chains accumulate D -> C whole (0 wait states); the VALU readers sit behind nop_mfma().
+__device__ __forceinline__ f32x4 mfma_v0(const bf16x8& a, const bf16x8& b) {
+  f32x4 d;
+  asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, 0" : "=&v"(d) : "v"(a), "v"(b));
+  return d;
+}
+__device__ __forceinline__ void mfma_v(f32x4& c, const bf16x8& a, const bf16x8& b) {
+  asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+v"(c) : "v"(a), "v"(b));
+}
+__device__ __forceinline__ void pin_acc(f32x4& c) { asm volatile("" : "+a"(c)); }  // (re)home a value in AGPRs
+__device__ __forceinline__ void nop_mfma() { asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 3" ::: "memory"); }
+
+template <int REP>
+__global__ __launch_bounds__(256, 1) void fwd6_kernel(const u16* __restrict__ qkv, u16* __restrict__ out,
+                                                      float* __restrict__ lse, const int* __restrict__ cu, int nq,
+                                                      int nkv, int total, float sl2, int causal) {
+  constexpr int TB = 64 * ROWB;  // one 64-row image: 16 KB
+  __shared__ __attribute__((aligned(16))) char smem[4 * TB];  // stage s: K image at 2 s TB, V image at (2 s + 1) TB
+  const int kvh = blockIdx.x, b = blockIdx.y, qb = gridDim.z - 1 - blockIdx.z;
+  const int start = cu[b], len = cu[b + 1] - start;
+  SFT_DASSERT(start >= 0 && len >= 0 && start + len <= total);
+  const int q0 = qb * 64;
+  if (q0 >= len) return;
+  const long ld = (long)(nq + 2 * nkv) * D;
+  const int tid = threadIdx.x, lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6), g = lane >> 4;
+  const int wfirst = q0 + 16 * w, qrow = wfirst + (lane & 15);
+  const bool qok = qrow < len;
+  const int nkb = (len + 63) / 64;
+  const int nkt = causal ? min(qb + 1, nkb) : nkb;
+  // DMA: piece j < 4 of wave w = image rows 4 (w + 4 j) .. + 3 of K and of V (1 KB each); lane -> row r0 + 16 j,
+  // LDS chunk lane & 15 = source chunk swz(row, lane & 15) — the same for every j (row & 3 and (row >> 2) & 3 are)
+  const int r0 = 4 * w + (lane >> 4);
+  const u16* kvsrc = qkv + (long)start * ld + (nq + kvh) * D + 8 * swz(r0, lane & 15);
+  auto dma = [&](int kt, char* stage) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const u16* src = kvsrc + (long)min(kt * 64 + r0 + 16 * j, len - 1) * ld;
+      glds16(src, stage + (w + 4 * j) * 1024);
+      glds16(src + nkv * D, stage + TB + (w + 4 * j) * 1024);
+    }
+  };
+  dma(0, smem);
+  Offs off;
+  off.init(lane);
+  bf16x8 qf[REP][4];
+#pragma unroll
+  for (int h = 0; h < REP; ++h) {
+    const u16* qp = qkv + (long)(start + qrow) * ld + (kvh * REP + h) * D + 8 * g;
+#pragma unroll
+    for (int s = 0; s < 4; ++s) qf[h][s] = load_frag_global(qp + 32 * s, qok);
+  }
+  f32x4 o[REP][8];
+  float m[REP], l[REP];
+#pragma unroll
+  for (int h = 0; h < REP; ++h) {
+#pragma unroll
+    for (int dt = 0; dt < 8; ++dt) {
+      o[h][dt] = f32x4{0.f, 0.f, 0.f, 0.f};
+      pin_acc(o[h][dt]);
+    }
+    m[h] = 0.f;  // set from tile 0
+    l[h] = 0.f;
+  }
+  __builtin_amdgcn_s_waitcnt(0);  // tile 0 landed (vmcnt / lgkmcnt 0)
+  __syncthreads();
+  // One K/V tile. FAST: no accumulator rescale — the running max m is set from tile 0 (o = 0 then) and P =
+  // exp2(s - m) may grow up to 2^THR_FAST (bf16 / fp32 hold that exactly enough: only the exponent grows); a tile
+  // whose max exceeds m + THR_FAST returns false BEFORE touching any state and the rest of the row block runs the
+  // SLOW variant (rescale by alpha, v3's deferred scheme). Keeping the rescale out of the fast loop keeps the
+  // accumulators in AGPRs there (a VALU rescale in the loop made hipcc copy all of them to VGPRs every tile).
+  auto tile = [&](int kt, auto slow_t) -> bool {
+    constexpr bool SLOW = decltype(slow_t)::value;
+    const int k0 = kt * 64;
+    const char* Ks = smem + (kt & 1) * 2 * TB;
+    const char* Vs = Ks + TB;
+    f32x4 sc[REP][4];
+#pragma unroll
+    for (int nt = 0; nt < 4; ++nt)
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {
+        const bf16x8 kf = lds_row(Ks, off.row[s] + nt * 16 * ROWB);
+#pragma unroll
+        for (int h = 0; h < REP; ++h) {
+          if (s == 0) sc[h][nt] = mfma_v0(kf, qf[h][s]);
+          else mfma_v(sc[h][nt], kf, qf[h][s]);
+        }
+      }
+    nop_mfma();  // MFMA D -> VALU: 12 wait states for the 8-pass MFMA
+    if ((k0 + 64 > len) || (causal && k0 + 63 > wfirst)) {
+#pragma unroll
+      for (int nt = 0; nt < 4; ++nt)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int key = k0 + 16 * nt + 4 * g + i;
+          if (key >= len || (causal && key > qrow)) {
+#pragma unroll
+            for (int h = 0; h < REP; ++h) sc[h][nt][i] = -INFINITY;
+          }
+        }
+    }
+    float tmax[REP];
+    bool big = false;
+#pragma unroll
+    for (int h = 0; h < REP; ++h) {
+      float t = fmaxf(fmaxf(fmaxf(sc[h][0][0], sc[h][0][1]), fmaxf(sc[h][0][2], sc[h][0][3])),
+                      fmaxf(fmaxf(sc[h][1][0], sc[h][1][1]), fmaxf(sc[h][1][2], sc[h][1][3])));
+      t = fmaxf(t, fmaxf(fmaxf(fmaxf(sc[h][2][0], sc[h][2][1]), fmaxf(sc[h][2][2], sc[h][2][3])),
+                         fmaxf(fmaxf(sc[h][3][0], sc[h][3][1]), fmaxf(sc[h][3][2], sc[h][3][3]))));
+      t = fmaxf(t, __shfl_xor(t, 16, 64));
+      t = fmaxf(t, __shfl_xor(t, 32, 64));
+      tmax[h] = t * sl2;
+      if constexpr (!SLOW) {
+        if (kt == 0) m[h] = tmax[h];  // o and l are still 0: no rescale
+        big |= tmax[h] > m[h] + THR_FAST;
+      }
+    }
+    if constexpr (!SLOW) {
+      if (__any(big)) return false;
+    }
+    bf16x8 pb[REP][2];
+#pragma unroll
+    for (int h = 0; h < REP; ++h) {
+      if constexpr (SLOW) {
+        if (__any(tmax[h] > m[h] + THR)) {
+          nop_mfma();
+          const float mnew = fmaxf(m[h], tmax[h]);
+          const float alpha = exp2f(m[h] - mnew);
+          l[h] *= alpha;
+#pragma unroll
+          for (int dt = 0; dt < 8; ++dt) o[h][dt] *= alpha;
+          m[h] = mnew;
+        }
+      }
+      float rs = 0.f;
+#pragma unroll
+      for (int nt = 0; nt < 4; ++nt)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const float p = exp2f(fmaf(sc[h][nt][i], sl2, -m[h]));
+          sc[h][nt][i] = p;
+          rs += p;
+        }
+      l[h] += rs;  // per-lane partial: the 4 lanes of a query share m, so their partials add up at the end
+      pb[h][0] = pack_acc(sc[h][0], sc[h][1]);
+      pb[h][1] = pack_acc(sc[h][2], sc[h][3]);
+    }
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+      for (int dt = 0; dt < 8; ++dt) {
+        const bf16x8 vf = lds_tr(Vs, off.tr[dt] + ks * 32 * ROWB);
+#pragma unroll
+        for (int h = 0; h < REP; ++h) mfma_acc(o[h][dt], vf, pb[h][ks]);
+      }
+    return true;
+  };
+  int kt = 0;
+#pragma nounroll
+  for (; kt < nkt; ++kt) {
+    if (kt + 1 < nkt) dma(kt + 1, smem + ((kt + 1) & 1) * 2 * TB);  // that stage's last reads: before the barrier
+    if (!tile(kt, std::false_type())) break;
+    __builtin_amdgcn_s_waitcnt(0);  // the next tile's DMA landed (this wave's pieces) ...
+    __syncthreads();                 // ... and every wave's; every wave is done reading this stage
+  }
+  if (kt < nkt) {  // rare: a score jumped past m + THR_FAST; tile kt again with rescaling, then the rest
+    nop_mfma();
+#pragma nounroll
+    for (int k2 = kt; k2 < nkt; ++k2) {
+      if (k2 > kt && k2 + 1 < nkt) dma(k2 + 1, smem + ((k2 + 1) & 1) * 2 * TB);
+      tile(k2, std::true_type());
+      __builtin_amdgcn_s_waitcnt(0);
+      __syncthreads();
+    }
+  }
+  nop_mfma();
+#pragma unroll
+  for (int h = 0; h < REP; ++h) {
+    float lt = l[h];
+    lt += __shfl_xor(lt, 16, 64);
+    lt += __shfl_xor(lt, 32, 64);
+    if (qok) {
+      const int hq = kvh * REP + h;
+      u16* op = out + (long)(start + qrow) * nq * D + hq * D + 4 * g;
+      const float inv = 1.f / lt;
+#pragma unroll
+      for (int dt = 0; dt < 8; ++dt) store4(op + 16 * dt, o[h][dt], inv);
+      if (g == 0) lse[(long)hq * total + start + qrow] = (m[h] + log2f(lt)) * LN2;
     }
   }
 }
@@ -1776,8 +1992,15 @@ static long attn_ds_budget() {  // read per call (cheap next to the kernels): te
   return (e && e[0] ? atol(e) : 2048L) * 1024L * 1024L;
 }
 
+// SFTAMD_ATTN_FWD6=1: the GQA-stacked v6 forward where it applies (2 or 4 query heads per kv head)
+static bool attn_fwd6() {
+  const char* e = std::getenv("SFTAMD_ATTN_FWD6");
+  return e && e[0] == '1';
+}
+
 static int attn_impl() {
   const char* e = std::getenv("SFTAMD_ATTN_IMPL");
+  if (e && e[0] == '6') return 6;
   if (e && e[0] == '1') return 1;
   if (e && e[0] == '2') return 2;
   if (e && e[0] == '4') return 4;  // forward v4 (measured slower, kept selectable: profiles/r1_attention_microbench.txt)
@@ -1818,6 +2041,20 @@ std::tuple<at::Tensor, at::Tensor> flash_fwd(const at::Tensor& qkv, const at::Te
     attn::fwd4_kernel<NW, RG><<<g4, NW * 64, 0, cur_stream()>>>((const u16*)qkv.data_ptr(), (u16*)out.data_ptr(),
                                                                lse.data_ptr<float>(), cu_c.data_ptr<int>(), nq, nkv,
                                                                total, sl2, causal ? 1 : 0);
+    SFT_LAUNCH_CHECK();
+    return {out, lse};
+  }
+  const int rep = (int)(nq / nkv);
+  if (attn_impl() == 6 || (attn_impl() == 3 && attn_fwd6() && (rep == 2 || rep == 4))) {
+    SFT_CHECK(rep == 2 || rep == 4, "attention forward v6: 2 or 4 query heads per kv head");
+    SFT_TRACE("attn.fwd6");
+    dim3 g6(nkv, nseq, (max_seqlen + 63) / 64);
+    auto go6 = [&](auto r) {
+      attn::fwd6_kernel<decltype(r)::value><<<g6, 256, 0, cur_stream()>>>(
+          (const u16*)qkv.data_ptr(), (u16*)out.data_ptr(), lse.data_ptr<float>(), cu_c.data_ptr<int>(), nq, nkv, total,
+          sl2, causal ? 1 : 0);
+    };
+    if (rep == 4) go6(std::integral_constant<int, 4>()); else go6(std::integral_constant<int, 2>());
     SFT_LAUNCH_CHECK();
     return {out, lse};
   }

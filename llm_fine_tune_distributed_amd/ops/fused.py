@@ -832,7 +832,100 @@ class LMHeadCEFn(Function):
         return dh, dw, None, None
 
 
+class LMHeadCEChunkedFn(Function):
+    """The LM head + CE over row chunks of ``chunk`` tokens: per chunk the logits GEMM, the CE pass (dlogits written
+    in place), the chunk's dh rows (dlogits @ W) and its dW contribution (dlogits^T h) — all in the FORWARD, assuming
+    a unit upstream gradient, so the [M, V] logits never exist (peak: one [chunk, V] buffer). backward scales dh and
+    dW by the actual upstream gradient g. dW goes straight into ``main_grad`` when this is the parameter's first
+    contribution of the accumulation window (``_sftamd_fresh``: the slice is then scaled by g in place), else into a
+    separate [V, K] buffer added as g * dW in backward. Costs over LMHeadCEFn (profiles/r3_lm_head_chunked.md): the
+    dW GEMM re-reads and re-writes its bf16 output once per chunk, and the dh GEMM per chunk has chunk x K outputs.
+    Opt-in (``set_lm_head_chunk`` / SFTAMD_LMHEAD_CHUNK): MI355X's 288 GB make the full logits affordable at the
+    bench shape; this is for the sizes where they are not (large merged GA passes, Llama-3-8B batches, eval)."""
+
+    @staticmethod
+    def forward(ctx, h, weight, labels, inv_count, chunk):
+        h2d = h.reshape(-1, h.shape[-1])
+        lab = labels.reshape(-1)
+        M = h2d.shape[0]
+        need_dh, need_dw = ctx.needs_input_grad[0], ctx.needs_input_grad[1]
+        hip = _ext.use_hip(h2d)
+        stats = torch.empty(4, M, dtype=torch.float32, device=h2d.device)
+        dh = torch.empty_like(h2d) if need_dh else None
+        mg = getattr(weight, "main_grad", None)
+        ctx.dw_in_mg = False
+        dw_buf = None
+        if need_dw:
+            if mg is not None and mg.dtype == h2d.dtype and getattr(weight, "_sftamd_fresh", False):
+                target, ctx.dw_in_mg = mg, True
+                weight._sftamd_fresh = False
+            else:
+                dw_buf = torch.empty(weight.shape, dtype=h2d.dtype if hip else torch.float32, device=h2d.device)
+                target = dw_buf
+        for r0 in range(0, M, chunk):
+            r1 = min(M, r0 + chunk)
+            hc = h2d[r0:r1]
+            logits = fwd_gemm(hc, weight) if hip else torch.nn.functional.linear(hc, weight)
+            stats[:, r0:r1] = _ce_rows(logits, lab[r0:r1], inv_count, need_dh or need_dw)
+            if need_dh:
+                torch.mm(logits, weight, out=dh[r0:r1])
+            if need_dw:
+                if hip:
+                    _wgrad_mm(target, logits, hc, accumulate=r0 > 0)
+                elif r0 == 0:
+                    torch.mm(logits.t().to(target.dtype), hc.to(target.dtype), out=target)
+                else:
+                    target.addmm_(logits.t().to(target.dtype), hc.to(target.dtype))
+            del logits
+        loss = (stats[0].sum() * inv_count.float()).reshape(())
+        ctx.save_for_backward(*(t for t in (dh, dw_buf) if t is not None))
+        ctx.has = (dh is not None, dw_buf is not None)
+        ctx.weight = weight
+        ctx.h_shape = h.shape
+        ctx.mark_non_differentiable(stats)
+        return loss, stats
+
+    @staticmethod
+    def backward(ctx, dloss, _dstats):
+        saved = iter(ctx.saved_tensors)
+        dh = next(saved) if ctx.has[0] else None
+        dw_buf = next(saved) if ctx.has[1] else None
+        w = ctx.weight
+        g = dloss.float()
+        dh_out = dw_out = None
+        if dh is not None:
+            dh_out = (dh * g.to(dh.dtype)).view(ctx.h_shape)
+        if ctx.needs_input_grad[1]:
+            mg = getattr(w, "main_grad", None)
+            if ctx.dw_in_mg:
+                mg.mul_(g.to(mg.dtype))
+                _weight_grad_done(w)
+            elif mg is not None:
+                mg.add_((dw_buf * g).to(mg.dtype))
+                w._sftamd_fresh = False
+                _weight_grad_done(w)
+            else:
+                dw_out = (dw_buf * g).to(w.dtype)
+        return dh_out, dw_out, None, None, None
+
+
+_LMHEAD_CHUNK = int(os.environ.get("SFTAMD_LMHEAD_CHUNK", "0") or 0)
+
+
+def set_lm_head_chunk(rows: int) -> None:
+    """Rows per LM-head + CE chunk (0 = off: one pass over the full [M, V] logits)."""
+    global _LMHEAD_CHUNK
+    _LMHEAD_CHUNK = max(0, int(rows))
+
+
+def lm_head_chunk() -> int:
+    return _LMHEAD_CHUNK
+
+
 def lm_head_cross_entropy(h, weight, labels, inv_count) -> Tuple[torch.Tensor, torch.Tensor]:
+    M = h.numel() // h.shape[-1]
+    if _LMHEAD_CHUNK and M > _LMHEAD_CHUNK:
+        return LMHeadCEChunkedFn.apply(h, weight, labels, inv_count, _LMHEAD_CHUNK)
     return LMHeadCEFn.apply(h, weight, labels, inv_count)
 
 

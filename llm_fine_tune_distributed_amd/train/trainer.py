@@ -140,6 +140,9 @@ class SFTTrainer:
             cap = -(-per_pass // self.cp_size)
             V = model.config.vocab_size
             self.engine.sparse_cap = cap if cap * self.dist.world_size < V else 0  # else: measured per step
+        if getattr(args, "lm_head_chunk_rows", 0):
+            from ..ops import set_lm_head_chunk
+            set_lm_head_chunk(args.lm_head_chunk_rows)
         opt_cls = ShardedAdamW if shard else FlatAdamW
         self.optimizer = opt_cls(self.engine, lr=args.learning_rate, betas=(args.adam_beta1, args.adam_beta2),
                                    eps=args.adam_epsilon, weight_decay=args.weight_decay,

@@ -305,6 +305,39 @@ def test_flash_attention_deferred_rescale_branch(impl, monkeypatch):
     assert rel_err(out, o_ref) < 2e-2
 
 
+@pytest.mark.parametrize("causal", [True, False])
+def test_flash_attention_fwd6_gqa_stacked(causal, monkeypatch):
+    """v6 forward (one workgroup per kv head x 64 positions, the 2 / 4 query heads of the kv head stacked in each
+    wave, K/V by global_load_lds) vs the fp32 reference: ragged lengths off the tile grid, rep 4 and rep 2, the
+    SmolLM3 shape; the backward (v5 + dq4) consumes its lse."""
+    monkeypatch.setenv("SFTAMD_ATTN_FWD6", "1")
+    _attn_case([100, 255, 64, 1, 300, 129], 8, 2, causal, "1", "3")
+    _attn_case([512, 511, 7], 16, 4, causal, "1", "3")
+    _attn_case([200, 65, 1000], 8, 4, causal, "1", "3")
+    _attn_case([512] * 4, 16, 4, causal, "1", "3")
+
+
+@pytest.mark.parametrize("spike", [20.0, 45.0])
+def test_flash_attention_fwd6_slow_path(spike, monkeypatch):
+    """v6's fast loop never rescales; a score jump past THR_FAST (spike 45: ~60 in log2 units at key tile 3) sends
+    the rest of that row block to the rescaling loop. Both must match the reference."""
+    monkeypatch.setenv("SFTAMD_ATTN_FWD6", "1")
+    monkeypatch.setenv("SFTAMD_ATTN_IMPL", "3")
+    torch.manual_seed(1)
+    D, nq, nkv = 128, 8, 2
+    T = 384
+    cu = torch.tensor([0, T], dtype=torch.int32, device=DEV)
+    qkv = (0.3 * torch.randn(T, (nq + 2 * nkv) * D, device=DEV)).to(torch.bfloat16)
+    k = qkv[:, nq * D:(nq + nkv) * D].view(T, nkv, D)
+    q = qkv[:, :nq * D].view(T, nq, D)
+    k[200] = (spike * q[300, 0].float()).to(k.dtype)
+    scale = 1 / math.sqrt(D)
+    out, lse = _ext.ops().flash_fwd(qkv, cu, T, nq, nkv, D, scale, True)
+    o_ref = ref.attention(qkv.float(), nq, nkv, D, cu, scale, True)
+    assert rel_err(out, o_ref) < 2e-2
+    assert torch.isfinite(lse).all()
+
+
 def test_flash_attention_concurrent_bwd_bitwise(monkeypatch):
     """dq on a side stream concurrently with dK/dV (default) == the serial launch order, bit for bit, and the
     result is complete when the op returns on the caller's stream (no extra sync)."""
