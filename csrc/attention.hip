@@ -1414,6 +1414,157 @@ __global__ __launch_bounds__(256, 1) void fwd6_kernel(const u16* __restrict__ qk
   }
 }
 
+// v6 dQ (recompute, GQA-stacked): the fwd6 geometry — one workgroup per (kv head, sequence, 64-query block), wave w
+// owns positions q0 + 16 w .. + 15 for all REP query heads — recomputing S^T = K Q^T and dP^T = V dO^T per 64-key
+// tile, dS^T = P o (dP - delta) with P = exp2(S sl2 - lse) (lse and delta are per-lane scalars in this layout: lane
+// (g, r) holds query r), and dQ^T += K^T dS^T. Every K row / V row / K^T fragment read from LDS feeds REP MFMAs. Against
+// dq4 it triples the MFMA work but drops the lp x lp bf16 dS^T round trip through HBM (stores in the dK/dV kernel,
+// loads here). Q and dO fragments and the dQ accumulators live in AGPRs (MFMA B / C operands), S and dP in VGPRs.
+__device__ __forceinline__ void pin_frag(bf16x8& x) { asm volatile("" : "+a"(x)); }
+__device__ __forceinline__ f32x4 mfma_v0_a(const bf16x8& a, const bf16x8& b) {
+  f32x4 d;
+  asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, 0" : "=&v"(d) : "v"(a), "a"(b));
+  return d;
+}
+__device__ __forceinline__ void mfma_v_a(f32x4& c, const bf16x8& a, const bf16x8& b) {
+  asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+v"(c) : "v"(a), "a"(b));
+}
+
+template <int REP>
+__global__ __launch_bounds__(256, 1) void dq6_kernel(const u16* __restrict__ qkv, const u16* __restrict__ dout,
+                                                     const float* __restrict__ lse, const float* __restrict__ delta,
+                                                     const int* __restrict__ cu, u16* __restrict__ dqkv, int nq,
+                                                     int nkv, int total, float sl2, float scale, int causal,
+                                                     const float* __restrict__ rcos, const float* __restrict__ rsin) {
+  constexpr int TB = 64 * ROWB;
+  __shared__ __attribute__((aligned(16))) char smem[4 * TB];  // stage s: K image at 2 s TB, V image at (2 s + 1) TB
+  const int kvh = blockIdx.x, b = blockIdx.y, qb = gridDim.z - 1 - blockIdx.z;
+  const int start = cu[b], len = cu[b + 1] - start;
+  SFT_DASSERT(start >= 0 && len >= 0 && start + len <= total);
+  const int q0 = qb * 64;
+  if (q0 >= len) return;
+  const long ld = (long)(nq + 2 * nkv) * D;
+  const long ldo = (long)nq * D;
+  const int tid = threadIdx.x, lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6), g = lane >> 4;
+  const int wfirst = q0 + 16 * w, qrow = wfirst + (lane & 15);
+  const bool qok = qrow < len;
+  const int nkb = (len + 63) / 64;
+  const int nkt = causal ? min(qb + 1, nkb) : nkb;
+  const int r0 = 4 * w + (lane >> 4);  // DMA as fwd6
+  const u16* kvsrc = qkv + (long)start * ld + (nq + kvh) * D + 8 * swz(r0, lane & 15);
+  auto dma = [&](int kt, char* stage) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const u16* src = kvsrc + (long)min(kt * 64 + r0 + 16 * j, len - 1) * ld;
+      glds16(src, stage + (w + 4 * j) * 1024);
+      glds16(src + nkv * D, stage + TB + (w + 4 * j) * 1024);
+    }
+  };
+  dma(0, smem);
+  Offs off;
+  off.init(lane);
+  bf16x8 qf[REP][4], df[REP][4];
+  float lse2[REP], dl[REP];
+#pragma unroll
+  for (int h = 0; h < REP; ++h) {
+    const int hq = kvh * REP + h;
+    const u16* qp = qkv + (long)(start + qrow) * ld + hq * D + 8 * g;
+    const u16* dp = dout + (long)(start + qrow) * ldo + hq * D + 8 * g;
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      qf[h][s] = load_frag_global(qp + 32 * s, qok);
+      df[h][s] = load_frag_global(dp + 32 * s, qok);
+      pin_frag(qf[h][s]);
+      pin_frag(df[h][s]);
+    }
+    lse2[h] = qok ? lse[(long)hq * total + start + qrow] * LOG2E : 0.f;
+    dl[h] = qok ? delta[(long)hq * total + start + qrow] : 0.f;
+  }
+  f32x4 dq[REP][8];
+#pragma unroll
+  for (int h = 0; h < REP; ++h)
+#pragma unroll
+    for (int dt = 0; dt < 8; ++dt) {
+      dq[h][dt] = f32x4{0.f, 0.f, 0.f, 0.f};
+      pin_acc(dq[h][dt]);
+    }
+  __builtin_amdgcn_s_waitcnt(0);
+  __syncthreads();
+  nop_mfma();  // AGPR writes of the Q / dO fragments -> MFMA operand reads
+#pragma nounroll
+  for (int kt = 0; kt < nkt; ++kt) {
+    const int k0 = kt * 64;
+    const char* Ks = smem + (kt & 1) * 2 * TB;
+    const char* Vs = Ks + TB;
+    if (kt + 1 < nkt) dma(kt + 1, smem + ((kt + 1) & 1) * 2 * TB);
+    f32x4 sc[REP][4], dp[REP][4];
+#pragma unroll
+    for (int nt = 0; nt < 4; ++nt)
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {
+        const bf16x8 kf = lds_row(Ks, off.row[s] + nt * 16 * ROWB);
+#pragma unroll
+        for (int h = 0; h < REP; ++h) {
+          if (s == 0) sc[h][nt] = mfma_v0_a(kf, qf[h][s]);
+          else mfma_v_a(sc[h][nt], kf, qf[h][s]);
+        }
+      }
+#pragma unroll
+    for (int nt = 0; nt < 4; ++nt)
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {
+        const bf16x8 vf = lds_row(Vs, off.row[s] + nt * 16 * ROWB);
+#pragma unroll
+        for (int h = 0; h < REP; ++h) {
+          if (s == 0) dp[h][nt] = mfma_v0_a(vf, df[h][s]);
+          else mfma_v_a(dp[h][nt], vf, df[h][s]);
+        }
+      }
+    nop_mfma();
+    const bool need_mask = (k0 + 64 > len) || (causal && k0 + 63 > wfirst);
+    bf16x8 db[REP][2];
+#pragma unroll
+    for (int h = 0; h < REP; ++h) {
+#pragma unroll
+      for (int nt = 0; nt < 4; ++nt)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          float p = exp2f(fmaf(sc[h][nt][i], sl2, -lse2[h]));
+          if (need_mask) {
+            const int key = k0 + 16 * nt + 4 * g + i;
+            if (key >= len || (causal && key > qrow)) p = 0.f;
+          }
+          dp[h][nt][i] = p * (dp[h][nt][i] - dl[h]);
+        }
+      db[h][0] = pack_acc(dp[h][0], dp[h][1]);
+      db[h][1] = pack_acc(dp[h][2], dp[h][3]);
+    }
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+      for (int dt = 0; dt < 8; ++dt) {
+        const bf16x8 kt_f = lds_tr(Ks, off.tr[dt] + ks * 32 * ROWB);
+#pragma unroll
+        for (int h = 0; h < REP; ++h) mfma_acc(dq[h][dt], kt_f, db[h][ks]);
+      }
+    __builtin_amdgcn_s_waitcnt(0);
+    __syncthreads();
+  }
+  nop_mfma();
+  if (!qok) return;
+#pragma unroll
+  for (int h = 0; h < REP; ++h) {
+    u16* qp = dqkv + (long)(start + qrow) * ld + (kvh * REP + h) * D + 4 * g;
+    if (rcos != nullptr) {
+      const long tr = (long)(start + qrow) * (D / 2) + 4 * g;
+      store4_rope_bwd(qp, dq[h], scale, rcos + tr, rsin + tr);
+    } else {
+#pragma unroll
+      for (int dt = 0; dt < 8; ++dt) store4(qp + 16 * dt, dq[h][dt], scale);
+    }
+  }
+}
+
 // dQ from the materialised dS (v4 backward): bwd_dkdv3_kernel already computes dS = P o (dP - delta) for
 // every (query, key) pair of a head; it stores it transposed, dS^T[b][h][key][query] (bf16, lp x lp per head),
 // so dQ^T = K^T dS^T is ONE MFMA product per 64-key tile here — 16 MFMA per wave per tile instead of the 48 of
@@ -1992,6 +2143,12 @@ static long attn_ds_budget() {  // read per call (cheap next to the kernels): te
   return (e && e[0] ? atol(e) : 2048L) * 1024L * 1024L;
 }
 
+// SFTAMD_ATTN_DQ6=1: backward v6 (dK/dV without dS^T stores + the recomputing GQA-stacked dQ kernel)
+static bool attn_dq6() {
+  const char* e = std::getenv("SFTAMD_ATTN_DQ6");
+  return e && e[0] == '1';
+}
+
 // SFTAMD_ATTN_FWD6=1: the GQA-stacked v6 forward where it applies (2 or 4 query heads per kv head)
 static bool attn_fwd6() {
   const char* e = std::getenv("SFTAMD_ATTN_FWD6");
@@ -2213,6 +2370,28 @@ static at::Tensor flash_bwd_impl(const at::Tensor& dout, const at::Tensor& qkv, 
   // SFTAMD_ATTN_DS_MB (default 2048); otherwise dq3 recomputes S / dP.
   const long lp = (max_seqlen + 127) / 128 * 128;
   const long ds_bytes = (long)nseq * nq * lp * lp * 2;
+  const int rep6 = nq / nkv;
+  if (attn_impl() >= 3 && !side && attn_dq6() && (rep6 == 2 || rep6 == 4) && attn_gqa_grouped()) {
+    // v6 backward: GQA-grouped dK/dV without the dS^T stores + the recomputing GQA-stacked dQ (no HBM round trip)
+    const bool rope = rcos != nullptr;
+    SFT_TRACE("attn.dkdv5");
+    SFT_TRACE("attn.dq6");
+    if (rope) SFT_TRACE("attn.bwd_rope_epi");
+    attn::launch_dkdv5((const u16*)qkv.data_ptr(), (const u16*)dout.data_ptr(), lse.data_ptr<float>(),
+                       delta.data_ptr<float>(), cu_c.data_ptr<int>(), (u16*)dqkv.data_ptr(), nq, nkv, total, nseq,
+                       max_seqlen, sl2, (float)scale, causal ? 1 : 0, nullptr, 0, cur_stream(), rcos, rsin);
+    SFT_LAUNCH_CHECK();
+    dim3 g6(nkv, nseq, (max_seqlen + 63) / 64);
+    auto go6 = [&](auto r) {
+      attn::dq6_kernel<decltype(r)::value><<<g6, 256, 0, cur_stream()>>>(
+          (const u16*)qkv.data_ptr(), (const u16*)dout.data_ptr(), lse.data_ptr<float>(), delta.data_ptr<float>(),
+          cu_c.data_ptr<int>(), (u16*)dqkv.data_ptr(), nq, nkv, total, sl2, (float)scale, causal ? 1 : 0, rcos, rsin);
+    };
+    if (rep6 == 4) go6(std::integral_constant<int, 4>()); else go6(std::integral_constant<int, 2>());
+    SFT_LAUNCH_CHECK();
+    rope_done = rope;
+    return dqkv;
+  }
   if (attn_impl() >= 3 && !side && ds_bytes <= attn_ds_budget() && hd == 128) {
     const int rep = nq / nkv;
     auto dst = at::empty({ds_bytes / 2}, qkv.options());

@@ -244,7 +244,7 @@ def test_flash_attention_bwd_gqa_grouped(causal, ds_mb, gqa, monkeypatch):
     _attn_case([130, 64], 12, 2, causal, "1", "3", "", ds_mb)
 
 
-@pytest.mark.parametrize("path", ["default", "gqa0", "ds0", "mha"])
+@pytest.mark.parametrize("path", ["default", "gqa0", "ds0", "mha", "dq6"])
 def test_flash_bwd_rope(path, monkeypatch):
     """flash_bwd_rope == inverse-RoPE(flash_bwd): fused into the dq / dK epilogues on the default path (one bf16
     rounding instead of two: close), the rope kernel after the backward on the others (bitwise)."""
@@ -252,6 +252,7 @@ def test_flash_bwd_rope(path, monkeypatch):
     monkeypatch.setenv("SFTAMD_ATTN_CFG", "")
     monkeypatch.setenv("SFTAMD_ATTN_GQA", "0" if path == "gqa0" else "1")
     monkeypatch.setenv("SFTAMD_ATTN_DS_MB", "0" if path == "ds0" else "")
+    monkeypatch.setenv("SFTAMD_ATTN_DQ6", "1" if path == "dq6" else "0")
     torch.manual_seed(5)
     D = 128
     nq, nkv = (4, 4) if path == "mha" else (8, 2)
@@ -269,7 +270,7 @@ def test_flash_bwd_rope(path, monkeypatch):
     got = _ext.ops().flash_bwd_rope(dout, qkv, out, lse, cu, max(lens), nq, nkv, D, scale, True, cos, sin)
     want = _ext.ops().flash_bwd(dout, qkv, out, lse, cu, max(lens), nq, nkv, D, scale, True)
     _ext.ops().rope_(want, cos, sin, nq, nkv, D, True)
-    if path == "default":
+    if path in ("default", "dq6"):
         assert rel_err(got, want) < 1e-2
         assert torch.equal(got[:, (nq + nkv) * D:], want[:, (nq + nkv) * D:])  # dV untouched by the rotation
     else:
@@ -315,6 +316,18 @@ def test_flash_attention_fwd6_gqa_stacked(causal, monkeypatch):
     _attn_case([512, 511, 7], 16, 4, causal, "1", "3")
     _attn_case([200, 65, 1000], 8, 4, causal, "1", "3")
     _attn_case([512] * 4, 16, 4, causal, "1", "3")
+
+
+@pytest.mark.parametrize("causal", [True, False])
+@pytest.mark.parametrize("fwd6", ["0", "1"])
+def test_flash_attention_bwd6_recompute_dq(causal, fwd6, monkeypatch):
+    """v6 backward: GQA-grouped dK/dV without dS^T stores + the recomputing GQA-stacked dQ kernel (rep 4 / 2), fed by
+    either forward's lse, vs the fp32 reference."""
+    monkeypatch.setenv("SFTAMD_ATTN_DQ6", "1")
+    monkeypatch.setenv("SFTAMD_ATTN_FWD6", fwd6)
+    _attn_case([100, 255, 64, 1, 300, 129], 8, 2, causal, "1", "3")
+    _attn_case([512, 511, 7], 16, 4, causal, "1", "3")
+    _attn_case([200, 65, 1000], 8, 4, causal, "1", "3")
 
 
 @pytest.mark.parametrize("spike", [20.0, 45.0])

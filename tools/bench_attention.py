@@ -41,8 +41,8 @@ CFGS = [("1", ""), ("2", "8,1"), ("3", "8,1"), ("3", "4,1"), ("4", ""), ("3", "8
         ("3", "8,1,ds,perhead")]
 if os.environ.get("ATTN_QUICK"):
     CFGS = [("3", "8,1,serial"), ("3", "8,1,ds,perhead"), ("3", "8,1,ds,nosplit"), ("3", "8,1,ds")]
-if os.environ.get("ATTN_FWD"):  # ",fwd6": the GQA-stacked v6 forward (SFTAMD_ATTN_FWD6=1)
-    CFGS = [("3", "8,1,ds"), ("3", "8,1,ds,fwd6")]
+if os.environ.get("ATTN_FWD"):  # ",fwd6": the GQA-stacked v6 forward (SFTAMD_ATTN_FWD6=1); ",dq6": v6 backward
+    CFGS = [("3", "8,1,ds"), ("3", "8,1,ds,fwd6"), ("3", "8,1,ds,fwd6,dq6")]
 res = {}
 ref = None
 for rnd in range(3):
@@ -50,9 +50,10 @@ for rnd in range(3):
         os.environ["SFTAMD_ATTN_IMPL"] = impl
         os.environ["SFTAMD_ATTN_GQA"] = "0" if cfg.endswith(",perhead") else "1"
         os.environ["SFTAMD_ATTN_GQA_SPLIT"] = "0" if cfg.endswith(",nosplit") else "1"
-        os.environ["SFTAMD_ATTN_FWD6"] = "1" if cfg.endswith(",fwd6") else "0"
+        os.environ["SFTAMD_ATTN_FWD6"] = "1" if ",fwd6" in cfg else "0"
+        os.environ["SFTAMD_ATTN_DQ6"] = "1" if ",dq6" in cfg else "0"
         tag = cfg
-        cfg = cfg.replace(",perhead", "").replace(",nosplit", "").replace(",fwd6", "")
+        cfg = cfg.replace(",perhead", "").replace(",nosplit", "").replace(",fwd6", "").replace(",dq6", "")
         os.environ["SFTAMD_ATTN_CFG"] = cfg.replace(",serial", "").replace(",ds", "")
         os.environ["SFTAMD_ATTN_CONC"] = "0" if cfg.endswith("serial") or cfg.endswith("ds") else "1"
         os.environ["SFTAMD_ATTN_DS_MB"] = "" if cfg.endswith("ds") else "0"

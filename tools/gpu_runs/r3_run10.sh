@@ -4,7 +4,7 @@
 cd $GRAFT_REPO_ROOT
 mkdir -p gpurun_out
 export TMPDIR=/tmp
-timeout -k 10 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_kernels_gpu.py -k "fwd6 or flash_attention_smollm3 or deferred_rescale" \
+timeout -k 10 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_kernels_gpu.py -k "fwd6 or bwd6 or flash_bwd_rope or flash_attention_smollm3 or deferred_rescale" \
   > gpurun_out/r3_10_test.log 2>&1 || { tail -40 gpurun_out/r3_10_test.log; exit 1; }
 tail -2 gpurun_out/r3_10_test.log
 B=16 ATTN_FWD=1 timeout -k 10 200 python -u tools/bench_attention.py > gpurun_out/r3_10_bench.log 2>&1 || { tail -30 gpurun_out/r3_10_bench.log; exit 1; }
