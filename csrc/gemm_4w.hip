@@ -1,0 +1,627 @@
+// 4-wave 256 x 256 MFMA GEMM for the two backward layouts on gfx950 (MI355X):
+//
+//   weight gradient  dW[N, K] (+)= dy[T, N]^T . x[T, K]      A = dy  (TR: reduction T is the ROW index)
+//                                                             B = x   (TR)
+//   input gradient   dX[M, N]   = dy[M, K] . W[K, N]          A = dy  (ROW: reduction K contiguous)
+//                                                             B = W   (TR: reduction K is the row index)
+//
+// C[m][n] = sum_k A'[m][k] B'[n][k]. One workgroup = 4 waves = one wave per SIMD, each wave a 128 x 128 output
+// tile whose 256 fp32 accumulators are pinned in the AGPR file: the MFMAs are inline asm with the accumulator TIED
+// ("+a"), which is what lets hipcc keep 256 accumulators next to double-buffered fragments without renaming them
+// through v_accvgpr_read / write or spilling (the forward kernel's experience, csrc/gemm_tn.hip cfg 12 and
+// profiles/r3_gemm_4wave.md). Why 4 waves: a 128 x 128 wave tile reads 16 fragments per 64 MFMAs instead of the 12
+// per 32 of the 8-wave 128 x 64 tiles of gemm_wgrad.hip / gemm_dgrad.hip — a third fewer LDS bytes per FLOP — and
+// one wave per SIMD leaves the matrix pipe to a single in-order instruction stream (MI355X_MICROARCH.md "Two waves
+// per SIMD", item 1). The 8-wave weight-gradient rings ran at 48-56 % MFMA busy inside the training step
+// (profiles/r2_step_pmc.md).
+//
+// Operand staging (global_load_lds, 16 B per lane, 1 KB per wave instruction; the chunk swizzle is applied to the
+// GLOBAL source address because the DMA writes LDS lane-linearly):
+//   ROW operand: image [256 rows][64 k], 128-B rows, chunk c of row r at slot c ^ ((r >> 1) & 7); a fragment is one
+//                ds_read_b128 per lane (lane group g: k 8g .. 8g + 7 of the 32-deep sub-step);
+//   TR operand:  two images [64 k][128 columns], 256-B rows, chunk c of row r at slot c ^ 2 ((r & 3) | ((r >> 3) & 1)
+//                << 2); a fragment is two ds_read_b64_tr_b16 per lane (rows 8g .. 8g + 3 and 8g + 4 .. 8g + 7 of the
+//                sub-step, i.e. the same k 8g .. 8g + 7 as the ROW side). Lane groups {0, 1} / {2, 3} of a 32-lane
+//                half read 8 rows whose 32-byte column pairs the swizzle spreads over all 64 banks: conflict-free.
+// MFMA v_mfma_f32_16x16x32_bf16 with the B fragment first (transposed C): each lane ends with 4 consecutive output
+// columns of one row per fragment, and v_permlane16_swap pairs two fragments into 8 consecutive columns, so the
+// epilogue writes 16-byte vectors straight from registers (no LDS round trip).
+//
+// Schedule per 64-deep K-tile t (stage X holds t, Y holds t + 1, 64 KB each, 128 KB in all):
+//   sub-step 0: 64 MFMA on F0 = (t, k 0..31) from registers | ds_read F1 = (t, k 32..63) from X
+//   vmcnt(0) lgkmcnt(0): this wave's DMA of tile t + 1 landed, its reads of X retired
+//   sub-step 1: group 0's MFMAs; barrier (every wave's DMA of t + 1 landed, every wave done with X); then
+//               MFMA on F1 | ds_read F0 = (t + 1, k 0..31) from Y | global_load_lds tile t + 2 -> X
+// The reduction length must be a multiple of 128 (an even number of K-tiles; the pair loop alternates X / Y with
+// compile-time stage pointers).
+//
+// Wave quantisation (weight gradients: gate_up 688 tiles = 2.69 rounds of 256 CUs, down_proj 344 = 1.34): the tiles
+// past the last whole round can be split S ways over the reduction (hybrid data-parallel + split-K, pairs of
+// K-tiles per split) into fp32 slabs summed in a fixed order by splitk_fixup_kernel (deterministic).
+#include "common.h"
+#include "splitk_fixup.h"
+
+#include <type_traits>
+
+namespace sftamd {
+namespace g4 {
+
+constexpr int BK = 64;
+constexpr int OPB = 256 * BK * 2;  // one operand's K-tile: 32 KB
+constexpr int STAGE = 2 * OPB;     // 64 KB
+constexpr int ROWB_T = 256;        // TR image row: 128 columns x bf16
+constexpr int IMG_T = BK * ROWB_T;  // 16 KB
+enum { ROW = 0, TR = 1 };
+enum { EPI_STORE = 0, EPI_SWIGLU_BWD = 1 };
+
+__device__ __forceinline__ int xr(int row) { return (row >> 1) & 7; }
+__device__ __forceinline__ int xt(int row) { return 2 * ((row & 3) | (((row >> 3) & 1) << 2)); }
+
+__device__ __forceinline__ void glds16(const u16* src, char* dst) {  // (unused: kept for the LDS-DMA debug variants)
+  __builtin_amdgcn_global_load_lds((const void __attribute__((address_space(1)))*)src,
+                                   (void __attribute__((address_space(3)))*)dst, 16, 0, 0);
+}
+
+// LDS-DMA through a buffer descriptor: the tile's base in the (wave-uniform) descriptor, each lane's byte offset in a
+// VGPR fixed for the whole loop, the piece / K-step offset in an SGPR — no per-piece 64-bit VALU address arithmetic
+// (the global_load_lds form cost a v_lshl_add_u64 per piece), as hipBLASLt's MT256x256x64 loop does.
+typedef __amdgpu_buffer_rsrc_t rsrc_t;
+__device__ __forceinline__ rsrc_t tile_rsrc(const u16* p) {
+  const unsigned long long a = (unsigned long long)p;
+  const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)a), hi = __builtin_amdgcn_readfirstlane((unsigned)(a >> 32));
+  return __builtin_amdgcn_make_buffer_rsrc((void*)(((unsigned long long)hi << 32) | lo), 0, 0xFFFFFFFFu, 0x00020000);
+}
+__device__ __forceinline__ void bldsx4(rsrc_t r, char* dst, unsigned voff, unsigned soff) {
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (__attribute__((address_space(3))) void*)dst, 16, voff, soff, 0, 0);
+}
+
+constexpr unsigned waitcnt_imm(int vm, int lgkm) {  // gfx9: vmcnt[3:0] expcnt[6:4] lgkmcnt[11:8] vmcnt[5:4]<<14
+  return (unsigned)((vm & 15) | (7 << 4) | ((lgkm & 15) << 8) | ((vm >> 4) << 14));
+}
+
+typedef __attribute__((address_space(3))) s16x4 lds_s4;
+typedef __attribute__((ext_vector_type(8))) short s16x8;
+
+__device__ __forceinline__ void mfma(f32x4& c, const bf16x8& b, const bf16x8& a) {
+  asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+a"(c) : "v"(b), "v"(a));
+}
+
+// One operand: the lane's DMA source for the wave's first piece, and its fragment read offsets.
+// `sub` = which 128-wide half of the 256 tile the wave computes on this side (wm for A, wn for B).
+template <int L>
+struct Op;
+
+template <>
+struct Op<ROW> {
+  rsrc_t r;
+  unsigned voff, jst, koff;  // lane offset; bytes between the wave's pieces j, j + 1 (32 rows); K progress
+  int off0, off1;  // fragment 0 of sub-steps 0 / 1 (fragment i is 2048 B further)
+  __device__ __forceinline__ void init(const u16* base, long ld, int r0, long k0, int w, int lane, int sub) {
+    // piece P = w + 4 j (8 rows, 8P + lr); (row >> 1) & 7 = 4 (w & 1) + (lr >> 1) for every piece of the wave
+    const int lr = lane >> 3, ch = (lane & 7) ^ (4 * (w & 1) + (lr >> 1));
+    r = tile_rsrc(base + (long)r0 * ld + k0);
+    voff = (unsigned)(((8 * w + lr) * ld + 8 * ch) * 2);
+    jst = (unsigned)(64 * ld);
+    koff = 0;
+    const int g = lane >> 4, ii = lane & 15;
+    const int r = 128 * sub + ii;
+    off0 = r * 128 + 16 * (g ^ xr(r));
+    off1 = r * 128 + 16 * ((4 + g) ^ xr(r));
+  }
+  __device__ __forceinline__ void advance() { koff += 2 * BK; }
+  __device__ __forceinline__ void piece(char* opb, int w, int j) const {
+    bldsx4(r, opb + (w + 4 * j) * 1024, voff, koff + j * jst);
+  }
+  __device__ __forceinline__ bf16x8 frag(const char* opb, int s, int i) const {
+    return *(const bf16x8*)(opb + (s ? off1 : off0) + 2048 * i);
+  }
+};
+
+template <>
+struct Op<TR> {
+  rsrc_t r;
+  unsigned voff, jst, kst, koff;  // lane offset; bytes per 16 rows; per K-tile (64 rows); K progress
+  int ob, x2;  // fragment i of sub-step s at ob + 32 (i ^ x2) + s * 32 rows
+  __device__ __forceinline__ void init(const u16* base, long ld, int c0, long k0, int w, int lane, int sub) {
+    // piece (image j >> 2, q = w + 4 (j & 3)): rows 4q + lr4; xt(row) = 2 (lr4 | ((w >> 1) & 1) << 2) for all
+    const int lr4 = lane >> 4, row = 4 * w + lr4, ch = (lane & 15) ^ xt(row);
+    r = tile_rsrc(base + k0 * ld + c0);
+    voff = (unsigned)((row * ld + 8 * ch) * 2);
+    jst = (unsigned)(32 * ld);
+    kst = (unsigned)(2 * BK * ld);
+    koff = 0;
+    const int g = lane >> 4, ii = lane & 15, qq = ii >> 2, pp = ii & 3;
+    x2 = qq | ((g & 1) << 2);  // xt(8g + qq) / 2
+    ob = sub * IMG_T + (8 * g + qq) * ROWB_T + 8 * pp;
+  }
+  __device__ __forceinline__ void advance() { koff += kst; }
+  __device__ __forceinline__ void piece(char* opb, int w, int j) const {
+    bldsx4(r, opb + (j >> 2) * IMG_T + (w + 4 * (j & 3)) * 1024, voff, koff + (j & 3) * jst + 256 * (j >> 2));
+  }
+  __device__ __forceinline__ bf16x8 frag(const char* opb, int s, int i) const {
+    const char* q = opb + ob + 32 * (i ^ x2) + s * 32 * ROWB_T;
+    s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4*)q);
+    s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4*)(q + 4 * ROWB_T));
+    s16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+    return __builtin_bit_cast(bf16x8, v);
+  }
+};
+
+struct Epi {
+  u16* C;          // output rows (STORE: [M, ldc]; SWIGLU_BWD: dgu [M, ldc = 2 I] with the up half I columns right)
+  const u16* gu;   // SWIGLU_BWD: gate | up, same row stride as C
+  float* P;        // split slabs (+ parked whole-tile norm partials) or the norm slots (no split)
+  long ldc;
+  int I;           // SWIGLU_BWD: column offset of the up half
+  int flags;       // bit 0: accumulate into C (beta = 1); bit 1: gradient-norm partials
+};
+
+// One sub-step: 8 MFMA groups (A fragment row i x the 8 B fragments); READ: the next sub-step's fragments from
+// `src` (sub-step index rs); NP DMA pieces of the next K-tile into `dst`, 2 per group; BAR: the K-tile barrier after
+// group 0's MFMAs (which only need registers), ahead of the group's reads and DMA.
+template <int LA, int LB, bool READ, int NP, bool BAR>
+__device__ __forceinline__ void sub(f32x4 (&acc)[8][8], const bf16x8 (&fa)[8], const bf16x8 (&fb)[8], bf16x8 (&ra)[8],
+                                    bf16x8 (&rb)[8], const char* __restrict__ src, int rs, Op<LA>& oa, Op<LB>& ob, char* __restrict__ dst, int w) {
+  static_assert(NP == 0 || NP == 16, "a whole K-tile per sub-step");
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) mfma(acc[i][j], fb[j], fa[i]);
+    if (BAR && i == 0) __builtin_amdgcn_s_barrier();
+    if (READ) {
+      ra[i] = oa.frag(src, rs, i);
+      rb[i] = ob.frag(src + OPB, rs, i);
+    }
+    if (NP) {  // pieces 2i, 2i + 1: A pieces 0..7 in groups 0..3, B pieces in groups 4..7
+      const int q = 2 * i;
+      if (q < 8) {
+        oa.piece(dst, w, q);
+        oa.piece(dst, w, q + 1);
+      } else {
+        ob.piece(dst + OPB, w, q - 8);
+        ob.piece(dst + OPB, w, q - 7);
+      }
+    }
+  }
+}
+
+__device__ __forceinline__ float fbits(unsigned u) { return __uint_as_float(u); }
+
+// TRC accumulators -> 8 consecutive fp32 columns per (fragment row i, fragment pair p) per lane: lane (g, ii) holds
+// row 16 i + ii, columns 32 p + 16 (g & 1) + 8 (g >> 1) + 0..7 of the wave tile.
+__device__ __forceinline__ void gather8(const f32x4 (&acc)[8][8], int i, int p, float (&v)[8]) {
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(acc[i][2 * p][e]), __float_as_uint(acc[i][2 * p + 1][e]),
+                                              false, false);
+    v[e] = fbits(r[0]);
+    v[4 + e] = fbits(r[1]);
+  }
+}
+
+template <int EPI>
+__device__ __forceinline__ void store_tile(const f32x4 (&acc)[8][8], const Epi& ea, int row0, int col0, int lane,
+                                           float* nrm) {
+  const int g = lane >> 4, ii = lane & 15;
+  const int cofs = col0 + 16 * (g & 1) + 8 * (g >> 1);
+  float ss = 0.f;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const long row = row0 + 16 * i + ii;
+#pragma unroll
+    for (int p = 0; p < 4; ++p) {
+      float v[8];
+      gather8(acc, i, p, v);
+      u16* out = ea.C + row * ea.ldc + cofs + 32 * p;
+      if constexpr (EPI == EPI_STORE) {
+        if (ea.flags & 1) {
+          float o[8];
+          unpack8(*(const uint4*)out, o);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) v[e] += o[e];
+        }
+        if (nrm != nullptr) {
+#pragma unroll
+          for (int e = 0; e < 8; ++e) ss += v[e] * v[e];
+        }
+        *(uint4*)out = pack8(v);
+      } else {  // SWIGLU_BWD: v = dact (fp32, never stored)
+        const u16* gp = ea.gu + row * ea.ldc + cofs + 32 * p;
+        float gt[8], up[8], dg[8], du[8];
+        unpack8(*(const uint4*)gp, gt);
+        unpack8(*(const uint4*)(gp + ea.I), up);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const float s = 1.f / (1.f + __expf(-gt[e]));
+          du[e] = v[e] * gt[e] * s;
+          dg[e] = v[e] * up[e] * s * (1.f + gt[e] * (1.f - s));
+        }
+        *(uint4*)out = pack8(dg);
+        *(uint4*)(out + ea.I) = pack8(du);
+      }
+    }
+  }
+  if (nrm != nullptr) {
+    ss = wave_sum(ss);
+    if (lane == 0) *nrm = ss;
+  }
+}
+
+// split piece: fp32 wave tile -> the piece's tile-local slab P[256][256]
+__device__ __forceinline__ void store_partial(const f32x4 (&acc)[8][8], float* __restrict__ P, int wm, int wn, int lane) {
+  const int g = lane >> 4, ii = lane & 15;
+  const int c = 128 * wn + 16 * (g & 1) + 8 * (g >> 1);
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    float* row = P + (long)(128 * wm + 16 * i + ii) * 256 + c;
+#pragma unroll
+    for (int p = 0; p < 4; ++p) {
+      float v[8];
+      gather8(acc, i, p, v);
+      *(float4*)(row + 32 * p) = make_float4(v[0], v[1], v[2], v[3]);
+      *(float4*)(row + 32 * p + 4) = make_float4(v[4], v[5], v[6], v[7]);
+    }
+  }
+}
+
+// One K-tile pair (t on X, t + 1 on Y); D: the DMA of tiles t + 2 (-> X) and t + 3 (-> Y) rides in the two
+// second sub-steps (not in the last pair).
+template <int LA, int LB, bool D>
+__device__ __forceinline__ void pair_step(char* __restrict__ X, char* __restrict__ Y, Op<LA>& oa, Op<LB>& ob, int w,
+                                          f32x4 (&acc)[8][8], bf16x8 (&a0)[8], bf16x8 (&b0)[8], bf16x8 (&a1)[8],
+                                          bf16x8 (&b1)[8]) {
+  __builtin_amdgcn_s_waitcnt(waitcnt_imm(63, 0));
+  sub<LA, LB, true, 0, false>(acc, a0, b0, a1, b1, X, 1, oa, ob, X, w);
+  __builtin_amdgcn_s_waitcnt(waitcnt_imm(0, 0));
+  sub<LA, LB, true, D ? 16 : 0, true>(acc, a1, b1, a0, b0, Y, 0, oa, ob, X, w);
+  if (D) {
+    oa.advance();
+    ob.advance();
+  }
+  __builtin_amdgcn_s_waitcnt(waitcnt_imm(63, 0));
+  sub<LA, LB, true, 0, false>(acc, a0, b0, a1, b1, Y, 1, oa, ob, Y, w);
+  __builtin_amdgcn_s_waitcnt(waitcnt_imm(0, 0));
+  if constexpr (D) {
+    sub<LA, LB, true, 16, true>(acc, a1, b1, a0, b0, X, 0, oa, ob, Y, w);
+    oa.advance();
+    ob.advance();
+  } else {
+    sub<LA, LB, false, 0, false>(acc, a1, b1, a0, b0, X, 0, oa, ob, Y, w);
+  }
+}
+
+// The stage pointers are separate __restrict__ parameters: once inlined, every ds_read and every LDS-DMA write
+// carries the alias scope of its stage, so the compiler's waitcnt pass does not drain vmcnt before a fragment read of
+// the other stage (a lambda capturing the pointers lost that: a vmcnt(0) after every DMA group).
+template <int LA, int LB>
+__device__ __forceinline__ void mainloop(char* __restrict__ X, char* __restrict__ Y, int np, Op<LA>& oa, Op<LB>& ob,
+                                         int w, f32x4 (&acc)[8][8]) {
+  bf16x8 a0[8], b0[8], a1[8], b1[8];
+  // prologue: K-tiles 0 -> X, 1 -> Y; wait for X; F0 of tile 0
+#pragma unroll
+  for (int j = 0; j < 8; ++j) oa.piece(X, w, j);
+#pragma unroll
+  for (int j = 0; j < 8; ++j) ob.piece(X + OPB, w, j);
+  oa.advance();
+  ob.advance();
+#pragma unroll
+  for (int j = 0; j < 8; ++j) oa.piece(Y, w, j);
+#pragma unroll
+  for (int j = 0; j < 8; ++j) ob.piece(Y + OPB, w, j);
+  oa.advance();
+  ob.advance();
+  __builtin_amdgcn_s_waitcnt(waitcnt_imm(16, 15));
+  __builtin_amdgcn_s_barrier();
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    a0[i] = oa.frag(X, 0, i);
+    b0[i] = ob.frag(X + OPB, 0, i);
+  }
+  for (int t = 0; t < np - 1; ++t) pair_step<LA, LB, true>(X, Y, oa, ob, w, acc, a0, b0, a1, b1);
+  pair_step<LA, LB, false>(X, Y, oa, ob, w, acc, a0, b0, a1, b1);
+}
+
+
+// ============================================================================================
+// Ring variant (cfg 13): 32-deep K-steps in NS = 4 slots of 32 KB, three steps in flight ahead of the one being
+// computed (the pair loop above keeps one 64-deep K-tile ahead, 1.5 sub-steps to land: load-latency bound on the
+// long-T weight gradients, as the 8-wave two-stage loop of gemm_wgrad.hip was). Per step u (slot u % 4):
+//   vmcnt: this wave's pieces of step u + 1 landed; lgkmcnt(0): F(u) (read during step u - 1) in registers
+//   MFMA group 0 | barrier (every wave's step u + 1 landed, every wave done reading slot u % 4)
+//   MFMA on F(u) | ds_read F(u + 1) from slot (u + 1) % 4 | global_load_lds step u + 4 -> slot u % 4 (1 piece/group)
+// ROW images: [256 rows][32 k], 64-B rows, chunk c at slot c ^ S((row >> 2) & 3), S = {0, 2, 3, 1} (the 16-lane
+// groups of ds_read_b128 conflict-free, csrc/gemm_tn.hip); TR images: [32 k][128 columns] as above.
+// ============================================================================================
+constexpr int BK32 = 32;
+constexpr int OPB32 = 256 * BK32 * 2;  // 16 KB
+constexpr int SLOT32 = 2 * OPB32;       // 32 KB
+constexpr int IMG32 = BK32 * ROWB_T;    // 8 KB
+
+__device__ __forceinline__ int sel4(int q) { return (0x78 >> (2 * q)) & 3; }
+
+template <int L>
+struct Op32;
+
+template <>
+struct Op32<ROW> {
+  rsrc_t r;
+  unsigned voff, jst, koff;  // lane offset; bytes per 64 rows; K progress
+  int off;   // fragment 0 (fragment i is 1024 B further)
+  __device__ __forceinline__ void init(const u16* base, long ld, int r0, long k0, int w, int lane, int sub) {
+    // piece P = w + 4 j: 16 rows 16 P + lr (lr = lane >> 2), slot lane & 3; (row >> 2) & 3 = lr >> 2 for all pieces
+    const int lr = lane >> 2, ch = (lane & 3) ^ sel4(lr >> 2);
+    r = tile_rsrc(base + (long)r0 * ld + k0);
+    voff = (unsigned)(((16 * w + lr) * ld + 8 * ch) * 2);
+    jst = (unsigned)(128 * ld);
+    koff = 0;
+    const int g = lane >> 4, ii = lane & 15;
+    off = (128 * sub + ii) * 64 + 16 * (g ^ sel4(ii >> 2));
+  }
+  __device__ __forceinline__ void advance() { koff += 2 * BK32; }
+  __device__ __forceinline__ void piece(char* opb, int w, int j) const {
+    bldsx4(r, opb + (w + 4 * j) * 1024, voff, koff + j * jst);
+  }
+  __device__ __forceinline__ bf16x8 frag(const char* opb, int i) const { return *(const bf16x8*)(opb + off + 1024 * i); }
+};
+
+template <>
+struct Op32<TR> {
+  rsrc_t r;
+  unsigned voff, jst, kst, koff;  // lane offset; bytes per 16 rows; per step (32 rows); K progress
+  int ob, x2;
+  __device__ __forceinline__ void init(const u16* base, long ld, int c0, long k0, int w, int lane, int sub) {
+    // piece (image j >> 1, q = w + 4 (j & 1)): rows 4q + lr4; xt(row) = 2 (lr4 | ((w >> 1) & 1) << 2) for all
+    const int lr4 = lane >> 4, row = 4 * w + lr4, ch = (lane & 15) ^ xt(row);
+    r = tile_rsrc(base + k0 * ld + c0);
+    voff = (unsigned)((row * ld + 8 * ch) * 2);
+    jst = (unsigned)(32 * ld);
+    kst = (unsigned)(2 * BK32 * ld);
+    koff = 0;
+    const int g = lane >> 4, ii = lane & 15, qq = ii >> 2, pp = ii & 3;
+    x2 = qq | ((g & 1) << 2);
+    ob = sub * IMG32 + (8 * g + qq) * ROWB_T + 8 * pp;
+  }
+  __device__ __forceinline__ void advance() { koff += kst; }
+  __device__ __forceinline__ void piece(char* opb, int w, int j) const {
+    bldsx4(r, opb + (j >> 1) * IMG32 + (w + 4 * (j & 1)) * 1024, voff, koff + (j & 1) * jst + 256 * (j >> 1));
+  }
+  __device__ __forceinline__ bf16x8 frag(const char* opb, int i) const {
+    const char* q = opb + ob + 32 * (i ^ x2);
+    s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4*)q);
+    s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4*)(q + 4 * ROWB_T));
+    s16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+    return __builtin_bit_cast(bf16x8, v);
+  }
+};
+
+// one 32-deep step on F(u) = (fa, fb); READ: F(u + 1) from `nxt` into (ra, rb); DMA: step u + 4 into `cur`
+template <int LA, int LB, bool READ, bool DMA, int VM, bool BAR>
+__device__ __forceinline__ void rstep(f32x4 (&acc)[8][8], const bf16x8 (&fa)[8], const bf16x8 (&fb)[8],
+                                      bf16x8 (&ra)[8], bf16x8 (&rb)[8], const char* __restrict__ nxt,
+                                      char* __restrict__ cur, Op32<LA>& oa, Op32<LB>& ob, int w) {
+  __builtin_amdgcn_s_waitcnt(waitcnt_imm(VM, 0));
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) mfma(acc[i][j], fb[j], fa[i]);
+    if (BAR && i == 0) __builtin_amdgcn_s_barrier();
+    if (READ) {
+      ra[i] = oa.frag(nxt, i);
+      rb[i] = ob.frag(nxt + OPB32, i);
+    }
+    if (DMA) {
+      if (i < 4) oa.piece(cur, w, i);
+      else ob.piece(cur + OPB32, w, i - 4);
+    }
+  }
+  if (DMA) {
+    oa.advance();
+    ob.advance();
+  }
+}
+
+// four steps (u = 4 b .. 4 b + 3 on slots S0..S3); LAST: no DMA (steps past the end), counted waits shrink
+template <int LA, int LB, bool LAST>
+__device__ __forceinline__ void rbody(char* __restrict__ S0, char* __restrict__ S1, char* __restrict__ S2,
+                                      char* __restrict__ S3, Op32<LA>& oa, Op32<LB>& ob, int w, f32x4 (&acc)[8][8],
+                                      bf16x8 (&a0)[8], bf16x8 (&b0)[8], bf16x8 (&a1)[8], bf16x8 (&b1)[8]) {
+  constexpr bool D = !LAST;
+  rstep<LA, LB, true, D, 16, true>(acc, a0, b0, a1, b1, S1, S0, oa, ob, w);
+  rstep<LA, LB, true, D, LAST ? 8 : 16, true>(acc, a1, b1, a0, b0, S2, S1, oa, ob, w);
+  rstep<LA, LB, true, D, LAST ? 0 : 16, true>(acc, a0, b0, a1, b1, S3, S2, oa, ob, w);
+  rstep<LA, LB, D, D, LAST ? 0 : 16, D>(acc, a1, b1, a0, b0, S0, S3, oa, ob, w);
+}
+
+template <int LA, int LB>
+__device__ __forceinline__ void mainloop_ring(char* __restrict__ S0, char* __restrict__ S1, char* __restrict__ S2,
+                                              char* __restrict__ S3, int nb, Op32<LA>& oa, Op32<LB>& ob, int w,
+                                              f32x4 (&acc)[8][8]) {
+  bf16x8 a0[8], b0[8], a1[8], b1[8];
+  auto issue = [&](char* __restrict__ s) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) oa.piece(s, w, j);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) ob.piece(s + OPB32, w, j);
+    oa.advance();
+    ob.advance();
+  };
+  issue(S0);
+  issue(S1);
+  issue(S2);
+  issue(S3);
+  __builtin_amdgcn_s_waitcnt(waitcnt_imm(24, 15));  // step 0 landed (steps 1..3 may fly)
+  __builtin_amdgcn_s_barrier();
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    a0[i] = oa.frag(S0, i);
+    b0[i] = ob.frag(S0 + OPB32, i);
+  }
+  for (int b = 0; b < nb - 1; ++b) rbody<LA, LB, false>(S0, S1, S2, S3, oa, ob, w, acc, a0, b0, a1, b1);
+  rbody<LA, LB, true>(S0, S1, S2, S3, oa, ob, w, acc, a0, b0, a1, b1);
+}
+
+template <int LA, int LB, int EPI, bool RING>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1)))
+g4_kernel(const u16* __restrict__ A, const u16* __restrict__ B, long lda, long ldb, int kred, int nbm, int nbn,
+          int group, int ndp, int splits, Epi ea) {
+  __shared__ __attribute__((aligned(16))) char smem[2 * STAGE];
+  // XCD-aware bijective remap: consecutive ids run on one XCD (shared L2 for the GROUP-blocked tile order)
+  const int nwg = gridDim.x, orig = blockIdx.x;
+  const int xcd = orig & 7, q8 = nwg >> 3, r8 = nwg & 7;
+  const int wgid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (orig >> 3);
+  const int npair_all = kred / (2 * BK);
+  int tile = wgid, sk = 0, p0 = 0, p1 = npair_all;
+  if (wgid >= ndp) {  // split piece sk of tile ndp + (wgid - ndp) / splits: K-tile pairs [p0, p1)
+    const int j = wgid - ndp;
+    sk = j % splits;
+    tile = ndp + j / splits;
+    p0 = (int)((long)sk * npair_all / splits);
+    p1 = (int)((long)(sk + 1) * npair_all / splits);
+  }
+  int m0, n0;
+  {
+    const int per_group = group * nbn;
+    const int grp = tile / per_group, first = grp * group;
+    const int gsz = min(nbm - first, group);
+    const int in = tile - grp * per_group;
+    m0 = (first + in % gsz) * 256;
+    n0 = (in / gsz) * 256;
+  }
+  const int tid = threadIdx.x, lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = w >> 1, wn = w & 1;
+  const long k0 = (long)p0 * 2 * BK;
+
+  f32x4 acc[8][8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  if constexpr (RING) {
+    Op32<LA> oa;
+    Op32<LB> ob;
+    oa.init(A, lda, m0, k0, w, lane, wm);
+    ob.init(B, ldb, n0, k0, w, lane, wn);
+    mainloop_ring<LA, LB>(smem, smem + SLOT32, smem + 2 * SLOT32, smem + 3 * SLOT32, p1 - p0, oa, ob, w, acc);
+  } else {
+    Op<LA> oa;
+    Op<LB> ob;
+    oa.init(A, lda, m0, k0, w, lane, wm);
+    ob.init(B, ldb, n0, k0, w, lane, wn);
+    mainloop<LA, LB>(smem, smem + STAGE, p1 - p0, oa, ob, w, acc);
+  }
+  // the epilogue's accumulator reads follow the last MFMAs: 20 wait states + a fence against hoisting
+  asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 3" ::: "memory");
+  __builtin_amdgcn_sched_barrier(0);
+  if (wgid >= ndp) {
+    store_partial(acc, ea.P + ((long)(tile - ndp) * splits + sk) * 65536, wm, wn, lane);
+    return;
+  }
+  float* nrm = nullptr;
+  if (EPI == EPI_STORE && (ea.flags & 2))
+    nrm = (splits <= 1 ? ea.P : ea.P + (long)(gridDim.x - ndp) * 65536) + tile * 8 + w;
+  store_tile<EPI>(acc, ea, m0 + 128 * wm, n0 + 128 * wn, lane, nrm);
+}
+
+static int group_m() {
+  static const int v = [] {
+    const char* e = std::getenv("SFTAMD_G4_GROUP");
+    return e && e[0] ? std::max(1, atoi(e)) : 8;
+  }();
+  return v;
+}
+
+template <int LA, int LB, int EPI, bool RING>
+static void launch(const u16* A, long lda, const u16* B, long ldb, int M, int N, int kred, int ndp, int splits,
+                   const Epi& ea) {
+  const int nbm = M / 256, nbn = N / 256, tiles = nbm * nbn;
+  const int grid = ndp + (tiles - ndp) * splits;
+  g4_kernel<LA, LB, EPI, RING><<<grid, 256, 0, cur_stream()>>>(A, B, lda, ldb, kred, nbm, nbn, std::min(group_m(), nbm), ndp,
+                                                          splits, ea);
+  SFT_LAUNCH_CHECK();
+}
+
+}  // namespace g4
+
+// Weight gradient out[N, K] (+)= dy[T, N]^T x[T, K] on the 4-wave kernel. splits > 1: the tiles past the last whole
+// round of 256 workgroups (hybrid) or all tiles are split over the token axis into fp32 slabs + ordered fixup.
+// nrm: gradient-norm slots (8 per whole tile, waves 0..3 written; one per fixup block of a split tile).
+void g4_wgrad(const at::Tensor& dy, const at::Tensor& x, at::Tensor& out, bool accumulate, int splits, bool hybrid,
+              float* nrm, long nrm_cap, bool ring) {
+  const int T = dy.size(0), N = dy.size(1), K = x.size(1);
+  SFT_CHECK(N % 256 == 0 && K % 256 == 0 && T % 128 == 0 && T > 0, "wgrad 4-wave: N, K % 256, T % 128");
+  SFT_CHECK((uintptr_t)dy.data_ptr() % 16 == 0 && (uintptr_t)x.data_ptr() % 16 == 0 &&
+                (uintptr_t)out.data_ptr() % 16 == 0, "wgrad 4-wave: 16-byte aligned operands");
+  const int tiles = (N / 256) * (K / 256);
+  if (splits < 1) splits = 1;
+  splits = std::min(splits, T / 128);
+  const int ndp = splits <= 1 ? tiles : (hybrid ? tiles / 256 * 256 : 0);
+  const int nsk = tiles - ndp;
+  const long slots = (long)ndp * 8 + (long)nsk * 32;
+  SFT_CHECK(nrm == nullptr || slots <= nrm_cap, "wgrad_gemm: norm slot buffer too small");
+  at::Tensor part;
+  if (nsk > 0)
+    part = at::empty({(long)nsk * splits * 65536 + (nrm != nullptr ? (long)ndp * 8 : 0)}, dy.options().dtype(at::kFloat));
+  g4::Epi ea{};
+  ea.C = (u16*)out.data_ptr();
+  ea.ldc = K;
+  ea.P = nsk > 0 ? part.data_ptr<float>() : nrm;
+  ea.flags = (accumulate ? 1 : 0) | (nrm != nullptr ? 2 : 0);
+  if (ring)
+    g4::launch<g4::TR, g4::TR, g4::EPI_STORE, true>((const u16*)dy.data_ptr(), N, (const u16*)x.data_ptr(), K, N, K, T,
+                                                    ndp, nsk > 0 ? splits : 1, ea);
+  else
+    g4::launch<g4::TR, g4::TR, g4::EPI_STORE, false>((const u16*)dy.data_ptr(), N, (const u16*)x.data_ptr(), K, N, K, T,
+                                                     ndp, nsk > 0 ? splits : 1, ea);
+  if (nsk > 0) {
+    const long n8 = (long)nsk * 65536 / 8;
+    splitk_fixup_kernel<256, 256><<<(unsigned)((n8 + 255) / 256), 256, 0, cur_stream()>>>(
+        part.data_ptr<float>(), (u16*)out.data_ptr(), ndp, nsk, splits, K / 256, K, accumulate ? 1 : 0, nrm, N / 256,
+        std::min(g4::group_m(), N / 256));
+    SFT_LAUNCH_CHECK();
+  }
+}
+
+// Input gradient dX[M, N] = dy[M, K] . w[K, N] (w may be a column slice: row stride w.stride(0)); gu != nullptr:
+// SwiGLU backward epilogue, out = dgu with row stride ldo = 2 I (gate at column n, up at n + I).
+void g4_dgrad(const at::Tensor& dy, const at::Tensor& w, u16* out, long ldo, const u16* gu, int I, bool ring) {
+  const int M = dy.size(0), K = dy.size(1), N = w.size(1);
+  SFT_CHECK(M % 256 == 0 && N % 256 == 0 && K % 128 == 0 && K > 0, "dgrad 4-wave: M, N % 256, K % 128");
+  g4::Epi ea{};
+  ea.C = out;
+  ea.ldc = ldo;
+  ea.gu = gu;
+  ea.I = I;
+  const int tiles = (M / 256) * (N / 256);
+  auto go = [&](auto epi, auto rg) {
+    g4::launch<g4::ROW, g4::TR, decltype(epi)::value, decltype(rg)::value>(
+        (const u16*)dy.data_ptr(), dy.stride(0), (const u16*)w.data_ptr(), w.stride(0), M, N, K, tiles, 1, ea);
+  };
+  using SW = std::integral_constant<int, g4::EPI_SWIGLU_BWD>;
+  using ST = std::integral_constant<int, g4::EPI_STORE>;
+  if (gu != nullptr) {
+    if (ring) go(SW(), std::true_type());
+    else go(SW(), std::false_type());
+  } else {
+    if (ring) go(ST(), std::true_type());
+    else go(ST(), std::false_type());
+  }
+}
+
+// Forward layout C[M, N] = a[M, K] . w[N, K]^T (both operands K-contiguous: ROW / ROW) on the same 4-wave kernel,
+// plain bf16 store (gemm_tn cfg 60 = ring, 61 = pair loop).
+void g4_tn(const at::Tensor& a, const at::Tensor& w, at::Tensor& c, bool ring) {
+  const int M = a.size(0), K = a.size(1), N = w.size(0);
+  SFT_CHECK(M % 256 == 0 && N % 256 == 0 && K % 128 == 0 && K > 0, "gemm_tn 4-wave: M, N % 256, K % 128");
+  g4::Epi ea{};
+  ea.C = (u16*)c.data_ptr();
+  ea.ldc = c.stride(0);
+  const int tiles = (M / 256) * (N / 256);
+  if (ring)
+    g4::launch<g4::ROW, g4::ROW, g4::EPI_STORE, true>((const u16*)a.data_ptr(), a.stride(0), (const u16*)w.data_ptr(),
+                                                      w.stride(0), M, N, K, tiles, 1, ea);
+  else
+    g4::launch<g4::ROW, g4::ROW, g4::EPI_STORE, false>((const u16*)a.data_ptr(), a.stride(0), (const u16*)w.data_ptr(),
+                                                       w.stride(0), M, N, K, tiles, 1, ea);
+}
+
+}  // namespace sftamd

@@ -1465,6 +1465,8 @@ static void check_tn(const at::Tensor& a, const at::Tensor& w) {
   SFT_CHECK(a.size(0) % 256 == 0 && a.size(1) % tn::BK == 0 && a.size(1) > 0, "gemm_tn: M % 256, K % 32");
 }
 
+void g4_tn(const at::Tensor& a, const at::Tensor& w, at::Tensor& c, bool ring);
+
 // cfg: 0 = 256x256 BK32 ring (NS 5), 1 = 256x128 BK32 ring (NS 6), 2 = 256x256 BK64 (NS 2; the fastest on the
 // SmolLM3 shapes, tools/bench_gemm_tn.py), 3 = BK64 early-release ring, 4 = BK64 with a pinned MFMA/DS/DMA
 // interleave (3 and 4 measured slower; kept for the microbench), 5 = BK64 transposed-C epilogue, 6 / 7 = BK64
@@ -1497,6 +1499,8 @@ at::Tensor gemm_tn(const at::Tensor& a, const at::Tensor& w, int64_t cfg) {
     else tn::launch3<tn::EPI_PLAIN, true, 2>(a, w, N, ea);
   } else if (cfg == 12) {  // 4 waves of 128 x 128 (one wave per SIMD, accumulators pinned in AGPRs), VAR 4
     tn::launch4<tn::EPI_PLAIN, 0, 4>(a, w, N, ea);
+  } else if (cfg == 60 || cfg == 61) {  // csrc/gemm_4w.hip: 4-slot ring of 32-deep steps (60) / 64-deep pairs (61)
+    g4_tn(a, w, c, cfg == 60);
   } else if (cfg == 50) {  // persistent 4-wave (register epilogue, next tile's loads under this tile's end)
     tn::launch5<tn::EPI_PLAIN>(a, w, N, ea);
   } else if (cfg >= 13 && cfg <= 44) {  // cfg 12 schedule variants (tn4_kernel VAR = cfg - 12)

@@ -23,6 +23,7 @@
 //   * epilogue through LDS (fp32, padded rows) so the beta-accumulate read-modify-write of the
 //     bf16 gradient is 16-byte vectorised.
 #include "common.h"
+#include "splitk_fixup.h"
 
 #include <type_traits>
 
@@ -463,54 +464,6 @@ __device__ __forceinline__ void epilogue_partial(f32x4 (&acc)[G::FM][G::FN], flo
         P[(wm * G::TM + 16 * i + 4 * g + e) * BN + wk * G::TN + 16 * j + ii] = acc[i][j][e];
 }
 
-// Split tiles t = tile0 .. tile0 + ntiles - 1: C[tile] = bf16(sum_s P[t][s] (+ C when accumulating)),
-// 8 elements per thread, slabs summed in order s = 0..S-1.
-template <int BM, int BN>
-__global__ void __launch_bounds__(256) splitk_fixup_kernel(const float* __restrict__ P, u16* __restrict__ C, int tile0,
-                                                           int ntiles, int splits, int nbk, int K, int accumulate,
-                                                           float* __restrict__ nrm) {
-  constexpr int E8 = BM * BN / 8;
-  if (nrm != nullptr && blockIdx.x == 0) {  // the whole tiles' partials, parked past the slabs by ring_kernel
-    const float* src = P + (long)ntiles * splits * BM * BN;
-    for (int i = threadIdx.x; i < tile0 * 8; i += 256) nrm[i] = src[i];
-  }
-  static_assert((BM * BN / 8) % 256 == 0, "fixup blocks cover whole tiles");
-  const long idx = (long)blockIdx.x * 256 + threadIdx.x;
-  if (idx >= (long)ntiles * E8) return;  // never taken: the grid covers whole tiles
-  const int t = (int)(idx / E8), e = (int)(idx - (long)t * E8) * 8;
-  const int row = e / BN, col = e - row * BN;
-  const float* q = P + (long)t * splits * BM * BN + e;
-  float v[8];
-  *(float4*)&v[0] = *(const float4*)q;
-  *(float4*)&v[4] = *(const float4*)(q + 4);
-  for (int s = 1; s < splits; ++s) {
-    const float4 a = *(const float4*)(q + (long)s * BM * BN), b = *(const float4*)(q + (long)s * BM * BN + 4);
-    v[0] += a.x; v[1] += a.y; v[2] += a.z; v[3] += a.w;
-    v[4] += b.x; v[5] += b.y; v[6] += b.z; v[7] += b.w;
-  }
-  const int tile = tile0 + t, bn = tile / nbk, bk = tile - bn * nbk;
-  u16* out = C + (long)(bn * BM + row) * K + bk * BN + col;
-  if (accumulate) {
-    float o[8];
-    unpack8(*(const uint4*)out, o);
-#pragma unroll
-    for (int i = 0; i < 8; ++i) v[i] += o[i];
-  }
-  const uint4 pk = pack8(v);
-  *(uint4*)out = pk;
-  if (nrm != nullptr) {  // per-block slot (blocks never straddle a tile: E8 % 256 == 0)
-    float r[8], ss = 0.f;
-    unpack8(pk, r);
-#pragma unroll
-    for (int i = 0; i < 8; ++i) ss += r[i] * r[i];
-    ss = wave_sum(ss);
-    __shared__ float red[4];
-    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = ss;
-    __syncthreads();
-    if (threadIdx.x == 0) nrm[(long)tile0 * 8 + blockIdx.x] = red[0] + red[1] + red[2] + red[3];
-  }
-}
-
 template <int BM, int BN, int WM, int WN, int NS, bool SCHED, bool NORM = false>
 __global__ void __launch_bounds__(NT) ring_kernel(const u16* __restrict__ A, const u16* __restrict__ B,
                                                   u16* __restrict__ C, int T, int N, int K, int nbk, int flags,
@@ -648,6 +601,9 @@ void launch(const at::Tensor& dy, const at::Tensor& x, at::Tensor& out, bool acc
 
 }  // namespace wgrad
 
+void g4_wgrad(const at::Tensor& dy, const at::Tensor& x, at::Tensor& out, bool accumulate, int splits, bool hybrid,
+              float* nrm, long nrm_cap, bool ring);
+
 // cfg: 0 = auto, 1 = 256x256 (8 waves 2x4), 2 = 256x128 (8 waves 4x2); +2 = register-pipelined loop
 // norm (optional, fp32, contiguous): gradient-norm partial slots for the ring variants (cfg 9 / 10 and their split-K
 // forms): every slot the launch owns is written, the rest are left untouched (the caller zeroes the buffer once per
@@ -677,15 +633,19 @@ void wgrad_gemm(at::Tensor out, at::Tensor dy, at::Tensor x, bool accumulate, in
   const bool hybrid = cfg >= 1000;
   const int splits = (int)((cfg % 1000) / 100);
   cfg %= 100;
-  SFT_CHECK(splits <= 1 || ((cfg == 9 || cfg == 10) && T / 32 >= splits),
-            "wgrad_gemm split-K: ring cfg 9/10 with at least one 32-token step per split");
+  SFT_CHECK(splits <= 1 || ((cfg == 9 || cfg == 10 || cfg == 12 || cfg == 13) && T / 32 >= splits),
+            "wgrad_gemm split-K: ring cfg 9/10 or the 4-wave cfg 12 with at least one 32-token step per split");
   float* nrm = nullptr;
   long nrm_cap = 0;
   if (norm.has_value() && norm->defined()) {
-    SFT_CHECK(cfg == 9 || cfg == 10, "wgrad_gemm: norm partials need the ring variants (cfg 9 / 10)");
+    SFT_CHECK(cfg == 9 || cfg == 10 || cfg == 12 || cfg == 13, "wgrad_gemm: norm partials need cfg 9 / 10 / 12 / 13");
     SFT_CHECK(norm->scalar_type() == at::kFloat && norm->is_contiguous() && norm->is_cuda(), "wgrad_gemm: fp32 norm slots");
     nrm = norm->data_ptr<float>();
     nrm_cap = norm->numel();
+  }
+  if (cfg == 12 || cfg == 13) {  // 4 waves of 128 x 128, AGPR accumulators (csrc/gemm_4w.hip); 13: 4-slot ring
+    g4_wgrad(dy, x, out, accumulate, splits, hybrid, nrm, nrm_cap, cfg == 13);
+    return;
   }
   if (splits > 1) {
     if (cfg == 10) {

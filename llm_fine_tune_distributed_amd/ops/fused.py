@@ -42,6 +42,9 @@ def _weight_grad_done(param: torch.Tensor) -> None:
 
 
 _WGRAD_MODE = os.environ.get("SFTAMD_WGRAD", "auto")  # auto | blas | <cfg int> (kernel variant)
+# SFTAMD_WGRAD_4W=1 (default): the 4-wave kernel (csrc/gemm_4w.hip, cfg 13: 128 x 128 wave tiles, AGPR accumulators,
+# 4-slot ring of 32-token steps) where it beat the 8-wave rings in tools/bench_wgrad.py (profiles/r3_bwd_gemm_4wave.md)
+_WGRAD_4W = os.environ.get("SFTAMD_WGRAD_4W", "1") == "1"
 
 
 def _wgrad_cfg(T: int, N: int, K: int) -> int:
@@ -57,7 +60,11 @@ def _wgrad_cfg(T: int, N: int, K: int) -> int:
         return 0
     if _WGRAD_MODE not in ("auto", ""):
         return int(_WGRAD_MODE)
-    if N % 256 == 0 and K % 256 == 0 and (N // 256) * (K // 256) >= 512:
+    tiles = (N // 256) * (K // 256)
+    if _WGRAD_4W and N % 256 == 0 and K % 256 == 0 and T % 128 == 0 and (tiles >= 2048 or 288 <= tiles < 512):
+        # lm_head / tied embedding (4008 tiles): 3.25 vs 3.29 ms; down_proj (344 tiles): 0.343 vs 0.347 ms (cfg 9)
+        return 13
+    if N % 256 == 0 and K % 256 == 0 and tiles >= 512:
         return 10
     if (N % 256 == 0 and K % 256 == 0 and 64 < (N // 256) * (K // 256) <= 128 and (T // 32) % 2 == 0
             and (N // 256) * (K // 128) < 256):
@@ -259,18 +266,30 @@ def _dgrad_ok(dy2d: torch.Tensor, w: torch.Tensor) -> bool:
             and w.data_ptr() % 16 == 0)
 
 
-def _dgrad_cfg(dy2d: torch.Tensor) -> int:
+_DGRAD_4W = os.environ.get("SFTAMD_DGRAD_4W", "1") == "1"
+
+
+def _dgrad_cfg(dy2d: torch.Tensor, swiglu: bool = False) -> int:
     """Kernel configuration: 7 = 256 x 256 tiles, 64-deep K stages (two 32-deep MFMA sub-steps per barrier);
-    5 = the 32-deep three-stage ring for reductions that are not a multiple of 64 (profiles/r2_dgrad.md)."""
-    return 7 if dy2d.shape[1] % 64 == 0 else 5
+    5 = the 32-deep three-stage ring for reductions that are not a multiple of 64 (profiles/r2_dgrad.md);
+    12 / 13 = the 4-wave kernel of csrc/gemm_4w.hip (128 x 128 wave tiles, AGPR accumulators; 13 = its 4-slot ring):
+    M = 8192, tools/bench_dgrad.py (profiles/r3_bwd_gemm_4wave.md): o 0.058 vs 0.059 ms (cfg 7), qkv 0.080 vs 0.083,
+    gate_up (K = 22016) 0.528 (cfg 13) vs 0.548 for hipBLASLt, lm_head (K = 128256) 2.98 vs 3.09. The fused SwiGLU
+    backward epilogue stays on cfg 7 (its LDS-staged epilogue: 0.436 vs 0.58 ms for the register epilogue)."""
+    K = dy2d.shape[1]
+    if _DGRAD_4W and not swiglu and K % 128 == 0:
+        return 13 if K > 4096 else 12
+    return 7 if K % 64 == 0 else 5
 
 
 def dgrad_mm(dy2d: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
-    """dX = dy @ W (W = the projection's [out, in] weight). The HIP kernel where it beats hipBLASLt
-    (profiles/r2_dgrad.md, M = 8192: o_proj 0.063 vs 0.078 ms, qkv 0.088 vs 0.097 ms): reductions of at most
-    4096 output features into at most 4096 inputs; gate_up (K = 22016) and lm_head stay on hipBLASLt."""
-    if _dgrad_ok(dy2d, w) and (_DGRAD_MODE == "hip" or (dy2d.shape[1] <= 4096 and w.shape[1] <= 4096)):
-        return _ext.ops().dgrad_gemm(dy2d, w, None, _dgrad_cfg(dy2d))
+    """dX = dy @ W (W = the projection's [out, in] weight). The HIP kernel where it beats hipBLASLt: every
+    SmolLM3 shape with M % 256 == 0 on the 4-wave kernel (gate_up and lm_head included, _dgrad_cfg); without it
+    (SFTAMD_DGRAD_4W=0) reductions of at most 4096 output features into at most 4096 inputs on cfg 7."""
+    if _dgrad_ok(dy2d, w):
+        cfg = _dgrad_cfg(dy2d)
+        if cfg in (12, 13) or _DGRAD_MODE == "hip" or (dy2d.shape[1] <= 4096 and w.shape[1] <= 4096):
+            return _ext.ops().dgrad_gemm(dy2d, w, None, cfg)
     return torch.mm(dy2d, w)
 
 
@@ -296,7 +315,7 @@ class SwiGLULinearFn(Function):
         dgu = dw = None
         if ctx.needs_input_grad[0]:
             if _dgrad_ok(dy2d, w) and gu2d.is_contiguous():
-                dgu = _ext.ops().dgrad_gemm(dy2d, w, gu2d, _dgrad_cfg(dy2d))
+                dgu = _ext.ops().dgrad_gemm(dy2d, w, gu2d, _dgrad_cfg(dy2d, swiglu=True))
             else:
                 dgu = _ext.ops().swiglu_bwd(torch.mm(dy2d, w), gu2d)
             dgu = dgu.view(gu.shape)
@@ -603,7 +622,7 @@ class SwiGLUDownFn(Function):
         dgu = dw = None
         if ctx.needs_input_grad[0]:
             if _dgrad_ok(dy2d, w):
-                dgu = _ext.ops().dgrad_gemm(dy2d, w, gu2d, _dgrad_cfg(dy2d))
+                dgu = _ext.ops().dgrad_gemm(dy2d, w, gu2d, _dgrad_cfg(dy2d, swiglu=True))
             else:
                 dgu = _ext.ops().swiglu_bwd(torch.mm(dy2d, w), gu2d)
             dgu = dgu.view(gu.shape)
@@ -826,7 +845,7 @@ class LMHeadCEFn(Function):
         g = dloss.float()
         dh = dw = None
         if ctx.needs_input_grad[0]:
-            dh = (torch.mm(dlogits, w) * g.to(dlogits.dtype)).view(ctx.h_shape)
+            dh = (dgrad_mm(dlogits, w) * g.to(dlogits.dtype)).view(ctx.h_shape)
         if ctx.needs_input_grad[1]:
             dw = _accumulate_weight_grad(w, dlogits, h2d, scale=g)
         return dh, dw, None, None

@@ -63,11 +63,14 @@ def test_default_path_smollm3_widths_vs_fp32_reference(monkeypatch):
     assert tr.get("tn.rope.c11", 0) == 3 and tr.get("tn.rope.tail", 0) == 3, tr  # qkv + RoPE, 384-tile tail split
     assert tr.get("attn.fwd3", 0) == 4 and tr.get("attn.dkdv5", 0) == 4 and tr.get("attn.dq4", 0) == 4, tr
     assert tr.get("attn.bwd_rope_epi", 0) == 3, tr  # inverse RoPE in the dq / dK epilogues of the 3 RoPE layers
-    for c in (10, 9, 209, 210):  # ring wgrad: gate_up / down+lm_head / o_proj (split 2) / qkv (split 2)
+    # wgrad: 8-wave rings for gate_up / lm_head (8192-vocab) / o_proj (split 2) / qkv (split 2), the 4-wave ring
+    # (csrc/gemm_4w.hip) for down_proj
+    for c in (10, 9, 209, 210, 13):
         assert tr.get(f"wgrad.c{c}", 0) > 0, (c, tr)
     assert tr.get("wgrad.norm_slots", 0) > 0, tr
     assert tr.get("dgrad.swiglu.c7", 0) >= 4 and tr.get("dgrad.tail", 0) > 0, tr  # down dgrad + SwiGLU bwd
-    assert tr.get("dgrad.c7", 0) > 0, tr  # o_proj / qkv dgrads
+    assert tr.get("dgrad.c12", 0) > 0, tr  # o_proj / qkv dgrads: 4-wave pair loop
+    assert tr.get("dgrad.c13", 0) >= 5, tr  # gate_up (K = 22016) x 4 + lm_head: 4-wave ring
     assert all(not k.startswith("attn.dq3") and k != "attn.fwd3.w4" for k in tr), tr
     # ---- numerics vs the fp32 reference path (same weights, PyTorch ops)
     monkeypatch.setenv("SFTAMD_DISABLE_HIP", "1")

@@ -1,0 +1,148 @@
+"""4-wave backward GEMMs (csrc/gemm_4w.hip, wgrad_gemm / dgrad_gemm cfg 12) against plain PyTorch fp32 references:
+weight gradients with and without accumulation, split-K / hybrid pieces, gradient-norm slots; input gradients plain,
+with the fused SwiGLU backward, on column-sliced weights and through the wave-tail split."""
+import pytest
+import torch
+
+from llm_fine_tune_distributed_amd.ops import _ext
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda"
+
+
+@pytest.fixture(autouse=True)
+def _need_ext():
+    assert _ext.load(), _ext.load_error()
+
+
+def rel_err(a, b):
+    a, b = a.float(), b.float()
+    return ((a - b).norm() / b.norm().clamp_min(1e-30)).item()
+
+
+@pytest.mark.parametrize("cfg,T,N,K", [(12, 128, 256, 256), (12, 256, 512, 768), (12, 384, 768, 512),
+                                       (12, 1024, 2304, 4352),     # 153 tiles, 8 K-tiles
+                                       (212, 512, 512, 512), (412, 1024, 256, 256), (312, 384, 512, 256),
+                                       (1312, 256, 4096, 4352),    # hybrid: 256 whole tiles + 16 split 3 ways
+                                       (1212, 384, 4352, 4096),
+                                       # cfg 13: the 4-slot ring of 32-deep steps
+                                       (13, 128, 256, 256), (13, 384, 768, 512), (13, 1024, 2304, 4352),
+                                       (213, 512, 512, 512), (313, 384, 512, 256), (1313, 256, 4096, 4352)])
+@pytest.mark.parametrize("accumulate", [False, True])
+def test_wgrad_4wave(cfg, T, N, K, accumulate):
+    torch.manual_seed(0)
+    dy = torch.randn(T, N, device=DEV, dtype=torch.bfloat16)
+    x = torch.randn(T, K, device=DEV, dtype=torch.bfloat16)
+    out = torch.randn(N, K, device=DEV, dtype=torch.bfloat16)
+    base = out.float().clone()
+    _ext.ops().wgrad_gemm(out, dy, x, accumulate, cfg)
+    want = dy.float().t() @ x.float() + (base if accumulate else 0)
+    assert rel_err(out, want) < 5e-3
+    err = (out.float() - want).abs().max().item()
+    assert err <= 0.02 * want.abs().max().item(), err
+
+
+@pytest.mark.parametrize("cfg", [12, 13])
+def test_wgrad_4wave_exact_structure(cfg):
+    """Integer-valued operands (exact in fp32): a permuted token, row or column mapping anywhere in the staging,
+    the transposed reads or the register epilogue changes the result bit for bit."""
+    T, N, K = 256, 512, 512
+    t = torch.arange(T, device=DEV)
+    dy = ((t[:, None] * 3 + torch.arange(N, device=DEV)[None, :] * 7) % 5 - 2).to(torch.bfloat16)
+    x = ((t[:, None] * 5 + torch.arange(K, device=DEV)[None, :] * 11) % 7 - 3).to(torch.bfloat16)
+    out = torch.empty(N, K, device=DEV, dtype=torch.bfloat16)
+    _ext.ops().wgrad_gemm(out, dy, x, False, cfg)
+    assert torch.equal(out, (dy.float().t() @ x.float()).to(torch.bfloat16))  # exact fp32 sums, one rounding
+
+
+@pytest.mark.parametrize("cfg,T,N,K", [(12, 256, 512, 768), (212, 512, 512, 512), (1312, 256, 4096, 4352),
+                                       (13, 256, 512, 768), (1313, 256, 4096, 4352)])
+@pytest.mark.parametrize("accumulate", [False, True])
+def test_wgrad_4wave_norm_slots(cfg, T, N, K, accumulate):
+    """Norm partials (register epilogue / split-K fixup) sum to the squared norm of the stored bf16 gradient
+    (within fp32-before-rounding tolerance); slots past the capacity stay untouched."""
+    torch.manual_seed(0)
+    dy = torch.randn(T, N, device=DEV, dtype=torch.bfloat16)
+    x = torch.randn(T, K, device=DEV, dtype=torch.bfloat16)
+    out = torch.randn(N, K, device=DEV, dtype=torch.bfloat16)
+    cap = -(-N // 256) * -(-K // 128) * 32
+    slots = torch.zeros(cap + 64, device=DEV)
+    slots[cap:] = 7.0
+    _ext.ops().wgrad_gemm(out, dy, x, accumulate, cfg, slots[:cap])
+    want = out.float().pow(2).sum().item()
+    assert abs(slots[:cap].sum().item() - want) <= 1e-3 * want
+    assert torch.all(slots[cap:] == 7.0)
+
+
+def test_wgrad_4wave_matches_ring_split_exactly():
+    """Split pieces are whole pairs of 64-token K-tiles summed in a fixed order: repeated launches are bitwise
+    identical (deterministic), and the result matches the fp32 reference."""
+    torch.manual_seed(3)
+    T, N, K = 1024, 512, 768
+    dy = torch.randn(T, N, device=DEV, dtype=torch.bfloat16)
+    x = torch.randn(T, K, device=DEV, dtype=torch.bfloat16)
+    o1 = torch.empty(N, K, device=DEV, dtype=torch.bfloat16)
+    o2 = torch.empty_like(o1)
+    _ext.ops().wgrad_gemm(o1, dy, x, False, 412)
+    _ext.ops().wgrad_gemm(o2, dy, x, False, 412)
+    assert torch.equal(o1, o2)
+    assert rel_err(o1, dy.float().t() @ x.float()) < 5e-3
+
+
+@pytest.mark.parametrize("M,K,N,wpad", [(256, 128, 256, 0), (512, 2048, 768, 0), (256, 384, 512, 64),
+                                        (768, 1024, 256, 0), (2048, 11008, 2048, 0)])
+@pytest.mark.parametrize("cfg", [12, 13])
+def test_dgrad_4wave_plain(M, K, N, wpad, cfg):
+    torch.manual_seed(0)
+    dy = torch.randn(M, K, device=DEV, dtype=torch.bfloat16)
+    wfull = torch.randn(K, N + wpad, device=DEV, dtype=torch.bfloat16)
+    w = wfull[:, :N]
+    out = _ext.ops().dgrad_gemm(dy, w, None, cfg)
+    assert out.shape == (M, N)
+    assert rel_err(out, dy.float() @ w.float()) < 5e-3
+    # asymmetric structure: a column-shifted identity catches any transposed / permuted mapping (exact)
+    eye = torch.zeros(K, N, device=DEV)
+    eye[torch.arange(min(K, N)), (torch.arange(min(K, N)) + 5) % N] = 1.0
+    ramp = (torch.arange(M * K, device=DEV) % 251).float().view(M, K).to(torch.bfloat16)
+    got = _ext.ops().dgrad_gemm(ramp, eye.to(torch.bfloat16), None, cfg).float()
+    assert torch.equal(got, ramp.float() @ eye)
+
+
+@pytest.mark.parametrize("M,K,N", [(256, 256, 256), (512, 2048, 512), (1024, 128, 768)])
+@pytest.mark.parametrize("cfg", [12, 13])
+def test_dgrad_4wave_swiglu_bwd(M, K, N, cfg):
+    torch.manual_seed(1)
+    dy = torch.randn(M, K, device=DEV, dtype=torch.bfloat16)
+    w = (0.05 * torch.randn(K, N, device=DEV)).to(torch.bfloat16)
+    gu = torch.randn(M, 2 * N, device=DEV, dtype=torch.bfloat16)
+    dgu = _ext.ops().dgrad_gemm(dy, w, gu, cfg)
+    dact = dy.float() @ w.float()
+    g, u = gu.float().chunk(2, dim=-1)
+    s = torch.sigmoid(g)
+    want = torch.cat([dact * u * s * (1 + g * (1 - s)), dact * g * s], dim=-1)
+    assert dgu.shape == (M, 2 * N)
+    assert rel_err(dgu, want) < 1e-2
+
+
+@pytest.mark.parametrize("cfg", [12, 13])
+@pytest.mark.parametrize("swiglu", [True, False])
+def test_dgrad_4wave_wave_tail(swiglu, cfg, monkeypatch):
+    """SmolLM3 down projection grid (43 x 32 tiles = 5.375 rounds): the whole rounds on the 4-wave kernel + the
+    leftover columns as 256 x 128 half tiles of the ring kernel (SFTAMD_DGRAD_TAIL=2) == the fp32 reference."""
+    torch.manual_seed(2)
+    M, K, N = 8192, 128, 11008
+    dy = torch.randn(M, K, device=DEV, dtype=torch.bfloat16)
+    w = (0.05 * torch.randn(K, N, device=DEV)).to(torch.bfloat16)
+    gu = torch.randn(M, 2 * N, device=DEV, dtype=torch.bfloat16) if swiglu else None
+    dact = dy.float() @ w.float()
+    if swiglu:
+        g, u = gu.float().chunk(2, dim=-1)
+        s = torch.sigmoid(g)
+        want = torch.cat([dact * u * s * (1 + g * (1 - s)), dact * g * s], dim=-1)
+    else:
+        want = dact
+    for tail in ("0", "2"):
+        monkeypatch.setenv("SFTAMD_DGRAD_TAIL", tail)
+        got = _ext.ops().dgrad_gemm(dy, w, gu, cfg)
+        assert rel_err(got, want) < 1e-2, tail

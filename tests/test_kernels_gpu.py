@@ -593,7 +593,7 @@ def test_gemm_tn_4wave(M, N, K):
     ref32 = x.float() @ w.float().t()
     # 13-44: schedule variants of the same kernel; 50: the persistent version (tiles > 256 walk several per
     # workgroup; K = 128 is its single-pair path)
-    for cfg in (12, 13, 16, 20, 21, 24, 25, 28, 44, 50):
+    for cfg in (12, 13, 16, 20, 21, 24, 25, 28, 44, 50, 60, 61):
         c = _ext.ops().gemm_tn(x, w, cfg)
         assert rel_err(c, ref32) < 5e-3, cfg
     gu_ref = x.float() @ (w * 0.1).float().t()
