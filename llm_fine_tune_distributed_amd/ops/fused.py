@@ -215,6 +215,14 @@ def _persist_ok(x2d: torch.Tensor, w: torch.Tensor) -> bool:
             and x2d.data_ptr() % 16 == 0 and w.data_ptr() % 16 == 0 and _grid_fills(x2d.shape[0], w.shape[0]))
 
 
+def _as_output(y2d: torch.Tensor, lead) -> torch.Tensor:
+    """[M, N] GEMM result -> [*lead, N] returned from a custom Function forward WITHOUT view semantics (the result
+    is an intermediate of the Function; a .view() of it would make in-place consumers such as rope_ fail autograd's
+    view + in-place check)."""
+    shape = (*lead, y2d.shape[-1])
+    return y2d if tuple(y2d.shape) == shape else torch.ops.aten._unsafe_view(y2d, shape)
+
+
 def fwd_gemm(x2d: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
     """y = x2d @ w^T for a projection forward: the persistent HIP GEMM where selected and it applies, else
     hipBLASLt (or the opt-in plain ping-pong GEMM, SFTAMD_TN_PLAIN)."""
@@ -233,7 +241,7 @@ class LinearFn(Function):
         ctx.weight = weight
         x2d = x.reshape(-1, x.shape[-1])
         if _ext.use_hip(x2d):
-            return fwd_gemm(x2d, weight).view(*x.shape[:-1], weight.shape[0])
+            return _as_output(fwd_gemm(x2d, weight), x.shape[:-1])
         return torch.nn.functional.linear(x, weight)
 
     @staticmethod
@@ -305,7 +313,7 @@ class SwiGLULinearFn(Function):
         ctx.save_for_backward(gu, act)
         ctx.weight = weight
         a2d = act.reshape(-1, act.shape[-1])
-        return fwd_gemm(a2d, weight).view(*gu.shape[:-1], weight.shape[0])
+        return _as_output(fwd_gemm(a2d, weight), gu.shape[:-1])
 
     @staticmethod
     def backward(ctx, dy):
@@ -612,7 +620,7 @@ class SwiGLUDownFn(Function):
         ctx.save_for_backward(gu, act)
         ctx.weight = weight
         a2d = act.reshape(-1, act.shape[-1])
-        return fwd_gemm(a2d, weight).view(*gu.shape[:-1], weight.shape[0])
+        return _as_output(fwd_gemm(a2d, weight), gu.shape[:-1])
 
     @staticmethod
     def backward(ctx, dy):

@@ -94,8 +94,9 @@ def test_model_fused_gemm_epilogues(mt, down_fused, monkeypatch):
     monkeypatch.setattr(F, "_TN_MODE", "1")
     l_f, g_f = _run(m, ids, labels, True)
     assert calls["swiglu"] == 4 and calls["rope"] == (3 if mt == "smollm3" else 4)  # NoPE layer 3
-    # plain HIP GEMM: o_proj (and down_proj unless it is SwiGLUDownFn) of every layer (+ the NoPE layer's qkv)
-    assert calls["plain"] == (4 if down_fused else 8) + (1 if mt == "smollm3" else 0), calls
+    # plain HIP GEMM (ops.fused.fwd_gemm): o_proj and down_proj of every layer (SwiGLUDownFn / LinearFn both route
+    # through fwd_gemm), the lm_head (1024-vocab), + the NoPE layer's qkv
+    assert calls["plain"] == 9 + (1 if mt == "smollm3" else 0), calls
     monkeypatch.setattr(F, "_TN_MODE", "0")
     calls["plain"] = 0
     l_u, g_u = _run(m, ids, labels, True)

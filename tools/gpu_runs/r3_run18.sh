@@ -4,7 +4,7 @@
 cd $GRAFT_REPO_ROOT
 mkdir -p gpurun_out
 export TMPDIR=/tmp
-timeout -k 10 900 python -u -m pytest -x -q --timeout 200 --timeout-method thread -m gpu tests/ > gpurun_out/r3_18_tests.log 2>&1 || { tail -40 gpurun_out/r3_18_tests.log; exit 1; }
+timeout -k 10 900 python -u -m pytest -q --timeout 200 --timeout-method thread -m gpu tests/ > gpurun_out/r3_18_tests.log 2>&1 || { tail -40 gpurun_out/r3_18_tests.log; exit 1; }
 tail -2 gpurun_out/r3_18_tests.log
 timeout -k 10 300 python -u bench.py --steps 20 --warmup 5 > gpurun_out/r3_18_bench.log 2>&1 || { tail -20 gpurun_out/r3_18_bench.log; exit 1; }
 grep '"metric"' gpurun_out/r3_18_bench.log
