@@ -69,6 +69,8 @@ def parse(argv=None):
     ap.add_argument("--bucket-mb", type=float, default=float(os.environ.get("SFTAMD_BUCKET_MB", "0")),
                     help="gradient bucket cap in MB; 0 (default) = the xGMI plan of parallel.ddp.plan_bucket_mb")
     ap.add_argument("--packing", action="store_true")
+    ap.add_argument("--padding-free", choices=["auto", "on", "off"], default="auto",
+                    help="SFTConfig.padding_free (auto: the trainer default, on for GPU training)")
     ap.add_argument("--freeze-policy", default="full", choices=["full", "last_n_layers", "lora"])
     ap.add_argument("--master-weights", action="store_true", help="fp32 master copy (default: bf16 params + SR)")
     ap.add_argument("--optim-state", default=os.environ.get("SFTAMD_OPTIM_STATE", "bf16"), choices=["fp32", "bf16"],
@@ -202,6 +204,7 @@ def run(a):
     args = SFTConfig(output_dir="/tmp/sftamd_bench", per_device_train_batch_size=a.micro_batch,
                      gradient_accumulation_steps=a.ga, learning_rate=5e-5 * st.world_size, max_grad_norm=1.0,
                      bf16=True, gradient_checkpointing=False, max_length=a.seq, packing=a.packing,
+                     padding_free={"auto": None, "on": True, "off": False}[a.padding_free],
                      ddp_bucket_cap_mb=a.bucket_mb or None, dataloader_drop_last=True, jsonl_log=False,
                      logging_steps=0, optimizer_overlap=not a.no_overlap, freeze_policy=a.freeze_policy,
                      master_weights=a.master_weights, optim_state_dtype=a.optim_state,
@@ -285,7 +288,8 @@ def run(a):
                        "ga_passes_per_step": 1 if (a.ga > 1 and a.micro_batch * a.ga * a.seq <= args.ga_merge_max_tokens)
                        else a.ga,
                        "optimizer_sharding": "zero1" if shard else "none",
-                       "gradient_checkpointing": False, "packing": a.packing},
+                       "gradient_checkpointing": False, "packing": a.packing,
+                       "padding_free": bool(getattr(trainer, "packed", False)) and not a.packing},
             "tokens_per_sec": round(tok_s, 1), "mfu": None if mfu is None else round(mfu, 4),
             "final_loss": round(loss, 4), "peak_mem_gb": max(r_["peak_mem_gb"] for r_ in ranks),
             "dist": {"backend": mine["backend"], "world_size": mine["world_size"],
@@ -355,6 +359,7 @@ def run_recipe(a):
                      jsonl_log=False, freeze_policy=a.freeze_policy, shard_optimizer_state=bool(a.zero),
                      dataset_cache=False, gemm_tuning=False,
                      lm_head_chunk_rows=a.lm_head_chunk,
+                     padding_free={"auto": None, "on": True, "off": False}[a.padding_free],
                      **({} if a.ga_merge_max_tokens is None else {"ga_merge_max_tokens": a.ga_merge_max_tokens}))
     trainer = SFTTrainer(model=model, args=args, train_dataset=train_rows, eval_dataset=val_rows,
                          processing_class=load_tokenizer(None))
@@ -376,7 +381,7 @@ def run_recipe(a):
                        "global_batch": samples_per_step, "per_device_batch": micro,
                        "gradient_accumulation_steps": ga, "seq_len": "ragged <= 1024 (padded to 64)",
                        "parallelism": f"dp{st.world_size}", "eval_steps": a.eval_steps,
-                       "per_device_eval_batch": a.eval_batch},
+                       "per_device_eval_batch": a.eval_batch, "padding_free": bool(trainer.packed)},
             "train_pure_samples_per_second": round(m["train_pure_samples_per_second"], 3),
             "train_tokens_per_second": round(m["train_tokens_per_second"], 1),
             "train_mfu": round(m.get("train_mfu", 0.0), 4), "train_runtime_s": round(m["train_runtime"], 3),

@@ -465,10 +465,16 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))
 g4_kernel(const u16* __restrict__ A, const u16* __restrict__ B, long lda, long ldb, int kred, int nbm, int nbn,
           int group, int ndp, int splits, Epi ea) {
   __shared__ __attribute__((aligned(16))) char smem[2 * STAGE];
-  // XCD-aware bijective remap: consecutive ids run on one XCD (shared L2 for the GROUP-blocked tile order)
-  const int nwg = gridDim.x, orig = blockIdx.x;
-  const int xcd = orig & 7, q8 = nwg >> 3, r8 = nwg & 7;
-  const int wgid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (orig >> 3);
+  // Blocks [0, ndp) own whole tiles, XCD-aware bijective remap among them (consecutive ids on one XCD: shared L2 for
+  // the GROUP-blocked tile order); blocks >= ndp are the split pieces. Classes by BLOCK index, not by remapped id:
+  // dispatch follows block order, so the whole tiles fill the first rounds and the short pieces the last one (a
+  // remap over the whole grid put half of each round's blocks on pieces and stretched the whole tiles to 2 rounds).
+  const int orig = blockIdx.x;
+  int wgid = orig;
+  if (orig < ndp) {
+    const int xcd = orig & 7, q8 = ndp >> 3, r8 = ndp & 7;
+    wgid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (orig >> 3);
+  }
   const int npair_all = kred / (2 * BK);
   int tile = wgid, sk = 0, p0 = 0, p1 = npair_all;
   if (wgid >= ndp) {  // split piece sk of tile ndp + (wgid - ndp) / splits: K-tile pairs [p0, p1)
@@ -583,6 +589,9 @@ void g4_wgrad(const at::Tensor& dy, const at::Tensor& x, at::Tensor& out, bool a
 
 // Input gradient dX[M, N] = dy[M, K] . w[K, N] (w may be a column slice: row stride w.stride(0)); gu != nullptr:
 // SwiGLU backward epilogue, out = dgu with row stride ldo = 2 I (gate at column n, up at n + I).
+// Wave quantisation (plain epilogue): a grid that is not whole rounds of 256 workgroups runs its whole rounds as
+// whole tiles and the leftover tiles split over the reduction into fp32 slabs + the ordered fixup, e.g. the recipe's
+// padding-free M = 10240: gate_up / lm_head dgrads are 40 x 8 = 320 tiles = 1.25 rounds -> 256 + 64 x 4 pieces.
 void g4_dgrad(const at::Tensor& dy, const at::Tensor& w, u16* out, long ldo, const u16* gu, int I, bool ring) {
   const int M = dy.size(0), K = dy.size(1), N = w.size(1);
   SFT_CHECK(M % 256 == 0 && N % 256 == 0 && K % 128 == 0 && K > 0, "dgrad 4-wave: M, N % 256, K % 128");
@@ -591,10 +600,28 @@ void g4_dgrad(const at::Tensor& dy, const at::Tensor& w, u16* out, long ldo, con
   ea.ldc = ldo;
   ea.gu = gu;
   ea.I = I;
-  const int tiles = (M / 256) * (N / 256);
+  const int nbm = M / 256, nbn = N / 256, tiles = nbm * nbn;
+  int ndp = tiles, splits = 1;
+  static const bool split_on = [] {
+    const char* e = std::getenv("SFTAMD_DGRAD_SPLITK");
+    return !(e && e[0] == '0');
+  }();
+  if (gu == nullptr && split_on && tiles % 256 != 0 && K >= 8192) {  // short reductions: the fixup costs more
+    const int rest = tiles > 256 ? tiles % 256 : tiles;
+    const int s = std::min(std::min(256 / rest, 8), K / 128);
+    if (s >= 2) {
+      ndp = tiles - rest;
+      splits = s;
+    }
+  }
+  at::Tensor part;
+  if (splits > 1) {
+    part = at::empty({(long)(tiles - ndp) * splits * 65536}, dy.options().dtype(at::kFloat));
+    ea.P = part.data_ptr<float>();
+  }
   auto go = [&](auto epi, auto rg) {
     g4::launch<g4::ROW, g4::TR, decltype(epi)::value, decltype(rg)::value>(
-        (const u16*)dy.data_ptr(), dy.stride(0), (const u16*)w.data_ptr(), w.stride(0), M, N, K, tiles, 1, ea);
+        (const u16*)dy.data_ptr(), dy.stride(0), (const u16*)w.data_ptr(), w.stride(0), M, N, K, ndp, splits, ea);
   };
   using SW = std::integral_constant<int, g4::EPI_SWIGLU_BWD>;
   using ST = std::integral_constant<int, g4::EPI_STORE>;
@@ -604,6 +631,14 @@ void g4_dgrad(const at::Tensor& dy, const at::Tensor& w, u16* out, long ldo, con
   } else {
     if (ring) go(ST(), std::true_type());
     else go(ST(), std::false_type());
+  }
+  if (splits > 1) {
+    SFT_TRACE("dgrad.splitk");
+    const int nsk = tiles - ndp;
+    const long n8 = (long)nsk * 65536 / 8;
+    splitk_fixup_kernel<256, 256><<<(unsigned)((n8 + 255) / 256), 256, 0, cur_stream()>>>(
+        part.data_ptr<float>(), out, ndp, nsk, splits, nbn, (int)ldo, 0, nullptr, nbm, std::min(g4::group_m(), nbm));
+    SFT_LAUNCH_CHECK();
   }
 }
 

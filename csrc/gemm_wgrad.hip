@@ -473,9 +473,14 @@ __global__ void __launch_bounds__(NT) ring_kernel(const u16* __restrict__ A, con
   // spills inside its main loop)
   using G = RCfg<BM, BN, WM, WN, NS>;
   __shared__ __attribute__((aligned(16))) char smem[G::LDS];
-  const int nwg = gridDim.x, orig = blockIdx.x;
-  const int xcd = orig & 7, q8 = nwg >> 3, r8 = nwg & 7;
-  const int wgid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (orig >> 3);
+  // whole tiles = blocks [0, ndp) (XCD-aware remap among them), split pieces = the blocks after them: by block index,
+  // so the whole tiles fill the first dispatch rounds and the short pieces the last (csrc/gemm_4w.hip)
+  const int orig = blockIdx.x;
+  int wgid = orig;
+  if (orig < ndp) {
+    const int nd = min(ndp, (int)gridDim.x), xcd = orig & 7, q8 = nd >> 3, r8 = nd & 7;
+    wgid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (orig >> 3);
+  }
   // Hybrid data-parallel + split-K: workgroups [0, ndp) own whole tiles (direct epilogue); the remaining
   // tiles (the partial last wave) are each split `splits` ways over the token axis — consecutive workgroups,
   // uneven step ranges allowed — into fp32 slabs reduced by splitk_fixup_kernel.

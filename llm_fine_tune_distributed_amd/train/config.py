@@ -49,6 +49,11 @@ class SFTConfig:
     dataloader_drop_last: bool = False
     max_length: Optional[int] = 1024
     packing: bool = False
+    # TRL's ``padding_free``: the batch's sequences flattened into one varlen sequence (``cu_seqlens`` / per-sample
+    # ``position_ids``; attention never crosses samples, pads carry no loss), so the loss and every gradient are those
+    # of the padded batch without the pad rows' FLOPs. None = on for GPU training without context parallelism (the
+    # reference recipe's padded micro-batches carry ~11 % pad tokens, profiles/r3_recipe.md), off on CPU.
+    padding_free: Optional[bool] = None
     ddp_backend: Optional[str] = None
     ddp_find_unused_parameters: Optional[bool] = None
     ddp_bucket_cap_mb: Optional[float] = None

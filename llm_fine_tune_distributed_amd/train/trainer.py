@@ -80,6 +80,10 @@ class SFTTrainer:
                 self.dist.world_size, self.dist.rank, self.cp_size)
         set_seed(args.seed)
         dev = self.dist.device
+        pf = getattr(args, "padding_free", None)
+        self.packed = bool(args.packing) or (bool(pf) if pf is not None else (dev.type == "cuda" and self.cp_size == 1))
+        if self.packed and self.cp_size > 1:
+            raise ValueError("context_parallel_size > 1 needs padded batches (packing / padding_free off)")
         if (args.gemm_tuning and dev.type == "cuda" and "PYTORCH_TUNABLEOP_ENABLED" not in os.environ
                 and not torch.cuda.tunable.is_enabled()):  # a caller's own TunableOp setup (e.g. tuning) wins
             from ..utils.gemm_tuning import enable_tuned_gemms
@@ -116,8 +120,10 @@ class SFTTrainer:
         self._pad_id = pad_id
         pad_mult = args.pad_to_multiple_of
         if pad_mult is None and dev.type == "cuda":
-            pad_mult = 256 if args.packing else 64
-        self.collator = data_collator or SFTCollator(pad_id, pad_mult, args.max_length, args.packing,
+            pad_mult = 256 if self.packed else 64
+        # explicit packing: at most per_device_train_batch_size x max_length tokens per batch; padding-free: the whole
+        # batch, however long (every sample of the padded batch, none dropped)
+        self.collator = data_collator or SFTCollator(pad_id, pad_mult, args.max_length, self.packed,
                                                      args.per_device_train_batch_size * (args.max_length or 1024)
                                                      if args.packing else None)
         # ------------------------------------------------------------ engine + optimizer
@@ -130,7 +136,7 @@ class SFTTrainer:
             # most tokens one synchronising pass can hold (every rank computes the same bound from the config):
             # the sparse tied-embedding exchange gathers that many rows without a device sync
             L = int(args.max_length or 1024)
-            if args.packing:
+            if self.packed:
                 per_pass = -(-args.per_device_train_batch_size * L // 256) * 256
             else:
                 pm = int(pad_mult or 1)

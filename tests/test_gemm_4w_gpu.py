@@ -146,3 +146,21 @@ def test_dgrad_4wave_wave_tail(swiglu, cfg, monkeypatch):
         monkeypatch.setenv("SFTAMD_DGRAD_TAIL", tail)
         got = _ext.ops().dgrad_gemm(dy, w, gu, cfg)
         assert rel_err(got, want) < 1e-2, tail
+
+
+@pytest.mark.parametrize("cfg", [12, 13])
+@pytest.mark.parametrize("M,K,N", [(10240, 1024, 2048), (2560, 4096, 2048), (4352, 512, 4096)])
+def test_dgrad_4wave_hybrid_splitk(M, K, N, cfg):
+    """Grids that are not whole rounds of 256 workgroups (the recipe's padding-free M = 10240: 320 tiles) run the
+    whole rounds as whole tiles and split the leftover tiles over the reduction (fp32 slabs + ordered fixup):
+    == the fp32 reference, deterministic, and exact on integer data."""
+    torch.manual_seed(5)
+    dy = torch.randn(M, K, device=DEV, dtype=torch.bfloat16)
+    w = (0.05 * torch.randn(K, N, device=DEV)).to(torch.bfloat16)
+    out = _ext.ops().dgrad_gemm(dy, w, None, cfg)
+    assert rel_err(out, dy.float() @ w.float()) < 5e-3
+    assert torch.equal(out, _ext.ops().dgrad_gemm(dy, w, None, cfg))
+    ramp = (torch.arange(M * K, device=DEV) % 7 - 3).float().view(M, K).to(torch.bfloat16)
+    wi = (torch.arange(K * N, device=DEV) % 5 - 2).float().view(K, N).to(torch.bfloat16)
+    got = _ext.ops().dgrad_gemm(ramp, wi, None, cfg)
+    assert torch.equal(got, (ramp.float() @ wi.float()).to(torch.bfloat16))

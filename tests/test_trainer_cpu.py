@@ -224,3 +224,31 @@ def test_ga_merge_matches_separate_passes(tmp_path, tk, packing):
     for a, b in zip(l0, l1):
         for k in ("loss", "grad_norm", "mean_token_accuracy", "entropy", "num_tokens"):
             assert abs(a[k] - b[k]) <= 1e-5 * max(1.0, abs(a[k])), (k, a[k], b[k])
+
+
+def test_padding_free_matches_padded_batches(tmp_path, tk):
+    """padding_free (TRL's name; the GPU default): every padded micro-batch flattened into one varlen sequence with
+    per-sample positions — the same losses, grad norms, token metrics and update as the padded batches, with the
+    eval metrics too (the whole batch is kept, nothing dropped at the pack boundary)."""
+    rows = generate_qa(24, seed=5)
+    res = {}
+    for pf in (False, True):
+        args = SFTConfig(output_dir=str(tmp_path / str(pf)), per_device_train_batch_size=4,
+                         per_device_eval_batch_size=8, gradient_accumulation_steps=2, learning_rate=1e-3, max_steps=2,
+                         logging_steps=1, eval_strategy="steps", eval_steps=2, save_strategy="no", jsonl_log=False,
+                         padding_free=pf, seed=1)
+        h = TrainingHistoryCallback()
+        t = SFTTrainer(model=_model(seed=3), args=args, train_dataset=rows[:16], eval_dataset=rows[16:],
+                       processing_class=tk, callbacks=[h])
+        assert t.packed == pf
+        t.train()
+        res[pf] = ([x for x in h.history if "loss" in x], [x for x in h.history if "eval_loss" in x],
+                   t.engine.param_flat.clone())
+    (l0, e0, p0), (l1, e1, p1) = res[False], res[True]
+    assert torch.allclose(p0, p1, atol=1e-5, rtol=1e-4)
+    for a, b in zip(l0, l1):
+        for k in ("loss", "grad_norm", "mean_token_accuracy", "entropy", "num_tokens"):
+            assert abs(a[k] - b[k]) <= 1e-5 * max(1.0, abs(a[k])), (k, a[k], b[k])
+    assert len(e0) == len(e1) == 1
+    for k in ("eval_loss", "eval_mean_token_accuracy", "eval_num_tokens"):
+        assert abs(e0[0][k] - e1[0][k]) <= 1e-5 * max(1.0, abs(e0[0][k])), k

@@ -15,13 +15,13 @@ def _cfg():
                 intermediate_size=512, vocab_size=1024, num_hidden_layers=3)
 
 
-def _run(overlap, packing=False, steps=4):
+def _run(overlap, packing=False, steps=4, padding_free=None):
     cfg = _cfg()
     m = build_model(cfg, device="cuda", dtype=torch.bfloat16, seed=0)
     ds = TokenizedDataset.synthetic(64, cfg.vocab_size, 30, 90, seed=2)
     a = SFTConfig(output_dir="/tmp/sftamd_t", per_device_train_batch_size=4, max_steps=steps, learning_rate=1e-3,
                   logging_steps=1, jsonl_log=False, save_strategy="no", optimizer_overlap=overlap, packing=packing,
-                  dataloader_drop_last=True)
+                  dataloader_drop_last=True, padding_free=padding_free)
     t = SFTTrainer(model=m, args=a, train_dataset=ds)
     t.train()
     return [h["loss"] for h in t.state.log_history if "loss" in h], t.engine.param_flat.float().clone()
@@ -37,3 +37,12 @@ def test_overlap_matches_serial_update():
 def test_packing_trains_on_gpu():
     l, p = _run(True, packing=True)
     assert all(torch.isfinite(torch.tensor(l)))
+
+
+def test_padding_free_default_matches_padded_on_gpu():
+    """The GPU default (padding_free) trains like the padded batches: same loss trajectory within bf16 tolerance
+    (different M, so different GEMM tilings), finite, and the trainer reports the flattened mode."""
+    l_pad, p_pad = _run(True, padding_free=False)
+    l_pf, p_pf = _run(True)
+    assert l_pf == pytest.approx(l_pad, rel=2e-2)
+    assert ((p_pf - p_pad).norm() / p_pad.norm()).item() < 1e-2
