@@ -241,9 +241,12 @@ __device__ __forceinline__ void store_tile(const f32x4 (&acc)[8][8], const Epi& 
       }
     }
   }
-  if (nrm != nullptr) {
-    ss = wave_sum(ss);
-    if (lane == 0) *nrm = ss;
+  if (nrm != nullptr) {  // 8 slots per tile (the 8-wave kernels' layout): waves 0..3 write theirs and zero w + 4, so
+    ss = wave_sum(ss);    // slots parked in an uninitialised split-K buffer (hybrid launches) are never garbage
+    if (lane == 0) {
+      nrm[0] = ss;
+      nrm[4] = 0.f;
+    }
   }
 }
 

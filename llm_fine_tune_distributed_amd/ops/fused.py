@@ -65,7 +65,7 @@ def _wgrad_cfg(T: int, N: int, K: int) -> int:
         # gate_up (688 tiles): 0.568 vs 0.578 ms (cfg 10); down_proj (344 tiles = 1.34 rounds): hybrid, the 88 tiles
         # past the whole round split 2 ways over the tokens (1213): 0.301 vs 0.341 (cfg 13) vs 0.349 (cfg 9);
         # lm_head / tied embedding (4008 tiles) stays on cfg 10: 3.195 vs 3.213 ms (profiles/r3_bwd_gemm_4wave.md)
-        return 1213 if tiles < 512 and (T // 128) >= 2 else 13
+        return 1213 if tiles < 512 and (T // 128) >= 2 and os.environ.get("SFTAMD_WGRAD_HYBRID", "1") == "1" else 13
     if N % 256 == 0 and K % 256 == 0 and tiles >= 512:
         return 10
     if (N % 256 == 0 and K % 256 == 0 and 64 < (N // 256) * (K // 256) <= 128 and (T // 32) % 2 == 0
@@ -89,7 +89,7 @@ def _wgrad_mm(out: torch.Tensor, dy2d: torch.Tensor, x2d: torch.Tensor, accumula
     if _ext.use_hip(dy2d) and dy2d.dtype == torch.bfloat16 and out.is_contiguous():
         cfg = _wgrad_cfg(dy2d.shape[0], dy2d.shape[1], x2d.shape[1])
     if cfg:
-        use_norm = norm is not None and cfg % 100 in (9, 10, 12, 13)
+        use_norm = norm is not None and cfg % 100 in ((9, 10, 12, 13) if os.environ.get("SFTAMD_NORM_4W", "1") == "1" else (9, 10))
         _ext.ops().wgrad_gemm(out, dy2d.contiguous(), x2d.contiguous(), accumulate, cfg, norm if use_norm else None,
                               0 if tail_stream is None else tail_stream.cuda_stream)
         return use_norm

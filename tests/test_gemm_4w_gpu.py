@@ -57,7 +57,7 @@ def test_wgrad_4wave_exact_structure(cfg):
 
 
 @pytest.mark.parametrize("cfg,T,N,K", [(12, 256, 512, 768), (212, 512, 512, 512), (1312, 256, 4096, 4352),
-                                       (13, 256, 512, 768), (1313, 256, 4096, 4352)])
+                                       (13, 256, 512, 768), (1313, 256, 4096, 4352), (1213, 1024, 2048, 11008)])
 @pytest.mark.parametrize("accumulate", [False, True])
 def test_wgrad_4wave_norm_slots(cfg, T, N, K, accumulate):
     """Norm partials (register epilogue / split-K fixup) sum to the squared norm of the stored bf16 gradient
@@ -69,6 +69,9 @@ def test_wgrad_4wave_norm_slots(cfg, T, N, K, accumulate):
     cap = -(-N // 256) * -(-K // 128) * 32
     slots = torch.zeros(cap + 64, device=DEV)
     slots[cap:] = 7.0
+    # garbage in the caching allocator's free blocks: a hybrid launch parks the whole tiles' slots in an
+    # uninitialised split-K buffer, every one of them must be written
+    torch.full((1 << 26,), float("nan"), device=DEV)
     _ext.ops().wgrad_gemm(out, dy, x, accumulate, cfg, slots[:cap])
     want = out.float().pow(2).sum().item()
     assert abs(slots[:cap].sum().item() - want) <= 1e-3 * want
