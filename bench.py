@@ -357,7 +357,7 @@ def run_recipe(a):
                      logging_first_step=True, eval_strategy="steps", eval_steps=a.eval_steps, save_strategy="no",
                      bf16=True, gradient_checkpointing=False, max_length=1024, dataloader_drop_last=True,
                      jsonl_log=False, freeze_policy=a.freeze_policy, shard_optimizer_state=bool(a.zero),
-                     dataset_cache=False, gemm_tuning=False,
+                     dataset_cache=False, gemm_tuning=False, optimizer_overlap=not a.no_overlap,
                      lm_head_chunk_rows=a.lm_head_chunk,
                      padding_free={"auto": None, "on": True, "off": False}[a.padding_free],
                      **({} if a.ga_merge_max_tokens is None else {"ga_merge_max_tokens": a.ga_merge_max_tokens}))

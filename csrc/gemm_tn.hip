@@ -1154,6 +1154,35 @@ void launch4(const at::Tensor& a, const at::Tensor& w, int N, const EpiArgs& ea)
 // vmcnt bookkeeping (loads and stores share the counter): next K0 (16) < stores (32) < next K1 (16), so "K0 landed"
 // is vmcnt(48) — within the counter's 63.
 // ============================================================================================
+// LDS-DMA of the persistent kernel through buffer descriptors (csrc/gemm_4w.hip, profiles/r3_bwd_gemm_4wave.md): the
+// A tile's rows in a per-tile descriptor, the whole weight in another, each lane's byte offset in a VGPR set once per
+// tile, the piece / K offsets in SGPRs — no per-piece 64-bit VALU address arithmetic in the loop.
+typedef __amdgpu_buffer_rsrc_t rsrc_t;
+__device__ __forceinline__ rsrc_t tile_rsrc(const u16* p) {
+  const unsigned long long a = (unsigned long long)p;
+  const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)a), hi = __builtin_amdgcn_readfirstlane((unsigned)(a >> 32));
+  return __builtin_amdgcn_make_buffer_rsrc((void*)(((unsigned long long)hi << 32) | lo), 0, 0xFFFFFFFFu, 0x00020000);
+}
+
+template <int EPI>
+struct Stager5 {
+  rsrc_t ra, rb;
+  unsigned va, vb;       // lane byte offsets (A: within the tile's rows; B: within the weight)
+  unsigned a32;          // bytes between A pieces j, j + 1 (32 rows)
+  unsigned boff[8];      // B piece q relative to piece 0 (EPI row permutation), bytes
+  unsigned kb;           // K progress, bytes
+  __device__ __forceinline__ void adv(int k) { kb += 2 * k; }
+  __device__ __forceinline__ void piece(char* stage, int w, int j, int koff = 0) {
+    char* dst = stage + (w + 4 * j) * 1024;
+    if (j < 8)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(ra, (__attribute__((address_space(3))) void*)dst, 16, va,
+                                               kb + 2 * koff + j * a32, 0, 0);
+    else
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rb, (__attribute__((address_space(3))) void*)dst, 16, vb,
+                                               kb + 2 * koff + boff[j - 8], 0, 0);
+  }
+};
+
 template <bool INIT>
 __device__ __forceinline__ void mfma_t(f32x4& c, const bf16x8& b, const bf16x8& a) {
   if constexpr (INIT)
@@ -1167,7 +1196,7 @@ __device__ __forceinline__ void mfma_t(f32x4& c, const bf16x8& b, const bf16x8& 
 template <int EPI, bool INIT, bool READ, int NP, bool BAR, int DG = 4>
 __device__ __forceinline__ void tn5_sub(f32x4 (&acc)[8][8], const bf16x8 (&fa)[8], const bf16x8 (&fb)[8],
                                         bf16x8 (&ra)[8], bf16x8 (&rb)[8], const char* img, int offA, int offB,
-                                        Stager4<EPI>& st, char* dst, int w, char* dst2 = nullptr) {
+                                        Stager5<EPI>& st, char* dst, int w, char* dst2 = nullptr) {
   static_assert(NP % DG == 0 && NP <= 32, "DMA pieces per group");
 #pragma unroll
   for (int i = 0; i < 8; ++i) {
@@ -1190,11 +1219,13 @@ __device__ __forceinline__ void tn5_sub(f32x4 (&acc)[8][8], const bf16x8 (&fa)[8
 }
 
 template <int EPI>
-__device__ __forceinline__ void tn5_stager(Stager4<EPI>& st, const u16* A, const u16* B, long lda, long ldb, int m0,
+__device__ __forceinline__ void tn5_stager(Stager5<EPI>& st, const u16* A, const u16* B, long lda, long ldb, int m0,
                                            int n0, int w, int lane, int I) {
   const int lr = lane >> 3, ch = (lane & 7) ^ (4 * (w & 1) + (lr >> 1));
-  st.pa = A + (long)(m0 + 8 * w + lr) * lda + 8 * ch;
-  st.pb = B + (long)(b2_row<EPI>(w, n0, I) + lr) * ldb + 8 * ch;
+  st.ra = tile_rsrc(A + (long)m0 * lda);
+  st.va = (unsigned)(((8 * w + lr) * lda + 8 * ch) * 2);
+  st.vb = (unsigned)(((long)(b2_row<EPI>(w, n0, I) + lr) * ldb + 8 * ch) * 2);
+  st.kb = 0;
 }
 
 __device__ __forceinline__ void tn5_coords(int tile, int nbm, int nbn, int group, int& m0, int& n0) {
@@ -1320,21 +1351,20 @@ tn5_kernel(const u16* __restrict__ A, const u16* __restrict__ B, int K, long lda
   const int offB0 = rb * ROWB2 + 16 * swz2(rb, g), offB1 = rb * ROWB2 + 16 * swz2(rb, 4 + g);
   char* X = smem;
   char* Y = smem + G::STAGE;
-  Stager4<EPI> st;
-  st.a32 = 32 * lda;
+  Stager5<EPI> st;
+  st.rb = tile_rsrc(B);
+  st.a32 = (unsigned)(64 * lda);
 #pragma unroll
-  for (int q = 0; q < 8; ++q) st.boff[q] = (long)b2_koff<EPI, 4>(q) * ldb;
+  for (int q = 0; q < 8; ++q) st.boff[q] = (unsigned)(b2_koff<EPI, 4>(q) * ldb * 2);
   int m0, n0;
   tn5_coords(tile, nbm, nbn, group, m0, n0);
   tn5_stager(st, A, B, lda, ldb, m0, n0, w, lane, ea.I);
 #pragma unroll
   for (int j = 0; j < 16; ++j) st.piece(X, w, j);
-  st.pa += BK2;
-  st.pb += BK2;
+  st.adv(BK2);
 #pragma unroll
   for (int j = 0; j < 16; ++j) st.piece(Y, w, j);
-  st.pa += BK2;
-  st.pb += BK2;
+  st.adv(BK2);
   __builtin_amdgcn_s_waitcnt(waitcnt_imm(16, 15));  // K0 of the first tile (its K1 may fly)
   f32x4 acc[8][8];
   bf16x8 a0[8], b0[8], a1[8], b1[8];
@@ -1364,8 +1394,7 @@ tn5_kernel(const u16* __restrict__ A, const u16* __restrict__ B, int K, long lda
       }
       tn5_sub<EPI, false, true, DM ? 16 : 0, true>(acc, a1, b1, a0, b0, Y, offA0, offB0, st, X, w);
       if (DM) {
-        st.pa += BK2;
-        st.pb += BK2;
+        st.adv(BK2);
       }
       __builtin_amdgcn_s_waitcnt(waitcnt_imm(63, 0));
       tn5_sub<EPI, false, true, 0, false>(acc, a0, b0, a1, b1, Y, offA1, offB1, st, Y, w);
@@ -1375,8 +1404,7 @@ tn5_kernel(const u16* __restrict__ A, const u16* __restrict__ B, int K, long lda
         tn5_sub<EPI, false, false, 32, true>(acc, a1, b1, a0, b0, X, offA0, offB0, st, X, w, Y);
       } else {
         tn5_sub<EPI, false, true, 16, true>(acc, a1, b1, a0, b0, X, offA0, offB0, st, Y, w);
-        st.pa += BK2;
-        st.pb += BK2;
+        st.adv(BK2);
       }
     };
     if constexpr (NK2) {
@@ -1392,8 +1420,7 @@ tn5_kernel(const u16* __restrict__ A, const u16* __restrict__ B, int K, long lda
     tn5_store<EPI>(acc, ea, m0 + wm * 128, EPI == EPI_SWIGLU ? (n0 >> 1) + 64 * wn : n0 + wn * 128, wn, lane);
     __builtin_amdgcn_sched_barrier(0);
     if (!has_next) break;
-    st.pa += 2 * BK2;
-    st.pb += 2 * BK2;
+    st.adv(2 * BK2);
     if constexpr (EPI == EPI_SWIGLU)
       __builtin_amdgcn_s_waitcnt(waitcnt_imm(NST, 15));  // K0 and K1 landed (the 48 stores may fly)
     else
