@@ -901,6 +901,27 @@ __device__ __forceinline__ bf16x8 lds_tr(const char* base, int off) {
   return __builtin_bit_cast(bf16x8, v);
 }
 
+// vmcnt(0) as the builtin (not inline asm), so the waitcnt pass sees it: a kernel whose loop-invariant operands (Q /
+// K fragments) are global loads issued before the loop must drain them there; otherwise the pass merges the loop-entry
+// state with the back edge and puts a vmcnt(0) before the loop's first MFMA, which also waits for the NEXT tile's
+// prefetch every iteration (its latency fully exposed: profiles/r3_attention.md).
+__device__ __forceinline__ void vm_drain() { __builtin_amdgcn_s_waitcnt(0x0F70); }
+
+// max / sum over the 4 lanes l, l ^ 16, l ^ 32, l ^ 48 (one query column's key groups) with VALU lane swaps
+// (v_permlane32_swap / v_permlane16_swap) instead of ds_bpermute round trips through the LDS unit.
+__device__ __forceinline__ float xmax4(float x) {
+  auto a = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+  x = fmaxf(__uint_as_float(a[0]), __uint_as_float(a[1]));
+  auto b = __builtin_amdgcn_permlane16_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+  return fmaxf(__uint_as_float(b[0]), __uint_as_float(b[1]));
+}
+__device__ __forceinline__ float xsum4(float x) {
+  auto a = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+  x = __uint_as_float(a[0]) + __uint_as_float(a[1]);
+  auto b = __builtin_amdgcn_permlane16_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+  return __uint_as_float(b[0]) + __uint_as_float(b[1]);
+}
+
 template <int R, int NT>
 struct Stage {
   static constexpr int N = (R * 16) / NT;
@@ -925,7 +946,8 @@ struct Stage {
 };
 
 // DIAG (timing-only ablations, wrong results): bit0 no next-tile loads/stores, bit1 no softmax math,
-// bit2 no PV MFMAs, bit3 no QK MFMAs
+// bit2 no PV MFMAs, bit3 no QK MFMAs. bit4 (results exact): the round-2 schedule for A/B runs (no vm_drain before
+// the loop, per-tile row-sum shuffles through ds_bpermute).
 template <int NW, int DIAG = 0>
 __global__ __launch_bounds__(NW * 64, NW == 8 ? 4 : 2) void fwd3_kernel(const u16* __restrict__ qkv, u16* __restrict__ out,
                                                        float* __restrict__ lse, const int* __restrict__ cu, int nq,
@@ -952,6 +974,13 @@ __global__ __launch_bounds__(NW * 64, NW == 8 ? 4 : 2) void fwd3_kernel(const u1
   const int nkt = causal ? min((q0 + BM + 63) / 64, nkb) : nkb;
   Offs off;
   off.init(lane);
+  constexpr bool LEG = DIAG & 16;
+  bf16x8 qf[4];
+  if constexpr (!LEG) {  // Q first: the (in-order) wait for the first K / V tile then covers it
+    const u16* qp = qkv + (long)(start + qrow) * ld + h * D + 8 * g;
+#pragma unroll
+    for (int s = 0; s < 4; ++s) qf[s] = load_frag_global(qp + 32 * s, qok);
+  }
   {
     Stage<64, NT> tk, tv;
     tk.load(kbase, ld, len, tid);
@@ -959,16 +988,16 @@ __global__ __launch_bounds__(NW * 64, NW == 8 ? 4 : 2) void fwd3_kernel(const u1
     tk.store(Ks, tid);
     tv.store(Vs, tid);
   }
-  bf16x8 qf[4];
-  {
+  if constexpr (LEG) {
     const u16* qp = qkv + (long)(start + qrow) * ld + h * D + 8 * g;
 #pragma unroll
     for (int s = 0; s < 4; ++s) qf[s] = load_frag_global(qp + 32 * s, qok);
   }
+  if constexpr (!LEG) vm_drain();
   f32x4 o[8];
 #pragma unroll
   for (int dt = 0; dt < 8; ++dt) o[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
-  float m = -1e30f, l = 0.f;
+  float m = -1e30f, l = 0.f;  // l: this lane's partial row sum (its 16 keys per tile) unless LEG
   __syncthreads();
   for (int kt = 0; kt < nkt; ++kt) {
     const int k0 = kt * 64;
@@ -1002,8 +1031,12 @@ __global__ __launch_bounds__(NW * 64, NW == 8 ? 4 : 2) void fwd3_kernel(const u1
                          fmaxf(fmaxf(sc[1][0], sc[1][1]), fmaxf(sc[1][2], sc[1][3])));
       tmax = fmaxf(tmax, fmaxf(fmaxf(fmaxf(sc[2][0], sc[2][1]), fmaxf(sc[2][2], sc[2][3])),
                                fmaxf(fmaxf(sc[3][0], sc[3][1]), fmaxf(sc[3][2], sc[3][3]))));
-      tmax = fmaxf(tmax, __shfl_xor(tmax, 16, 64));
-      tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64));
+      if constexpr (LEG) {
+        tmax = fmaxf(tmax, __shfl_xor(tmax, 16, 64));
+        tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64));
+      } else {
+        tmax = xmax4(tmax);
+      }
       tmax *= sl2;
       if (__any(tmax > m + THR)) {  // deferred rescale (rare after the first tiles)
         const float mnew = fmaxf(m, tmax);
@@ -1022,8 +1055,10 @@ __global__ __launch_bounds__(NW * 64, NW == 8 ? 4 : 2) void fwd3_kernel(const u1
           sc[nt][i] = p;
           rs += p;
         }
-      rs += __shfl_xor(rs, 16, 64);
-      rs += __shfl_xor(rs, 32, 64);
+      if constexpr (LEG) {
+        rs += __shfl_xor(rs, 16, 64);
+        rs += __shfl_xor(rs, 32, 64);
+      }
       l += rs;
       }
 #pragma unroll
@@ -1041,6 +1076,7 @@ __global__ __launch_bounds__(NW * 64, NW == 8 ? 4 : 2) void fwd3_kernel(const u1
     }
     __syncthreads();
   }
+  if constexpr (!LEG) l = xsum4(l);
   if (qok) {
     const float inv = 1.f / l;
     u16* op = out + (long)(start + qrow) * nq * D + h * D + 4 * g;
@@ -1573,8 +1609,8 @@ __global__ __launch_bounds__(256, 1) void dq6_kernel(const u16* __restrict__ qkv
 // the wave's 16 rows), so both MFMA operands come from LDS. Rows past the sequence end are zero-filled by the
 // stager; entries never written by dkdv (queries past the last 64-query tile, key tiles above a wave's causal
 // diagonal) are never used: a wave skips tiles above its diagonal and each query column is independent.
-template <int NW>
-__global__ __launch_bounds__(NW * 64) void bwd_dq4_kernel(const u16* __restrict__ qkv, const u16* __restrict__ dst,
+template <int NW, bool LEG = false>
+__global__ __launch_bounds__(NW * 64, 4) void bwd_dq4_kernel(const u16* __restrict__ qkv, const u16* __restrict__ dst,
                                                           const int* __restrict__ cu, u16* __restrict__ dqkv, int nq,
                                                           int nkv, int lp, float scale, int causal,
                                                           const float* __restrict__ rcos = nullptr,
@@ -1601,6 +1637,15 @@ __global__ __launch_bounds__(NW * 64) void bwd_dq4_kernel(const u16* __restrict_
   const int nkt = causal ? min((q0 + BM + 63) / 64, nkb) : nkb;
   Offs off;
   off.init(lane);
+  // the wave's own dS^T column block: computed, not off.tr[wave] (a runtime index into a register array sends
+  // the array to scratch, and the scratch load in the loop waited on the next tile's prefetch: vmcnt(0))
+  int trw;
+  if constexpr (LEG) {
+    trw = off.tr[wave];
+  } else {
+    const int r = lane & 15, q = r >> 2, p = r & 3;
+    trw = img_off(4 * g + q, 2 * wave + (p >> 1)) + 8 * (p & 1);
+  }
   {
     Stage<64, NT> tk, ts;
     tk.load(kbase, ld, len, tid);
@@ -1623,7 +1668,7 @@ __global__ __launch_bounds__(NW * 64) void bwd_dq4_kernel(const u16* __restrict_
     if (!causal || k0 <= wfirst + 15) {
 #pragma unroll
       for (int ks = 0; ks < 2; ++ks) {
-        const bf16x8 db = lds_tr(Ss, off.tr[wave] + ks * 32 * ROWB);
+        const bf16x8 db = lds_tr(Ss, trw + ks * 32 * ROWB);
 #pragma unroll
         for (int dt = 0; dt < 8; ++dt) dq[dt] = mfma(lds_tr(Ks, off.tr[dt] + ks * 32 * ROWB), db, dq[dt]);
       }
@@ -1917,7 +1962,7 @@ __global__ __launch_bounds__(256, 2) void bwd_dkdv3_kernel(const u16* __restrict
 // That halves the serial chain of the causally heaviest key block (block 0 walks rep x nqt tiles), which is what
 // bounds this kernel: at 16 x 512 tokens the MFMA work alone is ~18 us, one tile step ~3 us of latency.
 // blockIdx.z = key block, heaviest first.
-template <int G>
+template <int G, bool LEG = false>
 __global__ __launch_bounds__(256 * G, G == 1 ? 2 : 1) void bwd_dkdv5_kernel(
     const u16* __restrict__ qkv, const u16* __restrict__ dout, const float* __restrict__ lse,
     const float* __restrict__ delta, const int* __restrict__ cu, u16* __restrict__ dqkv, int nq, int nkv, int total,
@@ -1971,6 +2016,7 @@ __global__ __launch_bounds__(256 * G, G == 1 ? 2 : 1) void bwd_dkdv5_kernel(
       vf[s] = load_frag_global(vp + 32 * s, kok);
     }
   }
+  if constexpr (!LEG) vm_drain();  // see vm_drain: K / V fragments are loop-invariant MFMA operands
   f32x4 dk[8], dv[8];
 #pragma unroll
   for (int dt = 0; dt < 8; ++dt) {
@@ -1993,7 +2039,10 @@ __global__ __launch_bounds__(256 * G, G == 1 ? 2 : 1) void bwd_dkdv5_kernel(
       tq.load(qkv + (long)(start + qn) * ld + hn * D, ld, qv, gtid);
       to.load(dout + (long)(start + qn) * ldo + hn * D, ldo, qv, gtid);
       if (gtid < 64 && gtid < qv) {
-        pl = lse[(long)hn * total + start + qn + gtid] * LOG2E;
+        // the LOG2E scaling happens at the LDS store: a multiply here made the compiler wait for this load, and
+        // with it (in-order vmcnt) for the Q / dO prefetch issued just before
+        pl = lse[(long)hn * total + start + qn + gtid];
+        if constexpr (LEG) pl *= LOG2E;
         pd = delta[(long)hn * total + start + qn + gtid];
       }
     }
@@ -2047,7 +2096,8 @@ __global__ __launch_bounds__(256 * G, G == 1 ? 2 : 1) void bwd_dkdv5_kernel(
       tq.store(Qs, gtid);
       to.store(Os, gtid);
       if (gtid < 64) {
-        Ls[gtid] = pl;
+        if constexpr (!LEG) asm volatile("" : "+v"(pl));  // keeps the multiply (and the load's wait) here
+        Ls[gtid] = LEG ? pl : pl * LOG2E;
         Dl[gtid] = pd;
       }
     }
@@ -2093,6 +2143,13 @@ __global__ __launch_bounds__(256 * G, G == 1 ? 2 : 1) void bwd_dkdv5_kernel(
   }
 }
 
+// SFTAMD_ATTN_LEGWAIT=1: the round-2 instruction schedule of fwd3 / dq4 / dK-dV v5 (prefetch latency exposed by
+// compiler-inserted vmcnt(0) waits), kept for same-process A/B timing only (tools/bench_attention.py ATTN_LEG=1)
+static bool attn_legacy_wait() {
+  const char* e = std::getenv("SFTAMD_ATTN_LEGWAIT");
+  return e && e[0] == '1';
+}
+
 // host launcher: G = 2 head groups when rep is even (SFTAMD_ATTN_GQA_SPLIT=0 forces 1)
 static void launch_dkdv5(const u16* qkv, const u16* dout, const float* lse, const float* delta, const int* cu,
                          u16* dqkv, int nq, int nkv, int total, int nseq, int max_seqlen, float sl2, float scale,
@@ -2102,7 +2159,11 @@ static void launch_dkdv5(const u16* qkv, const u16* dout, const float* lse, cons
   const char* e = std::getenv("SFTAMD_ATTN_GQA_SPLIT");
   const bool split = rep % 2 == 0 && !(e && e[0] == '0');
   dim3 grid(nkv, nseq, (max_seqlen + 63) / 64);
-  if (split)
+  const bool leg = attn_legacy_wait();
+  if (split && leg)
+    bwd_dkdv5_kernel<2, true><<<grid, 512, 0, st>>>(qkv, dout, lse, delta, cu, dqkv, nq, nkv, total, sl2, scale,
+                                                    causal, dst, lp, rcos, rsin);
+  else if (split)
     bwd_dkdv5_kernel<2><<<grid, 512, 0, st>>>(qkv, dout, lse, delta, cu, dqkv, nq, nkv, total, sl2, scale, causal,
                                               dst, lp, rcos, rsin);
   else
@@ -2242,9 +2303,14 @@ std::tuple<at::Tensor, at::Tensor> flash_fwd(const at::Tensor& qkv, const at::Te
     auto go3 = [&](auto w) {
       constexpr int NW = decltype(w)::value;
       dim3 g3(nq, nseq, (max_seqlen + NW * 16 - 1) / (NW * 16));
-      attn::fwd3_kernel<NW><<<g3, NW * 64, 0, cur_stream()>>>((const u16*)qkv.data_ptr(), (u16*)out.data_ptr(),
-                                                             lse.data_ptr<float>(), cu_c.data_ptr<int>(), nq, nkv,
-                                                             total, sl2, causal ? 1 : 0);
+      if (NW == 8 && attn::attn_legacy_wait())
+        attn::fwd3_kernel<NW, 16><<<g3, NW * 64, 0, cur_stream()>>>(
+            (const u16*)qkv.data_ptr(), (u16*)out.data_ptr(), lse.data_ptr<float>(), cu_c.data_ptr<int>(), nq, nkv,
+            total, sl2, causal ? 1 : 0);
+      else
+        attn::fwd3_kernel<NW><<<g3, NW * 64, 0, cur_stream()>>>((const u16*)qkv.data_ptr(), (u16*)out.data_ptr(),
+                                                               lse.data_ptr<float>(), cu_c.data_ptr<int>(), nq, nkv,
+                                                               total, sl2, causal ? 1 : 0);
     };
     if (nw == 4) go3(std::integral_constant<int, 4>()); else go3(std::integral_constant<int, 8>());
     SFT_LAUNCH_CHECK();
@@ -2424,10 +2490,15 @@ static at::Tensor flash_bwd_impl(const at::Tensor& dout, const at::Tensor& qkv, 
       SFT_LAUNCH_CHECK();
     }
     dim3 gq4(nq, nseq, (max_seqlen + 127) / 128);
-    attn::bwd_dq4_kernel<8><<<gq4, 512, 0, cur_stream()>>>((const u16*)qkv.data_ptr(), (const u16*)dst.data_ptr(),
-                                                           cu_c.data_ptr<int>(), (u16*)dqkv.data_ptr(), nq, nkv,
-                                                           (int)lp, (float)scale, causal ? 1 : 0,
-                                                           rope ? rcos : nullptr, rope ? rsin : nullptr);
+    if (attn::attn_legacy_wait())
+      attn::bwd_dq4_kernel<8, true><<<gq4, 512, 0, cur_stream()>>>(
+          (const u16*)qkv.data_ptr(), (const u16*)dst.data_ptr(), cu_c.data_ptr<int>(), (u16*)dqkv.data_ptr(), nq, nkv,
+          (int)lp, (float)scale, causal ? 1 : 0, rope ? rcos : nullptr, rope ? rsin : nullptr);
+    else
+      attn::bwd_dq4_kernel<8><<<gq4, 512, 0, cur_stream()>>>((const u16*)qkv.data_ptr(), (const u16*)dst.data_ptr(),
+                                                             cu_c.data_ptr<int>(), (u16*)dqkv.data_ptr(), nq, nkv,
+                                                             (int)lp, (float)scale, causal ? 1 : 0,
+                                                             rope ? rcos : nullptr, rope ? rsin : nullptr);
     SFT_LAUNCH_CHECK();
     rope_done = rope;
     return dqkv;

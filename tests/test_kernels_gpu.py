@@ -244,6 +244,17 @@ def test_flash_attention_bwd_gqa_grouped(causal, ds_mb, gqa, monkeypatch):
     _attn_case([130, 64], 12, 2, causal, "1", "3", "", ds_mb)
 
 
+@pytest.mark.parametrize("causal", [True, False])
+@pytest.mark.parametrize("leg", ["1", "0"])
+def test_flash_attention_legacy_schedule(causal, leg, monkeypatch):
+    """The round-2 instruction schedule (SFTAMD_ATTN_LEGWAIT=1: compiler vmcnt(0) before the first MFMA, per-tile
+    row-sum shuffles) and the default one (vm_drain before the loop, lane-partial row sums, permlane swaps, dq4's
+    computed column offset) both match the fp32 reference; the default forward == the legacy one to fp32 order."""
+    monkeypatch.setenv("SFTAMD_ATTN_LEGWAIT", leg)
+    _attn_case([100, 255, 64, 1, 300, 129], 8, 2, causal, "1", "3", "", "")
+    _attn_case([621, 700, 553, 754], 16, 4, causal, "1", "3", "", "")
+
+
 @pytest.mark.parametrize("path", ["default", "gqa0", "ds0", "mha", "dq6"])
 def test_flash_bwd_rope(path, monkeypatch):
     """flash_bwd_rope == inverse-RoPE(flash_bwd): fused into the dq / dK epilogues on the default path (one bf16

@@ -14,10 +14,19 @@ assert _ext.load(), _ext.load_error()
 B, T, NQ, NKV, D = int(os.environ.get("B", 8)), int(os.environ.get("T", 512)), 16, 4, 128
 M = B * T
 cu = torch.arange(0, (B + 1) * T, T, dtype=torch.int32, device="cuda")
+if os.environ.get("RAGGED"):  # the recipe's padding-free batches: B sequences of 553..754 tokens (mean ~621)
+    g = torch.Generator().manual_seed(0)
+    lens = torch.randint(553, 755, (B,), generator=g)
+    T = int(lens.max())
+    cu = torch.cat([torch.zeros(1, dtype=torch.long), lens.cumsum(0)]).to(torch.int32).cuda()
+    M = int(lens.sum())
+    print(f"ragged: {B} sequences, {M} tokens, max {T}")
 qkv = torch.randn(M, (NQ + 2 * NKV) * D, device="cuda", dtype=torch.bfloat16)
 dout = torch.randn(M, NQ * D, device="cuda", dtype=torch.bfloat16)
 sc = 1 / math.sqrt(D)
 flops_f = 4.0 * B * NQ * T * T * D / 2  # causal
+if os.environ.get("RAGGED"):
+    flops_f = sum(4.0 * NQ * int(n) ** 2 * D / 2 for n in (cu[1:] - cu[:-1]).tolist())
 ops = _ext.ops()
 
 
@@ -43,6 +52,8 @@ if os.environ.get("ATTN_QUICK"):
     CFGS = [("3", "8,1,serial"), ("3", "8,1,ds,perhead"), ("3", "8,1,ds,nosplit"), ("3", "8,1,ds")]
 if os.environ.get("ATTN_FWD"):  # ",fwd6": the GQA-stacked v6 forward (SFTAMD_ATTN_FWD6=1); ",dq6": v6 backward
     CFGS = [("3", "8,1,ds"), ("3", "8,1,ds,fwd6"), ("3", "8,1,ds,fwd6,dq6")]
+if os.environ.get("ATTN_LEG"):  # ",leg": the round-2 instruction schedule (SFTAMD_ATTN_LEGWAIT=1) vs the default
+    CFGS = [("3", "8,1,ds,leg"), ("3", "8,1,ds")]
 res = {}
 ref = None
 for rnd in range(3):
@@ -52,8 +63,9 @@ for rnd in range(3):
         os.environ["SFTAMD_ATTN_GQA_SPLIT"] = "0" if cfg.endswith(",nosplit") else "1"
         os.environ["SFTAMD_ATTN_FWD6"] = "1" if ",fwd6" in cfg else "0"
         os.environ["SFTAMD_ATTN_DQ6"] = "1" if ",dq6" in cfg else "0"
+        os.environ["SFTAMD_ATTN_LEGWAIT"] = "1" if ",leg" in cfg else "0"
         tag = cfg
-        cfg = cfg.replace(",perhead", "").replace(",nosplit", "").replace(",fwd6", "").replace(",dq6", "")
+        cfg = cfg.replace(",leg", "").replace(",perhead", "").replace(",nosplit", "").replace(",fwd6", "").replace(",dq6", "")
         os.environ["SFTAMD_ATTN_CFG"] = cfg.replace(",serial", "").replace(",ds", "")
         os.environ["SFTAMD_ATTN_CONC"] = "0" if cfg.endswith("serial") or cfg.endswith("ds") else "1"
         os.environ["SFTAMD_ATTN_DS_MB"] = "" if cfg.endswith("ds") else "0"

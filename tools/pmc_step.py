@@ -52,6 +52,7 @@ def main():
     ap.add_argument("dirs", nargs="+")
     ap.add_argument("--top", type=int, default=30)
     ap.add_argument("--out")
+    ap.add_argument("--raw", action="store_true", help="every collected counter per call (stall breakdowns)")
     a = ap.parse_args()
     per = defaultdict(dict)
     dur, calls = {}, {}
@@ -65,6 +66,19 @@ def main():
             calls[k] = max(calls.get(k, 0), v)
     rows = sorted(per, key=lambda k: -dur.get(k, 0.0))[: a.top]
     tot = sum(dur.values())
+    if a.raw:
+        names = sorted({n for k in rows for n in per[k]})
+        lines = ["| kernel | calls | us/call | " + " | ".join(names) + " |", "|---|---:|---:|" + "---:|" * len(names)]
+        for k in rows:
+            n = max(calls.get(k, 1), 1)
+            lines.append(f"| `{k}` | {n} | {dur.get(k, 0.0) / n:.1f} | "
+                         + " | ".join(f"{per[k].get(c, 0.0) / n:.4g}" for c in names) + " |")
+        txt = "\n".join(lines) + "\n"
+        if a.out:
+            with open(a.out, "w") as fh:
+                fh.write(txt)
+        print(txt)
+        return
     lines = ["# Per-kernel hardware counters of the training step (rocprofv3 --pmc, serialised dispatches)", "",
              f"sources: {', '.join('`' + d + '`' for d in a.dirs)}; kernel time in the PMC passes {tot / 1e3:.1f} ms", "",
              "| kernel | calls | time us | MFMA busy % | eff. clock GHz | LDS bank-conflict % | HBM read GB | read TB/s |",
