@@ -915,6 +915,20 @@ __device__ __forceinline__ float xmax4(float x) {
   auto b = __builtin_amdgcn_permlane16_swap(__float_as_uint(x), __float_as_uint(x), false, false);
   return fmaxf(__uint_as_float(b[0]), __uint_as_float(b[1]));
 }
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+// max of a 16-score tile in 8 v_max3_f32 (fmaxf's NaN canonicalisation doubles the VALU count; scores are finite
+// or -inf here)
+__device__ __forceinline__ float max3f(float a, float b, float c) {
+  float r;
+  asm("v_max3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+  return r;
+}
+__device__ __forceinline__ float max16(const f32x4 (&v)[4]) {
+  const float a = max3f(v[0][0], v[0][1], v[0][2]), b = max3f(v[0][3], v[1][0], v[1][1]);
+  const float c = max3f(v[1][2], v[1][3], v[2][0]), d = max3f(v[2][1], v[2][2], v[2][3]);
+  const float e = max3f(v[3][0], v[3][1], v[3][2]);
+  return max3f(max3f(a, b, c), max3f(d, e, v[3][3]), -INFINITY);
+}
 __device__ __forceinline__ float xsum4(float x) {
   auto a = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
   x = __uint_as_float(a[0]) + __uint_as_float(a[1]);
@@ -1019,18 +1033,31 @@ __global__ __launch_bounds__(NW * 64, NW == 8 ? 4 : 2) void fwd3_kernel(const u1
       if constexpr (!(DIAG & 2)) {
       const bool need_mask = (k0 + 64 > len) || (causal && k0 + 63 > wfirst);
       if (need_mask) {
+        if constexpr (LEG) {
 #pragma unroll
-        for (int nt = 0; nt < 4; ++nt)
+          for (int nt = 0; nt < 4; ++nt)
 #pragma unroll
-          for (int i = 0; i < 4; ++i) {
-            const int key = k0 + 16 * nt + 4 * g + i;
-            if (key >= len || (causal && key > qrow)) sc[nt][i] = -INFINITY;
-          }
+            for (int i = 0; i < 4; ++i) {
+              const int key = k0 + 16 * nt + 4 * g + i;
+              if (key >= len || (causal && key > qrow)) sc[nt][i] = -INFINITY;
+            }
+        } else {  // one compare + select per score: key offset 16 nt + i against the lane's last visible key
+          const int lim = (causal ? min(len - 1, qrow) : len - 1) - k0 - 4 * g;
+#pragma unroll
+          for (int nt = 0; nt < 4; ++nt)
+#pragma unroll
+            for (int i = 0; i < 4; ++i) sc[nt][i] = 16 * nt + i > lim ? -INFINITY : sc[nt][i];
+        }
       }
-      float tmax = fmaxf(fmaxf(fmaxf(sc[0][0], sc[0][1]), fmaxf(sc[0][2], sc[0][3])),
-                         fmaxf(fmaxf(sc[1][0], sc[1][1]), fmaxf(sc[1][2], sc[1][3])));
-      tmax = fmaxf(tmax, fmaxf(fmaxf(fmaxf(sc[2][0], sc[2][1]), fmaxf(sc[2][2], sc[2][3])),
-                               fmaxf(fmaxf(sc[3][0], sc[3][1]), fmaxf(sc[3][2], sc[3][3]))));
+      float tmax;
+      if constexpr (LEG) {
+        tmax = fmaxf(fmaxf(fmaxf(sc[0][0], sc[0][1]), fmaxf(sc[0][2], sc[0][3])),
+                     fmaxf(fmaxf(sc[1][0], sc[1][1]), fmaxf(sc[1][2], sc[1][3])));
+        tmax = fmaxf(tmax, fmaxf(fmaxf(fmaxf(sc[2][0], sc[2][1]), fmaxf(sc[2][2], sc[2][3])),
+                                 fmaxf(fmaxf(sc[3][0], sc[3][1]), fmaxf(sc[3][2], sc[3][3]))));
+      } else {
+        tmax = max16(sc);
+      }
       if constexpr (LEG) {
         tmax = fmaxf(tmax, __shfl_xor(tmax, 16, 64));
         tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64));
@@ -1047,17 +1074,31 @@ __global__ __launch_bounds__(NW * 64, NW == 8 ? 4 : 2) void fwd3_kernel(const u1
         m = mnew;
       }
       float rs = 0.f;
-#pragma unroll
-      for (int nt = 0; nt < 4; ++nt)
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const float p = exp2f(fmaf(sc[nt][i], sl2, -m));
-          sc[nt][i] = p;
-          rs += p;
-        }
       if constexpr (LEG) {
+#pragma unroll
+        for (int nt = 0; nt < 4; ++nt)
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const float p = exp2f(fmaf(sc[nt][i], sl2, -m));
+            sc[nt][i] = p;
+            rs += p;
+          }
         rs += __shfl_xor(rs, 16, 64);
         rs += __shfl_xor(rs, 32, 64);
+      } else {  // packed fp32 (v_pk_fma_f32 / v_pk_add_f32): two scores per VALU op around the exp2
+        f32x2 acc = {0.f, 0.f};
+        const f32x2 sl = {sl2, sl2}, nm = {-m, -m};
+#pragma unroll
+        for (int nt = 0; nt < 4; ++nt)
+#pragma unroll
+          for (int i = 0; i < 4; i += 2) {
+            const f32x2 t = __builtin_elementwise_fma(f32x2{sc[nt][i], sc[nt][i + 1]}, sl, nm);
+            const f32x2 p = {exp2f(t.x), exp2f(t.y)};
+            sc[nt][i] = p.x;
+            sc[nt][i + 1] = p.y;
+            acc += p;
+          }
+        rs = acc.x + acc.y;
       }
       l += rs;
       }
@@ -2059,20 +2100,48 @@ __global__ __launch_bounds__(256 * G, G == 1 ? 2 : 1) void bwd_dkdv5_kernel(
         }
       }
       const bool need_mask = (q0 + 64 > len) || (causal && wfirst + 15 > q0);
+      if constexpr (LEG) {
 #pragma unroll
-      for (int mt = 0; mt < 4; ++mt) {
-        const float4 L4 = *(const float4*)(Ls + 16 * mt + 4 * g);
-        const float4 D4 = *(const float4*)(Dl + 16 * mt + 4 * g);
-        const float Lv[4] = {L4.x, L4.y, L4.z, L4.w}, Dv[4] = {D4.x, D4.y, D4.z, D4.w};
+        for (int mt = 0; mt < 4; ++mt) {
+          const float4 L4 = *(const float4*)(Ls + 16 * mt + 4 * g);
+          const float4 D4 = *(const float4*)(Dl + 16 * mt + 4 * g);
+          const float Lv[4] = {L4.x, L4.y, L4.z, L4.w}, Dv[4] = {D4.x, D4.y, D4.z, D4.w};
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          float p = exp2f(fmaf(sc[mt][i], sl2, -Lv[i]));
-          if (need_mask) {
-            const int q = q0 + 16 * mt + 4 * g + i;
-            if (q >= len || (causal && key > q)) p = 0.f;
+          for (int i = 0; i < 4; ++i) {
+            float p = exp2f(fmaf(sc[mt][i], sl2, -Lv[i]));
+            if (need_mask) {
+              const int q = q0 + 16 * mt + 4 * g + i;
+              if (q >= len || (causal && key > q)) p = 0.f;
+            }
+            sc[mt][i] = p;
+            dp[mt][i] = p * (dp[mt][i] - Dv[i]);
           }
-          sc[mt][i] = p;
-          dp[mt][i] = p * (dp[mt][i] - Dv[i]);
+        }
+      } else {  // packed fp32 pairs around the exp2; the mask as one compare per score (query offset 16 mt + i
+                // visible iff first <= it <= last)
+        const int qb0 = q0 + 4 * g;
+        const int lo = (causal ? key : 0) - qb0, hi = len - 1 - qb0;
+        const f32x2 sl = {sl2, sl2};
+#pragma unroll
+        for (int mt = 0; mt < 4; ++mt) {
+          const float4 L4 = *(const float4*)(Ls + 16 * mt + 4 * g);
+          const float4 D4 = *(const float4*)(Dl + 16 * mt + 4 * g);
+          const f32x2 L[2] = {{-L4.x, -L4.y}, {-L4.z, -L4.w}}, Dd[2] = {{D4.x, D4.y}, {D4.z, D4.w}};
+#pragma unroll
+          for (int i = 0; i < 4; i += 2) {
+            const f32x2 t = __builtin_elementwise_fma(f32x2{sc[mt][i], sc[mt][i + 1]}, sl, L[i / 2]);
+            f32x2 p = {exp2f(t.x), exp2f(t.y)};
+            if (need_mask) {
+              const int o = 16 * mt + i;
+              p.x = (o < lo || o > hi) ? 0.f : p.x;
+              p.y = (o + 1 < lo || o + 1 > hi) ? 0.f : p.y;
+            }
+            const f32x2 d = p * (f32x2{dp[mt][i], dp[mt][i + 1]} - Dd[i / 2]);
+            sc[mt][i] = p.x;
+            sc[mt][i + 1] = p.y;
+            dp[mt][i] = d.x;
+            dp[mt][i + 1] = d.y;
+          }
         }
       }
       if (dst != nullptr && kok) {
