@@ -959,15 +959,89 @@ struct Stage {
   }
 };
 
+// 16 B per lane HBM -> LDS (global_load_lds): lane-linear LDS destination, the image swizzle applied to the source
+__device__ __forceinline__ void lds_dma16(const u16* src, char* dst) {
+  __builtin_amdgcn_global_load_lds((const void __attribute__((address_space(1)))*)src,
+                                   (void __attribute__((address_space(3)))*)dst, 16, 0, 0);
+}
+
+// One 64-key tile of the LDS-DMA forward (fwd3 DIAG bit5): issue the next tile's K / V pieces into stage nxt, then
+// S^T = K Q^T, the online softmax and O^T += V^T P^T from stage cur. cur / nxt are __restrict__ parameters of ONE
+// frame, so the waitcnt pass knows the DMA (tracked by vmcnt) never feeds these LDS reads; as plain pointers it put
+// a vmcnt(0) before the first V^T read, i.e. waited for the next tile inside this one.
+__device__ __forceinline__ void fwd_step_dma(const char* __restrict__ cur, char* __restrict__ nxt, bool pre, bool active,
+                                             const u16* kbase, const u16* vbase, long ld, long kvoff, int r0, int wave,
+                                             int k0, int len, int causal, int wfirst, int qrow, int g, float sl2,
+                                             const Offs& off, const bf16x8 (&qf)[4], f32x4 (&o)[8], float& m,
+                                             float& l) {
+  constexpr int TB = 64 * ROWB;
+  if (pre) {
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const long row = min(k0 + 64 + r0 + 32 * j, len - 1);
+      lds_dma16(kbase + row * ld + kvoff, nxt + (wave + 8 * j) * 1024);
+      lds_dma16(vbase + row * ld + kvoff, nxt + TB + (wave + 8 * j) * 1024);
+    }
+  }
+  if (!active) return;
+  const char* Ks = cur;
+  const char* Vs = cur + TB;
+  f32x4 sc[4];
+#pragma unroll
+  for (int nt = 0; nt < 4; ++nt) {
+    sc[nt] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int s = 0; s < 4; ++s) sc[nt] = mfma(lds_row(Ks, off.row[s] + nt * 16 * ROWB), qf[s], sc[nt]);
+  }
+  if ((k0 + 64 > len) || (causal && k0 + 63 > wfirst)) {
+    const int lim = (causal ? min(len - 1, qrow) : len - 1) - k0 - 4 * g;
+#pragma unroll
+    for (int nt = 0; nt < 4; ++nt)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) sc[nt][i] = 16 * nt + i > lim ? -INFINITY : sc[nt][i];
+  }
+  const float tmax = xmax4(max16(sc)) * sl2;
+  if (__any(tmax > m + THR)) {
+    const float mnew = fmaxf(m, tmax);
+    const float alpha = exp2f(m - mnew);
+    l *= alpha;
+#pragma unroll
+    for (int dt = 0; dt < 8; ++dt) o[dt] *= alpha;
+    m = mnew;
+  }
+  f32x2 acc = {0.f, 0.f};
+  const f32x2 sl = {sl2, sl2}, nm = {-m, -m};
+#pragma unroll
+  for (int nt = 0; nt < 4; ++nt)
+#pragma unroll
+    for (int i = 0; i < 4; i += 2) {
+      const f32x2 t = __builtin_elementwise_fma(f32x2{sc[nt][i], sc[nt][i + 1]}, sl, nm);
+      const f32x2 p = {exp2f(t.x), exp2f(t.y)};
+      sc[nt][i] = p.x;
+      sc[nt][i + 1] = p.y;
+      acc += p;
+    }
+  l += acc.x + acc.y;
+#pragma unroll
+  for (int ks = 0; ks < 2; ++ks) {
+    const bf16x8 pb = pack_acc(sc[2 * ks], sc[2 * ks + 1]);
+#pragma unroll
+    for (int dt = 0; dt < 8; ++dt) o[dt] = mfma(lds_tr(Vs, off.tr[dt] + ks * 32 * ROWB), pb, o[dt]);
+  }
+}
+
 // DIAG (timing-only ablations, wrong results): bit0 no next-tile loads/stores, bit1 no softmax math,
 // bit2 no PV MFMAs, bit3 no QK MFMAs. bit4 (results exact): the round-2 schedule for A/B runs (no vm_drain before
-// the loop, per-tile row-sum shuffles through ds_bpermute).
+// the loop, per-tile row-sum shuffles through ds_bpermute). bit5: K / V tiles by LDS-DMA into two stages (no VGPR
+// staging / ds_write, one barrier per tile; NW = 8).
 template <int NW, int DIAG = 0>
 __global__ __launch_bounds__(NW * 64, NW == 8 ? 4 : 2) void fwd3_kernel(const u16* __restrict__ qkv, u16* __restrict__ out,
                                                        float* __restrict__ lse, const int* __restrict__ cu, int nq,
                                                        int nkv, int total, float sl2, int causal) {
   constexpr int NT = NW * 64, BM = NW * 16, TB = 64 * ROWB;
-  __shared__ __attribute__((aligned(16))) char smem[2 * TB];
+  constexpr bool DMA = DIAG & 32;
+  static_assert(!DMA || NW == 8, "LDS-DMA staging: 8 waves x 2 pieces per 64-row image");
+  __shared__ __attribute__((aligned(16))) char smem[(DMA ? 4 : 2) * TB];
   char* Ks = smem;
   char* Vs = smem + TB;
   // grid (heads, sequences, q-blocks) with the last (causally heaviest) q-block dispatched first: LPT order
@@ -995,7 +1069,18 @@ __global__ __launch_bounds__(NW * 64, NW == 8 ? 4 : 2) void fwd3_kernel(const u1
 #pragma unroll
     for (int s = 0; s < 4; ++s) qf[s] = load_frag_global(qp + 32 * s, qok);
   }
-  {
+  // DMA: lane (wave w, l) fills LDS rows 4 (w + 8 j) + (l >> 4), position l & 15 with the chunk swz(row, l & 15) of
+  // that row (rows past the sequence end clamped to its last row: their keys are masked)
+  const int r0 = 4 * wave + (lane >> 4);
+  const long kvoff = 8 * swz(r0, lane & 15);
+  if constexpr (DMA) {
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const long row = min(r0 + 32 * j, len - 1);
+      lds_dma16(kbase + row * ld + kvoff, smem + (wave + 8 * j) * 1024);
+      lds_dma16(vbase + row * ld + kvoff, smem + TB + (wave + 8 * j) * 1024);
+    }
+  } else {
     Stage<64, NT> tk, tv;
     tk.load(kbase, ld, len, tid);
     tv.load(vbase, ld, len, tid);
@@ -1013,7 +1098,18 @@ __global__ __launch_bounds__(NW * 64, NW == 8 ? 4 : 2) void fwd3_kernel(const u1
   for (int dt = 0; dt < 8; ++dt) o[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
   float m = -1e30f, l = 0.f;  // l: this lane's partial row sum (its 16 keys per tile) unless LEG
   __syncthreads();
-  for (int kt = 0; kt < nkt; ++kt) {
+  if constexpr (DMA) {
+    for (int kt = 0; kt < nkt; ++kt) {
+      const int k0 = kt * 64;
+      const bool pre = kt + 1 < nkt;
+      // stage (kt + 1) & 1's last reads ended at the previous iteration's barrier
+      fwd_step_dma(smem + (kt & 1) * 2 * TB, smem + ((kt + 1) & 1) * 2 * TB, pre, !causal || k0 <= wfirst + 15,
+                   kbase, vbase, ld, kvoff, r0, wave, k0, len, causal, wfirst, qrow, g, sl2, off, qf, o, m, l);
+      if (pre) vm_drain();  // this lane's pieces of the next tile landed ...
+      __syncthreads();      // ... and every lane's; every wave is done reading this stage
+    }
+  }
+  for (int kt = 0; kt < (DMA ? 0 : nkt); ++kt) {
     const int k0 = kt * 64;
     const bool pre = !(DIAG & 1) && kt + 1 < nkt;
     Stage<64, NT> tk, tv;
@@ -2003,16 +2099,105 @@ __global__ __launch_bounds__(256, 2) void bwd_dkdv3_kernel(const u16* __restrict
 // That halves the serial chain of the causally heaviest key block (block 0 walks rep x nqt tiles), which is what
 // bounds this kernel: at 16 x 512 tokens the MFMA work alone is ~18 us, one tile step ~3 us of latency.
 // blockIdx.z = key block, heaviest first.
-template <int G, bool LEG = false>
+// One query tile of the LDS-DMA GQA dK/dV kernel (bwd_dkdv5_kernel<G, false, true>): issue the next tile's Q / dO
+// pieces (4 x 1 KB per image per wave, source-swizzled, rows past the sequence end clamped: their P and dS are masked
+// to 0) and its lse / delta loads, compute this tile from stage cur, then park lse (x LOG2E) / delta in stage nxt.
+// cur / nxt are __restrict__ parameters of one frame (see fwd_step_dma). Stage: Q image, dO image, lse[64], delta[64].
+__device__ __forceinline__ void dkdv_step_dma(const char* __restrict__ cur, char* __restrict__ nxt, bool pre, bool active,
+                                              const u16* qsrc, const u16* osrc, long ld, long ldo, int qrow0, int qlast,
+                                              long kvoff, int wave, const float* lsrc, const float* dsrc, int gtid,
+                                              int q0, int len, int causal, int key, int wfirst, int g, float sl2,
+                                              u16* drow, const Offs& off, const bf16x8 (&kf)[4],
+                                              const bf16x8 (&vf)[4], f32x4 (&dk)[8], f32x4 (&dv)[8]) {
+  constexpr int TB = 64 * ROWB;
+  float pl = 0.f, pd = 0.f;
+  if (pre) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const long row = min(qrow0 + 16 * j, qlast);
+      lds_dma16(qsrc + row * ld + kvoff, nxt + (wave + 4 * j) * 1024);
+      lds_dma16(osrc + row * ldo + kvoff, nxt + TB + (wave + 4 * j) * 1024);
+    }
+    if (gtid < 64 && lsrc != nullptr) {
+      pl = lsrc[gtid];
+      pd = dsrc[gtid];
+    }
+  }
+  if (active) {
+    const char* Qs = cur;
+    const char* Os = cur + TB;
+    const float* Ls = (const float*)(cur + 2 * TB);
+    const float* Dl = Ls + 64;
+    f32x4 sc[4], dp[4];
+#pragma unroll
+    for (int mt = 0; mt < 4; ++mt) {
+      sc[mt] = f32x4{0.f, 0.f, 0.f, 0.f};
+      dp[mt] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {
+        sc[mt] = mfma(lds_row(Qs, off.row[s] + mt * 16 * ROWB), kf[s], sc[mt]);
+        dp[mt] = mfma(lds_row(Os, off.row[s] + mt * 16 * ROWB), vf[s], dp[mt]);
+      }
+    }
+    const bool need_mask = (q0 + 64 > len) || (causal && wfirst + 15 > q0);
+    const int qb0 = q0 + 4 * g;
+    const int lo = (causal ? key : 0) - qb0, hi = len - 1 - qb0;
+    const f32x2 sl = {sl2, sl2};
+#pragma unroll
+    for (int mt = 0; mt < 4; ++mt) {
+      const float4 L4 = *(const float4*)(Ls + 16 * mt + 4 * g);
+      const float4 D4 = *(const float4*)(Dl + 16 * mt + 4 * g);
+      const f32x2 L[2] = {{-L4.x, -L4.y}, {-L4.z, -L4.w}}, Dd[2] = {{D4.x, D4.y}, {D4.z, D4.w}};
+#pragma unroll
+      for (int i = 0; i < 4; i += 2) {
+        const f32x2 t = __builtin_elementwise_fma(f32x2{sc[mt][i], sc[mt][i + 1]}, sl, L[i / 2]);
+        f32x2 p = {exp2f(t.x), exp2f(t.y)};
+        if (need_mask) {
+          const int o = 16 * mt + i;
+          p.x = (o < lo || o > hi) ? 0.f : p.x;
+          p.y = (o + 1 < lo || o + 1 > hi) ? 0.f : p.y;
+        }
+        const f32x2 d = p * (f32x2{dp[mt][i], dp[mt][i + 1]} - Dd[i / 2]);
+        sc[mt][i] = p.x;
+        sc[mt][i + 1] = p.y;
+        dp[mt][i] = d.x;
+        dp[mt][i + 1] = d.y;
+      }
+    }
+    if (drow != nullptr) {
+#pragma unroll
+      for (int mt = 0; mt < 4; ++mt) store4(drow + 16 * mt, dp[mt], 1.f);
+    }
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      const bf16x8 pb = pack_acc(sc[2 * ks], sc[2 * ks + 1]);
+      const bf16x8 db = pack_acc(dp[2 * ks], dp[2 * ks + 1]);
+#pragma unroll
+      for (int dt = 0; dt < 8; ++dt) {
+        dv[dt] = mfma(lds_tr(Os, off.tr[dt] + ks * 32 * ROWB), pb, dv[dt]);
+        dk[dt] = mfma(lds_tr(Qs, off.tr[dt] + ks * 32 * ROWB), db, dk[dt]);
+      }
+    }
+  }
+  if (pre && gtid < 64) {  // the next stage's lse / delta (that stage's last reads ended at the previous barrier)
+    float* Ln = (float*)(nxt + 2 * TB);
+    asm volatile("" : "+v"(pl));  // keeps the multiply (and the loads' wait) after this tile's math
+    Ln[gtid] = pl * LOG2E;
+    Ln[64 + gtid] = pd;
+  }
+}
+
+template <int G, bool LEG = false, bool DMA = false>
 __global__ __launch_bounds__(256 * G, G == 1 ? 2 : 1) void bwd_dkdv5_kernel(
     const u16* __restrict__ qkv, const u16* __restrict__ dout, const float* __restrict__ lse,
     const float* __restrict__ delta, const int* __restrict__ cu, u16* __restrict__ dqkv, int nq, int nkv, int total,
     float sl2, float scale, int causal, u16* __restrict__ dst, int lp, const float* __restrict__ rcos,
     const float* __restrict__ rsin) {
   constexpr int NT = 256, TB = 64 * ROWB, GB = 2 * TB + 2 * 64 * 4;  // per group: Q, dO images + lse, delta
-  __shared__ __attribute__((aligned(16))) char smem[G * GB];
+  static_assert(!DMA || !LEG, "the LDS-DMA variant has the current schedule only");
+  __shared__ __attribute__((aligned(16))) char smem[G * GB * (DMA ? 2 : 1)];  // DMA: two stages per group
   const int tid = threadIdx.x, grp = tid >> 8, gtid = tid & 255;
-  char* Qs = smem + grp * GB;
+  char* Qs = smem + grp * GB * (DMA ? 2 : 1);
   char* Os = Qs + TB;
   float* Ls = (float*)(Qs + 2 * TB);
   float* Dl = Ls + 64;
@@ -2035,13 +2220,25 @@ __global__ __launch_bounds__(256 * G, G == 1 ? 2 : 1) void bwd_dkdv5_kernel(
   off.init(lane);
   // iteration it -> head h = kvh * rep + grp * hpg + it / nt, query tile qt0 + it % nt (kept incrementally)
   int h = kvh * rep + grp * hpg, qt = qt0;
+  // DMA: lane (wave w, l) fills image rows 4 (w + 4 j) + (l >> 4), position l & 15 with chunk swz(row, l & 15)
+  const int qr0 = 4 * wave + (lane >> 4);
+  const long qoff = 8 * swz(qr0, lane & 15);
   {
     const int q0 = qt0 * 64, qv = len - q0;
-    Stage<64, NT> tq, to;
-    tq.load(qkv + (long)(start + q0) * ld + h * D, ld, qv, gtid);
-    to.load(dout + (long)(start + q0) * ldo + h * D, ldo, qv, gtid);
-    tq.store(Qs, gtid);
-    to.store(Os, gtid);
+    if constexpr (DMA) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const long row = start + min(q0 + qr0 + 16 * j, len - 1);
+        lds_dma16(qkv + row * ld + h * D + qoff, Qs + (wave + 4 * j) * 1024);
+        lds_dma16(dout + row * ldo + h * D + qoff, Os + (wave + 4 * j) * 1024);
+      }
+    } else {
+      Stage<64, NT> tq, to;
+      tq.load(qkv + (long)(start + q0) * ld + h * D, ld, qv, gtid);
+      to.load(dout + (long)(start + q0) * ldo + h * D, ldo, qv, gtid);
+      tq.store(Qs, gtid);
+      to.store(Os, gtid);
+    }
     if (gtid < 64) {
       Ls[gtid] = gtid < qv ? lse[(long)h * total + start + q0 + gtid] * LOG2E : 0.f;
       Dl[gtid] = gtid < qv ? delta[(long)h * total + start + q0 + gtid] : 0.f;
@@ -2065,7 +2262,32 @@ __global__ __launch_bounds__(256 * G, G == 1 ? 2 : 1) void bwd_dkdv5_kernel(
     dv[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
   }
   __syncthreads();
-  for (int it = 0; it < niter; ++it) {
+  if constexpr (DMA) {
+    for (int it = 0; it < niter; ++it) {
+      const int q0 = qt * 64;
+      const bool pre = it + 1 < niter;
+      int hn = h, qtn = qt + 1;
+      if (qtn == nqt) {
+        qtn = qt0;
+        ++hn;
+      }
+      const int qn = qtn * 64;
+      const long lo = (long)hn * total + start + qn;
+      const bool lok = pre && qn + gtid < len;
+      char* cur = Qs + (it & 1) * GB;
+      char* nxt = Qs + ((it + 1) & 1) * GB;
+      u16* drow = (dst != nullptr && kok) ? dst + ((long)(b * nq + h) * lp + key) * lp + q0 + 4 * g : nullptr;
+      dkdv_step_dma(cur, nxt, pre, !causal || wfirst <= q0 + 63, qkv + (long)start * ld + hn * D,
+                    dout + (long)start * ldo + hn * D, ld, ldo, qn + qr0, len - 1, qoff, wave,
+                    lok ? lse + lo : nullptr, delta + lo, gtid, q0, len, causal, key, wfirst, g, sl2, drow, off, kf,
+                    vf, dk, dv);
+      if (pre) vm_drain();  // this lane's pieces of the next tile landed ...
+      __syncthreads();      // ... and every lane's; every wave is done reading this stage
+      h = hn;
+      qt = qtn;
+    }
+  }
+  for (int it = 0; it < (DMA ? 0 : niter); ++it) {
     const int q0 = qt * 64;
     const bool pre = it + 1 < niter;
     int hn = h, qtn = qt + 1;
@@ -2229,7 +2451,12 @@ static void launch_dkdv5(const u16* qkv, const u16* dout, const float* lse, cons
   const bool split = rep % 2 == 0 && !(e && e[0] == '0');
   dim3 grid(nkv, nseq, (max_seqlen + 63) / 64);
   const bool leg = attn_legacy_wait();
-  if (split && leg)
+  const char* ed = std::getenv("SFTAMD_ATTN_BWD_DMA");
+  const bool dma = !leg && !(ed && ed[0] == '0');
+  if (split && dma)
+    bwd_dkdv5_kernel<2, false, true><<<grid, 512, 0, st>>>(qkv, dout, lse, delta, cu, dqkv, nq, nkv, total, sl2,
+                                                           scale, causal, dst, lp, rcos, rsin);
+  else if (split && leg)
     bwd_dkdv5_kernel<2, true><<<grid, 512, 0, st>>>(qkv, dout, lse, delta, cu, dqkv, nq, nkv, total, sl2, scale,
                                                     causal, dst, lp, rcos, rsin);
   else if (split)
@@ -2283,6 +2510,13 @@ static bool attn_dq6() {
 static bool attn_fwd6() {
   const char* e = std::getenv("SFTAMD_ATTN_FWD6");
   return e && e[0] == '1';
+}
+
+// fwd3 with K / V staged by LDS-DMA into two stages, one barrier per tile (default; SFTAMD_ATTN_FWD_DMA=0: register
+// staging). B16 x T512: 46.0 vs 51.8 us, ragged 16 x ~640: 65.0 vs 71.8 us (profiles/r3_attention.md)
+static bool attn_fwd_dma() {
+  const char* e = std::getenv("SFTAMD_ATTN_FWD_DMA");
+  return !(e && e[0] == '0');
 }
 
 static int attn_impl() {
@@ -2372,7 +2606,11 @@ std::tuple<at::Tensor, at::Tensor> flash_fwd(const at::Tensor& qkv, const at::Te
     auto go3 = [&](auto w) {
       constexpr int NW = decltype(w)::value;
       dim3 g3(nq, nseq, (max_seqlen + NW * 16 - 1) / (NW * 16));
-      if (NW == 8 && attn::attn_legacy_wait())
+      if (NW == 8 && attn_fwd_dma() && !attn::attn_legacy_wait())
+        attn::fwd3_kernel<8, 32><<<g3, 512, 0, cur_stream()>>>(
+            (const u16*)qkv.data_ptr(), (u16*)out.data_ptr(), lse.data_ptr<float>(), cu_c.data_ptr<int>(), nq, nkv,
+            total, sl2, causal ? 1 : 0);
+      else if (NW == 8 && attn::attn_legacy_wait())
         attn::fwd3_kernel<NW, 16><<<g3, NW * 64, 0, cur_stream()>>>(
             (const u16*)qkv.data_ptr(), (u16*)out.data_ptr(), lse.data_ptr<float>(), cu_c.data_ptr<int>(), nq, nkv,
             total, sl2, causal ? 1 : 0);

@@ -245,6 +245,46 @@ def test_flash_attention_bwd_gqa_grouped(causal, ds_mb, gqa, monkeypatch):
 
 
 @pytest.mark.parametrize("causal", [True, False])
+def test_flash_attention_fwd_lds_dma(causal, monkeypatch):
+    """fwd3 with K / V staged by LDS-DMA into two stages (the default, SFTAMD_ATTN_FWD_DMA=1; source-swizzled pieces,
+    rows past the sequence end clamped) == the fp32 reference on ragged GQA batches, and == the register-staged fwd3
+    (SFTAMD_ATTN_FWD_DMA=0) bitwise (same MFMA order, same softmax)."""
+    monkeypatch.setenv("SFTAMD_ATTN_FWD_DMA", "1")
+    _attn_case([100, 255, 64, 1, 300, 129], 8, 2, causal, "1", "3", "", "")
+    _attn_case([621, 700, 553, 754], 16, 4, causal, "1", "3", "", "")
+    torch.manual_seed(1)
+    lens = [700, 63, 130]
+    cu = torch.tensor([0] + list(torch.tensor(lens).cumsum(0)), dtype=torch.int32, device=DEV)
+    qkv = torch.randn(int(cu[-1]), 24 * 128, device=DEV, dtype=torch.bfloat16)
+    o1, l1 = _ext.ops().flash_fwd(qkv, cu, max(lens), 16, 4, 128, 0.088, causal)
+    monkeypatch.setenv("SFTAMD_ATTN_FWD_DMA", "0")
+    o0, l0 = _ext.ops().flash_fwd(qkv, cu, max(lens), 16, 4, 128, 0.088, causal)
+    assert torch.equal(o1, o0) and torch.equal(l1, l0)
+
+
+@pytest.mark.parametrize("causal", [True, False])
+@pytest.mark.parametrize("dma", ["1", "0"])
+def test_flash_attention_bwd_lds_dma(causal, dma, monkeypatch):
+    """GQA dK/dV with Q / dO staged by LDS-DMA into two stages per head group (the default; SFTAMD_ATTN_BWD_DMA=0:
+    register staging) == the fp32 reference (rep 4 / 2 / 3, ragged lengths, both dq paths), and the two stagings
+    agree bitwise (same MFMA order)."""
+    monkeypatch.setenv("SFTAMD_ATTN_BWD_DMA", dma)
+    _attn_case([100, 255, 64, 1, 300, 129], 8, 2, causal, "1", "3", "", "")
+    _attn_case([621, 700, 553, 754], 16, 4, causal, "1", "3", "", "")
+    _attn_case([200, 65], 12, 3, causal, "1", "3", "", "0")
+    torch.manual_seed(2)
+    lens = [700, 63, 130]
+    cu = torch.tensor([0] + list(torch.tensor(lens).cumsum(0)), dtype=torch.int32, device=DEV)
+    qkv = torch.randn(int(cu[-1]), 24 * 128, device=DEV, dtype=torch.bfloat16)
+    out, lse = _ext.ops().flash_fwd(qkv, cu, max(lens), 16, 4, 128, 0.088, causal)
+    dout = torch.randn_like(out)
+    g1 = _ext.ops().flash_bwd(dout, qkv, out, lse, cu, max(lens), 16, 4, 128, 0.088, causal)
+    monkeypatch.setenv("SFTAMD_ATTN_BWD_DMA", "0" if dma == "1" else "1")
+    g0 = _ext.ops().flash_bwd(dout, qkv, out, lse, cu, max(lens), 16, 4, 128, 0.088, causal)
+    assert torch.equal(g1, g0)
+
+
+@pytest.mark.parametrize("causal", [True, False])
 @pytest.mark.parametrize("leg", ["1", "0"])
 def test_flash_attention_legacy_schedule(causal, leg, monkeypatch):
     """The round-2 instruction schedule (SFTAMD_ATTN_LEGWAIT=1: compiler vmcnt(0) before the first MFMA, per-tile
