@@ -1738,6 +1738,39 @@ __global__ __launch_bounds__(256, 1) void dq6_kernel(const u16* __restrict__ qkv
   }
 }
 
+// One key tile of the LDS-DMA dq4 (bwd_dq4_kernel<8, false, true>): issue the next tile's K / dS^T pieces into stage
+// nxt (2 x 1 KB per image per wave, source-swizzled; rows past the sequence end are ZERO-filled with LDS stores, as
+// dQ sums K x dS^T over keys and the dS^T rows there were never written), then dQ^T += K^T dS^T from stage cur.
+// cur / nxt: __restrict__ parameters of one frame (see fwd_step_dma).
+__device__ __forceinline__ void dq_step_dma(const char* __restrict__ cur, char* __restrict__ nxt, bool pre, bool active,
+                                            const u16* ksrc, const u16* ssrc, long ld, long lp, int row0, int len,
+                                            long coff, int wave, int lane, int trw, const Offs& off, f32x4 (&dq)[8]) {
+  constexpr int TB = 64 * ROWB;
+  if (pre) {
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int row = row0 + 32 * j;
+      char* dk = nxt + (wave + 8 * j) * 1024;
+      if (row < len) {
+        lds_dma16(ksrc + row * ld + coff, dk);
+        lds_dma16(ssrc + row * lp + coff, dk + TB);
+      } else {
+        *(uint4*)(dk + 16 * lane) = make_uint4(0, 0, 0, 0);
+        *(uint4*)(dk + TB + 16 * lane) = make_uint4(0, 0, 0, 0);
+      }
+    }
+  }
+  if (!active) return;
+  const char* Ks = cur;
+  const char* Ss = cur + TB;
+#pragma unroll
+  for (int ks = 0; ks < 2; ++ks) {
+    const bf16x8 db = lds_tr(Ss, trw + ks * 32 * ROWB);
+#pragma unroll
+    for (int dt = 0; dt < 8; ++dt) dq[dt] = mfma(lds_tr(Ks, off.tr[dt] + ks * 32 * ROWB), db, dq[dt]);
+  }
+}
+
 // dQ from the materialised dS (v4 backward): bwd_dkdv3_kernel already computes dS = P o (dP - delta) for
 // every (query, key) pair of a head; it stores it transposed, dS^T[b][h][key][query] (bf16, lp x lp per head),
 // so dQ^T = K^T dS^T is ONE MFMA product per 64-key tile here — 16 MFMA per wave per tile instead of the 48 of
@@ -1746,7 +1779,7 @@ __global__ __launch_bounds__(256, 1) void dq6_kernel(const u16* __restrict__ qkv
 // the wave's 16 rows), so both MFMA operands come from LDS. Rows past the sequence end are zero-filled by the
 // stager; entries never written by dkdv (queries past the last 64-query tile, key tiles above a wave's causal
 // diagonal) are never used: a wave skips tiles above its diagonal and each query column is independent.
-template <int NW, bool LEG = false>
+template <int NW, bool LEG = false, bool DMA = false>
 __global__ __launch_bounds__(NW * 64, 4) void bwd_dq4_kernel(const u16* __restrict__ qkv, const u16* __restrict__ dst,
                                                           const int* __restrict__ cu, u16* __restrict__ dqkv, int nq,
                                                           int nkv, int lp, float scale, int causal,
@@ -1754,7 +1787,8 @@ __global__ __launch_bounds__(NW * 64, 4) void bwd_dq4_kernel(const u16* __restri
                                                           const float* __restrict__ rsin = nullptr) {
   static_assert(NW == 8, "the dS^T image is 128 queries wide: 8 waves x 16 rows");
   constexpr int NT = NW * 64, BM = NW * 16, TB = 64 * ROWB;
-  __shared__ __attribute__((aligned(16))) char smem[2 * TB];
+  static_assert(!DMA || !LEG, "the LDS-DMA variant has the current schedule only");
+  __shared__ __attribute__((aligned(16))) char smem[(DMA ? 4 : 2) * TB];  // DMA: two stages of (K, dS^T) images
   char* Ks = smem;
   char* Ss = smem + TB;
   // grid (heads, sequences, q-blocks) with the last (causally heaviest) q-block dispatched first: LPT order
@@ -1783,18 +1817,34 @@ __global__ __launch_bounds__(NW * 64, 4) void bwd_dq4_kernel(const u16* __restri
     const int r = lane & 15, q = r >> 2, p = r & 3;
     trw = img_off(4 * g + q, 2 * wave + (p >> 1)) + 8 * (p & 1);
   }
-  {
+  f32x4 dq[8];
+#pragma unroll
+  for (int dt = 0; dt < 8; ++dt) dq[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
+  // DMA: lane (wave w, l) fills image rows 4 (w + 8 j) + (l >> 4), position l & 15 with chunk swz(row, l & 15)
+  const int r0 = 4 * wave + (lane >> 4);
+  const long coff = 8 * swz(r0, lane & 15);
+  if constexpr (DMA) {  // tile 0 into stage 0 (the "next" tile of a virtual tile -1)
+    dq_step_dma(smem + 2 * TB, smem, true, false, kbase, sbase, ld, lp, r0, len, coff, wave, lane, trw, off, dq);
+  } else {
     Stage<64, NT> tk, ts;
     tk.load(kbase, ld, len, tid);
     ts.load(sbase, lp, len, tid);
     tk.store(Ks, tid);
     ts.store(Ss, tid);
   }
-  f32x4 dq[8];
-#pragma unroll
-  for (int dt = 0; dt < 8; ++dt) dq[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
+  if constexpr (DMA) vm_drain();
   __syncthreads();
-  for (int kt = 0; kt < nkt; ++kt) {
+  if constexpr (DMA) {
+    for (int kt = 0; kt < nkt; ++kt) {
+      const int k0 = kt * 64;
+      const bool pre = kt + 1 < nkt;
+      dq_step_dma(smem + (kt & 1) * 2 * TB, smem + ((kt + 1) & 1) * 2 * TB, pre, !causal || k0 <= wfirst + 15, kbase,
+                  sbase, ld, lp, k0 + 64 + r0, len, coff, wave, lane, trw, off, dq);
+      if (pre) vm_drain();  // this lane's pieces of the next tile landed ...
+      __syncthreads();      // ... and every lane's (LDS zero stores too); every wave is done reading this stage
+    }
+  }
+  for (int kt = 0; kt < (DMA ? 0 : nkt); ++kt) {
     const int k0 = kt * 64;
     const bool pre = kt + 1 < nkt;
     Stage<64, NT> tk, ts;
@@ -2797,7 +2847,14 @@ static at::Tensor flash_bwd_impl(const at::Tensor& dout, const at::Tensor& qkv, 
       SFT_LAUNCH_CHECK();
     }
     dim3 gq4(nq, nseq, (max_seqlen + 127) / 128);
-    if (attn::attn_legacy_wait())
+    // SFTAMD_ATTN_DQ_DMA=1: K / dS^T by LDS-DMA (measured neutral: 130.2 vs 129.9 us bwd at B16 x T512, r3_run40;
+    // this kernel streams dS^T at ~60 % of HBM bandwidth, the staging is not its limit)
+    const char* edq = std::getenv("SFTAMD_ATTN_DQ_DMA");
+    if (!attn::attn_legacy_wait() && edq && edq[0] == '1')
+      attn::bwd_dq4_kernel<8, false, true><<<gq4, 512, 0, cur_stream()>>>(
+          (const u16*)qkv.data_ptr(), (const u16*)dst.data_ptr(), cu_c.data_ptr<int>(), (u16*)dqkv.data_ptr(), nq, nkv,
+          (int)lp, (float)scale, causal ? 1 : 0, rope ? rcos : nullptr, rope ? rsin : nullptr);
+    else if (attn::attn_legacy_wait())
       attn::bwd_dq4_kernel<8, true><<<gq4, 512, 0, cur_stream()>>>(
           (const u16*)qkv.data_ptr(), (const u16*)dst.data_ptr(), cu_c.data_ptr<int>(), (u16*)dqkv.data_ptr(), nq, nkv,
           (int)lp, (float)scale, causal ? 1 : 0, rope ? rcos : nullptr, rope ? rsin : nullptr);

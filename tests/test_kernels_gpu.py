@@ -269,6 +269,7 @@ def test_flash_attention_bwd_lds_dma(causal, dma, monkeypatch):
     register staging) == the fp32 reference (rep 4 / 2 / 3, ragged lengths, both dq paths), and the two stagings
     agree bitwise (same MFMA order)."""
     monkeypatch.setenv("SFTAMD_ATTN_BWD_DMA", dma)
+    monkeypatch.setenv("SFTAMD_ATTN_DQ_DMA", dma)  # the opt-in LDS-DMA dq4 (zero-filled tail rows) rides along
     _attn_case([100, 255, 64, 1, 300, 129], 8, 2, causal, "1", "3", "", "")
     _attn_case([621, 700, 553, 754], 16, 4, causal, "1", "3", "", "")
     _attn_case([200, 65], 12, 3, causal, "1", "3", "", "0")
@@ -280,6 +281,7 @@ def test_flash_attention_bwd_lds_dma(causal, dma, monkeypatch):
     dout = torch.randn_like(out)
     g1 = _ext.ops().flash_bwd(dout, qkv, out, lse, cu, max(lens), 16, 4, 128, 0.088, causal)
     monkeypatch.setenv("SFTAMD_ATTN_BWD_DMA", "0" if dma == "1" else "1")
+    monkeypatch.setenv("SFTAMD_ATTN_DQ_DMA", "0" if dma == "1" else "1")
     g0 = _ext.ops().flash_bwd(dout, qkv, out, lse, cu, max(lens), 16, 4, 128, 0.088, causal)
     assert torch.equal(g1, g0)
 
