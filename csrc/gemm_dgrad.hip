@@ -196,6 +196,60 @@ __device__ __forceinline__ void epilogue(char* smem, f32x4 (&acc)[G::FM][G::FN],
   const int g = lane >> 4, c = lane & 15;
   float* ep = reinterpret_cast<float*>(smem) + w * 16 * G::EPI_LD;
   constexpr int SEGS = G::TM / 8;  // 16-byte output segments per m row
+  if constexpr (EPI == EPI_SWIGLU_BWD) {
+    // gate / up are streamed through a PD-deep register ring: unit u's loads are issued PD units ahead, so each
+    // 16-row slice no longer waits out an HBM round trip per 64-segment step (the straight version issued the two
+    // loads, waited vmcnt(0), computed and stored, 16 times per wave per tile)
+    constexpr int IT = 16 * SEGS / 64, U = G::FN * IT, PD = U < 4 ? U : 4;  // 8 measured no better (r3_run44)
+    static_assert(U >= PD, "ring deeper than the epilogue");
+    auto base_of = [&](int u) -> long {
+      const int jf = u / IT, seg = (u - jf * IT) * 64 + lane, row = seg / SEGS, cs = seg - row * SEGS;
+      const long m = m0 + wn * G::TN + 16 * jf + row;
+      return m * 2L * ea.N + n0 + wm * G::TM + cs * 8;
+    };
+    uint4 rg[PD][2];
+#pragma unroll
+    for (int u = 0; u < PD; ++u) {
+      const long b = base_of(u);
+      rg[u][0] = *(const uint4*)(ea.gu + b);
+      rg[u][1] = *(const uint4*)(ea.gu + b + ea.N);
+    }
+#pragma unroll
+    for (int jf = 0; jf < G::FN; ++jf) {
+#pragma unroll
+      for (int i = 0; i < G::FM; ++i) *(f32x4*)(ep + c * G::EPI_LD + 16 * i + 4 * g) = acc[i][jf];
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // wave-private region: writes before reads
+#pragma unroll
+      for (int it = 0; it < IT; ++it) {
+        const int u = jf * IT + it;
+        const int seg = it * 64 + lane, row = seg / SEGS, cs = seg - row * SEGS;
+        const float* pr = ep + row * G::EPI_LD + cs * 8;
+        float v[8], gt[8], up[8], dg[8], du[8];
+        *(float4*)&v[0] = *(const float4*)pr;
+        *(float4*)&v[4] = *(const float4*)(pr + 4);
+        unpack8(rg[u % PD][0], gt);
+        unpack8(rg[u % PD][1], up);
+        if (u + PD < U) {
+          const long b = base_of(u + PD);
+          rg[u % PD][0] = *(const uint4*)(ea.gu + b);
+          rg[u % PD][1] = *(const uint4*)(ea.gu + b + ea.N);
+        }
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {  // explicit fma, no contraction: every tile config rounds identically
+#pragma clang fp contract(off)
+          const float sg = 1.f / (1.f + __expf(-gt[e]));
+          const float t = v[e] * sg;
+          du[e] = t * gt[e];
+          dg[e] = (t * up[e]) * __builtin_fmaf(gt[e], 1.f - sg, 1.f);
+        }
+        const long b = base_of(u);
+        *(uint4*)(ea.out + b) = pack8(dg);
+        *(uint4*)(ea.out + b + ea.N) = pack8(du);
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // reads done before the next slice overwrites
+    }
+    return;
+  }
 #pragma unroll
   for (int jf = 0; jf < G::FN; ++jf) {
 #pragma unroll
