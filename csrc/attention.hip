@@ -973,12 +973,12 @@ __device__ __forceinline__ void fwd_step_dma(const char* __restrict__ cur, char*
                                              const u16* kbase, const u16* vbase, long ld, long kvoff, int r0, int wave,
                                              int k0, int len, int causal, int wfirst, int qrow, int g, float sl2,
                                              const Offs& off, const bf16x8 (&qf)[4], f32x4 (&o)[8], float& m,
-                                             float& l) {
+                                             float& l, int ahead = 64) {
   constexpr int TB = 64 * ROWB;
-  if (pre) {
+  if (pre) {  // the tile `ahead` keys past this one
 #pragma unroll
     for (int j = 0; j < 2; ++j) {
-      const long row = min(k0 + 64 + r0 + 32 * j, len - 1);
+      const long row = min(k0 + ahead + r0 + 32 * j, len - 1);
       lds_dma16(kbase + row * ld + kvoff, nxt + (wave + 8 * j) * 1024);
       lds_dma16(vbase + row * ld + kvoff, nxt + TB + (wave + 8 * j) * 1024);
     }
@@ -1030,6 +1030,150 @@ __device__ __forceinline__ void fwd_step_dma(const char* __restrict__ cur, char*
   }
 }
 
+// fwd7: 4 waves x 2 row groups of 16 queries (BM = 128), K / V by LDS-DMA into two stages. Every K fragment and V^T
+// fragment read from LDS feeds two MFMAs (half fwd3's LDS bytes per MFMA), and each wave carries two independent
+// softmax chains (ILP for the one wave per SIMD of each workgroup; 64 KB LDS -> 2 workgroups per CU).
+// Opt-in: SFTAMD_ATTN_FWD7=1.
+__device__ __forceinline__ void fwd7_step(const char* __restrict__ cur, char* __restrict__ nxt, bool pre,
+                                          const u16* kbase, const u16* vbase, long ld, long kvoff, int r0, int wave,
+                                          int k0, int len, int causal, int wfirst, int g, int ql, float sl2,
+                                          const Offs& off, const bf16x8 (&qf)[2][4], f32x4 (&o)[2][8], float (&m)[2],
+                                          float (&l)[2]) {
+  constexpr int TB = 64 * ROWB;
+  if (pre) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const long row = min(k0 + 64 + r0 + 16 * j, len - 1);
+      lds_dma16(kbase + row * ld + kvoff, nxt + (wave + 4 * j) * 1024);
+      lds_dma16(vbase + row * ld + kvoff, nxt + TB + (wave + 4 * j) * 1024);
+    }
+  }
+  if (causal && k0 > wfirst + 31) return;  // both row groups above this tile's diagonal
+  const char* Ks = cur;
+  const char* Vs = cur + TB;
+  f32x4 sc[2][4];
+#pragma unroll
+  for (int nt = 0; nt < 4; ++nt) {
+    sc[0][nt] = f32x4{0.f, 0.f, 0.f, 0.f};
+    sc[1][nt] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      const bf16x8 kf = lds_row(Ks, off.row[s] + nt * 16 * ROWB);
+      sc[0][nt] = mfma(kf, qf[0][s], sc[0][nt]);
+      sc[1][nt] = mfma(kf, qf[1][s], sc[1][nt]);
+    }
+  }
+  bf16x8 pb[2][2];
+#pragma unroll
+  for (int r = 0; r < 2; ++r) {
+    const int rfirst = wfirst + 16 * r, qrow = rfirst + ql;
+    if ((k0 + 64 > len) || (causal && k0 + 63 > rfirst)) {
+      const int lim = (causal ? min(len - 1, qrow) : len - 1) - k0 - 4 * g;
+#pragma unroll
+      for (int nt = 0; nt < 4; ++nt)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) sc[r][nt][i] = 16 * nt + i > lim ? -INFINITY : sc[r][nt][i];
+    }
+    const float tmax = xmax4(max16(sc[r])) * sl2;
+    if (__any(tmax > m[r] + THR)) {
+      const float mnew = fmaxf(m[r], tmax);
+      const float alpha = exp2f(m[r] - mnew);
+      l[r] *= alpha;
+#pragma unroll
+      for (int dt = 0; dt < 8; ++dt) o[r][dt] *= alpha;
+      m[r] = mnew;
+    }
+    f32x2 acc = {0.f, 0.f};
+    const f32x2 sl = {sl2, sl2}, nm = {-m[r], -m[r]};
+#pragma unroll
+    for (int nt = 0; nt < 4; ++nt)
+#pragma unroll
+      for (int i = 0; i < 4; i += 2) {
+        const f32x2 t = __builtin_elementwise_fma(f32x2{sc[r][nt][i], sc[r][nt][i + 1]}, sl, nm);
+        const f32x2 p = {exp2f(t.x), exp2f(t.y)};
+        sc[r][nt][i] = p.x;
+        sc[r][nt][i + 1] = p.y;
+        acc += p;
+      }
+    l[r] += acc.x + acc.y;
+    pb[r][0] = pack_acc(sc[r][0], sc[r][1]);
+    pb[r][1] = pack_acc(sc[r][2], sc[r][3]);
+  }
+#pragma unroll
+  for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+    for (int dt = 0; dt < 8; ++dt) {
+      const bf16x8 vf = lds_tr(Vs, off.tr[dt] + ks * 32 * ROWB);
+      o[0][dt] = mfma(vf, pb[0][ks], o[0][dt]);
+      o[1][dt] = mfma(vf, pb[1][ks], o[1][dt]);
+    }
+}
+
+__global__ __launch_bounds__(256, 2) void fwd7_kernel(const u16* __restrict__ qkv, u16* __restrict__ out,
+                                                      float* __restrict__ lse, const int* __restrict__ cu, int nq,
+                                                      int nkv, int total, float sl2, int causal) {
+  constexpr int BM = 128, TB = 64 * ROWB;
+  __shared__ __attribute__((aligned(16))) char smem[4 * TB];  // two stages of (K, V) images
+  const int h = blockIdx.x, b = blockIdx.y, qb = gridDim.z - 1 - blockIdx.z;  // LPT: heaviest q-block first
+  const int start = cu[b], len = cu[b + 1] - start;
+  SFT_DASSERT(start >= 0 && len >= 0 && start + len <= total);
+  const int q0 = qb * BM;
+  if (q0 >= len) return;
+  const int kvh = h / (nq / nkv);
+  const long ld = (long)(nq + 2 * nkv) * D;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, g = lane >> 4, ql = lane & 15;
+  const int wfirst = q0 + wave * 32;
+  const u16* kbase = qkv + (long)start * ld + (nq + kvh) * D;
+  const u16* vbase = qkv + (long)start * ld + (nq + nkv + kvh) * D;
+  const int nkb = (len + 63) / 64;
+  const int nkt = causal ? min((q0 + BM + 63) / 64, nkb) : nkb;
+  Offs off;
+  off.init(lane);
+  bf16x8 qf[2][4];
+#pragma unroll
+  for (int r = 0; r < 2; ++r) {
+    const int qrow = wfirst + 16 * r + ql;
+    const u16* qp = qkv + (long)(start + qrow) * ld + h * D + 8 * g;
+#pragma unroll
+    for (int s = 0; s < 4; ++s) qf[r][s] = load_frag_global(qp + 32 * s, qrow < len);
+  }
+  const int r0 = 4 * wave + (lane >> 4);
+  const long kvoff = 8 * swz(r0, lane & 15);
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const long row = min(r0 + 16 * j, len - 1);
+    lds_dma16(kbase + row * ld + kvoff, smem + (wave + 4 * j) * 1024);
+    lds_dma16(vbase + row * ld + kvoff, smem + TB + (wave + 4 * j) * 1024);
+  }
+  vm_drain();
+  f32x4 o[2][8];
+  float m[2] = {-1e30f, -1e30f}, l[2] = {0.f, 0.f};
+#pragma unroll
+  for (int r = 0; r < 2; ++r)
+#pragma unroll
+    for (int dt = 0; dt < 8; ++dt) o[r][dt] = f32x4{0.f, 0.f, 0.f, 0.f};
+  __syncthreads();
+  for (int kt = 0; kt < nkt; ++kt) {
+    const bool pre = kt + 1 < nkt;
+    fwd7_step(smem + (kt & 1) * 2 * TB, smem + ((kt + 1) & 1) * 2 * TB, pre, kbase, vbase, ld, kvoff, r0, wave, kt * 64,
+              len, causal, wfirst, g, ql, sl2, off, qf, o, m, l);
+    if (pre) vm_drain();
+    __syncthreads();
+  }
+#pragma unroll
+  for (int r = 0; r < 2; ++r) {
+    const float lt = xsum4(l[r]);
+    const int qrow = wfirst + 16 * r + ql;
+    if (qrow < len) {
+      const float inv = 1.f / lt;
+      u16* op = out + (long)(start + qrow) * nq * D + h * D + 4 * g;
+#pragma unroll
+      for (int dt = 0; dt < 8; ++dt) store4(op + 16 * dt, o[r][dt], inv);
+      if (g == 0) lse[(long)h * total + start + qrow] = (m[r] + log2f(lt)) * LN2;
+    }
+  }
+}
+
 // DIAG (timing-only ablations, wrong results): bit0 no next-tile loads/stores, bit1 no softmax math,
 // bit2 no PV MFMAs, bit3 no QK MFMAs. bit4 (results exact): the round-2 schedule for A/B runs (no vm_drain before
 // the loop, per-tile row-sum shuffles through ds_bpermute). bit5: K / V tiles by LDS-DMA into two stages (no VGPR
@@ -1039,9 +1183,10 @@ __global__ __launch_bounds__(NW * 64, NW == 8 ? 4 : 2) void fwd3_kernel(const u1
                                                        float* __restrict__ lse, const int* __restrict__ cu, int nq,
                                                        int nkv, int total, float sl2, int causal) {
   constexpr int NT = NW * 64, BM = NW * 16, TB = 64 * ROWB;
-  constexpr bool DMA = DIAG & 32;
+  constexpr bool DMA3 = DIAG & 64;  // three stages, two tiles in flight (implies DMA)
+  constexpr bool DMA = (DIAG & 32) || DMA3;
   static_assert(!DMA || NW == 8, "LDS-DMA staging: 8 waves x 2 pieces per 64-row image");
-  __shared__ __attribute__((aligned(16))) char smem[(DMA ? 4 : 2) * TB];
+  __shared__ __attribute__((aligned(16))) char smem[(DMA3 ? 6 : DMA ? 4 : 2) * TB];
   char* Ks = smem;
   char* Vs = smem + TB;
   // grid (heads, sequences, q-blocks) with the last (causally heaviest) q-block dispatched first: LPT order
@@ -1073,7 +1218,10 @@ __global__ __launch_bounds__(NW * 64, NW == 8 ? 4 : 2) void fwd3_kernel(const u1
   // that row (rows past the sequence end clamped to its last row: their keys are masked)
   const int r0 = 4 * wave + (lane >> 4);
   const long kvoff = 8 * swz(r0, lane & 15);
-  if constexpr (DMA) {
+  if constexpr (DMA3) {
+    // tiles 0 and 1 are issued by the loop's first two (compute-free) iterations: the same code instance as every
+    // later DMA, so the waitcnt pass sees them in the loop's alias scopes and adds no vmcnt(0) before the loop
+  } else if constexpr (DMA) {
 #pragma unroll
     for (int j = 0; j < 2; ++j) {
       const long row = min(r0 + 32 * j, len - 1);
@@ -1098,7 +1246,22 @@ __global__ __launch_bounds__(NW * 64, NW == 8 ? 4 : 2) void fwd3_kernel(const u1
   for (int dt = 0; dt < 8; ++dt) o[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
   float m = -1e30f, l = 0.f;  // l: this lane's partial row sum (its 16 keys per tile) unless LEG
   __syncthreads();
-  if constexpr (DMA) {
+  if constexpr (DMA3) {
+    int sc = 1;  // stage of tile kt (kt = -2, -1: no tile, the DMA of tiles 0, 1); tile kt + 2 -> stage (sc + 2) % 3
+    for (int kt = -2; kt < nkt; ++kt) {
+      const int k0 = kt * 64;
+      const bool pre2 = kt + 2 < nkt;
+      const int sn = sc == 0 ? 2 : sc - 1;
+      fwd_step_dma(smem + sc * 2 * TB, smem + sn * 2 * TB, pre2, kt >= 0 && (!causal || k0 <= wfirst + 15), kbase,
+                   vbase, ld, kvoff, r0, wave, k0, len, causal, wfirst, qrow, g, sl2, off, qf, o, m, l, 128);
+      // vmcnt(4) + lgkmcnt(0): tile kt + 1 landed (kt + 2's 4 pieces may fly), this wave's LDS reads are done; a
+      // plain s_barrier, as __syncthreads' fence would wait for the in-flight DMA too (vmcnt(0))
+      if (pre2) __builtin_amdgcn_s_waitcnt(0x0074);
+      else __builtin_amdgcn_s_waitcnt(0x0070);
+      __builtin_amdgcn_s_barrier();
+      sc = sc == 2 ? 0 : sc + 1;
+    }
+  } else if constexpr (DMA) {
     for (int kt = 0; kt < nkt; ++kt) {
       const int k0 = kt * 64;
       const bool pre = kt + 1 < nkt;
@@ -2562,6 +2725,12 @@ static bool attn_fwd6() {
   return e && e[0] == '1';
 }
 
+// SFTAMD_ATTN_FWD7=1: the 4-wave, two-row-group LDS-DMA forward (fwd7_kernel)
+static bool attn_fwd7() {
+  const char* e = std::getenv("SFTAMD_ATTN_FWD7");
+  return e && e[0] == '1';
+}
+
 // fwd3 with K / V staged by LDS-DMA into two stages, one barrier per tile (default; SFTAMD_ATTN_FWD_DMA=0: register
 // staging). B16 x T512: 46.0 vs 51.8 us, ragged 16 x ~640: 65.0 vs 71.8 us (profiles/r3_attention.md)
 static bool attn_fwd_dma() {
@@ -2649,6 +2818,15 @@ std::tuple<at::Tensor, at::Tensor> flash_fwd(const at::Tensor& qkv, const at::Te
     SFT_LAUNCH_CHECK();
     return {out, lse};
   }
+  if (attn_impl() == 3 && attn_fwd7() && !attn::attn_legacy_wait()) {
+    SFT_TRACE("attn.fwd7");
+    dim3 g7(nq, nseq, (max_seqlen + 127) / 128);
+    attn::fwd7_kernel<<<g7, 256, 0, cur_stream()>>>((const u16*)qkv.data_ptr(), (u16*)out.data_ptr(),
+                                                    lse.data_ptr<float>(), cu_c.data_ptr<int>(), nq, nkv, total, sl2,
+                                                    causal ? 1 : 0);
+    SFT_LAUNCH_CHECK();
+    return {out, lse};
+  }
   if (attn_impl() == 3) {
     int nw, nbuf;
     attn_cfg(nw, nbuf);
@@ -2656,7 +2834,12 @@ std::tuple<at::Tensor, at::Tensor> flash_fwd(const at::Tensor& qkv, const at::Te
     auto go3 = [&](auto w) {
       constexpr int NW = decltype(w)::value;
       dim3 g3(nq, nseq, (max_seqlen + NW * 16 - 1) / (NW * 16));
-      if (NW == 8 && attn_fwd_dma() && !attn::attn_legacy_wait())
+      const char* e3 = std::getenv("SFTAMD_ATTN_FWD_DMA3");
+      if (NW == 8 && e3 && e3[0] == '1' && !attn::attn_legacy_wait())
+        attn::fwd3_kernel<8, 64><<<g3, 512, 0, cur_stream()>>>(
+            (const u16*)qkv.data_ptr(), (u16*)out.data_ptr(), lse.data_ptr<float>(), cu_c.data_ptr<int>(), nq, nkv,
+            total, sl2, causal ? 1 : 0);
+      else if (NW == 8 && attn_fwd_dma() && !attn::attn_legacy_wait())
         attn::fwd3_kernel<8, 32><<<g3, 512, 0, cur_stream()>>>(
             (const u16*)qkv.data_ptr(), (u16*)out.data_ptr(), lse.data_ptr<float>(), cu_c.data_ptr<int>(), nq, nkv,
             total, sl2, causal ? 1 : 0);

@@ -263,6 +263,40 @@ def test_flash_attention_fwd_lds_dma(causal, monkeypatch):
 
 
 @pytest.mark.parametrize("causal", [True, False])
+def test_flash_attention_fwd_three_stage_ring(causal, monkeypatch):
+    """fwd3 with a three-stage LDS-DMA ring (two K / V tiles in flight, counted vmcnt + fence-free barrier;
+    SFTAMD_ATTN_FWD_DMA3=1) == the fp32 reference and == the two-stage default bitwise; one-tile sequences too."""
+    monkeypatch.setenv("SFTAMD_ATTN_FWD_DMA3", "1")
+    _attn_case([100, 255, 64, 1, 300, 129], 8, 2, causal, "1", "3", "", "")
+    _attn_case([621, 700, 553, 754], 16, 4, causal, "1", "3", "", "")
+    torch.manual_seed(4)
+    lens = [700, 63, 130, 17, 64, 65]
+    cu = torch.tensor([0] + list(torch.tensor(lens).cumsum(0)), dtype=torch.int32, device=DEV)
+    qkv = torch.randn(int(cu[-1]), 24 * 128, device=DEV, dtype=torch.bfloat16)
+    o1, l1 = _ext.ops().flash_fwd(qkv, cu, max(lens), 16, 4, 128, 0.088, causal)
+    monkeypatch.setenv("SFTAMD_ATTN_FWD_DMA3", "0")
+    o0, l0 = _ext.ops().flash_fwd(qkv, cu, max(lens), 16, 4, 128, 0.088, causal)
+    assert torch.equal(o1, o0) and torch.equal(l1, l0)
+
+
+@pytest.mark.parametrize("causal", [True, False])
+def test_flash_attention_fwd7_two_row_groups(causal, monkeypatch):
+    """fwd7 (4 waves x 2 row groups, LDS-DMA K / V; SFTAMD_ATTN_FWD7=1) == the fp32 reference on ragged GQA batches,
+    and == the default forward bitwise (same per-row MFMA order, softmax and rescale decisions)."""
+    monkeypatch.setenv("SFTAMD_ATTN_FWD7", "1")
+    _attn_case([100, 255, 64, 1, 300, 129], 8, 2, causal, "1", "3", "", "")
+    _attn_case([621, 700, 553, 754], 16, 4, causal, "1", "3", "", "")
+    torch.manual_seed(3)
+    lens = [700, 63, 130, 17]
+    cu = torch.tensor([0] + list(torch.tensor(lens).cumsum(0)), dtype=torch.int32, device=DEV)
+    qkv = torch.randn(int(cu[-1]), 24 * 128, device=DEV, dtype=torch.bfloat16)
+    o1, l1 = _ext.ops().flash_fwd(qkv, cu, max(lens), 16, 4, 128, 0.088, causal)
+    monkeypatch.setenv("SFTAMD_ATTN_FWD7", "0")
+    o0, l0 = _ext.ops().flash_fwd(qkv, cu, max(lens), 16, 4, 128, 0.088, causal)
+    assert torch.equal(o1, o0) and torch.equal(l1, l0)
+
+
+@pytest.mark.parametrize("causal", [True, False])
 @pytest.mark.parametrize("dma", ["1", "0"])
 def test_flash_attention_bwd_lds_dma(causal, dma, monkeypatch):
     """GQA dK/dV with Q / dO staged by LDS-DMA into two stages per head group (the default; SFTAMD_ATTN_BWD_DMA=0:

@@ -53,7 +53,7 @@ if os.environ.get("ATTN_QUICK"):
 if os.environ.get("ATTN_FWD"):  # ",fwd6": the GQA-stacked v6 forward (SFTAMD_ATTN_FWD6=1); ",dq6": v6 backward
     CFGS = [("3", "8,1,ds"), ("3", "8,1,ds,fwd6"), ("3", "8,1,ds,fwd6,dq6")]
 if os.environ.get("ATTN_LEG"):  # ",leg": the round-2 instruction schedule (SFTAMD_ATTN_LEGWAIT=1) vs the default
-    CFGS = [("3", "8,1,ds,leg"), ("3", "8,1,ds,nodma"), ("3", "8,1,ds,nobdma"), ("3", "8,1,ds")]
+    CFGS = [("3", "8,1,ds,leg"), ("3", "8,1,ds"), ("3", "8,1,ds,dma3")]
 res = {}
 ref = None
 for rnd in range(int(os.environ.get("ROUNDS", 3))):
@@ -64,10 +64,12 @@ for rnd in range(int(os.environ.get("ROUNDS", 3))):
         os.environ["SFTAMD_ATTN_FWD6"] = "1" if ",fwd6" in cfg else "0"
         os.environ["SFTAMD_ATTN_DQ6"] = "1" if ",dq6" in cfg else "0"
         os.environ["SFTAMD_ATTN_LEGWAIT"] = "1" if ",leg" in cfg else "0"
+        os.environ["SFTAMD_ATTN_FWD7"] = "1" if ",fwd7" in cfg else "0"
+        os.environ["SFTAMD_ATTN_FWD_DMA3"] = "1" if ",dma3" in cfg else "0"
         os.environ["SFTAMD_ATTN_FWD_DMA"] = "0" if ",nodma" in cfg else "1"
         os.environ["SFTAMD_ATTN_BWD_DMA"] = "0" if ",nodma" in cfg or ",nobdma" in cfg else "1"
         tag = cfg
-        cfg = cfg.replace(",leg", "").replace(",nodma", "").replace(",nobdma", "").replace(",perhead", "").replace(",nosplit", "").replace(",fwd6", "").replace(",dq6", "")
+        cfg = cfg.replace(",leg", "").replace(",nodma", "").replace(",nobdma", "").replace(",fwd7", "").replace(",dma3", "").replace(",perhead", "").replace(",nosplit", "").replace(",fwd6", "").replace(",dq6", "")
         os.environ["SFTAMD_ATTN_CFG"] = cfg.replace(",serial", "").replace(",ds", "")
         os.environ["SFTAMD_ATTN_CONC"] = "0" if cfg.endswith("serial") or cfg.endswith("ds") else "1"
         os.environ["SFTAMD_ATTN_DS_MB"] = "" if cfg.endswith("ds") else "0"
