@@ -205,6 +205,52 @@ __device__ __forceinline__ void store_tile(const f32x4 (&acc)[8][8], const Epi& 
   const int g = lane >> 4, ii = lane & 15;
   const int cofs = col0 + 16 * (g & 1) + 8 * (g >> 1);
   float ss = 0.f;
+  if (EPI == EPI_SWIGLU_BWD || (ea.flags & 1)) {
+    // the epilogue's loads (gate / up, or the accumulated C) stream through a PD-deep register ring over the 32
+    // (fragment row, column pair) units: unit u + PD is issued while unit u computes, instead of one exposed HBM
+    // round trip per unit (the fragment registers of the main loop are free here)
+    constexpr int U = 32, PD = 8, NL = EPI == EPI_SWIGLU_BWD ? 2 : 1;
+    const u16* src = EPI == EPI_SWIGLU_BWD ? ea.gu : ea.C;
+    auto at = [&](int u) -> long { return (long)(row0 + 16 * (u >> 2) + ii) * ea.ldc + cofs + 32 * (u & 3); };
+    uint4 rg[PD][NL];
+#pragma unroll
+    for (int u = 0; u < PD; ++u)
+#pragma unroll
+      for (int k = 0; k < NL; ++k) rg[u][k] = *(const uint4*)(src + at(u) + k * ea.I);
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      float v[8], a[8], b[8];
+      gather8(acc, u >> 2, u & 3, v);
+      unpack8(rg[u % PD][0], a);
+      if constexpr (NL == 2) unpack8(rg[u % PD][NL - 1], b);
+      if (u + PD < U) {
+#pragma unroll
+        for (int k = 0; k < NL; ++k) rg[u % PD][k] = *(const uint4*)(src + at(u + PD) + k * ea.I);
+      }
+      u16* out = ea.C + at(u);
+      if constexpr (EPI == EPI_STORE) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[e] += a[e];
+        if (nrm != nullptr) {
+#pragma unroll
+          for (int e = 0; e < 8; ++e) ss += v[e] * v[e];
+        }
+        *(uint4*)out = pack8(v);
+      } else {  // SWIGLU_BWD: v = dact (fp32, never stored), a = gate, b = up; no contraction (config-independent)
+        float dg[8], du[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+#pragma clang fp contract(off)
+          const float sg = 1.f / (1.f + __expf(-a[e]));
+          const float t = v[e] * sg;
+          du[e] = t * a[e];
+          dg[e] = (t * b[e]) * __builtin_fmaf(a[e], 1.f - sg, 1.f);
+        }
+        *(uint4*)out = pack8(dg);
+        *(uint4*)(out + ea.I) = pack8(du);
+      }
+    }
+  } else {
 #pragma unroll
   for (int i = 0; i < 8; ++i) {
     const long row = row0 + 16 * i + ii;
@@ -240,6 +286,7 @@ __device__ __forceinline__ void store_tile(const f32x4 (&acc)[8][8], const Epi& 
         *(uint4*)(out + ea.I) = pack8(du);
       }
     }
+  }
   }
   if (nrm != nullptr) {  // 8 slots per tile (the 8-wave kernels' layout): waves 0..3 write theirs and zero w + 4, so
     ss = wave_sum(ss);    // slots parked in an uninitialised split-K buffer (hybrid launches) are never garbage
