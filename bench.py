@@ -95,8 +95,9 @@ def parse(argv=None):
     ap.add_argument("--eval-batch", type=int, default=32,
                     help="--recipe: per-device eval batch (eval loss is token-weighted, independent of it)")
     # hang protection for the first RCCL multi-rank runs (utils/heartbeat.py, launch.py): a wall-clock bound on the
-    # whole run, a no-progress bound per rank (also the process group's collective timeout), and opt-in RCCL INFO
-    # capture (SFTAMD_BENCH_RCCL_INFO=1) whose channel / transport summary lands in the JSON line's ``dist``
+    # whole run, a no-progress bound per rank (also the process group's collective timeout), and RCCL INFO capture
+    # (default at N > 1 on GPUs, SFTAMD_BENCH_RCCL_INFO=0 to opt out) whose channel / transport / rank-count summary
+    # lands in the JSON line's ``dist``
     ap.add_argument("--timeout-s", type=float, default=float(os.environ.get("SFTAMD_BENCH_TIMEOUT_S", "900")),
                     help="wall-clock limit of the whole run; on expiry every rank prints its last heartbeat and exits 124")
     ap.add_argument("--hang-timeout-s", type=float, default=float(os.environ.get("SFTAMD_BENCH_HANG_S", "300")),
@@ -126,7 +127,9 @@ def bucket_plan(engine) -> dict:
             "min_mb": round(srt[0], 3), "median_mb": round(srt[len(srt) // 2], 3), "max_mb": round(srt[-1], 3),
             "total_mb": round(sum(mb), 1), "split_params": engine.num_split_params,
             "tied_sparse": bool(getattr(engine, "tied_sparse", False)),
-            "replicated_buckets": sum(bool(getattr(b, "replicated", False)) for b in engine.buckets)}
+            "replicated_buckets": sum(bool(getattr(b, "replicated", False)) for b in engine.buckets),
+            "plan_source": getattr(engine, "plan_source", None), "alpha_us": round(getattr(engine, "link_alpha_us", 0), 2),
+            "link_gbps": round(getattr(engine, "link_gbps", 0), 2)}
 
 
 def comm_probe(dev, world: int, nbytes: int, iters: int = 5) -> dict:
@@ -165,7 +168,10 @@ def run(a):
     os.environ.setdefault("SFTAMD_HANG_TIMEOUT_S", str(a.hang_timeout_s))
     os.environ.setdefault("SFTAMD_RUN_DEADLINE_S", str(a.timeout_s))
     rccl_dir = None
-    if os.environ.get("SFTAMD_BENCH_RCCL_INFO", "0") == "1" and int(os.environ.get("WORLD_SIZE", "1")) > 1:
+    # N > 1: RCCL's INFO log is captured by default (SFTAMD_BENCH_RCCL_INFO=0 opts out), so the first multi-GPU record
+    # says which transport / how many channels each rank's communicator got and how many ranks RCCL saw
+    if (os.environ.get("SFTAMD_BENCH_RCCL_INFO", "1") == "1" and int(os.environ.get("WORLD_SIZE", "1")) > 1
+            and a.device != "cpu"):
         from llm_fine_tune_distributed_amd.parallel import rccl_info
         rccl_dir = os.environ.get("SFTAMD_RCCL_LOG_DIR", "/tmp/sftamd_rccl")
         rccl_info.enable(rccl_dir)
@@ -297,11 +303,16 @@ def run(a):
                                        for r_ in ranks),
                      "launcher": os.environ.get("SFTAMD_LAUNCHER", "external" if st.world_size > 1 else "none"),
                      "timeout_s": a.timeout_s, "hang_timeout_s": a.hang_timeout_s,
-                     **({"rccl": mine.get("rccl"),
-                         "p2p_transport": (mine.get("rccl") or {}).get("p2p_transport"),
-                         "n_channels": (mine.get("rccl") or {}).get("n_channels"),
-                         "n_channels_per_rank": [(r_.get("rccl") or {}).get("n_channels") for r_ in ranks]}
-                        if rccl_dir is not None else {})},
+                     "rccl_info": rccl_dir is not None,
+                     "rccl": mine.get("rccl"),
+                     "p2p_transport": (mine.get("rccl") or {}).get("p2p_transport"),
+                     "n_channels": (mine.get("rccl") or {}).get("n_channels"),
+                     "n_channels_per_rank": [(r_.get("rccl") or {}).get("n_channels") for r_ in ranks],
+                     "rccl_nranks_per_rank": [(r_.get("rccl") or {}).get("nranks") for r_ in ranks],
+                     # every rank's communicator reported WORLD_SIZE ranks (None: no RCCL log, e.g. gloo)
+                     "rccl_saw_all_ranks": (all((r_.get("rccl") or {}).get("nranks") == st.world_size for r_ in ranks)
+                                            if rccl_dir is not None else None),
+                     "link_probe": [[int(b), round(t * 1e3, 4)] for b, t in getattr(trainer, "link_points", [])]},
             "optimizer_sharding": "zero1" if shard else "none",
             "bucket_plan": bucket_plan(trainer.engine),
             "comm_probe": probe,

@@ -62,41 +62,6 @@ __device__ __forceinline__ void stage(char* lds, const u16* __restrict__ g, long
   }
 }
 
-// Operand along head_dim: rows rbase + (lane & 15), k-step s covers d = 32s .. 32s+31.
-__device__ __forceinline__ bf16x8 frag_row(const char* lds, int rbase, int s, int lane) {
-  return *(const bf16x8*)(lds + img_off(rbase + (lane & 15), 4 * s + (lane >> 4)));
-}
-
-// Operand along the row axis (transposed): lane gets column 16*cb + (lane & 15) of rows
-// rb + p(8g + j) (the accumulator permutation above). Two ds_read_b64_tr_b16.
-template <bool TR>
-__device__ __forceinline__ bf16x8 frag_tr(const char* lds, int rb, int cb, int lane) {
-  const int g = lane >> 4, i = lane & 15;
-  if constexpr (TR) {
-    const int q = i >> 2, p = i & 3;
-    const int ch = 2 * cb + (p >> 1);
-    const int r0 = rb + 4 * g + q;
-    const int o0 = img_off(r0, ch) + 8 * (p & 1);
-    const int o1 = img_off(r0 + 16, ch) + 8 * (p & 1);
-    typedef __attribute__((address_space(3))) s16x4 lds_s4;
-    s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4*)(lds + o0));
-    s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4*)(lds + o1));
-    typedef __attribute__((ext_vector_type(8))) short s16x8;
-    s16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-    return __builtin_bit_cast(bf16x8, v);
-  } else {
-    const int col = 16 * cb + i;
-    const int ch = col >> 3, e = col & 7;
-    typedef __attribute__((ext_vector_type(8))) short s16x8;
-    s16x8 v;
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const int row = rb + (j < 4 ? 4 * g + j : 16 + 4 * g + (j - 4));
-      v[j] = *(const short*)(lds + img_off(row, ch) + 2 * e);
-    }
-    return __builtin_bit_cast(bf16x8, v);
-  }
-}
 
 __device__ __forceinline__ bf16x8 pack_acc(const f32x4& t0, const f32x4& t1) {
   bf16x8 r;
@@ -145,96 +110,6 @@ __device__ __forceinline__ void store4_rope_bwd(u16* p, const f32x4 (&v)[8], flo
   }
 }
 
-// ------------------------------------------------------------------------------ forward
-// grid (q-blocks of 64, nq, nseq); 4 waves x 16 query rows. Per 64-key tile: S^T (16 MFMA),
-// online softmax in registers, O^T += V^T P^T (16 MFMA).
-template <bool TR>
-__global__ __launch_bounds__(256) void fwd_kernel(const u16* __restrict__ qkv, u16* __restrict__ out,
-                                                  float* __restrict__ lse, const int* __restrict__ cu, int nq, int nkv,
-                                                  int total, float sl2, int causal) {
-  __shared__ __attribute__((aligned(16))) char smem[2 * 64 * ROWB];
-  char* Ks = smem;
-  char* Vs = smem + 64 * ROWB;
-  const int qb = blockIdx.x, h = blockIdx.y, b = blockIdx.z;
-  const int start = cu[b], len = cu[b + 1] - start;
-  const int q0 = qb * 64;
-  if (q0 >= len) return;
-  const int kvh = h / (nq / nkv);
-  const long ld = (long)(nq + 2 * nkv) * D;
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, g = lane >> 4;
-  const int qrow = q0 + wave * 16 + (lane & 15);
-  const bool qok = qrow < len;
-  const u16* qp = qkv + (long)(start + qrow) * ld + h * D + 8 * g;
-  bf16x8 qf[4];
-#pragma unroll
-  for (int s = 0; s < 4; ++s) qf[s] = load_frag_global(qp + 32 * s, qok);
-
-  f32x4 o[8];
-#pragma unroll
-  for (int dt = 0; dt < 8; ++dt) o[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
-  float m = -1e30f, l = 0.f;
-  const int nkb = (len + 63) / 64;
-  const int nkt = causal ? min(qb + 1, nkb) : nkb;
-  for (int kt = 0; kt < nkt; ++kt) {
-    const int k0 = kt * 64;
-    const int kvalid = min(64, len - k0);
-    __syncthreads();
-    stage<64, 256>(Ks, qkv + (long)(start + k0) * ld + (nq + kvh) * D, ld, kvalid, tid);
-    stage<64, 256>(Vs, qkv + (long)(start + k0) * ld + (nq + nkv + kvh) * D, ld, kvalid, tid);
-    __syncthreads();
-    f32x4 sc[4];
-#pragma unroll
-    for (int nt = 0; nt < 4; ++nt) {
-      sc[nt] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-      for (int s = 0; s < 4; ++s) sc[nt] = mfma(frag_row(Ks, 16 * nt, s, lane), qf[s], sc[nt]);
-    }
-    float tmax = -INFINITY;
-#pragma unroll
-    for (int nt = 0; nt < 4; ++nt)
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int key = k0 + 16 * nt + 4 * g + i;
-        float v = sc[nt][i] * sl2;
-        if (key >= len || (causal && key > qrow)) v = -INFINITY;
-        sc[nt][i] = v;
-        tmax = fmaxf(tmax, v);
-      }
-    tmax = fmaxf(tmax, __shfl_xor(tmax, 16, 64));
-    tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64));
-    const float mnew = fmaxf(m, tmax);
-    const float alpha = exp2f(m - mnew);
-    float rs = 0.f;
-#pragma unroll
-    for (int nt = 0; nt < 4; ++nt)
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const float p = exp2f(sc[nt][i] - mnew);
-        sc[nt][i] = p;
-        rs += p;
-      }
-    rs += __shfl_xor(rs, 16, 64);
-    rs += __shfl_xor(rs, 32, 64);
-    l = l * alpha + rs;
-    m = mnew;
-#pragma unroll
-    for (int dt = 0; dt < 8; ++dt) o[dt] *= alpha;
-#pragma unroll
-    for (int ks = 0; ks < 2; ++ks) {
-      const bf16x8 pb = pack_acc(sc[2 * ks], sc[2 * ks + 1]);
-#pragma unroll
-      for (int dt = 0; dt < 8; ++dt) o[dt] = mfma(frag_tr<TR>(Vs, 32 * ks, dt, lane), pb, o[dt]);
-    }
-  }
-  if (qok) {
-    const float inv = 1.f / l;
-    u16* op = out + (long)(start + qrow) * nq * D + h * D + 4 * g;
-#pragma unroll
-    for (int dt = 0; dt < 8; ++dt) store4(op + 16 * dt, o[dt], inv);
-    if (g == 0) lse[(long)h * total + start + qrow] = (m + log2f(l)) * LN2;
-  }
-}
-
 // ------------------------------------------------------------------------------ backward
 // delta[h][m] = sum_d dO[m, h*D + d] * O[m, h*D + d]   (16 lanes per row)
 __global__ __launch_bounds__(256) void delta_kernel(const u16* __restrict__ dout, const u16* __restrict__ out,
@@ -257,609 +132,6 @@ __global__ __launch_bounds__(256) void delta_kernel(const u16* __restrict__ dout
     const long m = rowid / nq;
     const int h = (int)(rowid - m * nq);
     delta[(long)h * total + m] = s;
-  }
-}
-
-// dK/dV: grid (key blocks of 64, nkv, nseq); wave owns 16 keys (K, V fragments in registers,
-// dK^T/dV^T accumulators in registers); loops over the GQA group's query heads and 64-row
-// query tiles: S, dP (32 MFMA) -> P, dS -> dV^T += dO^T P, dK^T += Q^T dS (32 MFMA).
-template <bool TR>
-__global__ __launch_bounds__(256) void bwd_dkdv_kernel(const u16* __restrict__ qkv, const u16* __restrict__ dout,
-                                                       const float* __restrict__ lse, const float* __restrict__ delta,
-                                                       const int* __restrict__ cu, u16* __restrict__ dqkv, int nq,
-                                                       int nkv, int total, float sl2, float scale, int causal) {
-  __shared__ __attribute__((aligned(16))) char smem[2 * 64 * ROWB + 2 * 64 * 4];
-  char* Qs = smem;
-  char* Os = smem + 64 * ROWB;
-  float* Ls = (float*)(smem + 2 * 64 * ROWB);
-  float* Dl = Ls + 64;
-  const int kb = blockIdx.x, kvh = blockIdx.y, b = blockIdx.z;
-  const int start = cu[b], len = cu[b + 1] - start;
-  const int k0 = kb * 64;
-  if (k0 >= len) return;
-  const int rep = nq / nkv;
-  const long ld = (long)(nq + 2 * nkv) * D;
-  const long ldo = (long)nq * D;
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, g = lane >> 4;
-  const int key = k0 + wave * 16 + (lane & 15);
-  const bool kok = key < len;
-  bf16x8 kf[4], vf[4];
-  {
-    const u16* kp = qkv + (long)(start + key) * ld + (nq + kvh) * D + 8 * g;
-    const u16* vp = qkv + (long)(start + key) * ld + (nq + nkv + kvh) * D + 8 * g;
-#pragma unroll
-    for (int s = 0; s < 4; ++s) {
-      kf[s] = load_frag_global(kp + 32 * s, kok);
-      vf[s] = load_frag_global(vp + 32 * s, kok);
-    }
-  }
-  f32x4 dk[8], dv[8];
-#pragma unroll
-  for (int dt = 0; dt < 8; ++dt) {
-    dk[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
-    dv[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
-  }
-  const int qt0 = causal ? kb : 0;
-  const int nqt = (len + 63) / 64;
-  for (int r = 0; r < rep; ++r) {
-    const int h = kvh * rep + r;
-    for (int qt = qt0; qt < nqt; ++qt) {
-      const int q0 = qt * 64;
-      const int qvalid = min(64, len - q0);
-      __syncthreads();
-      stage<64, 256>(Qs, qkv + (long)(start + q0) * ld + h * D, ld, qvalid, tid);
-      stage<64, 256>(Os, dout + (long)(start + q0) * ldo + h * D, ldo, qvalid, tid);
-      if (tid < 64) {
-        const bool ok = tid < qvalid;
-        Ls[tid] = ok ? lse[(long)h * total + start + q0 + tid] * LOG2E : 0.f;
-        Dl[tid] = ok ? delta[(long)h * total + start + q0 + tid] : 0.f;
-      }
-      __syncthreads();
-      f32x4 sc[4], dp[4];
-#pragma unroll
-      for (int mt = 0; mt < 4; ++mt) {
-        sc[mt] = f32x4{0.f, 0.f, 0.f, 0.f};
-        dp[mt] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-        for (int s = 0; s < 4; ++s) {
-          sc[mt] = mfma(frag_row(Qs, 16 * mt, s, lane), kf[s], sc[mt]);
-          dp[mt] = mfma(frag_row(Os, 16 * mt, s, lane), vf[s], dp[mt]);
-        }
-      }
-      // lane: key column, query rows q0 + 16mt + 4g + i
-#pragma unroll
-      for (int mt = 0; mt < 4; ++mt)
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const int qi = 16 * mt + 4 * g + i;
-          const int q = q0 + qi;
-          float p = exp2f(sc[mt][i] * sl2 - Ls[qi]);
-          if (q >= len || (causal && key > q)) p = 0.f;
-          sc[mt][i] = p;
-          dp[mt][i] = p * (dp[mt][i] - Dl[qi]);
-        }
-#pragma unroll
-      for (int ks = 0; ks < 2; ++ks) {
-        const bf16x8 pb = pack_acc(sc[2 * ks], sc[2 * ks + 1]);
-        const bf16x8 db = pack_acc(dp[2 * ks], dp[2 * ks + 1]);
-#pragma unroll
-        for (int dt = 0; dt < 8; ++dt) {
-          dv[dt] = mfma(frag_tr<TR>(Os, 32 * ks, dt, lane), pb, dv[dt]);
-          dk[dt] = mfma(frag_tr<TR>(Qs, 32 * ks, dt, lane), db, dk[dt]);
-        }
-      }
-    }
-  }
-  if (kok) {
-    u16* kp = dqkv + (long)(start + key) * ld + (nq + kvh) * D + 4 * g;
-    u16* vp = dqkv + (long)(start + key) * ld + (nq + nkv + kvh) * D + 4 * g;
-#pragma unroll
-    for (int dt = 0; dt < 8; ++dt) {
-      store4(kp + 16 * dt, dk[dt], scale);
-      store4(vp + 16 * dt, dv[dt], 1.f);
-    }
-  }
-}
-
-// dQ: grid (q blocks of 64, nq, nseq); wave owns 16 query rows (Q, dO fragments in registers);
-// per 64-key tile: S^T, dP^T (32 MFMA) -> dS^T -> dQ^T += K^T dS^T (16 MFMA).
-template <bool TR>
-__global__ __launch_bounds__(256) void bwd_dq_kernel(const u16* __restrict__ qkv, const u16* __restrict__ dout,
-                                                     const float* __restrict__ lse, const float* __restrict__ delta,
-                                                     const int* __restrict__ cu, u16* __restrict__ dqkv, int nq,
-                                                     int nkv, int total, float sl2, float scale, int causal) {
-  __shared__ __attribute__((aligned(16))) char smem[2 * 64 * ROWB];
-  char* Ks = smem;
-  char* Vs = smem + 64 * ROWB;
-  const int qb = blockIdx.x, h = blockIdx.y, b = blockIdx.z;
-  const int start = cu[b], len = cu[b + 1] - start;
-  const int q0 = qb * 64;
-  if (q0 >= len) return;
-  const int kvh = h / (nq / nkv);
-  const long ld = (long)(nq + 2 * nkv) * D;
-  const long ldo = (long)nq * D;
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, g = lane >> 4;
-  const int qrow = q0 + wave * 16 + (lane & 15);
-  const bool qok = qrow < len;
-  bf16x8 qf[4], df[4];
-  {
-    const u16* qp = qkv + (long)(start + qrow) * ld + h * D + 8 * g;
-    const u16* dp = dout + (long)(start + qrow) * ldo + h * D + 8 * g;
-#pragma unroll
-    for (int s = 0; s < 4; ++s) {
-      qf[s] = load_frag_global(qp + 32 * s, qok);
-      df[s] = load_frag_global(dp + 32 * s, qok);
-    }
-  }
-  const float lse2 = qok ? lse[(long)h * total + start + qrow] * LOG2E : 0.f;
-  const float dl = qok ? delta[(long)h * total + start + qrow] : 0.f;
-  f32x4 dq[8];
-#pragma unroll
-  for (int dt = 0; dt < 8; ++dt) dq[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
-  const int nkb = (len + 63) / 64;
-  const int nkt = causal ? min(qb + 1, nkb) : nkb;
-  for (int kt = 0; kt < nkt; ++kt) {
-    const int k0 = kt * 64;
-    const int kvalid = min(64, len - k0);
-    __syncthreads();
-    stage<64, 256>(Ks, qkv + (long)(start + k0) * ld + (nq + kvh) * D, ld, kvalid, tid);
-    stage<64, 256>(Vs, qkv + (long)(start + k0) * ld + (nq + nkv + kvh) * D, ld, kvalid, tid);
-    __syncthreads();
-    f32x4 sc[4], dp[4];
-#pragma unroll
-    for (int nt = 0; nt < 4; ++nt) {
-      sc[nt] = f32x4{0.f, 0.f, 0.f, 0.f};
-      dp[nt] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-      for (int s = 0; s < 4; ++s) {
-        sc[nt] = mfma(frag_row(Ks, 16 * nt, s, lane), qf[s], sc[nt]);
-        dp[nt] = mfma(frag_row(Vs, 16 * nt, s, lane), df[s], dp[nt]);
-      }
-    }
-#pragma unroll
-    for (int nt = 0; nt < 4; ++nt)
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int key = k0 + 16 * nt + 4 * g + i;
-        float p = exp2f(sc[nt][i] * sl2 - lse2);
-        if (key >= len || (causal && key > qrow) || !qok) p = 0.f;
-        dp[nt][i] = p * (dp[nt][i] - dl);
-      }
-#pragma unroll
-    for (int ks = 0; ks < 2; ++ks) {
-      const bf16x8 db = pack_acc(dp[2 * ks], dp[2 * ks + 1]);
-#pragma unroll
-      for (int dt = 0; dt < 8; ++dt) dq[dt] = mfma(frag_tr<TR>(Ks, 32 * ks, dt, lane), db, dq[dt]);
-    }
-  }
-  if (qok) {
-    u16* qp = dqkv + (long)(start + qrow) * ld + h * D + 4 * g;
-#pragma unroll
-    for (int dt = 0; dt < 8; ++dt) store4(qp + 16 * dt, dq[dt], scale);
-  }
-}
-
-
-// ============================================================================== v2 kernels
-// Same math and lane maps as v1, restructured for latency hiding on CDNA4:
-// * K/V (fwd, dQ) and Q/dO (dK/dV) tiles are double-buffered in LDS; the next tile is issued
-//   global->registers BEFORE the current tile's MFMAs and written to the other LDS buffer after
-//   them (T14 async-STAGE split), so HBM/L2 latency hides under compute; one barrier per tile;
-// * fwd/dQ use 8-wave (512-thread) workgroups over 128 query rows, halving K/V staging per row
-//   and giving two waves per SIMD; waves whose 16 rows are entirely below a causal key tile skip
-//   its MFMAs (wave-uniform branch);
-// * dK/dV is split over the query heads of a GQA group (4x the workgroups, no causal tail of
-//   32 sequential tiles): each workgroup writes an fp32 partial slab, and a vectorised reduce
-//   kernel sums the rep partials in a fixed order (deterministic) straight into packed dqkv.
-
-template <int R, int NT>
-struct TileRegs {
-  static constexpr int N = (R * 16) / NT;
-  uint4 v[N];
-  __device__ __forceinline__ void load(const u16* __restrict__ g, long ld, int nvalid, int tid) {
-#pragma unroll
-    for (int it = 0; it < N; ++it) {
-      const int idx = tid + it * NT;
-      const int r = idx >> 4, ch = idx & 15;
-      v[it] = make_uint4(0, 0, 0, 0);
-      if (r < nvalid) v[it] = *(const uint4*)(g + (long)r * ld + ch * 8);
-    }
-  }
-  __device__ __forceinline__ void store(char* lds, int tid) const {
-#pragma unroll
-    for (int it = 0; it < N; ++it) {
-      const int idx = tid + it * NT;
-      *(uint4*)(lds + img_off(idx >> 4, idx & 15)) = v[it];
-    }
-  }
-};
-
-template <bool TR, int NW, int NBUF>
-__global__ __launch_bounds__(NW * 64) void fwd2_kernel(const u16* __restrict__ qkv, u16* __restrict__ out,
-                                                       float* __restrict__ lse, const int* __restrict__ cu, int nq,
-                                                       int nkv, int total, float sl2, int causal) {
-  constexpr int NT = NW * 64, BM = NW * 16, TB = 64 * ROWB;
-  __shared__ __attribute__((aligned(16))) char smem[2 * NBUF * TB];  // K0 V0 (K1 V1)
-  const int qb = blockIdx.x, h = blockIdx.y, b = blockIdx.z;
-  const int start = cu[b], len = cu[b + 1] - start;
-  SFT_DASSERT(start >= 0 && len >= 0 && start + len <= total);
-  const int q0 = qb * BM;
-  if (q0 >= len) return;
-  const int kvh = h / (nq / nkv);
-  const long ld = (long)(nq + 2 * nkv) * D;
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, g = lane >> 4;
-  const int qrow = q0 + wave * 16 + (lane & 15);
-  const int wlast = q0 + wave * 16 + 15;  // last query row of this wave
-  const bool qok = qrow < len;
-  const u16* kbase = qkv + (long)start * ld + (nq + kvh) * D;
-  const u16* vbase = qkv + (long)start * ld + (nq + nkv + kvh) * D;
-  const int nkb = (len + 63) / 64;
-  const int nkt = causal ? min((q0 + BM + 63) / 64, nkb) : nkb;
-  {
-    TileRegs<64, NT> tk, tv;
-    tk.load(kbase, ld, min(64, len), tid);
-    tv.load(vbase, ld, min(64, len), tid);
-    tk.store(smem, tid);
-    tv.store(smem + TB, tid);
-  }
-  bf16x8 qf[4];
-  {
-    const u16* qp = qkv + (long)(start + qrow) * ld + h * D + 8 * g;
-#pragma unroll
-    for (int s = 0; s < 4; ++s) qf[s] = load_frag_global(qp + 32 * s, qok);
-  }
-  f32x4 o[8];
-#pragma unroll
-  for (int dt = 0; dt < 8; ++dt) o[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
-  float m = -1e30f, l = 0.f;
-  __syncthreads();
-  for (int kt = 0; kt < nkt; ++kt) {
-    const int k0 = kt * 64;
-    char* Ks = smem + (NBUF == 2 ? (kt & 1) : 0) * 2 * TB;
-    char* Vs = Ks + TB;
-    const bool pre = kt + 1 < nkt;
-    TileRegs<64, NT> tk, tv;
-    if (pre) {
-      const int kv = min(64, len - k0 - 64);
-      tk.load(kbase + (long)(k0 + 64) * ld, ld, kv, tid);
-      tv.load(vbase + (long)(k0 + 64) * ld, ld, kv, tid);
-    }
-    if (!causal || k0 <= wlast) {
-      f32x4 sc[4];
-#pragma unroll
-      for (int nt = 0; nt < 4; ++nt) {
-        sc[nt] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-        for (int s = 0; s < 4; ++s) sc[nt] = mfma(frag_row(Ks, 16 * nt, s, lane), qf[s], sc[nt]);
-      }
-      float tmax = -INFINITY;
-#pragma unroll
-      for (int nt = 0; nt < 4; ++nt)
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const int key = k0 + 16 * nt + 4 * g + i;
-          float v = sc[nt][i] * sl2;
-          if (key >= len || (causal && key > qrow)) v = -INFINITY;
-          sc[nt][i] = v;
-          tmax = fmaxf(tmax, v);
-        }
-      tmax = fmaxf(tmax, __shfl_xor(tmax, 16, 64));
-      tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64));
-      const float mnew = fmaxf(m, tmax);
-      const float alpha = exp2f(m - mnew);
-      float rs = 0.f;
-#pragma unroll
-      for (int nt = 0; nt < 4; ++nt)
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const float p = exp2f(sc[nt][i] - mnew);
-          sc[nt][i] = p;
-          rs += p;
-        }
-      rs += __shfl_xor(rs, 16, 64);
-      rs += __shfl_xor(rs, 32, 64);
-      l = l * alpha + rs;
-      m = mnew;
-#pragma unroll
-      for (int dt = 0; dt < 8; ++dt) o[dt] *= alpha;
-#pragma unroll
-      for (int ks = 0; ks < 2; ++ks) {
-        const bf16x8 pb = pack_acc(sc[2 * ks], sc[2 * ks + 1]);
-#pragma unroll
-        for (int dt = 0; dt < 8; ++dt) o[dt] = mfma(frag_tr<TR>(Vs, 32 * ks, dt, lane), pb, o[dt]);
-      }
-    }
-    if (pre) {
-      if (NBUF == 1) __syncthreads();  // every wave is done reading the single buffer
-      char* Kn = smem + (NBUF == 2 ? ((kt + 1) & 1) : 0) * 2 * TB;
-      tk.store(Kn, tid);
-      tv.store(Kn + TB, tid);
-    }
-    __syncthreads();
-  }
-  if (qok) {
-    const float inv = 1.f / l;
-    u16* op = out + (long)(start + qrow) * nq * D + h * D + 4 * g;
-#pragma unroll
-    for (int dt = 0; dt < 8; ++dt) store4(op + 16 * dt, o[dt], inv);
-    if (g == 0) lse[(long)h * total + start + qrow] = (m + log2f(l)) * LN2;
-  }
-}
-
-template <bool TR, int NW, int NBUF>
-__global__ __launch_bounds__(NW * 64) void bwd_dq2_kernel(const u16* __restrict__ qkv, const u16* __restrict__ dout,
-                                                          const float* __restrict__ lse,
-                                                          const float* __restrict__ delta, const int* __restrict__ cu,
-                                                          u16* __restrict__ dqkv, int nq, int nkv, int total,
-                                                          float sl2, float scale, int causal) {
-  constexpr int NT = NW * 64, BM = NW * 16, TB = 64 * ROWB;
-  __shared__ __attribute__((aligned(16))) char smem[2 * NBUF * TB];
-  const int qb = blockIdx.x, h = blockIdx.y, b = blockIdx.z;
-  const int start = cu[b], len = cu[b + 1] - start;
-  SFT_DASSERT(start >= 0 && len >= 0 && start + len <= total);
-  const int q0 = qb * BM;
-  if (q0 >= len) return;
-  const int kvh = h / (nq / nkv);
-  const long ld = (long)(nq + 2 * nkv) * D;
-  const long ldo = (long)nq * D;
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, g = lane >> 4;
-  const int qrow = q0 + wave * 16 + (lane & 15);
-  const int wlast = q0 + wave * 16 + 15;
-  const bool qok = qrow < len;
-  const u16* kbase = qkv + (long)start * ld + (nq + kvh) * D;
-  const u16* vbase = qkv + (long)start * ld + (nq + nkv + kvh) * D;
-  const int nkb = (len + 63) / 64;
-  const int nkt = causal ? min((q0 + BM + 63) / 64, nkb) : nkb;
-  {
-    TileRegs<64, NT> tk, tv;
-    tk.load(kbase, ld, min(64, len), tid);
-    tv.load(vbase, ld, min(64, len), tid);
-    tk.store(smem, tid);
-    tv.store(smem + TB, tid);
-  }
-  bf16x8 qf[4], df[4];
-  {
-    const u16* qp = qkv + (long)(start + qrow) * ld + h * D + 8 * g;
-    const u16* dp = dout + (long)(start + qrow) * ldo + h * D + 8 * g;
-#pragma unroll
-    for (int s = 0; s < 4; ++s) {
-      qf[s] = load_frag_global(qp + 32 * s, qok);
-      df[s] = load_frag_global(dp + 32 * s, qok);
-    }
-  }
-  const float lse2 = qok ? lse[(long)h * total + start + qrow] * LOG2E : 0.f;
-  const float dl = qok ? delta[(long)h * total + start + qrow] : 0.f;
-  f32x4 dq[8];
-#pragma unroll
-  for (int dt = 0; dt < 8; ++dt) dq[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
-  __syncthreads();
-  for (int kt = 0; kt < nkt; ++kt) {
-    const int k0 = kt * 64;
-    char* Ks = smem + (NBUF == 2 ? (kt & 1) : 0) * 2 * TB;
-    char* Vs = Ks + TB;
-    const bool pre = kt + 1 < nkt;
-    TileRegs<64, NT> tk, tv;
-    if (pre) {
-      const int kv = min(64, len - k0 - 64);
-      tk.load(kbase + (long)(k0 + 64) * ld, ld, kv, tid);
-      tv.load(vbase + (long)(k0 + 64) * ld, ld, kv, tid);
-    }
-    if (!causal || k0 <= wlast) {
-      f32x4 sc[4], dp[4];
-#pragma unroll
-      for (int nt = 0; nt < 4; ++nt) {
-        sc[nt] = f32x4{0.f, 0.f, 0.f, 0.f};
-        dp[nt] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-        for (int s = 0; s < 4; ++s) {
-          sc[nt] = mfma(frag_row(Ks, 16 * nt, s, lane), qf[s], sc[nt]);
-          dp[nt] = mfma(frag_row(Vs, 16 * nt, s, lane), df[s], dp[nt]);
-        }
-      }
-#pragma unroll
-      for (int nt = 0; nt < 4; ++nt)
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const int key = k0 + 16 * nt + 4 * g + i;
-          float p = exp2f(sc[nt][i] * sl2 - lse2);
-          if (key >= len || (causal && key > qrow) || !qok) p = 0.f;
-          dp[nt][i] = p * (dp[nt][i] - dl);
-        }
-#pragma unroll
-      for (int ks = 0; ks < 2; ++ks) {
-        const bf16x8 db = pack_acc(dp[2 * ks], dp[2 * ks + 1]);
-#pragma unroll
-        for (int dt = 0; dt < 8; ++dt) dq[dt] = mfma(frag_tr<TR>(Ks, 32 * ks, dt, lane), db, dq[dt]);
-      }
-    }
-    if (pre) {
-      if (NBUF == 1) __syncthreads();  // every wave is done reading the single buffer
-      char* Kn = smem + (NBUF == 2 ? ((kt + 1) & 1) : 0) * 2 * TB;
-      tk.store(Kn, tid);
-      tv.store(Kn + TB, tid);
-    }
-    __syncthreads();
-  }
-  if (qok) {
-    u16* qp = dqkv + (long)(start + qrow) * ld + h * D + 4 * g;
-#pragma unroll
-    for (int dt = 0; dt < 8; ++dt) store4(qp + 16 * dt, dq[dt], scale);
-  }
-}
-
-// dK/dV partials for ONE query head h (grid (key blocks, nq, nseq)); writes fp32 slab
-// part[r][token][2*nkv*D] (r = h % rep; dK at kvh*D, dV at (nkv+kvh)*D). When rep == 1 the
-// result goes straight to dqkv (bf16, dK scaled).
-template <bool TR, int NBUF>
-__global__ __launch_bounds__(256, 2) void bwd_dkdv2_kernel(const u16* __restrict__ qkv, const u16* __restrict__ dout,
-                                                           const float* __restrict__ lse,
-                                                           const float* __restrict__ delta,
-                                                           const int* __restrict__ cu, float* __restrict__ part,
-                                                           u16* __restrict__ dqkv, int nq, int nkv, int total,
-                                                           float sl2, float scale, int causal) {
-  constexpr int NT = 256, TB = 64 * ROWB;
-  __shared__ __attribute__((aligned(16))) char smem[2 * NBUF * TB + NBUF * 2 * 64 * 4];
-  float* LDs = (float*)(smem + 2 * NBUF * TB);  // [buf][lse2 64 | delta 64]
-  const int kb = blockIdx.x, h = blockIdx.y, b = blockIdx.z;
-  const int start = cu[b], len = cu[b + 1] - start;
-  const int k0 = kb * 64;
-  if (k0 >= len) return;
-  const int rep = nq / nkv;
-  const int kvh = h / rep, r = h - kvh * rep;
-  const long ld = (long)(nq + 2 * nkv) * D;
-  const long ldo = (long)nq * D;
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, g = lane >> 4;
-  const int key = k0 + wave * 16 + (lane & 15);
-  const int wfirst = k0 + wave * 16;
-  const bool kok = key < len;
-  const u16* qbase = qkv + (long)start * ld + h * D;
-  const u16* obase = dout + (long)start * ldo + h * D;
-  const float* lbase = lse + (long)h * total + start;
-  const float* dbase = delta + (long)h * total + start;
-  const int qt0 = causal ? kb : 0;
-  const int nqt = (len + 63) / 64;
-  {
-    const int q0 = qt0 * 64, qv = min(64, len - q0);
-    TileRegs<64, NT> tq, to;
-    tq.load(qbase + (long)q0 * ld, ld, qv, tid);
-    to.load(obase + (long)q0 * ldo, ldo, qv, tid);
-    tq.store(smem, tid);
-    to.store(smem + TB, tid);
-    if (tid < 64) {
-      LDs[tid] = tid < qv ? lbase[q0 + tid] * LOG2E : 0.f;
-      LDs[64 + tid] = tid < qv ? dbase[q0 + tid] : 0.f;
-    }
-  }
-  bf16x8 kf[4], vf[4];
-  {
-    const u16* kp = qkv + (long)(start + key) * ld + (nq + kvh) * D + 8 * g;
-    const u16* vp = qkv + (long)(start + key) * ld + (nq + nkv + kvh) * D + 8 * g;
-#pragma unroll
-    for (int s = 0; s < 4; ++s) {
-      kf[s] = load_frag_global(kp + 32 * s, kok);
-      vf[s] = load_frag_global(vp + 32 * s, kok);
-    }
-  }
-  f32x4 dk[8], dv[8];
-#pragma unroll
-  for (int dt = 0; dt < 8; ++dt) {
-    dk[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
-    dv[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
-  }
-  __syncthreads();
-  for (int qt = qt0; qt < nqt; ++qt) {
-    const int q0 = qt * 64;
-    const int buf = NBUF == 2 ? ((qt - qt0) & 1) : 0;
-    char* Qs = smem + buf * 2 * TB;
-    char* Os = Qs + TB;
-    const float* Ls = LDs + buf * 128;
-    const float* Dl = Ls + 64;
-    const bool pre = qt + 1 < nqt;
-    TileRegs<64, NT> tq, to;
-    float pl = 0.f, pd = 0.f;
-    if (pre) {
-      const int qn = q0 + 64, qv = min(64, len - qn);
-      tq.load(qbase + (long)qn * ld, ld, qv, tid);
-      to.load(obase + (long)qn * ldo, ldo, qv, tid);
-      if (tid < 64 && tid < qv) {
-        pl = lbase[qn + tid] * LOG2E;
-        pd = dbase[qn + tid];
-      }
-    }
-    // a wave whose 16 keys are all later than every query of the tile contributes nothing
-    if (!causal || wfirst <= q0 + 63) {
-      f32x4 sc[4], dp[4];
-#pragma unroll
-      for (int mt = 0; mt < 4; ++mt) {
-        sc[mt] = f32x4{0.f, 0.f, 0.f, 0.f};
-        dp[mt] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-        for (int s = 0; s < 4; ++s) {
-          sc[mt] = mfma(frag_row(Qs, 16 * mt, s, lane), kf[s], sc[mt]);
-          dp[mt] = mfma(frag_row(Os, 16 * mt, s, lane), vf[s], dp[mt]);
-        }
-      }
-#pragma unroll
-      for (int mt = 0; mt < 4; ++mt)
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const int qi = 16 * mt + 4 * g + i;
-          const int q = q0 + qi;
-          float p = exp2f(sc[mt][i] * sl2 - Ls[qi]);
-          if (q >= len || (causal && key > q)) p = 0.f;
-          sc[mt][i] = p;
-          dp[mt][i] = p * (dp[mt][i] - Dl[qi]);
-        }
-#pragma unroll
-      for (int ks = 0; ks < 2; ++ks) {
-        const bf16x8 pb = pack_acc(sc[2 * ks], sc[2 * ks + 1]);
-        const bf16x8 db = pack_acc(dp[2 * ks], dp[2 * ks + 1]);
-#pragma unroll
-        for (int dt = 0; dt < 8; ++dt) {
-          dv[dt] = mfma(frag_tr<TR>(Os, 32 * ks, dt, lane), pb, dv[dt]);
-          dk[dt] = mfma(frag_tr<TR>(Qs, 32 * ks, dt, lane), db, dk[dt]);
-        }
-      }
-    }
-    if (pre) {
-      if (NBUF == 1) __syncthreads();
-      const int nb = NBUF == 2 ? (buf ^ 1) : 0;
-      char* Qn = smem + nb * 2 * TB;
-      tq.store(Qn, tid);
-      to.store(Qn + TB, tid);
-      if (tid < 64) {
-        float* Ln = LDs + nb * 128;
-        Ln[tid] = pl;
-        Ln[64 + tid] = pd;
-      }
-    }
-    __syncthreads();
-  }
-  if (!kok) return;
-  if (rep == 1) {
-    u16* kp = dqkv + (long)(start + key) * ld + (nq + kvh) * D + 4 * g;
-    u16* vp = dqkv + (long)(start + key) * ld + (nq + nkv + kvh) * D + 4 * g;
-#pragma unroll
-    for (int dt = 0; dt < 8; ++dt) {
-      store4(kp + 16 * dt, dk[dt], scale);
-      store4(vp + 16 * dt, dv[dt], 1.f);
-    }
-    return;
-  }
-  const long pld = 2L * nkv * D;
-  float* pk = part + ((long)r * total + start + key) * pld + kvh * D + 4 * g;
-  float* pv = pk + (long)nkv * D;
-#pragma unroll
-  for (int dt = 0; dt < 8; ++dt) {
-    *(float4*)(pk + 16 * dt) = make_float4(dk[dt][0], dk[dt][1], dk[dt][2], dk[dt][3]);
-    *(float4*)(pv + 16 * dt) = make_float4(dv[dt][0], dv[dt][1], dv[dt][2], dv[dt][3]);
-  }
-}
-
-// dqkv[m, nq*D + c] = bf16(sum_r part[r][m][c] * (c < nkv*D ? scale : 1)), fixed summation order.
-__global__ __launch_bounds__(256) void dkdv_reduce_kernel(const float* __restrict__ part, u16* __restrict__ dqkv,
-                                                          int total, int nq, int nkv, int rep, float scale) {
-  const int C = 2 * nkv * D;
-  const long nvec = (long)total * C / 8;
-  const long ld = (long)(nq + 2 * nkv) * D;
-  const long stride = (long)total * C;
-  for (long v = blockIdx.x * 256L + threadIdx.x; v < nvec; v += (long)gridDim.x * 256) {
-    const long e = v * 8;
-    const long m = e / C;
-    const int c = (int)(e - m * C);
-    float acc[8];
-    *(float4*)&acc[0] = *(const float4*)(part + e);
-    *(float4*)&acc[4] = *(const float4*)(part + e + 4);
-    for (int r = 1; r < rep; ++r) {
-      const float4 a = *(const float4*)(part + r * stride + e);
-      const float4 b2 = *(const float4*)(part + r * stride + e + 4);
-      acc[0] += a.x; acc[1] += a.y; acc[2] += a.z; acc[3] += a.w;
-      acc[4] += b2.x; acc[5] += b2.y; acc[6] += b2.z; acc[7] += b2.w;
-    }
-    const float sc = c < nkv * D ? scale : 1.f;
-#pragma unroll
-    for (int i = 0; i < 8; ++i) acc[i] *= sc;
-    *(uint4*)(dqkv + m * ld + (long)nq * D + c) = pack8(acc);
   }
 }
 
@@ -1027,150 +299,6 @@ __device__ __forceinline__ void fwd_step_dma(const char* __restrict__ cur, char*
     const bf16x8 pb = pack_acc(sc[2 * ks], sc[2 * ks + 1]);
 #pragma unroll
     for (int dt = 0; dt < 8; ++dt) o[dt] = mfma(lds_tr(Vs, off.tr[dt] + ks * 32 * ROWB), pb, o[dt]);
-  }
-}
-
-// fwd7: 4 waves x 2 row groups of 16 queries (BM = 128), K / V by LDS-DMA into two stages. Every K fragment and V^T
-// fragment read from LDS feeds two MFMAs (half fwd3's LDS bytes per MFMA), and each wave carries two independent
-// softmax chains (ILP for the one wave per SIMD of each workgroup; 64 KB LDS -> 2 workgroups per CU).
-// Opt-in: SFTAMD_ATTN_FWD7=1.
-__device__ __forceinline__ void fwd7_step(const char* __restrict__ cur, char* __restrict__ nxt, bool pre,
-                                          const u16* kbase, const u16* vbase, long ld, long kvoff, int r0, int wave,
-                                          int k0, int len, int causal, int wfirst, int g, int ql, float sl2,
-                                          const Offs& off, const bf16x8 (&qf)[2][4], f32x4 (&o)[2][8], float (&m)[2],
-                                          float (&l)[2]) {
-  constexpr int TB = 64 * ROWB;
-  if (pre) {
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const long row = min(k0 + 64 + r0 + 16 * j, len - 1);
-      lds_dma16(kbase + row * ld + kvoff, nxt + (wave + 4 * j) * 1024);
-      lds_dma16(vbase + row * ld + kvoff, nxt + TB + (wave + 4 * j) * 1024);
-    }
-  }
-  if (causal && k0 > wfirst + 31) return;  // both row groups above this tile's diagonal
-  const char* Ks = cur;
-  const char* Vs = cur + TB;
-  f32x4 sc[2][4];
-#pragma unroll
-  for (int nt = 0; nt < 4; ++nt) {
-    sc[0][nt] = f32x4{0.f, 0.f, 0.f, 0.f};
-    sc[1][nt] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int s = 0; s < 4; ++s) {
-      const bf16x8 kf = lds_row(Ks, off.row[s] + nt * 16 * ROWB);
-      sc[0][nt] = mfma(kf, qf[0][s], sc[0][nt]);
-      sc[1][nt] = mfma(kf, qf[1][s], sc[1][nt]);
-    }
-  }
-  bf16x8 pb[2][2];
-#pragma unroll
-  for (int r = 0; r < 2; ++r) {
-    const int rfirst = wfirst + 16 * r, qrow = rfirst + ql;
-    if ((k0 + 64 > len) || (causal && k0 + 63 > rfirst)) {
-      const int lim = (causal ? min(len - 1, qrow) : len - 1) - k0 - 4 * g;
-#pragma unroll
-      for (int nt = 0; nt < 4; ++nt)
-#pragma unroll
-        for (int i = 0; i < 4; ++i) sc[r][nt][i] = 16 * nt + i > lim ? -INFINITY : sc[r][nt][i];
-    }
-    const float tmax = xmax4(max16(sc[r])) * sl2;
-    if (__any(tmax > m[r] + THR)) {
-      const float mnew = fmaxf(m[r], tmax);
-      const float alpha = exp2f(m[r] - mnew);
-      l[r] *= alpha;
-#pragma unroll
-      for (int dt = 0; dt < 8; ++dt) o[r][dt] *= alpha;
-      m[r] = mnew;
-    }
-    f32x2 acc = {0.f, 0.f};
-    const f32x2 sl = {sl2, sl2}, nm = {-m[r], -m[r]};
-#pragma unroll
-    for (int nt = 0; nt < 4; ++nt)
-#pragma unroll
-      for (int i = 0; i < 4; i += 2) {
-        const f32x2 t = __builtin_elementwise_fma(f32x2{sc[r][nt][i], sc[r][nt][i + 1]}, sl, nm);
-        const f32x2 p = {exp2f(t.x), exp2f(t.y)};
-        sc[r][nt][i] = p.x;
-        sc[r][nt][i + 1] = p.y;
-        acc += p;
-      }
-    l[r] += acc.x + acc.y;
-    pb[r][0] = pack_acc(sc[r][0], sc[r][1]);
-    pb[r][1] = pack_acc(sc[r][2], sc[r][3]);
-  }
-#pragma unroll
-  for (int ks = 0; ks < 2; ++ks)
-#pragma unroll
-    for (int dt = 0; dt < 8; ++dt) {
-      const bf16x8 vf = lds_tr(Vs, off.tr[dt] + ks * 32 * ROWB);
-      o[0][dt] = mfma(vf, pb[0][ks], o[0][dt]);
-      o[1][dt] = mfma(vf, pb[1][ks], o[1][dt]);
-    }
-}
-
-__global__ __launch_bounds__(256, 2) void fwd7_kernel(const u16* __restrict__ qkv, u16* __restrict__ out,
-                                                      float* __restrict__ lse, const int* __restrict__ cu, int nq,
-                                                      int nkv, int total, float sl2, int causal) {
-  constexpr int BM = 128, TB = 64 * ROWB;
-  __shared__ __attribute__((aligned(16))) char smem[4 * TB];  // two stages of (K, V) images
-  const int h = blockIdx.x, b = blockIdx.y, qb = gridDim.z - 1 - blockIdx.z;  // LPT: heaviest q-block first
-  const int start = cu[b], len = cu[b + 1] - start;
-  SFT_DASSERT(start >= 0 && len >= 0 && start + len <= total);
-  const int q0 = qb * BM;
-  if (q0 >= len) return;
-  const int kvh = h / (nq / nkv);
-  const long ld = (long)(nq + 2 * nkv) * D;
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, g = lane >> 4, ql = lane & 15;
-  const int wfirst = q0 + wave * 32;
-  const u16* kbase = qkv + (long)start * ld + (nq + kvh) * D;
-  const u16* vbase = qkv + (long)start * ld + (nq + nkv + kvh) * D;
-  const int nkb = (len + 63) / 64;
-  const int nkt = causal ? min((q0 + BM + 63) / 64, nkb) : nkb;
-  Offs off;
-  off.init(lane);
-  bf16x8 qf[2][4];
-#pragma unroll
-  for (int r = 0; r < 2; ++r) {
-    const int qrow = wfirst + 16 * r + ql;
-    const u16* qp = qkv + (long)(start + qrow) * ld + h * D + 8 * g;
-#pragma unroll
-    for (int s = 0; s < 4; ++s) qf[r][s] = load_frag_global(qp + 32 * s, qrow < len);
-  }
-  const int r0 = 4 * wave + (lane >> 4);
-  const long kvoff = 8 * swz(r0, lane & 15);
-#pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const long row = min(r0 + 16 * j, len - 1);
-    lds_dma16(kbase + row * ld + kvoff, smem + (wave + 4 * j) * 1024);
-    lds_dma16(vbase + row * ld + kvoff, smem + TB + (wave + 4 * j) * 1024);
-  }
-  vm_drain();
-  f32x4 o[2][8];
-  float m[2] = {-1e30f, -1e30f}, l[2] = {0.f, 0.f};
-#pragma unroll
-  for (int r = 0; r < 2; ++r)
-#pragma unroll
-    for (int dt = 0; dt < 8; ++dt) o[r][dt] = f32x4{0.f, 0.f, 0.f, 0.f};
-  __syncthreads();
-  for (int kt = 0; kt < nkt; ++kt) {
-    const bool pre = kt + 1 < nkt;
-    fwd7_step(smem + (kt & 1) * 2 * TB, smem + ((kt + 1) & 1) * 2 * TB, pre, kbase, vbase, ld, kvoff, r0, wave, kt * 64,
-              len, causal, wfirst, g, ql, sl2, off, qf, o, m, l);
-    if (pre) vm_drain();
-    __syncthreads();
-  }
-#pragma unroll
-  for (int r = 0; r < 2; ++r) {
-    const float lt = xsum4(l[r]);
-    const int qrow = wfirst + 16 * r + ql;
-    if (qrow < len) {
-      const float inv = 1.f / lt;
-      u16* op = out + (long)(start + qrow) * nq * D + h * D + 4 * g;
-#pragma unroll
-      for (int dt = 0; dt < 8; ++dt) store4(op + 16 * dt, o[r][dt], inv);
-      if (g == 0) lse[(long)h * total + start + qrow] = (m[r] + log2f(lt)) * LN2;
-    }
   }
 }
 
@@ -1383,521 +511,6 @@ __global__ __launch_bounds__(NW * 64, NW == 8 ? 4 : 2) void fwd3_kernel(const u1
 #pragma unroll
     for (int dt = 0; dt < 8; ++dt) store4(op + 16 * dt, o[dt], inv);
     if (g == 0) lse[(long)h * total + start + qrow] = (m + log2f(l)) * LN2;
-  }
-}
-
-// v4 forward: every wave owns RG = 2 row groups of 16 queries, so each K fragment (row read) and V
-// fragment (transposed read) fetched from LDS feeds RG MFMAs — v3 reads 1 KB of LDS per MFMA, twice
-// what the LDS can deliver at the MFMA rate (256 B/clk/CU vs 4 SIMDs x 16x16x32 per 16 clk); v4 reads
-// 0.5 KB. Otherwise v3's structure: one LDS K/V buffer with register prefetch, masks only on
-// diagonal / tail tiles, exp2 with the scale folded in, deferred rescale (THR).
-template <int NW, int RG>
-__global__ __launch_bounds__(NW * 64) void fwd4_kernel(const u16* __restrict__ qkv, u16* __restrict__ out,
-                                                       float* __restrict__ lse, const int* __restrict__ cu, int nq,
-                                                       int nkv, int total, float sl2, int causal) {
-  constexpr int NT = NW * 64, BM = NW * 16 * RG, TB = 64 * ROWB;
-  __shared__ __attribute__((aligned(16))) char smem[2 * TB];
-  char* Ks = smem;
-  char* Vs = smem + TB;
-  const int qb = blockIdx.x, h = blockIdx.y, b = blockIdx.z;
-  const int start = cu[b], len = cu[b + 1] - start;
-  SFT_DASSERT(start >= 0 && len >= 0 && start + len <= total);
-  const int q0 = qb * BM;
-  if (q0 >= len) return;
-  const int kvh = h / (nq / nkv);
-  const long ld = (long)(nq + 2 * nkv) * D;
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, g = lane >> 4;
-  const int wfirst = q0 + wave * 16 * RG;  // first query row of the wave
-  const u16* kbase = qkv + (long)start * ld + (nq + kvh) * D;
-  const u16* vbase = qkv + (long)start * ld + (nq + nkv + kvh) * D;
-  const int nkb = (len + 63) / 64;
-  const int nkt = causal ? min((q0 + BM + 63) / 64, nkb) : nkb;
-  Offs off;
-  off.init(lane);
-  {
-    Stage<64, NT> tk, tv;
-    tk.load(kbase, ld, len, tid);
-    tv.load(vbase, ld, len, tid);
-    tk.store(Ks, tid);
-    tv.store(Vs, tid);
-  }
-  bf16x8 qf[RG][4];
-#pragma unroll
-  for (int r = 0; r < RG; ++r) {
-    const int qrow = wfirst + 16 * r + (lane & 15);
-    const u16* qp = qkv + (long)(start + qrow) * ld + h * D + 8 * g;
-#pragma unroll
-    for (int s2 = 0; s2 < 4; ++s2) qf[r][s2] = load_frag_global(qp + 32 * s2, qrow < len);
-  }
-  f32x4 o[RG][8];
-  float m[RG], l[RG];
-#pragma unroll
-  for (int r = 0; r < RG; ++r) {
-#pragma unroll
-    for (int dt = 0; dt < 8; ++dt) o[r][dt] = f32x4{0.f, 0.f, 0.f, 0.f};
-    m[r] = -1e30f;
-    l[r] = 0.f;
-  }
-  __syncthreads();
-  for (int kt = 0; kt < nkt; ++kt) {
-    const int k0 = kt * 64;
-    const bool pre = kt + 1 < nkt;
-    Stage<64, NT> tk, tv;
-    if (pre) {
-      tk.load(kbase + (long)(k0 + 64) * ld, ld, len - k0 - 64, tid);
-      tv.load(vbase + (long)(k0 + 64) * ld, ld, len - k0 - 64, tid);
-    }
-    if (!causal || k0 <= wfirst + 16 * RG - 1) {
-      f32x4 sc[RG][4];
-#pragma unroll
-      for (int r = 0; r < RG; ++r)
-#pragma unroll
-        for (int nt = 0; nt < 4; ++nt) sc[r][nt] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-      for (int nt = 0; nt < 4; ++nt)
-#pragma unroll
-        for (int s2 = 0; s2 < 4; ++s2) {
-          const bf16x8 kf = lds_row(Ks, off.row[s2] + nt * 16 * ROWB);
-#pragma unroll
-          for (int r = 0; r < RG; ++r) sc[r][nt] = mfma(kf, qf[r][s2], sc[r][nt]);
-        }
-      bf16x8 pb[RG][2];
-#pragma unroll
-      for (int r = 0; r < RG; ++r) {
-        const int rfirst = wfirst + 16 * r;
-        const int qrow = rfirst + (lane & 15);
-        const bool need_mask = (k0 + 64 > len) || (causal && k0 + 63 > rfirst);
-        if (need_mask) {
-#pragma unroll
-          for (int nt = 0; nt < 4; ++nt)
-#pragma unroll
-            for (int i = 0; i < 4; ++i) {
-              const int key = k0 + 16 * nt + 4 * g + i;
-              if (key >= len || (causal && key > qrow)) sc[r][nt][i] = -INFINITY;
-            }
-        }
-        float tmax = fmaxf(fmaxf(fmaxf(sc[r][0][0], sc[r][0][1]), fmaxf(sc[r][0][2], sc[r][0][3])),
-                           fmaxf(fmaxf(sc[r][1][0], sc[r][1][1]), fmaxf(sc[r][1][2], sc[r][1][3])));
-        tmax = fmaxf(tmax, fmaxf(fmaxf(fmaxf(sc[r][2][0], sc[r][2][1]), fmaxf(sc[r][2][2], sc[r][2][3])),
-                                 fmaxf(fmaxf(sc[r][3][0], sc[r][3][1]), fmaxf(sc[r][3][2], sc[r][3][3]))));
-        tmax = fmaxf(tmax, __shfl_xor(tmax, 16, 64));
-        tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64));
-        tmax *= sl2;
-        if (__any(tmax > m[r] + THR)) {
-          const float mnew = fmaxf(m[r], tmax);
-          const float alpha = exp2f(m[r] - mnew);
-          l[r] *= alpha;
-#pragma unroll
-          for (int dt = 0; dt < 8; ++dt) o[r][dt] *= alpha;
-          m[r] = mnew;
-        }
-        float rs = 0.f;
-#pragma unroll
-        for (int nt = 0; nt < 4; ++nt)
-#pragma unroll
-          for (int i = 0; i < 4; ++i) {
-            const float p = exp2f(fmaf(sc[r][nt][i], sl2, -m[r]));
-            sc[r][nt][i] = p;
-            rs += p;
-          }
-        rs += __shfl_xor(rs, 16, 64);
-        rs += __shfl_xor(rs, 32, 64);
-        l[r] += rs;
-        pb[r][0] = pack_acc(sc[r][0], sc[r][1]);
-        pb[r][1] = pack_acc(sc[r][2], sc[r][3]);
-      }
-#pragma unroll
-      for (int ks = 0; ks < 2; ++ks)
-#pragma unroll
-        for (int dt = 0; dt < 8; ++dt) {
-          const bf16x8 vf = lds_tr(Vs, off.tr[dt] + ks * 32 * ROWB);
-#pragma unroll
-          for (int r = 0; r < RG; ++r) o[r][dt] = mfma(vf, pb[r][ks], o[r][dt]);
-        }
-    }
-    if (pre) {
-      __syncthreads();
-      tk.store(Ks, tid);
-      tv.store(Vs, tid);
-    }
-    __syncthreads();
-  }
-#pragma unroll
-  for (int r = 0; r < RG; ++r) {
-    const int qrow = wfirst + 16 * r + (lane & 15);
-    if (qrow < len) {
-      const float inv = 1.f / l[r];
-      u16* op = out + (long)(start + qrow) * nq * D + h * D + 4 * g;
-#pragma unroll
-      for (int dt = 0; dt < 8; ++dt) store4(op + 16 * dt, o[r][dt], inv);
-      if (g == 0) lse[(long)h * total + start + qrow] = (m[r] + log2f(l[r])) * LN2;
-    }
-  }
-}
-
-// v6 forward (GQA-stacked): one workgroup per (kv head, sequence, 64-query block), 4 waves; wave w owns query
-// positions q0 + 16 w .. + 15 for ALL REP query heads of the kv head. A K fragment (S^T = K Q^T) and a V^T fragment
-// (O^T += V^T P^T) are read from LDS once and feed REP MFMAs, one per head — REP x fewer LDS bytes per MFMA than v3,
-// whose 1 KB per MFMA is twice what the LDS delivers at the MFMA rate. The causal / length masks are shared by the REP
-// heads (same positions). K / V tiles (64 keys) go HBM -> LDS by global_load_lds (16 B per lane, lane-linear LDS
-// writes: the image swizzle is applied to the SOURCE chunk, rows past the sequence end clamped to its last row so
-// nothing outside the sequence is read) into two stages, the next tile's DMA in flight under the current tile's math.
-// The row sums stay per-lane partials until the end (the running max is the only per-tile cross-lane reduction).
-// REP x (32 o + 16 Q) registers per lane: one wave per SIMD, one workgroup per CU; grid (nkv, nseq, q-blocks) with the
-// causally heaviest q-blocks dispatched first (LPT: a CU that drew block 4 of 8 takes block 3 next).
-__device__ __forceinline__ void glds16(const u16* src, char* dst) {
-  __builtin_amdgcn_global_load_lds((const void __attribute__((address_space(1)))*)src,
-                                   (void __attribute__((address_space(3)))*)dst, 16, 0, 0);
-}
-
-// O^T += V^T P^T with the accumulator tied to an AGPR: REP x 8 accumulators stay put across the K loop (as builtins,
-// hipcc shuffled them between AGPRs and VGPRs every tile: ~1250 v_accvgpr moves per tile at REP 4). The compiler does
-// not see these as MFMAs: VALU reads of the accumulators (rescale, epilogue) sit behind nop_mfma() wait states.
-// The leading s_nop 1: P arrives from VALU packs (VALU write -> MFMA operand read: 2 wait states hipcc does not pad
-// inside asm, cdna_hip_programming.md §5.7 item 2).
-__device__ __forceinline__ void mfma_acc(f32x4& c, const bf16x8& a, const bf16x8& b) {
-  asm volatile("s_nop 1\n\tv_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+a"(c) : "v"(a), "v"(b));
-}
-// S^T = K Q^T into VGPRs (the softmax reads them): hipcc's builtin put them in AGPRs and copied them back every tile.
-// Chains accumulate D -> C whole (0 wait states); the VALU readers sit behind nop_mfma().
-__device__ __forceinline__ f32x4 mfma_v0(const bf16x8& a, const bf16x8& b) {
-  f32x4 d;
-  asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, 0" : "=&v"(d) : "v"(a), "v"(b));
-  return d;
-}
-__device__ __forceinline__ void mfma_v(f32x4& c, const bf16x8& a, const bf16x8& b) {
-  asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+v"(c) : "v"(a), "v"(b));
-}
-__device__ __forceinline__ void pin_acc(f32x4& c) { asm volatile("" : "+a"(c)); }  // (re)home a value in AGPRs
-__device__ __forceinline__ void nop_mfma() { asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 3" ::: "memory"); }
-
-template <int REP>
-__global__ __launch_bounds__(256, 1) void fwd6_kernel(const u16* __restrict__ qkv, u16* __restrict__ out,
-                                                      float* __restrict__ lse, const int* __restrict__ cu, int nq,
-                                                      int nkv, int total, float sl2, int causal) {
-  constexpr int TB = 64 * ROWB;  // one 64-row image: 16 KB
-  __shared__ __attribute__((aligned(16))) char smem[4 * TB];  // stage s: K image at 2 s TB, V image at (2 s + 1) TB
-  const int kvh = blockIdx.x, b = blockIdx.y, qb = gridDim.z - 1 - blockIdx.z;
-  const int start = cu[b], len = cu[b + 1] - start;
-  SFT_DASSERT(start >= 0 && len >= 0 && start + len <= total);
-  const int q0 = qb * 64;
-  if (q0 >= len) return;
-  const long ld = (long)(nq + 2 * nkv) * D;
-  const int tid = threadIdx.x, lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6), g = lane >> 4;
-  const int wfirst = q0 + 16 * w, qrow = wfirst + (lane & 15);
-  const bool qok = qrow < len;
-  const int nkb = (len + 63) / 64;
-  const int nkt = causal ? min(qb + 1, nkb) : nkb;
-  // DMA: piece j < 4 of wave w = image rows 4 (w + 4 j) .. + 3 of K and of V (1 KB each); lane -> row r0 + 16 j,
-  // LDS chunk lane & 15 = source chunk swz(row, lane & 15) — the same for every j (row & 3 and (row >> 2) & 3 are)
-  const int r0 = 4 * w + (lane >> 4);
-  const u16* kvsrc = qkv + (long)start * ld + (nq + kvh) * D + 8 * swz(r0, lane & 15);
-  auto dma = [&](int kt, char* stage) {
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const u16* src = kvsrc + (long)min(kt * 64 + r0 + 16 * j, len - 1) * ld;
-      glds16(src, stage + (w + 4 * j) * 1024);
-      glds16(src + nkv * D, stage + TB + (w + 4 * j) * 1024);
-    }
-  };
-  dma(0, smem);
-  Offs off;
-  off.init(lane);
-  bf16x8 qf[REP][4];
-#pragma unroll
-  for (int h = 0; h < REP; ++h) {
-    const u16* qp = qkv + (long)(start + qrow) * ld + (kvh * REP + h) * D + 8 * g;
-#pragma unroll
-    for (int s = 0; s < 4; ++s) qf[h][s] = load_frag_global(qp + 32 * s, qok);
-  }
-  f32x4 o[REP][8];
-  float m[REP], l[REP];
-#pragma unroll
-  for (int h = 0; h < REP; ++h) {
-#pragma unroll
-    for (int dt = 0; dt < 8; ++dt) {
-      o[h][dt] = f32x4{0.f, 0.f, 0.f, 0.f};
-      pin_acc(o[h][dt]);
-    }
-    m[h] = 0.f;  // set from tile 0
-    l[h] = 0.f;
-  }
-  __builtin_amdgcn_s_waitcnt(0);  // tile 0 landed (vmcnt / lgkmcnt 0)
-  __syncthreads();
-  // One K/V tile. FAST: no accumulator rescale — the running max m is set from tile 0 (o = 0 then) and P =
-  // exp2(s - m) may grow up to 2^THR_FAST (bf16 / fp32 hold that exactly enough: only the exponent grows); a tile
-  // whose max exceeds m + THR_FAST returns false BEFORE touching any state and the rest of the row block runs the
-  // SLOW variant (rescale by alpha, v3's deferred scheme). Keeping the rescale out of the fast loop keeps the
-  // accumulators in AGPRs there (a VALU rescale in the loop made hipcc copy all of them to VGPRs every tile).
-  auto tile = [&](int kt, auto slow_t) -> bool {
-    constexpr bool SLOW = decltype(slow_t)::value;
-    const int k0 = kt * 64;
-    const char* Ks = smem + (kt & 1) * 2 * TB;
-    const char* Vs = Ks + TB;
-    f32x4 sc[REP][4];
-#pragma unroll
-    for (int nt = 0; nt < 4; ++nt)
-#pragma unroll
-      for (int s = 0; s < 4; ++s) {
-        const bf16x8 kf = lds_row(Ks, off.row[s] + nt * 16 * ROWB);
-#pragma unroll
-        for (int h = 0; h < REP; ++h) {
-          if (s == 0) sc[h][nt] = mfma_v0(kf, qf[h][s]);
-          else mfma_v(sc[h][nt], kf, qf[h][s]);
-        }
-      }
-    nop_mfma();  // MFMA D -> VALU: 12 wait states for the 8-pass MFMA
-    if ((k0 + 64 > len) || (causal && k0 + 63 > wfirst)) {
-#pragma unroll
-      for (int nt = 0; nt < 4; ++nt)
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const int key = k0 + 16 * nt + 4 * g + i;
-          if (key >= len || (causal && key > qrow)) {
-#pragma unroll
-            for (int h = 0; h < REP; ++h) sc[h][nt][i] = -INFINITY;
-          }
-        }
-    }
-    float tmax[REP];
-    bool big = false;
-#pragma unroll
-    for (int h = 0; h < REP; ++h) {
-      float t = fmaxf(fmaxf(fmaxf(sc[h][0][0], sc[h][0][1]), fmaxf(sc[h][0][2], sc[h][0][3])),
-                      fmaxf(fmaxf(sc[h][1][0], sc[h][1][1]), fmaxf(sc[h][1][2], sc[h][1][3])));
-      t = fmaxf(t, fmaxf(fmaxf(fmaxf(sc[h][2][0], sc[h][2][1]), fmaxf(sc[h][2][2], sc[h][2][3])),
-                         fmaxf(fmaxf(sc[h][3][0], sc[h][3][1]), fmaxf(sc[h][3][2], sc[h][3][3]))));
-      t = fmaxf(t, __shfl_xor(t, 16, 64));
-      t = fmaxf(t, __shfl_xor(t, 32, 64));
-      tmax[h] = t * sl2;
-      if constexpr (!SLOW) {
-        if (kt == 0) m[h] = tmax[h];  // o and l are still 0: no rescale
-        big |= tmax[h] > m[h] + THR_FAST;
-      }
-    }
-    if constexpr (!SLOW) {
-      if (__any(big)) return false;
-    }
-    bf16x8 pb[REP][2];
-#pragma unroll
-    for (int h = 0; h < REP; ++h) {
-      if constexpr (SLOW) {
-        if (__any(tmax[h] > m[h] + THR)) {
-          nop_mfma();
-          const float mnew = fmaxf(m[h], tmax[h]);
-          const float alpha = exp2f(m[h] - mnew);
-          l[h] *= alpha;
-#pragma unroll
-          for (int dt = 0; dt < 8; ++dt) o[h][dt] *= alpha;
-          m[h] = mnew;
-        }
-      }
-      float rs = 0.f;
-#pragma unroll
-      for (int nt = 0; nt < 4; ++nt)
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const float p = exp2f(fmaf(sc[h][nt][i], sl2, -m[h]));
-          sc[h][nt][i] = p;
-          rs += p;
-        }
-      l[h] += rs;  // per-lane partial: the 4 lanes of a query share m, so their partials add up at the end
-      pb[h][0] = pack_acc(sc[h][0], sc[h][1]);
-      pb[h][1] = pack_acc(sc[h][2], sc[h][3]);
-    }
-#pragma unroll
-    for (int ks = 0; ks < 2; ++ks)
-#pragma unroll
-      for (int dt = 0; dt < 8; ++dt) {
-        const bf16x8 vf = lds_tr(Vs, off.tr[dt] + ks * 32 * ROWB);
-#pragma unroll
-        for (int h = 0; h < REP; ++h) mfma_acc(o[h][dt], vf, pb[h][ks]);
-      }
-    return true;
-  };
-  int kt = 0;
-#pragma nounroll
-  for (; kt < nkt; ++kt) {
-    if (kt + 1 < nkt) dma(kt + 1, smem + ((kt + 1) & 1) * 2 * TB);  // that stage's last reads: before the barrier
-    if (!tile(kt, std::false_type())) break;
-    __builtin_amdgcn_s_waitcnt(0);  // the next tile's DMA landed (this wave's pieces) ...
-    __syncthreads();                 // ... and every wave's; every wave is done reading this stage
-  }
-  if (kt < nkt) {  // rare: a score jumped past m + THR_FAST; tile kt again with rescaling, then the rest
-    nop_mfma();
-#pragma nounroll
-    for (int k2 = kt; k2 < nkt; ++k2) {
-      if (k2 > kt && k2 + 1 < nkt) dma(k2 + 1, smem + ((k2 + 1) & 1) * 2 * TB);
-      tile(k2, std::true_type());
-      __builtin_amdgcn_s_waitcnt(0);
-      __syncthreads();
-    }
-  }
-  nop_mfma();
-#pragma unroll
-  for (int h = 0; h < REP; ++h) {
-    float lt = l[h];
-    lt += __shfl_xor(lt, 16, 64);
-    lt += __shfl_xor(lt, 32, 64);
-    if (qok) {
-      const int hq = kvh * REP + h;
-      u16* op = out + (long)(start + qrow) * nq * D + hq * D + 4 * g;
-      const float inv = 1.f / lt;
-#pragma unroll
-      for (int dt = 0; dt < 8; ++dt) store4(op + 16 * dt, o[h][dt], inv);
-      if (g == 0) lse[(long)hq * total + start + qrow] = (m[h] + log2f(lt)) * LN2;
-    }
-  }
-}
-
-// v6 dQ (recompute, GQA-stacked): the fwd6 geometry — one workgroup per (kv head, sequence, 64-query block), wave w
-// owns positions q0 + 16 w .. + 15 for all REP query heads — recomputing S^T = K Q^T and dP^T = V dO^T per 64-key
-// tile, dS^T = P o (dP - delta) with P = exp2(S sl2 - lse) (lse and delta are per-lane scalars in this layout: lane
-// (g, r) holds query r), and dQ^T += K^T dS^T. Every K row / V row / K^T fragment read from LDS feeds REP MFMAs. Against
-// dq4 it triples the MFMA work but drops the lp x lp bf16 dS^T round trip through HBM (stores in the dK/dV kernel,
-// loads here). Q and dO fragments and the dQ accumulators live in AGPRs (MFMA B / C operands), S and dP in VGPRs.
-__device__ __forceinline__ void pin_frag(bf16x8& x) { asm volatile("" : "+a"(x)); }
-__device__ __forceinline__ f32x4 mfma_v0_a(const bf16x8& a, const bf16x8& b) {
-  f32x4 d;
-  asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, 0" : "=&v"(d) : "v"(a), "a"(b));
-  return d;
-}
-__device__ __forceinline__ void mfma_v_a(f32x4& c, const bf16x8& a, const bf16x8& b) {
-  asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+v"(c) : "v"(a), "a"(b));
-}
-
-template <int REP>
-__global__ __launch_bounds__(256, 1) void dq6_kernel(const u16* __restrict__ qkv, const u16* __restrict__ dout,
-                                                     const float* __restrict__ lse, const float* __restrict__ delta,
-                                                     const int* __restrict__ cu, u16* __restrict__ dqkv, int nq,
-                                                     int nkv, int total, float sl2, float scale, int causal,
-                                                     const float* __restrict__ rcos, const float* __restrict__ rsin) {
-  constexpr int TB = 64 * ROWB;
-  __shared__ __attribute__((aligned(16))) char smem[4 * TB];  // stage s: K image at 2 s TB, V image at (2 s + 1) TB
-  const int kvh = blockIdx.x, b = blockIdx.y, qb = gridDim.z - 1 - blockIdx.z;
-  const int start = cu[b], len = cu[b + 1] - start;
-  SFT_DASSERT(start >= 0 && len >= 0 && start + len <= total);
-  const int q0 = qb * 64;
-  if (q0 >= len) return;
-  const long ld = (long)(nq + 2 * nkv) * D;
-  const long ldo = (long)nq * D;
-  const int tid = threadIdx.x, lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6), g = lane >> 4;
-  const int wfirst = q0 + 16 * w, qrow = wfirst + (lane & 15);
-  const bool qok = qrow < len;
-  const int nkb = (len + 63) / 64;
-  const int nkt = causal ? min(qb + 1, nkb) : nkb;
-  const int r0 = 4 * w + (lane >> 4);  // DMA as fwd6
-  const u16* kvsrc = qkv + (long)start * ld + (nq + kvh) * D + 8 * swz(r0, lane & 15);
-  auto dma = [&](int kt, char* stage) {
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const u16* src = kvsrc + (long)min(kt * 64 + r0 + 16 * j, len - 1) * ld;
-      glds16(src, stage + (w + 4 * j) * 1024);
-      glds16(src + nkv * D, stage + TB + (w + 4 * j) * 1024);
-    }
-  };
-  dma(0, smem);
-  Offs off;
-  off.init(lane);
-  bf16x8 qf[REP][4], df[REP][4];
-  float lse2[REP], dl[REP];
-#pragma unroll
-  for (int h = 0; h < REP; ++h) {
-    const int hq = kvh * REP + h;
-    const u16* qp = qkv + (long)(start + qrow) * ld + hq * D + 8 * g;
-    const u16* dp = dout + (long)(start + qrow) * ldo + hq * D + 8 * g;
-#pragma unroll
-    for (int s = 0; s < 4; ++s) {
-      qf[h][s] = load_frag_global(qp + 32 * s, qok);
-      df[h][s] = load_frag_global(dp + 32 * s, qok);
-      pin_frag(qf[h][s]);
-      pin_frag(df[h][s]);
-    }
-    lse2[h] = qok ? lse[(long)hq * total + start + qrow] * LOG2E : 0.f;
-    dl[h] = qok ? delta[(long)hq * total + start + qrow] : 0.f;
-  }
-  f32x4 dq[REP][8];
-#pragma unroll
-  for (int h = 0; h < REP; ++h)
-#pragma unroll
-    for (int dt = 0; dt < 8; ++dt) {
-      dq[h][dt] = f32x4{0.f, 0.f, 0.f, 0.f};
-      pin_acc(dq[h][dt]);
-    }
-  __builtin_amdgcn_s_waitcnt(0);
-  __syncthreads();
-  nop_mfma();  // AGPR writes of the Q / dO fragments -> MFMA operand reads
-#pragma nounroll
-  for (int kt = 0; kt < nkt; ++kt) {
-    const int k0 = kt * 64;
-    const char* Ks = smem + (kt & 1) * 2 * TB;
-    const char* Vs = Ks + TB;
-    if (kt + 1 < nkt) dma(kt + 1, smem + ((kt + 1) & 1) * 2 * TB);
-    f32x4 sc[REP][4], dp[REP][4];
-#pragma unroll
-    for (int nt = 0; nt < 4; ++nt)
-#pragma unroll
-      for (int s = 0; s < 4; ++s) {
-        const bf16x8 kf = lds_row(Ks, off.row[s] + nt * 16 * ROWB);
-#pragma unroll
-        for (int h = 0; h < REP; ++h) {
-          if (s == 0) sc[h][nt] = mfma_v0_a(kf, qf[h][s]);
-          else mfma_v_a(sc[h][nt], kf, qf[h][s]);
-        }
-      }
-#pragma unroll
-    for (int nt = 0; nt < 4; ++nt)
-#pragma unroll
-      for (int s = 0; s < 4; ++s) {
-        const bf16x8 vf = lds_row(Vs, off.row[s] + nt * 16 * ROWB);
-#pragma unroll
-        for (int h = 0; h < REP; ++h) {
-          if (s == 0) dp[h][nt] = mfma_v0_a(vf, df[h][s]);
-          else mfma_v_a(dp[h][nt], vf, df[h][s]);
-        }
-      }
-    nop_mfma();
-    const bool need_mask = (k0 + 64 > len) || (causal && k0 + 63 > wfirst);
-    bf16x8 db[REP][2];
-#pragma unroll
-    for (int h = 0; h < REP; ++h) {
-#pragma unroll
-      for (int nt = 0; nt < 4; ++nt)
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          float p = exp2f(fmaf(sc[h][nt][i], sl2, -lse2[h]));
-          if (need_mask) {
-            const int key = k0 + 16 * nt + 4 * g + i;
-            if (key >= len || (causal && key > qrow)) p = 0.f;
-          }
-          dp[h][nt][i] = p * (dp[h][nt][i] - dl[h]);
-        }
-      db[h][0] = pack_acc(dp[h][0], dp[h][1]);
-      db[h][1] = pack_acc(dp[h][2], dp[h][3]);
-    }
-#pragma unroll
-    for (int ks = 0; ks < 2; ++ks)
-#pragma unroll
-      for (int dt = 0; dt < 8; ++dt) {
-        const bf16x8 kt_f = lds_tr(Ks, off.tr[dt] + ks * 32 * ROWB);
-#pragma unroll
-        for (int h = 0; h < REP; ++h) mfma_acc(dq[h][dt], kt_f, db[h][ks]);
-      }
-    __builtin_amdgcn_s_waitcnt(0);
-    __syncthreads();
-  }
-  nop_mfma();
-  if (!qok) return;
-#pragma unroll
-  for (int h = 0; h < REP; ++h) {
-    u16* qp = dqkv + (long)(start + qrow) * ld + (kvh * REP + h) * D + 4 * g;
-    if (rcos != nullptr) {
-      const long tr = (long)(start + qrow) * (D / 2) + 4 * g;
-      store4_rope_bwd(qp, dq[h], scale, rcos + tr, rsin + tr);
-    } else {
-#pragma unroll
-      for (int dt = 0; dt < 8; ++dt) store4(qp + 16 * dt, dq[h][dt], scale);
-    }
   }
 }
 
@@ -2144,160 +757,6 @@ __global__ __launch_bounds__(NW * 64) void bwd_dq3_kernel(const u16* __restrict_
     u16* qp = dqkv + (long)(start + qrow) * ld + h * D + 4 * g;
 #pragma unroll
     for (int dt = 0; dt < 8; ++dt) store4(qp + 16 * dt, dq[dt], scale);
-  }
-}
-
-__global__ __launch_bounds__(256, 2) void bwd_dkdv3_kernel(const u16* __restrict__ qkv, const u16* __restrict__ dout,
-                                                           const float* __restrict__ lse,
-                                                           const float* __restrict__ delta,
-                                                           const int* __restrict__ cu, float* __restrict__ part,
-                                                           u16* __restrict__ dqkv, int nq, int nkv, int total,
-                                                           float sl2, float scale, int causal,
-                                                           u16* __restrict__ dst = nullptr, int lp = 0) {
-  constexpr int NT = 256, TB = 64 * ROWB;
-  __shared__ __attribute__((aligned(16))) char smem[2 * TB + 2 * 64 * 4];
-  char* Qs = smem;
-  char* Os = smem + TB;
-  float* Ls = (float*)(smem + 2 * TB);
-  float* Dl = Ls + 64;
-  // grid (heads, sequences, key blocks): key block 0 (causally heaviest: every query tile) dispatched first
-  const int h = blockIdx.x, b = blockIdx.y, kb = blockIdx.z;
-  const int start = cu[b], len = cu[b + 1] - start;
-  const int k0 = kb * 64;
-  if (k0 >= len) return;
-  const int rep = nq / nkv;
-  const int kvh = h / rep, r = h - kvh * rep;
-  const long ld = (long)(nq + 2 * nkv) * D;
-  const long ldo = (long)nq * D;
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, g = lane >> 4;
-  const int wfirst = k0 + wave * 16;
-  const int key = wfirst + (lane & 15);
-  const bool kok = key < len;
-  const u16* qbase = qkv + (long)start * ld + h * D;
-  const u16* obase = dout + (long)start * ldo + h * D;
-  const float* lbase = lse + (long)h * total + start;
-  const float* dbase = delta + (long)h * total + start;
-  const int qt0 = causal ? kb : 0;
-  const int nqt = (len + 63) / 64;
-  Offs off;
-  off.init(lane);
-  {
-    const int q0 = qt0 * 64, qv = len - q0;
-    Stage<64, NT> tq, to;
-    tq.load(qbase + (long)q0 * ld, ld, qv, tid);
-    to.load(obase + (long)q0 * ldo, ldo, qv, tid);
-    tq.store(Qs, tid);
-    to.store(Os, tid);
-    if (tid < 64) {
-      Ls[tid] = tid < qv ? lbase[q0 + tid] * LOG2E : 0.f;
-      Dl[tid] = tid < qv ? dbase[q0 + tid] : 0.f;
-    }
-  }
-  bf16x8 kf[4], vf[4];
-  {
-    const u16* kp = qkv + (long)(start + key) * ld + (nq + kvh) * D + 8 * g;
-    const u16* vp = qkv + (long)(start + key) * ld + (nq + nkv + kvh) * D + 8 * g;
-#pragma unroll
-    for (int s = 0; s < 4; ++s) {
-      kf[s] = load_frag_global(kp + 32 * s, kok);
-      vf[s] = load_frag_global(vp + 32 * s, kok);
-    }
-  }
-  f32x4 dk[8], dv[8];
-#pragma unroll
-  for (int dt = 0; dt < 8; ++dt) {
-    dk[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
-    dv[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
-  }
-  __syncthreads();
-  for (int qt = qt0; qt < nqt; ++qt) {
-    const int q0 = qt * 64;
-    const bool pre = qt + 1 < nqt;
-    Stage<64, NT> tq, to;
-    float pl = 0.f, pd = 0.f;
-    if (pre) {
-      const int qn = q0 + 64, qv = len - qn;
-      tq.load(qbase + (long)qn * ld, ld, qv, tid);
-      to.load(obase + (long)qn * ldo, ldo, qv, tid);
-      if (tid < 64 && tid < qv) {
-        pl = lbase[qn + tid] * LOG2E;
-        pd = dbase[qn + tid];
-      }
-    }
-    if (!causal || wfirst <= q0 + 63) {
-      f32x4 sc[4], dp[4];
-#pragma unroll
-      for (int mt = 0; mt < 4; ++mt) {
-        sc[mt] = f32x4{0.f, 0.f, 0.f, 0.f};
-        dp[mt] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-        for (int s = 0; s < 4; ++s) {
-          sc[mt] = mfma(lds_row(Qs, off.row[s] + mt * 16 * ROWB), kf[s], sc[mt]);
-          dp[mt] = mfma(lds_row(Os, off.row[s] + mt * 16 * ROWB), vf[s], dp[mt]);
-        }
-      }
-      const bool need_mask = (q0 + 64 > len) || (causal && wfirst + 15 > q0);
-#pragma unroll
-      for (int mt = 0; mt < 4; ++mt) {
-        const float4 L4 = *(const float4*)(Ls + 16 * mt + 4 * g);
-        const float4 D4 = *(const float4*)(Dl + 16 * mt + 4 * g);
-        const float Lv[4] = {L4.x, L4.y, L4.z, L4.w}, Dv[4] = {D4.x, D4.y, D4.z, D4.w};
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          float p = exp2f(fmaf(sc[mt][i], sl2, -Lv[i]));
-          if (need_mask) {
-            const int q = q0 + 16 * mt + 4 * g + i;
-            if (q >= len || (causal && key > q)) p = 0.f;
-          }
-          sc[mt][i] = p;
-          dp[mt][i] = p * (dp[mt][i] - Dv[i]);
-        }
-      }
-      if (dst != nullptr && kok) {  // dS^T row of this lane's key: 4 consecutive queries per fragment (bf16)
-        u16* drow = dst + ((long)(b * nq + h) * lp + key) * lp + q0 + 4 * g;
-#pragma unroll
-        for (int mt = 0; mt < 4; ++mt) store4(drow + 16 * mt, dp[mt], 1.f);
-      }
-#pragma unroll
-      for (int ks = 0; ks < 2; ++ks) {
-        const bf16x8 pb = pack_acc(sc[2 * ks], sc[2 * ks + 1]);
-        const bf16x8 db = pack_acc(dp[2 * ks], dp[2 * ks + 1]);
-#pragma unroll
-        for (int dt = 0; dt < 8; ++dt) {
-          dv[dt] = mfma(lds_tr(Os, off.tr[dt] + ks * 32 * ROWB), pb, dv[dt]);
-          dk[dt] = mfma(lds_tr(Qs, off.tr[dt] + ks * 32 * ROWB), db, dk[dt]);
-        }
-      }
-    }
-    if (pre) {
-      __syncthreads();
-      tq.store(Qs, tid);
-      to.store(Os, tid);
-      if (tid < 64) {
-        Ls[tid] = pl;
-        Dl[tid] = pd;
-      }
-    }
-    __syncthreads();
-  }
-  if (!kok) return;
-  if (rep == 1) {
-    u16* kp = dqkv + (long)(start + key) * ld + (nq + kvh) * D + 4 * g;
-    u16* vp = dqkv + (long)(start + key) * ld + (nq + nkv + kvh) * D + 4 * g;
-#pragma unroll
-    for (int dt = 0; dt < 8; ++dt) {
-      store4(kp + 16 * dt, dk[dt], scale);
-      store4(vp + 16 * dt, dv[dt], 1.f);
-    }
-    return;
-  }
-  const long pld = 2L * nkv * D;
-  float* pk = part + ((long)r * total + start + key) * pld + kvh * D + 4 * g;
-  float* pv = pk + (long)nkv * D;
-#pragma unroll
-  for (int dt = 0; dt < 8; ++dt) {
-    *(float4*)(pk + 16 * dt) = make_float4(dk[dt][0], dk[dt][1], dk[dt][2], dk[dt][3]);
-    *(float4*)(pv + 16 * dt) = make_float4(dv[dt][0], dv[dt][1], dv[dt][2], dv[dt][3]);
   }
 }
 
@@ -2647,46 +1106,22 @@ __global__ __launch_bounds__(256 * G, G == 1 ? 2 : 1) void bwd_dkdv5_kernel(
   }
 }
 
-// SFTAMD_ATTN_LEGWAIT=1: the round-2 instruction schedule of fwd3 / dq4 / dK-dV v5 (prefetch latency exposed by
-// compiler-inserted vmcnt(0) waits), kept for same-process A/B timing only (tools/bench_attention.py ATTN_LEG=1)
-static bool attn_legacy_wait() {
-  const char* e = std::getenv("SFTAMD_ATTN_LEGWAIT");
-  return e && e[0] == '1';
-}
-
-// host launcher: G = 2 head groups when rep is even (SFTAMD_ATTN_GQA_SPLIT=0 forces 1)
+// host launcher of the GQA-grouped dK/dV: G = 2 head groups (Q / dO by LDS-DMA) when rep is even, else G = 1
 static void launch_dkdv5(const u16* qkv, const u16* dout, const float* lse, const float* delta, const int* cu,
                          u16* dqkv, int nq, int nkv, int total, int nseq, int max_seqlen, float sl2, float scale,
                          int causal, u16* dst, int lp, hipStream_t st, const float* rcos = nullptr,
                          const float* rsin = nullptr) {
   const int rep = nq / nkv;
-  const char* e = std::getenv("SFTAMD_ATTN_GQA_SPLIT");
-  const bool split = rep % 2 == 0 && !(e && e[0] == '0');
   dim3 grid(nkv, nseq, (max_seqlen + 63) / 64);
-  const bool leg = attn_legacy_wait();
-  const char* ed = std::getenv("SFTAMD_ATTN_BWD_DMA");
-  const bool dma = !leg && !(ed && ed[0] == '0');
-  if (split && dma)
+  if (rep % 2 == 0)
     bwd_dkdv5_kernel<2, false, true><<<grid, 512, 0, st>>>(qkv, dout, lse, delta, cu, dqkv, nq, nkv, total, sl2,
                                                            scale, causal, dst, lp, rcos, rsin);
-  else if (split && leg)
-    bwd_dkdv5_kernel<2, true><<<grid, 512, 0, st>>>(qkv, dout, lse, delta, cu, dqkv, nq, nkv, total, sl2, scale,
-                                                    causal, dst, lp, rcos, rsin);
-  else if (split)
-    bwd_dkdv5_kernel<2><<<grid, 512, 0, st>>>(qkv, dout, lse, delta, cu, dqkv, nq, nkv, total, sl2, scale, causal,
-                                              dst, lp, rcos, rsin);
   else
     bwd_dkdv5_kernel<1><<<grid, 256, 0, st>>>(qkv, dout, lse, delta, cu, dqkv, nq, nkv, total, sl2, scale, causal,
                                               dst, lp, rcos, rsin);
 }
 
 }  // namespace attn
-
-// SFTAMD_ATTN_GQA=0: per-query-head dK/dV + fp32 partials + dkdv_reduce (v4) instead of the GQA-grouped v5 kernel
-static bool attn_gqa_grouped() {
-  const char* e = std::getenv("SFTAMD_ATTN_GQA");
-  return !(e && e[0] == '0');
-}
 
 static void check_attn_args(const at::Tensor& qkv, const at::Tensor& cu, int64_t nq, int64_t nkv, int64_t hd) {
   SFT_CHECK_CUDA(qkv);
@@ -2698,72 +1133,15 @@ static void check_attn_args(const at::Tensor& qkv, const at::Tensor& cu, int64_t
   SFT_CHECK(cu.scalar_type() == at::kInt && cu.is_cuda() && cu.dim() == 1 && cu.numel() >= 2, "cu_seqlens int32");
 }
 
-// variant: 1 = ds_read_b64_tr_b16 transposed operand reads (default), 0 = scalar LDS gathers
-// implementation: 2 = double-buffered v2 kernels (default), 1 = v1 (single-buffered)
-// SFTAMD_ATTN_CONC=1: dq and dK/dV backward kernels concurrently on two HIP streams (they write disjoint
-// column ranges of dqkv). Measured neutral at the SmolLM3 shape (bwd 266.5 vs 262.5 us serial, end to end
-// within noise: profiles/r1_attention_microbench.txt), so serial is the default.
-static bool attn_concurrent_bwd() {
-  const char* e = std::getenv("SFTAMD_ATTN_CONC");
-  return e && e[0] == '1';
-}
-
-static long attn_ds_budget() {  // read per call (cheap next to the kernels): tests switch paths in-process
+// The dq4 backward stores the bf16 dS^T blocks of every (sequence, head) — nseq x nq x lp^2 x 2 bytes (134 MB for
+// 16 x 512 tokens, 16 heads); past SFTAMD_ATTN_DS_MB (default 2048, read per call so tests can switch paths
+// in-process) the dq3 kernel recomputes S / dP instead (long contexts).
+static long attn_ds_budget() {
   const char* e = std::getenv("SFTAMD_ATTN_DS_MB");
   return (e && e[0] ? atol(e) : 2048L) * 1024L * 1024L;
 }
 
-// SFTAMD_ATTN_DQ6=1: backward v6 (dK/dV without dS^T stores + the recomputing GQA-stacked dQ kernel)
-static bool attn_dq6() {
-  const char* e = std::getenv("SFTAMD_ATTN_DQ6");
-  return e && e[0] == '1';
-}
-
-// SFTAMD_ATTN_FWD6=1: the GQA-stacked v6 forward where it applies (2 or 4 query heads per kv head)
-static bool attn_fwd6() {
-  const char* e = std::getenv("SFTAMD_ATTN_FWD6");
-  return e && e[0] == '1';
-}
-
-// SFTAMD_ATTN_FWD7=1: the 4-wave, two-row-group LDS-DMA forward (fwd7_kernel)
-static bool attn_fwd7() {
-  const char* e = std::getenv("SFTAMD_ATTN_FWD7");
-  return e && e[0] == '1';
-}
-
-// fwd3 with K / V staged by LDS-DMA into two stages, one barrier per tile (default; SFTAMD_ATTN_FWD_DMA=0: register
-// staging). B16 x T512: 46.0 vs 51.8 us, ragged 16 x ~640: 65.0 vs 71.8 us (profiles/r3_attention.md)
-static bool attn_fwd_dma() {
-  const char* e = std::getenv("SFTAMD_ATTN_FWD_DMA");
-  return !(e && e[0] == '0');
-}
-
-static int attn_impl() {
-  const char* e = std::getenv("SFTAMD_ATTN_IMPL");
-  if (e && e[0] == '6') return 6;
-  if (e && e[0] == '1') return 1;
-  if (e && e[0] == '2') return 2;
-  if (e && e[0] == '4') return 4;  // forward v4 (measured slower, kept selectable: profiles/r1_attention_microbench.txt)
-  return 3;
-}
-
-// launch geometry for the v2 kernels: SFTAMD_ATTN_CFG="<waves fwd/dq: 4|8>,<LDS buffers: 1|2>"
-static void attn_cfg(int& nw, int& nbuf) {
-  nw = 8;
-  nbuf = 2;
-  const char* e = std::getenv("SFTAMD_ATTN_CFG");
-  if (e && e[0]) {
-    nw = (e[0] == '4') ? 4 : 8;
-    const char* c = std::strchr(e, ',');
-    if (c && c[1] == '1') nbuf = 1;
-  }
-}
-
-static int attn_variant() {
-  const char* e = std::getenv("SFTAMD_ATTN_TR");
-  return (e && e[0] == '0') ? 0 : 1;
-}
-
+// forward: fwd3 (8 waves x 16 query rows, K / V staged by LDS-DMA into two stages, one barrier per 64-key tile)
 std::tuple<at::Tensor, at::Tensor> flash_fwd(const at::Tensor& qkv, const at::Tensor& cu, int64_t max_seqlen,
                                              int64_t nq, int64_t nkv, int64_t hd, double scale, bool causal) {
   check_attn_args(qkv, cu, nq, nkv, hd);
@@ -2772,127 +1150,21 @@ std::tuple<at::Tensor, at::Tensor> flash_fwd(const at::Tensor& qkv, const at::Te
   auto out = at::empty({total, nq * hd}, qkv.options());
   auto lse = at::empty({nq, total}, qkv.options().dtype(at::kFloat));
   if (total == 0 || max_seqlen == 0) return {out, lse};
-  dim3 grid((max_seqlen + 63) / 64, nq, nseq);
   const float sl2 = (float)scale * attn::LOG2E;
   auto cu_c = cu.contiguous();
-  if (attn_impl() == 4) {  // forward v4 (2 row groups per wave); backward stays on v3
-    constexpr int NW = 4, RG = 2;
-    dim3 g4((max_seqlen + NW * 16 * RG - 1) / (NW * 16 * RG), nq, nseq);
-    attn::fwd4_kernel<NW, RG><<<g4, NW * 64, 0, cur_stream()>>>((const u16*)qkv.data_ptr(), (u16*)out.data_ptr(),
-                                                               lse.data_ptr<float>(), cu_c.data_ptr<int>(), nq, nkv,
-                                                               total, sl2, causal ? 1 : 0);
-    SFT_LAUNCH_CHECK();
-    return {out, lse};
-  }
-  const int rep = (int)(nq / nkv);
-  if (attn_impl() == 6 || (attn_impl() == 3 && attn_fwd6() && (rep == 2 || rep == 4))) {
-    SFT_CHECK(rep == 2 || rep == 4, "attention forward v6: 2 or 4 query heads per kv head");
-    SFT_TRACE("attn.fwd6");
-    dim3 g6(nkv, nseq, (max_seqlen + 63) / 64);
-    auto go6 = [&](auto r) {
-      attn::fwd6_kernel<decltype(r)::value><<<g6, 256, 0, cur_stream()>>>(
-          (const u16*)qkv.data_ptr(), (u16*)out.data_ptr(), lse.data_ptr<float>(), cu_c.data_ptr<int>(), nq, nkv, total,
-          sl2, causal ? 1 : 0);
-    };
-    if (rep == 4) go6(std::integral_constant<int, 4>()); else go6(std::integral_constant<int, 2>());
-    SFT_LAUNCH_CHECK();
-    return {out, lse};
-  }
-  if (attn_impl() == 3 && std::getenv("SFTAMD_ATTN_DIAG")) {  // timing-only ablations of fwd v3 (8 waves)
-    const int diag = atoi(std::getenv("SFTAMD_ATTN_DIAG"));
-    dim3 g3(nq, nseq, (max_seqlen + 127) / 128);
-    auto gd = [&](auto dg) {
-      attn::fwd3_kernel<8, decltype(dg)::value><<<g3, 512, 0, cur_stream()>>>(
-          (const u16*)qkv.data_ptr(), (u16*)out.data_ptr(), lse.data_ptr<float>(), cu_c.data_ptr<int>(), nq, nkv, total,
-          sl2, causal ? 1 : 0);
-    };
-    switch (diag) {
-      case 1: gd(std::integral_constant<int, 1>()); break;
-      case 2: gd(std::integral_constant<int, 2>()); break;
-      case 4: gd(std::integral_constant<int, 4>()); break;
-      case 8: gd(std::integral_constant<int, 8>()); break;
-      case 12: gd(std::integral_constant<int, 12>()); break;
-      case 15: gd(std::integral_constant<int, 15>()); break;
-      default: gd(std::integral_constant<int, 0>()); break;
-    }
-    SFT_LAUNCH_CHECK();
-    return {out, lse};
-  }
-  if (attn_impl() == 3 && attn_fwd7() && !attn::attn_legacy_wait()) {
-    SFT_TRACE("attn.fwd7");
-    dim3 g7(nq, nseq, (max_seqlen + 127) / 128);
-    attn::fwd7_kernel<<<g7, 256, 0, cur_stream()>>>((const u16*)qkv.data_ptr(), (u16*)out.data_ptr(),
-                                                    lse.data_ptr<float>(), cu_c.data_ptr<int>(), nq, nkv, total, sl2,
-                                                    causal ? 1 : 0);
-    SFT_LAUNCH_CHECK();
-    return {out, lse};
-  }
-  if (attn_impl() == 3) {
-    int nw, nbuf;
-    attn_cfg(nw, nbuf);
-    SFT_TRACE(nw == 8 ? "attn.fwd3" : "attn.fwd3.w4");
-    auto go3 = [&](auto w) {
-      constexpr int NW = decltype(w)::value;
-      dim3 g3(nq, nseq, (max_seqlen + NW * 16 - 1) / (NW * 16));
-      const char* e3 = std::getenv("SFTAMD_ATTN_FWD_DMA3");
-      if (NW == 8 && e3 && e3[0] == '1' && !attn::attn_legacy_wait())
-        attn::fwd3_kernel<8, 64><<<g3, 512, 0, cur_stream()>>>(
-            (const u16*)qkv.data_ptr(), (u16*)out.data_ptr(), lse.data_ptr<float>(), cu_c.data_ptr<int>(), nq, nkv,
-            total, sl2, causal ? 1 : 0);
-      else if (NW == 8 && attn_fwd_dma() && !attn::attn_legacy_wait())
-        attn::fwd3_kernel<8, 32><<<g3, 512, 0, cur_stream()>>>(
-            (const u16*)qkv.data_ptr(), (u16*)out.data_ptr(), lse.data_ptr<float>(), cu_c.data_ptr<int>(), nq, nkv,
-            total, sl2, causal ? 1 : 0);
-      else if (NW == 8 && attn::attn_legacy_wait())
-        attn::fwd3_kernel<NW, 16><<<g3, NW * 64, 0, cur_stream()>>>(
-            (const u16*)qkv.data_ptr(), (u16*)out.data_ptr(), lse.data_ptr<float>(), cu_c.data_ptr<int>(), nq, nkv,
-            total, sl2, causal ? 1 : 0);
-      else
-        attn::fwd3_kernel<NW><<<g3, NW * 64, 0, cur_stream()>>>((const u16*)qkv.data_ptr(), (u16*)out.data_ptr(),
-                                                               lse.data_ptr<float>(), cu_c.data_ptr<int>(), nq, nkv,
-                                                               total, sl2, causal ? 1 : 0);
-    };
-    if (nw == 4) go3(std::integral_constant<int, 4>()); else go3(std::integral_constant<int, 8>());
-    SFT_LAUNCH_CHECK();
-    return {out, lse};
-  }
-  if (attn_impl() == 2) {
-    int nw, nbuf;
-    attn_cfg(nw, nbuf);
-    auto go = [&](auto tr, auto w, auto b) {
-      constexpr bool TR = decltype(tr)::value;
-      constexpr int NW = decltype(w)::value, NB = decltype(b)::value;
-      dim3 g2((max_seqlen + NW * 16 - 1) / (NW * 16), nq, nseq);
-      attn::fwd2_kernel<TR, NW, NB><<<g2, NW * 64, 0, cur_stream()>>>(
-          (const u16*)qkv.data_ptr(), (u16*)out.data_ptr(), lse.data_ptr<float>(), cu_c.data_ptr<int>(), nq, nkv,
-          total, sl2, causal ? 1 : 0);
-    };
-    using I4 = std::integral_constant<int, 4>;
-    using I8 = std::integral_constant<int, 8>;
-    using B1 = std::integral_constant<int, 1>;
-    using B2 = std::integral_constant<int, 2>;
-    if (!attn_variant()) go(std::false_type(), I8(), B2());
-    else if (nw == 8 && nbuf == 2) go(std::true_type(), I8(), B2());
-    else if (nw == 8) go(std::true_type(), I8(), B1());
-    else if (nbuf == 2) go(std::true_type(), I4(), B2());
-    else go(std::true_type(), I4(), B1());
-    SFT_LAUNCH_CHECK();
-    return {out, lse};
-  }
-  if (attn_variant())
-    attn::fwd_kernel<true><<<grid, 256, 0, cur_stream()>>>((const u16*)qkv.data_ptr(), (u16*)out.data_ptr(),
-                                                           lse.data_ptr<float>(), cu_c.data_ptr<int>(), nq, nkv, total,
-                                                           sl2, causal ? 1 : 0);
-  else
-    attn::fwd_kernel<false><<<grid, 256, 0, cur_stream()>>>((const u16*)qkv.data_ptr(), (u16*)out.data_ptr(),
-                                                            lse.data_ptr<float>(), cu_c.data_ptr<int>(), nq, nkv, total,
-                                                            sl2, causal ? 1 : 0);
+  SFT_TRACE("attn.fwd3");
+  dim3 g3(nq, nseq, (max_seqlen + 127) / 128);
+  attn::fwd3_kernel<8, 32><<<g3, 512, 0, cur_stream()>>>((const u16*)qkv.data_ptr(), (u16*)out.data_ptr(),
+                                                         lse.data_ptr<float>(), cu_c.data_ptr<int>(), nq, nkv, total,
+                                                         sl2, causal ? 1 : 0);
   SFT_LAUNCH_CHECK();
   return {out, lse};
 }
 
-// rcos / rsin (optional, [total, hd / 2] fp32): apply the inverse rotate_half RoPE to the dq and dk heads in the
-// epilogues (v4 dq path + GQA-grouped dK/dV); sets rope_done. Other paths leave it to the caller.
+// backward: delta = rowsum(dO * O); GQA-grouped dK/dV (bwd_dkdv5: all query heads of a kv head in one workgroup, no
+// partials) writing dS^T, then dQ = one product per tile (bwd_dq4); past the dS^T budget dK/dV + the recomputing dq3.
+// rcos / rsin (optional, [total, hd / 2] fp32): the inverse rotate_half RoPE applied to the dq and dk heads in the
+// dq4 / dK epilogues (sets rope_done); the dq3 path leaves it to the caller.
 static at::Tensor flash_bwd_impl(const at::Tensor& dout, const at::Tensor& qkv, const at::Tensor& out,
                                  const at::Tensor& lse, const at::Tensor& cu, int64_t max_seqlen, int64_t nq,
                                  int64_t nkv, int64_t hd, double scale, bool causal, const float* rcos,
@@ -2913,194 +1185,38 @@ static at::Tensor flash_bwd_impl(const at::Tensor& dout, const at::Tensor& qkv, 
   SFT_LAUNCH_CHECK();
   const float sl2 = (float)scale * attn::LOG2E;
   auto cu_c = cu.contiguous();
-  dim3 gk((max_seqlen + 63) / 64, nkv, nseq);
-  dim3 gq((max_seqlen + 63) / 64, nq, nseq);
-  auto run = [&](auto tr) {
-    constexpr bool TR = decltype(tr)::value;
-    attn::bwd_dkdv_kernel<TR><<<gk, 256, 0, cur_stream()>>>(
-        (const u16*)qkv.data_ptr(), (const u16*)dout.data_ptr(), lse.data_ptr<float>(), delta.data_ptr<float>(),
-        cu_c.data_ptr<int>(), (u16*)dqkv.data_ptr(), nq, nkv, total, sl2, (float)scale, causal ? 1 : 0);
-    SFT_LAUNCH_CHECK();
-    attn::bwd_dq_kernel<TR><<<gq, 256, 0, cur_stream()>>>(
-        (const u16*)qkv.data_ptr(), (const u16*)dout.data_ptr(), lse.data_ptr<float>(), delta.data_ptr<float>(),
-        cu_c.data_ptr<int>(), (u16*)dqkv.data_ptr(), nq, nkv, total, sl2, (float)scale, causal ? 1 : 0);
-    SFT_LAUNCH_CHECK();
-  };
-  int nw, nbuf;
-  attn_cfg(nw, nbuf);
-  auto run2 = [&](auto tr, auto w, auto bb) {
-    constexpr bool TR = decltype(tr)::value;
-    constexpr int NW = decltype(w)::value, NB = decltype(bb)::value;
-    const int rep = nq / nkv;
-    at::Tensor part;
-    if (rep > 1) part = at::empty({(long)rep * total * 2 * nkv * hd}, qkv.options().dtype(at::kFloat));
-    dim3 gk2((max_seqlen + 63) / 64, nq, nseq);
-    attn::bwd_dkdv2_kernel<TR, NB><<<gk2, 256, 0, cur_stream()>>>(
-        (const u16*)qkv.data_ptr(), (const u16*)dout.data_ptr(), lse.data_ptr<float>(), delta.data_ptr<float>(),
-        cu_c.data_ptr<int>(), rep > 1 ? part.data_ptr<float>() : nullptr, (u16*)dqkv.data_ptr(), nq, nkv, total, sl2,
-        (float)scale, causal ? 1 : 0);
-    SFT_LAUNCH_CHECK();
-    if (rep > 1) {
-      const long nvec = (long)total * 2 * nkv * hd / 8;
-      const int grid = (int)std::min<long>((nvec + 255) / 256, 2048);
-      attn::dkdv_reduce_kernel<<<grid, 256, 0, cur_stream()>>>(part.data_ptr<float>(), (u16*)dqkv.data_ptr(), total,
-                                                               nq, nkv, rep, (float)scale);
-      SFT_LAUNCH_CHECK();
-    }
-    dim3 gq2((max_seqlen + NW * 16 - 1) / (NW * 16), nq, nseq);
-    attn::bwd_dq2_kernel<TR, NW, NB><<<gq2, NW * 64, 0, cur_stream()>>>(
-        (const u16*)qkv.data_ptr(), (const u16*)dout.data_ptr(), lse.data_ptr<float>(), delta.data_ptr<float>(),
-        cu_c.data_ptr<int>(), (u16*)dqkv.data_ptr(), nq, nkv, total, sl2, (float)scale, causal ? 1 : 0);
-    SFT_LAUNCH_CHECK();
-  };
-  using I4 = std::integral_constant<int, 4>;
-  using I8 = std::integral_constant<int, 8>;
-  using B1 = std::integral_constant<int, 1>;
-  using B2 = std::integral_constant<int, 2>;
-  // side stream for the dq kernel: forked after the delta kernel, joined before returning
-  hipStream_t dq_stream = cur_stream();
-  static thread_local hipEvent_t ev_fork = nullptr, ev_join = nullptr;
-  c10::optional<c10::hip::HIPStream> side;
-  if (attn_impl() >= 3 && attn_concurrent_bwd()) {
-    if (!ev_fork) {
-      C10_HIP_CHECK(hipEventCreateWithFlags(&ev_fork, hipEventDisableTiming));
-      C10_HIP_CHECK(hipEventCreateWithFlags(&ev_join, hipEventDisableTiming));
-    }
-    side = c10::hip::getStreamFromPool(false, qkv.device().index());
-    dq_stream = side->stream();
-    C10_HIP_CHECK(hipEventRecord(ev_fork, cur_stream()));
-    C10_HIP_CHECK(hipStreamWaitEvent(dq_stream, ev_fork, 0));
-  }
-  // v4 backward: dkdv3 stores dS^T, dQ = one product per tile (bwd_dq4_kernel). Needs the lp x lp bf16 dS^T
-  // blocks of every (sequence, head) — 134 MB for 16 x 512 tokens, 16 heads — so it is used when they fit
-  // SFTAMD_ATTN_DS_MB (default 2048); otherwise dq3 recomputes S / dP.
+  const u16* q = (const u16*)qkv.data_ptr();
+  const u16* dO = (const u16*)dout.data_ptr();
   const long lp = (max_seqlen + 127) / 128 * 128;
   const long ds_bytes = (long)nseq * nq * lp * lp * 2;
-  const int rep6 = nq / nkv;
-  if (attn_impl() >= 3 && !side && attn_dq6() && (rep6 == 2 || rep6 == 4) && attn_gqa_grouped()) {
-    // v6 backward: GQA-grouped dK/dV without the dS^T stores + the recomputing GQA-stacked dQ (no HBM round trip)
+  if (ds_bytes <= attn_ds_budget()) {
+    auto dst = at::empty({ds_bytes / 2}, qkv.options());
     const bool rope = rcos != nullptr;
     SFT_TRACE("attn.dkdv5");
-    SFT_TRACE("attn.dq6");
-    if (rope) SFT_TRACE("attn.bwd_rope_epi");
-    attn::launch_dkdv5((const u16*)qkv.data_ptr(), (const u16*)dout.data_ptr(), lse.data_ptr<float>(),
-                       delta.data_ptr<float>(), cu_c.data_ptr<int>(), (u16*)dqkv.data_ptr(), nq, nkv, total, nseq,
-                       max_seqlen, sl2, (float)scale, causal ? 1 : 0, nullptr, 0, cur_stream(), rcos, rsin);
-    SFT_LAUNCH_CHECK();
-    dim3 g6(nkv, nseq, (max_seqlen + 63) / 64);
-    auto go6 = [&](auto r) {
-      attn::dq6_kernel<decltype(r)::value><<<g6, 256, 0, cur_stream()>>>(
-          (const u16*)qkv.data_ptr(), (const u16*)dout.data_ptr(), lse.data_ptr<float>(), delta.data_ptr<float>(),
-          cu_c.data_ptr<int>(), (u16*)dqkv.data_ptr(), nq, nkv, total, sl2, (float)scale, causal ? 1 : 0, rcos, rsin);
-    };
-    if (rep6 == 4) go6(std::integral_constant<int, 4>()); else go6(std::integral_constant<int, 2>());
-    SFT_LAUNCH_CHECK();
-    rope_done = rope;
-    return dqkv;
-  }
-  if (attn_impl() >= 3 && !side && ds_bytes <= attn_ds_budget() && hd == 128) {
-    const int rep = nq / nkv;
-    auto dst = at::empty({ds_bytes / 2}, qkv.options());
-    const bool grouped = rep > 1 && attn_gqa_grouped();
-    const bool rope = grouped && rcos != nullptr;
-    at::Tensor part;
-    SFT_TRACE(grouped ? "attn.dkdv5" : "attn.dkdv3");
     SFT_TRACE("attn.dq4");
     if (rope) SFT_TRACE("attn.bwd_rope_epi");
-    if (grouped) {
-      attn::launch_dkdv5((const u16*)qkv.data_ptr(), (const u16*)dout.data_ptr(), lse.data_ptr<float>(),
-                         delta.data_ptr<float>(), cu_c.data_ptr<int>(), (u16*)dqkv.data_ptr(), nq, nkv, total, nseq,
-                         max_seqlen, sl2, (float)scale, causal ? 1 : 0, (u16*)dst.data_ptr(), (int)lp, cur_stream(),
-                         rope ? rcos : nullptr, rope ? rsin : nullptr);
-      SFT_LAUNCH_CHECK();
-    } else {
-      if (rep > 1) part = at::empty({(long)rep * total * 2 * nkv * hd}, qkv.options().dtype(at::kFloat));
-      dim3 gk3(nq, nseq, (max_seqlen + 63) / 64);
-      attn::bwd_dkdv3_kernel<<<gk3, 256, 0, cur_stream()>>>(
-          (const u16*)qkv.data_ptr(), (const u16*)dout.data_ptr(), lse.data_ptr<float>(), delta.data_ptr<float>(),
-          cu_c.data_ptr<int>(), rep > 1 ? part.data_ptr<float>() : nullptr, (u16*)dqkv.data_ptr(), nq, nkv, total, sl2,
-          (float)scale, causal ? 1 : 0, (u16*)dst.data_ptr(), (int)lp);
-      SFT_LAUNCH_CHECK();
-    }
-    if (rep > 1 && !grouped) {
-      const long nvec = (long)total * 2 * nkv * hd / 8;
-      const int grid = (int)std::min<long>((nvec + 255) / 256, 2048);
-      attn::dkdv_reduce_kernel<<<grid, 256, 0, cur_stream()>>>(part.data_ptr<float>(), (u16*)dqkv.data_ptr(), total,
-                                                               nq, nkv, rep, (float)scale);
-      SFT_LAUNCH_CHECK();
-    }
+    attn::launch_dkdv5(q, dO, lse.data_ptr<float>(), delta.data_ptr<float>(), cu_c.data_ptr<int>(),
+                       (u16*)dqkv.data_ptr(), nq, nkv, total, nseq, max_seqlen, sl2, (float)scale, causal ? 1 : 0,
+                       (u16*)dst.data_ptr(), (int)lp, cur_stream(), rcos, rsin);
+    SFT_LAUNCH_CHECK();
     dim3 gq4(nq, nseq, (max_seqlen + 127) / 128);
-    // SFTAMD_ATTN_DQ_DMA=1: K / dS^T by LDS-DMA (measured neutral: 130.2 vs 129.9 us bwd at B16 x T512, r3_run40;
-    // this kernel streams dS^T at ~60 % of HBM bandwidth, the staging is not its limit)
-    const char* edq = std::getenv("SFTAMD_ATTN_DQ_DMA");
-    if (!attn::attn_legacy_wait() && edq && edq[0] == '1')
-      attn::bwd_dq4_kernel<8, false, true><<<gq4, 512, 0, cur_stream()>>>(
-          (const u16*)qkv.data_ptr(), (const u16*)dst.data_ptr(), cu_c.data_ptr<int>(), (u16*)dqkv.data_ptr(), nq, nkv,
-          (int)lp, (float)scale, causal ? 1 : 0, rope ? rcos : nullptr, rope ? rsin : nullptr);
-    else if (attn::attn_legacy_wait())
-      attn::bwd_dq4_kernel<8, true><<<gq4, 512, 0, cur_stream()>>>(
-          (const u16*)qkv.data_ptr(), (const u16*)dst.data_ptr(), cu_c.data_ptr<int>(), (u16*)dqkv.data_ptr(), nq, nkv,
-          (int)lp, (float)scale, causal ? 1 : 0, rope ? rcos : nullptr, rope ? rsin : nullptr);
-    else
-      attn::bwd_dq4_kernel<8><<<gq4, 512, 0, cur_stream()>>>((const u16*)qkv.data_ptr(), (const u16*)dst.data_ptr(),
-                                                             cu_c.data_ptr<int>(), (u16*)dqkv.data_ptr(), nq, nkv,
-                                                             (int)lp, (float)scale, causal ? 1 : 0,
-                                                             rope ? rcos : nullptr, rope ? rsin : nullptr);
+    attn::bwd_dq4_kernel<8><<<gq4, 512, 0, cur_stream()>>>(q, (const u16*)dst.data_ptr(), cu_c.data_ptr<int>(),
+                                                           (u16*)dqkv.data_ptr(), nq, nkv, (int)lp, (float)scale,
+                                                           causal ? 1 : 0, rcos, rsin);
     SFT_LAUNCH_CHECK();
     rope_done = rope;
     return dqkv;
   }
-  auto run3 = [&](auto w) {
-    constexpr int NW = decltype(w)::value;
-    const int rep = nq / nkv;
-    SFT_TRACE("attn.dq3");
-    // dq first: on the side stream it starts filling the GPU while dK/dV is enqueued
-    dim3 gq3(nq, nseq, (max_seqlen + NW * 16 - 1) / (NW * 16));
-    attn::bwd_dq3_kernel<NW><<<gq3, NW * 64, 0, dq_stream>>>(
-        (const u16*)qkv.data_ptr(), (const u16*)dout.data_ptr(), lse.data_ptr<float>(), delta.data_ptr<float>(),
-        cu_c.data_ptr<int>(), (u16*)dqkv.data_ptr(), nq, nkv, total, sl2, (float)scale, causal ? 1 : 0);
-    SFT_LAUNCH_CHECK();
-    const bool grouped = rep > 1 && attn_gqa_grouped();
-    at::Tensor part;
-    if (grouped) {
-      attn::launch_dkdv5((const u16*)qkv.data_ptr(), (const u16*)dout.data_ptr(), lse.data_ptr<float>(),
-                         delta.data_ptr<float>(), cu_c.data_ptr<int>(), (u16*)dqkv.data_ptr(), nq, nkv, total, nseq,
-                         max_seqlen, sl2, (float)scale, causal ? 1 : 0, nullptr, 0, cur_stream());
-      SFT_LAUNCH_CHECK();
-    } else {
-      if (rep > 1) part = at::empty({(long)rep * total * 2 * nkv * hd}, qkv.options().dtype(at::kFloat));
-      dim3 gk3(nq, nseq, (max_seqlen + 63) / 64);
-      attn::bwd_dkdv3_kernel<<<gk3, 256, 0, cur_stream()>>>(
-          (const u16*)qkv.data_ptr(), (const u16*)dout.data_ptr(), lse.data_ptr<float>(), delta.data_ptr<float>(),
-          cu_c.data_ptr<int>(), rep > 1 ? part.data_ptr<float>() : nullptr, (u16*)dqkv.data_ptr(), nq, nkv, total, sl2,
-          (float)scale, causal ? 1 : 0);
-      SFT_LAUNCH_CHECK();
-    }
-    if (rep > 1 && !grouped) {
-      const long nvec = (long)total * 2 * nkv * hd / 8;
-      const int grid = (int)std::min<long>((nvec + 255) / 256, 2048);
-      attn::dkdv_reduce_kernel<<<grid, 256, 0, cur_stream()>>>(part.data_ptr<float>(), (u16*)dqkv.data_ptr(), total,
-                                                               nq, nkv, rep, (float)scale);
-      SFT_LAUNCH_CHECK();
-    }
-  };
-  if (attn_impl() >= 3) {
-    if (nw == 4) run3(I4()); else run3(I8());
-    if (side) {  // join: everything after this op on the current stream sees dq
-      C10_HIP_CHECK(hipEventRecord(ev_join, dq_stream));
-      C10_HIP_CHECK(hipStreamWaitEvent(cur_stream(), ev_join, 0));
-    }
-  } else if (attn_impl() == 2) {
-    if (!attn_variant()) run2(std::false_type(), I8(), B2());
-    else if (nw == 8 && nbuf == 2) run2(std::true_type(), I8(), B2());
-    else if (nw == 8) run2(std::true_type(), I8(), B1());
-    else if (nbuf == 2) run2(std::true_type(), I4(), B2());
-    else run2(std::true_type(), I4(), B1());
-  } else if (attn_variant()) {
-    run(std::true_type());
-  } else {
-    run(std::false_type());
-  }
+  SFT_TRACE("attn.dq3");
+  dim3 gq3(nq, nseq, (max_seqlen + 127) / 128);
+  attn::bwd_dq3_kernel<8><<<gq3, 512, 0, cur_stream()>>>(q, dO, lse.data_ptr<float>(), delta.data_ptr<float>(),
+                                                         cu_c.data_ptr<int>(), (u16*)dqkv.data_ptr(), nq, nkv, total,
+                                                         sl2, (float)scale, causal ? 1 : 0);
+  SFT_LAUNCH_CHECK();
+  attn::launch_dkdv5(q, dO, lse.data_ptr<float>(), delta.data_ptr<float>(), cu_c.data_ptr<int>(),
+                     (u16*)dqkv.data_ptr(), nq, nkv, total, nseq, max_seqlen, sl2, (float)scale, causal ? 1 : 0,
+                     nullptr, 0, cur_stream());
+  SFT_LAUNCH_CHECK();
   return dqkv;
 }
 

@@ -1170,8 +1170,12 @@ struct Stager5 {
   unsigned va, vb;       // lane byte offsets (A: within the tile's rows; B: within the weight)
   unsigned a32;          // bytes between A pieces j, j + 1 (32 rows)
   unsigned boff[8];      // B piece q relative to piece 0 (EPI row permutation), bytes
-  unsigned kb;           // K progress, bytes
-  __device__ __forceinline__ void adv(int k) { kb += 2 * k; }
+  unsigned kb;           // K progress, bytes (wraps at kbytes: a staggered K start walks k0 .. K, 0 .. k0)
+  unsigned kbytes;       // K * 2
+  __device__ __forceinline__ void adv(int k) {
+    kb += 2 * k;
+    kb = kb >= kbytes ? kb - kbytes : kb;
+  }
   __device__ __forceinline__ void piece(char* stage, int w, int j, int koff = 0) {
     char* dst = stage + (w + 4 * j) * 1024;
     if (j < 8)
@@ -1218,14 +1222,28 @@ __device__ __forceinline__ void tn5_sub(f32x4 (&acc)[8][8], const bf16x8 (&fa)[8
   }
 }
 
+// StaggerU-style K start (VAR & 6): tiles that share an A or B panel start their K loops at different 256-byte
+// (K-tile pair) offsets, so the workgroups of an XCD do not all hit the same K slice of a panel (and the same HBM
+// channels: K = 2048 rows are 4 KB apart) at the same moment. S offsets over the tile's (m, n) block indices.
+template <int VAR>
+__device__ __forceinline__ unsigned tn5_kstart(int m0, int n0, int npair) {
+  if constexpr ((VAR & 6) == 0) {
+    return 0u;
+  } else {
+    constexpr int S = (VAR & 4) ? 16 : 4;
+    const int s = ((m0 >> 8) + 3 * (n0 >> 8)) % S;
+    return (unsigned)((s % npair) * 256);
+  }
+}
+
 template <int EPI>
 __device__ __forceinline__ void tn5_stager(Stager5<EPI>& st, const u16* A, const u16* B, long lda, long ldb, int m0,
-                                           int n0, int w, int lane, int I) {
+                                           int n0, int w, int lane, int I, unsigned kb0 = 0) {
   const int lr = lane >> 3, ch = (lane & 7) ^ (4 * (w & 1) + (lr >> 1));
   st.ra = tile_rsrc(A + (long)m0 * lda);
   st.va = (unsigned)(((8 * w + lr) * lda + 8 * ch) * 2);
   st.vb = (unsigned)(((long)(b2_row<EPI>(w, n0, I) + lr) * ldb + 8 * ch) * 2);
-  st.kb = 0;
+  st.kb = kb0;
 }
 
 __device__ __forceinline__ void tn5_coords(int tile, int nbm, int nbn, int group, int& m0, int& n0) {
@@ -1244,12 +1262,15 @@ __device__ __forceinline__ unsigned pack2(float a, float b) { return (unsigned)f
 // one lane): rotate in registers (bf16 projection values, as the unfused path sees them), then pair lo / hi with
 // permlane16_swap — 32 stores. SWIGLU (fragments 2q / 2q + 1 = gate / up of the same act columns): gate / up paired
 // with each other, act (q) with act (q + 1) — 48 stores.
-template <int EPI>
+template <int EPI, int SV = 0>
 __device__ __forceinline__ void tn5_store(f32x4 (&acc)[8][8], const EpiArgs& ea, int row0, int m_col0, int wn,
                                           int lane) {
   const int g = lane >> 4, ii = lane & 15;
   if constexpr (EPI == EPI_PLAIN) {
     u16* base = ea.C + (long)(row0 + ii) * ea.ldc + m_col0 + 16 * (g & 1) + 4 * (g & 2);
+    // SV & 2: timing experiment only (wrong placement): the same 32 stores per lane in hipBLASLt's pattern, each
+    // instruction 4 rows x 256 contiguous bytes instead of 16 rows x 64 bytes
+    u16* base2 = ea.C + (long)(row0 + 32 * g) * ea.ldc + m_col0 + 8 * ii;
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
 #pragma unroll
@@ -1259,7 +1280,15 @@ __device__ __forceinline__ void tn5_store(f32x4 (&acc)[8][8], const EpiArgs& ea,
         unsigned w1 = pack2(acc[i][2 * p + 1][2], acc[i][2 * p + 1][3]);
         auto r0 = __builtin_amdgcn_permlane16_swap(v0, w0, false, false);
         auto r1 = __builtin_amdgcn_permlane16_swap(v1, w1, false, false);
-        *(uint4*)(base + (long)(16 * i) * ea.ldc + 32 * p) = make_uint4(r0[0], r1[0], r0[1], r1[1]);
+        uint4* dst = (SV & 2) ? (uint4*)(base2 + (long)(4 * i + p) * ea.ldc)
+                              : (uint4*)(base + (long)(16 * i) * ea.ldc + 32 * p);
+        const uint4 val = make_uint4(r0[0], r1[0], r0[1], r1[1]);
+        if constexpr (SV & 1) {  // nt: streaming store, as hipBLASLt's epilogue
+          typedef unsigned u32x4v __attribute__((ext_vector_type(4)));
+          __builtin_nontemporal_store(u32x4v{val.x, val.y, val.z, val.w}, (u32x4v*)dst);
+        } else {
+          *dst = val;
+        }
       }
     }
   } else if constexpr (EPI == EPI_ROPE) {
@@ -1325,7 +1354,10 @@ __device__ __forceinline__ void tn5_store(f32x4 (&acc)[8][8], const EpiArgs& ea,
   }
 }
 
-template <int EPI, bool NK2>
+// VAR: bit 0 = timing ablation, no epilogue stores (wrong results); bits 1 / 2 = staggered K start over 4 / 16
+// offsets (tn5_kstart). Launched with one workgroup per CU (persistent) or one per tile (the same code: a workgroup
+// whose next tile is past its XCD's range ends after one tile).
+template <int EPI, bool NK2, int VAR = 0>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1)))
 tn5_kernel(const u16* __restrict__ A, const u16* __restrict__ B, int K, long lda, long ldb, int nbm, int nbn,
            int group, EpiArgs ea) {
@@ -1354,11 +1386,12 @@ tn5_kernel(const u16* __restrict__ A, const u16* __restrict__ B, int K, long lda
   Stager5<EPI> st;
   st.rb = tile_rsrc(B);
   st.a32 = (unsigned)(64 * lda);
+  st.kbytes = (unsigned)(2 * K);
 #pragma unroll
   for (int q = 0; q < 8; ++q) st.boff[q] = (unsigned)(b2_koff<EPI, 4>(q) * ldb * 2);
   int m0, n0;
   tn5_coords(tile, nbm, nbn, group, m0, n0);
-  tn5_stager(st, A, B, lda, ldb, m0, n0, w, lane, ea.I);
+  tn5_stager(st, A, B, lda, ldb, m0, n0, w, lane, ea.I, tn5_kstart<VAR>(m0, n0, nk / 2));
 #pragma unroll
   for (int j = 0; j < 16; ++j) st.piece(X, w, j);
   st.adv(BK2);
@@ -1366,6 +1399,10 @@ tn5_kernel(const u16* __restrict__ A, const u16* __restrict__ B, int K, long lda
   for (int j = 0; j < 16; ++j) st.piece(Y, w, j);
   st.adv(BK2);
   __builtin_amdgcn_s_waitcnt(waitcnt_imm(16, 15));  // K0 of the first tile (its K1 may fly)
+  if constexpr (VAR & 8) {  // experiment: desynchronise the workgroups' tile boundaries by a start delay
+    const long long t0 = clock64(), d = (long long)(l & 15) * 3000;
+    while (clock64() - t0 < d) __builtin_amdgcn_s_sleep(4);
+  }
   f32x4 acc[8][8];
   bf16x8 a0[8], b0[8], a1[8], b1[8];
   bool first = true;
@@ -1400,7 +1437,7 @@ tn5_kernel(const u16* __restrict__ A, const u16* __restrict__ B, int K, long lda
       tn5_sub<EPI, false, true, 0, false>(acc, a0, b0, a1, b1, Y, offA1, offB1, st, Y, w);
       __builtin_amdgcn_s_waitcnt(waitcnt_imm(0, 0));
       if constexpr (LA) {
-        tn5_stager(st, A, B, lda, ldb, m1, n1, w, lane, ea.I);
+        tn5_stager(st, A, B, lda, ldb, m1, n1, w, lane, ea.I, tn5_kstart<VAR>(m1, n1, nk / 2));
         tn5_sub<EPI, false, false, 32, true>(acc, a1, b1, a0, b0, X, offA0, offB0, st, X, w, Y);
       } else {
         tn5_sub<EPI, false, true, 16, true>(acc, a1, b1, a0, b0, X, offA0, offB0, st, Y, w);
@@ -1417,7 +1454,17 @@ tn5_kernel(const u16* __restrict__ A, const u16* __restrict__ B, int K, long lda
     // the epilogue's accumulator reads follow the last MFMAs: 20 wait states + a fence against hoisting
     asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 3" ::: "memory");
     __builtin_amdgcn_sched_barrier(0);
-    tn5_store<EPI>(acc, ea, m0 + wm * 128, EPI == EPI_SWIGLU ? (n0 >> 1) + 64 * wn : n0 + wn * 128, wn, lane);
+    if constexpr (VAR & 1) {  // timing only: no stores (one value per lane keeps the accumulators live)
+      float sum = 0.f;
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) sum += acc[i][j][0] + acc[i][j][1] + acc[i][j][2] + acc[i][j][3];
+      if (sum == 1.2345f) ea.C[tid] = 1;
+    } else {
+      tn5_store<EPI, (VAR >> 4) & 3>(acc, ea, m0 + wm * 128, EPI == EPI_SWIGLU ? (n0 >> 1) + 64 * wn : n0 + wn * 128,
+                                      wn, lane);
+    }
     __builtin_amdgcn_sched_barrier(0);
     if (!has_next) break;
     st.adv(2 * BK2);
@@ -1433,20 +1480,21 @@ tn5_kernel(const u16* __restrict__ A, const u16* __restrict__ B, int K, long lda
   __builtin_amdgcn_s_waitcnt(waitcnt_imm(0, 15));
 }
 
-template <int EPI>
-void launch5(const at::Tensor& a, const at::Tensor& w, int N, const EpiArgs& ea) {
+template <int EPI, int VAR = 0>
+void launch5(const at::Tensor& a, const at::Tensor& w, int N, const EpiArgs& ea, bool persistent = true) {
   const int M = a.size(0), K = a.size(1);
   SFT_CHECK(M % 256 == 0 && N % 256 == 0 && K % 128 == 0, "gemm_tn persistent: M, N % 256, K % 128");
   SFT_CHECK(ea.ldc % 8 == 0 && ((uintptr_t)ea.C) % 16 == 0, "gemm_tn persistent: 16-byte aligned output rows");
   const int nbm = M / 256, nbn = N / 256, tiles = nbm * nbn;
-  const int grid = std::min(tiles, num_cus());
+  // one workgroup per tile: round the grid up to whole XCD rows so every XCD's range is covered one tile per block
+  const int grid = persistent ? std::min(tiles, num_cus()) : (tiles + 7) / 8 * 8;
   const int grp = std::min(group_m(), nbm);
   if (K == 128)
-    tn5_kernel<EPI, true><<<grid, 256, 0, cur_stream()>>>((const u16*)a.data_ptr(), (const u16*)w.data_ptr(), K,
-                                                          a.stride(0), w.stride(0), nbm, nbn, grp, ea);
+    tn5_kernel<EPI, true, VAR><<<grid, 256, 0, cur_stream()>>>((const u16*)a.data_ptr(), (const u16*)w.data_ptr(), K,
+                                                               a.stride(0), w.stride(0), nbm, nbn, grp, ea);
   else
-    tn5_kernel<EPI, false><<<grid, 256, 0, cur_stream()>>>((const u16*)a.data_ptr(), (const u16*)w.data_ptr(), K,
-                                                           a.stride(0), w.stride(0), nbm, nbn, grp, ea);
+    tn5_kernel<EPI, false, VAR><<<grid, 256, 0, cur_stream()>>>((const u16*)a.data_ptr(), (const u16*)w.data_ptr(), K,
+                                                                a.stride(0), w.stride(0), nbm, nbn, grp, ea);
   SFT_LAUNCH_CHECK();
 }
 
@@ -1530,6 +1578,22 @@ at::Tensor gemm_tn(const at::Tensor& a, const at::Tensor& w, int64_t cfg) {
     g4_tn(a, w, c, cfg == 60);
   } else if (cfg == 50) {  // persistent 4-wave (register epilogue, next tile's loads under this tile's end)
     tn::launch5<tn::EPI_PLAIN>(a, w, N, ea);
+  } else if ((cfg >= 51 && cfg <= 59) || (cfg >= 160 && cfg <= 163)) {  // tn5 variants (one tile per workgroup / staggered K start / no stores)
+    switch (cfg) {
+      case 51: tn::launch5<tn::EPI_PLAIN, 0>(a, w, N, ea, false); break;
+      case 52: tn::launch5<tn::EPI_PLAIN, 2>(a, w, N, ea); break;
+      case 53: tn::launch5<tn::EPI_PLAIN, 4>(a, w, N, ea); break;
+      case 54: tn::launch5<tn::EPI_PLAIN, 1>(a, w, N, ea); break;  // timing only: no stores
+      case 55: tn::launch5<tn::EPI_PLAIN, 2>(a, w, N, ea, false); break;
+      case 56: tn::launch5<tn::EPI_PLAIN, 1>(a, w, N, ea, false); break;  // timing only
+      case 58: tn::launch5<tn::EPI_PLAIN, 10>(a, w, N, ea); break;  // stagger 4 + start delay (experiment)
+      case 60 + 100: tn::launch5<tn::EPI_PLAIN, 16>(a, w, N, ea); break;      // nt stores
+      case 61 + 100: tn::launch5<tn::EPI_PLAIN, 32>(a, w, N, ea); break;      // hipBLASLt store pattern (timing only)
+      case 62 + 100: tn::launch5<tn::EPI_PLAIN, 48>(a, w, N, ea); break;      // both (timing only)
+      case 63 + 100: tn::launch5<tn::EPI_PLAIN, 16 + 2>(a, w, N, ea); break;  // nt + stagger 4
+      case 59: tn::launch5<tn::EPI_PLAIN, 8>(a, w, N, ea); break;   // start delay (experiment)
+      default: tn::launch5<tn::EPI_PLAIN, 4>(a, w, N, ea, false); break;
+    }
   } else if (cfg >= 13 && cfg <= 44) {  // cfg 12 schedule variants (tn4_kernel VAR = cfg - 12)
     switch (cfg - 12) {
       case 1: tn::launch4<tn::EPI_PLAIN, 0, 1>(a, w, N, ea); break;

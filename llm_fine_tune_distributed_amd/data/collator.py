@@ -31,6 +31,26 @@ class SFTCollator:
         self.packing = packing
         self.max_tokens = max_tokens
 
+    def max_batch_tokens(self, ds: TokenizedDataset, batch_size: int) -> int:
+        """Hard upper bound of ``input_ids.numel()`` for any batch of ``batch_size`` samples of ``ds``, from the data
+        actually held (not from ``max_length``, which a pre-tokenized dataset need not respect): padded batches are
+        ``batch_size`` x the longest (truncated) sample rounded up to the pad multiple; packed ones the sum of the
+        ``batch_size`` longest samples (or ``max_tokens``) rounded up the same way."""
+        lens = ds.lengths().to(torch.int64)
+        if lens.numel() == 0:
+            return 0
+        m = self.pad_to_multiple_of
+        rup = lambda x: -(-max(int(x), 1) // m) * m  # noqa: E731
+        if self.packing:
+            if self.max_tokens:
+                return rup(self.max_tokens)
+            k = min(int(batch_size), lens.numel())
+            return rup(int(torch.topk(lens, k).values.sum()))
+        L = int(lens.max())
+        if self.max_length:
+            L = min(L, self.max_length)
+        return int(batch_size) * rup(L)
+
     def __call__(self, ds: TokenizedDataset, indices: torch.Tensor) -> Dict:
         indices = indices.to(torch.int64)
         if self.packing:

@@ -22,9 +22,11 @@ before tearing the group down, and exits with 124 for a hang / deadline.
 from __future__ import annotations
 
 import argparse
+import json
 import os
 import signal
 import socket
+import shutil
 import subprocess
 import sys
 import tempfile
@@ -122,8 +124,16 @@ def _hung(hb_dir: str, n: int, node_rank: int, procs, started: float, hang_timeo
         if line is None:
             if now - started > startup:
                 return lr, f"no heartbeat within {startup:.0f} s of the start"
-        elif age > hang_timeout:
-            return lr, f"heartbeat unchanged for {age:.0f} s (hang timeout {hang_timeout:.0f} s)"
+            continue
+        try:
+            rec = json.loads(line)
+        except ValueError:
+            rec = {}
+        if rec.get("paused"):  # outside the training loop (utils/heartbeat.py pause())
+            continue
+        limit = max(hang_timeout, float(rec.get("limit_s", 0) or 0))  # a slow phase under Heartbeat.hold
+        if age > limit:
+            return lr, f"heartbeat unchanged for {age:.0f} s (hang limit {limit:.0f} s)"
     return None
 
 
@@ -155,17 +165,27 @@ def run(argv=None) -> int:
         cmd = [sys.executable, "-u", a.script] + a.args
     else:
         ap.error("need a script or -m module")
-    restart = 0
+    own_dir = not a.heartbeat_dir
     hb_dir = a.heartbeat_dir or tempfile.mkdtemp(prefix="sftamd_hb_")
+    os.makedirs(hb_dir, exist_ok=True)
+    try:
+        return _run_group(a, cmd, hb_dir)
+    finally:
+        if own_dir:
+            shutil.rmtree(hb_dir, ignore_errors=True)
+
+
+def _run_group(a, cmd, hb_dir: str) -> int:
+    restart = 0
     t_run = time.time()
+    n = a.nproc_per_node
     while True:
         port = a.master_port or _free_port(a.master_addr)
-        for f in os.listdir(hb_dir):  # a restarted group starts with no heartbeats
-            if f.endswith(".hb"):
-                try:
-                    os.remove(os.path.join(hb_dir, f))
-                except OSError:
-                    pass
+        for r in range(a.node_rank * n, (a.node_rank + 1) * n):  # this node's ranks restart with no heartbeats
+            try:  # (a shared directory also holds the other nodes' files: leave those)
+                os.remove(os.path.join(hb_dir, f"rank{r}.hb"))
+            except OSError:
+                pass
         started = time.time()
         procs = _spawn(a.nproc_per_node, cmd, a.master_addr, port, restart, a.node_rank, a.nnodes,
                        new_session=not a.same_session, hb_dir=hb_dir)

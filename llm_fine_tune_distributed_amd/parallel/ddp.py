@@ -30,9 +30,10 @@ peer, and RCCL stripes a collective over channels that use all N-1 of them, so a
 bytes costs about ``alpha + S / (N * L)`` (``alpha`` = per-call latency, ``L`` = effective per-link
 bandwidth). The cap is the smallest S whose latency share is <= ~15% (``S >= 5.7 * alpha * N * L``),
 clamped to [16, 256] MB and to >= 8 buckets over the model, then rounded so every one of the N shards is a
-whole number of 4 KiB pages. With the default ``alpha`` = 30 us and ``L`` = 100 GB/s (env
-``SFTAMD_XGMI_ALPHA_US`` / ``SFTAMD_XGMI_LINK_GBPS``) this gives 33 / 65 / 130 MB at N = 2 / 4 / 8 — grown
-with N because each rank moves only 1/N of a bucket per link (the reference's 50 MB cap,
+whole number of 4 KiB pages. ``alpha`` and ``L`` are MEASURED at startup (``measure_link``: reduce-scatters of
+two sizes, the max over ranks, ``fit_link``; the trainer does this when no cap is given) and fall back to the
+modelled 30 us / 100 GB/s (env ``SFTAMD_XGMI_ALPHA_US`` / ``SFTAMD_XGMI_LINK_GBPS``): 33 / 65 / 130 MB at
+N = 2 / 4 / 8 — grown with N because each rank moves only 1/N of a bucket per link (the reference's 50 MB cap,
 ``training.py:253``, was sized for a single TCP ring). The first bucket stays small (4 MB) so
 communication starts early in backward.
 
@@ -232,13 +233,63 @@ def plan_bucket_mb(world_size: int, total_bytes: int = 0, alpha_us: Optional[flo
     return float(min(256.0, max(16.0, mb)))
 
 
+def fit_link(points, world_size: int):
+    """(alpha_us, link_gbps) of ``t = alpha + S / (N L)`` through measured (bytes, seconds) reduce-scatter points
+    (least squares over >= 2 sizes; the slope is 1 / (N L): each rank moves 1/N of the buffer per link). Guarded
+    against noise: alpha >= 1 us, L in [1, 1000] GB/s."""
+    pts = sorted((float(b), float(t)) for b, t in points)
+    if len(pts) < 2 or pts[-1][0] <= pts[0][0]:
+        raise ValueError("fit_link needs >= 2 distinct message sizes")
+    n = len(pts)
+    mx = sum(b for b, _ in pts) / n
+    my = sum(t for _, t in pts) / n
+    sxx = sum((b - mx) ** 2 for b, _ in pts)
+    slope = sum((b - mx) * (t - my) for b, t in pts) / sxx
+    slope = max(slope, 1e-15)
+    alpha = max(1e-6, my - slope * mx)
+    link = 1.0 / (slope * max(1, world_size))
+    return alpha * 1e6, float(min(1000.0, max(1.0, link / 1e9)))
+
+
+def measure_link(world_size: int, device, group=None, sizes_mb=(4.0, 32.0), iters: int = 3):
+    """Startup probe of the gradient collective: in-place reduce-scatter of bf16 buffers of ``sizes_mb``, timed on
+    every rank; the MAX over ranks of each size's mean time (so every rank fits the SAME alpha / L and builds the
+    same bucket plan). Returns [(bytes, seconds), ...]."""
+    if world_size <= 1:
+        return []
+    import time
+    on_gpu = torch.device(device).type == "cuda"
+    sync = torch.cuda.synchronize if on_gpu else (lambda: None)
+    rank = dist.get_rank(group)
+    out = []
+    for mb in sizes_mb:
+        n = max(world_size * 64, int(mb * 2 ** 20 / 2) // (world_size * 64) * (world_size * 64))
+        buf = torch.ones(n, dtype=torch.bfloat16, device=device)
+        part = buf[rank * (n // world_size):(rank + 1) * (n // world_size)]
+        dist.reduce_scatter_tensor(part, buf, group=group)  # warm (RCCL channel setup on the first call)
+        sync()
+        dist.barrier(group=group)
+        t0 = time.perf_counter()
+        for _ in range(iters):
+            dist.reduce_scatter_tensor(part, buf, group=group)
+        sync()
+        out.append([n * 2, (time.perf_counter() - t0) / iters])
+        del buf, part
+    t = torch.tensor([p[1] for p in out], dtype=torch.float64, device=device)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX, group=group)
+    return [(p[0], float(v)) for p, v in zip(out, t.tolist())]
+
+
 class DDPEngine:
     def __init__(self, model: torch.nn.Module, world_size: int = 1, rank: int = 0,
                  bucket_cap_mb: Optional[float] = None, first_bucket_mb: float = 4.0,
                  grad_dtype: Optional[torch.dtype] = None,
                  broadcast_params: bool = False, align: int = 64, process_group=None,
                  no_decay_fn: Callable[[str, torch.Tensor], bool] = _no_decay, shard: bool = False,
-                 track_norm: Optional[bool] = None, split_oversized: bool = True, tied_sparse: Optional[bool] = None):
+                 track_norm: Optional[bool] = None, split_oversized: bool = True, tied_sparse: Optional[bool] = None,
+                 link: Optional[tuple] = None):
+        """``link``: (alpha_us, link_gbps) of the collective as measured at startup (``fit_link(measure_link(...))``);
+        with no ``bucket_cap_mb`` the bucket cap is planned from it instead of the modelled defaults."""
         self.model = model
         self.world_size = world_size
         self.rank = rank
@@ -286,8 +337,12 @@ class DDPEngine:
         esz = torch.empty((), dtype=self.grad_dtype).element_size()
         # bucket boundaries: multiples of world_size * (4 KiB of elements) -> equal, page-aligned shards
         pad_unit = max(align, SHARD_PAGE_BYTES // esz) * max(1, world_size)
+        self.plan_source = "user" if bucket_cap_mb else ("probe" if link else "model")
+        self.link_alpha_us = float(link[0]) if link else float(os.environ.get("SFTAMD_XGMI_ALPHA_US", "30"))
+        self.link_gbps = float(link[1]) if link else float(os.environ.get("SFTAMD_XGMI_LINK_GBPS", "100"))
         if not bucket_cap_mb:
-            bucket_cap_mb = plan_bucket_mb(world_size, sum(p.numel() for _, p in named) * esz)
+            bucket_cap_mb = plan_bucket_mb(world_size, sum(p.numel() for _, p in named) * esz,
+                                           alpha_us=self.link_alpha_us, link_gbps=self.link_gbps)
         self.bucket_cap_mb = float(bucket_cap_mb)
         cap = max(pad_unit, int(bucket_cap_mb * 1024 * 1024 / esz))
         first_cap = max(pad_unit, int(first_bucket_mb * 1024 * 1024 / esz))

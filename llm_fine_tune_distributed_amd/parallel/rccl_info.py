@@ -10,7 +10,8 @@ NCCL_DEBUG=INFO"; the reference's job runs with ``NCCL_DEBUG=INFO``, ``deploy/py
 * ``n_channels``: the number of channels of the communicator (``Channel xx/NN`` lines; RCCL stripes a collective
   over them, so on an 8-GPU mesh it should be well above one ring per link);
 * ``coll_channels`` / ``p2p_channels``: from the ``N coll channels, ... M p2p channels`` summary line;
-* ``version``: the ``RCCL version`` line; ``init_ok``: an ``Init COMPLETE`` line was seen.
+* ``version``: the ``RCCL version`` line; ``init_ok``: an ``Init COMPLETE`` line was seen; ``nranks``: the rank
+  count of the communicator (``comm ... nranks N`` lines) — must equal WORLD_SIZE.
 """
 from __future__ import annotations
 
@@ -23,6 +24,7 @@ _CHAN = re.compile(r"Channel (\d+)/(\d+)")
 _VIA = re.compile(r"via ((?:P2P|SHM|NET|NVLS|COLLNET)[^\s,]*(?: pointer)?(?:/read)?)")
 _SUMMARY = re.compile(r"(\d+) coll channels.*?(\d+) p2p channels")
 _VERSION = re.compile(r"RCCL version[^\d]*([\d.]+)|NCCL version[^\d]*([\d.]+)")
+_NRANKS = re.compile(r"nranks (\d+)")
 
 
 def enable(directory: str) -> str:
@@ -40,6 +42,7 @@ def summarize_text(text: str) -> Dict:
     nmax = 0
     coll = p2p = None
     version = None
+    nranks = None
     for line in text.splitlines():
         if "NCCL INFO" not in line and "RCCL" not in line:
             continue
@@ -52,12 +55,15 @@ def summarize_text(text: str) -> Dict:
         m = _SUMMARY.search(line)
         if m:
             coll, p2p = int(m.group(1)), int(m.group(2))
+        m = _NRANKS.search(line)
+        if m:
+            nranks = max(nranks or 0, int(m.group(1)))
         m = _VERSION.search(line)
         if m and version is None:
             version = m.group(1) or m.group(2)
     n = max(len(chans), nmax)
     return {"p2p_transport": sorted(via) or None, "n_channels": n or None, "coll_channels": coll,
-            "p2p_channels": p2p, "version": version, "init_ok": "Init COMPLETE" in text}
+            "p2p_channels": p2p, "version": version, "init_ok": "Init COMPLETE" in text, "nranks": nranks}
 
 
 def summarize(directory: str, pid: Optional[int] = None) -> Optional[Dict]:

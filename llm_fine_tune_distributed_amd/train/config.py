@@ -91,7 +91,8 @@ class SFTConfig:
     # parameters and bf16 moments, every bf16 write-back stochastically rounded (unbiased, so not less precise than the
     # reference's round-to-nearest), 14 HBM bytes per parameter and step. "auto" (default) = the parameter dtype, as
     # in torch: bf16 moments for the bf16 model the trainer builds (what bench.py runs), fp32 for an fp32 model.
-    # "fp32" forces fp32 moments (22 bytes), master_weights=True adds an fp32 master copy.
+    # "fp32" forces fp32 moments (22 bytes), master_weights=True adds an fp32 master copy (and makes "auto" fp32
+    # moments: the master path rounds to nearest, where a bf16 exp_avg_sq would stall).
     master_weights: bool = False
     stochastic_rounding: bool = True
     optim_state_dtype: str = "auto"
@@ -103,6 +104,10 @@ class SFTConfig:
     context_parallel_size: int = 1
     context_parallel_layout: str = "zigzag"   # zigzag (causal work balanced across the group) | contiguous
     ddp_first_bucket_mb: float = 4.0
+    # world > 1 with no ddp_bucket_cap_mb: time reduce-scatters of two sizes at startup, fit the per-call latency and
+    # per-link bandwidth, and plan the bucket cap from them (parallel/ddp.py measure_link / fit_link); False = the
+    # modelled 30 us / 100 GB/s
+    ddp_link_probe: bool = True
     ddp_broadcast_params: bool = False      # weights are identical by construction (seeded / loaded)
     ddp_check_sync_every: int = 0           # cross-rank param checksum every N steps (0 = off)
     # None = auto: on the GPU, padded batches are padded to a multiple of 64 tokens (and packed batches to 256)

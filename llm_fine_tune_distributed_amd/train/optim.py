@@ -43,11 +43,15 @@ def _update_stream(device: torch.device):
     return st
 
 
-def _state_dtype(state_dtype, engine) -> torch.dtype:
+def _state_dtype(state_dtype, engine, master_weights: bool = False) -> torch.dtype:
     """Adam moment dtype: "auto" = the parameter dtype (torch AdamW's state follows its parameters: bf16 for the
-    reference's bf16 model, training.py:99), "bf16" / "fp32", or a torch dtype."""
+    reference's bf16 model, training.py:99) — except with an fp32 master copy, where the update runs without
+    stochastic rounding and a round-to-nearest bf16 exp_avg_sq would stall (beta2 = 0.999 moves it by less than
+    half a bf16 ulp per step), so "auto" means fp32 there; "bf16" / "fp32", or a torch dtype."""
     if isinstance(state_dtype, str):
         if state_dtype == "auto":
+            if master_weights:
+                return torch.float32
             return engine.dtype if engine.dtype in (torch.float32, torch.bfloat16) else torch.float32
         state_dtype = {"fp32": torch.float32, "float32": torch.float32, "bf16": torch.bfloat16,
                        "bfloat16": torch.bfloat16}[state_dtype]
@@ -82,7 +86,7 @@ class FlatAdamW:
         self.step_count = 0
         n = engine.numel
         dev = engine.device
-        state_dtype = _state_dtype(state_dtype, engine)
+        state_dtype = _state_dtype(state_dtype, engine, master_weights)
         if state_dtype not in (torch.float32, torch.bfloat16):
             raise ValueError(f"optimizer state dtype must be fp32 or bf16, got {state_dtype}")
         self.state_dtype = state_dtype
@@ -321,7 +325,7 @@ class ShardedAdamW(FlatAdamW):
         self.master_weights = master_weights
         self.stochastic_rounding = stochastic_rounding and not master_weights
         self.step_count = 0
-        self.state_dtype = state_dtype = _state_dtype(state_dtype, engine)
+        self.state_dtype = state_dtype = _state_dtype(state_dtype, engine, master_weights)
         e = engine
         # owned slice of every bucket -> offset in the local (sharded) state buffers
         self.slices = []  # (bucket, start, end, local_offset, decay)

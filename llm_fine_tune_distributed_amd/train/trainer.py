@@ -128,24 +128,18 @@ class SFTTrainer:
                                                      if args.packing else None)
         # ------------------------------------------------------------ engine + optimizer
         shard = bool(args.shard_optimizer_state) and self.dist.world_size > 1
+        link, self.link_points = None, []
+        if self.dist.world_size > 1 and not args.ddp_bucket_cap_mb and args.ddp_link_probe:
+            # measured collective cost -> bucket cap (every rank fits the same max-over-ranks timings)
+            from ..parallel.ddp import fit_link, measure_link
+            self.link_points = measure_link(self.dist.world_size, dev)
+            link = fit_link(self.link_points, self.dist.world_size)
         self.engine = DDPEngine(model, self.dist.world_size, self.dist.rank,
                                 bucket_cap_mb=args.ddp_bucket_cap_mb,  # None: xGMI plan (plan_bucket_mb)
                                 first_bucket_mb=args.ddp_first_bucket_mb,
-                                broadcast_params=args.ddp_broadcast_params, shard=shard)
+                                broadcast_params=args.ddp_broadcast_params, shard=shard, link=link)
         if self.engine.tied_sparse:
-            # most tokens one synchronising pass can hold (every rank computes the same bound from the config):
-            # the sparse tied-embedding exchange gathers that many rows without a device sync
-            L = int(args.max_length or 1024)
-            if self.packed:
-                per_pass = -(-args.per_device_train_batch_size * L // 256) * 256
-            else:
-                pm = int(pad_mult or 1)
-                per_pass = args.per_device_train_batch_size * (-(-L // pm) * pm)  # padded to the collator's multiple
-            if args.gradient_accumulation_steps > 1 and getattr(args, "ga_merge_max_tokens", 0):
-                per_pass = max(per_pass, int(args.ga_merge_max_tokens))
-            cap = -(-per_pass // self.cp_size)
-            V = model.config.vocab_size
-            self.engine.sparse_cap = cap if cap * self.dist.world_size < V else 0  # else: measured per step
+            self.engine.sparse_cap = self._sparse_cap()
         if getattr(args, "lm_head_chunk_rows", 0):
             from ..ops import set_lm_head_chunk
             set_lm_head_chunk(args.lm_head_chunk_rows)
@@ -179,6 +173,28 @@ class SFTTrainer:
         if self.heartbeat.info is None:  # a caller's heartbeat (bench.py): add this engine's bucket position
             self.heartbeat.info = info
         self._hb_step = 0
+
+    def _sparse_cap(self) -> int:
+        """Most tokens one synchronising pass can hold, identical on every rank: the sparse tied-embedding exchange
+        gathers that many rows without a device sync. Derived from the collator in use and the training data it
+        will see (``SFTCollator.max_batch_tokens``: the bound holds by construction, so no rank can overflow it while
+        the others wait in the gather). 0 (= every rank measures the pass with a MAX all-reduce) for a custom
+        collator, an unknown dataset, or a bound so large the dense path is as cheap."""
+        a = self.args
+        if type(self.collator) is not SFTCollator or not isinstance(self.train_dataset, TokenizedDataset):
+            return 0
+        B = a.per_device_train_batch_size
+        per_pass = self.collator.max_batch_tokens(self.train_dataset, B)
+        if per_pass <= 0:
+            return 0
+        if self.cp_size > 1:  # shard_batch pads T to 2 cp (zig-zag) / cp and hands each rank B x Tp / cp tokens
+            unit = 2 * self.cp_size if a.context_parallel_layout == "zigzag" else self.cp_size
+            T = per_pass // B
+            per_pass = B * (-(-T // unit) * unit) // self.cp_size
+        elif a.gradient_accumulation_steps > 1 and getattr(a, "ga_merge_max_tokens", 0):
+            per_pass = max(per_pass, int(a.ga_merge_max_tokens))  # a merged pass holds at most this many
+        V = self.model.config.vocab_size
+        return per_pass if per_pass * self.dist.world_size < V else 0
 
     # ------------------------------------------------------------------ data helpers
     @staticmethod
@@ -386,7 +402,9 @@ class SFTTrainer:
         self.model.eval()
         acc = torch.zeros(5, device=self.dist.device)  # loss_sum, correct, entropy_sum, valid, samples
         loader = self.get_eval_dataloader()
+        beat = self.heartbeat.beat
         for b in loader:
+            beat(self._hb_step, "eval")
             b = self._cp_shard(b)
             out = self.model(**self._model_inputs(b), num_items_in_batch=1.0)
             acc[0] += out.loss
@@ -417,6 +435,10 @@ class SFTTrainer:
         self.control = self.callback_handler.call("on_log", self.args, self.state, self.control, logs=logs)
 
     def _save_checkpoint(self):
+        with self.heartbeat.hold("ckpt_save", step=self._hb_step):  # rank 0 writes while the others wait
+            return self._save_checkpoint_impl()
+
+    def _save_checkpoint_impl(self):
         self.optimizer.synchronize()
         a = self.args
         path = os.path.join(a.output_dir, f"checkpoint-{self.state.global_step}")
@@ -439,10 +461,11 @@ class SFTTrainer:
         """Rank 0 writes the HF directory; every rank waits. ``merge_lora`` folds LoRA adapters into the
         saved weights (export for plain HF / llama.cpp consumers) instead of writing them separately."""
         output_dir = output_dir or self.args.output_dir
-        self.optimizer.synchronize()
-        if self.dist.is_main:
-            ckpt.save_pretrained(self.model, output_dir, tokenizer=self.tokenizer, merge_lora=merge_lora)
-        barrier()
+        with self.heartbeat.hold("save_model", step=self._hb_step):
+            self.optimizer.synchronize()
+            if self.dist.is_main:
+                ckpt.save_pretrained(self.model, output_dir, tokenizer=self.tokenizer, merge_lora=merge_lora)
+            barrier()
 
     def _update_best(self, metrics: Dict[str, float], ckpt_path: Optional[str]):
         key = self.args.metric_for_best_model or "eval_loss"
@@ -462,6 +485,15 @@ class SFTTrainer:
 
     # ------------------------------------------------------------------ train
     def train(self, resume_from_checkpoint: Optional[str] = None) -> TrainOutput:
+        """The training loop; the hang watchdog is armed only while it runs (slow phases inside it — checkpoint
+        load / save, the first step — under ``Heartbeat.hold``)."""
+        self.heartbeat.resume()
+        try:
+            return self._train(resume_from_checkpoint)
+        finally:
+            self.heartbeat.pause()
+
+    def _train(self, resume_from_checkpoint: Optional[str] = None) -> TrainOutput:
         a = self.args
         loader = self.get_train_dataloader()
         ga = max(1, a.gradient_accumulation_steps)
@@ -480,7 +512,8 @@ class SFTTrainer:
             if resume is True or resume == "auto":
                 resume = ckpt.latest_checkpoint(a.output_dir)
             if resume:
-                st, _ = ckpt.load_checkpoint(resume, self.model, self.optimizer, self.scheduler, self.dist.rank)
+                with self.heartbeat.hold("ckpt_load"):
+                    st, _ = ckpt.load_checkpoint(resume, self.model, self.optimizer, self.scheduler, self.dist.rank)
                 st.is_world_process_zero = self.dist.is_main
                 self.state = st
                 start_epoch = self.state.global_step // steps_per_epoch
@@ -526,7 +559,11 @@ class SFTTrainer:
                     break
                 self.control = self.callback_handler.call("on_step_begin", a, self.state, self.control)
                 lr = self.scheduler.get_lr()
-                r = self.optimizer_step(micro, lr)
+                if self.state.global_step == start_step:  # first step: GEMM tuning / warm-up may take a while
+                    with self.heartbeat.hold("first_step", step=self._hb_step + 1):
+                        r = self.optimizer_step(micro, lr)
+                else:
+                    r = self.optimizer_step(micro, lr)
                 self.scheduler.step()
                 run_acc += r["acc"]
                 total_loss += r["acc"][0]
@@ -606,6 +643,7 @@ class SFTTrainer:
                    "train_mfu": flops / pure / (PEAK_BF16_FLOPS * self.dist.world_size)
                    if self.dist.device.type == "cuda" else 0.0}
         if a.load_best_model_at_end and self.state.best_model_checkpoint:
+            self.heartbeat.pause()  # host-side load: nothing beats
             sd = ckpt.load_state_dict(self.state.best_model_checkpoint, device="cpu")
             with torch.no_grad():
                 self.model.load_hf_state_dict({k: v.to(torch.bfloat16) for k, v in sd.items()}, strict=False)

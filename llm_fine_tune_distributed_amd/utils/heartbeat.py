@@ -14,11 +14,18 @@ Every rank records where it is â€” step, phase, last gradient bucket launched â€
   (e.g. under an external ``torchrun``) â€” it prints the last heartbeat and exits the process with code 124 instead
   of waiting for the process-group timeout. ``deadline_s`` bounds the whole run the same way.
 
+Phases that legitimately run long without beats â€” checkpoint I/O (rank 0 writes while the others wait in a
+barrier), checkpoint loading, the first step (GEMM tuning, extension warm-up) â€” run inside ``hold(phase)``,
+which allows them the slow-phase limit (``SFTAMD_SLOW_PHASE_TIMEOUT_S``, default max(4 x hang timeout, 1800 s))
+instead of the hang timeout; ``pause()`` / ``resume()`` switch the hang check off outside the training loop
+(before ``train()`` and after it returns), where nothing beats at all. The deadline always applies.
+
 A beat is a few microseconds of host work (no device sync); with no directory, no stderr cadence and no
 watchdog configured, ``beat`` is a no-op.
 """
 from __future__ import annotations
 
+import contextlib
 import json
 import os
 import sys
@@ -44,6 +51,10 @@ class Heartbeat:
         if hang_timeout_s is None:
             hang_timeout_s = float(os.environ.get("SFTAMD_HANG_TIMEOUT_S", "0") or 0)
         self.hang_timeout = hang_timeout_s
+        slow = float(os.environ.get("SFTAMD_SLOW_PHASE_TIMEOUT_S", "0") or 0)
+        self.slow_timeout = slow if slow > 0 else max(4.0 * hang_timeout_s, 1800.0)
+        self._limit = hang_timeout_s  # the hang limit in force (raised inside hold())
+        self._paused = False
         if deadline_s is None:
             deadline_s = float(os.environ.get("SFTAMD_RUN_DEADLINE_S", "0") or 0) or None
         self.deadline = deadline_s
@@ -78,6 +89,10 @@ class Heartbeat:
             except Exception:
                 pass
         rec.update(extra)
+        if self._paused:
+            rec["paused"] = True  # launch.py skips the hang check of a paused rank
+        elif self._limit != self.hang_timeout:
+            rec["limit_s"] = self._limit  # ... and applies a hold's longer limit
         self.last = rec
         self._last_beat = time.monotonic()
         line = _fmt(rec)
@@ -96,14 +111,38 @@ class Heartbeat:
             self._err_steps.add(s)
             print(f"[heartbeat] {line}", file=sys.stderr, flush=True)
 
+    @contextlib.contextmanager
+    def hold(self, phase: str, timeout_s: Optional[float] = None, step: Optional[int] = None):
+        """A phase allowed ``timeout_s`` (default: the slow-phase limit) without beats; beats on entry and exit."""
+        prev = self._limit
+        if self.hang_timeout > 0:
+            self._limit = max(self.hang_timeout, timeout_s or self.slow_timeout)
+        self.beat(step, phase)
+        try:
+            yield
+        finally:
+            self._limit = prev
+            self.beat(step, f"{phase}_done")
+
+    def pause(self):
+        """No hang check until ``resume()`` (the deadline still applies)."""
+        self._paused = True
+        self.beat(None, "idle")
+
+    def resume(self):
+        self._last_beat = time.monotonic()
+        self._paused = False
+        self.beat(None, "resume")
+
     # ------------------------------------------------------------------ watchdog
     def _watch(self):
         while not self._stop.wait(1.0):
             idle = time.monotonic() - self._last_beat
             over = self.deadline and time.time() - self.t0 > self.deadline
-            if (self.hang_timeout > 0 and idle > self.hang_timeout) or over:
+            limit = self._limit
+            if (limit > 0 and not self._paused and idle > limit) or over:
                 why = (f"deadline of {self.deadline:.0f} s exceeded" if over else
-                       f"no progress for {idle:.0f} s (hang timeout {self.hang_timeout:.0f} s)")
+                       f"no progress for {idle:.0f} s (hang limit {limit:.0f} s)")
                 print(f"[watchdog] rank {self.rank}: {why}; last heartbeat {_fmt(self.last)}", file=sys.stderr,
                       flush=True)
                 os._exit(EXIT_HANG)

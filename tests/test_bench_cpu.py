@@ -37,9 +37,20 @@ def test_bench_self_launches_n_ranks(n):
     assert rec["config"]["global_batch"] == 2 * n and rec["config"]["parallelism"] == f"dp{n}"
     assert rec["dist"]["world_size"] == n and rec["dist"]["consistent"]
     assert len(rec["per_rank"]) == n
+    for k in ("rccl_info", "p2p_transport", "n_channels", "n_channels_per_rank", "rccl_nranks_per_rank",
+              "rccl_saw_all_ranks", "link_probe"):
+        assert k in rec["dist"], k  # the multi-GPU record explains itself (None / [] where it cannot apply)
+    for k in ("plan_source", "alpha_us", "link_gbps"):
+        assert k in rec["bucket_plan"], k
     if n > 1:
         assert rec["dist"]["backend"] == "gloo" and rec["dist"]["launcher"] == "sftamd"
         assert rec["optimizer_sharding"] == "zero1"
+        # gloo rehearsal: no RCCL log to read, but the startup link probe ran and planned the buckets
+        assert rec["dist"]["rccl_info"] is False and len(rec["dist"]["n_channels_per_rank"]) == n
+        assert rec["bucket_plan"]["plan_source"] == "probe" and len(rec["dist"]["link_probe"]) == 2
+        assert rec["bucket_plan"]["alpha_us"] >= 1.0 and rec["bucket_plan"]["link_gbps"] >= 1.0
+    else:
+        assert rec["bucket_plan"]["plan_source"] == "model" and rec["dist"]["link_probe"] == []
     assert rec["bucket_plan"]["count"] >= 1
     assert rec["scaling_efficiency"] == pytest.approx(rec["value"] / (n * 10), rel=1e-3)
     assert rec["value"] > 0 and rec["final_loss"] > 0
@@ -86,6 +97,7 @@ def test_rccl_info_summary_parser():
         "channels per peer",
         "host:1:1 [0] NCCL INFO comm 0x1 rank 0 nranks 8 cudaDev 0 busId 1000 - Init COMPLETE"])
     s = summarize_text(log)
+    assert s["nranks"] == 8
     assert s["n_channels"] == 32 and s["coll_channels"] == 32 and s["p2p_channels"] == 32
     assert s["p2p_transport"] == ["P2P/IPC", "P2P/direct pointer"] and s["init_ok"] and s["version"] == "2.22.3"
     assert summarize_text("")["n_channels"] is None

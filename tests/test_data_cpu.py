@@ -155,3 +155,22 @@ def test_tokenisation_on_main_process_first_with_cache():
     mp.spawn(_main_first_worker, args=(2, port(), d, True), nprocs=2, join=True)  # cache hit on every rank
     c0 = torch.load(os.path.join(d, "tok1_0.pt"))
     assert torch.equal(c0["tokens"], r0["tokens"])
+
+
+def test_collator_max_batch_tokens_bounds_every_batch():
+    """SFTCollator.max_batch_tokens is a hard bound of input_ids.numel() over every batch (padded, padding-free,
+    explicit packing), derived from the data itself: the sparse tied-embedding gather size relies on it."""
+    import torch
+    from llm_fine_tune_distributed_amd.data.collator import SFTCollator
+    from llm_fine_tune_distributed_amd.data.dataset import TokenizedDataset
+    ds = TokenizedDataset.synthetic(40, 500, 3, 37, seed=11)
+    g = torch.Generator().manual_seed(0)
+    for col in (SFTCollator(0, 64, None, False), SFTCollator(0, 8, 16, False), SFTCollator(0, 256, None, True),
+                SFTCollator(0, 1, None, True), SFTCollator(0, 16, 64, True, max_tokens=64)):
+        for B in (1, 3, 7):
+            cap = col.max_batch_tokens(ds, B)
+            worst = 0
+            for _ in range(30):
+                idx = torch.randperm(len(ds), generator=g)[:B]
+                worst = max(worst, col(ds, idx)["input_ids"].numel())
+            assert 0 < worst <= cap, (col.__dict__, B, worst, cap)

@@ -138,3 +138,65 @@ def test_engine_uses_native_reducer():
     m = build_model(tiny(), dtype=torch.float32, seed=0)
     eng = DDPEngine(m, world_size=2, rank=0, bucket_cap_mb=0.05, first_bucket_mb=0.01)
     assert eng._tracker.native
+
+
+def test_fit_link_recovers_alpha_and_bandwidth():
+    from llm_fine_tune_distributed_amd.parallel.ddp import fit_link
+    for world, alpha_us, gbps in ((2, 25.0, 80.0), (8, 60.0, 140.0), (4, 5.0, 40.0)):
+        pts = [(b, alpha_us * 1e-6 + b / (world * gbps * 1e9)) for b in (4 << 20, 16 << 20, 32 << 20)]
+        a, l = fit_link(pts, world)
+        assert a == pytest.approx(alpha_us, rel=1e-6) and l == pytest.approx(gbps, rel=1e-6)
+    with pytest.raises(ValueError):
+        fit_link([(1 << 20, 1e-4)], 2)
+
+
+def test_bucket_plan_follows_the_measured_link():
+    """The injected probe result (alpha, L) moves the bucket cap: a slower per-call latency or a faster link asks
+    for larger buckets (latency share <= ~15 %), the modelled defaults are used only without a probe."""
+    from llm_fine_tune_distributed_amd.models import smollm3_3b
+    c = smollm3_3b()
+    m = torch.nn.Module()  # SmolLM3-3B parameter shapes on the meta device (no 6 GB allocation)
+    m.embed_tokens = torch.nn.Parameter(torch.empty(c.vocab_size, c.hidden_size, device="meta", dtype=torch.bfloat16))
+    m.layers = torch.nn.ParameterList([torch.nn.Parameter(torch.empty(2 * c.intermediate_size, c.hidden_size,
+                                                                      device="meta", dtype=torch.bfloat16))
+                                       for _ in range(c.num_hidden_layers)])
+    caps = {}
+    for name, link in (("model", None), ("slow_call", (120.0, 100.0)), ("fast_call", (8.0, 100.0)),
+                       ("fast_link", (30.0, 300.0))):
+        eng = DDPEngine(m, world_size=4, rank=0, link=link)
+        assert eng.plan_source == ("model" if link is None else "probe")
+        caps[name] = eng.bucket_cap_mb
+        if link is not None:
+            assert caps[name] == plan_bucket_mb(4, alpha_us=link[0], link_gbps=link[1],
+                                                total_bytes=sum(p.numel() for p in m.parameters()) * 2)
+    assert caps["slow_call"] > caps["model"] > caps["fast_call"]
+    assert caps["fast_link"] > caps["model"]
+    assert DDPEngine(m, world_size=4, rank=0, bucket_cap_mb=20.0, link=(120.0, 100.0)).plan_source == "user"
+
+
+def _probe_rank(rank, world, port, out):
+    import os
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from llm_fine_tune_distributed_amd.parallel.ddp import fit_link, measure_link
+    pts = measure_link(world, torch.device("cpu"), sizes_mb=(0.25, 2.0), iters=2)
+    torch.save({"pts": pts, "fit": fit_link(pts, world)}, f"{out}/p{rank}.pt")
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_measure_link_is_identical_on_every_rank(world, tmp_path):
+    """The startup probe takes the max over ranks, so every rank fits the same alpha / L and builds the same plan."""
+    import socket
+    import torch.multiprocessing as mp
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    mp.spawn(_probe_rank, args=(world, port, str(tmp_path)), nprocs=world, join=True)
+    res = [torch.load(tmp_path / f"p{r}.pt") for r in range(world)]
+    assert len(res[0]["pts"]) == 2 and res[0]["pts"][1][0] > res[0]["pts"][0][0]
+    for r in res[1:]:
+        assert r["pts"] == res[0]["pts"] and r["fit"] == res[0]["fit"]
+    assert res[0]["fit"][0] >= 1.0 and 1.0 <= res[0]["fit"][1] <= 1000.0

@@ -188,9 +188,9 @@ def _env(**kv):
                 os.environ[k] = v
 
 
-def _attn_case(lens, nq, nkv, causal, variant, impl="2", cfg="", ds_mb=""):
-    # ds_mb: "" = default budget (materialised dS^T + dq4), "0" = dq3 path
-    with _env(SFTAMD_ATTN_TR=variant, SFTAMD_ATTN_IMPL=impl, SFTAMD_ATTN_CFG=cfg, SFTAMD_ATTN_DS_MB=ds_mb):
+def _attn_case(lens, nq, nkv, causal, ds_mb=""):
+    # ds_mb: "" = default budget (materialised dS^T + dq4), "0" = the dq3 recompute path
+    with _env(SFTAMD_ATTN_DS_MB=ds_mb):
         _attn_case_body(lens, nq, nkv, causal)
 
 
@@ -213,133 +213,34 @@ def _attn_case_body(lens, nq, nkv, causal):
         assert e < 3e-2, (name, e)
 
 
-@pytest.mark.parametrize("impl", ["4", "3", "2", "1"])
-@pytest.mark.parametrize("variant", ["1", "0"])
-@pytest.mark.parametrize("causal", [True, False])
-def test_flash_attention_varlen_gqa(variant, causal, impl):
-    _attn_case([100, 255, 64, 1, 300], 8, 2, causal, variant, impl)
-
-
 @pytest.mark.parametrize("causal", [True, False])
 @pytest.mark.parametrize("ds_mb", ["", "0"])
-def test_flash_attention_bwd_materialised_ds_vs_recompute(causal, ds_mb):
-    """v4 backward (dkdv stores dS^T, dq4 = one product per tile) and the dq3 recompute path (budget 0) both
-    match the fp32 reference on ragged GQA batches (lengths off the 64 / 128 tile grid)."""
-    _attn_case([100, 255, 64, 1, 300, 129], 8, 2, causal, "1", "3", "", ds_mb)
-    _attn_case([512, 511, 7], 16, 4, causal, "1", "3", "", ds_mb)
+def test_flash_attention_varlen_gqa(causal, ds_mb):
+    """fwd3 (K / V by LDS-DMA) + the GQA-grouped dK/dV with either dQ path (materialised dS^T + dq4, or the dq3
+    recompute past the dS^T budget) vs the fp32 reference: ragged lengths off the 64 / 128 tile grid, even GQA
+    ratios (two head groups, LDS-DMA Q / dO), odd ones (one group), MHA (rep 1) and the SmolLM3 shape."""
+    _attn_case([100, 255, 64, 1, 300, 129], 8, 2, causal, ds_mb)
+    _attn_case([512, 511, 7], 16, 4, causal, ds_mb)
+    _attn_case([200, 65], 12, 3, causal, ds_mb)
+    _attn_case([130, 64], 12, 2, causal, ds_mb)
+    _attn_case([621, 700, 553, 754], 16, 4, causal, ds_mb)
+    _attn_case([300, 17, 129], 4, 4, causal, ds_mb)
 
 
-@pytest.mark.parametrize("causal", [True, False])
-@pytest.mark.parametrize("ds_mb", ["", "0"])
-@pytest.mark.parametrize("gqa", ["1", "split0", "0"])
-def test_flash_attention_bwd_gqa_grouped(causal, ds_mb, gqa, monkeypatch):
-    """dK/dV with the GQA-grouped kernel (one workgroup walks every query head of its kv head; default: two
-    4-wave head groups combined through LDS, "split0" = one group) and the per-head kernel + fp32 partial
-    reduction (SFTAMD_ATTN_GQA=0), on both dq paths, vs the fp32 reference (rep 4 and odd rep 3)."""
-    monkeypatch.setenv("SFTAMD_ATTN_GQA", "0" if gqa == "0" else "1")
-    monkeypatch.setenv("SFTAMD_ATTN_GQA_SPLIT", "0" if gqa == "split0" else "1")
-    _attn_case([100, 255, 64, 1, 300, 129], 8, 2, causal, "1", "3", "", ds_mb)
-    _attn_case([512, 511, 7], 16, 4, causal, "1", "3", "", ds_mb)
-    _attn_case([200, 65], 12, 3, causal, "1", "3", "", ds_mb)
-    _attn_case([130, 64], 12, 2, causal, "1", "3", "", ds_mb)
+def test_flash_attention_mha_and_long():
+    _attn_case([1000, 37], 4, 4, True)
+    _attn_case([2048, 5], 16, 4, True)
 
 
-@pytest.mark.parametrize("causal", [True, False])
-def test_flash_attention_fwd_lds_dma(causal, monkeypatch):
-    """fwd3 with K / V staged by LDS-DMA into two stages (the default, SFTAMD_ATTN_FWD_DMA=1; source-swizzled pieces,
-    rows past the sequence end clamped) == the fp32 reference on ragged GQA batches, and == the register-staged fwd3
-    (SFTAMD_ATTN_FWD_DMA=0) bitwise (same MFMA order, same softmax)."""
-    monkeypatch.setenv("SFTAMD_ATTN_FWD_DMA", "1")
-    _attn_case([100, 255, 64, 1, 300, 129], 8, 2, causal, "1", "3", "", "")
-    _attn_case([621, 700, 553, 754], 16, 4, causal, "1", "3", "", "")
-    torch.manual_seed(1)
-    lens = [700, 63, 130]
-    cu = torch.tensor([0] + list(torch.tensor(lens).cumsum(0)), dtype=torch.int32, device=DEV)
-    qkv = torch.randn(int(cu[-1]), 24 * 128, device=DEV, dtype=torch.bfloat16)
-    o1, l1 = _ext.ops().flash_fwd(qkv, cu, max(lens), 16, 4, 128, 0.088, causal)
-    monkeypatch.setenv("SFTAMD_ATTN_FWD_DMA", "0")
-    o0, l0 = _ext.ops().flash_fwd(qkv, cu, max(lens), 16, 4, 128, 0.088, causal)
-    assert torch.equal(o1, o0) and torch.equal(l1, l0)
+def test_flash_attention_smollm3_shape():
+    _attn_case([512] * 4, 16, 4, True)
 
 
-@pytest.mark.parametrize("causal", [True, False])
-def test_flash_attention_fwd_three_stage_ring(causal, monkeypatch):
-    """fwd3 with a three-stage LDS-DMA ring (two K / V tiles in flight, counted vmcnt + fence-free barrier;
-    SFTAMD_ATTN_FWD_DMA3=1) == the fp32 reference and == the two-stage default bitwise; one-tile sequences too."""
-    monkeypatch.setenv("SFTAMD_ATTN_FWD_DMA3", "1")
-    _attn_case([100, 255, 64, 1, 300, 129], 8, 2, causal, "1", "3", "", "")
-    _attn_case([621, 700, 553, 754], 16, 4, causal, "1", "3", "", "")
-    torch.manual_seed(4)
-    lens = [700, 63, 130, 17, 64, 65]
-    cu = torch.tensor([0] + list(torch.tensor(lens).cumsum(0)), dtype=torch.int32, device=DEV)
-    qkv = torch.randn(int(cu[-1]), 24 * 128, device=DEV, dtype=torch.bfloat16)
-    o1, l1 = _ext.ops().flash_fwd(qkv, cu, max(lens), 16, 4, 128, 0.088, causal)
-    monkeypatch.setenv("SFTAMD_ATTN_FWD_DMA3", "0")
-    o0, l0 = _ext.ops().flash_fwd(qkv, cu, max(lens), 16, 4, 128, 0.088, causal)
-    assert torch.equal(o1, o0) and torch.equal(l1, l0)
-
-
-@pytest.mark.parametrize("causal", [True, False])
-def test_flash_attention_fwd7_two_row_groups(causal, monkeypatch):
-    """fwd7 (4 waves x 2 row groups, LDS-DMA K / V; SFTAMD_ATTN_FWD7=1) == the fp32 reference on ragged GQA batches,
-    and == the default forward bitwise (same per-row MFMA order, softmax and rescale decisions)."""
-    monkeypatch.setenv("SFTAMD_ATTN_FWD7", "1")
-    _attn_case([100, 255, 64, 1, 300, 129], 8, 2, causal, "1", "3", "", "")
-    _attn_case([621, 700, 553, 754], 16, 4, causal, "1", "3", "", "")
-    torch.manual_seed(3)
-    lens = [700, 63, 130, 17]
-    cu = torch.tensor([0] + list(torch.tensor(lens).cumsum(0)), dtype=torch.int32, device=DEV)
-    qkv = torch.randn(int(cu[-1]), 24 * 128, device=DEV, dtype=torch.bfloat16)
-    o1, l1 = _ext.ops().flash_fwd(qkv, cu, max(lens), 16, 4, 128, 0.088, causal)
-    monkeypatch.setenv("SFTAMD_ATTN_FWD7", "0")
-    o0, l0 = _ext.ops().flash_fwd(qkv, cu, max(lens), 16, 4, 128, 0.088, causal)
-    assert torch.equal(o1, o0) and torch.equal(l1, l0)
-
-
-@pytest.mark.parametrize("causal", [True, False])
-@pytest.mark.parametrize("dma", ["1", "0"])
-def test_flash_attention_bwd_lds_dma(causal, dma, monkeypatch):
-    """GQA dK/dV with Q / dO staged by LDS-DMA into two stages per head group (the default; SFTAMD_ATTN_BWD_DMA=0:
-    register staging) == the fp32 reference (rep 4 / 2 / 3, ragged lengths, both dq paths), and the two stagings
-    agree bitwise (same MFMA order)."""
-    monkeypatch.setenv("SFTAMD_ATTN_BWD_DMA", dma)
-    monkeypatch.setenv("SFTAMD_ATTN_DQ_DMA", dma)  # the opt-in LDS-DMA dq4 (zero-filled tail rows) rides along
-    _attn_case([100, 255, 64, 1, 300, 129], 8, 2, causal, "1", "3", "", "")
-    _attn_case([621, 700, 553, 754], 16, 4, causal, "1", "3", "", "")
-    _attn_case([200, 65], 12, 3, causal, "1", "3", "", "0")
-    torch.manual_seed(2)
-    lens = [700, 63, 130]
-    cu = torch.tensor([0] + list(torch.tensor(lens).cumsum(0)), dtype=torch.int32, device=DEV)
-    qkv = torch.randn(int(cu[-1]), 24 * 128, device=DEV, dtype=torch.bfloat16)
-    out, lse = _ext.ops().flash_fwd(qkv, cu, max(lens), 16, 4, 128, 0.088, causal)
-    dout = torch.randn_like(out)
-    g1 = _ext.ops().flash_bwd(dout, qkv, out, lse, cu, max(lens), 16, 4, 128, 0.088, causal)
-    monkeypatch.setenv("SFTAMD_ATTN_BWD_DMA", "0" if dma == "1" else "1")
-    monkeypatch.setenv("SFTAMD_ATTN_DQ_DMA", "0" if dma == "1" else "1")
-    g0 = _ext.ops().flash_bwd(dout, qkv, out, lse, cu, max(lens), 16, 4, 128, 0.088, causal)
-    assert torch.equal(g1, g0)
-
-
-@pytest.mark.parametrize("causal", [True, False])
-@pytest.mark.parametrize("leg", ["1", "0"])
-def test_flash_attention_legacy_schedule(causal, leg, monkeypatch):
-    """The round-2 instruction schedule (SFTAMD_ATTN_LEGWAIT=1: compiler vmcnt(0) before the first MFMA, per-tile
-    row-sum shuffles) and the default one (vm_drain before the loop, lane-partial row sums, permlane swaps, dq4's
-    computed column offset) both match the fp32 reference; the default forward == the legacy one to fp32 order."""
-    monkeypatch.setenv("SFTAMD_ATTN_LEGWAIT", leg)
-    _attn_case([100, 255, 64, 1, 300, 129], 8, 2, causal, "1", "3", "", "")
-    _attn_case([621, 700, 553, 754], 16, 4, causal, "1", "3", "", "")
-
-
-@pytest.mark.parametrize("path", ["default", "gqa0", "ds0", "mha", "dq6"])
+@pytest.mark.parametrize("path", ["default", "ds0", "mha"])
 def test_flash_bwd_rope(path, monkeypatch):
     """flash_bwd_rope == inverse-RoPE(flash_bwd): fused into the dq / dK epilogues on the default path (one bf16
-    rounding instead of two: close), the rope kernel after the backward on the others (bitwise)."""
-    monkeypatch.setenv("SFTAMD_ATTN_IMPL", "3")
-    monkeypatch.setenv("SFTAMD_ATTN_CFG", "")
-    monkeypatch.setenv("SFTAMD_ATTN_GQA", "0" if path == "gqa0" else "1")
+    rounding instead of two: close), the rope kernel after the backward on the dq3 path (bitwise)."""
     monkeypatch.setenv("SFTAMD_ATTN_DS_MB", "0" if path == "ds0" else "")
-    monkeypatch.setenv("SFTAMD_ATTN_DQ6", "1" if path == "dq6" else "0")
     torch.manual_seed(5)
     D = 128
     nq, nkv = (4, 4) if path == "mha" else (8, 2)
@@ -357,28 +258,15 @@ def test_flash_bwd_rope(path, monkeypatch):
     got = _ext.ops().flash_bwd_rope(dout, qkv, out, lse, cu, max(lens), nq, nkv, D, scale, True, cos, sin)
     want = _ext.ops().flash_bwd(dout, qkv, out, lse, cu, max(lens), nq, nkv, D, scale, True)
     _ext.ops().rope_(want, cos, sin, nq, nkv, D, True)
-    if path in ("default", "dq6"):
+    if path in ("default", "mha"):
         assert rel_err(got, want) < 1e-2
         assert torch.equal(got[:, (nq + nkv) * D:], want[:, (nq + nkv) * D:])  # dV untouched by the rotation
     else:
         assert torch.equal(got, want)
 
 
-def test_flash_attention_mha_and_long():
-    _attn_case([1000, 37], 4, 4, True, "1")
-
-
-@pytest.mark.parametrize("impl,cfg", [("2", "8,1"), ("2", "4,2"), ("2", "4,1"), ("3", "4,1"), ("3", "8,1"), ("4", "")])
-def test_flash_attention_launch_configs(impl, cfg):
-    _attn_case([100, 255, 64, 1, 300], 8, 2, True, "1", impl, cfg)
-    _attn_case([100, 255, 64, 1, 300], 8, 2, False, "1", impl, cfg)
-
-
-@pytest.mark.parametrize("impl", ["3", "4"])
-def test_flash_attention_deferred_rescale_branch(impl, monkeypatch):
+def test_flash_attention_deferred_rescale_branch():
     """Force the online-softmax max to jump past THR mid-sequence (CDNA guide rule 26)."""
-    monkeypatch.setenv("SFTAMD_ATTN_IMPL", impl)
-    monkeypatch.setenv("SFTAMD_ATTN_CFG", "")
     torch.manual_seed(1)
     D, nq, nkv = 128, 4, 2
     T = 384
@@ -391,79 +279,6 @@ def test_flash_attention_deferred_rescale_branch(impl, monkeypatch):
     out, lse = _ext.ops().flash_fwd(qkv, cu, T, nq, nkv, D, scale, True)
     o_ref = ref.attention(qkv.float(), nq, nkv, D, cu, scale, True)
     assert rel_err(out, o_ref) < 2e-2
-
-
-@pytest.mark.parametrize("causal", [True, False])
-def test_flash_attention_fwd6_gqa_stacked(causal, monkeypatch):
-    """v6 forward (one workgroup per kv head x 64 positions, the 2 / 4 query heads of the kv head stacked in each
-    wave, K/V by global_load_lds) vs the fp32 reference: ragged lengths off the tile grid, rep 4 and rep 2, the
-    SmolLM3 shape; the backward (v5 + dq4) consumes its lse."""
-    monkeypatch.setenv("SFTAMD_ATTN_FWD6", "1")
-    _attn_case([100, 255, 64, 1, 300, 129], 8, 2, causal, "1", "3")
-    _attn_case([512, 511, 7], 16, 4, causal, "1", "3")
-    _attn_case([200, 65, 1000], 8, 4, causal, "1", "3")
-    _attn_case([512] * 4, 16, 4, causal, "1", "3")
-
-
-@pytest.mark.parametrize("causal", [True, False])
-@pytest.mark.parametrize("fwd6", ["0", "1"])
-def test_flash_attention_bwd6_recompute_dq(causal, fwd6, monkeypatch):
-    """v6 backward: GQA-grouped dK/dV without dS^T stores + the recomputing GQA-stacked dQ kernel (rep 4 / 2), fed by
-    either forward's lse, vs the fp32 reference."""
-    monkeypatch.setenv("SFTAMD_ATTN_DQ6", "1")
-    monkeypatch.setenv("SFTAMD_ATTN_FWD6", fwd6)
-    _attn_case([100, 255, 64, 1, 300, 129], 8, 2, causal, "1", "3")
-    _attn_case([512, 511, 7], 16, 4, causal, "1", "3")
-    _attn_case([200, 65, 1000], 8, 4, causal, "1", "3")
-
-
-@pytest.mark.parametrize("spike", [20.0, 45.0])
-def test_flash_attention_fwd6_slow_path(spike, monkeypatch):
-    """v6's fast loop never rescales; a score jump past THR_FAST (spike 45: ~60 in log2 units at key tile 3) sends
-    the rest of that row block to the rescaling loop. Both must match the reference."""
-    monkeypatch.setenv("SFTAMD_ATTN_FWD6", "1")
-    monkeypatch.setenv("SFTAMD_ATTN_IMPL", "3")
-    torch.manual_seed(1)
-    D, nq, nkv = 128, 8, 2
-    T = 384
-    cu = torch.tensor([0, T], dtype=torch.int32, device=DEV)
-    qkv = (0.3 * torch.randn(T, (nq + 2 * nkv) * D, device=DEV)).to(torch.bfloat16)
-    k = qkv[:, nq * D:(nq + nkv) * D].view(T, nkv, D)
-    q = qkv[:, :nq * D].view(T, nq, D)
-    k[200] = (spike * q[300, 0].float()).to(k.dtype)
-    scale = 1 / math.sqrt(D)
-    out, lse = _ext.ops().flash_fwd(qkv, cu, T, nq, nkv, D, scale, True)
-    o_ref = ref.attention(qkv.float(), nq, nkv, D, cu, scale, True)
-    assert rel_err(out, o_ref) < 2e-2
-    assert torch.isfinite(lse).all()
-
-
-def test_flash_attention_concurrent_bwd_bitwise(monkeypatch):
-    """dq on a side stream concurrently with dK/dV (default) == the serial launch order, bit for bit, and the
-    result is complete when the op returns on the caller's stream (no extra sync)."""
-    monkeypatch.setenv("SFTAMD_ATTN_IMPL", "3")
-    monkeypatch.setenv("SFTAMD_ATTN_CFG", "")
-    monkeypatch.setenv("SFTAMD_ATTN_DS_MB", "0")  # the dq3 (recompute) path, which has the concurrent option
-    torch.manual_seed(3)
-    D, nq, nkv = 128, 16, 4
-    lens = [512, 300, 17, 512]
-    cu = torch.tensor([0] + list(torch.tensor(lens).cumsum(0)), dtype=torch.int32, device=DEV)
-    M = int(cu[-1])
-    qkv = torch.randn(M, (nq + 2 * nkv) * D, device=DEV, dtype=torch.bfloat16)
-    scale = 1 / math.sqrt(D)
-    out, lse = _ext.ops().flash_fwd(qkv, cu, max(lens), nq, nkv, D, scale, True)
-    dout = torch.randn_like(out)
-    res = {}
-    for conc in ("0", "1"):
-        monkeypatch.setenv("SFTAMD_ATTN_CONC", conc)
-        d = _ext.ops().flash_bwd(dout, qkv, out, lse, cu, max(lens), nq, nkv, D, scale, True)
-        res[conc] = (d * 1).clone()  # consumed on the current stream right away
-    assert torch.equal(res["0"], res["1"])
-
-
-@pytest.mark.parametrize("impl", ["3", "2", "1"])
-def test_flash_attention_smollm3_shape(impl):
-    _attn_case([512] * 4, 16, 4, True, "1", impl)
 
 
 def test_adamw_and_norm():

@@ -146,6 +146,19 @@ def test_bf16_optimizer_state_trains(tmp_path, tk):
     assert d < 1e-2
 
 
+def test_auto_state_dtype_follows_master_weights(tmp_path, tk):
+    """"auto" moments: bf16 for the bf16 model (torch parity), fp32 once an fp32 master copy is kept (that path
+    writes back with round-to-nearest, where a bf16 exp_avg_sq would stall)."""
+    for master, want in ((False, torch.bfloat16), (True, torch.float32)):
+        a = SFTConfig(output_dir=str(tmp_path / str(master)), per_device_train_batch_size=2, max_steps=1,
+                      jsonl_log=False, master_weights=master)
+        assert a.optim_state_dtype == "auto"
+        t = SFTTrainer(model=build_model(tiny(vocab_size=1024), dtype=torch.bfloat16, seed=0), args=a,
+                       train_dataset=generate_qa(4), processing_class=tk)
+        assert t.optimizer.exp_avg.dtype == want and t.optimizer.exp_avg_sq.dtype == want
+        assert (t.optimizer.master is not None) == master
+
+
 def test_reference_freeze_policy_counts(tmp_path, tk):
     a = SFTConfig(output_dir=str(tmp_path), freeze_policy="last_n_layers", max_steps=1, jsonl_log=False,
                   per_device_train_batch_size=2)
