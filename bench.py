@@ -64,8 +64,6 @@ def parse(argv=None):
                     help="run the GA micro-batches of a step as one pass up to this many tokens (SFTConfig default "
                          "32768); 0 = one fwd/bwd pass per micro-batch")
     ap.add_argument("--seq", type=int, default=512)
-    ap.add_argument("--lm-head-chunk", type=int, default=0,
-                    help="LM head + CE in row chunks of this many tokens (SFTConfig.lm_head_chunk_rows; 0 = one pass)")
     ap.add_argument("--bucket-mb", type=float, default=float(os.environ.get("SFTAMD_BUCKET_MB", "0")),
                     help="gradient bucket cap in MB; 0 (default) = the xGMI plan of parallel.ddp.plan_bucket_mb")
     ap.add_argument("--packing", action="store_true")
@@ -215,7 +213,6 @@ def run(a):
                      logging_steps=0, optimizer_overlap=not a.no_overlap, freeze_policy=a.freeze_policy,
                      master_weights=a.master_weights, optim_state_dtype=a.optim_state,
                      shard_optimizer_state=bool(a.zero), gemm_tuning=False,
-                     lm_head_chunk_rows=a.lm_head_chunk,
                      **({} if a.ga_merge_max_tokens is None else {"ga_merge_max_tokens": a.ga_merge_max_tokens}))
     trainer = SFTTrainer(model=model, args=args, train_dataset=ds)
     loader = trainer.get_train_dataloader()
@@ -369,7 +366,6 @@ def run_recipe(a):
                      bf16=True, gradient_checkpointing=False, max_length=1024, dataloader_drop_last=True,
                      jsonl_log=False, freeze_policy=a.freeze_policy, shard_optimizer_state=bool(a.zero),
                      dataset_cache=False, gemm_tuning=False, optimizer_overlap=not a.no_overlap,
-                     lm_head_chunk_rows=a.lm_head_chunk,
                      padding_free={"auto": None, "on": True, "off": False}[a.padding_free],
                      **({} if a.ga_merge_max_tokens is None else {"ga_merge_max_tokens": a.ga_merge_max_tokens}))
     trainer = SFTTrainer(model=model, args=args, train_dataset=train_rows, eval_dataset=val_rows,

@@ -1262,6 +1262,18 @@ __device__ __forceinline__ unsigned pack2(float a, float b) { return (unsigned)f
 // one lane): rotate in registers (bf16 projection values, as the unfused path sees them), then pair lo / hi with
 // permlane16_swap — 32 stores. SWIGLU (fragments 2q / 2q + 1 = gate / up of the same act columns): gate / up paired
 // with each other, act (q) with act (q + 1) — 48 stores.
+// 16-byte epilogue store; NT: non-temporal (streaming; what hipBLASLt's epilogue issues: `buffer_store_dwordx4 ...
+// nt`). Measured on the persistent kernel, gate_up M = 8192: 0.579 vs 0.648 ms (profiles/r4_gemm_fwd.md).
+template <bool NT>
+__device__ __forceinline__ void st16(void* dst, const uint4& val) {
+  if constexpr (NT) {
+    typedef unsigned u32x4v __attribute__((ext_vector_type(4)));
+    __builtin_nontemporal_store(u32x4v{val.x, val.y, val.z, val.w}, (u32x4v*)dst);
+  } else {
+    *(uint4*)dst = val;
+  }
+}
+
 template <int EPI, int SV = 0>
 __device__ __forceinline__ void tn5_store(f32x4 (&acc)[8][8], const EpiArgs& ea, int row0, int m_col0, int wn,
                                           int lane) {
@@ -1282,13 +1294,7 @@ __device__ __forceinline__ void tn5_store(f32x4 (&acc)[8][8], const EpiArgs& ea,
         auto r1 = __builtin_amdgcn_permlane16_swap(v1, w1, false, false);
         uint4* dst = (SV & 2) ? (uint4*)(base2 + (long)(4 * i + p) * ea.ldc)
                               : (uint4*)(base + (long)(16 * i) * ea.ldc + 32 * p);
-        const uint4 val = make_uint4(r0[0], r1[0], r0[1], r1[1]);
-        if constexpr (SV & 1) {  // nt: streaming store, as hipBLASLt's epilogue
-          typedef unsigned u32x4v __attribute__((ext_vector_type(4)));
-          __builtin_nontemporal_store(u32x4v{val.x, val.y, val.z, val.w}, (u32x4v*)dst);
-        } else {
-          *dst = val;
-        }
+        st16<(SV & 1) != 0>(dst, make_uint4(r0[0], r1[0], r0[1], r1[1]));
       }
     }
   } else if constexpr (EPI == EPI_ROPE) {
@@ -1319,7 +1325,7 @@ __device__ __forceinline__ void tn5_store(f32x4 (&acc)[8][8], const EpiArgs& ea,
         }
         auto r0 = __builtin_amdgcn_permlane16_swap(pack2(lo[0], lo[1]), pack2(hi[0], hi[1]), false, false);
         auto r1 = __builtin_amdgcn_permlane16_swap(pack2(lo[2], lo[3]), pack2(hi[2], hi[3]), false, false);
-        *(uint4*)(base + (long)(16 * i) * ea.ldc + 16 * q) = make_uint4(r0[0], r1[0], r0[1], r1[1]);
+        st16<(SV & 1) != 0>(base + (long)(16 * i) * ea.ldc + 16 * q, make_uint4(r0[0], r1[0], r0[1], r1[1]));
       }
     }
   } else {  // SWIGLU: m_col0 = first act column of the wave
@@ -1342,13 +1348,13 @@ __device__ __forceinline__ void tn5_store(f32x4 (&acc)[8][8], const EpiArgs& ea,
           }
           auto r0 = __builtin_amdgcn_permlane16_swap(pack2(ga[0], ga[1]), pack2(up[0], up[1]), false, false);
           auto r1 = __builtin_amdgcn_permlane16_swap(pack2(ga[2], ga[3]), pack2(up[2], up[3]), false, false);
-          *(uint4*)(gu + (long)(16 * i) * ea.ldc + 16 * q) = make_uint4(r0[0], r1[0], r0[1], r1[1]);
+          st16<(SV & 1) != 0>(gu + (long)(16 * i) * ea.ldc + 16 * q, make_uint4(r0[0], r1[0], r0[1], r1[1]));
           a01[h] = pack2(o[0], o[1]);
           a23[h] = pack2(o[2], o[3]);
         }
         auto r0 = __builtin_amdgcn_permlane16_swap(a01[0], a01[1], false, false);
         auto r1 = __builtin_amdgcn_permlane16_swap(a23[0], a23[1], false, false);
-        *(uint4*)(ac + (long)(16 * i) * ea.I + 32 * qq) = make_uint4(r0[0], r1[0], r0[1], r1[1]);
+        st16<(SV & 1) != 0>(ac + (long)(16 * i) * ea.I + 32 * qq, make_uint4(r0[0], r1[0], r0[1], r1[1]));
       }
     }
   }
@@ -1357,24 +1363,59 @@ __device__ __forceinline__ void tn5_store(f32x4 (&acc)[8][8], const EpiArgs& ea,
 // VAR: bit 0 = timing ablation, no epilogue stores (wrong results); bits 1 / 2 = staggered K start over 4 / 16
 // offsets (tn5_kstart). Launched with one workgroup per CU (persistent) or one per tile (the same code: a workgroup
 // whose next tile is past its XCD's range ends after one tile).
+// Dynamic tile queue (VAR & 128): the XCD ranges of the static order become 8 work counters (one per XCD) that the
+// workgroups draw tiles from (their own XCD's first, then the others': whatever is left), so workgroups that start
+// late — CUs held by a concurrent kernel such as the overlapped AdamW — take fewer tiles instead of stretching the
+// launch by their whole static share. One returning atomic per tile, issued by wave 0 lane 0 where its wave has no
+// vector-memory operation outstanding (its return then costs no wait on the DMA / stores), published through the
+// staging array's spare bytes behind the next barrier. The counters live in a per-launch slot of a device ring; the
+// last workgroup to finish resets its slot (the next launch on any stream that gets the slot is ordered after this
+// one completes: the ring holds 64 slots, handed out round-robin by the host).
+__device__ __forceinline__ int tn5_range_start(int x, int tiles) {
+  const int q8 = tiles >> 3, r8 = tiles & 7;
+  return x * q8 + min(x, r8);
+}
+__device__ __forceinline__ int tn5_grab(int* wq, int own, int tiles) {
+#pragma unroll 1
+  for (int i = 0; i < 8; ++i) {
+    const int x = (own + i) & 7;
+    const int s0 = tn5_range_start(x, tiles), len = tn5_range_start(x + 1, tiles) - s0;
+    const int t = __hip_atomic_fetch_add(wq + x, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (t < len) return s0 + t;
+  }
+  return -1;
+}
+
 template <int EPI, bool NK2, int VAR = 0>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1)))
 tn5_kernel(const u16* __restrict__ A, const u16* __restrict__ B, int K, long lda, long ldb, int nbm, int nbn,
-           int group, EpiArgs ea) {
+           int group, EpiArgs ea, int* __restrict__ wq) {
   using G = Cfg2<256, 256, 2, 2, 2>;
+  constexpr bool DYN = (VAR & 128) && !NK2;  // a one-pair tile has no barrier between the grab and its use
   // The next tile's K0 AND K1 go out in the last sub-step (both stages are free then), the epilogue's NST stores after
   // them: the next tile waits vmcnt(NST + 16) (PLAIN / ROPE) or vmcnt(NST) (SWIGLU, 48 stores: the counter holds 63)
   // for K0, and its first boundary only vmcnt(NST) for K1 — the stores drain under its first K-tile.
   constexpr int NST = EPI == EPI_SWIGLU ? 48 : 32;
-  __shared__ __attribute__((aligned(16))) char smem[2 * G::STAGE];
+  __shared__ __attribute__((aligned(16))) char smem[2 * G::STAGE + 16];  // + the dynamic queue's published tile
+  volatile int* slot = (volatile int*)(smem + 2 * G::STAGE);
   const int tiles = nbm * nbn, nwg = gridDim.x, orig = blockIdx.x;
   // this XCD's contiguous share of the tile order, walked round-robin by its workgroups (blocks b, b + 8, ...)
   const int xcd = orig & 7, l = orig >> 3, nx = (nwg - xcd + 7) >> 3;
-  const int q8 = tiles >> 3, r8 = tiles & 7;
-  const int t_end = xcd * q8 + min(xcd, r8) + q8 + (xcd < r8 ? 1 : 0);
-  int tile = xcd * q8 + min(xcd, r8) + l;
-  if (tile >= t_end) return;
+  const int t_end = tn5_range_start(xcd + 1, tiles);
+  int tile = tn5_range_start(xcd, tiles) + l;
   const int tid = threadIdx.x, lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  if constexpr (DYN) {
+    if (tid == 0) *slot = tn5_grab(wq, xcd, tiles);
+    __syncthreads();
+    tile = __builtin_amdgcn_readfirstlane(*slot);
+    if (tile < 0) {
+      if (tid == 0 && __hip_atomic_fetch_add(wq + 8, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == nwg - 1)
+        for (int i = 0; i < 9; ++i) __hip_atomic_store(wq + i, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      return;
+    }
+  } else {
+    if (tile >= t_end) return;
+  }
   const int wm = w >> 1, wn = w & 1;
   const int nk = K / BK2;
   const int g = lane >> 4, ii = lane & 15;
@@ -1406,6 +1447,7 @@ tn5_kernel(const u16* __restrict__ A, const u16* __restrict__ B, int K, long lda
   f32x4 acc[8][8];
   bf16x8 a0[8], b0[8], a1[8], b1[8];
   bool first = true;
+  int grabbed = -1;
   for (;;) {
     __builtin_amdgcn_s_barrier();
 #pragma unroll
@@ -1413,10 +1455,10 @@ tn5_kernel(const u16* __restrict__ A, const u16* __restrict__ B, int K, long lda
       a0[i] = lds_row(X, offA0 + 2048 * i);
       b0[i] = lds_row(X, offB0 + 2048 * i);
     }
-    const int next = tile + nx;
-    const bool has_next = next < t_end;
+    int next = tile + nx;
+    bool has_next = next < t_end;
     int m1 = m0, n1 = n0;
-    if (has_next) tn5_coords(next, nbm, nbn, group, m1, n1);
+    if (!DYN && has_next) tn5_coords(next, nbm, nbn, group, m1, n1);
     // K-tile pairs (t on X, t + 1 on Y); boundary = vmcnt(0) lgkmcnt(0) + the barrier after the next sub-step's
     // first MFMA group. LAST: the final sub-step DMAs the next tile's K0 into X (the current tile's K0 again when
     // there is none: branch-free, harmless) and reads nothing.
@@ -1436,12 +1478,23 @@ tn5_kernel(const u16* __restrict__ A, const u16* __restrict__ B, int K, long lda
       __builtin_amdgcn_s_waitcnt(waitcnt_imm(63, 0));
       tn5_sub<EPI, false, true, 0, false>(acc, a0, b0, a1, b1, Y, offA1, offB1, st, Y, w);
       __builtin_amdgcn_s_waitcnt(waitcnt_imm(0, 0));
+      if constexpr (DYN && IN) {  // no VMEM outstanding here: draw the next tile (its return waits for nothing else)
+        if (tid == 0) grabbed = tn5_grab(wq, xcd, tiles);
+      }
+      if constexpr (DYN && LA) {  // published behind the barrier of an earlier sub-step of this tile
+        next = __builtin_amdgcn_readfirstlane(*slot);
+        has_next = next >= 0;
+        if (has_next) tn5_coords(next, nbm, nbn, group, m1, n1);
+      }
       if constexpr (LA) {
         tn5_stager(st, A, B, lda, ldb, m1, n1, w, lane, ea.I, tn5_kstart<VAR>(m1, n1, nk / 2));
         tn5_sub<EPI, false, false, 32, true>(acc, a1, b1, a0, b0, X, offA0, offB0, st, X, w, Y);
       } else {
         tn5_sub<EPI, false, true, 16, true>(acc, a1, b1, a0, b0, X, offA0, offB0, st, Y, w);
         st.adv(BK2);
+        if constexpr (DYN && IN) {
+          if (tid == 0) *slot = grabbed;  // read after the next pair's first barrier
+        }
       }
     };
     if constexpr (NK2) {
@@ -1466,7 +1519,13 @@ tn5_kernel(const u16* __restrict__ A, const u16* __restrict__ B, int K, long lda
                                       wn, lane);
     }
     __builtin_amdgcn_sched_barrier(0);
-    if (!has_next) break;
+    if (!has_next) {
+      if constexpr (DYN) {  // every workgroup has drawn its last tile once the done counter reaches nwg: reset the slot
+        if (tid == 0 && __hip_atomic_fetch_add(wq + 8, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == nwg - 1)
+          for (int i = 0; i < 9; ++i) __hip_atomic_store(wq + i, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+      break;
+    }
     st.adv(2 * BK2);
     if constexpr (EPI == EPI_SWIGLU)
       __builtin_amdgcn_s_waitcnt(waitcnt_imm(NST, 15));  // K0 and K1 landed (the 48 stores may fly)
@@ -1480,6 +1539,21 @@ tn5_kernel(const u16* __restrict__ A, const u16* __restrict__ B, int K, long lda
   __builtin_amdgcn_s_waitcnt(waitcnt_imm(0, 15));
 }
 
+constexpr int TN5_DEFAULT = 16 | 2;  // nt epilogue stores + staggered K start (4 offsets)
+
+// per-device ring of 64 work-queue slots (8 XCD counters + a done counter each, 64 B apart), zeroed once; a slot is
+// reset by the last workgroup of the launch that used it
+static int* tn5_queue_slot() {
+  constexpr int NSLOT = 64, SLOT_INTS = 16;
+  static at::Tensor ring[16];
+  static int seq[16];
+  const int dev = c10::hip::current_device();
+  if (!ring[dev].defined())
+    ring[dev] = at::zeros({NSLOT * SLOT_INTS}, at::TensorOptions().dtype(at::kInt).device(at::kCUDA, dev));
+  const int s = seq[dev]++ % NSLOT;
+  return ring[dev].data_ptr<int>() + s * SLOT_INTS;
+}
+
 template <int EPI, int VAR = 0>
 void launch5(const at::Tensor& a, const at::Tensor& w, int N, const EpiArgs& ea, bool persistent = true) {
   const int M = a.size(0), K = a.size(1);
@@ -1489,12 +1563,13 @@ void launch5(const at::Tensor& a, const at::Tensor& w, int N, const EpiArgs& ea,
   // one workgroup per tile: round the grid up to whole XCD rows so every XCD's range is covered one tile per block
   const int grid = persistent ? std::min(tiles, num_cus()) : (tiles + 7) / 8 * 8;
   const int grp = std::min(group_m(), nbm);
+  int* wq = ((VAR & 128) && K != 128) ? tn5_queue_slot() : nullptr;
   if (K == 128)
     tn5_kernel<EPI, true, VAR><<<grid, 256, 0, cur_stream()>>>((const u16*)a.data_ptr(), (const u16*)w.data_ptr(), K,
-                                                               a.stride(0), w.stride(0), nbm, nbn, grp, ea);
+                                                               a.stride(0), w.stride(0), nbm, nbn, grp, ea, wq);
   else
     tn5_kernel<EPI, false, VAR><<<grid, 256, 0, cur_stream()>>>((const u16*)a.data_ptr(), (const u16*)w.data_ptr(), K,
-                                                                a.stride(0), w.stride(0), nbm, nbn, grp, ea);
+                                                                a.stride(0), w.stride(0), nbm, nbn, grp, ea, wq);
   SFT_LAUNCH_CHECK();
 }
 
@@ -1576,8 +1651,12 @@ at::Tensor gemm_tn(const at::Tensor& a, const at::Tensor& w, int64_t cfg) {
     tn::launch4<tn::EPI_PLAIN, 0, 4>(a, w, N, ea);
   } else if (cfg == 60 || cfg == 61) {  // csrc/gemm_4w.hip: 4-slot ring of 32-deep steps (60) / 64-deep pairs (61)
     g4_tn(a, w, c, cfg == 60);
-  } else if (cfg == 50) {  // persistent 4-wave (register epilogue, next tile's loads under this tile's end)
-    tn::launch5<tn::EPI_PLAIN>(a, w, N, ea);
+  } else if (cfg == 50) {  // persistent 4-wave (register epilogue with nt stores, next tile's loads under this tile's
+    tn::launch5<tn::EPI_PLAIN, tn::TN5_DEFAULT>(a, w, N, ea);  // end, K start staggered over 4 offsets)
+  } else if (cfg == 164) {  // the round-3 persistent kernel (plain stores, no stagger) for A/B runs
+    tn::launch5<tn::EPI_PLAIN, 0>(a, w, N, ea);
+  } else if (cfg == 165) {  // persistent with the dynamic tile queue (plain stores)
+    tn::launch5<tn::EPI_PLAIN, 128>(a, w, N, ea);
   } else if ((cfg >= 51 && cfg <= 59) || (cfg >= 160 && cfg <= 163)) {  // tn5 variants (one tile per workgroup / staggered K start / no stores)
     switch (cfg) {
       case 51: tn::launch5<tn::EPI_PLAIN, 0>(a, w, N, ea, false); break;
@@ -1642,7 +1721,10 @@ std::tuple<at::Tensor, at::Tensor> gemm_tn_swiglu(const at::Tensor& x, const at:
     const char* e = std::getenv("SFTAMD_TN_TRC");
     return !(e && e[0] == '0');
   }();
-  if (cfg == 50) tn::launch5<tn::EPI_SWIGLU>(x, w_gu, N, ea);
+  if (cfg == 50) tn::launch5<tn::EPI_SWIGLU, tn::TN5_DEFAULT>(x, w_gu, N, ea);
+  else if (cfg == 164) tn::launch5<tn::EPI_SWIGLU, 0>(x, w_gu, N, ea);
+  else if (cfg == 51) tn::launch5<tn::EPI_SWIGLU, 0>(x, w_gu, N, ea, false);
+  else if (cfg == 165) tn::launch5<tn::EPI_SWIGLU, 128>(x, w_gu, N, ea);
   else if (cfg == 12) tn::launch4<tn::EPI_SWIGLU, 0, 4>(x, w_gu, N, ea);
   else if (x.size(1) % 64 == 0 && N % 256 == 0 && cfg == 11) tn::launch3<tn::EPI_SWIGLU, true, 2>(x, w_gu, N, ea);
   else if (x.size(1) % 64 == 0 && trc) tn::launch2<256, 256, 2, 4, 2, tn::EPI_SWIGLU, 3>(x, w_gu, N, ea);
@@ -1665,7 +1747,10 @@ at::Tensor gemm_tn_rope(const at::Tensor& x, const at::Tensor& w, const at::Tens
   auto c = at::empty({M, N}, x.options());
   tn::EpiArgs ea{(u16*)c.data_ptr(), nullptr, cosb.data_ptr<float>(), sinb.data_ptr<float>(), (long)N, 0,
                  (int)rope_cols};
-  if (cfg == 50) tn::launch5<tn::EPI_ROPE>(x, w, N, ea);
+  if (cfg == 50) tn::launch5<tn::EPI_ROPE, tn::TN5_DEFAULT>(x, w, N, ea);
+  else if (cfg == 164) tn::launch5<tn::EPI_ROPE, 0>(x, w, N, ea);
+  else if (cfg == 51) tn::launch5<tn::EPI_ROPE, 0>(x, w, N, ea, false);
+  else if (cfg == 165) tn::launch5<tn::EPI_ROPE, 128>(x, w, N, ea);
   else if (cfg == 12) tn::launch4<tn::EPI_ROPE, 0, 4>(x, w, N, ea);
   else if (cfg == 1) tn::launch<256, 128, 4, 2, 6, tn::EPI_ROPE>(x, w, N, ea);
   else if (cfg == 2 && x.size(1) % 64 == 0) tn::launch2<256, 256, 2, 4, 2, tn::EPI_ROPE>(x, w, N, ea);

@@ -28,8 +28,8 @@ __device__ __forceinline__ f32x4 mfma(const bf16x8& a, const bf16x8& b, const f3
 // 32-column steps in flight per iteration (the kernel is a stream over x: latency, not math, bound).
 template <int RF>  // R = 16 * RF adapter columns
 __global__ __launch_bounds__(512) void fwd_kernel(const u16* __restrict__ x, const u16* __restrict__ A,
-                                                  u16* __restrict__ X, u16* __restrict__ xd, long T, int K, float s,
-                                                  unsigned thresh, float dscale, unsigned seed) {
+                                                  u16* __restrict__ X, u16* __restrict__ xd, long T, int K, long ldX,
+                                                  float s, unsigned thresh, float dscale, unsigned seed) {
   constexpr int R = 16 * RF;
   constexpr int NW = 8, U = 4;
   __shared__ float red[NW][16][R + 1];
@@ -40,7 +40,6 @@ __global__ __launch_bounds__(512) void fwd_kernel(const u16* __restrict__ x, con
   const bool rowok = t < T;
   const int KW = K / NW;
   const int kb = w * KW;
-  const long ldX = K + R;
   f32x4 acc[RF];
 #pragma unroll
   for (int j = 0; j < RF; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -88,6 +87,11 @@ __global__ __launch_bounds__(512) void fwd_kernel(const u16* __restrict__ x, con
       for (int q = 0; q < NW; ++q) v += red[q][row][col];
       X[tt * ldX + K + col] = f2bf(s * v);
     }
+  }
+  const int pad = (int)(ldX - K - R);  // zero columns [K + R, ldX) of the padded wide activation
+  for (int e = threadIdx.x; e < 16 * pad; e += NW * 64) {
+    const int row = e / pad, col = e - row * pad;
+    if (t0 + row < T) X[(t0 + row) * ldX + K + R + col] = 0;
   }
 }
 
@@ -163,8 +167,10 @@ static unsigned thresh_of(double p, float* dscale) {
 
 }  // namespace lora
 
-// x [T, K], A [R, K] (R = 16, 32, 48 or 64) -> (X' [T, K+R], xd [T, K] or empty when p == 0)
-std::tuple<at::Tensor, at::Tensor> lora_fwd(const at::Tensor& x, const at::Tensor& A, double s, double p, int64_t seed) {
+// x [T, K], A [R, K] (R = 16, 32, 48 or 64) -> (X' [T, ldX], xd [T, K] or empty when p == 0); ldX >= K + R (0 = K + R):
+// columns [K + R, ldX) are zero (the wide weight's padding to a whole K-tile pair of the HIP GEMMs)
+std::tuple<at::Tensor, at::Tensor> lora_fwd(const at::Tensor& x, const at::Tensor& A, double s, double p, int64_t seed,
+                                            int64_t ldX) {
   SFT_CHECK_CUDA(x);
   SFT_CHECK_BF16(x);
   SFT_CHECK_BF16(A);
@@ -173,7 +179,9 @@ std::tuple<at::Tensor, at::Tensor> lora_fwd(const at::Tensor& x, const at::Tenso
   const long T = x.size(0);
   const int K = x.size(1), R = A.size(0);
   SFT_CHECK(A.size(1) == K && K % 256 == 0 && R % 16 == 0 && R >= 16 && R <= 64, "lora_fwd: shapes");
-  auto X = at::empty({T, K + R}, x.options());
+  if (ldX <= 0) ldX = K + R;
+  SFT_CHECK(ldX >= K + R && ldX % 8 == 0, "lora_fwd: ldX >= K + R, multiple of 8");
+  auto X = at::empty({T, ldX}, x.options());
   at::Tensor xd = p > 0 ? at::empty_like(x) : at::empty({0}, x.options());
   if (T == 0) return {X, xd};
   float dscale;
@@ -182,7 +190,7 @@ std::tuple<at::Tensor, at::Tensor> lora_fwd(const at::Tensor& x, const at::Tenso
   u16* xdp = p > 0 ? (u16*)xd.data_ptr() : nullptr;
 #define LORA_FWD(RF)                                                                                              \
   lora::fwd_kernel<RF><<<grid, 512, 0, cur_stream()>>>((const u16*)x.data_ptr(), (const u16*)A.data_ptr(),     \
-                                                       (u16*)X.data_ptr(), xdp, T, K, (float)s, thresh, dscale, \
+                                                       (u16*)X.data_ptr(), xdp, T, K, ldX, (float)s, thresh, dscale, \
                                                        (unsigned)seed)
   switch (R / 16) {
     case 1: LORA_FWD(1); break;

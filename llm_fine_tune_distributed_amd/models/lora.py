@@ -102,7 +102,7 @@ def apply_lora(model, cfg: LoRAConfig = None):
 
 @torch.no_grad()
 def _widen(owner: nn.Module, wname: str, fl: FusedLoRA) -> None:
-    """Re-home the frozen base weight W [n, K] as the left block of W' = [W | B_blockdiag] [n, K+R]
+    """Re-home the frozen base weight W [n, K] as the left block of W' = [W | B_blockdiag | 0] [n, K+Rp]
     (ops.LoRAWideFn): the base Parameter becomes a column-slice view of W', so checkpoint I/O,
     merge_lora and plain inference keep working on it unchanged."""
     w = getattr(owner, wname)
@@ -111,7 +111,10 @@ def _widen(owner: nn.Module, wname: str, fl: FusedLoRA) -> None:
         return
     n, K = w.shape
     R = fl.r * len(act)
-    wide = torch.zeros(n, K + R, device=w.device, dtype=w.dtype)
+    # the adapter columns are padded to a whole 128-column K-tile pair (zeros in W' and in X'), so the widened GEMM
+    # runs on the hand-written HIP kernels (K' % 128 == 0); the pad costs 128 / K of the base GEMM's FLOPs
+    Rp = -(-R // 128) * 128 if K % 128 == 0 else R
+    wide = torch.zeros(n, K + Rp, device=w.device, dtype=w.dtype)
     wide[:, :K].copy_(w)
     setattr(owner, wname, nn.Parameter(wide[:, :K], requires_grad=False))
     offs = [sum(fl.out_splits[:i]) for i in range(len(fl.out_splits))]

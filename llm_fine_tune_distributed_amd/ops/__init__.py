@@ -4,6 +4,7 @@ from ._ext import load as load_extension, use_hip, hip_disabled
 from .fused import (
     IGNORE_INDEX,
     add_rms_norm,
+    bump_param_epoch,
     decode_attention,
     dgrad_mm,
     dropout_add,
@@ -13,13 +14,11 @@ from .fused import (
     linear,
     linear_rope,
     linear_swiglu,
-    lm_head_chunk,
     lm_head_cross_entropy,
     lora_linear,
     qkv_rope_attention,
     rms_norm,
     rope_,
-    set_lm_head_chunk,
     swiglu,
     swiglu_linear,
     swiglu_mlp,
@@ -27,7 +26,7 @@ from .fused import (
 from .optim_kernels import adamw_flat_, grad_norm_flat, sumsq_list
 
 __all__ = [
-    "reference", "load_extension", "use_hip", "hip_disabled", "IGNORE_INDEX", "add_rms_norm", "decode_attention", "dropout_add",
+    "reference", "load_extension", "use_hip", "hip_disabled", "IGNORE_INDEX", "add_rms_norm", "bump_param_epoch", "decode_attention", "dropout_add",
     "embedding", "flash_attention", "linear", "linear_rope", "linear_swiglu", "lora_linear", "lm_head_cross_entropy", "qkv_rope_attention", "rms_norm", "rope_", "swiglu",
-    "swiglu_linear", "swiglu_mlp", "dgrad_mm", "fuse_swiglu_down", "lm_head_chunk", "set_lm_head_chunk", "adamw_flat_", "grad_norm_flat", "sumsq_list",
+    "swiglu_linear", "swiglu_mlp", "dgrad_mm", "fuse_swiglu_down", "adamw_flat_", "grad_norm_flat", "sumsq_list",
 ]

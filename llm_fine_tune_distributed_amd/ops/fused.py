@@ -196,7 +196,7 @@ def _accumulate_small_grad(param: torch.Tensor, g: torch.Tensor):
 # GEMM with the SwiGLU epilogue (gu and act written by the GEMM, the SwiGLU pass over [M, 2I] gone).
 _FWD_GEMM = os.environ.get("SFTAMD_FWD_GEMM", "blas")
 _GATE_UP = os.environ.get("SFTAMD_GATE_UP", "blas")
-_PERSIST_CFG = 50
+_PERSIST_CFG = int(os.environ.get("SFTAMD_PERSIST_CFG", "50"))
 
 
 def _grid_fills(M: int, N: int) -> bool:
@@ -861,100 +861,7 @@ class LMHeadCEFn(Function):
         return dh, dw, None, None
 
 
-class LMHeadCEChunkedFn(Function):
-    """The LM head + CE over row chunks of ``chunk`` tokens: per chunk the logits GEMM, the CE pass (dlogits written
-    in place), the chunk's dh rows (dlogits @ W) and its dW contribution (dlogits^T h) — all in the FORWARD, assuming
-    a unit upstream gradient, so the [M, V] logits never exist (peak: one [chunk, V] buffer). backward scales dh and
-    dW by the actual upstream gradient g. dW goes straight into ``main_grad`` when this is the parameter's first
-    contribution of the accumulation window (``_sftamd_fresh``: the slice is then scaled by g in place), else into a
-    separate [V, K] buffer added as g * dW in backward. Costs over LMHeadCEFn (profiles/r3_lm_head_chunked.md): the
-    dW GEMM re-reads and re-writes its bf16 output once per chunk, and the dh GEMM per chunk has chunk x K outputs.
-    Opt-in (``set_lm_head_chunk`` / SFTAMD_LMHEAD_CHUNK): MI355X's 288 GB make the full logits affordable at the
-    bench shape; this is for the sizes where they are not (large merged GA passes, Llama-3-8B batches, eval)."""
-
-    @staticmethod
-    def forward(ctx, h, weight, labels, inv_count, chunk):
-        h2d = h.reshape(-1, h.shape[-1])
-        lab = labels.reshape(-1)
-        M = h2d.shape[0]
-        need_dh, need_dw = ctx.needs_input_grad[0], ctx.needs_input_grad[1]
-        hip = _ext.use_hip(h2d)
-        stats = torch.empty(4, M, dtype=torch.float32, device=h2d.device)
-        dh = torch.empty_like(h2d) if need_dh else None
-        mg = getattr(weight, "main_grad", None)
-        ctx.dw_in_mg = False
-        dw_buf = None
-        if need_dw:
-            if mg is not None and mg.dtype == h2d.dtype and getattr(weight, "_sftamd_fresh", False):
-                target, ctx.dw_in_mg = mg, True
-                weight._sftamd_fresh = False
-            else:
-                dw_buf = torch.empty(weight.shape, dtype=h2d.dtype if hip else torch.float32, device=h2d.device)
-                target = dw_buf
-        for r0 in range(0, M, chunk):
-            r1 = min(M, r0 + chunk)
-            hc = h2d[r0:r1]
-            logits = fwd_gemm(hc, weight) if hip else torch.nn.functional.linear(hc, weight)
-            stats[:, r0:r1] = _ce_rows(logits, lab[r0:r1], inv_count, need_dh or need_dw)
-            if need_dh:
-                torch.mm(logits, weight, out=dh[r0:r1])
-            if need_dw:
-                if hip:
-                    _wgrad_mm(target, logits, hc, accumulate=r0 > 0)
-                elif r0 == 0:
-                    torch.mm(logits.t().to(target.dtype), hc.to(target.dtype), out=target)
-                else:
-                    target.addmm_(logits.t().to(target.dtype), hc.to(target.dtype))
-            del logits
-        loss = (stats[0].sum() * inv_count.float()).reshape(())
-        ctx.save_for_backward(*(t for t in (dh, dw_buf) if t is not None))
-        ctx.has = (dh is not None, dw_buf is not None)
-        ctx.weight = weight
-        ctx.h_shape = h.shape
-        ctx.mark_non_differentiable(stats)
-        return loss, stats
-
-    @staticmethod
-    def backward(ctx, dloss, _dstats):
-        saved = iter(ctx.saved_tensors)
-        dh = next(saved) if ctx.has[0] else None
-        dw_buf = next(saved) if ctx.has[1] else None
-        w = ctx.weight
-        g = dloss.float()
-        dh_out = dw_out = None
-        if dh is not None:
-            dh_out = (dh * g.to(dh.dtype)).view(ctx.h_shape)
-        if ctx.needs_input_grad[1]:
-            mg = getattr(w, "main_grad", None)
-            if ctx.dw_in_mg:
-                mg.mul_(g.to(mg.dtype))
-                _weight_grad_done(w)
-            elif mg is not None:
-                mg.add_((dw_buf * g).to(mg.dtype))
-                w._sftamd_fresh = False
-                _weight_grad_done(w)
-            else:
-                dw_out = (dw_buf * g).to(w.dtype)
-        return dh_out, dw_out, None, None, None
-
-
-_LMHEAD_CHUNK = int(os.environ.get("SFTAMD_LMHEAD_CHUNK", "0") or 0)
-
-
-def set_lm_head_chunk(rows: int) -> None:
-    """Rows per LM-head + CE chunk (0 = off: one pass over the full [M, V] logits)."""
-    global _LMHEAD_CHUNK
-    _LMHEAD_CHUNK = max(0, int(rows))
-
-
-def lm_head_chunk() -> int:
-    return _LMHEAD_CHUNK
-
-
 def lm_head_cross_entropy(h, weight, labels, inv_count) -> Tuple[torch.Tensor, torch.Tensor]:
-    M = h.numel() // h.shape[-1]
-    if _LMHEAD_CHUNK and M > _LMHEAD_CHUNK:
-        return LMHeadCEChunkedFn.apply(h, weight, labels, inv_count, _LMHEAD_CHUNK)
     return LMHeadCEFn.apply(h, weight, labels, inv_count)
 
 
@@ -1040,11 +947,11 @@ def dropout_add(a: Optional[torch.Tensor], b: torch.Tensor, p: float, seed: int)
     return ref.dropout_add(a, b, p, seed)
 
 
-def _lora_fwd(x2d, acat, s, p, seed):
+def _lora_fwd(x2d, acat, s, p, seed, ldX=0):
     if _ext.use_hip(x2d) and x2d.shape[1] % 256 == 0 and acat.shape[0] % 16 == 0 and acat.shape[0] <= 64:
-        X, xd = _ext.ops().lora_fwd(x2d, acat, float(s), float(p), int(seed))
+        X, xd = _ext.ops().lora_fwd(x2d, acat, float(s), float(p), int(seed), int(ldX))
         return X, (xd if p > 0 else None)
-    return ref.lora_fwd(x2d, acat, s, p, seed)
+    return ref.lora_fwd(x2d, acat, s, p, seed, ldX)
 
 
 def _lora_bwd_dx(base, dxa, acat, p, seed):
@@ -1053,20 +960,56 @@ def _lora_bwd_dx(base, dxa, acat, p, seed):
     return ref.lora_bwd_dx(base, dxa, acat, p, seed)
 
 
+_PARAM_EPOCH = [0]
+
+
+def bump_param_epoch() -> None:
+    """Called by the optimizers after every update they issue (parameters change in place through a raw-pointer
+    kernel, which no tensor's version counter sees)."""
+    _PARAM_EPOCH[0] += 1
+
+
+def _sync_wide(wide: torch.Tensor, K: int, r: int, meta, Bs) -> None:
+    """Copy the adapters' B matrices into their blocks of the wide weight — only when one may have changed since
+    the last copy: an optimizer update (the parameter epoch) or an in-place edit / checkpoint load (the Bs' version
+    counters). GA micro-batches and eval passes between two updates copy nothing."""
+    key = (_PARAM_EPOCH[0],) + tuple((B._version, B.data_ptr()) for B in Bs)
+    if getattr(wide, "_sftamd_bkey", None) == key:
+        return
+    with torch.no_grad():
+        for (o, rows, c), B in zip(meta, Bs):
+            wide[o:o + rows, K + c:K + c + r].copy_(B)
+    wide._sftamd_bkey = key
+
+
+# SFTAMD_LORA_FWD: the widened LoRA forward GEMM X' W'^T on the hand-written persistent kernel ("hip", default: the
+# frozen base has no AdamW pass to overlap with the next forward, the one co-runner that costs persistent grids
+# their whole rounds in full SFT) or hipBLASLt ("blas")
+_LORA_FWD = os.environ.get("SFTAMD_LORA_FWD", "hip")
+
+
+def _lora_gemm(X: torch.Tensor, wide: torch.Tensor) -> torch.Tensor:
+    if (_LORA_FWD == "hip" and _ext.use_hip(X) and X.shape[0] % 256 == 0 and X.shape[1] % 128 == 0
+            and wide.shape[0] % 256 == 0 and wide.is_contiguous() and X.is_contiguous()):
+        return _ext.ops().gemm_tn(X, wide, _LORA_FWD_CFG)
+    return torch.mm(X, wide.t())
+
+
+_LORA_FWD_CFG = 164  # persistent 4-wave kernel, plain stores (csrc/gemm_tn.hip)
+
+
 class LoRAWideFn(Function):
     """LoRA folded into the base GEMM (models.lora.FusedLoRA.wide).
 
-    The frozen base weight W [n, K] lives in the left columns of W' = [W | B_blockdiag] [n, K+R]
-    (R = r x active sub-projections); the activation is widened the same way, X' = [x | s * xa] with
-    xa = dropout(x) A_cat^T (csrc/lora.hip lora_fwd: one pass over x). Then
-        forward:  y = X' W'^T                      (one GEMM, K+R deep: no rank-r pass over y)
-        backward: dX' = dy W'  (or dy W and dy B_blockdiag separately when n is large: the N = K+R
-                               dgrad tiles badly, profiles/r1_lora_microbench.md)
-                  dB = dy^T X'[:, K:]              (block-diagonal slices)
-                  dA = (s dX'[:, K:])^T dropout(x)
-                  dx = dX'[:, :K] + dropout((s dX'[:, K:]) A_cat)   (csrc/lora.hip lora_bwd_dx: one pass)"""
-
-    SPLIT_DGRAD_MIN_N = 8192
+    The frozen base weight W [n, K] lives in the left columns of W' = [W | B_blockdiag | 0] [n, K+Rp]
+    (R = r x active sub-projections, padded to Rp = a multiple of 128); the activation is widened the same way,
+    X' = [x | s * xa | 0] with xa = dropout(x) A_cat^T (csrc/lora.hip lora_fwd: one pass over x). Then
+        forward:  y = X' W'^T                      (one HIP GEMM, K+Rp deep: no rank-r pass over y)
+        backward: base = dy W                      (the 4-wave HIP dgrad on W's column block of W')
+                  dxa  = s dy B_blockdiag          (thin [T, R] product)
+                  dB = dy^T X'[:, K:K+R]           (block-diagonal slices)
+                  dA = dxa^T dropout(x)
+                  dx = base + dropout(dxa A_cat)   (csrc/lora.hip lora_bwd_dx: one pass)"""
 
     @staticmethod
     def forward(ctx, x, wide, K, scaling, p, seed, meta, *ab):
@@ -1077,12 +1020,10 @@ class LoRAWideFn(Function):
         x2d = x.reshape(-1, K)
         if not x2d.is_contiguous():
             x2d = x2d.contiguous()
-        with torch.no_grad():
-            for (o, rows, c), B in zip(meta, Bs):
-                wide[o:o + rows, K + c:K + c + r].copy_(B)
+        _sync_wide(wide, K, r, meta, Bs)
         acat = As[0].contiguous() if n == 1 else torch.cat(As, 0)
-        X, xd = _lora_fwd(x2d, acat, scaling, p, seed)
-        y = torch.mm(X, wide.t())
+        X, xd = _lora_fwd(x2d, acat, scaling, p, seed, wide.shape[1])
+        y = _lora_gemm(X, wide)
         ctx.save_for_backward(X, acat, xd if xd is not None else X.new_empty(0))
         ctx.wide = wide
         ctx.meta = (K, R, r, n, float(scaling), float(p), int(seed), tuple(meta), x.shape)
@@ -1098,14 +1039,9 @@ class LoRAWideFn(Function):
         dy2d = dy.reshape(-1, dy.shape[-1])
         if not dy2d.is_contiguous():
             dy2d = dy2d.contiguous()
-        if wide.shape[0] >= LoRAWideFn.SPLIT_DGRAD_MIN_N:
-            base = torch.mm(dy2d, wide[:, :K])
-            dxa = torch.mm(dy2d, wide[:, K:]).mul_(scaling)
-        else:
-            dX = torch.mm(dy2d, wide)                   # [T, K+R]
-            base = dX[:, :K]
-            dxa = dX[:, K:].mul(scaling)                # contiguous [T, R]
-        dBf = torch.mm(dy2d.t(), X[:, K:])              # [n_out, R]
+        base = dgrad_mm(dy2d, wide[:, :K])              # [T, K] (HIP 4-wave dgrad where the shapes allow)
+        dxa = torch.mm(dy2d, wide[:, K:K + R]).mul_(scaling)  # [T, R]
+        dBf = torch.mm(dy2d.t(), X[:, K:K + R])          # [n_out, R]
         dBs = [dBf[o:o + rows, c:c + r].contiguous() for (o, rows, c) in meta]
         dAf = torch.mm(dxa.t(), xd if p > 0 else X[:, :K])  # [R, K]
         dAs = [dAf[i * r:(i + 1) * r] for i in range(n)]

@@ -183,12 +183,16 @@ def dropout_add(a: Optional[torch.Tensor], b: torch.Tensor, p: float, seed: int)
     return out.to(b.dtype)
 
 
-def lora_fwd(x: torch.Tensor, A: torch.Tensor, s: float, p: float, seed: int):
-    """(X' = [x | s * dropout(x) A^T], xd = dropout(x) or None) — twin of csrc/lora.hip lora_fwd."""
+def lora_fwd(x: torch.Tensor, A: torch.Tensor, s: float, p: float, seed: int, ldX: int = 0):
+    """(X' = [x | s * dropout(x) A^T | 0], xd = dropout(x) or None) — twin of csrc/lora.hip lora_fwd; ``ldX`` (0 =
+    K + R) is the padded width of X'."""
     xd = dropout_add(None, x, p, seed) if p > 0 else None
     xa = (xd if xd is not None else x).float() @ A.float().t()
-    X = torch.cat([x, (xa * s).to(x.dtype)], dim=1)
-    return X, xd
+    parts = [x, (xa * s).to(x.dtype)]
+    pad = (ldX or x.shape[1] + A.shape[0]) - x.shape[1] - A.shape[0]
+    if pad > 0:
+        parts.append(x.new_zeros(x.shape[0], pad))
+    return torch.cat(parts, dim=1), xd
 
 
 def lora_bwd_dx(base: torch.Tensor, dxa: torch.Tensor, A: torch.Tensor, p: float, seed: int) -> torch.Tensor:

@@ -127,10 +127,6 @@ class SFTConfig:
     # normalisation (global token count) and metrics; only the fp32-vs-bf16 summation order of the weight
     # gradient changes (one fp32-accumulated GEMM instead of bf16 += per micro-batch). 0 = always run GA passes.
     ga_merge_max_tokens: int = 32768
-    # LM head + CE in row chunks of this many tokens (0 = one pass): the [tokens, vocab] logits never exist, at the
-    # cost of a dW output pass per chunk (ops.fused.LMHeadCEChunkedFn). For merged GA passes or batches beyond
-    # ga_merge_max_tokens whose logits would not fit; the bench shape fits and runs unchunked.
-    lm_head_chunk_rows: int = 0
     # tokenisation cache (TRL main_process_first): rank 0 tokenises, the others load; True = output_dir/.sftamd_cache,
     # a str = that directory, False = every rank tokenises
     dataset_cache: Union[bool, str] = True

@@ -194,6 +194,9 @@ class FlatAdamW:
             norm, coef = ops.grad_norm_flat([e.grad_flat], max_grad_norm if max_grad_norm else 0.0)
         self.last_grad_norm = norm
         b1, b2 = self.betas
+        # the parameters change in place through a raw-pointer kernel: tell caches of parameter copies (LoRA's wide
+        # weight, ops.fused._sync_wide) that they are stale
+        ops.bump_param_epoch()
 
         def upd(s, t, decay):
             ops.adamw_flat_(e.param_flat[s:t], e.grad_flat[s:t], None if self.master is None else self.master[s:t],
@@ -417,6 +420,7 @@ class ShardedAdamW(FlatAdamW):
         coef = (max_grad_norm / (norm + 1e-6)).clamp(max=1.0) if max_grad_norm else torch.ones_like(norm)
         self.last_grad_norm = norm
         b1, b2 = self.betas
+        ops.bump_param_epoch()  # see FlatAdamW.step
         seed = (0x5EED + 7919 * self.step_count) & 0x7FFFFFFF if self.stochastic_rounding else 0
         # Overlapped: updates AND gathers are issued from a side stream, so the next forward only waits
         # for the buckets each layer reads (update -> gather chain per bucket), not for the whole update.

@@ -140,9 +140,6 @@ class SFTTrainer:
                                 broadcast_params=args.ddp_broadcast_params, shard=shard, link=link)
         if self.engine.tied_sparse:
             self.engine.sparse_cap = self._sparse_cap()
-        if getattr(args, "lm_head_chunk_rows", 0):
-            from ..ops import set_lm_head_chunk
-            set_lm_head_chunk(args.lm_head_chunk_rows)
         opt_cls = ShardedAdamW if shard else FlatAdamW
         self.optimizer = opt_cls(self.engine, lr=args.learning_rate, betas=(args.adam_beta1, args.adam_beta2),
                                    eps=args.adam_epsilon, weight_decay=args.weight_decay,

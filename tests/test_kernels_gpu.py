@@ -459,10 +459,13 @@ def test_lora_fwd_bwd_kernels(K, R, p):
     T = 200
     x = torch.randn(T, K, device="cuda", dtype=torch.bfloat16)
     A = (torch.randn(R, K, device="cuda") * 0.05).to(torch.bfloat16)
-    X, xd = _ext.ops().lora_fwd(x, A, 0.5, p, 99)
-    Xr, xdr = ref.lora_fwd(x, A, 0.5, p, 99)
-    assert torch.equal(X[:, :K], x)
-    assert (X[:, K:].float() - Xr[:, K:].float()).abs().max().item() < 2e-2 * (Xr[:, K:].float().abs().max().item() + 1)
+    for ldX in (0, K + 128):  # unpadded and padded to a whole 128-column K-tile pair (zeros past K + R)
+        X, xd = _ext.ops().lora_fwd(x, A, 0.5, p, 99, ldX)
+        Xr, xdr = ref.lora_fwd(x, A, 0.5, p, 99, ldX)
+        assert X.shape == Xr.shape == (T, ldX or K + R)
+        assert torch.equal(X[:, :K], x)
+        assert (X[:, K:].float() - Xr[:, K:].float()).abs().max().item() < 2e-2 * (Xr[:, K:].float().abs().max().item() + 1)
+        assert not X[:, K + R:].any()
     if p > 0:
         assert torch.equal(xd, xdr)
     wideb = torch.randn(T, K + 64, device="cuda", dtype=torch.bfloat16)
@@ -495,11 +498,13 @@ def test_gemm_tn_4wave(M, N, K):
     ref32 = x.float() @ w.float().t()
     # 13-44: schedule variants of the same kernel; 50: the persistent version (tiles > 256 walk several per
     # workgroup; K = 128 is its single-pair path)
-    for cfg in (12, 13, 16, 20, 21, 24, 25, 28, 44, 50, 60, 61):
+    # 51: one tile per workgroup; 164: no stagger / plain stores; 165: the dynamic tile queue (run twice: the
+    # per-launch queue slot must come back reset)
+    for cfg in (12, 13, 16, 20, 21, 24, 25, 28, 44, 50, 51, 60, 61, 164, 165, 165):
         c = _ext.ops().gemm_tn(x, w, cfg)
         assert rel_err(c, ref32) < 5e-3, cfg
     gu_ref = x.float() @ (w * 0.1).float().t()
-    for cfg in (12, 50):
+    for cfg in (12, 50, 51, 164, 165):
         gu, act = _ext.ops().gemm_tn_swiglu(x, w * 0.1, cfg)
         assert rel_err(gu, gu_ref) < 5e-3, cfg
         assert rel_err(act, _ext.ops().swiglu_fwd(gu)) < 2e-3, cfg
@@ -513,9 +518,20 @@ def test_gemm_tn_4wave(M, N, K):
         y = (x.float() @ w.float().t()).to(torch.bfloat16)
         qk = y[:, :(nq + nkv) * D].view(M, nq + nkv, D)
         exp = torch.cat([ref.apply_rope(qk, cs, sn).reshape(M, -1), y[:, (nq + nkv) * D:]], dim=1)
-        for cfg in (12, 50):
+        for cfg in (12, 50, 51, 164, 165):
             out = _ext.ops().gemm_tn_rope(x, w, cs, sn, (nq + nkv) * D, cfg)
             assert rel_err(out, exp) < 1e-2, cfg
+
+
+def test_gemm_tn_dynamic_queue_many_launches():
+    """The dynamic tile queue over many back-to-back launches of different grids (every one of the 64 ring slots
+    reused): each result complete and exact vs the static kernel (same per-tile arithmetic)."""
+    torch.manual_seed(1)
+    for it in range(80):
+        M, N = (512, 768) if it % 3 else (2048, 4352)
+        x = torch.randn(M, 256, device=DEV, dtype=torch.bfloat16)
+        w = torch.randn(N, 256, device=DEV, dtype=torch.bfloat16)
+        assert torch.equal(_ext.ops().gemm_tn(x, w, 165), _ext.ops().gemm_tn(x, w, 164)), it
 
 
 def test_gemm_tn_strided_rows():

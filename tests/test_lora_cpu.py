@@ -125,3 +125,48 @@ def test_save_merged_lora_loads_in_transformers(tmp_path):
     with torch.no_grad():
         bo = base(input_ids=ids).logits
     assert (bo.reshape(mo.shape) - mo).abs().max() > 1e-3  # base weights alone differ: the merge did something
+
+
+def test_wide_weight_follows_adapter_updates():
+    """The B blocks of the wide weight are re-copied only when an adapter changed (version counters): a forward
+    after an in-place update (what the optimizer does through the flat buffer) uses the new B; a repeated
+    forward with unchanged adapters copies nothing."""
+    import llm_fine_tune_distributed_amd.ops.fused as F
+    torch.manual_seed(0)
+    m = build_model(tiny(), dtype=torch.float32)
+    apply_lora(m, LoRAConfig(r=4, lora_alpha=8, lora_dropout=0.0))
+    fl = m.model.layers[0].mlp.lora["gate_up"]
+    K = fl.in_features
+    ids = torch.randint(0, 1000, (2, 12))
+    m(ids, labels=ids)
+    key = fl.wide._sftamd_bkey
+    m(ids, labels=ids)
+    assert fl.wide._sftamd_bkey == key  # nothing changed: no copy
+    with torch.no_grad():
+        fl.B[1].add_(0.5)  # bumps the version counter like the optimizer's increment_version
+    m(ids, labels=ids)
+    assert fl.wide._sftamd_bkey != key
+    o, rows, c = fl.wide_meta[1]
+    assert torch.equal(fl.wide[o:o + rows, K + c:K + c + fl.r], fl.B[1].detach())
+    assert F._sync_wide is not None
+
+
+def test_lora_trainer_updates_reach_the_wide_weight(tmp_path):
+    """Through the real engine (adapters relocated into the flat parameter buffer) and the optimizer (a raw in-place
+    update + increment_version): after a training step the wide weight's B blocks equal the updated adapters."""
+    from llm_fine_tune_distributed_amd.data.dataset import TokenizedDataset
+    from llm_fine_tune_distributed_amd.train import SFTConfig, SFTTrainer
+    torch.manual_seed(0)
+    m = build_model(tiny(), dtype=torch.float32)
+    ds = TokenizedDataset.synthetic(16, m.config.vocab_size, 6, 12, seed=3)
+    a = SFTConfig(output_dir=str(tmp_path), per_device_train_batch_size=4, max_steps=2, learning_rate=1e-2,
+                  jsonl_log=False, logging_steps=0, save_strategy="no", freeze_policy="lora", lora_dropout=0.0)
+    t = SFTTrainer(model=m, args=a, train_dataset=ds)
+    t.train()
+    fl = m.model.layers[1].self_attn.lora["qkv"]
+    ids = torch.randint(0, 1000, (2, 12))
+    m(ids, labels=ids)  # the next forward syncs the last update
+    K = fl.in_features
+    for (o, rows, c), B in zip(fl.wide_meta, fl.B):
+        assert B.detach().abs().sum() > 0  # trained away from the zero init
+        assert torch.equal(fl.wide[o:o + rows, K + c:K + c + fl.r], B.detach())

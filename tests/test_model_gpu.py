@@ -193,6 +193,52 @@ def test_lora_wide_gpu_matches_unfused():
             assert rel < 5e-2, (n, rel.item())
 
 
+@pytest.mark.parametrize("name,K,outs", [("qkv", 2048, [2048, 512, 512]), ("o", 2048, [2048]),
+                                         ("gate_up", 2048, [11008, 11008]), ("down", 11008, [2048])])
+@pytest.mark.parametrize("p", [0.0, 0.05])
+def test_lora_linear_real_widths_vs_fp32(name, K, outs, p):
+    """ops.lora_linear on the HIP path (padded wide weight, persistent forward GEMM, 4-wave base dgrad, lora_fwd /
+    lora_bwd_dx kernels) at the SmolLM3-3B projection widths == an fp32 reference of the same LoRA math with the same
+    hash dropout mask: y, dx and every adapter's dA / dB."""
+    import llm_fine_tune_distributed_amd.ops as ops
+    from llm_fine_tune_distributed_amd.models.lora import FusedLoRA, LoRAConfig, _widen
+    torch.manual_seed(0)
+    M, n = 512, sum(outs)
+    owner = torch.nn.Module()
+    owner.w = torch.nn.Parameter((torch.randn(n, K, device="cuda") * K ** -0.5).to(torch.bfloat16), requires_grad=False)
+    fl = FusedLoRA(K, outs, [f"p{i}" for i in range(len(outs))], LoRAConfig(r=16, lora_alpha=8, lora_dropout=p),
+                   [True] * len(outs), device="cuda", dtype=torch.bfloat16)
+    for b in fl.B:
+        torch.nn.init.normal_(b, std=0.05)
+    _widen(owner, "w", fl)
+    assert fl.wide.shape[1] % 128 == 0 and owner.w.data_ptr() == fl.wide.data_ptr()
+    fl.train()
+    x = torch.randn(M, K, device="cuda", dtype=torch.bfloat16).requires_grad_(True)
+    torch.manual_seed(11)
+    y = ops.lora_linear(x, owner.w, fl)
+    dy = torch.randn_like(y)
+    y.backward(dy)
+    got = {"y": y.detach().float(), "dx": x.grad.float()}
+    got.update({f"A{i}": a.grad.float() for i, a in enumerate(fl.A)})
+    got.update({f"B{i}": b.grad.float() for i, b in enumerate(fl.B)})
+    # fp32 reference with the kernel's dropout mask (same seed: the RNG draw order of lora_linear)
+    torch.manual_seed(11)
+    seed = int(torch.randint(1, 2 ** 31 - 1, (1,)).item()) if p > 0 else 0
+    keep = ops.dropout_add(None, torch.ones(M, K, device="cuda", dtype=torch.bfloat16), p, seed) != 0 if p > 0 else 1
+    x32 = x.detach().float().requires_grad_(True)
+    As = [a.detach().float().requires_grad_(True) for a in fl.A]
+    Bs = [b.detach().float().requires_grad_(True) for b in fl.B]
+    xd = x32 * keep / (1 - p)
+    yr = x32 @ owner.w.float().t() + torch.cat([xd @ a.t() @ b.t() for a, b in zip(As, Bs)], -1) * fl.scaling
+    yr.backward(dy.float())
+    want = {"y": yr.detach(), "dx": x32.grad}
+    want.update({f"A{i}": a.grad for i, a in enumerate(As)})
+    want.update({f"B{i}": b.grad for i, b in enumerate(Bs)})
+    for k in want:
+        e = ((got[k] - want[k]).norm() / (want[k].norm() + 1e-12)).item()
+        assert e < 2e-2, (name, p, k, e)
+
+
 @pytest.mark.parametrize("vocab", [1024, 66560])
 def test_wgrad_side_stream_bitwise(vocab, monkeypatch):
     """Weight-gradient GEMMs on the side stream (whole: mode 1; only a partial last round: mode tail, which the
