@@ -139,15 +139,7 @@ at::Tensor ce_fwd(at::Tensor logits, const at::Tensor& labels, const at::Tensor&
   auto lab = labels.contiguous();
   auto stats = at::empty({4, M}, logits.options().dtype(at::kFloat));
   if (M == 0) return stats;
-  static const int unroll = [] {
-    const char* e = std::getenv("SFTAMD_CE_UNROLL");
-    return e && e[0] ? atoi(e) : 4;
-  }();
   auto* lg = (u16*)logits.data_ptr();
-  if (unroll == 1)
-    ce_fwd_kernel<1><<<M, 256, 0, cur_stream()>>>(lg, lab.data_ptr<int64_t>(), inv_count.data_ptr<float>(),
-                                                  stats.data_ptr<float>(), M, V, write_grad ? 1 : 0);
-  else
     ce_fwd_kernel<4><<<M, 256, 0, cur_stream()>>>(lg, lab.data_ptr<int64_t>(), inv_count.data_ptr<float>(),
                                                   stats.data_ptr<float>(), M, V, write_grad ? 1 : 0);
   SFT_LAUNCH_CHECK();

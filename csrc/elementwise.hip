@@ -89,11 +89,6 @@ __global__ __launch_bounds__(256) void swiglu_bwd_kernel(const u16* __restrict__
   }
 }
 
-static inline int sw_unroll() {  // SFTAMD_SWIGLU_UNR = 1 | 2 | 4 (A/B knob)
-  const char* e = std::getenv("SFTAMD_SWIGLU_UNR");
-  return e && e[0] == '1' ? 1 : (e && e[0] == '2' ? 2 : 4);
-}
-
 static inline int sw_grid(long nvec, int unr) {
   long g = (nvec + 256L * unr - 1) / (256L * unr);
   return (int)std::max<long>(1, std::min<long>(g, 256L * 8));
@@ -111,20 +106,8 @@ at::Tensor swiglu_fwd(const at::Tensor& gu) {
   if (M == 0) return out;
   const long nvec = M * I / 8;
   SFT_CHECK(nvec < (1L << 31) - 256L * 8 * 256 * SW_UNR, "swiglu: tensor too large for 32-bit indexing");
-  const int unr = sw_unroll();
-  switch (unr) {
-    case 1:
-      swiglu_fwd_kernel<1><<<sw_grid(nvec, 1), 256, 0, cur_stream()>>>((const u16*)gu.data_ptr(), (u16*)out.data_ptr(),
-                                                                       (int)nvec, I / 8);
-      break;
-    case 2:
-      swiglu_fwd_kernel<2><<<sw_grid(nvec, 2), 256, 0, cur_stream()>>>((const u16*)gu.data_ptr(), (u16*)out.data_ptr(),
-                                                                       (int)nvec, I / 8);
-      break;
-    default:
-      swiglu_fwd_kernel<4><<<sw_grid(nvec, 4), 256, 0, cur_stream()>>>((const u16*)gu.data_ptr(), (u16*)out.data_ptr(),
-                                                                       (int)nvec, I / 8);
-  }
+  swiglu_fwd_kernel<4><<<sw_grid(nvec, 4), 256, 0, cur_stream()>>>((const u16*)gu.data_ptr(), (u16*)out.data_ptr(),
+                                                                   (int)nvec, I / 8);
   SFT_LAUNCH_CHECK();
   return out;
 }
@@ -141,11 +124,7 @@ at::Tensor swiglu_bwd(const at::Tensor& dy, const at::Tensor& gu) {
   SFT_CHECK(nvec < (1L << 31) - 256L * 8 * 256 * SW_UNR, "swiglu: tensor too large for 32-bit indexing");
   const u16 *dp = (const u16*)dy.data_ptr(), *gp = (const u16*)gu.data_ptr();
   u16* op = (u16*)dgu.data_ptr();
-  switch (sw_unroll()) {
-    case 1: swiglu_bwd_kernel<1><<<sw_grid(nvec, 1), 256, 0, cur_stream()>>>(dp, gp, op, (int)nvec, I / 8); break;
-    case 2: swiglu_bwd_kernel<2><<<sw_grid(nvec, 2), 256, 0, cur_stream()>>>(dp, gp, op, (int)nvec, I / 8); break;
-    default: swiglu_bwd_kernel<4><<<sw_grid(nvec, 4), 256, 0, cur_stream()>>>(dp, gp, op, (int)nvec, I / 8);
-  }
+  swiglu_bwd_kernel<4><<<sw_grid(nvec, 4), 256, 0, cur_stream()>>>(dp, gp, op, (int)nvec, I / 8);
   SFT_LAUNCH_CHECK();
   return dgu;
 }

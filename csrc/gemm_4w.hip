@@ -578,13 +578,7 @@ g4_kernel(const u16* __restrict__ A, const u16* __restrict__ B, long lda, long l
   store_tile<EPI>(acc, ea, m0 + 128 * wm, n0 + 128 * wn, lane, nrm);
 }
 
-static int group_m() {
-  static const int v = [] {
-    const char* e = std::getenv("SFTAMD_G4_GROUP");
-    return e && e[0] ? std::max(1, atoi(e)) : 8;
-  }();
-  return v;
-}
+static int group_m() { return 8; }  // GROUP_M tile order
 
 template <int LA, int LB, int EPI, bool RING>
 static void launch(const u16* A, long lda, const u16* B, long ldb, int M, int N, int kred, int ndp, int splits,
@@ -652,11 +646,7 @@ void g4_dgrad(const at::Tensor& dy, const at::Tensor& w, u16* out, long ldo, con
   ea.I = I;
   const int nbm = M / 256, nbn = N / 256, tiles = nbm * nbn;
   int ndp = tiles, splits = 1;
-  static const bool split_on = [] {
-    const char* e = std::getenv("SFTAMD_DGRAD_SPLITK");
-    return !(e && e[0] == '0');
-  }();
-  if (gu == nullptr && split_on && tiles % 256 != 0 && K >= 8192) {  // short reductions: the fixup costs more
+  if (gu == nullptr && tiles % 256 != 0 && K >= 8192) {  // short reductions: the fixup costs more
     const int rest = tiles > 256 ? tiles % 256 : tiles;
     const int s = std::min(std::min(256 / rest, 8), K / 128);
     if (s >= 2) {

@@ -500,13 +500,7 @@ __global__ void __launch_bounds__(NT) dgrad2_kernel(const u16* __restrict__ dY, 
 template <int BM, int BN, int WM, int WN, int EPI>
 void launch2(const at::Tensor& dy, const at::Tensor& w, const EpiArgs& ea);
 
-static int group_n() {
-  static const int v = [] {
-    const char* e = std::getenv("SFTAMD_DGRAD_GROUP");
-    return e && e[0] ? std::max(1, atoi(e)) : 8;
-  }();
-  return v;
-}
+static int group_n() { return 8; }  // GROUP tile order over the output columns
 
 template <int BM, int BN, int WM, int WN, int NS, int EPI, int OCC = 1, bool SCHED = true>
 void launch(const at::Tensor& dy, const at::Tensor& w, const EpiArgs& ea) {

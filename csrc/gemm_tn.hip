@@ -28,13 +28,7 @@ namespace tn {
 constexpr int NT = 512;
 constexpr int BK = 32;     // k per stage
 constexpr int ROWB = 64;   // bytes per LDS image row
-static int group_m() {
-  static const int v = [] {
-    const char* e = std::getenv("SFTAMD_TN_GROUP");
-    return e && e[0] ? std::max(1, atoi(e)) : 8;
-  }();
-  return v;
-}
+static int group_m() { return 8; }  // GROUP_M tile order: 8 row blocks share each weight panel
 
 enum { EPI_PLAIN = 0, EPI_SWIGLU = 1, EPI_ROPE = 2 };
 

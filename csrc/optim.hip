@@ -253,10 +253,10 @@ void adamw_flat(at::Tensor param, const at::Tensor& grad, const c10::optional<at
   const long n = param.numel();
   SFT_CHECK(grad.numel() == n && exp_avg.numel() == n && exp_avg_sq.numel() == n, "sizes");
   if (n == 0) return;
-  // launch shape (A/B knobs, read per call): SFTAMD_ADAM_UNR vectors per thread step (1 | 2),
-  // SFTAMD_ADAM_BLOCKS block cap (fewer blocks measured slower under the overlapped forward: gpu_run49)
-  const int unr = env_long("SFTAMD_ADAM_UNR", 2) == 1 ? 1 : 2;
-  const long cap = std::max(1L, env_long("SFTAMD_ADAM_BLOCKS", 2048));
+  // launch shape: 2 vectors per thread step, at most 2048 blocks (fewer blocks measured slower under the overlapped
+  // forward: gpu_run49; one vector per step slower: gpu_run50)
+  const int unr = 2;
+  const long cap = 2048;
   int grid = (int)std::min<long>(std::max<long>(1, (n / 8 + 256L * unr - 1) / (256L * unr)), cap);
   const float rbc1 = (float)(1.0 / bc1), rsbc2 = (float)(1.0 / std::sqrt(bc2));
   const bool has_master = master.has_value() && master->defined();

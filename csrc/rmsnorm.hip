@@ -54,114 +54,7 @@ __global__ __launch_bounds__(256) void rmsnorm_fwd_kernel(const u16* __restrict_
   if (lane == 0) rstd_out[row] = rstd;
 }
 
-// Backward: 8 waves per block, each wave handles two rows per iteration (both rows' h/dy loads
-// are in flight together: 16 KB per wave, 128 KB per CU at one block per CU), dW accumulated in
-// registers across the grid-stride loop and reduced over the block's waves in LDS.
-template <int NV>
-constexpr int bwd_threads() { return NV <= 4 ? 512 : 256; }  // H = 4096 rows need > 256 VGPRs: 1 wave/SIMD
-
-template <int NV>
-__global__ __launch_bounds__(bwd_threads<NV>()) void rmsnorm_bwd_kernel(const u16* __restrict__ dy, const u16* __restrict__ h,
-                                                          const u16* __restrict__ w, const float* __restrict__ rstd,
-                                                          const u16* __restrict__ dres, u16* __restrict__ dx,
-                                                          float* __restrict__ dw_part, int M, int H) {
-  constexpr int RPI = NV <= 4 ? 2 : 1;  // rows in flight per wave (register budget: 2 waves/SIMD)
-  __shared__ float red[4096];
-  __shared__ float wl[4096];
-  const int lane = threadIdx.x & 63;
-  constexpr int NT = bwd_threads<NV>(), WPB = NT / 64;
-  const int nwaves = gridDim.x * WPB;
-  float dw[NV][8];
-#pragma unroll
-  for (int j = 0; j < NV; ++j)
-#pragma unroll
-    for (int i = 0; i < 8; ++i) dw[j][i] = 0.f;
-  for (int c = threadIdx.x; c < H; c += NT) {
-    red[c] = 0.f;
-    wl[c] = bf2f(w[c]);
-  }
-  __syncthreads();
-  for (int row0 = blockIdx.x * WPB + (threadIdx.x >> 6); row0 < M; row0 += RPI * nwaves) {
-    uint4 hv[RPI][NV], gv[RPI][NV];
-#pragma unroll
-    for (int q = 0; q < RPI; ++q) {
-      const int row = row0 + q * nwaves;
-      const long base = (long)row * H;
-#pragma unroll
-      for (int j = 0; j < NV; ++j) {
-        const int c = (lane + 64 * j) * 8;
-        if (c < H && row < M) {
-          hv[q][j] = *(const uint4*)(h + base + c);
-          gv[q][j] = *(const uint4*)(dy + base + c);
-        } else {
-          hv[q][j] = make_uint4(0, 0, 0, 0);
-          gv[q][j] = make_uint4(0, 0, 0, 0);
-        }
-      }
-    }
-#pragma unroll
-    for (int q = 0; q < RPI; ++q) {
-      const int row = row0 + q * nwaves;
-      if (row >= M) break;
-      const long base = (long)row * H;
-      const float r = rstd[row];
-      // rows stay packed (bf16) in registers and are unpacked again in the second pass: keeps
-      // the kernel at 2 waves/SIMD without spills up to H = 4096
-      float dot = 0.f;
-#pragma unroll
-      for (int j = 0; j < NV; ++j) {
-        const int c = (lane + 64 * j) * 8;
-        float wv[8], n[8], g[8];
-        *(float4*)&wv[0] = *(const float4*)&wl[c < H ? c : 0];
-        *(float4*)&wv[4] = *(const float4*)&wl[(c < H ? c : 0) + 4];
-        unpack8(hv[q][j], n);
-        unpack8(gv[q][j], g);
-#pragma unroll
-        for (int i = 0; i < 8; ++i) {
-          const float nn = n[i] * r;
-          dw[j][i] += g[i] * nn;
-          dot += g[i] * wv[i] * nn;
-        }
-      }
-      uint4 dv[NV];
-      if (dres) {
-#pragma unroll
-        for (int j = 0; j < NV; ++j) {
-          const int c = (lane + 64 * j) * 8;
-          dv[j] = c < H ? *(const uint4*)(dres + base + c) : make_uint4(0, 0, 0, 0);
-        }
-      }
-      dot = wave_sum(dot) / (float)H;
-#pragma unroll
-      for (int j = 0; j < NV; ++j) {
-        const int c = (lane + 64 * j) * 8;
-        if (c < H) {
-          float wv[8], n[8], g[8], o[8], d[8];
-          *(float4*)&wv[0] = *(const float4*)&wl[c];
-          *(float4*)&wv[4] = *(const float4*)&wl[c + 4];
-          unpack8(hv[q][j], n);
-          unpack8(gv[q][j], g);
-          if (dres) unpack8(dv[j], d);
-#pragma unroll
-          for (int i = 0; i < 8; ++i) o[i] = r * (g[i] * wv[i] - n[i] * r * dot) + (dres ? d[i] : 0.f);
-          *(uint4*)(dx + base + c) = pack8(o);
-        }
-      }
-    }
-  }
-#pragma unroll
-  for (int j = 0; j < NV; ++j) {
-    const int c = (lane + 64 * j) * 8;
-    if (c < H) {
-#pragma unroll
-      for (int i = 0; i < 8; ++i) atomicAdd(&red[c + i], dw[j][i]);
-    }
-  }
-  __syncthreads();
-  for (int c = threadIdx.x; c < H; c += NT) dw_part[(long)blockIdx.x * H + c] = red[c];
-}
-
-// Backward v2 (default): 4-wave blocks, ONE row per wave per iteration with every load of the row
+// Backward: 4-wave blocks, ONE row per wave per iteration with every load of the row
 // (h, dy, dres, rstd) issued together — v1 issues dres only after the dot-product reduction, so
 // each of its iterations pays two serialised HBM latencies. ~120 VGPRs -> 4 waves/SIMD, 16 rows
 // (192 KB) in flight per CU. The weight stays packed bf16 in registers; dW accumulates in fp32
@@ -295,28 +188,6 @@ __global__ __launch_bounds__(1024) void col_sum2_kernel(const float* __restrict_
   }
 }
 
-// out[c] = sum_b part[b][c] in a fixed order (deterministic). Block = 64 columns x 4 row
-// groups; each thread keeps 4 independent accumulators so the loads pipeline.
-__global__ __launch_bounds__(256) void col_sum_kernel(const float* __restrict__ part, float* __restrict__ out, int P,
-                                                      int H) {
-  __shared__ float red[4][64];
-  const int c = blockIdx.x * 64 + (threadIdx.x & 63);
-  const int rg = threadIdx.x >> 6;
-  float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
-  if (c < H) {
-    int b = rg;
-    for (; b + 12 < P; b += 16) {
-      a0 += part[(long)b * H + c];
-      a1 += part[(long)(b + 4) * H + c];
-      a2 += part[(long)(b + 8) * H + c];
-      a3 += part[(long)(b + 12) * H + c];
-    }
-    for (; b < P; b += 4) a0 += part[(long)b * H + c];
-  }
-  red[rg][threadIdx.x & 63] = (a0 + a1) + (a2 + a3);
-  __syncthreads();
-  if (rg == 0 && c < H) out[c] = (red[0][threadIdx.x] + red[1][threadIdx.x]) + (red[2][threadIdx.x] + red[3][threadIdx.x]);
-}
 
 #define NV_DISPATCH(H, ...)                      \
   if ((H) <= 512) {                              \
@@ -379,12 +250,8 @@ std::tuple<at::Tensor, at::Tensor> rmsnorm_bwd(const at::Tensor& dy, const at::T
   SFT_CHECK(rstd.numel() == M && weight.numel() == H && dy.numel() == h.numel(), "rmsnorm_bwd: shape mismatch");
   SFT_CHECK(H % 8 == 0 && H <= 4096, "rmsnorm_bwd: hidden size must be a multiple of 8 and <= 4096");
   auto dw = at::empty({H}, h.options().dtype(at::kFloat));
-  static const bool v1 = [] {
-    const char* e = std::getenv("SFTAMD_RMSNORM_BWD");
-    return e && e[0] == '1';
-  }();
   if (M == 0) return {dx, dw.zero_()};
-  if (!v1) {
+  {
     // 4 rows per wave at M = 8192 (512 blocks = 2 per CU): partials stay small (4 MB fp32)
     const int nblk = std::max(1, std::min((M + 15) / 16, 512));
     auto part = at::empty({nblk, H}, h.options().dtype(at::kFloat));
@@ -404,21 +271,6 @@ std::tuple<at::Tensor, at::Tensor> rmsnorm_bwd(const at::Tensor& dy, const at::T
     SFT_LAUNCH_CHECK();
     return {dx, obf ? at::empty({0}, dw.options()) : dw};
   }
-  int nblk = std::min((M + 15) / 16, 256);  // one 8-wave block per CU, >= 2 rows per wave
-  nblk = std::max(nblk, 1);
-  auto part = at::empty({nblk, H}, h.options().dtype(at::kFloat));
-  NV_DISPATCH(H, rmsnorm_bwd_kernel<NV><<<nblk, bwd_threads<NV>(), 0, cur_stream()>>>(
-                     (const u16*)dy.data_ptr(), (const u16*)h.data_ptr(), (const u16*)weight.data_ptr(),
-                     rstd.data_ptr<float>(), dr, (u16*)dx.data_ptr(), part.data_ptr<float>(), M, H));
-  SFT_LAUNCH_CHECK();
-  col_sum_kernel<<<(H + 63) / 64, 256, 0, cur_stream()>>>(part.data_ptr<float>(), dw.data_ptr<float>(), nblk, H);
-  SFT_LAUNCH_CHECK();
-  if (dw_out.has_value() && dw_out->defined()) {
-    at::Tensor o = *dw_out;
-    if (accumulate) o.add_(dw.to(o.scalar_type())); else o.copy_(dw);
-    return {dx, at::empty({0}, dw.options())};
-  }
-  return {dx, dw};
 }
 
 TORCH_LIBRARY_IMPL(sftamd, CUDA, m) {

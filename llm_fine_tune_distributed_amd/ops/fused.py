@@ -81,7 +81,7 @@ def _wgrad_cfg(T: int, N: int, K: int) -> int:
 
 
 def _wgrad_mm(out: torch.Tensor, dy2d: torch.Tensor, x2d: torch.Tensor, accumulate: bool,
-              norm: Optional[torch.Tensor] = None, tail_stream=None) -> bool:
+              norm: Optional[torch.Tensor] = None) -> bool:
     """out (+)= dy2d^T @ x2d, all bf16 (out is the flat-buffer gradient view). ``norm``: gradient-norm partial
     slots the ring kernels fill with the sum of squares of the values they store; returns whether they did
     (other variants leave the norm to DDPEngine.grad_norm_sq's leftover pass)."""
@@ -90,8 +90,7 @@ def _wgrad_mm(out: torch.Tensor, dy2d: torch.Tensor, x2d: torch.Tensor, accumula
         cfg = _wgrad_cfg(dy2d.shape[0], dy2d.shape[1], x2d.shape[1])
     if cfg:
         use_norm = norm is not None and cfg % 100 in ((9, 10, 12, 13) if os.environ.get("SFTAMD_NORM_4W", "1") == "1" else (9, 10))
-        _ext.ops().wgrad_gemm(out, dy2d.contiguous(), x2d.contiguous(), accumulate, cfg, norm if use_norm else None,
-                              0 if tail_stream is None else tail_stream.cuda_stream)
+        _ext.ops().wgrad_gemm(out, dy2d.contiguous(), x2d.contiguous(), accumulate, cfg, norm if use_norm else None)
         return use_norm
     if accumulate:
         out.addmm_(dy2d.t(), x2d)
@@ -100,39 +99,11 @@ def _wgrad_mm(out: torch.Tensor, dy2d: torch.Tensor, x2d: torch.Tensor, accumula
     return False
 
 
-# Optional (SFTAMD_WGRAD_STREAM=1): weight-gradient GEMMs off the critical path. Backward's dgrad
-# chain (dX of layer L feeds layer L-1) is serial, the weight gradients are not — they can go to a
-# side HIP stream to fill CUs the dgrad GEMMs / attention / norm kernels leave idle. Consumers of
-# main_grad wait for the side stream: the DDP bucket collectives (issued FROM the side stream, so the
-# compute stream never stalls), the end of backward and the tied-embedding backward, which
-# accumulates into the buffer the lm_head wgrad wrote. Measured on MI355X (profiles/r1_gemm_tn.md):
-# 3.5 % SLOWER end to end — two 256x256-tile GEMMs at one workgroup per CU thrash each other's L2
-# and LDS-DMA bandwidth — so it is off by default; the plumbing stays tested (bitwise-equal grads).
-_WGRAD_STREAM_MODE = os.environ.get("SFTAMD_WGRAD_STREAM", "0")
-# SFTAMD_WGRAD_STREAM=tail: only the partial last round of a weight-gradient grid (gate_up / down: 688 tiles = 2.69
-# rounds of 256 CUs) goes to the side stream, so the next backward kernels fill the CUs it leaves idle; the whole
-# rounds stay on the compute stream (csrc/gemm_wgrad.hip launch_ring tail_stream).
-_wgrad_streams = {}
-
-
-def _wgrad_stream(dev: torch.device):
-    if _WGRAD_STREAM_MODE == "0" or dev.type != "cuda":
-        return None
-    idx = dev.index if dev.index is not None else torch.cuda.current_device()
-    s = _wgrad_streams.get(idx)
-    if s is None:
-        s = _wgrad_streams[idx] = torch.cuda.Stream(device=idx)
-    return s
-
-
 def wgrad_sync(dev: Optional[torch.device] = None) -> None:
-    """Make the current stream wait for every weight-gradient GEMM issued on the side stream."""
-    if not _wgrad_streams:
-        return
-    idx = torch.cuda.current_device() if dev is None or dev.index is None else dev.index
-    s = _wgrad_streams.get(idx)
-    if s is not None:
-        torch.cuda.current_stream(idx).wait_stream(s)
+    """Weight gradients are produced in stream order on the compute stream (a side stream for them measured 3.5 %
+    slower end to end: two 256 x 256-tile GEMMs at one workgroup per CU thrash each other's L2 / LDS-DMA bandwidth,
+    profiles/r1_gemm_tn.md), so there is nothing to wait for; kept as the engine's synchronisation point."""
+    return None
 
 
 def _accumulate_weight_grad(param: torch.Tensor, dy2d: torch.Tensor, x2d: torch.Tensor,
@@ -149,20 +120,7 @@ def _accumulate_weight_grad(param: torch.Tensor, dy2d: torch.Tensor, x2d: torch.
             ns = getattr(param, "_sftamd_norm_slots", None)
             if ns is not None and getattr(param, "_sftamd_remaining", 1) != 1:
                 ns = None
-            ws = _wgrad_stream(dy2d.device)
-            if ws is not None and _WGRAD_STREAM_MODE == "tail":
-                ws.wait_stream(torch.cuda.current_stream(dy2d.device))  # the tail launch's operands are ready
-                done = _wgrad_mm(mg, dy2d, x2d, accumulate=not fresh, norm=ns, tail_stream=ws)
-                dy2d.record_stream(ws)
-                x2d.record_stream(ws)
-            elif ws is not None:
-                ws.wait_stream(torch.cuda.current_stream(dy2d.device))
-                with torch.cuda.stream(ws):
-                    done = _wgrad_mm(mg, dy2d, x2d, accumulate=not fresh, norm=ns)
-                dy2d.record_stream(ws)  # keep the operands alive until the side stream is done
-                x2d.record_stream(ws)
-            else:
-                done = _wgrad_mm(mg, dy2d, x2d, accumulate=not fresh, norm=ns)
+            done = _wgrad_mm(mg, dy2d, x2d, accumulate=not fresh, norm=ns)
             if done:
                 param._sftamd_norm_done = True
         elif fresh:
@@ -399,7 +357,6 @@ class EmbeddingFn(Function):
             if mg is not None and getattr(w, "_sftamd_fresh", False):
                 mg.zero_()  # untied embedding: the sparse row update needs a zeroed buffer
                 w._sftamd_fresh = False
-            wgrad_sync(dy2d.device)  # tied weight: the lm_head wgrad (side stream) wrote this buffer first
             _ext.ops().embedding_bwd(dy2d, sorted_ids, perm.to(torch.int32), target)
             if mg is not None:
                 _weight_grad_done(w)

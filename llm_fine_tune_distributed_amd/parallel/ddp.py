@@ -536,20 +536,8 @@ class DDPEngine:
     def _launch(self, b: Bucket):
         view = self.grad_flat[b.start:b.end]
         ws = None
-        if view.is_cuda:
-            from ..ops.fused import _wgrad_stream
-            ws = _wgrad_stream(view.device)
-        if ws is not None:
-            # the bucket's weight gradients may still be in flight on the side stream: issue the
-            # collective from that stream (after it has also caught up with the compute stream), so
-            # RCCL waits for them without ever stalling the compute stream's dgrad chain
-            ws.wait_stream(torch.cuda.current_stream(view.device))
         if self.world_size > 1:
-            if ws is not None:
-                with torch.cuda.stream(ws):
-                    self._collective(b, view)
-            else:
-                self._collective(b, view)
+            self._collective(b, view)
         if self.track_norm:
             self._bucket_norm(b, ws)
         b.launched = True
@@ -716,9 +704,6 @@ class DDPEngine:
 
     def finish_backward(self):
         """Wait for all bucket all-reduces (launching any bucket whose params had no grad)."""
-        if self.grad_flat.is_cuda:
-            from ..ops.fused import wgrad_sync
-            wgrad_sync(self.grad_flat.device)
         if not self.sync_grads:
             return
         self._zero_untouched()

@@ -151,10 +151,8 @@ class FlatAdamW:
         self._pending = False
         self._hooks = []
 
-        # SFTAMD_UPDATE_WAIT_STRIDE=s: layer i waits (every s-th layer) for the update of layer i + s - 1 instead
-        # of one stream wait per layer. Each wait is a barrier packet in the compute queue (~10 us of idle GPU at a
-        # layer boundary, profiles/r2_step_timeline.md) and the in-order update stream normally runs layers ahead.
-        stride = max(1, int(os.environ.get("SFTAMD_UPDATE_WAIT_STRIDE", "1") or 1))
+        # layer i's forward waits for the update of its own parameters (group i + 1; group 0 = the embedding) — one
+        # stream-wait packet per layer; the in-order update stream normally runs layers ahead of the forward
         nl = len(inner.layers)
 
         def waiter(i):
@@ -165,8 +163,7 @@ class FlatAdamW:
 
         self._hooks.append(model.register_forward_pre_hook(waiter(0)))
         for i, layer in enumerate(inner.layers):
-            if i % stride == 0:
-                self._hooks.append(layer.register_forward_pre_hook(waiter(min(i + stride, nl))))
+            self._hooks.append(layer.register_forward_pre_hook(waiter(min(i + 1, nl))))
         self._hooks.append(inner.layers[-1].register_forward_hook(waiter(len(groups) - 1)))
         self.overlap = True
         return True
