@@ -71,14 +71,14 @@ def parse(argv=None):
                     help="SFTConfig.padding_free (auto: the trainer default, on for GPU training)")
     ap.add_argument("--freeze-policy", default="full", choices=["full", "last_n_layers", "lora"])
     ap.add_argument("--master-weights", action="store_true", help="fp32 master copy (default: bf16 params + SR)")
-    ap.add_argument("--optim-state", default=os.environ.get("SFTAMD_OPTIM_STATE", "bf16"), choices=["fp32", "bf16"],
+    ap.add_argument("--optim-state", default="bf16", choices=["fp32", "bf16"],
                     help="Adam moment dtype. bf16 (default) = the reference's: torch AdamW keeps exp_avg / exp_avg_sq "
                          "in the parameter dtype, bf16 for its bf16 model (training.py:99); here stored with "
                          "stochastic rounding (unbiased), so not less precise than the reference")
-    ap.add_argument("--zero", type=int, default=int(os.environ.get("SFTAMD_ZERO", "1")), choices=[0, 1],
+    ap.add_argument("--zero", type=int, default=1, choices=[0, 1],
                     help="1 (default): ZeRO-1 over the DDP buckets when N > 1 (reduce-scatter grads, 1/N of AdamW "
                          "per rank, all-gather params under the next forward); 0: replicated all-reduce DDP")
-    ap.add_argument("--tunableop", default=os.environ.get("SFTAMD_TUNABLEOP", "auto"),
+    ap.add_argument("--tunableop", default="auto",
                     help="auto: load the committed GEMM selections; tune: tune missing shapes into it; off")
     ap.add_argument("--baseline-1gpu", type=float, default=float(os.environ.get("SFTAMD_BENCH_1GPU", "0")),
                     help="1-GPU samples/s of the same config: adds scaling_efficiency = value / (N * this)")

@@ -8,7 +8,6 @@
 #include <vector>
 
 namespace sftamd {
-int64_t cu_masked_stream(int64_t n, int64_t stride, int64_t offset);  // csrc/optim.hip
 // csrc/ipc_allreduce.hip: one-shot peer-memory all-reduce for small messages
 int64_t ipc_ar_create(int64_t cap, int64_t world, int64_t rank);
 std::vector<int64_t> ipc_ar_handle(int64_t id);
@@ -33,7 +32,6 @@ std::string dispatch_trace_read();
 
 TORCH_LIBRARY(sftamd, m) {
   // runtime: CU-restricted HIP stream for the optimizer's side stream (no tensor arguments: catch-all kernel)
-  m.def("cu_masked_stream(int n, int stride=1, int offset=0) -> int", &sftamd::cu_masked_stream);
   // runtime: IPC peer-memory all-reduce contexts (no tensor arguments: catch-all kernels)
   m.def("ipc_ar_create(int cap, int world, int rank) -> int", &sftamd::ipc_ar_create);
   m.def("ipc_ar_handle(int ctx) -> int[]", &sftamd::ipc_ar_handle);

@@ -1711,18 +1711,13 @@ std::tuple<at::Tensor, at::Tensor> gemm_tn_swiglu(const at::Tensor& x, const at:
   auto gu = at::empty({M, N}, x.options());
   auto act = at::empty({M, I}, x.options());
   tn::EpiArgs ea{(u16*)gu.data_ptr(), (u16*)act.data_ptr(), nullptr, nullptr, (long)N, I, 0};
-  static const bool trc = [] {
-    const char* e = std::getenv("SFTAMD_TN_TRC");
-    return !(e && e[0] == '0');
-  }();
   if (cfg == 50) tn::launch5<tn::EPI_SWIGLU, tn::TN5_DEFAULT>(x, w_gu, N, ea);
   else if (cfg == 164) tn::launch5<tn::EPI_SWIGLU, 0>(x, w_gu, N, ea);
   else if (cfg == 51) tn::launch5<tn::EPI_SWIGLU, 0>(x, w_gu, N, ea, false);
   else if (cfg == 165) tn::launch5<tn::EPI_SWIGLU, 128>(x, w_gu, N, ea);
   else if (cfg == 12) tn::launch4<tn::EPI_SWIGLU, 0, 4>(x, w_gu, N, ea);
   else if (x.size(1) % 64 == 0 && N % 256 == 0 && cfg == 11) tn::launch3<tn::EPI_SWIGLU, true, 2>(x, w_gu, N, ea);
-  else if (x.size(1) % 64 == 0 && trc) tn::launch2<256, 256, 2, 4, 2, tn::EPI_SWIGLU, 3>(x, w_gu, N, ea);
-  else if (x.size(1) % 64 == 0) tn::launch2<256, 256, 2, 4, 2, tn::EPI_SWIGLU>(x, w_gu, N, ea);
+  else if (x.size(1) % 64 == 0) tn::launch2<256, 256, 2, 4, 2, tn::EPI_SWIGLU, 3>(x, w_gu, N, ea);
   else tn::launch<256, 256, 2, 4, 5, tn::EPI_SWIGLU>(x, w_gu, N, ea);
   return {gu, act};
 }

@@ -89,27 +89,6 @@ at::Tensor sumsq_chunks(const at::Tensor& x, const at::Tensor& chunks) {
   return part;
 }
 
-// A HIP stream restricted to ``n`` CUs (CU i * stride + offset, modulo the CU count): the optimizer's side
-// stream, so the HBM-bound update streams on a few CUs instead of time-sharing every CU with the forward's
-// 256x256-tile GEMM workgroups (which need a whole CU's VGPRs and cannot co-reside with update waves). The stream
-// lives for the process (returned as an integer handle for torch.cuda.ExternalStream).
-int64_t cu_masked_stream(int64_t n, int64_t stride, int64_t offset) {
-  int dev = 0, ncu = 0;
-  SFT_CHECK(hipGetDevice(&dev) == hipSuccess, "cu_masked_stream: no device");
-  SFT_CHECK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && ncu > 0,
-            "cu_masked_stream: CU count");
-  SFT_CHECK(n > 0 && n <= ncu && stride > 0, "cu_masked_stream: 0 < n <= CU count, stride > 0");
-  std::vector<uint32_t> mask((ncu + 31) / 32, 0u);
-  for (long i = 0; i < n; ++i) {
-    const long c = (offset + i * stride) % ncu;
-    mask[c / 32] |= 1u << (c % 32);
-  }
-  hipStream_t st = nullptr;
-  SFT_CHECK(hipExtStreamCreateWithCUMask(&st, (uint32_t)mask.size(), mask.data()) == hipSuccess,
-            "hipExtStreamCreateWithCUMask failed");
-  return (int64_t)(intptr_t)st;
-}
-
 // omb1 = 1 - beta1, omb2 = 1 - beta2 computed in double on the host (torch AdamW's constants:
 // 1.f - 0.999f would be 1.0000467e-3, not fp32(1e-3)).
 __device__ __forceinline__ void adam_elem(float& w, float g, float& m, float& v, float lr, float b1, float b2, float eps,

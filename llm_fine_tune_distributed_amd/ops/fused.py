@@ -42,9 +42,6 @@ def _weight_grad_done(param: torch.Tensor) -> None:
 
 
 _WGRAD_MODE = os.environ.get("SFTAMD_WGRAD", "auto")  # auto | blas | <cfg int> (kernel variant)
-# SFTAMD_WGRAD_4W=1 (default): the 4-wave kernel (csrc/gemm_4w.hip, cfg 13: 128 x 128 wave tiles, AGPR accumulators,
-# 4-slot ring of 32-token steps) where it beat the 8-wave rings in tools/bench_wgrad.py (profiles/r3_bwd_gemm_4wave.md)
-_WGRAD_4W = os.environ.get("SFTAMD_WGRAD_4W", "1") == "1"
 
 
 def _wgrad_cfg(T: int, N: int, K: int) -> int:
@@ -61,11 +58,13 @@ def _wgrad_cfg(T: int, N: int, K: int) -> int:
     if _WGRAD_MODE not in ("auto", ""):
         return int(_WGRAD_MODE)
     tiles = (N // 256) * (K // 256)
-    if _WGRAD_4W and N % 256 == 0 and K % 256 == 0 and T % 128 == 0 and 288 <= tiles < 2048:
+    if N % 256 == 0 and K % 256 == 0 and T % 128 == 0 and 288 <= tiles < 2048:
+        # the 4-wave kernel (csrc/gemm_4w.hip, cfg 13: 128 x 128 wave tiles, AGPR accumulators, 4-slot ring of 32-token
+        # steps) where it beat the 8-wave rings in tools/bench_wgrad.py (profiles/r3_bwd_gemm_4wave.md).
         # gate_up (688 tiles): 0.568 vs 0.578 ms (cfg 10); down_proj (344 tiles = 1.34 rounds): hybrid, the 88 tiles
         # past the whole round split 2 ways over the tokens (1213): 0.301 vs 0.341 (cfg 13) vs 0.349 (cfg 9);
         # lm_head / tied embedding (4008 tiles) stays on cfg 10: 3.195 vs 3.213 ms (profiles/r3_bwd_gemm_4wave.md)
-        return 1213 if tiles < 512 and (T // 128) >= 2 and os.environ.get("SFTAMD_WGRAD_HYBRID", "1") == "1" else 13
+        return 1213 if tiles < 512 and (T // 128) >= 2 else 13
     if N % 256 == 0 and K % 256 == 0 and tiles >= 512:
         return 10
     if (N % 256 == 0 and K % 256 == 0 and 64 < (N // 256) * (K // 256) <= 128 and (T // 32) % 2 == 0
@@ -89,7 +88,7 @@ def _wgrad_mm(out: torch.Tensor, dy2d: torch.Tensor, x2d: torch.Tensor, accumula
     if _ext.use_hip(dy2d) and dy2d.dtype == torch.bfloat16 and out.is_contiguous():
         cfg = _wgrad_cfg(dy2d.shape[0], dy2d.shape[1], x2d.shape[1])
     if cfg:
-        use_norm = norm is not None and cfg % 100 in ((9, 10, 12, 13) if os.environ.get("SFTAMD_NORM_4W", "1") == "1" else (9, 10))
+        use_norm = norm is not None and cfg % 100 in (9, 10, 12, 13)
         _ext.ops().wgrad_gemm(out, dy2d.contiguous(), x2d.contiguous(), accumulate, cfg, norm if use_norm else None)
         return use_norm
     if accumulate:
@@ -234,9 +233,6 @@ def _dgrad_ok(dy2d: torch.Tensor, w: torch.Tensor) -> bool:
             and w.data_ptr() % 16 == 0)
 
 
-_DGRAD_4W = os.environ.get("SFTAMD_DGRAD_4W", "1") == "1"
-
-
 def _dgrad_cfg(dy2d: torch.Tensor, swiglu: bool = False) -> int:
     """Kernel configuration: 7 = 256 x 256 tiles, 64-deep K stages (two 32-deep MFMA sub-steps per barrier);
     5 = the 32-deep three-stage ring for reductions that are not a multiple of 64 (profiles/r2_dgrad.md);
@@ -245,15 +241,15 @@ def _dgrad_cfg(dy2d: torch.Tensor, swiglu: bool = False) -> int:
     gate_up (K = 22016) 0.528 (cfg 13) vs 0.548 for hipBLASLt, lm_head (K = 128256) 2.98 vs 3.09. The fused SwiGLU
     backward epilogue stays on cfg 7 (its LDS-staged epilogue: 0.436 vs 0.58 ms for the register epilogue)."""
     K = dy2d.shape[1]
-    if _DGRAD_4W and not swiglu and K % 128 == 0:
+    if not swiglu and K % 128 == 0:
         return 13 if K > 4096 else 12
     return 7 if K % 64 == 0 else 5
 
 
 def dgrad_mm(dy2d: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
     """dX = dy @ W (W = the projection's [out, in] weight). The HIP kernel where it beats hipBLASLt: every
-    SmolLM3 shape with M % 256 == 0 on the 4-wave kernel (gate_up and lm_head included, _dgrad_cfg); without it
-    (SFTAMD_DGRAD_4W=0) reductions of at most 4096 output features into at most 4096 inputs on cfg 7."""
+    SmolLM3 shape with M % 256 == 0 on the 4-wave kernel (gate_up and lm_head included, _dgrad_cfg); reductions that
+    are not a multiple of 128 of at most 4096 output features into at most 4096 inputs on cfg 7 / 5."""
     if _dgrad_ok(dy2d, w):
         cfg = _dgrad_cfg(dy2d)
         if cfg in (12, 13) or _DGRAD_MODE == "hip" or (dy2d.shape[1] <= 4096 and w.shape[1] <= 4096):
@@ -292,12 +288,12 @@ class SwiGLULinearFn(Function):
         return dgu, dw
 
 
-_SWIGLU_DOWN = os.environ.get("SFTAMD_SWIGLU_DOWN", "1") == "1"
+_SWIGLU_DOWN = True  # (a test seam: tests/test_model_gpu.py switches the MLP split off)
 
 
 def fuse_swiglu_down() -> bool:
     """MLP split (default): gate_up GEMM | down GEMM with the SwiGLU backward fused into its dgrad. Off when the
-    forward-fused gate_up + SwiGLU epilogue is requested instead (SFTAMD_TN=swiglu / 1) or SFTAMD_SWIGLU_DOWN=0."""
+    forward-fused gate_up + SwiGLU epilogue is requested instead (SFTAMD_TN=swiglu / 1)."""
     return _SWIGLU_DOWN and _TN_MODE not in ("1", "swiglu")
 
 
@@ -479,15 +475,12 @@ _TN_PLAIN = os.environ.get("SFTAMD_TN_PLAIN", "0") == "1"
 _TN_SMALL_TILES = os.environ.get("SFTAMD_TN_SMALL_TILES", "0")
 
 
-_TN_PINGPONG = os.environ.get("SFTAMD_TN_PINGPONG", "1") == "1"
-
-
 def _tn_cfg(M: int, N: int) -> int:
     """Forward GEMM configuration. Default: the ping-pong 8-phase schedule (cfg 11, csrc/gemm_tn.hip: the two
     wave rows one barrier apart, transposed-C epilogue) wherever N % 256 == 0 — 2-6 % faster than the BK64 ring
     (cfg 2) on every SmolLM3 shape (profiles/r2_gemm_pingpong.md). SFTAMD_TN_SMALL_TILES=1: 256x128 tiles
     (cfg 6) when the 256x256 grid does not fill whole waves of the 256 CUs."""
-    if _TN_PINGPONG and N % 256 == 0:
+    if N % 256 == 0:
         return 11
     if _TN_SMALL_TILES == "0":
         return 2
@@ -531,7 +524,7 @@ class GateUpSwiGLUFn(Function):
 def _tn_swiglu_cfg(weight: torch.Tensor) -> int:
     if _GATE_UP not in ("blas", "") and weight.shape[0] % 256 == 0 and weight.shape[1] % 128 == 0:
         return int(_GATE_UP)
-    return 11 if _TN_PINGPONG and weight.shape[0] % 256 == 0 else 5
+    return 11 if weight.shape[0] % 256 == 0 else 5
 
 
 def linear_swiglu(x: torch.Tensor, weight: torch.Tensor) -> torch.Tensor:
@@ -754,12 +747,12 @@ class QKVRopeAttnFn(Function):
         return dx, dw, None, None, None, None, None, None, None, None, None
 
 
-_ROPE_ATTN_FUSED = os.environ.get("SFTAMD_ROPE_ATTN", "1") == "1"
+_ROPE_ATTN_FUSED = True  # (a test seam: tests/test_model_gpu.py compares against the two separate nodes)
 
 
 def qkv_rope_attention(x, weight, cos, sin, cu_seqlens, max_seqlen, n_q, n_kv, head_dim, scale=None, causal=True):
     """flash_attention(linear_rope(x, W_qkv, cos, sin)) — one fused autograd node when the HIP paths apply
-    (SFTAMD_ROPE_ATTN=0: the two separate nodes)."""
+    (the two separate nodes otherwise)."""
     scale = scale if scale is not None else 1.0 / math.sqrt(head_dim)
     x2d = x.reshape(-1, x.shape[-1])
     if (_ROPE_ATTN_FUSED and _TN_MODE in ("1", "rope") and head_dim == 128 and _tn_ok(x2d, weight)

@@ -47,12 +47,9 @@ def read_env():
 
 
 def nccl_options():
-    """RCCL process-group options: collectives on a HIGH-PRIORITY HIP stream (SFTAMD_NCCL_HIGH_PRIORITY,
-    default on). The bucket reduce-scatters / all-reduces (backward) and the ZeRO-1 all-gathers (forward)
+    """RCCL process-group options: collectives on a HIGH-PRIORITY HIP stream. The bucket reduce-scatters / all-reduces (backward) and the ZeRO-1 all-gathers (forward)
     are meant to run under the compute kernels; on a busy device a high-priority queue gets their
     kernels dispatched as soon as CUs free up instead of behind the queued GEMMs."""
-    if os.environ.get("SFTAMD_NCCL_HIGH_PRIORITY", "1") != "1":
-        return None
     try:
         opts = dist.ProcessGroupNCCL.Options()
         opts.is_high_priority_stream = True

@@ -13,7 +13,6 @@ from __future__ import annotations
 
 import contextlib
 import math
-import os
 from typing import Callable, Dict, Optional
 
 import torch
@@ -21,26 +20,10 @@ import torch
 from .. import ops
 
 
-_UPDATE_STREAMS = {}
-
-
 def _update_stream(device: torch.device):
-    """Side stream of the overlapped optimizer update. SFTAMD_ADAMW_CUS=n (> 0) restricts it to n CUs (CU
-    i * SFTAMD_ADAMW_CU_STRIDE, hipExtStreamCreateWithCUMask): the HBM-bound update then streams on a few CUs
-    instead of time-sharing every CU with the next forward's GEMM workgroups. Default: unrestricted."""
-    n = int(os.environ.get("SFTAMD_ADAMW_CUS", "0") or 0)
-    if n <= 0:
-        return torch.cuda.Stream(device=device)
-    idx = device.index if device.index is not None else torch.cuda.current_device()
-    key = (idx, n)
-    st = _UPDATE_STREAMS.get(key)
-    if st is None:
-        from ..ops import _ext
-        stride = int(os.environ.get("SFTAMD_ADAMW_CU_STRIDE", "1") or 1)
-        with torch.cuda.device(idx):
-            handle = _ext.ops().cu_masked_stream(n, stride, 0)
-        st = _UPDATE_STREAMS[key] = torch.cuda.ExternalStream(handle, device=torch.device("cuda", idx))
-    return st
+    """Side stream of the overlapped optimizer update (restricting it to a few CUs with a CU-masked stream measured
+    neutral to negative, profiles/r2_gemm_pingpong.md)."""
+    return torch.cuda.Stream(device=device)
 
 
 def _state_dtype(state_dtype, engine, master_weights: bool = False) -> torch.dtype:

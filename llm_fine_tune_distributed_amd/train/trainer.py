@@ -332,30 +332,8 @@ class SFTTrainer:
 
     def optimizer_step(self, micro: List[Dict], lr: float) -> Dict[str, torch.Tensor]:
         """One optimizer step over ``micro`` (GA micro-batches). Returns device-side sums:
-        loss (this rank's share of the global mean), correct, entropy_sum, valid tokens.
-
-        SFTAMD_COMPUTE_PRIO=1: the step's forward / backward run on a HIGH-priority HIP stream, so the overlapped
-        optimizer update (a normal-priority side stream) only gets the workgroup slots the compute kernels leave
-        free (GEMM tail rounds, small kernels) instead of competing for every CU. The caller's stream is ordered
-        before and after the step, so callers see the same stream semantics either way."""
-        hp = self._compute_stream()
-        if hp is None:
-            return self._optimizer_step(micro, lr)
-        cur = torch.cuda.current_stream(self.dist.device)
-        hp.wait_stream(cur)
-        with torch.cuda.stream(hp):
-            r = self._optimizer_step(micro, lr)
-        cur.wait_stream(hp)
-        return r
-
-    def _compute_stream(self):
-        if self.dist.device.type != "cuda" or os.environ.get("SFTAMD_COMPUTE_PRIO", "0") != "1":
-            return None
-        st = getattr(self, "_hp_stream", None)
-        if st is None:
-            lo, hi = torch.cuda.Stream.priority_range()
-            st = self._hp_stream = torch.cuda.Stream(device=self.dist.device, priority=min(lo, hi))
-        return st
+        loss (this rank's share of the global mean), correct, entropy_sum, valid tokens."""
+        return self._optimizer_step(micro, lr)
 
     def _optimizer_step(self, micro: List[Dict], lr: float) -> Dict[str, torch.Tensor]:
         model, eng = self.model, self.engine
