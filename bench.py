@@ -64,7 +64,7 @@ def parse(argv=None):
                     help="run the GA micro-batches of a step as one pass up to this many tokens (SFTConfig default "
                          "32768); 0 = one fwd/bwd pass per micro-batch")
     ap.add_argument("--seq", type=int, default=512)
-    ap.add_argument("--bucket-mb", type=float, default=float(os.environ.get("SFTAMD_BUCKET_MB", "0")),
+    ap.add_argument("--bucket-mb", type=float, default=0.0,
                     help="gradient bucket cap in MB; 0 (default) = the xGMI plan of parallel.ddp.plan_bucket_mb")
     ap.add_argument("--packing", action="store_true")
     ap.add_argument("--padding-free", choices=["auto", "on", "off"], default="auto",
@@ -80,7 +80,7 @@ def parse(argv=None):
                          "per rank, all-gather params under the next forward); 0: replicated all-reduce DDP")
     ap.add_argument("--tunableop", default="auto",
                     help="auto: load the committed GEMM selections; tune: tune missing shapes into it; off")
-    ap.add_argument("--baseline-1gpu", type=float, default=float(os.environ.get("SFTAMD_BENCH_1GPU", "0")),
+    ap.add_argument("--baseline-1gpu", type=float, default=0.0,
                     help="1-GPU samples/s of the same config: adds scaling_efficiency = value / (N * this)")
     ap.add_argument("--profile-steps", type=int, default=0)
     # --recipe: the reference recipe end to end instead of the synthetic step loop: its own parquet
@@ -94,12 +94,15 @@ def parse(argv=None):
                     help="--recipe: per-device eval batch (eval loss is token-weighted, independent of it)")
     # hang protection for the first RCCL multi-rank runs (utils/heartbeat.py, launch.py): a wall-clock bound on the
     # whole run, a no-progress bound per rank (also the process group's collective timeout), and RCCL INFO capture
-    # (default at N > 1 on GPUs, SFTAMD_BENCH_RCCL_INFO=0 to opt out) whose channel / transport / rank-count summary
-    # lands in the JSON line's ``dist``
-    ap.add_argument("--timeout-s", type=float, default=float(os.environ.get("SFTAMD_BENCH_TIMEOUT_S", "900")),
+    # (default at N > 1 on GPUs, --no-rccl-info to opt out) whose channel / transport / rank-count summary lands in the
+    # JSON line's ``dist``
+    ap.add_argument("--timeout-s", type=float, default=900.0,
                     help="wall-clock limit of the whole run; on expiry every rank prints its last heartbeat and exits 124")
-    ap.add_argument("--hang-timeout-s", type=float, default=float(os.environ.get("SFTAMD_BENCH_HANG_S", "300")),
+    ap.add_argument("--hang-timeout-s", type=float, default=300.0,
                     help="seconds without progress (no heartbeat) before a rank is declared hung")
+    ap.add_argument("--no-rccl-info", action="store_true", help="N > 1: do not capture RCCL's INFO log")
+    ap.add_argument("--rccl-log-dir", default="/tmp/sftamd_rccl")
+    ap.add_argument("--no-comm-probe", action="store_true", help="N > 1: skip the post-warmup collective probe")
     return ap.parse_args(argv)
 
 
@@ -166,12 +169,11 @@ def run(a):
     os.environ.setdefault("SFTAMD_HANG_TIMEOUT_S", str(a.hang_timeout_s))
     os.environ.setdefault("SFTAMD_RUN_DEADLINE_S", str(a.timeout_s))
     rccl_dir = None
-    # N > 1: RCCL's INFO log is captured by default (SFTAMD_BENCH_RCCL_INFO=0 opts out), so the first multi-GPU record
-    # says which transport / how many channels each rank's communicator got and how many ranks RCCL saw
-    if (os.environ.get("SFTAMD_BENCH_RCCL_INFO", "1") == "1" and int(os.environ.get("WORLD_SIZE", "1")) > 1
-            and a.device != "cpu"):
+    # N > 1: RCCL's INFO log is captured by default (--no-rccl-info opts out), so the first multi-GPU record says which
+    # transport / how many channels each rank's communicator got and how many ranks RCCL saw
+    if not a.no_rccl_info and int(os.environ.get("WORLD_SIZE", "1")) > 1 and a.device != "cpu":
         from llm_fine_tune_distributed_amd.parallel import rccl_info
-        rccl_dir = os.environ.get("SFTAMD_RCCL_LOG_DIR", "/tmp/sftamd_rccl")
+        rccl_dir = a.rccl_log_dir
         rccl_info.enable(rccl_dir)
     import torch
     import torch.distributed as dist
@@ -233,7 +235,7 @@ def run(a):
     sync()
     beat(None, "warmup_done")
     probe = None
-    if st.world_size > 1 and os.environ.get("SFTAMD_BENCH_COMM_PROBE", "1") == "1":
+    if st.world_size > 1 and not a.no_comm_probe:
         probe = comm_probe(st.device, st.world_size, int(trainer.engine.bucket_cap_mb * 2 ** 20))
     barrier()
     sync()

@@ -11,7 +11,7 @@
 // through v_accvgpr_read / write or spilling (the forward kernel's experience, csrc/gemm_tn.hip cfg 12 and
 // profiles/r3_gemm_4wave.md). Why 4 waves: a 128 x 128 wave tile reads 16 fragments per 64 MFMAs instead of the 12
 // per 32 of the 8-wave 128 x 64 tiles of gemm_wgrad.hip / gemm_dgrad.hip — a third fewer LDS bytes per FLOP — and
-// one wave per SIMD leaves the matrix pipe to a single in-order instruction stream (MI355X_MICROARCH.md "Two waves
+// one wave per SIMD leaves the matrix pipe to a single in-order instruction stream (/opt/skills/guides/MI355X_MICROARCH.md "Two waves
 // per SIMD", item 1). The 8-wave weight-gradient rings ran at 48-56 % MFMA busy inside the training step
 // (profiles/r2_step_pmc.md).
 //

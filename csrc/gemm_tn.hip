@@ -32,7 +32,7 @@ static int group_m() { return 8; }  // GROUP_M tile order: 8 row blocks share ea
 
 enum { EPI_PLAIN = 0, EPI_SWIGLU = 1, EPI_ROPE = 2 };
 
-// ds_read_b128 is serviced in four NON-contiguous 16-lane groups (MI355X_MICROARCH.md §LDS:
+// ds_read_b128 is serviced in four NON-contiguous 16-lane groups (/opt/skills/guides/MI355X_MICROARCH.md §LDS:
 // {0-3,12-15,20-27}, {4-11,16-19,28-31}, ...). A fragment read has lane (g = lane>>4, ii = lane&15) at
 // image row R + ii, chunk g: its 16-B slot in the 256-B bank row is 4 (ii & 3) + (g ^ S(ii >> 2)).
 // S = {0, 2, 3, 1} makes the 16 slots of every group distinct (the plain S(q) = q is 2-way).
@@ -686,12 +686,12 @@ __global__ void __launch_bounds__(WM * WN * 64) tn2_kernel(const u16* __restrict
 }
 
 // ============================================================================================
-// Ping-pong 8-phase schedule (cfg 8 / 9), cdna_hip_programming.md §5 "The 256² 8-phase template".
+// Ping-pong 8-phase schedule (cfg 8 / 9), /opt/skills/guides/cdna_hip_programming.md §5 "The 256² 8-phase template".
 // Same tile (256 x 256, BK = 64, 8 waves of 128 x 64) and the same two 64 KB LDS stages as the BK = 64
 // ring above, but each K-tile runs as FOUR phases, one output quadrant (64 x 32 per wave, 16 MFMAs)
 // each, and the two wave rows run ONE BARRIER APART: while wave row 0 is in a phase's MFMA segment,
 // wave row 1 (its partner on the same SIMD) issues the next phase's LDS reads and DMA, and vice versa
-// — matrix beside memory on every SIMD (MI355X_MICROARCH.md §Two waves per SIMD). Every phase is
+// — matrix beside memory on every SIMD (/opt/skills/guides/MI355X_MICROARCH.md §Two waves per SIMD). Every phase is
 //   [L: ds_reads of this phase's fragments | DMA of one class of tile t + 2 | counted vmcnt]
 //   lgkmcnt(0); s_barrier; setprio 1; 16 MFMA; setprio 0; s_barrier
 // The stage is laid out in four 16 KB CLASS images, one per group of fragments read together:
@@ -782,7 +782,7 @@ __device__ __forceinline__ void pp_read_b(const char* img, int offB0, int offB1,
 
 // End of a phase's load segment, then its MFMA segment. D = 1: lgkmcnt(0) before the first barrier
 // (a class may be refilled ONE phase after it is read); D = 2: lgkmcnt(0) after it (refilled two
-// phases after: cdna_hip_programming.md §5, "Read a staged buffer ... WAR").
+// phases after: /opt/skills/guides/cdna_hip_programming.md §5, "Read a staged buffer ... WAR").
 template <int D, bool TRC, int I0, int J0>
 __device__ __forceinline__ void pp_phase(f32x4 (&acc)[8][4], const bf16x8 (&fa)[4][2], const bf16x8 (&fb)[2][2]) {
   if (D == 1) lgkm0();
@@ -932,12 +932,12 @@ __global__ void __launch_bounds__(512) tn3_kernel(const u16* __restrict__ A, con
 // 4-wave 128 x 128 wave tiles (cfg 12): ONE wave per SIMD, 256 fp32 accumulators in the AGPR file.
 // Why: at 8 waves of 128 x 64 every 32 MFMAs of a wave need 12 fragment reads (8 A + 4 B); a 128 x 128
 // wave tile needs 16 per 64 MFMAs — a third fewer LDS read bytes per FLOP, which is what the chip's clock
-// under load responds to (MI355X_MICROARCH.md 'DVFS give-back'; hipBLASLt's 4-wave kernel holds ~2.17 GHz
+// under load responds to (/opt/skills/guides/MI355X_MICROARCH.md 'DVFS give-back'; hipBLASLt's 4-wave kernel holds ~2.17 GHz
 // vs ~1.94 for the 8-wave ping-pong on gate_up, profiles/r2_gemm_pingpong.md). hipcc cannot allocate
 // 256 accumulators next to double-buffered fragments when they are builtin MFMA values (it renames and
 // shuffles them through v_accvgpr_read/write, or spills: profiles/r1_gemm_tn.md); the MFMAs are therefore
 // inline asm with the accumulator TIED in an AGPR ("+a"), which pins every accumulator in place.
-// Hazards hipcc does not see for those asm MFMAs (cdna_hip_programming.md §5.7): fragment operands come
+// Hazards hipcc does not see for those asm MFMAs (/opt/skills/guides/cdna_hip_programming.md §5.7): fragment operands come
 // only from ds_read (retired by the explicit lgkmcnt(0) at every sub-step boundary, no VALU writer), and
 // the accumulators are read only after the loop, behind 20 wait states + a scheduling fence.
 // Schedule per 64-deep K-tile t (stage X = t, Y = t + 1, 64 KB each, 128-byte image rows, swz2):

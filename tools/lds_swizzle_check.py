@@ -1,5 +1,5 @@
 """Exhaustive LDS bank-conflict check of the swizzles used by the HIP kernels, against the MI355X
-lane groups of MI355X_MICROARCH.md §LDS (ds_read_b128: four non-contiguous 16-lane groups;
+lane groups of /opt/skills/guides/MI355X_MICROARCH.md §LDS (ds_read_b128: four non-contiguous 16-lane groups;
 ds_read_b64 / ds_read_b64_tr_b16: two 32-lane halves; 64 x 4-byte banks = one 256-byte bank row).
 
     python tools/lds_swizzle_check.py
