@@ -302,6 +302,227 @@ __device__ __forceinline__ void fwd_step_dma(const char* __restrict__ cur, char*
   }
 }
 
+// ============================================================================== fwd32: 32x32x16 forward
+// v_mfma_f32_32x32x16_bf16 lane maps (hi = lane >> 5, c = lane & 31, j = 0..7, i = 0..15):
+//   A[row c][k 8hi+j], B[k 8hi+j][col c], C[row crow(i, hi)][col c], crow(i, hi) = (i & 3) + 8 (i >> 2) + 4 hi.
+// S^T = K Q^T with the query on the lane: lane (hi, c) holds 16 keys of each 32-key block for query c, so the row max
+// and sum are lane-local plus ONE permlane32 swap, and the accumulator registers 8 sub .. 8 sub + 7 of block kb are
+// already the B operand (P^T) of k-step 2 kb + sub of O^T += V^T P^T: they hold keys 16 ks + 4 hi + {0..3} and
+// 16 ks + 8 + 4 hi + {0..3}, so the V^T A operand is read with that key order (two ds_read_b64_tr_b16, rows
+// 16 ks + 4 hi + q and 16 ks + 8 + 4 hi + q). Per 64-key tile and 32 queries: 16 + 16 MFMAs (each 2x the work of a
+// 16x16x32), 16 ds_read_b128 + 32 ds_read_b64_tr_b16 — half fwd3's LDS bytes per FLOP.
+// A workgroup = 4 waves = HW query heads of one kv head x (4 / HW) 32-query position blocks (HW = gcd(rep, 4)): at
+// GQA rep 4 the four waves share their positions, so the key range, the K / V tiles and the causal work are the same
+// for every wave and a 32-key half tile past the diagonal is skipped by all of them.
+typedef __attribute__((ext_vector_type(16))) float f32x16;
+
+__device__ __forceinline__ f32x16 mfma32(const bf16x8& a, const bf16x8& b, const f32x16& c) {
+  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
+}
+
+struct Offs32 {
+  int k[8];  // K row reads (A of S^T), k-step s: image row c, chunk 2 s + hi
+  int v[8];  // V^T transposed reads, [2 db + part]: rows 8 part + 4 hi + q, columns 32 db + 16 (a & 1) + 4 p ..
+  __device__ __forceinline__ void init(int lane) {
+    const int c = lane & 31, hi = lane >> 5, a = lane >> 4, q = (lane & 15) >> 2, p = lane & 3;
+#pragma unroll
+    for (int s = 0; s < 8; ++s) k[s] = img_off(c, 2 * s + hi);
+#pragma unroll
+    for (int db = 0; db < 4; ++db)
+#pragma unroll
+      for (int part = 0; part < 2; ++part)
+        v[2 * db + part] = img_off(8 * part + 4 * hi + q, 4 * db + 2 * (a & 1) + (p >> 1)) + 8 * (p & 1);
+  }
+};
+
+__device__ __forceinline__ bf16x8 lds_tr2(const char* base, int lo, int hi) {
+  typedef __attribute__((address_space(3))) s16x4 lds_s4;
+  s16x4 a = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4*)(base + lo));
+  s16x4 b = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4*)(base + hi));
+  typedef __attribute__((ext_vector_type(8))) short s16x8;
+  s16x8 v = {a[0], a[1], a[2], a[3], b[0], b[1], b[2], b[3]};
+  return __builtin_bit_cast(bf16x8, v);
+}
+
+__device__ __forceinline__ bf16x8 pack8(const f32x16& t, int base) {
+  bf16x8 r;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) r[j] = (__bf16)t[base + j];
+  return r;
+}
+
+__device__ __forceinline__ float swap32max(float x) {
+  auto a = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+  return fmaxf(__uint_as_float(a[0]), __uint_as_float(a[1]));
+}
+__device__ __forceinline__ float swap32sum(float x) {
+  auto a = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+  return __uint_as_float(a[0]) + __uint_as_float(a[1]);
+}
+
+// T21 epilogue of a 32x32 accumulator row: lane (hi, c) holds columns 32 db + 8 m + 4 hi + {0..3} (registers
+// 4 m .. 4 m + 3 of block db) of row c; one permlane32 swap per dword pair (m = 2u, 2u + 1) gives each half 8
+// consecutive columns -> 8 x 16-B stores per lane. row: the row's first column; every lane must call (the swaps).
+__device__ __forceinline__ void store_t21(u16* row, const f32x16 (&a)[4], float s, bool ok) {
+  const int hi = (threadIdx.x >> 5) & 1;
+#pragma unroll
+  for (int db = 0; db < 4; ++db)
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int i0 = 8 * u;
+      const unsigned ax = (unsigned)f2bf(a[db][i0] * s) | ((unsigned)f2bf(a[db][i0 + 1] * s) << 16);
+      const unsigned ay = (unsigned)f2bf(a[db][i0 + 2] * s) | ((unsigned)f2bf(a[db][i0 + 3] * s) << 16);
+      const unsigned bx = (unsigned)f2bf(a[db][i0 + 4] * s) | ((unsigned)f2bf(a[db][i0 + 5] * s) << 16);
+      const unsigned by = (unsigned)f2bf(a[db][i0 + 6] * s) | ((unsigned)f2bf(a[db][i0 + 7] * s) << 16);
+      const auto rx = __builtin_amdgcn_permlane32_swap(ax, bx, false, false);
+      const auto ry = __builtin_amdgcn_permlane32_swap(ay, by, false, false);
+      if (ok) *(uint4*)(row + 32 * db + 16 * u + 8 * hi) = make_uint4(rx[0], ry[0], rx[1], ry[1]);
+    }
+}
+
+// One 64-key tile: issue the next tile's K / V pieces into nxt (4 x 1 KB per image per wave, source-swizzled, rows
+// past the sequence end clamped: their keys are masked), then S^T, the online softmax and O^T += V^T P^T from cur.
+// lastkey: the wave's last visible key (causal: its last query); rel: this lane's last visible key - k0 - 4 hi.
+__device__ __forceinline__ void fwd32_step(const char* __restrict__ cur, char* __restrict__ nxt, bool pre,
+                                           const u16* kbase, const u16* vbase, long ld, long kvoff, int r0, int wave,
+                                           int k0, int len, int lastkey, bool need_mask, int rel, float sl2,
+                                           const Offs32& off, const bf16x8 (&qf)[8], f32x16 (&o)[4], float& m,
+                                           float& l) {
+  constexpr int TB = 64 * ROWB;
+  if (pre) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const long row = min(k0 + 64 + r0 + 16 * j, len - 1);
+      lds_dma16(kbase + row * ld + kvoff, nxt + (wave + 4 * j) * 1024);
+      lds_dma16(vbase + row * ld + kvoff, nxt + TB + (wave + 4 * j) * 1024);
+    }
+  }
+  if (k0 > lastkey) return;
+  const bool two = k0 + 32 <= lastkey;  // wave-uniform: the second 32-key half has a visible key
+  const char* Ks = cur;
+  const char* Vs = cur + TB;
+  f32x16 s[2];
+#pragma unroll
+  for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+    for (int i = 0; i < 16; ++i) s[kb][i] = 0.f;
+#pragma unroll
+  for (int st = 0; st < 8; ++st) s[0] = mfma32(lds_row(Ks, off.k[st]), qf[st], s[0]);
+  if (two) {
+#pragma unroll
+    for (int st = 0; st < 8; ++st) s[1] = mfma32(lds_row(Ks, off.k[st] + 32 * ROWB), qf[st], s[1]);
+  }
+  if (need_mask || !two) {
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+      for (int i = 0; i < 16; ++i)
+        s[kb][i] = 32 * kb + (i & 3) + 8 * (i >> 2) > rel ? -INFINITY : s[kb][i];
+  }
+  float mx = max3f(s[0][0], s[0][1], s[0][2]);
+#pragma unroll
+  for (int i = 3; i < 15; i += 2) mx = max3f(mx, s[0][i], s[0][i + 1]);
+  mx = max3f(mx, s[0][15], s[1][0]);
+#pragma unroll
+  for (int i = 1; i < 15; i += 2) mx = max3f(mx, s[1][i], s[1][i + 1]);
+  mx = fmaxf(mx, s[1][15]);
+  const float tmax = swap32max(mx) * sl2;
+  if (__any(tmax > m + THR)) {  // deferred rescale (T13): P stays <= 2^THR
+    const float mnew = fmaxf(m, tmax);
+    const float alpha = exp2f(m - mnew);
+    l *= alpha;
+#pragma unroll
+    for (int db = 0; db < 4; ++db) o[db] *= alpha;
+    m = mnew;
+  }
+  float acc0 = 0.f, acc1 = 0.f;
+#pragma unroll
+  for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+    for (int i = 0; i < 16; i += 2) {
+      const float p0 = exp2f(__builtin_fmaf(s[kb][i], sl2, -m));
+      const float p1 = exp2f(__builtin_fmaf(s[kb][i + 1], sl2, -m));
+      s[kb][i] = p0;
+      s[kb][i + 1] = p1;
+      acc0 += p0;
+      acc1 += p1;
+    }
+  l += acc0 + acc1;
+#pragma unroll
+  for (int ks = 0; ks < 4; ++ks) {
+    if (ks >= 2 && !two) break;
+    const bf16x8 pb = pack8(s[ks >> 1], 8 * (ks & 1));
+#pragma unroll
+    for (int db = 0; db < 4; ++db)
+      o[db] = mfma32(lds_tr2(Vs, off.v[2 * db] + 16 * ks * ROWB, off.v[2 * db + 1] + 16 * ks * ROWB), pb, o[db]);
+  }
+}
+
+// grid (nq / HW, sequences, position blocks of 32 (4 / HW)) with the last (causally heaviest) block first; 256 threads
+template <int HW>
+__global__ __launch_bounds__(256, 2) void fwd32_kernel(const u16* __restrict__ qkv, u16* __restrict__ out,
+                                                       float* __restrict__ lse, const int* __restrict__ cu, int nq,
+                                                       int nkv, int total, float sl2, int causal) {
+  constexpr int PB = 4 / HW, TB = 64 * ROWB;
+  __shared__ __attribute__((aligned(16))) char smem[4 * TB];
+  const int b = blockIdx.y, qb = gridDim.z - 1 - blockIdx.z;
+  const int start = cu[b], len = cu[b + 1] - start;
+  SFT_DASSERT(start >= 0 && len >= 0 && start + len <= total);
+  const int q0 = qb * 32 * PB;
+  if (q0 >= len) return;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, hi = lane >> 5;
+  const int h = blockIdx.x * HW + wave % HW;
+  const int kvh = (blockIdx.x * HW) / (nq / nkv);
+  const long ld = (long)(nq + 2 * nkv) * D;
+  const int wq0 = q0 + 32 * (wave / HW);
+  const int qi = wq0 + (lane & 31);
+  const bool qok = qi < len;
+  const u16* kbase = qkv + (long)start * ld + (nq + kvh) * D;
+  const u16* vbase = qkv + (long)start * ld + (nq + nkv + kvh) * D;
+  const int nkb = (len + 63) / 64;
+  const int nkt = causal ? min((min(q0 + 32 * PB, len) - 1) / 64 + 1, nkb) : nkb;
+  const int lastkey = causal ? min(wq0 + 31, len - 1) : len - 1;
+  const int lim = causal ? min(len - 1, qi) : len - 1;
+  Offs32 off;
+  off.init(lane);
+  bf16x8 qf[8];
+  {
+    const u16* qp = qkv + (long)(start + qi) * ld + h * D + 8 * hi;
+#pragma unroll
+    for (int st = 0; st < 8; ++st) qf[st] = load_frag_global(qp + 16 * st, qok);
+  }
+  // DMA: lane (wave w, l) fills LDS rows 4 (w + 4 j) + (l >> 4), position l & 15, with the chunk swz(row, l & 15)
+  const int r0 = 4 * wave + (lane >> 4);
+  const long kvoff = 8 * swz(r0, lane & 15);
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const long row = min(r0 + 16 * j, len - 1);
+    lds_dma16(kbase + row * ld + kvoff, smem + (wave + 4 * j) * 1024);
+    lds_dma16(vbase + row * ld + kvoff, smem + TB + (wave + 4 * j) * 1024);
+  }
+  vm_drain();
+  f32x16 o[4];
+#pragma unroll
+  for (int db = 0; db < 4; ++db)
+#pragma unroll
+    for (int i = 0; i < 16; ++i) o[db][i] = 0.f;
+  float m = -1e30f, l = 0.f;  // l: this lane's partial row sum (its 16 keys of each 32-key block)
+  __syncthreads();
+  for (int kt = 0; kt < nkt; ++kt) {
+    const int k0 = kt * 64;
+    const bool pre = kt + 1 < nkt;
+    const bool need_mask = (k0 + 64 > len) || (causal && k0 + 63 > wq0);
+    fwd32_step(smem + (kt & 1) * 2 * TB, smem + ((kt + 1) & 1) * 2 * TB, pre, kbase, vbase, ld, kvoff, r0, wave, k0,
+               len, lastkey, need_mask, lim - k0 - 4 * hi, sl2, off, qf, o, m, l);
+    if (pre) vm_drain();
+    __syncthreads();
+  }
+  l = swap32sum(l);
+  const float inv = 1.f / l;
+  store_t21(out + (long)(start + qi) * nq * D + h * D, o, inv, qok);
+  if (qok && hi == 0) lse[(long)h * total + start + qi] = (m + log2f(l)) * LN2;
+}
+
 // DIAG (timing-only ablations, wrong results): bit0 no next-tile loads/stores, bit1 no softmax math,
 // bit2 no PV MFMAs, bit3 no QK MFMAs. bit4 (results exact): the round-2 schedule for A/B runs (no vm_drain before
 // the loop, per-tile row-sum shuffles through ds_bpermute). bit5: K / V tiles by LDS-DMA into two stages (no VGPR
@@ -771,6 +992,337 @@ __global__ __launch_bounds__(NW * 64) void bwd_dq3_kernel(const u16* __restrict_
 // That halves the serial chain of the causally heaviest key block (block 0 walks rep x nqt tiles), which is what
 // bounds this kernel: at 16 x 512 tokens the MFMA work alone is ~18 us, one tile step ~3 us of latency.
 // blockIdx.z = key block, heaviest first.
+// ============================================================================== dQ with 32x32x16 MFMAs
+// dQ^T = K^T dS^T over the key tiles of the materialised dS^T (written by bwd_dkdv32): the query on the lane, so the
+// accumulator is the forward's O^T layout (T21 stores). A workgroup = 4 waves = HW query heads of one kv head x
+// (4 / HW) 32-query position blocks (as fwd32): the K tile is shared, each wave stages its own [64 keys][32 queries]
+// dS^T block (64-B rows: a transposed read's four rows x 64 B of a 32-lane half cover the 64 banks once, no swizzle).
+// Rows past the sequence end are zero-filled (the dS^T rows there were never written). Per tile and wave: 16 MFMAs,
+// 32 + 8 ds_read_b64_tr_b16.
+__device__ __forceinline__ void rope_bwd32(f32x16 (&a)[4], const float* cs, const float* sn, float s) {
+  const int hi = (threadIdx.x >> 5) & 1;
+#pragma unroll
+  for (int d4 = 0; d4 < 2; ++d4)
+#pragma unroll
+    for (int m = 0; m < 4; ++m) {
+      const int d = 32 * d4 + 8 * m + 4 * hi;
+      const float4 c4 = *(const float4*)(cs + d), s4 = *(const float4*)(sn + d);
+      const float c[4] = {c4.x, c4.y, c4.z, c4.w}, n[4] = {s4.x, s4.y, s4.z, s4.w};
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        const int i = 4 * m + t;
+        const float x = a[d4][i] * s, y = a[d4 + 2][i] * s;
+        a[d4][i] = x * c[t] + y * n[t];
+        a[d4 + 2][i] = y * c[t] - x * n[t];
+      }
+    }
+}
+
+__device__ __forceinline__ void dq32_step(const char* __restrict__ cur, char* __restrict__ nxt, bool pre, bool active,
+                                          const u16* kbase, const u16* sbase, long ld, long lp, int k0n, int len,
+                                          long kvoff, int r0, int wave, int lane, const Offs32& off, int sofs,
+                                          f32x16 (&dq)[4]) {
+  constexpr int TB = 64 * ROWB, SB = 64 * 64;  // K image, per-wave dS^T block
+  if (pre) {  // the next tile (keys k0n ..): K pieces wave + 4 j, this wave's dS^T pieces j (rows 16 j + lane / 4)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int kr = k0n + r0 + 16 * j;
+      char* kd = nxt + (wave + 4 * j) * 1024;
+      if (kr < len) lds_dma16(kbase + kr * ld + kvoff, kd);
+      else *(uint4*)(kd + 16 * lane) = make_uint4(0, 0, 0, 0);
+      const int sr = k0n + 16 * j + (lane >> 2);
+      char* sd = nxt + TB + wave * SB + j * 1024;
+      if (sr < len) lds_dma16(sbase + sr * lp + 8 * (lane & 3), sd);
+      else *(uint4*)(sd + 16 * lane) = make_uint4(0, 0, 0, 0);
+    }
+  }
+  if (!active) return;
+  const char* Ks = cur;
+  const char* Ss = cur + TB + wave * SB;
+#pragma unroll
+  for (int ks = 0; ks < 4; ++ks) {
+    const bf16x8 sb = lds_tr2(Ss, sofs + ks * 16 * 64, sofs + ks * 16 * 64 + 8 * 64);
+#pragma unroll
+    for (int d4 = 0; d4 < 4; ++d4)
+      dq[d4] = mfma32(lds_tr2(Ks, off.v[2 * d4] + ks * 16 * ROWB, off.v[2 * d4 + 1] + ks * 16 * ROWB), sb, dq[d4]);
+  }
+}
+
+template <int HW>
+__global__ __launch_bounds__(256, 2) void bwd_dq32_kernel(const u16* __restrict__ qkv, const u16* __restrict__ dst,
+                                                          const int* __restrict__ cu, u16* __restrict__ dqkv, int nq,
+                                                          int nkv, int lp, float scale, int causal,
+                                                          const float* __restrict__ rcos,
+                                                          const float* __restrict__ rsin) {
+  constexpr int PB = 4 / HW, TB = 64 * ROWB, SB = 64 * 64, STG = TB + 4 * SB;
+  __shared__ __attribute__((aligned(16))) char smem[2 * STG];
+  const int b = blockIdx.y, qb = gridDim.z - 1 - blockIdx.z;
+  const int start = cu[b], len = cu[b + 1] - start;
+  const int q0 = qb * 32 * PB;
+  if (q0 >= len) return;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, hi = lane >> 5;
+  const int h = blockIdx.x * HW + wave % HW;
+  const int kvh = (blockIdx.x * HW) / (nq / nkv);
+  const long ld = (long)(nq + 2 * nkv) * D;
+  const int wq0 = q0 + 32 * (wave / HW);
+  const int qi = wq0 + (lane & 31);
+  SFT_DASSERT(wq0 + 32 <= lp);
+  const int lastq = min(wq0 + 31, len - 1);  // the wave's last query: keys past it are causally invisible
+  const u16* kbase = qkv + (long)start * ld + (nq + kvh) * D;
+  const u16* sbase = dst + (long)(b * nq + h) * lp * lp + wq0;
+  const int nkb = (len + 63) / 64;
+  const int nkt = causal ? min((min(q0 + 32 * PB, len) - 1) / 64 + 1, nkb) : nkb;
+  Offs32 off;
+  off.init(lane);
+  // this lane's dS^T transposed read: group a = lane >> 4 reads rows 4 hi + q (+ 8) of a 16-key step, columns
+  // 16 (a & 1) + 4 p .. + 3 (64-B rows)
+  const int sofs = (4 * hi + ((lane & 15) >> 2)) * 64 + 32 * ((lane >> 4) & 1) + 8 * (lane & 3);
+  const int r0 = 4 * wave + (lane >> 4);
+  const long kvoff = 8 * swz(r0, lane & 15);
+  f32x16 dq[4];
+#pragma unroll
+  for (int d4 = 0; d4 < 4; ++d4)
+#pragma unroll
+    for (int i = 0; i < 16; ++i) dq[d4][i] = 0.f;
+  dq32_step(smem + STG, smem, true, false, kbase, sbase, ld, lp, 0, len, kvoff, r0, wave, lane, off, sofs, dq);
+  vm_drain();
+  __syncthreads();
+  for (int kt = 0; kt < nkt; ++kt) {
+    const int k0 = kt * 64;
+    const bool pre = kt + 1 < nkt;
+    dq32_step(smem + (kt & 1) * STG, smem + ((kt + 1) & 1) * STG, pre, !causal || k0 <= lastq, kbase, sbase, ld, lp,
+              k0 + 64, len, kvoff, r0, wave, lane, off, sofs, dq);
+    if (pre) vm_drain();  // this lane's pieces of the next tile landed ...
+    __syncthreads();      // ... and every lane's (LDS zero stores too); every wave is done reading this stage
+  }
+  const bool qok = qi < len;
+  float s = scale;
+  if (rcos != nullptr && qok) {
+    const long tr = (long)(start + qi) * (D / 2);
+    rope_bwd32(dq, rcos + tr, rsin + tr, scale);
+    s = 1.f;
+  }
+  store_t21(dqkv + (long)(start + qi) * ld + h * D, dq, s, qok);
+}
+
+// ============================================================================== dK / dV with 32x32x16 MFMAs
+// S = Q K^T and dP = dO V^T with the KEY on the lane (the K / V fragments are loop-invariant B operands in registers):
+// lane (hi, c) holds S[q = crow(i, hi)][key c], so its accumulator registers 8 sub .. 8 sub + 7 are already the B
+// operand (k = query) of dV^T += dO^T P and dK^T += Q^T dS, whose A operands are transposed reads of the dO / Q
+// images (the forward's V^T read). P = exp2(S sl2 - lse log2 e) needs no row max; lse / delta of the tile's 64 queries
+// ride with the Q / dO images. A workgroup = 64 keys of one kv head = 2 key halves x G head groups (G = 2 when rep is
+// even; the groups' dK / dV are summed through LDS at the end), 64-query tiles of Q / dO by LDS-DMA in two stages per
+// group, one wave per SIMD (dK^T / dV^T: 128 fp32 accumulators per lane). Per tile and wave: 64 MFMAs (32 keys x 64
+// queries x 4 products), 32 ds_read_b128 + 64 ds_read_b64_tr_b16 — half dkdv5's LDS bytes per FLOP.
+// dS^T ([b][h][key][q], row stride lp) is written for bwd_dq4 when drow is given (T21-paired 16-B stores).
+__device__ __forceinline__ void dkdv32_step(const char* __restrict__ cur, char* __restrict__ nxt, bool pre,
+                                            const u16* qsrc, const u16* osrc, long ld, long ldo, int nrow0, int qlast,
+                                            long qoff0, long qoff1, int wv, const float* lsrc, const float* dsrc,
+                                            int gl, int q0, int len, int causal, int kw0, int key, float sl2,
+                                            u16* drow, bool dok, const Offs32& off, const bf16x8 (&kf)[8],
+                                            const bf16x8 (&vf)[8], f32x16 (&dk)[4], f32x16 (&dv)[4]) {
+  constexpr int TB = 64 * ROWB;
+  float pl = 0.f, pd = 0.f;
+  if (pre) {  // the next tile: image rows 4 (wv + 2 j) + (lane >> 4) = nrow0 + 8 j - first row
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const long row = min(nrow0 + 8 * j, qlast);
+      const long o = (j & 1) ? qoff1 : qoff0;
+      lds_dma16(qsrc + row * ld + o, nxt + (wv + 2 * j) * 1024);
+      lds_dma16(osrc + row * ldo + o, nxt + TB + (wv + 2 * j) * 1024);
+    }
+    if (gl < 64 && lsrc != nullptr) {
+      pl = lsrc[gl];
+      pd = dsrc[gl];
+    }
+  }
+  const char* Qs = cur;
+  const char* Os = cur + TB;
+  const float* Ls = (const float*)(cur + 2 * TB);
+  const float* Dl = Ls + 64;
+  const int hi = (threadIdx.x >> 5) & 1;
+#pragma unroll
+  for (int qb = 0; qb < 2; ++qb) {
+    f32x16 s, dp;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) s[i] = dp[i] = 0.f;
+#pragma unroll
+    for (int st = 0; st < 8; ++st) {
+      s = mfma32(lds_row(Qs, off.k[st] + qb * 32 * ROWB), kf[st], s);
+      dp = mfma32(lds_row(Os, off.k[st] + qb * 32 * ROWB), vf[st], dp);
+    }
+    // query q = q0 + 32 qb + 4 hi + o, o = 8 m + t for register 4 m + t; visible iff lo <= o <= hq
+    const int qbase = q0 + 32 * qb + 4 * hi;
+    const int lo = (causal ? key : 0) - qbase, hq = len - 1 - qbase;
+    const bool need_mask = (q0 + 32 * qb + 31 >= len) || (causal && kw0 + 31 > q0 + 32 * qb);
+#pragma unroll
+    for (int m = 0; m < 4; ++m) {
+      const float4 L4 = *(const float4*)(Ls + 32 * qb + 8 * m + 4 * hi);
+      const float4 D4 = *(const float4*)(Dl + 32 * qb + 8 * m + 4 * hi);
+      const float L[4] = {L4.x, L4.y, L4.z, L4.w}, Dd[4] = {D4.x, D4.y, D4.z, D4.w};
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        const int i = 4 * m + t, o = 8 * m + t;
+        float p = exp2f(__builtin_fmaf(s[i], sl2, -L[t]));
+        if (need_mask) p = (o < lo || o > hq) ? 0.f : p;
+        dp[i] = p * (dp[i] - Dd[t]);
+        s[i] = p;
+      }
+    }
+    if (drow != nullptr) {  // dS^T[key][q]: registers 8 u .. 8 u + 7 = queries 16 u + 4 hi + {0..3, 8..11}
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        const int i0 = 8 * u;
+        const unsigned ax = (unsigned)f2bf(dp[i0]) | ((unsigned)f2bf(dp[i0 + 1]) << 16);
+        const unsigned ay = (unsigned)f2bf(dp[i0 + 2]) | ((unsigned)f2bf(dp[i0 + 3]) << 16);
+        const unsigned bx = (unsigned)f2bf(dp[i0 + 4]) | ((unsigned)f2bf(dp[i0 + 5]) << 16);
+        const unsigned by = (unsigned)f2bf(dp[i0 + 6]) | ((unsigned)f2bf(dp[i0 + 7]) << 16);
+        const auto rx = __builtin_amdgcn_permlane32_swap(ax, bx, false, false);
+        const auto ry = __builtin_amdgcn_permlane32_swap(ay, by, false, false);
+        if (dok) *(uint4*)(drow + 32 * qb + 16 * u + 8 * hi) = make_uint4(rx[0], ry[0], rx[1], ry[1]);
+      }
+    }
+#pragma unroll
+    for (int sub = 0; sub < 2; ++sub) {
+      const bf16x8 pb = pack8(s, 8 * sub), db = pack8(dp, 8 * sub);
+      const int ko = (2 * qb + sub) * 16 * ROWB;
+#pragma unroll
+      for (int d4 = 0; d4 < 4; ++d4) {
+        dv[d4] = mfma32(lds_tr2(Os, off.v[2 * d4] + ko, off.v[2 * d4 + 1] + ko), pb, dv[d4]);
+        dk[d4] = mfma32(lds_tr2(Qs, off.v[2 * d4] + ko, off.v[2 * d4 + 1] + ko), db, dk[d4]);
+      }
+    }
+  }
+  if (pre && gl < 64) {  // the next stage's lse / delta (that stage's last reads ended at the previous barrier)
+    float* Ln = (float*)(nxt + 2 * TB);
+    asm volatile("" : "+v"(pl));  // keeps the multiply (and the loads' wait) after this tile's math
+    Ln[gl] = pl * LOG2E;
+    Ln[64 + gl] = pd;
+  }
+}
+
+template <int G>
+__global__ __launch_bounds__(128 * G, 1) void bwd_dkdv32_kernel(
+    const u16* __restrict__ qkv, const u16* __restrict__ dout, const float* __restrict__ lse,
+    const float* __restrict__ delta, const int* __restrict__ cu, u16* __restrict__ dqkv, int nq, int nkv, int total,
+    float sl2, float scale, int causal, u16* __restrict__ dst, int lp, const float* __restrict__ rcos,
+    const float* __restrict__ rsin) {
+  constexpr int TB = 64 * ROWB, GB = 2 * TB + 2 * 64 * 4;  // per stage: Q, dO images + lse, delta
+  __shared__ __attribute__((aligned(16))) char smem[G * 2 * GB];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, grp = w >> 1, kh = w & 1, gl = tid & 127;
+  const int hi = lane >> 5;
+  char* base = smem + grp * 2 * GB;
+  const int kvh = blockIdx.x, b = blockIdx.y, kb = blockIdx.z;  // z = 0 first: the causally heaviest key blocks
+  const int start = cu[b], len = cu[b + 1] - start;
+  SFT_DASSERT(start >= 0 && len >= 0 && start + len <= total);
+  const int k0 = kb * 64;
+  if (k0 >= len) return;
+  const int rep = nq / nkv, hpg = rep / G;
+  const long ld = (long)(nq + 2 * nkv) * D;
+  const long ldo = (long)nq * D;
+  const int kw0 = k0 + 32 * kh, key = kw0 + (lane & 31);
+  const bool kok = key < len;
+  const int qt0 = causal ? kb : 0, nqt = (len + 63) / 64, nt = nqt - qt0, niter = hpg * nt;
+  Offs32 off;
+  off.init(lane);
+  int h = kvh * rep + grp * hpg, qt = qt0;
+  // DMA: lane (wave kh, l) fills image rows 4 (kh + 2 j) + (l >> 4), position l & 15, with chunk swz(row, l & 15)
+  const int qr0 = 4 * kh + (lane >> 4);
+  const long qoff0 = 8 * swz(qr0, lane & 15), qoff1 = 8 * swz(qr0 + 8, lane & 15);
+  {
+    const int q0 = qt0 * 64, qv = len - q0;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const long row = start + min(q0 + qr0 + 8 * j, len - 1);
+      const long o = (j & 1) ? qoff1 : qoff0;
+      lds_dma16(qkv + row * ld + h * D + o, base + (kh + 2 * j) * 1024);
+      lds_dma16(dout + row * ldo + h * D + o, base + TB + (kh + 2 * j) * 1024);
+    }
+    if (gl < 64) {
+      float* Ls = (float*)(base + 2 * TB);
+      Ls[gl] = gl < qv ? lse[(long)h * total + start + q0 + gl] * LOG2E : 0.f;
+      Ls[64 + gl] = gl < qv ? delta[(long)h * total + start + q0 + gl] : 0.f;
+    }
+  }
+  bf16x8 kf[8], vf[8];
+  {
+    const u16* kp = qkv + (long)(start + key) * ld + (nq + kvh) * D + 8 * hi;
+    const u16* vp = qkv + (long)(start + key) * ld + (nq + nkv + kvh) * D + 8 * hi;
+#pragma unroll
+    for (int st = 0; st < 8; ++st) {
+      kf[st] = load_frag_global(kp + 16 * st, kok);
+      vf[st] = load_frag_global(vp + 16 * st, kok);
+    }
+  }
+  vm_drain();
+  f32x16 dk[4], dv[4];
+#pragma unroll
+  for (int d4 = 0; d4 < 4; ++d4)
+#pragma unroll
+    for (int i = 0; i < 16; ++i) dk[d4][i] = dv[d4][i] = 0.f;
+  __syncthreads();
+  for (int it = 0; it < niter; ++it) {
+    const int q0 = qt * 64;
+    const bool pre = it + 1 < niter;
+    int hn = h, qtn = qt + 1;
+    if (qtn == nqt) {
+      qtn = qt0;
+      ++hn;
+    }
+    const int qn = qtn * 64;
+    const long lo = (long)hn * total + start + qn;
+    const bool lok = pre && qn + gl < len;
+    u16* drow = dst != nullptr ? dst + ((long)(b * nq + h) * lp + key) * lp + q0 : nullptr;
+    dkdv32_step(base + (it & 1) * GB, base + ((it + 1) & 1) * GB, pre, qkv + (long)start * ld + hn * D,
+                dout + (long)start * ldo + hn * D, ld, ldo, qn + qr0, len - 1, qoff0, qoff1, kh,
+                lok ? lse + lo : nullptr, delta + lo, gl, q0, len, causal, kw0, key, sl2, drow, kok, off, kf, vf, dk,
+                dv);
+    if (pre) vm_drain();  // this lane's pieces of the next tile landed ...
+    __syncthreads();      // ... and every lane's; every wave is done reading this stage
+    h = hn;
+    qt = qtn;
+  }
+  if constexpr (G == 2) {  // group 1 hands its dK / dV partial sums to group 0 through the (now idle) stages
+    float4* xk = (float4*)smem;
+    float4* xv = xk + 2 * 16 * 64;
+    if (grp == 1) {
+#pragma unroll
+      for (int d4 = 0; d4 < 4; ++d4)
+#pragma unroll
+        for (int v = 0; v < 4; ++v) {
+          const int ix = (kh * 16 + 4 * d4 + v) * 64 + lane;
+          xk[ix] = make_float4(dk[d4][4 * v], dk[d4][4 * v + 1], dk[d4][4 * v + 2], dk[d4][4 * v + 3]);
+          xv[ix] = make_float4(dv[d4][4 * v], dv[d4][4 * v + 1], dv[d4][4 * v + 2], dv[d4][4 * v + 3]);
+        }
+    }
+    __syncthreads();
+    if (grp == 1) return;
+#pragma unroll
+    for (int d4 = 0; d4 < 4; ++d4)
+#pragma unroll
+      for (int v = 0; v < 4; ++v) {
+        const int ix = (kh * 16 + 4 * d4 + v) * 64 + lane;
+        const float4 a = xk[ix], c = xv[ix];
+        dk[d4][4 * v] += a.x;
+        dk[d4][4 * v + 1] += a.y;
+        dk[d4][4 * v + 2] += a.z;
+        dk[d4][4 * v + 3] += a.w;
+        dv[d4][4 * v] += c.x;
+        dv[d4][4 * v + 1] += c.y;
+        dv[d4][4 * v + 2] += c.z;
+        dv[d4][4 * v + 3] += c.w;
+      }
+  }
+  float ks = scale;
+  if (rcos != nullptr && kok) {  // inverse rotate_half RoPE on dK: columns d and d + 64 are blocks d4 and d4 + 2
+    const long tr = (long)(start + key) * (D / 2);
+    rope_bwd32(dk, rcos + tr, rsin + tr, scale);
+    ks = 1.f;
+  }
+  store_t21(dqkv + (long)(start + key) * ld + (nq + kvh) * D, dk, ks, kok);
+  store_t21(dqkv + (long)(start + key) * ld + (nq + nkv + kvh) * D, dv, 1.f, kok);
+}
+
 // One query tile of the LDS-DMA GQA dK/dV kernel (bwd_dkdv5_kernel<G, false, true>): issue the next tile's Q / dO
 // pieces (4 x 1 KB per image per wave, source-swizzled, rows past the sequence end clamped: their P and dS are masked
 // to 0) and its lse / delta loads, compute this tile from stage cur, then park lse (x LOG2E) / delta in stage nxt.
@@ -1113,6 +1665,16 @@ static void launch_dkdv5(const u16* qkv, const u16* dout, const float* lse, cons
                          const float* rsin = nullptr) {
   const int rep = nq / nkv;
   dim3 grid(nkv, nseq, (max_seqlen + 63) / 64);
+  const char* e5 = std::getenv("SFTAMD_ATTN_DKDV5");  // A/B against the 16x16x32 dkdv5 (read per call)
+  if (!(e5 && std::strcmp(e5, "1") == 0)) {
+    if (rep % 2 == 0)
+      bwd_dkdv32_kernel<2><<<grid, 256, 0, st>>>(qkv, dout, lse, delta, cu, dqkv, nq, nkv, total, sl2, scale, causal,
+                                                 dst, lp, rcos, rsin);
+    else
+      bwd_dkdv32_kernel<1><<<grid, 128, 0, st>>>(qkv, dout, lse, delta, cu, dqkv, nq, nkv, total, sl2, scale, causal,
+                                                 dst, lp, rcos, rsin);
+    return;
+  }
   if (rep % 2 == 0)
     bwd_dkdv5_kernel<2, false, true><<<grid, 512, 0, st>>>(qkv, dout, lse, delta, cu, dqkv, nq, nkv, total, sl2,
                                                            scale, causal, dst, lp, rcos, rsin);
@@ -1152,11 +1714,25 @@ std::tuple<at::Tensor, at::Tensor> flash_fwd(const at::Tensor& qkv, const at::Te
   if (total == 0 || max_seqlen == 0) return {out, lse};
   const float sl2 = (float)scale * attn::LOG2E;
   auto cu_c = cu.contiguous();
-  SFT_TRACE("attn.fwd3");
-  dim3 g3(nq, nseq, (max_seqlen + 127) / 128);
-  attn::fwd3_kernel<8, 32><<<g3, 512, 0, cur_stream()>>>((const u16*)qkv.data_ptr(), (u16*)out.data_ptr(),
-                                                         lse.data_ptr<float>(), cu_c.data_ptr<int>(), nq, nkv, total,
-                                                         sl2, causal ? 1 : 0);
+  const char* e16 = std::getenv("SFTAMD_ATTN_FWD16");  // A/B against the 16x16x32 fwd3 (read per call)
+  const bool use16 = e16 && std::strcmp(e16, "1") == 0;
+  const u16* q = (const u16*)qkv.data_ptr();
+  u16* o = (u16*)out.data_ptr();
+  float* lp = lse.data_ptr<float>();
+  const int* cp = cu_c.data_ptr<int>();
+  const int ca = causal ? 1 : 0;
+  if (use16) {
+    SFT_TRACE("attn.fwd3");
+    dim3 g3(nq, nseq, (max_seqlen + 127) / 128);
+    attn::fwd3_kernel<8, 32><<<g3, 512, 0, cur_stream()>>>(q, o, lp, cp, nq, nkv, total, sl2, ca);
+  } else {
+    SFT_TRACE("attn.fwd32");
+    const int rep = nq / nkv, hw = rep % 4 == 0 ? 4 : rep % 2 == 0 ? 2 : 1, span = 32 * (4 / hw);
+    dim3 g(nq / hw, nseq, (max_seqlen + span - 1) / span);
+    if (hw == 4) attn::fwd32_kernel<4><<<g, 256, 0, cur_stream()>>>(q, o, lp, cp, nq, nkv, total, sl2, ca);
+    else if (hw == 2) attn::fwd32_kernel<2><<<g, 256, 0, cur_stream()>>>(q, o, lp, cp, nq, nkv, total, sl2, ca);
+    else attn::fwd32_kernel<1><<<g, 256, 0, cur_stream()>>>(q, o, lp, cp, nq, nkv, total, sl2, ca);
+  }
   SFT_LAUNCH_CHECK();
   return {out, lse};
 }
@@ -1199,10 +1775,23 @@ static at::Tensor flash_bwd_impl(const at::Tensor& dout, const at::Tensor& qkv, 
                        (u16*)dqkv.data_ptr(), nq, nkv, total, nseq, max_seqlen, sl2, (float)scale, causal ? 1 : 0,
                        (u16*)dst.data_ptr(), (int)lp, cur_stream(), rcos, rsin);
     SFT_LAUNCH_CHECK();
-    dim3 gq4(nq, nseq, (max_seqlen + 127) / 128);
-    attn::bwd_dq4_kernel<8><<<gq4, 512, 0, cur_stream()>>>(q, (const u16*)dst.data_ptr(), cu_c.data_ptr<int>(),
-                                                           (u16*)dqkv.data_ptr(), nq, nkv, (int)lp, (float)scale,
-                                                           causal ? 1 : 0, rcos, rsin);
+    const char* e5 = std::getenv("SFTAMD_ATTN_DKDV5");  // A/B: the 16x16x32 dkdv5 + dq4 pair (read per call)
+    if (e5 && std::strcmp(e5, "1") == 0) {
+      dim3 gq4(nq, nseq, (max_seqlen + 127) / 128);
+      attn::bwd_dq4_kernel<8><<<gq4, 512, 0, cur_stream()>>>(q, (const u16*)dst.data_ptr(), cu_c.data_ptr<int>(),
+                                                             (u16*)dqkv.data_ptr(), nq, nkv, (int)lp, (float)scale,
+                                                             causal ? 1 : 0, rcos, rsin);
+    } else {
+      const int rep = nq / nkv, hw = rep % 4 == 0 ? 4 : rep % 2 == 0 ? 2 : 1, span = 32 * (4 / hw);
+      dim3 g(nq / hw, nseq, (max_seqlen + span - 1) / span);
+      const u16* ds = (const u16*)dst.data_ptr();
+      u16* dx = (u16*)dqkv.data_ptr();
+      const int* cp = cu_c.data_ptr<int>();
+      const int ca = causal ? 1 : 0;
+      if (hw == 4) attn::bwd_dq32_kernel<4><<<g, 256, 0, cur_stream()>>>(q, ds, cp, dx, nq, nkv, (int)lp, (float)scale, ca, rcos, rsin);
+      else if (hw == 2) attn::bwd_dq32_kernel<2><<<g, 256, 0, cur_stream()>>>(q, ds, cp, dx, nq, nkv, (int)lp, (float)scale, ca, rcos, rsin);
+      else attn::bwd_dq32_kernel<1><<<g, 256, 0, cur_stream()>>>(q, ds, cp, dx, nq, nkv, (int)lp, (float)scale, ca, rcos, rsin);
+    }
     SFT_LAUNCH_CHECK();
     rope_done = rope;
     return dqkv;

@@ -227,6 +227,36 @@ def test_flash_attention_varlen_gqa(causal, ds_mb):
     _attn_case([300, 17, 129], 4, 4, causal, ds_mb)
 
 
+@pytest.mark.parametrize("fwd16", ["", "1"])
+@pytest.mark.parametrize("causal", [True, False])
+def test_flash_fwd_out_and_lse(fwd16, causal):
+    """The 32x32x16 forward (fwd32: HW = gcd(rep, 4) heads per workgroup -> rep 4 / 8, 2 / 6, 1 / 3 paths) and the
+    16x16x32 fwd3 vs fp32 softmax(QK^T) V and logsumexp, on lengths off the 32 / 64 grids."""
+    torch.manual_seed(1)
+    D = 128
+    for lens, nq, nkv in (([512, 511, 7, 33], 16, 4), ([100, 255, 64, 1, 300, 129], 8, 2), ([200, 65], 12, 3),
+                          ([130, 64, 31], 12, 2), ([300, 17, 129], 4, 4), ([257, 96], 16, 2)):
+        cu = torch.tensor([0] + list(torch.tensor(lens).cumsum(0)), dtype=torch.int32, device=DEV)
+        M = int(cu[-1])
+        qkv = torch.randn(M, (nq + 2 * nkv) * D, device=DEV, dtype=torch.bfloat16)
+        scale = 1 / math.sqrt(D)
+        with _env(SFTAMD_ATTN_FWD16=fwd16):
+            out, lse = _ext.ops().flash_fwd(qkv, cu, max(lens), nq, nkv, D, scale, causal)
+        q32 = qkv.float()
+        o_ref = ref.attention(q32, nq, nkv, D, cu, scale, causal)
+        assert rel_err(out, o_ref) < 1e-2, (lens, nq, nkv, rel_err(out, o_ref))
+        rep = nq // nkv
+        for b in range(len(lens)):
+            s, e = int(cu[b]), int(cu[b + 1])
+            q = q32[s:e, :nq * D].view(e - s, nq, D).transpose(0, 1)
+            k = q32[s:e, nq * D:(nq + nkv) * D].view(e - s, nkv, D).transpose(0, 1).repeat_interleave(rep, 0)
+            sc = (q @ k.transpose(1, 2)) * scale
+            if causal:
+                sc = sc.masked_fill(torch.ones(e - s, e - s, device=DEV, dtype=torch.bool).triu(1), float("-inf"))
+            want = torch.logsumexp(sc, -1)
+            torch.testing.assert_close(lse[:, s:e], want, atol=2e-3, rtol=1e-3)
+
+
 def test_flash_attention_mha_and_long():
     _attn_case([1000, 37], 4, 4, True)
     _attn_case([2048, 5], 16, 4, True)
