@@ -237,6 +237,24 @@ __device__ __forceinline__ void lds_dma16(const u16* src, char* dst) {
                                    (void __attribute__((address_space(3)))*)dst, 16, 0, 0);
 }
 
+// Buffer-descriptor forms (the 32x32 kernels): the tile's base and byte range in a wave-uniform descriptor, the lane's
+// row / chunk in a loop-invariant VGPR offset, the tile's row offset in an SGPR. Rows past the sequence end fall
+// outside the range and read as ZERO (no clamps, no per-row branches, no 64-bit VALU address math per piece).
+typedef __amdgpu_buffer_rsrc_t rsrc_t;
+__device__ __forceinline__ rsrc_t make_rsrc(const void* p, long bytes) {
+  const unsigned long long a = (unsigned long long)p;
+  const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)a), hi = __builtin_amdgcn_readfirstlane((unsigned)(a >> 32));
+  const unsigned n = __builtin_amdgcn_readfirstlane((unsigned)(bytes < 0 ? 0 : bytes));
+  return __builtin_amdgcn_make_buffer_rsrc((void*)(((unsigned long long)hi << 32) | lo), 0, n, 0x00020000);
+}
+__device__ __forceinline__ void bdma16(rsrc_t r, char* dst, unsigned voff, unsigned soff) {
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (__attribute__((address_space(3))) void*)dst, 16, voff, soff, 0, 0);
+}
+__device__ __forceinline__ bf16x8 bload16(rsrc_t r, unsigned voff) {
+  const auto v = __builtin_amdgcn_raw_buffer_load_b128(r, voff, 0, 0);
+  return __builtin_bit_cast(bf16x8, v);
+}
+
 // One 64-key tile of the LDS-DMA forward (fwd3 DIAG bit5): issue the next tile's K / V pieces into stage nxt, then
 // S^T = K Q^T, the online softmax and O^T += V^T P^T from stage cur. cur / nxt are __restrict__ parameters of ONE
 // frame, so the waitcnt pass knows the DMA (tracked by vmcnt) never feeds these LDS reads; as plain pointers it put
@@ -383,18 +401,17 @@ __device__ __forceinline__ void store_t21(u16* row, const f32x16 (&a)[4], float 
 // One 64-key tile: issue the next tile's K / V pieces into nxt (4 x 1 KB per image per wave, source-swizzled, rows
 // past the sequence end clamped: their keys are masked), then S^T, the online softmax and O^T += V^T P^T from cur.
 // lastkey: the wave's last visible key (causal: its last query); rel: this lane's last visible key - k0 - 4 hi.
-__device__ __forceinline__ void fwd32_step(const char* __restrict__ cur, char* __restrict__ nxt, bool pre,
-                                           const u16* kbase, const u16* vbase, long ld, long kvoff, int r0, int wave,
-                                           int k0, int len, int lastkey, bool need_mask, int rel, float sl2,
-                                           const Offs32& off, const bf16x8 (&qf)[8], f32x16 (&o)[4], float& m,
-                                           float& l) {
+__device__ __forceinline__ void fwd32_step(const char* __restrict__ cur, char* __restrict__ nxt, bool pre, rsrc_t kv,
+                                           unsigned voffk, unsigned voffv, unsigned rowb, int wave, int k0, int lastkey,
+                                           bool need_mask, int rel, float sl2, const Offs32& off,
+                                           const bf16x8 (&qf)[8], f32x16 (&o)[4], float& m, float& l) {
   constexpr int TB = 64 * ROWB;
   if (pre) {
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-      const long row = min(k0 + 64 + r0 + 16 * j, len - 1);
-      lds_dma16(kbase + row * ld + kvoff, nxt + (wave + 4 * j) * 1024);
-      lds_dma16(vbase + row * ld + kvoff, nxt + TB + (wave + 4 * j) * 1024);
+      const unsigned so = (unsigned)(k0 + 64 + 16 * j) * rowb;
+      bdma16(kv, nxt + (wave + 4 * j) * 1024, voffk, so);
+      bdma16(kv, nxt + TB + (wave + 4 * j) * 1024, voffv, so);
     }
   }
   if (k0 > lastkey) return;
@@ -402,17 +419,18 @@ __device__ __forceinline__ void fwd32_step(const char* __restrict__ cur, char* _
   const char* Ks = cur;
   const char* Vs = cur + TB;
   f32x16 s[2];
+  s[0] = mfma32(lds_row(Ks, off.k[0]), qf[0], f32x16{});
 #pragma unroll
-  for (int kb = 0; kb < 2; ++kb)
+  for (int st = 1; st < 8; ++st) s[0] = mfma32(lds_row(Ks, off.k[st]), qf[st], s[0]);
+  if (two) {  // (each path writes s[1] itself: a zero-filled s[1] before the branch costs 48 moves per tile)
+    s[1] = mfma32(lds_row(Ks, off.k[0] + 32 * ROWB), qf[0], f32x16{});
 #pragma unroll
-    for (int i = 0; i < 16; ++i) s[kb][i] = 0.f;
+    for (int st = 1; st < 8; ++st) s[1] = mfma32(lds_row(Ks, off.k[st] + 32 * ROWB), qf[st], s[1]);
+  } else {
 #pragma unroll
-  for (int st = 0; st < 8; ++st) s[0] = mfma32(lds_row(Ks, off.k[st]), qf[st], s[0]);
-  if (two) {
-#pragma unroll
-    for (int st = 0; st < 8; ++st) s[1] = mfma32(lds_row(Ks, off.k[st] + 32 * ROWB), qf[st], s[1]);
+    for (int i = 0; i < 16; ++i) s[1][i] = -INFINITY;
   }
-  if (need_mask || !two) {
+  if (need_mask) {
 #pragma unroll
     for (int kb = 0; kb < 2; ++kb)
 #pragma unroll
@@ -470,35 +488,36 @@ __global__ __launch_bounds__(256, 2) void fwd32_kernel(const u16* __restrict__ q
   SFT_DASSERT(start >= 0 && len >= 0 && start + len <= total);
   const int q0 = qb * 32 * PB;
   if (q0 >= len) return;
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, hi = lane >> 5;
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6), hi = lane >> 5;
   const int h = blockIdx.x * HW + wave % HW;
   const int kvh = (blockIdx.x * HW) / (nq / nkv);
   const long ld = (long)(nq + 2 * nkv) * D;
   const int wq0 = q0 + 32 * (wave / HW);
   const int qi = wq0 + (lane & 31);
   const bool qok = qi < len;
-  const u16* kbase = qkv + (long)start * ld + (nq + kvh) * D;
-  const u16* vbase = qkv + (long)start * ld + (nq + nkv + kvh) * D;
   const int nkb = (len + 63) / 64;
   const int nkt = causal ? min((min(q0 + 32 * PB, len) - 1) / 64 + 1, nkb) : nkb;
   const int lastkey = causal ? min(wq0 + 31, len - 1) : len - 1;
   const int lim = causal ? min(len - 1, qi) : len - 1;
   Offs32 off;
   off.init(lane);
+  const unsigned rowb = (unsigned)ld * 2;
   bf16x8 qf[8];
-  {
-    const u16* qp = qkv + (long)(start + qi) * ld + h * D + 8 * hi;
+  {  // Q rows past the sequence end read as zero (outside the descriptor's range)
+    const rsrc_t qr = make_rsrc(qkv + (long)start * ld + h * D, (long)(len - 1) * ld * 2 + ROWB);
+    const unsigned vo = (unsigned)qi * rowb + 16 * hi;
 #pragma unroll
-    for (int st = 0; st < 8; ++st) qf[st] = load_frag_global(qp + 16 * st, qok);
+    for (int st = 0; st < 8; ++st) qf[st] = bload16(qr, vo + 32 * st);
   }
-  // DMA: lane (wave w, l) fills LDS rows 4 (w + 4 j) + (l >> 4), position l & 15, with the chunk swz(row, l & 15)
+  // K and V of rows [0, len) of this kv head in one descriptor (V = K + nkv * D); DMA lane (wave w, l) fills LDS
+  // rows 4 (w + 4 j) + (l >> 4), position l & 15, with the chunk swz(row, l & 15)
+  const rsrc_t kv = make_rsrc(qkv + (long)start * ld + (nq + kvh) * D, (long)len * ld * 2 - (long)(nq + kvh) * ROWB);
   const int r0 = 4 * wave + (lane >> 4);
-  const long kvoff = 8 * swz(r0, lane & 15);
+  const unsigned voffk = (unsigned)r0 * rowb + 16 * swz(r0, lane & 15), voffv = voffk + nkv * ROWB;
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
-    const long row = min(r0 + 16 * j, len - 1);
-    lds_dma16(kbase + row * ld + kvoff, smem + (wave + 4 * j) * 1024);
-    lds_dma16(vbase + row * ld + kvoff, smem + TB + (wave + 4 * j) * 1024);
+    bdma16(kv, smem + (wave + 4 * j) * 1024, voffk, 16 * j * rowb);
+    bdma16(kv, smem + TB + (wave + 4 * j) * 1024, voffv, 16 * j * rowb);
   }
   vm_drain();
   f32x16 o[4];
@@ -512,8 +531,8 @@ __global__ __launch_bounds__(256, 2) void fwd32_kernel(const u16* __restrict__ q
     const int k0 = kt * 64;
     const bool pre = kt + 1 < nkt;
     const bool need_mask = (k0 + 64 > len) || (causal && k0 + 63 > wq0);
-    fwd32_step(smem + (kt & 1) * 2 * TB, smem + ((kt + 1) & 1) * 2 * TB, pre, kbase, vbase, ld, kvoff, r0, wave, k0,
-               len, lastkey, need_mask, lim - k0 - 4 * hi, sl2, off, qf, o, m, l);
+    fwd32_step(smem + (kt & 1) * 2 * TB, smem + ((kt + 1) & 1) * 2 * TB, pre, kv, voffk, voffv, rowb, wave, k0,
+               lastkey, need_mask, lim - k0 - 4 * hi, sl2, off, qf, o, m, l);
     if (pre) vm_drain();
     __syncthreads();
   }
@@ -997,7 +1016,7 @@ __global__ __launch_bounds__(NW * 64) void bwd_dq3_kernel(const u16* __restrict_
 // accumulator is the forward's O^T layout (T21 stores). A workgroup = 4 waves = HW query heads of one kv head x
 // (4 / HW) 32-query position blocks (as fwd32): the K tile is shared, each wave stages its own [64 keys][32 queries]
 // dS^T block (64-B rows: a transposed read's four rows x 64 B of a 32-lane half cover the 64 banks once, no swizzle).
-// Rows past the sequence end are zero-filled (the dS^T rows there were never written). Per tile and wave: 16 MFMAs,
+// Rows past the sequence end read as zero (the dS^T rows there were never written; buffer-descriptor range). Per tile and wave: 16 MFMAs,
 // 32 + 8 ds_read_b64_tr_b16.
 __device__ __forceinline__ void rope_bwd32(f32x16 (&a)[4], const float* cs, const float* sn, float s) {
   const int hi = (threadIdx.x >> 5) & 1;
@@ -1019,21 +1038,16 @@ __device__ __forceinline__ void rope_bwd32(f32x16 (&a)[4], const float* cs, cons
 }
 
 __device__ __forceinline__ void dq32_step(const char* __restrict__ cur, char* __restrict__ nxt, bool pre, bool active,
-                                          const u16* kbase, const u16* sbase, long ld, long lp, int k0n, int len,
-                                          long kvoff, int r0, int wave, int lane, const Offs32& off, int sofs,
+                                          rsrc_t kr, rsrc_t sr, unsigned voffk, unsigned voffs, unsigned rowb,
+                                          unsigned rows, int k0n, int wave, const Offs32& off, int sofs,
                                           f32x16 (&dq)[4]) {
   constexpr int TB = 64 * ROWB, SB = 64 * 64;  // K image, per-wave dS^T block
-  if (pre) {  // the next tile (keys k0n ..): K pieces wave + 4 j, this wave's dS^T pieces j (rows 16 j + lane / 4)
+  if (pre) {  // the next tile (keys k0n ..): K pieces wave + 4 j, this wave's dS^T pieces j (rows 16 j + lane / 4);
+              // rows past the sequence end read as zero (outside the descriptors' ranges)
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-      const int kr = k0n + r0 + 16 * j;
-      char* kd = nxt + (wave + 4 * j) * 1024;
-      if (kr < len) lds_dma16(kbase + kr * ld + kvoff, kd);
-      else *(uint4*)(kd + 16 * lane) = make_uint4(0, 0, 0, 0);
-      const int sr = k0n + 16 * j + (lane >> 2);
-      char* sd = nxt + TB + wave * SB + j * 1024;
-      if (sr < len) lds_dma16(sbase + sr * lp + 8 * (lane & 3), sd);
-      else *(uint4*)(sd + 16 * lane) = make_uint4(0, 0, 0, 0);
+      bdma16(kr, nxt + (wave + 4 * j) * 1024, voffk, (unsigned)(k0n + 16 * j) * rowb);
+      bdma16(sr, nxt + TB + wave * SB + j * 1024, voffs, (unsigned)(k0n + 16 * j) * rows);
     }
   }
   if (!active) return;
@@ -1060,7 +1074,7 @@ __global__ __launch_bounds__(256, 2) void bwd_dq32_kernel(const u16* __restrict_
   const int start = cu[b], len = cu[b + 1] - start;
   const int q0 = qb * 32 * PB;
   if (q0 >= len) return;
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, hi = lane >> 5;
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6), hi = lane >> 5;
   const int h = blockIdx.x * HW + wave % HW;
   const int kvh = (blockIdx.x * HW) / (nq / nkv);
   const long ld = (long)(nq + 2 * nkv) * D;
@@ -1078,20 +1092,24 @@ __global__ __launch_bounds__(256, 2) void bwd_dq32_kernel(const u16* __restrict_
   // 16 (a & 1) + 4 p .. + 3 (64-B rows)
   const int sofs = (4 * hi + ((lane & 15) >> 2)) * 64 + 32 * ((lane >> 4) & 1) + 8 * (lane & 3);
   const int r0 = 4 * wave + (lane >> 4);
-  const long kvoff = 8 * swz(r0, lane & 15);
+  const unsigned rowb = (unsigned)ld * 2, rows = (unsigned)lp * 2;
+  const rsrc_t kr = make_rsrc(kbase, (long)(len - 1) * ld * 2 + ROWB);
+  const rsrc_t sr = make_rsrc(sbase, (long)(len - 1) * lp * 2 + 64);
+  const unsigned voffk = (unsigned)r0 * rowb + 16 * swz(r0, lane & 15);
+  const unsigned voffs = (unsigned)(lane >> 2) * rows + 16 * (lane & 3);
   f32x16 dq[4];
 #pragma unroll
   for (int d4 = 0; d4 < 4; ++d4)
 #pragma unroll
     for (int i = 0; i < 16; ++i) dq[d4][i] = 0.f;
-  dq32_step(smem + STG, smem, true, false, kbase, sbase, ld, lp, 0, len, kvoff, r0, wave, lane, off, sofs, dq);
+  dq32_step(smem + STG, smem, true, false, kr, sr, voffk, voffs, rowb, rows, 0, wave, off, sofs, dq);
   vm_drain();
   __syncthreads();
   for (int kt = 0; kt < nkt; ++kt) {
     const int k0 = kt * 64;
     const bool pre = kt + 1 < nkt;
-    dq32_step(smem + (kt & 1) * STG, smem + ((kt + 1) & 1) * STG, pre, !causal || k0 <= lastq, kbase, sbase, ld, lp,
-              k0 + 64, len, kvoff, r0, wave, lane, off, sofs, dq);
+    dq32_step(smem + (kt & 1) * STG, smem + ((kt + 1) & 1) * STG, pre, !causal || k0 <= lastq, kr, sr, voffk, voffs,
+              rowb, rows, k0 + 64, wave, off, sofs, dq);
     if (pre) vm_drain();  // this lane's pieces of the next tile landed ...
     __syncthreads();      // ... and every lane's (LDS zero stores too); every wave is done reading this stage
   }
@@ -1116,20 +1134,20 @@ __global__ __launch_bounds__(256, 2) void bwd_dq32_kernel(const u16* __restrict_
 // queries x 4 products), 32 ds_read_b128 + 64 ds_read_b64_tr_b16 — half dkdv5's LDS bytes per FLOP.
 // dS^T ([b][h][key][q], row stride lp) is written for bwd_dq4 when drow is given (T21-paired 16-B stores).
 __device__ __forceinline__ void dkdv32_step(const char* __restrict__ cur, char* __restrict__ nxt, bool pre,
-                                            const u16* qsrc, const u16* osrc, long ld, long ldo, int nrow0, int qlast,
-                                            long qoff0, long qoff1, int wv, const float* lsrc, const float* dsrc,
-                                            int gl, int q0, int len, int causal, int kw0, int key, float sl2,
-                                            u16* drow, bool dok, const Offs32& off, const bf16x8 (&kf)[8],
-                                            const bf16x8 (&vf)[8], f32x16 (&dk)[4], f32x16 (&dv)[4]) {
+                                            rsrc_t qr, rsrc_t orr, unsigned vq0, unsigned vq1, unsigned vo0,
+                                            unsigned vo1, unsigned qso, unsigned oso, unsigned rowb, unsigned rowo,
+                                            int wv, const float* lsrc, const float* dsrc, int gl, int q0, int len,
+                                            int causal, int kw0, int key, float sl2, u16* drow, bool dok,
+                                            const Offs32& off, const bf16x8 (&kf)[8], const char* Vk,
+                                            f32x16 (&dk)[4], f32x16 (&dv)[4]) {
   constexpr int TB = 64 * ROWB;
   float pl = 0.f, pd = 0.f;
-  if (pre) {  // the next tile: image rows 4 (wv + 2 j) + (lane >> 4) = nrow0 + 8 j - first row
+  if (pre) {  // the next tile (rows from qso / oso): image rows 4 (wv + 2 j) + (lane >> 4); rows past the sequence
+              // end read as zero (outside the descriptors' ranges)
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
-      const long row = min(nrow0 + 8 * j, qlast);
-      const long o = (j & 1) ? qoff1 : qoff0;
-      lds_dma16(qsrc + row * ld + o, nxt + (wv + 2 * j) * 1024);
-      lds_dma16(osrc + row * ldo + o, nxt + TB + (wv + 2 * j) * 1024);
+      bdma16(qr, nxt + (wv + 2 * j) * 1024, (j & 1) ? vq1 : vq0, qso + 16 * (j >> 1) * rowb);
+      bdma16(orr, nxt + TB + (wv + 2 * j) * 1024, (j & 1) ? vo1 : vo0, oso + 16 * (j >> 1) * rowo);
     }
     if (gl < 64 && lsrc != nullptr) {
       pl = lsrc[gl];
@@ -1141,15 +1159,15 @@ __device__ __forceinline__ void dkdv32_step(const char* __restrict__ cur, char* 
   const float* Ls = (const float*)(cur + 2 * TB);
   const float* Dl = Ls + 64;
   const int hi = (threadIdx.x >> 5) & 1;
-#pragma unroll
-  for (int qb = 0; qb < 2; ++qb) {
+#pragma unroll 1
+  for (int qb = 0; qb < 2; ++qb) {  // (not unrolled: hoisting the second half's LDS reads ran out of VGPRs)
     f32x16 s, dp;
 #pragma unroll
     for (int i = 0; i < 16; ++i) s[i] = dp[i] = 0.f;
 #pragma unroll
     for (int st = 0; st < 8; ++st) {
       s = mfma32(lds_row(Qs, off.k[st] + qb * 32 * ROWB), kf[st], s);
-      dp = mfma32(lds_row(Os, off.k[st] + qb * 32 * ROWB), vf[st], dp);
+      dp = mfma32(lds_row(Os, off.k[st] + qb * 32 * ROWB), lds_row(Vk, off.k[st]), dp);
     }
     // query q = q0 + 32 qb + 4 hi + o, o = 8 m + t for register 4 m + t; visible iff lo <= o <= hq
     const int qbase = q0 + 32 * qb + 4 * hi;
@@ -1208,8 +1226,9 @@ __global__ __launch_bounds__(128 * G, 1) void bwd_dkdv32_kernel(
     float sl2, float scale, int causal, u16* __restrict__ dst, int lp, const float* __restrict__ rcos,
     const float* __restrict__ rsin) {
   constexpr int TB = 64 * ROWB, GB = 2 * TB + 2 * 64 * 4;  // per stage: Q, dO images + lse, delta
-  __shared__ __attribute__((aligned(16))) char smem[G * 2 * GB];
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, grp = w >> 1, kh = w & 1, gl = tid & 127;
+  __shared__ __attribute__((aligned(16))) char smem[G * 2 * GB + TB];  // + the workgroup's V image (64 keys)
+  const int tid = threadIdx.x, lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6), grp = w >> 1, kh = w & 1;
+  const int gl = tid & 127;
   const int hi = lane >> 5;
   char* base = smem + grp * 2 * GB;
   const int kvh = blockIdx.x, b = blockIdx.y, kb = blockIdx.z;  // z = 0 first: the causally heaviest key blocks
@@ -1228,15 +1247,20 @@ __global__ __launch_bounds__(128 * G, 1) void bwd_dkdv32_kernel(
   int h = kvh * rep + grp * hpg, qt = qt0;
   // DMA: lane (wave kh, l) fills image rows 4 (kh + 2 j) + (l >> 4), position l & 15, with chunk swz(row, l & 15)
   const int qr0 = 4 * kh + (lane >> 4);
-  const long qoff0 = 8 * swz(qr0, lane & 15), qoff1 = 8 * swz(qr0 + 8, lane & 15);
+  const unsigned rowb = (unsigned)ld * 2, rowo = (unsigned)ldo * 2;
+  // Q rows [0, len) of every head of the sequence (rows past it fall outside the range: zero), dO likewise
+  const rsrc_t qr = make_rsrc(qkv + (long)start * ld, (long)(len - 1) * ld * 2 + (long)nq * ROWB);
+  const rsrc_t orr = make_rsrc(dout + (long)start * ldo, (long)len * ldo * 2);
+  // lane offsets of the even / odd pieces (image rows qr0 + 16 u and qr0 + 8 + 16 u: two swizzles)
+  const unsigned sw0 = 16 * swz(qr0, lane & 15), sw1 = 16 * swz(qr0 + 8, lane & 15);
+  const unsigned vq0 = (unsigned)qr0 * rowb + sw0, vq1 = (unsigned)(qr0 + 8) * rowb + sw1;
+  const unsigned vo0 = (unsigned)qr0 * rowo + sw0, vo1 = (unsigned)(qr0 + 8) * rowo + sw1;
   {
     const int q0 = qt0 * 64, qv = len - q0;
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const long row = start + min(q0 + qr0 + 8 * j, len - 1);
-      const long o = (j & 1) ? qoff1 : qoff0;
-      lds_dma16(qkv + row * ld + h * D + o, base + (kh + 2 * j) * 1024);
-      lds_dma16(dout + row * ldo + h * D + o, base + TB + (kh + 2 * j) * 1024);
+    for (int j = 0; j < 8; ++j) {  // piece j: rows qr0 + 8 j (vq1 / vo1 carry the + 8 of odd j)
+      bdma16(qr, base + (kh + 2 * j) * 1024, (j & 1) ? vq1 : vq0, (unsigned)(q0 + 16 * (j >> 1)) * rowb + h * ROWB);
+      bdma16(orr, base + TB + (kh + 2 * j) * 1024, (j & 1) ? vo1 : vo0, (unsigned)(q0 + 16 * (j >> 1)) * rowo + h * ROWB);
     }
     if (gl < 64) {
       float* Ls = (float*)(base + 2 * TB);
@@ -1244,15 +1268,24 @@ __global__ __launch_bounds__(128 * G, 1) void bwd_dkdv32_kernel(
       Ls[64 + gl] = gl < qv ? delta[(long)h * total + start + q0 + gl] : 0.f;
     }
   }
-  bf16x8 kf[8], vf[8];
+  // K fragments (B of S = Q K^T) in registers; the V rows (B of dP = dO V^T) read from an LDS image of the
+  // workgroup's 64 keys (keeping them in registers too pushed the accumulators through v_accvgpr moves every tile)
+  bf16x8 kf[8];
+  char* Vk = smem + G * 2 * GB + kh * 32 * ROWB;
   {
-    const u16* kp = qkv + (long)(start + key) * ld + (nq + kvh) * D + 8 * hi;
-    const u16* vp = qkv + (long)(start + key) * ld + (nq + nkv + kvh) * D + 8 * hi;
+    const rsrc_t kr = make_rsrc(qkv + (long)start * ld + (nq + kvh) * D, (long)(len - 1) * ld * 2 + (long)(nkv + 1) * ROWB);
+    const unsigned vo = (unsigned)key * rowb + 16 * hi;
 #pragma unroll
-    for (int st = 0; st < 8; ++st) {
-      kf[st] = load_frag_global(kp + 16 * st, kok);
-      vf[st] = load_frag_global(vp + 16 * st, kok);
-    }
+    for (int st = 0; st < 8; ++st) kf[st] = bload16(kr, vo + 32 * st);
+    // V image rows 4 p + (lane >> 4) of piece p = w + 2 G j (keys k0 + row; past the sequence end: zero)
+    // (G = 1: pieces w + 2 j, rows vr + 8 j — odd j is 8 rows on, with the swizzle of vr + 8)
+    const int vr = 4 * w + (lane >> 4);
+    const unsigned vv0 = (unsigned)(k0 + vr) * rowb + nkv * ROWB + 16 * swz(vr, lane & 15);
+    const unsigned vv1 = (unsigned)(k0 + vr) * rowb + nkv * ROWB + 16 * swz(vr + 8, lane & 15);
+#pragma unroll
+    for (int j = 0; j < 8 / G; ++j)
+      bdma16(kr, smem + G * 2 * GB + (w + 2 * G * j) * 1024, (G == 1 && (j & 1)) ? vv1 : vv0,
+             (unsigned)(8 * G * j) * rowb);
   }
   vm_drain();
   f32x16 dk[4], dv[4];
@@ -1273,9 +1306,9 @@ __global__ __launch_bounds__(128 * G, 1) void bwd_dkdv32_kernel(
     const long lo = (long)hn * total + start + qn;
     const bool lok = pre && qn + gl < len;
     u16* drow = dst != nullptr ? dst + ((long)(b * nq + h) * lp + key) * lp + q0 : nullptr;
-    dkdv32_step(base + (it & 1) * GB, base + ((it + 1) & 1) * GB, pre, qkv + (long)start * ld + hn * D,
-                dout + (long)start * ldo + hn * D, ld, ldo, qn + qr0, len - 1, qoff0, qoff1, kh,
-                lok ? lse + lo : nullptr, delta + lo, gl, q0, len, causal, kw0, key, sl2, drow, kok, off, kf, vf, dk,
+    dkdv32_step(base + (it & 1) * GB, base + ((it + 1) & 1) * GB, pre, qr, orr, vq0, vq1, vo0, vo1,
+                (unsigned)qn * rowb + hn * ROWB, (unsigned)qn * rowo + hn * ROWB, rowb, rowo, kh,
+                lok ? lse + lo : nullptr, delta + lo, gl, q0, len, causal, kw0, key, sl2, drow, kok, off, kf, Vk, dk,
                 dv);
     if (pre) vm_drain();  // this lane's pieces of the next tile landed ...
     __syncthreads();      // ... and every lane's; every wave is done reading this stage
