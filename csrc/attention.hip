@@ -5,22 +5,22 @@
 // natural log). Backward returns dqkv in the same packed layout, ready for the fused QKV
 // linear's backward.
 //
-// CDNA4 mapping:
-// * MFMA v_mfma_f32_16x16x32_bf16 throughout (wave64; lane maps below), fp32 accumulate;
-// * "swapped" products (S^T = K Q^T, dP^T = V dO^T, ...) put the reduction index of the next
-//   product in the accumulator registers, so P / dS feed the next MFMA straight from
-//   registers (cvt to bf16, no LDS round trip, no cross-lane shuffles);
-// * K/V/Q/dO tiles are staged in LDS as [rows][128] bf16 images with an XOR swizzle that is
-//   conflict-free for both 16-byte row reads (MFMA operands along head_dim) and the gfx950
-//   transposed read ds_read_b64_tr_b16 (MFMA operands along the key/query axis);
-// * online softmax in the exp2 domain with fp32 running max/sum per query row; the four lanes
-//   that share a query column combine with two xor-shuffles.
+// Kernels (all on gfx950 MFMA, fp32 accumulate, bf16 I/O):
+// * fwd32_kernel: v_mfma_f32_32x32x16_bf16, S^T = K Q^T with the query on the lane (row max / sum lane-local + one
+//   permlane32 swap), P^T fed to O^T += V^T P^T straight from the accumulator registers; the GQA heads of a kv head
+//   share each K / V tile (LDS-DMA, two stages, buffer descriptors: rows past the sequence end read as zero);
+// * bwd: delta_kernel (rowsum dO . O), bwd_dkdv32_kernel (S and dP with the KEY on the lane, P / dS as the register
+//   B operands of dV^T / dK^T, dS^T materialised for dQ), bwd_dq32_kernel (dQ^T = K^T dS^T). Past the dS^T budget
+//   (SFTAMD_ATTN_DS_MB) the recomputing bwd_dq3_kernel (16x16x32) replaces dq32.
+// * LDS images [rows][128] bf16 with an XOR swizzle that is conflict-free for both the 16-byte row reads and the
+//   gfx950 transposed read ds_read_b64_tr_b16 (tools/lds_swizzle_check.py).
 //
-// mfma_f32_16x16x32_bf16 lane maps (g = lane >> 4, r = lane & 15, j = 0..7, i = 0..3):
+// mfma_f32_16x16x32_bf16 lane maps (dq3; g = lane >> 4, r = lane & 15, j = 0..7, i = 0..3):
 //   A[row r][k 8g+j], B[k 8g+j][col r], C[row 4g+i][col r].
 // Accumulator-as-operand: two 16-row C tiles (t0, t1) give lane (g, r) the k values
 //   {4g+i} from t0 and {16+4g+i} from t1; we use that order as the k permutation
 //   p(8g+j) = j<4 ? 4g+j : 16+4g+(j-4) on BOTH operands of the next MFMA.
+// The 32x32x16 lane maps are at fwd32 below.
 #include "common.h"
 
 #include <cstring>
@@ -88,27 +88,6 @@ __device__ __forceinline__ void store4(u16* p, const f32x4& v, float s) {
   *(uint2*)p = w;
 }
 
-// Store a lane's 8 x 4 head-dim values (columns 16 dt + 4g + i, p = row + 4g) with the rotate_half RoPE inverted
-// first — the backward of the forward rotation (x1, x2) -> (x1 c - x2 s, x2 c + x1 s) is
-// (g1, g2) -> (g1 c + g2 s, g2 c - g1 s). Columns c and c + 64 of a pair sit in the same lane (dt and dt + 4), so
-// the rotation is in-register, on the fp32 accumulators before the single bf16 rounding. cs / sn: this row's
-// [64] fp32 cos / sin table + 4g.
-__device__ __forceinline__ void store4_rope_bwd(u16* p, const f32x4 (&v)[8], float s, const float* cs, const float* sn) {
-#pragma unroll
-  for (int dt = 0; dt < 4; ++dt) {
-    const float4 c4 = *(const float4*)(cs + 16 * dt), s4 = *(const float4*)(sn + 16 * dt);
-    const float c[4] = {c4.x, c4.y, c4.z, c4.w}, n[4] = {s4.x, s4.y, s4.z, s4.w};
-    f32x4 lo, hi;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const float a = v[dt][i] * s, b = v[dt + 4][i] * s;
-      lo[i] = a * c[i] + b * n[i];
-      hi[i] = b * c[i] - a * n[i];
-    }
-    store4(p + 16 * dt, lo, 1.f);
-    store4(p + 16 * dt + 64, hi, 1.f);
-  }
-}
 
 // ------------------------------------------------------------------------------ backward
 // delta[h][m] = sum_d dO[m, h*D + d] * O[m, h*D + d]   (16 lanes per row)
@@ -147,7 +126,6 @@ __global__ __launch_bounds__(256) void delta_kernel(const u16* __restrict__ dout
 //   THR = 8 (log2 domain; T13 deferred rescale: P stays <= 2^8, exact in bf16 exponent range);
 // * full tiles are staged without per-row bounds checks; one LDS buffer (register prefetch).
 constexpr float THR = 8.f;
-constexpr float THR_FAST = 40.f;  // v6 fast loop: P = exp2(s - m) <= 2^40, o <= 2^49 |V|: far from fp32 / bf16 limits
 
 struct Offs {
   int row[4];  // frag_row bases, k-step s
@@ -179,33 +157,12 @@ __device__ __forceinline__ bf16x8 lds_tr(const char* base, int off) {
 // prefetch every iteration (its latency fully exposed: profiles/r3_attention.md).
 __device__ __forceinline__ void vm_drain() { __builtin_amdgcn_s_waitcnt(0x0F70); }
 
-// max / sum over the 4 lanes l, l ^ 16, l ^ 32, l ^ 48 (one query column's key groups) with VALU lane swaps
-// (v_permlane32_swap / v_permlane16_swap) instead of ds_bpermute round trips through the LDS unit.
-__device__ __forceinline__ float xmax4(float x) {
-  auto a = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
-  x = fmaxf(__uint_as_float(a[0]), __uint_as_float(a[1]));
-  auto b = __builtin_amdgcn_permlane16_swap(__float_as_uint(x), __float_as_uint(x), false, false);
-  return fmaxf(__uint_as_float(b[0]), __uint_as_float(b[1]));
-}
 typedef float f32x2 __attribute__((ext_vector_type(2)));
-// max of a 16-score tile in 8 v_max3_f32 (fmaxf's NaN canonicalisation doubles the VALU count; scores are finite
-// or -inf here)
+// v_max3_f32 (fmaxf's NaN canonicalisation doubles the VALU count; scores are finite or -inf here)
 __device__ __forceinline__ float max3f(float a, float b, float c) {
   float r;
   asm("v_max3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
   return r;
-}
-__device__ __forceinline__ float max16(const f32x4 (&v)[4]) {
-  const float a = max3f(v[0][0], v[0][1], v[0][2]), b = max3f(v[0][3], v[1][0], v[1][1]);
-  const float c = max3f(v[1][2], v[1][3], v[2][0]), d = max3f(v[2][1], v[2][2], v[2][3]);
-  const float e = max3f(v[3][0], v[3][1], v[3][2]);
-  return max3f(max3f(a, b, c), max3f(d, e, v[3][3]), -INFINITY);
-}
-__device__ __forceinline__ float xsum4(float x) {
-  auto a = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
-  x = __uint_as_float(a[0]) + __uint_as_float(a[1]);
-  auto b = __builtin_amdgcn_permlane16_swap(__float_as_uint(x), __float_as_uint(x), false, false);
-  return __uint_as_float(b[0]) + __uint_as_float(b[1]);
 }
 
 template <int R, int NT>
@@ -231,11 +188,6 @@ struct Stage {
   }
 };
 
-// 16 B per lane HBM -> LDS (global_load_lds): lane-linear LDS destination, the image swizzle applied to the source
-__device__ __forceinline__ void lds_dma16(const u16* src, char* dst) {
-  __builtin_amdgcn_global_load_lds((const void __attribute__((address_space(1)))*)src,
-                                   (void __attribute__((address_space(3)))*)dst, 16, 0, 0);
-}
 
 // Buffer-descriptor forms (the 32x32 kernels): the tile's base and byte range in a wave-uniform descriptor, the lane's
 // row / chunk in a loop-invariant VGPR offset, the tile's row offset in an SGPR. Rows past the sequence end fall
@@ -255,71 +207,6 @@ __device__ __forceinline__ bf16x8 bload16(rsrc_t r, unsigned voff) {
   return __builtin_bit_cast(bf16x8, v);
 }
 
-// One 64-key tile of the LDS-DMA forward (fwd3 DIAG bit5): issue the next tile's K / V pieces into stage nxt, then
-// S^T = K Q^T, the online softmax and O^T += V^T P^T from stage cur. cur / nxt are __restrict__ parameters of ONE
-// frame, so the waitcnt pass knows the DMA (tracked by vmcnt) never feeds these LDS reads; as plain pointers it put
-// a vmcnt(0) before the first V^T read, i.e. waited for the next tile inside this one.
-__device__ __forceinline__ void fwd_step_dma(const char* __restrict__ cur, char* __restrict__ nxt, bool pre, bool active,
-                                             const u16* kbase, const u16* vbase, long ld, long kvoff, int r0, int wave,
-                                             int k0, int len, int causal, int wfirst, int qrow, int g, float sl2,
-                                             const Offs& off, const bf16x8 (&qf)[4], f32x4 (&o)[8], float& m,
-                                             float& l, int ahead = 64) {
-  constexpr int TB = 64 * ROWB;
-  if (pre) {  // the tile `ahead` keys past this one
-#pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      const long row = min(k0 + ahead + r0 + 32 * j, len - 1);
-      lds_dma16(kbase + row * ld + kvoff, nxt + (wave + 8 * j) * 1024);
-      lds_dma16(vbase + row * ld + kvoff, nxt + TB + (wave + 8 * j) * 1024);
-    }
-  }
-  if (!active) return;
-  const char* Ks = cur;
-  const char* Vs = cur + TB;
-  f32x4 sc[4];
-#pragma unroll
-  for (int nt = 0; nt < 4; ++nt) {
-    sc[nt] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int s = 0; s < 4; ++s) sc[nt] = mfma(lds_row(Ks, off.row[s] + nt * 16 * ROWB), qf[s], sc[nt]);
-  }
-  if ((k0 + 64 > len) || (causal && k0 + 63 > wfirst)) {
-    const int lim = (causal ? min(len - 1, qrow) : len - 1) - k0 - 4 * g;
-#pragma unroll
-    for (int nt = 0; nt < 4; ++nt)
-#pragma unroll
-      for (int i = 0; i < 4; ++i) sc[nt][i] = 16 * nt + i > lim ? -INFINITY : sc[nt][i];
-  }
-  const float tmax = xmax4(max16(sc)) * sl2;
-  if (__any(tmax > m + THR)) {
-    const float mnew = fmaxf(m, tmax);
-    const float alpha = exp2f(m - mnew);
-    l *= alpha;
-#pragma unroll
-    for (int dt = 0; dt < 8; ++dt) o[dt] *= alpha;
-    m = mnew;
-  }
-  f32x2 acc = {0.f, 0.f};
-  const f32x2 sl = {sl2, sl2}, nm = {-m, -m};
-#pragma unroll
-  for (int nt = 0; nt < 4; ++nt)
-#pragma unroll
-    for (int i = 0; i < 4; i += 2) {
-      const f32x2 t = __builtin_elementwise_fma(f32x2{sc[nt][i], sc[nt][i + 1]}, sl, nm);
-      const f32x2 p = {exp2f(t.x), exp2f(t.y)};
-      sc[nt][i] = p.x;
-      sc[nt][i + 1] = p.y;
-      acc += p;
-    }
-  l += acc.x + acc.y;
-#pragma unroll
-  for (int ks = 0; ks < 2; ++ks) {
-    const bf16x8 pb = pack_acc(sc[2 * ks], sc[2 * ks + 1]);
-#pragma unroll
-    for (int dt = 0; dt < 8; ++dt) o[dt] = mfma(lds_tr(Vs, off.tr[dt] + ks * 32 * ROWB), pb, o[dt]);
-  }
-}
-
 // ============================================================================== fwd32: 32x32x16 forward
 // v_mfma_f32_32x32x16_bf16 lane maps (hi = lane >> 5, c = lane & 31, j = 0..7, i = 0..15):
 //   A[row c][k 8hi+j], B[k 8hi+j][col c], C[row crow(i, hi)][col c], crow(i, hi) = (i & 3) + 8 (i >> 2) + 4 hi.
@@ -328,7 +215,8 @@ __device__ __forceinline__ void fwd_step_dma(const char* __restrict__ cur, char*
 // already the B operand (P^T) of k-step 2 kb + sub of O^T += V^T P^T: they hold keys 16 ks + 4 hi + {0..3} and
 // 16 ks + 8 + 4 hi + {0..3}, so the V^T A operand is read with that key order (two ds_read_b64_tr_b16, rows
 // 16 ks + 4 hi + q and 16 ks + 8 + 4 hi + q). Per 64-key tile and 32 queries: 16 + 16 MFMAs (each 2x the work of a
-// 16x16x32), 16 ds_read_b128 + 32 ds_read_b64_tr_b16 — half fwd3's LDS bytes per FLOP.
+// 16x16x32), 16 ds_read_b128 + 32 ds_read_b64_tr_b16 — half the LDS bytes per FLOP of the 16x16x32 forward it
+// replaced (46 -> 35 us at 16 x 512, SmolLM3 heads).
 // A workgroup = 4 waves = HW query heads of one kv head x (4 / HW) 32-query position blocks (HW = gcd(rep, 4)): at
 // GQA rep 4 the four waves share their positions, so the key range, the K / V tiles and the causal work are the same
 // for every wave and a 32-key half tile past the diagonal is skipped by all of them.
@@ -542,359 +430,8 @@ __global__ __launch_bounds__(256, 2) void fwd32_kernel(const u16* __restrict__ q
   if (qok && hi == 0) lse[(long)h * total + start + qi] = (m + log2f(l)) * LN2;
 }
 
-// DIAG (timing-only ablations, wrong results): bit0 no next-tile loads/stores, bit1 no softmax math,
-// bit2 no PV MFMAs, bit3 no QK MFMAs. bit4 (results exact): the round-2 schedule for A/B runs (no vm_drain before
-// the loop, per-tile row-sum shuffles through ds_bpermute). bit5: K / V tiles by LDS-DMA into two stages (no VGPR
-// staging / ds_write, one barrier per tile; NW = 8).
-template <int NW, int DIAG = 0>
-__global__ __launch_bounds__(NW * 64, NW == 8 ? 4 : 2) void fwd3_kernel(const u16* __restrict__ qkv, u16* __restrict__ out,
-                                                       float* __restrict__ lse, const int* __restrict__ cu, int nq,
-                                                       int nkv, int total, float sl2, int causal) {
-  constexpr int NT = NW * 64, BM = NW * 16, TB = 64 * ROWB;
-  constexpr bool DMA3 = DIAG & 64;  // three stages, two tiles in flight (implies DMA)
-  constexpr bool DMA = (DIAG & 32) || DMA3;
-  static_assert(!DMA || NW == 8, "LDS-DMA staging: 8 waves x 2 pieces per 64-row image");
-  __shared__ __attribute__((aligned(16))) char smem[(DMA3 ? 6 : DMA ? 4 : 2) * TB];
-  char* Ks = smem;
-  char* Vs = smem + TB;
-  // grid (heads, sequences, q-blocks) with the last (causally heaviest) q-block dispatched first: LPT order
-  const int h = blockIdx.x, b = blockIdx.y, qb = gridDim.z - 1 - blockIdx.z;
-  const int start = cu[b], len = cu[b + 1] - start;
-  SFT_DASSERT(start >= 0 && len >= 0 && start + len <= total);
-  const int q0 = qb * BM;
-  if (q0 >= len) return;
-  const int kvh = h / (nq / nkv);
-  const long ld = (long)(nq + 2 * nkv) * D;
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, g = lane >> 4;
-  const int wfirst = q0 + wave * 16;
-  const int qrow = wfirst + (lane & 15);
-  const bool qok = qrow < len;
-  const u16* kbase = qkv + (long)start * ld + (nq + kvh) * D;
-  const u16* vbase = qkv + (long)start * ld + (nq + nkv + kvh) * D;
-  const int nkb = (len + 63) / 64;
-  const int nkt = causal ? min((q0 + BM + 63) / 64, nkb) : nkb;
-  Offs off;
-  off.init(lane);
-  constexpr bool LEG = DIAG & 16;
-  bf16x8 qf[4];
-  if constexpr (!LEG) {  // Q first: the (in-order) wait for the first K / V tile then covers it
-    const u16* qp = qkv + (long)(start + qrow) * ld + h * D + 8 * g;
-#pragma unroll
-    for (int s = 0; s < 4; ++s) qf[s] = load_frag_global(qp + 32 * s, qok);
-  }
-  // DMA: lane (wave w, l) fills LDS rows 4 (w + 8 j) + (l >> 4), position l & 15 with the chunk swz(row, l & 15) of
-  // that row (rows past the sequence end clamped to its last row: their keys are masked)
-  const int r0 = 4 * wave + (lane >> 4);
-  const long kvoff = 8 * swz(r0, lane & 15);
-  if constexpr (DMA3) {
-    // tiles 0 and 1 are issued by the loop's first two (compute-free) iterations: the same code instance as every
-    // later DMA, so the waitcnt pass sees them in the loop's alias scopes and adds no vmcnt(0) before the loop
-  } else if constexpr (DMA) {
-#pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      const long row = min(r0 + 32 * j, len - 1);
-      lds_dma16(kbase + row * ld + kvoff, smem + (wave + 8 * j) * 1024);
-      lds_dma16(vbase + row * ld + kvoff, smem + TB + (wave + 8 * j) * 1024);
-    }
-  } else {
-    Stage<64, NT> tk, tv;
-    tk.load(kbase, ld, len, tid);
-    tv.load(vbase, ld, len, tid);
-    tk.store(Ks, tid);
-    tv.store(Vs, tid);
-  }
-  if constexpr (LEG) {
-    const u16* qp = qkv + (long)(start + qrow) * ld + h * D + 8 * g;
-#pragma unroll
-    for (int s = 0; s < 4; ++s) qf[s] = load_frag_global(qp + 32 * s, qok);
-  }
-  if constexpr (!LEG) vm_drain();
-  f32x4 o[8];
-#pragma unroll
-  for (int dt = 0; dt < 8; ++dt) o[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
-  float m = -1e30f, l = 0.f;  // l: this lane's partial row sum (its 16 keys per tile) unless LEG
-  __syncthreads();
-  if constexpr (DMA3) {
-    int sc = 1;  // stage of tile kt (kt = -2, -1: no tile, the DMA of tiles 0, 1); tile kt + 2 -> stage (sc + 2) % 3
-    for (int kt = -2; kt < nkt; ++kt) {
-      const int k0 = kt * 64;
-      const bool pre2 = kt + 2 < nkt;
-      const int sn = sc == 0 ? 2 : sc - 1;
-      fwd_step_dma(smem + sc * 2 * TB, smem + sn * 2 * TB, pre2, kt >= 0 && (!causal || k0 <= wfirst + 15), kbase,
-                   vbase, ld, kvoff, r0, wave, k0, len, causal, wfirst, qrow, g, sl2, off, qf, o, m, l, 128);
-      // vmcnt(4) + lgkmcnt(0): tile kt + 1 landed (kt + 2's 4 pieces may fly), this wave's LDS reads are done; a
-      // plain s_barrier, as __syncthreads' fence would wait for the in-flight DMA too (vmcnt(0))
-      if (pre2) __builtin_amdgcn_s_waitcnt(0x0074);
-      else __builtin_amdgcn_s_waitcnt(0x0070);
-      __builtin_amdgcn_s_barrier();
-      sc = sc == 2 ? 0 : sc + 1;
-    }
-  } else if constexpr (DMA) {
-    for (int kt = 0; kt < nkt; ++kt) {
-      const int k0 = kt * 64;
-      const bool pre = kt + 1 < nkt;
-      // stage (kt + 1) & 1's last reads ended at the previous iteration's barrier
-      fwd_step_dma(smem + (kt & 1) * 2 * TB, smem + ((kt + 1) & 1) * 2 * TB, pre, !causal || k0 <= wfirst + 15,
-                   kbase, vbase, ld, kvoff, r0, wave, k0, len, causal, wfirst, qrow, g, sl2, off, qf, o, m, l);
-      if (pre) vm_drain();  // this lane's pieces of the next tile landed ...
-      __syncthreads();      // ... and every lane's; every wave is done reading this stage
-    }
-  }
-  for (int kt = 0; kt < (DMA ? 0 : nkt); ++kt) {
-    const int k0 = kt * 64;
-    const bool pre = !(DIAG & 1) && kt + 1 < nkt;
-    Stage<64, NT> tk, tv;
-    if (pre) {
-      tk.load(kbase + (long)(k0 + 64) * ld, ld, len - k0 - 64, tid);
-      tv.load(vbase + (long)(k0 + 64) * ld, ld, len - k0 - 64, tid);
-    }
-    if (!causal || k0 <= wfirst + 15) {
-      f32x4 sc[4];
-#pragma unroll
-      for (int nt = 0; nt < 4; ++nt) {
-        sc[nt] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-        for (int s = 0; s < 4; ++s)
-          if (!(DIAG & 8)) sc[nt] = mfma(lds_row(Ks, off.row[s] + nt * 16 * ROWB), qf[s], sc[nt]);
-      }
-      if constexpr (!(DIAG & 2)) {
-      const bool need_mask = (k0 + 64 > len) || (causal && k0 + 63 > wfirst);
-      if (need_mask) {
-        if constexpr (LEG) {
-#pragma unroll
-          for (int nt = 0; nt < 4; ++nt)
-#pragma unroll
-            for (int i = 0; i < 4; ++i) {
-              const int key = k0 + 16 * nt + 4 * g + i;
-              if (key >= len || (causal && key > qrow)) sc[nt][i] = -INFINITY;
-            }
-        } else {  // one compare + select per score: key offset 16 nt + i against the lane's last visible key
-          const int lim = (causal ? min(len - 1, qrow) : len - 1) - k0 - 4 * g;
-#pragma unroll
-          for (int nt = 0; nt < 4; ++nt)
-#pragma unroll
-            for (int i = 0; i < 4; ++i) sc[nt][i] = 16 * nt + i > lim ? -INFINITY : sc[nt][i];
-        }
-      }
-      float tmax;
-      if constexpr (LEG) {
-        tmax = fmaxf(fmaxf(fmaxf(sc[0][0], sc[0][1]), fmaxf(sc[0][2], sc[0][3])),
-                     fmaxf(fmaxf(sc[1][0], sc[1][1]), fmaxf(sc[1][2], sc[1][3])));
-        tmax = fmaxf(tmax, fmaxf(fmaxf(fmaxf(sc[2][0], sc[2][1]), fmaxf(sc[2][2], sc[2][3])),
-                                 fmaxf(fmaxf(sc[3][0], sc[3][1]), fmaxf(sc[3][2], sc[3][3]))));
-      } else {
-        tmax = max16(sc);
-      }
-      if constexpr (LEG) {
-        tmax = fmaxf(tmax, __shfl_xor(tmax, 16, 64));
-        tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64));
-      } else {
-        tmax = xmax4(tmax);
-      }
-      tmax *= sl2;
-      if (__any(tmax > m + THR)) {  // deferred rescale (rare after the first tiles)
-        const float mnew = fmaxf(m, tmax);
-        const float alpha = exp2f(m - mnew);
-        l *= alpha;
-#pragma unroll
-        for (int dt = 0; dt < 8; ++dt) o[dt] *= alpha;
-        m = mnew;
-      }
-      float rs = 0.f;
-      if constexpr (LEG) {
-#pragma unroll
-        for (int nt = 0; nt < 4; ++nt)
-#pragma unroll
-          for (int i = 0; i < 4; ++i) {
-            const float p = exp2f(fmaf(sc[nt][i], sl2, -m));
-            sc[nt][i] = p;
-            rs += p;
-          }
-        rs += __shfl_xor(rs, 16, 64);
-        rs += __shfl_xor(rs, 32, 64);
-      } else {  // packed fp32 (v_pk_fma_f32 / v_pk_add_f32): two scores per VALU op around the exp2
-        f32x2 acc = {0.f, 0.f};
-        const f32x2 sl = {sl2, sl2}, nm = {-m, -m};
-#pragma unroll
-        for (int nt = 0; nt < 4; ++nt)
-#pragma unroll
-          for (int i = 0; i < 4; i += 2) {
-            const f32x2 t = __builtin_elementwise_fma(f32x2{sc[nt][i], sc[nt][i + 1]}, sl, nm);
-            const f32x2 p = {exp2f(t.x), exp2f(t.y)};
-            sc[nt][i] = p.x;
-            sc[nt][i + 1] = p.y;
-            acc += p;
-          }
-        rs = acc.x + acc.y;
-      }
-      l += rs;
-      }
-#pragma unroll
-      for (int ks = 0; ks < 2; ++ks) {
-        const bf16x8 pb = pack_acc(sc[2 * ks], sc[2 * ks + 1]);
-#pragma unroll
-        for (int dt = 0; dt < 8; ++dt)
-          if (!(DIAG & 4)) o[dt] = mfma(lds_tr(Vs, off.tr[dt] + ks * 32 * ROWB), pb, o[dt]);
-      }
-    }
-    if (pre) {
-      __syncthreads();
-      tk.store(Ks, tid);
-      tv.store(Vs, tid);
-    }
-    __syncthreads();
-  }
-  if constexpr (!LEG) l = xsum4(l);
-  if (qok) {
-    const float inv = 1.f / l;
-    u16* op = out + (long)(start + qrow) * nq * D + h * D + 4 * g;
-#pragma unroll
-    for (int dt = 0; dt < 8; ++dt) store4(op + 16 * dt, o[dt], inv);
-    if (g == 0) lse[(long)h * total + start + qrow] = (m + log2f(l)) * LN2;
-  }
-}
-
-// One key tile of the LDS-DMA dq4 (bwd_dq4_kernel<8, false, true>): issue the next tile's K / dS^T pieces into stage
-// nxt (2 x 1 KB per image per wave, source-swizzled; rows past the sequence end are ZERO-filled with LDS stores, as
-// dQ sums K x dS^T over keys and the dS^T rows there were never written), then dQ^T += K^T dS^T from stage cur.
-// cur / nxt: __restrict__ parameters of one frame (see fwd_step_dma).
-__device__ __forceinline__ void dq_step_dma(const char* __restrict__ cur, char* __restrict__ nxt, bool pre, bool active,
-                                            const u16* ksrc, const u16* ssrc, long ld, long lp, int row0, int len,
-                                            long coff, int wave, int lane, int trw, const Offs& off, f32x4 (&dq)[8]) {
-  constexpr int TB = 64 * ROWB;
-  if (pre) {
-#pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      const int row = row0 + 32 * j;
-      char* dk = nxt + (wave + 8 * j) * 1024;
-      if (row < len) {
-        lds_dma16(ksrc + row * ld + coff, dk);
-        lds_dma16(ssrc + row * lp + coff, dk + TB);
-      } else {
-        *(uint4*)(dk + 16 * lane) = make_uint4(0, 0, 0, 0);
-        *(uint4*)(dk + TB + 16 * lane) = make_uint4(0, 0, 0, 0);
-      }
-    }
-  }
-  if (!active) return;
-  const char* Ks = cur;
-  const char* Ss = cur + TB;
-#pragma unroll
-  for (int ks = 0; ks < 2; ++ks) {
-    const bf16x8 db = lds_tr(Ss, trw + ks * 32 * ROWB);
-#pragma unroll
-    for (int dt = 0; dt < 8; ++dt) dq[dt] = mfma(lds_tr(Ks, off.tr[dt] + ks * 32 * ROWB), db, dq[dt]);
-  }
-}
-
-// dQ from the materialised dS (v4 backward): bwd_dkdv3_kernel already computes dS = P o (dP - delta) for
-// every (query, key) pair of a head; it stores it transposed, dS^T[b][h][key][query] (bf16, lp x lp per head),
-// so dQ^T = K^T dS^T is ONE MFMA product per 64-key tile here — 16 MFMA per wave per tile instead of the 48 of
-// dq3 (which recomputes S and dP), no exp2 / softmax VALU, no lse / delta reads. The dS^T tile [64 keys][128
-// queries] is staged exactly like a K/V image and read with the same transposed reads (query column block =
-// the wave's 16 rows), so both MFMA operands come from LDS. Rows past the sequence end are zero-filled by the
-// stager; entries never written by dkdv (queries past the last 64-query tile, key tiles above a wave's causal
-// diagonal) are never used: a wave skips tiles above its diagonal and each query column is independent.
-template <int NW, bool LEG = false, bool DMA = false>
-__global__ __launch_bounds__(NW * 64, 4) void bwd_dq4_kernel(const u16* __restrict__ qkv, const u16* __restrict__ dst,
-                                                          const int* __restrict__ cu, u16* __restrict__ dqkv, int nq,
-                                                          int nkv, int lp, float scale, int causal,
-                                                          const float* __restrict__ rcos = nullptr,
-                                                          const float* __restrict__ rsin = nullptr) {
-  static_assert(NW == 8, "the dS^T image is 128 queries wide: 8 waves x 16 rows");
-  constexpr int NT = NW * 64, BM = NW * 16, TB = 64 * ROWB;
-  static_assert(!DMA || !LEG, "the LDS-DMA variant has the current schedule only");
-  __shared__ __attribute__((aligned(16))) char smem[(DMA ? 4 : 2) * TB];  // DMA: two stages of (K, dS^T) images
-  char* Ks = smem;
-  char* Ss = smem + TB;
-  // grid (heads, sequences, q-blocks) with the last (causally heaviest) q-block dispatched first: LPT order
-  const int h = blockIdx.x, b = blockIdx.y, qb = gridDim.z - 1 - blockIdx.z;
-  const int start = cu[b], len = cu[b + 1] - start;
-  const int q0 = qb * BM;
-  if (q0 >= len) return;
-  SFT_DASSERT(q0 + BM <= lp);
-  const int kvh = h / (nq / nkv);
-  const long ld = (long)(nq + 2 * nkv) * D;
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, g = lane >> 4;
-  const int wfirst = q0 + wave * 16;
-  const int qrow = wfirst + (lane & 15);
-  const u16* kbase = qkv + (long)start * ld + (nq + kvh) * D;
-  const u16* sbase = dst + (long)(b * nq + h) * lp * lp + q0;
-  const int nkb = (len + 63) / 64;
-  const int nkt = causal ? min((q0 + BM + 63) / 64, nkb) : nkb;
-  Offs off;
-  off.init(lane);
-  // the wave's own dS^T column block: computed, not off.tr[wave] (a runtime index into a register array sends
-  // the array to scratch, and the scratch load in the loop waited on the next tile's prefetch: vmcnt(0))
-  int trw;
-  if constexpr (LEG) {
-    trw = off.tr[wave];
-  } else {
-    const int r = lane & 15, q = r >> 2, p = r & 3;
-    trw = img_off(4 * g + q, 2 * wave + (p >> 1)) + 8 * (p & 1);
-  }
-  f32x4 dq[8];
-#pragma unroll
-  for (int dt = 0; dt < 8; ++dt) dq[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
-  // DMA: lane (wave w, l) fills image rows 4 (w + 8 j) + (l >> 4), position l & 15 with chunk swz(row, l & 15)
-  const int r0 = 4 * wave + (lane >> 4);
-  const long coff = 8 * swz(r0, lane & 15);
-  if constexpr (DMA) {  // tile 0 into stage 0 (the "next" tile of a virtual tile -1)
-    dq_step_dma(smem + 2 * TB, smem, true, false, kbase, sbase, ld, lp, r0, len, coff, wave, lane, trw, off, dq);
-  } else {
-    Stage<64, NT> tk, ts;
-    tk.load(kbase, ld, len, tid);
-    ts.load(sbase, lp, len, tid);
-    tk.store(Ks, tid);
-    ts.store(Ss, tid);
-  }
-  if constexpr (DMA) vm_drain();
-  __syncthreads();
-  if constexpr (DMA) {
-    for (int kt = 0; kt < nkt; ++kt) {
-      const int k0 = kt * 64;
-      const bool pre = kt + 1 < nkt;
-      dq_step_dma(smem + (kt & 1) * 2 * TB, smem + ((kt + 1) & 1) * 2 * TB, pre, !causal || k0 <= wfirst + 15, kbase,
-                  sbase, ld, lp, k0 + 64 + r0, len, coff, wave, lane, trw, off, dq);
-      if (pre) vm_drain();  // this lane's pieces of the next tile landed ...
-      __syncthreads();      // ... and every lane's (LDS zero stores too); every wave is done reading this stage
-    }
-  }
-  for (int kt = 0; kt < (DMA ? 0 : nkt); ++kt) {
-    const int k0 = kt * 64;
-    const bool pre = kt + 1 < nkt;
-    Stage<64, NT> tk, ts;
-    if (pre) {
-      tk.load(kbase + (long)(k0 + 64) * ld, ld, len - k0 - 64, tid);
-      ts.load(sbase + (long)(k0 + 64) * lp, lp, len - k0 - 64, tid);
-    }
-    if (!causal || k0 <= wfirst + 15) {
-#pragma unroll
-      for (int ks = 0; ks < 2; ++ks) {
-        const bf16x8 db = lds_tr(Ss, trw + ks * 32 * ROWB);
-#pragma unroll
-        for (int dt = 0; dt < 8; ++dt) dq[dt] = mfma(lds_tr(Ks, off.tr[dt] + ks * 32 * ROWB), db, dq[dt]);
-      }
-    }
-    if (pre) {
-      __syncthreads();
-      tk.store(Ks, tid);
-      ts.store(Ss, tid);
-    }
-    __syncthreads();
-  }
-  if (qrow < len) {
-    u16* qp = dqkv + (long)(start + qrow) * ld + h * D + 4 * g;
-    if (rcos != nullptr) {
-      const long tr = (long)(start + qrow) * (D / 2) + 4 * g;
-      store4_rope_bwd(qp, dq, scale, rcos + tr, rsin + tr);
-    } else {
-#pragma unroll
-      for (int dt = 0; dt < 8; ++dt) store4(qp + 16 * dt, dq[dt], scale);
-    }
-  }
-}
-
+// dQ past the dS^T budget (long contexts): per 64-key tile S^T and dP^T are recomputed from Q, K, V, dO, lse and delta
+// (16x16x32 MFMAs, 48 per tile and wave instead of dq32's 16) and dQ^T += K^T dS^T; 8 waves x 16 queries.
 template <int NW>
 __global__ __launch_bounds__(NW * 64) void bwd_dq3_kernel(const u16* __restrict__ qkv, const u16* __restrict__ dout,
                                                           const float* __restrict__ lse,
@@ -1000,17 +537,6 @@ __global__ __launch_bounds__(NW * 64) void bwd_dq3_kernel(const u16* __restrict_
   }
 }
 
-// GQA-grouped dK/dV (v5): one workgroup per (kv head, sequence, 64-key block) walks the query tiles of ALL
-// rep = nq / nkv query heads that share the kv head, keeping K/V fragments and the dK/dV accumulators in
-// registers across heads. dK/dV are written once, in bf16, straight into dqkv: no rep x [total, 2*nkv*128] fp32
-// partial slabs (134 MB written + re-read at 16 x 512 tokens, 16q/4kv) and no dkdv_reduce pass. The per-tile
-// math (S^T, dP^T, dS^T store for dq4) is bwd_dkdv3_kernel's; the iteration space is flattened over
-// (head, query tile) so the register prefetch of the next tile crosses head boundaries.
-// G = 2 (default when rep is even): the workgroup is two 4-wave groups over the SAME 64 keys, each walking half
-// of the heads with its own Q/dO LDS images; group 1 hands its fp32 dK/dV to group 0 through LDS at the end.
-// That halves the serial chain of the causally heaviest key block (block 0 walks rep x nqt tiles), which is what
-// bounds this kernel: at 16 x 512 tokens the MFMA work alone is ~18 us, one tile step ~3 us of latency.
-// blockIdx.z = key block, heaviest first.
 // ============================================================================== dQ with 32x32x16 MFMAs
 // dQ^T = K^T dS^T over the key tiles of the materialised dS^T (written by bwd_dkdv32): the query on the lane, so the
 // accumulator is the forward's O^T layout (T21 stores). A workgroup = 4 waves = HW query heads of one kv head x
@@ -1131,8 +657,9 @@ __global__ __launch_bounds__(256, 2) void bwd_dq32_kernel(const u16* __restrict_
 // ride with the Q / dO images. A workgroup = 64 keys of one kv head = 2 key halves x G head groups (G = 2 when rep is
 // even; the groups' dK / dV are summed through LDS at the end), 64-query tiles of Q / dO by LDS-DMA in two stages per
 // group, one wave per SIMD (dK^T / dV^T: 128 fp32 accumulators per lane). Per tile and wave: 64 MFMAs (32 keys x 64
-// queries x 4 products), 32 ds_read_b128 + 64 ds_read_b64_tr_b16 — half dkdv5's LDS bytes per FLOP.
-// dS^T ([b][h][key][q], row stride lp) is written for bwd_dq4 when drow is given (T21-paired 16-B stores).
+// queries x 4 products), 32 ds_read_b128 + 64 ds_read_b64_tr_b16 — half the LDS bytes per FLOP of the 16x16x32
+// dK/dV kernel it replaced. dS^T ([b][h][key][q], row stride lp) is written for bwd_dq32 when drow is given
+// (T21-paired 16-B stores).
 __device__ __forceinline__ void dkdv32_step(const char* __restrict__ cur, char* __restrict__ nxt, bool pre,
                                             rsrc_t qr, rsrc_t orr, unsigned vq0, unsigned vq1, unsigned vo0,
                                             unsigned vo1, unsigned qso, unsigned oso, unsigned rowb, unsigned rowo,
@@ -1356,364 +883,18 @@ __global__ __launch_bounds__(128 * G, 1) void bwd_dkdv32_kernel(
   store_t21(dqkv + (long)(start + key) * ld + (nq + nkv + kvh) * D, dv, 1.f, kok);
 }
 
-// One query tile of the LDS-DMA GQA dK/dV kernel (bwd_dkdv5_kernel<G, false, true>): issue the next tile's Q / dO
-// pieces (4 x 1 KB per image per wave, source-swizzled, rows past the sequence end clamped: their P and dS are masked
-// to 0) and its lse / delta loads, compute this tile from stage cur, then park lse (x LOG2E) / delta in stage nxt.
-// cur / nxt are __restrict__ parameters of one frame (see fwd_step_dma). Stage: Q image, dO image, lse[64], delta[64].
-__device__ __forceinline__ void dkdv_step_dma(const char* __restrict__ cur, char* __restrict__ nxt, bool pre, bool active,
-                                              const u16* qsrc, const u16* osrc, long ld, long ldo, int qrow0, int qlast,
-                                              long kvoff, int wave, const float* lsrc, const float* dsrc, int gtid,
-                                              int q0, int len, int causal, int key, int wfirst, int g, float sl2,
-                                              u16* drow, const Offs& off, const bf16x8 (&kf)[4],
-                                              const bf16x8 (&vf)[4], f32x4 (&dk)[8], f32x4 (&dv)[8]) {
-  constexpr int TB = 64 * ROWB;
-  float pl = 0.f, pd = 0.f;
-  if (pre) {
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const long row = min(qrow0 + 16 * j, qlast);
-      lds_dma16(qsrc + row * ld + kvoff, nxt + (wave + 4 * j) * 1024);
-      lds_dma16(osrc + row * ldo + kvoff, nxt + TB + (wave + 4 * j) * 1024);
-    }
-    if (gtid < 64 && lsrc != nullptr) {
-      pl = lsrc[gtid];
-      pd = dsrc[gtid];
-    }
-  }
-  if (active) {
-    const char* Qs = cur;
-    const char* Os = cur + TB;
-    const float* Ls = (const float*)(cur + 2 * TB);
-    const float* Dl = Ls + 64;
-    f32x4 sc[4], dp[4];
-#pragma unroll
-    for (int mt = 0; mt < 4; ++mt) {
-      sc[mt] = f32x4{0.f, 0.f, 0.f, 0.f};
-      dp[mt] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-      for (int s = 0; s < 4; ++s) {
-        sc[mt] = mfma(lds_row(Qs, off.row[s] + mt * 16 * ROWB), kf[s], sc[mt]);
-        dp[mt] = mfma(lds_row(Os, off.row[s] + mt * 16 * ROWB), vf[s], dp[mt]);
-      }
-    }
-    const bool need_mask = (q0 + 64 > len) || (causal && wfirst + 15 > q0);
-    const int qb0 = q0 + 4 * g;
-    const int lo = (causal ? key : 0) - qb0, hi = len - 1 - qb0;
-    const f32x2 sl = {sl2, sl2};
-#pragma unroll
-    for (int mt = 0; mt < 4; ++mt) {
-      const float4 L4 = *(const float4*)(Ls + 16 * mt + 4 * g);
-      const float4 D4 = *(const float4*)(Dl + 16 * mt + 4 * g);
-      const f32x2 L[2] = {{-L4.x, -L4.y}, {-L4.z, -L4.w}}, Dd[2] = {{D4.x, D4.y}, {D4.z, D4.w}};
-#pragma unroll
-      for (int i = 0; i < 4; i += 2) {
-        const f32x2 t = __builtin_elementwise_fma(f32x2{sc[mt][i], sc[mt][i + 1]}, sl, L[i / 2]);
-        f32x2 p = {exp2f(t.x), exp2f(t.y)};
-        if (need_mask) {
-          const int o = 16 * mt + i;
-          p.x = (o < lo || o > hi) ? 0.f : p.x;
-          p.y = (o + 1 < lo || o + 1 > hi) ? 0.f : p.y;
-        }
-        const f32x2 d = p * (f32x2{dp[mt][i], dp[mt][i + 1]} - Dd[i / 2]);
-        sc[mt][i] = p.x;
-        sc[mt][i + 1] = p.y;
-        dp[mt][i] = d.x;
-        dp[mt][i + 1] = d.y;
-      }
-    }
-    if (drow != nullptr) {
-#pragma unroll
-      for (int mt = 0; mt < 4; ++mt) store4(drow + 16 * mt, dp[mt], 1.f);
-    }
-#pragma unroll
-    for (int ks = 0; ks < 2; ++ks) {
-      const bf16x8 pb = pack_acc(sc[2 * ks], sc[2 * ks + 1]);
-      const bf16x8 db = pack_acc(dp[2 * ks], dp[2 * ks + 1]);
-#pragma unroll
-      for (int dt = 0; dt < 8; ++dt) {
-        dv[dt] = mfma(lds_tr(Os, off.tr[dt] + ks * 32 * ROWB), pb, dv[dt]);
-        dk[dt] = mfma(lds_tr(Qs, off.tr[dt] + ks * 32 * ROWB), db, dk[dt]);
-      }
-    }
-  }
-  if (pre && gtid < 64) {  // the next stage's lse / delta (that stage's last reads ended at the previous barrier)
-    float* Ln = (float*)(nxt + 2 * TB);
-    asm volatile("" : "+v"(pl));  // keeps the multiply (and the loads' wait) after this tile's math
-    Ln[gtid] = pl * LOG2E;
-    Ln[64 + gtid] = pd;
-  }
-}
-
-template <int G, bool LEG = false, bool DMA = false>
-__global__ __launch_bounds__(256 * G, G == 1 ? 2 : 1) void bwd_dkdv5_kernel(
-    const u16* __restrict__ qkv, const u16* __restrict__ dout, const float* __restrict__ lse,
-    const float* __restrict__ delta, const int* __restrict__ cu, u16* __restrict__ dqkv, int nq, int nkv, int total,
-    float sl2, float scale, int causal, u16* __restrict__ dst, int lp, const float* __restrict__ rcos,
-    const float* __restrict__ rsin) {
-  constexpr int NT = 256, TB = 64 * ROWB, GB = 2 * TB + 2 * 64 * 4;  // per group: Q, dO images + lse, delta
-  static_assert(!DMA || !LEG, "the LDS-DMA variant has the current schedule only");
-  __shared__ __attribute__((aligned(16))) char smem[G * GB * (DMA ? 2 : 1)];  // DMA: two stages per group
-  const int tid = threadIdx.x, grp = tid >> 8, gtid = tid & 255;
-  char* Qs = smem + grp * GB * (DMA ? 2 : 1);
-  char* Os = Qs + TB;
-  float* Ls = (float*)(Qs + 2 * TB);
-  float* Dl = Ls + 64;
-  const int kvh = blockIdx.x, b = blockIdx.y, kb = blockIdx.z;
-  const int start = cu[b], len = cu[b + 1] - start;
-  const int k0 = kb * 64;
-  if (k0 >= len) return;
-  const int rep = nq / nkv, hpg = rep / G;  // heads per group
-  const long ld = (long)(nq + 2 * nkv) * D;
-  const long ldo = (long)nq * D;
-  const int lane = tid & 63, wave = (tid >> 6) & 3, g = lane >> 4;
-  const int wfirst = k0 + wave * 16;
-  const int key = wfirst + (lane & 15);
-  const bool kok = key < len;
-  const int qt0 = causal ? kb : 0;
-  const int nqt = (len + 63) / 64;
-  const int nt = nqt - qt0;        // query tiles per head
-  const int niter = hpg * nt;      // the same in every group: the loop's barriers line up
-  Offs off;
-  off.init(lane);
-  // iteration it -> head h = kvh * rep + grp * hpg + it / nt, query tile qt0 + it % nt (kept incrementally)
-  int h = kvh * rep + grp * hpg, qt = qt0;
-  // DMA: lane (wave w, l) fills image rows 4 (w + 4 j) + (l >> 4), position l & 15 with chunk swz(row, l & 15)
-  const int qr0 = 4 * wave + (lane >> 4);
-  const long qoff = 8 * swz(qr0, lane & 15);
-  {
-    const int q0 = qt0 * 64, qv = len - q0;
-    if constexpr (DMA) {
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const long row = start + min(q0 + qr0 + 16 * j, len - 1);
-        lds_dma16(qkv + row * ld + h * D + qoff, Qs + (wave + 4 * j) * 1024);
-        lds_dma16(dout + row * ldo + h * D + qoff, Os + (wave + 4 * j) * 1024);
-      }
-    } else {
-      Stage<64, NT> tq, to;
-      tq.load(qkv + (long)(start + q0) * ld + h * D, ld, qv, gtid);
-      to.load(dout + (long)(start + q0) * ldo + h * D, ldo, qv, gtid);
-      tq.store(Qs, gtid);
-      to.store(Os, gtid);
-    }
-    if (gtid < 64) {
-      Ls[gtid] = gtid < qv ? lse[(long)h * total + start + q0 + gtid] * LOG2E : 0.f;
-      Dl[gtid] = gtid < qv ? delta[(long)h * total + start + q0 + gtid] : 0.f;
-    }
-  }
-  bf16x8 kf[4], vf[4];
-  {
-    const u16* kp = qkv + (long)(start + key) * ld + (nq + kvh) * D + 8 * g;
-    const u16* vp = qkv + (long)(start + key) * ld + (nq + nkv + kvh) * D + 8 * g;
-#pragma unroll
-    for (int s = 0; s < 4; ++s) {
-      kf[s] = load_frag_global(kp + 32 * s, kok);
-      vf[s] = load_frag_global(vp + 32 * s, kok);
-    }
-  }
-  if constexpr (!LEG) vm_drain();  // see vm_drain: K / V fragments are loop-invariant MFMA operands
-  f32x4 dk[8], dv[8];
-#pragma unroll
-  for (int dt = 0; dt < 8; ++dt) {
-    dk[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
-    dv[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
-  }
-  __syncthreads();
-  if constexpr (DMA) {
-    for (int it = 0; it < niter; ++it) {
-      const int q0 = qt * 64;
-      const bool pre = it + 1 < niter;
-      int hn = h, qtn = qt + 1;
-      if (qtn == nqt) {
-        qtn = qt0;
-        ++hn;
-      }
-      const int qn = qtn * 64;
-      const long lo = (long)hn * total + start + qn;
-      const bool lok = pre && qn + gtid < len;
-      char* cur = Qs + (it & 1) * GB;
-      char* nxt = Qs + ((it + 1) & 1) * GB;
-      u16* drow = (dst != nullptr && kok) ? dst + ((long)(b * nq + h) * lp + key) * lp + q0 + 4 * g : nullptr;
-      dkdv_step_dma(cur, nxt, pre, !causal || wfirst <= q0 + 63, qkv + (long)start * ld + hn * D,
-                    dout + (long)start * ldo + hn * D, ld, ldo, qn + qr0, len - 1, qoff, wave,
-                    lok ? lse + lo : nullptr, delta + lo, gtid, q0, len, causal, key, wfirst, g, sl2, drow, off, kf,
-                    vf, dk, dv);
-      if (pre) vm_drain();  // this lane's pieces of the next tile landed ...
-      __syncthreads();      // ... and every lane's; every wave is done reading this stage
-      h = hn;
-      qt = qtn;
-    }
-  }
-  for (int it = 0; it < (DMA ? 0 : niter); ++it) {
-    const int q0 = qt * 64;
-    const bool pre = it + 1 < niter;
-    int hn = h, qtn = qt + 1;
-    if (qtn == nqt) {
-      qtn = qt0;
-      ++hn;
-    }
-    Stage<64, NT> tq, to;
-    float pl = 0.f, pd = 0.f;
-    if (pre) {
-      const int qn = qtn * 64, qv = len - qn;
-      tq.load(qkv + (long)(start + qn) * ld + hn * D, ld, qv, gtid);
-      to.load(dout + (long)(start + qn) * ldo + hn * D, ldo, qv, gtid);
-      if (gtid < 64 && gtid < qv) {
-        // the LOG2E scaling happens at the LDS store: a multiply here made the compiler wait for this load, and
-        // with it (in-order vmcnt) for the Q / dO prefetch issued just before
-        pl = lse[(long)hn * total + start + qn + gtid];
-        if constexpr (LEG) pl *= LOG2E;
-        pd = delta[(long)hn * total + start + qn + gtid];
-      }
-    }
-    if (!causal || wfirst <= q0 + 63) {
-      f32x4 sc[4], dp[4];
-#pragma unroll
-      for (int mt = 0; mt < 4; ++mt) {
-        sc[mt] = f32x4{0.f, 0.f, 0.f, 0.f};
-        dp[mt] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-        for (int s = 0; s < 4; ++s) {
-          sc[mt] = mfma(lds_row(Qs, off.row[s] + mt * 16 * ROWB), kf[s], sc[mt]);
-          dp[mt] = mfma(lds_row(Os, off.row[s] + mt * 16 * ROWB), vf[s], dp[mt]);
-        }
-      }
-      const bool need_mask = (q0 + 64 > len) || (causal && wfirst + 15 > q0);
-      if constexpr (LEG) {
-#pragma unroll
-        for (int mt = 0; mt < 4; ++mt) {
-          const float4 L4 = *(const float4*)(Ls + 16 * mt + 4 * g);
-          const float4 D4 = *(const float4*)(Dl + 16 * mt + 4 * g);
-          const float Lv[4] = {L4.x, L4.y, L4.z, L4.w}, Dv[4] = {D4.x, D4.y, D4.z, D4.w};
-#pragma unroll
-          for (int i = 0; i < 4; ++i) {
-            float p = exp2f(fmaf(sc[mt][i], sl2, -Lv[i]));
-            if (need_mask) {
-              const int q = q0 + 16 * mt + 4 * g + i;
-              if (q >= len || (causal && key > q)) p = 0.f;
-            }
-            sc[mt][i] = p;
-            dp[mt][i] = p * (dp[mt][i] - Dv[i]);
-          }
-        }
-      } else {  // packed fp32 pairs around the exp2; the mask as one compare per score (query offset 16 mt + i
-                // visible iff first <= it <= last)
-        const int qb0 = q0 + 4 * g;
-        const int lo = (causal ? key : 0) - qb0, hi = len - 1 - qb0;
-        const f32x2 sl = {sl2, sl2};
-#pragma unroll
-        for (int mt = 0; mt < 4; ++mt) {
-          const float4 L4 = *(const float4*)(Ls + 16 * mt + 4 * g);
-          const float4 D4 = *(const float4*)(Dl + 16 * mt + 4 * g);
-          const f32x2 L[2] = {{-L4.x, -L4.y}, {-L4.z, -L4.w}}, Dd[2] = {{D4.x, D4.y}, {D4.z, D4.w}};
-#pragma unroll
-          for (int i = 0; i < 4; i += 2) {
-            const f32x2 t = __builtin_elementwise_fma(f32x2{sc[mt][i], sc[mt][i + 1]}, sl, L[i / 2]);
-            f32x2 p = {exp2f(t.x), exp2f(t.y)};
-            if (need_mask) {
-              const int o = 16 * mt + i;
-              p.x = (o < lo || o > hi) ? 0.f : p.x;
-              p.y = (o + 1 < lo || o + 1 > hi) ? 0.f : p.y;
-            }
-            const f32x2 d = p * (f32x2{dp[mt][i], dp[mt][i + 1]} - Dd[i / 2]);
-            sc[mt][i] = p.x;
-            sc[mt][i + 1] = p.y;
-            dp[mt][i] = d.x;
-            dp[mt][i + 1] = d.y;
-          }
-        }
-      }
-      if (dst != nullptr && kok) {
-        u16* drow = dst + ((long)(b * nq + h) * lp + key) * lp + q0 + 4 * g;
-#pragma unroll
-        for (int mt = 0; mt < 4; ++mt) store4(drow + 16 * mt, dp[mt], 1.f);
-      }
-#pragma unroll
-      for (int ks = 0; ks < 2; ++ks) {
-        const bf16x8 pb = pack_acc(sc[2 * ks], sc[2 * ks + 1]);
-        const bf16x8 db = pack_acc(dp[2 * ks], dp[2 * ks + 1]);
-#pragma unroll
-        for (int dt = 0; dt < 8; ++dt) {
-          dv[dt] = mfma(lds_tr(Os, off.tr[dt] + ks * 32 * ROWB), pb, dv[dt]);
-          dk[dt] = mfma(lds_tr(Qs, off.tr[dt] + ks * 32 * ROWB), db, dk[dt]);
-        }
-      }
-    }
-    if (pre) {
-      __syncthreads();
-      tq.store(Qs, gtid);
-      to.store(Os, gtid);
-      if (gtid < 64) {
-        if constexpr (!LEG) asm volatile("" : "+v"(pl));  // keeps the multiply (and the load's wait) here
-        Ls[gtid] = LEG ? pl : pl * LOG2E;
-        Dl[gtid] = pd;
-      }
-    }
-    __syncthreads();
-    h = hn;
-    qt = qtn;
-  }
-  if constexpr (G == 2) {
-    // group 1 -> LDS (fp32, [wave][dt][lane] float4: consecutive lanes, conflict-free) -> group 0 adds.
-    // 2 x 4 waves x 8 x 64 x 16 B = 64 KB = both groups' Q/dO images, free after the loop's last barrier.
-    float4* xk = (float4*)smem;
-    float4* xv = xk + 4 * 8 * 64;
-    if (grp == 1) {
-#pragma unroll
-      for (int dt = 0; dt < 8; ++dt) {
-        xk[(wave * 8 + dt) * 64 + lane] = make_float4(dk[dt][0], dk[dt][1], dk[dt][2], dk[dt][3]);
-        xv[(wave * 8 + dt) * 64 + lane] = make_float4(dv[dt][0], dv[dt][1], dv[dt][2], dv[dt][3]);
-      }
-    }
-    __syncthreads();
-    if (grp == 1) return;
-#pragma unroll
-    for (int dt = 0; dt < 8; ++dt) {
-      const float4 a = xk[(wave * 8 + dt) * 64 + lane], c = xv[(wave * 8 + dt) * 64 + lane];
-      dk[dt] += f32x4{a.x, a.y, a.z, a.w};
-      dv[dt] += f32x4{c.x, c.y, c.z, c.w};
-    }
-  }
-  if (!kok) return;
-  u16* kp = dqkv + (long)(start + key) * ld + (nq + kvh) * D + 4 * g;
-  u16* vp = dqkv + (long)(start + key) * ld + (nq + nkv + kvh) * D + 4 * g;
-  if (rcos != nullptr) {
-    const long tr = (long)(start + key) * (D / 2) + 4 * g;
-    store4_rope_bwd(kp, dk, scale, rcos + tr, rsin + tr);
-#pragma unroll
-    for (int dt = 0; dt < 8; ++dt) store4(vp + 16 * dt, dv[dt], 1.f);
-    return;
-  }
-#pragma unroll
-  for (int dt = 0; dt < 8; ++dt) {
-    store4(kp + 16 * dt, dk[dt], scale);
-    store4(vp + 16 * dt, dv[dt], 1.f);
-  }
-}
-
-// host launcher of the GQA-grouped dK/dV: G = 2 head groups (Q / dO by LDS-DMA) when rep is even, else G = 1
-static void launch_dkdv5(const u16* qkv, const u16* dout, const float* lse, const float* delta, const int* cu,
-                         u16* dqkv, int nq, int nkv, int total, int nseq, int max_seqlen, float sl2, float scale,
-                         int causal, u16* dst, int lp, hipStream_t st, const float* rcos = nullptr,
-                         const float* rsin = nullptr) {
-  const int rep = nq / nkv;
+// host launcher of the GQA-grouped dK/dV: G = 2 head groups when rep is even, else G = 1
+static void launch_dkdv(const u16* qkv, const u16* dout, const float* lse, const float* delta, const int* cu,
+                        u16* dqkv, int nq, int nkv, int total, int nseq, int max_seqlen, float sl2, float scale,
+                        int causal, u16* dst, int lp, hipStream_t st, const float* rcos = nullptr,
+                        const float* rsin = nullptr) {
   dim3 grid(nkv, nseq, (max_seqlen + 63) / 64);
-  const char* e5 = std::getenv("SFTAMD_ATTN_DKDV5");  // A/B against the 16x16x32 dkdv5 (read per call)
-  if (!(e5 && std::strcmp(e5, "1") == 0)) {
-    if (rep % 2 == 0)
-      bwd_dkdv32_kernel<2><<<grid, 256, 0, st>>>(qkv, dout, lse, delta, cu, dqkv, nq, nkv, total, sl2, scale, causal,
-                                                 dst, lp, rcos, rsin);
-    else
-      bwd_dkdv32_kernel<1><<<grid, 128, 0, st>>>(qkv, dout, lse, delta, cu, dqkv, nq, nkv, total, sl2, scale, causal,
-                                                 dst, lp, rcos, rsin);
-    return;
-  }
-  if (rep % 2 == 0)
-    bwd_dkdv5_kernel<2, false, true><<<grid, 512, 0, st>>>(qkv, dout, lse, delta, cu, dqkv, nq, nkv, total, sl2,
-                                                           scale, causal, dst, lp, rcos, rsin);
+  if ((nq / nkv) % 2 == 0)
+    bwd_dkdv32_kernel<2><<<grid, 256, 0, st>>>(qkv, dout, lse, delta, cu, dqkv, nq, nkv, total, sl2, scale, causal,
+                                               dst, lp, rcos, rsin);
   else
-    bwd_dkdv5_kernel<1><<<grid, 256, 0, st>>>(qkv, dout, lse, delta, cu, dqkv, nq, nkv, total, sl2, scale, causal,
-                                              dst, lp, rcos, rsin);
+    bwd_dkdv32_kernel<1><<<grid, 128, 0, st>>>(qkv, dout, lse, delta, cu, dqkv, nq, nkv, total, sl2, scale, causal,
+                                               dst, lp, rcos, rsin);
 }
 
 }  // namespace attn
@@ -1728,7 +909,7 @@ static void check_attn_args(const at::Tensor& qkv, const at::Tensor& cu, int64_t
   SFT_CHECK(cu.scalar_type() == at::kInt && cu.is_cuda() && cu.dim() == 1 && cu.numel() >= 2, "cu_seqlens int32");
 }
 
-// The dq4 backward stores the bf16 dS^T blocks of every (sequence, head) — nseq x nq x lp^2 x 2 bytes (134 MB for
+// The default backward stores the bf16 dS^T blocks of every (sequence, head) — nseq x nq x lp^2 x 2 bytes (134 MB for
 // 16 x 512 tokens, 16 heads); past SFTAMD_ATTN_DS_MB (default 2048, read per call so tests can switch paths
 // in-process) the dq3 kernel recomputes S / dP instead (long contexts).
 static long attn_ds_budget() {
@@ -1736,7 +917,7 @@ static long attn_ds_budget() {
   return (e && e[0] ? atol(e) : 2048L) * 1024L * 1024L;
 }
 
-// forward: fwd3 (8 waves x 16 query rows, K / V staged by LDS-DMA into two stages, one barrier per 64-key tile)
+// forward: fwd32 (4 waves = HW GQA heads x 4 / HW 32-query blocks sharing each K / V tile)
 std::tuple<at::Tensor, at::Tensor> flash_fwd(const at::Tensor& qkv, const at::Tensor& cu, int64_t max_seqlen,
                                              int64_t nq, int64_t nkv, int64_t hd, double scale, bool causal) {
   check_attn_args(qkv, cu, nq, nkv, hd);
@@ -1747,33 +928,25 @@ std::tuple<at::Tensor, at::Tensor> flash_fwd(const at::Tensor& qkv, const at::Te
   if (total == 0 || max_seqlen == 0) return {out, lse};
   const float sl2 = (float)scale * attn::LOG2E;
   auto cu_c = cu.contiguous();
-  const char* e16 = std::getenv("SFTAMD_ATTN_FWD16");  // A/B against the 16x16x32 fwd3 (read per call)
-  const bool use16 = e16 && std::strcmp(e16, "1") == 0;
   const u16* q = (const u16*)qkv.data_ptr();
   u16* o = (u16*)out.data_ptr();
   float* lp = lse.data_ptr<float>();
   const int* cp = cu_c.data_ptr<int>();
   const int ca = causal ? 1 : 0;
-  if (use16) {
-    SFT_TRACE("attn.fwd3");
-    dim3 g3(nq, nseq, (max_seqlen + 127) / 128);
-    attn::fwd3_kernel<8, 32><<<g3, 512, 0, cur_stream()>>>(q, o, lp, cp, nq, nkv, total, sl2, ca);
-  } else {
-    SFT_TRACE("attn.fwd32");
-    const int rep = nq / nkv, hw = rep % 4 == 0 ? 4 : rep % 2 == 0 ? 2 : 1, span = 32 * (4 / hw);
-    dim3 g(nq / hw, nseq, (max_seqlen + span - 1) / span);
-    if (hw == 4) attn::fwd32_kernel<4><<<g, 256, 0, cur_stream()>>>(q, o, lp, cp, nq, nkv, total, sl2, ca);
-    else if (hw == 2) attn::fwd32_kernel<2><<<g, 256, 0, cur_stream()>>>(q, o, lp, cp, nq, nkv, total, sl2, ca);
-    else attn::fwd32_kernel<1><<<g, 256, 0, cur_stream()>>>(q, o, lp, cp, nq, nkv, total, sl2, ca);
-  }
+  SFT_TRACE("attn.fwd32");
+  const int rep = nq / nkv, hw = rep % 4 == 0 ? 4 : rep % 2 == 0 ? 2 : 1, span = 32 * (4 / hw);
+  dim3 g(nq / hw, nseq, (max_seqlen + span - 1) / span);
+  if (hw == 4) attn::fwd32_kernel<4><<<g, 256, 0, cur_stream()>>>(q, o, lp, cp, nq, nkv, total, sl2, ca);
+  else if (hw == 2) attn::fwd32_kernel<2><<<g, 256, 0, cur_stream()>>>(q, o, lp, cp, nq, nkv, total, sl2, ca);
+  else attn::fwd32_kernel<1><<<g, 256, 0, cur_stream()>>>(q, o, lp, cp, nq, nkv, total, sl2, ca);
   SFT_LAUNCH_CHECK();
   return {out, lse};
 }
 
-// backward: delta = rowsum(dO * O); GQA-grouped dK/dV (bwd_dkdv5: all query heads of a kv head in one workgroup, no
-// partials) writing dS^T, then dQ = one product per tile (bwd_dq4); past the dS^T budget dK/dV + the recomputing dq3.
+// backward: delta = rowsum(dO * O); GQA-grouped dK/dV (bwd_dkdv32: all query heads of a kv head in one workgroup, no
+// partials) writing dS^T, then dQ = one product per tile (bwd_dq32); past the dS^T budget dK/dV + the recomputing dq3.
 // rcos / rsin (optional, [total, hd / 2] fp32): the inverse rotate_half RoPE applied to the dq and dk heads in the
-// dq4 / dK epilogues (sets rope_done); the dq3 path leaves it to the caller.
+// dq32 / dK epilogues (sets rope_done); the dq3 path leaves it to the caller.
 static at::Tensor flash_bwd_impl(const at::Tensor& dout, const at::Tensor& qkv, const at::Tensor& out,
                                  const at::Tensor& lse, const at::Tensor& cu, int64_t max_seqlen, int64_t nq,
                                  int64_t nkv, int64_t hd, double scale, bool causal, const float* rcos,
@@ -1801,20 +974,14 @@ static at::Tensor flash_bwd_impl(const at::Tensor& dout, const at::Tensor& qkv, 
   if (ds_bytes <= attn_ds_budget()) {
     auto dst = at::empty({ds_bytes / 2}, qkv.options());
     const bool rope = rcos != nullptr;
-    SFT_TRACE("attn.dkdv5");
-    SFT_TRACE("attn.dq4");
+    SFT_TRACE("attn.dkdv32");
+    SFT_TRACE("attn.dq32");
     if (rope) SFT_TRACE("attn.bwd_rope_epi");
-    attn::launch_dkdv5(q, dO, lse.data_ptr<float>(), delta.data_ptr<float>(), cu_c.data_ptr<int>(),
+    attn::launch_dkdv(q, dO, lse.data_ptr<float>(), delta.data_ptr<float>(), cu_c.data_ptr<int>(),
                        (u16*)dqkv.data_ptr(), nq, nkv, total, nseq, max_seqlen, sl2, (float)scale, causal ? 1 : 0,
                        (u16*)dst.data_ptr(), (int)lp, cur_stream(), rcos, rsin);
     SFT_LAUNCH_CHECK();
-    const char* e5 = std::getenv("SFTAMD_ATTN_DKDV5");  // A/B: the 16x16x32 dkdv5 + dq4 pair (read per call)
-    if (e5 && std::strcmp(e5, "1") == 0) {
-      dim3 gq4(nq, nseq, (max_seqlen + 127) / 128);
-      attn::bwd_dq4_kernel<8><<<gq4, 512, 0, cur_stream()>>>(q, (const u16*)dst.data_ptr(), cu_c.data_ptr<int>(),
-                                                             (u16*)dqkv.data_ptr(), nq, nkv, (int)lp, (float)scale,
-                                                             causal ? 1 : 0, rcos, rsin);
-    } else {
+    {
       const int rep = nq / nkv, hw = rep % 4 == 0 ? 4 : rep % 2 == 0 ? 2 : 1, span = 32 * (4 / hw);
       dim3 g(nq / hw, nseq, (max_seqlen + span - 1) / span);
       const u16* ds = (const u16*)dst.data_ptr();
@@ -1835,7 +1002,7 @@ static at::Tensor flash_bwd_impl(const at::Tensor& dout, const at::Tensor& qkv, 
                                                          cu_c.data_ptr<int>(), (u16*)dqkv.data_ptr(), nq, nkv, total,
                                                          sl2, (float)scale, causal ? 1 : 0);
   SFT_LAUNCH_CHECK();
-  attn::launch_dkdv5(q, dO, lse.data_ptr<float>(), delta.data_ptr<float>(), cu_c.data_ptr<int>(),
+  attn::launch_dkdv(q, dO, lse.data_ptr<float>(), delta.data_ptr<float>(), cu_c.data_ptr<int>(),
                      (u16*)dqkv.data_ptr(), nq, nkv, total, nseq, max_seqlen, sl2, (float)scale, causal ? 1 : 0,
                      nullptr, 0, cur_stream());
   SFT_LAUNCH_CHECK();

@@ -682,21 +682,4 @@ void g4_dgrad(const at::Tensor& dy, const at::Tensor& w, u16* out, long ldo, con
   }
 }
 
-// Forward layout C[M, N] = a[M, K] . w[N, K]^T (both operands K-contiguous: ROW / ROW) on the same 4-wave kernel,
-// plain bf16 store (gemm_tn cfg 60 = ring, 61 = pair loop).
-void g4_tn(const at::Tensor& a, const at::Tensor& w, at::Tensor& c, bool ring) {
-  const int M = a.size(0), K = a.size(1), N = w.size(0);
-  SFT_CHECK(M % 256 == 0 && N % 256 == 0 && K % 128 == 0 && K > 0, "gemm_tn 4-wave: M, N % 256, K % 128");
-  g4::Epi ea{};
-  ea.C = (u16*)c.data_ptr();
-  ea.ldc = c.stride(0);
-  const int tiles = (M / 256) * (N / 256);
-  if (ring)
-    g4::launch<g4::ROW, g4::ROW, g4::EPI_STORE, true>((const u16*)a.data_ptr(), a.stride(0), (const u16*)w.data_ptr(),
-                                                      w.stride(0), M, N, K, tiles, 1, ea);
-  else
-    g4::launch<g4::ROW, g4::ROW, g4::EPI_STORE, false>((const u16*)a.data_ptr(), a.stride(0), (const u16*)w.data_ptr(),
-                                                       w.stride(0), M, N, K, tiles, 1, ea);
-}
-
 }  // namespace sftamd

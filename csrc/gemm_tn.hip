@@ -1164,12 +1164,8 @@ struct Stager5 {
   unsigned va, vb;       // lane byte offsets (A: within the tile's rows; B: within the weight)
   unsigned a32;          // bytes between A pieces j, j + 1 (32 rows)
   unsigned boff[8];      // B piece q relative to piece 0 (EPI row permutation), bytes
-  unsigned kb;           // K progress, bytes (wraps at kbytes: a staggered K start walks k0 .. K, 0 .. k0)
-  unsigned kbytes;       // K * 2
-  __device__ __forceinline__ void adv(int k) {
-    kb += 2 * k;
-    kb = kb >= kbytes ? kb - kbytes : kb;
-  }
+  unsigned kb;           // K progress, bytes
+  __device__ __forceinline__ void adv(int k) { kb += 2 * k; }
   __device__ __forceinline__ void piece(char* stage, int w, int j, int koff = 0) {
     char* dst = stage + (w + 4 * j) * 1024;
     if (j < 8)
@@ -1216,28 +1212,14 @@ __device__ __forceinline__ void tn5_sub(f32x4 (&acc)[8][8], const bf16x8 (&fa)[8
   }
 }
 
-// StaggerU-style K start (VAR & 6): tiles that share an A or B panel start their K loops at different 256-byte
-// (K-tile pair) offsets, so the workgroups of an XCD do not all hit the same K slice of a panel (and the same HBM
-// channels: K = 2048 rows are 4 KB apart) at the same moment. S offsets over the tile's (m, n) block indices.
-template <int VAR>
-__device__ __forceinline__ unsigned tn5_kstart(int m0, int n0, int npair) {
-  if constexpr ((VAR & 6) == 0) {
-    return 0u;
-  } else {
-    constexpr int S = (VAR & 4) ? 16 : 4;
-    const int s = ((m0 >> 8) + 3 * (n0 >> 8)) % S;
-    return (unsigned)((s % npair) * 256);
-  }
-}
-
 template <int EPI>
 __device__ __forceinline__ void tn5_stager(Stager5<EPI>& st, const u16* A, const u16* B, long lda, long ldb, int m0,
-                                           int n0, int w, int lane, int I, unsigned kb0 = 0) {
+                                           int n0, int w, int lane, int I) {
   const int lr = lane >> 3, ch = (lane & 7) ^ (4 * (w & 1) + (lr >> 1));
   st.ra = tile_rsrc(A + (long)m0 * lda);
   st.va = (unsigned)(((8 * w + lr) * lda + 8 * ch) * 2);
   st.vb = (unsigned)(((long)(b2_row<EPI>(w, n0, I) + lr) * ldb + 8 * ch) * 2);
-  st.kb = kb0;
+  st.kb = 0;
 }
 
 __device__ __forceinline__ void tn5_coords(int tile, int nbm, int nbn, int group, int& m0, int& n0) {
@@ -1256,27 +1238,12 @@ __device__ __forceinline__ unsigned pack2(float a, float b) { return (unsigned)f
 // one lane): rotate in registers (bf16 projection values, as the unfused path sees them), then pair lo / hi with
 // permlane16_swap — 32 stores. SWIGLU (fragments 2q / 2q + 1 = gate / up of the same act columns): gate / up paired
 // with each other, act (q) with act (q + 1) — 48 stores.
-// 16-byte epilogue store; NT: non-temporal (streaming; what hipBLASLt's epilogue issues: `buffer_store_dwordx4 ...
-// nt`). Measured on the persistent kernel, gate_up M = 8192: 0.579 vs 0.648 ms (profiles/r4_gemm_fwd.md).
-template <bool NT>
-__device__ __forceinline__ void st16(void* dst, const uint4& val) {
-  if constexpr (NT) {
-    typedef unsigned u32x4v __attribute__((ext_vector_type(4)));
-    __builtin_nontemporal_store(u32x4v{val.x, val.y, val.z, val.w}, (u32x4v*)dst);
-  } else {
-    *(uint4*)dst = val;
-  }
-}
-
-template <int EPI, int SV = 0>
+template <int EPI>
 __device__ __forceinline__ void tn5_store(f32x4 (&acc)[8][8], const EpiArgs& ea, int row0, int m_col0, int wn,
                                           int lane) {
   const int g = lane >> 4, ii = lane & 15;
   if constexpr (EPI == EPI_PLAIN) {
     u16* base = ea.C + (long)(row0 + ii) * ea.ldc + m_col0 + 16 * (g & 1) + 4 * (g & 2);
-    // SV & 2: timing experiment only (wrong placement): the same 32 stores per lane in hipBLASLt's pattern, each
-    // instruction 4 rows x 256 contiguous bytes instead of 16 rows x 64 bytes
-    u16* base2 = ea.C + (long)(row0 + 32 * g) * ea.ldc + m_col0 + 8 * ii;
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
 #pragma unroll
@@ -1286,9 +1253,7 @@ __device__ __forceinline__ void tn5_store(f32x4 (&acc)[8][8], const EpiArgs& ea,
         unsigned w1 = pack2(acc[i][2 * p + 1][2], acc[i][2 * p + 1][3]);
         auto r0 = __builtin_amdgcn_permlane16_swap(v0, w0, false, false);
         auto r1 = __builtin_amdgcn_permlane16_swap(v1, w1, false, false);
-        uint4* dst = (SV & 2) ? (uint4*)(base2 + (long)(4 * i + p) * ea.ldc)
-                              : (uint4*)(base + (long)(16 * i) * ea.ldc + 32 * p);
-        st16<(SV & 1) != 0>(dst, make_uint4(r0[0], r1[0], r0[1], r1[1]));
+        *(uint4*)(base + (long)(16 * i) * ea.ldc + 32 * p) = make_uint4(r0[0], r1[0], r0[1], r1[1]);
       }
     }
   } else if constexpr (EPI == EPI_ROPE) {
@@ -1319,7 +1284,7 @@ __device__ __forceinline__ void tn5_store(f32x4 (&acc)[8][8], const EpiArgs& ea,
         }
         auto r0 = __builtin_amdgcn_permlane16_swap(pack2(lo[0], lo[1]), pack2(hi[0], hi[1]), false, false);
         auto r1 = __builtin_amdgcn_permlane16_swap(pack2(lo[2], lo[3]), pack2(hi[2], hi[3]), false, false);
-        st16<(SV & 1) != 0>(base + (long)(16 * i) * ea.ldc + 16 * q, make_uint4(r0[0], r1[0], r0[1], r1[1]));
+        *(uint4*)(base + (long)(16 * i) * ea.ldc + 16 * q) = make_uint4(r0[0], r1[0], r0[1], r1[1]);
       }
     }
   } else {  // SWIGLU: m_col0 = first act column of the wave
@@ -1342,74 +1307,41 @@ __device__ __forceinline__ void tn5_store(f32x4 (&acc)[8][8], const EpiArgs& ea,
           }
           auto r0 = __builtin_amdgcn_permlane16_swap(pack2(ga[0], ga[1]), pack2(up[0], up[1]), false, false);
           auto r1 = __builtin_amdgcn_permlane16_swap(pack2(ga[2], ga[3]), pack2(up[2], up[3]), false, false);
-          st16<(SV & 1) != 0>(gu + (long)(16 * i) * ea.ldc + 16 * q, make_uint4(r0[0], r1[0], r0[1], r1[1]));
+          *(uint4*)(gu + (long)(16 * i) * ea.ldc + 16 * q) = make_uint4(r0[0], r1[0], r0[1], r1[1]);
           a01[h] = pack2(o[0], o[1]);
           a23[h] = pack2(o[2], o[3]);
         }
         auto r0 = __builtin_amdgcn_permlane16_swap(a01[0], a01[1], false, false);
         auto r1 = __builtin_amdgcn_permlane16_swap(a23[0], a23[1], false, false);
-        st16<(SV & 1) != 0>(ac + (long)(16 * i) * ea.I + 32 * qq, make_uint4(r0[0], r1[0], r0[1], r1[1]));
+        *(uint4*)(ac + (long)(16 * i) * ea.I + 32 * qq) = make_uint4(r0[0], r1[0], r0[1], r1[1]);
       }
     }
   }
 }
 
-// VAR: bit 0 = timing ablation, no epilogue stores (wrong results); bits 1 / 2 = staggered K start over 4 / 16
-// offsets (tn5_kstart). Launched with one workgroup per CU (persistent) or one per tile (the same code: a workgroup
-// whose next tile is past its XCD's range ends after one tile).
-// Dynamic tile queue (VAR & 128): the XCD ranges of the static order become 8 work counters (one per XCD) that the
-// workgroups draw tiles from (their own XCD's first, then the others': whatever is left), so workgroups that start
-// late — CUs held by a concurrent kernel such as the overlapped AdamW — take fewer tiles instead of stretching the
-// launch by their whole static share. One returning atomic per tile, issued by wave 0 lane 0 where its wave has no
-// vector-memory operation outstanding (its return then costs no wait on the DMA / stores), published through the
-// staging array's spare bytes behind the next barrier. The counters live in a per-launch slot of a device ring; the
-// last workgroup to finish resets its slot (the next launch on any stream that gets the slot is ordered after this
-// one completes: the ring holds 64 slots, handed out round-robin by the host).
+// Launched with one workgroup per CU (persistent): each walks its XCD's contiguous share of the tile order.
 __device__ __forceinline__ int tn5_range_start(int x, int tiles) {
   const int q8 = tiles >> 3, r8 = tiles & 7;
   return x * q8 + min(x, r8);
 }
-__device__ __forceinline__ int tn5_grab(int* wq, int own, int tiles) {
-#pragma unroll 1
-  for (int i = 0; i < 8; ++i) {
-    const int x = (own + i) & 7;
-    const int s0 = tn5_range_start(x, tiles), len = tn5_range_start(x + 1, tiles) - s0;
-    const int t = __hip_atomic_fetch_add(wq + x, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (t < len) return s0 + t;
-  }
-  return -1;
-}
 
-template <int EPI, bool NK2, int VAR = 0>
+template <int EPI, bool NK2>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1)))
 tn5_kernel(const u16* __restrict__ A, const u16* __restrict__ B, int K, long lda, long ldb, int nbm, int nbn,
-           int group, EpiArgs ea, int* __restrict__ wq) {
+           int group, EpiArgs ea) {
   using G = Cfg2<256, 256, 2, 2, 2>;
-  constexpr bool DYN = (VAR & 128) && !NK2;  // a one-pair tile has no barrier between the grab and its use
   // The next tile's K0 AND K1 go out in the last sub-step (both stages are free then), the epilogue's NST stores after
   // them: the next tile waits vmcnt(NST + 16) (PLAIN / ROPE) or vmcnt(NST) (SWIGLU, 48 stores: the counter holds 63)
   // for K0, and its first boundary only vmcnt(NST) for K1 — the stores drain under its first K-tile.
   constexpr int NST = EPI == EPI_SWIGLU ? 48 : 32;
-  __shared__ __attribute__((aligned(16))) char smem[2 * G::STAGE + 16];  // + the dynamic queue's published tile
-  volatile int* slot = (volatile int*)(smem + 2 * G::STAGE);
+  __shared__ __attribute__((aligned(16))) char smem[2 * G::STAGE];
   const int tiles = nbm * nbn, nwg = gridDim.x, orig = blockIdx.x;
   // this XCD's contiguous share of the tile order, walked round-robin by its workgroups (blocks b, b + 8, ...)
   const int xcd = orig & 7, l = orig >> 3, nx = (nwg - xcd + 7) >> 3;
   const int t_end = tn5_range_start(xcd + 1, tiles);
   int tile = tn5_range_start(xcd, tiles) + l;
   const int tid = threadIdx.x, lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6);
-  if constexpr (DYN) {
-    if (tid == 0) *slot = tn5_grab(wq, xcd, tiles);
-    __syncthreads();
-    tile = __builtin_amdgcn_readfirstlane(*slot);
-    if (tile < 0) {
-      if (tid == 0 && __hip_atomic_fetch_add(wq + 8, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == nwg - 1)
-        for (int i = 0; i < 9; ++i) __hip_atomic_store(wq + i, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      return;
-    }
-  } else {
-    if (tile >= t_end) return;
-  }
+  if (tile >= t_end) return;
   const int wm = w >> 1, wn = w & 1;
   const int nk = K / BK2;
   const int g = lane >> 4, ii = lane & 15;
@@ -1421,12 +1353,11 @@ tn5_kernel(const u16* __restrict__ A, const u16* __restrict__ B, int K, long lda
   Stager5<EPI> st;
   st.rb = tile_rsrc(B);
   st.a32 = (unsigned)(64 * lda);
-  st.kbytes = (unsigned)(2 * K);
 #pragma unroll
   for (int q = 0; q < 8; ++q) st.boff[q] = (unsigned)(b2_koff<EPI, 4>(q) * ldb * 2);
   int m0, n0;
   tn5_coords(tile, nbm, nbn, group, m0, n0);
-  tn5_stager(st, A, B, lda, ldb, m0, n0, w, lane, ea.I, tn5_kstart<VAR>(m0, n0, nk / 2));
+  tn5_stager(st, A, B, lda, ldb, m0, n0, w, lane, ea.I);
 #pragma unroll
   for (int j = 0; j < 16; ++j) st.piece(X, w, j);
   st.adv(BK2);
@@ -1434,14 +1365,9 @@ tn5_kernel(const u16* __restrict__ A, const u16* __restrict__ B, int K, long lda
   for (int j = 0; j < 16; ++j) st.piece(Y, w, j);
   st.adv(BK2);
   __builtin_amdgcn_s_waitcnt(waitcnt_imm(16, 15));  // K0 of the first tile (its K1 may fly)
-  if constexpr (VAR & 8) {  // experiment: desynchronise the workgroups' tile boundaries by a start delay
-    const long long t0 = clock64(), d = (long long)(l & 15) * 3000;
-    while (clock64() - t0 < d) __builtin_amdgcn_s_sleep(4);
-  }
   f32x4 acc[8][8];
   bf16x8 a0[8], b0[8], a1[8], b1[8];
   bool first = true;
-  int grabbed = -1;
   for (;;) {
     __builtin_amdgcn_s_barrier();
 #pragma unroll
@@ -1449,10 +1375,10 @@ tn5_kernel(const u16* __restrict__ A, const u16* __restrict__ B, int K, long lda
       a0[i] = lds_row(X, offA0 + 2048 * i);
       b0[i] = lds_row(X, offB0 + 2048 * i);
     }
-    int next = tile + nx;
-    bool has_next = next < t_end;
+    const int next = tile + nx;
+    const bool has_next = next < t_end;
     int m1 = m0, n1 = n0;
-    if (!DYN && has_next) tn5_coords(next, nbm, nbn, group, m1, n1);
+    if (has_next) tn5_coords(next, nbm, nbn, group, m1, n1);
     // K-tile pairs (t on X, t + 1 on Y); boundary = vmcnt(0) lgkmcnt(0) + the barrier after the next sub-step's
     // first MFMA group. LAST: the final sub-step DMAs the next tile's K0 into X (the current tile's K0 again when
     // there is none: branch-free, harmless) and reads nothing.
@@ -1472,23 +1398,12 @@ tn5_kernel(const u16* __restrict__ A, const u16* __restrict__ B, int K, long lda
       __builtin_amdgcn_s_waitcnt(waitcnt_imm(63, 0));
       tn5_sub<EPI, false, true, 0, false>(acc, a0, b0, a1, b1, Y, offA1, offB1, st, Y, w);
       __builtin_amdgcn_s_waitcnt(waitcnt_imm(0, 0));
-      if constexpr (DYN && IN) {  // no VMEM outstanding here: draw the next tile (its return waits for nothing else)
-        if (tid == 0) grabbed = tn5_grab(wq, xcd, tiles);
-      }
-      if constexpr (DYN && LA) {  // published behind the barrier of an earlier sub-step of this tile
-        next = __builtin_amdgcn_readfirstlane(*slot);
-        has_next = next >= 0;
-        if (has_next) tn5_coords(next, nbm, nbn, group, m1, n1);
-      }
       if constexpr (LA) {
-        tn5_stager(st, A, B, lda, ldb, m1, n1, w, lane, ea.I, tn5_kstart<VAR>(m1, n1, nk / 2));
+        tn5_stager(st, A, B, lda, ldb, m1, n1, w, lane, ea.I);
         tn5_sub<EPI, false, false, 32, true>(acc, a1, b1, a0, b0, X, offA0, offB0, st, X, w, Y);
       } else {
         tn5_sub<EPI, false, true, 16, true>(acc, a1, b1, a0, b0, X, offA0, offB0, st, Y, w);
         st.adv(BK2);
-        if constexpr (DYN && IN) {
-          if (tid == 0) *slot = grabbed;  // read after the next pair's first barrier
-        }
       }
     };
     if constexpr (NK2) {
@@ -1501,25 +1416,9 @@ tn5_kernel(const u16* __restrict__ A, const u16* __restrict__ B, int K, long lda
     // the epilogue's accumulator reads follow the last MFMAs: 20 wait states + a fence against hoisting
     asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 3" ::: "memory");
     __builtin_amdgcn_sched_barrier(0);
-    if constexpr (VAR & 1) {  // timing only: no stores (one value per lane keeps the accumulators live)
-      float sum = 0.f;
-#pragma unroll
-      for (int i = 0; i < 8; ++i)
-#pragma unroll
-        for (int j = 0; j < 8; ++j) sum += acc[i][j][0] + acc[i][j][1] + acc[i][j][2] + acc[i][j][3];
-      if (sum == 1.2345f) ea.C[tid] = 1;
-    } else {
-      tn5_store<EPI, (VAR >> 4) & 3>(acc, ea, m0 + wm * 128, EPI == EPI_SWIGLU ? (n0 >> 1) + 64 * wn : n0 + wn * 128,
-                                      wn, lane);
-    }
+    tn5_store<EPI>(acc, ea, m0 + wm * 128, EPI == EPI_SWIGLU ? (n0 >> 1) + 64 * wn : n0 + wn * 128, wn, lane);
     __builtin_amdgcn_sched_barrier(0);
-    if (!has_next) {
-      if constexpr (DYN) {  // every workgroup has drawn its last tile once the done counter reaches nwg: reset the slot
-        if (tid == 0 && __hip_atomic_fetch_add(wq + 8, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == nwg - 1)
-          for (int i = 0; i < 9; ++i) __hip_atomic_store(wq + i, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      }
-      break;
-    }
+    if (!has_next) break;
     st.adv(2 * BK2);
     if constexpr (EPI == EPI_SWIGLU)
       __builtin_amdgcn_s_waitcnt(waitcnt_imm(NST, 15));  // K0 and K1 landed (the 48 stores may fly)
@@ -1533,37 +1432,20 @@ tn5_kernel(const u16* __restrict__ A, const u16* __restrict__ B, int K, long lda
   __builtin_amdgcn_s_waitcnt(waitcnt_imm(0, 15));
 }
 
-constexpr int TN5_DEFAULT = 16 | 2;  // nt epilogue stores + staggered K start (4 offsets)
-
-// per-device ring of 64 work-queue slots (8 XCD counters + a done counter each, 64 B apart), zeroed once; a slot is
-// reset by the last workgroup of the launch that used it
-static int* tn5_queue_slot() {
-  constexpr int NSLOT = 64, SLOT_INTS = 16;
-  static at::Tensor ring[16];
-  static int seq[16];
-  const int dev = c10::hip::current_device();
-  if (!ring[dev].defined())
-    ring[dev] = at::zeros({NSLOT * SLOT_INTS}, at::TensorOptions().dtype(at::kInt).device(at::kCUDA, dev));
-  const int s = seq[dev]++ % NSLOT;
-  return ring[dev].data_ptr<int>() + s * SLOT_INTS;
-}
-
-template <int EPI, int VAR = 0>
-void launch5(const at::Tensor& a, const at::Tensor& w, int N, const EpiArgs& ea, bool persistent = true) {
+template <int EPI>
+void launch5(const at::Tensor& a, const at::Tensor& w, int N, const EpiArgs& ea) {
   const int M = a.size(0), K = a.size(1);
   SFT_CHECK(M % 256 == 0 && N % 256 == 0 && K % 128 == 0, "gemm_tn persistent: M, N % 256, K % 128");
   SFT_CHECK(ea.ldc % 8 == 0 && ((uintptr_t)ea.C) % 16 == 0, "gemm_tn persistent: 16-byte aligned output rows");
   const int nbm = M / 256, nbn = N / 256, tiles = nbm * nbn;
-  // one workgroup per tile: round the grid up to whole XCD rows so every XCD's range is covered one tile per block
-  const int grid = persistent ? std::min(tiles, num_cus()) : (tiles + 7) / 8 * 8;
+  const int grid = std::min(tiles, num_cus());
   const int grp = std::min(group_m(), nbm);
-  int* wq = ((VAR & 128) && K != 128) ? tn5_queue_slot() : nullptr;
   if (K == 128)
-    tn5_kernel<EPI, true, VAR><<<grid, 256, 0, cur_stream()>>>((const u16*)a.data_ptr(), (const u16*)w.data_ptr(), K,
-                                                               a.stride(0), w.stride(0), nbm, nbn, grp, ea, wq);
+    tn5_kernel<EPI, true><<<grid, 256, 0, cur_stream()>>>((const u16*)a.data_ptr(), (const u16*)w.data_ptr(), K,
+                                                          a.stride(0), w.stride(0), nbm, nbn, grp, ea);
   else
-    tn5_kernel<EPI, false, VAR><<<grid, 256, 0, cur_stream()>>>((const u16*)a.data_ptr(), (const u16*)w.data_ptr(), K,
-                                                                a.stride(0), w.stride(0), nbm, nbn, grp, ea, wq);
+    tn5_kernel<EPI, false><<<grid, 256, 0, cur_stream()>>>((const u16*)a.data_ptr(), (const u16*)w.data_ptr(), K,
+                                                           a.stride(0), w.stride(0), nbm, nbn, grp, ea);
   SFT_LAUNCH_CHECK();
 }
 
@@ -1609,93 +1491,32 @@ static void check_tn(const at::Tensor& a, const at::Tensor& w) {
   SFT_CHECK(a.size(0) % 256 == 0 && a.size(1) % tn::BK == 0 && a.size(1) > 0, "gemm_tn: M % 256, K % 32");
 }
 
-void g4_tn(const at::Tensor& a, const at::Tensor& w, at::Tensor& c, bool ring);
-
-// cfg: 0 = 256x256 BK32 ring (NS 5), 1 = 256x128 BK32 ring (NS 6), 2 = 256x256 BK64 (NS 2; the fastest on the
-// SmolLM3 shapes, tools/bench_gemm_tn.py), 3 = BK64 early-release ring, 4 = BK64 with a pinned MFMA/DS/DMA
-// interleave (3 and 4 measured slower; kept for the microbench), 5 = BK64 transposed-C epilogue, 6 / 7 = BK64
-// 256x128 tiles with 3 / 2 LDS stages (twice the workgroups: 3 full waves on qkv's 384-tile grid)
+// cfg: 0 = 256x256 BK32 ring (NS 5; any K % 32), 2 = 256x256 BK64 (NS 2), 5 = BK64 transposed-C epilogue, 6 = BK64
+// 256x128 tiles with 3 LDS stages (twice the workgroups; the qkv + RoPE tail), 11 = the ping-pong 8-phase schedule
+// (transposed-C, D = 2; the default for qkv + RoPE), 12 = 4 waves of 128 x 128 (one wave per SIMD, AGPR accumulators),
+// 164 = the persistent 4-wave kernel (the LoRA wide GEMM). Measurements: profiles/r1_gemm_tn.md, r2_gemm_pingpong.md,
+// r3_gemm_4wave.md, r4_gemm_fwd.md.
 at::Tensor gemm_tn(const at::Tensor& a, const at::Tensor& w, int64_t cfg) {
   check_tn(a, w);
   SFT_TRACE(trace_name("tn.c", cfg));
   const int M = a.size(0), N = w.size(0);
   auto c = at::empty({M, N}, a.options());
   tn::EpiArgs ea{(u16*)c.data_ptr(), nullptr, nullptr, nullptr, (long)N, 0, 0};
-  if (cfg == 1) {
-    SFT_CHECK(N % 128 == 0, "gemm_tn 256x128: N % 128");
-    tn::launch<256, 128, 4, 2, 6, tn::EPI_PLAIN>(a, w, N, ea);
-  } else if (cfg == 2 || cfg == 3) {
-    SFT_CHECK(N % 256 == 0 && a.size(1) % 64 == 0, "gemm_tn BK64: N % 256, K % 64");
+  const bool k64 = a.size(1) % 64 == 0;
+  if (cfg == 2 || cfg == 5 || cfg == 11) {
+    SFT_CHECK(N % 256 == 0 && k64, "gemm_tn BK64: N % 256, K % 64");
     if (cfg == 2) tn::launch2<256, 256, 2, 4, 2, tn::EPI_PLAIN>(a, w, N, ea);
-    else tn::launch2<256, 256, 2, 4, 2, tn::EPI_PLAIN, 1>(a, w, N, ea);
-  } else if (cfg == 5) {  // BK64, transposed-C fragments, packed-bf16 LDS epilogue
-    SFT_CHECK(N % 256 == 0 && a.size(1) % 64 == 0, "gemm_tn BK64: N % 256, K % 64");
-    tn::launch2<256, 256, 2, 4, 2, tn::EPI_PLAIN, 3>(a, w, N, ea);
-  } else if (cfg == 6 || cfg == 7) {  // BK64 256x128 tiles (64x64 per wave): 3 (cfg 6) or 2 LDS stages
-    SFT_CHECK(N % 128 == 0 && a.size(1) % 64 == 0, "gemm_tn BK64 256x128: N % 128, K % 64");
-    if (cfg == 6) tn::launch2<256, 128, 4, 2, 3, tn::EPI_PLAIN>(a, w, N, ea);
-    else tn::launch2<256, 128, 4, 2, 2, tn::EPI_PLAIN>(a, w, N, ea);
-  } else if (cfg >= 8 && cfg <= 11) {  // ping-pong 8-phase schedule (9, 11: transposed-C epilogue; 10, 11: D = 2)
-    SFT_CHECK(N % 256 == 0 && a.size(1) % 64 == 0, "gemm_tn ping-pong: N % 256, K % 64");
-    if (cfg == 8) tn::launch3<tn::EPI_PLAIN, false, 1>(a, w, N, ea);
-    else if (cfg == 9) tn::launch3<tn::EPI_PLAIN, true, 1>(a, w, N, ea);
-    else if (cfg == 10) tn::launch3<tn::EPI_PLAIN, false, 2>(a, w, N, ea);
+    else if (cfg == 5) tn::launch2<256, 256, 2, 4, 2, tn::EPI_PLAIN, 3>(a, w, N, ea);
     else tn::launch3<tn::EPI_PLAIN, true, 2>(a, w, N, ea);
-  } else if (cfg == 12) {  // 4 waves of 128 x 128 (one wave per SIMD, accumulators pinned in AGPRs), VAR 4
+  } else if (cfg == 6) {
+    SFT_CHECK(N % 128 == 0 && k64, "gemm_tn BK64 256x128: N % 128, K % 64");
+    tn::launch2<256, 128, 4, 2, 3, tn::EPI_PLAIN>(a, w, N, ea);
+  } else if (cfg == 12) {
     tn::launch4<tn::EPI_PLAIN, 0, 4>(a, w, N, ea);
-  } else if (cfg == 60 || cfg == 61) {  // csrc/gemm_4w.hip: 4-slot ring of 32-deep steps (60) / 64-deep pairs (61)
-    g4_tn(a, w, c, cfg == 60);
-  } else if (cfg == 50) {  // persistent 4-wave (register epilogue with nt stores, next tile's loads under this tile's
-    tn::launch5<tn::EPI_PLAIN, tn::TN5_DEFAULT>(a, w, N, ea);  // end, K start staggered over 4 offsets)
-  } else if (cfg == 164) {  // the round-3 persistent kernel (plain stores, no stagger) for A/B runs
-    tn::launch5<tn::EPI_PLAIN, 0>(a, w, N, ea);
-  } else if (cfg == 165) {  // persistent with the dynamic tile queue (plain stores)
-    tn::launch5<tn::EPI_PLAIN, 128>(a, w, N, ea);
-  } else if ((cfg >= 51 && cfg <= 59) || (cfg >= 160 && cfg <= 163)) {  // tn5 variants (one tile per workgroup / staggered K start / no stores)
-    switch (cfg) {
-      case 51: tn::launch5<tn::EPI_PLAIN, 0>(a, w, N, ea, false); break;
-      case 52: tn::launch5<tn::EPI_PLAIN, 2>(a, w, N, ea); break;
-      case 53: tn::launch5<tn::EPI_PLAIN, 4>(a, w, N, ea); break;
-      case 54: tn::launch5<tn::EPI_PLAIN, 1>(a, w, N, ea); break;  // timing only: no stores
-      case 55: tn::launch5<tn::EPI_PLAIN, 2>(a, w, N, ea, false); break;
-      case 56: tn::launch5<tn::EPI_PLAIN, 1>(a, w, N, ea, false); break;  // timing only
-      case 58: tn::launch5<tn::EPI_PLAIN, 10>(a, w, N, ea); break;  // stagger 4 + start delay (experiment)
-      case 60 + 100: tn::launch5<tn::EPI_PLAIN, 16>(a, w, N, ea); break;      // nt stores
-      case 61 + 100: tn::launch5<tn::EPI_PLAIN, 32>(a, w, N, ea); break;      // hipBLASLt store pattern (timing only)
-      case 62 + 100: tn::launch5<tn::EPI_PLAIN, 48>(a, w, N, ea); break;      // both (timing only)
-      case 63 + 100: tn::launch5<tn::EPI_PLAIN, 16 + 2>(a, w, N, ea); break;  // nt + stagger 4
-      case 59: tn::launch5<tn::EPI_PLAIN, 8>(a, w, N, ea); break;   // start delay (experiment)
-      default: tn::launch5<tn::EPI_PLAIN, 4>(a, w, N, ea, false); break;
-    }
-  } else if (cfg >= 13 && cfg <= 44) {  // cfg 12 schedule variants (tn4_kernel VAR = cfg - 12)
-    switch (cfg - 12) {
-      case 1: tn::launch4<tn::EPI_PLAIN, 0, 1>(a, w, N, ea); break;
-      case 4: tn::launch4<tn::EPI_PLAIN, 0, 4>(a, w, N, ea); break;
-      case 32: tn::launch4<tn::EPI_PLAIN, 0, 0>(a, w, N, ea); break;  // cfg 44: the first (VAR 0) schedule
-      case 8: tn::launch4<tn::EPI_PLAIN, 0, 8>(a, w, N, ea); break;
-      case 9: tn::launch4<tn::EPI_PLAIN, 0, 9>(a, w, N, ea); break;
-      case 12: tn::launch4<tn::EPI_PLAIN, 0, 12>(a, w, N, ea); break;
-      case 13: tn::launch4<tn::EPI_PLAIN, 0, 13>(a, w, N, ea); break;
-      case 16: tn::launch4<tn::EPI_PLAIN, 0, 16>(a, w, N, ea); break;
-      default: SFT_CHECK(false, "gemm_tn: 4-wave variant cfg ", cfg, " not built");
-    }
-  } else if (cfg >= 1201 && cfg <= 1231) {  // timing-only ablations of cfg 12 (wrong results)
-    switch (cfg - 1200) {
-      case 8: tn::launch4<tn::EPI_PLAIN, 8, 4>(a, w, N, ea); break;
-      case 16: tn::launch4<tn::EPI_PLAIN, 16, 4>(a, w, N, ea); break;
-      case 24: tn::launch4<tn::EPI_PLAIN, 24, 4>(a, w, N, ea); break;
-      case 1: tn::launch4<tn::EPI_PLAIN, 1>(a, w, N, ea); break;
-      case 2: tn::launch4<tn::EPI_PLAIN, 2>(a, w, N, ea); break;
-      case 3: tn::launch4<tn::EPI_PLAIN, 3>(a, w, N, ea); break;
-      case 4: tn::launch4<tn::EPI_PLAIN, 4>(a, w, N, ea); break;
-      case 5: tn::launch4<tn::EPI_PLAIN, 5>(a, w, N, ea); break;
-      case 6: tn::launch4<tn::EPI_PLAIN, 6>(a, w, N, ea); break;
-      default: tn::launch4<tn::EPI_PLAIN, 7>(a, w, N, ea); break;
-    }
-  } else if (cfg == 4) {  // BK64 with sched_group_barrier interleave pinned (measured slower: diagnostics)
-    SFT_CHECK(N % 256 == 0 && a.size(1) % 64 == 0, "gemm_tn BK64: N % 256, K % 64");
-    tn::launch2<256, 256, 2, 4, 2, tn::EPI_PLAIN, 2>(a, w, N, ea);
+  } else if (cfg == 164) {
+    tn::launch5<tn::EPI_PLAIN>(a, w, N, ea);
   } else {
+    SFT_CHECK(cfg == 0, "gemm_tn: cfg ", cfg, " not built (0, 2, 5, 6, 11, 12, 164)");
     SFT_CHECK(N % 256 == 0, "gemm_tn 256x256: N % 256");
     tn::launch<256, 256, 2, 4, 5, tn::EPI_PLAIN>(a, w, N, ea);
   }
@@ -1711,10 +1532,7 @@ std::tuple<at::Tensor, at::Tensor> gemm_tn_swiglu(const at::Tensor& x, const at:
   auto gu = at::empty({M, N}, x.options());
   auto act = at::empty({M, I}, x.options());
   tn::EpiArgs ea{(u16*)gu.data_ptr(), (u16*)act.data_ptr(), nullptr, nullptr, (long)N, I, 0};
-  if (cfg == 50) tn::launch5<tn::EPI_SWIGLU, tn::TN5_DEFAULT>(x, w_gu, N, ea);
-  else if (cfg == 164) tn::launch5<tn::EPI_SWIGLU, 0>(x, w_gu, N, ea);
-  else if (cfg == 51) tn::launch5<tn::EPI_SWIGLU, 0>(x, w_gu, N, ea, false);
-  else if (cfg == 165) tn::launch5<tn::EPI_SWIGLU, 128>(x, w_gu, N, ea);
+  if (cfg == 164) tn::launch5<tn::EPI_SWIGLU>(x, w_gu, N, ea);
   else if (cfg == 12) tn::launch4<tn::EPI_SWIGLU, 0, 4>(x, w_gu, N, ea);
   else if (x.size(1) % 64 == 0 && N % 256 == 0 && cfg == 11) tn::launch3<tn::EPI_SWIGLU, true, 2>(x, w_gu, N, ea);
   else if (x.size(1) % 64 == 0) tn::launch2<256, 256, 2, 4, 2, tn::EPI_SWIGLU, 3>(x, w_gu, N, ea);
@@ -1736,16 +1554,11 @@ at::Tensor gemm_tn_rope(const at::Tensor& x, const at::Tensor& w, const at::Tens
   auto c = at::empty({M, N}, x.options());
   tn::EpiArgs ea{(u16*)c.data_ptr(), nullptr, cosb.data_ptr<float>(), sinb.data_ptr<float>(), (long)N, 0,
                  (int)rope_cols};
-  if (cfg == 50) tn::launch5<tn::EPI_ROPE, tn::TN5_DEFAULT>(x, w, N, ea);
-  else if (cfg == 164) tn::launch5<tn::EPI_ROPE, 0>(x, w, N, ea);
-  else if (cfg == 51) tn::launch5<tn::EPI_ROPE, 0>(x, w, N, ea, false);
-  else if (cfg == 165) tn::launch5<tn::EPI_ROPE, 128>(x, w, N, ea);
+  if (cfg == 164) tn::launch5<tn::EPI_ROPE>(x, w, N, ea);
   else if (cfg == 12) tn::launch4<tn::EPI_ROPE, 0, 4>(x, w, N, ea);
-  else if (cfg == 1) tn::launch<256, 128, 4, 2, 6, tn::EPI_ROPE>(x, w, N, ea);
   else if (cfg == 2 && x.size(1) % 64 == 0) tn::launch2<256, 256, 2, 4, 2, tn::EPI_ROPE>(x, w, N, ea);
   else if (cfg == 5 && x.size(1) % 64 == 0) tn::launch2<256, 256, 2, 4, 2, tn::EPI_ROPE, 3>(x, w, N, ea);
   else if (cfg == 6 && x.size(1) % 64 == 0) tn::launch2<256, 128, 4, 2, 3, tn::EPI_ROPE>(x, w, N, ea);
-  else if (cfg == 7 && x.size(1) % 64 == 0) tn::launch2<256, 128, 4, 2, 2, tn::EPI_ROPE>(x, w, N, ea);
   else if (cfg == 11 && x.size(1) % 64 == 0) {
     // Wave-quantisation tail (gemm_dgrad.hip does the same): the SmolLM3 qkv grid is 32 x 12 = 384 tiles of
     // 256 x 256 = 1.5 rounds of 256 CUs. The whole round runs as one launch over the leading columns and the

@@ -146,31 +146,10 @@ def _accumulate_small_grad(param: torch.Tensor, g: torch.Tensor):
 
 
 # ----------------------------------------------------------------------------- forward GEMMs
-# SFTAMD_FWD_GEMM: which kernel runs the plain projection forwards (o_proj, down_proj, lm_head, NoPE-layer qkv).
-# "persist" = the persistent 4-wave HIP GEMM (csrc/gemm_tn.hip cfg 50: 128 x 128 wave tiles, the next tile's loads and
-# this tile's register epilogue overlapped, profiles/r3_gemm_4wave.md); "blas" = hipBLASLt / rocBLAS through torch.
-# SFTAMD_GATE_UP: the gate_up projection — "blas" (+ the separate SwiGLU kernel) or the config (11 / 12 / 50) of the HIP
-# GEMM with the SwiGLU epilogue (gu and act written by the GEMM, the SwiGLU pass over [M, 2I] gone).
-_FWD_GEMM = os.environ.get("SFTAMD_FWD_GEMM", "blas")
-_GATE_UP = os.environ.get("SFTAMD_GATE_UP", "blas")
-_PERSIST_CFG = int(os.environ.get("SFTAMD_PERSIST_CFG", "50"))
-
-
-def _grid_fills(M: int, N: int) -> bool:
-    """256 x 256 tiles over 256 CUs: whole rounds, a last round at least 3/4 full, or enough rounds that a partial one
-    does not matter. Ragged shapes (e.g. down_proj at M = 10240: 1.25 rounds) stay on hipBLASLt, whose stream-K
-    kernels split the partial round (profiles/r3_gemm_4wave.md, M = 10240 table)."""
-    tiles = (M // 256) * (N // 256)
-    rest = tiles % 256
-    return rest == 0 or rest >= 192 or tiles >= 8 * 256
-
-
-def _persist_ok(x2d: torch.Tensor, w: torch.Tensor) -> bool:
-    """Shapes the persistent forward GEMM takes: M, N multiples of 256, K of 128, K-contiguous 16-byte rows."""
-    return (_ext.use_hip(x2d) and x2d.dtype == torch.bfloat16 and w.dtype == torch.bfloat16
-            and x2d.dim() == 2 and x2d.shape[0] % 256 == 0 and x2d.shape[0] > 0 and x2d.shape[1] % 128 == 0
-            and w.shape[0] % 256 == 0 and x2d.stride(1) == 1 and x2d.stride(0) % 8 == 0 and w.is_contiguous()
-            and x2d.data_ptr() % 16 == 0 and w.data_ptr() % 16 == 0 and _grid_fills(x2d.shape[0], w.shape[0]))
+# The plain projection forwards (o_proj, down_proj, lm_head, NoPE-layer qkv) are plain library GEMMs with nothing to
+# fuse: hipBLASLt (TunableOp selections). The hand-written persistent 4-wave kernel lost to it end to end by 3-5 %
+# (static, per-tile and work-stealing launches, with and without the overlapped AdamW: profiles/r4_gemm_fwd.md); the
+# hand-written forward GEMMs keep the fused epilogues — qkv + RoPE, the optional gate_up + SwiGLU, the LoRA wide GEMM.
 
 
 def _as_output(y2d: torch.Tensor, lead) -> torch.Tensor:
@@ -182,12 +161,7 @@ def _as_output(y2d: torch.Tensor, lead) -> torch.Tensor:
 
 
 def fwd_gemm(x2d: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
-    """y = x2d @ w^T for a projection forward: the persistent HIP GEMM where selected and it applies, else
-    hipBLASLt (or the opt-in plain ping-pong GEMM, SFTAMD_TN_PLAIN)."""
-    if _FWD_GEMM == "persist" and _persist_ok(x2d, w):
-        return _ext.ops().gemm_tn(x2d, w, _PERSIST_CFG)
-    if _tn_plain_ok(x2d, w):
-        return _ext.ops().gemm_tn(x2d, w, _tn_cfg(x2d.shape[0], w.shape[0]))
+    """y = x2d @ w^T for a plain projection forward (hipBLASLt)."""
     return torch.nn.functional.linear(x2d, w)
 
 
@@ -468,31 +442,11 @@ def _tn_ok(x2d: torch.Tensor, w: torch.Tensor) -> bool:
             and x2d.stride(1) == 1 and x2d.stride(0) % 8 == 0 and w.is_contiguous() and w.shape[0] % 256 == 0)
 
 
-# Both win in the isolated microbench but lose inside the training step. Same-box interleaved bench.py
-# (gpu_run57): 98.36 samples/s with both, 98.71 / 98.70 with either one off, 98.84 at the session-start
-# commit. Both are opt-in.
-_TN_PLAIN = os.environ.get("SFTAMD_TN_PLAIN", "0") == "1"
-_TN_SMALL_TILES = os.environ.get("SFTAMD_TN_SMALL_TILES", "0")
-
-
 def _tn_cfg(M: int, N: int) -> int:
-    """Forward GEMM configuration. Default: the ping-pong 8-phase schedule (cfg 11, csrc/gemm_tn.hip: the two
-    wave rows one barrier apart, transposed-C epilogue) wherever N % 256 == 0 — 2-6 % faster than the BK64 ring
-    (cfg 2) on every SmolLM3 shape (profiles/r2_gemm_pingpong.md). SFTAMD_TN_SMALL_TILES=1: 256x128 tiles
-    (cfg 6) when the 256x256 grid does not fill whole waves of the 256 CUs."""
-    if N % 256 == 0:
-        return 11
-    if _TN_SMALL_TILES == "0":
-        return 2
-    tiles = (M // 256) * (N // 256)
-    return 2 if (N % 256 == 0 and tiles % 256 == 0) or N % 128 != 0 else 6
-
-
-def _tn_plain_ok(x2d: torch.Tensor, w: torch.Tensor) -> bool:
-    """Plain projections where the BK64 HIP GEMM beats hipBLASLt (profiles/r1_gemm_tn.md: o_proj
-    [8192 x 2048 x 2048] 0.059 vs 0.063 ms, NoPE-layer qkv [8192 x 3072 x 2048] 0.101 vs 0.119 ms): N and K
-    up to 4096. The large-N/K shapes (gate_up, down, lm_head) stay on hipBLASLt."""
-    return _TN_PLAIN and w.shape[0] <= 4096 and w.shape[1] <= 4096 and _tn_ok(x2d, w)
+    """Forward GEMM with an epilogue (qkv + RoPE): the ping-pong 8-phase schedule (cfg 11, csrc/gemm_tn.hip: the two
+    wave rows one barrier apart, transposed-C epilogue) wherever N % 256 == 0 — 2-6 % faster than the BK64 ring (cfg 2)
+    on every SmolLM3 shape (profiles/r2_gemm_pingpong.md)."""
+    return 11 if N % 256 == 0 else 2
 
 
 class GateUpSwiGLUFn(Function):
@@ -522,8 +476,10 @@ class GateUpSwiGLUFn(Function):
 
 
 def _tn_swiglu_cfg(weight: torch.Tensor) -> int:
-    if _GATE_UP not in ("blas", "") and weight.shape[0] % 256 == 0 and weight.shape[1] % 128 == 0:
-        return int(_GATE_UP)
+    """gate_up + SwiGLU epilogue (SFTAMD_TN=swiglu / 1): the persistent 4-wave kernel where it applies (0.669 vs
+    0.705 ms for hipBLASLt + the SwiGLU kernel at M = 8192, profiles/r4_gemm_fwd.md), else the ping-pong kernel."""
+    if weight.shape[0] % 256 == 0 and weight.shape[1] % 128 == 0:
+        return 164
     return 11 if weight.shape[0] % 256 == 0 else 5
 
 
@@ -597,7 +553,7 @@ def swiglu_mlp(h: torch.Tensor, w_gate_up: torch.Tensor, w_down: torch.Tensor) -
     (no separate SwiGLU kernel in either direction); default: hipBLASLt gate_up + SwiGLU kernel + the fused down
     dgrad (SFTAMD_SWIGLU_DOWN=1); otherwise the unfused chain."""
     h2d = h.reshape(-1, h.shape[-1])
-    fused_gu = _TN_MODE in ("1", "swiglu") or (_GATE_UP not in ("blas", "") and _persist_ok(h2d, w_gate_up))
+    fused_gu = _TN_MODE in ("1", "swiglu")
     if (fused_gu and _SWIGLU_DOWN and _tn_ok(h2d, w_gate_up) and w_gate_up.shape[0] % 256 == 0
             and (w_gate_up.shape[0] // 2) % 128 == 0):
         gu, act = GateUpActFn.apply(h, w_gate_up)

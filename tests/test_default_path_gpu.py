@@ -61,7 +61,7 @@ def test_default_path_smollm3_widths_vs_fp32_reference(monkeypatch):
     tr = _trace()
     # ---- which variants ran (the defaults of ops/fused.py and the C++ launchers at these shapes)
     assert tr.get("tn.rope.c11", 0) == 3 and tr.get("tn.rope.tail", 0) == 3, tr  # qkv + RoPE, 384-tile tail split
-    assert tr.get("attn.fwd3", 0) == 4 and tr.get("attn.dkdv5", 0) == 4 and tr.get("attn.dq4", 0) == 4, tr
+    assert tr.get("attn.fwd32", 0) == 4 and tr.get("attn.dkdv32", 0) == 4 and tr.get("attn.dq32", 0) == 4, tr
     assert tr.get("attn.bwd_rope_epi", 0) == 3, tr  # inverse RoPE in the dq / dK epilogues of the 3 RoPE layers
     # wgrad: the 4-wave ring (csrc/gemm_4w.hip) for gate_up and, hybrid split-K, down_proj; 8-wave rings for lm_head
     # (8192-vocab: 256 tiles of 256 x 128) / o_proj (split 2) / qkv (split 2)
@@ -71,7 +71,7 @@ def test_default_path_smollm3_widths_vs_fp32_reference(monkeypatch):
     assert tr.get("dgrad.swiglu.c7", 0) >= 4 and tr.get("dgrad.tail", 0) > 0, tr  # down dgrad + SwiGLU bwd
     assert tr.get("dgrad.c12", 0) > 0, tr  # o_proj / qkv dgrads: 4-wave pair loop
     assert tr.get("dgrad.c13", 0) >= 5, tr  # gate_up (K = 22016) x 4 + lm_head: 4-wave ring
-    assert all(not k.startswith("attn.dq3") and k != "attn.fwd3.w4" for k in tr), tr
+    assert "attn.dq3" not in tr, tr  # (the recompute path: past the dS^T budget only)
     # ---- numerics vs the fp32 reference path (same weights, PyTorch ops)
     monkeypatch.setenv("SFTAMD_DISABLE_HIP", "1")
     ref.train()

@@ -189,7 +189,7 @@ def _env(**kv):
 
 
 def _attn_case(lens, nq, nkv, causal, ds_mb=""):
-    # ds_mb: "" = default budget (materialised dS^T + dq4), "0" = the dq3 recompute path
+    # ds_mb: "" = default budget (materialised dS^T + dq32), "0" = the dq3 recompute path
     with _env(SFTAMD_ATTN_DS_MB=ds_mb):
         _attn_case_body(lens, nq, nkv, causal)
 
@@ -218,7 +218,7 @@ def _attn_case_body(lens, nq, nkv, causal):
 @pytest.mark.parametrize("causal", [True, False])
 @pytest.mark.parametrize("ds_mb", ["", "0"])
 def test_flash_attention_varlen_gqa(causal, ds_mb):
-    """fwd3 (K / V by LDS-DMA) + the GQA-grouped dK/dV with either dQ path (materialised dS^T + dq4, or the dq3
+    """fwd32 + the GQA-grouped dK/dV (dkdv32) with either dQ path (materialised dS^T + dq32, or the dq3
     recompute past the dS^T budget) vs the fp32 reference: ragged lengths off the 64 / 128 tile grid, even GQA
     ratios (two head groups, LDS-DMA Q / dO), odd ones (one group), MHA (rep 1) and the SmolLM3 shape."""
     _attn_case([100, 255, 64, 1, 300, 129], 8, 2, causal, ds_mb)
@@ -229,11 +229,10 @@ def test_flash_attention_varlen_gqa(causal, ds_mb):
     _attn_case([300, 17, 129], 4, 4, causal, ds_mb)
 
 
-@pytest.mark.parametrize("fwd16", ["", "1"])
 @pytest.mark.parametrize("causal", [True, False])
-def test_flash_fwd_out_and_lse(fwd16, causal):
-    """The 32x32x16 forward (fwd32: HW = gcd(rep, 4) heads per workgroup -> rep 4 / 8, 2 / 6, 1 / 3 paths) and the
-    16x16x32 fwd3 vs fp32 softmax(QK^T) V and logsumexp, on lengths off the 32 / 64 grids."""
+def test_flash_fwd_out_and_lse(causal):
+    """The 32x32x16 forward (fwd32: HW = gcd(rep, 4) heads per workgroup -> rep 4 / 8, 2 / 6, 1 / 3 paths) vs fp32
+    softmax(QK^T) V and logsumexp, on lengths off the 32 / 64 grids."""
     torch.manual_seed(1)
     D = 128
     for lens, nq, nkv in (([512, 511, 7, 33], 16, 4), ([100, 255, 64, 1, 300, 129], 8, 2), ([200, 65], 12, 3),
@@ -242,8 +241,7 @@ def test_flash_fwd_out_and_lse(fwd16, causal):
         M = int(cu[-1])
         qkv = torch.randn(M, (nq + 2 * nkv) * D, device=DEV, dtype=torch.bfloat16)
         scale = 1 / math.sqrt(D)
-        with _env(SFTAMD_ATTN_FWD16=fwd16):
-            out, lse = _ext.ops().flash_fwd(qkv, cu, max(lens), nq, nkv, D, scale, causal)
+        out, lse = _ext.ops().flash_fwd(qkv, cu, max(lens), nq, nkv, D, scale, causal)
         q32 = qkv.float()
         o_ref = ref.attention(q32, nq, nkv, D, cu, scale, causal)
         assert rel_err(out, o_ref) < 1e-2, (lens, nq, nkv, rel_err(out, o_ref))
@@ -508,7 +506,7 @@ def test_lora_fwd_bwd_kernels(K, R, p):
     assert (dx.float() - dxr.float()).abs().max().item() < 3e-2
 
 
-@pytest.mark.parametrize("cfg", [0, 1, 2, 3, 5, 6, 7, 8, 9, 10, 11])
+@pytest.mark.parametrize("cfg", [0, 2, 5, 6, 11])
 @pytest.mark.parametrize("M,N,K", [(256, 256, 64), (512, 512, 128), (256, 512, 192), (512, 768, 256), (768, 512, 2112),
                                    (2048, 3072, 320)])
 def test_gemm_tn_plain(cfg, M, N, K):
@@ -522,21 +520,18 @@ def test_gemm_tn_plain(cfg, M, N, K):
 @pytest.mark.parametrize("M,N,K", [(256, 256, 128), (512, 512, 256), (768, 512, 2176), (2048, 3072, 384),
                                    (512, 1280, 11008), (4096, 4352, 256), (2304, 7424, 128)])
 def test_gemm_tn_4wave(M, N, K):
-    """cfg 12: 4 waves of 128 x 128 (accumulators pinned in AGPRs by inline-asm MFMAs) vs the fp32 reference, plus the
-    fused SwiGLU / RoPE epilogues of the same kernel against their unfused twins."""
+    """cfg 12: 4 waves of 128 x 128 (accumulators pinned in AGPRs by inline-asm MFMAs) and cfg 164, its persistent
+    version (tiles > 256 walk several per workgroup; K = 128 is its single-pair path), vs the fp32 reference, plus the
+    fused SwiGLU / RoPE epilogues of both against their unfused twins."""
     torch.manual_seed(0)
     x = torch.randn(M, K, device=DEV, dtype=torch.bfloat16)
     w = torch.randn(N, K, device=DEV, dtype=torch.bfloat16)
     ref32 = x.float() @ w.float().t()
-    # 13-44: schedule variants of the same kernel; 50: the persistent version (tiles > 256 walk several per
-    # workgroup; K = 128 is its single-pair path)
-    # 51: one tile per workgroup; 164: no stagger / plain stores; 165: the dynamic tile queue (run twice: the
-    # per-launch queue slot must come back reset)
-    for cfg in (12, 13, 16, 20, 21, 24, 25, 28, 44, 50, 51, 60, 61, 164, 165, 165):
+    for cfg in (12, 164):
         c = _ext.ops().gemm_tn(x, w, cfg)
         assert rel_err(c, ref32) < 5e-3, cfg
     gu_ref = x.float() @ (w * 0.1).float().t()
-    for cfg in (12, 50, 51, 164, 165):
+    for cfg in (12, 164):
         gu, act = _ext.ops().gemm_tn_swiglu(x, w * 0.1, cfg)
         assert rel_err(gu, gu_ref) < 5e-3, cfg
         assert rel_err(act, _ext.ops().swiglu_fwd(gu)) < 2e-3, cfg
@@ -550,20 +545,9 @@ def test_gemm_tn_4wave(M, N, K):
         y = (x.float() @ w.float().t()).to(torch.bfloat16)
         qk = y[:, :(nq + nkv) * D].view(M, nq + nkv, D)
         exp = torch.cat([ref.apply_rope(qk, cs, sn).reshape(M, -1), y[:, (nq + nkv) * D:]], dim=1)
-        for cfg in (12, 50, 51, 164, 165):
+        for cfg in (12, 164):
             out = _ext.ops().gemm_tn_rope(x, w, cs, sn, (nq + nkv) * D, cfg)
             assert rel_err(out, exp) < 1e-2, cfg
-
-
-def test_gemm_tn_dynamic_queue_many_launches():
-    """The dynamic tile queue over many back-to-back launches of different grids (every one of the 64 ring slots
-    reused): each result complete and exact vs the static kernel (same per-tile arithmetic)."""
-    torch.manual_seed(1)
-    for it in range(80):
-        M, N = (512, 768) if it % 3 else (2048, 4352)
-        x = torch.randn(M, 256, device=DEV, dtype=torch.bfloat16)
-        w = torch.randn(N, 256, device=DEV, dtype=torch.bfloat16)
-        assert torch.equal(_ext.ops().gemm_tn(x, w, 165), _ext.ops().gemm_tn(x, w, 164)), it
 
 
 def test_gemm_tn_strided_rows():
@@ -590,7 +574,7 @@ def test_gemm_tn_swiglu(I, K, cfg):
     assert rel_err(act, _ext.ops().swiglu_fwd(gu)) < 2e-3
 
 
-@pytest.mark.parametrize("cfg", [0, 1, 2, 5, 6, 7, 11])
+@pytest.mark.parametrize("cfg", [0, 2, 5, 6, 11])
 def test_gemm_tn_rope(cfg):
     torch.manual_seed(0)
     M, K, nq, nkv, D = 512, 256, 2, 1, 128

@@ -44,16 +44,13 @@ def timeit(fn, n=20):
     return statistics.median(ts)
 
 
-# "ds": the default backward (materialised dS^T + dq4); "dq3": the recompute path used past the dS^T budget;
-# "fwd16" / "dkdv5": the 16x16x32 forward (fwd3) / dK-dV kernel (dkdv5) instead of the 32x32x16 fwd32 / dkdv32
-CFGS = os.environ.get("CFGS", "ds,dq3,fwd16,dkdv5").split(",")
+# "ds": the default backward (materialised dS^T + dq32); "dq3": the recompute path used past the dS^T budget
+CFGS = os.environ.get("CFGS", "ds,dq3").split(",")
 res = {}
 ref = None
 for rnd in range(int(os.environ.get("ROUNDS", 3))):
     for cfg in CFGS:
         os.environ["SFTAMD_ATTN_DS_MB"] = "0" if cfg == "dq3" else ""
-        os.environ["SFTAMD_ATTN_FWD16"] = "1" if cfg == "fwd16" else ""
-        os.environ["SFTAMD_ATTN_DKDV5"] = "1" if cfg == "dkdv5" else ""
         out, lse = ops.flash_fwd(qkv, cu, T, NQ, NKV, D, sc, True)
         dq = ops.flash_bwd(dout, qkv, out, lse, cu, T, NQ, NKV, D, sc, True)
         if ref is None:

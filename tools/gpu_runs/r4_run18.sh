@@ -1,0 +1,9 @@
+#!/bin/bash
+# full GPU suite after pruning the 16x16 attention kernels, the tn5 experiment variants and the forward-routing knobs
+cd $GRAFT_REPO_ROOT
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+timeout -k 10 900 python -u -m pytest -x -q --timeout 300 --timeout-method thread tests -m gpu > gpurun_out/r4_18_tests.log 2>&1 || { tail -40 gpurun_out/r4_18_tests.log; exit 1; }
+tail -2 gpurun_out/r4_18_tests.log
+timeout -k 10 300 python -u bench.py --steps 20 --warmup 5 > gpurun_out/r4_18_bench.log 2>&1 || { tail -20 gpurun_out/r4_18_bench.log; exit 1; }
+grep -o '"value": [0-9.]*' gpurun_out/r4_18_bench.log
