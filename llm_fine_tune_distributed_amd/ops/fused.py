@@ -551,7 +551,7 @@ def swiglu_mlp(h: torch.Tensor, w_gate_up: torch.Tensor, w_down: torch.Tensor) -
     """down(swiglu(gate_up(h))) — the SwiGLU MLP without LoRA, on the fastest available fusion:
     SFTAMD_TN=1 / swiglu: gate_up GEMM with the SwiGLU epilogue + down GEMM with the SwiGLU backward in its dgrad
     (no separate SwiGLU kernel in either direction); default: hipBLASLt gate_up + SwiGLU kernel + the fused down
-    dgrad (SFTAMD_SWIGLU_DOWN=1); otherwise the unfused chain."""
+    dgrad; otherwise the unfused chain."""
     h2d = h.reshape(-1, h.shape[-1])
     fused_gu = _TN_MODE in ("1", "swiglu")
     if (fused_gu and _SWIGLU_DOWN and _tn_ok(h2d, w_gate_up) and w_gate_up.shape[0] % 256 == 0
@@ -888,14 +888,10 @@ def _sync_wide(wide: torch.Tensor, K: int, r: int, meta, Bs) -> None:
     wide._sftamd_bkey = key
 
 
-# SFTAMD_LORA_FWD: the widened LoRA forward GEMM X' W'^T on the hand-written persistent kernel ("hip", default: the
-# frozen base has no AdamW pass to overlap with the next forward, the one co-runner that costs persistent grids
-# their whole rounds in full SFT) or hipBLASLt ("blas")
-_LORA_FWD = os.environ.get("SFTAMD_LORA_FWD", "hip")
-
-
 def _lora_gemm(X: torch.Tensor, wide: torch.Tensor) -> torch.Tensor:
-    if (_LORA_FWD == "hip" and _ext.use_hip(X) and X.shape[0] % 256 == 0 and X.shape[1] % 128 == 0
+    """The widened LoRA forward GEMM X' W'^T on the hand-written persistent kernel (113.0 samples/s vs 112.9 with
+    hipBLASLt, profiles/r4_lora.md)."""
+    if (_ext.use_hip(X) and X.shape[0] % 256 == 0 and X.shape[1] % 128 == 0
             and wide.shape[0] % 256 == 0 and wide.is_contiguous() and X.is_contiguous()):
         return _ext.ops().gemm_tn(X, wide, _LORA_FWD_CFG)
     return torch.mm(X, wide.t())
