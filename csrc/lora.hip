@@ -29,7 +29,7 @@ __device__ __forceinline__ f32x4 mfma(const bf16x8& a, const bf16x8& b, const f3
 template <int RF>  // R = 16 * RF adapter columns
 __global__ __launch_bounds__(512) void fwd_kernel(const u16* __restrict__ x, const u16* __restrict__ A,
                                                   u16* __restrict__ X, u16* __restrict__ xd, long T, int K, long ldX,
-                                                  float s, unsigned thresh, float dscale, unsigned seed) {
+                                                  float s, unsigned thresh, float dscale, unsigned seed, int drop) {
   constexpr int R = 16 * RF;
   constexpr int NW = 8, U = 4;
   __shared__ float red[NW][16][R + 1];
@@ -55,14 +55,14 @@ __global__ __launch_bounds__(512) void fwd_kernel(const u16* __restrict__ x, con
       const int kk = k + 32 * u + 8 * g;
       if (kk >= kb + KW) break;
       if (rowok) *(uint4*)(X + t * ldX + kk) = v[u];
-      if (xd) {
+      if (drop) {
         float f[8];
         unpack8(v[u], f);
         const unsigned long long idx = (unsigned long long)t * K + kk;
 #pragma unroll
         for (int i = 0; i < 8; ++i) f[i] = hash_u32(idx + i, seed) >= thresh ? f[i] * dscale : 0.f;
         v[u] = pack8(f);
-        if (rowok) *(uint4*)(xd + t * K + kk) = v[u];
+        if (xd && rowok) *(uint4*)(xd + t * K + kk) = v[u];
       }
       const bf16x8 a = __builtin_bit_cast(bf16x8, v[u]);
 #pragma unroll
@@ -159,6 +159,134 @@ __global__ __launch_bounds__(512) void bwd_dx_kernel(const u16* __restrict__ bas
   }
 }
 
+// Thin token reductions of the adapter backward, one pass over the wide operand:
+//   out [R, K] (fp32, accumulated with atomics) = sum_t S[t, r] * Xd[t, k]
+// with Xd = dropout(X) (the forward's mask regenerated from the seed) or X itself.
+//   dA    = dxa^T dropout(x):  X = X'[:, :K] (the widened activation), S = dxa [T, R]
+//   dB^T  = (s xa)^T dy:       X = dy [T, n],                          S = X'[:, K:K+R] (the adapter columns)
+// Workgroup = 64 columns of k x a chunk of tc tokens, 64 tokens per stage: the X tile (masked and scaled in registers)
+// and the S tile go into LDS row-major with 16-byte stores, and both MFMA fragments are transposed reads
+// (ds_read_b64_tr_b16: A = X^T rows k, B = S^T rows r, 8 consecutive tokens per lane); the next stage's global loads
+// are issued before this stage's MFMAs. Wave w owns k rows 16 w .. 16 w + 15 of the tile.
+__device__ __forceinline__ bf16x8 lds_tr8(const u16* p0, const u16* p1) {
+  typedef __attribute__((address_space(3))) s16x4 lds_s4;
+  const s16x4 a = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4*)p0);
+  const s16x4 b = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4*)p1);
+  typedef __attribute__((ext_vector_type(8))) short s16x8;
+  const s16x8 v = {a[0], a[1], a[2], a[3], b[0], b[1], b[2], b[3]};
+  return __builtin_bit_cast(bf16x8, v);
+}
+
+template <int RF>
+__global__ __launch_bounds__(256) void tsum_kernel(const u16* __restrict__ X, long ldX, const u16* __restrict__ S,
+                                                   long ldS, float* __restrict__ out, long T, int K, long tc,
+                                                   unsigned thresh, float dscale, unsigned seed, int drop) {
+  constexpr int R = 16 * RF, ST = 64, XP = 64 + 8, SP = R + 8;  // row pitches padded by 16 bytes (2-way at most)
+  constexpr int SCH = ST * R / 8, SPT = (SCH + 255) / 256;       // S chunks of 8 per stage, per thread
+  __shared__ __attribute__((aligned(16))) u16 xs[ST][XP];
+  __shared__ __attribute__((aligned(16))) u16 ss[ST][SP];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, g = lane >> 4, r16 = lane & 15;
+  const int k0 = blockIdx.x * 64;
+  const long t_begin = (long)blockIdx.y * tc, t_end = min(T, t_begin + tc);
+  const int tr = tid >> 3, c8 = tid & 7;  // X chunks: rows tr and tr + 32 of the stage, columns 8 c8 .. 8 c8 + 7
+  const int k = k0 + 8 * c8;
+  f32x4 acc[RF];
+#pragma unroll
+  for (int j = 0; j < RF; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  uint4 xv[2], sv[SPT];
+  auto load = [&](long t0) {
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const long t = t0 + tr + 32 * h;
+      xv[h] = (t < t_end && k < K) ? *(const uint4*)(X + t * ldX + k) : make_uint4(0, 0, 0, 0);
+    }
+#pragma unroll
+    for (int u = 0; u < SPT; ++u) {
+      const int e = tid + 256 * u, row = e / (R / 8), cc = e - row * (R / 8);
+      const long t = t0 + row;
+      sv[u] = (e < SCH && t < t_end) ? *(const uint4*)(S + t * ldS + 8 * cc) : make_uint4(0, 0, 0, 0);
+    }
+  };
+  // transposed-read lane addresses: group g reads tokens 8 (g & 1) + 16 (g >> 1)... of a 32-token k-step: rows
+  // 8 gg + q (lo) and 8 gg + 4 + q (hi) with gg = g, columns c0 + 4 p
+  const int q = r16 >> 2, p = r16 & 3;
+  load(t_begin);
+  for (long t0 = t_begin; t0 < t_end; t0 += ST) {
+    __syncthreads();  // the previous stage's reads are done
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      uint4 v = xv[h];
+      if (drop) {
+        const long t = t0 + tr + 32 * h;
+        float f[8];
+        unpack8(v, f);
+        const unsigned long long idx = (unsigned long long)t * K + k;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) f[i] = hash_u32(idx + i, seed) >= thresh ? f[i] * dscale : 0.f;
+        v = pack8(f);
+      }
+      *(uint4*)&xs[tr + 32 * h][8 * c8] = v;
+    }
+#pragma unroll
+    for (int u = 0; u < SPT; ++u) {
+      const int e = tid + 256 * u, row = e / (R / 8), cc = e - row * (R / 8);
+      if (e < SCH) *(uint4*)&ss[row][8 * cc] = sv[u];
+    }
+    __syncthreads();
+    if (t0 + ST < t_end) load(t0 + ST);  // the next stage's loads fly under this stage's MFMAs
+#pragma unroll
+    for (int ks = 0; ks < ST / 32; ++ks) {
+      const int rl = 32 * ks + 8 * g + q;
+      const bf16x8 a = lds_tr8(&xs[rl][16 * w + 4 * p], &xs[rl + 4][16 * w + 4 * p]);
+#pragma unroll
+      for (int j = 0; j < RF; ++j)
+        acc[j] = mfma(a, lds_tr8(&ss[rl][16 * j + 4 * p], &ss[rl + 4][16 * j + 4 * p]), acc[j]);
+    }
+  }
+  // C layout: lane (g, r16) holds rows 4 g + i (k), column r16 (r) of each 16 x 16 block
+#pragma unroll
+  for (int j = 0; j < RF; ++j)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int kk = k0 + 16 * w + 4 * g + i;
+      if (kk < K) atomicAdd(out + (long)(16 * j + r16) * K + kk, acc[j][i]);
+    }
+}
+
+// Scatter blocks of an fp32 [R, K] sum into up to 4 parameter gradients (bf16 or fp32, written or accumulated), one
+// launch for all adapters of a projection: output q is rows [r0, r0 + nr) x columns [c0, c0 + nc) of the sum,
+// transposed when tr (dB = (dB^T)^T: out[i][j] = sum[r0 + j][c0 + i]).
+struct GradOuts {
+  void* ptr[4];
+  int r0[4], c0[4], nr[4], nc[4];
+  int f32[4], acc[4];
+};
+
+__global__ __launch_bounds__(256) void grad_out_kernel(const float* __restrict__ sum, int K, GradOuts go, int tr) {
+  const int q = blockIdx.y;
+  const int n = go.nr[q] * go.nc[q];  // elements of output q ([nc, nr] when tr, else [nr, nc])
+  for (int e = blockIdx.x * 256 + threadIdx.x; e < n; e += gridDim.x * 256) {
+    int i, j;
+    float v;
+    if (tr) {  // out [nc][nr]: element (i, j) = sum[r0 + j][c0 + i]
+      i = e / go.nr[q];
+      j = e - i * go.nr[q];
+      v = sum[(long)(go.r0[q] + j) * K + go.c0[q] + i];
+    } else {
+      i = e / go.nc[q];
+      j = e - i * go.nc[q];
+      v = sum[(long)(go.r0[q] + i) * K + go.c0[q] + j];
+    }
+    if (go.f32[q]) {
+      float* o = (float*)go.ptr[q] + e;
+      *o = go.acc[q] ? *o + v : v;
+    } else {
+      u16* o = (u16*)go.ptr[q] + e;
+      *o = f2bf(go.acc[q] ? bf2f(*o) + v : v);
+    }
+  }
+}
+
 static unsigned thresh_of(double p, float* dscale) {
   const double pc = p < 0 ? 0 : (p > 0.999 ? 0.999 : p);
   *dscale = (float)(1.0 / (1.0 - pc));
@@ -167,10 +295,11 @@ static unsigned thresh_of(double p, float* dscale) {
 
 }  // namespace lora
 
-// x [T, K], A [R, K] (R = 16, 32, 48 or 64) -> (X' [T, ldX], xd [T, K] or empty when p == 0); ldX >= K + R (0 = K + R):
-// columns [K + R, ldX) are zero (the wide weight's padding to a whole K-tile pair of the HIP GEMMs)
+// x [T, K], A [R, K] (R = 16, 32, 48 or 64) -> (X' [T, ldX], xd): xd = dropout(x) [T, K] only with save_xd and
+// p > 0, else empty (the backward regenerates the mask from the seed: lora_da). ldX >= K + R (0 = K + R): columns
+// [K + R, ldX) are zero (the wide weight's padding to a whole K-tile pair of the HIP GEMMs)
 std::tuple<at::Tensor, at::Tensor> lora_fwd(const at::Tensor& x, const at::Tensor& A, double s, double p, int64_t seed,
-                                            int64_t ldX) {
+                                            int64_t ldX, bool save_xd) {
   SFT_CHECK_CUDA(x);
   SFT_CHECK_BF16(x);
   SFT_CHECK_BF16(A);
@@ -182,16 +311,16 @@ std::tuple<at::Tensor, at::Tensor> lora_fwd(const at::Tensor& x, const at::Tenso
   if (ldX <= 0) ldX = K + R;
   SFT_CHECK(ldX >= K + R && ldX % 8 == 0, "lora_fwd: ldX >= K + R, multiple of 8");
   auto X = at::empty({T, ldX}, x.options());
-  at::Tensor xd = p > 0 ? at::empty_like(x) : at::empty({0}, x.options());
+  at::Tensor xd = (p > 0 && save_xd) ? at::empty_like(x) : at::empty({0}, x.options());
   if (T == 0) return {X, xd};
   float dscale;
   const unsigned thresh = lora::thresh_of(p, &dscale);
   const int grid = (int)((T + 15) / 16);
-  u16* xdp = p > 0 ? (u16*)xd.data_ptr() : nullptr;
+  u16* xdp = (p > 0 && save_xd) ? (u16*)xd.data_ptr() : nullptr;
 #define LORA_FWD(RF)                                                                                              \
   lora::fwd_kernel<RF><<<grid, 512, 0, cur_stream()>>>((const u16*)x.data_ptr(), (const u16*)A.data_ptr(),     \
                                                        (u16*)X.data_ptr(), xdp, T, K, ldX, (float)s, thresh, dscale, \
-                                                       (unsigned)seed)
+                                                       (unsigned)seed, p > 0 ? 1 : 0)
   switch (R / 16) {
     case 1: LORA_FWD(1); break;
     case 2: LORA_FWD(2); break;
@@ -237,9 +366,77 @@ at::Tensor lora_bwd_dx(const at::Tensor& base, const at::Tensor& dxa, const at::
   return dx;
 }
 
+// out [R, K] fp32 = S^T dropout(X[:, :K]) (the mask regenerated from seed when p > 0); X rows of stride >= K, S [T, R]
+// (a column slice of a wider tensor is fine)
+at::Tensor lora_tsum(const at::Tensor& X, int64_t K, const at::Tensor& S, double p, int64_t seed) {
+  SFT_CHECK_CUDA(X);
+  SFT_CHECK_BF16(X);
+  SFT_CHECK_BF16(S);
+  const long T = X.size(0);
+  const int R = S.size(1);
+  SFT_CHECK(X.stride(1) == 1 && X.stride(0) % 8 == 0 && X.size(1) >= K && K % 8 == 0, "lora_tsum: X layout");
+  SFT_CHECK(S.stride(1) == 1 && S.stride(0) % 8 == 0 && (uintptr_t)S.data_ptr() % 16 == 0, "lora_tsum: S layout");
+  SFT_CHECK(S.size(0) == T && R % 16 == 0 && R >= 16 && R <= 64, "lora_tsum: S [T, R], R in 16..64");
+  auto out = at::zeros({R, K}, X.options().dtype(at::kFloat));
+  if (T == 0) return out;
+  float dscale;
+  const unsigned thresh = lora::thresh_of(p, &dscale);
+  const int nkb = (int)((K + 63) / 64);
+  // about 1024 workgroups: the token range split into chunks of whole 64-token stages
+  long splits = std::max(1L, std::min((T + 63) / 64, 1024L / nkb));
+  const long tc = ((T + splits - 1) / splits + 63) / 64 * 64;
+  splits = (T + tc - 1) / tc;
+  dim3 grid(nkb, (unsigned)splits);
+#define LORA_TSUM(RF)                                                                                             \
+  lora::tsum_kernel<RF><<<grid, 256, 0, cur_stream()>>>((const u16*)X.data_ptr(), X.stride(0),                   \
+                                                        (const u16*)S.data_ptr(), S.stride(0), out.data_ptr<float>(), \
+                                                        T, (int)K, tc, thresh, dscale, (unsigned)seed, p > 0 ? 1 : 0)
+  switch (R / 16) {
+    case 1: LORA_TSUM(1); break;
+    case 2: LORA_TSUM(2); break;
+    case 3: LORA_TSUM(3); break;
+    default: LORA_TSUM(4); break;
+  }
+#undef LORA_TSUM
+  SFT_LAUNCH_CHECK();
+  return out;
+}
+
+// outs[q] (+)= block q of sum ([R, K] fp32): rows [r0[q], +nr), columns [c0[q], +nc), transposed when tr; one launch
+void lora_grad_out(const at::Tensor& sum, at::TensorList outs, at::IntArrayRef r0, at::IntArrayRef c0, bool tr,
+                   at::IntArrayRef accumulate) {
+  SFT_CHECK(sum.scalar_type() == at::kFloat && sum.is_contiguous() && sum.dim() == 2, "lora_grad_out: fp32 [R, K]");
+  const int n = outs.size();
+  SFT_CHECK(n >= 1 && n <= 4 && (int)r0.size() == n && (int)c0.size() == n && (int)accumulate.size() == n,
+            "lora_grad_out: 1..4 outputs");
+  const int R = sum.size(0), K = sum.size(1);
+  lora::GradOuts go{};
+  long most = 0;
+  for (int q = 0; q < n; ++q) {
+    const at::Tensor& o = outs[q];
+    SFT_CHECK(o.is_contiguous() && o.dim() == 2 &&
+                  (o.scalar_type() == at::kBFloat16 || o.scalar_type() == at::kFloat), "lora_grad_out: contiguous bf16 / fp32 2-D outputs");
+    const int nr = tr ? o.size(1) : o.size(0), nc = tr ? o.size(0) : o.size(1);
+    SFT_CHECK(r0[q] >= 0 && r0[q] + nr <= R && c0[q] >= 0 && c0[q] + nc <= K, "lora_grad_out: block out of range");
+    go.ptr[q] = o.data_ptr();
+    go.r0[q] = (int)r0[q];
+    go.c0[q] = (int)c0[q];
+    go.nr[q] = nr;
+    go.nc[q] = nc;
+    go.f32[q] = o.scalar_type() == at::kFloat;
+    go.acc[q] = accumulate[q] != 0;
+    most = std::max(most, (long)nr * nc);
+  }
+  dim3 grid((unsigned)std::min(1024L, (most + 255) / 256), (unsigned)n);
+  lora::grad_out_kernel<<<grid, 256, 0, cur_stream()>>>(sum.data_ptr<float>(), K, go, tr ? 1 : 0);
+  SFT_LAUNCH_CHECK();
+}
+
 TORCH_LIBRARY_IMPL(sftamd, CUDA, m) {
   m.impl("lora_fwd", &lora_fwd);
   m.impl("lora_bwd_dx", &lora_bwd_dx);
+  m.impl("lora_tsum", &lora_tsum);
+  m.impl("lora_grad_out", &lora_grad_out);
 }
 
 }  // namespace sftamd

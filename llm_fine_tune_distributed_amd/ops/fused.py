@@ -853,11 +853,48 @@ def dropout_add(a: Optional[torch.Tensor], b: torch.Tensor, p: float, seed: int)
     return ref.dropout_add(a, b, p, seed)
 
 
+def _lora_hip(x2d, acat) -> bool:
+    return _ext.use_hip(x2d) and x2d.shape[1] % 256 == 0 and acat.shape[0] % 16 == 0 and acat.shape[0] <= 64
+
+
 def _lora_fwd(x2d, acat, s, p, seed, ldX=0):
-    if _ext.use_hip(x2d) and x2d.shape[1] % 256 == 0 and acat.shape[0] % 16 == 0 and acat.shape[0] <= 64:
-        X, xd = _ext.ops().lora_fwd(x2d, acat, float(s), float(p), int(seed), int(ldX))
-        return X, (xd if p > 0 else None)
-    return ref.lora_fwd(x2d, acat, s, p, seed, ldX)
+    """X' = [x | s dropout(x) A^T | 0]; dropout(x) is not saved (lora_da regenerates the mask from the seed)."""
+    if _lora_hip(x2d, acat):
+        return _ext.ops().lora_fwd(x2d, acat, float(s), float(p), int(seed), int(ldX))[0]
+    return ref.lora_fwd(x2d, acat, s, p, seed, ldX)[0]
+
+
+def _lora_tsum(Xm, K, S, p, seed) -> torch.Tensor:
+    """[R, K] fp32 = S^T dropout(Xm[:, :K]) (the forward's mask regenerated from the seed when p > 0): one pass over the
+    wide operand (csrc/lora.hip tsum_kernel)."""
+    R = S.shape[1]
+    if (_ext.use_hip(Xm) and Xm.dtype == torch.bfloat16 and S.dtype == torch.bfloat16 and K % 8 == 0
+            and R % 16 == 0 and 16 <= R <= 64 and Xm.stride(1) == 1 and Xm.stride(0) % 8 == 0 and S.stride(1) == 1
+            and S.stride(0) % 8 == 0 and S.data_ptr() % 16 == 0):
+        return _ext.ops().lora_tsum(Xm, int(K), S, float(p), int(seed))
+    xs = ref.dropout_add(None, Xm[:, :K], p, seed) if p > 0 else Xm[:, :K]
+    return S.float().t() @ xs.float()
+
+
+def _scatter_grads(total: torch.Tensor, params, blocks, tr: bool):
+    """Per-adapter gradients from one fp32 sum [R, K]: param q's block starts at (r0, c0) of ``total`` (transposed when
+    ``tr``). With DDP main_grad slices they are written / accumulated in ONE launch and None is returned to autograd;
+    otherwise the blocks are returned."""
+    shapes = [(p.shape[1], p.shape[0]) if tr else tuple(p.shape) for p in params]
+    mgs = [getattr(p, "main_grad", None) for p in params]
+    if (all(m is not None for m in mgs) and _ext.use_hip(total) and len(params) <= 4
+            and all(m.is_contiguous() and m.dtype in (torch.bfloat16, torch.float32) for m in mgs)):
+        acc = [0 if getattr(p, "_sftamd_fresh", False) else 1 for p in params]
+        _ext.ops().lora_grad_out(total, mgs, [b[0] for b in blocks], [b[1] for b in blocks], bool(tr), acc)
+        for p in params:
+            p._sftamd_fresh = False
+            _weight_grad_done(p)
+        return [None] * len(params)
+    out = []
+    for p, (r0, c0), (nr, nc) in zip(params, blocks, shapes):
+        g = total[r0:r0 + nr, c0:c0 + nc]
+        out.append(_accumulate_small_grad(p, g.t() if tr else g))
+    return out
 
 
 def _lora_bwd_dx(base, dxa, acat, p, seed):
@@ -908,9 +945,9 @@ class LoRAWideFn(Function):
     X' = [x | s * xa | 0] with xa = dropout(x) A_cat^T (csrc/lora.hip lora_fwd: one pass over x). Then
         forward:  y = X' W'^T                      (one HIP GEMM, K+Rp deep: no rank-r pass over y)
         backward: base = dy W                      (the 4-wave HIP dgrad on W's column block of W')
-                  dxa  = s dy B_blockdiag          (thin [T, R] product)
-                  dB = dy^T X'[:, K:K+R]           (block-diagonal slices)
-                  dA = dxa^T dropout(x)
+                  dxa  = s dy B_blockdiag          (thin [T, R] product, s as the GEMM's alpha)
+                  dB_i = dy_i^T X'[:, K+c_i:K+c_i+r] (per adapter, into its main_grad slice)
+                  dA = dxa^T dropout(x)            (csrc/lora.hip lora_da: the mask regenerated from the seed)
                   dx = base + dropout(dxa A_cat)   (csrc/lora.hip lora_bwd_dx: one pass)"""
 
     @staticmethod
@@ -924,10 +961,11 @@ class LoRAWideFn(Function):
             x2d = x2d.contiguous()
         _sync_wide(wide, K, r, meta, Bs)
         acat = As[0].contiguous() if n == 1 else torch.cat(As, 0)
-        X, xd = _lora_fwd(x2d, acat, scaling, p, seed, wide.shape[1])
+        X = _lora_fwd(x2d, acat, scaling, p, seed, wide.shape[1])
         y = _lora_gemm(X, wide)
-        ctx.save_for_backward(X, acat, xd if xd is not None else X.new_empty(0))
+        ctx.save_for_backward(X, acat)
         ctx.wide = wide
+        ctx.adapters = ab  # the parameters themselves: their gradients go to main_grad directly
         ctx.meta = (K, R, r, n, float(scaling), float(p), int(seed), tuple(meta), x.shape)
         if x.dim() == 2:
             return y
@@ -935,18 +973,24 @@ class LoRAWideFn(Function):
 
     @staticmethod
     def backward(ctx, dy):
-        X, acat, xd = ctx.saved_tensors
+        X, acat = ctx.saved_tensors
         K, R, r, n, scaling, p, seed, meta, xshape = ctx.meta
         wide = ctx.wide
+        As, Bs = ctx.adapters[:n], ctx.adapters[n:]
         dy2d = dy.reshape(-1, dy.shape[-1])
         if not dy2d.is_contiguous():
             dy2d = dy2d.contiguous()
         base = dgrad_mm(dy2d, wide[:, :K])              # [T, K] (HIP 4-wave dgrad where the shapes allow)
-        dxa = torch.mm(dy2d, wide[:, K:K + R]).mul_(scaling)  # [T, R]
-        dBf = torch.mm(dy2d.t(), X[:, K:K + R])          # [n_out, R]
-        dBs = [dBf[o:o + rows, c:c + r].contiguous() for (o, rows, c) in meta]
-        dAf = torch.mm(dxa.t(), xd if p > 0 else X[:, :K])  # [R, K]
-        dAs = [dAf[i * r:(i + 1) * r] for i in range(n)]
+        # dxa = s dy B_blockdiag [T, R] (the scale as the GEMM's alpha, no extra pass)
+        dxa = torch.addmm(dy2d.new_empty(dy2d.shape[0], R), dy2d, wide[:, K:K + R], beta=0, alpha=scaling)
+        # the adapter gradients of all sub-projections, each from one pass over its wide operand, scattered straight into
+        # the parameters' flat gradient slices in one launch (no per-adapter GEMMs, slicing copies or autograd
+        # accumulation): dB^T = (s xa)^T dy [R, n_out] (block (c_i, o_i) transposed is dB_i); dA = dxa^T dropout(x)
+        # [R, K] (the forward's dropout mask regenerated from the seed: nothing saved)
+        n_out = dy2d.shape[1]
+        dBs = _scatter_grads(_lora_tsum(dy2d, n_out, X[:, K:K + R], 0.0, 0), Bs, [(c, o) for (o, rows, c) in meta],
+                             tr=True)
+        dAs = _scatter_grads(_lora_tsum(X, K, dxa, p, seed), As, [(i * r, 0) for i in range(n)], tr=False)
         dx = None
         if ctx.needs_input_grad[0]:
             dx = _lora_bwd_dx(base, dxa, acat, p, seed).view(xshape)

@@ -490,8 +490,10 @@ def test_lora_fwd_bwd_kernels(K, R, p):
     x = torch.randn(T, K, device="cuda", dtype=torch.bfloat16)
     A = (torch.randn(R, K, device="cuda") * 0.05).to(torch.bfloat16)
     for ldX in (0, K + 128):  # unpadded and padded to a whole 128-column K-tile pair (zeros past K + R)
-        X, xd = _ext.ops().lora_fwd(x, A, 0.5, p, 99, ldX)
+        X, xd = _ext.ops().lora_fwd(x, A, 0.5, p, 99, ldX, True)
         Xr, xdr = ref.lora_fwd(x, A, 0.5, p, 99, ldX)
+        X2, xd2 = _ext.ops().lora_fwd(x, A, 0.5, p, 99, ldX)  # default: no saved dropout(x)
+        assert torch.equal(X2, X) and xd2.numel() == 0
         assert X.shape == Xr.shape == (T, ldX or K + R)
         assert torch.equal(X[:, :K], x)
         assert (X[:, K:].float() - Xr[:, K:].float()).abs().max().item() < 2e-2 * (Xr[:, K:].float().abs().max().item() + 1)
@@ -504,6 +506,25 @@ def test_lora_fwd_bwd_kernels(K, R, p):
     dx = _ext.ops().lora_bwd_dx(base, dxa, A, p, 99)
     dxr = ref.lora_bwd_dx(base, dxa, A, p, 99)
     assert (dx.float() - dxr.float()).abs().max().item() < 3e-2
+    # dA = dxa^T dropout(x) with the mask regenerated from the seed, x read from the widened activation X'
+    dA = _ext.ops().lora_tsum(X, K, dxa, p, 99)
+    xs = ref.dropout_add(None, x, p, 99) if p > 0 else x
+    dAr = dxa.float().t() @ xs.float()
+    assert dA.dtype == torch.float32 and dA.shape == (R, K)
+    assert rel_err(dA, dAr) < 1e-2
+    # dB^T = (s xa)^T dy with S a column slice of X' (row stride ldX), no dropout; then the one-launch scatter into
+    # bf16 / fp32 gradients, written and accumulated, transposed
+    n_out = 640
+    dy = torch.randn(T, n_out, device="cuda", dtype=torch.bfloat16)
+    S = X[:, K:K + R]
+    sB = _ext.ops().lora_tsum(dy, n_out, S, 0.0, 0)
+    assert rel_err(sB, S.float().t() @ dy.float()) < 1e-2
+    o1 = torch.randn(n_out // 2, 16, device="cuda", dtype=torch.bfloat16)
+    o2 = torch.zeros(n_out - n_out // 2, 16, device="cuda", dtype=torch.float32)
+    o1_ref = o1.float() + sB[0:16, 0:n_out // 2].t()
+    _ext.ops().lora_grad_out(sB, [o1, o2], [0, R - 16], [0, n_out // 2], True, [1, 0])
+    assert rel_err(o1, o1_ref) < 1e-2
+    assert torch.allclose(o2, sB[R - 16:R, n_out // 2:].t())
 
 
 @pytest.mark.parametrize("cfg", [0, 2, 5, 6, 11])
