@@ -97,10 +97,13 @@ __global__ __launch_bounds__(512) void fwd_kernel(const u16* __restrict__ x, con
 
 // tile: 64 rows x 512 columns per 512-thread block; thread = 8 rows x 8 columns (the A tile in LDS is
 // reused by 64 rows).
-template <int R>
+// With gu ([T, 2K] = gate | up, the SwiGLU input): the SwiGLU backward is applied to dx on the way out and
+// dgu [T, 2K] is written instead (the down projection of a LoRA MLP: no dx round trip through HBM).
+template <int R, bool SWIGLU>
 __global__ __launch_bounds__(512) void bwd_dx_kernel(const u16* __restrict__ base, long ldb, const u16* __restrict__ dxa,
                                                      const u16* __restrict__ A, u16* __restrict__ dx, long T, int K,
-                                                     unsigned thresh, float dscale, unsigned seed, int drop) {
+                                                     unsigned thresh, float dscale, unsigned seed, int drop,
+                                                     const u16* __restrict__ gu) {
   __shared__ float As[R][512];
   __shared__ float Ds[64][R];
   const int tid = threadIdx.x;
@@ -155,7 +158,22 @@ __global__ __launch_bounds__(512) void bwd_dx_kernel(const u16* __restrict__ bas
       const bool keep = !drop || hash_u32(idx + j, seed) >= thresh;
       o[j] += keep ? acc[i][j] * dscale : 0.f;
     }
-    *(uint4*)(dx + t * (long)K + k) = pack8(o);
+    if constexpr (SWIGLU) {  // o = dact (fp32); the same arithmetic as swiglu_bwd_kernel on the bf16-rounded dact
+      float gt[8], up[8], dg[8], du[8];
+      unpack8(*(const uint4*)(gu + t * 2L * K + k), gt);
+      unpack8(*(const uint4*)(gu + t * 2L * K + K + k), up);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float d = bf2f(f2bf(o[j]));
+        const float sg = 1.f / (1.f + __expf(-gt[j]));
+        du[j] = d * gt[j] * sg;
+        dg[j] = d * up[j] * sg * (1.f + gt[j] * (1.f - sg));
+      }
+      *(uint4*)(dx + t * 2L * K + k) = pack8(dg);
+      *(uint4*)(dx + t * 2L * K + K + k) = pack8(du);
+    } else {
+      *(uint4*)(dx + t * (long)K + k) = pack8(o);
+    }
   }
 }
 
@@ -332,8 +350,10 @@ std::tuple<at::Tensor, at::Tensor> lora_fwd(const at::Tensor& x, const at::Tenso
   return {X, xd};
 }
 
-// dx = base + keep * (dxa @ A) / (1-p); base [T, K] with row stride ldb (a column slice is fine)
-at::Tensor lora_bwd_dx(const at::Tensor& base, const at::Tensor& dxa, const at::Tensor& A, double p, int64_t seed) {
+// dx = base + keep * (dxa @ A) / (1-p); base [T, K] with row stride ldb (a column slice is fine). With gu [T, 2K]
+// (gate | up): returns dgu = swiglu_bwd(dx, gu) [T, 2K] instead.
+at::Tensor lora_bwd_dx(const at::Tensor& base, const at::Tensor& dxa, const at::Tensor& A, double p, int64_t seed,
+                       const c10::optional<at::Tensor>& gu) {
   SFT_CHECK_CUDA(base);
   SFT_CHECK_BF16(base);
   SFT_CHECK_BF16(dxa);
@@ -344,17 +364,27 @@ at::Tensor lora_bwd_dx(const at::Tensor& base, const at::Tensor& dxa, const at::
   const int K = base.size(1), R = A.size(0);
   SFT_CHECK(base.stride(1) == 1 && base.stride(0) % 8 == 0 && K % 8 == 0, "lora_bwd_dx: base layout");
   SFT_CHECK(dxa.size(0) == T && dxa.size(1) == R && A.size(1) == K && R % 16 == 0 && R <= 64, "lora_bwd_dx: shapes");
-  auto dx = at::empty({T, K}, base.options());
+  const bool sw = gu.has_value() && gu->defined();
+  if (sw) {
+    SFT_CHECK_BF16(*gu);
+    SFT_CHECK_CONTIG(*gu);
+    SFT_CHECK(gu->size(0) == T && gu->size(1) == 2L * K, "lora_bwd_dx: gu [T, 2K]");
+  }
+  auto dx = at::empty({T, sw ? 2L * K : (long)K}, base.options());
   if (T == 0) return dx;
   float dscale;
   const unsigned thresh = lora::thresh_of(p, &dscale);
   dim3 grid((K + 511) / 512, (unsigned)((T + 63) / 64));
   SFT_CHECK(grid.y <= 65535u, "lora_bwd_dx: T too large");
 #define LORA_BWD(RR)                                                                                              \
-  lora::bwd_dx_kernel<RR><<<grid, 512, 0, cur_stream()>>>((const u16*)base.data_ptr(), base.stride(0),            \
-                                                          (const u16*)dxa.data_ptr(), (const u16*)A.data_ptr(),    \
-                                                          (u16*)dx.data_ptr(), T, K, thresh, dscale, (unsigned)seed, \
-                                                          p > 0 ? 1 : 0)
+  if (sw)                                                                                                         \
+    lora::bwd_dx_kernel<RR, true><<<grid, 512, 0, cur_stream()>>>(                                               \
+        (const u16*)base.data_ptr(), base.stride(0), (const u16*)dxa.data_ptr(), (const u16*)A.data_ptr(),        \
+        (u16*)dx.data_ptr(), T, K, thresh, dscale, (unsigned)seed, p > 0 ? 1 : 0, (const u16*)gu->data_ptr());    \
+  else                                                                                                            \
+    lora::bwd_dx_kernel<RR, false><<<grid, 512, 0, cur_stream()>>>(                                              \
+        (const u16*)base.data_ptr(), base.stride(0), (const u16*)dxa.data_ptr(), (const u16*)A.data_ptr(),        \
+        (u16*)dx.data_ptr(), T, K, thresh, dscale, (unsigned)seed, p > 0 ? 1 : 0, nullptr)
   switch (R / 16) {
     case 1: LORA_BWD(16); break;
     case 2: LORA_BWD(32); break;

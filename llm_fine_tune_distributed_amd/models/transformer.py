@@ -93,8 +93,7 @@ class MLP(nn.Module):
         L = self.lora
         if L is None:  # SwiGLU fused into the GEMM epilogues where the kernels apply (ops.swiglu_mlp)
             return ops.swiglu_mlp(h, self.gate_up_proj, self.down_proj)
-        a = ops.swiglu(ops.lora_linear(h, self.gate_up_proj, L["gate_up"]))
-        return ops.lora_linear(a, self.down_proj, L["down"])
+        return ops.lora_swiglu_mlp(h, self.gate_up_proj, self.down_proj, L["gate_up"], L["down"])
 
 
 class DecoderLayer(nn.Module):

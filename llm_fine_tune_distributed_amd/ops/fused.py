@@ -897,10 +897,13 @@ def _scatter_grads(total: torch.Tensor, params, blocks, tr: bool):
     return out
 
 
-def _lora_bwd_dx(base, dxa, acat, p, seed):
+def _lora_bwd_dx(base, dxa, acat, p, seed, gu=None):
+    """dx = base + dropout(dxa A_cat); with gu (the SwiGLU input of a LoRA MLP's down projection) dgu =
+    swiglu_bwd(dx, gu) instead, in the same pass (csrc/lora.hip bwd_dx_kernel: no dx round trip)."""
     if _ext.use_hip(base) and acat.shape[0] % 16 == 0 and acat.shape[0] <= 64:
-        return _ext.ops().lora_bwd_dx(base, dxa, acat, float(p), int(seed))
-    return ref.lora_bwd_dx(base, dxa, acat, p, seed)
+        return _ext.ops().lora_bwd_dx(base, dxa, acat, float(p), int(seed), gu)
+    dx = ref.lora_bwd_dx(base, dxa, acat, p, seed)
+    return dx if gu is None else swiglu_bwd(dx, gu)
 
 
 _PARAM_EPOCH = [0]
@@ -937,6 +940,52 @@ def _lora_gemm(X: torch.Tensor, wide: torch.Tensor) -> torch.Tensor:
 _LORA_FWD_CFG = 164  # persistent 4-wave kernel, plain stores (csrc/gemm_tn.hip)
 
 
+def _lora_wide_prep(x, wide, K, scaling, p, seed, meta, ab):
+    """X' = [x | s dropout(x) A_cat^T | 0] for the wide GEMM (and the adapters' B blocks synced into W')."""
+    n = len(ab) // 2
+    As, Bs = ab[:n], ab[n:]
+    r = As[0].shape[0]
+    x2d = x.reshape(-1, K)
+    if not x2d.is_contiguous():
+        x2d = x2d.contiguous()
+    _sync_wide(wide, K, r, meta, Bs)
+    acat = As[0].contiguous() if n == 1 else torch.cat(As, 0)
+    X = _lora_fwd(x2d, acat, scaling, p, seed, wide.shape[1])
+    return X, acat, (K, r * n, r, n, float(scaling), float(p), int(seed), tuple(meta), x.shape)
+
+
+def _lora_wide_bwd(X, acat, wide, ab, state, dy2d, need_dx, gu=None):
+    """The wide LoRA backward (see LoRAWideFn). Returns (dx — or dgu = swiglu_bwd(dx, gu) when gu is given —, dAs,
+    dBs); the adapter gradients are None where they went straight into main_grad."""
+    K, R, r, n, scaling, p, seed, meta, _ = state
+    As, Bs = ab[:n], ab[n:]
+    if not dy2d.is_contiguous():
+        dy2d = dy2d.contiguous()
+    base = dgrad_mm(dy2d, wide[:, :K])              # [T, K] (HIP 4-wave dgrad where the shapes allow)
+    # dxa = s dy B_blockdiag [T, R] (the scale as the GEMM's alpha, no extra pass)
+    dxa = torch.addmm(dy2d.new_empty(dy2d.shape[0], R), dy2d, wide[:, K:K + R], beta=0, alpha=scaling)
+    # the adapter gradients of all sub-projections, each from one pass over its wide operand, scattered straight into
+    # the parameters' flat gradient slices in one launch (no per-adapter GEMMs, slicing copies or autograd
+    # accumulation): dB^T = (s xa)^T dy [R, n_out] (block (c_i, o_i) transposed is dB_i); dA = dxa^T dropout(x)
+    # [R, K] (the forward's dropout mask regenerated from the seed: nothing saved)
+    n_out = dy2d.shape[1]
+    dBs = _scatter_grads(_lora_tsum(dy2d, n_out, X[:, K:K + R], 0.0, 0), Bs, [(c, o) for (o, rows, c) in meta],
+                         tr=True)
+    dAs = _scatter_grads(_lora_tsum(X, K, dxa, p, seed), As, [(i * r, 0) for i in range(n)], tr=False)
+    dx = _lora_bwd_dx(base, dxa, acat, p, seed, gu) if need_dx else None
+    return dx, dAs, dBs
+
+
+def swiglu_bwd(dact: torch.Tensor, gu: torch.Tensor) -> torch.Tensor:
+    """dgu = d(silu(gate) * up) / d(gate, up) for the upstream dact (the SwiGLU kernel's backward)."""
+    if _ext.use_hip(gu):
+        return _ext.ops().swiglu_bwd(dact.contiguous(), gu)
+    g, u = gu.float().chunk(2, dim=-1)
+    sg = torch.sigmoid(g)
+    d = dact.float()
+    return torch.cat([d * u * (sg * (1 + g * (1 - sg))), d * g * sg], dim=-1).to(gu.dtype)
+
+
 class LoRAWideFn(Function):
     """LoRA folded into the base GEMM (models.lora.FusedLoRA.wide).
 
@@ -946,27 +995,16 @@ class LoRAWideFn(Function):
         forward:  y = X' W'^T                      (one HIP GEMM, K+Rp deep: no rank-r pass over y)
         backward: base = dy W                      (the 4-wave HIP dgrad on W's column block of W')
                   dxa  = s dy B_blockdiag          (thin [T, R] product, s as the GEMM's alpha)
-                  dB_i = dy_i^T X'[:, K+c_i:K+c_i+r] (per adapter, into its main_grad slice)
-                  dA = dxa^T dropout(x)            (csrc/lora.hip lora_da: the mask regenerated from the seed)
+                  dB^T = (s xa)^T dy, dA = dxa^T dropout(x) (csrc/lora.hip tsum: one pass over dy / x each, the
+                                                   dropout mask regenerated from the seed; scattered into main_grad)
                   dx = base + dropout(dxa A_cat)   (csrc/lora.hip lora_bwd_dx: one pass)"""
 
     @staticmethod
     def forward(ctx, x, wide, K, scaling, p, seed, meta, *ab):
-        n = len(ab) // 2
-        As, Bs = ab[:n], ab[n:]
-        r = As[0].shape[0]
-        R = r * n
-        x2d = x.reshape(-1, K)
-        if not x2d.is_contiguous():
-            x2d = x2d.contiguous()
-        _sync_wide(wide, K, r, meta, Bs)
-        acat = As[0].contiguous() if n == 1 else torch.cat(As, 0)
-        X = _lora_fwd(x2d, acat, scaling, p, seed, wide.shape[1])
+        X, acat, state = _lora_wide_prep(x, wide, K, scaling, p, seed, meta, ab)
         y = _lora_gemm(X, wide)
         ctx.save_for_backward(X, acat)
-        ctx.wide = wide
-        ctx.adapters = ab  # the parameters themselves: their gradients go to main_grad directly
-        ctx.meta = (K, R, r, n, float(scaling), float(p), int(seed), tuple(meta), x.shape)
+        ctx.wide, ctx.adapters, ctx.meta = wide, ab, state  # adapter gradients go to main_grad directly
         if x.dim() == 2:
             return y
         return y.view(*x.shape[:-1], wide.shape[0])
@@ -974,40 +1012,98 @@ class LoRAWideFn(Function):
     @staticmethod
     def backward(ctx, dy):
         X, acat = ctx.saved_tensors
-        K, R, r, n, scaling, p, seed, meta, xshape = ctx.meta
-        wide = ctx.wide
-        As, Bs = ctx.adapters[:n], ctx.adapters[n:]
-        dy2d = dy.reshape(-1, dy.shape[-1])
-        if not dy2d.is_contiguous():
-            dy2d = dy2d.contiguous()
-        base = dgrad_mm(dy2d, wide[:, :K])              # [T, K] (HIP 4-wave dgrad where the shapes allow)
-        # dxa = s dy B_blockdiag [T, R] (the scale as the GEMM's alpha, no extra pass)
-        dxa = torch.addmm(dy2d.new_empty(dy2d.shape[0], R), dy2d, wide[:, K:K + R], beta=0, alpha=scaling)
-        # the adapter gradients of all sub-projections, each from one pass over its wide operand, scattered straight into
-        # the parameters' flat gradient slices in one launch (no per-adapter GEMMs, slicing copies or autograd
-        # accumulation): dB^T = (s xa)^T dy [R, n_out] (block (c_i, o_i) transposed is dB_i); dA = dxa^T dropout(x)
-        # [R, K] (the forward's dropout mask regenerated from the seed: nothing saved)
-        n_out = dy2d.shape[1]
-        dBs = _scatter_grads(_lora_tsum(dy2d, n_out, X[:, K:K + R], 0.0, 0), Bs, [(c, o) for (o, rows, c) in meta],
-                             tr=True)
-        dAs = _scatter_grads(_lora_tsum(X, K, dxa, p, seed), As, [(i * r, 0) for i in range(n)], tr=False)
-        dx = None
-        if ctx.needs_input_grad[0]:
-            dx = _lora_bwd_dx(base, dxa, acat, p, seed).view(xshape)
+        dx, dAs, dBs = _lora_wide_bwd(X, acat, ctx.wide, ctx.adapters, ctx.meta, dy.reshape(-1, dy.shape[-1]),
+                                      ctx.needs_input_grad[0])
+        if dx is not None:
+            dx = dx.view(ctx.meta[-1])
         return (dx, None, None, None, None, None, None, *dAs, *dBs)
+
+
+class LoRAGateUpActFn(Function):
+    """(gu, act) = the LoRA-widened gate_up GEMM and its SwiGLU; act is non-differentiable here — its consumer
+    (LoRASwiGLUDownFn) returns the gradient of gu directly. (The persistent GEMM's SwiGLU epilogue, writing both in one
+    pass, measured slower here than the plain wide GEMM + the SwiGLU kernel: 688 vs ~665 us at 8192 x 22016, r4_run20.)"""
+
+    @staticmethod
+    def forward(ctx, x, wide, K, scaling, p, seed, meta, *ab):
+        X, acat, state = _lora_wide_prep(x, wide, K, scaling, p, seed, meta, ab)
+        gu = _lora_gemm(X, wide)
+        act = _ext.ops().swiglu_fwd(gu)
+        ctx.save_for_backward(X, acat)
+        ctx.wide, ctx.adapters, ctx.meta = wide, ab, state
+        ctx.mark_non_differentiable(act)
+        lead = tuple(x.shape[:-1])
+        return gu.view(*lead, gu.shape[-1]), act.view(*lead, act.shape[-1])
+
+    @staticmethod
+    def backward(ctx, dgu, _dact):
+        X, acat = ctx.saved_tensors
+        dx, dAs, dBs = _lora_wide_bwd(X, acat, ctx.wide, ctx.adapters, ctx.meta, dgu.reshape(-1, dgu.shape[-1]),
+                                      ctx.needs_input_grad[0])
+        if dx is not None:
+            dx = dx.view(ctx.meta[-1])
+        return (dx, None, None, None, None, None, None, *dAs, *dBs)
+
+
+class LoRASwiGLUDownFn(Function):
+    """y = the LoRA-widened down projection of act (produced together with gu by LoRAGateUpActFn); the backward
+    applies the SwiGLU backward to its dx and returns dgu (the gradient of gu) directly."""
+
+    @staticmethod
+    def forward(ctx, gu, act, wide, K, scaling, p, seed, meta, *ab):
+        X, acat, state = _lora_wide_prep(act, wide, K, scaling, p, seed, meta, ab)
+        y = _lora_gemm(X, wide)
+        ctx.save_for_backward(X, acat, gu)
+        ctx.wide, ctx.adapters, ctx.meta = wide, ab, state
+        return y.view(*act.shape[:-1], wide.shape[0])
+
+    @staticmethod
+    def backward(ctx, dy):
+        X, acat, gu = ctx.saved_tensors
+        gu2d = gu.reshape(-1, gu.shape[-1])
+        dgu, dAs, dBs = _lora_wide_bwd(X, acat, ctx.wide, ctx.adapters, ctx.meta, dy.reshape(-1, dy.shape[-1]),
+                                       ctx.needs_input_grad[0], gu=gu2d)
+        if dgu is not None:
+            dgu = dgu.view(gu.shape)
+        return (dgu, None, None, None, None, None, None, None, *dAs, *dBs)
+
+
+def _lora_wide_args(lora, weight):
+    """(wide args, As, Bs) when the adapter runs on the wide path for this weight, else None."""
+    wide = getattr(lora, "wide", None)
+    if wide is None or weight.data_ptr() != wide.data_ptr() or weight.shape[1] != lora.in_features:
+        return None
+    As = [a for a, act in zip(lora.A, lora.active) if act]
+    Bs = [b for b, act in zip(lora.B, lora.active) if act]
+    if not As:
+        return None
+    p = lora.dropout.p if isinstance(lora.dropout, torch.nn.Dropout) and lora.training else 0.0
+    seed = int(torch.randint(1, 2 ** 31 - 1, (1,)).item()) if p > 0 else 0
+    return (wide, lora.in_features, float(lora.scaling), float(p), seed, tuple(lora.wide_meta)), As, Bs
+
+
+def lora_swiglu_mlp(h, w_gate_up, w_down, l_gate_up, l_down) -> torch.Tensor:
+    """down(swiglu(gate_up(h))) with LoRA adapters on both projections: on the HIP wide path one node per projection
+    with the down projection's backward returning dgu (the SwiGLU backward applied to its dx); otherwise the plain
+    composition of lora_linear and swiglu."""
+    gu_args, dn_args = _lora_wide_args(l_gate_up, w_gate_up), _lora_wide_args(l_down, w_down)
+    h2d = h.reshape(-1, h.shape[-1])
+    if (gu_args is not None and dn_args is not None and _ext.use_hip(h2d) and h2d.shape[0] % 256 == 0
+            and gu_args[0][0].shape[0] % 256 == 0 and (gu_args[0][0].shape[0] // 2) % 128 == 0
+            and gu_args[0][0].shape[1] % 128 == 0):
+        (a, ga_As, ga_Bs), (b, dn_As, dn_Bs) = gu_args, dn_args
+        gu, act = LoRAGateUpActFn.apply(h, *a, *ga_As, *ga_Bs)
+        return LoRASwiGLUDownFn.apply(gu, act, *b, *dn_As, *dn_Bs)
+    return lora_linear(swiglu(lora_linear(h, w_gate_up, l_gate_up)), w_down, l_down)
 
 
 def lora_linear(x, weight, lora) -> torch.Tensor:
     """``lora``: a models.lora.FusedLoRA module (adapters per sub-projection)."""
+    w = _lora_wide_args(lora, weight)
+    if w is not None:
+        a, As, Bs = w
+        return LoRAWideFn.apply(x, *a, *As, *Bs)
     p = lora.dropout.p if isinstance(lora.dropout, torch.nn.Dropout) and lora.training else 0.0
-    wide = getattr(lora, "wide", None)
-    if wide is not None and weight.data_ptr() == wide.data_ptr() and weight.shape[1] == lora.in_features:
-        As = [a for a, act in zip(lora.A, lora.active) if act]
-        Bs = [b for b, act in zip(lora.B, lora.active) if act]
-        if As:
-            seed = int(torch.randint(1, 2 ** 31 - 1, (1,)).item()) if p > 0 else 0
-            return LoRAWideFn.apply(x, wide, lora.in_features, float(lora.scaling), float(p), seed,
-                                    tuple(lora.wide_meta), *As, *Bs)
     return LoRALinearFn.apply(x, weight, float(lora.scaling), float(p), tuple(lora.out_splits), *lora.A, *lora.B)
 
 

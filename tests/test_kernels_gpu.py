@@ -506,6 +506,10 @@ def test_lora_fwd_bwd_kernels(K, R, p):
     dx = _ext.ops().lora_bwd_dx(base, dxa, A, p, 99)
     dxr = ref.lora_bwd_dx(base, dxa, A, p, 99)
     assert (dx.float() - dxr.float()).abs().max().item() < 3e-2
+    # with the SwiGLU input: dgu = swiglu_bwd(dx, gu) in the same pass == the two kernels back to back
+    gu = torch.randn(T, 2 * K, device="cuda", dtype=torch.bfloat16)
+    dgu = _ext.ops().lora_bwd_dx(base, dxa, A, p, 99, gu)
+    assert torch.equal(dgu, _ext.ops().swiglu_bwd(dx, gu))
     # dA = dxa^T dropout(x) with the mask regenerated from the seed, x read from the widened activation X'
     dA = _ext.ops().lora_tsum(X, K, dxa, p, 99)
     xs = ref.dropout_add(None, x, p, 99) if p > 0 else x

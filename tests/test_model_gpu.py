@@ -160,8 +160,11 @@ def test_lora_wide_gpu_matches_unfused():
     out = m(ids, labels=ids)
     out.loss.backward()
     g1 = {n: p.grad.float().clone() for n, p in m.named_parameters() if p.grad is not None}
-    orig = T.ops.lora_linear
+    # the HIP run above took the fused MLP (gate_up GEMM with the SwiGLU epilogue, down backward returning dgu:
+    # ops.lora_swiglu_mlp); the reference composes the unfused LoRA linears with the SwiGLU op (same seed order)
+    orig, orig_mlp = T.ops.lora_linear, T.ops.lora_swiglu_mlp
     T.ops.lora_linear = unfused
+    T.ops.lora_swiglu_mlp = lambda h, wg, wd, lg, ld: unfused(ops.swiglu(unfused(h, wg, lg)), wd, ld)
     try:
         for p in m.parameters():
             p.grad = None
@@ -169,7 +172,7 @@ def test_lora_wide_gpu_matches_unfused():
         out2 = m(ids, labels=ids)
         out2.loss.backward()
     finally:
-        T.ops.lora_linear = orig
+        T.ops.lora_linear, T.ops.lora_swiglu_mlp = orig, orig_mlp
     assert abs(out.loss.item() - out2.loss.item()) < 2e-2
     for n, p in m.named_parameters():
         if p.grad is not None:
