@@ -62,7 +62,7 @@ TORCH_LIBRARY(sftamd, m) {
   m.def("embedding_fwd(Tensor ids, Tensor weight) -> Tensor");
   m.def("dropout_add(Tensor? a, Tensor b, float p, int seed) -> Tensor");
   m.def("lora_widen(Tensor x, int R, float p, int seed) -> (Tensor, Tensor)");
-  m.def("lora_fwd(Tensor x, Tensor A, float s, float p, int seed, int ldX=0, bool save_xd=False) -> (Tensor, Tensor)");
+  m.def("lora_fwd(Tensor x, Tensor A, float s, float p, int seed, int ldX=0, bool save_xd=False, bool swiglu=False) -> (Tensor, Tensor)");
   m.def("lora_bwd_dx(Tensor base, Tensor dxa, Tensor A, float p, int seed, Tensor? gu=None) -> Tensor");
   m.def("lora_tsum(Tensor X, int K, Tensor S, float p, int seed) -> Tensor");
   m.def("lora_grad_out(Tensor sum, Tensor(a!)[] outs, int[] r0, int[] c0, bool tr, int[] accumulate) -> ()");

@@ -26,7 +26,9 @@ __device__ __forceinline__ f32x4 mfma(const bf16x8& a, const bf16x8& b, const f3
 
 // block = 8 waves, 16 rows; wave w reduces k in [w*KW, (w+1)*KW), KW = K/8 (multiple of 32), four
 // 32-column steps in flight per iteration (the kernel is a stream over x: latency, not math, bound).
-template <int RF>  // R = 16 * RF adapter columns
+// SW: x is the SwiGLU input gu [T, 2K] (gate | up) and the widened activation is act = silu(gate) * up, rounded to bf16
+// as the SwiGLU kernel does (the LoRA MLP's down projection: no separate SwiGLU pass, no act tensor).
+template <int RF, bool SW = false>  // R = 16 * RF adapter columns
 __global__ __launch_bounds__(512) void fwd_kernel(const u16* __restrict__ x, const u16* __restrict__ A,
                                                   u16* __restrict__ X, u16* __restrict__ xd, long T, int K, long ldX,
                                                   float s, unsigned thresh, float dscale, unsigned seed, int drop) {
@@ -43,34 +45,65 @@ __global__ __launch_bounds__(512) void fwd_kernel(const u16* __restrict__ x, con
   f32x4 acc[RF];
 #pragma unroll
   for (int j = 0; j < RF; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  for (int k = kb; k < kb + KW; k += 32 * U) {
-    uint4 v[U];
+  // software pipeline: the next 128 columns' loads are in flight while this step's are processed (row index clamped
+  // for the loads, the store predicated; columns past the wave's range reload its first chunk and are skipped)
+  constexpr int NV = SW ? 2 : 1;
+  const long tc = rowok ? t : T - 1;
+  const int kend = kb + KW;
+  auto load = [&](int k, uint4(&rw)[U][NV]) {
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-      const int kk = k + 32 * u + 8 * g;
-      v[u] = (rowok && kk < kb + KW) ? *(const uint4*)(x + t * K + kk) : make_uint4(0, 0, 0, 0);
+      const int kk = k + 32 * u + 8 * g, kc = kk < kend ? kk : kb;
+      if constexpr (SW) {
+        rw[u][0] = *(const uint4*)(x + tc * 2L * K + kc);
+        rw[u][1] = *(const uint4*)(x + tc * 2L * K + K + kc);
+      } else {
+        rw[u][0] = *(const uint4*)(x + tc * K + kc);
+      }
     }
+  };
+  auto step = [&](int k, const uint4(&rw)[U][NV]) {
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const int kk = k + 32 * u + 8 * g;
-      if (kk >= kb + KW) break;
-      if (rowok) *(uint4*)(X + t * ldX + kk) = v[u];
+      if (kk >= kend) break;
+      uint4 v;
+      if constexpr (SW) {
+        float ga[8], up[8], o[8];
+        unpack8(rw[u][0], ga);
+        unpack8(rw[u][1], up);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) o[i] = ga[i] / (1.f + __expf(-ga[i])) * up[i];
+        v = pack8(o);
+      } else {
+        v = rw[u][0];
+      }
+      if (rowok) *(uint4*)(X + t * ldX + kk) = v;
       if (drop) {
         float f[8];
-        unpack8(v[u], f);
+        unpack8(v, f);
         const unsigned long long idx = (unsigned long long)t * K + kk;
 #pragma unroll
         for (int i = 0; i < 8; ++i) f[i] = hash_u32(idx + i, seed) >= thresh ? f[i] * dscale : 0.f;
-        v[u] = pack8(f);
-        if (xd && rowok) *(uint4*)(xd + t * K + kk) = v[u];
+        v = pack8(f);
+        if (xd && rowok) *(uint4*)(xd + t * K + kk) = v;
       }
-      const bf16x8 a = __builtin_bit_cast(bf16x8, v[u]);
+      const bf16x8 a = __builtin_bit_cast(bf16x8, v);
 #pragma unroll
       for (int j = 0; j < RF; ++j) {
         const bf16x8 b = __builtin_bit_cast(bf16x8, *(const uint4*)(A + (long)(16 * j + r) * K + kk));
         acc[j] = mfma(a, b, acc[j]);
       }
     }
+  };
+  uint4 ra[U][NV], rb[U][NV];
+  load(kb, ra);
+  for (int k = kb; k < kend; k += 64 * U) {
+    if (k + 32 * U < kend) load(k + 32 * U, rb);
+    step(k, ra);
+    if (k + 32 * U >= kend) break;
+    if (k + 64 * U < kend) load(k + 64 * U, ra);
+    step(k + 32 * U, rb);
   }
   // C layout: lane (g, r) holds rows 4g+i, column 16j + r
 #pragma unroll
@@ -95,8 +128,9 @@ __global__ __launch_bounds__(512) void fwd_kernel(const u16* __restrict__ x, con
   }
 }
 
-// tile: 64 rows x 512 columns per 512-thread block; thread = 8 rows x 8 columns (the A tile in LDS is
-// reused by 64 rows).
+// tile: 32 rows x 512 columns per 512-thread block; thread = 4 rows x 8 columns (the A tile in LDS is
+// reused by 32 rows). The thread's base (and gu) rows are loaded BEFORE the rank-R product loop (row indices
+// clamped, stores predicated), so the HBM latency hides under the FMAs instead of serialising row by row after it.
 // With gu ([T, 2K] = gate | up, the SwiGLU input): the SwiGLU backward is applied to dx on the way out and
 // dgu [T, 2K] is written instead (the down projection of a LoRA MLP: no dx round trip through HBM).
 template <int R, bool SWIGLU>
@@ -104,33 +138,45 @@ __global__ __launch_bounds__(512) void bwd_dx_kernel(const u16* __restrict__ bas
                                                      const u16* __restrict__ A, u16* __restrict__ dx, long T, int K,
                                                      unsigned thresh, float dscale, unsigned seed, int drop,
                                                      const u16* __restrict__ gu) {
+  constexpr int RPT = 4, TR = 8 * RPT;
   __shared__ float As[R][512];
-  __shared__ float Ds[64][R];
+  __shared__ float Ds[TR][R];
   const int tid = threadIdx.x;
   const int k0 = blockIdx.x * 512;
-  const long t0 = (long)blockIdx.y * 64;
+  const long t0 = (long)blockIdx.y * TR;
+  const int c8 = tid & 63, rg = tid >> 6;
+  const int k = k0 + c8 * 8;
+  const int kc = k < K ? k : K - 8;
+  uint4 vb[RPT], vg[RPT], vu[RPT];
+#pragma unroll
+  for (int i = 0; i < RPT; ++i) {
+    const long t = min(t0 + rg * RPT + i, T - 1);
+    vb[i] = *(const uint4*)(base + t * ldb + kc);
+    if constexpr (SWIGLU) {
+      vg[i] = *(const uint4*)(gu + t * 2L * K + kc);
+      vu[i] = *(const uint4*)(gu + t * 2L * K + K + kc);
+    }
+  }
   for (int e = tid; e < R * 64; e += 512) {  // A[:, k0:k0+512] as 8-wide vectors
-    const int rr = e >> 6, c8 = e & 63, k = k0 + c8 * 8;
+    const int rr = e >> 6, cc = e & 63, kk = k0 + cc * 8;
     float f[8];
-    if (k < K) {
-      unpack8(*(const uint4*)(A + (long)rr * K + k), f);
+    if (kk < K) {
+      unpack8(*(const uint4*)(A + (long)rr * K + kk), f);
     } else {
 #pragma unroll
       for (int i = 0; i < 8; ++i) f[i] = 0.f;
     }
 #pragma unroll
-    for (int i = 0; i < 8; ++i) As[rr][c8 * 8 + i] = f[i];
+    for (int i = 0; i < 8; ++i) As[rr][cc * 8 + i] = f[i];
   }
-  for (int e = tid; e < 64 * R; e += 512) {
+  for (int e = tid; e < TR * R; e += 512) {
     const int row = e / R, col = e - row * R;
     Ds[row][col] = (t0 + row < T) ? bf2f(dxa[(t0 + row) * R + col]) : 0.f;
   }
   __syncthreads();
-  const int c8 = tid & 63, rg = tid >> 6;
-  const int k = k0 + c8 * 8;
-  float acc[8][8];
+  float acc[RPT][8];
 #pragma unroll
-  for (int i = 0; i < 8; ++i)
+  for (int i = 0; i < RPT; ++i)
 #pragma unroll
     for (int j = 0; j < 8; ++j) acc[i][j] = 0.f;
 #pragma unroll 4
@@ -139,19 +185,18 @@ __global__ __launch_bounds__(512) void bwd_dx_kernel(const u16* __restrict__ bas
     *(float4*)&a[0] = *(const float4*)&As[rr][c8 * 8];
     *(float4*)&a[4] = *(const float4*)&As[rr][c8 * 8 + 4];
 #pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      const float d = Ds[rg * 8 + i][rr];
+    for (int i = 0; i < RPT; ++i) {
+      const float d = Ds[rg * RPT + i][rr];
 #pragma unroll
       for (int j = 0; j < 8; ++j) acc[i][j] += d * a[j];
     }
   }
   if (k >= K) return;
 #pragma unroll
-  for (int i = 0; i < 8; ++i) {
-    const long t = t0 + rg * 8 + i;
-    if (t >= T) break;
+  for (int i = 0; i < RPT; ++i) {
+    const long t = t0 + rg * RPT + i;
     float o[8];
-    unpack8(*(const uint4*)(base + t * ldb + k), o);
+    unpack8(vb[i], o);
     const unsigned long long idx = (unsigned long long)t * K + k;
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
@@ -160,8 +205,8 @@ __global__ __launch_bounds__(512) void bwd_dx_kernel(const u16* __restrict__ bas
     }
     if constexpr (SWIGLU) {  // o = dact (fp32); the same arithmetic as swiglu_bwd_kernel on the bf16-rounded dact
       float gt[8], up[8], dg[8], du[8];
-      unpack8(*(const uint4*)(gu + t * 2L * K + k), gt);
-      unpack8(*(const uint4*)(gu + t * 2L * K + K + k), up);
+      unpack8(vg[i], gt);
+      unpack8(vu[i], up);
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
         const float d = bf2f(f2bf(o[j]));
@@ -169,10 +214,12 @@ __global__ __launch_bounds__(512) void bwd_dx_kernel(const u16* __restrict__ bas
         du[j] = d * gt[j] * sg;
         dg[j] = d * up[j] * sg * (1.f + gt[j] * (1.f - sg));
       }
-      *(uint4*)(dx + t * 2L * K + k) = pack8(dg);
-      *(uint4*)(dx + t * 2L * K + K + k) = pack8(du);
+      if (t < T) {
+        *(uint4*)(dx + t * 2L * K + k) = pack8(dg);
+        *(uint4*)(dx + t * 2L * K + K + k) = pack8(du);
+      }
     } else {
-      *(uint4*)(dx + t * (long)K + k) = pack8(o);
+      if (t < T) *(uint4*)(dx + t * (long)K + k) = pack8(o);
     }
   }
 }
@@ -316,29 +363,36 @@ static unsigned thresh_of(double p, float* dscale) {
 // x [T, K], A [R, K] (R = 16, 32, 48 or 64) -> (X' [T, ldX], xd): xd = dropout(x) [T, K] only with save_xd and
 // p > 0, else empty (the backward regenerates the mask from the seed: lora_da). ldX >= K + R (0 = K + R): columns
 // [K + R, ldX) are zero (the wide weight's padding to a whole K-tile pair of the HIP GEMMs)
+// swiglu: x is gu [T, 2K] and the widened activation is act = silu(gate) * up (see fwd_kernel SW)
 std::tuple<at::Tensor, at::Tensor> lora_fwd(const at::Tensor& x, const at::Tensor& A, double s, double p, int64_t seed,
-                                            int64_t ldX, bool save_xd) {
+                                            int64_t ldX, bool save_xd, bool swiglu) {
   SFT_CHECK_CUDA(x);
   SFT_CHECK_BF16(x);
   SFT_CHECK_BF16(A);
   SFT_CHECK_CONTIG(x);
   SFT_CHECK_CONTIG(A);
   const long T = x.size(0);
-  const int K = x.size(1), R = A.size(0);
+  SFT_CHECK(!swiglu || (x.size(1) % 2 == 0 && !save_xd), "lora_fwd swiglu: gu [T, 2K], no saved dropout(x)");
+  const int K = swiglu ? x.size(1) / 2 : x.size(1), R = A.size(0);
   SFT_CHECK(A.size(1) == K && K % 256 == 0 && R % 16 == 0 && R >= 16 && R <= 64, "lora_fwd: shapes");
   if (ldX <= 0) ldX = K + R;
   SFT_CHECK(ldX >= K + R && ldX % 8 == 0, "lora_fwd: ldX >= K + R, multiple of 8");
   auto X = at::empty({T, ldX}, x.options());
-  at::Tensor xd = (p > 0 && save_xd) ? at::empty_like(x) : at::empty({0}, x.options());
+  at::Tensor xd = (p > 0 && save_xd) ? at::empty({T, (long)K}, x.options()) : at::empty({0}, x.options());
   if (T == 0) return {X, xd};
   float dscale;
   const unsigned thresh = lora::thresh_of(p, &dscale);
   const int grid = (int)((T + 15) / 16);
   u16* xdp = (p > 0 && save_xd) ? (u16*)xd.data_ptr() : nullptr;
 #define LORA_FWD(RF)                                                                                              \
-  lora::fwd_kernel<RF><<<grid, 512, 0, cur_stream()>>>((const u16*)x.data_ptr(), (const u16*)A.data_ptr(),     \
-                                                       (u16*)X.data_ptr(), xdp, T, K, ldX, (float)s, thresh, dscale, \
-                                                       (unsigned)seed, p > 0 ? 1 : 0)
+  if (swiglu)                                                                                                     \
+    lora::fwd_kernel<RF, true><<<grid, 512, 0, cur_stream()>>>((const u16*)x.data_ptr(), (const u16*)A.data_ptr(), \
+                                                               (u16*)X.data_ptr(), xdp, T, K, ldX, (float)s, thresh, \
+                                                               dscale, (unsigned)seed, p > 0 ? 1 : 0);            \
+  else                                                                                                            \
+    lora::fwd_kernel<RF, false><<<grid, 512, 0, cur_stream()>>>((const u16*)x.data_ptr(), (const u16*)A.data_ptr(), \
+                                                                (u16*)X.data_ptr(), xdp, T, K, ldX, (float)s, thresh, \
+                                                                dscale, (unsigned)seed, p > 0 ? 1 : 0)
   switch (R / 16) {
     case 1: LORA_FWD(1); break;
     case 2: LORA_FWD(2); break;
@@ -374,7 +428,7 @@ at::Tensor lora_bwd_dx(const at::Tensor& base, const at::Tensor& dxa, const at::
   if (T == 0) return dx;
   float dscale;
   const unsigned thresh = lora::thresh_of(p, &dscale);
-  dim3 grid((K + 511) / 512, (unsigned)((T + 63) / 64));
+  dim3 grid((K + 511) / 512, (unsigned)((T + 31) / 32));
   SFT_CHECK(grid.y <= 65535u, "lora_bwd_dx: T too large");
 #define LORA_BWD(RR)                                                                                              \
   if (sw)                                                                                                         \

@@ -857,10 +857,13 @@ def _lora_hip(x2d, acat) -> bool:
     return _ext.use_hip(x2d) and x2d.shape[1] % 256 == 0 and acat.shape[0] % 16 == 0 and acat.shape[0] <= 64
 
 
-def _lora_fwd(x2d, acat, s, p, seed, ldX=0):
-    """X' = [x | s dropout(x) A^T | 0]; dropout(x) is not saved (lora_da regenerates the mask from the seed)."""
+def _lora_fwd(x2d, acat, s, p, seed, ldX=0, swiglu=False):
+    """X' = [x | s dropout(x) A^T | 0]; dropout(x) is not saved (lora_tsum regenerates the mask from the seed). swiglu:
+    x2d is gu [T, 2K] and x = silu(gate) * up is formed on the fly (no SwiGLU pass, no act tensor)."""
     if _lora_hip(x2d, acat):
-        return _ext.ops().lora_fwd(x2d, acat, float(s), float(p), int(seed), int(ldX))[0]
+        return _ext.ops().lora_fwd(x2d, acat, float(s), float(p), int(seed), int(ldX), False, bool(swiglu))[0]
+    if swiglu:
+        x2d = ref.swiglu(x2d.float()).to(x2d.dtype)
     return ref.lora_fwd(x2d, acat, s, p, seed, ldX)[0]
 
 
@@ -940,17 +943,18 @@ def _lora_gemm(X: torch.Tensor, wide: torch.Tensor) -> torch.Tensor:
 _LORA_FWD_CFG = 164  # persistent 4-wave kernel, plain stores (csrc/gemm_tn.hip)
 
 
-def _lora_wide_prep(x, wide, K, scaling, p, seed, meta, ab):
-    """X' = [x | s dropout(x) A_cat^T | 0] for the wide GEMM (and the adapters' B blocks synced into W')."""
+def _lora_wide_prep(x, wide, K, scaling, p, seed, meta, ab, swiglu=False):
+    """X' = [x | s dropout(x) A_cat^T | 0] for the wide GEMM (and the adapters' B blocks synced into W'); swiglu: x is
+    the SwiGLU input gu [.., 2K] and the activation silu(gate) * up is formed inside lora_fwd."""
     n = len(ab) // 2
     As, Bs = ab[:n], ab[n:]
     r = As[0].shape[0]
-    x2d = x.reshape(-1, K)
+    x2d = x.reshape(-1, 2 * K if swiglu else K)
     if not x2d.is_contiguous():
         x2d = x2d.contiguous()
     _sync_wide(wide, K, r, meta, Bs)
     acat = As[0].contiguous() if n == 1 else torch.cat(As, 0)
-    X = _lora_fwd(x2d, acat, scaling, p, seed, wide.shape[1])
+    X = _lora_fwd(x2d, acat, scaling, p, seed, wide.shape[1], swiglu)
     return X, acat, (K, r * n, r, n, float(scaling), float(p), int(seed), tuple(meta), x.shape)
 
 
@@ -1019,24 +1023,21 @@ class LoRAWideFn(Function):
         return (dx, None, None, None, None, None, None, *dAs, *dBs)
 
 
-class LoRAGateUpActFn(Function):
-    """(gu, act) = the LoRA-widened gate_up GEMM and its SwiGLU; act is non-differentiable here — its consumer
-    (LoRASwiGLUDownFn) returns the gradient of gu directly. (The persistent GEMM's SwiGLU epilogue, writing both in one
-    pass, measured slower here than the plain wide GEMM + the SwiGLU kernel: 688 vs ~665 us at 8192 x 22016, r4_run20.)"""
+class LoRAGateUpFn(Function):
+    """gu = the LoRA-widened gate_up GEMM (its SwiGLU is formed by the consumer, LoRASwiGLUDownFn, inside the down
+    projection's widening pass). (The persistent GEMM's SwiGLU epilogue writing gu and act measured slower than the
+    plain wide GEMM + the SwiGLU kernel: 688 vs ~665 us at 8192 x 22016, r4_run20.)"""
 
     @staticmethod
     def forward(ctx, x, wide, K, scaling, p, seed, meta, *ab):
         X, acat, state = _lora_wide_prep(x, wide, K, scaling, p, seed, meta, ab)
         gu = _lora_gemm(X, wide)
-        act = _ext.ops().swiglu_fwd(gu)
         ctx.save_for_backward(X, acat)
         ctx.wide, ctx.adapters, ctx.meta = wide, ab, state
-        ctx.mark_non_differentiable(act)
-        lead = tuple(x.shape[:-1])
-        return gu.view(*lead, gu.shape[-1]), act.view(*lead, act.shape[-1])
+        return gu.view(*x.shape[:-1], gu.shape[-1])
 
     @staticmethod
-    def backward(ctx, dgu, _dact):
+    def backward(ctx, dgu):
         X, acat = ctx.saved_tensors
         dx, dAs, dBs = _lora_wide_bwd(X, acat, ctx.wide, ctx.adapters, ctx.meta, dgu.reshape(-1, dgu.shape[-1]),
                                       ctx.needs_input_grad[0])
@@ -1046,16 +1047,17 @@ class LoRAGateUpActFn(Function):
 
 
 class LoRASwiGLUDownFn(Function):
-    """y = the LoRA-widened down projection of act (produced together with gu by LoRAGateUpActFn); the backward
-    applies the SwiGLU backward to its dx and returns dgu (the gradient of gu) directly."""
+    """y = the LoRA-widened down projection of silu(gate) * up: the widening pass reads gu and forms the activation on
+    the fly (csrc/lora.hip lora_fwd swiglu: no SwiGLU kernel, no act tensor); the backward applies the SwiGLU backward
+    inside the adapter-dx pass and returns dgu (the gradient of gu) directly."""
 
     @staticmethod
-    def forward(ctx, gu, act, wide, K, scaling, p, seed, meta, *ab):
-        X, acat, state = _lora_wide_prep(act, wide, K, scaling, p, seed, meta, ab)
+    def forward(ctx, gu, wide, K, scaling, p, seed, meta, *ab):
+        X, acat, state = _lora_wide_prep(gu, wide, K, scaling, p, seed, meta, ab, swiglu=True)
         y = _lora_gemm(X, wide)
         ctx.save_for_backward(X, acat, gu)
         ctx.wide, ctx.adapters, ctx.meta = wide, ab, state
-        return y.view(*act.shape[:-1], wide.shape[0])
+        return y.view(*gu.shape[:-1], wide.shape[0])
 
     @staticmethod
     def backward(ctx, dy):
@@ -1065,7 +1067,7 @@ class LoRASwiGLUDownFn(Function):
                                        ctx.needs_input_grad[0], gu=gu2d)
         if dgu is not None:
             dgu = dgu.view(gu.shape)
-        return (dgu, None, None, None, None, None, None, None, *dAs, *dBs)
+        return (dgu, None, None, None, None, None, None, *dAs, *dBs)
 
 
 def _lora_wide_args(lora, weight):
@@ -1083,17 +1085,17 @@ def _lora_wide_args(lora, weight):
 
 
 def lora_swiglu_mlp(h, w_gate_up, w_down, l_gate_up, l_down) -> torch.Tensor:
-    """down(swiglu(gate_up(h))) with LoRA adapters on both projections: on the HIP wide path one node per projection
-    with the down projection's backward returning dgu (the SwiGLU backward applied to its dx); otherwise the plain
-    composition of lora_linear and swiglu."""
+    """down(swiglu(gate_up(h))) with LoRA adapters on both projections: on the HIP wide path one node per projection,
+    the SwiGLU formed inside the down projection's widening pass and its backward inside the adapter-dx pass (the
+    node returns dgu); otherwise the plain composition of lora_linear and swiglu."""
     gu_args, dn_args = _lora_wide_args(l_gate_up, w_gate_up), _lora_wide_args(l_down, w_down)
     h2d = h.reshape(-1, h.shape[-1])
     if (gu_args is not None and dn_args is not None and _ext.use_hip(h2d) and h2d.shape[0] % 256 == 0
             and gu_args[0][0].shape[0] % 256 == 0 and (gu_args[0][0].shape[0] // 2) % 128 == 0
             and gu_args[0][0].shape[1] % 128 == 0):
         (a, ga_As, ga_Bs), (b, dn_As, dn_Bs) = gu_args, dn_args
-        gu, act = LoRAGateUpActFn.apply(h, *a, *ga_As, *ga_Bs)
-        return LoRASwiGLUDownFn.apply(gu, act, *b, *dn_As, *dn_Bs)
+        gu = LoRAGateUpFn.apply(h, *a, *ga_As, *ga_Bs)
+        return LoRASwiGLUDownFn.apply(gu, *b, *dn_As, *dn_Bs)
     return lora_linear(swiglu(lora_linear(h, w_gate_up, l_gate_up)), w_down, l_down)
 
 

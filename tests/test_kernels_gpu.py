@@ -500,7 +500,13 @@ def test_lora_fwd_bwd_kernels(K, R, p):
         assert not X[:, K + R:].any()
     if p > 0:
         assert torch.equal(xd, xdr)
-    wideb = torch.randn(T, K + 64, device="cuda", dtype=torch.bfloat16)
+    # swiglu: the widening pass reads gu [T, 2K] and forms silu(gate) * up itself == the SwiGLU kernel then lora_fwd
+    gu = torch.randn(T, 2 * K, device="cuda", dtype=torch.bfloat16)
+    act = _ext.ops().swiglu_fwd(gu)
+    Xs = _ext.ops().lora_fwd(gu, A, 0.5, p, 99, K + 128, False, True)[0]
+    Xa = _ext.ops().lora_fwd(act, A, 0.5, p, 99, K + 128)[0]
+    assert torch.equal(Xs, Xa)
+    wideb =torch.randn(T, K + 64, device="cuda", dtype=torch.bfloat16)
     base = wideb[:, :K]
     dxa = (torch.randn(T, R, device="cuda") * 0.1).to(torch.bfloat16)
     dx = _ext.ops().lora_bwd_dx(base, dxa, A, p, 99)

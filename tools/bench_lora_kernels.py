@@ -1,0 +1,50 @@
+"""Standalone timings of the LoRA streaming kernels (csrc/lora.hip) on the 7B MLP shapes (T = 8192 tokens):
+lora_fwd (plain and with the SwiGLU formed on the fly) and lora_bwd_dx (plain and writing dgu), vs their HBM floor."""
+import torch
+
+from llm_fine_tune_distributed_amd.ops import _ext
+
+
+def timeit(fn, it=20):
+    for _ in range(3):
+        fn()
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(it):
+        fn()
+    e1.record()
+    torch.cuda.synchronize()
+    return e0.elapsed_time(e1) / it * 1e3
+
+
+def main():
+    ops = _ext.ops()
+    T, H, I, R = 8192, 4096, 11008, 16
+    dev = "cuda"
+    gu = torch.randn(T, 2 * I, device=dev, dtype=torch.bfloat16)
+    x = torch.randn(T, I, device=dev, dtype=torch.bfloat16)
+    xh = torch.randn(T, H, device=dev, dtype=torch.bfloat16)
+    A = torch.randn(R, I, device=dev, dtype=torch.bfloat16) * 0.05
+    Ah = torch.randn(3 * R, H, device=dev, dtype=torch.bfloat16) * 0.05
+    dxa = torch.randn(T, R, device=dev, dtype=torch.bfloat16)
+    dxah = torch.randn(T, 3 * R, device=dev, dtype=torch.bfloat16)
+    base = torch.randn(T, I + 128, device=dev, dtype=torch.bfloat16)[:, :I]
+    baseh = torch.randn(T, H, device=dev, dtype=torch.bfloat16)
+    gb = 1e-9
+    rows = [
+        ("lora_fwd K=4096 R=48", lambda: ops.lora_fwd(xh, Ah, 0.5, 0.05, 1, H + 128), 2 * T * H * 2),
+        ("lora_fwd K=11008 R=16", lambda: ops.lora_fwd(x, A, 0.5, 0.05, 1, I + 128), 2 * T * I * 2),
+        ("lora_fwd swiglu K=11008", lambda: ops.lora_fwd(gu, A, 0.5, 0.05, 1, I + 128, False, True), 3 * T * I * 2),
+        ("lora_bwd_dx K=4096 R=48", lambda: ops.lora_bwd_dx(baseh, dxah, Ah, 0.05, 1), 2 * T * H * 2),
+        ("lora_bwd_dx K=11008 R=16", lambda: ops.lora_bwd_dx(base, dxa, A, 0.05, 1), 2 * T * I * 2),
+        ("lora_bwd_dx swiglu K=11008", lambda: ops.lora_bwd_dx(base, dxa, A, 0.05, 1, gu), 5 * T * I * 2),
+    ]
+    for name, fn, nbytes in rows:
+        us = timeit(fn)
+        print(f"{name:28s} {us:8.1f} us  {nbytes  / (us * 1e-6) * 1e-12:6.2f} TB/s ... floor {nbytes / 8e12 * 1e6:6.1f} us",
+              flush=True)
+
+
+if __name__ == "__main__":
+    main()
