@@ -352,6 +352,22 @@ __global__ __launch_bounds__(256) void grad_out_kernel(const float* __restrict__
   }
 }
 
+// Batched strided 2-D copies of 16-bit elements, one launch for any number of them: row d of the int64 descriptor
+// table is {src, dst, rows, cols, src row stride, dst row stride} (pointers as integers, strides in elements).
+// ops/fused.py syncs every adapter's B into its wide weight W' and every A into its projection's A_cat with it, once
+// per optimizer step for the whole model (it replaced ~7 copy kernels and 2 concatenations per layer and step).
+__global__ __launch_bounds__(256) void copy2d_batch_kernel(const long long* __restrict__ desc) {
+  const long long* d = desc + 6L * blockIdx.y;
+  const u16* src = (const u16*)d[0];
+  u16* dst = (u16*)d[1];
+  const long rows = d[2], cols = d[3], lds = d[4], ldd = d[5];
+  const long n = rows * cols;
+  for (long e = blockIdx.x * 256L + threadIdx.x; e < n; e += gridDim.x * 256L) {
+    const long i = e / cols, j = e - i * cols;
+    dst[i * ldd + j] = src[i * lds + j];
+  }
+}
+
 static unsigned thresh_of(double p, float* dscale) {
   const double pc = p < 0 ? 0 : (p > 0.999 ? 0.999 : p);
   *dscale = (float)(1.0 / (1.0 - pc));
@@ -516,8 +532,22 @@ void lora_grad_out(const at::Tensor& sum, at::TensorList outs, at::IntArrayRef r
   SFT_LAUNCH_CHECK();
 }
 
+// desc: int64 [n, 6] device table (see copy2d_batch_kernel); max_elems: the largest rows * cols in it
+void copy2d_batch(const at::Tensor& desc, int64_t max_elems) {
+  SFT_CHECK_CUDA(desc);
+  SFT_CHECK(desc.scalar_type() == at::kLong && desc.is_contiguous() && desc.dim() == 2 && desc.size(1) == 6,
+            "copy2d_batch: int64 [n, 6] descriptors");
+  const long n = desc.size(0);
+  SFT_CHECK(n <= 65535, "copy2d_batch: at most 65535 copies per launch");
+  if (n == 0 || max_elems <= 0) return;
+  dim3 grid((unsigned)std::min(64L, (long)((max_elems + 255) / 256)), (unsigned)n);
+  lora::copy2d_batch_kernel<<<grid, 256, 0, cur_stream()>>>((const long long*)desc.data_ptr());
+  SFT_LAUNCH_CHECK();
+}
+
 TORCH_LIBRARY_IMPL(sftamd, CUDA, m) {
   m.impl("lora_fwd", &lora_fwd);
+  m.impl("copy2d_batch", &copy2d_batch);
   m.impl("lora_bwd_dx", &lora_bwd_dx);
   m.impl("lora_tsum", &lora_tsum);
   m.impl("lora_grad_out", &lora_grad_out);

@@ -17,6 +17,7 @@ from __future__ import annotations
 
 import math
 import os
+import weakref
 from typing import Optional, Tuple
 
 import torch
@@ -931,6 +932,64 @@ def _sync_wide(wide: torch.Tensor, K: int, r: int, meta, Bs) -> None:
     wide._sftamd_bkey = key
 
 
+class _WideEntry:
+    """A wide weight's adapters on the HIP path: the B blocks it holds, its persistent A_cat buffer, the key of the
+    parameter state they were last copied from, and their copy descriptors."""
+    __slots__ = ("ids", "K", "r", "meta", "As", "Bs", "acat", "key")
+
+    def __init__(self, wide, K, r, meta, As, Bs):
+        self.ids = tuple(id(t) for t in (*As, *Bs))
+        self.K, self.r, self.meta, self.As, self.Bs = K, r, tuple(meta), list(As), list(Bs)
+        self.acat = torch.empty(r * len(As), K, device=wide.device, dtype=wide.dtype)
+        self.key = None
+
+    def state(self):
+        return (_PARAM_EPOCH[0],) + tuple((t._version, t.data_ptr()) for t in (*self.As, *self.Bs))
+
+    def descs(self, wide):
+        ld, K, r, es = wide.stride(0), self.K, self.r, wide.element_size()
+        d = [(B.data_ptr(), wide.data_ptr() + es * (o * ld + K + c), rows, r, B.stride(0), ld)
+             for (o, rows, c), B in zip(self.meta, self.Bs)]
+        d += [(A.data_ptr(), self.acat.data_ptr() + es * i * r * K, r, K, A.stride(0), K) for i, A in enumerate(self.As)]
+        return d
+
+
+_WIDE_REG: list = []        # weakrefs to the wide weights on the HIP path
+_WIDE_TABLE = [None, None]  # (descriptor-set key, (device table, max elements)) of the last batched sync
+
+
+def _wide_sync(wide, K, r, meta, As, Bs) -> torch.Tensor:
+    """The HIP path's _sync_wide + A concatenation: returns this projection's persistent A_cat. When any adapter may
+    have changed (the same epoch / version keys as _sync_wide), EVERY registered wide weight that is stale — after an
+    optimizer step, all of them — is refreshed by one copy2d_batch launch (B blocks into W', A rows into A_cat); the
+    device descriptor table is rebuilt only when the set of copies or their addresses change."""
+    ent = getattr(wide, "_sftamd_sync", None)
+    if ent is None or ent.ids != tuple(id(t) for t in (*As, *Bs)):
+        ent = _WideEntry(wide, K, r, meta, As, Bs)
+        wide._sftamd_sync = ent
+        _WIDE_REG.append(weakref.ref(wide))
+    if ent.key == ent.state():
+        return ent.acat
+    live = [w for w in (ref() for ref in _WIDE_REG) if w is not None]
+    _WIDE_REG[:] = [weakref.ref(w) for w in live]
+    stale = [w for w in live if w.device == wide.device and w._sftamd_sync.key != w._sftamd_sync.state()]
+    rows = [d for w in stale for d in w._sftamd_sync.descs(w)]
+    tkey = tuple(rows)
+    if _WIDE_TABLE[0] != tkey:
+        table = torch.tensor(rows, dtype=torch.int64).to(wide.device)
+        _WIDE_TABLE[0], _WIDE_TABLE[1] = tkey, (table, max(d[2] * d[3] for d in rows))
+    table, most = _WIDE_TABLE[1]
+    _ext.ops().copy2d_batch(table, int(most))
+    for w in stale:
+        w._sftamd_sync.key = w._sftamd_sync.state()
+    return ent.acat
+
+
+def _wide_sync_ok(wide, As, Bs) -> bool:
+    return (_ext.use_hip(wide) and wide.dtype == torch.bfloat16 and wide.stride(1) == 1
+            and all(t.dtype == torch.bfloat16 and t.stride(1) == 1 and t.device == wide.device for t in (*As, *Bs)))
+
+
 def _lora_gemm(X: torch.Tensor, wide: torch.Tensor) -> torch.Tensor:
     """The widened LoRA forward GEMM X' W'^T on the hand-written persistent kernel (113.0 samples/s vs 112.9 with
     hipBLASLt, profiles/r4_lora.md)."""
@@ -952,8 +1011,11 @@ def _lora_wide_prep(x, wide, K, scaling, p, seed, meta, ab, swiglu=False):
     x2d = x.reshape(-1, 2 * K if swiglu else K)
     if not x2d.is_contiguous():
         x2d = x2d.contiguous()
-    _sync_wide(wide, K, r, meta, Bs)
-    acat = As[0].contiguous() if n == 1 else torch.cat(As, 0)
+    if _wide_sync_ok(wide, As, Bs):
+        acat = _wide_sync(wide, K, r, meta, As, Bs)
+    else:
+        _sync_wide(wide, K, r, meta, Bs)
+        acat = As[0].contiguous() if n == 1 else torch.cat(As, 0)
     X = _lora_fwd(x2d, acat, scaling, p, seed, wide.shape[1], swiglu)
     return X, acat, (K, r * n, r, n, float(scaling), float(p), int(seed), tuple(meta), x.shape)
 

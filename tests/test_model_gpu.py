@@ -180,6 +180,60 @@ def test_lora_wide_gpu_matches_unfused():
             assert rel < 5e-2, (n, rel.item())
 
 
+def test_lora_wide_sync_after_edits():
+    """The HIP path keeps every adapter's B inside its wide weight and its A rows in a persistent A_cat, refreshed for
+    the whole model by one batched copy (ops/fused.py _wide_sync) after an optimizer epoch or an in-place edit: the
+    fused forward after (a) in-place edits (version counters) and (b) raw edits + bump_param_epoch (what the flat
+    optimizers do) == the unfused LoRA composition."""
+    from llm_fine_tune_distributed_amd.models.lora import LoRAConfig, apply_lora
+    import llm_fine_tune_distributed_amd.models.transformer as T
+    import llm_fine_tune_distributed_amd.ops as ops
+    torch.manual_seed(0)
+    cfg = tiny(hidden_size=512, num_attention_heads=4, num_key_value_heads=2, head_dim=128, intermediate_size=1024,
+               vocab_size=1024, num_hidden_layers=2)
+    m = build_model(cfg, device="cuda", dtype=torch.bfloat16, seed=1)
+    apply_lora(m, LoRAConfig(r=16, lora_alpha=8, lora_dropout=0.0))
+    fls = [fl for l in m.model.layers
+           for fl in (l.self_attn.lora["qkv"], l.self_attn.lora["o"], l.mlp.lora["gate_up"], l.mlp.lora["down"])]
+    for fl in fls:
+        for bb in fl.B:
+            torch.nn.init.normal_(bb, std=0.05)
+    m.eval()
+    ids = torch.randint(0, 1024, (4, 128), device="cuda")
+
+    def unfused(x, w, lora):
+        x2d = x.reshape(-1, x.shape[-1])
+        outs = [(x2d.float() @ a.float().t() @ b.float().t()) for a, b in zip(lora.A, lora.B)]
+        y = x2d.float() @ w.float().t() + torch.cat(outs, -1) * lora.scaling
+        return y.to(x.dtype).view(*x.shape[:-1], -1)
+
+    def reference():
+        orig, orig_mlp = T.ops.lora_linear, T.ops.lora_swiglu_mlp
+        T.ops.lora_linear = unfused
+        T.ops.lora_swiglu_mlp = lambda h, wg, wd, lg, ld: unfused(ops.swiglu(unfused(h, wg, lg)), wd, ld)
+        try:
+            with torch.no_grad():
+                return m(ids, labels=ids).loss.item()
+        finally:
+            T.ops.lora_linear, T.ops.lora_swiglu_mlp = orig, orig_mlp
+
+    with torch.no_grad():
+        l0 = m(ids, labels=ids).loss.item()
+    assert abs(l0 - reference()) < 2e-2
+    with torch.no_grad():  # (a) in-place edits bump the parameters' version counters
+        for fl in fls:
+            fl.A[0].mul_(1.5)
+            fl.B[-1].add_(0.02)
+        l1 = m(ids, labels=ids).loss.item()
+    assert abs(l1 - l0) > 1e-3 and abs(l1 - reference()) < 2e-2
+    with torch.no_grad():  # (b) raw edits (no version bump) announced by the optimizer epoch
+        for fl in fls:
+            fl.B[0].data.mul_(-1.0)
+        ops.bump_param_epoch()
+        l2 = m(ids, labels=ids).loss.item()
+    assert abs(l2 - l1) > 1e-3 and abs(l2 - reference()) < 2e-2
+
+
 @pytest.mark.parametrize("name,K,outs", [("qkv", 2048, [2048, 512, 512]), ("o", 2048, [2048]),
                                          ("gate_up", 2048, [11008, 11008]), ("down", 11008, [2048])])
 @pytest.mark.parametrize("p", [0.0, 0.05])

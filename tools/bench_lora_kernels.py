@@ -1,12 +1,12 @@
-"""Standalone timings of the LoRA streaming kernels (csrc/lora.hip) on the 7B MLP shapes (T = 8192 tokens):
-lora_fwd (plain and with the SwiGLU formed on the fly) and lora_bwd_dx (plain and writing dgu), vs their HBM floor."""
+"""Standalone timings of the LoRA streaming kernels (csrc/lora.hip) on the 7B shapes (T = 8192 tokens): lora_fwd (plain
+and with the SwiGLU formed on the fly), lora_bwd_dx (plain and writing dgu) and lora_tsum, vs their HBM floor at 8 TB/s."""
 import torch
 
 from llm_fine_tune_distributed_amd.ops import _ext
 
 
 def timeit(fn, it=20):
-    for _ in range(3):
+    for _ in range(10):
         fn()
     torch.cuda.synchronize()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -28,6 +28,7 @@ def main():
     A = torch.randn(R, I, device=dev, dtype=torch.bfloat16) * 0.05
     Ah = torch.randn(3 * R, H, device=dev, dtype=torch.bfloat16) * 0.05
     dxa = torch.randn(T, R, device=dev, dtype=torch.bfloat16)
+    dxa2 = torch.randn(T, 2 * R, device=dev, dtype=torch.bfloat16)
     dxah = torch.randn(T, 3 * R, device=dev, dtype=torch.bfloat16)
     base = torch.randn(T, I + 128, device=dev, dtype=torch.bfloat16)[:, :I]
     baseh = torch.randn(T, H, device=dev, dtype=torch.bfloat16)
@@ -39,7 +40,14 @@ def main():
         ("lora_bwd_dx K=4096 R=48", lambda: ops.lora_bwd_dx(baseh, dxah, Ah, 0.05, 1), 2 * T * H * 2),
         ("lora_bwd_dx K=11008 R=16", lambda: ops.lora_bwd_dx(base, dxa, A, 0.05, 1), 2 * T * I * 2),
         ("lora_bwd_dx swiglu K=11008", lambda: ops.lora_bwd_dx(base, dxa, A, 0.05, 1, gu), 5 * T * I * 2),
+        ("lora_tsum dA K=4096 R=48", lambda: ops.lora_tsum(xh, H, dxah, 0.05, 1), T * H * 2),
+        ("lora_tsum dA K=11008 R=16", lambda: ops.lora_tsum(base, I, dxa, 0.05, 1), T * I * 2),
+        ("lora_tsum dB n=22016 R=32", lambda: ops.lora_tsum(gu, 2 * I, dxa2, 0.0, 0), T * 2 * I * 2),
+        ("lora_tsum dB n=4096 R=16", lambda: ops.lora_tsum(xh, H, dxa, 0.0, 0), T * H * 2),
     ]
+    a = torch.randn(8192, 8192, device=dev, dtype=torch.bfloat16)
+    for _ in range(200):  # ~1 s of GEMMs first: the clocks ramp up before anything is timed
+        a @ a
     for name, fn, nbytes in rows:
         us = timeit(fn)
         print(f"{name:28s} {us:8.1f} us  {nbytes  / (us * 1e-6) * 1e-12:6.2f} TB/s ... floor {nbytes / 8e12 * 1e6:6.1f} us",
