@@ -4,14 +4,14 @@
 // widened to X' = [x | s * dropout(x) A^T], so the adapter forward rides inside the base GEMM. What
 // is left are two thin, memory-bound passes per adapted projection, each fused into one kernel:
 //
-//   lora_fwd:    X'[:, :K] = x,  X'[:, K:] = s * (dropout(x) @ A^T),  xd = dropout(x) (saved for dA)
-//                one read of x. v_mfma_f32_16x16x32_bf16 with BOTH operands loaded straight from global
-//                memory in fragment layout (x rows are the A operand, rows of A_cat the B operand:
-//                16 contiguous bytes per lane each); each of the block's 8 waves reduces an eighth of
-//                K and the partial 16 x R tiles are summed through LDS.
+//   lora_fwd:    X'[:, :K] = x,  X'[:, K:] = s * (dropout(x) @ A^T)  (xd = dropout(x) only when asked)
+//                one read of x, streamed row-contiguously through LDS into v_mfma_f32_16x16x32_bf16
+//                fragments (rows of A_cat loaded from global memory in fragment layout); the partial
+//                16 x R tiles of the block's 8 waves are summed through LDS.
 //   lora_bwd_dx: dx = base + keep * (dxa @ A) / (1-p), base = the base-weight dgrad (possibly a
 //                column slice of dX'), one read of base and one write of dx; the rank-R product is a
 //                VALU outer-product loop over an LDS-resident A tile (R <= 64 FMAs per output).
+//   lora_tsum:   the adapter gradients' token reductions (dA, dB^T), one pass over the wide operand.
 //
 // The dropout mask is hash_u32(t*K + k, seed) >= p * 2^32 (common.h), identical to dropout_add and to
 // the PyTorch reference, so nothing but the seed is stored between forward and backward.
@@ -24,94 +24,101 @@ __device__ __forceinline__ f32x4 mfma(const bf16x8& a, const bf16x8& b, const f3
   return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
 }
 
-// block = 8 waves, 16 rows; wave w reduces k in [w*KW, (w+1)*KW), KW = K/8 (multiple of 32), four
-// 32-column steps in flight per iteration (the kernel is a stream over x: latency, not math, bound).
+// block = 8 waves, 16 rows, streamed in 512-column chunks: each wave instruction reads or writes 2 rows x 512
+// contiguous bytes. The thread's piece of the chunk is copied to X', masked (dropout) into an LDS tile [16][512 + 8]
+// (and to xd when asked), and wave w reads its 64 columns of the tile as MFMA A fragments (ds_read_b128; the 16-byte
+// row padding spreads the 16 rows over all banks) against rows of A_cat loaded straight from global memory in
+// fragment layout. The next chunk's global loads are issued before this chunk's stores, LDS write and MFMAs; two LDS
+// tiles alternate, one barrier per chunk. (The first version loaded x itself in fragment layout, every wave
+// instruction touching 16 rows x 64 B: 153.9 vs 128.5 us for the SwiGLU-fused K = 11008 case, 115.8 vs 91.2 plain,
+// tools/bench_lora_kernels.py, r4_run29.)
 // SW: x is the SwiGLU input gu [T, 2K] (gate | up) and the widened activation is act = silu(gate) * up, rounded to bf16
 // as the SwiGLU kernel does (the LoRA MLP's down projection: no separate SwiGLU pass, no act tensor).
 template <int RF, bool SW = false>  // R = 16 * RF adapter columns
 __global__ __launch_bounds__(512) void fwd_kernel(const u16* __restrict__ x, const u16* __restrict__ A,
                                                   u16* __restrict__ X, u16* __restrict__ xd, long T, int K, long ldX,
                                                   float s, unsigned thresh, float dscale, unsigned seed, int drop) {
-  constexpr int R = 16 * RF;
-  constexpr int NW = 8, U = 4;
+  constexpr int R = 16 * RF, NW = 8, CK = 512, XP = CK + 8, NV = SW ? 2 : 1;
+  __shared__ __attribute__((aligned(16))) u16 xs[2][16][XP];
   __shared__ float red[NW][16][R + 1];
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int g = lane >> 4, r = lane & 15;
   const long t0 = (long)blockIdx.x * 16;
-  const long t = t0 + r;
-  const bool rowok = t < T;
-  const int KW = K / NW;
-  const int kb = w * KW;
+  // loader role: row lr of the block, columns 8 lc + 256 h of the chunk
+  const int lr = tid >> 5, lc = (tid & 31) * 8;
+  const long lt = t0 + lr;
+  const bool lok = lt < T;
+  const long ltc = lok ? lt : T - 1;
+  const u16* xrow = x + ltc * (SW ? 2L * K : (long)K);
   f32x4 acc[RF];
 #pragma unroll
   for (int j = 0; j < RF; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  // software pipeline: the next 128 columns' loads are in flight while this step's are processed (row index clamped
-  // for the loads, the store predicated; columns past the wave's range reload its first chunk and are skipped)
-  constexpr int NV = SW ? 2 : 1;
-  const long tc = rowok ? t : T - 1;
-  const int kend = kb + KW;
-  auto load = [&](int k, uint4(&rw)[U][NV]) {
+  uint4 rw[2][NV];
+  auto load = [&](int k0) {
 #pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const int kk = k + 32 * u + 8 * g, kc = kk < kend ? kk : kb;
-      if constexpr (SW) {
-        rw[u][0] = *(const uint4*)(x + tc * 2L * K + kc);
-        rw[u][1] = *(const uint4*)(x + tc * 2L * K + K + kc);
-      } else {
-        rw[u][0] = *(const uint4*)(x + tc * K + kc);
-      }
+    for (int h = 0; h < 2; ++h) {
+      const int c = k0 + lc + 256 * h, cc = c < K ? c : 0;
+      rw[h][0] = *(const uint4*)(xrow + cc);
+      if constexpr (SW) rw[h][1] = *(const uint4*)(xrow + K + cc);
     }
   };
-  auto step = [&](int k, const uint4(&rw)[U][NV]) {
+  const int nch = (K + CK - 1) / CK;
+  load(0);
+  for (int ch = 0; ch < nch; ++ch) {
+    const int k0 = ch * CK;
+    uint4 v[2];
 #pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const int kk = k + 32 * u + 8 * g;
-      if (kk >= kend) break;
-      uint4 v;
+    for (int h = 0; h < 2; ++h) {
       if constexpr (SW) {
         float ga[8], up[8], o[8];
-        unpack8(rw[u][0], ga);
-        unpack8(rw[u][1], up);
+        unpack8(rw[h][0], ga);
+        unpack8(rw[h][1], up);
 #pragma unroll
         for (int i = 0; i < 8; ++i) o[i] = ga[i] / (1.f + __expf(-ga[i])) * up[i];
-        v = pack8(o);
+        v[h] = pack8(o);
       } else {
-        v = rw[u][0];
-      }
-      if (rowok) *(uint4*)(X + t * ldX + kk) = v;
-      if (drop) {
-        float f[8];
-        unpack8(v, f);
-        const unsigned long long idx = (unsigned long long)t * K + kk;
-#pragma unroll
-        for (int i = 0; i < 8; ++i) f[i] = hash_u32(idx + i, seed) >= thresh ? f[i] * dscale : 0.f;
-        v = pack8(f);
-        if (xd && rowok) *(uint4*)(xd + t * K + kk) = v;
-      }
-      const bf16x8 a = __builtin_bit_cast(bf16x8, v);
-#pragma unroll
-      for (int j = 0; j < RF; ++j) {
-        const bf16x8 b = __builtin_bit_cast(bf16x8, *(const uint4*)(A + (long)(16 * j + r) * K + kk));
-        acc[j] = mfma(a, b, acc[j]);
+        v[h] = rw[h][0];
       }
     }
-  };
-  uint4 ra[U][NV], rb[U][NV];
-  load(kb, ra);
-  for (int k = kb; k < kend; k += 64 * U) {
-    if (k + 32 * U < kend) load(k + 32 * U, rb);
-    step(k, ra);
-    if (k + 32 * U >= kend) break;
-    if (k + 64 * U < kend) load(k + 64 * U, ra);
-    step(k + 32 * U, rb);
+    if (ch + 1 < nch) load(k0 + CK);  // the next chunk flies under this chunk's stores, LDS write and MFMAs
+    u16(*tile)[XP] = xs[ch & 1];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int c = k0 + lc + 256 * h;
+      if (c < K) {
+        if (lok) *(uint4*)(X + lt * ldX + c) = v[h];
+        if (drop) {
+          float f[8];
+          unpack8(v[h], f);
+          const unsigned long long idx = (unsigned long long)lt * K + c;
+#pragma unroll
+          for (int i = 0; i < 8; ++i) f[i] = hash_u32(idx + i, seed) >= thresh ? f[i] * dscale : 0.f;
+          v[h] = pack8(f);
+          if (xd && lok) *(uint4*)(xd + lt * K + c) = v[h];
+        }
+        *(uint4*)&tile[lr][lc + 256 * h] = v[h];
+      }
+    }
+    __syncthreads();  // the tile is complete (and the other tile's readers finished before the previous barrier)
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      const int kl = 64 * w + 32 * ks + 8 * g;
+      if (k0 + 64 * w + 32 * ks < K) {
+        const bf16x8 a = __builtin_bit_cast(bf16x8, *(const uint4*)&tile[r][kl]);
+#pragma unroll
+        for (int j = 0; j < RF; ++j) {
+          const bf16x8 b = __builtin_bit_cast(bf16x8, *(const uint4*)(A + (long)(16 * j + r) * K + k0 + kl));
+          acc[j] = mfma(a, b, acc[j]);
+        }
+      }
+    }
   }
-  // C layout: lane (g, r) holds rows 4g+i, column 16j + r
 #pragma unroll
   for (int j = 0; j < RF; ++j)
 #pragma unroll
     for (int i = 0; i < 4; ++i) red[w][4 * g + i][16 * j + r] = acc[j][i];
   __syncthreads();
-  for (int e = threadIdx.x; e < 16 * R; e += NW * 64) {
+  for (int e = tid; e < 16 * R; e += NW * 64) {
     const int row = e / R, col = e - row * R;
     const long tt = t0 + row;
     if (tt < T) {
@@ -121,8 +128,8 @@ __global__ __launch_bounds__(512) void fwd_kernel(const u16* __restrict__ x, con
       X[tt * ldX + K + col] = f2bf(s * v);
     }
   }
-  const int pad = (int)(ldX - K - R);  // zero columns [K + R, ldX) of the padded wide activation
-  for (int e = threadIdx.x; e < 16 * pad; e += NW * 64) {
+  const int pad = (int)(ldX - K - R);
+  for (int e = tid; e < 16 * pad; e += NW * 64) {
     const int row = e / pad, col = e - row * pad;
     if (t0 + row < T) X[(t0 + row) * ldX + K + R + col] = 0;
   }
