@@ -232,7 +232,9 @@ __global__ __launch_bounds__(512) void bwd_dx_kernel(const u16* __restrict__ bas
 }
 
 // Thin token reductions of the adapter backward, one pass over the wide operand:
-//   out [R, K] (fp32, accumulated with atomics) = sum_t S[t, r] * Xd[t, k]
+//   out [splits, R, K] (fp32 partial sums, one slab per token chunk, plain stores) = sum_t S[t, r] * Xd[t, k]
+// (lora_grad_out sums the slabs while it scatters them into the gradients: no zero fill and no atomics, which at
+// ~3 M fp32 atomics per call for the qkv shapes had made these reductions 3-5x slower than their HBM traffic)
 // with Xd = dropout(X) (the forward's mask regenerated from the seed) or X itself.
 //   dA    = dxa^T dropout(x):  X = X'[:, :K] (the widened activation), S = dxa [T, R]
 //   dB^T  = (s xa)^T dy:       X = dy [T, n],                          S = X'[:, K:K+R] (the adapter columns)
@@ -315,26 +317,32 @@ __global__ __launch_bounds__(256) void tsum_kernel(const u16* __restrict__ X, lo
         acc[j] = mfma(a, lds_tr8(&ss[rl][16 * j + 4 * p], &ss[rl + 4][16 * j + 4 * p]), acc[j]);
     }
   }
-  // C layout: lane (g, r16) holds rows 4 g + i (k), column r16 (r) of each 16 x 16 block
+  // C layout: lane (g, r16) holds rows 4 g + i (k), column r16 (r) of each 16 x 16 block: 4 consecutive k per lane
+  float* slab = out + (long)blockIdx.y * R * K;
+  const int kk = k0 + 16 * w + 4 * g;
+  if (kk < K) {  // K % 8 == 0: the lane's 4 columns are all in range or all out
 #pragma unroll
-  for (int j = 0; j < RF; ++j)
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int kk = k0 + 16 * w + 4 * g + i;
-      if (kk < K) atomicAdd(out + (long)(16 * j + r16) * K + kk, acc[j][i]);
-    }
+    for (int j = 0; j < RF; ++j) *(f32x4*)(slab + (long)(16 * j + r16) * K + kk) = acc[j];
+  }
 }
 
 // Scatter blocks of an fp32 [R, K] sum into up to 4 parameter gradients (bf16 or fp32, written or accumulated), one
 // launch for all adapters of a projection: output q is rows [r0, r0 + nr) x columns [c0, c0 + nc) of the sum,
 // transposed when tr (dB = (dB^T)^T: out[i][j] = sum[r0 + j][c0 + i]).
+__device__ __forceinline__ float slab_sum(const float* __restrict__ p, long o, long slab, int ns) {
+  float v = 0.f;
+  for (int z = 0; z < ns; ++z) v += p[o + z * slab];
+  return v;
+}
+
 struct GradOuts {
   void* ptr[4];
   int r0[4], c0[4], nr[4], nc[4];
   int f32[4], acc[4];
 };
 
-__global__ __launch_bounds__(256) void grad_out_kernel(const float* __restrict__ sum, int K, GradOuts go, int tr) {
+__global__ __launch_bounds__(256) void grad_out_kernel(const float* __restrict__ sum, int K, long slab, int ns,
+                                                       GradOuts go, int tr) {
   const int q = blockIdx.y;
   const int n = go.nr[q] * go.nc[q];  // elements of output q ([nc, nr] when tr, else [nr, nc])
   for (int e = blockIdx.x * 256 + threadIdx.x; e < n; e += gridDim.x * 256) {
@@ -343,11 +351,11 @@ __global__ __launch_bounds__(256) void grad_out_kernel(const float* __restrict__
     if (tr) {  // out [nc][nr]: element (i, j) = sum[r0 + j][c0 + i]
       i = e / go.nr[q];
       j = e - i * go.nr[q];
-      v = sum[(long)(go.r0[q] + j) * K + go.c0[q] + i];
+      v = slab_sum(sum, (long)(go.r0[q] + j) * K + go.c0[q] + i, slab, ns);
     } else {
       i = e / go.nc[q];
       j = e - i * go.nc[q];
-      v = sum[(long)(go.r0[q] + i) * K + go.c0[q] + j];
+      v = slab_sum(sum, (long)(go.r0[q] + i) * K + go.c0[q] + j, slab, ns);
     }
     if (go.f32[q]) {
       float* o = (float*)go.ptr[q] + e;
@@ -473,7 +481,7 @@ at::Tensor lora_bwd_dx(const at::Tensor& base, const at::Tensor& dxa, const at::
   return dx;
 }
 
-// out [R, K] fp32 = S^T dropout(X[:, :K]) (the mask regenerated from seed when p > 0); X rows of stride >= K, S [T, R]
+// out [splits, R, K] fp32 partial sums (over token chunks; lora_grad_out or .sum(0) adds them) of S^T dropout(X[:, :K]) (the mask regenerated from seed when p > 0); X rows of stride >= K, S [T, R]
 // (a column slice of a wider tensor is fine)
 at::Tensor lora_tsum(const at::Tensor& X, int64_t K, const at::Tensor& S, double p, int64_t seed) {
   SFT_CHECK_CUDA(X);
@@ -484,8 +492,7 @@ at::Tensor lora_tsum(const at::Tensor& X, int64_t K, const at::Tensor& S, double
   SFT_CHECK(X.stride(1) == 1 && X.stride(0) % 8 == 0 && X.size(1) >= K && K % 8 == 0, "lora_tsum: X layout");
   SFT_CHECK(S.stride(1) == 1 && S.stride(0) % 8 == 0 && (uintptr_t)S.data_ptr() % 16 == 0, "lora_tsum: S layout");
   SFT_CHECK(S.size(0) == T && R % 16 == 0 && R >= 16 && R <= 64, "lora_tsum: S [T, R], R in 16..64");
-  auto out = at::zeros({R, K}, X.options().dtype(at::kFloat));
-  if (T == 0) return out;
+  if (T == 0) return at::zeros({1, R, K}, X.options().dtype(at::kFloat));
   float dscale;
   const unsigned thresh = lora::thresh_of(p, &dscale);
   const int nkb = (int)((K + 63) / 64);
@@ -493,6 +500,7 @@ at::Tensor lora_tsum(const at::Tensor& X, int64_t K, const at::Tensor& S, double
   long splits = std::max(1L, std::min((T + 63) / 64, 1024L / nkb));
   const long tc = ((T + splits - 1) / splits + 63) / 64 * 64;
   splits = (T + tc - 1) / tc;
+  auto out = at::empty({splits, R, K}, X.options().dtype(at::kFloat));  // every element written by one workgroup
   dim3 grid(nkb, (unsigned)splits);
 #define LORA_TSUM(RF)                                                                                             \
   lora::tsum_kernel<RF><<<grid, 256, 0, cur_stream()>>>((const u16*)X.data_ptr(), X.stride(0),                   \
@@ -509,14 +517,16 @@ at::Tensor lora_tsum(const at::Tensor& X, int64_t K, const at::Tensor& S, double
   return out;
 }
 
-// outs[q] (+)= block q of sum ([R, K] fp32): rows [r0[q], +nr), columns [c0[q], +nc), transposed when tr; one launch
+// outs[q] (+)= block q of sum ([R, K] fp32, or [splits, R, K] slabs summed on the fly): rows [r0[q], +nr), columns [c0[q], +nc), transposed when tr; one launch
 void lora_grad_out(const at::Tensor& sum, at::TensorList outs, at::IntArrayRef r0, at::IntArrayRef c0, bool tr,
                    at::IntArrayRef accumulate) {
-  SFT_CHECK(sum.scalar_type() == at::kFloat && sum.is_contiguous() && sum.dim() == 2, "lora_grad_out: fp32 [R, K]");
+  SFT_CHECK(sum.scalar_type() == at::kFloat && sum.is_contiguous() && (sum.dim() == 2 || sum.dim() == 3),
+            "lora_grad_out: fp32 [R, K] or [splits, R, K]");
   const int n = outs.size();
   SFT_CHECK(n >= 1 && n <= 4 && (int)r0.size() == n && (int)c0.size() == n && (int)accumulate.size() == n,
             "lora_grad_out: 1..4 outputs");
-  const int R = sum.size(0), K = sum.size(1);
+  const int ns = sum.dim() == 3 ? sum.size(0) : 1;
+  const int R = sum.size(sum.dim() - 2), K = sum.size(sum.dim() - 1);
   lora::GradOuts go{};
   long most = 0;
   for (int q = 0; q < n; ++q) {
@@ -535,7 +545,7 @@ void lora_grad_out(const at::Tensor& sum, at::TensorList outs, at::IntArrayRef r
     most = std::max(most, (long)nr * nc);
   }
   dim3 grid((unsigned)std::min(1024L, (most + 255) / 256), (unsigned)n);
-  lora::grad_out_kernel<<<grid, 256, 0, cur_stream()>>>(sum.data_ptr<float>(), K, go, tr ? 1 : 0);
+  lora::grad_out_kernel<<<grid, 256, 0, cur_stream()>>>(sum.data_ptr<float>(), K, (long)R * K, ns, go, tr ? 1 : 0);
   SFT_LAUNCH_CHECK();
 }
 

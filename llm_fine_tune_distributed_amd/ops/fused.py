@@ -869,8 +869,9 @@ def _lora_fwd(x2d, acat, s, p, seed, ldX=0, swiglu=False):
 
 
 def _lora_tsum(Xm, K, S, p, seed) -> torch.Tensor:
-    """[R, K] fp32 = S^T dropout(Xm[:, :K]) (the forward's mask regenerated from the seed when p > 0): one pass over the
-    wide operand (csrc/lora.hip tsum_kernel)."""
+    """S^T dropout(Xm[:, :K]) in fp32 (the forward's mask regenerated from the seed when p > 0): one pass over the
+    wide operand (csrc/lora.hip tsum_kernel), returned as [splits, R, K] partial sums over token chunks on the HIP
+    path (summed by lora_grad_out as it scatters them, or by _scatter_grads' fallback), [R, K] otherwise."""
     R = S.shape[1]
     if (_ext.use_hip(Xm) and Xm.dtype == torch.bfloat16 and S.dtype == torch.bfloat16 and K % 8 == 0
             and R % 16 == 0 and 16 <= R <= 64 and Xm.stride(1) == 1 and Xm.stride(0) % 8 == 0 and S.stride(1) == 1
@@ -894,6 +895,8 @@ def _scatter_grads(total: torch.Tensor, params, blocks, tr: bool):
             p._sftamd_fresh = False
             _weight_grad_done(p)
         return [None] * len(params)
+    if total.dim() == 3:
+        total = total.sum(0)
     out = []
     for p, (r0, c0), (nr, nc) in zip(params, blocks, shapes):
         g = total[r0:r0 + nr, c0:c0 + nc]

@@ -518,7 +518,7 @@ def test_lora_fwd_bwd_kernels(K, R, p):
     dgu = _ext.ops().lora_bwd_dx(base, dxa, A, p, 99, gu)
     assert torch.equal(dgu, _ext.ops().swiglu_bwd(dx, gu))
     # dA = dxa^T dropout(x) with the mask regenerated from the seed, x read from the widened activation X'
-    dA = _ext.ops().lora_tsum(X, K, dxa, p, 99)
+    dA = _ext.ops().lora_tsum(X, K, dxa, p, 99).sum(0)  # [splits, R, K] partial sums
     xs = ref.dropout_add(None, x, p, 99) if p > 0 else x
     dAr = dxa.float().t() @ xs.float()
     assert dA.dtype == torch.float32 and dA.shape == (R, K)
@@ -528,12 +528,13 @@ def test_lora_fwd_bwd_kernels(K, R, p):
     n_out = 640
     dy = torch.randn(T, n_out, device="cuda", dtype=torch.bfloat16)
     S = X[:, K:K + R]
-    sB = _ext.ops().lora_tsum(dy, n_out, S, 0.0, 0)
+    sBp = _ext.ops().lora_tsum(dy, n_out, S, 0.0, 0)
+    sB = sBp.sum(0)
     assert rel_err(sB, S.float().t() @ dy.float()) < 1e-2
     o1 = torch.randn(n_out // 2, 16, device="cuda", dtype=torch.bfloat16)
     o2 = torch.zeros(n_out - n_out // 2, 16, device="cuda", dtype=torch.float32)
     o1_ref = o1.float() + sB[0:16, 0:n_out // 2].t()
-    _ext.ops().lora_grad_out(sB, [o1, o2], [0, R - 16], [0, n_out // 2], True, [1, 0])
+    _ext.ops().lora_grad_out(sBp, [o1, o2], [0, R - 16], [0, n_out // 2], True, [1, 0])  # sums the slabs
     assert rel_err(o1, o1_ref) < 1e-2
     assert torch.allclose(o2, sB[R - 16:R, n_out // 2:].t())
 

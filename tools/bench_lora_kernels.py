@@ -37,6 +37,7 @@ def main():
         ("lora_fwd K=4096 R=48", lambda: ops.lora_fwd(xh, Ah, 0.5, 0.05, 1, H + 128), 2 * T * H * 2),
         ("lora_fwd K=11008 R=16", lambda: ops.lora_fwd(x, A, 0.5, 0.05, 1, I + 128), 2 * T * I * 2),
         ("lora_fwd swiglu K=11008", lambda: ops.lora_fwd(gu, A, 0.5, 0.05, 1, I + 128, False, True), 3 * T * I * 2),
+        ("lora_fwd swiglu K=11008 p=0", lambda: ops.lora_fwd(gu, A, 0.5, 0.0, 1, I + 128, False, True), 3 * T * I * 2),
         ("lora_bwd_dx K=4096 R=48", lambda: ops.lora_bwd_dx(baseh, dxah, Ah, 0.05, 1), 2 * T * H * 2),
         ("lora_bwd_dx K=11008 R=16", lambda: ops.lora_bwd_dx(base, dxa, A, 0.05, 1), 2 * T * I * 2),
         ("lora_bwd_dx swiglu K=11008", lambda: ops.lora_bwd_dx(base, dxa, A, 0.05, 1, gu), 5 * T * I * 2),
