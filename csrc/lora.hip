@@ -348,20 +348,23 @@ __global__ __launch_bounds__(256) void grad_out_kernel(const float* __restrict__
   for (int e = blockIdx.x * 256 + threadIdx.x; e < n; e += gridDim.x * 256) {
     int i, j;
     float v;
-    if (tr) {  // out [nc][nr]: element (i, j) = sum[r0 + j][c0 + i]
-      i = e / go.nr[q];
-      j = e - i * go.nr[q];
+    long oe = e;
+    if (tr) {  // out [nc][nr]: element (i, j) = sum[r0 + j][c0 + i]; consecutive threads read consecutive i (the
+               // slab reads dominate), the writes go nr elements apart
+      j = e / go.nc[q];
+      i = e - j * go.nc[q];
       v = slab_sum(sum, (long)(go.r0[q] + j) * K + go.c0[q] + i, slab, ns);
+      oe = (long)i * go.nr[q] + j;
     } else {
       i = e / go.nc[q];
       j = e - i * go.nc[q];
       v = slab_sum(sum, (long)(go.r0[q] + i) * K + go.c0[q] + j, slab, ns);
     }
     if (go.f32[q]) {
-      float* o = (float*)go.ptr[q] + e;
+      float* o = (float*)go.ptr[q] + oe;
       *o = go.acc[q] ? *o + v : v;
     } else {
-      u16* o = (u16*)go.ptr[q] + e;
+      u16* o = (u16*)go.ptr[q] + oe;
       *o = f2bf(go.acc[q] ? bf2f(*o) + v : v);
     }
   }
