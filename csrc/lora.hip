@@ -135,23 +135,28 @@ __global__ __launch_bounds__(512) void fwd_kernel(const u16* __restrict__ x, con
   }
 }
 
-// tile: 32 rows x 512 columns per 512-thread block; thread = 4 rows x 8 columns (the A tile in LDS is
-// reused by 32 rows). The thread's base (and gu) rows are loaded BEFORE the rank-R product loop (row indices
+// tile: 32 rows x 512 columns (64 x 256 for R >= 48) per 512-thread block; thread = 4 rows x 8 columns (the A tile in
+// LDS is reused by all rows of the block). The thread's base (and gu) rows are loaded BEFORE the rank-R product loop (row indices
 // clamped, stores predicated), so the HBM latency hides under the FMAs instead of serialising row by row after it.
 // With gu ([T, 2K] = gate | up, the SwiGLU input): the SwiGLU backward is applied to dx on the way out and
 // dgu [T, 2K] is written instead (the down projection of a LoRA MLP: no dx round trip through HBM).
+// Column width of a bwd_dx block: 256 for R >= 48 (the fp32 A tile [R][512] alone was 96 KB for the qkv adapters, one
+// workgroup per CU: 52 us for 67 MB of traffic), 512 otherwise.
+template <int R>
+constexpr int dx_cols() { return R >= 48 ? 256 : 512; }
+
 template <int R, bool SWIGLU>
 __global__ __launch_bounds__(512) void bwd_dx_kernel(const u16* __restrict__ base, long ldb, const u16* __restrict__ dxa,
                                                      const u16* __restrict__ A, u16* __restrict__ dx, long T, int K,
                                                      unsigned thresh, float dscale, unsigned seed, int drop,
                                                      const u16* __restrict__ gu) {
-  constexpr int RPT = 4, TR = 8 * RPT;
-  __shared__ float As[R][512];
+  constexpr int CW = dx_cols<R>(), NC8 = CW / 8, RPT = 4, TR = 512 / NC8 * RPT;
+  __shared__ float As[R][CW];
   __shared__ float Ds[TR][R];
   const int tid = threadIdx.x;
-  const int k0 = blockIdx.x * 512;
+  const int k0 = blockIdx.x * CW;
   const long t0 = (long)blockIdx.y * TR;
-  const int c8 = tid & 63, rg = tid >> 6;
+  const int c8 = tid % NC8, rg = tid / NC8;
   const int k = k0 + c8 * 8;
   const int kc = k < K ? k : K - 8;
   uint4 vb[RPT], vg[RPT], vu[RPT];
@@ -164,8 +169,8 @@ __global__ __launch_bounds__(512) void bwd_dx_kernel(const u16* __restrict__ bas
       vu[i] = *(const uint4*)(gu + t * 2L * K + K + kc);
     }
   }
-  for (int e = tid; e < R * 64; e += 512) {  // A[:, k0:k0+512] as 8-wide vectors
-    const int rr = e >> 6, cc = e & 63, kk = k0 + cc * 8;
+  for (int e = tid; e < R * NC8; e += 512) {  // A[:, k0:k0+CW] as 8-wide vectors
+    const int rr = e / NC8, cc = e % NC8, kk = k0 + cc * 8;
     float f[8];
     if (kk < K) {
       unpack8(*(const uint4*)(A + (long)rr * K + kk), f);
@@ -462,7 +467,8 @@ at::Tensor lora_bwd_dx(const at::Tensor& base, const at::Tensor& dxa, const at::
   if (T == 0) return dx;
   float dscale;
   const unsigned thresh = lora::thresh_of(p, &dscale);
-  dim3 grid((K + 511) / 512, (unsigned)((T + 31) / 32));
+  const int cw = R >= 48 ? 256 : 512, tr = 512 / (cw / 8) * 4;  // = dx_cols<R>() and the kernel's TR
+  dim3 grid((K + cw - 1) / cw, (unsigned)((T + tr - 1) / tr));
   SFT_CHECK(grid.y <= 65535u, "lora_bwd_dx: T too large");
 #define LORA_BWD(RR)                                                                                              \
   if (sw)                                                                                                         \
