@@ -83,6 +83,9 @@ def parse(argv=None):
     ap.add_argument("--baseline-1gpu", type=float, default=0.0,
                     help="1-GPU samples/s of the same config: adds scaling_efficiency = value / (N * this)")
     ap.add_argument("--profile-steps", type=int, default=0)
+    ap.add_argument("--torch-profile", default="",
+                    help="with --profile-steps: record those steps with torch.profiler and write the ops by device "
+                         "time (with input shapes) to this file (attributes small copy / fill kernels to their op)")
     # --recipe: the reference recipe end to end instead of the synthetic step loop: its own parquet
     # (data/qa_dataset.parquet, 90/10 split, system prompt + chat template), per-device batch 8 x GA 2 (README.md:69),
     # eval every 10 steps, through SFTTrainer.train(); reports HF's train_samples_per_second (wall time INCLUDING the
@@ -324,10 +327,22 @@ def run(a):
         print(json.dumps(rec), flush=True)
     if a.profile_steps:
         sync()
+        prof = None
+        if a.torch_profile:
+            from torch.profiler import ProfilerActivity, profile
+            prof = profile(activities=[ProfilerActivity.CPU, ProfilerActivity.CUDA], record_shapes=True)
+            prof.__enter__()
         for _ in range(a.profile_steps):
             step()
         trainer.optimizer.synchronize()
         sync()
+        if prof is not None:
+            prof.__exit__(None, None, None)
+            if st.rank == 0:
+                with open(a.torch_profile, "w") as f:
+                    f.write(prof.key_averages(group_by_input_shape=True).table(
+                        sort_by="self_device_time_total", row_limit=80, max_name_column_width=60,
+                        max_shapes_column_width=90))
     if st.world_size > 1:
         barrier()
         dist.destroy_process_group()
