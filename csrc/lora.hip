@@ -256,27 +256,33 @@ __device__ __forceinline__ bf16x8 lds_tr8(const u16* p0, const u16* p1) {
   return __builtin_bit_cast(bf16x8, v);
 }
 
-template <int RF>
+template <int RF, int KT>  // KT 16-row k tiles per wave: a workgroup covers 64 KT columns of k
 __global__ __launch_bounds__(256) void tsum_kernel(const u16* __restrict__ X, long ldX, const u16* __restrict__ S,
                                                    long ldS, float* __restrict__ out, long T, int K, long tc,
                                                    unsigned thresh, float dscale, unsigned seed, int drop) {
-  constexpr int R = 16 * RF, ST = 64, XP = 64 + 8, SP = R + 8;  // row pitches padded by 16 bytes (2-way at most)
+  constexpr int R = 16 * RF, ST = 64, NK = 64 * KT;
+  // row pitches padded so that a transposed read's 4 rows x 4 column groups hit distinct banks (pitch = 36 dwords
+  // mod 64) and rows stay 16-byte aligned
+  constexpr int XP = NK + (KT == 1 ? 8 : 72), SP = R + 8;
+  constexpr int TPR = NK / 8, RPP = 256 / TPR, XH = ST / RPP;  // X chunk threads per row, rows per pass, passes
   constexpr int SCH = ST * R / 8, SPT = (SCH + 255) / 256;       // S chunks of 8 per stage, per thread
   __shared__ __attribute__((aligned(16))) u16 xs[ST][XP];
   __shared__ __attribute__((aligned(16))) u16 ss[ST][SP];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, g = lane >> 4, r16 = lane & 15;
-  const int k0 = blockIdx.x * 64;
+  const int k0 = blockIdx.x * NK;
   const long t_begin = (long)blockIdx.y * tc, t_end = min(T, t_begin + tc);
-  const int tr = tid >> 3, c8 = tid & 7;  // X chunks: rows tr and tr + 32 of the stage, columns 8 c8 .. 8 c8 + 7
+  const int tr = tid / TPR, c8 = tid % TPR;  // X chunks: rows tr + RPP h of the stage, columns 8 c8 .. 8 c8 + 7
   const int k = k0 + 8 * c8;
-  f32x4 acc[RF];
+  f32x4 acc[KT][RF];
 #pragma unroll
-  for (int j = 0; j < RF; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  uint4 xv[2], sv[SPT];
+  for (int kt = 0; kt < KT; ++kt)
+#pragma unroll
+    for (int j = 0; j < RF; ++j) acc[kt][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  uint4 xv[XH], sv[SPT];
   auto load = [&](long t0) {
 #pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      const long t = t0 + tr + 32 * h;
+    for (int h = 0; h < XH; ++h) {
+      const long t = t0 + tr + RPP * h;
       xv[h] = (t < t_end && k < K) ? *(const uint4*)(X + t * ldX + k) : make_uint4(0, 0, 0, 0);
     }
 #pragma unroll
@@ -293,10 +299,10 @@ __global__ __launch_bounds__(256) void tsum_kernel(const u16* __restrict__ X, lo
   for (long t0 = t_begin; t0 < t_end; t0 += ST) {
     __syncthreads();  // the previous stage's reads are done
 #pragma unroll
-    for (int h = 0; h < 2; ++h) {
+    for (int h = 0; h < XH; ++h) {
       uint4 v = xv[h];
       if (drop) {
-        const long t = t0 + tr + 32 * h;
+        const long t = t0 + tr + RPP * h;
         float f[8];
         unpack8(v, f);
         const unsigned long long idx = (unsigned long long)t * K + k;
@@ -304,7 +310,7 @@ __global__ __launch_bounds__(256) void tsum_kernel(const u16* __restrict__ X, lo
         for (int i = 0; i < 8; ++i) f[i] = hash_u32(idx + i, seed) >= thresh ? f[i] * dscale : 0.f;
         v = pack8(f);
       }
-      *(uint4*)&xs[tr + 32 * h][8 * c8] = v;
+      *(uint4*)&xs[tr + RPP * h][8 * c8] = v;
     }
 #pragma unroll
     for (int u = 0; u < SPT; ++u) {
@@ -316,18 +322,27 @@ __global__ __launch_bounds__(256) void tsum_kernel(const u16* __restrict__ X, lo
 #pragma unroll
     for (int ks = 0; ks < ST / 32; ++ks) {
       const int rl = 32 * ks + 8 * g + q;
-      const bf16x8 a = lds_tr8(&xs[rl][16 * w + 4 * p], &xs[rl + 4][16 * w + 4 * p]);
+      bf16x8 b[RF];
 #pragma unroll
-      for (int j = 0; j < RF; ++j)
-        acc[j] = mfma(a, lds_tr8(&ss[rl][16 * j + 4 * p], &ss[rl + 4][16 * j + 4 * p]), acc[j]);
+      for (int j = 0; j < RF; ++j) b[j] = lds_tr8(&ss[rl][16 * j + 4 * p], &ss[rl + 4][16 * j + 4 * p]);
+#pragma unroll
+      for (int kt = 0; kt < KT; ++kt) {
+        const int c0 = 16 * (KT * w + kt) + 4 * p;
+        const bf16x8 a = lds_tr8(&xs[rl][c0], &xs[rl + 4][c0]);
+#pragma unroll
+        for (int j = 0; j < RF; ++j) acc[kt][j] = mfma(a, b[j], acc[kt][j]);
+      }
     }
   }
   // C layout: lane (g, r16) holds rows 4 g + i (k), column r16 (r) of each 16 x 16 block: 4 consecutive k per lane
   float* slab = out + (long)blockIdx.y * R * K;
-  const int kk = k0 + 16 * w + 4 * g;
-  if (kk < K) {  // K % 8 == 0: the lane's 4 columns are all in range or all out
 #pragma unroll
-    for (int j = 0; j < RF; ++j) *(f32x4*)(slab + (long)(16 * j + r16) * K + kk) = acc[j];
+  for (int kt = 0; kt < KT; ++kt) {
+    const int kk = k0 + 16 * (KT * w + kt) + 4 * g;
+    if (kk < K) {  // K % 8 == 0: the lane's 4 columns are all in range or all out
+#pragma unroll
+      for (int j = 0; j < RF; ++j) *(f32x4*)(slab + (long)(16 * j + r16) * K + kk) = acc[kt][j];
+    }
   }
 }
 
@@ -504,17 +519,25 @@ at::Tensor lora_tsum(const at::Tensor& X, int64_t K, const at::Tensor& S, double
   if (T == 0) return at::zeros({1, R, K}, X.options().dtype(at::kFloat));
   float dscale;
   const unsigned thresh = lora::thresh_of(p, &dscale);
-  const int nkb = (int)((K + 63) / 64);
-  // about 1024 workgroups: the token range split into chunks of whole 64-token stages
-  long splits = std::max(1L, std::min((T + 63) / 64, 1024L / nkb));
+  // wide operands (K >= 8192: the down projection's dA, gate_up's dB) take 256-column workgroups, each wave
+  // instruction reading 2 rows x 512 B (64-column ones read 8 rows x 128 B), on about 512 workgroups; the rest
+  // 64-column ones on about 1024. The token range is split into chunks of whole 64-token stages.
+  const bool wide = K >= 8192;
+  const int nk = wide ? 256 : 64, nkb = (int)((K + nk - 1) / nk);
+  long splits = std::max(1L, std::min((T + 63) / 64, (wide ? 512L : 1024L) / nkb));
   const long tc = ((T + splits - 1) / splits + 63) / 64 * 64;
   splits = (T + tc - 1) / tc;
   auto out = at::empty({splits, R, K}, X.options().dtype(at::kFloat));  // every element written by one workgroup
   dim3 grid(nkb, (unsigned)splits);
 #define LORA_TSUM(RF)                                                                                             \
-  lora::tsum_kernel<RF><<<grid, 256, 0, cur_stream()>>>((const u16*)X.data_ptr(), X.stride(0),                   \
-                                                        (const u16*)S.data_ptr(), S.stride(0), out.data_ptr<float>(), \
-                                                        T, (int)K, tc, thresh, dscale, (unsigned)seed, p > 0 ? 1 : 0)
+  if (wide)                                                                                                       \
+    lora::tsum_kernel<RF, 4><<<grid, 256, 0, cur_stream()>>>((const u16*)X.data_ptr(), X.stride(0),              \
+        (const u16*)S.data_ptr(), S.stride(0), out.data_ptr<float>(), T, (int)K, tc, thresh, dscale,             \
+        (unsigned)seed, p > 0 ? 1 : 0);                                                                          \
+  else                                                                                                            \
+    lora::tsum_kernel<RF, 1><<<grid, 256, 0, cur_stream()>>>((const u16*)X.data_ptr(), X.stride(0),              \
+        (const u16*)S.data_ptr(), S.stride(0), out.data_ptr<float>(), T, (int)K, tc, thresh, dscale,             \
+        (unsigned)seed, p > 0 ? 1 : 0)
   switch (R / 16) {
     case 1: LORA_TSUM(1); break;
     case 2: LORA_TSUM(2); break;
