@@ -349,9 +349,18 @@ __global__ __launch_bounds__(256) void tsum_kernel(const u16* __restrict__ X, lo
 // Scatter blocks of an fp32 [R, K] sum into up to 4 parameter gradients (bf16 or fp32, written or accumulated), one
 // launch for all adapters of a projection: output q is rows [r0, r0 + nr) x columns [c0, c0 + nc) of the sum,
 // transposed when tr (dB = (dB^T)^T: out[i][j] = sum[r0 + j][c0 + i]).
+// sum over the ns slabs (fixed order): eight independent loads in flight per step, not one dependent chain
 __device__ __forceinline__ float slab_sum(const float* __restrict__ p, long o, long slab, int ns) {
   float v = 0.f;
-  for (int z = 0; z < ns; ++z) v += p[o + z * slab];
+  int z = 0;
+  for (; z + 8 <= ns; z += 8) {
+    float f[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) f[i] = p[o + (z + i) * slab];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) v += f[i];
+  }
+  for (; z < ns; ++z) v += p[o + z * slab];
   return v;
 }
 
