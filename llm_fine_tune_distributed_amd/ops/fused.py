@@ -71,8 +71,9 @@ def _wgrad_cfg(T: int, N: int, K: int) -> int:
     if (N % 256 == 0 and K % 256 == 0 and 64 < (N // 256) * (K // 256) <= 128 and (T // 32) % 2 == 0
             and (N // 256) * (K // 128) < 256):
         # e.g. qkv [3072 x 2048]: 96 tiles of 256 x 256 split 2 ways over the tokens fill 192 CUs with
-        # half-depth pieces, vs 192 tiles of 256 x 128 at 0.75 of a round: 0.113 vs 0.118 ms (r2_run48)
-        return 210
+        # half-depth pieces, vs 192 tiles of 256 x 128 at 0.75 of a round: 0.113 vs 0.118 ms (r2_run48); on the
+        # 4-wave kernel (cfg 1212): 0.106 vs 0.117 ms for the 8-wave ring split the same way (cfg 210, r4_run41)
+        return 1212 if T % 128 == 0 else 210
     if N % 256 == 0 and K % 128 == 0 and (N // 256) * (K // 128) >= 160:
         return 9
     if N % 256 == 0 and K % 128 == 0 and (T // 32) % 2 == 0 and (N // 256) * (K // 128) >= 32:

@@ -63,9 +63,9 @@ def test_default_path_smollm3_widths_vs_fp32_reference(monkeypatch):
     assert tr.get("tn.rope.c11", 0) == 3 and tr.get("tn.rope.tail", 0) == 3, tr  # qkv + RoPE, 384-tile tail split
     assert tr.get("attn.fwd32", 0) == 4 and tr.get("attn.dkdv32", 0) == 4 and tr.get("attn.dq32", 0) == 4, tr
     assert tr.get("attn.bwd_rope_epi", 0) == 3, tr  # inverse RoPE in the dq / dK epilogues of the 3 RoPE layers
-    # wgrad: the 4-wave ring (csrc/gemm_4w.hip) for gate_up and, hybrid split-K, down_proj; 8-wave rings for lm_head
-    # (8192-vocab: 256 tiles of 256 x 128) / o_proj (split 2) / qkv (split 2)
-    for c in (13, 1213, 9, 209, 210):
+    # wgrad: the 4-wave ring (csrc/gemm_4w.hip) for gate_up and, hybrid split-K, down_proj; the 4-wave kernel split 2
+    # ways over the tokens for qkv; 8-wave rings for lm_head (8192-vocab: 256 tiles of 256 x 128) / o_proj (split 2)
+    for c in (13, 1213, 9, 209, 1212):
         assert tr.get(f"wgrad.c{c}", 0) > 0, (c, tr)
     assert tr.get("wgrad.norm_slots", 0) > 0, tr
     assert tr.get("dgrad.swiglu.c7", 0) >= 4 and tr.get("dgrad.tail", 0) > 0, tr  # down dgrad + SwiGLU bwd
