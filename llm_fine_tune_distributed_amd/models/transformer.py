@@ -64,6 +64,12 @@ class Attention(nn.Module):
             a = ops.qkv_rope_attention(h, self.qkv_proj, rope_cs[0], rope_cs[1], cu_seqlens, max_seqlen,
                                        c.num_attention_heads, c.num_key_value_heads, c.head_dim)
             return ops.linear(a, self.o_proj)
+        if self.lora is not None and self.use_rope and self.cp_group is None:
+            # the LoRA-widened qkv GEMM with the RoPE epilogue + attention as one node (inverse RoPE in the backward's
+            # dq / dK epilogues), the plain composition where the HIP path does not apply
+            a = ops.lora_qkv_rope_attention(h, self.qkv_proj, self.lora["qkv"], rope_cs[0], rope_cs[1], cu_seqlens,
+                                            max_seqlen, c.num_attention_heads, c.num_key_value_heads, c.head_dim)
+            return ops.lora_linear(a, self.o_proj, self.lora["o"])
         if self.lora is None and self.use_rope:
             # projection + RoPE in one HIP GEMM (epilogue rotation) where the shapes allow
             qkv = ops.linear_rope(h, self.qkv_proj, rope_cs[0], rope_cs[1], c.num_attention_heads,

@@ -1165,6 +1165,55 @@ def lora_swiglu_mlp(h, w_gate_up, w_down, l_gate_up, l_down) -> torch.Tensor:
     return lora_linear(swiglu(lora_linear(h, w_gate_up, l_gate_up)), w_down, l_down)
 
 
+class LoRAQKVRopeAttnFn(Function):
+    """attention(rope(x' W'^T)) for a LoRA-adapted qkv projection as ONE autograd node (the LoRA twin of
+    QKVRopeAttnFn): the widened activation X' (lora_fwd) goes through the forward GEMM with the RoPE epilogue, the
+    backward's flash_bwd_rope applies the inverse rotation in its dq / dK epilogues, and its dqkv feeds the wide LoRA
+    backward (base dgrad, adapter dx, dA / dB straight into main_grad) — no separate RoPE pass either way."""
+
+    @staticmethod
+    def forward(ctx, x, cos, sin, cu_seqlens, max_seqlen, n_q, n_kv, head_dim, scale, causal, wide, K, scaling, p,
+                seed, meta, *ab):
+        X, acat, state = _lora_wide_prep(x, wide, K, scaling, p, seed, meta, ab)
+        qkv = _ext.ops().gemm_tn_rope(X, wide, cos, sin, (n_q + n_kv) * head_dim, _tn_cfg(X.shape[0], wide.shape[0]))
+        out, lse = _ext.ops().flash_fwd(qkv, cu_seqlens, max_seqlen, n_q, n_kv, head_dim, scale, causal)
+        ctx.save_for_backward(X, acat, qkv, cu_seqlens, out, lse, cos, sin)
+        ctx.wide, ctx.adapters, ctx.meta = wide, ab, state
+        ctx.dims = (max_seqlen, n_q, n_kv, head_dim, scale, causal)
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        X, acat, qkv, cu, out, lse, cos, sin = ctx.saved_tensors
+        max_seqlen, n_q, n_kv, hd, scale, causal = ctx.dims
+        dqkv = _ext.ops().flash_bwd_rope(dout.contiguous(), qkv, out, lse, cu, max_seqlen, n_q, n_kv, hd, scale, causal,
+                                         cos, sin)
+        del qkv, out, lse
+        dx, dAs, dBs = _lora_wide_bwd(X, acat, ctx.wide, ctx.adapters, ctx.meta, dqkv, ctx.needs_input_grad[0])
+        if dx is not None:
+            dx = dx.view(ctx.meta[-1])
+        return (dx, None, None, None, None, None, None, None, None, None, None, None, None, None, None, None,
+                *dAs, *dBs)
+
+
+def lora_qkv_rope_attention(x, weight, lora, cos, sin, cu_seqlens, max_seqlen, n_q, n_kv, head_dim, scale=None,
+                            causal=True):
+    """flash_attention(rope_(lora_linear(x, W_qkv, lora))) — one fused autograd node on the HIP wide path
+    (LoRAQKVRopeAttnFn), the composition of the three otherwise."""
+    scale = scale if scale is not None else 1.0 / math.sqrt(head_dim)
+    args = _lora_wide_args(lora, weight)
+    x2d = x.reshape(-1, x.shape[-1])
+    if (args is not None and _ROPE_ATTN_FUSED and head_dim == 128 and _ext.use_hip(x2d)
+            and x2d.shape[0] % 256 == 0 and args[0][0].shape[0] % 256 == 0 and args[0][0].shape[1] % 128 == 0
+            and cos.dtype == torch.float32 and cos.is_contiguous() and sin.is_contiguous()
+            and cos.shape == (x2d.shape[0], 64)):
+        a, As, Bs = args
+        return LoRAQKVRopeAttnFn.apply(x, cos, sin, cu_seqlens, int(max_seqlen), n_q, n_kv, head_dim, float(scale),
+                                       bool(causal), *a, *As, *Bs)
+    qkv = rope_(lora_linear(x, weight, lora), cos, sin, n_q, n_kv, head_dim)
+    return flash_attention(qkv, cu_seqlens, max_seqlen, n_q, n_kv, head_dim, scale, causal)
+
+
 def lora_linear(x, weight, lora) -> torch.Tensor:
     """``lora``: a models.lora.FusedLoRA module (adapters per sub-projection)."""
     w = _lora_wide_args(lora, weight)

@@ -162,9 +162,11 @@ def test_lora_wide_gpu_matches_unfused():
     g1 = {n: p.grad.float().clone() for n, p in m.named_parameters() if p.grad is not None}
     # the HIP run above took the fused MLP (gate_up GEMM with the SwiGLU epilogue, down backward returning dgu:
     # ops.lora_swiglu_mlp); the reference composes the unfused LoRA linears with the SwiGLU op (same seed order)
-    orig, orig_mlp = T.ops.lora_linear, T.ops.lora_swiglu_mlp
+    orig, orig_mlp, orig_att = T.ops.lora_linear, T.ops.lora_swiglu_mlp, T.ops.lora_qkv_rope_attention
     T.ops.lora_linear = unfused
     T.ops.lora_swiglu_mlp = lambda h, wg, wd, lg, ld: unfused(ops.swiglu(unfused(h, wg, lg)), wd, ld)
+    T.ops.lora_qkv_rope_attention = lambda h, w, lq, cos, sin, cu, ms, nq, nkv, hd: ops.flash_attention(
+        ops.rope_(unfused(h, w, lq), cos, sin, nq, nkv, hd), cu, ms, nq, nkv, hd)
     try:
         for p in m.parameters():
             p.grad = None
@@ -172,7 +174,7 @@ def test_lora_wide_gpu_matches_unfused():
         out2 = m(ids, labels=ids)
         out2.loss.backward()
     finally:
-        T.ops.lora_linear, T.ops.lora_swiglu_mlp = orig, orig_mlp
+        T.ops.lora_linear, T.ops.lora_swiglu_mlp, T.ops.lora_qkv_rope_attention = orig, orig_mlp, orig_att
     assert abs(out.loss.item() - out2.loss.item()) < 2e-2
     for n, p in m.named_parameters():
         if p.grad is not None:
@@ -208,14 +210,16 @@ def test_lora_wide_sync_after_edits():
         return y.to(x.dtype).view(*x.shape[:-1], -1)
 
     def reference():
-        orig, orig_mlp = T.ops.lora_linear, T.ops.lora_swiglu_mlp
+        orig, orig_mlp, orig_att = T.ops.lora_linear, T.ops.lora_swiglu_mlp, T.ops.lora_qkv_rope_attention
         T.ops.lora_linear = unfused
         T.ops.lora_swiglu_mlp = lambda h, wg, wd, lg, ld: unfused(ops.swiglu(unfused(h, wg, lg)), wd, ld)
+        T.ops.lora_qkv_rope_attention = lambda h, w, lq, cos, sin, cu, ms, nq, nkv, hd: ops.flash_attention(
+            ops.rope_(unfused(h, w, lq), cos, sin, nq, nkv, hd), cu, ms, nq, nkv, hd)
         try:
             with torch.no_grad():
                 return m(ids, labels=ids).loss.item()
         finally:
-            T.ops.lora_linear, T.ops.lora_swiglu_mlp = orig, orig_mlp
+            T.ops.lora_linear, T.ops.lora_swiglu_mlp, T.ops.lora_qkv_rope_attention = orig, orig_mlp, orig_att
 
     with torch.no_grad():
         l0 = m(ids, labels=ids).loss.item()
