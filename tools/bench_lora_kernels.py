@@ -43,6 +43,7 @@ def main():
         ("lora_bwd_dx swiglu K=11008", lambda: ops.lora_bwd_dx(base, dxa, A, 0.05, 1, gu), 5 * T * I * 2),
         ("lora_tsum dA K=4096 R=48", lambda: ops.lora_tsum(xh, H, dxah, 0.05, 1), T * H * 2),
         ("lora_tsum dA K=11008 R=16", lambda: ops.lora_tsum(base, I, dxa, 0.05, 1), T * I * 2),
+        ("lora_tsum dA K=11008 p=0", lambda: ops.lora_tsum(base, I, dxa, 0.0, 1), T * I * 2),
         ("lora_tsum dB n=22016 R=32", lambda: ops.lora_tsum(gu, 2 * I, dxa2, 0.0, 0), T * 2 * I * 2),
         ("lora_tsum dB n=4096 R=16", lambda: ops.lora_tsum(xh, H, dxa, 0.0, 0), T * H * 2),
     ]
