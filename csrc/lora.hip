@@ -20,6 +20,26 @@
 namespace sftamd {
 namespace lora {
 
+// keep bits of the 8 elements i0 .. i0 + 7 (bit j: hash_u32(i0 + j, seed) >= thresh), bit-identical to hash_u32:
+// with i0 % 8 == 0 the eight indices share the high word (no carry out of the low one), so the first multiply of the
+// hash becomes a constant add per element and the high-word / seed terms are computed once per chunk.
+__device__ __forceinline__ unsigned keep8(unsigned long long i0, unsigned seed, unsigned thresh) {
+  const unsigned lo = (unsigned)i0 * 0x9E3779B9u;
+  const unsigned hi = (unsigned)(i0 >> 32) * 0x85EBCA6Bu ^ seed * 0xC2B2AE35u;
+  unsigned bits = 0;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    unsigned x = (lo + (unsigned)j * 0x9E3779B9u) ^ hi;
+    x ^= x >> 16;
+    x *= 0x7FEB352Du;
+    x ^= x >> 15;
+    x *= 0x846CA68Bu;
+    x ^= x >> 16;
+    bits |= (unsigned)(x >= thresh) << j;
+  }
+  return bits;
+}
+
 __device__ __forceinline__ f32x4 mfma(const bf16x8& a, const bf16x8& b, const f32x4& c) {
   return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
 }
@@ -90,9 +110,9 @@ __global__ __launch_bounds__(512) void fwd_kernel(const u16* __restrict__ x, con
         if (drop) {
           float f[8];
           unpack8(v[h], f);
-          const unsigned long long idx = (unsigned long long)lt * K + c;
+          const unsigned bits = keep8((unsigned long long)lt * K + c, seed, thresh);
 #pragma unroll
-          for (int i = 0; i < 8; ++i) f[i] = hash_u32(idx + i, seed) >= thresh ? f[i] * dscale : 0.f;
+          for (int i = 0; i < 8; ++i) f[i] = ((bits >> i) & 1u) ? f[i] * dscale : 0.f;
           v[h] = pack8(f);
           if (xd && lok) *(uint4*)(xd + lt * K + c) = v[h];
         }
@@ -209,12 +229,9 @@ __global__ __launch_bounds__(512) void bwd_dx_kernel(const u16* __restrict__ bas
     const long t = t0 + rg * RPT + i;
     float o[8];
     unpack8(vb[i], o);
-    const unsigned long long idx = (unsigned long long)t * K + k;
+    const unsigned bits = drop ? keep8((unsigned long long)t * K + k, seed, thresh) : 0xFFu;
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const bool keep = !drop || hash_u32(idx + j, seed) >= thresh;
-      o[j] += keep ? acc[i][j] * dscale : 0.f;
-    }
+    for (int j = 0; j < 8; ++j) o[j] += ((bits >> j) & 1u) ? acc[i][j] * dscale : 0.f;
     if constexpr (SWIGLU) {  // o = dact (fp32); the same arithmetic as swiglu_bwd_kernel on the bf16-rounded dact
       float gt[8], up[8], dg[8], du[8];
       unpack8(vg[i], gt);
@@ -305,9 +322,9 @@ __global__ __launch_bounds__(256) void tsum_kernel(const u16* __restrict__ X, lo
         const long t = t0 + tr + RPP * h;
         float f[8];
         unpack8(v, f);
-        const unsigned long long idx = (unsigned long long)t * K + k;
+        const unsigned bits = keep8((unsigned long long)t * K + k, seed, thresh);
 #pragma unroll
-        for (int i = 0; i < 8; ++i) f[i] = hash_u32(idx + i, seed) >= thresh ? f[i] * dscale : 0.f;
+        for (int i = 0; i < 8; ++i) f[i] = ((bits >> i) & 1u) ? f[i] * dscale : 0.f;
         v = pack8(f);
       }
       *(uint4*)&xs[tr + RPP * h][8 * c8] = v;
