@@ -40,6 +40,15 @@ __device__ __forceinline__ unsigned keep8(unsigned long long i0, unsigned seed, 
   return bits;
 }
 
+// zero the dropped bf16 elements of an 8-element chunk (bit j of `bits` = keep element j): pure bit selects, the
+// 1 / (1 - p) scale is applied to the reduction's fp32 result instead of to every element
+__device__ __forceinline__ uint4 mask8(uint4 v, unsigned bits) {
+  auto m = [&](int j) {
+    return ((0u - ((bits >> j) & 1u)) & 0xFFFFu) | ((0u - ((bits >> (j + 1)) & 1u)) & 0xFFFF0000u);
+  };
+  return make_uint4(v.x & m(0), v.y & m(2), v.z & m(4), v.w & m(6));
+}
+
 __device__ __forceinline__ f32x4 mfma(const bf16x8& a, const bf16x8& b, const f32x4& c) {
   return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
 }
@@ -108,13 +117,15 @@ __global__ __launch_bounds__(512) void fwd_kernel(const u16* __restrict__ x, con
       if (c < K) {
         if (lok) *(uint4*)(X + lt * ldX + c) = v[h];
         if (drop) {
-          float f[8];
-          unpack8(v[h], f);
           const unsigned bits = keep8((unsigned long long)lt * K + c, seed, thresh);
+          if (xd && lok) {  // dropout(x) itself, scaled (tests / save_xd only)
+            float f[8];
+            unpack8(v[h], f);
 #pragma unroll
-          for (int i = 0; i < 8; ++i) f[i] = ((bits >> i) & 1u) ? f[i] * dscale : 0.f;
-          v[h] = pack8(f);
-          if (xd && lok) *(uint4*)(xd + lt * K + c) = v[h];
+            for (int i = 0; i < 8; ++i) f[i] = ((bits >> i) & 1u) ? f[i] * dscale : 0.f;
+            *(uint4*)(xd + lt * K + c) = pack8(f);
+          }
+          v[h] = mask8(v[h], bits);  // the 1 / (1 - p) scale goes into s below
         }
         *(uint4*)&tile[lr][lc + 256 * h] = v[h];
       }
@@ -145,7 +156,7 @@ __global__ __launch_bounds__(512) void fwd_kernel(const u16* __restrict__ x, con
       float v = 0.f;
 #pragma unroll
       for (int q = 0; q < NW; ++q) v += red[q][row][col];
-      X[tt * ldX + K + col] = f2bf(s * v);
+      X[tt * ldX + K + col] = f2bf((drop ? s * dscale : s) * v);  // kept elements entered the MFMAs unscaled
     }
   }
   const int pad = (int)(ldX - K - R);
@@ -318,15 +329,7 @@ __global__ __launch_bounds__(256) void tsum_kernel(const u16* __restrict__ X, lo
 #pragma unroll
     for (int h = 0; h < XH; ++h) {
       uint4 v = xv[h];
-      if (drop) {
-        const long t = t0 + tr + RPP * h;
-        float f[8];
-        unpack8(v, f);
-        const unsigned bits = keep8((unsigned long long)t * K + k, seed, thresh);
-#pragma unroll
-        for (int i = 0; i < 8; ++i) f[i] = ((bits >> i) & 1u) ? f[i] * dscale : 0.f;
-        v = pack8(f);
-      }
+      if (drop) v = mask8(v, keep8((unsigned long long)(t0 + tr + RPP * h) * K + k, seed, thresh));
       *(uint4*)&xs[tr + RPP * h][8 * c8] = v;
     }
 #pragma unroll
@@ -353,12 +356,13 @@ __global__ __launch_bounds__(256) void tsum_kernel(const u16* __restrict__ X, lo
   }
   // C layout: lane (g, r16) holds rows 4 g + i (k), column r16 (r) of each 16 x 16 block: 4 consecutive k per lane
   float* slab = out + (long)blockIdx.y * R * K;
+  const float sc = drop ? dscale : 1.f;  // the dropout scale of the kept elements
 #pragma unroll
   for (int kt = 0; kt < KT; ++kt) {
     const int kk = k0 + 16 * (KT * w + kt) + 4 * g;
     if (kk < K) {  // K % 8 == 0: the lane's 4 columns are all in range or all out
 #pragma unroll
-      for (int j = 0; j < RF; ++j) *(f32x4*)(slab + (long)(16 * j + r16) * K + kk) = acc[kt][j];
+      for (int j = 0; j < RF; ++j) *(f32x4*)(slab + (long)(16 * j + r16) * K + kk) = acc[kt][j] * sc;
     }
   }
 }
