@@ -13,8 +13,9 @@
 //                VALU outer-product loop over an LDS-resident A tile (R <= 64 FMAs per output).
 //   lora_tsum:   the adapter gradients' token reductions (dA, dB^T), one pass over the wide operand.
 //
-// The dropout mask is hash_u32(t*K + k, seed) >= p * 2^32 (common.h), identical to dropout_add and to
-// the PyTorch reference, so nothing but the seed is stored between forward and backward.
+// The dropout mask is hash_u32(t*K + k, seed) >= p * 2^32 (common.h; keep8 below computes it per 8-element chunk),
+// identical to dropout_add and to the PyTorch reference, so nothing but the seed is stored between forward and
+// backward.
 #include "common.h"
 
 namespace sftamd {
@@ -271,10 +272,11 @@ __global__ __launch_bounds__(512) void bwd_dx_kernel(const u16* __restrict__ bas
 // with Xd = dropout(X) (the forward's mask regenerated from the seed) or X itself.
 //   dA    = dxa^T dropout(x):  X = X'[:, :K] (the widened activation), S = dxa [T, R]
 //   dB^T  = (s xa)^T dy:       X = dy [T, n],                          S = X'[:, K:K+R] (the adapter columns)
-// Workgroup = 64 columns of k x a chunk of tc tokens, 64 tokens per stage: the X tile (masked and scaled in registers)
-// and the S tile go into LDS row-major with 16-byte stores, and both MFMA fragments are transposed reads
-// (ds_read_b64_tr_b16: A = X^T rows k, B = S^T rows r, 8 consecutive tokens per lane); the next stage's global loads
-// are issued before this stage's MFMAs. Wave w owns k rows 16 w .. 16 w + 15 of the tile.
+// Workgroup = 64 KT columns of k x a chunk of tc tokens, 64 tokens per stage: the X tile (dropped elements zeroed by
+// bit selects; the 1 / (1 - p) scale is applied to the fp32 result) and the S tile go into LDS row-major with 16-byte
+// stores, and both MFMA fragments are transposed reads (ds_read_b64_tr_b16: A = X^T rows k, B = S^T rows r, 8
+// consecutive tokens per lane); the next stage's global loads are issued before this stage's MFMAs. Wave w owns k
+// rows 16 KT w .. 16 KT (w + 1) - 1 of the tile.
 __device__ __forceinline__ bf16x8 lds_tr8(const u16* p0, const u16* p1) {
   typedef __attribute__((address_space(3))) s16x4 lds_s4;
   const s16x4 a = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4*)p0);
@@ -445,7 +447,7 @@ static unsigned thresh_of(double p, float* dscale) {
 }  // namespace lora
 
 // x [T, K], A [R, K] (R = 16, 32, 48 or 64) -> (X' [T, ldX], xd): xd = dropout(x) [T, K] only with save_xd and
-// p > 0, else empty (the backward regenerates the mask from the seed: lora_da). ldX >= K + R (0 = K + R): columns
+// p > 0, else empty (the backward regenerates the mask from the seed: lora_tsum, lora_bwd_dx). ldX >= K + R (0 = K + R): columns
 // [K + R, ldX) are zero (the wide weight's padding to a whole K-tile pair of the HIP GEMMs)
 // swiglu: x is gu [T, 2K] and the widened activation is act = silu(gate) * up (see fwd_kernel SW)
 std::tuple<at::Tensor, at::Tensor> lora_fwd(const at::Tensor& x, const at::Tensor& A, double s, double p, int64_t seed,
