@@ -106,6 +106,10 @@ def parse(argv=None):
     ap.add_argument("--no-rccl-info", action="store_true", help="N > 1: do not capture RCCL's INFO log")
     ap.add_argument("--rccl-log-dir", default="/tmp/sftamd_rccl")
     ap.add_argument("--no-comm-probe", action="store_true", help="N > 1: skip the post-warmup collective probe")
+    ap.add_argument("--no-strict-dist", action="store_true",
+                    help="N > 1 on GPUs: still exit 0 when RCCL's log shows a degraded path (non-P2P transport, rank "
+                         "count mismatch, failed init, fewer channels than peer links); by default the JSON line is "
+                         "printed with dist.warnings and the run exits 3")
     return ap.parse_args(argv)
 
 
@@ -257,7 +261,9 @@ def run(a):
     mine = {"rank": st.rank, "world_size": dist.get_world_size() if dist.is_initialized() else 1,
             "backend": dist.get_backend() if dist.is_initialized() else None,
             "device": str(st.device), "ms_per_step": round(dt / a.steps * 1e3, 3), "peak_mem_gb": round(peak, 2),
-            "comm_exposed_ms": round(comm_ms, 3)}
+            "comm_exposed_ms": round(comm_ms, 3),
+            # after the timed steps (untimed): every rank must hold bitwise the same parameters (DDP / ZeRO-1 gather)
+            "param_sum": float(trainer.engine.param_flat.double().sum())}
     if rccl_dir is not None:
         from llm_fine_tune_distributed_amd.parallel import rccl_info
         mine["rccl"] = rccl_info.summarize(rccl_dir)
@@ -277,6 +283,14 @@ def run(a):
     full = a.freeze_policy == "full"
     mfu = tok_s * cfg.flops_per_token(a.seq) / (2.5e15 * st.world_size) if (full and on_gpu) else None
     shard = trainer.engine.shard
+    dist_warn, fatal = [], False
+    if st.world_size > 1 and rccl_dir is not None:
+        from llm_fine_tune_distributed_amd.parallel import rccl_info
+        dist_warn, fatal = rccl_info.dist_warnings([r_.get("rccl") for r_ in ranks], st.world_size)
+    if st.world_size > 1 and len({r_["param_sum"] for r_ in ranks}) != 1:
+        dist_warn.append("parameters differ across ranks after the timed steps")
+        fatal = True
+    strict = st.world_size > 1 and not a.no_strict_dist
     if st.is_main:
         rec = {
             "metric": ("samples/sec SmolLM3-3B full SFT bf16 (DDP)" if a.model == "smollm3-3b" and full
@@ -314,7 +328,9 @@ def run(a):
                      # every rank's communicator reported WORLD_SIZE ranks (None: no RCCL log, e.g. gloo)
                      "rccl_saw_all_ranks": (all((r_.get("rccl") or {}).get("nranks") == st.world_size for r_ in ranks)
                                             if rccl_dir is not None else None),
-                     "link_probe": [[int(b), round(t * 1e3, 4)] for b, t in getattr(trainer, "link_points", [])]},
+                     "link_probe": [[int(b), round(t * 1e3, 4)] for b, t in getattr(trainer, "link_points", [])],
+                     "params_equal_across_ranks": len({r_["param_sum"] for r_ in ranks}) == 1,
+                     "warnings": dist_warn, "strict": strict},
             "optimizer_sharding": "zero1" if shard else "none",
             "bucket_plan": bucket_plan(trainer.engine),
             "comm_probe": probe,
@@ -325,6 +341,8 @@ def run(a):
         if a.baseline_1gpu > 0:
             rec["scaling_efficiency"] = round(value / (st.world_size * a.baseline_1gpu), 4)
         print(json.dumps(rec), flush=True)
+        for w in dist_warn:
+            print(f"[bench] dist warning: {w}", file=sys.stderr, flush=True)
     if a.profile_steps:
         sync()
         prof = None
@@ -346,6 +364,10 @@ def run(a):
     if st.world_size > 1:
         barrier()
         dist.destroy_process_group()
+    if strict and fatal:
+        # the record above is printed (with dist.warnings) but the run fails loud: a scaling number measured over a
+        # degraded transport must not pass as a healthy one
+        sys.exit(3)
 
 
 def run_recipe(a):

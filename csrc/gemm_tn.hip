@@ -1152,6 +1152,7 @@ void launch4(const at::Tensor& a, const at::Tensor& w, int N, const EpiArgs& ea)
 // A tile's rows in a per-tile descriptor, the whole weight in another, each lane's byte offset in a VGPR set once per
 // tile, the piece / K offsets in SGPRs — no per-piece 64-bit VALU address arithmetic in the loop.
 typedef __amdgpu_buffer_rsrc_t rsrc_t;
+typedef __attribute__((ext_vector_type(4))) unsigned u32x4;
 __device__ __forceinline__ rsrc_t tile_rsrc(const u16* p) {
   const unsigned long long a = (unsigned long long)p;
   const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)a), hi = __builtin_amdgcn_readfirstlane((unsigned)(a >> 32));
@@ -1187,7 +1188,7 @@ __device__ __forceinline__ void mfma_t(f32x4& c, const bf16x8& b, const bf16x8& 
 
 // one sub-step: 8 MFMA groups (fragment row i x 8 B fragments, TRC); READ: the next sub-step's 16 fragments from img;
 // NP DMA pieces spread over the first DG groups; BAR: the K-tile barrier after group 0
-template <int EPI, bool INIT, bool READ, int NP, bool BAR, int DG = 4>
+template <int EPI, bool INIT, bool READ, int NP, bool BAR, int DG = 4, bool ROWC = false>
 __device__ __forceinline__ void tn5_sub(f32x4 (&acc)[8][8], const bf16x8 (&fa)[8], const bf16x8 (&fb)[8],
                                         bf16x8 (&ra)[8], bf16x8 (&rb)[8], const char* img, int offA, int offB,
                                         Stager5<EPI>& st, char* dst, int w, char* dst2 = nullptr) {
@@ -1195,7 +1196,10 @@ __device__ __forceinline__ void tn5_sub(f32x4 (&acc)[8][8], const bf16x8 (&fa)[8
 #pragma unroll
   for (int i = 0; i < 8; ++i) {
 #pragma unroll
-    for (int j = 0; j < 8; ++j) mfma_t<INIT>(acc[i][j], fb[j], fa[i]);
+    for (int j = 0; j < 8; ++j) {
+      if constexpr (ROWC) mfma_t<INIT>(acc[i][j], fa[i], fb[j]);  // A first: rows on the register index
+      else mfma_t<INIT>(acc[i][j], fb[j], fa[i]);                  // TRC: columns on the register index
+    }
     if (BAR && i == 0) __builtin_amdgcn_s_barrier();
     if (READ) {
       ra[i] = lds_row(img, offA + 2048 * i);
@@ -1449,6 +1453,267 @@ void launch5(const at::Tensor& a, const at::Tensor& w, int N, const EpiArgs& ea)
   SFT_LAUNCH_CHECK();
 }
 
+// ============================================================================================
+// Row-contiguous store epilogue (cfg 60 / 61 = plain / nt stores): the persistent kernel above with the MFMA operands
+// in natural order (A fragment first: lane (g, ii) of fragment (i, j) holds rows 16 i + 4 g + e, column 16 j + ii of
+// the wave tile) and the B image rows PERMUTED in the LDS-DMA (each lane of a piece just points at another weight
+// row) so that image row 16 j + ii of a wave's 128 columns is output column 8 ii + j. A lane's 8 fragments then hold 8
+// CONSECUTIVE columns of each of its rows: one 16-byte store per (fragment row i, register e), 4 rows x 256 contiguous
+// bytes per wave instruction = 8 whole cache lines (hipBLASLt's pattern, profiles/r4_gemm_fwd.md; the TRC kernel's
+// stores cover 16 rows x 64 bytes = 16 half lines), no lane shuffles, 32 stores per lane and tile.
+// Paired epilogues put the two columns an output combines into fragments j and j + 4 of ONE lane: image row 16 j + ii
+// <- column 4 ii + j of the "lo" half (SWIGLU: gate, ROPE: head dim d), 16 (j + 4) + ii <- the same column of the "hi"
+// half (up, d + 64). A lane then holds 4 consecutive columns of each output per row; one DPP exchange with the
+// neighbour lane (ii ^ 1) turns two rows x 8 bytes into one row x 16 bytes per lane (8 rows x 128 bytes = 8 whole
+// lines per instruction). SWIGLU: 48 stores per lane and tile (gate, up, act), ROPE: 32.
+// B piece q (= image piece w + 4 q) of wave w holds weight rows r6_base + r6_off(q) + {8 or 4} x (lane >> 3).
+// ============================================================================================
+template <int EPI>
+__device__ __forceinline__ int r6_base(int n0, int w, int lr) {
+  if constexpr (EPI == EPI_PLAIN) return n0 + 64 * (w & 1) + (w >> 1) + 8 * lr;
+  else if constexpr (EPI == EPI_SWIGLU) return (n0 >> 1) + 32 * (w & 1) + (w >> 1) + 4 * lr;
+  else return n0 + 32 * (w & 1) + (w >> 1) + 4 * lr;
+}
+template <int EPI>
+__device__ __forceinline__ int r6_off(int q, int I) {
+  if constexpr (EPI == EPI_PLAIN) return 128 * (q >> 2) + 2 * (q & 3);
+  const int S = EPI == EPI_SWIGLU ? 64 : 128, H = EPI == EPI_SWIGLU ? I : 64;
+  return S * (q >> 2) + 2 * (q & 1) + ((q & 2) ? H : 0);
+}
+
+template <int EPI>
+__device__ __forceinline__ void tn6_stager(Stager5<EPI>& st, const u16* A, long lda, long ldb, int m0, int n0, int w,
+                                           int lane) {
+  const int lr = lane >> 3, ch = (lane & 7) ^ (4 * (w & 1) + (lr >> 1));
+  st.ra = tile_rsrc(A + (long)m0 * lda);
+  st.va = (unsigned)(((8 * w + lr) * lda + 8 * ch) * 2);
+  st.vb = (unsigned)(((long)r6_base<EPI>(n0, w, lr) * ldb + 8 * ch) * 2);
+  st.kb = 0;
+}
+
+__device__ __forceinline__ unsigned dpp_swap1(unsigned v) {  // value of lane ii ^ 1 (quad_perm [1, 0, 3, 2])
+  return (unsigned)__builtin_amdgcn_mov_dpp((int)v, 0xB1, 0xF, 0xF, false);
+}
+
+// Two rows (registers e, e + 1) x 4 columns per lane -> one row x 8 columns: the even lane of a pair keeps row e and
+// takes its neighbour's 4 columns of it, the odd lane keeps row e + 1 (columns 4 (ii - 1) ..).
+__device__ __forceinline__ u32x4 pair_rows(uint2 x0, uint2 x1, bool odd) {
+  const unsigned sx = odd ? x0.x : x1.x, sy = odd ? x0.y : x1.y;
+  const unsigned rx = dpp_swap1(sx), ry = dpp_swap1(sy);
+  return odd ? u32x4{rx, ry, x1.x, x1.y} : u32x4{x0.x, x0.y, rx, ry};
+}
+
+template <int EPI, int AUX>
+__device__ __forceinline__ void tn6_store(f32x4 (&acc)[8][8], const EpiArgs& ea, int m0, int n0, int wm, int wn,
+                                          int lane) {
+  const int g = lane >> 4, ii = lane & 15;
+  const int r0 = m0 + wm * 128;  // the wave's first row
+  if constexpr (EPI == EPI_PLAIN) {
+    const rsrc_t rc = tile_rsrc(ea.C + (long)r0 * ea.ldc);
+    const unsigned v = (unsigned)(((long)(4 * g) * ea.ldc + n0 + 128 * wn + 8 * ii) * 2);
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const u32x4 d = {pack2(acc[i][0][e], acc[i][1][e]), pack2(acc[i][2][e], acc[i][3][e]),
+                         pack2(acc[i][4][e], acc[i][5][e]), pack2(acc[i][6][e], acc[i][7][e])};
+        __builtin_amdgcn_raw_buffer_store_b128(d, rc, v, (int)((16 * i + e) * ea.ldc * 2), AUX);
+      }
+  } else {
+    const bool odd = ii & 1;
+    const int cpair = 4 * (ii & ~1);  // first column of the lane pair's 8
+    if constexpr (EPI == EPI_SWIGLU) {
+      const int c0 = (n0 >> 1) + 64 * wn;  // first act column of the wave
+      const rsrc_t rg = tile_rsrc(ea.C + (long)r0 * ea.ldc), rat = tile_rsrc(ea.act + (long)r0 * ea.I);
+      const unsigned vg = (unsigned)(((long)(4 * g + odd) * ea.ldc + c0 + cpair) * 2);
+      const unsigned vu = vg + (unsigned)(ea.I * 2);
+      const unsigned va = (unsigned)(((long)(4 * g + odd) * ea.I + c0 + cpair) * 2);
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int ep = 0; ep < 2; ++ep) {
+          uint2 G[2], U[2], Ac[2];
+#pragma unroll
+          for (int h = 0; h < 2; ++h) {
+            const int e = 2 * ep + h;
+            float ga[4], up[4], o[4];
+#pragma unroll
+            for (int jj = 0; jj < 4; ++jj) {
+              ga[jj] = rbf(acc[i][jj][e]);  // act from the bf16 gate / up the backward will see
+              up[jj] = rbf(acc[i][4 + jj][e]);
+              o[jj] = silu(ga[jj]) * up[jj];
+            }
+            G[h] = make_uint2(pack2(ga[0], ga[1]), pack2(ga[2], ga[3]));
+            U[h] = make_uint2(pack2(up[0], up[1]), pack2(up[2], up[3]));
+            Ac[h] = make_uint2(pack2(o[0], o[1]), pack2(o[2], o[3]));
+          }
+          const int so = (16 * i + 2 * ep);
+          __builtin_amdgcn_raw_buffer_store_b128(pair_rows(G[0], G[1], odd), rg, vg, (int)(so * ea.ldc * 2), AUX);
+          __builtin_amdgcn_raw_buffer_store_b128(pair_rows(U[0], U[1], odd), rg, vu, (int)(so * ea.ldc * 2), AUX);
+          __builtin_amdgcn_raw_buffer_store_b128(pair_rows(Ac[0], Ac[1], odd), rat, va, (int)(so * ea.I * 2), AUX);
+        }
+    } else {  // ROPE: the wave's 128 columns are one head; lo = dims 4 ii + jj, hi = + 64
+      const int hc = n0 + 128 * wn;
+      const bool rot = hc < ea.rope_cols;  // a q / k head (wave-uniform)
+      const rsrc_t rc = tile_rsrc(ea.C + (long)r0 * ea.ldc);
+      const unsigned vl = (unsigned)(((long)(4 * g + odd) * ea.ldc + hc + cpair) * 2);
+      const unsigned vh = vl + 128;
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int ep = 0; ep < 2; ++ep) {
+          uint2 L[2], H[2];
+#pragma unroll
+          for (int h = 0; h < 2; ++h) {
+            const int e = 2 * ep + h;
+            float lo[4], hi[4];
+#pragma unroll
+            for (int jj = 0; jj < 4; ++jj) {
+              lo[jj] = acc[i][jj][e];
+              hi[jj] = acc[i][4 + jj][e];
+            }
+            if (rot) {
+              const long row = r0 + 16 * i + 4 * g + e;
+              const float4 c4 = *(const float4*)(ea.cosb + row * 64 + 4 * ii);
+              const float4 s4 = *(const float4*)(ea.sinb + row * 64 + 4 * ii);
+              const float cs[4] = {c4.x, c4.y, c4.z, c4.w}, sn[4] = {s4.x, s4.y, s4.z, s4.w};
+#pragma unroll
+              for (int jj = 0; jj < 4; ++jj) {
+                const float x1 = rbf(lo[jj]), x2 = rbf(hi[jj]);  // rope of the bf16 projection (unfused twin)
+                lo[jj] = x1 * cs[jj] - x2 * sn[jj];
+                hi[jj] = x2 * cs[jj] + x1 * sn[jj];
+              }
+            }
+            L[h] = make_uint2(pack2(lo[0], lo[1]), pack2(lo[2], lo[3]));
+            H[h] = make_uint2(pack2(hi[0], hi[1]), pack2(hi[2], hi[3]));
+          }
+          const int so = (16 * i + 2 * ep) * ea.ldc * 2;
+          __builtin_amdgcn_raw_buffer_store_b128(pair_rows(L[0], L[1], odd), rc, vl, so, AUX);
+          __builtin_amdgcn_raw_buffer_store_b128(pair_rows(H[0], H[1], odd), rc, vh, so, AUX);
+        }
+    }
+  }
+}
+
+template <int EPI, bool NK2, int AUX>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1)))
+tn6_kernel(const u16* __restrict__ A, const u16* __restrict__ B, int K, long lda, long ldb, int nbm, int nbn,
+           int group, EpiArgs ea) {
+  using G = Cfg2<256, 256, 2, 2, 2>;
+  constexpr int NST = EPI == EPI_SWIGLU ? 48 : 32;  // stores per lane and tile
+  __shared__ __attribute__((aligned(16))) char smem[2 * G::STAGE];
+  const int tiles = nbm * nbn, nwg = gridDim.x, orig = blockIdx.x;
+  const int xcd = orig & 7, l = orig >> 3, nx = (nwg - xcd + 7) >> 3;
+  const int t_end = tn5_range_start(xcd + 1, tiles);
+  int tile = tn5_range_start(xcd, tiles) + l;
+  const int tid = threadIdx.x, lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  if (tile >= t_end) return;
+  const int wm = w >> 1, wn = w & 1;
+  const int nk = K / BK2;
+  const int g = lane >> 4, ii = lane & 15;
+  const int ra = wm * 128 + ii, rb = 256 + wn * 128 + ii;
+  const int offA0 = ra * ROWB2 + 16 * swz2(ra, g), offA1 = ra * ROWB2 + 16 * swz2(ra, 4 + g);
+  const int offB0 = rb * ROWB2 + 16 * swz2(rb, g), offB1 = rb * ROWB2 + 16 * swz2(rb, 4 + g);
+  char* X = smem;
+  char* Y = smem + G::STAGE;
+  Stager5<EPI> st;
+  st.rb = tile_rsrc(B);
+  st.a32 = (unsigned)(64 * lda);
+#pragma unroll
+  for (int q = 0; q < 8; ++q) st.boff[q] = (unsigned)((long)r6_off<EPI>(q, ea.I) * ldb * 2);
+  int m0, n0;
+  tn5_coords(tile, nbm, nbn, group, m0, n0);
+  tn6_stager(st, A, lda, ldb, m0, n0, w, lane);
+#pragma unroll
+  for (int j = 0; j < 16; ++j) st.piece(X, w, j);
+  st.adv(BK2);
+#pragma unroll
+  for (int j = 0; j < 16; ++j) st.piece(Y, w, j);
+  st.adv(BK2);
+  __builtin_amdgcn_s_waitcnt(waitcnt_imm(16, 15));  // K0 of the first tile (its K1 may fly)
+  f32x4 acc[8][8];
+  bf16x8 a0[8], b0[8], a1[8], b1[8];
+  bool first = true;
+  for (;;) {
+    __builtin_amdgcn_s_barrier();
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      a0[i] = lds_row(X, offA0 + 2048 * i);
+      b0[i] = lds_row(X, offB0 + 2048 * i);
+    }
+    const int next = tile + nx;
+    const bool has_next = next < t_end;
+    int m1 = m0, n1 = n0;
+    if (has_next) tn5_coords(next, nbm, nbn, group, m1, n1);
+    // the K-tile pairs of tn5_kernel (same boundaries, DMA placement and vmcnt accounting)
+    auto pair = [&](auto init, auto dma, auto last) {
+      constexpr bool IN = decltype(init)::value, DM = decltype(dma)::value, LA = decltype(last)::value;
+      __builtin_amdgcn_s_waitcnt(waitcnt_imm(63, 0));
+      tn5_sub<EPI, IN, true, 0, false, 4, true>(acc, a0, b0, a1, b1, X, offA1, offB1, st, X, w);
+      if (IN && !first) {
+        __builtin_amdgcn_s_waitcnt(waitcnt_imm(NST, 0));  // K1 landed; the previous tile's stores may still drain
+      } else {
+        __builtin_amdgcn_s_waitcnt(waitcnt_imm(0, 0));
+      }
+      tn5_sub<EPI, false, true, DM ? 16 : 0, true, 4, true>(acc, a1, b1, a0, b0, Y, offA0, offB0, st, X, w);
+      if (DM) st.adv(BK2);
+      __builtin_amdgcn_s_waitcnt(waitcnt_imm(63, 0));
+      tn5_sub<EPI, false, true, 0, false, 4, true>(acc, a0, b0, a1, b1, Y, offA1, offB1, st, Y, w);
+      __builtin_amdgcn_s_waitcnt(waitcnt_imm(0, 0));
+      if constexpr (LA) {
+        tn6_stager(st, A, lda, ldb, m1, n1, w, lane);
+        tn5_sub<EPI, false, false, 32, true, 4, true>(acc, a1, b1, a0, b0, X, offA0, offB0, st, X, w, Y);
+      } else {
+        tn5_sub<EPI, false, true, 16, true, 4, true>(acc, a1, b1, a0, b0, X, offA0, offB0, st, Y, w);
+        st.adv(BK2);
+      }
+    };
+    if constexpr (NK2) {
+      pair(std::true_type(), std::false_type(), std::true_type());
+    } else {
+      pair(std::true_type(), std::true_type(), std::false_type());
+      for (int t = 2; t < nk - 2; t += 2) pair(std::false_type(), std::true_type(), std::false_type());
+      pair(std::false_type(), std::false_type(), std::true_type());
+    }
+    asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 3" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+    tn6_store<EPI, AUX>(acc, ea, m0, n0, wm, wn, lane);
+    __builtin_amdgcn_sched_barrier(0);
+    if (!has_next) break;
+    st.adv(2 * BK2);
+    if constexpr (EPI == EPI_SWIGLU)
+      __builtin_amdgcn_s_waitcnt(waitcnt_imm(NST, 15));  // K0 and K1 landed (the 48 stores may fly)
+    else
+      __builtin_amdgcn_s_waitcnt(waitcnt_imm(NST + 16, 15));  // K0 landed (K1 and the 32 stores may fly)
+    first = false;
+    tile = next;
+    m0 = m1;
+    n0 = n1;
+  }
+  __builtin_amdgcn_s_waitcnt(waitcnt_imm(0, 15));
+}
+
+template <int EPI>
+void launch6(const at::Tensor& a, const at::Tensor& w, int N, const EpiArgs& ea, bool nt) {
+  const int M = a.size(0), K = a.size(1);
+  SFT_CHECK(M % 256 == 0 && N % 256 == 0 && K % 128 == 0, "gemm_tn row-contiguous: M, N % 256, K % 128");
+  SFT_CHECK(ea.ldc % 8 == 0 && ((uintptr_t)ea.C) % 16 == 0, "gemm_tn row-contiguous: 16-byte aligned output rows");
+  const int nbm = M / 256, nbn = N / 256, tiles = nbm * nbn;
+  const int grid = std::min(tiles, num_cus());
+  const int grp = std::min(group_m(), nbm);
+  auto A = (const u16*)a.data_ptr();
+  auto B = (const u16*)w.data_ptr();
+  const long lda = a.stride(0), ldb = w.stride(0);
+  if (K == 128) {
+    if (nt) tn6_kernel<EPI, true, 2><<<grid, 256, 0, cur_stream()>>>(A, B, K, lda, ldb, nbm, nbn, grp, ea);
+    else tn6_kernel<EPI, true, 0><<<grid, 256, 0, cur_stream()>>>(A, B, K, lda, ldb, nbm, nbn, grp, ea);
+  } else {
+    if (nt) tn6_kernel<EPI, false, 2><<<grid, 256, 0, cur_stream()>>>(A, B, K, lda, ldb, nbm, nbn, grp, ea);
+    else tn6_kernel<EPI, false, 0><<<grid, 256, 0, cur_stream()>>>(A, B, K, lda, ldb, nbm, nbn, grp, ea);
+  }
+  SFT_LAUNCH_CHECK();
+}
+
 template <int EPI, bool TRC, int D = 1>
 void launch3(const at::Tensor& a, const at::Tensor& w, int N, const EpiArgs& ea) {
   const int M = a.size(0), K = a.size(1);
@@ -1515,8 +1780,10 @@ at::Tensor gemm_tn(const at::Tensor& a, const at::Tensor& w, int64_t cfg) {
     tn::launch4<tn::EPI_PLAIN, 0, 4>(a, w, N, ea);
   } else if (cfg == 164) {
     tn::launch5<tn::EPI_PLAIN>(a, w, N, ea);
+  } else if (cfg == 60 || cfg == 61) {
+    tn::launch6<tn::EPI_PLAIN>(a, w, N, ea, cfg == 61);
   } else {
-    SFT_CHECK(cfg == 0, "gemm_tn: cfg ", cfg, " not built (0, 2, 5, 6, 11, 12, 164)");
+    SFT_CHECK(cfg == 0, "gemm_tn: cfg ", cfg, " not built (0, 2, 5, 6, 11, 12, 60, 61, 164)");
     SFT_CHECK(N % 256 == 0, "gemm_tn 256x256: N % 256");
     tn::launch<256, 256, 2, 4, 5, tn::EPI_PLAIN>(a, w, N, ea);
   }
@@ -1533,6 +1800,7 @@ std::tuple<at::Tensor, at::Tensor> gemm_tn_swiglu(const at::Tensor& x, const at:
   auto act = at::empty({M, I}, x.options());
   tn::EpiArgs ea{(u16*)gu.data_ptr(), (u16*)act.data_ptr(), nullptr, nullptr, (long)N, I, 0};
   if (cfg == 164) tn::launch5<tn::EPI_SWIGLU>(x, w_gu, N, ea);
+  else if (cfg == 60 || cfg == 61) tn::launch6<tn::EPI_SWIGLU>(x, w_gu, N, ea, cfg == 61);
   else if (cfg == 12) tn::launch4<tn::EPI_SWIGLU, 0, 4>(x, w_gu, N, ea);
   else if (x.size(1) % 64 == 0 && N % 256 == 0 && cfg == 11) tn::launch3<tn::EPI_SWIGLU, true, 2>(x, w_gu, N, ea);
   else if (x.size(1) % 64 == 0) tn::launch2<256, 256, 2, 4, 2, tn::EPI_SWIGLU, 3>(x, w_gu, N, ea);
@@ -1555,6 +1823,7 @@ at::Tensor gemm_tn_rope(const at::Tensor& x, const at::Tensor& w, const at::Tens
   tn::EpiArgs ea{(u16*)c.data_ptr(), nullptr, cosb.data_ptr<float>(), sinb.data_ptr<float>(), (long)N, 0,
                  (int)rope_cols};
   if (cfg == 164) tn::launch5<tn::EPI_ROPE>(x, w, N, ea);
+  else if (cfg == 60 || cfg == 61) tn::launch6<tn::EPI_ROPE>(x, w, N, ea, cfg == 61);
   else if (cfg == 12) tn::launch4<tn::EPI_ROPE, 0, 4>(x, w, N, ea);
   else if (cfg == 2 && x.size(1) % 64 == 0) tn::launch2<256, 256, 2, 4, 2, tn::EPI_ROPE>(x, w, N, ea);
   else if (cfg == 5 && x.size(1) % 64 == 0) tn::launch2<256, 256, 2, 4, 2, tn::EPI_ROPE, 3>(x, w, N, ea);

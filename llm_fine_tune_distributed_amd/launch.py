@@ -59,8 +59,10 @@ def _spawn(n: int, cmd: List[str], addr: str, port: int, restart: int, node_rank
         env = dict(os.environ)
         env.update(WORLD_SIZE=str(n * nnodes), RANK=str(node_rank * n + lr), LOCAL_RANK=str(lr),
                    LOCAL_WORLD_SIZE=str(n), GROUP_RANK=str(node_rank), MASTER_ADDR=addr, MASTER_PORT=str(port),
-                   SFTAMD_RESTART_COUNT=str(restart), HSA_ENABLE_IPC_MODE_LEGACY="0", SFTAMD_LAUNCHER="sftamd",
-                   SFTAMD_HEARTBEAT_DIR=hb_dir)
+                   SFTAMD_RESTART_COUNT=str(restart), SFTAMD_LAUNCHER="sftamd", SFTAMD_HEARTBEAT_DIR=hb_dir)
+        # dmabuf IPC (the only IPC mode the hosts' driver supports; rationale: parallel/process_group.py) unless the
+        # caller set the mode explicitly
+        env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
         env.setdefault("OMP_NUM_THREADS", "1")
         procs.append(subprocess.Popen(cmd, env=env, start_new_session=new_session, preexec_fn=_die_with_parent))
     return procs

@@ -162,8 +162,23 @@ def _as_output(y2d: torch.Tensor, lead) -> torch.Tensor:
     return y2d if tuple(y2d.shape) == shape else torch.ops.aten._unsafe_view(y2d, shape)
 
 
+_FWD_HIP_MAXN = int(os.environ.get("SFTAMD_FWD_HIP_MAXN", "0"))  # plain forwards with N, K <= this on cfg 61
+_ROWC_CFG = int(os.environ.get("SFTAMD_TN_CFG", "61"))  # the row-contiguous persistent kernel (61 = nt stores)
+
+
+def _rowc_ok(x2d: torch.Tensor, w: torch.Tensor) -> bool:
+    """Shapes the row-contiguous persistent forward GEMM (csrc/gemm_tn.hip cfg 60 / 61) takes."""
+    M, K = x2d.shape
+    return (_ext.use_hip(x2d) and x2d.dtype == torch.bfloat16 and w.dtype == torch.bfloat16 and M % 256 == 0
+            and M > 0 and K % 128 == 0 and w.shape[0] % 256 == 0 and x2d.stride(1) == 1 and x2d.stride(0) % 8 == 0
+            and w.is_contiguous() and x2d.data_ptr() % 16 == 0 and w.data_ptr() % 16 == 0)
+
+
 def fwd_gemm(x2d: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
-    """y = x2d @ w^T for a plain projection forward (hipBLASLt)."""
+    """y = x2d @ w^T for a plain projection forward (hipBLASLt, or the row-contiguous HIP kernel for the shapes where
+    it wins: SFTAMD_FWD_HIP_MAXN)."""
+    if _FWD_HIP_MAXN and w.shape[0] <= _FWD_HIP_MAXN and w.shape[1] <= _FWD_HIP_MAXN and _rowc_ok(x2d, w):
+        return _ext.ops().gemm_tn(x2d, w, _ROWC_CFG)
     return torch.nn.functional.linear(x2d, w)
 
 
@@ -444,10 +459,13 @@ def _tn_ok(x2d: torch.Tensor, w: torch.Tensor) -> bool:
             and x2d.stride(1) == 1 and x2d.stride(0) % 8 == 0 and w.is_contiguous() and w.shape[0] % 256 == 0)
 
 
-def _tn_cfg(M: int, N: int) -> int:
-    """Forward GEMM with an epilogue (qkv + RoPE): the ping-pong 8-phase schedule (cfg 11, csrc/gemm_tn.hip: the two
-    wave rows one barrier apart, transposed-C epilogue) wherever N % 256 == 0 — 2-6 % faster than the BK64 ring (cfg 2)
-    on every SmolLM3 shape (profiles/r2_gemm_pingpong.md)."""
+def _tn_cfg(M: int, N: int, K: int = 64) -> int:
+    """Forward GEMM with an epilogue (qkv + RoPE): the row-contiguous persistent kernel (SFTAMD_TN_CFG, default 61)
+    where K % 128 == 0; else the ping-pong 8-phase schedule (cfg 11, csrc/gemm_tn.hip: the two wave rows one barrier
+    apart, transposed-C epilogue) wherever N % 256 == 0 — 2-6 % faster than the BK64 ring (cfg 2) on every SmolLM3
+    shape (profiles/r2_gemm_pingpong.md)."""
+    if _ROWC_CFG in (60, 61) and M % 256 == 0 and N % 256 == 0 and K % 128 == 0:
+        return _ROWC_CFG
     return 11 if N % 256 == 0 else 2
 
 
@@ -481,7 +499,7 @@ def _tn_swiglu_cfg(weight: torch.Tensor) -> int:
     """gate_up + SwiGLU epilogue (SFTAMD_TN=swiglu / 1): the persistent 4-wave kernel where it applies (0.669 vs
     0.705 ms for hipBLASLt + the SwiGLU kernel at M = 8192, profiles/r4_gemm_fwd.md), else the ping-pong kernel."""
     if weight.shape[0] % 256 == 0 and weight.shape[1] % 128 == 0:
-        return 164
+        return _ROWC_CFG
     return 11 if weight.shape[0] % 256 == 0 else 5
 
 
@@ -571,7 +589,7 @@ class QKVRopeFn(Function):
     @staticmethod
     def forward(ctx, x, weight, cos, sin, n_q, n_kv, head_dim):
         x2d = x.reshape(-1, x.shape[-1])
-        qkv = _ext.ops().gemm_tn_rope(x2d, weight, cos, sin, (n_q + n_kv) * head_dim, _tn_cfg(x2d.shape[0], weight.shape[0]))
+        qkv = _ext.ops().gemm_tn_rope(x2d, weight, cos, sin, (n_q + n_kv) * head_dim, _tn_cfg(x2d.shape[0], weight.shape[0], x2d.shape[1]))
         ctx.save_for_backward(x2d, cos, sin)
         ctx.weight = weight
         ctx.dims = (n_q, n_kv, head_dim)
@@ -681,7 +699,7 @@ class QKVRopeAttnFn(Function):
     def forward(ctx, x, weight, cos, sin, cu_seqlens, max_seqlen, n_q, n_kv, head_dim, scale, causal):
         x2d = x.reshape(-1, x.shape[-1])
         qkv = _ext.ops().gemm_tn_rope(x2d, weight, cos, sin, (n_q + n_kv) * head_dim,
-                                      _tn_cfg(x2d.shape[0], weight.shape[0]))
+                                      _tn_cfg(x2d.shape[0], weight.shape[0], x2d.shape[1]))
         out, lse = _ext.ops().flash_fwd(qkv, cu_seqlens, max_seqlen, n_q, n_kv, head_dim, scale, causal)
         ctx.save_for_backward(x2d, qkv, cu_seqlens, out, lse, cos, sin)
         ctx.weight = weight
@@ -923,6 +941,24 @@ def bump_param_epoch() -> None:
     _PARAM_EPOCH[0] += 1
 
 
+_PARAM_SYNCS: list = []  # weak refs to the overlapped optimizers' synchronize(): order the stream after the updates
+
+
+def register_param_sync(fn) -> None:
+    """An optimizer that runs its update on a side stream under the next forward registers its ``synchronize`` here.
+    A copy that reads MANY layers' parameters at once (the batched LoRA wide-weight refresh) calls every registered
+    one first: the per-layer forward pre-hooks only order each layer after its OWN update / all-gather."""
+    _PARAM_SYNCS[:] = [r for r in _PARAM_SYNCS if r() is not None and r() != fn]
+    _PARAM_SYNCS.append(weakref.WeakMethod(fn) if hasattr(fn, "__self__") else (lambda f=fn: f))
+
+
+def _await_param_updates() -> None:
+    for r in list(_PARAM_SYNCS):
+        f = r()
+        if f is not None:
+            f()
+
+
 def _sync_wide(wide: torch.Tensor, K: int, r: int, meta, Bs) -> None:
     """Copy the adapters' B matrices into their blocks of the wide weight — only when one may have changed since
     the last copy: an optimizer update (the parameter epoch) or an in-place edit / checkpoint load (the Bs' version
@@ -930,6 +966,7 @@ def _sync_wide(wide: torch.Tensor, K: int, r: int, meta, Bs) -> None:
     key = (_PARAM_EPOCH[0],) + tuple((B._version, B.data_ptr()) for B in Bs)
     if getattr(wide, "_sftamd_bkey", None) == key:
         return
+    _await_param_updates()
     with torch.no_grad():
         for (o, rows, c), B in zip(meta, Bs):
             wide[o:o + rows, K + c:K + c + r].copy_(B)
@@ -983,6 +1020,9 @@ def _wide_sync(wide, K, r, meta, As, Bs) -> torch.Tensor:
         table = torch.tensor(rows, dtype=torch.int64).to(wide.device)
         _WIDE_TABLE[0], _WIDE_TABLE[1] = tkey, (table, max(d[2] * d[3] for d in rows))
     table, most = _WIDE_TABLE[1]
+    # the copy reads every stale layer's adapters: wait for ALL overlapped updates / ZeRO-1 gathers first (LoRA's
+    # update is a few MB, so the overlap it gives up is negligible)
+    _await_param_updates()
     _ext.ops().copy2d_batch(table, int(most))
     for w in stale:
         w._sftamd_sync.key = w._sftamd_sync.state()
@@ -1175,7 +1215,7 @@ class LoRAQKVRopeAttnFn(Function):
     def forward(ctx, x, cos, sin, cu_seqlens, max_seqlen, n_q, n_kv, head_dim, scale, causal, wide, K, scaling, p,
                 seed, meta, *ab):
         X, acat, state = _lora_wide_prep(x, wide, K, scaling, p, seed, meta, ab)
-        qkv = _ext.ops().gemm_tn_rope(X, wide, cos, sin, (n_q + n_kv) * head_dim, _tn_cfg(X.shape[0], wide.shape[0]))
+        qkv = _ext.ops().gemm_tn_rope(X, wide, cos, sin, (n_q + n_kv) * head_dim, _tn_cfg(X.shape[0], wide.shape[0], X.shape[1]))
         out, lse = _ext.ops().flash_fwd(qkv, cu_seqlens, max_seqlen, n_q, n_kv, head_dim, scale, causal)
         ctx.save_for_backward(X, acat, qkv, cu_seqlens, out, lse, cos, sin)
         ctx.wide, ctx.adapters, ctx.meta = wide, ab, state

@@ -233,10 +233,12 @@ def plan_bucket_mb(world_size: int, total_bytes: int = 0, alpha_us: Optional[flo
     return float(min(256.0, max(16.0, mb)))
 
 
-def fit_link(points, world_size: int):
+def fit_link(points, world_size: int, strict: bool = False):
     """(alpha_us, link_gbps) of ``t = alpha + S / (N L)`` through measured (bytes, seconds) reduce-scatter points
     (least squares over >= 2 sizes; the slope is 1 / (N L): each rank moves 1/N of the buffer per link). Guarded
-    against noise: alpha >= 1 us, L in [1, 1000] GB/s."""
+    against noise: alpha >= 1 us, L in [1, 1000] GB/s. ``strict``: None instead of a fit above 1000 GB/s (a flat or
+    negative slope from a noisy probe would otherwise pin L at 1000 GB/s and the bucket cap at its ceiling — the
+    caller then keeps the modelled plan)."""
     pts = sorted((float(b), float(t)) for b, t in points)
     if len(pts) < 2 or pts[-1][0] <= pts[0][0]:
         raise ValueError("fit_link needs >= 2 distinct message sizes")
@@ -247,14 +249,16 @@ def fit_link(points, world_size: int):
     slope = sum((b - mx) * (t - my) for b, t in pts) / sxx
     slope = max(slope, 1e-15)
     alpha = max(1e-6, my - slope * mx)
-    link = 1.0 / (slope * max(1, world_size))
-    return alpha * 1e6, float(min(1000.0, max(1.0, link / 1e9)))
+    link = 1.0 / (slope * max(1, world_size)) / 1e9
+    if strict and link > 1000.0:  # the clamp that matters: it would set the bucket cap to its ceiling
+        return None
+    return alpha * 1e6, float(min(1000.0, max(1.0, link)))
 
 
-def measure_link(world_size: int, device, group=None, sizes_mb=(4.0, 32.0), iters: int = 3):
-    """Startup probe of the gradient collective: in-place reduce-scatter of bf16 buffers of ``sizes_mb``, timed on
-    every rank; the MAX over ranks of each size's mean time (so every rank fits the SAME alpha / L and builds the
-    same bucket plan). Returns [(bytes, seconds), ...]."""
+def measure_link(world_size: int, device, group=None, sizes_mb=(4.0, 32.0), iters: int = 7):
+    """Startup probe of the gradient collective: in-place reduce-scatter of bf16 buffers of ``sizes_mb``, each call
+    timed on every rank (two warm-up calls first); the MAX over ranks of each size's MEDIAN time (robust to one slow
+    call; every rank fits the SAME alpha / L and builds the same bucket plan). Returns [(bytes, seconds), ...]."""
     if world_size <= 1:
         return []
     import time
@@ -266,14 +270,18 @@ def measure_link(world_size: int, device, group=None, sizes_mb=(4.0, 32.0), iter
         n = max(world_size * 64, int(mb * 2 ** 20 / 2) // (world_size * 64) * (world_size * 64))
         buf = torch.ones(n, dtype=torch.bfloat16, device=device)
         part = buf[rank * (n // world_size):(rank + 1) * (n // world_size)]
-        dist.reduce_scatter_tensor(part, buf, group=group)  # warm (RCCL channel setup on the first call)
-        sync()
-        dist.barrier(group=group)
-        t0 = time.perf_counter()
-        for _ in range(iters):
+        for _ in range(2):  # warm (RCCL channel setup on the first call)
             dist.reduce_scatter_tensor(part, buf, group=group)
         sync()
-        out.append([n * 2, (time.perf_counter() - t0) / iters])
+        dist.barrier(group=group)
+        ts = []
+        for _ in range(iters):
+            t0 = time.perf_counter()
+            dist.reduce_scatter_tensor(part, buf, group=group)
+            sync()
+            ts.append(time.perf_counter() - t0)
+        ts.sort()
+        out.append([n * 2, ts[len(ts) // 2]])
         del buf, part
     t = torch.tensor([p[1] for p in out], dtype=torch.float64, device=device)
     dist.all_reduce(t, op=dist.ReduceOp.MAX, group=group)

@@ -65,8 +65,12 @@ def setup_distributed(backend: Optional[str] = None, timeout_s: float = 1800.0, 
     if _STATE is not None:
         return _STATE
     ws, rank, local_rank = read_env()
-    # dmabuf IPC for RCCL / CUDA-tensor sharing between ranks: the HSA runtime reads this once, when it initialises,
-    # which torch.cuda.is_available() below triggers — so it must be in the environment before that call
+    # dmabuf IPC for RCCL / CUDA-tensor sharing between ranks. Why it is on by default: the MI355X hosts this runs on
+    # ship a kernel driver that supports ONLY dmabuf IPC — with the legacy mode, hipIpcGetMemHandle fails with
+    # "invalid argument", which is what RCCL's intra-node P2P/IPC transport (and any CUDA-tensor sharing between
+    # ranks) calls at communicator setup; dmabuf is also the upstream ROCm 7 default path. An explicit setting in the
+    # environment wins (setdefault). The HSA runtime reads it once, when it initialises, which
+    # torch.cuda.is_available() below triggers — so it must be in the environment before that call.
     os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
     use_gpu = (device != "cpu") and torch.cuda.is_available()
     if use_gpu:

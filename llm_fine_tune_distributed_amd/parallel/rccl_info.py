@@ -80,3 +80,32 @@ def summarize(directory: str, pid: Optional[int] = None) -> Optional[Dict]:
         except OSError:
             return None
     return summarize_text(text)
+
+
+def dist_warnings(per_rank, world_size: int):
+    """(warnings, fatal) for the multi-GPU record from every rank's ``summarize`` result (None = no log).
+
+    Fatal = positive evidence of a degraded collective path: a non-P2P transport (SHM / NET instead of xGMI P2P),
+    a communicator that saw a different rank count, an init that never completed, or fewer channels than peer links
+    (world_size - 1: one xGMI link per GPU pair on an MI355X node). A missing log is a (non-fatal) warning: nothing is
+    known about that rank."""
+    warnings, fatal = [], False
+    for r, s in enumerate(per_rank):
+        if not s:
+            warnings.append(f"rank {r}: no RCCL INFO log (transport unknown)")
+            continue
+        bad = [t for t in (s.get("p2p_transport") or []) if not str(t).startswith("P2P")]
+        if bad:
+            warnings.append(f"rank {r}: transport {','.join(bad)} (expected P2P over xGMI)")
+            fatal = True
+        if s.get("nranks") is not None and s["nranks"] != world_size:
+            warnings.append(f"rank {r}: communicator saw {s['nranks']} ranks, WORLD_SIZE={world_size}")
+            fatal = True
+        if s.get("init_ok") is False:
+            warnings.append(f"rank {r}: no 'Init COMPLETE' in the RCCL log")
+            fatal = True
+        nch = s.get("n_channels")
+        if nch is not None and nch < world_size - 1:
+            warnings.append(f"rank {r}: {nch} channels < {world_size - 1} peer links")
+            fatal = True
+    return warnings, fatal

@@ -148,6 +148,7 @@ class FlatAdamW:
         for i, layer in enumerate(inner.layers):
             self._hooks.append(layer.register_forward_pre_hook(waiter(min(i + 1, nl))))
         self._hooks.append(inner.layers[-1].register_forward_hook(waiter(len(groups) - 1)))
+        ops.register_param_sync(self.synchronize)  # reads of many layers' parameters at once (LoRA wide refresh)
         self.overlap = True
         return True
 
@@ -371,6 +372,7 @@ class ShardedAdamW(FlatAdamW):
             self._hooks.append(layer.register_forward_pre_hook(waiter(i + 1)))
         self._hooks.append(inner.layers[-1].register_forward_hook(waiter(last)))
         self._stream = _update_stream(e.device) if e.device.type == "cuda" else None
+        ops.register_param_sync(self.synchronize)
         self.overlap = True
         return True
 

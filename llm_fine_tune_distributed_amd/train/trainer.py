@@ -133,7 +133,8 @@ class SFTTrainer:
             # measured collective cost -> bucket cap (every rank fits the same max-over-ranks timings)
             from ..parallel.ddp import fit_link, measure_link
             self.link_points = measure_link(self.dist.world_size, dev)
-            link = fit_link(self.link_points, self.dist.world_size)
+            # None (a clamped fit: noise) -> the modelled 30 us / 100 GB/s plan, recorded as plan_source "model"
+            link = fit_link(self.link_points, self.dist.world_size, strict=True)
         self.engine = DDPEngine(model, self.dist.world_size, self.dist.rank,
                                 bucket_cap_mb=args.ddp_bucket_cap_mb,  # None: xGMI plan (plan_bucket_mb)
                                 first_bucket_mb=args.ddp_first_bucket_mb,

@@ -17,8 +17,9 @@ Every rank records where it is â€” step, phase, last gradient bucket launched â€
 Phases that legitimately run long without beats â€” checkpoint I/O (rank 0 writes while the others wait in a
 barrier), checkpoint loading, the first step (GEMM tuning, extension warm-up) â€” run inside ``hold(phase)``,
 which allows them the slow-phase limit (``SFTAMD_SLOW_PHASE_TIMEOUT_S``, default max(4 x hang timeout, 1800 s))
-instead of the hang timeout; ``pause()`` / ``resume()`` switch the hang check off outside the training loop
-(before ``train()`` and after it returns), where nothing beats at all. The deadline always applies.
+instead of the hang timeout (the limit goes into every beat record as ``limit_s``, which the launcher's watchdog
+honours too); ``pause()`` / ``resume()`` switch the hang check off outside the training loop (before ``train()``
+and after it returns), where nothing beats at all â€” except inside a ``hold``. The deadline always applies.
 
 A beat is a few microseconds of host work (no device sync); with no directory, no stderr cadence and no
 watchdog configured, ``beat`` is a no-op.
@@ -53,7 +54,8 @@ class Heartbeat:
         self.hang_timeout = hang_timeout_s
         slow = float(os.environ.get("SFTAMD_SLOW_PHASE_TIMEOUT_S", "0") or 0)
         self.slow_timeout = slow if slow > 0 else max(4.0 * hang_timeout_s, 1800.0)
-        self._limit = hang_timeout_s  # the hang limit in force (raised inside hold())
+        self._limit = hang_timeout_s  # the in-process hang limit in force (raised inside hold())
+        self._hold_limit = 0.0  # > 0 inside hold(): the slow-phase limit, written into every record for launch.py
         self._paused = False
         if deadline_s is None:
             deadline_s = float(os.environ.get("SFTAMD_RUN_DEADLINE_S", "0") or 0) or None
@@ -91,8 +93,10 @@ class Heartbeat:
         rec.update(extra)
         if self._paused:
             rec["paused"] = True  # launch.py skips the hang check of a paused rank
-        elif self._limit != self.hang_timeout:
-            rec["limit_s"] = self._limit  # ... and applies a hold's longer limit
+        elif self._hold_limit > 0:
+            # ... and applies a hold's longer limit â€” written whether or not THIS process runs its own watchdog: a
+            # launcher-only watchdog (launch.py --hang-timeout, children without SFTAMD_HANG_TIMEOUT_S) reads it too
+            rec["limit_s"] = self._hold_limit
         self.last = rec
         self._last_beat = time.monotonic()
         line = _fmt(rec)
@@ -113,15 +117,21 @@ class Heartbeat:
 
     @contextlib.contextmanager
     def hold(self, phase: str, timeout_s: Optional[float] = None, step: Optional[int] = None):
-        """A phase allowed ``timeout_s`` (default: the slow-phase limit) without beats; beats on entry and exit."""
-        prev = self._limit
+        """A phase allowed ``timeout_s`` (default: the slow-phase limit) without beats; beats on entry and exit.
+        A hold also lifts ``pause()`` for its duration: a held phase outside the training loop (the final save and
+        its barrier) keeps the slow-phase limit instead of no hang check at all."""
+        prev, prev_hold, prev_paused = self._limit, self._hold_limit, self._paused
+        self._hold_limit = max(self.hang_timeout, timeout_s or self.slow_timeout)
         if self.hang_timeout > 0:
-            self._limit = max(self.hang_timeout, timeout_s or self.slow_timeout)
+            self._limit = self._hold_limit
+        self._paused = False
         self.beat(step, phase)
         try:
             yield
         finally:
-            self._limit = prev
+            self._limit, self._hold_limit = prev, prev_hold
+            self._last_beat = time.monotonic()
+            self._paused = prev_paused
             self.beat(step, f"{phase}_done")
 
     def pause(self):

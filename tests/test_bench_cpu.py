@@ -23,9 +23,11 @@ def _json_lines(out):
     return [json.loads(l) for l in out.splitlines() if l.startswith("{") and '"metric"' in l]
 
 
-@pytest.mark.parametrize("n", [1, 2, 4])
+@pytest.mark.parametrize("n", [1, 2, 4, 8])
 def test_bench_self_launches_n_ranks(n):
-    r = _bench(n, ["--baseline-1gpu", "10"])
+    """n = 8 rehearses the driver's scaling run (bench.py --gpus 8) end to end on gloo: pad unit, shard sizes, the
+    sparse tied-embedding exchange, sparse_cap and the probe-planned buckets all take their 8-rank values."""
+    r = _bench(n, ["--baseline-1gpu", "10"], timeout=600)
     assert r.returncode == 0, r.stderr[-3000:]
     recs = _json_lines(r.stdout)
     assert len(recs) == 1, r.stdout  # exactly one JSON line, from rank 0
@@ -42,7 +44,10 @@ def test_bench_self_launches_n_ranks(n):
         assert k in rec["dist"], k  # the multi-GPU record explains itself (None / [] where it cannot apply)
     for k in ("plan_source", "alpha_us", "link_gbps"):
         assert k in rec["bucket_plan"], k
+    assert rec["dist"]["params_equal_across_ranks"] and rec["dist"]["warnings"] == []
     if n > 1:
+        assert rec["dist"]["strict"] is True
+        assert rec["bucket_plan"]["tied_sparse"]  # tiny ties its embedding: the sparse exchange ran
         assert rec["dist"]["backend"] == "gloo" and rec["dist"]["launcher"] == "sftamd"
         assert rec["optimizer_sharding"] == "zero1"
         # gloo rehearsal: no RCCL log to read, but the startup link probe ran and planned the buckets
@@ -83,6 +88,19 @@ def test_bench_hang_is_detected_and_reported():
     assert "last heartbeat" in r.stderr and '"rank":1' in r.stderr, r.stderr[-3000:]
     assert '"bucket"' in r.stderr  # the DDP engine's position rides in every heartbeat
     assert not _json_lines(r.stdout)
+
+
+def test_dist_warnings_fail_loud_on_degraded_transport():
+    from llm_fine_tune_distributed_amd.parallel.rccl_info import dist_warnings
+    ok = {"p2p_transport": ["P2P/IPC"], "n_channels": 16, "nranks": 8, "init_ok": True}
+    assert dist_warnings([ok] * 8, 8) == ([], False)
+    w, fatal = dist_warnings([ok] * 7 + [dict(ok, p2p_transport=["SHM/direct/direct"])], 8)
+    assert fatal and "rank 7" in w[0] and "SHM" in w[0]
+    assert dist_warnings([ok] * 7 + [dict(ok, nranks=4)], 8)[1]
+    assert dist_warnings([dict(ok, n_channels=4)] * 8, 8)[1]
+    assert dist_warnings([dict(ok, n_channels=1, nranks=2)] * 2, 2) == ([], False)  # one link per GPU pair
+    w, fatal = dist_warnings([ok] * 7 + [None], 8)  # no log: unknown, not degraded
+    assert not fatal and "no RCCL INFO log" in w[0]
 
 
 def test_rccl_info_summary_parser():

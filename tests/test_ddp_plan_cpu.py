@@ -148,6 +148,13 @@ def test_fit_link_recovers_alpha_and_bandwidth():
         assert a == pytest.approx(alpha_us, rel=1e-6) and l == pytest.approx(gbps, rel=1e-6)
     with pytest.raises(ValueError):
         fit_link([(1 << 20, 1e-4)], 2)
+    # a noisy probe whose larger message was no slower (slope <= 0) clamps L to 1000 GB/s; strict -> None (the
+    # trainer then keeps the modelled plan) instead of a 256 MB bucket cap
+    noisy = [(4 << 20, 3e-4), (32 << 20, 2.9e-4)]
+    assert fit_link(noisy, 8)[1] == 1000.0
+    assert fit_link(noisy, 8, strict=True) is None
+    good = [(b, 30e-6 + b / (8 * 100e9)) for b in (4 << 20, 32 << 20)]
+    assert fit_link(good, 8, strict=True) == pytest.approx(fit_link(good, 8))
 
 
 def test_bucket_plan_follows_the_measured_link():

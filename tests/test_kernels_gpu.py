@@ -583,6 +583,46 @@ def test_gemm_tn_4wave(M, N, K):
             assert rel_err(out, exp) < 1e-2, cfg
 
 
+def _elem_ok(out, exp, tol=1e-2):
+    """every element within tol x max|exp| (a wrong column / row permutation or a skipped tail tile is O(max) off;
+    bf16 rounding is 2^-8 of the element)."""
+    d = (out.float() - exp.float()).abs()
+    return bool((d <= tol * exp.float().abs().max()).all())
+
+
+@pytest.mark.parametrize("M,N,K", [(256, 256, 128), (512, 512, 256), (768, 2560, 2176), (4096, 4352, 256),
+                                   (2304, 7424, 128), (8192, 3072, 2048)])
+@pytest.mark.parametrize("cfg", [60, 61])
+def test_gemm_tn_rowc(cfg, M, N, K):
+    """cfg 60 / 61: the persistent 4-wave kernel with the row-contiguous store epilogue (B image rows permuted so a
+    lane holds 8 consecutive output columns; 61 = nt stores). Plain, SwiGLU and RoPE epilogues vs the fp32 reference,
+    every element checked: grids with several tiles per workgroup (> 256 tiles), the K = 128 single-pair path and
+    the ragged last round."""
+    torch.manual_seed(0)
+    x = torch.randn(M, K, device=DEV, dtype=torch.bfloat16)
+    w = torch.randn(N, K, device=DEV, dtype=torch.bfloat16)
+    ref32 = x.float() @ w.float().t()
+    c = _ext.ops().gemm_tn(x, w, cfg)
+    assert rel_err(c, ref32) < 5e-3 and _elem_ok(c, ref32)
+    w1 = w * 0.1
+    gu_ref = x.float() @ w1.float().t()
+    gu, act = _ext.ops().gemm_tn_swiglu(x, w1, cfg)
+    assert rel_err(gu, gu_ref) < 5e-3 and _elem_ok(gu, gu_ref)
+    act_ref = _ext.ops().swiglu_fwd(gu)  # act from the bf16 gate / up, as the unfused kernel computes it
+    assert rel_err(act, act_ref) < 2e-3 and _elem_ok(act, act_ref.float())
+    D, nkv = 128, 1
+    nq = N // D - 2 * nkv
+    pos = (torch.arange(M, device=DEV) % 1000).float()
+    inv = 1.0 / (10000 ** (torch.arange(0, D, 2, device=DEV).float() / D))
+    fr = pos[:, None] * inv[None, :]
+    cs, sn = fr.cos().contiguous(), fr.sin().contiguous()
+    y = (x.float() @ w.float().t()).to(torch.bfloat16)
+    qk = y[:, :(nq + nkv) * D].view(M, nq + nkv, D)
+    exp = torch.cat([ref.apply_rope(qk, cs, sn).reshape(M, -1), y[:, (nq + nkv) * D:]], dim=1)
+    out = _ext.ops().gemm_tn_rope(x, w, cs, sn, (nq + nkv) * D, cfg)
+    assert rel_err(out, exp) < 1e-2 and _elem_ok(out, exp, 2e-2)
+
+
 def test_gemm_tn_strided_rows():
     """a may be a row-strided view (e.g. a column slice of a wider activation)."""
     torch.manual_seed(0)
