@@ -263,7 +263,7 @@ def run(a):
             "device": str(st.device), "ms_per_step": round(dt / a.steps * 1e3, 3), "peak_mem_gb": round(peak, 2),
             "comm_exposed_ms": round(comm_ms, 3),
             # after the timed steps (untimed): every rank must hold bitwise the same parameters (DDP / ZeRO-1 gather)
-            "param_sum": float(trainer.engine.param_flat.double().sum())}
+            "param_sum": float(torch.sum(trainer.engine.param_flat, dtype=torch.float64))}
     if rccl_dir is not None:
         from llm_fine_tune_distributed_amd.parallel import rccl_info
         mine["rccl"] = rccl_info.summarize(rccl_dir)

@@ -65,6 +65,7 @@ TORCH_LIBRARY(sftamd, m) {
   m.def("lora_fwd(Tensor x, Tensor A, float s, float p, int seed, int ldX=0, bool save_xd=False, bool swiglu=False) -> (Tensor, Tensor)");
   m.def("lora_bwd_dx(Tensor base, Tensor dxa, Tensor A, float p, int seed, Tensor? gu=None) -> Tensor");
   m.def("lora_tsum(Tensor X, int K, Tensor S, float p, int seed) -> Tensor");
+  m.def("lora_dxa(Tensor dy, Tensor Bc, float s) -> Tensor");
   m.def("lora_grad_out(Tensor sum, Tensor(a!)[] outs, int[] r0, int[] c0, bool tr, int[] accumulate) -> ()");
   m.def("copy2d_batch(Tensor desc, int max_elems) -> ()");
   m.def("embedding_bwd(Tensor dy, Tensor sorted_ids, Tensor perm, Tensor(a!) grad_weight) -> ()");

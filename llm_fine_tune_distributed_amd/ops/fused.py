@@ -162,7 +162,8 @@ def _as_output(y2d: torch.Tensor, lead) -> torch.Tensor:
     return y2d if tuple(y2d.shape) == shape else torch.ops.aten._unsafe_view(y2d, shape)
 
 
-_FWD_HIP_MAXN = int(os.environ.get("SFTAMD_FWD_HIP_MAXN", "0"))  # plain forwards with N, K <= this on cfg 61
+# plain projection forwards whose output width N is listed here run on the row-contiguous kernel (reduction <= 4096)
+_FWD_HIP_N = {int(v) for v in os.environ.get("SFTAMD_FWD_HIP_N", "").split(",") if v.strip()}
 _ROWC_CFG = int(os.environ.get("SFTAMD_TN_CFG", "61"))  # the row-contiguous persistent kernel (61 = nt stores)
 
 
@@ -175,9 +176,9 @@ def _rowc_ok(x2d: torch.Tensor, w: torch.Tensor) -> bool:
 
 
 def fwd_gemm(x2d: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
-    """y = x2d @ w^T for a plain projection forward (hipBLASLt, or the row-contiguous HIP kernel for the shapes where
-    it wins: SFTAMD_FWD_HIP_MAXN)."""
-    if _FWD_HIP_MAXN and w.shape[0] <= _FWD_HIP_MAXN and w.shape[1] <= _FWD_HIP_MAXN and _rowc_ok(x2d, w):
+    """y = x2d @ w^T for a plain projection forward (hipBLASLt, or the row-contiguous HIP kernel for the output widths
+    listed in SFTAMD_FWD_HIP_N)."""
+    if w.shape[0] in _FWD_HIP_N and w.shape[1] <= 4096 and _rowc_ok(x2d, w):
         return _ext.ops().gemm_tn(x2d, w, _ROWC_CFG)
     return torch.nn.functional.linear(x2d, w)
 
@@ -460,12 +461,11 @@ def _tn_ok(x2d: torch.Tensor, w: torch.Tensor) -> bool:
 
 
 def _tn_cfg(M: int, N: int, K: int = 64) -> int:
-    """Forward GEMM with an epilogue (qkv + RoPE): the row-contiguous persistent kernel (SFTAMD_TN_CFG, default 61)
-    where K % 128 == 0; else the ping-pong 8-phase schedule (cfg 11, csrc/gemm_tn.hip: the two wave rows one barrier
-    apart, transposed-C epilogue) wherever N % 256 == 0 — 2-6 % faster than the BK64 ring (cfg 2) on every SmolLM3
-    shape (profiles/r2_gemm_pingpong.md)."""
-    if _ROWC_CFG in (60, 61) and M % 256 == 0 and N % 256 == 0 and K % 128 == 0:
-        return _ROWC_CFG
+    """Forward GEMM with an epilogue (qkv + RoPE): the ping-pong 8-phase schedule (cfg 11, csrc/gemm_tn.hip: the two
+    wave rows one barrier apart, transposed-C epilogue) wherever N % 256 == 0 — 2-6 % faster than the BK64 ring (cfg 2)
+    on every SmolLM3 shape (profiles/r2_gemm_pingpong.md). The persistent row-contiguous kernel (cfg 61) is faster in
+    isolation (0.121 vs 0.131 ms) but slower in the step: 137 vs 106 us per call, its 384 tiles are 1.5 rounds of one
+    workgroup per CU and the cos / sin loads of its epilogue wait behind the next tile's DMA (profiles/r5_gemm_fwd.md)."""
     return 11 if N % 256 == 0 else 2
 
 
@@ -523,6 +523,8 @@ class GateUpActFn(Function):
         ctx.weight = weight
         ctx.x_shape = x.shape
         ctx.mark_non_differentiable(act)
+        # act never receives a gradient: without this autograd would zero-fill a [T, I] tensor for it every backward
+        ctx.set_materialize_grads(False)
         return gu.view(*x.shape[:-1], gu.shape[-1]), act.view(*x.shape[:-1], act.shape[-1])
 
     @staticmethod
@@ -756,6 +758,25 @@ def _ce_rows(logits: torch.Tensor, labels: torch.Tensor, inv_count: torch.Tensor
     return torch.stack([loss, lse, ent, correct.float()])
 
 
+_UNIT_LOSS_GRAD = [False]
+
+
+class unit_loss_grad:
+    """Context for ``loss.backward()`` called on the LM-head loss itself (the trainer's step): the incoming gradient
+    of the loss is the implicit 1, so LMHeadCEFn.backward skips the two scale passes (dh * g over [T, hidden] and
+    h * g before the lm_head weight gradient) instead of multiplying by a device scalar it cannot inspect without a
+    host sync. Any other caller (a scaled or combined loss) keeps the general path."""
+
+    def __enter__(self):
+        self._prev = _UNIT_LOSS_GRAD[0]
+        _UNIT_LOSS_GRAD[0] = True
+        return self
+
+    def __exit__(self, *exc):
+        _UNIT_LOSS_GRAD[0] = self._prev
+        return False
+
+
 class LMHeadCEFn(Function):
     """loss = sum_t CE(h_t W^T, y_t) * inv_count, with dlogits computed in the forward pass
     (written over the logits buffer), so the fp32 logits are never materialised."""
@@ -778,10 +799,13 @@ class LMHeadCEFn(Function):
     def backward(ctx, dloss, _dstats):
         h2d, dlogits = ctx.saved_tensors
         w = ctx.weight
-        g = dloss.float()
+        g = None if _UNIT_LOSS_GRAD[0] else dloss.float()  # unit_loss_grad: d(loss) is exactly 1
         dh = dw = None
         if ctx.needs_input_grad[0]:
-            dh = (dgrad_mm(dlogits, w) * g.to(dlogits.dtype)).view(ctx.h_shape)
+            dh = dgrad_mm(dlogits, w)
+            if g is not None:
+                dh = dh * g.to(dlogits.dtype)
+            dh = dh.view(ctx.h_shape)
         if ctx.needs_input_grad[1]:
             dw = _accumulate_weight_grad(w, dlogits, h2d, scale=g)
         return dh, dw, None, None
@@ -923,6 +947,17 @@ def _scatter_grads(total: torch.Tensor, params, blocks, tr: bool):
     return out
 
 
+def _lora_dxa(dy2d: torch.Tensor, bc: torch.Tensor, s: float) -> torch.Tensor:
+    """s dy Bc for the adapters' B columns Bc [n, R] of the wide weight (a thin-N GEMM: the HIP streaming kernel where
+    the layout allows, torch.addmm with the scale as alpha otherwise)."""
+    R = bc.shape[1]
+    if (_ext.use_hip(dy2d) and dy2d.dtype == torch.bfloat16 and bc.dtype == torch.bfloat16 and R % 16 == 0
+            and 16 <= R <= 64 and dy2d.stride(1) == 1 and dy2d.stride(0) % 8 == 0 and dy2d.data_ptr() % 16 == 0
+            and dy2d.shape[1] % 8 == 0 and bc.stride(1) == 1 and bc.stride(0) % 8 == 0 and bc.data_ptr() % 16 == 0):
+        return _ext.ops().lora_dxa(dy2d, bc, float(s))
+    return torch.addmm(dy2d.new_empty(dy2d.shape[0], R), dy2d, bc, beta=0, alpha=s)
+
+
 def _lora_bwd_dx(base, dxa, acat, p, seed, gu=None):
     """dx = base + dropout(dxa A_cat); with gu (the SwiGLU input of a LoRA MLP's down projection) dgu =
     swiglu_bwd(dx, gu) instead, in the same pass (csrc/lora.hip bwd_dx_kernel: no dx round trip)."""
@@ -1043,7 +1078,7 @@ def _lora_gemm(X: torch.Tensor, wide: torch.Tensor) -> torch.Tensor:
     return torch.mm(X, wide.t())
 
 
-_LORA_FWD_CFG = 164  # persistent 4-wave kernel, plain stores (csrc/gemm_tn.hip)
+_LORA_FWD_CFG = int(os.environ.get("SFTAMD_LORA_FWD_CFG", "164"))  # persistent 4-wave kernel (csrc/gemm_tn.hip)
 
 
 def _lora_wide_prep(x, wide, K, scaling, p, seed, meta, ab, swiglu=False):
@@ -1072,8 +1107,8 @@ def _lora_wide_bwd(X, acat, wide, ab, state, dy2d, need_dx, gu=None):
     if not dy2d.is_contiguous():
         dy2d = dy2d.contiguous()
     base = dgrad_mm(dy2d, wide[:, :K])              # [T, K] (HIP 4-wave dgrad where the shapes allow)
-    # dxa = s dy B_blockdiag [T, R] (the scale as the GEMM's alpha, no extra pass)
-    dxa = torch.addmm(dy2d.new_empty(dy2d.shape[0], R), dy2d, wide[:, K:K + R], beta=0, alpha=scaling)
+    # dxa = s dy B_blockdiag [T, R]: one streaming pass over dy (csrc/lora.hip dxa_kernel, the scale in its epilogue)
+    dxa = _lora_dxa(dy2d, wide[:, K:K + R], scaling)
     # the adapter gradients of all sub-projections, each from one pass over its wide operand, scattered straight into
     # the parameters' flat gradient slices in one launch (no per-adapter GEMMs, slicing copies or autograd
     # accumulation): dB^T = (s xa)^T dy [R, n_out] (block (c_i, o_i) transposed is dB_i); dA = dxa^T dropout(x)

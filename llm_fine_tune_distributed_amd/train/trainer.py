@@ -33,6 +33,7 @@ import torch
 
 from ..data.collator import DataLoader, DistributedBatchSampler, SFTCollator
 from ..data.dataset import TokenizedDataset, cached_tokenize
+from .. import ops
 from ..models import CausalLM, apply_freeze_policy, build_model, get_config
 from ..models.lora import LoRAConfig
 from ..parallel.ddp import DDPEngine
@@ -353,7 +354,7 @@ class SFTTrainer:
                 with self._phase("fwd"):
                     out = model(**self._model_inputs(b), num_items_in_batch=n_items)
                 beat(self._hb_step, "bwd", micro=i)
-                with self._phase("bwd"):
+                with self._phase("bwd"), ops.unit_loss_grad():  # out.loss IS the LM-head loss: d(loss) = 1
                     out.loss.backward()
             acc[0] += out.loss.detach()
             acc[1:] += out.metrics

@@ -22,27 +22,47 @@ def _trace():
     return out
 
 
+# Per-parameter relative gradient error bounds, ~2x the maxima measured on MI355X (tools/gpu_runs/r5_run03.sh:
+# profiles/r5_default_path_errors.md). The errors come from bf16 activations (every parameter of a class sits at about
+# the same value), so a kernel bug touching a few percent of a weight's rows or columns stands far above them.
+SMOLLM3_BOUNDS = [("model.norm", 1.6e-2), ("layernorm", 4e-2), ("mlp", 4e-2), ("self_attn", 3.6e-2),
+                  ("embed", 3.6e-2)]
+LLAMA_BOUNDS = [("model.norm", 2.1e-2), ("input_layernorm", 8e-2), ("qkv", 8e-2), ("o_proj", 6e-2),
+                ("post_attention_layernorm", 5.5e-2), ("mlp", 5.4e-2), ("embed", 5.4e-2), ("lm_head", 4e-2)]
+
+
 def _cfg():
     return tiny("smollm3", hidden_size=2048, num_attention_heads=16, num_key_value_heads=4, head_dim=128,
                 intermediate_size=11008, vocab_size=8192, num_hidden_layers=4, max_position_embeddings=4096,
                 rope_theta=2e6)
 
 
-def test_default_path_smollm3_widths_vs_fp32_reference(monkeypatch):
+def _report(tag, errs, tr=None):
+    """DEFAULT_PATH_REPORT=<file>: append the per-parameter relative gradient errors (how the bounds were set) and the
+    dispatch trace."""
+    import json
+    import os
+    path = os.environ.get("DEFAULT_PATH_REPORT")
+    if path:
+        with open(path, "a") as f:
+            f.write(json.dumps({"test": tag, "errors": errs, "trace": tr}) + "\n")
+
+
+def _run_vs_reference(cfg, monkeypatch, B=16, T=512):
+    """Default-path fwd + bwd (dispatch trace on) and the fp32 PyTorch reference with the same weights.
+    Returns (trace, loss, ref loss, {param: relative grad error}, fused clip norm^2, reference norm^2)."""
     from llm_fine_tune_distributed_amd.parallel.ddp import DDPEngine
     assert _ext.load(), _ext.load_error()
     torch.manual_seed(0)
-    cfg = _cfg()
     m = build_model(cfg, device="cuda", dtype=torch.bfloat16, seed=11)
     ref = build_model(cfg, device="cuda", dtype=torch.float32, seed=11)
     with torch.no_grad():
         for (n, p), (n2, q) in zip(m.named_parameters(), ref.named_parameters()):
             assert n == n2
             q.copy_(p.float())
-    B, T = 16, 512
     ids = torch.randint(0, cfg.vocab_size, (B, T), device="cuda")
     labels = ids.clone()
-    labels[:, 400:] = -100  # padded-batch style ignored tail
+    labels[:, T - T // 5:] = -100  # padded-batch style ignored tail
 
     eng = DDPEngine(m, 1, 0)  # world 1 on GPU: gradients into the flat buffer, fused clip-norm slots
     assert eng.fused_norm
@@ -59,6 +79,33 @@ def test_default_path_smollm3_widths_vs_fp32_reference(monkeypatch):
     finally:
         _ext.ops().dispatch_trace(False)
     tr = _trace()
+    monkeypatch.setenv("SFTAMD_DISABLE_HIP", "1")
+    ref.train()
+    out_r = ref(ids, labels=labels)
+    out_r.loss.backward()
+    monkeypatch.delenv("SFTAMD_DISABLE_HIP")
+    gref = {n: p.grad.float() for n, p in ref.named_parameters()}
+    errs, total_ref = {}, 0.0
+    for p, _, _, _ in eng.layout:
+        name = eng.param_names[id(p)]
+        g = p.main_grad.float()
+        errs[name] = ((g - gref[name]).norm() / (gref[name].norm() + 1e-12)).item()
+        total_ref += gref[name].pow(2).sum().item()
+    assert norm2 is not None
+    return tr, out.loss.item(), out_r.loss.item(), errs, norm2.item(), total_ref
+
+
+def _check_errors(errs, bounds):
+    """bounds: (substring, max relative error) pairs, first match wins — about 2x the maxima measured on MI355X."""
+    for name, e in errs.items():
+        lim = next(b for key, b in bounds if key in name)
+        assert e < lim, (name, e, lim)
+
+
+def test_default_path_smollm3_widths_vs_fp32_reference(monkeypatch):
+    cfg = _cfg()
+    tr, loss, loss_r, errs, norm2, total_ref = _run_vs_reference(cfg, monkeypatch)
+    _report("smollm3", errs, tr)
     # ---- which variants ran (the defaults of ops/fused.py and the C++ launchers at these shapes)
     assert tr.get("tn.rope.c11", 0) == 3 and tr.get("tn.rope.tail", 0) == 3, tr  # qkv + RoPE, 384-tile tail split
     assert tr.get("attn.fwd32", 0) == 4 and tr.get("attn.dkdv32", 0) == 4 and tr.get("attn.dq32", 0) == 4, tr
@@ -73,20 +120,25 @@ def test_default_path_smollm3_widths_vs_fp32_reference(monkeypatch):
     assert tr.get("dgrad.c13", 0) >= 5, tr  # gate_up (K = 22016) x 4 + lm_head: 4-wave ring
     assert "attn.dq3" not in tr, tr  # (the recompute path: past the dS^T budget only)
     # ---- numerics vs the fp32 reference path (same weights, PyTorch ops)
-    monkeypatch.setenv("SFTAMD_DISABLE_HIP", "1")
-    ref.train()
-    out_r = ref(ids, labels=labels)
-    out_r.loss.backward()
-    monkeypatch.delenv("SFTAMD_DISABLE_HIP")
-    assert abs(out.loss.item() - out_r.loss.item()) < 2e-2 * abs(out_r.loss.item())
-    gref = {n: p.grad.float() for n, p in ref.named_parameters()}
-    total_ref = 0.0
-    for p, _, _, _ in eng.layout:
-        name = eng.param_names[id(p)]
-        g = p.main_grad.float()
-        e = ((g - gref[name]).norm() / (gref[name].norm() + 1e-12)).item()
-        assert e < 5e-2, (name, e)
-        total_ref += gref[name].pow(2).sum().item()
+    assert abs(loss - loss_r) < 2e-2 * abs(loss_r)
+    _check_errors(errs, SMOLLM3_BOUNDS)
     # the clip norm from the wgrad-epilogue slots + the leftover pass == the reference gradient norm
-    assert norm2 is not None
-    assert abs(norm2.sqrt().item() - total_ref ** 0.5) < 3e-2 * total_ref ** 0.5
+    assert abs(norm2 ** 0.5 - total_ref ** 0.5) < 3e-2 * total_ref ** 0.5
+
+
+def test_default_path_llama3_8b_widths_vs_fp32_reference(monkeypatch):
+    """BASELINE config 5's architecture at its real widths (hidden 4096, intermediate 14336 -> gate_up 28672, 32 q / 8
+    kv heads x 128, every layer RoPE, untied head), 4 layers, 8192-token vocabulary, 16 x 512 tokens: the default
+    dispatch at those shapes and every gradient vs the fp32 reference."""
+    from llm_fine_tune_distributed_amd.models.config import llama3_8b
+    cfg = llama3_8b()
+    cfg.num_hidden_layers = 4
+    cfg.vocab_size = 8192
+    cfg.eos_token_id = 2
+    tr, loss, loss_r, errs, norm2, total_ref = _run_vs_reference(cfg, monkeypatch)
+    _report("llama3_8b", errs, tr)
+    assert tr.get("attn.fwd32", 0) == 4 and tr.get("attn.dkdv32", 0) == 4 and tr.get("attn.dq32", 0) == 4, tr
+    assert tr.get("attn.bwd_rope_epi", 0) == 4, tr  # every Llama layer is a RoPE layer
+    assert abs(loss - loss_r) < 2e-2 * abs(loss_r)
+    _check_errors(errs, LLAMA_BOUNDS)
+    assert abs(norm2 ** 0.5 - total_ref ** 0.5) < 3e-2 * total_ref ** 0.5

@@ -539,6 +539,22 @@ def test_lora_fwd_bwd_kernels(K, R, p):
     assert torch.allclose(o2, sB[R - 16:R, n_out // 2:].t())
 
 
+@pytest.mark.parametrize("T,n,R,ldb", [(8192, 22016, 32, 2176), (256, 2048, 16, 2048 + 128), (300, 3072, 48, 2176),
+                                        (64, 11008 // 8 * 8, 64, 11008 + 128), (33, 520, 32, 600)])
+def test_lora_dxa_vs_fp32(T, n, R, ldb):
+    """dxa = s dy Bc (the adapter-dx thin GEMM, csrc/lora.hip dxa_kernel): Bc a column slice of a wider weight, ragged
+    token counts (T % 32 != 0) and reductions that are not a multiple of the 256-column chunk, every element checked."""
+    torch.manual_seed(3)
+    dy = torch.randn(T, n, device=DEV, dtype=torch.bfloat16)
+    wide = torch.randn(n, ldb, device=DEV, dtype=torch.bfloat16)
+    bc = wide[:, ldb - R - 8:ldb - 8] if ldb - R - 8 >= 0 else wide[:, :R]
+    bc = bc if bc.data_ptr() % 16 == 0 else wide[:, :R]
+    got = _ext.ops().lora_dxa(dy, bc, 0.5)
+    want = 0.5 * (dy.float() @ bc.float())
+    assert got.shape == (T, R)
+    assert rel_err(got, want) < 5e-3 and _elem_ok(got, want)
+
+
 @pytest.mark.parametrize("cfg", [0, 2, 5, 6, 11])
 @pytest.mark.parametrize("M,N,K", [(256, 256, 64), (512, 512, 128), (256, 512, 192), (512, 768, 256), (768, 512, 2112),
                                    (2048, 3072, 320)])
@@ -732,7 +748,7 @@ def test_dgrad_gemm_wave_tail_split(M, K, N, swiglu, monkeypatch):
     assert rel_err(res["2"], want) < 1e-2
 
 
-@pytest.mark.parametrize("M,K,N", [(256, 256, 256), (512, 2048, 512), (256, 64, 768)])
+@pytest.mark.parametrize("M,K,N", [(256, 256, 256), (512, 2048, 512), (256, 64, 768), (2048, 2048, 2816)])
 def test_dgrad_gemm_swiglu_bwd(M, K, N):
     """Down-projection dgrad with the SwiGLU backward fused into the epilogue == swiglu_bwd(dy @ w, gu) in fp32."""
     torch.manual_seed(1)

@@ -110,3 +110,31 @@ def test_saved_model_loads_in_transformers(tmp_path, mt):
         ho = hm(input_ids=ids).logits
         mo = m(ids, return_logits=True).logits
     assert (ho.reshape(-1, cfg.vocab_size) - mo).abs().max() < 1e-4
+
+
+def test_unit_loss_grad_skips_only_the_identity_scale():
+    """ops.unit_loss_grad (the trainer's ``out.loss.backward()``): the LM head skips its d(loss) scale passes — the
+    gradients equal the general path's at d(loss) = 1; a scaled loss outside the context is still scaled."""
+    import torch
+    from llm_fine_tune_distributed_amd import ops
+    torch.manual_seed(0)
+    h = torch.randn(8, 16, requires_grad=True)
+    w = torch.randn(32, 16, requires_grad=True)
+    labels = torch.randint(0, 32, (8,))
+    inv = torch.tensor([1.0 / 8])
+
+    def grads(scale, unit):
+        h.grad = w.grad = None
+        loss, _ = ops.lm_head_cross_entropy(h, w, labels, inv)
+        if unit:
+            with ops.unit_loss_grad():
+                loss.backward()
+        else:
+            (loss * scale).backward()
+        return h.grad.clone(), w.grad.clone()
+
+    g1, w1 = grads(1.0, False)
+    gu, wu = grads(1.0, True)
+    g3, w3 = grads(3.0, False)
+    assert torch.allclose(g1, gu) and torch.allclose(w1, wu)
+    assert torch.allclose(g3, 3 * g1, rtol=1e-5) and torch.allclose(w3, 3 * w1, rtol=1e-5)

@@ -1,0 +1,23 @@
+#!/bin/bash
+# round 5: LoRA dxa kernel (tests + microbench), LoRA trainer overlap test, default-path tests with the tightened bounds,
+# LoRA bench (wide GEMM cfg 164 vs 61), Llama-3-8B bench
+cd $GRAFT_REPO_ROOT
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+timeout -k 10 400 python -u -m pytest -x -q --timeout 300 --timeout-method thread tests/test_kernels_gpu.py tests/test_trainer_gpu.py tests/test_default_path_gpu.py -m gpu -k "dxa or lora_overlap or default_path or overlap_matches" > gpurun_out/r5_06_tests.log 2>&1 || { tail -40 gpurun_out/r5_06_tests.log; exit 1; }
+tail -1 gpurun_out/r5_06_tests.log
+timeout -k 10 200 python -u tools/bench_lora_dxa.py > gpurun_out/r5_06_dxa.log 2>&1 || { tail -20 gpurun_out/r5_06_dxa.log; exit 1; }
+cat gpurun_out/r5_06_dxa.log
+run() {
+  local n=$1; shift
+  local envs=()
+  while [ "$1" != "--" ]; do envs+=("$1"); shift; done; shift
+  env "${envs[@]}" timeout -k 10 300 python -u bench.py --steps 20 --warmup 5 "$@" > gpurun_out/r5_06_$n.log 2>&1 || { tail -20 gpurun_out/r5_06_$n.log; exit 1; }
+  echo "$n $(grep -o '"value": [0-9.]*' gpurun_out/r5_06_$n.log)"
+}
+for r in 1 2; do
+  run lora164_$r X=1 -- --freeze-policy lora
+  run lora61_$r SFTAMD_LORA_FWD_CFG=61 -- --freeze-policy lora
+done
+run llama X=1 -- --model llama3-8b --steps 10 --warmup 3
+grep '"metric"' gpurun_out/r5_06_llama.log | cut -c1-400
