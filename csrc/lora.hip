@@ -538,32 +538,38 @@ at::Tensor lora_bwd_dx(const at::Tensor& base, const at::Tensor& dxa, const at::
 }
 
 // dxa [T, R] = s * dy [T, n] . Bc [n, R]  (Bc = the adapters' B columns of the wide weight W', row stride ldb): the
-// adapter-dx projection, a thin-N GEMM that is one streaming pass over dy (360 MB for the gate_up projection of a
-// 16 x 512-token step) — it replaced torch.addmm on hipBLASLt. Workgroup = 32 token rows x all R columns, dy streamed in
-// 256-column chunks: every wave instruction loads 2 rows x 512 contiguous bytes into registers, the chunk goes to an LDS
-// tile [32][256 + 8]; the chunk's Bc rows [256][R] are loaded 4 n-rows x 8 columns per thread and written TRANSPOSED into
-// an LDS tile [R][256 + 8] (ds_write_b64 of 4 n-values), so both MFMA operands are plain row reads with k = n
-// contiguous (ds_read_b128). Wave w owns columns 64 w .. 64 w + 63 of each chunk (2 k-steps of 32, every row and R
-// fragment); the 4 waves' fp32 partials are summed through LDS at the end. The next chunk's global loads are issued
-// before this chunk's MFMAs.
+// adapter-dx projection, a thin-N GEMM that is one streaming pass over dy. Workgroup = 32 token rows x all R columns,
+// dy streamed in chunks of CH = 256 CW columns: every wave instruction loads 32 CW contiguous 16-byte pieces of one row
+// into registers, the chunk goes to an LDS tile [32][CH + 8]; the chunk's Bc rows [CH][R] are loaded 4 n-rows x 8
+// columns per thread and written TRANSPOSED into an LDS tile [R][CH + 8] (ds_write_b64 of 4 n-values), so both MFMA
+// operands are plain row reads with k = n contiguous (ds_read_b128). Wave w owns columns CH/4 w .. of each chunk (every
+// row and R fragment); the 4 waves' fp32 partials are summed through LDS (aliasing the tiles) at the end. The next
+// chunk's global loads are issued before this chunk's MFMAs. Faster than hipBLASLt's addmm for the 2048 / 3072-column
+// dy of the o / down / qkv adapters (13 / 13 / 24 vs 26 / 25 / 34 us at 8192 tokens); on gate_up's 22016 columns
+// every workgroup re-reads all of Bc in 64-byte row pieces, as many bytes as its dy rows, and addmm stays ahead (CW = 1:
+// 133 vs 107 us; CW = 2 was slower still, 150 us): ops/fused.py routes only narrow dy here (profiles/r5_lora.md).
 namespace lora {
-template <int RF>  // R = 16 RF
+template <int RF, int CW>  // R = 16 RF, chunk = 256 CW columns
 __global__ __launch_bounds__(256) void dxa_kernel(const u16* __restrict__ dy, long ldy, const u16* __restrict__ Bc,
                                                   long ldb, u16* __restrict__ out, long T, int n, float s) {
-  constexpr int R = 16 * RF, CH = 256, LD = CH + 8;
+  constexpr int R = 16 * RF, CH = 256 * CW, LD = CH + 8;
+  constexpr int XP = 4 * CW;              // dy pieces per thread per chunk
+  constexpr int TPR = CH / 8, RPP = 256 / TPR;  // threads per row, rows per pass
   constexpr int BT = R * CH / 32;         // B tasks per chunk (4 n-rows x 8 columns each)
   constexpr int BPT = (BT + 255) / 256;   // per thread
-  __shared__ __attribute__((aligned(16))) u16 xs[32][LD];
-  __shared__ __attribute__((aligned(16))) u16 bs[R][LD];
-  __shared__ __attribute__((aligned(16))) float red[4][32][R + 4];
+  constexpr int TILES = (32 + R) * LD * 2, RED = 4 * 32 * (R + 4) * 4;
+  __shared__ __attribute__((aligned(16))) char smem[TILES > RED ? TILES : RED];
+  u16 (*xs)[LD] = reinterpret_cast<u16 (*)[LD]>(smem);
+  u16 (*bs)[LD] = reinterpret_cast<u16 (*)[LD]>(smem + 32 * LD * 2);
+  float (*red)[32][R + 4] = reinterpret_cast<float (*)[32][R + 4]>(smem);
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, g = lane >> 4, ii = lane & 15;
   const long t0 = (long)blockIdx.x * 32;
-  const int xr = tid >> 5, xc = 8 * (tid & 31);  // dy piece: rows xr + 8 q, columns xc .. xc + 7 of the chunk
-  uint4 xv[4], bv[BPT][4];
+  const int xr = tid / TPR, xc = 8 * (tid % TPR);  // dy piece: rows xr + RPP q, columns xc .. xc + 7 of the chunk
+  uint4 xv[XP], bv[BPT][4];
   auto load = [&](int c0) {
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const long t = t0 + xr + 8 * q;
+    for (int q = 0; q < XP; ++q) {
+      const long t = t0 + xr + RPP * q;
       xv[q] = (t < T && c0 + xc < n) ? *(const uint4*)(dy + t * ldy + c0 + xc) : make_uint4(0, 0, 0, 0);
     }
 #pragma unroll
@@ -585,7 +591,7 @@ __global__ __launch_bounds__(256) void dxa_kernel(const u16* __restrict__ dy, lo
   for (int c0 = 0; c0 < n; c0 += CH) {
     __syncthreads();  // the previous chunk's reads are done
 #pragma unroll
-    for (int q = 0; q < 4; ++q) *(uint4*)&xs[xr + 8 * q][xc] = xv[q];
+    for (int q = 0; q < XP; ++q) *(uint4*)&xs[xr + RPP * q][xc] = xv[q];
 #pragma unroll
     for (int u = 0; u < BPT; ++u) {
       const int task = tid + 256 * u, ng = task / (R / 8), rg = task - ng * (R / 8);
@@ -606,8 +612,8 @@ __global__ __launch_bounds__(256) void dxa_kernel(const u16* __restrict__ dy, lo
     __syncthreads();
     if (c0 + CH < n) load(c0 + CH);  // the next chunk's loads fly under this chunk's MFMAs
 #pragma unroll
-    for (int ks = 0; ks < 2; ++ks) {
-      const int kc = 64 * w + 32 * ks + 8 * g;
+    for (int ks = 0; ks < 2 * CW; ++ks) {
+      const int kc = (CH / 4) * w + 32 * ks + 8 * g;
       bf16x8 a[2], b[RF];
 #pragma unroll
       for (int i = 0; i < 2; ++i) a[i] = *(const bf16x8*)&xs[16 * i + ii][kc];
@@ -619,6 +625,7 @@ __global__ __launch_bounds__(256) void dxa_kernel(const u16* __restrict__ dy, lo
         for (int j = 0; j < RF; ++j) acc[i][j] = mfma(a[i], b[j], acc[i][j]);
     }
   }
+  __syncthreads();  // the tiles are reused for the partial sums
   // C layout: lane (g, ii) holds rows 16 i + 4 g + e, column 16 j + ii
 #pragma unroll
   for (int i = 0; i < 2; ++i)
@@ -657,7 +664,7 @@ at::Tensor lora_dxa(const at::Tensor& dy, const at::Tensor& Bc, double s) {
   if (T == 0) return out;
   const unsigned grid = (unsigned)((T + 31) / 32);
 #define LORA_DXA(RF)                                                                                              \
-  lora::dxa_kernel<RF><<<grid, 256, 0, cur_stream()>>>((const u16*)dy.data_ptr(), dy.stride(0),                   \
+  lora::dxa_kernel<RF, 1><<<grid, 256, 0, cur_stream()>>>((const u16*)dy.data_ptr(), dy.stride(0),                \
       (const u16*)Bc.data_ptr(), Bc.stride(0), (u16*)out.data_ptr(), T, n, (float)s)
   switch (R / 16) {
     case 1: LORA_DXA(1); break;

@@ -162,9 +162,13 @@ def _as_output(y2d: torch.Tensor, lead) -> torch.Tensor:
     return y2d if tuple(y2d.shape) == shape else torch.ops.aten._unsafe_view(y2d, shape)
 
 
-# plain projection forwards whose output width N is listed here run on the row-contiguous kernel (reduction <= 4096)
-_FWD_HIP_N = {int(v) for v in os.environ.get("SFTAMD_FWD_HIP_N", "").split(",") if v.strip()}
-_ROWC_CFG = int(os.environ.get("SFTAMD_TN_CFG", "61"))  # the row-contiguous persistent kernel (61 = nt stores)
+# Plain projection forwards: hipBLASLt where TunableOp holds a measured selection for the exact shape (the bench's
+# 16 x 512 tokens: it stays 1 % ahead of the hand-written kernel in the step), the row-contiguous persistent kernel
+# everywhere else — the ragged padding-free batches of real data (M ~ 10k, a new M almost every step) and eval batches,
+# where hipBLASLt's default heuristics pick split-K kernels that took 36 % of the recipe's kernel time
+# (profiles/r5_recipe.md). SFTAMD_FWD_GEMM: auto (this rule) | blas | hip.
+_FWD_GEMM = os.environ.get("SFTAMD_FWD_GEMM", "auto")
+_ROWC_CFG = int(os.environ.get("SFTAMD_TN_CFG", "60"))  # row-contiguous persistent kernel (60: cacheable stores)
 
 
 def _rowc_ok(x2d: torch.Tensor, w: torch.Tensor) -> bool:
@@ -175,10 +179,19 @@ def _rowc_ok(x2d: torch.Tensor, w: torch.Tensor) -> bool:
             and w.is_contiguous() and x2d.data_ptr() % 16 == 0 and w.data_ptr() % 16 == 0)
 
 
+def _fwd_on_hip(x2d: torch.Tensor, w: torch.Tensor) -> bool:
+    if _FWD_GEMM == "blas" or not _rowc_ok(x2d, w):
+        return False
+    if _FWD_GEMM == "hip":
+        return True
+    from ..utils.gemm_tuning import tuned_tn_shapes
+    return (w.shape[0], x2d.shape[0], x2d.shape[1]) not in tuned_tn_shapes() or x2d.stride(0) != x2d.shape[1]
+
+
 def fwd_gemm(x2d: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
-    """y = x2d @ w^T for a plain projection forward (hipBLASLt, or the row-contiguous HIP kernel for the output widths
-    listed in SFTAMD_FWD_HIP_N)."""
-    if w.shape[0] in _FWD_HIP_N and w.shape[1] <= 4096 and _rowc_ok(x2d, w):
+    """y = x2d @ w^T for a plain projection forward: hipBLASLt for shapes with a TunableOp selection, the
+    row-contiguous HIP kernel (csrc/gemm_tn.hip tn6) otherwise (see _FWD_GEMM)."""
+    if _fwd_on_hip(x2d, w):
         return _ext.ops().gemm_tn(x2d, w, _ROWC_CFG)
     return torch.nn.functional.linear(x2d, w)
 
@@ -951,7 +964,10 @@ def _lora_dxa(dy2d: torch.Tensor, bc: torch.Tensor, s: float) -> torch.Tensor:
     """s dy Bc for the adapters' B columns Bc [n, R] of the wide weight (a thin-N GEMM: the HIP streaming kernel where
     the layout allows, torch.addmm with the scale as alpha otherwise)."""
     R = bc.shape[1]
-    if (_ext.use_hip(dy2d) and dy2d.dtype == torch.bfloat16 and bc.dtype == torch.bfloat16 and R % 16 == 0
+    # wide dy (gate_up's 22016 columns): every workgroup re-reads all of Bc from L2 in 64-B row pieces, as many bytes
+    # as its dy rows — hipBLASLt's addmm is faster there (107 vs 133 us, profiles/r5_lora.md)
+    if (dy2d.shape[1] <= 4096 and _ext.use_hip(dy2d) and dy2d.dtype == torch.bfloat16 and bc.dtype == torch.bfloat16
+            and R % 16 == 0
             and 16 <= R <= 64 and dy2d.stride(1) == 1 and dy2d.stride(0) % 8 == 0 and dy2d.data_ptr() % 16 == 0
             and dy2d.shape[1] % 8 == 0 and bc.stride(1) == 1 and bc.stride(0) % 8 == 0 and bc.data_ptr() % 16 == 0):
         return _ext.ops().lora_dxa(dy2d, bc, float(s))
@@ -1071,14 +1087,16 @@ def _wide_sync_ok(wide, As, Bs) -> bool:
 
 def _lora_gemm(X: torch.Tensor, wide: torch.Tensor) -> torch.Tensor:
     """The widened LoRA forward GEMM X' W'^T on the hand-written persistent kernel (113.0 samples/s vs 112.9 with
-    hipBLASLt, profiles/r4_lora.md)."""
+    hipBLASLt, profiles/r4_lora.md; the row-contiguous store epilogue since round 5, profiles/r5_gemm_fwd.md)."""
     if (_ext.use_hip(X) and X.shape[0] % 256 == 0 and X.shape[1] % 128 == 0
             and wide.shape[0] % 256 == 0 and wide.is_contiguous() and X.is_contiguous()):
         return _ext.ops().gemm_tn(X, wide, _LORA_FWD_CFG)
     return torch.mm(X, wide.t())
 
 
-_LORA_FWD_CFG = int(os.environ.get("SFTAMD_LORA_FWD_CFG", "164"))  # persistent 4-wave kernel (csrc/gemm_tn.hip)
+# the persistent 4-wave kernel with the row-contiguous nt store epilogue (csrc/gemm_tn.hip cfg 61): 131.3 vs 130.2
+# samples/s for cfg 164 (r5_run08, one box)
+_LORA_FWD_CFG = int(os.environ.get("SFTAMD_LORA_FWD_CFG", "61"))
 
 
 def _lora_wide_prep(x, wide, K, scaling, p, seed, meta, ab, swiglu=False):

@@ -34,6 +34,37 @@ def enable_tuned_gemms(path: Optional[str] = None, tune: bool = False, verbose: 
     ok = False
     if os.path.exists(path):
         ok = bool(tun.read_file(path))
+    _TUNED[0] = _tuned_tn(path) if ok else frozenset()
     if verbose:
         print(f"[gemm] TunableOp enabled (tuning={tune}) selections={path if ok else 'none'}", flush=True)
     return ok
+
+
+_TUNED = [frozenset()]
+
+
+def _tuned_tn(path: str) -> frozenset:
+    """(N, M, K) of every contiguous TN GEMM (y[M, N] = x[M, K] W[N, K]^T, torch's column-major naming
+    ``tn_N_M_K_ld_K_K_N``) with a selection in the TunableOp file."""
+    out = set()
+    try:
+        with open(path) as f:
+            for line in f:
+                parts = line.split(",")
+                if len(parts) < 2 or not parts[1].startswith("tn_"):
+                    continue
+                f_ = parts[1].split("_")  # tn, N, M, K, ld, lda, ldb, ldc
+                try:
+                    n, m, k, lda, ldb, ldc = (int(f_[i]) for i in (1, 2, 3, 5, 6, 7))
+                except (ValueError, IndexError):
+                    continue
+                if lda == k and ldb == k and ldc == n:
+                    out.add((n, m, k))
+    except OSError:
+        pass
+    return frozenset(out)
+
+
+def tuned_tn_shapes() -> frozenset:
+    """The forward-projection GEMM shapes hipBLASLt has a TunableOp selection for (empty until enable_tuned_gemms)."""
+    return _TUNED[0]

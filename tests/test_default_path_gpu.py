@@ -52,7 +52,9 @@ def _run_vs_reference(cfg, monkeypatch, B=16, T=512):
     """Default-path fwd + bwd (dispatch trace on) and the fp32 PyTorch reference with the same weights.
     Returns (trace, loss, ref loss, {param: relative grad error}, fused clip norm^2, reference norm^2)."""
     from llm_fine_tune_distributed_amd.parallel.ddp import DDPEngine
+    from llm_fine_tune_distributed_amd.utils.gemm_tuning import enable_tuned_gemms
     assert _ext.load(), _ext.load_error()
+    enable_tuned_gemms()  # as SFTTrainer does (SFTConfig.gemm_tuning): the shipped hipBLASLt selections
     torch.manual_seed(0)
     m = build_model(cfg, device="cuda", dtype=torch.bfloat16, seed=11)
     ref = build_model(cfg, device="cuda", dtype=torch.float32, seed=11)
@@ -108,6 +110,9 @@ def test_default_path_smollm3_widths_vs_fp32_reference(monkeypatch):
     _report("smollm3", errs, tr)
     # ---- which variants ran (the defaults of ops/fused.py and the C++ launchers at these shapes)
     assert tr.get("tn.rope.c11", 0) == 3 and tr.get("tn.rope.tail", 0) == 3, tr  # qkv + RoPE, 384-tile tail split
+    # plain forwards: hipBLASLt for the shapes with a TunableOp selection (SmolLM3 widths at 8192 tokens), the
+    # row-contiguous kernel for the rest — here only the lm_head of the reduced 8192-token vocabulary
+    assert tr.get("tn.c60", 0) == 1, tr
     assert tr.get("attn.fwd32", 0) == 4 and tr.get("attn.dkdv32", 0) == 4 and tr.get("attn.dq32", 0) == 4, tr
     assert tr.get("attn.bwd_rope_epi", 0) == 3, tr  # inverse RoPE in the dq / dK epilogues of the 3 RoPE layers
     # wgrad: the 4-wave ring (csrc/gemm_4w.hip) for gate_up and, hybrid split-K, down_proj; the 4-wave kernel split 2
@@ -139,6 +144,15 @@ def test_default_path_llama3_8b_widths_vs_fp32_reference(monkeypatch):
     _report("llama3_8b", errs, tr)
     assert tr.get("attn.fwd32", 0) == 4 and tr.get("attn.dkdv32", 0) == 4 and tr.get("attn.dq32", 0) == 4, tr
     assert tr.get("attn.bwd_rope_epi", 0) == 4, tr  # every Llama layer is a RoPE layer
+    # qkv + RoPE: 32 x 24 = 768 tiles = 3 whole rounds, so no 256 x 128 tail launch
+    assert tr.get("tn.rope.c11", 0) == 4 and "tn.rope.tail" not in tr, tr
+    # no Llama shape has a TunableOp selection: o / gate_up / down of the 4 layers + lm_head on the row-contiguous kernel
+    assert tr.get("tn.c60", 0) == 13, tr
+    for c in (13, 1213, 9):  # wgrad: gate_up / down / lm_head (4-wave ring), qkv (hybrid split-K), o (8-wave ring)
+        assert tr.get(f"wgrad.c{c}", 0) > 0, (c, tr)
+    assert tr.get("wgrad.norm_slots", 0) > 0, tr
+    assert tr.get("dgrad.swiglu.c7", 0) == 4, tr  # down dgrad + SwiGLU bwd: 56 x 32 tiles = 7 whole rounds
+    assert tr.get("dgrad.c13", 0) >= 5 and tr.get("dgrad.c12", 0) > 0, tr  # gate_up (K = 28672) + lm_head; qkv / o
     assert abs(loss - loss_r) < 2e-2 * abs(loss_r)
     _check_errors(errs, LLAMA_BOUNDS)
     assert abs(norm2 ** 0.5 - total_ref ** 0.5) < 3e-2 * total_ref ** 0.5

@@ -540,7 +540,8 @@ def test_lora_fwd_bwd_kernels(K, R, p):
 
 
 @pytest.mark.parametrize("T,n,R,ldb", [(8192, 22016, 32, 2176), (256, 2048, 16, 2048 + 128), (300, 3072, 48, 2176),
-                                        (64, 11008 // 8 * 8, 64, 11008 + 128), (33, 520, 32, 600)])
+                                        (64, 11008 // 8 * 8, 64, 11008 + 128), (33, 520, 32, 600),
+                                        (96, 4104, 16, 2176)])
 def test_lora_dxa_vs_fp32(T, n, R, ldb):
     """dxa = s dy Bc (the adapter-dx thin GEMM, csrc/lora.hip dxa_kernel): Bc a column slice of a wider weight, ragged
     token counts (T % 32 != 0) and reductions that are not a multiple of the 256-column chunk, every element checked."""

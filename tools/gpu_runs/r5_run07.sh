@@ -11,7 +11,7 @@ run() {
 }
 for r in 1 2; do
   run base$r X=1
-  run fwd$r SFTAMD_FWD_HIP_N=22016,2048,3072
+  run fwd$r SFTAMD_TN_CFG=60 SFTAMD_FWD_HIP_N=22016,2048,3072
 done
 timeout -k 10 600 rocprofv3 --kernel-trace --stats -d /tmp/prof07 -o run -- python bench.py --recipe --steps 40 --warmup 0 > gpurun_out/r5_07_p.log 2>&1 || { tail -20 gpurun_out/r5_07_p.log; exit 1; }
 db=$(ls /tmp/prof07/*/run_results.db /tmp/prof07/run_results.db 2>/dev/null | head -1)
