@@ -72,16 +72,18 @@ constexpr unsigned waitcnt_imm(int vm, int lgkm) {  // gfx9: vmcnt[3:0] expcnt[6
 template <int BM, int BN, int WM, int WN, int NS_>
 struct Cfg {
   static constexpr int NS = NS_;
+  static constexpr int NW = WM * WN;                // 8 waves, or 4 (two workgroups per CU: cfg 8)
   static constexpr int TM = BM / WM, TN = BN / WN;  // wave tile: TM n x TN m
   static constexpr int FM = TM / 16, FN = TN / 16;
   static constexpr int IA = BM / 128;               // A images per stage
+  static constexpr int QA = 8 / NW;                 // A pieces (4 rows x 256 B) per image and wave
   static constexpr int STAGE_A = IA * AIMG, STAGE = STAGE_A + BN * BROWB;
-  static constexpr int PB = BN / 128;               // B pieces (16 rows x 64 B) per wave per stage
-  static constexpr int PPW = IA + PB;               // DMA pieces per wave per stage
+  static constexpr int PB = BN / (16 * NW);         // B pieces (16 rows x 64 B) per wave per stage
+  static constexpr int PPW = IA * QA + PB;          // DMA pieces per wave per stage
   static constexpr int EPI_LD = TM + 4;
-  static constexpr int EPI = 8 * 16 * EPI_LD * 4;
+  static constexpr int EPI = NW * 16 * EPI_LD * 4;
   static constexpr int LDS = (NS * STAGE > EPI) ? NS * STAGE : EPI;
-  static_assert(WM * WN == 8 && BM % 128 == 0 && BN % 128 == 0 && FM >= PPW, "config");
+  static_assert((NW == 8 || NW == 4) && BM % 128 == 0 && BN % (16 * NW) == 0 && FM >= PPW, "config");
   static_assert(LDS <= 160 * 1024, "LDS budget");
 };
 
@@ -105,11 +107,12 @@ struct Stager {
   // Past the last step the same rows are fetched again into a slot nobody reads, so every step issues
   // exactly PPW DMAs and the counted waits stay compile-time constants (see gemm_wgrad.hip).
   __device__ __forceinline__ void piece(char* buf, int j) {
-    if (j < G::IA) {
-      glds16(pa + j * 128, buf + j * AIMG + w * 1024);
+    if (j < G::IA * G::QA) {  // A image j % IA, rows 4 (w + NW q) .. (the swizzle depends on row & 15 only)
+      const int img = j % G::IA, q = j / G::IA;
+      glds16(pa + img * 128 + (long)(4 * G::NW * q) * lda, buf + img * AIMG + (w + G::NW * q) * 1024);
     } else {
-      const int jj = j - G::IA;  // B piece w + 8 jj: rows 16 (w + 8 jj) ..
-      glds16(pb + (long)(128 * jj) * ldb, buf + G::STAGE_A + (w + 8 * jj) * 1024);
+      const int jj = j - G::IA * G::QA;  // B piece w + NW jj: rows 16 (w + NW jj) ..
+      glds16(pb + (long)(16 * G::NW * jj) * ldb, buf + G::STAGE_A + (w + G::NW * jj) * 1024);
     }
   }
   __device__ __forceinline__ void advance() {
@@ -286,7 +289,7 @@ __device__ __forceinline__ void epilogue(char* smem, f32x4 (&acc)[G::FM][G::FN],
 }
 
 template <int BM, int BN, int WM, int WN, int NS, int EPI, int OCC = 1, bool SCHED = true>
-__global__ void __launch_bounds__(NT, OCC) dgrad_kernel(const u16* __restrict__ dY, const u16* __restrict__ W, int K,
+__global__ void __launch_bounds__(WM * WN * 64, OCC) dgrad_kernel(const u16* __restrict__ dY, const u16* __restrict__ W, int K,
                                                         long ldd, long ldw, int nbn, int nbm, int group, EpiArgs ea) {
   using G = Cfg<BM, BN, WM, WN, NS>;
   __shared__ __attribute__((aligned(16))) char smem[G::LDS];
@@ -506,7 +509,7 @@ template <int BM, int BN, int WM, int WN, int NS, int EPI, int OCC = 1, bool SCH
 void launch(const at::Tensor& dy, const at::Tensor& w, const EpiArgs& ea) {
   const int M = dy.size(0), K = dy.size(1), N = w.size(1);
   const int nbn = N / BM, nbm = M / BN;
-  dgrad_kernel<BM, BN, WM, WN, NS, EPI, OCC, SCHED><<<nbn * nbm, NT, 0, cur_stream()>>>(
+  dgrad_kernel<BM, BN, WM, WN, NS, EPI, OCC, SCHED><<<nbn * nbm, WM * WN * 64, 0, cur_stream()>>>(
       (const u16*)dy.data_ptr(), (const u16*)w.data_ptr(), K, dy.stride(0), w.stride(0), nbn, nbm,
       std::min(group_n(), nbn), ea);
   SFT_LAUNCH_CHECK();
@@ -542,7 +545,7 @@ at::Tensor dgrad_gemm(const at::Tensor& dy, const at::Tensor& w, const c10::opti
   SFT_CHECK(cfg != 7 || K % 64 == 0, "dgrad_gemm cfg 7 (BK 64): K multiple of 64");
   SFT_CHECK((cfg != 12 && cfg != 13) || K % 128 == 0, "dgrad_gemm cfg 12 / 13 (4-wave): K multiple of 128");
   SFT_CHECK(M % 128 == 0 && N % 256 == 0 && K % 32 == 0 && K >= 32, "dgrad_gemm: M multiple of 128 (256 for cfg 0/1), N of 256, K of 32");
-  SFT_CHECK(cfg == 2 || cfg == 3 || M % 256 == 0, "dgrad_gemm: 256 x 256 tiles need M % 256 == 0");
+  SFT_CHECK(cfg == 2 || cfg == 3 || cfg == 8 || M % 256 == 0, "dgrad_gemm: 256 x 256 tiles need M % 256 == 0");
   SFT_CHECK(dy.stride(0) % 8 == 0 && w.stride(0) % 8 == 0 && (uintptr_t)dy.data_ptr() % 16 == 0 &&
                 (uintptr_t)w.data_ptr() % 16 == 0,
             "dgrad_gemm: 16-byte aligned rows");
@@ -580,6 +583,11 @@ at::Tensor dgrad_gemm(const at::Tensor& dy, const at::Tensor& w, const c10::opti
       case 5: dgrad::launch<256, 256, 2, 4, 3, E, 1, false>(dy, wv, e); break;  // no sched_group_barrier pinning
       case 6: dgrad::launch<256, 256, 2, 4, 4, E, 1, false>(dy, wv, e); break;
       case 7: dgrad::launch2<256, 256, 2, 4, E>(dy, wv, e); break;
+      // 8: 4-wave workgroups of 256 n x 128 m (128 x 64 per wave), 3 x 24 KB stages: two workgroups per CU, so one's
+      // SwiGLU-backward epilogue (gate / up reads, dgu writes) can run under the other's main loop. Measured
+      // (profiles/r5_dgrad.md): 0.411 vs 0.416 ms for cfg 7 with the SwiGLU epilogue, 0.325 vs 0.319 plain — the two
+      // co-resident workgroups stay nearly in step (a start stagger of half a tile moved it by +-1 %), so cfg 7 stays
+      case 8: dgrad::launch<256, 128, 2, 2, 3, E, 2>(dy, wv, e); break;
       case 12:  // 4-wave (csrc/gemm_4w.hip); 13: its 4-slot ring
       case 13: g4_dgrad(dy, wv, e.out, e.ldo, E == dgrad::EPI_SWIGLU_BWD ? e.gu : nullptr, e.N, c == 13); break;
       default: dgrad::launch<256, 256, 2, 4, 4, E>(dy, wv, e);
@@ -591,7 +599,7 @@ at::Tensor dgrad_gemm(const at::Tensor& dy, const at::Tensor& w, const c10::opti
   }();
   auto run = [&](auto epi) {
     const long nbn = N / 256, nbm = M / 256, tiles = nbn * nbm;
-    const bool full = cfg != 2 && cfg != 3;
+    const bool full = cfg != 2 && cfg != 3 && cfg != 8;
     long main_n = 0;
     if (full && tail_cfg >= 2 && tail_cfg <= 3 && tiles % 256 != 0 && 256 % nbm == 0) {
       main_n = tiles / 256 * (256 / nbm);                  // n-tiles of the whole rounds
@@ -609,7 +617,7 @@ at::Tensor dgrad_gemm(const at::Tensor& dy, const at::Tensor& w, const c10::opti
     if (et.gu != nullptr) et.gu = ea.gu + n_split;
     run1(epi, tail_cfg, w.narrow(1, n_split, N - n_split), et);
   };
-  if (cfg == 2 || cfg == 3) SFT_CHECK(M % 128 == 0, "dgrad_gemm: M multiple of 128");
+  if (cfg == 2 || cfg == 3 || cfg == 8) SFT_CHECK(M % 128 == 0, "dgrad_gemm: M multiple of 128");
   if (swiglu) run(std::integral_constant<int, dgrad::EPI_SWIGLU_BWD>());
   else run(std::integral_constant<int, dgrad::EPI_PLAIN>());
   return out;

@@ -234,8 +234,8 @@ void adamw_flat(at::Tensor param, const at::Tensor& grad, const c10::optional<at
   if (n == 0) return;
   // launch shape: 2 vectors per thread step, at most 2048 blocks (fewer blocks measured slower under the overlapped
   // forward: gpu_run49; one vector per step slower: gpu_run50)
-  const int unr = 2;
-  const long cap = 2048;
+  const int unr = (int)env_long("SFTAMD_ADAMW_UNR", 2);
+  const long cap = env_long("SFTAMD_ADAMW_BLOCKS", 2048);
   int grid = (int)std::min<long>(std::max<long>(1, (n / 8 + 256L * unr - 1) / (256L * unr)), cap);
   const float rbc1 = (float)(1.0 / bc1), rsbc2 = (float)(1.0 / std::sqrt(bc2));
   const bool has_master = master.has_value() && master->defined();
@@ -254,6 +254,7 @@ void adamw_flat(at::Tensor param, const at::Tensor& grad, const c10::optional<at
           rbc1, rsbc2, (float)(1.0 - beta1), (float)(1.0 - beta2), seed, (long)sr_offset);
     };
     if (unr == 1) launch(std::integral_constant<int, 1>());
+    else if (unr == 4) launch(std::integral_constant<int, 4>());
     else launch(std::integral_constant<int, 2>());
   };
   auto go2 = [&](auto ms, auto sr) {

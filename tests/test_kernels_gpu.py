@@ -710,7 +710,7 @@ def test_dgrad_gemm_plain(M, K, N, wpad):
     dy = torch.randn(M, K, device="cuda", dtype=torch.bfloat16)
     wfull = torch.randn(K, N + wpad, device="cuda", dtype=torch.bfloat16)
     w = wfull[:, :N]
-    for cfg in (0, 1, 2, 3, 5, 7) if K % 64 == 0 else (0, 1, 2, 3, 5):
+    for cfg in (0, 1, 2, 3, 5, 7, 8) if K % 64 == 0 else (0, 1, 2, 3, 5, 8):
         out = _ext.ops().dgrad_gemm(dy, w, None, cfg)
         want = dy.float() @ w.float()
         assert out.shape == (M, N)
@@ -759,6 +759,7 @@ def test_dgrad_gemm_swiglu_bwd(M, K, N):
     dgu = _ext.ops().dgrad_gemm(dy, w, gu, 0)
     assert torch.equal(_ext.ops().dgrad_gemm(dy, w, gu, 2), dgu)  # 256 x 128 tiles: same fp32 sums per element
     assert torch.equal(_ext.ops().dgrad_gemm(dy, w, gu, 7), dgu)  # BK 64: same k order within each 32-deep MFMA
+    assert torch.equal(_ext.ops().dgrad_gemm(dy, w, gu, 8), dgu)  # 4-wave 256 x 128, two workgroups per CU
     dact = dy.float() @ w.float()
     g, u = gu.float().chunk(2, dim=-1)
     s = torch.sigmoid(g)

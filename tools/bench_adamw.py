@@ -1,5 +1,9 @@
-"""AdamW flat-update bandwidth on 1x MI355X: launch shapes (SFTAMD_ADAM_UNR x SFTAMD_ADAM_BLOCKS), fp32 and bf16
-moments, stochastic rounding on (the training default). Interleaved rounds, median of 10 timed calls each."""
+"""AdamW flat-update bandwidth on 1x MI355X (csrc/optim.hip adamw_kernel): bf16 params + bf16 moments with stochastic
+rounding (the training default) against round-to-nearest (sr_seed = 0: same bytes, no hashing) and fp32 moments —
+whether the update is HBM- or VALU-bound. Interleaved rounds, median of 10 timed calls each.
+
+    python tools/bench_adamw.py [N elements, default 256M]
+"""
 import os
 import statistics
 import sys
@@ -11,7 +15,7 @@ from llm_fine_tune_distributed_amd.ops import _ext  # noqa: E402
 
 assert _ext.load(), _ext.load_error()
 ops = _ext.ops()
-n = int(os.environ.get("N", 256 * 1024 * 1024))
+n = int(sys.argv[1]) if len(sys.argv) > 1 else 256 * 1024 * 1024
 p = torch.randn(n, device="cuda").to(torch.bfloat16)
 g = torch.randn(n, device="cuda").to(torch.bfloat16)
 coef = torch.ones(1, device="cuda")
@@ -33,15 +37,17 @@ def t(fn, reps=10):
     return statistics.median(ts)
 
 
-cfgs = [(u, b) for u in ("1", "2") for b in ("1024", "2048", "4096", "8192")]
+# launch shapes (read per call by the launcher): vectors of 8 per thread step x block cap
+SHAPES = [(u, b) for u, b in (("2", "2048"), ("4", "1024"), ("4", "2048"), ("2", "4096"))]
 res = {}
 for rnd in range(3):
     for dt, (m, v) in state.items():
-        for u, b in cfgs:
-            os.environ["SFTAMD_ADAM_UNR"], os.environ["SFTAMD_ADAM_BLOCKS"] = u, b
-            ms = t(lambda: ops.adamw_flat(p, g, None, m, v, coef, 1e-4, 0.9, 0.999, 1e-8, 0.0, 0.1, 0.001, 1234, 0))
-            res.setdefault((str(dt), u, b), []).append(ms)
-for (dt, u, b), v in res.items():
+        for sr in (1234, 0):
+            for u, b in SHAPES:
+                os.environ["SFTAMD_ADAMW_UNR"], os.environ["SFTAMD_ADAMW_BLOCKS"] = u, b
+                ms = t(lambda: ops.adamw_flat(p, g, None, m, v, coef, 1e-4, 0.9, 0.999, 1e-8, 0.0, 0.1, 0.001, sr, 0))
+                res.setdefault((str(dt).replace("torch.", ""), "SR" if sr else "RN", u, b), []).append(ms)
+for (dt, sr, u, b), v in res.items():
     ms = statistics.median(v)
-    bpp = 22 if "float32" in dt else 14
-    print(f"{dt:15s} UNR {u} blocks {b:>5s}: {ms * 1e3:8.1f} us  {n * bpp / ms / 1e9:.2f} TB/s")
+    bpp = 22 if dt == "float32" else 14
+    print(f"moments {dt:8s} {sr} UNR {u} blocks {b:>5s}: {ms * 1e3:8.1f} us  {n * bpp / ms / 1e9:.2f} TB/s", flush=True)
