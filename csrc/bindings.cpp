@@ -67,6 +67,8 @@ TORCH_LIBRARY(sftamd, m) {
   m.def("lora_tsum(Tensor X, int K, Tensor S, float p, int seed) -> Tensor");
   m.def("lora_dxa(Tensor dy, Tensor Bc, float s) -> Tensor");
   m.def("lora_grad_out(Tensor sum, Tensor(a!)[] outs, int[] r0, int[] c0, bool tr, int[] accumulate) -> ()");
+  m.def("lora_grad_out2(Tensor sa, Tensor(a!)[] oa, int[] ra, int[] ca, bool ta, int[] aa, Tensor sb, "
+        "Tensor(b!)[] ob, int[] rb, int[] cb, bool tb, int[] ab) -> ()");
   m.def("copy2d_batch(Tensor desc, int max_elems) -> ()");
   m.def("embedding_bwd(Tensor dy, Tensor sorted_ids, Tensor perm, Tensor(a!) grad_weight) -> ()");
   // loss

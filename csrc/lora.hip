@@ -64,11 +64,11 @@ __device__ __forceinline__ f32x4 mfma(const bf16x8& a, const bf16x8& b, const f3
 // tools/bench_lora_kernels.py, r4_run29.)
 // SW: x is the SwiGLU input gu [T, 2K] (gate | up) and the widened activation is act = silu(gate) * up, rounded to bf16
 // as the SwiGLU kernel does (the LoRA MLP's down projection: no separate SwiGLU pass, no act tensor).
-template <int RF, bool SW = false>  // R = 16 * RF adapter columns
+template <int RF, bool SW = false, int NCH = 0>  // R = 16 * RF adapter columns; NCH > 0: K == 512 NCH
 __global__ __launch_bounds__(512) void fwd_kernel(const u16* __restrict__ x, const u16* __restrict__ A,
                                                   u16* __restrict__ X, u16* __restrict__ xd, long T, int K, long ldX,
                                                   float s, unsigned thresh, float dscale, unsigned seed, int drop) {
-  constexpr int R = 16 * RF, NW = 8, CK = 512, XP = CK + 8, NV = SW ? 2 : 1;
+  constexpr int R = 16 * RF, NW = 8, CK = 512, XP = CK + 8, NV = SW ? 2 : 1, DEP = NCH > 0 ? NCH : 1;
   __shared__ __attribute__((aligned(16))) u16 xs[2][16][XP];
   __shared__ float red[NW][16][R + 1];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
@@ -83,34 +83,65 @@ __global__ __launch_bounds__(512) void fwd_kernel(const u16* __restrict__ x, con
   f32x4 acc[RF];
 #pragma unroll
   for (int j = 0; j < RF; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  uint4 rw[2][NV];
-  auto load = [&](int k0) {
+  uint4 rw[DEP][2][NV];
+  auto load = [&](uint4 (&dst)[2][NV], int k0) {
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
       const int c = k0 + lc + 256 * h, cc = c < K ? c : 0;
-      rw[h][0] = *(const uint4*)(xrow + cc);
-      if constexpr (SW) rw[h][1] = *(const uint4*)(xrow + K + cc);
+      dst[h][0] = *(const uint4*)(xrow + cc);
+      if constexpr (SW) dst[h][1] = *(const uint4*)(xrow + K + cc);
     }
   };
-  const int nch = (K + CK - 1) / CK;
-  load(0);
+  // the wave's A_cat fragments of a chunk (rows 16 j + r, columns 64 w + 32 ks + 8 g): loaded one chunk ahead for
+  // R <= 32 (for R >= 48 the two copies pushed the kernel past 128 VGPRs: half the occupancy, or spills)
+  constexpr bool PFA = RF <= 2;
+  uint4 an[2][RF];
+  auto load_a = [&](int k0) {
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      const int kk = k0 + 64 * w + 32 * ks + 8 * g;
+#pragma unroll
+      for (int j = 0; j < RF; ++j)
+        an[ks][j] = kk < K ? *(const uint4*)(A + (long)(16 * j + r) * K + kk) : make_uint4(0, 0, 0, 0);
+    }
+  };
+  const int nch = NCH > 0 ? NCH : (K + CK - 1) / CK;
+  if constexpr (NCH > 0) {  // short rows: every chunk's loads in flight at once
+#pragma unroll
+    for (int c = 0; c < NCH; ++c) load(rw[c], c * CK);
+  } else {
+    load(rw[0], 0);
+  }
+  if constexpr (PFA) load_a(0);
+#pragma unroll
   for (int ch = 0; ch < nch; ++ch) {
     const int k0 = ch * CK;
+    const int sl = NCH > 0 ? ch : 0;
     uint4 v[2];
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
       if constexpr (SW) {
         float ga[8], up[8], o[8];
-        unpack8(rw[h][0], ga);
-        unpack8(rw[h][1], up);
+        unpack8(rw[sl][h][0], ga);
+        unpack8(rw[sl][h][1], up);
 #pragma unroll
         for (int i = 0; i < 8; ++i) o[i] = ga[i] / (1.f + __expf(-ga[i])) * up[i];
         v[h] = pack8(o);
       } else {
-        v[h] = rw[h][0];
+        v[h] = rw[sl][h][0];
       }
     }
-    if (ch + 1 < nch) load(k0 + CK);  // the next chunk flies under this chunk's stores, LDS write and MFMAs
+    uint4 ac[2][RF];
+    if constexpr (PFA) {
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+        for (int j = 0; j < RF; ++j) ac[ks][j] = an[ks][j];
+    }
+    if (ch + 1 < nch) {  // the next chunk flies under this chunk's stores, LDS write and MFMAs
+      if constexpr (NCH == 0) load(rw[0], k0 + CK);
+      if constexpr (PFA) load_a(k0 + CK);
+    }
     u16(*tile)[XP] = xs[ch & 1];
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
@@ -139,8 +170,8 @@ __global__ __launch_bounds__(512) void fwd_kernel(const u16* __restrict__ x, con
         const bf16x8 a = __builtin_bit_cast(bf16x8, *(const uint4*)&tile[r][kl]);
 #pragma unroll
         for (int j = 0; j < RF; ++j) {
-          const bf16x8 b = __builtin_bit_cast(bf16x8, *(const uint4*)(A + (long)(16 * j + r) * K + k0 + kl));
-          acc[j] = mfma(a, b, acc[j]);
+          const uint4 b = PFA ? ac[ks][j] : *(const uint4*)(A + (long)(16 * j + r) * K + k0 + kl);
+          acc[j] = mfma(a, __builtin_bit_cast(bf16x8, b), acc[j]);
         }
       }
     }
@@ -261,6 +292,102 @@ __global__ __launch_bounds__(512) void bwd_dx_kernel(const u16* __restrict__ bas
       }
     } else {
       if (t < T) *(uint4*)(dx + t * (long)K + k) = pack8(o);
+    }
+  }
+}
+
+// The same pass with the rank-R product on the matrix cores and no LDS: wave = 16 token rows x 128 columns, the
+// product dxa [16, R] . A [R, 128] as eight v_mfma_f32_16x16x16_bf16 tiles whose B columns are PERMUTED — tile j,
+// column c is output column 8 c + j — so lane (g = l >> 4, c = l & 15) ends up holding rows 4 g .. 4 g + 3 x the 8
+// CONTIGUOUS columns 8 c .. 8 c + 7: exactly the 16-byte pieces of base / gu / dx it loads and stores (each wave
+// instruction touches 4 rows x 256 contiguous bytes). The B fragments come from 16-byte loads of A rows (8 columns
+// of one k) repacked by bit selects; dxa and A are loaded first, so the MFMAs wait only for them while base / gu fly.
+__device__ __forceinline__ f32x4 mfma16(const uint2& a, const uint2& b, const f32x4& c) {
+  return __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(__builtin_bit_cast(s16x4, a), __builtin_bit_cast(s16x4, b), c, 0,
+                                                   0, 0);
+}
+
+template <int R, bool SWIGLU>
+__global__ __launch_bounds__(256) void bwd_dx_mfma_kernel(const u16* __restrict__ base, long ldb,
+                                                          const u16* __restrict__ dxa, const u16* __restrict__ A,
+                                                          u16* __restrict__ dx, long T, int K, unsigned thresh,
+                                                          float dscale, unsigned seed, int drop,
+                                                          const u16* __restrict__ gu) {
+  constexpr int KS = R / 16;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, g = lane >> 4, c = lane & 15;
+  const int kw = blockIdx.x * 512 + 128 * w;
+  if (kw >= K) return;  // whole wave past the last column (no barriers in this kernel)
+  const long t0 = (long)blockIdx.y * 16;
+  const int k = kw + 8 * c;
+  const bool kok = k < K;
+  const int kc = kok ? k : K - 8;
+  uint2 da[KS];
+  uint4 av[KS][4];
+  const long ta = min(t0 + c, T - 1);
+#pragma unroll
+  for (int s = 0; s < KS; ++s) {
+    da[s] = *(const uint2*)(dxa + ta * R + 16 * s + 4 * g);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) av[s][i] = *(const uint4*)(A + (long)(16 * s + 4 * g + i) * K + kc);
+  }
+  uint4 vb[4], vg[4], vu[4];
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    const long t = min(t0 + 4 * g + e, T - 1);
+    vb[e] = *(const uint4*)(base + t * ldb + kc);
+    if constexpr (SWIGLU) {
+      vg[e] = *(const uint4*)(gu + t * 2L * K + kc);
+      vu[e] = *(const uint4*)(gu + t * 2L * K + K + kc);
+    }
+  }
+  f32x4 acc[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int s = 0; s < KS; ++s) {
+    const unsigned* p0 = (const unsigned*)&av[s][0];
+    const unsigned* p1 = (const unsigned*)&av[s][1];
+    const unsigned* p2 = (const unsigned*)&av[s][2];
+    const unsigned* p3 = (const unsigned*)&av[s][3];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {  // B fragment of tile j: A[4 g .. 4 g + 3][column 8 c + j]
+      const int h = j >> 1;
+      uint2 b;
+      if (j & 1) {
+        b.x = (p0[h] >> 16) | (p1[h] & 0xFFFF0000u);
+        b.y = (p2[h] >> 16) | (p3[h] & 0xFFFF0000u);
+      } else {
+        b.x = (p0[h] & 0xFFFFu) | (p1[h] << 16);
+        b.y = (p2[h] & 0xFFFFu) | (p3[h] << 16);
+      }
+      acc[j] = mfma16(da[s], b, acc[j]);
+    }
+  }
+  if (!kok) return;
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    const long t = t0 + 4 * g + e;
+    if (t >= T) break;
+    float o[8];
+    unpack8(vb[e], o);
+    const unsigned bits = drop ? keep8((unsigned long long)t * K + k, seed, thresh) : 0xFFu;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) o[j] += ((bits >> j) & 1u) ? acc[j][e] * dscale : 0.f;
+    if constexpr (SWIGLU) {  // o = dact (fp32); the same arithmetic as swiglu_bwd_kernel on the bf16-rounded dact
+      float gt[8], up[8], dg[8], du[8];
+      unpack8(vg[e], gt);
+      unpack8(vu[e], up);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float d = bf2f(f2bf(o[j]));
+        const float sg = 1.f / (1.f + __expf(-gt[j]));
+        du[j] = d * gt[j] * sg;
+        dg[j] = d * up[j] * sg * (1.f + gt[j] * (1.f - sg));
+      }
+      *(uint4*)(dx + t * 2L * K + k) = pack8(dg);
+      *(uint4*)(dx + t * 2L * K + K + k) = pack8(du);
+    } else {
+      *(uint4*)(dx + t * (long)K + k) = pack8(o);
     }
   }
 }
@@ -387,22 +514,27 @@ __device__ __forceinline__ float slab_sum(const float* __restrict__ p, long o, l
   return v;
 }
 
-struct GradOuts {
-  void* ptr[4];
-  int r0[4], c0[4], nr[4], nc[4];
-  int f32[4], acc[4];
+struct GradOuts {  // up to 8 outputs, each a block of one of two fp32 sums
+  const float* sum[2];
+  int K[2], ns[2];
+  long slab[2];
+  void* ptr[8];
+  int src[8], tr[8], r0[8], c0[8], nr[8], nc[8];
+  int f32[8], acc[8];
 };
 
-__global__ __launch_bounds__(256) void grad_out_kernel(const float* __restrict__ sum, int K, long slab, int ns,
-                                                       GradOuts go, int tr) {
+__global__ __launch_bounds__(256) void grad_out_kernel(GradOuts go) {
   const int q = blockIdx.y;
   const int n = go.nr[q] * go.nc[q];  // elements of output q ([nc, nr] when tr, else [nr, nc])
+  const int sq = go.src[q], K = go.K[sq], ns = go.ns[sq];
+  const float* __restrict__ sum = go.sum[sq];
+  const long slab = go.slab[sq];
   for (int e = blockIdx.x * 256 + threadIdx.x; e < n; e += gridDim.x * 256) {
     int i, j;
     float v;
     long oe = e;
-    if (tr) {  // out [nc][nr]: element (i, j) = sum[r0 + j][c0 + i]; consecutive threads read consecutive i (the
-               // slab reads dominate), the writes go nr elements apart
+    if (go.tr[q]) {  // out [nc][nr]: element (i, j) = sum[r0 + j][c0 + i]; consecutive threads read consecutive i
+                     // (the slab reads dominate), the writes go nr elements apart
       j = e / go.nc[q];
       i = e - j * go.nc[q];
       v = slab_sum(sum, (long)(go.r0[q] + j) * K + go.c0[q] + i, slab, ns);
@@ -471,7 +603,12 @@ std::tuple<at::Tensor, at::Tensor> lora_fwd(const at::Tensor& x, const at::Tenso
   const int grid = (int)((T + 15) / 16);
   u16* xdp = (p > 0 && save_xd) ? (u16*)xd.data_ptr() : nullptr;
 #define LORA_FWD(RF)                                                                                              \
-  if (swiglu)                                                                                                     \
+  if (!swiglu && K == 2048)                                                                                       \
+    lora::fwd_kernel<RF, false, 4><<<grid, 512, 0, cur_stream()>>>((const u16*)x.data_ptr(),                     \
+                                                                   (const u16*)A.data_ptr(), (u16*)X.data_ptr(), xdp, \
+                                                                   T, K, ldX, (float)s, thresh, dscale,          \
+                                                                   (unsigned)seed, p > 0 ? 1 : 0);               \
+  else if (swiglu)                                                                                                \
     lora::fwd_kernel<RF, true><<<grid, 512, 0, cur_stream()>>>((const u16*)x.data_ptr(), (const u16*)A.data_ptr(), \
                                                                (u16*)X.data_ptr(), xdp, T, K, ldX, (float)s, thresh, \
                                                                dscale, (unsigned)seed, p > 0 ? 1 : 0);            \
@@ -514,6 +651,29 @@ at::Tensor lora_bwd_dx(const at::Tensor& base, const at::Tensor& dxa, const at::
   if (T == 0) return dx;
   float dscale;
   const unsigned thresh = lora::thresh_of(p, &dscale);
+  const char* ev = getenv("SFTAMD_LORA_DX");
+  if (!(ev && ev[0] == '0')) {
+    dim3 grid((K + 511) / 512, (unsigned)((T + 15) / 16));
+    SFT_CHECK(grid.y <= 65535u, "lora_bwd_dx: T too large");
+#define LORA_BWD(RR)                                                                                              \
+  if (sw)                                                                                                         \
+    lora::bwd_dx_mfma_kernel<RR, true><<<grid, 256, 0, cur_stream()>>>(                                          \
+        (const u16*)base.data_ptr(), base.stride(0), (const u16*)dxa.data_ptr(), (const u16*)A.data_ptr(),        \
+        (u16*)dx.data_ptr(), T, K, thresh, dscale, (unsigned)seed, p > 0 ? 1 : 0, (const u16*)gu->data_ptr());    \
+  else                                                                                                            \
+    lora::bwd_dx_mfma_kernel<RR, false><<<grid, 256, 0, cur_stream()>>>(                                         \
+        (const u16*)base.data_ptr(), base.stride(0), (const u16*)dxa.data_ptr(), (const u16*)A.data_ptr(),        \
+        (u16*)dx.data_ptr(), T, K, thresh, dscale, (unsigned)seed, p > 0 ? 1 : 0, nullptr)
+    switch (R / 16) {
+      case 1: LORA_BWD(16); break;
+      case 2: LORA_BWD(32); break;
+      case 3: LORA_BWD(48); break;
+      default: LORA_BWD(64); break;
+    }
+#undef LORA_BWD
+    SFT_LAUNCH_CHECK();
+    return dx;
+  }
   const int cw = R >= 48 ? 256 : 512, tr = 512 / (cw / 8) * 4;  // = dx_cols<R>() and the kernel's TR
   dim3 grid((K + cw - 1) / cw, (unsigned)((T + tr - 1) / tr));
   SFT_CHECK(grid.y <= 65535u, "lora_bwd_dx: T too large");
@@ -694,7 +854,9 @@ at::Tensor lora_tsum(const at::Tensor& X, int64_t K, const at::Tensor& S, double
   // 64-column ones on about 1024. The token range is split into chunks of whole 64-token stages.
   const bool wide = K >= 8192;
   const int nk = wide ? 256 : 64, nkb = (int)((K + nk - 1) / nk);
-  long splits = std::max(1L, std::min((T + 63) / 64, (wide ? 512L : 1024L) / nkb));
+  const char* ew = getenv("SFTAMD_LORA_TSUM_WG");
+  const long wg_wide = (ew && ew[0] && p > 0) ? atol(ew) : 512L;
+  long splits = std::max(1L, std::min((T + 63) / 64, (wide ? wg_wide : 1024L) / nkb));
   const long tc = ((T + splits - 1) / splits + 63) / 64 * 64;
   splits = (T + tc - 1) / tc;
   auto out = at::empty({splits, R, K}, X.options().dtype(at::kFloat));  // every element written by one workgroup
@@ -719,36 +881,66 @@ at::Tensor lora_tsum(const at::Tensor& X, int64_t K, const at::Tensor& S, double
   return out;
 }
 
-// outs[q] (+)= block q of sum ([R, K] fp32, or [splits, R, K] slabs summed on the fly): rows [r0[q], +nr), columns [c0[q], +nc), transposed when tr; one launch
-void lora_grad_out(const at::Tensor& sum, at::TensorList outs, at::IntArrayRef r0, at::IntArrayRef c0, bool tr,
-                   at::IntArrayRef accumulate) {
+// outs[q] (+)= block q of sum ([R, K] fp32, or [splits, R, K] slabs summed on the fly): rows [r0[q], +nr), columns
+// [c0[q], +nc), transposed when tr. lora_grad_out2 does two such groups (a projection's dB^T and dA sums) in ONE
+// launch.
+namespace lora {
+static void add_group(GradOuts& go, int& n, long& most, int g, const at::Tensor& sum, at::TensorList outs,
+                      at::IntArrayRef r0, at::IntArrayRef c0, bool tr, at::IntArrayRef accumulate) {
   SFT_CHECK(sum.scalar_type() == at::kFloat && sum.is_contiguous() && (sum.dim() == 2 || sum.dim() == 3),
             "lora_grad_out: fp32 [R, K] or [splits, R, K]");
-  const int n = outs.size();
-  SFT_CHECK(n >= 1 && n <= 4 && (int)r0.size() == n && (int)c0.size() == n && (int)accumulate.size() == n,
-            "lora_grad_out: 1..4 outputs");
-  const int ns = sum.dim() == 3 ? sum.size(0) : 1;
+  const int m = outs.size();
+  SFT_CHECK(m >= 1 && n + m <= 8 && (int)r0.size() == m && (int)c0.size() == m && (int)accumulate.size() == m,
+            "lora_grad_out: 1..4 outputs per sum");
   const int R = sum.size(sum.dim() - 2), K = sum.size(sum.dim() - 1);
-  lora::GradOuts go{};
-  long most = 0;
-  for (int q = 0; q < n; ++q) {
-    const at::Tensor& o = outs[q];
+  go.sum[g] = sum.data_ptr<float>();
+  go.K[g] = K;
+  go.ns[g] = sum.dim() == 3 ? sum.size(0) : 1;
+  go.slab[g] = (long)R * K;
+  for (int i = 0; i < m; ++i, ++n) {
+    const at::Tensor& o = outs[i];
     SFT_CHECK(o.is_contiguous() && o.dim() == 2 &&
                   (o.scalar_type() == at::kBFloat16 || o.scalar_type() == at::kFloat), "lora_grad_out: contiguous bf16 / fp32 2-D outputs");
     const int nr = tr ? o.size(1) : o.size(0), nc = tr ? o.size(0) : o.size(1);
-    SFT_CHECK(r0[q] >= 0 && r0[q] + nr <= R && c0[q] >= 0 && c0[q] + nc <= K, "lora_grad_out: block out of range");
-    go.ptr[q] = o.data_ptr();
-    go.r0[q] = (int)r0[q];
-    go.c0[q] = (int)c0[q];
-    go.nr[q] = nr;
-    go.nc[q] = nc;
-    go.f32[q] = o.scalar_type() == at::kFloat;
-    go.acc[q] = accumulate[q] != 0;
+    SFT_CHECK(r0[i] >= 0 && r0[i] + nr <= R && c0[i] >= 0 && c0[i] + nc <= K, "lora_grad_out: block out of range");
+    go.ptr[n] = o.data_ptr();
+    go.src[n] = g;
+    go.tr[n] = tr ? 1 : 0;
+    go.r0[n] = (int)r0[i];
+    go.c0[n] = (int)c0[i];
+    go.nr[n] = nr;
+    go.nc[n] = nc;
+    go.f32[n] = o.scalar_type() == at::kFloat;
+    go.acc[n] = accumulate[i] != 0;
     most = std::max(most, (long)nr * nc);
   }
+}
+
+static void launch_grad_out(const GradOuts& go, int n, long most) {
   dim3 grid((unsigned)std::min(1024L, (most + 255) / 256), (unsigned)n);
-  lora::grad_out_kernel<<<grid, 256, 0, cur_stream()>>>(sum.data_ptr<float>(), K, (long)R * K, ns, go, tr ? 1 : 0);
+  grad_out_kernel<<<grid, 256, 0, cur_stream()>>>(go);
   SFT_LAUNCH_CHECK();
+}
+}  // namespace lora
+
+void lora_grad_out(const at::Tensor& sum, at::TensorList outs, at::IntArrayRef r0, at::IntArrayRef c0, bool tr,
+                   at::IntArrayRef accumulate) {
+  lora::GradOuts go{};
+  int n = 0;
+  long most = 0;
+  lora::add_group(go, n, most, 0, sum, outs, r0, c0, tr, accumulate);
+  lora::launch_grad_out(go, n, most);
+}
+
+void lora_grad_out2(const at::Tensor& sa, at::TensorList oa, at::IntArrayRef ra, at::IntArrayRef ca, bool ta,
+                    at::IntArrayRef aa, const at::Tensor& sb, at::TensorList ob, at::IntArrayRef rb,
+                    at::IntArrayRef cb, bool tb, at::IntArrayRef ab) {
+  lora::GradOuts go{};
+  int n = 0;
+  long most = 0;
+  lora::add_group(go, n, most, 0, sa, oa, ra, ca, ta, aa);
+  lora::add_group(go, n, most, 1, sb, ob, rb, cb, tb, ab);
+  lora::launch_grad_out(go, n, most);
 }
 
 // desc: int64 [n, 6] device table (see copy2d_batch_kernel); max_elems: the largest rows * cols in it
@@ -771,6 +963,7 @@ TORCH_LIBRARY_IMPL(sftamd, CUDA, m) {
   m.impl("lora_tsum", &lora_tsum);
   m.impl("lora_dxa", &lora_dxa);
   m.impl("lora_grad_out", &lora_grad_out);
+  m.impl("lora_grad_out2", &lora_grad_out2);
 }
 
 }  // namespace sftamd

@@ -937,20 +937,44 @@ def _lora_tsum(Xm, K, S, p, seed) -> torch.Tensor:
     return S.float().t() @ xs.float()
 
 
+def _scatter_direct(total: torch.Tensor, params):
+    """The main_grad slices ``params``' gradients go to when lora_grad_out can write them directly, else None."""
+    mgs = [getattr(p, "main_grad", None) for p in params]
+    if (all(m is not None for m in mgs) and _ext.use_hip(total) and len(params) <= 4
+            and all(m.is_contiguous() and m.dtype in (torch.bfloat16, torch.float32) for m in mgs)):
+        return mgs
+    return None
+
+
+def _scatter_done(params):
+    for p in params:
+        p._sftamd_fresh = False
+        _weight_grad_done(p)
+    return [None] * len(params)
+
+
+def _scatter_pair(tot_b, Bs, blocks_b, tot_a, As, blocks_a):
+    """A projection's dB^T and dA scatters (_scatter_grads) in ONE lora_grad_out2 launch when both go straight into
+    main_grad."""
+    mb, ma = _scatter_direct(tot_b, Bs), _scatter_direct(tot_a, As)
+    if mb is None or ma is None:
+        return _scatter_grads(tot_b, Bs, blocks_b, tr=True), _scatter_grads(tot_a, As, blocks_a, tr=False)
+    acc = [[0 if getattr(p, "_sftamd_fresh", False) else 1 for p in ps] for ps in (Bs, As)]
+    _ext.ops().lora_grad_out2(tot_b, mb, [b[0] for b in blocks_b], [b[1] for b in blocks_b], True, acc[0],
+                              tot_a, ma, [b[0] for b in blocks_a], [b[1] for b in blocks_a], False, acc[1])
+    return _scatter_done(Bs), _scatter_done(As)
+
+
 def _scatter_grads(total: torch.Tensor, params, blocks, tr: bool):
     """Per-adapter gradients from one fp32 sum [R, K]: param q's block starts at (r0, c0) of ``total`` (transposed when
     ``tr``). With DDP main_grad slices they are written / accumulated in ONE launch and None is returned to autograd;
     otherwise the blocks are returned."""
     shapes = [(p.shape[1], p.shape[0]) if tr else tuple(p.shape) for p in params]
-    mgs = [getattr(p, "main_grad", None) for p in params]
-    if (all(m is not None for m in mgs) and _ext.use_hip(total) and len(params) <= 4
-            and all(m.is_contiguous() and m.dtype in (torch.bfloat16, torch.float32) for m in mgs)):
+    mgs = _scatter_direct(total, params)
+    if mgs is not None:
         acc = [0 if getattr(p, "_sftamd_fresh", False) else 1 for p in params]
         _ext.ops().lora_grad_out(total, mgs, [b[0] for b in blocks], [b[1] for b in blocks], bool(tr), acc)
-        for p in params:
-            p._sftamd_fresh = False
-            _weight_grad_done(p)
-        return [None] * len(params)
+        return _scatter_done(params)
     if total.dim() == 3:
         total = total.sum(0)
     out = []
@@ -1132,9 +1156,8 @@ def _lora_wide_bwd(X, acat, wide, ab, state, dy2d, need_dx, gu=None):
     # accumulation): dB^T = (s xa)^T dy [R, n_out] (block (c_i, o_i) transposed is dB_i); dA = dxa^T dropout(x)
     # [R, K] (the forward's dropout mask regenerated from the seed: nothing saved)
     n_out = dy2d.shape[1]
-    dBs = _scatter_grads(_lora_tsum(dy2d, n_out, X[:, K:K + R], 0.0, 0), Bs, [(c, o) for (o, rows, c) in meta],
-                         tr=True)
-    dAs = _scatter_grads(_lora_tsum(X, K, dxa, p, seed), As, [(i * r, 0) for i in range(n)], tr=False)
+    dBs, dAs = _scatter_pair(_lora_tsum(dy2d, n_out, X[:, K:K + R], 0.0, 0), Bs, [(c, o) for (o, rows, c) in meta],
+                             _lora_tsum(X, K, dxa, p, seed), As, [(i * r, 0) for i in range(n)])
     dx = _lora_bwd_dx(base, dxa, acat, p, seed, gu) if need_dx else None
     return dx, dAs, dBs
 

@@ -537,6 +537,18 @@ def test_lora_fwd_bwd_kernels(K, R, p):
     _ext.ops().lora_grad_out(sBp, [o1, o2], [0, R - 16], [0, n_out // 2], True, [1, 0])  # sums the slabs
     assert rel_err(o1, o1_ref) < 1e-2
     assert torch.allclose(o2, sB[R - 16:R, n_out // 2:].t())
+    # both of a projection's scatters in one launch: dB^T blocks transposed from sBp, dA blocks straight from the dA
+    # slabs, written / accumulated, bf16 / fp32
+    dAp = _ext.ops().lora_tsum(X, K, dxa, p, 99)
+    b1 = torch.randn(n_out // 2, 16, device="cuda", dtype=torch.bfloat16)
+    b2 = torch.zeros(n_out - n_out // 2, 16, device="cuda", dtype=torch.float32)
+    a1 = torch.zeros(16, K, device="cuda", dtype=torch.float32)
+    a2 = torch.randn(16, K, device="cuda", dtype=torch.bfloat16)
+    b1_ref, a2_ref = b1.float() + sB[0:16, 0:n_out // 2].t(), a2.float() + dA[R - 16:R]
+    _ext.ops().lora_grad_out2(sBp, [b1, b2], [0, R - 16], [0, n_out // 2], True, [1, 0],
+                              dAp, [a1, a2], [0, R - 16], [0, 0], False, [0, 1])
+    assert rel_err(b1, b1_ref) < 1e-2 and torch.allclose(b2, sB[R - 16:R, n_out // 2:].t())
+    assert torch.allclose(a1, dA[0:16]) and rel_err(a2, a2_ref) < 1e-2
 
 
 @pytest.mark.parametrize("T,n,R,ldb", [(8192, 22016, 32, 2176), (256, 2048, 16, 2048 + 128), (300, 3072, 48, 2176),
