@@ -9,8 +9,8 @@
 //                fragments (rows of A_cat loaded from global memory in fragment layout); the partial
 //                16 x R tiles of the block's 8 waves are summed through LDS.
 //   lora_bwd_dx: dx = base + keep * (dxa @ A) / (1-p), base = the base-weight dgrad (possibly a
-//                column slice of dX'), one read of base and one write of dx; the rank-R product is a
-//                VALU outer-product loop over an LDS-resident A tile (R <= 64 FMAs per output).
+//                column slice of dX'), one read of base and one write of dx; the rank-R product on
+//                16x16x16 MFMAs whose B columns are permuted so every lane holds 8 contiguous outputs.
 //   lora_tsum:   the adapter gradients' token reductions (dA, dB^T), one pass over the wide operand.
 //
 // The dropout mask is hash_u32(t*K + k, seed) >= p * 2^32 (common.h; keep8 below computes it per 8-element chunk),
@@ -198,117 +198,24 @@ __global__ __launch_bounds__(512) void fwd_kernel(const u16* __restrict__ x, con
   }
 }
 
-// tile: 32 rows x 512 columns (64 x 256 for R >= 48) per 512-thread block; thread = 4 rows x 8 columns (the A tile in
-// LDS is reused by all rows of the block). The thread's base (and gu) rows are loaded BEFORE the rank-R product loop (row indices
-// clamped, stores predicated), so the HBM latency hides under the FMAs instead of serialising row by row after it.
-// With gu ([T, 2K] = gate | up, the SwiGLU input): the SwiGLU backward is applied to dx on the way out and
-// dgu [T, 2K] is written instead (the down projection of a LoRA MLP: no dx round trip through HBM).
-// Column width of a bwd_dx block: 256 for R >= 48 (the fp32 A tile [R][512] alone was 96 KB for the qkv adapters, one
-// workgroup per CU: 52 us for 67 MB of traffic), 512 otherwise.
-template <int R>
-constexpr int dx_cols() { return R >= 48 ? 256 : 512; }
-
-template <int R, bool SWIGLU>
-__global__ __launch_bounds__(512) void bwd_dx_kernel(const u16* __restrict__ base, long ldb, const u16* __restrict__ dxa,
-                                                     const u16* __restrict__ A, u16* __restrict__ dx, long T, int K,
-                                                     unsigned thresh, float dscale, unsigned seed, int drop,
-                                                     const u16* __restrict__ gu) {
-  constexpr int CW = dx_cols<R>(), NC8 = CW / 8, RPT = 4, TR = 512 / NC8 * RPT;
-  __shared__ float As[R][CW];
-  __shared__ float Ds[TR][R];
-  const int tid = threadIdx.x;
-  const int k0 = blockIdx.x * CW;
-  const long t0 = (long)blockIdx.y * TR;
-  const int c8 = tid % NC8, rg = tid / NC8;
-  const int k = k0 + c8 * 8;
-  const int kc = k < K ? k : K - 8;
-  uint4 vb[RPT], vg[RPT], vu[RPT];
-#pragma unroll
-  for (int i = 0; i < RPT; ++i) {
-    const long t = min(t0 + rg * RPT + i, T - 1);
-    vb[i] = *(const uint4*)(base + t * ldb + kc);
-    if constexpr (SWIGLU) {
-      vg[i] = *(const uint4*)(gu + t * 2L * K + kc);
-      vu[i] = *(const uint4*)(gu + t * 2L * K + K + kc);
-    }
-  }
-  for (int e = tid; e < R * NC8; e += 512) {  // A[:, k0:k0+CW] as 8-wide vectors
-    const int rr = e / NC8, cc = e % NC8, kk = k0 + cc * 8;
-    float f[8];
-    if (kk < K) {
-      unpack8(*(const uint4*)(A + (long)rr * K + kk), f);
-    } else {
-#pragma unroll
-      for (int i = 0; i < 8; ++i) f[i] = 0.f;
-    }
-#pragma unroll
-    for (int i = 0; i < 8; ++i) As[rr][cc * 8 + i] = f[i];
-  }
-  for (int e = tid; e < TR * R; e += 512) {
-    const int row = e / R, col = e - row * R;
-    Ds[row][col] = (t0 + row < T) ? bf2f(dxa[(t0 + row) * R + col]) : 0.f;
-  }
-  __syncthreads();
-  float acc[RPT][8];
-#pragma unroll
-  for (int i = 0; i < RPT; ++i)
-#pragma unroll
-    for (int j = 0; j < 8; ++j) acc[i][j] = 0.f;
-#pragma unroll 4
-  for (int rr = 0; rr < R; ++rr) {
-    float a[8];
-    *(float4*)&a[0] = *(const float4*)&As[rr][c8 * 8];
-    *(float4*)&a[4] = *(const float4*)&As[rr][c8 * 8 + 4];
-#pragma unroll
-    for (int i = 0; i < RPT; ++i) {
-      const float d = Ds[rg * RPT + i][rr];
-#pragma unroll
-      for (int j = 0; j < 8; ++j) acc[i][j] += d * a[j];
-    }
-  }
-  if (k >= K) return;
-#pragma unroll
-  for (int i = 0; i < RPT; ++i) {
-    const long t = t0 + rg * RPT + i;
-    float o[8];
-    unpack8(vb[i], o);
-    const unsigned bits = drop ? keep8((unsigned long long)t * K + k, seed, thresh) : 0xFFu;
-#pragma unroll
-    for (int j = 0; j < 8; ++j) o[j] += ((bits >> j) & 1u) ? acc[i][j] * dscale : 0.f;
-    if constexpr (SWIGLU) {  // o = dact (fp32); the same arithmetic as swiglu_bwd_kernel on the bf16-rounded dact
-      float gt[8], up[8], dg[8], du[8];
-      unpack8(vg[i], gt);
-      unpack8(vu[i], up);
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const float d = bf2f(f2bf(o[j]));
-        const float sg = 1.f / (1.f + __expf(-gt[j]));
-        du[j] = d * gt[j] * sg;
-        dg[j] = d * up[j] * sg * (1.f + gt[j] * (1.f - sg));
-      }
-      if (t < T) {
-        *(uint4*)(dx + t * 2L * K + k) = pack8(dg);
-        *(uint4*)(dx + t * 2L * K + K + k) = pack8(du);
-      }
-    } else {
-      if (t < T) *(uint4*)(dx + t * (long)K + k) = pack8(o);
-    }
-  }
-}
-
-// The same pass with the rank-R product on the matrix cores and no LDS: wave = 16 token rows x 128 columns, the
+// lora_bwd_dx: dx = base + keep * (dxa @ A) / (1-p) in one pass over base (and gu, writing dgu = swiglu_bwd(dx, gu)
+// for the down projection of a LoRA MLP: no dx round trip through HBM), the rank-R product on the matrix cores and no
+// LDS: wave = 16 token rows x 128 columns, the
 // product dxa [16, R] . A [R, 128] as eight v_mfma_f32_16x16x16_bf16 tiles whose B columns are PERMUTED — tile j,
 // column c is output column 8 c + j — so lane (g = l >> 4, c = l & 15) ends up holding rows 4 g .. 4 g + 3 x the 8
 // CONTIGUOUS columns 8 c .. 8 c + 7: exactly the 16-byte pieces of base / gu / dx it loads and stores (each wave
 // instruction touches 4 rows x 256 contiguous bytes). The B fragments come from 16-byte loads of A rows (8 columns
 // of one k) repacked by bit selects; dxa and A are loaded first, so the MFMAs wait only for them while base / gu fly.
+// (Replaced a VALU outer product over an fp32 A tile staged in LDS, 32 rows x 512 columns per 512-thread block:
+// 39.1 / 30.5 / 22.6 -> 17.5 / 16.7 / 14.8 us for the R = 48 / 32 / 16 adapters at K = 2048, 197.9 -> 159.5 us for the
+// dgu-writing K = 11008 pass, T = 8192; LoRA 133.2 -> 135.8 samples/s, r5_run16.)
 __device__ __forceinline__ f32x4 mfma16(const uint2& a, const uint2& b, const f32x4& c) {
   return __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(__builtin_bit_cast(s16x4, a), __builtin_bit_cast(s16x4, b), c, 0,
                                                    0, 0);
 }
 
 template <int R, bool SWIGLU>
-__global__ __launch_bounds__(256) void bwd_dx_mfma_kernel(const u16* __restrict__ base, long ldb,
+__global__ __launch_bounds__(256) void bwd_dx_kernel(const u16* __restrict__ base, long ldb,
                                                           const u16* __restrict__ dxa, const u16* __restrict__ A,
                                                           u16* __restrict__ dx, long T, int K, unsigned thresh,
                                                           float dscale, unsigned seed, int drop,
@@ -651,39 +558,15 @@ at::Tensor lora_bwd_dx(const at::Tensor& base, const at::Tensor& dxa, const at::
   if (T == 0) return dx;
   float dscale;
   const unsigned thresh = lora::thresh_of(p, &dscale);
-  const char* ev = getenv("SFTAMD_LORA_DX");
-  if (!(ev && ev[0] == '0')) {
-    dim3 grid((K + 511) / 512, (unsigned)((T + 15) / 16));
-    SFT_CHECK(grid.y <= 65535u, "lora_bwd_dx: T too large");
-#define LORA_BWD(RR)                                                                                              \
-  if (sw)                                                                                                         \
-    lora::bwd_dx_mfma_kernel<RR, true><<<grid, 256, 0, cur_stream()>>>(                                          \
-        (const u16*)base.data_ptr(), base.stride(0), (const u16*)dxa.data_ptr(), (const u16*)A.data_ptr(),        \
-        (u16*)dx.data_ptr(), T, K, thresh, dscale, (unsigned)seed, p > 0 ? 1 : 0, (const u16*)gu->data_ptr());    \
-  else                                                                                                            \
-    lora::bwd_dx_mfma_kernel<RR, false><<<grid, 256, 0, cur_stream()>>>(                                         \
-        (const u16*)base.data_ptr(), base.stride(0), (const u16*)dxa.data_ptr(), (const u16*)A.data_ptr(),        \
-        (u16*)dx.data_ptr(), T, K, thresh, dscale, (unsigned)seed, p > 0 ? 1 : 0, nullptr)
-    switch (R / 16) {
-      case 1: LORA_BWD(16); break;
-      case 2: LORA_BWD(32); break;
-      case 3: LORA_BWD(48); break;
-      default: LORA_BWD(64); break;
-    }
-#undef LORA_BWD
-    SFT_LAUNCH_CHECK();
-    return dx;
-  }
-  const int cw = R >= 48 ? 256 : 512, tr = 512 / (cw / 8) * 4;  // = dx_cols<R>() and the kernel's TR
-  dim3 grid((K + cw - 1) / cw, (unsigned)((T + tr - 1) / tr));
+  dim3 grid((K + 511) / 512, (unsigned)((T + 15) / 16));
   SFT_CHECK(grid.y <= 65535u, "lora_bwd_dx: T too large");
 #define LORA_BWD(RR)                                                                                              \
   if (sw)                                                                                                         \
-    lora::bwd_dx_kernel<RR, true><<<grid, 512, 0, cur_stream()>>>(                                               \
+    lora::bwd_dx_kernel<RR, true><<<grid, 256, 0, cur_stream()>>>(                                               \
         (const u16*)base.data_ptr(), base.stride(0), (const u16*)dxa.data_ptr(), (const u16*)A.data_ptr(),        \
         (u16*)dx.data_ptr(), T, K, thresh, dscale, (unsigned)seed, p > 0 ? 1 : 0, (const u16*)gu->data_ptr());    \
   else                                                                                                            \
-    lora::bwd_dx_kernel<RR, false><<<grid, 512, 0, cur_stream()>>>(                                              \
+    lora::bwd_dx_kernel<RR, false><<<grid, 256, 0, cur_stream()>>>(                                              \
         (const u16*)base.data_ptr(), base.stride(0), (const u16*)dxa.data_ptr(), (const u16*)A.data_ptr(),        \
         (u16*)dx.data_ptr(), T, K, thresh, dscale, (unsigned)seed, p > 0 ? 1 : 0, nullptr)
   switch (R / 16) {
@@ -854,9 +737,8 @@ at::Tensor lora_tsum(const at::Tensor& X, int64_t K, const at::Tensor& S, double
   // 64-column ones on about 1024. The token range is split into chunks of whole 64-token stages.
   const bool wide = K >= 8192;
   const int nk = wide ? 256 : 64, nkb = (int)((K + nk - 1) / nk);
-  const char* ew = getenv("SFTAMD_LORA_TSUM_WG");
-  const long wg_wide = (ew && ew[0] && p > 0) ? atol(ew) : 512L;
-  long splits = std::max(1L, std::min((T + 63) / 64, (wide ? wg_wide : 1024L) / nkb));
+  // (768 / 1024 workgroups for the dropout-regenerating wide dA measured neutral in the LoRA step, r5_run16)
+  long splits = std::max(1L, std::min((T + 63) / 64, (wide ? 512L : 1024L) / nkb));
   const long tc = ((T + splits - 1) / splits + 63) / 64 * 64;
   splits = (T + tc - 1) / tc;
   auto out = at::empty({splits, R, K}, X.options().dtype(at::kFloat));  // every element written by one workgroup

@@ -213,11 +213,6 @@ __global__ __launch_bounds__(256) void adamw_kernel(u16* __restrict__ p, const u
   }
 }
 
-static long env_long(const char* name, long dflt) {
-  const char* e = std::getenv(name);
-  return e && e[0] ? atol(e) : dflt;
-}
-
 void adamw_flat(at::Tensor param, const at::Tensor& grad, const c10::optional<at::Tensor>& master, at::Tensor exp_avg,
                 at::Tensor exp_avg_sq, const at::Tensor& clip_coef, double lr, double beta1, double beta2, double eps,
                 double weight_decay, double bc1, double bc2, int64_t sr_seed, int64_t sr_offset) {
@@ -232,11 +227,11 @@ void adamw_flat(at::Tensor param, const at::Tensor& grad, const c10::optional<at
   const long n = param.numel();
   SFT_CHECK(grad.numel() == n && exp_avg.numel() == n && exp_avg_sq.numel() == n, "sizes");
   if (n == 0) return;
-  // launch shape: 2 vectors per thread step, at most 2048 blocks (fewer blocks measured slower under the overlapped
-  // forward: gpu_run49; one vector per step slower: gpu_run50)
-  const int unr = (int)env_long("SFTAMD_ADAMW_UNR", 2);
-  const long cap = env_long("SFTAMD_ADAMW_BLOCKS", 2048);
-  int grid = (int)std::min<long>(std::max<long>(1, (n / 8 + 256L * unr - 1) / (256L * unr)), cap);
+  // launch shape: 4 vectors of 8 per thread step, at most 2048 blocks. bf16 moments with SR: 759 vs 822 us for 2
+  // vectors per step (256 M elements, tools/bench_adamw.py, r5_run14; fp32 moments unchanged), neutral inside the
+  // overlapped training step (r5_run16). Fewer blocks measured slower under the overlapped forward (gpu_run49).
+  constexpr int UNR = 4;
+  int grid = (int)std::min<long>(std::max<long>(1, (n / 8 + 256L * UNR - 1) / (256L * UNR)), 2048L);
   const float rbc1 = (float)(1.0 / bc1), rsbc2 = (float)(1.0 / std::sqrt(bc2));
   const bool has_master = master.has_value() && master->defined();
   if (has_master)
@@ -246,16 +241,10 @@ void adamw_flat(at::Tensor param, const at::Tensor& grad, const c10::optional<at
   SFT_CHECK(clip_coef.scalar_type() == at::kFloat && clip_coef.numel() >= 1 && clip_coef.is_cuda(), "clip_coef");
   auto go = [&](auto ms, auto sr, auto bm) {
     constexpr bool M = decltype(ms)::value, S = decltype(sr)::value, B = decltype(bm)::value;
-    auto launch = [&](auto u) {
-      constexpr int U = decltype(u)::value;
-      adamw_kernel<M, S, B, U><<<grid, 256, 0, cur_stream()>>>(
-          (u16*)param.data_ptr(), (const u16*)grad.data_ptr(), mp, exp_avg.data_ptr(), exp_avg_sq.data_ptr(),
-          clip_coef.data_ptr<float>(), n, (float)lr, (float)beta1, (float)beta2, (float)eps, (float)weight_decay,
-          rbc1, rsbc2, (float)(1.0 - beta1), (float)(1.0 - beta2), seed, (long)sr_offset);
-    };
-    if (unr == 1) launch(std::integral_constant<int, 1>());
-    else if (unr == 4) launch(std::integral_constant<int, 4>());
-    else launch(std::integral_constant<int, 2>());
+    adamw_kernel<M, S, B, UNR><<<grid, 256, 0, cur_stream()>>>(
+        (u16*)param.data_ptr(), (const u16*)grad.data_ptr(), mp, exp_avg.data_ptr(), exp_avg_sq.data_ptr(),
+        clip_coef.data_ptr<float>(), n, (float)lr, (float)beta1, (float)beta2, (float)eps, (float)weight_decay,
+        rbc1, rsbc2, (float)(1.0 - beta1), (float)(1.0 - beta2), seed, (long)sr_offset);
   };
   auto go2 = [&](auto ms, auto sr) {
     if (bf16m) go(ms, sr, std::true_type());

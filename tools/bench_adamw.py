@@ -37,17 +37,15 @@ def t(fn, reps=10):
     return statistics.median(ts)
 
 
-# launch shapes (read per call by the launcher): vectors of 8 per thread step x block cap
-SHAPES = [(u, b) for u, b in (("2", "2048"), ("4", "1024"), ("4", "2048"), ("2", "4096"))]
+# (round 5, r5_run14: launch shapes of 2 / 4 vectors of 8 per thread step x 1024 / 2048 / 4096 blocks; 4 x 2048, now
+# the default, was fastest for bf16 moments: 759 vs 822 us with SR)
 res = {}
 for rnd in range(3):
     for dt, (m, v) in state.items():
         for sr in (1234, 0):
-            for u, b in SHAPES:
-                os.environ["SFTAMD_ADAMW_UNR"], os.environ["SFTAMD_ADAMW_BLOCKS"] = u, b
-                ms = t(lambda: ops.adamw_flat(p, g, None, m, v, coef, 1e-4, 0.9, 0.999, 1e-8, 0.0, 0.1, 0.001, sr, 0))
-                res.setdefault((str(dt).replace("torch.", ""), "SR" if sr else "RN", u, b), []).append(ms)
-for (dt, sr, u, b), v in res.items():
+            ms = t(lambda: ops.adamw_flat(p, g, None, m, v, coef, 1e-4, 0.9, 0.999, 1e-8, 0.0, 0.1, 0.001, sr, 0))
+            res.setdefault((str(dt).replace("torch.", ""), "SR" if sr else "RN"), []).append(ms)
+for (dt, sr), v in res.items():
     ms = statistics.median(v)
     bpp = 22 if dt == "float32" else 14
-    print(f"moments {dt:8s} {sr} UNR {u} blocks {b:>5s}: {ms * 1e3:8.1f} us  {n * bpp / ms / 1e9:.2f} TB/s", flush=True)
+    print(f"moments {dt:8s} {sr}: {ms * 1e3:8.1f} us  {n * bpp / ms / 1e9:.2f} TB/s", flush=True)

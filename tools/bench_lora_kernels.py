@@ -51,23 +51,16 @@ def main():
         ("lora_tsum dB n=22016 R=32", lambda: ops.lora_tsum(gu, 2 * I, dxa2, 0.0, 0), T * 2 * I * 2),
         ("lora_tsum dB n=4096 R=16", lambda: ops.lora_tsum(xh, H, dxa, 0.0, 0), T * H * 2),
     ]
-    # SmolLM3-3B adapter-dx shapes (hidden 2048: qkv R 48, gate_up R 32, o R 16; the down projection's dgu pass),
-    # the LDS / VALU kernel (SFTAMD_LORA_DX=0) against the MFMA one
+    # SmolLM3-3B adapter-dx shapes (hidden 2048: qkv R 48, gate_up R 32, o R 16)
     Hs = 2048
     bs = torch.randn(T, Hs + 128, device=dev, dtype=torch.bfloat16)[:, :Hs]
     As = {r: torch.randn(r, Hs, device=dev, dtype=torch.bfloat16) * 0.05 for r in (16, 32, 48)}
     ds = {r: torch.randn(T, r, device=dev, dtype=torch.bfloat16) for r in (16, 32, 48)}
-    for v in ("0", "1"):
-        def env(fn, v=v):
-            def run():
-                os.environ["SFTAMD_LORA_DX"] = v
-                return fn()
-            return run
-        rows += [
-            (f"[dx{v}] bwd_dx K=2048 R={r}", env(lambda r=r: ops.lora_bwd_dx(bs, ds[r], As[r], 0.05, 1)), 2 * T * Hs * 2)
-            for r in (48, 32, 16)]
-        rows.append((f"[dx{v}] bwd_dx swiglu K=11008", env(lambda: ops.lora_bwd_dx(base, dxa, A, 0.05, 1, gu)),
-                     5 * T * I * 2))
+    xs = torch.randn(T, Hs, device=dev, dtype=torch.bfloat16)
+    rows += [(f"lora_bwd_dx K=2048 R={r}", lambda r=r: ops.lora_bwd_dx(bs, ds[r], As[r], 0.05, 1), 2 * T * Hs * 2)
+             for r in (48, 32, 16)]
+    rows += [(f"lora_fwd K=2048 R={r}", lambda r=r: ops.lora_fwd(xs, As[r], 0.5, 0.05, 1, Hs + 128), 2 * T * Hs * 2)
+             for r in (48, 32, 16)]
     a = torch.randn(8192, 8192, device=dev, dtype=torch.bfloat16)
     for _ in range(200):  # ~1 s of GEMMs first: the clocks ramp up before anything is timed
         a @ a
