@@ -66,6 +66,7 @@ TORCH_LIBRARY(sftamd, m) {
   m.def("lora_bwd_dx(Tensor base, Tensor dxa, Tensor A, float p, int seed, Tensor? gu=None) -> Tensor");
   m.def("lora_tsum(Tensor X, int K, Tensor S, float p, int seed) -> Tensor");
   m.def("lora_dxa(Tensor dy, Tensor Bc, float s) -> Tensor");
+  m.def("lora_dxa_blocks(Tensor dy, Tensor Bc, int[] o, int[] rows, int[] c, int r, float s) -> Tensor");
   m.def("lora_grad_out(Tensor sum, Tensor(a!)[] outs, int[] r0, int[] c0, bool tr, int[] accumulate) -> ()");
   m.def("lora_grad_out2(Tensor sa, Tensor(a!)[] oa, int[] ra, int[] ca, bool ta, int[] aa, Tensor sb, "
         "Tensor(b!)[] ob, int[] rb, int[] cb, bool tb, int[] ab) -> ()");

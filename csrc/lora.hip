@@ -687,6 +687,114 @@ __global__ __launch_bounds__(256) void dxa_kernel(const u16* __restrict__ dy, lo
     }
   }
 }
+
+// Wide dy (gate_up: n = 22016): Bc = B_blockdiag is zero outside its sub-projections' blocks (rows [o_b, o_b + rows_b)
+// x columns [c_b, c_b + r)), so each block's r columns of dxa only need dy's columns [o_b, o_b + rows_b) — half of
+// gate_up's dy per output column, and 16 instead of 32 MFMA columns. Work item = 64 token rows x one PIECE of a block's
+// n-range (pieces cut so the grid is ~512 workgroups): every workgroup reads its dy rows once and only its piece of Bc
+// (the dense kernel above re-read all of Bc per 32 token rows, as many bytes as dy itself). Wave w owns token rows
+// 16 w .. 16 w + 15 of the block and the whole chunk (no cross-wave reduction); fp32 partials [piece][T][r] are summed
+// per block and scaled by dxa_finish_kernel.
+constexpr int DXA_MAXP = 16;
+struct DxaPieces {
+  int n0[DXA_MAXP], n1[DXA_MAXP], blk[DXA_MAXP];  // dy column range, block index
+  int c[4], p0[4], np[4];                          // per block: first dxa column, first piece, pieces
+};
+
+template <int RF>  // r = 16 RF columns per block
+__global__ __launch_bounds__(256) void dxa_piece_kernel(const u16* __restrict__ dy, long ldy,
+                                                        const u16* __restrict__ Bc, long ldb,
+                                                        float* __restrict__ part, long T, DxaPieces pc) {
+  constexpr int r = 16 * RF, CH = 256, LD = CH + 8, XP = 8, TPR = CH / 8, RPP = 256 / TPR;
+  constexpr int BT = r * CH / 32, BPT = (BT + 255) / 256;  // Bc tasks (4 n-rows x 8 columns) per chunk / thread
+  __shared__ __attribute__((aligned(16))) u16 xs[64][LD];
+  __shared__ __attribute__((aligned(16))) u16 bs[r][LD];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, g = lane >> 4, ii = lane & 15;
+  const long t0 = (long)blockIdx.x * 64;
+  const int pi = blockIdx.y, n0 = pc.n0[pi], n1 = pc.n1[pi], cb = pc.c[pc.blk[pi]];
+  const int xr = tid / TPR, xc = 8 * (tid % TPR);  // dy piece: rows xr + RPP q, columns xc .. xc + 7 of the chunk
+  uint4 xv[XP], bv[BPT][4];
+  auto load = [&](int c0) {
+#pragma unroll
+    for (int q = 0; q < XP; ++q) {
+      const long t = t0 + xr + RPP * q;
+      xv[q] = (t < T && c0 + xc < n1) ? *(const uint4*)(dy + t * ldy + c0 + xc) : make_uint4(0, 0, 0, 0);
+    }
+#pragma unroll
+    for (int u = 0; u < BPT; ++u) {
+      const int task = tid + 256 * u, ng = task / (r / 8), rg = task - ng * (r / 8);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int nn = c0 + 4 * ng + e;
+        bv[u][e] = (task < BT && nn < n1) ? *(const uint4*)(Bc + (long)nn * ldb + cb + 8 * rg)
+                                          : make_uint4(0, 0, 0, 0);
+      }
+    }
+  };
+  f32x4 acc[RF];
+#pragma unroll
+  for (int j = 0; j < RF; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  load(n0);
+  for (int c0 = n0; c0 < n1; c0 += CH) {
+    __syncthreads();  // the previous chunk's reads are done
+#pragma unroll
+    for (int q = 0; q < XP; ++q) *(uint4*)&xs[xr + RPP * q][xc] = xv[q];
+#pragma unroll
+    for (int u = 0; u < BPT; ++u) {
+      const int task = tid + 256 * u, ng = task / (r / 8), rg = task - ng * (r / 8);
+      if (task < BT) {
+        const unsigned* b0 = (const unsigned*)&bv[u][0];
+        const unsigned* b1 = (const unsigned*)&bv[u][1];
+        const unsigned* b2 = (const unsigned*)&bv[u][2];
+        const unsigned* b3 = (const unsigned*)&bv[u][3];
+#pragma unroll
+        for (int h = 0; h < 4; ++h) {  // columns 8 rg + 2 h (low halves) and + 1 (high halves) of the 4 n-rows
+          const unsigned lo01 = (b0[h] & 0xFFFFu) | (b1[h] << 16), lo23 = (b2[h] & 0xFFFFu) | (b3[h] << 16);
+          const unsigned hi01 = (b0[h] >> 16) | (b1[h] & 0xFFFF0000u), hi23 = (b2[h] >> 16) | (b3[h] & 0xFFFF0000u);
+          *(uint2*)&bs[8 * rg + 2 * h][4 * ng] = make_uint2(lo01, lo23);
+          *(uint2*)&bs[8 * rg + 2 * h + 1][4 * ng] = make_uint2(hi01, hi23);
+        }
+      }
+    }
+    __syncthreads();
+    if (c0 + CH < n1) load(c0 + CH);  // the next chunk's loads fly under this chunk's MFMAs
+#pragma unroll
+    for (int ks = 0; ks < CH / 32; ++ks) {
+      const int kc = 32 * ks + 8 * g;
+      const bf16x8 a = *(const bf16x8*)&xs[16 * w + ii][kc];
+#pragma unroll
+      for (int j = 0; j < RF; ++j) acc[j] = mfma(a, *(const bf16x8*)&bs[16 * j + ii][kc], acc[j]);
+    }
+  }
+  // C layout: lane (g, ii) holds token rows 16 w + 4 g + e, column 16 j + ii
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    const long t = t0 + 16 * w + 4 * g + e;
+    if (t < T) {
+#pragma unroll
+      for (int j = 0; j < RF; ++j) part[((long)pi * T + t) * r + 16 * j + ii] = acc[j][e];
+    }
+  }
+}
+
+// dxa[t][c_b + j] = s * (sum of block b's pieces, in piece order)[t][j]; columns outside every block are zero
+template <int RF>
+__global__ __launch_bounds__(256) void dxa_finish_kernel(const float* __restrict__ part, u16* __restrict__ out,
+                                                         long T, int R, int nblk, DxaPieces pc, float s) {
+  constexpr int r = 16 * RF;
+  const long e = (long)blockIdx.x * 256 + threadIdx.x;
+  if (e >= T * R) return;
+  const long t = e / R;
+  const int col = (int)(e - t * R);
+  float v = 0.f;
+  for (int b = 0; b < nblk; ++b) {
+    const int j = col - pc.c[b];
+    if (j >= 0 && j < r) {
+      for (int q = 0; q < pc.np[b]; ++q) v += part[((long)(pc.p0[b] + q) * T + t) * r + j];
+    }
+  }
+  out[e] = f2bf(v * s);
+}
 }  // namespace lora
 
 // out [splits, R, K] fp32 partial sums (over token chunks; lora_grad_out or .sum(0) adds them) of S^T dropout(X[:, :K]) (the mask regenerated from seed when p > 0); X rows of stride >= K, S [T, R]
@@ -716,6 +824,68 @@ at::Tensor lora_dxa(const at::Tensor& dy, const at::Tensor& Bc, double s) {
     default: LORA_DXA(4); break;
   }
 #undef LORA_DXA
+  SFT_LAUNCH_CHECK();
+  return out;
+}
+
+// The same product when Bc is block-diagonal: block b = rows [o[b], o[b] + rows[b]) x columns [c[b], c[b] + r) of Bc,
+// every other element zero (the wide weight's B_blockdiag; the caller guarantees it). Up to 4 blocks.
+at::Tensor lora_dxa_blocks(const at::Tensor& dy, const at::Tensor& Bc, at::IntArrayRef o, at::IntArrayRef rows,
+                           at::IntArrayRef c, int64_t r, double s) {
+  SFT_CHECK_CUDA(dy);
+  SFT_CHECK_BF16(dy);
+  SFT_CHECK_BF16(Bc);
+  const long T = dy.size(0);
+  const int n = dy.size(1), R = Bc.size(1), nb = o.size();
+  SFT_CHECK(dy.stride(1) == 1 && dy.stride(0) % 8 == 0 && (uintptr_t)dy.data_ptr() % 16 == 0 && n % 8 == 0,
+            "lora_dxa_blocks: dy rows 16-byte aligned");
+  SFT_CHECK(Bc.size(0) == n && Bc.stride(1) == 1 && Bc.stride(0) % 8 == 0 && (uintptr_t)Bc.data_ptr() % 16 == 0,
+            "lora_dxa_blocks: Bc [n, R] with 16-byte aligned rows");
+  SFT_CHECK(nb >= 1 && nb <= 4 && (int)rows.size() == nb && (int)c.size() == nb && (r == 16 || r == 32),
+            "lora_dxa_blocks: 1..4 blocks of rank 16 or 32");
+  long total = 0;
+  for (int b = 0; b < nb; ++b) {
+    SFT_CHECK(o[b] >= 0 && rows[b] > 0 && o[b] + rows[b] <= n && o[b] % 8 == 0 && c[b] >= 0 && c[b] + r <= R &&
+                  c[b] % 8 == 0, "lora_dxa_blocks: block out of range / misaligned");
+    total += rows[b];
+  }
+  auto out = at::empty({T, R}, dy.options());
+  if (T == 0) return out;
+  // pieces: ~512 workgroups over the token blocks, piece sizes a multiple of the 256-column chunk
+  const long tb = (T + 63) / 64;
+  const long want = std::max<long>(nb, std::min<long>(lora::DXA_MAXP, (512 + tb - 1) / tb));
+  lora::DxaPieces pc{};
+  int np = 0;
+  for (int b = 0; b < nb; ++b) {
+    const long pb = std::max<long>(1, (want * rows[b] + total - 1) / total);
+    const long sz = ((rows[b] + pb - 1) / pb + 255) / 256 * 256;
+    pc.c[b] = (int)c[b];
+    pc.p0[b] = np;
+    for (long a = 0; a < rows[b]; a += sz) {
+      SFT_CHECK(np < lora::DXA_MAXP, "lora_dxa_blocks: too many pieces");
+      pc.n0[np] = (int)(o[b] + a);
+      pc.n1[np] = (int)(o[b] + std::min(rows[b], a + sz));
+      pc.blk[np] = b;
+      ++np;
+    }
+    pc.np[b] = np - pc.p0[b];
+  }
+  auto part = at::empty({(long)np, T, r}, dy.options().dtype(at::kFloat));
+  dim3 grid((unsigned)tb, (unsigned)np);
+  const unsigned fgrid = (unsigned)((T * R + 255) / 256);
+  if (r == 16) {
+    lora::dxa_piece_kernel<1><<<grid, 256, 0, cur_stream()>>>((const u16*)dy.data_ptr(), dy.stride(0),
+        (const u16*)Bc.data_ptr(), Bc.stride(0), part.data_ptr<float>(), T, pc);
+    SFT_LAUNCH_CHECK();
+    lora::dxa_finish_kernel<1><<<fgrid, 256, 0, cur_stream()>>>(part.data_ptr<float>(), (u16*)out.data_ptr(), T, R,
+                                                                nb, pc, (float)s);
+  } else {
+    lora::dxa_piece_kernel<2><<<grid, 256, 0, cur_stream()>>>((const u16*)dy.data_ptr(), dy.stride(0),
+        (const u16*)Bc.data_ptr(), Bc.stride(0), part.data_ptr<float>(), T, pc);
+    SFT_LAUNCH_CHECK();
+    lora::dxa_finish_kernel<2><<<fgrid, 256, 0, cur_stream()>>>(part.data_ptr<float>(), (u16*)out.data_ptr(), T, R,
+                                                                nb, pc, (float)s);
+  }
   SFT_LAUNCH_CHECK();
   return out;
 }
@@ -844,6 +1014,7 @@ TORCH_LIBRARY_IMPL(sftamd, CUDA, m) {
   m.impl("lora_bwd_dx", &lora_bwd_dx);
   m.impl("lora_tsum", &lora_tsum);
   m.impl("lora_dxa", &lora_dxa);
+  m.impl("lora_dxa_blocks", &lora_dxa_blocks);
   m.impl("lora_grad_out", &lora_grad_out);
   m.impl("lora_grad_out2", &lora_grad_out2);
 }

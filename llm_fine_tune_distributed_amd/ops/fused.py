@@ -984,17 +984,22 @@ def _scatter_grads(total: torch.Tensor, params, blocks, tr: bool):
     return out
 
 
-def _lora_dxa(dy2d: torch.Tensor, bc: torch.Tensor, s: float) -> torch.Tensor:
-    """s dy Bc for the adapters' B columns Bc [n, R] of the wide weight (a thin-N GEMM: the HIP streaming kernel where
-    the layout allows, torch.addmm with the scale as alpha otherwise)."""
+def _lora_dxa(dy2d: torch.Tensor, bc: torch.Tensor, s: float, meta=None, r: int = 0) -> torch.Tensor:
+    """s dy Bc for the adapters' B columns Bc [n, R] of the wide weight (a thin-N GEMM: the HIP streaming kernels where
+    the layout allows, torch.addmm with the scale as alpha otherwise). ``meta`` [(o, rows, c)] / ``r``: Bc's
+    block-diagonal layout (sub-projection rows [o, o + rows) x columns [c, c + r), zero elsewhere)."""
     R = bc.shape[1]
-    # wide dy (gate_up's 22016 columns): every workgroup re-reads all of Bc from L2 in 64-B row pieces, as many bytes
-    # as its dy rows — hipBLASLt's addmm is faster there (107 vs 133 us, profiles/r5_lora.md)
-    if (dy2d.shape[1] <= 4096 and _ext.use_hip(dy2d) and dy2d.dtype == torch.bfloat16 and bc.dtype == torch.bfloat16
-            and R % 16 == 0
+    if not (_ext.use_hip(dy2d) and dy2d.dtype == torch.bfloat16 and bc.dtype == torch.bfloat16 and R % 16 == 0
             and 16 <= R <= 64 and dy2d.stride(1) == 1 and dy2d.stride(0) % 8 == 0 and dy2d.data_ptr() % 16 == 0
             and dy2d.shape[1] % 8 == 0 and bc.stride(1) == 1 and bc.stride(0) % 8 == 0 and bc.data_ptr() % 16 == 0):
+        return torch.addmm(dy2d.new_empty(dy2d.shape[0], R), dy2d, bc, beta=0, alpha=s)
+    if dy2d.shape[1] <= 4096:
         return _ext.ops().lora_dxa(dy2d, bc, float(s))
+    # wide dy (gate_up's 22016 columns): the dense kernel re-reads all of Bc per 32 token rows (133 vs 107 us for
+    # addmm); the block kernel reads each block's dy columns against only that block's r columns, in pieces
+    if meta is not None and r in (16, 32) and len(meta) <= 4 and all(o % 8 == 0 and c % 8 == 0 for o, _, c in meta):
+        return _ext.ops().lora_dxa_blocks(dy2d, bc, [m[0] for m in meta], [m[1] for m in meta], [m[2] for m in meta],
+                                          int(r), float(s))
     return torch.addmm(dy2d.new_empty(dy2d.shape[0], R), dy2d, bc, beta=0, alpha=s)
 
 
@@ -1150,7 +1155,7 @@ def _lora_wide_bwd(X, acat, wide, ab, state, dy2d, need_dx, gu=None):
         dy2d = dy2d.contiguous()
     base = dgrad_mm(dy2d, wide[:, :K])              # [T, K] (HIP 4-wave dgrad where the shapes allow)
     # dxa = s dy B_blockdiag [T, R]: one streaming pass over dy (csrc/lora.hip dxa_kernel, the scale in its epilogue)
-    dxa = _lora_dxa(dy2d, wide[:, K:K + R], scaling)
+    dxa = _lora_dxa(dy2d, wide[:, K:K + R], scaling, meta, r)
     # the adapter gradients of all sub-projections, each from one pass over its wide operand, scattered straight into
     # the parameters' flat gradient slices in one launch (no per-adapter GEMMs, slicing copies or autograd
     # accumulation): dB^T = (s xa)^T dy [R, n_out] (block (c_i, o_i) transposed is dB_i); dA = dxa^T dropout(x)

@@ -568,6 +568,28 @@ def test_lora_dxa_vs_fp32(T, n, R, ldb):
     assert rel_err(got, want) < 5e-3 and _elem_ok(got, want)
 
 
+@pytest.mark.parametrize("T,blocks,r", [(8192, (11008, 11008), 16), (200, (2048, 512, 512), 16), (77, (1000, 1512), 32),
+                                        (640, (3000,), 16), (130, (256, 264, 8, 4096), 16)])
+def test_lora_dxa_blocks_vs_fp32(T, blocks, r):
+    """dxa = s dy Bc for a block-diagonal Bc (csrc/lora.hip dxa_piece_kernel + dxa_finish_kernel): each block's dy
+    columns cut into pieces, partials summed per block; ragged T, blocks that are not a multiple of the 256-column
+    chunk, up to 4 blocks, every element checked (columns outside every block stay zero)."""
+    torch.manual_seed(5)
+    n, K = sum(blocks), 64
+    R = r * len(blocks)
+    dy = torch.randn(T, n, device=DEV, dtype=torch.bfloat16)
+    wide = torch.zeros(n, K + R + 64, device=DEV, dtype=torch.bfloat16)
+    o = [sum(blocks[:i]) for i in range(len(blocks))]
+    c = [r * i for i in range(len(blocks))]
+    for i, rows in enumerate(blocks):
+        wide[o[i]:o[i] + rows, K + c[i]:K + c[i] + r] = torch.randn(rows, r, device=DEV).to(torch.bfloat16)
+    bc = wide[:, K:K + R]
+    got = _ext.ops().lora_dxa_blocks(dy, bc, o, list(blocks), c, r, 0.5)
+    want = 0.5 * (dy.float() @ bc.float())
+    assert got.shape == (T, R)
+    assert rel_err(got, want) < 5e-3 and _elem_ok(got, want)
+
+
 @pytest.mark.parametrize("cfg", [0, 2, 5, 6, 11])
 @pytest.mark.parametrize("M,N,K", [(256, 256, 64), (512, 512, 128), (256, 512, 192), (512, 768, 256), (768, 512, 2112),
                                    (2048, 3072, 320)])
