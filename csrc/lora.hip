@@ -54,12 +54,12 @@ __device__ __forceinline__ f32x4 mfma(const bf16x8& a, const bf16x8& b, const f3
   return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
 }
 
-// block = 8 waves, 16 rows, streamed in 512-column chunks: each wave instruction reads or writes 2 rows x 512
-// contiguous bytes. The thread's piece of the chunk is copied to X', masked (dropout) into an LDS tile [16][512 + 8]
-// (and to xd when asked), and wave w reads its 64 columns of the tile as MFMA A fragments (ds_read_b128; the 16-byte
-// row padding spreads the 16 rows over all banks) against rows of A_cat loaded straight from global memory in
-// fragment layout. The next chunk's global loads are issued before this chunk's stores, LDS write and MFMAs; two LDS
-// tiles alternate, one barrier per chunk. (The first version loaded x itself in fragment layout, every wave
+// block = 8 waves, 16 rows, streamed in 512-column chunks; wave w loads and consumes columns 64 w .. 64 w + 63 of
+// each chunk (each wave instruction reads or writes 8 rows x 128 contiguous bytes). The lane's pieces are copied to
+// X', masked (dropout) into an LDS tile [16][512 + 8] (and to xd when asked), and the wave reads its 64 columns of the
+// tile back as MFMA A fragments (ds_read_b128; the 16-byte row padding spreads the 16 rows over all banks) against
+// rows of A_cat loaded straight from global memory in fragment layout. The next chunk's global loads are issued before
+// this chunk's stores, LDS write and MFMAs; two LDS tiles alternate; the waves only meet at the final reduction. (The first version loaded x itself in fragment layout, every wave
 // instruction touching 16 rows x 64 B: 153.9 vs 128.5 us for the SwiGLU-fused K = 11008 case, 115.8 vs 91.2 plain,
 // tools/bench_lora_kernels.py, r4_run29.)
 // SW: x is the SwiGLU input gu [T, 2K] (gate | up) and the widened activation is act = silu(gate) * up, rounded to bf16
@@ -74,12 +74,19 @@ __global__ __launch_bounds__(512) void fwd_kernel(const u16* __restrict__ x, con
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int g = lane >> 4, r = lane & 15;
   const long t0 = (long)blockIdx.x * 16;
-  // loader role: row lr of the block, columns 8 lc + 256 h of the chunk
-  const int lr = tid >> 5, lc = (tid & 31) * 8;
-  const long lt = t0 + lr;
-  const bool lok = lt < T;
-  const long ltc = lok ? lt : T - 1;
-  const u16* xrow = x + ltc * (SW ? 2L * K : (long)K);
+  // loader role: rows (lane >> 3) + 8 h of the block, columns lc .. lc + 7 of the chunk — wave w loads exactly the
+  // 64 columns its MFMAs read (8 rows x 128 B per wave instruction), so the LDS tile regions are wave-private and the
+  // chunk loop needs no workgroup barrier
+  const int lc = 64 * w + 8 * (lane & 7);
+  long lt[2];
+  bool lok[2];
+  const u16* xrow[2];
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    lt[h] = t0 + (lane >> 3) + 8 * h;
+    lok[h] = lt[h] < T;
+    xrow[h] = x + (lok[h] ? lt[h] : T - 1) * (SW ? 2L * K : (long)K);
+  }
   f32x4 acc[RF];
 #pragma unroll
   for (int j = 0; j < RF; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -87,9 +94,9 @@ __global__ __launch_bounds__(512) void fwd_kernel(const u16* __restrict__ x, con
   auto load = [&](uint4 (&dst)[2][NV], int k0) {
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
-      const int c = k0 + lc + 256 * h, cc = c < K ? c : 0;
-      dst[h][0] = *(const uint4*)(xrow + cc);
-      if constexpr (SW) dst[h][1] = *(const uint4*)(xrow + K + cc);
+      const int c = k0 + lc, cc = c < K ? c : 0;
+      dst[h][0] = *(const uint4*)(xrow[h] + cc);
+      if constexpr (SW) dst[h][1] = *(const uint4*)(xrow[h] + K + cc);
     }
   };
   // the wave's A_cat fragments of a chunk (rows 16 j + r, columns 64 w + 32 ks + 8 g): loaded one chunk ahead for
@@ -145,24 +152,27 @@ __global__ __launch_bounds__(512) void fwd_kernel(const u16* __restrict__ x, con
     u16(*tile)[XP] = xs[ch & 1];
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
-      const int c = k0 + lc + 256 * h;
+      const int c = k0 + lc;
       if (c < K) {
-        if (lok) *(uint4*)(X + lt * ldX + c) = v[h];
+        if (lok[h]) *(uint4*)(X + lt[h] * ldX + c) = v[h];
         if (drop) {
-          const unsigned bits = keep8((unsigned long long)lt * K + c, seed, thresh);
-          if (xd && lok) {  // dropout(x) itself, scaled (tests / save_xd only)
+          const unsigned bits = keep8((unsigned long long)lt[h] * K + c, seed, thresh);
+          if (xd && lok[h]) {  // dropout(x) itself, scaled (tests / save_xd only)
             float f[8];
             unpack8(v[h], f);
 #pragma unroll
             for (int i = 0; i < 8; ++i) f[i] = ((bits >> i) & 1u) ? f[i] * dscale : 0.f;
-            *(uint4*)(xd + lt * K + c) = pack8(f);
+            *(uint4*)(xd + lt[h] * K + c) = pack8(f);
           }
           v[h] = mask8(v[h], bits);  // the 1 / (1 - p) scale goes into s below
         }
-        *(uint4*)&tile[lr][lc + 256 * h] = v[h];
+        *(uint4*)&tile[(lane >> 3) + 8 * h][lc] = v[h];
       }
     }
-    __syncthreads();  // the tile is complete (and the other tile's readers finished before the previous barrier)
+    // the wave's own tile columns are complete (its reads of this tile two chunks ago came earlier in program order)
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
       const int kl = 64 * w + 32 * ks + 8 * g;
