@@ -65,6 +65,21 @@ __device__ __forceinline__ unsigned hash_u32(unsigned long long i, unsigned seed
   return x;
 }
 
+// Dropout keep bit of element i (LoRA dropout, dropout_add): the even / odd element of each pair shares ONE hash, its
+// low / high 16 bits compared against a 16-bit threshold p * 65536 (half the hashing of one hash per element; p is
+// resolved to 1 / 65536). Regenerated in backward from (seed, index); twin: ops/reference.py dropout_keep.
+__device__ __forceinline__ bool drop_keep(unsigned long long i, unsigned seed, unsigned thresh16) {
+  const unsigned h = hash_u32(i >> 1, seed);
+  return ((i & 1) ? (h >> 16) : (h & 0xFFFFu)) >= thresh16;
+}
+
+// (16-bit keep threshold, 1 / (1 - p)) of a dropout probability (clamped to [0, 0.999])
+inline unsigned drop_thresh16(double p, float* scale) {
+  const double pc = p < 0 ? 0 : (p > 0.999 ? 0.999 : p);
+  *scale = (float)(1.0 / (1.0 - pc));
+  return (unsigned)(pc * 65536.0);
+}
+
 inline hipStream_t cur_stream() { return c10::hip::getCurrentHIPStream().stream(); }
 
 inline int num_cus() { return 256; }  // MI355X: 8 XCDs x 32 CUs

@@ -298,7 +298,7 @@ void embedding_bwd(const at::Tensor& dy, const at::Tensor& sorted_ids, const at:
 }
 
 // ---------------------------------------------------------------------------------------------
-// LoRA dropout: out[t,k] = a[t,k] + keep(t*K+k) * b[t,k] / (1-p), keep = hash(index, seed) >= p*2^32.
+// LoRA dropout: out[t,k] = a[t,k] + keep(t*K+k) * b[t,k] / (1-p), keep = drop_keep(index, seed) (common.h).
 // The mask is a pure function of (seed, element index), so backward regenerates it instead of
 // storing it; a and b may be column slices of wider buffers (row strides lda, ldb).
 // grid: (column blocks of 256 x 8 elements, rows); no integer division in the index math
@@ -318,7 +318,7 @@ __global__ __launch_bounds__(256) void dropout_add_kernel(const u16* __restrict_
   }
   const unsigned long long idx = (unsigned long long)t * K + k;
 #pragma unroll
-  for (int i = 0; i < 8; ++i) o[i] += hash_u32(idx + i, seed) >= thresh ? bv[i] * scale : 0.f;
+  for (int i = 0; i < 8; ++i) o[i] += drop_keep(idx + i, seed, thresh) ? bv[i] * scale : 0.f;
   *(uint4*)(out + t * ldo + k) = pack8(o);
   }
 }
@@ -337,17 +337,12 @@ __global__ __launch_bounds__(256) void lora_widen_kernel(const u16* __restrict__
     unpack8(v, f);
     const unsigned long long idx = (unsigned long long)t * K + k;
 #pragma unroll
-    for (int i = 0; i < 8; ++i) f[i] = hash_u32(idx + i, seed) >= thresh ? f[i] * scale : 0.f;
+    for (int i = 0; i < 8; ++i) f[i] = drop_keep(idx + i, seed, thresh) ? f[i] * scale : 0.f;
     *(uint4*)(xd + t * (long)K + k) = pack8(f);
   }
   }
 }
 
-static unsigned drop_thresh(double p, float* scale) {
-  const double pc = p < 0 ? 0 : (p > 0.999 ? 0.999 : p);
-  *scale = (float)(1.0 / (1.0 - pc));
-  return (unsigned)(pc * 4294967296.0);
-}
 
 at::Tensor dropout_add(const c10::optional<at::Tensor>& a, const at::Tensor& b, double p, int64_t seed) {
   SFT_CHECK_CUDA(b);
@@ -366,7 +361,7 @@ at::Tensor dropout_add(const c10::optional<at::Tensor>& a, const at::Tensor& b, 
   auto out = at::empty({T, K}, b.options());
   if (T == 0) return out;
   float scale;
-  const unsigned thresh = drop_thresh(p, &scale);
+  const unsigned thresh = drop_thresh16(p, &scale);
   dim3 grid((K / 8 + 255) / 256, (unsigned)std::min<long>(T, 65535));
   dropout_add_kernel<<<grid, 256, 0, cur_stream()>>>(ap, lda, (const u16*)b.data_ptr(), b.stride(0), (u16*)out.data_ptr(),
                                                      K, T, K, thresh, scale, (unsigned)seed);
@@ -386,7 +381,7 @@ std::tuple<at::Tensor, at::Tensor> lora_widen(const at::Tensor& x, int64_t R, do
   at::Tensor xd = p > 0 ? at::empty_like(x) : at::empty({0}, x.options());
   if (T == 0) return {X, xd};
   float scale;
-  const unsigned thresh = drop_thresh(p, &scale);
+  const unsigned thresh = drop_thresh16(p, &scale);
   dim3 grid((K / 8 + 255) / 256, (unsigned)std::min<long>(T, 65535));
   lora_widen_kernel<<<grid, 256, 0, cur_stream()>>>((const u16*)x.data_ptr(), (u16*)X.data_ptr(), K + R,
                                                     p > 0 ? (u16*)xd.data_ptr() : nullptr, T, K, thresh, scale,

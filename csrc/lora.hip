@@ -13,7 +13,7 @@
 //                16x16x16 MFMAs whose B columns are permuted so every lane holds 8 contiguous outputs.
 //   lora_tsum:   the adapter gradients' token reductions (dA, dB^T), one pass over the wide operand.
 //
-// The dropout mask is hash_u32(t*K + k, seed) >= p * 2^32 (common.h; keep8 below computes it per 8-element chunk),
+// The dropout mask is drop_keep(t*K + k, seed, p * 65536) (common.h; keep8 below computes it per 8-element chunk),
 // identical to dropout_add and to the PyTorch reference, so nothing but the seed is stored between forward and
 // backward.
 #include "common.h"
@@ -21,22 +21,24 @@
 namespace sftamd {
 namespace lora {
 
-// keep bits of the 8 elements i0 .. i0 + 7 (bit j: hash_u32(i0 + j, seed) >= thresh), bit-identical to hash_u32:
-// with i0 % 8 == 0 the eight indices share the high word (no carry out of the low one), so the first multiply of the
-// hash becomes a constant add per element and the high-word / seed terms are computed once per chunk.
+// keep bits of the 8 elements i0 .. i0 + 7 (bit j: drop_keep(i0 + j, seed, thresh16), common.h), bit-identical: the 8
+// elements are 4 pairs, one hash each (low / high 16 bits for the even / odd element); with i0 % 8 == 0 the 4 pair
+// indices share the high word (no carry out of the low one), so the first multiply of the hash becomes a constant add
+// per pair and the high-word / seed terms are computed once per chunk.
 __device__ __forceinline__ unsigned keep8(unsigned long long i0, unsigned seed, unsigned thresh) {
-  const unsigned lo = (unsigned)i0 * 0x9E3779B9u;
-  const unsigned hi = (unsigned)(i0 >> 32) * 0x85EBCA6Bu ^ seed * 0xC2B2AE35u;
+  const unsigned long long q0 = i0 >> 1;
+  const unsigned lo = (unsigned)q0 * 0x9E3779B9u;
+  const unsigned hi = (unsigned)(q0 >> 32) * 0x85EBCA6Bu ^ seed * 0xC2B2AE35u;
   unsigned bits = 0;
 #pragma unroll
-  for (int j = 0; j < 8; ++j) {
+  for (int j = 0; j < 4; ++j) {
     unsigned x = (lo + (unsigned)j * 0x9E3779B9u) ^ hi;
     x ^= x >> 16;
     x *= 0x7FEB352Du;
     x ^= x >> 15;
     x *= 0x846CA68Bu;
     x ^= x >> 16;
-    bits |= (unsigned)(x >= thresh) << j;
+    bits |= ((unsigned)((x & 0xFFFFu) >= thresh) << (2 * j)) | ((unsigned)((x >> 16) >= thresh) << (2 * j + 1));
   }
   return bits;
 }
@@ -487,11 +489,7 @@ __global__ __launch_bounds__(256) void copy2d_batch_kernel(const long long* __re
   }
 }
 
-static unsigned thresh_of(double p, float* dscale) {
-  const double pc = p < 0 ? 0 : (p > 0.999 ? 0.999 : p);
-  *dscale = (float)(1.0 / (1.0 - pc));
-  return (unsigned)(pc * 4294967296.0);
-}
+static unsigned thresh_of(double p, float* dscale) { return drop_thresh16(p, dscale); }
 
 }  // namespace lora
 

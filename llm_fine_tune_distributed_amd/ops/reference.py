@@ -171,12 +171,20 @@ def bf16_stochastic_round(x: torch.Tensor, seed: int, offset: int = 0) -> torch.
     return torch.where(finite, res, xf.to(torch.bfloat16)).view(x.shape)
 
 
+def dropout_keep(idx: torch.Tensor, seed: int, p: float) -> torch.Tensor:
+    """Twin of csrc/common.h drop_keep: elements 2q and 2q + 1 share hash(q, seed), whose low / high 16 bits are
+    compared with int(p * 65536)."""
+    h = hash_u32(idx >> 1, seed)
+    half = torch.where((idx & 1) == 1, h >> 16, h & 0xFFFF)
+    return half >= int(min(max(float(p), 0.0), 0.999) * 65536.0)
+
+
 def dropout_add(a: Optional[torch.Tensor], b: torch.Tensor, p: float, seed: int) -> torch.Tensor:
-    """(a or 0) + b * keep / (1-p), keep = hash(t*K + k, seed) >= p * 2^32 (same mask as the HIP kernel)."""
+    """(a or 0) + b * keep / (1-p), keep = dropout_keep(t*K + k) (same mask as the HIP kernels)."""
     T, K = b.shape
     p = min(max(float(p), 0.0), 0.999)
     idx = torch.arange(T * K, device=b.device, dtype=torch.int64).view(T, K)
-    keep = hash_u32(idx, seed) >= int(p * 4294967296.0)
+    keep = dropout_keep(idx, seed, p)
     out = torch.where(keep, b.float() * (1.0 / (1.0 - p)), torch.zeros((), device=b.device))
     if a is not None:
         out = out + a.float()

@@ -4,7 +4,7 @@ set -o pipefail
 cd $GRAFT_REPO_ROOT
 mkdir -p gpurun_out
 export TMPDIR=/tmp
-timeout -k 10 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_kernels_gpu.py tests/test_model_gpu.py -k "lora" > gpurun_out/r5_20_tests.log 2>&1 || { tail -30 gpurun_out/r5_20_tests.log; exit 1; }
+timeout -k 10 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_kernels_gpu.py tests/test_model_gpu.py -k "lora or dropout" > gpurun_out/r5_20_tests.log 2>&1 || { tail -30 gpurun_out/r5_20_tests.log; exit 1; }
 tail -1 gpurun_out/r5_20_tests.log
 timeout -k 10 200 python -u tools/bench_lora_kernels.py > gpurun_out/r5_20_kern.log 2>&1 || { tail -20 gpurun_out/r5_20_kern.log; exit 1; }
 grep -v amdgpu.ids gpurun_out/r5_20_kern.log
