@@ -1,5 +1,6 @@
 #!/bin/bash
-# LoRA: block dxa + wave-private widening — tests, standalone kernels, dxa microbench, LoRA step x2
+# LoRA: block dxa, wave-private widening, paired-hash dropout, wave-private wide tsum (A/B) — tests, standalone
+# kernels, dxa microbench, LoRA step A/B
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 mkdir -p gpurun_out
@@ -10,7 +11,7 @@ timeout -k 10 200 python -u tools/bench_lora_kernels.py > gpurun_out/r5_20_kern.
 grep -v amdgpu.ids gpurun_out/r5_20_kern.log
 timeout -k 10 200 python -u tools/bench_lora_dxa.py > gpurun_out/r5_20_dxa.log 2>&1 || { tail -20 gpurun_out/r5_20_dxa.log; exit 1; }
 grep -v amdgpu.ids gpurun_out/r5_20_dxa.log
-for i in 1 2; do
-  timeout -k 10 200 python -u bench.py --freeze-policy lora --steps 20 --warmup 5 > gpurun_out/r5_20_lora$i.log 2>&1 || { tail -20 gpurun_out/r5_20_lora$i.log; exit 1; }
-  echo "lora $(grep -o '"value": [0-9.]*' gpurun_out/r5_20_lora$i.log)"
+for v in 1 0 1 0; do
+  SFTAMD_LORA_TSUM_WP=$v timeout -k 10 200 python -u bench.py --freeze-policy lora --steps 20 --warmup 5 > gpurun_out/r5_20_lora$v.log 2>&1 || { tail -20 gpurun_out/r5_20_lora$v.log; exit 1; }
+  echo "lora wp$v $(grep -o '"value": [0-9.]*' gpurun_out/r5_20_lora$v.log)"
 done
