@@ -146,8 +146,9 @@ def test_default_path_llama3_8b_widths_vs_fp32_reference(monkeypatch):
     assert tr.get("attn.bwd_rope_epi", 0) == 4, tr  # every Llama layer is a RoPE layer
     # qkv + RoPE: 32 x 24 = 768 tiles = 3 whole rounds, so no 256 x 128 tail launch
     assert tr.get("tn.rope.c11", 0) == 4 and "tn.rope.tail" not in tr, tr
-    # no Llama shape has a TunableOp selection: o / gate_up / down of the 4 layers + lm_head on the row-contiguous kernel
-    assert tr.get("tn.c60", 0) == 13, tr
+    # o / gate_up / down at 8192 tokens have TunableOp selections (hipBLASLt / rocBLAS, 49.6 vs 48.3 samples/s for the
+    # row-contiguous kernel in the 8B bench); the reduced-vocabulary lm_head has none: the row-contiguous kernel
+    assert tr.get("tn.c60", 0) == 1, tr
     for c in (13, 1213, 9):  # wgrad: gate_up / down / lm_head (4-wave ring), qkv (hybrid split-K), o (8-wave ring)
         assert tr.get(f"wgrad.c{c}", 0) > 0, (c, tr)
     assert tr.get("wgrad.norm_slots", 0) > 0, tr
