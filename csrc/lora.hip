@@ -332,28 +332,22 @@ __device__ __forceinline__ bf16x8 lds_tr8(const u16* p0, const u16* p1) {
   return __builtin_bit_cast(bf16x8, v);
 }
 
-// WP (KT = 4): wave-private stages — wave w loads the 64 columns of X it reduces (8 rows x 128 B per instruction)
-// and its own copy of the S tile, so the stage loop needs no workgroup barrier.
-template <int RF, int KT, bool WP = false>  // KT 16-row k tiles per wave: a workgroup covers 64 KT columns of k
+template <int RF, int KT>  // KT 16-row k tiles per wave: a workgroup covers 64 KT columns of k
 __global__ __launch_bounds__(256) void tsum_kernel(const u16* __restrict__ X, long ldX, const u16* __restrict__ S,
                                                    long ldS, float* __restrict__ out, long T, int K, long tc,
                                                    unsigned thresh, float dscale, unsigned seed, int drop) {
-  static_assert(!WP || KT == 4, "wave-private stages: 64 columns per wave");
   constexpr int R = 16 * RF, ST = 64, NK = 64 * KT;
   // row pitches padded so that a transposed read's 4 rows x 4 column groups hit distinct banks (pitch = 36 dwords
   // mod 64) and rows stay 16-byte aligned
   constexpr int XP = NK + (KT == 1 ? 8 : 72), SP = R + 8;
-  constexpr int TPR = WP ? 8 : NK / 8, RPP = WP ? 8 : 256 / TPR, XH = ST / RPP;  // X threads per row, rows per pass
-  constexpr int SCH = ST * R / 8, NT = WP ? 64 : 256, SPT = (SCH + NT - 1) / NT;  // S chunks of 8: per stage, thread
+  constexpr int TPR = NK / 8, RPP = 256 / TPR, XH = ST / RPP;  // X chunk threads per row, rows per pass, passes
+  constexpr int SCH = ST * R / 8, SPT = (SCH + 255) / 256;       // S chunks of 8 per stage, per thread
   __shared__ __attribute__((aligned(16))) u16 xs[ST][XP];
-  __shared__ __attribute__((aligned(16))) u16 ssm[WP ? 4 : 1][ST][SP];
+  __shared__ __attribute__((aligned(16))) u16 ss[ST][SP];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, g = lane >> 4, r16 = lane & 15;
-  u16 (*ss)[SP] = ssm[WP ? w : 0];
-  const int st_id = WP ? lane : tid;  // S loader index
   const int k0 = blockIdx.x * NK;
   const long t_begin = (long)blockIdx.y * tc, t_end = min(T, t_begin + tc);
-  // X chunks: rows tr + RPP h of the stage, columns cx .. cx + 7 of the tile
-  const int tr = WP ? lane >> 3 : tid / TPR, cx = WP ? 64 * w + 8 * (lane & 7) : 8 * (tid % TPR);
+  const int tr = tid / TPR, cx = 8 * (tid % TPR);  // X chunks: rows tr + RPP h of the stage, columns cx .. cx + 7
   const int k = k0 + cx;
   f32x4 acc[KT][RF];
 #pragma unroll
@@ -369,7 +363,7 @@ __global__ __launch_bounds__(256) void tsum_kernel(const u16* __restrict__ X, lo
     }
 #pragma unroll
     for (int u = 0; u < SPT; ++u) {
-      const int e = st_id + NT * u, row = e / (R / 8), cc = e - row * (R / 8);
+      const int e = tid + 256 * u, row = e / (R / 8), cc = e - row * (R / 8);
       const long t = t0 + row;
       sv[u] = (e < SCH && t < t_end) ? *(const uint4*)(S + t * ldS + 8 * cc) : make_uint4(0, 0, 0, 0);
     }
@@ -379,7 +373,7 @@ __global__ __launch_bounds__(256) void tsum_kernel(const u16* __restrict__ X, lo
   const int q = r16 >> 2, p = r16 & 3;
   load(t_begin);
   for (long t0 = t_begin; t0 < t_end; t0 += ST) {
-    if constexpr (!WP) __syncthreads();  // the previous stage's reads are done (WP: the wave's own, in order)
+    __syncthreads();  // the previous stage's reads are done
 #pragma unroll
     for (int h = 0; h < XH; ++h) {
       uint4 v = xv[h];
@@ -388,16 +382,10 @@ __global__ __launch_bounds__(256) void tsum_kernel(const u16* __restrict__ X, lo
     }
 #pragma unroll
     for (int u = 0; u < SPT; ++u) {
-      const int e = st_id + NT * u, row = e / (R / 8), cc = e - row * (R / 8);
+      const int e = tid + 256 * u, row = e / (R / 8), cc = e - row * (R / 8);
       if (e < SCH) *(uint4*)&ss[row][8 * cc] = sv[u];
     }
-    if constexpr (WP) {
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-      __builtin_amdgcn_wave_barrier();
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    } else {
-      __syncthreads();
-    }
+    __syncthreads();
     if (t0 + ST < t_end) load(t0 + ST);  // the next stage's loads fly under this stage's MFMAs
 #pragma unroll
     for (int ks = 0; ks < ST / 32; ++ks) {
@@ -927,20 +915,16 @@ at::Tensor lora_tsum(const at::Tensor& X, int64_t K, const at::Tensor& S, double
   // 64-column ones on about 1024. The token range is split into chunks of whole 64-token stages.
   const bool wide = K >= 8192;
   const int nk = wide ? 256 : 64, nkb = (int)((K + nk - 1) / nk);
-  // (768 / 1024 workgroups for the dropout-regenerating wide dA measured neutral in the LoRA step, r5_run16)
+  // (768 / 1024 workgroups for the dropout-regenerating wide dA measured neutral in the LoRA step, r5_run16; wave-private
+  // stages — each wave loading its own 64 columns and S copy, no barriers — 37.3 vs 38.0 us for dA but 74.1 vs 68.0
+  // for gate_up's dB^T, r5_run20: not kept)
   long splits = std::max(1L, std::min((T + 63) / 64, (wide ? 512L : 1024L) / nkb));
   const long tc = ((T + splits - 1) / splits + 63) / 64 * 64;
   splits = (T + tc - 1) / tc;
   auto out = at::empty({splits, R, K}, X.options().dtype(at::kFloat));  // every element written by one workgroup
   dim3 grid(nkb, (unsigned)splits);
-  const char* ewp = getenv("SFTAMD_LORA_TSUM_WP");  // temporary A/B switch
-  const bool wp = !(ewp && ewp[0] == '0');
 #define LORA_TSUM(RF)                                                                                             \
-  if (wide && wp)                                                                                                 \
-    lora::tsum_kernel<RF, 4, true><<<grid, 256, 0, cur_stream()>>>((const u16*)X.data_ptr(), X.stride(0),        \
-        (const u16*)S.data_ptr(), S.stride(0), out.data_ptr<float>(), T, (int)K, tc, thresh, dscale,             \
-        (unsigned)seed, p > 0 ? 1 : 0);                                                                          \
-  else if (wide)                                                                                                  \
+  if (wide)                                                                                                       \
     lora::tsum_kernel<RF, 4><<<grid, 256, 0, cur_stream()>>>((const u16*)X.data_ptr(), X.stride(0),              \
         (const u16*)S.data_ptr(), S.stride(0), out.data_ptr<float>(), T, (int)K, tc, thresh, dscale,             \
         (unsigned)seed, p > 0 ? 1 : 0);                                                                          \

@@ -993,13 +993,15 @@ def _lora_dxa(dy2d: torch.Tensor, bc: torch.Tensor, s: float, meta=None, r: int 
             and 16 <= R <= 64 and dy2d.stride(1) == 1 and dy2d.stride(0) % 8 == 0 and dy2d.data_ptr() % 16 == 0
             and dy2d.shape[1] % 8 == 0 and bc.stride(1) == 1 and bc.stride(0) % 8 == 0 and bc.data_ptr() % 16 == 0):
         return torch.addmm(dy2d.new_empty(dy2d.shape[0], R), dy2d, bc, beta=0, alpha=s)
-    if dy2d.shape[1] <= 4096:
-        return _ext.ops().lora_dxa(dy2d, bc, float(s))
-    # wide dy (gate_up's 22016 columns): the dense kernel re-reads all of Bc per 32 token rows (133 vs 107 us for
-    # addmm); the block kernel reads each block's dy columns against only that block's r columns, in pieces
-    if meta is not None and r in (16, 32) and len(meta) <= 4 and all(o % 8 == 0 and c % 8 == 0 for o, _, c in meta):
+    # several sub-projections (qkv, gate_up): the block kernel reads each block's dy columns against only that block's
+    # r columns, in pieces (gate_up 89.5 vs 107.0 us for addmm and 135.1 for the dense kernel, which re-reads all of
+    # Bc per 32 token rows; qkv 17.8 vs 23.9 dense; r5_run20); one block (o, down): the dense kernel (13.0-13.2 vs 14.4)
+    if (meta is not None and len(meta) > 1 and r in (16, 32) and len(meta) <= 4
+            and all(o % 8 == 0 and c % 8 == 0 for o, _, c in meta)):
         return _ext.ops().lora_dxa_blocks(dy2d, bc, [m[0] for m in meta], [m[1] for m in meta], [m[2] for m in meta],
                                           int(r), float(s))
+    if dy2d.shape[1] <= 4096:
+        return _ext.ops().lora_dxa(dy2d, bc, float(s))
     return torch.addmm(dy2d.new_empty(dy2d.shape[0], R), dy2d, bc, beta=0, alpha=s)
 
 

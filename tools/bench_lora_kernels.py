@@ -61,15 +61,6 @@ def main():
              for r in (48, 32, 16)]
     rows += [(f"lora_fwd K=2048 R={r}", lambda r=r: ops.lora_fwd(xs, As[r], 0.5, 0.05, 1, Hs + 128), 2 * T * Hs * 2)
              for r in (48, 32, 16)]
-    def env(fn, v):  # temporary A/B: the wide tsum's wave-private stages (SFTAMD_LORA_TSUM_WP=0: shared stages)
-        def run():
-            os.environ["SFTAMD_LORA_TSUM_WP"] = v
-            return fn()
-        return run
-    for v in ("0", "1"):
-        rows += [(f"[wp{v}] lora_tsum dA K=11008 R=16", env(lambda: ops.lora_tsum(base, I, dxa, 0.05, 1), v), T * I * 2),
-                 (f"[wp{v}] lora_tsum dB n=22016 R=32", env(lambda: ops.lora_tsum(gu, 2 * I, dxa2, 0.0, 0), v),
-                  T * 2 * I * 2)]
     a = torch.randn(8192, 8192, device=dev, dtype=torch.bfloat16)
     for _ in range(200):  # ~1 s of GEMMs first: the clocks ramp up before anything is timed
         a @ a

@@ -74,7 +74,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--model", default="llama3-8b")
     ap.add_argument("--steps", type=int, default=13)
-    ap.add_argument("--reps", type=int, default=4)
+    ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--batch", type=int, default=16)
     ap.add_argument("--seq", type=int, default=512)
     ap.add_argument("--no-overlap", action="store_true")
