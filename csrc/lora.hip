@@ -66,11 +66,12 @@ __device__ __forceinline__ f32x4 mfma(const bf16x8& a, const bf16x8& b, const f3
 // tools/bench_lora_kernels.py, r4_run29.)
 // SW: x is the SwiGLU input gu [T, 2K] (gate | up) and the widened activation is act = silu(gate) * up, rounded to bf16
 // as the SwiGLU kernel does (the LoRA MLP's down projection: no separate SwiGLU pass, no act tensor).
-template <int RF, bool SW = false, int NCH = 0>  // R = 16 * RF adapter columns; NCH > 0: K == 512 NCH
+// PD: streamed chunks in flight ahead of the one being processed (NCH == 0)
+template <int RF, bool SW = false, int NCH = 0, int PD = 1>  // R = 16 * RF adapter columns; NCH > 0: K == 512 NCH
 __global__ __launch_bounds__(512) void fwd_kernel(const u16* __restrict__ x, const u16* __restrict__ A,
                                                   u16* __restrict__ X, u16* __restrict__ xd, long T, int K, long ldX,
                                                   float s, unsigned thresh, float dscale, unsigned seed, int drop) {
-  constexpr int R = 16 * RF, NW = 8, CK = 512, XP = CK + 8, NV = SW ? 2 : 1, DEP = NCH > 0 ? NCH : 1;
+  constexpr int R = 16 * RF, NW = 8, CK = 512, XP = CK + 8, NV = SW ? 2 : 1, DEP = NCH > 0 ? NCH : PD;
   __shared__ __attribute__((aligned(16))) u16 xs[2][16][XP];
   __shared__ float red[NW][16][R + 1];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
@@ -119,7 +120,9 @@ __global__ __launch_bounds__(512) void fwd_kernel(const u16* __restrict__ x, con
 #pragma unroll
     for (int c = 0; c < NCH; ++c) load(rw[c], c * CK);
   } else {
-    load(rw[0], 0);
+#pragma unroll
+    for (int c = 0; c < PD; ++c)
+      if (c < nch) load(rw[c], c * CK);
   }
   if constexpr (PFA) load_a(0);
 #pragma unroll
@@ -147,8 +150,16 @@ __global__ __launch_bounds__(512) void fwd_kernel(const u16* __restrict__ x, con
 #pragma unroll
         for (int j = 0; j < RF; ++j) ac[ks][j] = an[ks][j];
     }
-    if (ch + 1 < nch) {  // the next chunk flies under this chunk's stores, LDS write and MFMAs
-      if constexpr (NCH == 0) load(rw[0], k0 + CK);
+    if constexpr (NCH == 0) {  // the chunk PD ahead flies under this chunk's stores, LDS write and MFMAs
+#pragma unroll
+      for (int i = 0; i + 1 < PD; ++i)
+#pragma unroll
+        for (int h = 0; h < 2; ++h)
+#pragma unroll
+          for (int q = 0; q < NV; ++q) rw[i][h][q] = rw[i + 1][h][q];
+      if (ch + PD < nch) load(rw[PD - 1], k0 + PD * CK);
+    }
+    if (ch + 1 < nch) {
       if constexpr (PFA) load_a(k0 + CK);
     }
     u16(*tile)[XP] = xs[ch & 1];
@@ -517,20 +528,31 @@ std::tuple<at::Tensor, at::Tensor> lora_fwd(const at::Tensor& x, const at::Tenso
   const unsigned thresh = lora::thresh_of(p, &dscale);
   const int grid = (int)((T + 15) / 16);
   u16* xdp = (p > 0 && save_xd) ? (u16*)xd.data_ptr() : nullptr;
+  const char* epd = getenv("SFTAMD_LORA_FWD_PD");  // temporary A/B switch
+  const int pd = epd && epd[0] ? atoi(epd) : 1;
+#define LORA_FWD_PD(RF, SWB)                                                                                      \
+  if (pd == 3)                                                                                                    \
+    lora::fwd_kernel<RF, SWB, 0, 3><<<grid, 512, 0, cur_stream()>>>((const u16*)x.data_ptr(),                    \
+        (const u16*)A.data_ptr(), (u16*)X.data_ptr(), xdp, T, K, ldX, (float)s, thresh, dscale, (unsigned)seed,   \
+        p > 0 ? 1 : 0);                                                                                           \
+  else if (pd == 2)                                                                                               \
+    lora::fwd_kernel<RF, SWB, 0, 2><<<grid, 512, 0, cur_stream()>>>((const u16*)x.data_ptr(),                    \
+        (const u16*)A.data_ptr(), (u16*)X.data_ptr(), xdp, T, K, ldX, (float)s, thresh, dscale, (unsigned)seed,   \
+        p > 0 ? 1 : 0);                                                                                           \
+  else                                                                                                            \
+    lora::fwd_kernel<RF, SWB><<<grid, 512, 0, cur_stream()>>>((const u16*)x.data_ptr(), (const u16*)A.data_ptr(), \
+        (u16*)X.data_ptr(), xdp, T, K, ldX, (float)s, thresh, dscale, (unsigned)seed, p > 0 ? 1 : 0)
 #define LORA_FWD(RF)                                                                                              \
   if (!swiglu && K == 2048)                                                                                       \
     lora::fwd_kernel<RF, false, 4><<<grid, 512, 0, cur_stream()>>>((const u16*)x.data_ptr(),                     \
                                                                    (const u16*)A.data_ptr(), (u16*)X.data_ptr(), xdp, \
                                                                    T, K, ldX, (float)s, thresh, dscale,          \
                                                                    (unsigned)seed, p > 0 ? 1 : 0);               \
-  else if (swiglu)                                                                                                \
-    lora::fwd_kernel<RF, true><<<grid, 512, 0, cur_stream()>>>((const u16*)x.data_ptr(), (const u16*)A.data_ptr(), \
-                                                               (u16*)X.data_ptr(), xdp, T, K, ldX, (float)s, thresh, \
-                                                               dscale, (unsigned)seed, p > 0 ? 1 : 0);            \
-  else                                                                                                            \
-    lora::fwd_kernel<RF, false><<<grid, 512, 0, cur_stream()>>>((const u16*)x.data_ptr(), (const u16*)A.data_ptr(), \
-                                                                (u16*)X.data_ptr(), xdp, T, K, ldX, (float)s, thresh, \
-                                                                dscale, (unsigned)seed, p > 0 ? 1 : 0)
+  else if (swiglu) {                                                                                              \
+    LORA_FWD_PD(RF, true);                                                                                        \
+  } else {                                                                                                        \
+    LORA_FWD_PD(RF, false);                                                                                       \
+  }
   switch (R / 16) {
     case 1: LORA_FWD(1); break;
     case 2: LORA_FWD(2); break;
@@ -538,6 +560,7 @@ std::tuple<at::Tensor, at::Tensor> lora_fwd(const at::Tensor& x, const at::Tenso
     default: LORA_FWD(4); break;
   }
 #undef LORA_FWD
+#undef LORA_FWD_PD
   SFT_LAUNCH_CHECK();
   return {X, xd};
 }

@@ -61,6 +61,15 @@ def main():
              for r in (48, 32, 16)]
     rows += [(f"lora_fwd K=2048 R={r}", lambda r=r: ops.lora_fwd(xs, As[r], 0.5, 0.05, 1, Hs + 128), 2 * T * Hs * 2)
              for r in (48, 32, 16)]
+    def env(fn, v):  # temporary A/B: the streamed widening's prefetch depth (SFTAMD_LORA_FWD_PD)
+        def run():
+            os.environ["SFTAMD_LORA_FWD_PD"] = v
+            return fn()
+        return run
+    for v in ("1", "2", "3"):
+        rows += [(f"[pd{v}] lora_fwd swiglu K=11008", env(lambda: ops.lora_fwd(gu, A, 0.5, 0.05, 1, I + 128, False, True), v),
+                  3 * T * I * 2),
+                 (f"[pd{v}] lora_fwd K=11008 R=16", env(lambda: ops.lora_fwd(x, A, 0.5, 0.05, 1, I + 128), v), 2 * T * I * 2)]
     a = torch.randn(8192, 8192, device=dev, dtype=torch.bfloat16)
     for _ in range(200):  # ~1 s of GEMMs first: the clocks ramp up before anything is timed
         a @ a
