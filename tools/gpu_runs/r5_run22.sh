@@ -14,3 +14,8 @@ for v in 2 1 3 2 1 3; do
   SFTAMD_LORA_FWD_PD=$v timeout -k 10 300 python -u bench.py --freeze-policy lora --steps 20 --warmup 5 > gpurun_out/r5_22_lora$v.log 2>&1 || { tail -20 gpurun_out/r5_22_lora$v.log; exit 1; }
   echo "lora pd$v $(grep -o '"value": [0-9.]*\|"final_loss": [a-zA-Z0-9.]*' gpurun_out/r5_22_lora$v.log | tr '\n' ' ')"
 done
+# recipe: gate_up + SwiGLU fused by default for the untuned (ragged) shapes vs the plain kernel + SwiGLU pass
+for v in 1 0 1 0; do
+  SFTAMD_GU_AUTO=$v timeout -k 10 400 python -u bench.py --recipe --steps 40 --warmup 0 > gpurun_out/r5_22_recipe$v.log 2>&1 || { tail -20 gpurun_out/r5_22_recipe$v.log; exit 1; }
+  echo "recipe gu_auto$v $(grep '"metric"' gpurun_out/r5_22_recipe$v.log | python -c 'import json,sys; r=json.loads(sys.stdin.read()); print(r["value"], r.get("train_pure_samples_per_second",""), r.get("final_loss", ""))')"
+done
