@@ -343,7 +343,7 @@ __device__ __forceinline__ bf16x8 lds_tr8(const u16* p0, const u16* p1) {
   return __builtin_bit_cast(bf16x8, v);
 }
 
-template <int RF, int KT>  // KT 16-row k tiles per wave: a workgroup covers 64 KT columns of k
+template <int RF, int KT, int PD = 1>  // KT 16-row k tiles per wave: 64 KT columns of k; PD stages loaded ahead
 __global__ __launch_bounds__(256) void tsum_kernel(const u16* __restrict__ X, long ldX, const u16* __restrict__ S,
                                                    long ldS, float* __restrict__ out, long T, int K, long tc,
                                                    unsigned thresh, float dscale, unsigned seed, int drop) {
@@ -365,39 +365,48 @@ __global__ __launch_bounds__(256) void tsum_kernel(const u16* __restrict__ X, lo
   for (int kt = 0; kt < KT; ++kt)
 #pragma unroll
     for (int j = 0; j < RF; ++j) acc[kt][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  uint4 xv[XH], sv[SPT];
-  auto load = [&](long t0) {
+  uint4 xv[PD][XH], sv[PD][SPT];
+  auto load = [&](uint4 (&xd)[XH], uint4 (&sd)[SPT], long t0) {
 #pragma unroll
     for (int h = 0; h < XH; ++h) {
       const long t = t0 + tr + RPP * h;
-      xv[h] = (t < t_end && k < K) ? *(const uint4*)(X + t * ldX + k) : make_uint4(0, 0, 0, 0);
+      xd[h] = (t < t_end && k < K) ? *(const uint4*)(X + t * ldX + k) : make_uint4(0, 0, 0, 0);
     }
 #pragma unroll
     for (int u = 0; u < SPT; ++u) {
       const int e = tid + 256 * u, row = e / (R / 8), cc = e - row * (R / 8);
       const long t = t0 + row;
-      sv[u] = (e < SCH && t < t_end) ? *(const uint4*)(S + t * ldS + 8 * cc) : make_uint4(0, 0, 0, 0);
+      sd[u] = (e < SCH && t < t_end) ? *(const uint4*)(S + t * ldS + 8 * cc) : make_uint4(0, 0, 0, 0);
     }
   };
   // transposed-read lane addresses: group g reads tokens 8 (g & 1) + 16 (g >> 1)... of a 32-token k-step: rows
   // 8 gg + q (lo) and 8 gg + 4 + q (hi) with gg = g, columns c0 + 4 p
   const int q = r16 >> 2, p = r16 & 3;
-  load(t_begin);
+#pragma unroll
+  for (int i = 0; i < PD; ++i)
+    if (t_begin + ST * i < t_end) load(xv[i], sv[i], t_begin + ST * i);
   for (long t0 = t_begin; t0 < t_end; t0 += ST) {
     __syncthreads();  // the previous stage's reads are done
 #pragma unroll
     for (int h = 0; h < XH; ++h) {
-      uint4 v = xv[h];
+      uint4 v = xv[0][h];
       if (drop) v = mask8(v, keep8((unsigned long long)(t0 + tr + RPP * h) * K + k, seed, thresh));
       *(uint4*)&xs[tr + RPP * h][cx] = v;
     }
 #pragma unroll
     for (int u = 0; u < SPT; ++u) {
       const int e = tid + 256 * u, row = e / (R / 8), cc = e - row * (R / 8);
-      if (e < SCH) *(uint4*)&ss[row][8 * cc] = sv[u];
+      if (e < SCH) *(uint4*)&ss[row][8 * cc] = sv[0][u];
+    }
+#pragma unroll
+    for (int i = 0; i + 1 < PD; ++i) {
+#pragma unroll
+      for (int h = 0; h < XH; ++h) xv[i][h] = xv[i + 1][h];
+#pragma unroll
+      for (int u = 0; u < SPT; ++u) sv[i][u] = sv[i + 1][u];
     }
     __syncthreads();
-    if (t0 + ST < t_end) load(t0 + ST);  // the next stage's loads fly under this stage's MFMAs
+    if (t0 + PD * ST < t_end) load(xv[PD - 1], sv[PD - 1], t0 + PD * ST);  // flies under this stage's MFMAs
 #pragma unroll
     for (int ks = 0; ks < ST / 32; ++ks) {
       const int rl = 32 * ks + 8 * g + q;
@@ -946,15 +955,22 @@ at::Tensor lora_tsum(const at::Tensor& X, int64_t K, const at::Tensor& S, double
   splits = (T + tc - 1) / tc;
   auto out = at::empty({splits, R, K}, X.options().dtype(at::kFloat));  // every element written by one workgroup
   dim3 grid(nkb, (unsigned)splits);
+  const char* etp = getenv("SFTAMD_LORA_TSUM_PD");  // temporary A/B switch
+  const int tpd = etp && etp[0] ? atoi(etp) : 1;
+#define LORA_TSUM_K(RF, KT, PDV)                                                                                   \
+  lora::tsum_kernel<RF, KT, PDV><<<grid, 256, 0, cur_stream()>>>((const u16*)X.data_ptr(), X.stride(0),          \
+      (const u16*)S.data_ptr(), S.stride(0), out.data_ptr<float>(), T, (int)K, tc, thresh, dscale, (unsigned)seed, \
+      p > 0 ? 1 : 0)
+#define LORA_TSUM_P(RF, KT)                                                                                       \
+  if (tpd == 3) LORA_TSUM_K(RF, KT, 3);                                                                           \
+  else if (tpd == 2) LORA_TSUM_K(RF, KT, 2);                                                                      \
+  else LORA_TSUM_K(RF, KT, 1)
 #define LORA_TSUM(RF)                                                                                             \
-  if (wide)                                                                                                       \
-    lora::tsum_kernel<RF, 4><<<grid, 256, 0, cur_stream()>>>((const u16*)X.data_ptr(), X.stride(0),              \
-        (const u16*)S.data_ptr(), S.stride(0), out.data_ptr<float>(), T, (int)K, tc, thresh, dscale,             \
-        (unsigned)seed, p > 0 ? 1 : 0);                                                                          \
-  else                                                                                                            \
-    lora::tsum_kernel<RF, 1><<<grid, 256, 0, cur_stream()>>>((const u16*)X.data_ptr(), X.stride(0),              \
-        (const u16*)S.data_ptr(), S.stride(0), out.data_ptr<float>(), T, (int)K, tc, thresh, dscale,             \
-        (unsigned)seed, p > 0 ? 1 : 0)
+  if (wide) {                                                                                                     \
+    LORA_TSUM_P(RF, 4);                                                                                           \
+  } else {                                                                                                        \
+    LORA_TSUM_P(RF, 1);                                                                                           \
+  }
   switch (R / 16) {
     case 1: LORA_TSUM(1); break;
     case 2: LORA_TSUM(2); break;
@@ -962,6 +978,8 @@ at::Tensor lora_tsum(const at::Tensor& X, int64_t K, const at::Tensor& S, double
     default: LORA_TSUM(4); break;
   }
 #undef LORA_TSUM
+#undef LORA_TSUM_P
+#undef LORA_TSUM_K
   SFT_LAUNCH_CHECK();
   return out;
 }

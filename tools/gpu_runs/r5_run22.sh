@@ -5,11 +5,11 @@ cd $GRAFT_REPO_ROOT
 mkdir -p gpurun_out
 export TMPDIR=/tmp
 for v in 2 3; do
-  SFTAMD_LORA_FWD_PD=$v timeout -k 10 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_kernels_gpu.py -k "lora_fwd_bwd" > gpurun_out/r5_22_tests$v.log 2>&1 || { tail -30 gpurun_out/r5_22_tests$v.log; exit 1; }
+  SFTAMD_LORA_TSUM_PD=$v SFTAMD_LORA_FWD_PD=$v timeout -k 10 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_kernels_gpu.py -k "lora_fwd_bwd" > gpurun_out/r5_22_tests$v.log 2>&1 || { tail -30 gpurun_out/r5_22_tests$v.log; exit 1; }
   tail -1 gpurun_out/r5_22_tests$v.log
 done
 timeout -k 10 200 python -u tools/bench_lora_kernels.py > gpurun_out/r5_22_kern.log 2>&1 || { tail -20 gpurun_out/r5_22_kern.log; exit 1; }
-grep "pd\|swiglu" gpurun_out/r5_22_kern.log
+grep "pd\|swiglu\|tsum" gpurun_out/r5_22_kern.log
 for v in 2 1 3 2 1 3; do
   SFTAMD_LORA_FWD_PD=$v timeout -k 10 300 python -u bench.py --freeze-policy lora --steps 20 --warmup 5 > gpurun_out/r5_22_lora$v.log 2>&1 || { tail -20 gpurun_out/r5_22_lora$v.log; exit 1; }
   echo "lora pd$v $(grep -o '"value": [0-9.]*\|"final_loss": [a-zA-Z0-9.]*' gpurun_out/r5_22_lora$v.log | tr '\n' ' ')"
