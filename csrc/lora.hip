@@ -103,8 +103,8 @@ __global__ __launch_bounds__(512) void fwd_kernel(const u16* __restrict__ x, con
     }
   };
   // the wave's A_cat fragments of a chunk (rows 16 j + r, columns 64 w + 32 ks + 8 g): loaded one chunk ahead for
-  // R <= 32 (for R >= 48 the two copies pushed the kernel past 128 VGPRs: half the occupancy, or spills)
-  constexpr bool PFA = RF <= 2;
+  // R <= 32 or short rows (for R >= 48 the streamed variants went past 128 VGPRs: half the occupancy, or spills)
+  constexpr bool PFA = RF <= 2 || (NCH > 0 && RF <= 3);
   uint4 an[2][RF];
   auto load_a = [&](int k0) {
 #pragma unroll
