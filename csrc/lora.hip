@@ -66,12 +66,11 @@ __device__ __forceinline__ f32x4 mfma(const bf16x8& a, const bf16x8& b, const f3
 // tools/bench_lora_kernels.py, r4_run29.)
 // SW: x is the SwiGLU input gu [T, 2K] (gate | up) and the widened activation is act = silu(gate) * up, rounded to bf16
 // as the SwiGLU kernel does (the LoRA MLP's down projection: no separate SwiGLU pass, no act tensor).
-// PD: streamed chunks in flight ahead of the one being processed (NCH == 0)
-template <int RF, bool SW = false, int NCH = 0, int PD = 1>  // R = 16 * RF adapter columns; NCH > 0: K == 512 NCH
+template <int RF, bool SW = false, int NCH = 0>  // R = 16 * RF adapter columns; NCH > 0: K == 512 NCH
 __global__ __launch_bounds__(512) void fwd_kernel(const u16* __restrict__ x, const u16* __restrict__ A,
                                                   u16* __restrict__ X, u16* __restrict__ xd, long T, int K, long ldX,
                                                   float s, unsigned thresh, float dscale, unsigned seed, int drop) {
-  constexpr int R = 16 * RF, NW = 8, CK = 512, XP = CK + 8, NV = SW ? 2 : 1, DEP = NCH > 0 ? NCH : PD;
+  constexpr int R = 16 * RF, NW = 8, CK = 512, XP = CK + 8, NV = SW ? 2 : 1, DEP = NCH > 0 ? NCH : 1;
   __shared__ __attribute__((aligned(16))) u16 xs[2][16][XP];
   __shared__ float red[NW][16][R + 1];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
@@ -120,9 +119,7 @@ __global__ __launch_bounds__(512) void fwd_kernel(const u16* __restrict__ x, con
 #pragma unroll
     for (int c = 0; c < NCH; ++c) load(rw[c], c * CK);
   } else {
-#pragma unroll
-    for (int c = 0; c < PD; ++c)
-      if (c < nch) load(rw[c], c * CK);
+    load(rw[0], 0);
   }
   if constexpr (PFA) load_a(0);
 #pragma unroll
@@ -150,16 +147,9 @@ __global__ __launch_bounds__(512) void fwd_kernel(const u16* __restrict__ x, con
 #pragma unroll
         for (int j = 0; j < RF; ++j) ac[ks][j] = an[ks][j];
     }
-    if constexpr (NCH == 0) {  // the chunk PD ahead flies under this chunk's stores, LDS write and MFMAs
-#pragma unroll
-      for (int i = 0; i + 1 < PD; ++i)
-#pragma unroll
-        for (int h = 0; h < 2; ++h)
-#pragma unroll
-          for (int q = 0; q < NV; ++q) rw[i][h][q] = rw[i + 1][h][q];
-      if (ch + PD < nch) load(rw[PD - 1], k0 + PD * CK);
-    }
-    if (ch + 1 < nch) {
+    if (ch + 1 < nch) {  // the next chunk flies under this chunk's stores, LDS write and MFMAs (loading two or three
+                         // ahead measured slower: 127.6 / 135.8 vs 126.1 us SwiGLU-fused, r5_run22)
+      if constexpr (NCH == 0) load(rw[0], k0 + CK);
       if constexpr (PFA) load_a(k0 + CK);
     }
     u16(*tile)[XP] = xs[ch & 1];
@@ -343,7 +333,7 @@ __device__ __forceinline__ bf16x8 lds_tr8(const u16* p0, const u16* p1) {
   return __builtin_bit_cast(bf16x8, v);
 }
 
-template <int RF, int KT, int PD = 1>  // KT 16-row k tiles per wave: 64 KT columns of k; PD stages loaded ahead
+template <int RF, int KT>  // KT 16-row k tiles per wave: a workgroup covers 64 KT columns of k
 __global__ __launch_bounds__(256) void tsum_kernel(const u16* __restrict__ X, long ldX, const u16* __restrict__ S,
                                                    long ldS, float* __restrict__ out, long T, int K, long tc,
                                                    unsigned thresh, float dscale, unsigned seed, int drop) {
@@ -365,7 +355,7 @@ __global__ __launch_bounds__(256) void tsum_kernel(const u16* __restrict__ X, lo
   for (int kt = 0; kt < KT; ++kt)
 #pragma unroll
     for (int j = 0; j < RF; ++j) acc[kt][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  uint4 xv[PD][XH], sv[PD][SPT];
+  uint4 xv[XH], sv[SPT];
   auto load = [&](uint4 (&xd)[XH], uint4 (&sd)[SPT], long t0) {
 #pragma unroll
     for (int h = 0; h < XH; ++h) {
@@ -382,31 +372,23 @@ __global__ __launch_bounds__(256) void tsum_kernel(const u16* __restrict__ X, lo
   // transposed-read lane addresses: group g reads tokens 8 (g & 1) + 16 (g >> 1)... of a 32-token k-step: rows
   // 8 gg + q (lo) and 8 gg + 4 + q (hi) with gg = g, columns c0 + 4 p
   const int q = r16 >> 2, p = r16 & 3;
-#pragma unroll
-  for (int i = 0; i < PD; ++i)
-    if (t_begin + ST * i < t_end) load(xv[i], sv[i], t_begin + ST * i);
+  load(xv, sv, t_begin);
   for (long t0 = t_begin; t0 < t_end; t0 += ST) {
     __syncthreads();  // the previous stage's reads are done
 #pragma unroll
     for (int h = 0; h < XH; ++h) {
-      uint4 v = xv[0][h];
+      uint4 v = xv[h];
       if (drop) v = mask8(v, keep8((unsigned long long)(t0 + tr + RPP * h) * K + k, seed, thresh));
       *(uint4*)&xs[tr + RPP * h][cx] = v;
     }
 #pragma unroll
     for (int u = 0; u < SPT; ++u) {
       const int e = tid + 256 * u, row = e / (R / 8), cc = e - row * (R / 8);
-      if (e < SCH) *(uint4*)&ss[row][8 * cc] = sv[0][u];
-    }
-#pragma unroll
-    for (int i = 0; i + 1 < PD; ++i) {
-#pragma unroll
-      for (int h = 0; h < XH; ++h) xv[i][h] = xv[i + 1][h];
-#pragma unroll
-      for (int u = 0; u < SPT; ++u) sv[i][u] = sv[i + 1][u];
+      if (e < SCH) *(uint4*)&ss[row][8 * cc] = sv[u];
     }
     __syncthreads();
-    if (t0 + PD * ST < t_end) load(xv[PD - 1], sv[PD - 1], t0 + PD * ST);  // flies under this stage's MFMAs
+    // the next stage's loads fly under this stage's MFMAs (two / three stages ahead measured slower: r5_run22)
+    if (t0 + ST < t_end) load(xv, sv, t0 + ST);
 #pragma unroll
     for (int ks = 0; ks < ST / 32; ++ks) {
       const int rl = 32 * ks + 8 * g + q;
@@ -537,31 +519,18 @@ std::tuple<at::Tensor, at::Tensor> lora_fwd(const at::Tensor& x, const at::Tenso
   const unsigned thresh = lora::thresh_of(p, &dscale);
   const int grid = (int)((T + 15) / 16);
   u16* xdp = (p > 0 && save_xd) ? (u16*)xd.data_ptr() : nullptr;
-  const char* epd = getenv("SFTAMD_LORA_FWD_PD");  // temporary A/B switch
-  const int pd = epd && epd[0] ? atoi(epd) : 1;
-#define LORA_FWD_PD(RF, SWB)                                                                                      \
-  if (pd == 3)                                                                                                    \
-    lora::fwd_kernel<RF, SWB, 0, 3><<<grid, 512, 0, cur_stream()>>>((const u16*)x.data_ptr(),                    \
-        (const u16*)A.data_ptr(), (u16*)X.data_ptr(), xdp, T, K, ldX, (float)s, thresh, dscale, (unsigned)seed,   \
-        p > 0 ? 1 : 0);                                                                                           \
-  else if (pd == 2)                                                                                               \
-    lora::fwd_kernel<RF, SWB, 0, 2><<<grid, 512, 0, cur_stream()>>>((const u16*)x.data_ptr(),                    \
-        (const u16*)A.data_ptr(), (u16*)X.data_ptr(), xdp, T, K, ldX, (float)s, thresh, dscale, (unsigned)seed,   \
-        p > 0 ? 1 : 0);                                                                                           \
-  else                                                                                                            \
-    lora::fwd_kernel<RF, SWB><<<grid, 512, 0, cur_stream()>>>((const u16*)x.data_ptr(), (const u16*)A.data_ptr(), \
-        (u16*)X.data_ptr(), xdp, T, K, ldX, (float)s, thresh, dscale, (unsigned)seed, p > 0 ? 1 : 0)
 #define LORA_FWD(RF)                                                                                              \
   if (!swiglu && K == 2048)                                                                                       \
     lora::fwd_kernel<RF, false, 4><<<grid, 512, 0, cur_stream()>>>((const u16*)x.data_ptr(),                     \
                                                                    (const u16*)A.data_ptr(), (u16*)X.data_ptr(), xdp, \
                                                                    T, K, ldX, (float)s, thresh, dscale,          \
                                                                    (unsigned)seed, p > 0 ? 1 : 0);               \
-  else if (swiglu) {                                                                                              \
-    LORA_FWD_PD(RF, true);                                                                                        \
-  } else {                                                                                                        \
-    LORA_FWD_PD(RF, false);                                                                                       \
-  }
+  else if (swiglu)                                                                                                \
+    lora::fwd_kernel<RF, true><<<grid, 512, 0, cur_stream()>>>((const u16*)x.data_ptr(), (const u16*)A.data_ptr(), \
+        (u16*)X.data_ptr(), xdp, T, K, ldX, (float)s, thresh, dscale, (unsigned)seed, p > 0 ? 1 : 0);             \
+  else                                                                                                            \
+    lora::fwd_kernel<RF, false><<<grid, 512, 0, cur_stream()>>>((const u16*)x.data_ptr(), (const u16*)A.data_ptr(), \
+        (u16*)X.data_ptr(), xdp, T, K, ldX, (float)s, thresh, dscale, (unsigned)seed, p > 0 ? 1 : 0)
   switch (R / 16) {
     case 1: LORA_FWD(1); break;
     case 2: LORA_FWD(2); break;
@@ -569,7 +538,6 @@ std::tuple<at::Tensor, at::Tensor> lora_fwd(const at::Tensor& x, const at::Tenso
     default: LORA_FWD(4); break;
   }
 #undef LORA_FWD
-#undef LORA_FWD_PD
   SFT_LAUNCH_CHECK();
   return {X, xd};
 }
@@ -955,22 +923,15 @@ at::Tensor lora_tsum(const at::Tensor& X, int64_t K, const at::Tensor& S, double
   splits = (T + tc - 1) / tc;
   auto out = at::empty({splits, R, K}, X.options().dtype(at::kFloat));  // every element written by one workgroup
   dim3 grid(nkb, (unsigned)splits);
-  const char* etp = getenv("SFTAMD_LORA_TSUM_PD");  // temporary A/B switch
-  const int tpd = etp && etp[0] ? atoi(etp) : 1;
-#define LORA_TSUM_K(RF, KT, PDV)                                                                                   \
-  lora::tsum_kernel<RF, KT, PDV><<<grid, 256, 0, cur_stream()>>>((const u16*)X.data_ptr(), X.stride(0),          \
-      (const u16*)S.data_ptr(), S.stride(0), out.data_ptr<float>(), T, (int)K, tc, thresh, dscale, (unsigned)seed, \
-      p > 0 ? 1 : 0)
-#define LORA_TSUM_P(RF, KT)                                                                                       \
-  if (tpd == 3) LORA_TSUM_K(RF, KT, 3);                                                                           \
-  else if (tpd == 2) LORA_TSUM_K(RF, KT, 2);                                                                      \
-  else LORA_TSUM_K(RF, KT, 1)
 #define LORA_TSUM(RF)                                                                                             \
-  if (wide) {                                                                                                     \
-    LORA_TSUM_P(RF, 4);                                                                                           \
-  } else {                                                                                                        \
-    LORA_TSUM_P(RF, 1);                                                                                           \
-  }
+  if (wide)                                                                                                       \
+    lora::tsum_kernel<RF, 4><<<grid, 256, 0, cur_stream()>>>((const u16*)X.data_ptr(), X.stride(0),              \
+        (const u16*)S.data_ptr(), S.stride(0), out.data_ptr<float>(), T, (int)K, tc, thresh, dscale,             \
+        (unsigned)seed, p > 0 ? 1 : 0);                                                                          \
+  else                                                                                                            \
+    lora::tsum_kernel<RF, 1><<<grid, 256, 0, cur_stream()>>>((const u16*)X.data_ptr(), X.stride(0),              \
+        (const u16*)S.data_ptr(), S.stride(0), out.data_ptr<float>(), T, (int)K, tc, thresh, dscale,             \
+        (unsigned)seed, p > 0 ? 1 : 0)
   switch (R / 16) {
     case 1: LORA_TSUM(1); break;
     case 2: LORA_TSUM(2); break;
@@ -978,8 +939,6 @@ at::Tensor lora_tsum(const at::Tensor& X, int64_t K, const at::Tensor& S, double
     default: LORA_TSUM(4); break;
   }
 #undef LORA_TSUM
-#undef LORA_TSUM_P
-#undef LORA_TSUM_K
   SFT_LAUNCH_CHECK();
   return out;
 }

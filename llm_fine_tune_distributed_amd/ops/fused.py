@@ -584,15 +584,13 @@ class SwiGLUDownFn(Function):
 
 def swiglu_mlp(h: torch.Tensor, w_gate_up: torch.Tensor, w_down: torch.Tensor) -> torch.Tensor:
     """down(swiglu(gate_up(h))) — the SwiGLU MLP without LoRA, on the fastest available fusion:
-    gate_up GEMM with the SwiGLU epilogue + down GEMM with the SwiGLU backward in its dgrad (no separate SwiGLU kernel
-    in either direction) for SFTAMD_TN=1 / swiglu and, by default, for gate_up shapes without a TunableOp selection;
-    hipBLASLt gate_up + SwiGLU kernel + the fused down dgrad for the tuned shapes; otherwise the unfused chain."""
+    SFTAMD_TN=1 / swiglu: gate_up GEMM with the SwiGLU epilogue + down GEMM with the SwiGLU backward in its dgrad
+    (no separate SwiGLU kernel in either direction); default: gate_up GEMM (fwd_gemm) + SwiGLU kernel + the fused
+    down dgrad; otherwise the unfused chain."""
     h2d = h.reshape(-1, h.shape[-1])
-    # by default also where the plain gate_up would run on the row-contiguous persistent kernel anyway (no TunableOp
-    # selection: ragged padding-free / eval batches): its SwiGLU epilogue (659 us in the step at 8192 tokens) replaces
-    # the plain store + the separate SwiGLU pass (580 + 109 us, profiles/r5_step_nooverlap_gateup_rowc.md)
-    fused_gu = _TN_MODE in ("1", "swiglu") or (_TN_MODE == "rope" and _SWIGLU_DOWN and _fwd_on_hip(h2d, w_gate_up)
-                                               and os.environ.get("SFTAMD_GU_AUTO", "1") != "0")  # temporary A/B
+    # (fusing it by default where gate_up has no TunableOp selection — the recipe's ragged batches — measured neutral:
+    # 55.28 / 55.12 vs 55.01 / 55.04 HF, 82.84 / 82.68 vs 83.14 / 83.15 pure samples/s, r5_run22)
+    fused_gu = _TN_MODE in ("1", "swiglu")
     if (fused_gu and _SWIGLU_DOWN and _tn_ok(h2d, w_gate_up) and w_gate_up.shape[0] % 256 == 0
             and (w_gate_up.shape[0] // 2) % 128 == 0):
         gu, act = GateUpActFn.apply(h, w_gate_up)

@@ -57,33 +57,10 @@ def main():
     As = {r: torch.randn(r, Hs, device=dev, dtype=torch.bfloat16) * 0.05 for r in (16, 32, 48)}
     ds = {r: torch.randn(T, r, device=dev, dtype=torch.bfloat16) for r in (16, 32, 48)}
     xs = torch.randn(T, Hs, device=dev, dtype=torch.bfloat16)
-    qd = torch.randn(T, 3072, device=dev, dtype=torch.bfloat16)
     rows += [(f"lora_bwd_dx K=2048 R={r}", lambda r=r: ops.lora_bwd_dx(bs, ds[r], As[r], 0.05, 1), 2 * T * Hs * 2)
              for r in (48, 32, 16)]
     rows += [(f"lora_fwd K=2048 R={r}", lambda r=r: ops.lora_fwd(xs, As[r], 0.5, 0.05, 1, Hs + 128), 2 * T * Hs * 2)
              for r in (48, 32, 16)]
-    def env(fn, v):  # temporary A/B: the streamed widening's prefetch depth (SFTAMD_LORA_FWD_PD)
-        def run():
-            os.environ["SFTAMD_LORA_FWD_PD"] = v
-            return fn()
-        return run
-    for v in ("1", "2", "3"):
-        rows += [(f"[pd{v}] lora_fwd swiglu K=11008", env(lambda: ops.lora_fwd(gu, A, 0.5, 0.05, 1, I + 128, False, True), v),
-                  3 * T * I * 2),
-                 (f"[pd{v}] lora_fwd K=11008 R=16", env(lambda: ops.lora_fwd(x, A, 0.5, 0.05, 1, I + 128), v), 2 * T * I * 2)]
-    def envt(fn, v):  # temporary A/B: the adapter-gradient reductions' prefetch depth (SFTAMD_LORA_TSUM_PD)
-        def run():
-            os.environ["SFTAMD_LORA_TSUM_PD"] = v
-            return fn()
-        return run
-    for v in ("1", "2", "3"):
-        rows += [(f"[tpd{v}] lora_tsum dA K=11008 R=16", envt(lambda: ops.lora_tsum(base, I, dxa, 0.05, 1), v), T * I * 2),
-                 (f"[tpd{v}] lora_tsum dB n=22016 R=32", envt(lambda: ops.lora_tsum(gu, 2 * I, dxa2, 0.0, 0), v),
-                  T * 2 * I * 2),
-                 (f"[tpd{v}] lora_tsum dA K=2048 R=48", envt(lambda: ops.lora_tsum(xs, Hs, ds[48], 0.05, 1), v),
-                  T * Hs * 2),
-                 (f"[tpd{v}] lora_tsum dB n=3072 R=48", envt(lambda: ops.lora_tsum(qd, 3072, ds[48], 0.0, 0), v),
-                  T * 3072 * 2)]
     a = torch.randn(8192, 8192, device=dev, dtype=torch.bfloat16)
     for _ in range(200):  # ~1 s of GEMMs first: the clocks ramp up before anything is timed
         a @ a
