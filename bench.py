@@ -37,6 +37,7 @@ from __future__ import annotations
 
 import argparse
 import json
+import math
 import os
 import sys
 import time
@@ -313,7 +314,8 @@ def run(a):
                        "gradient_checkpointing": False, "packing": a.packing,
                        "padding_free": bool(getattr(trainer, "packed", False)) and not a.packing},
             "tokens_per_sec": round(tok_s, 1), "mfu": None if mfu is None else round(mfu, 4),
-            "final_loss": round(loss, 4), "peak_mem_gb": max(r_["peak_mem_gb"] for r_ in ranks),
+            "final_loss": round(loss, 4), "loss_finite": math.isfinite(loss),
+            "peak_mem_gb": max(r_["peak_mem_gb"] for r_ in ranks),
             "dist": {"backend": mine["backend"], "world_size": mine["world_size"],
                      "consistent": all(r_["world_size"] == st.world_size and r_["backend"] == mine["backend"]
                                        for r_ in ranks),
@@ -341,6 +343,10 @@ def run(a):
         if a.baseline_1gpu > 0:
             rec["scaling_efficiency"] = round(value / (st.world_size * a.baseline_1gpu), 4)
         print(json.dumps(rec), flush=True)
+        if not math.isfinite(loss):
+            # a non-finite loss makes the step faster (NaN / zero data toggles fewer bits, the clocks rise): the
+            # throughput of such a run is not a measurement (profiles/r5_llama.md)
+            print("[bench] WARNING: the loss is not finite; this run's throughput is void", file=sys.stderr, flush=True)
         for w in dist_warn:
             print(f"[bench] dist warning: {w}", file=sys.stderr, flush=True)
     if a.profile_steps:

@@ -45,6 +45,7 @@ def test_bench_self_launches_n_ranks(n):
     for k in ("plan_source", "alpha_us", "link_gbps"):
         assert k in rec["bucket_plan"], k
     assert rec["dist"]["params_equal_across_ranks"] and rec["dist"]["warnings"] == []
+    assert rec["loss_finite"] is True  # a NaN run's throughput is void (bench.py flags it)
     if n > 1:
         assert rec["dist"]["strict"] is True
         assert rec["bucket_plan"]["tied_sparse"]  # tiny ties its embedding: the sparse exchange ran
