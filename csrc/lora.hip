@@ -861,23 +861,31 @@ at::Tensor lora_dxa_blocks(const at::Tensor& dy, const at::Tensor& Bc, at::IntAr
   if (T == 0) return out;
   // pieces: ~512 workgroups over the token blocks, piece sizes a multiple of the 256-column chunk
   const long tb = (T + 63) / 64;
-  const long want = std::max<long>(nb, std::min<long>(lora::DXA_MAXP, (512 + tb - 1) / tb));
   lora::DxaPieces pc{};
   int np = 0;
-  for (int b = 0; b < nb; ++b) {
-    const long pb = std::max<long>(1, (want * rows[b] + total - 1) / total);
-    const long sz = ((rows[b] + pb - 1) / pb + 255) / 256 * 256;
-    pc.c[b] = (int)c[b];
-    pc.p0[b] = np;
-    for (long a = 0; a < rows[b]; a += sz) {
-      SFT_CHECK(np < lora::DXA_MAXP, "lora_dxa_blocks: too many pieces");
-      pc.n0[np] = (int)(o[b] + a);
-      pc.n1[np] = (int)(o[b] + std::min(rows[b], a + sz));
-      pc.blk[np] = b;
-      ++np;
+  // piece sizes per block (a multiple of the chunk): the largest target that keeps every piece in the table
+  for (long want = std::max<long>(nb, std::min<long>(lora::DXA_MAXP, (512 + tb - 1) / tb)); want >= 1; --want) {
+    long sz[4], count = 0;
+    for (int b = 0; b < nb; ++b) {
+      const long pb = std::max<long>(1, (want * rows[b] + total - 1) / total);
+      sz[b] = ((rows[b] + pb - 1) / pb + 255) / 256 * 256;
+      count += (rows[b] + sz[b] - 1) / sz[b];
     }
-    pc.np[b] = np - pc.p0[b];
+    if (count > lora::DXA_MAXP) continue;
+    for (int b = 0; b < nb; ++b) {
+      pc.c[b] = (int)c[b];
+      pc.p0[b] = np;
+      for (long a = 0; a < rows[b]; a += sz[b]) {
+        pc.n0[np] = (int)(o[b] + a);
+        pc.n1[np] = (int)(o[b] + std::min(rows[b], a + sz[b]));
+        pc.blk[np] = b;
+        ++np;
+      }
+      pc.np[b] = np - pc.p0[b];
+    }
+    break;
   }
+  SFT_CHECK(np >= nb, "lora_dxa_blocks: piece table");
   auto part = at::empty({(long)np, T, r}, dy.options().dtype(at::kFloat));
   dim3 grid((unsigned)tb, (unsigned)np);
   const unsigned fgrid = (unsigned)((T * R + 255) / 256);

@@ -569,7 +569,8 @@ def test_lora_dxa_vs_fp32(T, n, R, ldb):
 
 
 @pytest.mark.parametrize("T,blocks,r", [(8192, (11008, 11008), 16), (200, (2048, 512, 512), 16), (77, (1000, 1512), 32),
-                                        (640, (3000,), 16), (130, (256, 264, 8, 4096), 16)])
+                                        (640, (3000,), 16), (130, (256, 264, 8, 4096), 16),
+                                        (64, (2048, 2048, 2048, 30000), 16)])  # piece table at its 16-entry limit
 def test_lora_dxa_blocks_vs_fp32(T, blocks, r):
     """dxa = s dy Bc for a block-diagonal Bc (csrc/lora.hip dxa_piece_kernel + dxa_finish_kernel): each block's dy
     columns cut into pieces, partials summed per block; ragged T, blocks that are not a multiple of the 256-column
