@@ -54,7 +54,7 @@ TORCH_LIBRARY(sftamd, m) {
   m.def("dispatch_trace(bool on) -> ()", &sftamd::dispatch_trace);
   m.def("dispatch_trace_read() -> str", &sftamd::dispatch_trace_read);
   // norms / elementwise
-  m.def("rmsnorm_fwd(Tensor x, Tensor? residual, Tensor weight, float eps) -> (Tensor, Tensor, Tensor)");
+  m.def("rmsnorm_fwd(Tensor x, Tensor? residual, Tensor weight, float eps, int y_ld=0) -> (Tensor, Tensor, Tensor)");
   m.def("rmsnorm_bwd(Tensor dy, Tensor h, Tensor weight, Tensor rstd, Tensor? dres, Tensor(a!)? dw_out=None, bool accumulate=False) -> (Tensor, Tensor)");
   m.def("swiglu_fwd(Tensor gate_up) -> Tensor");
   m.def("swiglu_bwd(Tensor dy, Tensor gate_up) -> Tensor");
@@ -65,6 +65,7 @@ TORCH_LIBRARY(sftamd, m) {
   m.def("lora_fwd(Tensor x, Tensor A, float s, float p, int seed, int ldX=0, bool save_xd=False, bool swiglu=False) -> (Tensor, Tensor)");
   m.def("lora_bwd_dx(Tensor base, Tensor dxa, Tensor A, float p, int seed, Tensor? gu=None) -> Tensor");
   m.def("lora_tsum(Tensor X, int K, Tensor S, float p, int seed) -> Tensor");
+  m.def("lora_fwd_inplace(Tensor(a!) X, int K, Tensor A, float s, float p, int seed) -> ()");
   m.def("lora_dxa(Tensor dy, Tensor Bc, float s) -> Tensor");
   m.def("lora_dxa_blocks(Tensor dy, Tensor Bc, int[] o, int[] rows, int[] c, int r, float s) -> Tensor");
   m.def("lora_grad_out(Tensor sum, Tensor(a!)[] outs, int[] r0, int[] c0, bool tr, int[] accumulate) -> ()");

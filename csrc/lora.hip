@@ -69,7 +69,8 @@ __device__ __forceinline__ f32x4 mfma(const bf16x8& a, const bf16x8& b, const f3
 template <int RF, bool SW = false, int NCH = 0>  // R = 16 * RF adapter columns; NCH > 0: K == 512 NCH
 __global__ __launch_bounds__(512) void fwd_kernel(const u16* __restrict__ x, const u16* __restrict__ A,
                                                   u16* __restrict__ X, u16* __restrict__ xd, long T, int K, long ldX,
-                                                  float s, unsigned thresh, float dscale, unsigned seed, int drop) {
+                                                  float s, unsigned thresh, float dscale, unsigned seed, int drop,
+                                                  long ldx, int copy) {
   constexpr int R = 16 * RF, NW = 8, CK = 512, XP = CK + 8, NV = SW ? 2 : 1, DEP = NCH > 0 ? NCH : 1;
   __shared__ __attribute__((aligned(16))) u16 xs[2][16][XP];
   __shared__ float red[NW][16][R + 1];
@@ -87,7 +88,7 @@ __global__ __launch_bounds__(512) void fwd_kernel(const u16* __restrict__ x, con
   for (int h = 0; h < 2; ++h) {
     lt[h] = t0 + (lane >> 3) + 8 * h;
     lok[h] = lt[h] < T;
-    xrow[h] = x + (lok[h] ? lt[h] : T - 1) * (SW ? 2L * K : (long)K);
+    xrow[h] = x + (lok[h] ? lt[h] : T - 1) * ldx;
   }
   f32x4 acc[RF];
 #pragma unroll
@@ -157,7 +158,7 @@ __global__ __launch_bounds__(512) void fwd_kernel(const u16* __restrict__ x, con
     for (int h = 0; h < 2; ++h) {
       const int c = k0 + lc;
       if (c < K) {
-        if (lok[h]) *(uint4*)(X + lt[h] * ldX + c) = v[h];
+        if (copy && lok[h]) *(uint4*)(X + lt[h] * ldX + c) = v[h];  // (!copy: x IS X[:, :K], written by its producer)
         if (drop) {
           const unsigned bits = keep8((unsigned long long)lt[h] * K + c, seed, thresh);
           if (xd && lok[h]) {  // dropout(x) itself, scaled (tests / save_xd only)
@@ -499,6 +500,36 @@ static unsigned thresh_of(double p, float* dscale) { return drop_thresh16(p, dsc
 // p > 0, else empty (the backward regenerates the mask from the seed: lora_tsum, lora_bwd_dx). ldX >= K + R (0 = K + R): columns
 // [K + R, ldX) are zero (the wide weight's padding to a whole K-tile pair of the HIP GEMMs)
 // swiglu: x is gu [T, 2K] and the widened activation is act = silu(gate) * up (see fwd_kernel SW)
+namespace lora {
+// one widening launch: x rows of stride ldx (copy = 0: x IS X's left block, produced in place by its producer)
+static void launch_fwd(const u16* x, long ldx, int copy, const at::Tensor& A, u16* X, u16* xdp, long T, int K, long ldX,
+                       double s, double p, int64_t seed, bool swiglu) {
+  const int R = A.size(0);
+  float dscale;
+  const unsigned thresh = thresh_of(p, &dscale);
+  const int grid = (int)((T + 15) / 16);
+  const u16* Ap = (const u16*)A.data_ptr();
+#define LORA_FWD(RF)                                                                                              \
+  if (!swiglu && K == 2048)                                                                                       \
+    fwd_kernel<RF, false, 4><<<grid, 512, 0, cur_stream()>>>(x, Ap, X, xdp, T, K, ldX, (float)s, thresh, dscale,  \
+                                                             (unsigned)seed, p > 0 ? 1 : 0, ldx, copy);           \
+  else if (swiglu)                                                                                                \
+    fwd_kernel<RF, true><<<grid, 512, 0, cur_stream()>>>(x, Ap, X, xdp, T, K, ldX, (float)s, thresh, dscale,      \
+                                                         (unsigned)seed, p > 0 ? 1 : 0, ldx, copy);               \
+  else                                                                                                            \
+    fwd_kernel<RF, false><<<grid, 512, 0, cur_stream()>>>(x, Ap, X, xdp, T, K, ldX, (float)s, thresh, dscale,     \
+                                                          (unsigned)seed, p > 0 ? 1 : 0, ldx, copy)
+  switch (R / 16) {
+    case 1: LORA_FWD(1); break;
+    case 2: LORA_FWD(2); break;
+    case 3: LORA_FWD(3); break;
+    default: LORA_FWD(4); break;
+  }
+#undef LORA_FWD
+  SFT_LAUNCH_CHECK();
+}
+}  // namespace lora
+
 std::tuple<at::Tensor, at::Tensor> lora_fwd(const at::Tensor& x, const at::Tensor& A, double s, double p, int64_t seed,
                                             int64_t ldX, bool save_xd, bool swiglu) {
   SFT_CHECK_CUDA(x);
@@ -515,31 +546,27 @@ std::tuple<at::Tensor, at::Tensor> lora_fwd(const at::Tensor& x, const at::Tenso
   auto X = at::empty({T, ldX}, x.options());
   at::Tensor xd = (p > 0 && save_xd) ? at::empty({T, (long)K}, x.options()) : at::empty({0}, x.options());
   if (T == 0) return {X, xd};
-  float dscale;
-  const unsigned thresh = lora::thresh_of(p, &dscale);
-  const int grid = (int)((T + 15) / 16);
-  u16* xdp = (p > 0 && save_xd) ? (u16*)xd.data_ptr() : nullptr;
-#define LORA_FWD(RF)                                                                                              \
-  if (!swiglu && K == 2048)                                                                                       \
-    lora::fwd_kernel<RF, false, 4><<<grid, 512, 0, cur_stream()>>>((const u16*)x.data_ptr(),                     \
-                                                                   (const u16*)A.data_ptr(), (u16*)X.data_ptr(), xdp, \
-                                                                   T, K, ldX, (float)s, thresh, dscale,          \
-                                                                   (unsigned)seed, p > 0 ? 1 : 0);               \
-  else if (swiglu)                                                                                                \
-    lora::fwd_kernel<RF, true><<<grid, 512, 0, cur_stream()>>>((const u16*)x.data_ptr(), (const u16*)A.data_ptr(), \
-        (u16*)X.data_ptr(), xdp, T, K, ldX, (float)s, thresh, dscale, (unsigned)seed, p > 0 ? 1 : 0);             \
-  else                                                                                                            \
-    lora::fwd_kernel<RF, false><<<grid, 512, 0, cur_stream()>>>((const u16*)x.data_ptr(), (const u16*)A.data_ptr(), \
-        (u16*)X.data_ptr(), xdp, T, K, ldX, (float)s, thresh, dscale, (unsigned)seed, p > 0 ? 1 : 0)
-  switch (R / 16) {
-    case 1: LORA_FWD(1); break;
-    case 2: LORA_FWD(2); break;
-    case 3: LORA_FWD(3); break;
-    default: LORA_FWD(4); break;
-  }
-#undef LORA_FWD
-  SFT_LAUNCH_CHECK();
+  lora::launch_fwd((const u16*)x.data_ptr(), x.size(1), 1, A, (u16*)X.data_ptr(),
+                   (p > 0 && save_xd) ? (u16*)xd.data_ptr() : nullptr, T, K, ldX, s, p, seed, swiglu);
   return {X, xd};
+}
+
+// The same widening when x already sits in X's left columns (X [T, ldX], x = X[:, :K], written there by its producer:
+// the RMSNorm forward's strided output): fills only the adapter columns [K, K + R) and the zero padding.
+void lora_fwd_inplace(at::Tensor X, int64_t K, const at::Tensor& A, double s, double p, int64_t seed) {
+  SFT_CHECK_CUDA(X);
+  SFT_CHECK_BF16(X);
+  SFT_CHECK_BF16(A);
+  SFT_CHECK_CONTIG(A);
+  SFT_CHECK(X.dim() == 2 && X.stride(1) == 1 && X.stride(0) == X.size(1) && (uintptr_t)X.data_ptr() % 16 == 0,
+            "lora_fwd_inplace: X [T, ldX] row-contiguous");
+  const long T = X.size(0), ldX = X.size(1);
+  const int R = A.size(0);
+  SFT_CHECK(A.size(1) == K && K % 256 == 0 && R % 16 == 0 && R >= 16 && R <= 64 && ldX >= K + R && ldX % 8 == 0,
+            "lora_fwd_inplace: shapes");
+  if (T == 0) return;
+  lora::launch_fwd((const u16*)X.data_ptr(), ldX, 0, A, (u16*)X.data_ptr(), nullptr, T, (int)K, ldX, s, p, seed,
+                   false);
 }
 
 // dx = base + keep * (dxa @ A) / (1-p); base [T, K] with row stride ldb (a column slice is fine). With gu [T, 2K]
@@ -1031,6 +1058,7 @@ TORCH_LIBRARY_IMPL(sftamd, CUDA, m) {
   m.impl("copy2d_batch", &copy2d_batch);
   m.impl("lora_bwd_dx", &lora_bwd_dx);
   m.impl("lora_tsum", &lora_tsum);
+  m.impl("lora_fwd_inplace", &lora_fwd_inplace);
   m.impl("lora_dxa", &lora_dxa);
   m.impl("lora_dxa_blocks", &lora_dxa_blocks);
   m.impl("lora_grad_out", &lora_grad_out);

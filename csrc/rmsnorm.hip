@@ -14,7 +14,7 @@ template <int NV>
 __global__ __launch_bounds__(256) void rmsnorm_fwd_kernel(const u16* __restrict__ x, const u16* __restrict__ res,
                                                           const u16* __restrict__ w, u16* __restrict__ y,
                                                           u16* __restrict__ res_out, float* __restrict__ rstd_out,
-                                                          int M, int H, float eps) {
+                                                          int M, int H, float eps, long ldy) {
   const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
   if (row >= M) return;
@@ -48,7 +48,7 @@ __global__ __launch_bounds__(256) void rmsnorm_fwd_kernel(const u16* __restrict_
       unpack8(*(const uint4*)(w + c), wf);
 #pragma unroll
       for (int i = 0; i < 8; ++i) o[i] = bf2f(f2bf(v[j][i] * rstd)) * wf[i];
-      *(uint4*)(y + base + c) = pack8(o);
+      *(uint4*)(y + (long)row * ldy + c) = pack8(o);
     }
   }
   if (lane == 0) rstd_out[row] = rstd;
@@ -204,8 +204,10 @@ __global__ __launch_bounds__(1024) void col_sum2_kernel(const float* __restrict_
     __VA_ARGS__;                                 \
   }
 
+// y_ld > H: y is the left [.., H] block of a [M, y_ld] buffer (row stride y_ld; columns H.. left for the consumer: the
+// LoRA widening fills them in place, ops/fused.py _lora_wide_prep)
 std::tuple<at::Tensor, at::Tensor, at::Tensor> rmsnorm_fwd(const at::Tensor& x, const c10::optional<at::Tensor>& residual,
-                                                           const at::Tensor& weight, double eps) {
+                                                           const at::Tensor& weight, double eps, int64_t y_ld) {
   SFT_CHECK_CUDA(x);
   SFT_CHECK_BF16(x);
   SFT_CHECK_CONTIG(x);
@@ -213,7 +215,17 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor> rmsnorm_fwd(const at::Tensor& x, 
   const int H = x.size(-1);
   const int M = x.numel() / H;
   SFT_CHECK(H % 8 == 0 && H <= 4096, "hidden size must be a multiple of 8 and <= 4096");
-  auto y = at::empty_like(x);
+  if (y_ld <= 0) y_ld = H;
+  SFT_CHECK(y_ld >= H && y_ld % 8 == 0, "rmsnorm_fwd: y_ld >= H, multiple of 8");
+  at::Tensor y;
+  if (y_ld == H) {
+    y = at::empty_like(x);
+  } else {
+    auto buf = at::empty({(long)M, y_ld}, x.options());
+    std::vector<int64_t> st(x.dim(), 1);
+    for (int d = x.dim() - 2; d >= 0; --d) st[d] = (d == x.dim() - 2 ? y_ld : st[d + 1] * x.size(d + 1));
+    y = buf.as_strided(x.sizes(), st);
+  }
   auto rstd = at::empty({M}, x.options().dtype(at::kFloat));
   at::Tensor res_out = x;
   const u16* rp = nullptr;
@@ -226,7 +238,7 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor> rmsnorm_fwd(const at::Tensor& x, 
   dim3 grid((M + 3) / 4);
   NV_DISPATCH(H, rmsnorm_fwd_kernel<NV><<<grid, 256, 0, cur_stream()>>>(
                      (const u16*)x.data_ptr(), rp, (const u16*)weight.data_ptr(), (u16*)y.data_ptr(),
-                     (u16*)res_out.data_ptr(), rstd.data_ptr<float>(), M, H, (float)eps));
+                     (u16*)res_out.data_ptr(), rstd.data_ptr<float>(), M, H, (float)eps, (long)y_ld));
   SFT_LAUNCH_CHECK();
   return {y, res_out, rstd};
 }

@@ -102,6 +102,16 @@ class MLP(nn.Module):
         return ops.lora_swiglu_mlp(h, self.gate_up_proj, self.down_proj, L["gate_up"], L["down"])
 
 
+def _wide_ld(lora, key: str, weight) -> int:
+    """Row width of the LoRA wide weight W' that consumes this norm's output (0: none), so the norm writes its output
+    straight into the left block of the consumer's widened activation X' (ops.add_rms_norm y_ld)."""
+    fl = None if lora is None else lora[key]
+    wide = getattr(fl, "wide", None)
+    if wide is None or not any(fl.active) or weight.data_ptr() != wide.data_ptr():
+        return 0
+    return wide.shape[1]
+
+
 class DecoderLayer(nn.Module):
     def __init__(self, cfg: ModelConfig, layer_idx: int):
         super().__init__()
@@ -114,11 +124,12 @@ class DecoderLayer(nn.Module):
         """Pre-norm block with the residual add fused into the norms:
         (x: previous sublayer output, residual: residual stream before adding x)."""
         ln = self.input_layernorm
-        h, residual = ops.add_rms_norm(x, residual, ln.weight, ln.eps)
-        a = self.self_attn(h, rope_cs, cu_seqlens, max_seqlen)
+        at, ml = self.self_attn, self.mlp
+        h, residual = ops.add_rms_norm(x, residual, ln.weight, ln.eps, _wide_ld(at.lora, "qkv", at.qkv_proj))
+        a = at(h, rope_cs, cu_seqlens, max_seqlen)
         ln2 = self.post_attention_layernorm
-        h, residual = ops.add_rms_norm(a, residual, ln2.weight, ln2.eps)
-        return self.mlp(h), residual
+        h, residual = ops.add_rms_norm(a, residual, ln2.weight, ln2.eps, _wide_ld(ml.lora, "gate_up", ml.gate_up_proj))
+        return ml(h), residual
 
 
 class Model(nn.Module):

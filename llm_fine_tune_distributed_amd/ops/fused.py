@@ -374,12 +374,14 @@ def embedding(ids: torch.Tensor, weight: torch.Tensor) -> torch.Tensor:
 
 # ----------------------------------------------------------------------------- RMSNorm (+residual)
 class AddRMSNormFn(Function):
-    """res_out = x (+ residual); y = rmsnorm(res_out) * w. Returns (y, res_out)."""
+    """res_out = x (+ residual); y = rmsnorm(res_out) * w. Returns (y, res_out). y_ld > H (HIP path): y is the left
+    block of a [tokens, y_ld] buffer, so a LoRA-widened consumer fills its adapter columns in place (_lora_wide_prep)
+    instead of copying y into its X'."""
 
     @staticmethod
-    def forward(ctx, x, residual, weight, eps):
+    def forward(ctx, x, residual, weight, eps, y_ld=0):
         if _ext.use_hip(x):
-            y, res_out, rstd = _ext.ops().rmsnorm_fwd(x, residual, weight, eps)
+            y, res_out, rstd = _ext.ops().rmsnorm_fwd(x, residual, weight, eps, int(y_ld))
         else:
             res_out = x if residual is None else (x.float() + residual.float()).to(x.dtype)
             y, rstd = ref.rms_norm(res_out, weight, eps)
@@ -404,7 +406,7 @@ class AddRMSNormFn(Function):
             if direct:
                 w._sftamd_fresh = False
                 _weight_grad_done(w)
-                return dx, (dx if ctx.has_residual else None), None, None
+                return dx, (dx if ctx.has_residual else None), None, None, None
         else:
             hf = h.float()
             n = hf * rstd[..., None]
@@ -419,11 +421,12 @@ class AddRMSNormFn(Function):
         if ctx.needs_input_grad[2]:
             dweight = _accumulate_small_grad(w, dw)
         dresid = dx if ctx.has_residual else None
-        return dx, dresid, dweight, None
+        return dx, dresid, dweight, None, None
 
 
-def add_rms_norm(x, residual, weight, eps) -> Tuple[torch.Tensor, torch.Tensor]:
-    return AddRMSNormFn.apply(x, residual, weight, eps)
+def add_rms_norm(x, residual, weight, eps, y_ld: int = 0) -> Tuple[torch.Tensor, torch.Tensor]:
+    """(y, res_out); y_ld: see AddRMSNormFn (ignored off the HIP path)."""
+    return AddRMSNormFn.apply(x, residual, weight, eps, y_ld)
 
 
 def rms_norm(x, weight, eps) -> torch.Tensor:
@@ -1139,15 +1142,30 @@ def _lora_wide_prep(x, wide, K, scaling, p, seed, meta, ab, swiglu=False):
     As, Bs = ab[:n], ab[n:]
     r = As[0].shape[0]
     x2d = x.reshape(-1, 2 * K if swiglu else K)
-    if not x2d.is_contiguous():
-        x2d = x2d.contiguous()
     if _wide_sync_ok(wide, As, Bs):
         acat = _wide_sync(wide, K, r, meta, As, Bs)
     else:
         _sync_wide(wide, K, r, meta, Bs)
         acat = As[0].contiguous() if n == 1 else torch.cat(As, 0)
-    X = _lora_fwd(x2d, acat, scaling, p, seed, wide.shape[1], swiglu)
+    X = _prewidened(x2d, wide.shape[1]) if not swiglu else None
+    if X is not None:  # x was written into X's left block by its producer (add_rms_norm y_ld): fill the rest in place
+        _ext.ops().lora_fwd_inplace(X, K, acat, float(scaling), float(p), int(seed))
+    else:
+        X = _lora_fwd(x2d.contiguous(), acat, scaling, p, seed, wide.shape[1], swiglu)
     return X, acat, (K, r * n, r, n, float(scaling), float(p), int(seed), tuple(meta), x.shape)
+
+
+def _prewidened(x2d: torch.Tensor, ldX: int) -> Optional[torch.Tensor]:
+    """X [T, ldX] when x2d [T, K] is the left block of a row-contiguous [T, ldX] buffer (row stride ldX, the rest of
+    each row inside the same storage), on the HIP path; else None."""
+    T, K = x2d.shape
+    if (T == 0 or K >= ldX or x2d.stride(1) != 1 or x2d.stride(0) != ldX or not _ext.use_hip(x2d)
+            or x2d.dtype != torch.bfloat16 or x2d.data_ptr() % 16 != 0):
+        return None
+    st = x2d.untyped_storage()
+    if (x2d.storage_offset() + T * ldX) * x2d.element_size() > st.nbytes():
+        return None
+    return x2d.as_strided((T, ldX), (ldX, 1))
 
 
 def _lora_wide_bwd(X, acat, wide, ab, state, dy2d, need_dx, gu=None):

@@ -501,6 +501,11 @@ def test_lora_fwd_bwd_kernels(K, R, p):
         assert not X[:, K + R:].any()
     if p > 0:
         assert torch.equal(xd, xdr)
+    # in place: x already in the left block of X (the producer wrote it there), only [K, ldX) filled
+    Xi = torch.full((T, K + 128), 7.0, device="cuda", dtype=torch.bfloat16)
+    Xi[:, :K] = x
+    _ext.ops().lora_fwd_inplace(Xi, K, A, 0.5, p, 99)
+    assert torch.equal(Xi, _ext.ops().lora_fwd(x, A, 0.5, p, 99, K + 128)[0])
     # swiglu: the widening pass reads gu [T, 2K] and forms silu(gate) * up itself == the SwiGLU kernel then lora_fwd
     gu = torch.randn(T, 2 * K, device="cuda", dtype=torch.bfloat16)
     act = _ext.ops().swiglu_fwd(gu)

@@ -182,6 +182,44 @@ def test_lora_wide_gpu_matches_unfused():
             assert rel < 5e-2, (n, rel.item())
 
 
+def test_lora_norm_writes_widened_activation_in_place():
+    """The RMSNorm forward writes its output into the left block of the consumer's widened activation X' (qkv /
+    gate_up: add_rms_norm y_ld) and lora_fwd_inplace fills only the adapter columns: bitwise the same loss and
+    gradients as the copying widening (the norm output as its own tensor, X' written by lora_fwd)."""
+    from llm_fine_tune_distributed_amd.models.lora import LoRAConfig, apply_lora
+    import llm_fine_tune_distributed_amd.models.transformer as T
+    cfg = tiny(hidden_size=512, num_attention_heads=4, num_key_value_heads=2, head_dim=128, intermediate_size=1024,
+               vocab_size=1024, num_hidden_layers=2)
+    m = build_model(cfg, device="cuda", dtype=torch.bfloat16, seed=1)
+    apply_lora(m, LoRAConfig(r=16, lora_alpha=8, lora_dropout=0.1))
+    for l in m.model.layers:
+        for fl in (l.self_attn.lora["qkv"], l.mlp.lora["gate_up"]):
+            for bb in fl.B:
+                torch.nn.init.normal_(bb, std=0.05)
+    m.train()
+    ids = torch.randint(0, 1024, (4, 128), device="cuda")
+    assert T._wide_ld(m.model.layers[0].self_attn.lora, "qkv", m.model.layers[0].self_attn.qkv_proj) == 640
+
+    def run():
+        for p in m.parameters():
+            p.grad = None
+        torch.manual_seed(7)
+        out = m(ids, labels=ids)
+        out.loss.backward()
+        return out.loss.detach().clone(), {n: p.grad.clone() for n, p in m.named_parameters() if p.grad is not None}
+
+    l1, g1 = run()
+    orig = T._wide_ld
+    T._wide_ld = lambda *a: 0
+    try:
+        l2, g2 = run()
+    finally:
+        T._wide_ld = orig
+    assert torch.equal(l1, l2) and g1.keys() == g2.keys()
+    for n in g1:
+        assert torch.equal(g1[n], g2[n]), n
+
+
 def test_lora_wide_sync_after_edits():
     """The HIP path keeps every adapter's B inside its wide weight and its A rows in a persistent A_cat, refreshed for
     the whole model by one batched copy (ops/fused.py _wide_sync) after an optimizer epoch or an in-place edit: the
