@@ -1122,10 +1122,10 @@ def _wide_sync_ok(wide, As, Bs) -> bool:
 
 
 def _lora_gemm(X: torch.Tensor, wide: torch.Tensor) -> torch.Tensor:
-    """The widened LoRA forward GEMM X' W'^T on the hand-written persistent kernel (113.0 samples/s vs 112.9 with
-    hipBLASLt, profiles/r4_lora.md; the row-contiguous store epilogue since round 5, profiles/r5_gemm_fwd.md)."""
-    if (_ext.use_hip(X) and X.shape[0] % 256 == 0 and X.shape[1] % 128 == 0
-            and wide.shape[0] % 256 == 0 and wide.is_contiguous() and X.is_contiguous()):
+    """The widened LoRA forward GEMM X' W'^T: the routing rule of fwd_gemm (hipBLASLt where TunableOp holds a selection
+    for the exact wide shape, SFTAMD_FWD_GEMM), else the hand-written persistent kernel with the row-contiguous store
+    epilogue (113.0 samples/s vs 112.9 for untuned hipBLASLt, profiles/r4_lora.md; profiles/r5_gemm_fwd.md)."""
+    if _fwd_on_hip(X, wide) and X.is_contiguous():
         return _ext.ops().gemm_tn(X, wide, _LORA_FWD_CFG)
     return torch.mm(X, wide.t())
 
