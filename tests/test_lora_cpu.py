@@ -170,3 +170,21 @@ def test_lora_trainer_updates_reach_the_wide_weight(tmp_path):
     for (o, rows, c), B in zip(fl.wide_meta, fl.B):
         assert B.detach().abs().sum() > 0  # trained away from the zero init
         assert torch.equal(fl.wide[o:o + rows, K + c:K + c + fl.r], B.detach())
+
+
+def test_prewidened_view_detection(monkeypatch):
+    """_prewidened (the in-place LoRA widening): only the left [T, K] block of a row-contiguous [T, ldX] buffer
+    whose rows lie wholly inside the storage is taken as X'; contiguous inputs, other strides and short storages
+    are not."""
+    import llm_fine_tune_distributed_amd.ops.fused as F
+    monkeypatch.setattr(F._ext, "use_hip", lambda t: True)
+    T, K, ldX = 6, 16, 24
+    buf = torch.zeros(T, ldX, dtype=torch.bfloat16)
+    X = F._prewidened(buf[:, :K], ldX)
+    assert X is not None and X.shape == (T, ldX) and X.data_ptr() == buf.data_ptr() and X.stride() == (ldX, 1)
+    X[:, K:] = 1  # the view covers the buffer's adapter / padding columns
+    assert (buf[:, K:] == 1).all()
+    assert F._prewidened(torch.zeros(T, K, dtype=torch.bfloat16), ldX) is None            # contiguous [T, K]
+    assert F._prewidened(buf[:, :K], ldX + 8) is None                                     # another width
+    assert F._prewidened(torch.zeros(T * ldX - 8, dtype=torch.bfloat16).as_strided((T, K), (ldX, 1)), ldX) is None
+    assert F._prewidened(buf[:, :K].float(), ldX) is None                                 # not bf16
