@@ -617,11 +617,11 @@ void g4_wgrad(const at::Tensor& dy, const at::Tensor& x, at::Tensor& out, bool a
   ea.P = nsk > 0 ? part.data_ptr<float>() : nrm;
   ea.flags = (accumulate ? 1 : 0) | (nrm != nullptr ? 2 : 0);
   if (ring)
-    g4::launch<g4::TR, g4::TR, g4::EPI_STORE, true>((const u16*)dy.data_ptr(), N, (const u16*)x.data_ptr(), K, N, K, T,
-                                                    ndp, nsk > 0 ? splits : 1, ea);
+    g4::launch<g4::TR, g4::TR, g4::EPI_STORE, true>((const u16*)dy.data_ptr(), N, (const u16*)x.data_ptr(), x.stride(0),
+                                                    N, K, T, ndp, nsk > 0 ? splits : 1, ea);
   else
-    g4::launch<g4::TR, g4::TR, g4::EPI_STORE, false>((const u16*)dy.data_ptr(), N, (const u16*)x.data_ptr(), K, N, K, T,
-                                                     ndp, nsk > 0 ? splits : 1, ea);
+    g4::launch<g4::TR, g4::TR, g4::EPI_STORE, false>((const u16*)dy.data_ptr(), N, (const u16*)x.data_ptr(), x.stride(0),
+                                                     N, K, T, ndp, nsk > 0 ? splits : 1, ea);
   if (nsk > 0) {
     const long n8 = (long)nsk * 65536 / 8;
     splitk_fixup_kernel<256, 256><<<(unsigned)((n8 + 255) / 256), 256, 0, cur_stream()>>>(

@@ -621,9 +621,11 @@ void wgrad_gemm(at::Tensor out, at::Tensor dy, at::Tensor x, bool accumulate, in
   SFT_CHECK_BF16(x);
   SFT_CHECK_BF16(out);
   SFT_CHECK_CONTIG(dy);
-  SFT_CHECK_CONTIG(x);
   SFT_CHECK_CONTIG(out);
   SFT_CHECK(dy.dim() == 2 && x.dim() == 2 && out.dim() == 2, "wgrad_gemm: 2-D operands");
+  // x may have a padded row pitch (a [T, K] view into a wider buffer) on the 4-wave kernel (cfg 12 / 13 family)
+  SFT_CHECK(x.stride(1) == 1 && x.stride(0) % 8 == 0 && x.stride(0) >= x.size(1), "wgrad_gemm: x rows contiguous");
+  SFT_CHECK(x.stride(0) == x.size(1) || cfg % 100 == 12 || cfg % 100 == 13, "wgrad_gemm: a padded x pitch needs cfg 12 / 13");
   const int64_t T = dy.size(0), N = dy.size(1), K = x.size(1);
   SFT_CHECK(x.size(0) == T && out.size(0) == N && out.size(1) == K, "wgrad_gemm: shape mismatch");
   SFT_CHECK(T % 32 == 0 && T > 0, "wgrad_gemm: T must be a positive multiple of 32");

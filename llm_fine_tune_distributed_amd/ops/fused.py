@@ -91,7 +91,10 @@ def _wgrad_mm(out: torch.Tensor, dy2d: torch.Tensor, x2d: torch.Tensor, accumula
         cfg = _wgrad_cfg(dy2d.shape[0], dy2d.shape[1], x2d.shape[1])
     if cfg:
         use_norm = norm is not None and cfg % 100 in (9, 10, 12, 13)
-        _ext.ops().wgrad_gemm(out, dy2d.contiguous(), x2d.contiguous(), accumulate, cfg, norm if use_norm else None)
+        # the 4-wave kernel reads x through its row pitch (a padded [T, K] view, e.g. the gate_up input); others copy
+        strided_ok = cfg % 100 in (12, 13) and x2d.stride(1) == 1 and x2d.stride(0) % 8 == 0 and x2d.data_ptr() % 16 == 0
+        _ext.ops().wgrad_gemm(out, dy2d.contiguous(), x2d if strided_ok else x2d.contiguous(), accumulate, cfg,
+                              norm if use_norm else None)
         return use_norm
     if accumulate:
         out.addmm_(dy2d.t(), x2d)

@@ -167,3 +167,20 @@ def test_dgrad_4wave_hybrid_splitk(M, K, N, cfg):
     wi = (torch.arange(K * N, device=DEV) % 5 - 2).float().view(K, N).to(torch.bfloat16)
     got = _ext.ops().dgrad_gemm(ramp, wi, None, cfg)
     assert torch.equal(got, (ramp.float() @ wi.float()).to(torch.bfloat16))
+
+
+@pytest.mark.parametrize("cfg,T,N,K", [(13, 512, 22016 // 86 * 2, 2048), (13, 1024, 512, 768), (1213, 1024, 2048, 11008 // 256 * 256)])
+def test_wgrad_4wave_padded_x_pitch(cfg, T, N, K):
+    """x [T, K] as a view into a wider buffer (padded row pitch, e.g. the gate_up input written by the norm with
+    y_ld): bitwise the same dW (and norm slots) as from a contiguous x."""
+    torch.manual_seed(1)
+    dy = torch.randn(T, N, device=DEV, dtype=torch.bfloat16)
+    x = torch.randn(T, K, device=DEV, dtype=torch.bfloat16)
+    buf = torch.randn(T, K + 64, device=DEV, dtype=torch.bfloat16)
+    buf[:, :K] = x
+    cap = -(-N // 256) * -(-K // 128) * 32
+    o1, o2 = torch.empty(N, K, device=DEV, dtype=torch.bfloat16), torch.empty(N, K, device=DEV, dtype=torch.bfloat16)
+    s1, s2 = torch.zeros(cap, device=DEV), torch.zeros(cap, device=DEV)
+    _ext.ops().wgrad_gemm(o1, dy, x, False, cfg, s1)
+    _ext.ops().wgrad_gemm(o2, dy, buf[:, :K], False, cfg, s2)
+    assert torch.equal(o1, o2) and torch.equal(s1, s2)
