@@ -103,9 +103,6 @@ class MLP(nn.Module):
         return ops.lora_swiglu_mlp(h, self.gate_up_proj, self.down_proj, L["gate_up"], L["down"])
 
 
-_GU_PAD = int(os.environ.get("SFTAMD_GU_PAD", "0"))  # temporary A/B switch
-
-
 def _wide_ld(lora, key: str, weight) -> int:
     """Row width of the LoRA wide weight W' that consumes this norm's output (0: none), so the norm writes its output
     straight into the left block of the consumer's widened activation X' (ops.add_rms_norm y_ld)."""
@@ -132,10 +129,7 @@ class DecoderLayer(nn.Module):
         h, residual = ops.add_rms_norm(x, residual, ln.weight, ln.eps, _wide_ld(at.lora, "qkv", at.qkv_proj))
         a = at(h, rope_cs, cu_seqlens, max_seqlen)
         ln2 = self.post_attention_layernorm
-        ld2 = _wide_ld(ml.lora, "gate_up", ml.gate_up_proj)
-        if not ld2 and ml.lora is None and _GU_PAD:  # temporary A/B: gate_up input with a padded row pitch
-            ld2 = ml.gate_up_proj.shape[1] + _GU_PAD
-        h, residual = ops.add_rms_norm(a, residual, ln2.weight, ln2.eps, ld2)
+        h, residual = ops.add_rms_norm(a, residual, ln2.weight, ln2.eps, _wide_ld(ml.lora, "gate_up", ml.gate_up_proj))
         return ml(h), residual
 
 
