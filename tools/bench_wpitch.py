@@ -1,6 +1,6 @@
 """hipBLASLt / rocBLAS forward GEMMs y = x W^T with the WEIGHT's row pitch padded (W a [N, K] view into a [N, K + pad]
 buffer): SmolLM3's weights have 4 KiB rows (K = 2048 bf16). TunableOp tunes every (shape, pitch) in this process
-(written to gpurun_out/tune_wpitch.csv), then each variant is timed (median of 20), M = 8192.
+(written to gpurun_out/tune_wpitch.csv at exit), then each variant is timed (median of 20), M = 8192.
 
     python tools/bench_wpitch.py
 """
@@ -44,7 +44,6 @@ def main():
             w = buf[:, :K]
             t = timeit(lambda: torch.mm(x, w.t()))
             print(f"{name:8s} W pitch +{pad:3d}: {t:8.1f} us", flush=True)
-    tun.write_file()
 
 
 if __name__ == "__main__":
