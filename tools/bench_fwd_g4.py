@@ -1,5 +1,6 @@
 """Forward projections y = x W^T (M = 8192, SmolLM3 shapes) on the 4-wave backward kernel in its ROW / ROW form
-(gemm_tn cfg 70: 64-deep pair loop, 71: 4-slot ring of 32-deep steps) vs the row-contiguous persistent kernel (cfg 60)
+(gemm_tn cfg 70: 64-deep pair loop, 71: 4-slot ring of 32-deep steps; measured in r5_run33 and removed again,
+profiles/r5_gemm_fwd.md — the tool reports them as n/a on the current build) vs the row-contiguous persistent kernel (cfg 60)
 and torch.mm on its shipped TunableOp selection. Median of 20, us; max |diff| vs torch.mm.
 
     python tools/bench_fwd_g4.py
@@ -49,7 +50,11 @@ def main():
             t = timeit(lambda: torch.mm(x, w.t()))
             row.append(f"blas {t:8.1f}")
             for cfg in (60, 70, 71):
-                y = ops.gemm_tn(x, w, cfg)
+                try:
+                    y = ops.gemm_tn(x, w, cfg)
+                except RuntimeError:
+                    row.append(f"c{cfg}      n/a")
+                    continue
                 if rep == 0:
                     err = (y.float() - ref.float()).abs().max().item()
                     assert err < 0.05, (name, cfg, err)
