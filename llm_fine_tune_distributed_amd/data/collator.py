@@ -195,25 +195,41 @@ class DataLoader:
     def iter(self, skip: int = 0):
         q: "queue.Queue" = queue.Queue(maxsize=self.prefetch)
         sentinel = object()
+        stop = threading.Event()
+
+        def put(item) -> bool:  # False once the consumer has gone away
+            while not stop.is_set():
+                try:
+                    q.put(item, timeout=0.1)
+                    return True
+                except queue.Full:
+                    continue
+            return False
 
         def work():
             try:
                 for b in self._host_batches(skip):
-                    q.put(b)
+                    if not put(b):
+                        return
             except BaseException as e:  # surface errors in the main thread
-                q.put(e)
-            q.put(sentinel)
+                put(e)
+            put(sentinel)
 
-        t = threading.Thread(target=work, daemon=True)
+        t = threading.Thread(target=work, name="sftamd-collate", daemon=True)
         t.start()
-        while True:
-            b = q.get()
-            if b is sentinel:
-                break
-            if isinstance(b, BaseException):
-                raise b
-            yield {k: (v.to(self.device, non_blocking=True) if torch.is_tensor(v) else v) for k, v in b.items()}
-        t.join()
+        try:
+            while True:
+                b = q.get()
+                if b is sentinel:
+                    break
+                if isinstance(b, BaseException):
+                    raise b
+                yield {k: (v.to(self.device, non_blocking=True) if torch.is_tensor(v) else v) for k, v in b.items()}
+        finally:
+            # a consumer that stops early (max_steps inside an epoch, an exception) closes the generator: the
+            # producer must not stay parked on a full queue holding its pinned batches for the life of the process
+            stop.set()
+            t.join()
 
     def __iter__(self):
         return self.iter(0)

@@ -174,3 +174,18 @@ def test_collator_max_batch_tokens_bounds_every_batch():
                 idx = torch.randperm(len(ds), generator=g)[:B]
                 worst = max(worst, col(ds, idx)["input_ids"].numel())
             assert 0 < worst <= cap, (col.__dict__, B, worst, cap)
+
+
+def test_loader_producer_thread_ends_when_the_consumer_stops_early():
+    """A consumer that stops mid-epoch (max_steps) closes the loader's generator: the collate thread parked on the
+    full prefetch queue must exit instead of living on with its batches."""
+    import threading
+    ds = TokenizedDataset.synthetic(64, 1024, 16, 32, seed=0)
+    dl = C.DataLoader(ds, C.SFTCollator(pad_token_id=0), C.DistributedBatchSampler(len(ds), 2, 1, 0, shuffle=False),
+                      torch.device("cpu"), prefetch=1)
+    it = dl.iter()
+    next(it)
+    assert any(t.name == "sftamd-collate" for t in threading.enumerate())
+    it.close()
+    assert not any(t.name == "sftamd-collate" and t.is_alive() for t in threading.enumerate())
+    assert sum(1 for _ in dl) == len(dl)  # a full pass still sees every batch
