@@ -66,7 +66,9 @@ def test_ddp2_on_gpu_matches_single():
 def _rccl_world1(port, out):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     import torch.distributed as dist
+    from llm_fine_tune_distributed_amd.parallel import rccl_info
     from llm_fine_tune_distributed_amd.parallel.process_group import all_reduce_sum_async, nccl_options
+    rccl_info.enable(os.path.join(out, "rccl_log"))  # the parser of the N > 1 bench record, on a real RCCL log
     torch.cuda.set_device(0)
     dev = torch.device("cuda", 0)
     opts = nccl_options()
@@ -85,14 +87,17 @@ def _rccl_world1(port, out):
     w2.wait()
     cnt = pc.resolve()
     torch.cuda.synchronize()
+    summ = rccl_info.summarize(os.path.join(out, "rccl_log"))
     torch.save({"ok": bool(torch.equal(x, ref)), "cnt": float(cnt.item()),
-                "hp": bool(getattr(opts, "is_high_priority_stream", False))}, os.path.join(out, "rccl.pt"))
+                "hp": bool(getattr(opts, "is_high_priority_stream", False)), "summ": summ,
+                "warn": rccl_info.dist_warnings([summ], 1)}, os.path.join(out, "rccl.pt"))
     dist.destroy_process_group()
 
 
 def test_rccl_process_group_options_and_side_stream_collectives():
     """The RCCL (nccl backend) path itself on one MI355X: high-priority collective streams, in-place
-    reduce-scatter / all-gather issued from a side stream, and the async token-count all-reduce."""
+    reduce-scatter / all-gather issued from a side stream, the async token-count all-reduce, and the RCCL INFO-log
+    summary of parallel/rccl_info.py on the real log."""
     d = tempfile.mkdtemp()
     p = mp.get_context("spawn").Process(target=_rccl_world1, args=(_port(), d))
     p.start()
@@ -100,6 +105,11 @@ def test_rccl_process_group_options_and_side_stream_collectives():
     assert p.exitcode == 0
     r = torch.load(os.path.join(d, "rccl.pt"))
     assert r["ok"] and r["cnt"] == 3.0 and r["hp"]
+    # the INFO-log summary bench.py's strict N > 1 check relies on reads this RCCL's real log correctly (r5_run36:
+    # init_ok, nranks 1, version 2.26.6, 128 channels) and raises nothing at world size 1
+    s = r["summ"]
+    assert s is not None and s["init_ok"] and s["nranks"] == 1 and s["version"] and s["n_channels"]
+    assert r["warn"] == ([], False)
 
 
 @pytest.mark.parametrize("ipc", ["0", "1"])
