@@ -3,6 +3,12 @@ import sys
 
 import pytest
 
+# CPU threads per process: the multi-process tests run 2-8 ranks on this machine at once, each with torch's default
+# of one OpenMP thread per CPU, i.e. up to 8x oversubscribed spin-waiting teams. A quarter of the CPUs per process
+# unless the environment already says (the GPU boxes set OMP_NUM_THREADS); set before any test module imports torch,
+# and inherited by the spawned ranks.
+os.environ.setdefault("OMP_NUM_THREADS", str(max(1, (os.cpu_count() or 8) // 4)))
+
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 if ROOT not in sys.path:
     sys.path.insert(0, ROOT)
