@@ -410,7 +410,7 @@ struct Op32;
 template <>
 struct Op32<ROW> {
   rsrc_t r;
-  unsigned voff, jst, koff;  // lane offset; bytes per 64 rows; K progress
+  unsigned voff, jst, koff, kmax;  // lane offset; bytes per 64 rows; K progress; its cap (the last step)
   int off;   // fragment 0 (fragment i is 1024 B further)
   __device__ __forceinline__ void init(const u16* base, long ld, int r0, long k0, int w, int lane, int sub) {
     // piece P = w + 4 j: 16 rows 16 P + lr (lr = lane >> 2), slot lane & 3; (row >> 2) & 3 = lr >> 2 for all pieces
@@ -419,10 +419,12 @@ struct Op32<ROW> {
     voff = (unsigned)(((16 * w + lr) * ld + 8 * ch) * 2);
     jst = (unsigned)(128 * ld);
     koff = 0;
+    kmax = 0xFFFFFFFFu;
     const int g = lane >> 4, ii = lane & 15;
     off = (128 * sub + ii) * 64 + 16 * (g ^ sel4(ii >> 2));
   }
-  __device__ __forceinline__ void advance() { koff += 2 * BK32; }
+  __device__ __forceinline__ void limit(int nsteps) { kmax = (unsigned)(nsteps - 1) * 2 * BK32; }
+  __device__ __forceinline__ void advance() { koff = min(koff + 2 * BK32, kmax); }
   __device__ __forceinline__ void piece(char* opb, int w, int j) const {
     bldsx4(r, opb + (w + 4 * j) * 1024, voff, koff + j * jst);
   }
@@ -432,7 +434,7 @@ struct Op32<ROW> {
 template <>
 struct Op32<TR> {
   rsrc_t r;
-  unsigned voff, jst, kst, koff;  // lane offset; bytes per 16 rows; per step (32 rows); K progress
+  unsigned voff, jst, kst, koff, kmax;  // lane offset; bytes per 16 rows; per step (32 rows); K progress; its cap
   int ob, x2;
   __device__ __forceinline__ void init(const u16* base, long ld, int c0, long k0, int w, int lane, int sub) {
     // piece (image j >> 1, q = w + 4 (j & 1)): rows 4q + lr4; xt(row) = 2 (lr4 | ((w >> 1) & 1) << 2) for all
@@ -442,11 +444,13 @@ struct Op32<TR> {
     jst = (unsigned)(32 * ld);
     kst = (unsigned)(2 * BK32 * ld);
     koff = 0;
+    kmax = 0xFFFFFFFFu;
     const int g = lane >> 4, ii = lane & 15, qq = ii >> 2, pp = ii & 3;
     x2 = qq | ((g & 1) << 2);
     ob = sub * IMG32 + (8 * g + qq) * ROWB_T + 8 * pp;
   }
-  __device__ __forceinline__ void advance() { koff += kst; }
+  __device__ __forceinline__ void limit(int nsteps) { kmax = (unsigned)(nsteps - 1) * kst; }
+  __device__ __forceinline__ void advance() { koff = min(koff + kst, kmax); }
   __device__ __forceinline__ void piece(char* opb, int w, int j) const {
     bldsx4(r, opb + (j >> 1) * IMG32 + (w + 4 * (j & 1)) * 1024, voff, koff + (j & 1) * jst + 256 * (j >> 1));
   }
@@ -493,19 +497,84 @@ __device__ __forceinline__ void rstep(f32x4 (&acc)[8][8], const bf16x8 (&fa)[8],
   }
 }
 
+// Interleaved form of rstep (cfg 14): the same work, but after the barrier the 16 fragment reads and the 8 DMA pieces
+// go ONE PER MFMA GAP (op k after MFMA 8 + 7k/3, in the order B0 B1 D0 B2 B3 D1 .. A6 A7 D7) instead of a burst of
+// 2 fragments + 1 piece + their SALU behind every 8 MFMAs. One wave per SIMD issues in order: a burst that outlasts
+// the 16-cycle gap of v_mfma_f32_16x16x32_bf16 idles the matrix pipe (hipBLASLt's MT256x256x64 loop places one
+// ds_read / buffer_load between consecutive MFMAs). B fragments first: the next step's group 0 needs all 8 B and A0.
+template <int LA, int LB, bool READ, bool DMA, int VM, bool BAR, int IL>
+__device__ __forceinline__ void rstep_il(f32x4 (&acc)[8][8], const bf16x8 (&fa)[8], const bf16x8 (&fb)[8],
+                                         bf16x8 (&ra)[8], bf16x8 (&rb)[8], const char* __restrict__ nxt,
+                                         char* __restrict__ cur, Op32<LA>& oa, Op32<LB>& ob, int w) {
+  // IL bit 0: fragment reads interleaved (else 2 behind each group), bit 1: DMA pieces interleaved (else 1 per group)
+  __builtin_amdgcn_s_waitcnt(waitcnt_imm(VM, 15));
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      mfma(acc[i][j], fb[j], fa[i]);
+      if (BAR && i == 0 && j == 7) {
+        __builtin_amdgcn_s_waitcnt(waitcnt_imm(63, 0));
+        __builtin_amdgcn_s_barrier();
+      }
+      const int n = 8 * i + j;
+      const int k = n < 8 ? -1 : ((n - 8) * 3 + 6) / 7;  // the op placed after MFMA n, if any
+      const bool slot = k >= 0 && k < 24 && 8 + (k * 7) / 3 == n;
+      const int t = k / 3, r = k % 3;
+      if (READ) {
+        int f = -1;
+        if ((IL & 1) && slot && r < 2) f = 2 * t + r;
+        if (!(IL & 1) && j == 7) {
+          if (i < 4) {
+            rb[2 * i] = ob.frag(nxt + OPB32, 2 * i);
+            rb[2 * i + 1] = ob.frag(nxt + OPB32, 2 * i + 1);
+          } else {
+            ra[2 * i - 8] = oa.frag(nxt, 2 * i - 8);
+            ra[2 * i - 7] = oa.frag(nxt, 2 * i - 7);
+          }
+        }
+        if (f >= 0) {
+          if (f < 8) rb[f] = ob.frag(nxt + OPB32, f);
+          else ra[f - 8] = oa.frag(nxt, f - 8);
+        }
+      }
+      if (DMA) {
+        int d = -1;
+        if ((IL & 2) && slot && r == 2) d = t;
+        if (!(IL & 2) && j == 7) d = i;
+        if (d >= 0) {
+          if (d < 4) oa.piece(cur, w, d);
+          else ob.piece(cur + OPB32, w, d - 4);
+        }
+      }
+    }
+  }
+  if (DMA) {
+    oa.advance();
+    ob.advance();
+  }
+}
+
 // four steps (u = 4 b .. 4 b + 3 on slots S0..S3); LAST: no DMA (steps past the end), counted waits shrink
-template <int LA, int LB, bool LAST>
+template <int LA, int LB, bool LAST, int IL>
 __device__ __forceinline__ void rbody(char* __restrict__ S0, char* __restrict__ S1, char* __restrict__ S2,
                                       char* __restrict__ S3, Op32<LA>& oa, Op32<LB>& ob, int w, f32x4 (&acc)[8][8],
                                       bf16x8 (&a0)[8], bf16x8 (&b0)[8], bf16x8 (&a1)[8], bf16x8 (&b1)[8]) {
   constexpr bool D = !LAST;
-  rstep<LA, LB, true, D, 16, true>(acc, a0, b0, a1, b1, S1, S0, oa, ob, w);
-  rstep<LA, LB, true, D, LAST ? 8 : 16, true>(acc, a1, b1, a0, b0, S2, S1, oa, ob, w);
-  rstep<LA, LB, true, D, LAST ? 0 : 16, true>(acc, a0, b0, a1, b1, S3, S2, oa, ob, w);
-  rstep<LA, LB, D, D, LAST ? 0 : 16, D>(acc, a1, b1, a0, b0, S0, S3, oa, ob, w);
+  if constexpr (IL != 0) {
+    rstep_il<LA, LB, true, D, 16, true, IL>(acc, a0, b0, a1, b1, S1, S0, oa, ob, w);
+    rstep_il<LA, LB, true, D, LAST ? 8 : 16, true, IL>(acc, a1, b1, a0, b0, S2, S1, oa, ob, w);
+    rstep_il<LA, LB, true, D, LAST ? 0 : 16, true, IL>(acc, a0, b0, a1, b1, S3, S2, oa, ob, w);
+    rstep_il<LA, LB, D, D, LAST ? 0 : 16, D, IL>(acc, a1, b1, a0, b0, S0, S3, oa, ob, w);
+  } else {
+    rstep<LA, LB, true, D, 16, true>(acc, a0, b0, a1, b1, S1, S0, oa, ob, w);
+    rstep<LA, LB, true, D, LAST ? 8 : 16, true>(acc, a1, b1, a0, b0, S2, S1, oa, ob, w);
+    rstep<LA, LB, true, D, LAST ? 0 : 16, true>(acc, a0, b0, a1, b1, S3, S2, oa, ob, w);
+    rstep<LA, LB, D, D, LAST ? 0 : 16, D>(acc, a1, b1, a0, b0, S0, S3, oa, ob, w);
+  }
 }
 
-template <int LA, int LB>
+template <int LA, int LB, int IL>
 __device__ __forceinline__ void mainloop_ring(char* __restrict__ S0, char* __restrict__ S1, char* __restrict__ S2,
                                               char* __restrict__ S3, int nb, Op32<LA>& oa, Op32<LB>& ob, int w,
                                               f32x4 (&acc)[8][8]) {
@@ -528,11 +597,21 @@ __device__ __forceinline__ void mainloop_ring(char* __restrict__ S0, char* __res
   for (int i = 0; i < 8; ++i) b0[i] = ob.frag(S0 + OPB32, i);
 #pragma unroll
   for (int i = 0; i < 8; ++i) a0[i] = oa.frag(S0, i);
-  for (int b = 0; b < nb - 1; ++b) rbody<LA, LB, false>(S0, S1, S2, S3, oa, ob, w, acc, a0, b0, a1, b1);
-  rbody<LA, LB, true>(S0, S1, S2, S3, oa, ob, w, acc, a0, b0, a1, b1);
+  if constexpr (IL == 0) {
+    for (int b = 0; b < nb - 1; ++b) rbody<LA, LB, false, IL>(S0, S1, S2, S3, oa, ob, w, acc, a0, b0, a1, b1);
+    rbody<LA, LB, true, IL>(S0, S1, S2, S3, oa, ob, w, acc, a0, b0, a1, b1);
+  } else {
+    // ONE loop body for every K block, the last included: its DMA re-reads the final step (the offsets saturate,
+    // Op32::limit) into slots nobody reads again, and its reads of "step 4 nb" are never used. No MFMA code after
+    // the loop, so the register allocator has no loop-exit block in which to move accumulators between AGPRs and
+    // VGPRs right behind an asm MFMA it cannot see the latency of (it did, at the LAST body: wrong sums).
+    for (int b = 0; b < nb; ++b) rbody<LA, LB, false, IL>(S0, S1, S2, S3, oa, ob, w, acc, a0, b0, a1, b1);
+    __builtin_amdgcn_s_waitcnt(waitcnt_imm(0, 0));  // the LDS-DMA past the end lands before the LDS is released
+  }
 }
 
-template <int LA, int LB, int EPI, bool RING>
+// RING: 0 = the K-tile pair loop, 1 = the 4-slot ring, 2..4 = the ring with interleaved issue (rstep_il, IL = RING - 1)
+template <int LA, int LB, int EPI, int RING>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1)))
 g4_kernel(const u16* __restrict__ A, const u16* __restrict__ B, long lda, long ldb, int kred, int nbm, int nbn,
           int group, int ndp, int splits, Epi ea) {
@@ -574,12 +653,16 @@ g4_kernel(const u16* __restrict__ A, const u16* __restrict__ B, long lda, long l
   for (int i = 0; i < 8; ++i)
 #pragma unroll
     for (int j = 0; j < 8; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  if constexpr (RING) {
+  if constexpr (RING != 0) {
     Op32<LA> oa;
     Op32<LB> ob;
     oa.init(A, lda, m0, k0, w, lane, wm);
     ob.init(B, ldb, n0, k0, w, lane, wn);
-    mainloop_ring<LA, LB>(smem, smem + SLOT32, smem + 2 * SLOT32, smem + 3 * SLOT32, p1 - p0, oa, ob, w, acc);
+    if constexpr (RING >= 2) {
+      oa.limit(4 * (p1 - p0));
+      ob.limit(4 * (p1 - p0));
+    }
+    mainloop_ring<LA, LB, RING - 1>(smem, smem + SLOT32, smem + 2 * SLOT32, smem + 3 * SLOT32, p1 - p0, oa, ob, w, acc);
   } else {
     Op<LA> oa;
     Op<LB> ob;
@@ -602,7 +685,7 @@ g4_kernel(const u16* __restrict__ A, const u16* __restrict__ B, long lda, long l
 
 static int group_m() { return 8; }  // GROUP_M tile order
 
-template <int LA, int LB, int EPI, bool RING>
+template <int LA, int LB, int EPI, int RING>
 static void launch(const u16* A, long lda, const u16* B, long ldb, int M, int N, int kred, int ndp, int splits,
                    const Epi& ea) {
   const int nbm = M / 256, nbn = N / 256, tiles = nbm * nbn;
@@ -618,7 +701,7 @@ static void launch(const u16* A, long lda, const u16* B, long ldb, int M, int N,
 // round of 256 workgroups (hybrid) or all tiles are split over the token axis into fp32 slabs + ordered fixup.
 // nrm: gradient-norm slots (8 per whole tile, waves 0..3 written; one per fixup block of a split tile).
 void g4_wgrad(const at::Tensor& dy, const at::Tensor& x, at::Tensor& out, bool accumulate, int splits, bool hybrid,
-              float* nrm, long nrm_cap, bool ring) {
+              float* nrm, long nrm_cap, int ring) {
   const int T = dy.size(0), N = dy.size(1), K = x.size(1);
   SFT_CHECK(N % 256 == 0 && K % 256 == 0 && T % 128 == 0 && T > 0, "wgrad 4-wave: N, K % 256, T % 128");
   SFT_CHECK((uintptr_t)dy.data_ptr() % 16 == 0 && (uintptr_t)x.data_ptr() % 16 == 0 &&
@@ -638,12 +721,15 @@ void g4_wgrad(const at::Tensor& dy, const at::Tensor& x, at::Tensor& out, bool a
   ea.ldc = K;
   ea.P = nsk > 0 ? part.data_ptr<float>() : nrm;
   ea.flags = (accumulate ? 1 : 0) | (nrm != nullptr ? 2 : 0);
-  if (ring)
-    g4::launch<g4::TR, g4::TR, g4::EPI_STORE, true>((const u16*)dy.data_ptr(), N, (const u16*)x.data_ptr(), x.stride(0),
-                                                    N, K, T, ndp, nsk > 0 ? splits : 1, ea);
-  else
-    g4::launch<g4::TR, g4::TR, g4::EPI_STORE, false>((const u16*)dy.data_ptr(), N, (const u16*)x.data_ptr(), x.stride(0),
-                                                     N, K, T, ndp, nsk > 0 ? splits : 1, ea);
+  auto go = [&](auto rg) {
+    g4::launch<g4::TR, g4::TR, g4::EPI_STORE, decltype(rg)::value>((const u16*)dy.data_ptr(), N, (const u16*)x.data_ptr(),
+                                                                   x.stride(0), N, K, T, ndp, nsk > 0 ? splits : 1, ea);
+  };
+  if (ring == 2) go(std::integral_constant<int, 4>());
+  else if (ring == 3) go(std::integral_constant<int, 2>());
+  else if (ring == 4) go(std::integral_constant<int, 3>());
+  else if (ring == 1) go(std::integral_constant<int, 1>());
+  else go(std::integral_constant<int, 0>());
   if (nsk > 0) {
     const long n8 = (long)nsk * 65536 / 8;
     splitk_fixup_kernel<256, 256><<<(unsigned)((n8 + 255) / 256), 256, 0, cur_stream()>>>(
@@ -658,7 +744,7 @@ void g4_wgrad(const at::Tensor& dy, const at::Tensor& x, at::Tensor& out, bool a
 // Wave quantisation (plain epilogue): a grid that is not whole rounds of 256 workgroups runs its whole rounds as
 // whole tiles and the leftover tiles split over the reduction into fp32 slabs + the ordered fixup, e.g. the recipe's
 // padding-free M = 10240: gate_up / lm_head dgrads are 40 x 8 = 320 tiles = 1.25 rounds -> 256 + 64 x 4 pieces.
-void g4_dgrad(const at::Tensor& dy, const at::Tensor& w, u16* out, long ldo, const u16* gu, int I, bool ring) {
+void g4_dgrad(const at::Tensor& dy, const at::Tensor& w, u16* out, long ldo, const u16* gu, int I, int ring) {
   const int M = dy.size(0), K = dy.size(1), N = w.size(1);
   SFT_CHECK(M % 256 == 0 && N % 256 == 0 && K % 128 == 0 && K > 0, "dgrad 4-wave: M, N % 256, K % 128");
   g4::Epi ea{};
@@ -687,12 +773,17 @@ void g4_dgrad(const at::Tensor& dy, const at::Tensor& w, u16* out, long ldo, con
   };
   using SW = std::integral_constant<int, g4::EPI_SWIGLU_BWD>;
   using ST = std::integral_constant<int, g4::EPI_STORE>;
+  using R0 = std::integral_constant<int, 0>;
+  using R1 = std::integral_constant<int, 1>;
+  using R2 = std::integral_constant<int, 4>;  // interleaved reads and DMA
   if (gu != nullptr) {
-    if (ring) go(SW(), std::true_type());
-    else go(SW(), std::false_type());
+    if (ring == 2) go(SW(), R2());
+    else if (ring == 1) go(SW(), R1());
+    else go(SW(), R0());
   } else {
-    if (ring) go(ST(), std::true_type());
-    else go(ST(), std::false_type());
+    if (ring == 2) go(ST(), R2());
+    else if (ring == 1) go(ST(), R1());
+    else go(ST(), R0());
   }
   if (splits > 1) {
     SFT_TRACE("dgrad.splitk");

@@ -607,7 +607,7 @@ void launch(const at::Tensor& dy, const at::Tensor& x, at::Tensor& out, bool acc
 }  // namespace wgrad
 
 void g4_wgrad(const at::Tensor& dy, const at::Tensor& x, at::Tensor& out, bool accumulate, int splits, bool hybrid,
-              float* nrm, long nrm_cap, bool ring);
+              float* nrm, long nrm_cap, int ring);
 
 // cfg: 0 = auto, 1 = 256x256 (8 waves 2x4), 2 = 256x128 (8 waves 4x2); +2 = register-pipelined loop
 // norm (optional, fp32, contiguous): gradient-norm partial slots for the ring variants (cfg 9 / 10 and their split-K
@@ -625,7 +625,7 @@ void wgrad_gemm(at::Tensor out, at::Tensor dy, at::Tensor x, bool accumulate, in
   SFT_CHECK(dy.dim() == 2 && x.dim() == 2 && out.dim() == 2, "wgrad_gemm: 2-D operands");
   // x may have a padded row pitch (a [T, K] view into a wider buffer) on the 4-wave kernel (cfg 12 / 13 family)
   SFT_CHECK(x.stride(1) == 1 && x.stride(0) % 8 == 0 && x.stride(0) >= x.size(1), "wgrad_gemm: x rows contiguous");
-  SFT_CHECK(x.stride(0) == x.size(1) || cfg % 100 == 12 || cfg % 100 == 13, "wgrad_gemm: a padded x pitch needs cfg 12 / 13");
+  SFT_CHECK(x.stride(0) == x.size(1) || (cfg % 100 >= 12 && cfg % 100 <= 16), "wgrad_gemm: a padded x pitch needs cfg 12 / 13 / 14");
   const int64_t T = dy.size(0), N = dy.size(1), K = x.size(1);
   SFT_CHECK(x.size(0) == T && out.size(0) == N && out.size(1) == K, "wgrad_gemm: shape mismatch");
   SFT_CHECK(T % 32 == 0 && T > 0, "wgrad_gemm: T must be a positive multiple of 32");
@@ -640,18 +640,18 @@ void wgrad_gemm(at::Tensor out, at::Tensor dy, at::Tensor x, bool accumulate, in
   const bool hybrid = cfg >= 1000;
   const int splits = (int)((cfg % 1000) / 100);
   cfg %= 100;
-  SFT_CHECK(splits <= 1 || ((cfg == 9 || cfg == 10 || cfg == 12 || cfg == 13) && T / 32 >= splits),
+  SFT_CHECK(splits <= 1 || ((cfg == 9 || cfg == 10 || (cfg >= 12 && cfg <= 16)) && T / 32 >= splits),
             "wgrad_gemm split-K: ring cfg 9/10 or the 4-wave cfg 12 with at least one 32-token step per split");
   float* nrm = nullptr;
   long nrm_cap = 0;
   if (norm.has_value() && norm->defined()) {
-    SFT_CHECK(cfg == 9 || cfg == 10 || cfg == 12 || cfg == 13, "wgrad_gemm: norm partials need cfg 9 / 10 / 12 / 13");
+    SFT_CHECK(cfg == 9 || cfg == 10 || (cfg >= 12 && cfg <= 16), "wgrad_gemm: norm partials need cfg 9 / 10 / 12-14");
     SFT_CHECK(norm->scalar_type() == at::kFloat && norm->is_contiguous() && norm->is_cuda(), "wgrad_gemm: fp32 norm slots");
     nrm = norm->data_ptr<float>();
     nrm_cap = norm->numel();
   }
-  if (cfg == 12 || cfg == 13) {  // 4 waves of 128 x 128, AGPR accumulators (csrc/gemm_4w.hip); 13: 4-slot ring
-    g4_wgrad(dy, x, out, accumulate, splits, hybrid, nrm, nrm_cap, cfg == 13);
+  if (cfg >= 12 && cfg <= 16) {  // 4 waves of 128 x 128, AGPR accumulators (csrc/gemm_4w.hip); 13: 4-slot ring;
+    g4_wgrad(dy, x, out, accumulate, splits, hybrid, nrm, nrm_cap, (int)cfg - 12);  // 14: ring, interleaved issue
     return;
   }
   if (splits > 1) {

@@ -30,8 +30,9 @@ import shutil
 import subprocess
 import sys
 import tempfile
+import threading
 import time
-from typing import List
+from typing import List, Tuple
 
 
 def _free_port(addr: str) -> int:
@@ -66,6 +67,36 @@ def _spawn(n: int, cmd: List[str], addr: str, port: int, restart: int, node_rank
         env.setdefault("OMP_NUM_THREADS", "1")
         procs.append(subprocess.Popen(cmd, env=env, start_new_session=new_session, preexec_fn=_die_with_parent))
     return procs
+
+
+class _ExitLog:
+    """Children's exits in ARRIVAL order: one reaper thread per child blocks in its waitpid and appends
+    (local rank, code) the moment that child exits. A polling loop that collects every exit seen in one interval
+    and takes the lowest rank misattributes a failure when the faulting rank's peer dies on the broken collective
+    inside the same interval (rank 1 exits 23, rank 0 then exits 1: the group must be reported as failed by rank 1)."""
+
+    def __init__(self, procs: List[subprocess.Popen]):
+        self._lock = threading.Lock()
+        self.order: List[Tuple[int, int]] = []
+        self._threads = [threading.Thread(target=self._reap, args=(i, p), daemon=True) for i, p in enumerate(procs)]
+        for t in self._threads:
+            t.start()
+
+    def _reap(self, i: int, p: subprocess.Popen):
+        code = p.wait()
+        with self._lock:
+            self.order.append((i, code))
+
+    def first_failure(self):
+        with self._lock:
+            for i, c in self.order:
+                if c != 0:
+                    return i, c
+        return None
+
+    def count(self) -> int:
+        with self._lock:
+            return len(self.order)
 
 
 def _signal(p: subprocess.Popen, sig, group: bool):
@@ -192,15 +223,15 @@ def _run_group(a, cmd, hb_dir: str) -> int:
         procs = _spawn(a.nproc_per_node, cmd, a.master_addr, port, restart, a.node_rank, a.nnodes,
                        new_session=not a.same_session, hb_dir=hb_dir)
         grp = not a.same_session
+        exits = _ExitLog(procs)
         failed = None
         try:
             while True:
-                codes = [p.poll() for p in procs]
-                bad = [(i, c) for i, c in enumerate(codes) if c not in (None, 0)]
-                if bad:
-                    failed = bad[0]
+                bad = exits.first_failure()
+                if bad is not None:
+                    failed = bad
                     break
-                if all(c == 0 for c in codes):
+                if exits.count() == len(procs):
                     return 0
                 if a.deadline > 0 and time.time() - t_run > a.deadline:
                     failed = (-1, 124, f"deadline of {a.deadline:.0f} s exceeded")

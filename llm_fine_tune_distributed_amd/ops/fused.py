@@ -43,6 +43,10 @@ def _weight_grad_done(param: torch.Tensor) -> None:
 
 
 _WGRAD_MODE = os.environ.get("SFTAMD_WGRAD", "auto")  # auto | blas | <cfg int> (kernel variant)
+# the 4-wave ring's issue schedule (csrc/gemm_4w.hip): 13 = 2 fragments + 1 DMA piece behind every 8 MFMAs,
+# 14 = one LDS read / DMA piece per MFMA gap (rstep_il): 110.8 / 111.0 vs 109.7 / 109.5 samples/s in the step
+# (interleaved A/B, identical loss; profiles/r6_g4_interleave.md)
+_G4_RING = int(os.environ.get("SFTAMD_G4_RING", "14"))
 
 
 def _wgrad_cfg(T: int, N: int, K: int) -> int:
@@ -65,7 +69,7 @@ def _wgrad_cfg(T: int, N: int, K: int) -> int:
         # gate_up (688 tiles): 0.568 vs 0.578 ms (cfg 10); down_proj (344 tiles = 1.34 rounds): hybrid, the 88 tiles
         # past the whole round split 2 ways over the tokens (1213): 0.301 vs 0.341 (cfg 13) vs 0.349 (cfg 9);
         # lm_head / tied embedding (4008 tiles) stays on cfg 10: 3.195 vs 3.213 ms (profiles/r3_bwd_gemm_4wave.md)
-        return 1213 if tiles < 512 and (T // 128) >= 2 else 13
+        return 1200 + _G4_RING if tiles < 512 and (T // 128) >= 2 else _G4_RING
     if N % 256 == 0 and K % 256 == 0 and tiles >= 512:
         return 10
     if (N % 256 == 0 and K % 256 == 0 and 64 < (N // 256) * (K // 256) <= 128 and (T // 32) % 2 == 0
@@ -90,9 +94,9 @@ def _wgrad_mm(out: torch.Tensor, dy2d: torch.Tensor, x2d: torch.Tensor, accumula
     if _ext.use_hip(dy2d) and dy2d.dtype == torch.bfloat16 and out.is_contiguous():
         cfg = _wgrad_cfg(dy2d.shape[0], dy2d.shape[1], x2d.shape[1])
     if cfg:
-        use_norm = norm is not None and cfg % 100 in (9, 10, 12, 13)
+        use_norm = norm is not None and cfg % 100 in (9, 10, 12, 13, 14)
         # the 4-wave kernel reads x through its row pitch (a padded [T, K] view, e.g. the gate_up input); others copy
-        strided_ok = cfg % 100 in (12, 13) and x2d.stride(1) == 1 and x2d.stride(0) % 8 == 0 and x2d.data_ptr() % 16 == 0
+        strided_ok = cfg % 100 in (12, 13, 14) and x2d.stride(1) == 1 and x2d.stride(0) % 8 == 0 and x2d.data_ptr() % 16 == 0
         _ext.ops().wgrad_gemm(out, dy2d.contiguous(), x2d if strided_ok else x2d.contiguous(), accumulate, cfg,
                               norm if use_norm else None)
         return use_norm
@@ -250,7 +254,7 @@ def _dgrad_cfg(dy2d: torch.Tensor, swiglu: bool = False) -> int:
     backward epilogue stays on cfg 7 (its LDS-staged epilogue: 0.436 vs 0.58 ms for the register epilogue)."""
     K = dy2d.shape[1]
     if not swiglu and K % 128 == 0:
-        return 13 if K > 4096 else 12
+        return _G4_RING if K > 4096 else 12
     return 7 if K % 64 == 0 else 5
 
 
@@ -260,7 +264,7 @@ def dgrad_mm(dy2d: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
     are not a multiple of 128 of at most 4096 output features into at most 4096 inputs on cfg 7 / 5."""
     if _dgrad_ok(dy2d, w):
         cfg = _dgrad_cfg(dy2d)
-        if cfg in (12, 13) or _DGRAD_MODE == "hip" or (dy2d.shape[1] <= 4096 and w.shape[1] <= 4096):
+        if cfg in (12, 13, 14) or _DGRAD_MODE == "hip" or (dy2d.shape[1] <= 4096 and w.shape[1] <= 4096):
             return _ext.ops().dgrad_gemm(dy2d, w, None, cfg)
     return torch.mm(dy2d, w)
 

@@ -73,3 +73,20 @@ def test_zero1_checkpoint_kill_resume_is_bit_exact(n):
     # resumed call ran steps 3..6: its train_loss is their mean (not a sum over 4 steps divided by 6)
     assert abs(res["train_loss"] - sum(res["log"][-4:]) / 4) < 1e-6
     assert abs(base["train_loss"] - sum(base["log"][-6:]) / 6) < 1e-6
+
+
+def test_launcher_reports_the_first_rank_to_fail(tmp_path):
+    """Rank 1 exits 23; rank 0 dies with 1 a moment later (as on a broken collective) — both inside ONE monitor
+    interval. The launcher must blame rank 1 and return 23 (arrival order), not the lowest failing rank index."""
+    script = tmp_path / "two_failures.py"
+    script.write_text(
+        "import os, sys, time\n"
+        "r = int(os.environ['RANK'])\n"
+        "time.sleep(0.5 if r == 1 else 0.9)\n"
+        "sys.exit(23 if r == 1 else 1)\n")
+    env = dict(os.environ, PYTHONPATH=ROOT)
+    cmd = [sys.executable, "-m", "llm_fine_tune_distributed_amd.launch", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--monitor-interval", "3", "--grace", "2", str(script)]
+    r = subprocess.run(cmd, env=env, cwd=ROOT, capture_output=True, text=True, timeout=60)
+    assert r.returncode == 23, (r.returncode, r.stderr[-2000:])
+    assert "local rank 1 exited with code 23" in r.stderr

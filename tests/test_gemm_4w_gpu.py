@@ -28,7 +28,9 @@ def rel_err(a, b):
                                        (1212, 384, 4352, 4096),
                                        # cfg 13: the 4-slot ring of 32-deep steps
                                        (13, 128, 256, 256), (13, 384, 768, 512), (13, 1024, 2304, 4352),
-                                       (213, 512, 512, 512), (313, 384, 512, 256), (1313, 256, 4096, 4352)])
+                                       (213, 512, 512, 512), (313, 384, 512, 256), (1313, 256, 4096, 4352),
+                                       # cfg 14: the same ring with one read / DMA piece per MFMA gap
+                                       (14, 128, 256, 256), (14, 1024, 2304, 4352), (1314, 256, 4096, 4352)])
 @pytest.mark.parametrize("accumulate", [False, True])
 def test_wgrad_4wave(cfg, T, N, K, accumulate):
     torch.manual_seed(0)
@@ -43,7 +45,7 @@ def test_wgrad_4wave(cfg, T, N, K, accumulate):
     assert err <= 0.02 * want.abs().max().item(), err
 
 
-@pytest.mark.parametrize("cfg", [12, 13])
+@pytest.mark.parametrize("cfg", [12, 13, 14])
 def test_wgrad_4wave_exact_structure(cfg):
     """Integer-valued operands (exact in fp32): a permuted token, row or column mapping anywhere in the staging,
     the transposed reads or the register epilogue changes the result bit for bit."""
@@ -57,7 +59,8 @@ def test_wgrad_4wave_exact_structure(cfg):
 
 
 @pytest.mark.parametrize("cfg,T,N,K", [(12, 256, 512, 768), (212, 512, 512, 512), (1312, 256, 4096, 4352),
-                                       (13, 256, 512, 768), (1313, 256, 4096, 4352), (1213, 1024, 2048, 11008)])
+                                       (13, 256, 512, 768), (1313, 256, 4096, 4352), (1213, 1024, 2048, 11008),
+                                       (1214, 1024, 2048, 11008)])
 @pytest.mark.parametrize("accumulate", [False, True])
 def test_wgrad_4wave_norm_slots(cfg, T, N, K, accumulate):
     """Norm partials (register epilogue / split-K fixup) sum to the squared norm of the stored bf16 gradient
@@ -95,7 +98,7 @@ def test_wgrad_4wave_matches_ring_split_exactly():
 
 @pytest.mark.parametrize("M,K,N,wpad", [(256, 128, 256, 0), (512, 2048, 768, 0), (256, 384, 512, 64),
                                         (768, 1024, 256, 0), (2048, 11008, 2048, 0)])
-@pytest.mark.parametrize("cfg", [12, 13])
+@pytest.mark.parametrize("cfg", [12, 13, 14])
 def test_dgrad_4wave_plain(M, K, N, wpad, cfg):
     torch.manual_seed(0)
     dy = torch.randn(M, K, device=DEV, dtype=torch.bfloat16)
@@ -113,7 +116,7 @@ def test_dgrad_4wave_plain(M, K, N, wpad, cfg):
 
 
 @pytest.mark.parametrize("M,K,N", [(256, 256, 256), (512, 2048, 512), (1024, 128, 768)])
-@pytest.mark.parametrize("cfg", [12, 13])
+@pytest.mark.parametrize("cfg", [12, 13, 14])
 def test_dgrad_4wave_swiglu_bwd(M, K, N, cfg):
     torch.manual_seed(1)
     dy = torch.randn(M, K, device=DEV, dtype=torch.bfloat16)
@@ -128,7 +131,7 @@ def test_dgrad_4wave_swiglu_bwd(M, K, N, cfg):
     assert rel_err(dgu, want) < 1e-2
 
 
-@pytest.mark.parametrize("cfg", [12, 13])
+@pytest.mark.parametrize("cfg", [12, 13, 14])
 @pytest.mark.parametrize("swiglu", [True, False])
 def test_dgrad_4wave_wave_tail(swiglu, cfg, monkeypatch):
     """SmolLM3 down projection grid (43 x 32 tiles = 5.375 rounds): the whole rounds on the 4-wave kernel + the
@@ -151,7 +154,7 @@ def test_dgrad_4wave_wave_tail(swiglu, cfg, monkeypatch):
         assert rel_err(got, want) < 1e-2, tail
 
 
-@pytest.mark.parametrize("cfg", [12, 13])
+@pytest.mark.parametrize("cfg", [12, 13, 14])
 @pytest.mark.parametrize("M,K,N", [(10240, 1024, 2048), (2560, 4096, 2048), (4352, 512, 4096)])
 def test_dgrad_4wave_hybrid_splitk(M, K, N, cfg):
     """Grids that are not whole rounds of 256 workgroups (the recipe's padding-free M = 10240: 320 tiles) run the
@@ -184,3 +187,25 @@ def test_wgrad_4wave_padded_x_pitch(cfg, T, N, K):
     _ext.ops().wgrad_gemm(o1, dy, x, False, cfg, s1)
     _ext.ops().wgrad_gemm(o2, dy, buf[:, :K], False, cfg, s2)
     assert torch.equal(o1, o2) and torch.equal(s1, s2)
+
+
+@pytest.mark.parametrize("kind", ["wgrad", "dgrad"])
+def test_4wave_interleaved_ring_is_bitwise_the_ring(kind):
+    """cfg 14 issues the same fragment reads, DMA pieces and MFMAs as cfg 13 in another order (one read / piece per
+    MFMA gap): every accumulator sees the same MFMA sequence, so the outputs are bitwise equal."""
+    torch.manual_seed(5)
+    if kind == "wgrad":
+        T, N, K = 1024, 768, 1024
+        dy = torch.randn(T, N, device=DEV, dtype=torch.bfloat16)
+        x = torch.randn(T, K, device=DEV, dtype=torch.bfloat16)
+        o13 = torch.empty(N, K, device=DEV, dtype=torch.bfloat16)
+        o14 = torch.empty_like(o13)
+        _ext.ops().wgrad_gemm(o13, dy, x, False, 13)
+        _ext.ops().wgrad_gemm(o14, dy, x, False, 14)
+    else:
+        M, K, N = 1024, 4608, 768
+        dy = torch.randn(M, K, device=DEV, dtype=torch.bfloat16)
+        w = (0.02 * torch.randn(K, N, device=DEV)).to(torch.bfloat16)
+        o13 = _ext.ops().dgrad_gemm(dy, w, None, 13)
+        o14 = _ext.ops().dgrad_gemm(dy, w, None, 14)
+    assert torch.equal(o13, o14)
