@@ -228,12 +228,15 @@ def run(a):
     loader = trainer.get_train_dataloader()
     it = iter(loader)
 
-    from llm_fine_tune_distributed_amd.utils.faults import maybe_inject
+    from llm_fine_tune_distributed_amd.utils.faults import maybe_inject, nan_injection
     n_step = [0]
 
     def step():
         n_step[0] += 1
         maybe_inject(st.rank, n_step[0])  # SFTAMD_FAULT_INJECT=rank:step (launcher teardown test)
+        if nan_injection(st.rank, n_step[0]):  # SFTAMD_FAULT_INJECT=rank:step:nan (the non-finite-loss exit test)
+            with torch.no_grad():
+                trainer.engine.param_flat.view(-1)[0] = float("nan")
         return trainer.optimizer_step([next(it) for _ in range(a.ga)], lr=args.learning_rate)
 
     beat(0, "warmup")
@@ -288,7 +291,7 @@ def run(a):
     if st.world_size > 1 and rccl_dir is not None:
         from llm_fine_tune_distributed_amd.parallel import rccl_info
         dist_warn, fatal = rccl_info.dist_warnings([r_.get("rccl") for r_ in ranks], st.world_size)
-    if st.world_size > 1 and len({r_["param_sum"] for r_ in ranks}) != 1:
+    if st.world_size > 1 and len({_sum_key(r_["param_sum"]) for r_ in ranks}) != 1:
         dist_warn.append("parameters differ across ranks after the timed steps")
         fatal = True
     strict = st.world_size > 1 and not a.no_strict_dist
@@ -331,7 +334,7 @@ def run(a):
                      "rccl_saw_all_ranks": (all((r_.get("rccl") or {}).get("nranks") == st.world_size for r_ in ranks)
                                             if rccl_dir is not None else None),
                      "link_probe": [[int(b), round(t * 1e3, 4)] for b, t in getattr(trainer, "link_points", [])],
-                     "params_equal_across_ranks": len({r_["param_sum"] for r_ in ranks}) == 1,
+                     "params_equal_across_ranks": len({_sum_key(r_["param_sum"]) for r_ in ranks}) == 1,
                      "warnings": dist_warn, "strict": strict},
             "optimizer_sharding": "zero1" if shard else "none",
             "bucket_plan": bucket_plan(trainer.engine),
@@ -374,6 +377,10 @@ def run(a):
         # the record above is printed (with dist.warnings) but the run fails loud: a scaling number measured over a
         # degraded transport must not pass as a healthy one
         sys.exit(3)
+    if not math.isfinite(loss):
+        # every rank holds the all-reduced loss: all exit non-zero, so a NaN run's throughput can never become a
+        # BENCH / SCALE value (the record above carries loss_finite: false for the post-mortem)
+        sys.exit(4)
 
 
 def run_recipe(a):
@@ -444,6 +451,11 @@ def run_recipe(a):
         }
         print(json.dumps(rec), flush=True)
     cleanup_distributed()
+
+
+def _sum_key(x: float):
+    """param_sum as a set key: every NaN the same (a NaN run is caught by the loss check, not as a rank mismatch)."""
+    return "nan" if math.isnan(x) else x
 
 
 def main(argv=None):

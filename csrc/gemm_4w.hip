@@ -776,12 +776,16 @@ void g4_dgrad(const at::Tensor& dy, const at::Tensor& w, u16* out, long ldo, con
   using R0 = std::integral_constant<int, 0>;
   using R1 = std::integral_constant<int, 1>;
   using R2 = std::integral_constant<int, 4>;  // interleaved reads and DMA
+  using R3 = std::integral_constant<int, 2>;  // interleaved reads only
+  using R4 = std::integral_constant<int, 3>;  // interleaved DMA only
   if (gu != nullptr) {
     if (ring == 2) go(SW(), R2());
     else if (ring == 1) go(SW(), R1());
     else go(SW(), R0());
   } else {
     if (ring == 2) go(ST(), R2());
+    else if (ring == 3) go(ST(), R3());
+    else if (ring == 4) go(ST(), R4());
     else if (ring == 1) go(ST(), R1());
     else go(ST(), R0());
   }

@@ -543,7 +543,7 @@ at::Tensor dgrad_gemm(const at::Tensor& dy, const at::Tensor& w, const c10::opti
   const int64_t M = dy.size(0), K = dy.size(1), N = w.size(1);
   SFT_CHECK(w.size(0) == K, "dgrad_gemm: dy [M, K] . w [K, N]");
   SFT_CHECK(cfg != 7 || K % 64 == 0, "dgrad_gemm cfg 7 (BK 64): K multiple of 64");
-  SFT_CHECK((cfg < 12 || cfg > 14) || K % 128 == 0, "dgrad_gemm cfg 12 / 13 / 14 (4-wave): K multiple of 128");
+  SFT_CHECK((cfg < 12 || cfg > 16) || K % 128 == 0, "dgrad_gemm cfg 12-16 (4-wave): K multiple of 128");
   SFT_CHECK(M % 128 == 0 && N % 256 == 0 && K % 32 == 0 && K >= 32, "dgrad_gemm: M multiple of 128 (256 for cfg 0/1), N of 256, K of 32");
   SFT_CHECK(cfg == 2 || cfg == 3 || cfg == 8 || M % 256 == 0, "dgrad_gemm: 256 x 256 tiles need M % 256 == 0");
   SFT_CHECK(dy.stride(0) % 8 == 0 && w.stride(0) % 8 == 0 && (uintptr_t)dy.data_ptr() % 16 == 0 &&
@@ -590,7 +590,9 @@ at::Tensor dgrad_gemm(const at::Tensor& dy, const at::Tensor& w, const c10::opti
       case 8: dgrad::launch<256, 128, 2, 2, 3, E, 2>(dy, wv, e); break;
       case 12:  // 4-wave (csrc/gemm_4w.hip); 13: its 4-slot ring; 14: the ring with interleaved issue
       case 13:
-      case 14: g4_dgrad(dy, wv, e.out, e.ldo, E == dgrad::EPI_SWIGLU_BWD ? e.gu : nullptr, e.N, c - 12); break;
+      case 14:
+      case 15:
+      case 16: g4_dgrad(dy, wv, e.out, e.ldo, E == dgrad::EPI_SWIGLU_BWD ? e.gu : nullptr, e.N, c - 12); break;
       default: dgrad::launch<256, 256, 2, 4, 4, E>(dy, wv, e);
     }
   };

@@ -110,6 +110,10 @@ def _wide_ld(lora, key: str, weight) -> int:
     wide = getattr(fl, "wide", None)
     if wide is None or not any(fl.active) or weight.data_ptr() != wide.data_ptr():
         return 0
+    # only where the consumer's in-place widening kernel takes the shape (else the norm writes a plain y and the
+    # consumer copies it into X')
+    if not ops.lora_inplace_ok(fl.in_features, fl.r * sum(1 for a in fl.active if a)):
+        return 0
     return wide.shape[1]
 
 

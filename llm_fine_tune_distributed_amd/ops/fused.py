@@ -70,6 +70,10 @@ def _wgrad_cfg(T: int, N: int, K: int) -> int:
         # past the whole round split 2 ways over the tokens (1213): 0.301 vs 0.341 (cfg 13) vs 0.349 (cfg 9);
         # lm_head / tied embedding (4008 tiles) stays on cfg 10: 3.195 vs 3.213 ms (profiles/r3_bwd_gemm_4wave.md)
         return 1200 + _G4_RING if tiles < 512 and (T // 128) >= 2 else _G4_RING
+    if N % 256 == 0 and K % 256 == 0 and T % 128 == 0 and tiles >= 2048 and (T // 128) >= 2:
+        # lm_head / tied embedding (4008 tiles = 15.7 rounds): the 4-wave ring, its last partial round split 2 ways:
+        # 2.969 ms vs 3.237 for the 8-wave ring (cfg 10) and 3.023 unsplit (interleaved, profiles/r6_gemm_routing.md)
+        return 1200 + _G4_RING
     if N % 256 == 0 and K % 256 == 0 and tiles >= 512:
         return 10
     if (N % 256 == 0 and K % 256 == 0 and 64 < (N // 256) * (K // 256) <= 128 and (T // 32) % 2 == 0
@@ -254,7 +258,9 @@ def _dgrad_cfg(dy2d: torch.Tensor, swiglu: bool = False) -> int:
     backward epilogue stays on cfg 7 (its LDS-staged epilogue: 0.436 vs 0.58 ms for the register epilogue)."""
     K = dy2d.shape[1]
     if not swiglu and K % 128 == 0:
-        return _G4_RING if K > 4096 else 12
+        # the 4-slot ring with interleaved issue on every reduction length now (o 0.0577 vs 0.0604 ms for the pair
+        # loop cfg 12, qkv 0.0786 vs 0.0800; profiles/r6_gemm_routing.md)
+        return _G4_RING
     return 7 if K % 64 == 0 else 5
 
 
@@ -432,8 +438,13 @@ class AddRMSNormFn(Function):
 
 
 def add_rms_norm(x, residual, weight, eps, y_ld: int = 0) -> Tuple[torch.Tensor, torch.Tensor]:
-    """(y, res_out); y_ld: see AddRMSNormFn (ignored off the HIP path)."""
-    return AddRMSNormFn.apply(x, residual, weight, eps, y_ld)
+    """(y, res_out); y_ld: see AddRMSNormFn (ignored off the HIP path). A widened y is marked with its row width
+    (``_sftamd_wide_ld``): the LoRA consumer fills the rest of the row in place ONLY for a buffer marked this way,
+    never for an arbitrary view whose row stride happens to match."""
+    y, res = AddRMSNormFn.apply(x, residual, weight, eps, y_ld)
+    if y_ld > x.shape[-1] and _ext.use_hip(x) and y.stride(-2) == y_ld:
+        y._sftamd_wide_ld = int(y_ld)
+    return y, res
 
 
 def rms_norm(x, weight, eps) -> torch.Tensor:
@@ -922,8 +933,14 @@ def dropout_add(a: Optional[torch.Tensor], b: torch.Tensor, p: float, seed: int)
     return ref.dropout_add(a, b, p, seed)
 
 
+def lora_inplace_ok(K: int, R: int) -> bool:
+    """Shapes csrc/lora.hip's widening kernels (lora_fwd / lora_fwd_inplace) take: K % 256, R = r x active
+    sub-projections a multiple of 16 in [16, 64]."""
+    return K % 256 == 0 and R % 16 == 0 and 16 <= R <= 64
+
+
 def _lora_hip(x2d, acat) -> bool:
-    return _ext.use_hip(x2d) and x2d.shape[1] % 256 == 0 and acat.shape[0] % 16 == 0 and acat.shape[0] <= 64
+    return _ext.use_hip(x2d) and lora_inplace_ok(x2d.shape[1], acat.shape[0])
 
 
 def _lora_fwd(x2d, acat, s, p, seed, ldX=0, swiglu=False):
@@ -1154,7 +1171,7 @@ def _lora_wide_prep(x, wide, K, scaling, p, seed, meta, ab, swiglu=False):
     else:
         _sync_wide(wide, K, r, meta, Bs)
         acat = As[0].contiguous() if n == 1 else torch.cat(As, 0)
-    X = _prewidened(x2d, wide.shape[1]) if not swiglu else None
+    X = _prewidened(x, x2d, wide.shape[1], acat) if not swiglu else None
     if X is not None:  # x was written into X's left block by its producer (add_rms_norm y_ld): fill the rest in place
         _ext.ops().lora_fwd_inplace(X, K, acat, float(scaling), float(p), int(seed))
     else:
@@ -1162,11 +1179,12 @@ def _lora_wide_prep(x, wide, K, scaling, p, seed, meta, ab, swiglu=False):
     return X, acat, (K, r * n, r, n, float(scaling), float(p), int(seed), tuple(meta), x.shape)
 
 
-def _prewidened(x2d: torch.Tensor, ldX: int) -> Optional[torch.Tensor]:
-    """X [T, ldX] when x2d [T, K] is the left block of a row-contiguous [T, ldX] buffer (row stride ldX, the rest of
-    each row inside the same storage), on the HIP path; else None."""
+def _prewidened(x: torch.Tensor, x2d: torch.Tensor, ldX: int, acat: torch.Tensor) -> Optional[torch.Tensor]:
+    """X [T, ldX] when x is a norm output add_rms_norm wrote as the left block of its own [T, ldX] buffer (marked
+    ``_sftamd_wide_ld``) and the in-place widening kernel takes the shape; else None (the copying path)."""
     T, K = x2d.shape
-    if (T == 0 or K >= ldX or x2d.stride(1) != 1 or x2d.stride(0) != ldX or not _ext.use_hip(x2d)
+    if (getattr(x, "_sftamd_wide_ld", 0) != ldX or not _lora_hip(x2d, acat)
+            or T == 0 or K >= ldX or x2d.stride(1) != 1 or x2d.stride(0) != ldX
             or x2d.dtype != torch.bfloat16 or x2d.data_ptr() % 16 != 0):
         return None
     st = x2d.untyped_storage()

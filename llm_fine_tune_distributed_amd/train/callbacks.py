@@ -30,6 +30,7 @@ class TrainerState:
     train_batch_size: int = 0
     samples_seen: int = 0
     tokens_seen: int = 0
+    nonfinite_loss_steps: List[int] = field(default_factory=list)  # logged steps whose loss was NaN / inf
 
     def to_json(self, path: str):
         with open(path, "w") as f:

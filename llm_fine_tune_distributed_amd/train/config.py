@@ -135,6 +135,9 @@ class SFTConfig:
     # (utilisation / power / temperature / HBM via amdsmi or rocm-smi) every N log steps into the trackers
     log_step_phases: bool = False
     log_system_metrics_every: int = 0
+    # a non-finite logged loss (read at the logging cadence only: no extra host sync) is reported on stderr and in the
+    # heartbeat (phase "nonfinite_loss"); True also stops training at that step
+    stop_on_nonfinite_loss: bool = False
 
     def __post_init__(self):
         pass

@@ -584,6 +584,14 @@ class SFTTrainer:
                         from ..utils.telemetry import system_log_entries
                         logs.update(system_log_entries())
                     self.log(logs)
+                    if not math.isfinite(logs["loss"]):
+                        # (the loss was read for the log anyway: the check adds no host sync)
+                        self.state.nonfinite_loss_steps.append(gs)
+                        self.heartbeat.beat(gs, "nonfinite_loss", loss=str(logs["loss"]))
+                        if self.dist.is_main:
+                            print(f"[trainer] WARNING: non-finite loss {logs['loss']} at step {gs}", flush=True)
+                        if a.stop_on_nonfinite_loss:
+                            self.control.should_training_stop = True
                     run_acc.zero_()
                     steps_since_log = 0
                 if a.ddp_check_sync_every and gs % a.ddp_check_sync_every == 0:

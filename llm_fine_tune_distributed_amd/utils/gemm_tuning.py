@@ -44,14 +44,16 @@ _TUNED = [frozenset()]
 
 
 def _tuned_tn(path: str) -> frozenset:
-    """(N, M, K) of every contiguous TN GEMM (y[M, N] = x[M, K] W[N, K]^T, torch's column-major naming
-    ``tn_N_M_K_ld_K_K_N``) with a selection in the TunableOp file."""
+    """(N, M, K) of every contiguous bf16 TN GEMM (y[M, N] = x[M, K] W[N, K]^T, torch's column-major naming
+    ``tn_N_M_K_ld_K_K_N``) with a selection in the TunableOp file. Only ``GemmTunableOp_BFloat16_TN`` rows count: an
+    fp16 / fp32 selection of the same shape says nothing about the bf16 projection. The set is read once, at
+    enable_tuned_gemms: shapes tuned in-process (tune=True) route to hipBLASLt from the next start on."""
     out = set()
     try:
         with open(path) as f:
             for line in f:
                 parts = line.split(",")
-                if len(parts) < 2 or not parts[1].startswith("tn_"):
+                if len(parts) < 2 or parts[0] != "GemmTunableOp_BFloat16_TN" or not parts[1].startswith("tn_"):
                     continue
                 f_ = parts[1].split("_")  # tn, N, M, K, ld, lda, ldb, ldc
                 try:

@@ -68,6 +68,17 @@ def test_bench_replicated_ddp_path():
     assert _json_lines(r.stdout)[0]["optimizer_sharding"] == "none"
 
 
+@pytest.mark.parametrize("n", [1, 2])
+def test_bench_nonfinite_loss_fails_the_run(n):
+    """A NaN parameter (injected before step 2) makes the loss non-finite: the record is still printed for the
+    post-mortem (loss_finite false) but the run exits non-zero, so its throughput can never pass as a measurement."""
+    r = _bench(n, env_extra={"SFTAMD_FAULT_INJECT": "0:2:nan"}, timeout=300)
+    assert r.returncode == 4, (r.returncode, r.stderr[-2000:])
+    recs = _json_lines(r.stdout)
+    assert len(recs) == 1 and recs[0]["loss_finite"] is False
+    assert "throughput is void" in r.stderr
+
+
 def test_bench_failing_rank_tears_down_the_group():
     r = _bench(2, env_extra={"SFTAMD_FAULT_INJECT": "1:2:23"}, timeout=200)
     assert r.returncode == 23, (r.returncode, r.stderr[-2000:])

@@ -182,23 +182,27 @@ def test_lora_wide_gpu_matches_unfused():
             assert rel < 5e-2, (n, rel.item())
 
 
-def test_lora_norm_writes_widened_activation_in_place():
+@pytest.mark.parametrize("r", [16, 8, 32])
+def test_lora_norm_writes_widened_activation_in_place(r):
     """The RMSNorm forward writes its output into the left block of the consumer's widened activation X' (qkv /
     gate_up: add_rms_norm y_ld) and lora_fwd_inplace fills only the adapter columns: bitwise the same loss and
-    gradients as the copying widening (the norm output as its own tensor, X' written by lora_fwd)."""
+    gradients as the copying widening (the norm output as its own tensor, X' written by lora_fwd). r = 8 / 32 (qkv
+    R = 24 / 96, outside the widening kernel's 16..64 multiples of 16): the norm writes a plain y and the copying path
+    runs (no 'lora_fwd_inplace: shapes' error)."""
     from llm_fine_tune_distributed_amd.models.lora import LoRAConfig, apply_lora
     import llm_fine_tune_distributed_amd.models.transformer as T
     cfg = tiny(hidden_size=512, num_attention_heads=4, num_key_value_heads=2, head_dim=128, intermediate_size=1024,
                vocab_size=1024, num_hidden_layers=2)
     m = build_model(cfg, device="cuda", dtype=torch.bfloat16, seed=1)
-    apply_lora(m, LoRAConfig(r=16, lora_alpha=8, lora_dropout=0.1))
+    apply_lora(m, LoRAConfig(r=r, lora_alpha=8, lora_dropout=0.1))
     for l in m.model.layers:
         for fl in (l.self_attn.lora["qkv"], l.mlp.lora["gate_up"]):
             for bb in fl.B:
                 torch.nn.init.normal_(bb, std=0.05)
     m.train()
     ids = torch.randint(0, 1024, (4, 128), device="cuda")
-    assert T._wide_ld(m.model.layers[0].self_attn.lora, "qkv", m.model.layers[0].self_attn.qkv_proj) == 640
+    ld = T._wide_ld(m.model.layers[0].self_attn.lora, "qkv", m.model.layers[0].self_attn.qkv_proj)
+    assert ld == (640 if r == 16 else 0), ld
 
     def run():
         for p in m.parameters():

@@ -265,3 +265,24 @@ def test_padding_free_matches_padded_batches(tmp_path, tk):
     assert len(e0) == len(e1) == 1
     for k in ("eval_loss", "eval_mean_token_accuracy", "eval_num_tokens"):
         assert abs(e0[0][k] - e1[0][k]) <= 1e-5 * max(1.0, abs(e0[0][k])), k
+
+
+@pytest.mark.parametrize("stop", [False, True])
+def test_nonfinite_loss_is_reported_at_the_log_cadence(tmp_path, tk, stop):
+    """A NaN parameter makes the logged loss non-finite: the trainer records the step (state.nonfinite_loss_steps),
+    beats phase "nonfinite_loss" and, with stop_on_nonfinite_loss, stops at that step."""
+    rows = generate_qa(16, seed=0)
+    args = SFTConfig(output_dir=str(tmp_path / "o"), per_device_train_batch_size=2, gradient_accumulation_steps=1,
+                     max_steps=4, logging_steps=1, save_strategy="no", eval_strategy="no", jsonl_log=False,
+                     dataset_cache=False, stop_on_nonfinite_loss=stop)
+    m = _model()
+    t = SFTTrainer(model=m, args=args, train_dataset=rows, processing_class=tk)
+    with torch.no_grad():
+        t.engine.param_flat.view(-1)[0] = float("nan")
+    seen = []
+    orig = t.heartbeat.beat
+    t.heartbeat.beat = lambda step=None, phase="", **kw: (seen.append(phase), orig(step, phase, **kw))
+    out = t.train()
+    assert t.state.nonfinite_loss_steps[:1] == [1]
+    assert "nonfinite_loss" in seen
+    assert out.global_step == (1 if stop else 4)
