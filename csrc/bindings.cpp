@@ -83,9 +83,9 @@ TORCH_LIBRARY(sftamd, m) {
   // fused decode sampler: penalty -> temperature -> top-k -> top-p -> draw, device-resident state
   m.def("sample_token(Tensor logits, Tensor(a!) presence, Tensor(b!) state, Tensor(c!)? tok_out, Tensor(d!)? pos_out, Tensor(e!)? len_out, Tensor(f!)? log, float temperature, int top_k, float top_p, float repetition_penalty, bool do_sample, int seed) -> ()");
   // weight-gradient GEMM: out[N,K] (+)= dy[T,N]^T x[T,K]
-  m.def("wgrad_gemm(Tensor(a!) out, Tensor dy, Tensor x, bool accumulate, int cfg=0, Tensor(b!)? norm=None, int tail_stream=0) -> ()");
+  m.def("wgrad_gemm(Tensor(a!) out, Tensor dy, Tensor x, bool accumulate, int cfg=14, Tensor(b!)? norm=None) -> ()");
   // input-gradient GEMM dX = dy w (w [K, N]), optional fused SwiGLU backward (csrc/gemm_dgrad.hip)
-  m.def("dgrad_gemm(Tensor dy, Tensor w, Tensor? gate_up=None, int cfg=0) -> Tensor");
+  m.def("dgrad_gemm(Tensor dy, Tensor w, Tensor? gate_up=None, int cfg=14) -> Tensor");
   // forward-layout GEMM C = a w^T with fused epilogues (csrc/gemm_tn.hip)
   m.def("gemm_tn(Tensor a, Tensor w, int cfg=0) -> Tensor");
   m.def("gemm_tn_swiglu(Tensor x, Tensor w_gate_up, int cfg=5) -> (Tensor, Tensor)");

@@ -8,65 +8,56 @@
 // C[m][n] = sum_k A'[m][k] B'[n][k]. One workgroup = 4 waves = one wave per SIMD, each wave a 128 x 128 output
 // tile whose 256 fp32 accumulators are pinned in the AGPR file: the MFMAs are inline asm with the accumulator TIED
 // ("+a"), which is what lets hipcc keep 256 accumulators next to double-buffered fragments without renaming them
-// through v_accvgpr_read / write or spilling (the forward kernel's experience, csrc/gemm_tn.hip cfg 12 and
-// profiles/r3_gemm_4wave.md). Why 4 waves: a 128 x 128 wave tile reads 16 fragments per 64 MFMAs instead of the 12
-// per 32 of the 8-wave 128 x 64 tiles of gemm_wgrad.hip / gemm_dgrad.hip — a third fewer LDS bytes per FLOP — and
-// one wave per SIMD leaves the matrix pipe to a single in-order instruction stream (/opt/skills/guides/MI355X_MICROARCH.md "Two waves
-// per SIMD", item 1). The 8-wave weight-gradient rings ran at 48-56 % MFMA busy inside the training step
+// through v_accvgpr_read / write or spilling (profiles/r3_gemm_4wave.md). Why 4 waves: a 128 x 128 wave tile reads 16
+// fragments per 64 MFMAs instead of the 12 per 32 of 128 x 64 tiles — a third fewer LDS bytes per FLOP — and one
+// wave per SIMD leaves the matrix pipe to a single in-order instruction stream (/opt/skills/guides/MI355X_MICROARCH.md
+// "Two waves per SIMD", item 1). The 8-wave weight-gradient rings ran at 48-56 % MFMA busy inside the training step
 // (profiles/r2_step_pmc.md).
 //
-// Operand staging (global_load_lds, 16 B per lane, 1 KB per wave instruction; the chunk swizzle is applied to the
-// GLOBAL source address because the DMA writes LDS lane-linearly):
-//   ROW operand: image [256 rows][64 k], 128-B rows, chunk c of row r at slot c ^ ((r >> 1) & 7); a fragment is one
-//                ds_read_b128 per lane (lane group g: k 8g .. 8g + 7 of the 32-deep sub-step);
-//   TR operand:  two images [64 k][128 columns], 256-B rows, chunk c of row r at slot c ^ 2 ((r & 3) | ((r >> 3) & 1)
-//                << 2); a fragment is two ds_read_b64_tr_b16 per lane (rows 8g .. 8g + 3 and 8g + 4 .. 8g + 7 of the
-//                sub-step, i.e. the same k 8g .. 8g + 7 as the ROW side). Lane groups {0, 1} / {2, 3} of a 32-lane
-//                half read 8 rows whose 32-byte column pairs the swizzle spreads over all 64 banks: conflict-free.
+// Main loop: 32-deep K-steps in NS = 4 LDS slots of 32 KB (128 KB), three steps in flight ahead of the one being
+// computed. Per step u (slot u % 4):
+//   vmcnt: this wave's pieces of step u + 1 landed (F(u) was read during step u - 1: the compiler's counted LDS waits)
+//   MFMA group 0 | lgkmcnt(0), barrier (every wave's step u + 1 landed, every wave done reading slot u % 4)
+//   MFMA on F(u) | ds_read F(u + 1) from slot (u + 1) % 4 | LDS-DMA of step u + 4 -> slot u % 4
+// with the 16 fragment reads and 8 DMA pieces placed ONE PER MFMA GAP (op k after MFMA 8 + 7k/3, order B0 B1 D0 B2
+// B3 D1 .. A6 A7 D7): one wave per SIMD issues in order, and a burst that outlasts the 16-cycle gap of
+// v_mfma_f32_16x16x32_bf16 idles the matrix pipe (hipBLASLt's MT256x256x64 loop places one ds_read / buffer_load
+// between consecutive MFMAs: profiles/r6_g4_interleave.md, +1.3 % in the step over 2 reads + 1 piece per 8 MFMAs).
+// B fragments first: the next step's group 0 needs all 8 B and A0. The reduction length must be a multiple of 128 (one
+// loop body = 4 steps on compile-time slot pointers).
+//
+// Operand staging (LDS-DMA through a buffer descriptor, 16 B per lane, 1 KB per wave instruction; the chunk swizzle is
+// applied to the GLOBAL source address because the DMA writes LDS lane-linearly):
+//   ROW operand: image [256 rows][32 k], 64-B rows, chunk c at slot c ^ S((row >> 2) & 3), S = {0, 2, 3, 1}: the
+//                16-lane groups of ds_read_b128 conflict-free; a fragment is one ds_read_b128 per lane;
+//   TR operand:  two images [32 k][128 columns], 256-B rows, chunk c of row r at slot c ^ 2 ((r & 3) | ((r >> 3) & 1)
+//                << 2); a fragment is two ds_read_b64_tr_b16 per lane (rows 8g .. 8g + 3 and 8g + 4 .. 8g + 7), i.e.
+//                the same k 8g .. 8g + 7 as the ROW side. Lane groups {0, 1} / {2, 3} of a 32-lane half read 8 rows
+//                whose 32-byte column pairs the swizzle spreads over all 64 banks: conflict-free.
 // MFMA v_mfma_f32_16x16x32_bf16 with the B fragment first (transposed C): each lane ends with 4 consecutive output
 // columns of one row per fragment, and v_permlane16_swap pairs two fragments into 8 consecutive columns, so the
 // epilogue writes 16-byte vectors straight from registers (no LDS round trip).
 //
-// Schedule per 64-deep K-tile t (stage X holds t, Y holds t + 1, 64 KB each, 128 KB in all):
-//   sub-step 0: 64 MFMA on F0 = (t, k 0..31) from registers | ds_read F1 = (t, k 32..63) from X
-//   vmcnt(0): this wave's DMA of tile t + 1 landed
-//   sub-step 1: group 0's MFMAs; lgkmcnt(0) (this wave's reads of X retired); barrier (every wave's DMA of t + 1
-//               landed, every wave done with X); then
-//               MFMA on F1 | ds_read F0 = (t + 1, k 0..31) from Y | global_load_lds tile t + 2 -> X
-// The reduction length must be a multiple of 128 (an even number of K-tiles; the pair loop alternates X / Y with
-// compile-time stage pointers).
-// Read order: a sub-step reads the next one's B fragments in MFMA groups 0..3 and its A fragments in groups 4..7, so
-// the next sub-step's group 0 (all 8 B fragments, A row 0) never waits on a read issued by the group just before it;
-// no LDS wait at the sub-step start (the compiler's counted waits cover each fragment), lgkmcnt(0) only ahead of the
-// barrier that releases a stage to the DMA. vs reading A row i / B column i in group i with lgkmcnt(0) at the start:
-// 109.78 / 109.51 vs 109.56 / 109.28 samples/s in the step (interleaved, bitwise-identical results, r5_run32).
-//
-// Wave quantisation (weight gradients: gate_up 688 tiles = 2.69 rounds of 256 CUs, down_proj 344 = 1.34): the tiles
-// past the last whole round can be split S ways over the reduction (hybrid data-parallel + split-K, pairs of
-// K-tiles per split) into fp32 slabs summed in a fixed order by splitk_fixup_kernel (deterministic).
+// Wave quantisation (weight gradients: down_proj 344 tiles = 1.34 rounds of 256 CUs, lm_head 4008 = 15.7): the tiles
+// past the last whole round can be split S ways over the reduction (hybrid data-parallel + split-K, 128-deep blocks
+// per split) into fp32 slabs summed in a fixed order by splitk_fixup_kernel (deterministic); small grids (qkv 96
+// tiles, o_proj 64) split every tile. A stream-K partition of the last round (ranges crossing tile boundaries) was
+// measured and dropped: no faster on any SmolLM3 shape (profiles/r6_gemm_routing.md).
 #include "common.h"
 #include "splitk_fixup.h"
-
-#include <type_traits>
 
 namespace sftamd {
 namespace g4 {
 
-constexpr int BK = 64;
-constexpr int OPB = 256 * BK * 2;  // one operand's K-tile: 32 KB
-constexpr int STAGE = 2 * OPB;     // 64 KB
-constexpr int ROWB_T = 256;        // TR image row: 128 columns x bf16
-constexpr int IMG_T = BK * ROWB_T;  // 16 KB
+constexpr int BK32 = 32;
+constexpr int OPB32 = 256 * BK32 * 2;  // one operand's 32-deep K-step: 16 KB
+constexpr int SLOT32 = 2 * OPB32;      // 32 KB
+constexpr int ROWB_T = 256;            // TR image row: 128 columns x bf16
+constexpr int IMG32 = BK32 * ROWB_T;   // 8 KB
 enum { ROW = 0, TR = 1 };
-enum { EPI_STORE = 0, EPI_SWIGLU_BWD = 1 };
 
-__device__ __forceinline__ int xr(int row) { return (row >> 1) & 7; }
 __device__ __forceinline__ int xt(int row) { return 2 * ((row & 3) | (((row >> 3) & 1) << 2)); }
-
-__device__ __forceinline__ void glds16(const u16* src, char* dst) {  // (unused: kept for the LDS-DMA debug variants)
-  __builtin_amdgcn_global_load_lds((const void __attribute__((address_space(1)))*)src,
-                                   (void __attribute__((address_space(3)))*)dst, 16, 0, 0);
-}
+__device__ __forceinline__ int sel4(int q) { return (0x78 >> (2 * q)) & 3; }
 
 // LDS-DMA through a buffer descriptor: the tile's base in the (wave-uniform) descriptor, each lane's byte offset in a
 // VGPR fixed for the whole loop, the piece / K-step offset in an SGPR — no per-piece 64-bit VALU address arithmetic
@@ -92,318 +83,8 @@ __device__ __forceinline__ void mfma(f32x4& c, const bf16x8& b, const bf16x8& a)
   asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+a"(c) : "v"(b), "v"(a));
 }
 
-// One operand: the lane's DMA source for the wave's first piece, and its fragment read offsets.
+// One operand: the lane's DMA source for the wave's first piece of a step, and its fragment read offsets.
 // `sub` = which 128-wide half of the 256 tile the wave computes on this side (wm for A, wn for B).
-template <int L>
-struct Op;
-
-template <>
-struct Op<ROW> {
-  rsrc_t r;
-  unsigned voff, jst, koff;  // lane offset; bytes between the wave's pieces j, j + 1 (32 rows); K progress
-  int off0, off1;  // fragment 0 of sub-steps 0 / 1 (fragment i is 2048 B further)
-  __device__ __forceinline__ void init(const u16* base, long ld, int r0, long k0, int w, int lane, int sub) {
-    // piece P = w + 4 j (8 rows, 8P + lr); (row >> 1) & 7 = 4 (w & 1) + (lr >> 1) for every piece of the wave
-    const int lr = lane >> 3, ch = (lane & 7) ^ (4 * (w & 1) + (lr >> 1));
-    r = tile_rsrc(base + (long)r0 * ld + k0);
-    voff = (unsigned)(((8 * w + lr) * ld + 8 * ch) * 2);
-    jst = (unsigned)(64 * ld);
-    koff = 0;
-    const int g = lane >> 4, ii = lane & 15;
-    const int r = 128 * sub + ii;
-    off0 = r * 128 + 16 * (g ^ xr(r));
-    off1 = r * 128 + 16 * ((4 + g) ^ xr(r));
-  }
-  __device__ __forceinline__ void advance() { koff += 2 * BK; }
-  __device__ __forceinline__ void piece(char* opb, int w, int j) const {
-    bldsx4(r, opb + (w + 4 * j) * 1024, voff, koff + j * jst);
-  }
-  __device__ __forceinline__ bf16x8 frag(const char* opb, int s, int i) const {
-    return *(const bf16x8*)(opb + (s ? off1 : off0) + 2048 * i);
-  }
-};
-
-template <>
-struct Op<TR> {
-  rsrc_t r;
-  unsigned voff, jst, kst, koff;  // lane offset; bytes per 16 rows; per K-tile (64 rows); K progress
-  int ob, x2;  // fragment i of sub-step s at ob + 32 (i ^ x2) + s * 32 rows
-  __device__ __forceinline__ void init(const u16* base, long ld, int c0, long k0, int w, int lane, int sub) {
-    // piece (image j >> 2, q = w + 4 (j & 3)): rows 4q + lr4; xt(row) = 2 (lr4 | ((w >> 1) & 1) << 2) for all
-    const int lr4 = lane >> 4, row = 4 * w + lr4, ch = (lane & 15) ^ xt(row);
-    r = tile_rsrc(base + k0 * ld + c0);
-    voff = (unsigned)((row * ld + 8 * ch) * 2);
-    jst = (unsigned)(32 * ld);
-    kst = (unsigned)(2 * BK * ld);
-    koff = 0;
-    const int g = lane >> 4, ii = lane & 15, qq = ii >> 2, pp = ii & 3;
-    x2 = qq | ((g & 1) << 2);  // xt(8g + qq) / 2
-    ob = sub * IMG_T + (8 * g + qq) * ROWB_T + 8 * pp;
-  }
-  __device__ __forceinline__ void advance() { koff += kst; }
-  __device__ __forceinline__ void piece(char* opb, int w, int j) const {
-    bldsx4(r, opb + (j >> 2) * IMG_T + (w + 4 * (j & 3)) * 1024, voff, koff + (j & 3) * jst + 256 * (j >> 2));
-  }
-  __device__ __forceinline__ bf16x8 frag(const char* opb, int s, int i) const {
-    const char* q = opb + ob + 32 * (i ^ x2) + s * 32 * ROWB_T;
-    s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4*)q);
-    s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4*)(q + 4 * ROWB_T));
-    s16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-    return __builtin_bit_cast(bf16x8, v);
-  }
-};
-
-struct Epi {
-  u16* C;          // output rows (STORE: [M, ldc]; SWIGLU_BWD: dgu [M, ldc = 2 I] with the up half I columns right)
-  const u16* gu;   // SWIGLU_BWD: gate | up, same row stride as C
-  float* P;        // split slabs (+ parked whole-tile norm partials) or the norm slots (no split)
-  long ldc;
-  int I;           // SWIGLU_BWD: column offset of the up half
-  int flags;       // bit 0: accumulate into C (beta = 1); bit 1: gradient-norm partials
-};
-
-// One sub-step: 8 MFMA groups (A fragment row i x the 8 B fragments); READ: the next sub-step's fragments from
-// `src` (sub-step index rs); NP DMA pieces of the next K-tile into `dst`, 2 per group; BAR: the K-tile barrier after
-// group 0's MFMAs (which only need registers), ahead of the group's reads and DMA.
-template <int LA, int LB, bool READ, int NP, bool BAR>
-__device__ __forceinline__ void sub(f32x4 (&acc)[8][8], const bf16x8 (&fa)[8], const bf16x8 (&fb)[8], bf16x8 (&ra)[8],
-                                    bf16x8 (&rb)[8], const char* __restrict__ src, int rs, Op<LA>& oa, Op<LB>& ob, char* __restrict__ dst, int w) {
-  static_assert(NP == 0 || NP == 16, "a whole K-tile per sub-step");
-#pragma unroll
-  for (int i = 0; i < 8; ++i) {
-#pragma unroll
-    for (int j = 0; j < 8; ++j) mfma(acc[i][j], fb[j], fa[i]);
-    if (BAR && i == 0) {  // this wave's reads of the stage the DMA below overwrites have retired
-      __builtin_amdgcn_s_waitcnt(waitcnt_imm(63, 0));
-      __builtin_amdgcn_s_barrier();
-    }
-    if (READ) {  // B fragments in groups 0..3, A in 4..7 (see the read-order note above)
-      if (i < 4) {
-        rb[2 * i] = ob.frag(src + OPB, rs, 2 * i);
-        rb[2 * i + 1] = ob.frag(src + OPB, rs, 2 * i + 1);
-      } else {
-        ra[2 * i - 8] = oa.frag(src, rs, 2 * i - 8);
-        ra[2 * i - 7] = oa.frag(src, rs, 2 * i - 7);
-      }
-    }
-    if (NP) {  // pieces 2i, 2i + 1: A pieces 0..7 in groups 0..3, B pieces in groups 4..7
-      const int q = 2 * i;
-      if (q < 8) {
-        oa.piece(dst, w, q);
-        oa.piece(dst, w, q + 1);
-      } else {
-        ob.piece(dst + OPB, w, q - 8);
-        ob.piece(dst + OPB, w, q - 7);
-      }
-    }
-  }
-}
-
-__device__ __forceinline__ float fbits(unsigned u) { return __uint_as_float(u); }
-
-// TRC accumulators -> 8 consecutive fp32 columns per (fragment row i, fragment pair p) per lane: lane (g, ii) holds
-// row 16 i + ii, columns 32 p + 16 (g & 1) + 8 (g >> 1) + 0..7 of the wave tile.
-__device__ __forceinline__ void gather8(const f32x4 (&acc)[8][8], int i, int p, float (&v)[8]) {
-#pragma unroll
-  for (int e = 0; e < 4; ++e) {
-    auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(acc[i][2 * p][e]), __float_as_uint(acc[i][2 * p + 1][e]),
-                                              false, false);
-    v[e] = fbits(r[0]);
-    v[4 + e] = fbits(r[1]);
-  }
-}
-
-template <int EPI>
-__device__ __forceinline__ void store_tile(const f32x4 (&acc)[8][8], const Epi& ea, int row0, int col0, int lane,
-                                           float* nrm) {
-  const int g = lane >> 4, ii = lane & 15;
-  const int cofs = col0 + 16 * (g & 1) + 8 * (g >> 1);
-  float ss = 0.f;
-  if (EPI == EPI_SWIGLU_BWD || (ea.flags & 1)) {
-    // the epilogue's loads (gate / up, or the accumulated C) stream through a PD-deep register ring over the 32
-    // (fragment row, column pair) units: unit u + PD is issued while unit u computes, instead of one exposed HBM
-    // round trip per unit (the fragment registers of the main loop are free here)
-    constexpr int U = 32, PD = 8, NL = EPI == EPI_SWIGLU_BWD ? 2 : 1;
-    const u16* src = EPI == EPI_SWIGLU_BWD ? ea.gu : ea.C;
-    auto at = [&](int u) -> long { return (long)(row0 + 16 * (u >> 2) + ii) * ea.ldc + cofs + 32 * (u & 3); };
-    uint4 rg[PD][NL];
-#pragma unroll
-    for (int u = 0; u < PD; ++u)
-#pragma unroll
-      for (int k = 0; k < NL; ++k) rg[u][k] = *(const uint4*)(src + at(u) + k * ea.I);
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      float v[8], a[8], b[8];
-      gather8(acc, u >> 2, u & 3, v);
-      unpack8(rg[u % PD][0], a);
-      if constexpr (NL == 2) unpack8(rg[u % PD][NL - 1], b);
-      if (u + PD < U) {
-#pragma unroll
-        for (int k = 0; k < NL; ++k) rg[u % PD][k] = *(const uint4*)(src + at(u + PD) + k * ea.I);
-      }
-      u16* out = ea.C + at(u);
-      if constexpr (EPI == EPI_STORE) {
-#pragma unroll
-        for (int e = 0; e < 8; ++e) v[e] += a[e];
-        if (nrm != nullptr) {
-#pragma unroll
-          for (int e = 0; e < 8; ++e) ss += v[e] * v[e];
-        }
-        *(uint4*)out = pack8(v);
-      } else {  // SWIGLU_BWD: v = dact (fp32, never stored), a = gate, b = up; no contraction (config-independent)
-        float dg[8], du[8];
-#pragma unroll
-        for (int e = 0; e < 8; ++e) {
-#pragma clang fp contract(off)
-          const float sg = 1.f / (1.f + __expf(-a[e]));
-          const float t = v[e] * sg;
-          du[e] = t * a[e];
-          dg[e] = (t * b[e]) * __builtin_fmaf(a[e], 1.f - sg, 1.f);
-        }
-        *(uint4*)out = pack8(dg);
-        *(uint4*)(out + ea.I) = pack8(du);
-      }
-    }
-  } else {
-#pragma unroll
-  for (int i = 0; i < 8; ++i) {
-    const long row = row0 + 16 * i + ii;
-#pragma unroll
-    for (int p = 0; p < 4; ++p) {
-      float v[8];
-      gather8(acc, i, p, v);
-      u16* out = ea.C + row * ea.ldc + cofs + 32 * p;
-      if constexpr (EPI == EPI_STORE) {
-        if (ea.flags & 1) {
-          float o[8];
-          unpack8(*(const uint4*)out, o);
-#pragma unroll
-          for (int e = 0; e < 8; ++e) v[e] += o[e];
-        }
-        if (nrm != nullptr) {
-#pragma unroll
-          for (int e = 0; e < 8; ++e) ss += v[e] * v[e];
-        }
-        *(uint4*)out = pack8(v);
-      } else {  // SWIGLU_BWD: v = dact (fp32, never stored)
-        const u16* gp = ea.gu + row * ea.ldc + cofs + 32 * p;
-        float gt[8], up[8], dg[8], du[8];
-        unpack8(*(const uint4*)gp, gt);
-        unpack8(*(const uint4*)(gp + ea.I), up);
-#pragma unroll
-        for (int e = 0; e < 8; ++e) {
-          const float s = 1.f / (1.f + __expf(-gt[e]));
-          du[e] = v[e] * gt[e] * s;
-          dg[e] = v[e] * up[e] * s * (1.f + gt[e] * (1.f - s));
-        }
-        *(uint4*)out = pack8(dg);
-        *(uint4*)(out + ea.I) = pack8(du);
-      }
-    }
-  }
-  }
-  if (nrm != nullptr) {  // 8 slots per tile (the 8-wave kernels' layout): waves 0..3 write theirs and zero w + 4, so
-    ss = wave_sum(ss);    // slots parked in an uninitialised split-K buffer (hybrid launches) are never garbage
-    if (lane == 0) {
-      nrm[0] = ss;
-      nrm[4] = 0.f;
-    }
-  }
-}
-
-// split piece: fp32 wave tile -> the piece's tile-local slab P[256][256]
-__device__ __forceinline__ void store_partial(const f32x4 (&acc)[8][8], float* __restrict__ P, int wm, int wn, int lane) {
-  const int g = lane >> 4, ii = lane & 15;
-  const int c = 128 * wn + 16 * (g & 1) + 8 * (g >> 1);
-#pragma unroll
-  for (int i = 0; i < 8; ++i) {
-    float* row = P + (long)(128 * wm + 16 * i + ii) * 256 + c;
-#pragma unroll
-    for (int p = 0; p < 4; ++p) {
-      float v[8];
-      gather8(acc, i, p, v);
-      *(float4*)(row + 32 * p) = make_float4(v[0], v[1], v[2], v[3]);
-      *(float4*)(row + 32 * p + 4) = make_float4(v[4], v[5], v[6], v[7]);
-    }
-  }
-}
-
-// One K-tile pair (t on X, t + 1 on Y); D: the DMA of tiles t + 2 (-> X) and t + 3 (-> Y) rides in the two
-// second sub-steps (not in the last pair).
-template <int LA, int LB, bool D>
-__device__ __forceinline__ void pair_step(char* __restrict__ X, char* __restrict__ Y, Op<LA>& oa, Op<LB>& ob, int w,
-                                          f32x4 (&acc)[8][8], bf16x8 (&a0)[8], bf16x8 (&b0)[8], bf16x8 (&a1)[8],
-                                          bf16x8 (&b1)[8]) {
-  constexpr int LG = 15;  // no LDS wait here: the compiler's counted waits cover the fragments
-  __builtin_amdgcn_s_waitcnt(waitcnt_imm(63, LG));
-  sub<LA, LB, true, 0, false>(acc, a0, b0, a1, b1, X, 1, oa, ob, X, w);
-  __builtin_amdgcn_s_waitcnt(waitcnt_imm(0, LG));
-  sub<LA, LB, true, D ? 16 : 0, true>(acc, a1, b1, a0, b0, Y, 0, oa, ob, X, w);
-  if (D) {
-    oa.advance();
-    ob.advance();
-  }
-  __builtin_amdgcn_s_waitcnt(waitcnt_imm(63, LG));
-  sub<LA, LB, true, 0, false>(acc, a0, b0, a1, b1, Y, 1, oa, ob, Y, w);
-  __builtin_amdgcn_s_waitcnt(waitcnt_imm(0, LG));
-  if constexpr (D) {
-    sub<LA, LB, true, 16, true>(acc, a1, b1, a0, b0, X, 0, oa, ob, Y, w);
-    oa.advance();
-    ob.advance();
-  } else {
-    sub<LA, LB, false, 0, false>(acc, a1, b1, a0, b0, X, 0, oa, ob, Y, w);
-  }
-}
-
-// The stage pointers are separate __restrict__ parameters: once inlined, every ds_read and every LDS-DMA write
-// carries the alias scope of its stage, so the compiler's waitcnt pass does not drain vmcnt before a fragment read of
-// the other stage (a lambda capturing the pointers lost that: a vmcnt(0) after every DMA group).
-template <int LA, int LB>
-__device__ __forceinline__ void mainloop(char* __restrict__ X, char* __restrict__ Y, int np, Op<LA>& oa, Op<LB>& ob,
-                                         int w, f32x4 (&acc)[8][8]) {
-  bf16x8 a0[8], b0[8], a1[8], b1[8];
-  // prologue: K-tiles 0 -> X, 1 -> Y; wait for X; F0 of tile 0
-#pragma unroll
-  for (int j = 0; j < 8; ++j) oa.piece(X, w, j);
-#pragma unroll
-  for (int j = 0; j < 8; ++j) ob.piece(X + OPB, w, j);
-  oa.advance();
-  ob.advance();
-#pragma unroll
-  for (int j = 0; j < 8; ++j) oa.piece(Y, w, j);
-#pragma unroll
-  for (int j = 0; j < 8; ++j) ob.piece(Y + OPB, w, j);
-  oa.advance();
-  ob.advance();
-  __builtin_amdgcn_s_waitcnt(waitcnt_imm(16, 15));
-  __builtin_amdgcn_s_barrier();
-  // the loop's read order (B fragments first): one waitcnt state at the loop head
-#pragma unroll
-  for (int i = 0; i < 8; ++i) b0[i] = ob.frag(X + OPB, 0, i);
-#pragma unroll
-  for (int i = 0; i < 8; ++i) a0[i] = oa.frag(X, 0, i);
-  for (int t = 0; t < np - 1; ++t) pair_step<LA, LB, true>(X, Y, oa, ob, w, acc, a0, b0, a1, b1);
-  pair_step<LA, LB, false>(X, Y, oa, ob, w, acc, a0, b0, a1, b1);
-}
-
-
-// ============================================================================================
-// Ring variant (cfg 13): 32-deep K-steps in NS = 4 slots of 32 KB, three steps in flight ahead of the one being
-// computed (the pair loop above keeps one 64-deep K-tile ahead, 1.5 sub-steps to land: load-latency bound on the
-// long-T weight gradients, as the 8-wave two-stage loop of gemm_wgrad.hip was). Per step u (slot u % 4):
-//   vmcnt: this wave's pieces of step u + 1 landed (F(u), read during step u - 1: the compiler's counted LDS waits)
-//   MFMA group 0 | lgkmcnt(0), barrier (every wave's step u + 1 landed, every wave done reading slot u % 4)
-//   MFMA on F(u) | ds_read F(u + 1) from slot (u + 1) % 4 | global_load_lds step u + 4 -> slot u % 4 (1 piece/group)
-// ROW images: [256 rows][32 k], 64-B rows, chunk c at slot c ^ S((row >> 2) & 3), S = {0, 2, 3, 1} (the 16-lane
-// groups of ds_read_b128 conflict-free, csrc/gemm_tn.hip); TR images: [32 k][128 columns] as above.
-// ============================================================================================
-constexpr int BK32 = 32;
-constexpr int OPB32 = 256 * BK32 * 2;  // 16 KB
-constexpr int SLOT32 = 2 * OPB32;       // 32 KB
-constexpr int IMG32 = BK32 * ROWB_T;    // 8 KB
-
-__device__ __forceinline__ int sel4(int q) { return (0x78 >> (2 * q)) & 3; }
-
 template <int L>
 struct Op32;
 
@@ -463,121 +144,143 @@ struct Op32<TR> {
   }
 };
 
-// one 32-deep step on F(u) = (fa, fb); READ: F(u + 1) from `nxt` into (ra, rb); DMA: step u + 4 into `cur`
-template <int LA, int LB, bool READ, bool DMA, int VM, bool BAR>
-__device__ __forceinline__ void rstep(f32x4 (&acc)[8][8], const bf16x8 (&fa)[8], const bf16x8 (&fb)[8],
-                                      bf16x8 (&ra)[8], bf16x8 (&rb)[8], const char* __restrict__ nxt,
-                                      char* __restrict__ cur, Op32<LA>& oa, Op32<LB>& ob, int w) {
-  __builtin_amdgcn_s_waitcnt(waitcnt_imm(VM, 15));
+struct Epi {
+  u16* C;          // output rows [M, ldc]
+  float* P;        // split slabs (+ parked whole-tile norm partials) or the norm slots (no split)
+  long ldc;
+  int flags;       // bit 0: accumulate into C (beta = 1); bit 1: gradient-norm partials
+};
+
+__device__ __forceinline__ float fbits(unsigned u) { return __uint_as_float(u); }
+
+// TRC accumulators -> 8 consecutive fp32 columns per (fragment row i, fragment pair p) per lane: lane (g, ii) holds
+// row 16 i + ii, columns 32 p + 16 (g & 1) + 8 (g >> 1) + 0..7 of the wave tile.
+__device__ __forceinline__ void gather8(const f32x4 (&acc)[8][8], int i, int p, float (&v)[8]) {
 #pragma unroll
-  for (int i = 0; i < 8; ++i) {
-#pragma unroll
-    for (int j = 0; j < 8; ++j) mfma(acc[i][j], fb[j], fa[i]);
-    if (BAR && i == 0) {
-      __builtin_amdgcn_s_waitcnt(waitcnt_imm(63, 0));
-      __builtin_amdgcn_s_barrier();
-    }
-    if (READ) {
-      if (i < 4) {
-        rb[2 * i] = ob.frag(nxt + OPB32, 2 * i);
-        rb[2 * i + 1] = ob.frag(nxt + OPB32, 2 * i + 1);
-      } else {
-        ra[2 * i - 8] = oa.frag(nxt, 2 * i - 8);
-        ra[2 * i - 7] = oa.frag(nxt, 2 * i - 7);
-      }
-    }
-    if (DMA) {
-      if (i < 4) oa.piece(cur, w, i);
-      else ob.piece(cur + OPB32, w, i - 4);
-    }
-  }
-  if (DMA) {
-    oa.advance();
-    ob.advance();
+  for (int e = 0; e < 4; ++e) {
+    auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(acc[i][2 * p][e]), __float_as_uint(acc[i][2 * p + 1][e]),
+                                              false, false);
+    v[e] = fbits(r[0]);
+    v[4 + e] = fbits(r[1]);
   }
 }
 
-// Interleaved form of rstep (cfg 14): the same work, but after the barrier the 16 fragment reads and the 8 DMA pieces
-// go ONE PER MFMA GAP (op k after MFMA 8 + 7k/3, in the order B0 B1 D0 B2 B3 D1 .. A6 A7 D7) instead of a burst of
-// 2 fragments + 1 piece + their SALU behind every 8 MFMAs. One wave per SIMD issues in order: a burst that outlasts
-// the 16-cycle gap of v_mfma_f32_16x16x32_bf16 idles the matrix pipe (hipBLASLt's MT256x256x64 loop places one
-// ds_read / buffer_load between consecutive MFMAs). B fragments first: the next step's group 0 needs all 8 B and A0.
-template <int LA, int LB, bool READ, bool DMA, int VM, bool BAR, int IL>
-__device__ __forceinline__ void rstep_il(f32x4 (&acc)[8][8], const bf16x8 (&fa)[8], const bf16x8 (&fb)[8],
-                                         bf16x8 (&ra)[8], bf16x8 (&rb)[8], const char* __restrict__ nxt,
-                                         char* __restrict__ cur, Op32<LA>& oa, Op32<LB>& ob, int w) {
-  // IL bit 0: fragment reads interleaved (else 2 behind each group), bit 1: DMA pieces interleaved (else 1 per group)
-  __builtin_amdgcn_s_waitcnt(waitcnt_imm(VM, 15));
+// Whole tile -> C (bf16, optionally + C); nrm: this wave's gradient-norm slot (sum of squares of the stored values).
+__device__ __forceinline__ void store_tile(const f32x4 (&acc)[8][8], const Epi& ea, int row0, int col0, int lane,
+                                           float* nrm) {
+  const int g = lane >> 4, ii = lane & 15;
+  const int cofs = col0 + 16 * (g & 1) + 8 * (g >> 1);
+  float ss = 0.f;
+  if (ea.flags & 1) {
+    // the accumulated C streams through a PD-deep register ring over the 32 (fragment row, column pair) units: unit
+    // u + PD is loaded while unit u computes, instead of one exposed HBM round trip per unit (the fragment registers
+    // of the main loop are free here)
+    constexpr int U = 32, PD = 8;
+    auto at = [&](int u) -> long { return (long)(row0 + 16 * (u >> 2) + ii) * ea.ldc + cofs + 32 * (u & 3); };
+    uint4 rg[PD];
+#pragma unroll
+    for (int u = 0; u < PD; ++u) rg[u] = *(const uint4*)(ea.C + at(u));
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      float v[8], a[8];
+      gather8(acc, u >> 2, u & 3, v);
+      unpack8(rg[u % PD], a);
+      if (u + PD < U) rg[u % PD] = *(const uint4*)(ea.C + at(u + PD));
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] += a[e];
+      if (nrm != nullptr) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) ss += v[e] * v[e];
+      }
+      *(uint4*)(ea.C + at(u)) = pack8(v);
+    }
+  } else {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const long row = row0 + 16 * i + ii;
+#pragma unroll
+      for (int p = 0; p < 4; ++p) {
+        float v[8];
+        gather8(acc, i, p, v);
+        if (nrm != nullptr) {
+#pragma unroll
+          for (int e = 0; e < 8; ++e) ss += v[e] * v[e];
+        }
+        *(uint4*)(ea.C + row * ea.ldc + cofs + 32 * p) = pack8(v);
+      }
+    }
+  }
+  if (nrm != nullptr) {  // 8 slots per tile (the 8-wave kernels' layout): waves 0..3 write theirs and zero w + 4, so
+    ss = wave_sum(ss);    // slots parked in an uninitialised split-K buffer (hybrid launches) are never garbage
+    if (lane == 0) {
+      nrm[0] = ss;
+      nrm[4] = 0.f;
+    }
+  }
+}
+
+// split piece: fp32 wave tile -> the piece's tile-local slab P[256][256]
+__device__ __forceinline__ void store_partial(const f32x4 (&acc)[8][8], float* __restrict__ P, int wm, int wn, int lane) {
+  const int g = lane >> 4, ii = lane & 15;
+  const int c = 128 * wn + 16 * (g & 1) + 8 * (g >> 1);
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    float* row = P + (long)(128 * wm + 16 * i + ii) * 256 + c;
+#pragma unroll
+    for (int p = 0; p < 4; ++p) {
+      float v[8];
+      gather8(acc, i, p, v);
+      *(float4*)(row + 32 * p) = make_float4(v[0], v[1], v[2], v[3]);
+      *(float4*)(row + 32 * p + 4) = make_float4(v[4], v[5], v[6], v[7]);
+    }
+  }
+}
+
+// One 32-deep step on F(u) = (fa, fb): MFMAs, and one memory op per MFMA gap after the barrier — the 16 reads of
+// F(u + 1) from `nxt` into (ra, rb) and the 8 LDS-DMA pieces of step u + 4 into `cur` (op k after MFMA 8 + 7k/3, in the
+// order B0 B1 D0 B2 B3 D1 .. A6 A7 D7).
+template <int LA, int LB>
+__device__ __forceinline__ void rstep(f32x4 (&acc)[8][8], const bf16x8 (&fa)[8], const bf16x8 (&fb)[8],
+                                      bf16x8 (&ra)[8], bf16x8 (&rb)[8], const char* __restrict__ nxt,
+                                      char* __restrict__ cur, Op32<LA>& oa, Op32<LB>& ob, int w) {
+  __builtin_amdgcn_s_waitcnt(waitcnt_imm(16, 15));
 #pragma unroll
   for (int i = 0; i < 8; ++i) {
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       mfma(acc[i][j], fb[j], fa[i]);
-      if (BAR && i == 0 && j == 7) {
+      if (i == 0 && j == 7) {  // this wave's reads of the slot the DMA below overwrites have retired
         __builtin_amdgcn_s_waitcnt(waitcnt_imm(63, 0));
         __builtin_amdgcn_s_barrier();
       }
       const int n = 8 * i + j;
       const int k = n < 8 ? -1 : ((n - 8) * 3 + 6) / 7;  // the op placed after MFMA n, if any
-      const bool slot = k >= 0 && k < 24 && 8 + (k * 7) / 3 == n;
+      if (k < 0 || k >= 24 || 8 + (k * 7) / 3 != n) continue;
       const int t = k / 3, r = k % 3;
-      if (READ) {
-        int f = -1;
-        if ((IL & 1) && slot && r < 2) f = 2 * t + r;
-        if (!(IL & 1) && j == 7) {
-          if (i < 4) {
-            rb[2 * i] = ob.frag(nxt + OPB32, 2 * i);
-            rb[2 * i + 1] = ob.frag(nxt + OPB32, 2 * i + 1);
-          } else {
-            ra[2 * i - 8] = oa.frag(nxt, 2 * i - 8);
-            ra[2 * i - 7] = oa.frag(nxt, 2 * i - 7);
-          }
-        }
-        if (f >= 0) {
-          if (f < 8) rb[f] = ob.frag(nxt + OPB32, f);
-          else ra[f - 8] = oa.frag(nxt, f - 8);
-        }
-      }
-      if (DMA) {
-        int d = -1;
-        if ((IL & 2) && slot && r == 2) d = t;
-        if (!(IL & 2) && j == 7) d = i;
-        if (d >= 0) {
-          if (d < 4) oa.piece(cur, w, d);
-          else ob.piece(cur + OPB32, w, d - 4);
-        }
+      if (r < 2) {
+        const int f = 2 * t + r;
+        if (f < 8) rb[f] = ob.frag(nxt + OPB32, f);
+        else ra[f - 8] = oa.frag(nxt, f - 8);
+      } else if (t < 4) {
+        oa.piece(cur, w, t);
+      } else {
+        ob.piece(cur + OPB32, w, t - 4);
       }
     }
   }
-  if (DMA) {
-    oa.advance();
-    ob.advance();
-  }
+  oa.advance();
+  ob.advance();
 }
 
-// four steps (u = 4 b .. 4 b + 3 on slots S0..S3); LAST: no DMA (steps past the end), counted waits shrink
-template <int LA, int LB, bool LAST, int IL>
-__device__ __forceinline__ void rbody(char* __restrict__ S0, char* __restrict__ S1, char* __restrict__ S2,
-                                      char* __restrict__ S3, Op32<LA>& oa, Op32<LB>& ob, int w, f32x4 (&acc)[8][8],
-                                      bf16x8 (&a0)[8], bf16x8 (&b0)[8], bf16x8 (&a1)[8], bf16x8 (&b1)[8]) {
-  constexpr bool D = !LAST;
-  if constexpr (IL != 0) {
-    rstep_il<LA, LB, true, D, 16, true, IL>(acc, a0, b0, a1, b1, S1, S0, oa, ob, w);
-    rstep_il<LA, LB, true, D, LAST ? 8 : 16, true, IL>(acc, a1, b1, a0, b0, S2, S1, oa, ob, w);
-    rstep_il<LA, LB, true, D, LAST ? 0 : 16, true, IL>(acc, a0, b0, a1, b1, S3, S2, oa, ob, w);
-    rstep_il<LA, LB, D, D, LAST ? 0 : 16, D, IL>(acc, a1, b1, a0, b0, S0, S3, oa, ob, w);
-  } else {
-    rstep<LA, LB, true, D, 16, true>(acc, a0, b0, a1, b1, S1, S0, oa, ob, w);
-    rstep<LA, LB, true, D, LAST ? 8 : 16, true>(acc, a1, b1, a0, b0, S2, S1, oa, ob, w);
-    rstep<LA, LB, true, D, LAST ? 0 : 16, true>(acc, a0, b0, a1, b1, S3, S2, oa, ob, w);
-    rstep<LA, LB, D, D, LAST ? 0 : 16, D>(acc, a1, b1, a0, b0, S0, S3, oa, ob, w);
-  }
-}
-
-template <int LA, int LB, int IL>
-__device__ __forceinline__ void mainloop_ring(char* __restrict__ S0, char* __restrict__ S1, char* __restrict__ S2,
-                                              char* __restrict__ S3, int nb, Op32<LA>& oa, Op32<LB>& ob, int w,
-                                              f32x4 (&acc)[8][8]) {
+// nb blocks of four steps (u = 4 b .. 4 b + 3 on slots S0..S3), ONE loop body for every block, the last included: its
+// DMA re-reads the final step (the offsets saturate, Op32::limit) into slots nobody reads again, and its reads of
+// "step 4 nb" are never used. No MFMA code after the loop, so the register allocator has no loop-exit block in which
+// to move accumulators between AGPRs and VGPRs right behind an asm MFMA it cannot see the latency of (it did, in a
+// separately compiled last body: wrong sums, profiles/r6_g4_interleave.md).
+template <int LA, int LB>
+__device__ __forceinline__ void mainloop(char* __restrict__ S0, char* __restrict__ S1, char* __restrict__ S2,
+                                         char* __restrict__ S3, int nb, Op32<LA>& oa, Op32<LB>& ob, int w,
+                                         f32x4 (&acc)[8][8]) {
   bf16x8 a0[8], b0[8], a1[8], b1[8];
   auto issue = [&](char* __restrict__ s) {
 #pragma unroll
@@ -597,25 +300,31 @@ __device__ __forceinline__ void mainloop_ring(char* __restrict__ S0, char* __res
   for (int i = 0; i < 8; ++i) b0[i] = ob.frag(S0 + OPB32, i);
 #pragma unroll
   for (int i = 0; i < 8; ++i) a0[i] = oa.frag(S0, i);
-  if constexpr (IL == 0) {
-    for (int b = 0; b < nb - 1; ++b) rbody<LA, LB, false, IL>(S0, S1, S2, S3, oa, ob, w, acc, a0, b0, a1, b1);
-    rbody<LA, LB, true, IL>(S0, S1, S2, S3, oa, ob, w, acc, a0, b0, a1, b1);
-  } else {
-    // ONE loop body for every K block, the last included: its DMA re-reads the final step (the offsets saturate,
-    // Op32::limit) into slots nobody reads again, and its reads of "step 4 nb" are never used. No MFMA code after
-    // the loop, so the register allocator has no loop-exit block in which to move accumulators between AGPRs and
-    // VGPRs right behind an asm MFMA it cannot see the latency of (it did, at the LAST body: wrong sums).
-    for (int b = 0; b < nb; ++b) rbody<LA, LB, false, IL>(S0, S1, S2, S3, oa, ob, w, acc, a0, b0, a1, b1);
-    __builtin_amdgcn_s_waitcnt(waitcnt_imm(0, 0));  // the LDS-DMA past the end lands before the LDS is released
+  for (int b = 0; b < nb; ++b) {
+    rstep<LA, LB>(acc, a0, b0, a1, b1, S1, S0, oa, ob, w);
+    rstep<LA, LB>(acc, a1, b1, a0, b0, S2, S1, oa, ob, w);
+    rstep<LA, LB>(acc, a0, b0, a1, b1, S3, S2, oa, ob, w);
+    rstep<LA, LB>(acc, a1, b1, a0, b0, S0, S3, oa, ob, w);
   }
+  __builtin_amdgcn_s_waitcnt(waitcnt_imm(0, 0));  // the LDS-DMA past the end lands before the LDS is released
 }
 
-// RING: 0 = the K-tile pair loop, 1 = the 4-slot ring, 2..4 = the ring with interleaved issue (rstep_il, IL = RING - 1)
-template <int LA, int LB, int EPI, int RING>
+__device__ __forceinline__ void tile_origin(int tile, int nbm, int nbn, int group, int& m0, int& n0) {
+  const int per_group = group * nbn;
+  const int grp = tile / per_group, first = grp * group;
+  const int gsz = min(nbm - first, group);
+  const int in = tile - grp * per_group;
+  m0 = (first + in % gsz) * 256;
+  n0 = (in / gsz) * 256;
+}
+
+// splits > 1: the tiles past ndp are split into `splits` equal ranges of 128-deep blocks (pieces -> fp32 slabs,
+// splitk_fixup_kernel).
+template <int LA, int LB>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1)))
 g4_kernel(const u16* __restrict__ A, const u16* __restrict__ B, long lda, long ldb, int kred, int nbm, int nbn,
           int group, int ndp, int splits, Epi ea) {
-  __shared__ __attribute__((aligned(16))) char smem[2 * STAGE];
+  __shared__ __attribute__((aligned(16))) char smem[4 * SLOT32];
   // Blocks [0, ndp) own whole tiles, XCD-aware bijective remap among them (consecutive ids on one XCD: shared L2 for
   // the GROUP-blocked tile order); blocks >= ndp are the split pieces. Classes by BLOCK index, not by remapped id:
   // dispatch follows block order, so the whole tiles fill the first rounds and the short pieces the last one (a
@@ -626,50 +335,33 @@ g4_kernel(const u16* __restrict__ A, const u16* __restrict__ B, long lda, long l
     const int xcd = orig & 7, q8 = ndp >> 3, r8 = ndp & 7;
     wgid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (orig >> 3);
   }
-  const int npair_all = kred / (2 * BK);
-  int tile = wgid, sk = 0, p0 = 0, p1 = npair_all;
-  if (wgid >= ndp) {  // split piece sk of tile ndp + (wgid - ndp) / splits: K-tile pairs [p0, p1)
+  const int nb_all = kred / (4 * BK32);
+  int tile = wgid, sk = 0, p0 = 0, p1 = nb_all;
+  if (wgid >= ndp) {  // split piece sk of tile ndp + (wgid - ndp) / splits: blocks [p0, p1)
     const int j = wgid - ndp;
     sk = j % splits;
     tile = ndp + j / splits;
-    p0 = (int)((long)sk * npair_all / splits);
-    p1 = (int)((long)(sk + 1) * npair_all / splits);
+    p0 = (int)((long)sk * nb_all / splits);
+    p1 = (int)((long)(sk + 1) * nb_all / splits);
   }
   int m0, n0;
-  {
-    const int per_group = group * nbn;
-    const int grp = tile / per_group, first = grp * group;
-    const int gsz = min(nbm - first, group);
-    const int in = tile - grp * per_group;
-    m0 = (first + in % gsz) * 256;
-    n0 = (in / gsz) * 256;
-  }
+  tile_origin(tile, nbm, nbn, group, m0, n0);
   const int tid = threadIdx.x, lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = w >> 1, wn = w & 1;
-  const long k0 = (long)p0 * 2 * BK;
+  const long k0 = (long)p0 * 4 * BK32;
 
   f32x4 acc[8][8];
 #pragma unroll
   for (int i = 0; i < 8; ++i)
 #pragma unroll
     for (int j = 0; j < 8; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  if constexpr (RING != 0) {
-    Op32<LA> oa;
-    Op32<LB> ob;
-    oa.init(A, lda, m0, k0, w, lane, wm);
-    ob.init(B, ldb, n0, k0, w, lane, wn);
-    if constexpr (RING >= 2) {
-      oa.limit(4 * (p1 - p0));
-      ob.limit(4 * (p1 - p0));
-    }
-    mainloop_ring<LA, LB, RING - 1>(smem, smem + SLOT32, smem + 2 * SLOT32, smem + 3 * SLOT32, p1 - p0, oa, ob, w, acc);
-  } else {
-    Op<LA> oa;
-    Op<LB> ob;
-    oa.init(A, lda, m0, k0, w, lane, wm);
-    ob.init(B, ldb, n0, k0, w, lane, wn);
-    mainloop<LA, LB>(smem, smem + STAGE, p1 - p0, oa, ob, w, acc);
-  }
+  Op32<LA> oa;
+  Op32<LB> ob;
+  oa.init(A, lda, m0, k0, w, lane, wm);
+  ob.init(B, ldb, n0, k0, w, lane, wn);
+  oa.limit(4 * (p1 - p0));
+  ob.limit(4 * (p1 - p0));
+  mainloop<LA, LB>(smem, smem + SLOT32, smem + 2 * SLOT32, smem + 3 * SLOT32, p1 - p0, oa, ob, w, acc);
   // the epilogue's accumulator reads follow the last MFMAs: 20 wait states + a fence against hoisting
   asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 3" ::: "memory");
   __builtin_amdgcn_sched_barrier(0);
@@ -678,20 +370,20 @@ g4_kernel(const u16* __restrict__ A, const u16* __restrict__ B, long lda, long l
     return;
   }
   float* nrm = nullptr;
-  if (EPI == EPI_STORE && (ea.flags & 2))
+  if (ea.flags & 2)  // whole tiles of a split launch park theirs past the slabs
     nrm = (splits <= 1 ? ea.P : ea.P + (long)(gridDim.x - ndp) * 65536) + tile * 8 + w;
-  store_tile<EPI>(acc, ea, m0 + 128 * wm, n0 + 128 * wn, lane, nrm);
+  store_tile(acc, ea, m0 + 128 * wm, n0 + 128 * wn, lane, nrm);
 }
 
 static int group_m() { return 8; }  // GROUP_M tile order
 
-template <int LA, int LB, int EPI, int RING>
+template <int LA, int LB>
 static void launch(const u16* A, long lda, const u16* B, long ldb, int M, int N, int kred, int ndp, int splits,
                    const Epi& ea) {
   const int nbm = M / 256, nbn = N / 256, tiles = nbm * nbn;
   const int grid = ndp + (tiles - ndp) * splits;
-  g4_kernel<LA, LB, EPI, RING><<<grid, 256, 0, cur_stream()>>>(A, B, lda, ldb, kred, nbm, nbn, std::min(group_m(), nbm), ndp,
-                                                          splits, ea);
+  g4_kernel<LA, LB><<<grid, 256, 0, cur_stream()>>>(A, B, lda, ldb, kred, nbm, nbn, std::min(group_m(), nbm), ndp,
+                                                     splits, ea);
   SFT_LAUNCH_CHECK();
 }
 
@@ -701,7 +393,7 @@ static void launch(const u16* A, long lda, const u16* B, long ldb, int M, int N,
 // round of 256 workgroups (hybrid) or all tiles are split over the token axis into fp32 slabs + ordered fixup.
 // nrm: gradient-norm slots (8 per whole tile, waves 0..3 written; one per fixup block of a split tile).
 void g4_wgrad(const at::Tensor& dy, const at::Tensor& x, at::Tensor& out, bool accumulate, int splits, bool hybrid,
-              float* nrm, long nrm_cap, int ring) {
+              float* nrm, long nrm_cap) {
   const int T = dy.size(0), N = dy.size(1), K = x.size(1);
   SFT_CHECK(N % 256 == 0 && K % 256 == 0 && T % 128 == 0 && T > 0, "wgrad 4-wave: N, K % 256, T % 128");
   SFT_CHECK((uintptr_t)dy.data_ptr() % 16 == 0 && (uintptr_t)x.data_ptr() % 16 == 0 &&
@@ -721,15 +413,8 @@ void g4_wgrad(const at::Tensor& dy, const at::Tensor& x, at::Tensor& out, bool a
   ea.ldc = K;
   ea.P = nsk > 0 ? part.data_ptr<float>() : nrm;
   ea.flags = (accumulate ? 1 : 0) | (nrm != nullptr ? 2 : 0);
-  auto go = [&](auto rg) {
-    g4::launch<g4::TR, g4::TR, g4::EPI_STORE, decltype(rg)::value>((const u16*)dy.data_ptr(), N, (const u16*)x.data_ptr(),
-                                                                   x.stride(0), N, K, T, ndp, nsk > 0 ? splits : 1, ea);
-  };
-  if (ring == 2) go(std::integral_constant<int, 4>());
-  else if (ring == 3) go(std::integral_constant<int, 2>());
-  else if (ring == 4) go(std::integral_constant<int, 3>());
-  else if (ring == 1) go(std::integral_constant<int, 1>());
-  else go(std::integral_constant<int, 0>());
+  g4::launch<g4::TR, g4::TR>((const u16*)dy.data_ptr(), N, (const u16*)x.data_ptr(), x.stride(0), N, K, T, ndp,
+                             nsk > 0 ? splits : 1, ea);
   if (nsk > 0) {
     const long n8 = (long)nsk * 65536 / 8;
     splitk_fixup_kernel<256, 256><<<(unsigned)((n8 + 255) / 256), 256, 0, cur_stream()>>>(
@@ -739,22 +424,20 @@ void g4_wgrad(const at::Tensor& dy, const at::Tensor& x, at::Tensor& out, bool a
   }
 }
 
-// Input gradient dX[M, N] = dy[M, K] . w[K, N] (w may be a column slice: row stride w.stride(0)); gu != nullptr:
-// SwiGLU backward epilogue, out = dgu with row stride ldo = 2 I (gate at column n, up at n + I).
-// Wave quantisation (plain epilogue): a grid that is not whole rounds of 256 workgroups runs its whole rounds as
-// whole tiles and the leftover tiles split over the reduction into fp32 slabs + the ordered fixup, e.g. the recipe's
-// padding-free M = 10240: gate_up / lm_head dgrads are 40 x 8 = 320 tiles = 1.25 rounds -> 256 + 64 x 4 pieces.
-void g4_dgrad(const at::Tensor& dy, const at::Tensor& w, u16* out, long ldo, const u16* gu, int I, int ring) {
+// Input gradient dX[M, N] = dy[M, K] . w[K, N] into out (row stride ldo; w may be a column slice: row stride
+// w.stride(0)). Wave quantisation: a grid that is not whole rounds of 256 workgroups runs its whole rounds as whole
+// tiles and, for long reductions, the leftover tiles split over the reduction into fp32 slabs + the ordered fixup, e.g.
+// the recipe's padding-free M = 10240: gate_up / lm_head dgrads are 40 x 8 = 320 tiles = 1.25 rounds -> 256 + 64 x 4
+// pieces.
+void g4_dgrad(const at::Tensor& dy, const at::Tensor& w, u16* out, long ldo) {
   const int M = dy.size(0), K = dy.size(1), N = w.size(1);
   SFT_CHECK(M % 256 == 0 && N % 256 == 0 && K % 128 == 0 && K > 0, "dgrad 4-wave: M, N % 256, K % 128");
   g4::Epi ea{};
   ea.C = out;
   ea.ldc = ldo;
-  ea.gu = gu;
-  ea.I = I;
   const int nbm = M / 256, nbn = N / 256, tiles = nbm * nbn;
   int ndp = tiles, splits = 1;
-  if (gu == nullptr && tiles % 256 != 0 && K >= 8192) {  // short reductions: the fixup costs more
+  if (tiles % 256 != 0 && K >= 8192) {  // short reductions: the fixup costs more
     const int rest = tiles > 256 ? tiles % 256 : tiles;
     const int s = std::min(std::min(256 / rest, 8), K / 128);
     if (s >= 2) {
@@ -767,28 +450,8 @@ void g4_dgrad(const at::Tensor& dy, const at::Tensor& w, u16* out, long ldo, con
     part = at::empty({(long)(tiles - ndp) * splits * 65536}, dy.options().dtype(at::kFloat));
     ea.P = part.data_ptr<float>();
   }
-  auto go = [&](auto epi, auto rg) {
-    g4::launch<g4::ROW, g4::TR, decltype(epi)::value, decltype(rg)::value>(
-        (const u16*)dy.data_ptr(), dy.stride(0), (const u16*)w.data_ptr(), w.stride(0), M, N, K, ndp, splits, ea);
-  };
-  using SW = std::integral_constant<int, g4::EPI_SWIGLU_BWD>;
-  using ST = std::integral_constant<int, g4::EPI_STORE>;
-  using R0 = std::integral_constant<int, 0>;
-  using R1 = std::integral_constant<int, 1>;
-  using R2 = std::integral_constant<int, 4>;  // interleaved reads and DMA
-  using R3 = std::integral_constant<int, 2>;  // interleaved reads only
-  using R4 = std::integral_constant<int, 3>;  // interleaved DMA only
-  if (gu != nullptr) {
-    if (ring == 2) go(SW(), R2());
-    else if (ring == 1) go(SW(), R1());
-    else go(SW(), R0());
-  } else {
-    if (ring == 2) go(ST(), R2());
-    else if (ring == 3) go(ST(), R3());
-    else if (ring == 4) go(ST(), R4());
-    else if (ring == 1) go(ST(), R1());
-    else go(ST(), R0());
-  }
+  g4::launch<g4::ROW, g4::TR>((const u16*)dy.data_ptr(), dy.stride(0), (const u16*)w.data_ptr(), w.stride(0), M, N,
+                              K, ndp, splits, ea);
   if (splits > 1) {
     SFT_TRACE("dgrad.splitk");
     const int nsk = tiles - ndp;

@@ -527,12 +527,13 @@ void launch2(const at::Tensor& dy, const at::Tensor& w, const EpiArgs& ea) {
 
 }  // namespace dgrad
 
-void g4_dgrad(const at::Tensor& dy, const at::Tensor& w, u16* out, long ldo, const u16* gu, int I, int ring);
+void g4_dgrad(const at::Tensor& dy, const at::Tensor& w, u16* out, long ldo);
 
 // dX = dy @ w (w [K, N]); with gate_up ([M, 2N], the SwiGLU input saved by the forward) the SwiGLU backward
-// is fused: returns dgu [M, 2N] instead of dX. cfg (tile n x m, LDS stages): 0 = 256 x 256 / 4, 1 = 256 x 256 / 3,
-// 2 = 256 x 128 / 3, 3 = 256 x 128 / 4 (156 VGPRs: three waves per SIMD; capping at 128 for two workgroups
-// per CU spills).
+// is fused: returns dgu [M, 2N] instead of dX. cfg: 14 = the 4-wave ring (csrc/gemm_4w.hip; every plain SmolLM3 /
+// Llama dgrad), 7 = 256 x 256 tiles with 64-deep stages (the SwiGLU-backward epilogue: 0.425 vs 0.483 ms for the
+// 4-wave kernel's register epilogue, profiles/r6_gemm_routing.md), 5 = the 32-deep ring (K % 64 != 0), 2 = 256 x 128
+// tiles (the wave-tail launch below).
 at::Tensor dgrad_gemm(const at::Tensor& dy, const at::Tensor& w, const c10::optional<at::Tensor>& gate_up,
                       int64_t cfg) {
   SFT_CHECK_CUDA(dy);
@@ -543,9 +544,9 @@ at::Tensor dgrad_gemm(const at::Tensor& dy, const at::Tensor& w, const c10::opti
   const int64_t M = dy.size(0), K = dy.size(1), N = w.size(1);
   SFT_CHECK(w.size(0) == K, "dgrad_gemm: dy [M, K] . w [K, N]");
   SFT_CHECK(cfg != 7 || K % 64 == 0, "dgrad_gemm cfg 7 (BK 64): K multiple of 64");
-  SFT_CHECK((cfg < 12 || cfg > 16) || K % 128 == 0, "dgrad_gemm cfg 12-16 (4-wave): K multiple of 128");
+  SFT_CHECK(cfg != 14 || K % 128 == 0, "dgrad_gemm cfg 14 (4-wave): K multiple of 128");
   SFT_CHECK(M % 128 == 0 && N % 256 == 0 && K % 32 == 0 && K >= 32, "dgrad_gemm: M multiple of 128 (256 for cfg 0/1), N of 256, K of 32");
-  SFT_CHECK(cfg == 2 || cfg == 3 || cfg == 8 || M % 256 == 0, "dgrad_gemm: 256 x 256 tiles need M % 256 == 0");
+  SFT_CHECK(cfg == 2 || M % 256 == 0, "dgrad_gemm: 256 x 256 tiles need M % 256 == 0");
   SFT_CHECK(dy.stride(0) % 8 == 0 && w.stride(0) % 8 == 0 && (uintptr_t)dy.data_ptr() % 16 == 0 &&
                 (uintptr_t)w.data_ptr() % 16 == 0,
             "dgrad_gemm: 16-byte aligned rows");
@@ -572,28 +573,19 @@ at::Tensor dgrad_gemm(const at::Tensor& dy, const at::Tensor& w, const c10::opti
   // one round as 256 x 128 half tiles, the whole rounds run as one launch over the leading columns and the leftover
   // columns as a second launch of half tiles (5 + 0.5 rounds). Column sub-ranges are plain pointer offsets: the
   // W columns (stride stays N), the output / gate / up columns (ea.N keeps the full width for the up half).
-  // SFTAMD_DGRAD_TAIL: 0 = off, 2 / 3 = the half-tile config (default 2).
+  // SFTAMD_DGRAD_TAIL: 0 = off, 2 = the half-tile config (default).
   auto run1 = [&](auto epi, int c, const at::Tensor& wv, const dgrad::EpiArgs& e) {
     constexpr int E = decltype(epi)::value;
     SFT_TRACE(trace_name(E == dgrad::EPI_SWIGLU_BWD ? "dgrad.swiglu.c" : "dgrad.c", c));
     switch (c) {
-      case 1: dgrad::launch<256, 256, 2, 4, 3, E>(dy, wv, e); break;
-      case 2: dgrad::launch<256, 128, 4, 2, 3, E>(dy, wv, e); break;
-      case 3: dgrad::launch<256, 128, 4, 2, 4, E>(dy, wv, e); break;
-      case 5: dgrad::launch<256, 256, 2, 4, 3, E, 1, false>(dy, wv, e); break;  // no sched_group_barrier pinning
-      case 6: dgrad::launch<256, 256, 2, 4, 4, E, 1, false>(dy, wv, e); break;
-      case 7: dgrad::launch2<256, 256, 2, 4, E>(dy, wv, e); break;
-      // 8: 4-wave workgroups of 256 n x 128 m (128 x 64 per wave), 3 x 24 KB stages: two workgroups per CU, so one's
-      // SwiGLU-backward epilogue (gate / up reads, dgu writes) can run under the other's main loop. Measured
-      // (profiles/r5_dgrad.md): 0.411 vs 0.416 ms for cfg 7 with the SwiGLU epilogue, 0.325 vs 0.319 plain — the two
-      // co-resident workgroups stay nearly in step (a start stagger of half a tile moved it by +-1 %), so cfg 7 stays
-      case 8: dgrad::launch<256, 128, 2, 2, 3, E, 2>(dy, wv, e); break;
-      case 12:  // 4-wave (csrc/gemm_4w.hip); 13: its 4-slot ring; 14: the ring with interleaved issue
-      case 13:
-      case 14:
-      case 15:
-      case 16: g4_dgrad(dy, wv, e.out, e.ldo, E == dgrad::EPI_SWIGLU_BWD ? e.gu : nullptr, e.N, c - 12); break;
-      default: dgrad::launch<256, 256, 2, 4, 4, E>(dy, wv, e);
+      case 2: dgrad::launch<256, 128, 4, 2, 3, E>(dy, wv, e); break;   // 256 x 128 tiles (the wave-tail launch)
+      case 5: dgrad::launch<256, 256, 2, 4, 3, E, 1, false>(dy, wv, e); break;  // 32-deep ring: K % 64 != 0
+      case 7: dgrad::launch2<256, 256, 2, 4, E>(dy, wv, e); break;      // 64-deep stages: the SwiGLU-backward epilogue
+      case 14:  // the 4-wave ring with interleaved issue (csrc/gemm_4w.hip), plain epilogue
+        SFT_CHECK(E == dgrad::EPI_PLAIN, "dgrad_gemm cfg 14: plain epilogue only");
+        g4_dgrad(dy, wv, e.out, e.ldo);
+        break;
+      default: SFT_CHECK(false, "dgrad_gemm: cfg ", c, " not built (2, 5, 7, 14)");
     }
   };
   const int tail_cfg = [] {
@@ -602,9 +594,9 @@ at::Tensor dgrad_gemm(const at::Tensor& dy, const at::Tensor& w, const c10::opti
   }();
   auto run = [&](auto epi) {
     const long nbn = N / 256, nbm = M / 256, tiles = nbn * nbm;
-    const bool full = cfg != 2 && cfg != 3 && cfg != 8;
+    const bool full = cfg != 2;
     long main_n = 0;
-    if (full && tail_cfg >= 2 && tail_cfg <= 3 && tiles % 256 != 0 && 256 % nbm == 0) {
+    if (full && tail_cfg == 2 && tiles % 256 != 0 && 256 % nbm == 0) {
       main_n = tiles / 256 * (256 / nbm);                  // n-tiles of the whole rounds
       if ((nbn - main_n) * (M / 128) > 256) main_n = 0;      // the half tiles must fit one round
     }
@@ -620,7 +612,6 @@ at::Tensor dgrad_gemm(const at::Tensor& dy, const at::Tensor& w, const c10::opti
     if (et.gu != nullptr) et.gu = ea.gu + n_split;
     run1(epi, tail_cfg, w.narrow(1, n_split, N - n_split), et);
   };
-  if (cfg == 2 || cfg == 3 || cfg == 8) SFT_CHECK(M % 128 == 0, "dgrad_gemm: M multiple of 128");
   if (swiglu) run(std::integral_constant<int, dgrad::EPI_SWIGLU_BWD>());
   else run(std::integral_constant<int, dgrad::EPI_PLAIN>());
   return out;

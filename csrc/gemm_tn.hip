@@ -929,212 +929,8 @@ __global__ void __launch_bounds__(512) tn3_kernel(const u16* __restrict__ A, con
 }
 
 // ============================================================================================
-// 4-wave 128 x 128 wave tiles (cfg 12): ONE wave per SIMD, 256 fp32 accumulators in the AGPR file.
-// Why: at 8 waves of 128 x 64 every 32 MFMAs of a wave need 12 fragment reads (8 A + 4 B); a 128 x 128
-// wave tile needs 16 per 64 MFMAs — a third fewer LDS read bytes per FLOP, which is what the chip's clock
-// under load responds to (/opt/skills/guides/MI355X_MICROARCH.md 'DVFS give-back'; hipBLASLt's 4-wave kernel holds ~2.17 GHz
-// vs ~1.94 for the 8-wave ping-pong on gate_up, profiles/r2_gemm_pingpong.md). hipcc cannot allocate
-// 256 accumulators next to double-buffered fragments when they are builtin MFMA values (it renames and
-// shuffles them through v_accvgpr_read/write, or spills: profiles/r1_gemm_tn.md); the MFMAs are therefore
-// inline asm with the accumulator TIED in an AGPR ("+a"), which pins every accumulator in place.
-// Hazards hipcc does not see for those asm MFMAs (/opt/skills/guides/cdna_hip_programming.md §5.7): fragment operands come
-// only from ds_read (retired by the explicit lgkmcnt(0) at every sub-step boundary, no VALU writer), and
-// the accumulators are read only after the loop, behind 20 wait states + a scheduling fence.
-// Schedule per 64-deep K-tile t (stage X = t, Y = t + 1, 64 KB each, 128-byte image rows, swz2):
-//   sub-step 0: 64 MFMA on F0 = (t, k 0..31) | ds_read F1 = (t, k 32..63) from X
-//   vmcnt(0) lgkmcnt(0) + barrier: tile t + 1 landed in Y, every wave is done reading X
-//   sub-step 1: 64 MFMA on F1 | ds_read F0 = (t + 1, k 0..31) from Y | glds tile t + 2 -> X (16 pieces/wave)
-// One barrier per K-tile; a tile's DMA has 1.5 sub-steps to land. K % 128 == 0 (even tile count).
-// ============================================================================================
-__device__ __forceinline__ void mfma_a(f32x4& c, const bf16x8& a, const bf16x8& b) {
-  asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+a"(c) : "v"(a), "v"(b));
-}
-
-template <int EPI>
-struct Stager4 {
-  const u16* pa;  // this lane's source in the wave's first A piece (image rows 8 w + lr)
-  const u16* pb;  // ... first B piece
-  long a32;       // A pieces j, j + 1 are 32 rows apart
-  long boff[8];   // B piece q relative to piece 0 (EPI row permutation)
-  __device__ __forceinline__ void piece(char* stage, int w, int j, int koff = 0) {
-    const u16* src = (j < 8 ? pa + j * a32 : pb + boff[j - 8]) + koff;
-    glds16(src, stage + (w + 4 * j) * 1024);
-  }
-};
-
-// DIAG (timing-only builds, wrong results; tools/bench_gemm_tn.py cfg 1200 + DIAG): bit 0 = no DMA in the loop,
-// bit 1 = no fragment reads in the loop, bit 2 = no barriers in the loop.
-// One sub-step = 8 MFMA groups (fragment row i x the 8 B fragments). FRONT: the 16 fragment reads for the next
-// sub-step are issued after groups 0..3 (4 per group) so they have half a sub-step to land before the boundary's
-// lgkmcnt(0), instead of trailing into it. DMA pieces [J0, J0 + NP) of the wave are spread over the 8 groups. BAR: the
-// K-tile barrier is issued after group 0's MFMAs (which need only registers), ahead of the group's reads / DMA.
-template <int EPI, int DIAG, bool FRONT, int J0, int NP, bool BAR, int DG = 8>
-__device__ __forceinline__ void tn4_sub(f32x4 (&acc)[8][8], const bf16x8 (&fa)[8], const bf16x8 (&fb)[8],
-                                        bf16x8 (&ra)[8], bf16x8 (&rb)[8], const char* img, int offA, int offB,
-                                        Stager4<EPI>& st, char* dst, int w) {
-  static_assert(NP % DG == 0 && J0 + NP <= 16, "DMA pieces per group");
-#pragma unroll
-  for (int i = 0; i < 8; ++i) {
-#pragma unroll
-    for (int j = 0; j < 8; ++j) mfma_a(acc[i][j], fa[i], fb[j]);
-    if (BAR && i == 0 && !(DIAG & 4)) __builtin_amdgcn_s_barrier();
-    if (!(DIAG & 2)) {
-      if (!FRONT) {
-        ra[i] = lds_row(img, offA + 2048 * i);
-        rb[i] = lds_row(img, offB + 2048 * i);
-      } else if (i < 4) {
-        ra[2 * i] = lds_row(img, offA + 2048 * (2 * i));
-        rb[2 * i] = lds_row(img, offB + 2048 * (2 * i));
-        ra[2 * i + 1] = lds_row(img, offA + 2048 * (2 * i + 1));
-        rb[2 * i + 1] = lds_row(img, offB + 2048 * (2 * i + 1));
-      }
-    } else {
-      asm volatile("" : "+v"(ra[i]), "+v"(rb[i]));
-    }
-    if (!(DIAG & 1)) {
-      // DG = groups the DMA is spread over (8: the whole sub-step; 4 / 2: front-loaded, more time to land)
-      if (i < DG) {
-#pragma unroll
-        for (int k = 0; k < NP / DG; ++k) st.piece(dst, w, J0 + i * (NP / DG) + k);
-      }
-    }
-  }
-}
-
-// VAR: bit 0 FRONT reads, bit 1 split DMA (8 pieces in sub-step 1 of tile t, 8 in sub-step 0 of tile t + 1 — the
-// tile's 64 KB spread over a whole K-tile of MFMA instead of one sub-step), bit 2 barrier after the first MFMA group,
-// bit 3 / bit 4: the sub-step-1 DMA front-loaded into MFMA groups 0-3 / 0-1 (more time to land before the next
-// boundary's vmcnt(0))
-template <int EPI, int DIAG = 0, int VAR = 0>
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1)))
-tn4_kernel(const u16* __restrict__ A, const u16* __restrict__ B, int K, long lda, long ldb, int nbm, int nbn,
-           int group, EpiArgs ea) {
-  using G = Cfg2<256, 256, 2, 2, 2>;
-  constexpr bool FRONT = VAR & 1, BAR = VAR & 4;
-  constexpr int P1 = (VAR & 2) ? 8 : 16, NB = 16 - P1;  // DMA pieces per wave in sub-step 1 / the next sub-step 0
-  constexpr int DG1 = (VAR & 16) ? 2 : ((VAR & 8) ? 4 : 8);
-  __shared__ __attribute__((aligned(16))) char smem[G::LDS];
-  const int nwg = gridDim.x, orig = blockIdx.x;
-  const int xcd = orig & 7, q8 = nwg >> 3, r8 = nwg & 7;
-  const int wgid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (orig >> 3);
-  const int per_group = group * nbn;
-  const int grp = wgid / per_group, first = grp * group;
-  const int gsz = min(nbm - first, group);
-  const int in = wgid - grp * per_group;
-  const int bm = first + in % gsz, bn = in / gsz;
-  const int m0 = bm * 256, n0 = bn * 256;
-  const int tid = threadIdx.x, lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wm = w >> 1, wn = w & 1;
-  const int nk = K / BK2;
-
-  Stager4<EPI> st;
-  {
-    // piece P = w + 4 j holds image rows 8 P + lr (lr = lane >> 3), slot lane & 7; (row >> 1) & 7 = 4 (P & 1) +
-    // (lr >> 1) and P & 1 = w & 1 for every piece of the wave
-    const int lr = lane >> 3, ch = (lane & 7) ^ (4 * (w & 1) + (lr >> 1));
-    st.pa = A + (long)(m0 + 8 * w + lr) * lda + 8 * ch;
-    st.a32 = 32 * lda;
-    const int r0 = b2_row<EPI>(w, n0, ea.I);
-    st.pb = B + (long)(r0 + lr) * ldb + 8 * ch;
-#pragma unroll
-    for (int q = 0; q < 8; ++q) st.boff[q] = (long)b2_koff<EPI, 4>(q) * ldb;
-  }
-  const int g = lane >> 4, ii = lane & 15;
-  const int ra = wm * 128 + ii, rb = 256 + wn * 128 + ii;
-  const int offA0 = ra * ROWB2 + 16 * swz2(ra, g), offA1 = ra * ROWB2 + 16 * swz2(ra, 4 + g);
-  const int offB0 = rb * ROWB2 + 16 * swz2(rb, g), offB1 = rb * ROWB2 + 16 * swz2(rb, 4 + g);
-  f32x4 acc[8][8];
-#pragma unroll
-  for (int i = 0; i < 8; ++i)
-#pragma unroll
-    for (int j = 0; j < 8; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  char* X = smem;
-  char* Y = smem + G::STAGE;
-  // prologue: tile 0 -> X, the first P1 pieces of tile 1 -> Y (the rest in sub-step 0 of tile 0)
-#pragma unroll
-  for (int j = 0; j < 16; ++j) st.piece(X, w, j);
-  st.pa += BK2;
-  st.pb += BK2;
-#pragma unroll
-  for (int j = 0; j < P1; ++j) st.piece(Y, w, j);
-  if (NB == 0) {
-    st.pa += BK2;
-    st.pb += BK2;
-  }
-  if (!(DIAG & 16)) {  // DIAG 16 (timing only): the prologue's wait for tile 0 skipped
-    __builtin_amdgcn_s_waitcnt(waitcnt_imm(P1, 15));  // tile 0 landed (tile 1 may fly)
-    __builtin_amdgcn_s_barrier();
-  }
-  bf16x8 a0[8], b0[8], a1[8], b1[8];
-#pragma unroll
-  for (int i = 0; i < 8; ++i) {
-    a0[i] = lds_row(X, offA0 + 2048 * i);
-    b0[i] = lds_row(X, offB0 + 2048 * i);
-  }
-  // Two K-tiles per pass: t on X, t + 1 on Y. Branch-free (a conditional sub-step splits the accumulators' live
-  // ranges and hipcc spills them); the last pass, whose only DMA is the rest of tile nk - 1, is peeled.
-  auto body = [&](auto d0, auto d1) {
-    constexpr bool D0 = decltype(d0)::value, D1 = decltype(d1)::value;  // DMA of the first / the other sub-steps
-    __builtin_amdgcn_s_waitcnt(waitcnt_imm(63, 0));
-    tn4_sub<EPI, DIAG, FRONT, P1, D0 ? NB : 0, false>(acc, a0, b0, a1, b1, X, offA1, offB1, st, Y, w);
-    if (D0 && NB) {
-      st.pa += BK2;
-      st.pb += BK2;
-    }
-    __builtin_amdgcn_s_waitcnt(waitcnt_imm(0, 0));
-    if (!BAR && !(DIAG & 4)) __builtin_amdgcn_s_barrier();
-    tn4_sub<EPI, DIAG, FRONT, 0, D1 ? P1 : 0, BAR, DG1>(acc, a1, b1, a0, b0, Y, offA0, offB0, st, X, w);
-    if (D1 && NB == 0) {
-      st.pa += BK2;
-      st.pb += BK2;
-    }
-    __builtin_amdgcn_s_waitcnt(waitcnt_imm(63, 0));
-    tn4_sub<EPI, DIAG, FRONT, P1, D1 ? NB : 0, false>(acc, a0, b0, a1, b1, Y, offA1, offB1, st, X, w);
-    if (D1 && NB) {
-      st.pa += BK2;
-      st.pb += BK2;
-    }
-    __builtin_amdgcn_s_waitcnt(waitcnt_imm(0, 0));
-    if (!BAR && !(DIAG & 4)) __builtin_amdgcn_s_barrier();
-    tn4_sub<EPI, DIAG, FRONT, 0, D1 ? P1 : 0, BAR, DG1>(acc, a1, b1, a0, b0, X, offA0, offB0, st, Y, w);
-    if (D1 && NB == 0) {
-      st.pa += BK2;
-      st.pb += BK2;
-    }
-  };
-  for (int t = 0; t < nk - 2; t += 2) body(std::true_type(), std::true_type());
-  body(std::true_type(), std::false_type());
-  // the last MFMAs' results are read by the epilogue's v_accvgpr_read: 20 wait states, then a fence that keeps
-  // the compiler from hoisting those reads above the nops
-  asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 3" ::: "memory");
-  __builtin_amdgcn_sched_barrier(0);
-  __builtin_amdgcn_s_waitcnt(waitcnt_imm(0, 0));
-  __syncthreads();
-  if constexpr (DIAG & 8) {  // timing only: no epilogue (one value per lane keeps the accumulators live)
-    float sum = 0.f;
-#pragma unroll
-    for (int i = 0; i < 8; ++i)
-#pragma unroll
-      for (int j = 0; j < 8; ++j) sum += acc[i][j][0] + acc[i][j][1] + acc[i][j][2] + acc[i][j][3];
-    if (sum == 1.2345f) ea.C[tid] = 1;
-  } else {
-    epilogue<G, EPI>(smem, acc, ea, m0, n0, wm, wn, w, lane);
-  }
-}
-
-template <int EPI, int DIAG = 0, int VAR = 0>
-void launch4(const at::Tensor& a, const at::Tensor& w, int N, const EpiArgs& ea) {
-  const int M = a.size(0), K = a.size(1);
-  SFT_CHECK(M % 256 == 0 && N % 256 == 0 && K % 128 == 0, "gemm_tn 4-wave: M, N % 256, K % 128");
-  const int nbm = M / 256, nbn = N / 256;
-  tn4_kernel<EPI, DIAG, VAR><<<nbm * nbn, 256, 0, cur_stream()>>>((const u16*)a.data_ptr(), (const u16*)w.data_ptr(), K,
-                                                       a.stride(0), w.stride(0), nbm, nbn, std::min(group_m(), nbm),
-                                                       ea);
-  SFT_LAUNCH_CHECK();
-}
-
-// ============================================================================================
-// Persistent 4-wave GEMM (cfg 50): the cfg 12 main loop with the per-tile fixed cost taken off the critical path.
+// Persistent 4-wave GEMM (the main loop of tn6 below): 4 waves of 128 x 128 (one wave per SIMD, 256 fp32 accumulators
+// pinned in AGPRs by tied inline-asm MFMAs, csrc/gemm_4w.hip) with the per-tile fixed cost taken off the critical path.
 // A K = 2048 tile round of the non-persistent kernels costs ~16 us besides its K loop (K sweep: 0.228 ms per 1024 of
 // K + 0.18 ms fixed on gate_up, profiles/r3_gemm_4wave.md): the prologue's 128 KB burst of every CU at once and the
 // LDS-staged epilogue's store burst. Here one workgroup per CU walks its XCD's tiles (per-XCD contiguous ranges of
@@ -1216,16 +1012,6 @@ __device__ __forceinline__ void tn5_sub(f32x4 (&acc)[8][8], const bf16x8 (&fa)[8
   }
 }
 
-template <int EPI>
-__device__ __forceinline__ void tn5_stager(Stager5<EPI>& st, const u16* A, const u16* B, long lda, long ldb, int m0,
-                                           int n0, int w, int lane, int I) {
-  const int lr = lane >> 3, ch = (lane & 7) ^ (4 * (w & 1) + (lr >> 1));
-  st.ra = tile_rsrc(A + (long)m0 * lda);
-  st.va = (unsigned)(((8 * w + lr) * lda + 8 * ch) * 2);
-  st.vb = (unsigned)(((long)(b2_row<EPI>(w, n0, I) + lr) * ldb + 8 * ch) * 2);
-  st.kb = 0;
-}
-
 __device__ __forceinline__ void tn5_coords(int tile, int nbm, int nbn, int group, int& m0, int& n0) {
   const int per_group = group * nbn;
   const int grp = tile / per_group, first = grp * group;
@@ -1237,224 +1023,14 @@ __device__ __forceinline__ void tn5_coords(int tile, int nbm, int nbn, int group
 
 __device__ __forceinline__ unsigned pack2(float a, float b) { return (unsigned)f2bf(a) | ((unsigned)f2bf(b) << 16); }
 
-// TRC accumulators of the wave's 128 x 128 tile -> C, 16-byte stores straight from registers (see above).
-// PLAIN: 32 stores per lane. ROPE (the wave's 128 columns are one head, fragments 2q / 2q + 1 = head dims d / d + 64 of
-// one lane): rotate in registers (bf16 projection values, as the unfused path sees them), then pair lo / hi with
-// permlane16_swap — 32 stores. SWIGLU (fragments 2q / 2q + 1 = gate / up of the same act columns): gate / up paired
-// with each other, act (q) with act (q + 1) — 48 stores.
-template <int EPI>
-__device__ __forceinline__ void tn5_store(f32x4 (&acc)[8][8], const EpiArgs& ea, int row0, int m_col0, int wn,
-                                          int lane) {
-  const int g = lane >> 4, ii = lane & 15;
-  if constexpr (EPI == EPI_PLAIN) {
-    u16* base = ea.C + (long)(row0 + ii) * ea.ldc + m_col0 + 16 * (g & 1) + 4 * (g & 2);
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {
-#pragma unroll
-      for (int p = 0; p < 4; ++p) {
-        unsigned v0 = pack2(acc[i][2 * p][0], acc[i][2 * p][1]), v1 = pack2(acc[i][2 * p][2], acc[i][2 * p][3]);
-        unsigned w0 = pack2(acc[i][2 * p + 1][0], acc[i][2 * p + 1][1]);
-        unsigned w1 = pack2(acc[i][2 * p + 1][2], acc[i][2 * p + 1][3]);
-        auto r0 = __builtin_amdgcn_permlane16_swap(v0, w0, false, false);
-        auto r1 = __builtin_amdgcn_permlane16_swap(v1, w1, false, false);
-        *(uint4*)(base + (long)(16 * i) * ea.ldc + 32 * p) = make_uint4(r0[0], r1[0], r0[1], r1[1]);
-      }
-    }
-  } else if constexpr (EPI == EPI_ROPE) {
-    const bool rot = m_col0 < ea.rope_cols;  // the wave's head is a q / k head (wave-uniform)
-    u16* base = ea.C + (long)(row0 + ii) * ea.ldc + m_col0 + 4 * (g & 2) + 64 * (g & 1);
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      const long row = row0 + 16 * i + ii;
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        float lo[4], hi[4];
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          lo[e] = acc[i][2 * q][e];
-          hi[e] = acc[i][2 * q + 1][e];
-        }
-        if (rot) {
-          const int d = 16 * q + 4 * g;
-          const float4 c4 = *(const float4*)(ea.cosb + row * 64 + d);
-          const float4 s4 = *(const float4*)(ea.sinb + row * 64 + d);
-          const float cs[4] = {c4.x, c4.y, c4.z, c4.w}, sn[4] = {s4.x, s4.y, s4.z, s4.w};
-#pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            const float x1 = rbf(lo[e]), x2 = rbf(hi[e]);
-            lo[e] = x1 * cs[e] - x2 * sn[e];
-            hi[e] = x2 * cs[e] + x1 * sn[e];
-          }
-        }
-        auto r0 = __builtin_amdgcn_permlane16_swap(pack2(lo[0], lo[1]), pack2(hi[0], hi[1]), false, false);
-        auto r1 = __builtin_amdgcn_permlane16_swap(pack2(lo[2], lo[3]), pack2(hi[2], hi[3]), false, false);
-        *(uint4*)(base + (long)(16 * i) * ea.ldc + 16 * q) = make_uint4(r0[0], r1[0], r0[1], r1[1]);
-      }
-    }
-  } else {  // SWIGLU: m_col0 = first act column of the wave
-    u16* gu = ea.C + (long)(row0 + ii) * ea.ldc + m_col0 + 4 * (g & 2) + (long)ea.I * (g & 1);
-    u16* ac = ea.act + (long)(row0 + ii) * ea.I + m_col0 + 4 * (g & 2) + 16 * (g & 1);
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {
-#pragma unroll
-      for (int qq = 0; qq < 2; ++qq) {
-        unsigned a01[2], a23[2];
-#pragma unroll
-        for (int h = 0; h < 2; ++h) {
-          const int q = 2 * qq + h;
-          float ga[4], up[4], o[4];
-#pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            ga[e] = rbf(acc[i][2 * q][e]);  // act from the bf16 gate / up the backward will see
-            up[e] = rbf(acc[i][2 * q + 1][e]);
-            o[e] = silu(ga[e]) * up[e];
-          }
-          auto r0 = __builtin_amdgcn_permlane16_swap(pack2(ga[0], ga[1]), pack2(up[0], up[1]), false, false);
-          auto r1 = __builtin_amdgcn_permlane16_swap(pack2(ga[2], ga[3]), pack2(up[2], up[3]), false, false);
-          *(uint4*)(gu + (long)(16 * i) * ea.ldc + 16 * q) = make_uint4(r0[0], r1[0], r0[1], r1[1]);
-          a01[h] = pack2(o[0], o[1]);
-          a23[h] = pack2(o[2], o[3]);
-        }
-        auto r0 = __builtin_amdgcn_permlane16_swap(a01[0], a01[1], false, false);
-        auto r1 = __builtin_amdgcn_permlane16_swap(a23[0], a23[1], false, false);
-        *(uint4*)(ac + (long)(16 * i) * ea.I + 32 * qq) = make_uint4(r0[0], r1[0], r0[1], r1[1]);
-      }
-    }
-  }
-}
-
 // Launched with one workgroup per CU (persistent): each walks its XCD's contiguous share of the tile order.
 __device__ __forceinline__ int tn5_range_start(int x, int tiles) {
   const int q8 = tiles >> 3, r8 = tiles & 7;
   return x * q8 + min(x, r8);
 }
 
-template <int EPI, bool NK2>
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1)))
-tn5_kernel(const u16* __restrict__ A, const u16* __restrict__ B, int K, long lda, long ldb, int nbm, int nbn,
-           int group, EpiArgs ea) {
-  using G = Cfg2<256, 256, 2, 2, 2>;
-  // The next tile's K0 AND K1 go out in the last sub-step (both stages are free then), the epilogue's NST stores after
-  // them: the next tile waits vmcnt(NST + 16) (PLAIN / ROPE) or vmcnt(NST) (SWIGLU, 48 stores: the counter holds 63)
-  // for K0, and its first boundary only vmcnt(NST) for K1 — the stores drain under its first K-tile.
-  constexpr int NST = EPI == EPI_SWIGLU ? 48 : 32;
-  __shared__ __attribute__((aligned(16))) char smem[2 * G::STAGE];
-  const int tiles = nbm * nbn, nwg = gridDim.x, orig = blockIdx.x;
-  // this XCD's contiguous share of the tile order, walked round-robin by its workgroups (blocks b, b + 8, ...)
-  const int xcd = orig & 7, l = orig >> 3, nx = (nwg - xcd + 7) >> 3;
-  const int t_end = tn5_range_start(xcd + 1, tiles);
-  int tile = tn5_range_start(xcd, tiles) + l;
-  const int tid = threadIdx.x, lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6);
-  if (tile >= t_end) return;
-  const int wm = w >> 1, wn = w & 1;
-  const int nk = K / BK2;
-  const int g = lane >> 4, ii = lane & 15;
-  const int ra = wm * 128 + ii, rb = 256 + wn * 128 + ii;
-  const int offA0 = ra * ROWB2 + 16 * swz2(ra, g), offA1 = ra * ROWB2 + 16 * swz2(ra, 4 + g);
-  const int offB0 = rb * ROWB2 + 16 * swz2(rb, g), offB1 = rb * ROWB2 + 16 * swz2(rb, 4 + g);
-  char* X = smem;
-  char* Y = smem + G::STAGE;
-  Stager5<EPI> st;
-  st.rb = tile_rsrc(B);
-  st.a32 = (unsigned)(64 * lda);
-#pragma unroll
-  for (int q = 0; q < 8; ++q) st.boff[q] = (unsigned)(b2_koff<EPI, 4>(q) * ldb * 2);
-  int m0, n0;
-  tn5_coords(tile, nbm, nbn, group, m0, n0);
-  tn5_stager(st, A, B, lda, ldb, m0, n0, w, lane, ea.I);
-#pragma unroll
-  for (int j = 0; j < 16; ++j) st.piece(X, w, j);
-  st.adv(BK2);
-#pragma unroll
-  for (int j = 0; j < 16; ++j) st.piece(Y, w, j);
-  st.adv(BK2);
-  __builtin_amdgcn_s_waitcnt(waitcnt_imm(16, 15));  // K0 of the first tile (its K1 may fly)
-  f32x4 acc[8][8];
-  bf16x8 a0[8], b0[8], a1[8], b1[8];
-  bool first = true;
-  for (;;) {
-    __builtin_amdgcn_s_barrier();
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      a0[i] = lds_row(X, offA0 + 2048 * i);
-      b0[i] = lds_row(X, offB0 + 2048 * i);
-    }
-    const int next = tile + nx;
-    const bool has_next = next < t_end;
-    int m1 = m0, n1 = n0;
-    if (has_next) tn5_coords(next, nbm, nbn, group, m1, n1);
-    // K-tile pairs (t on X, t + 1 on Y); boundary = vmcnt(0) lgkmcnt(0) + the barrier after the next sub-step's
-    // first MFMA group. LAST: the final sub-step DMAs the next tile's K0 into X (the current tile's K0 again when
-    // there is none: branch-free, harmless) and reads nothing.
-    auto pair = [&](auto init, auto dma, auto last) {
-      constexpr bool IN = decltype(init)::value, DM = decltype(dma)::value, LA = decltype(last)::value;
-      __builtin_amdgcn_s_waitcnt(waitcnt_imm(63, 0));
-      tn5_sub<EPI, IN, true, 0, false>(acc, a0, b0, a1, b1, X, offA1, offB1, st, X, w);
-      if (IN && !first) {
-        __builtin_amdgcn_s_waitcnt(waitcnt_imm(NST, 0));  // K1 landed; the previous tile's stores may still drain
-      } else {
-        __builtin_amdgcn_s_waitcnt(waitcnt_imm(0, 0));
-      }
-      tn5_sub<EPI, false, true, DM ? 16 : 0, true>(acc, a1, b1, a0, b0, Y, offA0, offB0, st, X, w);
-      if (DM) {
-        st.adv(BK2);
-      }
-      __builtin_amdgcn_s_waitcnt(waitcnt_imm(63, 0));
-      tn5_sub<EPI, false, true, 0, false>(acc, a0, b0, a1, b1, Y, offA1, offB1, st, Y, w);
-      __builtin_amdgcn_s_waitcnt(waitcnt_imm(0, 0));
-      if constexpr (LA) {
-        tn5_stager(st, A, B, lda, ldb, m1, n1, w, lane, ea.I);
-        tn5_sub<EPI, false, false, 32, true>(acc, a1, b1, a0, b0, X, offA0, offB0, st, X, w, Y);
-      } else {
-        tn5_sub<EPI, false, true, 16, true>(acc, a1, b1, a0, b0, X, offA0, offB0, st, Y, w);
-        st.adv(BK2);
-      }
-    };
-    if constexpr (NK2) {
-      pair(std::true_type(), std::false_type(), std::true_type());
-    } else {
-      pair(std::true_type(), std::true_type(), std::false_type());
-      for (int t = 2; t < nk - 2; t += 2) pair(std::false_type(), std::true_type(), std::false_type());
-      pair(std::false_type(), std::false_type(), std::true_type());
-    }
-    // the epilogue's accumulator reads follow the last MFMAs: 20 wait states + a fence against hoisting
-    asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 3" ::: "memory");
-    __builtin_amdgcn_sched_barrier(0);
-    tn5_store<EPI>(acc, ea, m0 + wm * 128, EPI == EPI_SWIGLU ? (n0 >> 1) + 64 * wn : n0 + wn * 128, wn, lane);
-    __builtin_amdgcn_sched_barrier(0);
-    if (!has_next) break;
-    st.adv(2 * BK2);
-    if constexpr (EPI == EPI_SWIGLU)
-      __builtin_amdgcn_s_waitcnt(waitcnt_imm(NST, 15));  // K0 and K1 landed (the 48 stores may fly)
-    else
-      __builtin_amdgcn_s_waitcnt(waitcnt_imm(NST + 16, 15));  // K0 landed (K1 and the 32 stores may fly)
-    first = false;
-    tile = next;
-    m0 = m1;
-    n0 = n1;
-  }
-  __builtin_amdgcn_s_waitcnt(waitcnt_imm(0, 15));
-}
-
-template <int EPI>
-void launch5(const at::Tensor& a, const at::Tensor& w, int N, const EpiArgs& ea) {
-  const int M = a.size(0), K = a.size(1);
-  SFT_CHECK(M % 256 == 0 && N % 256 == 0 && K % 128 == 0, "gemm_tn persistent: M, N % 256, K % 128");
-  SFT_CHECK(ea.ldc % 8 == 0 && ((uintptr_t)ea.C) % 16 == 0, "gemm_tn persistent: 16-byte aligned output rows");
-  const int nbm = M / 256, nbn = N / 256, tiles = nbm * nbn;
-  const int grid = std::min(tiles, num_cus());
-  const int grp = std::min(group_m(), nbm);
-  if (K == 128)
-    tn5_kernel<EPI, true><<<grid, 256, 0, cur_stream()>>>((const u16*)a.data_ptr(), (const u16*)w.data_ptr(), K,
-                                                          a.stride(0), w.stride(0), nbm, nbn, grp, ea);
-  else
-    tn5_kernel<EPI, false><<<grid, 256, 0, cur_stream()>>>((const u16*)a.data_ptr(), (const u16*)w.data_ptr(), K,
-                                                           a.stride(0), w.stride(0), nbm, nbn, grp, ea);
-  SFT_LAUNCH_CHECK();
-}
-
 // ============================================================================================
-// Row-contiguous store epilogue (cfg 60 / 61 = plain / nt stores): the persistent kernel above with the MFMA operands
+// Row-contiguous store epilogue (cfg 60 / 61 = plain / nt stores): the persistent main loop above with the MFMA operands
 // in natural order (A fragment first: lane (g, ii) of fragment (i, j) holds rows 16 i + 4 g + e, column 16 j + ii of
 // the wave tile) and the B image rows PERMUTED in the LDS-DMA (each lane of a piece just points at another weight
 // row) so that image row 16 j + ii of a wave's 128 columns is output column 8 ii + j. A lane's 8 fragments then hold 8
@@ -1645,7 +1221,7 @@ tn6_kernel(const u16* __restrict__ A, const u16* __restrict__ B, int K, long lda
     const bool has_next = next < t_end;
     int m1 = m0, n1 = n0;
     if (has_next) tn5_coords(next, nbm, nbn, group, m1, n1);
-    // the K-tile pairs of tn5_kernel (same boundaries, DMA placement and vmcnt accounting)
+    // the K-tile pairs of the persistent main loop (tn5_sub: boundaries, DMA placement and vmcnt accounting)
     auto pair = [&](auto init, auto dma, auto last) {
       constexpr bool IN = decltype(init)::value, DM = decltype(dma)::value, LA = decltype(last)::value;
       __builtin_amdgcn_s_waitcnt(waitcnt_imm(63, 0));
@@ -1756,11 +1332,11 @@ static void check_tn(const at::Tensor& a, const at::Tensor& w) {
   SFT_CHECK(a.size(0) % 256 == 0 && a.size(1) % tn::BK == 0 && a.size(1) > 0, "gemm_tn: M % 256, K % 32");
 }
 
-// cfg: 0 = 256x256 BK32 ring (NS 5; any K % 32), 2 = 256x256 BK64 (NS 2), 5 = BK64 transposed-C epilogue, 6 = BK64
-// 256x128 tiles with 3 LDS stages (twice the workgroups; the qkv + RoPE tail), 11 = the ping-pong 8-phase schedule
-// (transposed-C, D = 2; the default for qkv + RoPE), 12 = 4 waves of 128 x 128 (one wave per SIMD, AGPR accumulators),
-// 164 = the persistent 4-wave kernel (the LoRA wide GEMM). Measurements: profiles/r1_gemm_tn.md, r2_gemm_pingpong.md,
-// r3_gemm_4wave.md, r4_gemm_fwd.md.
+// cfg: 0 = 256x256 BK32 ring (NS 5; any K % 32), 2 = 256x256 BK64 (NS 2), 5 = BK64 transposed-C epilogue, 11 = the
+// ping-pong 8-phase schedule (transposed-C, D = 2; the default for qkv + RoPE, with a 256 x 128 tail launch), 60 / 61 =
+// the persistent 4-wave kernel with the row-contiguous store epilogue (plain / nt stores: the plain forwards without a
+// TunableOp selection, the LoRA wide GEMM). Measurements: profiles/r1_gemm_tn.md, r2_gemm_pingpong.md,
+// r4_gemm_fwd.md, r5_gemm_fwd.md.
 at::Tensor gemm_tn(const at::Tensor& a, const at::Tensor& w, int64_t cfg) {
   check_tn(a, w);
   SFT_TRACE(trace_name("tn.c", cfg));
@@ -1773,17 +1349,10 @@ at::Tensor gemm_tn(const at::Tensor& a, const at::Tensor& w, int64_t cfg) {
     if (cfg == 2) tn::launch2<256, 256, 2, 4, 2, tn::EPI_PLAIN>(a, w, N, ea);
     else if (cfg == 5) tn::launch2<256, 256, 2, 4, 2, tn::EPI_PLAIN, 3>(a, w, N, ea);
     else tn::launch3<tn::EPI_PLAIN, true, 2>(a, w, N, ea);
-  } else if (cfg == 6) {
-    SFT_CHECK(N % 128 == 0 && k64, "gemm_tn BK64 256x128: N % 128, K % 64");
-    tn::launch2<256, 128, 4, 2, 3, tn::EPI_PLAIN>(a, w, N, ea);
-  } else if (cfg == 12) {
-    tn::launch4<tn::EPI_PLAIN, 0, 4>(a, w, N, ea);
-  } else if (cfg == 164) {
-    tn::launch5<tn::EPI_PLAIN>(a, w, N, ea);
   } else if (cfg == 60 || cfg == 61) {
     tn::launch6<tn::EPI_PLAIN>(a, w, N, ea, cfg == 61);
   } else {
-    SFT_CHECK(cfg == 0, "gemm_tn: cfg ", cfg, " not built (0, 2, 5, 6, 11, 12, 60, 61, 164)");
+    SFT_CHECK(cfg == 0, "gemm_tn: cfg ", cfg, " not built (0, 2, 5, 11, 60, 61)");
     SFT_CHECK(N % 256 == 0, "gemm_tn 256x256: N % 256");
     tn::launch<256, 256, 2, 4, 5, tn::EPI_PLAIN>(a, w, N, ea);
   }
@@ -1799,9 +1368,9 @@ std::tuple<at::Tensor, at::Tensor> gemm_tn_swiglu(const at::Tensor& x, const at:
   auto gu = at::empty({M, N}, x.options());
   auto act = at::empty({M, I}, x.options());
   tn::EpiArgs ea{(u16*)gu.data_ptr(), (u16*)act.data_ptr(), nullptr, nullptr, (long)N, I, 0};
-  if (cfg == 164) tn::launch5<tn::EPI_SWIGLU>(x, w_gu, N, ea);
-  else if (cfg == 60 || cfg == 61) tn::launch6<tn::EPI_SWIGLU>(x, w_gu, N, ea, cfg == 61);
-  else if (cfg == 12) tn::launch4<tn::EPI_SWIGLU, 0, 4>(x, w_gu, N, ea);
+  SFT_CHECK(cfg == 0 || cfg == 2 || cfg == 5 || cfg == 11 || cfg == 60 || cfg == 61,
+            "gemm_tn_swiglu: cfg ", cfg, " not built (0, 2, 5, 11, 60, 61)");
+  if (cfg == 60 || cfg == 61) tn::launch6<tn::EPI_SWIGLU>(x, w_gu, N, ea, cfg == 61);
   else if (x.size(1) % 64 == 0 && N % 256 == 0 && cfg == 11) tn::launch3<tn::EPI_SWIGLU, true, 2>(x, w_gu, N, ea);
   else if (x.size(1) % 64 == 0) tn::launch2<256, 256, 2, 4, 2, tn::EPI_SWIGLU, 3>(x, w_gu, N, ea);
   else tn::launch<256, 256, 2, 4, 5, tn::EPI_SWIGLU>(x, w_gu, N, ea);
@@ -1822,12 +1391,11 @@ at::Tensor gemm_tn_rope(const at::Tensor& x, const at::Tensor& w, const at::Tens
   auto c = at::empty({M, N}, x.options());
   tn::EpiArgs ea{(u16*)c.data_ptr(), nullptr, cosb.data_ptr<float>(), sinb.data_ptr<float>(), (long)N, 0,
                  (int)rope_cols};
-  if (cfg == 164) tn::launch5<tn::EPI_ROPE>(x, w, N, ea);
-  else if (cfg == 60 || cfg == 61) tn::launch6<tn::EPI_ROPE>(x, w, N, ea, cfg == 61);
-  else if (cfg == 12) tn::launch4<tn::EPI_ROPE, 0, 4>(x, w, N, ea);
+  SFT_CHECK(cfg == 0 || cfg == 2 || cfg == 5 || cfg == 11 || cfg == 60 || cfg == 61,
+            "gemm_tn_rope: cfg ", cfg, " not built (0, 2, 5, 11, 60, 61)");
+  if (cfg == 60 || cfg == 61) tn::launch6<tn::EPI_ROPE>(x, w, N, ea, cfg == 61);
   else if (cfg == 2 && x.size(1) % 64 == 0) tn::launch2<256, 256, 2, 4, 2, tn::EPI_ROPE>(x, w, N, ea);
   else if (cfg == 5 && x.size(1) % 64 == 0) tn::launch2<256, 256, 2, 4, 2, tn::EPI_ROPE, 3>(x, w, N, ea);
-  else if (cfg == 6 && x.size(1) % 64 == 0) tn::launch2<256, 128, 4, 2, 3, tn::EPI_ROPE>(x, w, N, ea);
   else if (cfg == 11 && x.size(1) % 64 == 0) {
     // Wave-quantisation tail (gemm_dgrad.hip does the same): the SmolLM3 qkv grid is 32 x 12 = 384 tiles of
     // 256 x 256 = 1.5 rounds of 256 CUs. The whole round runs as one launch over the leading columns and the

@@ -1,27 +1,26 @@
-// Weight-gradient GEMM for gfx950: dW[N, K] (+)= dy[T, N]^T @ x[T, K], bf16 in, fp32 accumulate,
-// written (or accumulated, beta = 1) straight into the bf16 flat gradient buffer.
+// Weight-gradient GEMMs for gfx950: dW[N, K] (+)= dy[T, N]^T @ x[T, K], bf16 in, fp32 accumulate, written (or
+// accumulated, beta = 1) straight into the bf16 flat gradient buffer, with optional gradient-norm partials of the
+// stored values.
 //
-// Why a hand-written kernel: both operands of a weight gradient are stored "reduction-major"
-// (the token index T is the ROW index of dy and of x), the layout that hipBLASLt/rocBLAS run at
-// ~1.0 PF/s on MI355X for the SmolLM3 shapes (NT in BLAS terms, profiles/), against ~1.4 PF/s
-// for the forward (TN) GEMMs. On CDNA4 that layout costs nothing extra: the tiles are staged
-// row-major into LDS exactly as they sit in HBM (global_load_lds, 16 B per lane, no register
-// round trip) and BOTH MFMA operands are read with the gfx950 transposed LDS read
-// ds_read_b64_tr_b16, which delivers 4 rows x 16 columns column-major per 16-lane group.
+// Why hand-written kernels: both operands of a weight gradient are stored "reduction-major" (the token index T is the
+// ROW index of dy and of x), the layout that hipBLASLt/rocBLAS run at ~1.0 PF/s on MI355X for the SmolLM3 shapes (NT
+// in BLAS terms, profiles/), against ~1.4 PF/s for the forward (TN) GEMMs. On CDNA4 that layout costs nothing extra:
+// the tiles are staged row-major into LDS exactly as they sit in HBM (LDS-DMA, 16 B per lane, no register round
+// trip) and BOTH MFMA operands are read with the gfx950 transposed LDS read ds_read_b64_tr_b16.
 //
-// Kernel structure (CDNA guide §5 "glds vs register staging"):
-//   * BM x BN output tile per 512-thread workgroup (8 waves, WM x WN wave grid), BK = 64 tokens
-//     per K-step, two LDS stages: glds of step k+1 in flight while step k is computed;
-//   * LDS images are [64 tokens][128 columns] bf16 (256-byte rows) with the chunk XOR swizzle
-//     ch ^ ((row&3)<<2 | (row>>2)&3), applied on the GLOBAL source address (glds writes
-//     lane-linear), which keeps the transposed reads bank-conflict free;
-//   * v_mfma_f32_16x16x32_bf16; lane (g = lane>>4, i = lane&15) gets the reduction indices
-//     {4g..4g+3, 16+4g..16+4g+3} of the 32-token chunk on both operands (the order is irrelevant
-//     to a reduction as long as it is the same on both sides);
-//   * XCD-aware workgroup remap: consecutive tiles along K (which share the dy column slab) land
-//     on the same XCD / L2;
-//   * epilogue through LDS (fp32, padded rows) so the beta-accumulate read-modify-write of the
-//     bf16 gradient is 16-byte vectorised.
+// Variants (wgrad_gemm cfg = 1000 H + 100 S + c):
+//   c = 14  the 4-wave 256 x 256 ring of csrc/gemm_4w.hip — every SmolLM3 / Llama shape with N, K % 256, T % 128;
+//   c = 9   the 8-wave ring below, 256 x 128 tiles (K % 128 only, or T % 128 != 0);
+//   c = 10  the 8-wave ring below, 256 x 256 tiles;
+//   S >= 2  tiles split S ways over the token axis into fp32 slabs + the ordered fixup (deterministic): every tile
+//           (H = 0; small grids such as o_proj's 64 tiles) or only the tiles past the last whole round of 256
+//           workgroups (H = 1, hybrid).
+//
+// The 8-wave ring: BM x BN output tile per 512-thread workgroup (8 waves), 32 tokens per stage, NS stages of LDS-DMA
+// in flight; LDS images are [32 tokens][128 columns] bf16 (256-byte rows) with the chunk XOR swizzle
+// ch ^ ((row&3)<<2 | (row>>2)&3), applied on the GLOBAL source address (the DMA writes lane-linear), which keeps the
+// transposed reads bank-conflict free; v_mfma_f32_16x16x32_bf16; XCD-aware workgroup remap; epilogue through LDS
+// (fp32, padded rows) so the beta-accumulate read-modify-write of the bf16 gradient is 16-byte vectorised.
 #include "common.h"
 #include "splitk_fixup.h"
 
@@ -30,9 +29,7 @@
 namespace sftamd {
 namespace wgrad {
 
-constexpr int BK = 64;
 constexpr int ROWB = 256;             // bytes per LDS image row (128 bf16)
-constexpr int IMG = BK * ROWB;        // 16 KB per [64][128] image
 constexpr int NT = 512;
 
 __device__ __forceinline__ int swz(int row, int ch) { return ch ^ (((row & 3) << 2) | ((row >> 2) & 3)); }
@@ -51,149 +48,6 @@ __device__ __forceinline__ bf16x8 lds_tr(const char* base, int off) {
 __device__ __forceinline__ void glds16(const u16* src, char* dst) {
   __builtin_amdgcn_global_load_lds((const void __attribute__((address_space(1)))*)src,
                                    (void __attribute__((address_space(3)))*)dst, 16, 0, 0);
-}
-
-template <int BM, int BN, int WM, int WN>
-struct Cfg {
-  static constexpr int TM = BM / WM, TN = BN / WN;  // wave tile
-  static constexpr int FM = TM / 16, FN = TN / 16;  // 16x16 fragments per wave
-  static constexpr int IA = BM / 128, IB = BN / 128;
-  static constexpr int STAGE = (IA + IB) * IMG;
-  static constexpr int PIECES = (IA + IB) * 16;     // 1 KB glds pieces per stage
-  static constexpr int PPW = PIECES / 8;            // per wave
-  static constexpr int EPI_ROWS = 64;               // rows per epilogue pass per wave
-  static constexpr int EPI_LD = TN + 4;             // padded fp32 row (bank-conflict free)
-  static constexpr int EPI = 8 * EPI_ROWS * EPI_LD * 4;
-  static constexpr int LDS = (2 * STAGE > EPI) ? 2 * STAGE : EPI;
-  static_assert(WM * WN == 8, "8 waves");
-  static_assert(PIECES % 8 == 0, "pieces per wave");
-  static_assert(TM % EPI_ROWS == 0 || TM < EPI_ROWS, "epilogue passes");
-};
-
-// LDS-DMA staging of one K-tile. Piece j (1 KB = 4 image rows) of wave w is image j>>1, rows
-// 32*(j&1) + 4w .. +3, so the image (hence the matrix) of every piece is a compile-time constant
-// and the per-lane part of the address (row 4w + lane/16, swizzled chunk) is shared by all pieces:
-// two 64-bit lane pointers plus scalar offsets instead of one pointer per piece.
-template <class G>
-struct Stager {
-  const u16* pa;
-  const u16* pb;
-  long lda, ldb;
-  int w;
-  __device__ __forceinline__ void init(const u16* A, const u16* B, int N, int K, int n0, int k0, int wave, int lane) {
-    w = wave;
-    lda = N;
-    ldb = K;
-    const int r = 4 * wave + (lane >> 4), c = lane & 15;
-    pa = A + (long)r * N + n0 + 8 * swz(r, c);
-    pb = B + (long)r * K + k0 + 8 * swz(r, c);
-  }
-  __device__ __forceinline__ void issue(char* buf) {
-#pragma unroll
-    for (int j = 0; j < G::PPW; ++j) {
-      const int img = j >> 1, half = j & 1;
-      const u16* p = img < G::IA ? pa + 32 * half * lda + img * 128 : pb + 32 * half * ldb + (img - G::IA) * 128;
-      glds16(p, buf + img * IMG + (half * 8 + w) * 1024);
-    }
-    pa += BK * lda;
-    pb += BK * ldb;
-  }
-};
-
-// One K-step: wait for the current stage, start the global_load_lds of the next one, MFMA over the
-// current one. ``cur`` and ``nxt`` are __restrict__ so that, once inlined, the ds_reads of ``cur``
-// carry alias scopes disjoint from the LDS-DMA writes into ``nxt``: without that the compiler's
-// waitcnt pass drains vmcnt(0) before the first ds_read and the prefetch overlaps nothing.
-template <class G>
-__device__ __forceinline__ void kstep(const char* __restrict__ cur, char* __restrict__ nxt, int kt, int nk, Stager<G>& st,
-                                      const int (&offA)[G::FM], const int (&offB)[G::FN], f32x4 (&acc)[G::FM][G::FN]) {
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (kt + 1 < nk) st.issue(nxt);
-#pragma unroll
-  for (int ks = 0; ks < 2; ++ks) {
-    bf16x8 af[G::FM], bfr[G::FN];
-#pragma unroll
-    for (int j = 0; j < G::FN; ++j) bfr[j] = lds_tr(cur, offB[j] + ks * 32 * ROWB);
-#pragma unroll
-    for (int i = 0; i < G::FM; ++i) af[i] = lds_tr(cur, offA[i] + ks * 32 * ROWB);
-    __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-    for (int i = 0; i < G::FM; ++i)
-#pragma unroll
-      for (int j = 0; j < G::FN; ++j)
-        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
-    __builtin_amdgcn_s_setprio(0);
-  }
-}
-
-template <class G>
-__device__ __forceinline__ void read_frags(const char* base, int ks, const int (&offA)[G::FM], const int (&offB)[G::FN],
-                                           bf16x8 (&af)[G::FM], bf16x8 (&bf)[G::FN]) {
-#pragma unroll
-  for (int j = 0; j < G::FN; ++j) bf[j] = lds_tr(base, offB[j] + ks * 32 * ROWB);
-#pragma unroll
-  for (int i = 0; i < G::FM; ++i) af[i] = lds_tr(base, offA[i] + ks * 32 * ROWB);
-}
-
-template <class G>
-__device__ __forceinline__ void mfma_block(const bf16x8 (&af)[G::FM], const bf16x8 (&bf)[G::FN], f32x4 (&acc)[G::FM][G::FN]) {
-  __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-  for (int i = 0; i < G::FM; ++i)
-#pragma unroll
-    for (int j = 0; j < G::FN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bf[j], acc[i][j], 0, 0, 0);
-  __builtin_amdgcn_s_setprio(0);
-}
-
-// One K-step of the register-pipelined loop on stage ``cur`` (``oth`` = the other stage).
-template <class G, int DIAG>
-__device__ __forceinline__ void pipe_step(char* __restrict__ cur, char* __restrict__ oth, int kt, int nk, Stager<G>& st,
-                                          const int (&offA)[G::FM], const int (&offB)[G::FN], bf16x8 (&a0)[G::FM],
-                                          bf16x8 (&c0)[G::FN], bf16x8 (&a1)[G::FM], bf16x8 (&c1)[G::FN],
-                                          f32x4 (&acc)[G::FM][G::FN]) {
-  constexpr unsigned LGKM0 = 0xC07F, VM0_LGKM0 = 0x0070;
-  __builtin_amdgcn_s_waitcnt(LGKM0);  // F0 landed (read during the previous MFMA block)
-  read_frags<G>(cur, 1, offA, offB, a1, c1);
-  mfma_block<G>(a0, c0, acc);
-  __builtin_amdgcn_s_waitcnt(VM0_LGKM0);  // K-tile kt+1 landed; this wave's reads of cur done
-  if (DIAG != 2) __builtin_amdgcn_s_barrier();
-  if (DIAG != 1 && kt + 2 < nk) st.issue(cur);
-  if (kt + 1 < nk) read_frags<G>(oth, 0, offA, offB, a0, c0);
-  mfma_block<G>(a1, c1, acc);
-}
-
-// Register-pipelined main loop (PIPE = 1). Every MFMA block finds its operands already in registers:
-//   K-step kt on stage S:  [read F1 = (kt, tokens 32..63) from S | MFMA F0]
-//                          wait vmcnt(0) (K-tile kt+1 landed), lgkmcnt(0) (S fully read); barrier
-//                          [glds K-tile kt+2 -> S; read F0 = (kt+1, tokens 0..31) from S^1 | MFMA F1]
-// so the barrier is the only bubble, and each K-tile's loads have one full K-step to land. The
-// whole loop lives in one function whose two stage pointers are __restrict__: every ds_read then
-// carries an alias scope disjoint from the LDS-DMA writes into the other stage, and the compiler's
-// waitcnt pass does not drain vmcnt before it.
-template <class G, int DIAG>
-__device__ __forceinline__ void mainloop_pipe(char* __restrict__ b0, char* __restrict__ b1, int nk, Stager<G>& st,
-                                              const int (&offA)[G::FM], const int (&offB)[G::FN],
-                                              f32x4 (&acc)[G::FM][G::FN]) {
-  bf16x8 a0[G::FM], c0[G::FN], a1[G::FM], c1[G::FN];
-  auto issue = [&](char* buf) { st.issue(buf); };
-  // s_waitcnt through the builtin (not inline asm) so that the compiler's waitcnt pass sees the drain:
-  // gfx9 encoding vmcnt[3:0] | expcnt[6:4] | lgkmcnt[11:8] | vmcnt[5:4] << 14.
-  constexpr unsigned VM0_LGKM0 = 0x0070;
-  constexpr unsigned VM_PPW = (G::PPW & 15) | ((G::PPW >> 4) << 14) | 0x70 | 0xF00;
-  issue(b0);
-  if (nk > 1) {
-    issue(b1);
-    __builtin_amdgcn_s_waitcnt(VM_PPW);
-  } else {
-    __builtin_amdgcn_s_waitcnt(VM0_LGKM0);
-  }
-  __builtin_amdgcn_s_barrier();
-  read_frags<G>(b0, 0, offA, offB, a0, c0);
-  for (int kt = 0; kt < nk; kt += 2) {
-    pipe_step<G, DIAG>(b0, b1, kt, nk, st, offA, offB, a0, c0, a1, c1, acc);
-    if (kt + 1 < nk) pipe_step<G, DIAG>(b1, b0, kt + 1, nk, st, offA, offB, a0, c0, a1, c1, acc);
-  }
 }
 
 // Epilogue: fp32 wave tile -> LDS (rows padded to TN + 4 floats: conflict-free) -> 16-byte
@@ -248,69 +102,10 @@ __device__ __forceinline__ void epilogue(char* smem, f32x4 (&acc)[G::FM][G::FN],
   }
 }
 
-template <int BM, int BN, int WM, int WN, int PIPE>
-__global__ void __launch_bounds__(NT) wgrad_kernel(const u16* __restrict__ A, const u16* __restrict__ B,
-                                                   u16* __restrict__ C, int T, int N, int K, int nbk, int accumulate) {
-  using G = Cfg<BM, BN, WM, WN>;
-  __shared__ __attribute__((aligned(16))) char smem[G::LDS];
-
-  // XCD-aware bijective remap (CDNA guide §5: consecutive remapped ids share an XCD)
-  const int nwg = gridDim.x, orig = blockIdx.x;
-  const int xcd = orig & 7, q8 = nwg >> 3, r8 = nwg & 7;
-  const int wgid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (orig >> 3);
-  const int bn = wgid / nbk, bk = wgid - bn * nbk;
-  const int n0 = bn * BM, k0 = bk * BN;
-
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  const int wm = w / WN, wk = w - wm * WN;
-
-  Stager<G> st;
-  st.init(A, B, N, K, n0, k0, w, lane);
-
-  // ---- fragment read offsets (transposed reads, see attention.hip Offs::tr)
-  // 16-lane group g reads token rows 4b..4b+3 and 16+4b..16+4b+3 with b = ((g&1)<<1)|(g>>1): the two
-  // groups of each 32-lane half then read blocks 8 rows apart, which is bank-conflict free for
-  // ds_read_b64_tr_b16 on this swizzle (b = g, i.e. stacked blocks, is 2-way).
-  const int g = lane >> 4, ii = lane & 15, qq = ii >> 2, pp = ii & 3;
-  const int r0 = 4 * (((g & 1) << 1) | (g >> 1)) + qq;
-  int offA[G::FM], offB[G::FN];
-#pragma unroll
-  for (int i = 0; i < G::FM; ++i) {
-    const int nl = wm * G::TM + 16 * i;
-    offA[i] = (nl >> 7) * IMG + img_off(r0, 2 * ((nl & 127) >> 4) + (pp >> 1)) + 8 * (pp & 1);
-  }
-#pragma unroll
-  for (int j = 0; j < G::FN; ++j) {
-    const int kl = wk * G::TN + 16 * j;
-    offB[j] = (G::IA + (kl >> 7)) * IMG + img_off(r0, 2 * ((kl & 127) >> 4) + (pp >> 1)) + 8 * (pp & 1);
-  }
-
-  f32x4 acc[G::FM][G::FN];
-#pragma unroll
-  for (int i = 0; i < G::FM; ++i)
-#pragma unroll
-    for (int j = 0; j < G::FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-  const int nk = T / BK;
-  if constexpr (PIPE) {
-    mainloop_pipe<G, PIPE - 1>(smem, smem + G::STAGE, nk, st, offA, offB, acc);
-  } else {
-    st.issue(smem);
-    for (int kt = 0; kt < nk; kt += 2) {
-      kstep<G>(smem, smem + G::STAGE, kt, nk, st, offA, offB, acc);
-      if (kt + 1 < nk) kstep<G>(smem + G::STAGE, smem, kt + 1, nk, st, offA, offB, acc);
-    }
-  }
-  __syncthreads();
-
-  epilogue<G>(smem, acc, C, K, n0, k0, wm, wk, w, lane, accumulate);
-}
-
 // ============================================================================================
-// Ring-pipelined variant: BK = 32 tokens per stage, NS stages (up to all 160 KB of LDS), the
-// global_load_lds of a stage issued NS-1 steps before it is read. The 64-token, two-stage loop
-// above keeps only one 64 KB K-tile in flight per CU and measures load-latency bound (removing
-// its loads makes it 1.46x faster); the ring keeps up to NS x 32 KB in flight. Per 32-token step:
+// The 8-wave ring: BK = 32 tokens per stage, NS stages (up to all 160 KB of LDS), the LDS-DMA of a
+// stage issued NS-1 steps before it is read (a 64-token two-stage loop kept only one 64 KB K-tile in
+// flight per CU and measured load-latency bound: 1.46x faster without its loads). Per 32-token step:
 //   wait vmcnt((NS-2) x pieces) -> step t+1 landed; lgkmcnt(0) -> this wave's reads of slot t done
 //   barrier; glds step t+NS -> slot t % NS; ds_read fragments of step t+1; MFMA on step t (regs).
 // ============================================================================================
@@ -540,35 +335,11 @@ static long ring_norm_slots(int tiles, int ndp, int BM, int BN) { return (long)n
 
 // splits > 1: tiles beyond the first `full_waves` x 256 (or all of them when full_waves == 0) are split over the
 // token axis; full_waves < 0 = split every tile.
-// tail_stream (data-parallel launches only): when the grid ends in a partial round of 256 workgroups, the whole
-// rounds run on the current stream and the leftover tiles as a second launch on tail_stream (which the caller has
-// ordered after the operands and joins before the gradient is consumed), so the next kernels of backward fill the
-// CUs the partial round leaves idle.
 template <int BM, int BN, int WM, int WN, int NS, bool SCHED = false>
 void launch_ring(const at::Tensor& dy, const at::Tensor& x, at::Tensor& out, bool accumulate, int splits = 1,
-                 bool hybrid = false, float* nrm = nullptr, long nrm_cap = 0, hipStream_t tail_stream = nullptr) {
+                 bool hybrid = false, float* nrm = nullptr, long nrm_cap = 0) {
   const int T = dy.size(0), N = dy.size(1), K = x.size(1);
   const int nbn = N / BM, nbk = K / BN, tiles = nbn * nbk;
-  if (tail_stream != nullptr && splits <= 1 && tiles > 256 && tiles % 256 != 0) {
-    SFT_CHECK(nrm == nullptr || ring_norm_slots(tiles, tiles, BM, BN) <= nrm_cap, "wgrad_gemm: norm slot buffer too small");
-    const int main_tiles = tiles / 256 * 256;
-    const int flags = (accumulate ? 1 : 0) | (nrm != nullptr ? 2 : 0);
-    constexpr bool SCHED_N = BN == 256 ? false : SCHED;
-    auto go = [&](int grid, int tile0, hipStream_t st) {
-      if (nrm != nullptr)
-        ring_kernel<BM, BN, WM, WN, NS, SCHED_N, true><<<grid, NT, 0, st>>>(
-            (const u16*)dy.data_ptr(), (const u16*)x.data_ptr(), (u16*)out.data_ptr(), T, N, K, nbk, flags, nrm,
-            tiles, 1, tile0);
-      else
-        ring_kernel<BM, BN, WM, WN, NS, SCHED><<<grid, NT, 0, st>>>(
-            (const u16*)dy.data_ptr(), (const u16*)x.data_ptr(), (u16*)out.data_ptr(), T, N, K, nbk, flags, nullptr,
-            tiles, 1, tile0);
-      SFT_LAUNCH_CHECK();
-    };
-    go(main_tiles, 0, cur_stream());
-    go(tiles - main_tiles, main_tiles, tail_stream);
-    return;
-  }
   const int ndp = splits <= 1 ? tiles : (hybrid ? tiles / 256 * 256 : 0);
   const int nsk = tiles - ndp;
   SFT_CHECK(nrm == nullptr || ring_norm_slots(tiles, ndp, BM, BN) <= nrm_cap, "wgrad_gemm: norm slot buffer too small");
@@ -595,27 +366,15 @@ void launch_ring(const at::Tensor& dy, const at::Tensor& x, at::Tensor& out, boo
   }
 }
 
-template <int BM, int BN, int WM, int WN, int PIPE>
-void launch(const at::Tensor& dy, const at::Tensor& x, at::Tensor& out, bool accumulate) {
-  const int T = dy.size(0), N = dy.size(1), K = x.size(1);
-  const int nbn = N / BM, nbk = K / BN;
-  wgrad_kernel<BM, BN, WM, WN, PIPE><<<nbn * nbk, NT, 0, cur_stream()>>>(
-      (const u16*)dy.data_ptr(), (const u16*)x.data_ptr(), (u16*)out.data_ptr(), T, N, K, nbk, accumulate ? 1 : 0);
-  SFT_LAUNCH_CHECK();
-}
-
 }  // namespace wgrad
 
 void g4_wgrad(const at::Tensor& dy, const at::Tensor& x, at::Tensor& out, bool accumulate, int splits, bool hybrid,
-              float* nrm, long nrm_cap, int ring);
+              float* nrm, long nrm_cap);
 
-// cfg: 0 = auto, 1 = 256x256 (8 waves 2x4), 2 = 256x128 (8 waves 4x2); +2 = register-pipelined loop
-// norm (optional, fp32, contiguous): gradient-norm partial slots for the ring variants (cfg 9 / 10 and their split-K
-// forms): every slot the launch owns is written, the rest are left untouched (the caller zeroes the buffer once per
-// step); other variants reject it.
+// cfg: see the header. norm (optional, fp32, contiguous): gradient-norm partial slots — every slot the launch owns is
+// written, the rest are left untouched (the caller zeroes the buffer once per step).
 void wgrad_gemm(at::Tensor out, at::Tensor dy, at::Tensor x, bool accumulate, int64_t cfg,
-                const c10::optional<at::Tensor>& norm, int64_t tail_stream) {
-  hipStream_t ts = (hipStream_t)(intptr_t)tail_stream;
+                const c10::optional<at::Tensor>& norm) {
   SFT_CHECK_CUDA(dy);
   SFT_CHECK_BF16(dy);
   SFT_CHECK_BF16(x);
@@ -623,73 +382,38 @@ void wgrad_gemm(at::Tensor out, at::Tensor dy, at::Tensor x, bool accumulate, in
   SFT_CHECK_CONTIG(dy);
   SFT_CHECK_CONTIG(out);
   SFT_CHECK(dy.dim() == 2 && x.dim() == 2 && out.dim() == 2, "wgrad_gemm: 2-D operands");
-  // x may have a padded row pitch (a [T, K] view into a wider buffer) on the 4-wave kernel (cfg 12 / 13 family)
+  // x may have a padded row pitch (a [T, K] view into a wider buffer) on the 4-wave kernel
   SFT_CHECK(x.stride(1) == 1 && x.stride(0) % 8 == 0 && x.stride(0) >= x.size(1), "wgrad_gemm: x rows contiguous");
-  SFT_CHECK(x.stride(0) == x.size(1) || (cfg % 100 >= 12 && cfg % 100 <= 16), "wgrad_gemm: a padded x pitch needs cfg 12 / 13 / 14");
+  SFT_CHECK(x.stride(0) == x.size(1) || cfg % 100 == 14, "wgrad_gemm: a padded x pitch needs cfg 14");
   const int64_t T = dy.size(0), N = dy.size(1), K = x.size(1);
   SFT_CHECK(x.size(0) == T && out.size(0) == N && out.size(1) == K, "wgrad_gemm: shape mismatch");
   SFT_CHECK(T % 32 == 0 && T > 0, "wgrad_gemm: T must be a positive multiple of 32");
-  SFT_CHECK(cfg >= 7 || cfg == 0 || T % wgrad::BK == 0, "wgrad_gemm: cfg 1-6 need T % 64 == 0");
-  if (cfg == 0) cfg = (N % 256 == 0 && K % 256 == 0 && (N / 256) * (K / 256) >= 512) ? 1 : 2;
   SFT_TRACE(trace_name("wgrad.c", cfg));
   if (norm.has_value() && norm->defined()) SFT_TRACE("wgrad.norm_slots");
-  // cfg = 1000 * H + 100 * S + c: ring variant c (9 / 10) with tiles split S ways over the token (reduction)
-  // axis — all tiles (H = 0: fills the chip for small outputs, o_proj 2048 x 2048 = 64 tiles of 256 x 256) or
-  // only those past the last full wave of 256 workgroups (H = 1, hybrid data-parallel + split-K: the partial
-  // last wave of e.g. down_proj's 344 tiles becomes ~1 wave of thinner pieces); fp32 slabs + ordered fixup
   const bool hybrid = cfg >= 1000;
   const int splits = (int)((cfg % 1000) / 100);
+  SFT_CHECK(cfg < 2000, "wgrad_gemm: cfg ", cfg, " not built");
   cfg %= 100;
-  SFT_CHECK(splits <= 1 || ((cfg == 9 || cfg == 10 || (cfg >= 12 && cfg <= 16)) && T / 32 >= splits),
-            "wgrad_gemm split-K: ring cfg 9/10 or the 4-wave cfg 12 with at least one 32-token step per split");
+  SFT_CHECK(cfg == 9 || cfg == 10 || cfg == 14, "wgrad_gemm: cfg ", cfg, " not built (9, 10, 14)");
+  SFT_CHECK(splits <= 1 || T / 32 >= splits, "wgrad_gemm split-K: at least one 32-token step per split");
   float* nrm = nullptr;
   long nrm_cap = 0;
   if (norm.has_value() && norm->defined()) {
-    SFT_CHECK(cfg == 9 || cfg == 10 || (cfg >= 12 && cfg <= 16), "wgrad_gemm: norm partials need cfg 9 / 10 / 12-14");
     SFT_CHECK(norm->scalar_type() == at::kFloat && norm->is_contiguous() && norm->is_cuda(), "wgrad_gemm: fp32 norm slots");
     nrm = norm->data_ptr<float>();
     nrm_cap = norm->numel();
   }
-  if (cfg >= 12 && cfg <= 16) {  // 4 waves of 128 x 128, AGPR accumulators (csrc/gemm_4w.hip); 13: 4-slot ring;
-    g4_wgrad(dy, x, out, accumulate, splits, hybrid, nrm, nrm_cap, (int)cfg - 12);  // 14: ring, interleaved issue
+  if (cfg == 14) {  // 4 waves of 128 x 128, AGPR accumulators (csrc/gemm_4w.hip)
+    g4_wgrad(dy, x, out, accumulate, splits, hybrid, nrm, nrm_cap);
     return;
   }
-  if (splits > 1) {
-    if (cfg == 10) {
-      SFT_CHECK(N % 256 == 0 && K % 256 == 0, "wgrad_gemm ring 256x256: N, K multiples of 256");
-      wgrad::launch_ring<256, 256, 2, 4, 5, true>(dy, x, out, accumulate, splits, hybrid, nrm, nrm_cap);
-    } else {
-      SFT_CHECK(N % 256 == 0 && K % 128 == 0, "wgrad_gemm ring 256x128: N multiple of 256, K of 128");
-      wgrad::launch_ring<256, 128, 4, 2, 6, true>(dy, x, out, accumulate, splits, hybrid, nrm, nrm_cap);
-    }
-    return;
-  }
-  if (cfg == 1 || cfg == 3) {
-    SFT_CHECK(N % 256 == 0 && K % 256 == 0, "wgrad_gemm 256x256: N, K multiples of 256");
-    if (cfg == 1) wgrad::launch<256, 256, 2, 4, 0>(dy, x, out, accumulate);
-    else wgrad::launch<256, 256, 2, 4, 1>(dy, x, out, accumulate);
-  } else if (cfg == 7) {
-    SFT_CHECK(N % 256 == 0 && K % 256 == 0 && T % 32 == 0, "wgrad_gemm ring 256x256: N, K multiples of 256");
-    wgrad::launch_ring<256, 256, 2, 4, 5>(dy, x, out, accumulate);
-  } else if (cfg == 8) {
-    SFT_CHECK(N % 256 == 0 && K % 256 == 0 && T % 32 == 0, "wgrad_gemm ring 256x256: N, K multiples of 256");
-    wgrad::launch_ring<256, 256, 2, 4, 4>(dy, x, out, accumulate);
-  } else if (cfg == 9) {
-    SFT_CHECK(N % 256 == 0 && K % 128 == 0 && T % 32 == 0, "wgrad_gemm ring 256x128: N multiple of 256, K of 128");
-    wgrad::launch_ring<256, 128, 4, 2, 6>(dy, x, out, accumulate, 1, false, nrm, nrm_cap, ts);
-  } else if (cfg == 10) {
-    SFT_CHECK(N % 256 == 0 && K % 256 == 0 && T % 32 == 0, "wgrad_gemm ring 256x256: N, K multiples of 256");
-    wgrad::launch_ring<256, 256, 2, 4, 5, true>(dy, x, out, accumulate, 1, false, nrm, nrm_cap, ts);
-  } else if (cfg == 11) {
-    SFT_CHECK(N % 256 == 0 && K % 128 == 0 && T % 32 == 0, "wgrad_gemm ring 256x128: N multiple of 256, K of 128");
-    wgrad::launch_ring<256, 128, 4, 2, 6, true>(dy, x, out, accumulate);
-  } else if (cfg == 5 || cfg == 6) {  // diagnostics (wrong results): 5 = no loads in loop, 6 = no barrier
-    if (cfg == 5) wgrad::launch<256, 256, 2, 4, 2>(dy, x, out, accumulate);
-    else wgrad::launch<256, 256, 2, 4, 3>(dy, x, out, accumulate);
+  if (cfg == 10) {
+    SFT_CHECK(N % 256 == 0 && K % 256 == 0, "wgrad_gemm ring 256x256: N, K multiples of 256");
+    wgrad::launch_ring<256, 256, 2, 4, 5, true>(dy, x, out, accumulate, splits, hybrid, nrm, nrm_cap);
   } else {
-    SFT_CHECK(N % 256 == 0 && K % 128 == 0, "wgrad_gemm 256x128: N multiple of 256, K of 128");
-    if (cfg == 2) wgrad::launch<256, 128, 4, 2, 0>(dy, x, out, accumulate);
-    else wgrad::launch<256, 128, 4, 2, 1>(dy, x, out, accumulate);
+    SFT_CHECK(N % 256 == 0 && K % 128 == 0, "wgrad_gemm ring 256x128: N multiple of 256, K of 128");
+    if (splits > 1) wgrad::launch_ring<256, 128, 4, 2, 6, true>(dy, x, out, accumulate, splits, hybrid, nrm, nrm_cap);
+    else wgrad::launch_ring<256, 128, 4, 2, 6>(dy, x, out, accumulate, 1, false, nrm, nrm_cap);
   }
 }
 

@@ -43,45 +43,34 @@ def _weight_grad_done(param: torch.Tensor) -> None:
 
 
 _WGRAD_MODE = os.environ.get("SFTAMD_WGRAD", "auto")  # auto | blas | <cfg int> (kernel variant)
-# the 4-wave ring's issue schedule (csrc/gemm_4w.hip): 13 = 2 fragments + 1 DMA piece behind every 8 MFMAs,
-# 14 = one LDS read / DMA piece per MFMA gap (rstep_il): 110.8 / 111.0 vs 109.7 / 109.5 samples/s in the step
-# (interleaved A/B, identical loss; profiles/r6_g4_interleave.md)
-_G4_RING = int(os.environ.get("SFTAMD_G4_RING", "14"))
 
 
 def _wgrad_cfg(T: int, N: int, K: int) -> int:
-    """Which wgrad GEMM runs dW[N,K] = dy[T,N]^T x[T,K]: 0 = hipBLASLt/rocBLAS, else a variant of the
-    hand-written gfx950 kernel (csrc/gemm_wgrad.hip). Chosen from tools/bench_wgrad.py on MI355X
-    (profiles/r1_wgrad_microbench.md): the 256x256 ring kernel wherever it fills >= 2 waves of the
-    256 CUs (gate_up 0.58 vs 0.74 ms, lm_head 3.2 vs 3.9 ms at T=8192), the 256x128 ring kernel on
-    mid-size grids (qkv 0.113 vs 0.139 ms, down 0.337 vs 0.349 ms); on small grids (o_proj 2048 x 2048 = 128
-    tiles of 256 x 128) the same kernel split 2 ways over the tokens (cfg 209, fp32 slabs + ordered reduce):
-    0.071 vs 0.090 ms for hipBLASLt (profiles/r2_wgrad_splitk.md); mid grids of 64-128 256 x 256 tiles (qkv) split 2
-    ways (cfg 210)."""
+    """Which wgrad GEMM runs dW[N,K] = dy[T,N]^T x[T,K]: 0 = hipBLASLt/rocBLAS, else a csrc/gemm_wgrad.hip cfg
+    (1000 H + 100 S + c). From interleaved A/Bs on MI355X at T = 8192 (tools/bench_ab.py, profiles/r6_gemm_routing.md):
+    the 4-wave ring with one read / DMA piece per MFMA gap (c = 14, csrc/gemm_4w.hip) on every shape with N, K % 256 and
+    T % 128 — small grids split over the tokens so they fill the chip (qkv 96 tiles x 2: 0.1025 vs 0.1155 ms for the
+    pair-loop kernel; o_proj 64 tiles x 4: 0.0705 vs 0.0715 for the 8-wave 256 x 128 ring split 2), grids whose last
+    round is partial hybrid-split (down_proj 344 tiles: 0.274 vs 0.310 unsplit; lm_head 4008: 2.969 vs 3.237 for the
+    8-wave 256 x 256 ring), gate_up (688 tiles) unsplit (0.534 vs 0.575 hybrid). Stream-K over the last round was
+    no faster on any of them. The 8-wave rings (c = 9 / 10) remain for K % 256 != 0 or T % 128 != 0."""
     if _WGRAD_MODE == "blas" or T % 32 or T < 1024:
         return 0
     if _WGRAD_MODE not in ("auto", ""):
         return int(_WGRAD_MODE)
     tiles = (N // 256) * (K // 256)
-    if N % 256 == 0 and K % 256 == 0 and T % 128 == 0 and 288 <= tiles < 2048:
-        # the 4-wave kernel (csrc/gemm_4w.hip, cfg 13: 128 x 128 wave tiles, AGPR accumulators, 4-slot ring of 32-token
-        # steps) where it beat the 8-wave rings in tools/bench_wgrad.py (profiles/r3_bwd_gemm_4wave.md).
-        # gate_up (688 tiles): 0.568 vs 0.578 ms (cfg 10); down_proj (344 tiles = 1.34 rounds): hybrid, the 88 tiles
-        # past the whole round split 2 ways over the tokens (1213): 0.301 vs 0.341 (cfg 13) vs 0.349 (cfg 9);
-        # lm_head / tied embedding (4008 tiles) stays on cfg 10: 3.195 vs 3.213 ms (profiles/r3_bwd_gemm_4wave.md)
-        return 1200 + _G4_RING if tiles < 512 and (T // 128) >= 2 else _G4_RING
-    if N % 256 == 0 and K % 256 == 0 and T % 128 == 0 and tiles >= 2048 and (T // 128) >= 2:
-        # lm_head / tied embedding (4008 tiles = 15.7 rounds): the 4-wave ring, its last partial round split 2 ways:
-        # 2.969 ms vs 3.237 for the 8-wave ring (cfg 10) and 3.023 unsplit (interleaved, profiles/r6_gemm_routing.md)
-        return 1200 + _G4_RING
+    if N % 256 == 0 and K % 256 == 0 and T % 128 == 0:
+        if tiles < 256:
+            s = min(8, 256 // tiles, T // 128)
+            return 100 * s + 14 if s >= 2 else 14
+        if (tiles < 512 or tiles >= 2048) and tiles % 256 and T // 128 >= 2:
+            return 1214
+        return 14
     if N % 256 == 0 and K % 256 == 0 and tiles >= 512:
         return 10
-    if (N % 256 == 0 and K % 256 == 0 and 64 < (N // 256) * (K // 256) <= 128 and (T // 32) % 2 == 0
+    if (N % 256 == 0 and K % 256 == 0 and 64 < tiles <= 128 and (T // 32) % 2 == 0
             and (N // 256) * (K // 128) < 256):
-        # e.g. qkv [3072 x 2048]: 96 tiles of 256 x 256 split 2 ways over the tokens fill 192 CUs with
-        # half-depth pieces, vs 192 tiles of 256 x 128 at 0.75 of a round: 0.113 vs 0.118 ms (r2_run48); on the
-        # 4-wave kernel (cfg 1212): 0.106 vs 0.117 ms for the 8-wave ring split the same way (cfg 210, r4_run41)
-        return 1212 if T % 128 == 0 else 210
+        return 210
     if N % 256 == 0 and K % 128 == 0 and (N // 256) * (K // 128) >= 160:
         return 9
     if N % 256 == 0 and K % 128 == 0 and (T // 32) % 2 == 0 and (N // 256) * (K // 128) >= 32:
@@ -98,9 +87,9 @@ def _wgrad_mm(out: torch.Tensor, dy2d: torch.Tensor, x2d: torch.Tensor, accumula
     if _ext.use_hip(dy2d) and dy2d.dtype == torch.bfloat16 and out.is_contiguous():
         cfg = _wgrad_cfg(dy2d.shape[0], dy2d.shape[1], x2d.shape[1])
     if cfg:
-        use_norm = norm is not None and cfg % 100 in (9, 10, 12, 13, 14)
+        use_norm = norm is not None and cfg % 100 in (9, 10, 14)
         # the 4-wave kernel reads x through its row pitch (a padded [T, K] view, e.g. the gate_up input); others copy
-        strided_ok = cfg % 100 in (12, 13, 14) and x2d.stride(1) == 1 and x2d.stride(0) % 8 == 0 and x2d.data_ptr() % 16 == 0
+        strided_ok = cfg % 100 == 14 and x2d.stride(1) == 1 and x2d.stride(0) % 8 == 0 and x2d.data_ptr() % 16 == 0
         _ext.ops().wgrad_gemm(out, dy2d.contiguous(), x2d if strided_ok else x2d.contiguous(), accumulate, cfg,
                               norm if use_norm else None)
         return use_norm
@@ -109,13 +98,6 @@ def _wgrad_mm(out: torch.Tensor, dy2d: torch.Tensor, x2d: torch.Tensor, accumula
     else:
         torch.mm(dy2d.t(), x2d, out=out)
     return False
-
-
-def wgrad_sync(dev: Optional[torch.device] = None) -> None:
-    """Weight gradients are produced in stream order on the compute stream (a side stream for them measured 3.5 %
-    slower end to end: two 256 x 256-tile GEMMs at one workgroup per CU thrash each other's L2 / LDS-DMA bandwidth,
-    profiles/r1_gemm_tn.md), so there is nothing to wait for; kept as the engine's synchronisation point."""
-    return None
 
 
 def _accumulate_weight_grad(param: torch.Tensor, dy2d: torch.Tensor, x2d: torch.Tensor,
@@ -250,17 +232,14 @@ def _dgrad_ok(dy2d: torch.Tensor, w: torch.Tensor) -> bool:
 
 
 def _dgrad_cfg(dy2d: torch.Tensor, swiglu: bool = False) -> int:
-    """Kernel configuration: 7 = 256 x 256 tiles, 64-deep K stages (two 32-deep MFMA sub-steps per barrier);
-    5 = the 32-deep three-stage ring for reductions that are not a multiple of 64 (profiles/r2_dgrad.md);
-    12 / 13 = the 4-wave kernel of csrc/gemm_4w.hip (128 x 128 wave tiles, AGPR accumulators; 13 = its 4-slot ring):
-    M = 8192, tools/bench_dgrad.py (profiles/r3_bwd_gemm_4wave.md): o 0.058 vs 0.059 ms (cfg 7), qkv 0.080 vs 0.083,
-    gate_up (K = 22016) 0.528 (cfg 13) vs 0.548 for hipBLASLt, lm_head (K = 128256) 2.98 vs 3.09. The fused SwiGLU
-    backward epilogue stays on cfg 7 (its LDS-staged epilogue: 0.436 vs 0.58 ms for the register epilogue)."""
+    """Kernel configuration (csrc/gemm_dgrad.hip): 14 = the 4-wave ring of csrc/gemm_4w.hip (one read / DMA piece per
+    MFMA gap) on every plain reduction length that is a multiple of 128 (M = 8192, profiles/r6_gemm_routing.md: o 0.0577
+    ms, qkv 0.0786, down 0.297 vs 0.315 for hipBLASLt, gate_up 0.543, lm_head 2.95 vs 3.09); 7 = 256 x 256 tiles with
+    64-deep stages for the fused SwiGLU-backward epilogue (0.425 vs 0.483 ms for the 4-wave kernel's register
+    epilogue) and K % 128 != 0; 5 = the 32-deep three-stage ring for K % 64 != 0."""
     K = dy2d.shape[1]
     if not swiglu and K % 128 == 0:
-        # the 4-slot ring with interleaved issue on every reduction length now (o 0.0577 vs 0.0604 ms for the pair
-        # loop cfg 12, qkv 0.0786 vs 0.0800; profiles/r6_gemm_routing.md)
-        return _G4_RING
+        return 14
     return 7 if K % 64 == 0 else 5
 
 
@@ -270,7 +249,7 @@ def dgrad_mm(dy2d: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
     are not a multiple of 128 of at most 4096 output features into at most 4096 inputs on cfg 7 / 5."""
     if _dgrad_ok(dy2d, w):
         cfg = _dgrad_cfg(dy2d)
-        if cfg in (12, 13, 14) or _DGRAD_MODE == "hip" or (dy2d.shape[1] <= 4096 and w.shape[1] <= 4096):
+        if cfg == 14 or _DGRAD_MODE == "hip" or (dy2d.shape[1] <= 4096 and w.shape[1] <= 4096):
             return _ext.ops().dgrad_gemm(dy2d, w, None, cfg)
     return torch.mm(dy2d, w)
 

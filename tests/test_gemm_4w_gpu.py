@@ -1,6 +1,7 @@
-"""4-wave backward GEMMs (csrc/gemm_4w.hip, wgrad_gemm / dgrad_gemm cfg 12) against plain PyTorch fp32 references:
-weight gradients with and without accumulation, split-K / hybrid pieces, gradient-norm slots; input gradients plain,
-with the fused SwiGLU backward, on column-sliced weights and through the wave-tail split."""
+"""4-wave backward GEMMs (csrc/gemm_4w.hip: the 4-slot ring with one read / DMA piece per MFMA gap, wgrad_gemm /
+dgrad_gemm cfg 14) against plain PyTorch fp32 references: weight gradients with and without accumulation, split-K /
+hybrid pieces, gradient-norm slots, a padded x pitch; input gradients plain, on column-sliced weights, through the
+wave-tail split and the hybrid split-K."""
 import pytest
 import torch
 
@@ -21,16 +22,11 @@ def rel_err(a, b):
     return ((a - b).norm() / b.norm().clamp_min(1e-30)).item()
 
 
-@pytest.mark.parametrize("cfg,T,N,K", [(12, 128, 256, 256), (12, 256, 512, 768), (12, 384, 768, 512),
-                                       (12, 1024, 2304, 4352),     # 153 tiles, 8 K-tiles
-                                       (212, 512, 512, 512), (412, 1024, 256, 256), (312, 384, 512, 256),
-                                       (1312, 256, 4096, 4352),    # hybrid: 256 whole tiles + 16 split 3 ways
-                                       (1212, 384, 4352, 4096),
-                                       # cfg 13: the 4-slot ring of 32-deep steps
-                                       (13, 128, 256, 256), (13, 384, 768, 512), (13, 1024, 2304, 4352),
-                                       (213, 512, 512, 512), (313, 384, 512, 256), (1313, 256, 4096, 4352),
-                                       # cfg 14: the same ring with one read / DMA piece per MFMA gap
-                                       (14, 128, 256, 256), (14, 1024, 2304, 4352), (1314, 256, 4096, 4352)])
+@pytest.mark.parametrize("cfg,T,N,K", [(14, 128, 256, 256), (14, 256, 512, 768), (14, 384, 768, 512),
+                                       (14, 1024, 2304, 4352),     # 153 tiles, 8 blocks of 128 tokens
+                                       (214, 512, 512, 512), (414, 1024, 256, 256), (314, 384, 512, 256),
+                                       (1314, 256, 4096, 4352),    # hybrid: 256 whole tiles + 16 split 2 ways
+                                       (1214, 384, 4352, 4096)])
 @pytest.mark.parametrize("accumulate", [False, True])
 def test_wgrad_4wave(cfg, T, N, K, accumulate):
     torch.manual_seed(0)
@@ -45,7 +41,7 @@ def test_wgrad_4wave(cfg, T, N, K, accumulate):
     assert err <= 0.02 * want.abs().max().item(), err
 
 
-@pytest.mark.parametrize("cfg", [12, 13, 14])
+@pytest.mark.parametrize("cfg", [14, 214])
 def test_wgrad_4wave_exact_structure(cfg):
     """Integer-valued operands (exact in fp32): a permuted token, row or column mapping anywhere in the staging,
     the transposed reads or the register epilogue changes the result bit for bit."""
@@ -58,9 +54,8 @@ def test_wgrad_4wave_exact_structure(cfg):
     assert torch.equal(out, (dy.float().t() @ x.float()).to(torch.bfloat16))  # exact fp32 sums, one rounding
 
 
-@pytest.mark.parametrize("cfg,T,N,K", [(12, 256, 512, 768), (212, 512, 512, 512), (1312, 256, 4096, 4352),
-                                       (13, 256, 512, 768), (1313, 256, 4096, 4352), (1213, 1024, 2048, 11008),
-                                       (1214, 1024, 2048, 11008)])
+@pytest.mark.parametrize("cfg,T,N,K", [(14, 256, 512, 768), (214, 512, 512, 512), (1314, 256, 4096, 4352),
+                                       (1214, 1024, 2048, 11008), (414, 1024, 2048, 2048), (214, 1024, 3072, 2048)])
 @pytest.mark.parametrize("accumulate", [False, True])
 def test_wgrad_4wave_norm_slots(cfg, T, N, K, accumulate):
     """Norm partials (register epilogue / split-K fixup) sum to the squared norm of the stored bf16 gradient
@@ -81,24 +76,25 @@ def test_wgrad_4wave_norm_slots(cfg, T, N, K, accumulate):
     assert torch.all(slots[cap:] == 7.0)
 
 
-def test_wgrad_4wave_matches_ring_split_exactly():
-    """Split pieces are whole pairs of 64-token K-tiles summed in a fixed order: repeated launches are bitwise
-    identical (deterministic), and the result matches the fp32 reference."""
+@pytest.mark.parametrize("cfg", [414, 1214])
+def test_wgrad_4wave_matches_ring_split_exactly(cfg):
+    """Split pieces (414: 4 equal token ranges per tile; 1214: the hybrid split) are whole 128-token blocks summed in a
+    fixed order: repeated launches are bitwise identical (deterministic), and the result matches the fp32 reference."""
     torch.manual_seed(3)
     T, N, K = 1024, 512, 768
     dy = torch.randn(T, N, device=DEV, dtype=torch.bfloat16)
     x = torch.randn(T, K, device=DEV, dtype=torch.bfloat16)
     o1 = torch.empty(N, K, device=DEV, dtype=torch.bfloat16)
     o2 = torch.empty_like(o1)
-    _ext.ops().wgrad_gemm(o1, dy, x, False, 412)
-    _ext.ops().wgrad_gemm(o2, dy, x, False, 412)
+    _ext.ops().wgrad_gemm(o1, dy, x, False, cfg)
+    _ext.ops().wgrad_gemm(o2, dy, x, False, cfg)
     assert torch.equal(o1, o2)
     assert rel_err(o1, dy.float().t() @ x.float()) < 5e-3
 
 
 @pytest.mark.parametrize("M,K,N,wpad", [(256, 128, 256, 0), (512, 2048, 768, 0), (256, 384, 512, 64),
                                         (768, 1024, 256, 0), (2048, 11008, 2048, 0)])
-@pytest.mark.parametrize("cfg", [12, 13, 14])
+@pytest.mark.parametrize("cfg", [14])
 def test_dgrad_4wave_plain(M, K, N, wpad, cfg):
     torch.manual_seed(0)
     dy = torch.randn(M, K, device=DEV, dtype=torch.bfloat16)
@@ -115,27 +111,21 @@ def test_dgrad_4wave_plain(M, K, N, wpad, cfg):
     assert torch.equal(got, ramp.float() @ eye)
 
 
-@pytest.mark.parametrize("M,K,N", [(256, 256, 256), (512, 2048, 512), (1024, 128, 768)])
-@pytest.mark.parametrize("cfg", [12, 13, 14])
-def test_dgrad_4wave_swiglu_bwd(M, K, N, cfg):
-    torch.manual_seed(1)
-    dy = torch.randn(M, K, device=DEV, dtype=torch.bfloat16)
-    w = (0.05 * torch.randn(K, N, device=DEV)).to(torch.bfloat16)
-    gu = torch.randn(M, 2 * N, device=DEV, dtype=torch.bfloat16)
-    dgu = _ext.ops().dgrad_gemm(dy, w, gu, cfg)
-    dact = dy.float() @ w.float()
-    g, u = gu.float().chunk(2, dim=-1)
-    s = torch.sigmoid(g)
-    want = torch.cat([dact * u * s * (1 + g * (1 - s)), dact * g * s], dim=-1)
-    assert dgu.shape == (M, 2 * N)
-    assert rel_err(dgu, want) < 1e-2
+def test_dgrad_4wave_refuses_the_swiglu_epilogue():
+    """The SwiGLU-backward epilogue runs on cfg 7 (its LDS-staged epilogue: 0.425 vs 0.483 ms for the 4-wave kernel's
+    register epilogue, profiles/r6_gemm_routing.md); the 4-wave kernel refuses it instead of computing a plain dX."""
+    dy = torch.randn(256, 256, device=DEV, dtype=torch.bfloat16)
+    w = torch.randn(256, 256, device=DEV, dtype=torch.bfloat16)
+    gu = torch.randn(256, 512, device=DEV, dtype=torch.bfloat16)
+    with pytest.raises(RuntimeError):
+        _ext.ops().dgrad_gemm(dy, w, gu, 14)
 
 
-@pytest.mark.parametrize("cfg", [12, 13, 14])
-@pytest.mark.parametrize("swiglu", [True, False])
+@pytest.mark.parametrize("cfg,swiglu", [(14, False), (7, True), (7, False)])
 def test_dgrad_4wave_wave_tail(swiglu, cfg, monkeypatch):
-    """SmolLM3 down projection grid (43 x 32 tiles = 5.375 rounds): the whole rounds on the 4-wave kernel + the
-    leftover columns as 256 x 128 half tiles of the ring kernel (SFTAMD_DGRAD_TAIL=2) == the fp32 reference."""
+    """SmolLM3 down projection grid (43 x 32 tiles = 5.375 rounds): the whole rounds on the 4-wave kernel (or cfg 7
+    with the SwiGLU backward) + the leftover columns as 256 x 128 half tiles of the ring kernel (SFTAMD_DGRAD_TAIL=2)
+    == the fp32 reference."""
     torch.manual_seed(2)
     M, K, N = 8192, 128, 11008
     dy = torch.randn(M, K, device=DEV, dtype=torch.bfloat16)
@@ -154,7 +144,7 @@ def test_dgrad_4wave_wave_tail(swiglu, cfg, monkeypatch):
         assert rel_err(got, want) < 1e-2, tail
 
 
-@pytest.mark.parametrize("cfg", [12, 13, 14])
+@pytest.mark.parametrize("cfg", [14])
 @pytest.mark.parametrize("M,K,N", [(10240, 1024, 2048), (2560, 4096, 2048), (4352, 512, 4096)])
 def test_dgrad_4wave_hybrid_splitk(M, K, N, cfg):
     """Grids that are not whole rounds of 256 workgroups (the recipe's padding-free M = 10240: 320 tiles) run the
@@ -172,7 +162,7 @@ def test_dgrad_4wave_hybrid_splitk(M, K, N, cfg):
     assert torch.equal(got, (ramp.float() @ wi.float()).to(torch.bfloat16))
 
 
-@pytest.mark.parametrize("cfg,T,N,K", [(13, 512, 22016 // 86 * 2, 2048), (13, 1024, 512, 768), (1213, 1024, 2048, 11008 // 256 * 256)])
+@pytest.mark.parametrize("cfg,T,N,K", [(14, 512, 22016 // 86 * 2, 2048), (14, 1024, 512, 768), (1214, 1024, 2048, 11008 // 256 * 256)])
 def test_wgrad_4wave_padded_x_pitch(cfg, T, N, K):
     """x [T, K] as a view into a wider buffer (padded row pitch, e.g. the gate_up input written by the norm with
     y_ld): bitwise the same dW (and norm slots) as from a contiguous x."""
@@ -187,25 +177,3 @@ def test_wgrad_4wave_padded_x_pitch(cfg, T, N, K):
     _ext.ops().wgrad_gemm(o1, dy, x, False, cfg, s1)
     _ext.ops().wgrad_gemm(o2, dy, buf[:, :K], False, cfg, s2)
     assert torch.equal(o1, o2) and torch.equal(s1, s2)
-
-
-@pytest.mark.parametrize("kind", ["wgrad", "dgrad"])
-def test_4wave_interleaved_ring_is_bitwise_the_ring(kind):
-    """cfg 14 issues the same fragment reads, DMA pieces and MFMAs as cfg 13 in another order (one read / piece per
-    MFMA gap): every accumulator sees the same MFMA sequence, so the outputs are bitwise equal."""
-    torch.manual_seed(5)
-    if kind == "wgrad":
-        T, N, K = 1024, 768, 1024
-        dy = torch.randn(T, N, device=DEV, dtype=torch.bfloat16)
-        x = torch.randn(T, K, device=DEV, dtype=torch.bfloat16)
-        o13 = torch.empty(N, K, device=DEV, dtype=torch.bfloat16)
-        o14 = torch.empty_like(o13)
-        _ext.ops().wgrad_gemm(o13, dy, x, False, 13)
-        _ext.ops().wgrad_gemm(o14, dy, x, False, 14)
-    else:
-        M, K, N = 1024, 4608, 768
-        dy = torch.randn(M, K, device=DEV, dtype=torch.bfloat16)
-        w = (0.02 * torch.randn(K, N, device=DEV)).to(torch.bfloat16)
-        o13 = _ext.ops().dgrad_gemm(dy, w, None, 13)
-        o14 = _ext.ops().dgrad_gemm(dy, w, None, 14)
-    assert torch.equal(o13, o14)

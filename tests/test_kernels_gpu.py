@@ -395,9 +395,7 @@ def test_decode_attention(L):
     assert rel_err(out, ref_o) < 1e-2
 
 
-@pytest.mark.parametrize("cfg,T,N,K", [(1, 256, 512, 512), (2, 192, 512, 256), (0, 128, 256, 384), (1, 64, 256, 256),
-                                       (3, 256, 512, 512), (4, 192, 512, 256), (7, 352, 512, 512), (7, 96, 256, 256),
-                                       (8, 256, 512, 768), (9, 416, 512, 384), (9, 32, 256, 128), (10, 352, 512, 512), (11, 96, 256, 384),
+@pytest.mark.parametrize("cfg,T,N,K", [(9, 416, 512, 384), (9, 32, 256, 128), (10, 352, 512, 512), (10, 96, 256, 256),
                                        # split-K ring (cfg = 100 * splits + variant): fp32 slabs + ordered reduce
                                        (210, 512, 512, 512), (410, 1024, 256, 256), (309, 384, 512, 384),
                                        (209, 64, 256, 128), (310, 320, 256, 256),
@@ -433,30 +431,8 @@ def test_wgrad_gemm_norm_slots(cfg, T, N, K, accumulate):
     want = out.float().pow(2).sum().item()
     assert abs(slots[:cap].sum().item() - want) <= 1e-4 * want
     assert torch.all(slots[cap:] == 7.0)
-    with pytest.raises(RuntimeError):  # the non-ring variants have no norm epilogue
+    with pytest.raises(RuntimeError):  # configurations that are not built are refused
         _ext.ops().wgrad_gemm(out, dy, x, accumulate, 1, slots[:cap])
-
-
-@pytest.mark.parametrize("cfg,N,K", [(10, 4352, 4096), (9, 4352, 2048)])
-@pytest.mark.parametrize("accumulate", [False, True])
-def test_wgrad_gemm_tail_stream(cfg, N, K, accumulate):
-    """A grid with a partial last round (272 tiles) split into the whole round on the current stream and the
-    leftover tiles on a side stream == one launch, bit for bit, including the gradient-norm slots."""
-    torch.manual_seed(4)
-    T = 256
-    dy = torch.randn(T, N, device="cuda", dtype=torch.bfloat16)
-    x = torch.randn(T, K, device="cuda", dtype=torch.bfloat16)
-    base = torch.randn(N, K, device="cuda", dtype=torch.bfloat16)
-    cap = -(-N // 256) * -(-K // 128) * 32
-    o1, o2 = base.clone(), base.clone()
-    n1, n2 = torch.zeros(cap, device="cuda"), torch.zeros(cap, device="cuda")
-    _ext.ops().wgrad_gemm(o1, dy, x, accumulate, cfg, n1)
-    side = torch.cuda.Stream()
-    side.wait_stream(torch.cuda.current_stream())
-    _ext.ops().wgrad_gemm(o2, dy, x, accumulate, cfg, n2, side.cuda_stream)
-    torch.cuda.current_stream().wait_stream(side)
-    assert torch.equal(o1, o2)
-    assert torch.equal(n1, n2)
 
 
 def test_sumsq_chunks():
@@ -596,7 +572,7 @@ def test_lora_dxa_blocks_vs_fp32(T, blocks, r):
     assert rel_err(got, want) < 5e-3 and _elem_ok(got, want)
 
 
-@pytest.mark.parametrize("cfg", [0, 2, 5, 6, 11])
+@pytest.mark.parametrize("cfg", [0, 2, 5, 11])
 @pytest.mark.parametrize("M,N,K", [(256, 256, 64), (512, 512, 128), (256, 512, 192), (512, 768, 256), (768, 512, 2112),
                                    (2048, 3072, 320)])
 def test_gemm_tn_plain(cfg, M, N, K):
@@ -605,39 +581,6 @@ def test_gemm_tn_plain(cfg, M, N, K):
     w = torch.randn(N, K, device=DEV, dtype=torch.bfloat16)
     c = _ext.ops().gemm_tn(x, w, cfg)
     assert rel_err(c, x.float() @ w.float().t()) < 5e-3
-
-
-@pytest.mark.parametrize("M,N,K", [(256, 256, 128), (512, 512, 256), (768, 512, 2176), (2048, 3072, 384),
-                                   (512, 1280, 11008), (4096, 4352, 256), (2304, 7424, 128)])
-def test_gemm_tn_4wave(M, N, K):
-    """cfg 12: 4 waves of 128 x 128 (accumulators pinned in AGPRs by inline-asm MFMAs) and cfg 164, its persistent
-    version (tiles > 256 walk several per workgroup; K = 128 is its single-pair path), vs the fp32 reference, plus the
-    fused SwiGLU / RoPE epilogues of both against their unfused twins."""
-    torch.manual_seed(0)
-    x = torch.randn(M, K, device=DEV, dtype=torch.bfloat16)
-    w = torch.randn(N, K, device=DEV, dtype=torch.bfloat16)
-    ref32 = x.float() @ w.float().t()
-    for cfg in (12, 164):
-        c = _ext.ops().gemm_tn(x, w, cfg)
-        assert rel_err(c, ref32) < 5e-3, cfg
-    gu_ref = x.float() @ (w * 0.1).float().t()
-    for cfg in (12, 164):
-        gu, act = _ext.ops().gemm_tn_swiglu(x, w * 0.1, cfg)
-        assert rel_err(gu, gu_ref) < 5e-3, cfg
-        assert rel_err(act, _ext.ops().swiglu_fwd(gu)) < 2e-3, cfg
-    if N % 128 == 0 and N >= 512:
-        D, nkv = 128, 1
-        nq = N // D - 2 * nkv
-        pos = torch.arange(M, device=DEV).float()
-        inv = 1.0 / (10000 ** (torch.arange(0, D, 2, device=DEV).float() / D))
-        fr = pos[:, None] * inv[None, :]
-        cs, sn = fr.cos().contiguous(), fr.sin().contiguous()
-        y = (x.float() @ w.float().t()).to(torch.bfloat16)
-        qk = y[:, :(nq + nkv) * D].view(M, nq + nkv, D)
-        exp = torch.cat([ref.apply_rope(qk, cs, sn).reshape(M, -1), y[:, (nq + nkv) * D:]], dim=1)
-        for cfg in (12, 164):
-            out = _ext.ops().gemm_tn_rope(x, w, cs, sn, (nq + nkv) * D, cfg)
-            assert rel_err(out, exp) < 1e-2, cfg
 
 
 def _elem_ok(out, exp, tol=1e-2):
@@ -704,7 +647,7 @@ def test_gemm_tn_swiglu(I, K, cfg):
     assert rel_err(act, _ext.ops().swiglu_fwd(gu)) < 2e-3
 
 
-@pytest.mark.parametrize("cfg", [0, 2, 5, 6, 11])
+@pytest.mark.parametrize("cfg", [0, 2, 5, 11])
 def test_gemm_tn_rope(cfg):
     torch.manual_seed(0)
     M, K, nq, nkv, D = 512, 256, 2, 1, 128
@@ -750,7 +693,7 @@ def test_dgrad_gemm_plain(M, K, N, wpad):
     dy = torch.randn(M, K, device="cuda", dtype=torch.bfloat16)
     wfull = torch.randn(K, N + wpad, device="cuda", dtype=torch.bfloat16)
     w = wfull[:, :N]
-    for cfg in (0, 1, 2, 3, 5, 7, 8) if K % 64 == 0 else (0, 1, 2, 3, 5, 8):
+    for cfg in (2, 5, 7) if K % 64 == 0 else (2, 5):
         out = _ext.ops().dgrad_gemm(dy, w, None, cfg)
         want = dy.float() @ w.float()
         assert out.shape == (M, N)
@@ -759,7 +702,7 @@ def test_dgrad_gemm_plain(M, K, N, wpad):
     eye = torch.zeros(K, N, device="cuda")
     eye[torch.arange(min(K, N)), (torch.arange(min(K, N)) + 5) % N] = 1.0
     ramp = (torch.arange(M * K, device="cuda") % 251).float().view(M, K).to(torch.bfloat16)
-    for cfg in (0, 7) if K % 64 == 0 else (0,):
+    for cfg in (5, 7) if K % 64 == 0 else (5,):
         got = _ext.ops().dgrad_gemm(ramp, eye.to(torch.bfloat16), None, cfg).float()
         assert torch.equal(got, ramp.float() @ eye), cfg
 
@@ -774,11 +717,11 @@ def test_dgrad_gemm_wave_tail_split(M, K, N, swiglu, monkeypatch):
     w = (0.05 * torch.randn(K, N, device="cuda")).to(torch.bfloat16)
     gu = torch.randn(M, 2 * N, device="cuda", dtype=torch.bfloat16) if swiglu else None
     res = {}
-    for cfg in (0, 7) if K % 64 == 0 else (0,):
-        for tail in ("0", "2", "3"):
+    for cfg in (5, 7) if K % 64 == 0 else (5,):
+        for tail in ("0", "2"):
             monkeypatch.setenv("SFTAMD_DGRAD_TAIL", tail)
             res[tail] = _ext.ops().dgrad_gemm(dy, w, gu, cfg)
-        assert torch.equal(res["0"], res["2"]) and torch.equal(res["0"], res["3"]), cfg
+        assert torch.equal(res["0"], res["2"]), cfg
     dact = dy.float() @ w.float()
     if swiglu:
         g, u = gu.float().chunk(2, dim=-1)
@@ -796,10 +739,10 @@ def test_dgrad_gemm_swiglu_bwd(M, K, N):
     dy = torch.randn(M, K, device="cuda", dtype=torch.bfloat16)
     w = (0.05 * torch.randn(K, N, device="cuda")).to(torch.bfloat16)
     gu = torch.randn(M, 2 * N, device="cuda", dtype=torch.bfloat16)
-    dgu = _ext.ops().dgrad_gemm(dy, w, gu, 0)
+    dgu = _ext.ops().dgrad_gemm(dy, w, gu, 5)
     assert torch.equal(_ext.ops().dgrad_gemm(dy, w, gu, 2), dgu)  # 256 x 128 tiles: same fp32 sums per element
-    assert torch.equal(_ext.ops().dgrad_gemm(dy, w, gu, 7), dgu)  # BK 64: same k order within each 32-deep MFMA
-    assert torch.equal(_ext.ops().dgrad_gemm(dy, w, gu, 8), dgu)  # 4-wave 256 x 128, two workgroups per CU
+    if K % 64 == 0:
+        assert torch.equal(_ext.ops().dgrad_gemm(dy, w, gu, 7), dgu)  # BK 64: same k order within each 32-deep MFMA
     dact = dy.float() @ w.float()
     g, u = gu.float().chunk(2, dim=-1)
     s = torch.sigmoid(g)

@@ -173,18 +173,50 @@ def test_lora_trainer_updates_reach_the_wide_weight(tmp_path):
 
 
 def test_prewidened_view_detection(monkeypatch):
-    """_prewidened (the in-place LoRA widening): only the left [T, K] block of a row-contiguous [T, ldX] buffer
-    whose rows lie wholly inside the storage is taken as X'; contiguous inputs, other strides and short storages
-    are not."""
+    """_prewidened (the in-place LoRA widening): only a norm output add_rms_norm marked as the left [T, K] block of its
+    own [T, ldX] buffer (``_sftamd_wide_ld``), at a shape the widening kernel takes (K % 256, R a multiple of 16 in
+    16..64), is taken as X'. An unmarked view with the same strides (e.g. a column slice of someone else's
+    activation), an unsupported rank (qkv r = 8: R = 24; r = 32: R = 96), other widths, short storages and non-bf16
+    inputs are not."""
     import llm_fine_tune_distributed_amd.ops.fused as F
     monkeypatch.setattr(F._ext, "use_hip", lambda t: True)
-    T, K, ldX = 6, 16, 24
+    T, K, ldX = 6, 256, 384
+    acat = torch.zeros(48, K, dtype=torch.bfloat16)
     buf = torch.zeros(T, ldX, dtype=torch.bfloat16)
-    X = F._prewidened(buf[:, :K], ldX)
+    x = buf[:, :K]
+    assert F._prewidened(x, x, ldX, acat) is None  # not marked by the norm
+    x._sftamd_wide_ld = ldX
+    X = F._prewidened(x, x, ldX, acat)
     assert X is not None and X.shape == (T, ldX) and X.data_ptr() == buf.data_ptr() and X.stride() == (ldX, 1)
     X[:, K:] = 1  # the view covers the buffer's adapter / padding columns
     assert (buf[:, K:] == 1).all()
-    assert F._prewidened(torch.zeros(T, K, dtype=torch.bfloat16), ldX) is None            # contiguous [T, K]
-    assert F._prewidened(buf[:, :K], ldX + 8) is None                                     # another width
-    assert F._prewidened(torch.zeros(T * ldX - 8, dtype=torch.bfloat16).as_strided((T, K), (ldX, 1)), ldX) is None
-    assert F._prewidened(buf[:, :K].float(), ldX) is None                                 # not bf16
+    for R in (24, 96, 8):
+        assert F._prewidened(x, x, ldX, torch.zeros(R, K, dtype=torch.bfloat16)) is None, R
+    assert F._prewidened(x, x, ldX + 8, acat) is None                                    # another width
+    c = torch.zeros(T, K, dtype=torch.bfloat16)
+    c._sftamd_wide_ld = ldX
+    assert F._prewidened(c, c, ldX, acat) is None                                        # contiguous [T, K]
+    short = torch.zeros(T * ldX - 8, dtype=torch.bfloat16).as_strided((T, K), (ldX, 1))
+    short._sftamd_wide_ld = ldX
+    assert F._prewidened(short, short, ldX, acat) is None                                # rows past the storage
+    xf = buf[:, :K].float()
+    xf._sftamd_wide_ld = ldX
+    assert F._prewidened(xf, xf, ldX, acat) is None                                      # not bf16
+
+
+def test_wide_ld_only_for_supported_ranks():
+    """The norm writes into the consumer's widened buffer only where the widening kernel takes the shape: qkv with
+    r = 8 (R = 24) or r = 32 (R = 96) gets a plain y (the copying widening runs instead of failing)."""
+    import llm_fine_tune_distributed_amd.models.transformer as TR
+    from llm_fine_tune_distributed_amd.models import build_model, tiny
+    from llm_fine_tune_distributed_amd.models.lora import LoRAConfig, apply_lora
+    for r, want in ((16, True), (8, False), (32, False)):
+        cfg = tiny(hidden_size=256, num_attention_heads=2, num_key_value_heads=1, head_dim=128, intermediate_size=512,
+                   vocab_size=512, num_hidden_layers=1)
+        m = build_model(cfg, dtype=torch.float32, seed=0)
+        apply_lora(m, LoRAConfig(r=r, lora_alpha=8))
+        at = m.model.layers[0].self_attn
+        fl = at.lora["qkv"]
+        if getattr(fl, "wide", None) is None:
+            continue  # no wide weight on this path: nothing is widened in place
+        assert (TR._wide_ld(at.lora, "qkv", at.qkv_proj) > 0) == want, r

@@ -16,7 +16,7 @@ from llm_fine_tune_distributed_amd.ops import _ext  # noqa: E402
 from llm_fine_tune_distributed_amd.utils.gemm_tuning import enable_tuned_gemms  # noqa: E402
 
 
-CFGS = [int(c) for c in os.environ.get("DGRAD_CFGS", "7,12").split(",")]
+CFGS = [int(c) for c in os.environ.get("DGRAD_CFGS", "7,14").split(",")]
 
 
 def timeit(fn, iters=20):

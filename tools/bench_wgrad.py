@@ -31,7 +31,7 @@ def timeit(fn, iters=20):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--tokens", type=int, default=8192)
-    ap.add_argument("--cfgs", default="1,2,3,4")
+    ap.add_argument("--cfgs", default="14,1214,10")
     ap.add_argument("--only", default="")
     ap.add_argument("--no-blas", action="store_true")
     a = ap.parse_args()
