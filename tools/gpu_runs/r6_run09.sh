@@ -5,6 +5,7 @@ set -o pipefail
 cd $GRAFT_REPO_ROOT
 mkdir -p gpurun_out
 export TMPDIR=/tmp
+timeout -k 10 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_default_path_gpu.py > gpurun_out/r6_09_dp.log 2>&1 || { tail -40 gpurun_out/r6_09_dp.log; exit 1; }
 timeout -k 10 900 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests -m gpu > gpurun_out/r6_09_tests.log 2>&1 || { tail -40 gpurun_out/r6_09_tests.log; exit 1; }
 tail -2 gpurun_out/r6_09_tests.log
 for i in 1 2; do
