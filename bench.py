@@ -60,7 +60,11 @@ def parse(argv=None):
     # token count either way); --micro-batch 8 --ga 2 reproduces the reference split.
     ap.add_argument("--micro-batch", type=int, default=16)
     ap.add_argument("--ga", type=int, default=1)
-    ap.add_argument("--no-overlap", action="store_true", help="disable AdamW/forward overlap")
+    ap.add_argument("--overlap", default="auto", choices=["auto", "on", "off"],
+                    help="AdamW / ZeRO-1 gathers under the next forward on a side stream: auto = on for N > 1 (hides "
+                         "the parameter all-gathers), off for one GPU (the overlapped update slowed the step by 1 %%: "
+                         "112.7 / 112.5 vs 113.8 / 113.6 samples/s, profiles/r6_adamw_overlap.md)")
+    ap.add_argument("--no-overlap", action="store_true", help="= --overlap off")
     ap.add_argument("--ga-merge-max-tokens", type=int, default=None,
                     help="run the GA micro-batches of a step as one pass up to this many tokens (SFTConfig default "
                          "32768); 0 = one fwd/bwd pass per micro-batch")
@@ -220,7 +224,7 @@ def run(a):
                      bf16=True, gradient_checkpointing=False, max_length=a.seq, packing=a.packing,
                      padding_free={"auto": None, "on": True, "off": False}[a.padding_free],
                      ddp_bucket_cap_mb=a.bucket_mb or None, dataloader_drop_last=True, jsonl_log=False,
-                     logging_steps=0, optimizer_overlap=not a.no_overlap, freeze_policy=a.freeze_policy,
+                     logging_steps=0, optimizer_overlap=_overlap_arg(a), freeze_policy=a.freeze_policy,
                      master_weights=a.master_weights, optim_state_dtype=a.optim_state,
                      shard_optimizer_state=bool(a.zero), gemm_tuning=False,
                      **({} if a.ga_merge_max_tokens is None else {"ga_merge_max_tokens": a.ga_merge_max_tokens}))
@@ -417,7 +421,7 @@ def run_recipe(a):
                      logging_first_step=True, eval_strategy="steps", eval_steps=a.eval_steps, save_strategy="no",
                      bf16=True, gradient_checkpointing=False, max_length=1024, dataloader_drop_last=True,
                      jsonl_log=False, freeze_policy=a.freeze_policy, shard_optimizer_state=bool(a.zero),
-                     dataset_cache=False, gemm_tuning=False, optimizer_overlap=not a.no_overlap,
+                     dataset_cache=False, gemm_tuning=False, optimizer_overlap=_overlap_arg(a),
                      padding_free={"auto": None, "on": True, "off": False}[a.padding_free],
                      **({} if a.ga_merge_max_tokens is None else {"ga_merge_max_tokens": a.ga_merge_max_tokens}))
     trainer = SFTTrainer(model=model, args=args, train_dataset=train_rows, eval_dataset=val_rows,
@@ -451,6 +455,13 @@ def run_recipe(a):
         }
         print(json.dumps(rec), flush=True)
     cleanup_distributed()
+
+
+def _overlap_arg(a):
+    """SFTConfig.optimizer_overlap from --overlap / --no-overlap."""
+    if a.no_overlap:
+        return False
+    return {"auto": "auto", "on": True, "off": False}[a.overlap]
 
 
 def _sum_key(x: float):

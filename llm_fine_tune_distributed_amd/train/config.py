@@ -119,7 +119,10 @@ class SFTConfig:
     eval_accumulation: bool = True
     jsonl_log: bool = True
     prefetch_batches: int = 2
-    optimizer_overlap: bool = True          # pipeline AdamW under the next forward (side HIP stream)
+    # pipeline AdamW (and ZeRO-1's parameter all-gathers) under the next forward on a side HIP stream: "auto" = on
+    # when world_size > 1 (hides the gathers), off on one GPU, where the overlapped update slowed the step by 1 %
+    # (profiles/r6_adamw_overlap.md); True / False force it
+    optimizer_overlap: Union[bool, str] = "auto"
     gemm_tuning: bool = True                # load shipped hipBLASLt/rocBLAS selections (utils/gemm_tuning.py)
     # GA micro-batch merging (MI355X-first): gradient accumulation exists to fit a per-device batch into
     # memory; when the step's GA micro-batches together hold at most this many tokens (288 GB of HBM holds
@@ -197,6 +200,8 @@ def _coerce(field_type, raw: str):
             return True
         if low in ("0", "false", "no", "off"):
             return False
+        if "str" in t:  # Union[bool, str] (optimizer_overlap "auto", dataset_cache path)
+            return raw
         raise ValueError(f"not a boolean: {raw!r}")
     if "List" in t or "Dict" in t:
         return json.loads(raw)

@@ -148,7 +148,10 @@ class SFTTrainer:
                                    master_weights=args.master_weights,
                                    stochastic_rounding=args.stochastic_rounding,
                                    state_dtype=args.optim_state_dtype)
-        if args.optimizer_overlap and dev.type == "cuda":
+        overlap = args.optimizer_overlap
+        if overlap == "auto":
+            overlap = self.dist.world_size > 1
+        if overlap and dev.type == "cuda":
             self.optimizer.enable_overlap(model)
         self.scheduler: Optional[LRScheduler] = None
         # ------------------------------------------------------------ callbacks / state
