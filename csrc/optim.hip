@@ -99,8 +99,13 @@ __device__ __forceinline__ void adam_elem(float& w, float g, float& m, float& v,
   w = w * (1.f - lr * wd) - lr * rbc1 * m / denom;
 }
 
-// Stateless per-element hash (Wang/PCG-style mix) for stochastic rounding.
-__device__ __forceinline__ unsigned sr_hash(unsigned long long i, unsigned seed) { return hash_u32(i, seed); }
+// Stochastic-rounding noise of element i: 16 bits of the stateless hash of its PAIR (elements 2q, 2q + 1 share
+// hash(q, seed): low / high half), half the hashing of one hash per element — the bf16-moment update was VALU-bound on
+// its three roundings per element (nt streams: 734 us with one hash per element vs 660 us round-to-nearest per 256 M
+// elements, profiles/r6_adamw_overlap.md). Twin: ops/reference.py bf16_stochastic_round.
+__device__ __forceinline__ unsigned sr_hash(unsigned long long i, unsigned seed) {
+  return hash_u32(i >> 1, seed) >> (16 * (unsigned)(i & 1));
+}
 
 // fp32 -> bf16 with stochastic rounding: add uniform noise below the bf16 ulp, then truncate.
 // E[bf16(w)] = w, so pure-bf16 weights do not lose small Adam updates to round-to-nearest.
@@ -111,10 +116,21 @@ __device__ __forceinline__ u16 f2bf_sr(float f, unsigned r) {
   return (u16)(u >> 16);
 }
 
+// 8 consecutive elements idx .. idx + 7: 4 pair hashes (5 when idx is odd: the pairs straddle the vector)
 __device__ __forceinline__ uint4 pack8_sr(const float* f, unsigned long long idx, unsigned seed) {
+  const unsigned long long q = idx >> 1;
+  const bool odd = idx & 1;
+  unsigned h[5];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) h[k] = hash_u32(q + k, seed);
+  h[4] = odd ? hash_u32(q + 4, seed) : 0u;
   u16 b[8];
 #pragma unroll
-  for (int i = 0; i < 8; ++i) b[i] = f2bf_sr(f[i], sr_hash(idx + i, seed));
+  for (int i = 0; i < 8; ++i) {
+    const unsigned r0 = (i & 1) ? (h[i >> 1] >> 16) : h[i >> 1];              // element idx + i, idx even
+    const unsigned r1 = (i & 1) ? h[(i + 1) >> 1] : (h[(i + 1) >> 1] >> 16);  // idx odd: pair of idx + i shifted
+    b[i] = f2bf_sr(f[i], odd ? r1 : r0);
+  }
   return make_uint4(b[0] | (b[1] << 16), b[2] | (b[3] << 16), b[4] | (b[5] << 16), b[6] | (b[7] << 16));
 }
 
@@ -156,7 +172,29 @@ constexpr unsigned SEED_M = 0x68E31DA4u, SEED_V = 0xB5297A4Du;
 
 // UNR vectors of 8 elements per thread per grid-stride step, all loads issued before any math: the update
 // streams 22 (fp32 moments) or 14 (bf16) bytes per parameter, so bytes in flight per wave set its speed.
-template <bool MASTER, bool SR, bool BF16M, int UNR>
+// Streams touched once per update: nontemporal loads / stores (720 vs 760 us per 256 M elements with bf16 moments +
+// SR, 1127 vs 1154 with fp32 moments; profiles/r6_adamw_overlap.md)
+typedef unsigned __attribute__((ext_vector_type(4))) u32v4;
+template <bool NT>
+__device__ __forceinline__ uint4 ld16(const void* p) {
+  if constexpr (NT) {
+    const u32v4 v = __builtin_nontemporal_load((const u32v4*)p);
+    return make_uint4(v.x, v.y, v.z, v.w);
+  } else {
+    return *(const uint4*)p;
+  }
+}
+template <bool NT>
+__device__ __forceinline__ void st16(void* p, const uint4& x) {
+  if constexpr (NT) {
+    const u32v4 v = {x.x, x.y, x.z, x.w};
+    __builtin_nontemporal_store(v, (u32v4*)p);
+  } else {
+    *(uint4*)p = x;
+  }
+}
+
+template <bool MASTER, bool SR, bool BF16M, int UNR, bool NT = false>
 __global__ __launch_bounds__(256) void adamw_kernel(u16* __restrict__ p, const u16* __restrict__ g,
                                                     float* __restrict__ master, void* __restrict__ mom,
                                                     void* __restrict__ var, const float* __restrict__ coef, long n,
@@ -173,15 +211,20 @@ __global__ __launch_bounds__(256) void adamw_kernel(u16* __restrict__ p, const u
       const long v = v0 + k * 256;
       if (v < nv) {
         const long o = v * 8;
-        unpack8(*(const uint4*)(g + o), gf[k]);
+        unpack8(ld16<NT>(g + o), gf[k]);
         if (MASTER) {
           *(float4*)&w[k][0] = *(const float4*)(master + o);
           *(float4*)&w[k][4] = *(const float4*)(master + o + 4);
         } else {
-          unpack8(*(const uint4*)(p + o), w[k]);
+          unpack8(ld16<NT>(p + o), w[k]);
         }
-        Mo::load(mom, o, mm[k]);
-        Mo::load(var, o, vv[k]);
+        if constexpr (BF16M && NT) {
+          unpack8(ld16<NT>((const u16*)mom + o), mm[k]);
+          unpack8(ld16<NT>((const u16*)var + o), vv[k]);
+        } else {
+          Mo::load(mom, o, mm[k]);
+          Mo::load(var, o, vv[k]);
+        }
       }
     }
 #pragma unroll
@@ -196,9 +239,14 @@ __global__ __launch_bounds__(256) void adamw_kernel(u16* __restrict__ p, const u
           *(float4*)(master + o) = *(float4*)&w[k][0];
           *(float4*)(master + o + 4) = *(float4*)&w[k][4];
         }
-        Mo::store(mom, o, mm[k], SR, idx0 + o, seed ^ SEED_M);
-        Mo::store(var, o, vv[k], SR, idx0 + o, seed ^ SEED_V);
-        *(uint4*)(p + o) = SR ? pack8_sr(w[k], idx0 + o, seed) : pack8(w[k]);
+        if constexpr (BF16M && NT) {
+          st16<NT>((u16*)mom + o, SR ? pack8_sr(mm[k], idx0 + o, seed ^ SEED_M) : pack8(mm[k]));
+          st16<NT>((u16*)var + o, SR ? pack8_sr(vv[k], idx0 + o, seed ^ SEED_V) : pack8(vv[k]));
+        } else {
+          Mo::store(mom, o, mm[k], SR, idx0 + o, seed ^ SEED_M);
+          Mo::store(var, o, vv[k], SR, idx0 + o, seed ^ SEED_V);
+        }
+        st16<NT>(p + o, SR ? pack8_sr(w[k], idx0 + o, seed) : pack8(w[k]));
       }
     }
   }
@@ -241,7 +289,7 @@ void adamw_flat(at::Tensor param, const at::Tensor& grad, const c10::optional<at
   SFT_CHECK(clip_coef.scalar_type() == at::kFloat && clip_coef.numel() >= 1 && clip_coef.is_cuda(), "clip_coef");
   auto go = [&](auto ms, auto sr, auto bm) {
     constexpr bool M = decltype(ms)::value, S = decltype(sr)::value, B = decltype(bm)::value;
-    adamw_kernel<M, S, B, UNR><<<grid, 256, 0, cur_stream()>>>(
+    adamw_kernel<M, S, B, UNR, true><<<grid, 256, 0, cur_stream()>>>(
         (u16*)param.data_ptr(), (const u16*)grad.data_ptr(), mp, exp_avg.data_ptr(), exp_avg_sq.data_ptr(),
         clip_coef.data_ptr<float>(), n, (float)lr, (float)beta1, (float)beta2, (float)eps, (float)weight_decay,
         rbc1, rsbc2, (float)(1.0 - beta1), (float)(1.0 - beta2), seed, (long)sr_offset);

@@ -158,13 +158,15 @@ def hash_u32(idx: torch.Tensor, seed: int) -> torch.Tensor:
 
 
 def bf16_stochastic_round(x: torch.Tensor, seed: int, offset: int = 0) -> torch.Tensor:
-    """fp32 -> bf16 with stochastic rounding: bits + (hash(offset + i, seed) & 0xffff), truncated.
-    Twin of csrc/optim.hip f2bf_sr over a flat tensor (E[result] = x)."""
+    """fp32 -> bf16 with stochastic rounding: bits + noise(offset + i), truncated, where elements 2q / 2q + 1 take the
+    low / high 16 bits of hash(q, seed). Twin of csrc/optim.hip f2bf_sr / sr_hash over a flat tensor (E[result] = x)."""
     xf = x.float().contiguous().reshape(-1)
     idx = torch.arange(xf.numel(), dtype=torch.int64, device=xf.device) + int(offset)
     bits = xf.view(torch.int32).to(torch.int64) & _M32
     finite = (bits & 0x7F800000) != 0x7F800000
-    rounded = ((bits + (hash_u32(idx, seed) & 0xFFFF)) >> 16) << 16
+    h = hash_u32(idx >> 1, seed)
+    noise = torch.where((idx & 1) == 1, h >> 16, h & 0xFFFF)
+    rounded = ((bits + noise) >> 16) << 16
     out = torch.where(finite, rounded, bits)
     out = torch.where(out >= 1 << 31, out - (1 << 32), out).to(torch.int32).view(torch.float32)
     res = out.to(torch.bfloat16)  # exact: low 16 bits are zero (non-finite: round-to-nearest, as f2bf)
