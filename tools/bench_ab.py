@@ -6,7 +6,7 @@ error against the first variant.
     python tools/bench_ab.py dgrad gate_up 14,15,16
     python tools/bench_ab.py wgrad lm_head 10,1214 --rounds 5
 
-wgrad: dW[N, K] = dy[T, N]^T x[T, K] (sftamd.wgrad_gemm cfg); dgrad: dX[T, N] = dy[T, K] W[K, N] (sftamd.dgrad_gemm cfg;
+wgrad: dW[N, K] = dy[T, N]^T x[T, K] (sftamd.wgrad_gemm cfg); fwd: y[T, N] = x[T, K] W[N, K]^T (sftamd.gemm_tn cfg); dgrad: dX[T, N] = dy[T, K] W[K, N] (sftamd.dgrad_gemm cfg;
 'blas' = torch.mm on the TunableOp selection). SmolLM3-3B shapes at T = 8192 tokens.
 """
 import argparse
@@ -41,7 +41,7 @@ def timeit(fn, iters):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("kind", choices=["wgrad", "dgrad"])
+    ap.add_argument("kind", choices=["wgrad", "dgrad", "fwd"])
     ap.add_argument("shapes")
     ap.add_argument("variants")
     ap.add_argument("--rounds", type=int, default=7)
@@ -66,6 +66,15 @@ def main():
                 else:
                     ops.wgrad_gemm(out, dy, x, False, int(v))
                 return out
+        elif a.kind == "fwd":
+            N, K = WGRAD[name]  # y[T, N] = x[T, K] W[N, K]^T
+            x = torch.randn(T, K, device="cuda", dtype=torch.bfloat16)
+            w = (0.02 * torch.randn(N, K, device="cuda")).to(torch.bfloat16)
+            hold = [None]
+
+            def run(v):
+                hold[0] = torch.mm(x, w.t()) if v == "blas" else ops.gemm_tn(x, w, int(v))
+                return hold[0]
         else:
             K, N = DGRAD[name]
             dy = torch.randn(T, K, device="cuda", dtype=torch.bfloat16)
