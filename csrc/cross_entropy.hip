@@ -4,7 +4,7 @@
 // loads and keeps an online (max, sum e^(x-max), sum e^(x-max)*x, argmax) per thread; the
 // block combines them to get logsumexp, the per-token loss, the entropy and the argmax
 // accuracy bit (the TRL training metrics, at no extra pass). Pass 2 re-reads the row (L2 /
-// Infinity-Cache resident) and overwrites it IN PLACE with the bf16 gradient
+// Infinity-Cache resident: the launch caps the rows in flight, see ce_fwd) and overwrites it IN PLACE with the bf16 gradient
 // (softmax - onehot) * (1/num_items_in_batch): fp32 logits are never materialised.
 #include "common.h"
 
@@ -140,7 +140,18 @@ at::Tensor ce_fwd(at::Tensor logits, const at::Tensor& labels, const at::Tensor&
   auto stats = at::empty({4, M}, logits.options().dtype(at::kFloat));
   if (M == 0) return stats;
   auto* lg = (u16*)logits.data_ptr();
-    ce_fwd_kernel<4><<<M, 256, 0, cur_stream()>>>(lg, lab.data_ptr<int64_t>(), inv_count.data_ptr<float>(),
+  // Pass 2 re-reads the row from the Infinity Cache only while the rows in flight fit it: with 8 blocks per CU the
+  // SmolLM3 bench's 2048 rows x 256 KB = 512 MB of rows in flight overflow the 256 MB cache and pass 2 goes back to HBM.
+  // With the gradient written, cap the blocks per CU so the rows in flight stay near 200 MB by reserving dynamic LDS
+  // (nothing is stored in it): 3 blocks per CU at V = 128,256 — 1.037 vs 1.227 ms per call at 8192 rows
+  // (tools/bench_ce.py, profiles/r6_memory_kernels.md); the stats-only pass (eval) keeps full occupancy.
+  int pad = 0;
+  if (write_grad) {
+    const long row_bytes = (long)V * 2;
+    const long bpc = std::max(1L, std::min(8L, (200L << 20) / ((long)num_cus() * row_bytes)));
+    if (bpc < 8) pad = (int)((160L * 1024) / bpc - 1024);
+  }
+    ce_fwd_kernel<4><<<M, 256, pad, cur_stream()>>>(lg, lab.data_ptr<int64_t>(), inv_count.data_ptr<float>(),
                                                   stats.data_ptr<float>(), M, V, write_grad ? 1 : 0);
   SFT_LAUNCH_CHECK();
   return stats;

@@ -102,7 +102,7 @@ __device__ __forceinline__ void adam_elem(float& w, float g, float& m, float& v,
 // Stochastic-rounding noise of element i: 16 bits of the stateless hash of its PAIR (elements 2q, 2q + 1 share
 // hash(q, seed): low / high half), half the hashing of one hash per element — the bf16-moment update was VALU-bound on
 // its three roundings per element (nt streams: 734 us with one hash per element vs 660 us round-to-nearest per 256 M
-// elements, profiles/r6_adamw_overlap.md). Twin: ops/reference.py bf16_stochastic_round.
+// elements, profiles/r6_memory_kernels.md). Twin: ops/reference.py bf16_stochastic_round.
 __device__ __forceinline__ unsigned sr_hash(unsigned long long i, unsigned seed) {
   return hash_u32(i >> 1, seed) >> (16 * (unsigned)(i & 1));
 }
@@ -173,7 +173,7 @@ constexpr unsigned SEED_M = 0x68E31DA4u, SEED_V = 0xB5297A4Du;
 // UNR vectors of 8 elements per thread per grid-stride step, all loads issued before any math: the update
 // streams 22 (fp32 moments) or 14 (bf16) bytes per parameter, so bytes in flight per wave set its speed.
 // Streams touched once per update: nontemporal loads / stores (720 vs 760 us per 256 M elements with bf16 moments +
-// SR, 1127 vs 1154 with fp32 moments; profiles/r6_adamw_overlap.md)
+// SR, 1127 vs 1154 with fp32 moments; profiles/r6_memory_kernels.md)
 typedef unsigned __attribute__((ext_vector_type(4))) u32v4;
 template <bool NT>
 __device__ __forceinline__ uint4 ld16(const void* p) {
