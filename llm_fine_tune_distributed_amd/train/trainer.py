@@ -357,7 +357,7 @@ class SFTTrainer:
                 with self._phase("fwd"):
                     out = model(**self._model_inputs(b), num_items_in_batch=n_items)
                 beat(self._hb_step, "bwd", micro=i)
-                with self._phase("bwd"), ops.unit_loss_grad():  # out.loss IS the LM-head loss: d(loss) = 1
+                with self._phase("bwd"):
                     out.loss.backward()
             acc[0] += out.loss.detach()
             acc[1:] += out.metrics

@@ -112,9 +112,9 @@ def test_saved_model_loads_in_transformers(tmp_path, mt):
     assert (ho.reshape(-1, cfg.vocab_size) - mo).abs().max() < 1e-4
 
 
-def test_unit_loss_grad_skips_only_the_identity_scale():
-    """ops.unit_loss_grad (the trainer's ``out.loss.backward()``): the LM head skips its d(loss) scale passes — the
-    gradients equal the general path's at d(loss) = 1; a scaled loss outside the context is still scaled."""
+def test_lm_head_loss_gradient_scale():
+    """The LM head scales its [T, hidden] operands by the incoming d(loss) (no global unit-gradient switch): the
+    trainer's plain loss.backward() and a scaled loss both get the right gradients."""
     import torch
     from llm_fine_tune_distributed_amd import ops
     torch.manual_seed(0)
@@ -123,18 +123,18 @@ def test_unit_loss_grad_skips_only_the_identity_scale():
     labels = torch.randint(0, 32, (8,))
     inv = torch.tensor([1.0 / 8])
 
-    def grads(scale, unit):
+    def grads(scale):
         h.grad = w.grad = None
         loss, _ = ops.lm_head_cross_entropy(h, w, labels, inv)
-        if unit:
-            with ops.unit_loss_grad():
-                loss.backward()
-        else:
-            (loss * scale).backward()
+        (loss if scale is None else loss * scale).backward()
         return h.grad.clone(), w.grad.clone()
 
-    g1, w1 = grads(1.0, False)
-    gu, wu = grads(1.0, True)
-    g3, w3 = grads(3.0, False)
-    assert torch.allclose(g1, gu) and torch.allclose(w1, wu)
+    g1, w1 = grads(None)
+    gs, ws = grads(1.0)
+    g3, w3 = grads(3.0)
+    assert torch.equal(g1, gs) and torch.equal(w1, ws)
     assert torch.allclose(g3, 3 * g1, rtol=1e-5) and torch.allclose(w3, 3 * w1, rtol=1e-5)
+    hr = h.detach().clone().requires_grad_(True)
+    wr = w.detach().clone().requires_grad_(True)
+    torch.nn.functional.cross_entropy(hr @ wr.t(), labels, reduction="sum").mul(inv[0]).backward()
+    assert torch.allclose(g1, hr.grad, atol=1e-5) and torch.allclose(w1, wr.grad, atol=1e-5)
