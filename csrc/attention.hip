@@ -64,16 +64,8 @@ __device__ __forceinline__ void stage(char* lds, const u16* __restrict__ g, long
 
 
 __device__ __forceinline__ bf16x8 pack_acc(const f32x4& t0, const f32x4& t1) {
-  bf16x8 r;
-  r[0] = (__bf16)t0[0];
-  r[1] = (__bf16)t0[1];
-  r[2] = (__bf16)t0[2];
-  r[3] = (__bf16)t0[3];
-  r[4] = (__bf16)t1[0];
-  r[5] = (__bf16)t1[1];
-  r[6] = (__bf16)t1[2];
-  r[7] = (__bf16)t1[3];
-  return r;
+  typedef __attribute__((ext_vector_type(4))) unsigned w4;
+  return __builtin_bit_cast(bf16x8, w4{pk2bf(t0[0], t0[1]), pk2bf(t0[2], t0[3]), pk2bf(t1[0], t1[1]), pk2bf(t1[2], t1[3])});
 }
 
 __device__ __forceinline__ bf16x8 load_frag_global(const u16* p, bool ok) {
@@ -83,8 +75,8 @@ __device__ __forceinline__ bf16x8 load_frag_global(const u16* p, bool ok) {
 
 __device__ __forceinline__ void store4(u16* p, const f32x4& v, float s) {
   uint2 w;
-  w.x = (unsigned)f2bf(v[0] * s) | ((unsigned)f2bf(v[1] * s) << 16);
-  w.y = (unsigned)f2bf(v[2] * s) | ((unsigned)f2bf(v[3] * s) << 16);
+  w.x = pk2bf(v[0] * s, v[1] * s);
+  w.y = pk2bf(v[2] * s, v[3] * s);
   *(uint2*)p = w;
 }
 
@@ -250,11 +242,13 @@ __device__ __forceinline__ bf16x8 lds_tr2(const char* base, int lo, int hi) {
   return __builtin_bit_cast(bf16x8, v);
 }
 
+typedef __attribute__((ext_vector_type(4))) unsigned u32x4;
+__device__ __forceinline__ u32x4 pack8w(const f32x16& t, int base) {  // t[base .. base + 7] as 4 bf16 pairs
+  return u32x4{pk2bf(t[base], t[base + 1]), pk2bf(t[base + 2], t[base + 3]), pk2bf(t[base + 4], t[base + 5]),
+               pk2bf(t[base + 6], t[base + 7])};
+}
 __device__ __forceinline__ bf16x8 pack8(const f32x16& t, int base) {
-  bf16x8 r;
-#pragma unroll
-  for (int j = 0; j < 8; ++j) r[j] = (__bf16)t[base + j];
-  return r;
+  return __builtin_bit_cast(bf16x8, pack8w(t, base));
 }
 
 __device__ __forceinline__ float swap32max(float x) {
@@ -276,10 +270,10 @@ __device__ __forceinline__ void store_t21(u16* row, const f32x16 (&a)[4], float 
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
       const int i0 = 8 * u;
-      const unsigned ax = (unsigned)f2bf(a[db][i0] * s) | ((unsigned)f2bf(a[db][i0 + 1] * s) << 16);
-      const unsigned ay = (unsigned)f2bf(a[db][i0 + 2] * s) | ((unsigned)f2bf(a[db][i0 + 3] * s) << 16);
-      const unsigned bx = (unsigned)f2bf(a[db][i0 + 4] * s) | ((unsigned)f2bf(a[db][i0 + 5] * s) << 16);
-      const unsigned by = (unsigned)f2bf(a[db][i0 + 6] * s) | ((unsigned)f2bf(a[db][i0 + 7] * s) << 16);
+      const unsigned ax = pk2bf(a[db][i0] * s, a[db][i0 + 1] * s);
+      const unsigned ay = pk2bf(a[db][i0 + 2] * s, a[db][i0 + 3] * s);
+      const unsigned bx = pk2bf(a[db][i0 + 4] * s, a[db][i0 + 5] * s);
+      const unsigned by = pk2bf(a[db][i0 + 6] * s, a[db][i0 + 7] * s);
       const auto rx = __builtin_amdgcn_permlane32_swap(ax, bx, false, false);
       const auto ry = __builtin_amdgcn_permlane32_swap(ay, by, false, false);
       if (ok) *(uint4*)(row + 32 * db + 16 * u + 8 * hi) = make_uint4(rx[0], ry[0], rx[1], ry[1]);
@@ -707,29 +701,34 @@ __device__ __forceinline__ void dkdv32_step(const char* __restrict__ cur, char* 
       const float L[4] = {L4.x, L4.y, L4.z, L4.w}, Dd[4] = {D4.x, D4.y, D4.z, D4.w};
 #pragma unroll
       for (int t = 0; t < 4; ++t) {
-        const int i = 4 * m + t, o = 8 * m + t;
-        float p = exp2f(__builtin_fmaf(s[i], sl2, -L[t]));
-        if (need_mask) p = (o < lo || o > hq) ? 0.f : p;
+        const int i = 4 * m + t;
+        const float p = exp2f(__builtin_fmaf(s[i], sl2, -L[t]));
         dp[i] = p * (dp[i] - Dd[t]);
         s[i] = p;
       }
     }
-    if (drow != nullptr) {  // dS^T[key][q]: registers 8 u .. 8 u + 7 = queries 16 u + 4 hi + {0..3, 8..11}
+    // The mask as a real (wave-uniform) branch: only the diagonal and the sequence-end tiles take it. Folded into the
+    // loop above as selects it cost 50 of the ~245 VALU per half tile on every tile, and this loop is VALU-bound
+    // (~10 VALU per 32x32x16 MFMA, PMC in profiles/r6_attention.md). A masked element's p (possibly inf / NaN from an
+    // unmasked exp) is replaced, so the result is the select form's.
+    if (need_mask) {
+      int vlo = lo, vhi = hq;
+      asm volatile("" : "+v"(vlo), "+v"(vhi));  // the compares depend on volatile code: not hoisted out of the branch
 #pragma unroll
-      for (int u = 0; u < 2; ++u) {
-        const int i0 = 8 * u;
-        const unsigned ax = (unsigned)f2bf(dp[i0]) | ((unsigned)f2bf(dp[i0 + 1]) << 16);
-        const unsigned ay = (unsigned)f2bf(dp[i0 + 2]) | ((unsigned)f2bf(dp[i0 + 3]) << 16);
-        const unsigned bx = (unsigned)f2bf(dp[i0 + 4]) | ((unsigned)f2bf(dp[i0 + 5]) << 16);
-        const unsigned by = (unsigned)f2bf(dp[i0 + 6]) | ((unsigned)f2bf(dp[i0 + 7]) << 16);
-        const auto rx = __builtin_amdgcn_permlane32_swap(ax, bx, false, false);
-        const auto ry = __builtin_amdgcn_permlane32_swap(ay, by, false, false);
-        if (dok) *(uint4*)(drow + 32 * qb + 16 * u + 8 * hi) = make_uint4(rx[0], ry[0], rx[1], ry[1]);
+      for (int i = 0; i < 16; ++i) {
+        const int o = 8 * (i >> 2) + (i & 3);
+        if (o < vlo || o > vhi) s[i] = dp[i] = 0.f;
       }
     }
 #pragma unroll
     for (int sub = 0; sub < 2; ++sub) {
-      const bf16x8 pb = pack8(s, 8 * sub), db = pack8(dp, 8 * sub);
+      const u32x4 dw = pack8w(dp, 8 * sub);  // dS (bf16) once, for the MFMA operand and the dS^T store
+      if (drow != nullptr) {  // dS^T[key][q]: registers 8 sub .. 8 sub + 7 = queries 16 sub + 4 hi + {0..3, 8..11}
+        const auto rx = __builtin_amdgcn_permlane32_swap(dw[0], dw[2], false, false);
+        const auto ry = __builtin_amdgcn_permlane32_swap(dw[1], dw[3], false, false);
+        if (dok) *(uint4*)(drow + 32 * qb + 16 * sub + 8 * hi) = make_uint4(rx[0], ry[0], rx[1], ry[1]);
+      }
+      const bf16x8 pb = pack8(s, 8 * sub), db = __builtin_bit_cast(bf16x8, dw);
       const int ko = (2 * qb + sub) * 16 * ROWB;
 #pragma unroll
       for (int d4 = 0; d4 < 4; ++d4) {

@@ -24,6 +24,24 @@ constexpr int WAVE = 64;
 __device__ __forceinline__ float bf2f(u16 u) { return __uint_as_float(((unsigned)u) << 16); }
 __device__ __forceinline__ u16 f2bf(float f) { return __builtin_bit_cast(u16, (__bf16)f); }
 
+// two floats -> two round-to-nearest-even bf16 in one word (low = a): one v_cvt_pk_bf16_f32. Two scalar (__bf16)
+// conversions compile to two half-used cvt_pk plus a shift and an or.
+__device__ __forceinline__ unsigned pk2bf(float a, float b) {
+  typedef __attribute__((ext_vector_type(2))) float f32x2_t;
+  typedef __attribute__((ext_vector_type(2))) __bf16 bf16x2_t;
+  return __builtin_bit_cast(unsigned, __builtin_convertvector((f32x2_t){a, b}, bf16x2_t));
+}
+
+// SwiGLU backward of one element, the rounding pinned (explicit fma, no contraction): dact d, gate g, up u ->
+// dgate = d u sg (1 + g (1 - sg)), dup = d g sg with sg = sigmoid(g). Shared by the standalone kernel and the fused
+// epilogues that promise bitwise-equal results.
+__device__ __forceinline__ void swiglu_grad(float d, float g, float u, float& dg, float& du) {
+#pragma clang fp contract(off)
+  const float sg = 1.f / (1.f + __expf(-g));
+  du = (d * g) * sg;
+  dg = ((d * u) * sg) * __builtin_fmaf(g, 1.f - sg, 1.f);
+}
+
 // 8 x bf16 in a uint4 <-> 8 floats
 __device__ __forceinline__ void unpack8(const uint4& v, float* f) {
   const unsigned w[4] = {v.x, v.y, v.z, v.w};
@@ -34,12 +52,7 @@ __device__ __forceinline__ void unpack8(const uint4& v, float* f) {
   }
 }
 __device__ __forceinline__ uint4 pack8(const float* f) {
-  uint4 v;
-  v.x = (unsigned)f2bf(f[0]) | ((unsigned)f2bf(f[1]) << 16);
-  v.y = (unsigned)f2bf(f[2]) | ((unsigned)f2bf(f[3]) << 16);
-  v.z = (unsigned)f2bf(f[4]) | ((unsigned)f2bf(f[5]) << 16);
-  v.w = (unsigned)f2bf(f[6]) | ((unsigned)f2bf(f[7]) << 16);
-  return v;
+  return make_uint4(pk2bf(f[0], f[1]), pk2bf(f[2], f[3]), pk2bf(f[4], f[5]), pk2bf(f[6], f[7]));
 }
 
 __device__ __forceinline__ float wave_sum(float v) {

@@ -78,9 +78,7 @@ __global__ __launch_bounds__(256) void swiglu_bwd_kernel(const u16* __restrict__
         unpack8(da[k], d);
 #pragma unroll
         for (int i = 0; i < 8; ++i) {
-          const float sg = 1.f / (1.f + __expf(-g[i]));
-          du[i] = d[i] * g[i] * sg;
-          dg[i] = d[i] * u[i] * sg * (1.f + g[i] * (1.f - sg));
+          swiglu_grad(d[i], g[i], u[i], dg[i], du[i]);
         }
         *(uint4*)(dgu + grow[k]) = pack8(dg);
         *(uint4*)(dgu + grow[k] + I) = pack8(du);

@@ -276,9 +276,7 @@ __device__ __forceinline__ void epilogue(char* smem, f32x4 (&acc)[G::FM][G::FN],
         unpack8(*(const uint4*)(ea.gu + base + ea.N), up);
 #pragma unroll
         for (int e = 0; e < 8; ++e) {
-          const float s = 1.f / (1.f + __expf(-gt[e]));
-          du[e] = v[e] * gt[e] * s;
-          dg[e] = v[e] * up[e] * s * (1.f + gt[e] * (1.f - s));
+          swiglu_grad(v[e], gt[e], up[e], dg[e], du[e]);
         }
         *(uint4*)(ea.out + base) = pack8(dg);
         *(uint4*)(ea.out + base + ea.N) = pack8(du);

@@ -543,7 +543,7 @@ __device__ __forceinline__ void ring2e_loop(char* __restrict__ b0, char* __restr
 // ds_write_b32 of fp32) and back as 16-byte rows for the global stores; the paired fragments (2q,
 // 2q + 1) of SWIGLU / ROPE meet in one lane and are combined in registers before staging.
 __device__ __forceinline__ uint2 pack4(const float* f) {
-  return make_uint2((unsigned)f2bf(f[0]) | ((unsigned)f2bf(f[1]) << 16), (unsigned)f2bf(f[2]) | ((unsigned)f2bf(f[3]) << 16));
+  return make_uint2(pk2bf(f[0], f[1]), pk2bf(f[2], f[3]));
 }
 
 template <class G, int EPI>
@@ -1021,7 +1021,7 @@ __device__ __forceinline__ void tn5_coords(int tile, int nbm, int nbn, int group
   n0 = (in / gsz) * 256;
 }
 
-__device__ __forceinline__ unsigned pack2(float a, float b) { return (unsigned)f2bf(a) | ((unsigned)f2bf(b) << 16); }
+__device__ __forceinline__ unsigned pack2(float a, float b) { return pk2bf(a, b); }
 
 // Launched with one workgroup per CU (persistent): each walks its XCD's contiguous share of the tile order.
 __device__ __forceinline__ int tn5_range_start(int x, int tiles) {

@@ -293,17 +293,15 @@ __global__ __launch_bounds__(256) void bwd_dx_kernel(const u16* __restrict__ bas
     unpack8(vb[e], o);
     const unsigned bits = drop ? keep8((unsigned long long)t * K + k, seed, thresh) : 0xFFu;
 #pragma unroll
-    for (int j = 0; j < 8; ++j) o[j] += ((bits >> j) & 1u) ? acc[j][e] * dscale : 0.f;
+    for (int j = 0; j < 8; ++j)  // an explicit fma: the SWIGLU and plain instantiations must round identically
+      o[j] = ((bits >> j) & 1u) ? __builtin_fmaf(acc[j][e], dscale, o[j]) : o[j];
     if constexpr (SWIGLU) {  // o = dact (fp32); the same arithmetic as swiglu_bwd_kernel on the bf16-rounded dact
       float gt[8], up[8], dg[8], du[8];
       unpack8(vg[e], gt);
       unpack8(vu[e], up);
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
-        const float d = bf2f(f2bf(o[j]));
-        const float sg = 1.f / (1.f + __expf(-gt[j]));
-        du[j] = d * gt[j] * sg;
-        dg[j] = d * up[j] * sg * (1.f + gt[j] * (1.f - sg));
+        swiglu_grad(bf2f(f2bf(o[j])), gt[j], up[j], dg[j], du[j]);
       }
       *(uint4*)(dx + t * 2L * K + k) = pack8(dg);
       *(uint4*)(dx + t * 2L * K + K + k) = pack8(du);
@@ -718,7 +716,7 @@ __global__ __launch_bounds__(256) void dxa_kernel(const u16* __restrict__ dy, lo
     if (t < T) {
       const float v0 = ((red[0][row][col] + red[1][row][col]) + red[2][row][col]) + red[3][row][col];
       const float v1 = ((red[0][row][col + 1] + red[1][row][col + 1]) + red[2][row][col + 1]) + red[3][row][col + 1];
-      *(unsigned*)(out + t * R + col) = (unsigned)f2bf(v0 * s) | ((unsigned)f2bf(v1 * s) << 16);
+      *(unsigned*)(out + t * R + col) = pk2bf(v0 * s, v1 * s);
     }
   }
 }

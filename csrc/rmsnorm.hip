@@ -180,8 +180,8 @@ __global__ __launch_bounds__(1024) void col_sum2_kernel(const float* __restrict_
         r.z += __uint_as_float(o.y << 16);
         r.w += __uint_as_float(o.y & 0xffff0000u);
       }
-      *(uint2*)(out_bf + c) = make_uint2((unsigned)f2bf(r.x) | ((unsigned)f2bf(r.y) << 16),
-                                         (unsigned)f2bf(r.z) | ((unsigned)f2bf(r.w) << 16));
+      *(uint2*)(out_bf + c) = make_uint2(pk2bf(r.x, r.y),
+                                         pk2bf(r.z, r.w));
     } else {
       *(float4*)(out + c) = r;
     }

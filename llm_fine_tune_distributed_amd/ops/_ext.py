@@ -20,6 +20,8 @@ _PKG = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
 def _select_lib() -> str:
+    if os.environ.get("SFTAMD_LIB"):  # an alternative build (A/B tooling: tools/bench_attention.py old vs new)
+        return os.path.abspath(os.environ["SFTAMD_LIB"])
     return os.path.join(_PKG, "_C_debug.so" if os.environ.get("SFTAMD_DEBUG", "0") == "1" else "_C.so")
 
 
