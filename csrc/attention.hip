@@ -658,7 +658,7 @@ __device__ __forceinline__ void dkdv32_step(const char* __restrict__ cur, char* 
                                             rsrc_t qr, rsrc_t orr, unsigned vq0, unsigned vq1, unsigned vo0,
                                             unsigned vo1, unsigned qso, unsigned oso, unsigned rowb, unsigned rowo,
                                             int wv, const float* lsrc, const float* dsrc, int gl, int q0, int len,
-                                            int causal, int kw0, int key, float sl2, u16* drow, bool dok,
+                                            int causal, int kw0, int key, float sl2, u16* drow,
                                             const Offs32& off, const bf16x8 (&kf)[8], const char* Vk,
                                             f32x16 (&dk)[4], f32x16 (&dv)[4]) {
   constexpr int TB = 64 * ROWB;
@@ -680,6 +680,7 @@ __device__ __forceinline__ void dkdv32_step(const char* __restrict__ cur, char* 
   const float* Ls = (const float*)(cur + 2 * TB);
   const float* Dl = Ls + 64;
   const int hi = (threadIdx.x >> 5) & 1;
+  const bool wds = __builtin_amdgcn_readfirstlane((int)(drow != nullptr));  // (drow is per lane, the test uniform)
 #pragma unroll 1
   for (int qb = 0; qb < 2; ++qb) {  // (not unrolled: hoisting the second half's LDS reads ran out of VGPRs)
     f32x16 s, dp;
@@ -723,10 +724,12 @@ __device__ __forceinline__ void dkdv32_step(const char* __restrict__ cur, char* 
 #pragma unroll
     for (int sub = 0; sub < 2; ++sub) {
       const u32x4 dw = pack8w(dp, 8 * sub);  // dS (bf16) once, for the MFMA operand and the dS^T store
-      if (drow != nullptr) {  // dS^T[key][q]: registers 8 sub .. 8 sub + 7 = queries 16 sub + 4 hi + {0..3, 8..11}
+      if (wds) {  // dS^T[key][q]: registers 8 sub .. 8 sub + 7 = queries 16 sub + 4 hi + {0..3, 8..11}
         const auto rx = __builtin_amdgcn_permlane32_swap(dw[0], dw[2], false, false);
         const auto ry = __builtin_amdgcn_permlane32_swap(dw[1], dw[3], false, false);
-        if (dok) *(uint4*)(drow + 32 * qb + 16 * sub + 8 * hi) = make_uint4(rx[0], ry[0], rx[1], ry[1]);
+        // (also for keys past the sequence end: their rows are inside the [lp][lp] block, key < k0 + 64 <= lp, and
+        // bwd_dq32 never reads them — no divergent branch around the store)
+        *(uint4*)(drow + 32 * qb + 16 * sub + 8 * hi) = make_uint4(rx[0], ry[0], rx[1], ry[1]);
       }
       const bf16x8 pb = pack8(s, 8 * sub), db = __builtin_bit_cast(bf16x8, dw);
       const int ko = (2 * qb + sub) * 16 * ROWB;
@@ -834,7 +837,7 @@ __global__ __launch_bounds__(128 * G, 1) void bwd_dkdv32_kernel(
     u16* drow = dst != nullptr ? dst + ((long)(b * nq + h) * lp + key) * lp + q0 : nullptr;
     dkdv32_step(base + (it & 1) * GB, base + ((it + 1) & 1) * GB, pre, qr, orr, vq0, vq1, vo0, vo1,
                 (unsigned)qn * rowb + hn * ROWB, (unsigned)qn * rowo + hn * ROWB, rowb, rowo, kh,
-                lok ? lse + lo : nullptr, delta + lo, gl, q0, len, causal, kw0, key, sl2, drow, kok, off, kf, Vk, dk,
+                lok ? lse + lo : nullptr, delta + lo, gl, q0, len, causal, kw0, key, sl2, drow, off, kf, Vk, dk,
                 dv);
     if (pre) vm_drain();  // this lane's pieces of the next tile landed ...
     __syncthreads();      // ... and every lane's; every wave is done reading this stage
@@ -949,7 +952,7 @@ std::tuple<at::Tensor, at::Tensor> flash_fwd(const at::Tensor& qkv, const at::Te
 static at::Tensor flash_bwd_impl(const at::Tensor& dout, const at::Tensor& qkv, const at::Tensor& out,
                                  const at::Tensor& lse, const at::Tensor& cu, int64_t max_seqlen, int64_t nq,
                                  int64_t nkv, int64_t hd, double scale, bool causal, const float* rcos,
-                                 const float* rsin, bool& rope_done) {
+                                 const float* rsin, bool& rope_done, const c10::optional<at::Tensor>& delta_in) {
   rope_done = false;
   check_attn_args(qkv, cu, nq, nkv, hd);
   SFT_CHECK_CONTIG(dout);
@@ -959,11 +962,21 @@ static at::Tensor flash_bwd_impl(const at::Tensor& dout, const at::Tensor& qkv, 
   const int nseq = cu.numel() - 1;
   auto dqkv = at::empty_like(qkv);
   if (total == 0 || max_seqlen == 0) return dqkv;
-  auto delta = at::empty({nq, total}, qkv.options().dtype(at::kFloat));
-  const long rows = (long)total * nq;
-  attn::delta_kernel<<<(rows + 15) / 16, 256, 0, cur_stream()>>>((const u16*)dout.data_ptr(), (const u16*)out.data_ptr(),
-                                                                  delta.data_ptr<float>(), total, nq);
-  SFT_LAUNCH_CHECK();
+  at::Tensor delta;
+  if (delta_in.has_value() && delta_in->defined()) {  // computed by the producer of dO (dgrad_gemm_delta's epilogue)
+    delta = *delta_in;
+    SFT_CHECK(delta.scalar_type() == at::kFloat && delta.is_contiguous() && delta.dim() == 2 && delta.size(0) == nq &&
+                  delta.size(1) == total && delta.device() == qkv.device(),
+              "flash_bwd: delta must be contiguous fp32 [n_q, total]");
+  } else {
+    SFT_TRACE("attn.delta_kernel");
+    delta = at::empty({nq, total}, qkv.options().dtype(at::kFloat));
+    const long rows = (long)total * nq;
+    attn::delta_kernel<<<(rows + 15) / 16, 256, 0, cur_stream()>>>((const u16*)dout.data_ptr(),
+                                                                    (const u16*)out.data_ptr(), delta.data_ptr<float>(),
+                                                                    total, nq);
+    SFT_LAUNCH_CHECK();
+  }
   const float sl2 = (float)scale * attn::LOG2E;
   auto cu_c = cu.contiguous();
   const u16* q = (const u16*)qkv.data_ptr();
@@ -1010,9 +1023,10 @@ static at::Tensor flash_bwd_impl(const at::Tensor& dout, const at::Tensor& qkv, 
 
 at::Tensor flash_bwd(const at::Tensor& dout, const at::Tensor& qkv, const at::Tensor& out, const at::Tensor& lse,
                      const at::Tensor& cu, int64_t max_seqlen, int64_t nq, int64_t nkv, int64_t hd, double scale,
-                     bool causal) {
+                     bool causal, const c10::optional<at::Tensor>& delta) {
   bool rope_done;
-  return flash_bwd_impl(dout, qkv, out, lse, cu, max_seqlen, nq, nkv, hd, scale, causal, nullptr, nullptr, rope_done);
+  return flash_bwd_impl(dout, qkv, out, lse, cu, max_seqlen, nq, nkv, hd, scale, causal, nullptr, nullptr, rope_done,
+                        delta);
 }
 
 void rope_(at::Tensor qkv, const at::Tensor& cos, const at::Tensor& sin, int64_t n_q, int64_t n_kv, int64_t head_dim,
@@ -1023,14 +1037,15 @@ void rope_(at::Tensor qkv, const at::Tensor& cos, const at::Tensor& sin, int64_t
 // runs after the backward.
 at::Tensor flash_bwd_rope(const at::Tensor& dout, const at::Tensor& qkv, const at::Tensor& out, const at::Tensor& lse,
                           const at::Tensor& cu, int64_t max_seqlen, int64_t nq, int64_t nkv, int64_t hd, double scale,
-                          bool causal, const at::Tensor& cos, const at::Tensor& sin) {
+                          bool causal, const at::Tensor& cos, const at::Tensor& sin,
+                          const c10::optional<at::Tensor>& delta) {
   SFT_CHECK(cos.scalar_type() == at::kFloat && sin.scalar_type() == at::kFloat && cos.is_contiguous() &&
                 sin.is_contiguous() && cos.is_cuda() && sin.is_cuda(),
             "flash_bwd_rope: contiguous fp32 cos / sin");
   SFT_CHECK(cos.numel() == qkv.size(0) * hd / 2 && sin.numel() == cos.numel(), "flash_bwd_rope: cos / sin [total, hd/2]");
   bool rope_done;
   auto dqkv = flash_bwd_impl(dout, qkv, out, lse, cu, max_seqlen, nq, nkv, hd, scale, causal, cos.data_ptr<float>(),
-                             sin.data_ptr<float>(), rope_done);
+                             sin.data_ptr<float>(), rope_done, delta);
   if (!rope_done) rope_(dqkv, cos, sin, nq, nkv, hd, true);
   return dqkv;
 }

@@ -77,8 +77,8 @@ TORCH_LIBRARY(sftamd, m) {
   m.def("ce_fwd(Tensor(a!) logits, Tensor labels, Tensor inv_count, bool write_grad) -> Tensor");
   // attention
   m.def("flash_fwd(Tensor qkv, Tensor cu_seqlens, int max_seqlen, int n_q, int n_kv, int head_dim, float scale, bool causal) -> (Tensor, Tensor)");
-  m.def("flash_bwd(Tensor dout, Tensor qkv, Tensor out, Tensor lse, Tensor cu_seqlens, int max_seqlen, int n_q, int n_kv, int head_dim, float scale, bool causal) -> Tensor");
-  m.def("flash_bwd_rope(Tensor dout, Tensor qkv, Tensor out, Tensor lse, Tensor cu_seqlens, int max_seqlen, int n_q, int n_kv, int head_dim, float scale, bool causal, Tensor cos, Tensor sin) -> Tensor");
+  m.def("flash_bwd(Tensor dout, Tensor qkv, Tensor out, Tensor lse, Tensor cu_seqlens, int max_seqlen, int n_q, int n_kv, int head_dim, float scale, bool causal, Tensor? delta=None) -> Tensor");
+  m.def("flash_bwd_rope(Tensor dout, Tensor qkv, Tensor out, Tensor lse, Tensor cu_seqlens, int max_seqlen, int n_q, int n_kv, int head_dim, float scale, bool causal, Tensor cos, Tensor sin, Tensor? delta=None) -> Tensor");
   m.def("decode_attention(Tensor q, Tensor kcache, Tensor vcache, Tensor cache_len, int n_q, int n_kv, float scale) -> Tensor");
   // fused decode sampler: penalty -> temperature -> top-k -> top-p -> draw, device-resident state
   m.def("sample_token(Tensor logits, Tensor(a!) presence, Tensor(b!) state, Tensor(c!)? tok_out, Tensor(d!)? pos_out, Tensor(e!)? len_out, Tensor(f!)? log, float temperature, int top_k, float top_p, float repetition_penalty, bool do_sample, int seed) -> ()");
@@ -86,6 +86,7 @@ TORCH_LIBRARY(sftamd, m) {
   m.def("wgrad_gemm(Tensor(a!) out, Tensor dy, Tensor x, bool accumulate, int cfg=14, Tensor(b!)? norm=None) -> ()");
   // input-gradient GEMM dX = dy w (w [K, N]), optional fused SwiGLU backward (csrc/gemm_dgrad.hip)
   m.def("dgrad_gemm(Tensor dy, Tensor w, Tensor? gate_up=None, int cfg=14) -> Tensor");
+  m.def("dgrad_gemm_delta(Tensor dy, Tensor w, Tensor attn_out) -> (Tensor, Tensor)");
   // forward-layout GEMM C = a w^T with fused epilogues (csrc/gemm_tn.hip)
   m.def("gemm_tn(Tensor a, Tensor w, int cfg=0) -> Tensor");
   m.def("gemm_tn_swiglu(Tensor x, Tensor w_gate_up, int cfg=5) -> (Tensor, Tensor)");

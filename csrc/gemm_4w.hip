@@ -148,7 +148,11 @@ struct Epi {
   u16* C;          // output rows [M, ldc]
   float* P;        // split slabs (+ parked whole-tile norm partials) or the norm slots (no split)
   long ldc;
-  int flags;       // bit 0: accumulate into C (beta = 1); bit 1: gradient-norm partials
+  int flags;       // bit 0: accumulate into C (beta = 1); bit 1: gradient-norm partials; bit 2: attention delta
+  const u16* O;    // flags & 4: the attention output [M, ldO] (C = dO, its gradient) ...
+  float* Dl;       // ... and delta [C columns / 128][dM] = per-head rowsum(bf16(dO) * O)
+  long ldO;
+  int dM;
 };
 
 __device__ __forceinline__ float fbits(unsigned u) { return __uint_as_float(u); }
@@ -193,6 +197,35 @@ __device__ __forceinline__ void store_tile(const f32x4 (&acc)[8][8], const Epi& 
         for (int e = 0; e < 8; ++e) ss += v[e] * v[e];
       }
       *(uint4*)(ea.C + at(u)) = pack8(v);
+    }
+  } else if (ea.flags & 4) {
+    // the input gradient of the attention output projection, dO, with flash attention's delta = rowsum(dO . O) per
+    // head fused (the backward's first kernel otherwise: a full re-read of dO and O): the wave tile is 128 rows x ONE
+    // head's 128 columns, each row on the 4 lanes ii + 16 g. O streams through a PD-deep register ring as C does above;
+    // the products use the stored (bf16-rounded) dO, as the standalone kernel would read it.
+    constexpr int U = 32, PD = 8;
+    auto ato = [&](int u) -> long { return (long)(row0 + 16 * (u >> 2) + ii) * ea.ldO + cofs + 32 * (u & 3); };
+    uint4 rg[PD];
+#pragma unroll
+    for (int u = 0; u < PD; ++u) rg[u] = *(const uint4*)(ea.O + ato(u));
+    float part = 0.f;
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      float v[8], o[8], r[8];
+      gather8(acc, u >> 2, u & 3, v);
+      unpack8(rg[u % PD], o);
+      if (u + PD < U) rg[u % PD] = *(const uint4*)(ea.O + ato(u + PD));
+      const uint4 pk = pack8(v);
+      *(uint4*)(ea.C + (long)(row0 + 16 * (u >> 2) + ii) * ea.ldc + cofs + 32 * (u & 3)) = pk;
+      unpack8(pk, r);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) part = __builtin_fmaf(r[e], o[e], part);
+      if ((u & 3) == 3) {  // the row's 4 column pairs done: sum over the 4 lanes holding it
+        part += __shfl_xor(part, 16, 64);
+        part += __shfl_xor(part, 32, 64);
+        if (g == 0) ea.Dl[(long)(col0 >> 7) * ea.dM + row0 + 16 * (u >> 2) + ii] = part;
+        part = 0.f;
+      }
     }
   } else {
 #pragma unroll
@@ -429,12 +462,25 @@ void g4_wgrad(const at::Tensor& dy, const at::Tensor& x, at::Tensor& out, bool a
 // tiles and, for long reductions, the leftover tiles split over the reduction into fp32 slabs + the ordered fixup, e.g.
 // the recipe's padding-free M = 10240: gate_up / lm_head dgrads are 40 x 8 = 320 tiles = 1.25 rounds -> 256 + 64 x 4
 // pieces.
-void g4_dgrad(const at::Tensor& dy, const at::Tensor& w, u16* out, long ldo) {
+// attn_out / delta (optional): the attention output O [M, N] (row stride ld_attn) and delta [N / 128][M] fp32 =
+// per-head rowsum(bf16(dX) . O), fused into the epilogue (flags bit 2; whole tiles only: no split-K).
+void g4_dgrad(const at::Tensor& dy, const at::Tensor& w, u16* out, long ldo, const u16* attn_out, long ld_attn,
+              float* delta) {
   const int M = dy.size(0), K = dy.size(1), N = w.size(1);
   SFT_CHECK(M % 256 == 0 && N % 256 == 0 && K % 128 == 0 && K > 0, "dgrad 4-wave: M, N % 256, K % 128");
   g4::Epi ea{};
   ea.C = out;
   ea.ldc = ldo;
+  if (delta != nullptr) {
+    SFT_CHECK(attn_out != nullptr && ld_attn % 8 == 0 && (uintptr_t)attn_out % 16 == 0,
+              "dgrad 4-wave delta: 16-byte aligned attention output rows");
+    SFT_CHECK(K < 8192 || (M / 256) * (N / 256) % 256 == 0, "dgrad 4-wave delta: whole tiles only (no split-K)");
+    ea.flags = 4;
+    ea.O = attn_out;
+    ea.Dl = delta;
+    ea.ldO = ld_attn;
+    ea.dM = M;
+  }
   const int nbm = M / 256, nbn = N / 256, tiles = nbm * nbn;
   int ndp = tiles, splits = 1;
   if (tiles % 256 != 0 && K >= 8192) {  // short reductions: the fixup costs more

@@ -525,7 +525,34 @@ void launch2(const at::Tensor& dy, const at::Tensor& w, const EpiArgs& ea) {
 
 }  // namespace dgrad
 
-void g4_dgrad(const at::Tensor& dy, const at::Tensor& w, u16* out, long ldo);
+void g4_dgrad(const at::Tensor& dy, const at::Tensor& w, u16* out, long ldo, const u16* attn_out = nullptr,
+              long ld_attn = 0, float* delta = nullptr);
+
+// dO = dy @ w_o on the 4-wave kernel with flash attention's delta fused into the epilogue: returns (dO [M, N],
+// delta [N / 128, M] fp32 = per-head rowsum(dO . attn_out)), the layout flash_bwd takes (its `delta` argument).
+std::tuple<at::Tensor, at::Tensor> dgrad_gemm_delta(const at::Tensor& dy, const at::Tensor& w,
+                                                    const at::Tensor& attn_out) {
+  SFT_CHECK_CUDA(dy);
+  SFT_CHECK_BF16(dy);
+  SFT_CHECK_BF16(w);
+  SFT_CHECK_BF16(attn_out);
+  SFT_CHECK(dy.dim() == 2 && w.dim() == 2 && attn_out.dim() == 2, "dgrad_gemm_delta: 2-D operands");
+  SFT_CHECK(dy.stride(1) == 1 && w.stride(1) == 1 && attn_out.stride(1) == 1, "dgrad_gemm_delta: contiguous rows");
+  const int64_t M = dy.size(0), K = dy.size(1), N = w.size(1);
+  SFT_CHECK(w.size(0) == K && attn_out.size(0) == M && attn_out.size(1) == N,
+            "dgrad_gemm_delta: dy [M, K] . w [K, N], attn_out [M, N]");
+  SFT_CHECK(M % 256 == 0 && N % 256 == 0 && K % 128 == 0 && K > 0 && K < 8192,
+            "dgrad_gemm_delta: M, N % 256, K % 128, K < 8192 (whole tiles)");
+  SFT_CHECK(dy.stride(0) % 8 == 0 && w.stride(0) % 8 == 0 && (uintptr_t)dy.data_ptr() % 16 == 0 &&
+                (uintptr_t)w.data_ptr() % 16 == 0,
+            "dgrad_gemm_delta: 16-byte aligned rows");
+  auto out = at::empty({M, N}, dy.options());
+  auto delta = at::empty({N / 128, M}, dy.options().dtype(at::kFloat));
+  SFT_TRACE("dgrad.c14.delta");
+  g4_dgrad(dy, w, (u16*)out.data_ptr(), N, (const u16*)attn_out.data_ptr(), attn_out.stride(0),
+           delta.data_ptr<float>());
+  return {out, delta};
+}
 
 // dX = dy @ w (w [K, N]); with gate_up ([M, 2N], the SwiGLU input saved by the forward) the SwiGLU backward
 // is fused: returns dgu [M, 2N] instead of dX. cfg: 14 = the 4-wave ring (csrc/gemm_4w.hip; every plain SmolLM3 /
@@ -615,6 +642,9 @@ at::Tensor dgrad_gemm(const at::Tensor& dy, const at::Tensor& w, const c10::opti
   return out;
 }
 
-TORCH_LIBRARY_IMPL(sftamd, CUDA, m) { m.impl("dgrad_gemm", &dgrad_gemm); }
+TORCH_LIBRARY_IMPL(sftamd, CUDA, m) {
+  m.impl("dgrad_gemm", &dgrad_gemm);
+  m.impl("dgrad_gemm_delta", &dgrad_gemm_delta);
+}
 
 }  // namespace sftamd

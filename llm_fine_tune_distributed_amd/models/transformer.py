@@ -62,9 +62,11 @@ class Attention(nn.Module):
         if self.lora is None and self.use_rope and self.cp_group is None:
             # projection + RoPE (GEMM epilogue) + attention as one autograd node: the backward applies the inverse
             # rotation inside the attention kernels' dq / dK epilogues
+            # the o_proj backward computes the attention backward's delta in its dgrad epilogue (box: the hand-off)
+            box = {}
             a = ops.qkv_rope_attention(h, self.qkv_proj, rope_cs[0], rope_cs[1], cu_seqlens, max_seqlen,
-                                       c.num_attention_heads, c.num_key_value_heads, c.head_dim)
-            return ops.linear(a, self.o_proj)
+                                       c.num_attention_heads, c.num_key_value_heads, c.head_dim, delta_box=box)
+            return ops.attn_out_linear(a, self.o_proj, box)
         if self.lora is not None and self.use_rope and self.cp_group is None:
             # the LoRA-widened qkv GEMM with the RoPE epilogue + attention as one node (inverse RoPE in the backward's
             # dq / dK epilogues), the plain composition where the HIP path does not apply
@@ -84,8 +86,11 @@ class Attention(nn.Module):
             a = ring_attention(qkv, cu_seqlens, max_seqlen, c.num_attention_heads, c.num_key_value_heads, c.head_dim,
                                self.cp_group, layout=self.cp_layout)
         else:
+            box = {} if self.lora is None else None
             a = ops.flash_attention(qkv, cu_seqlens, max_seqlen, c.num_attention_heads, c.num_key_value_heads,
-                                    c.head_dim)
+                                    c.head_dim, delta_box=box)
+            if box is not None:
+                return ops.attn_out_linear(a, self.o_proj, box)
         return ops.linear(a, self.o_proj) if self.lora is None else ops.lora_linear(a, self.o_proj, self.lora["o"])
 
 

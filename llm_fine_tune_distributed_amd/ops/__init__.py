@@ -9,6 +9,7 @@ from .fused import (
     dgrad_mm,
     dropout_add,
     embedding,
+    attn_out_linear,
     flash_attention,
     fuse_swiglu_down,
     linear,
@@ -31,6 +32,6 @@ from .optim_kernels import adamw_flat_, grad_norm_flat, sumsq_list
 
 __all__ = [
     "reference", "load_extension", "use_hip", "hip_disabled", "IGNORE_INDEX", "add_rms_norm", "bump_param_epoch", "decode_attention", "dropout_add",
-    "embedding", "flash_attention", "linear", "linear_rope", "linear_swiglu", "lora_inplace_ok", "lora_linear", "lora_qkv_rope_attention", "lora_swiglu_mlp", "lm_head_cross_entropy", "qkv_rope_attention", "register_param_sync", "rms_norm", "rope_", "swiglu",
+    "attn_out_linear", "embedding", "flash_attention", "linear", "linear_rope", "linear_swiglu", "lora_inplace_ok", "lora_linear", "lora_qkv_rope_attention", "lora_swiglu_mlp", "lm_head_cross_entropy", "qkv_rope_attention", "register_param_sync", "rms_norm", "rope_", "swiglu",
     "swiglu_linear", "swiglu_mlp", "dgrad_mm", "fuse_swiglu_down", "adamw_flat_", "grad_norm_flat", "sumsq_list",
 ]

@@ -217,6 +217,77 @@ def linear(x: torch.Tensor, weight: torch.Tensor) -> torch.Tensor:
     return LinearFn.apply(x, weight)
 
 
+def _delta_ok(dy2d: torch.Tensor, w: torch.Tensor, a2d: torch.Tensor) -> bool:
+    """Shapes dgrad_gemm_delta takes: the 4-wave dgrad (cfg 14) without split-K, a [M, N] attention output with
+    16-byte aligned rows, head_dim 128 (N % 256)."""
+    M, K = dy2d.shape
+    return (_dgrad_ok(dy2d, w) and _dgrad_cfg(dy2d) == 14 and K < 8192 and a2d.dtype == torch.bfloat16
+            and a2d.shape == (M, w.shape[1]) and a2d.stride(1) == 1 and a2d.stride(0) % 8 == 0
+            and a2d.data_ptr() % 16 == 0)
+
+
+class AttnOutLinearFn(Function):
+    """The attention output projection y = a W_o^T behind a fused attention node (QKVRopeAttnFn / FlashAttnFn). Its
+    backward computes dO = dy W_o on the 4-wave kernel with flash attention's delta = rowsum(dO . a) per head in the
+    epilogue (dgrad_gemm_delta: `a` is this node's saved input, the attention output) and leaves it in `box` for the
+    attention node, whose backward then skips its delta kernel (a full re-read of dO and O, ~13 us per layer at
+    16 x 512). The attention node checks that the gradient it receives IS that dO (same storage) before using it."""
+
+    @staticmethod
+    def forward(ctx, x, weight, box):
+        ctx.save_for_backward(x)
+        ctx.weight = weight
+        ctx.box = box
+        x2d = x.reshape(-1, x.shape[-1])
+        return _as_output(fwd_gemm(x2d, weight), x.shape[:-1])
+
+    @staticmethod
+    def backward(ctx, dy):
+        (x,) = ctx.saved_tensors
+        w = ctx.weight
+        dy2d = dy.reshape(-1, dy.shape[-1])
+        x2d = x.reshape(-1, x.shape[-1])
+        dx = dw = None
+        if ctx.needs_input_grad[0]:
+            if ctx.box.get("armed") and _delta_ok(dy2d, w, x2d):
+                d2d, delta = _ext.ops().dgrad_gemm_delta(dy2d, w, x2d)
+                ctx.box["delta"] = (delta, d2d.data_ptr(), d2d.shape)
+            else:
+                d2d = dgrad_mm(dy2d, w)
+            dx = d2d.view(*dy.shape[:-1], w.shape[1])
+        if ctx.needs_input_grad[1]:
+            dw = _accumulate_weight_grad(w, dy2d, x2d)
+        return dx, dw, None
+
+
+# SFTAMD_ATTN_DELTA=0: the attention node computes its own delta (delta kernel); also a test seam
+_DELTA_FUSED = os.environ.get("SFTAMD_ATTN_DELTA", "1") != "0"
+
+
+def attn_out_linear(a: torch.Tensor, weight: torch.Tensor, box: Optional[dict]) -> torch.Tensor:
+    """o_proj(a) for `a` from qkv_rope_attention / flash_attention called with the same `box` (a fresh dict per
+    layer call): the delta hand-off above when the HIP paths apply, linear() otherwise."""
+    if _DELTA_FUSED and box is not None and box.get("armed") and _ext.use_hip(a):
+        return AttnOutLinearFn.apply(a, weight, box)
+    return LinearFn.apply(a, weight)
+
+
+def _take_delta(box: Optional[dict], dout: torch.Tensor, n_q: int):
+    """The delta AttnOutLinearFn left for this attention node, if the incoming gradient is the dO it computed it for
+    (the same storage and shape: no other consumer of the attention output added into it)."""
+    if box is None:
+        return None
+    got = box.pop("delta", None)
+    if got is None:
+        return None
+    delta, ptr, shape = got
+    if dout.data_ptr() != ptr or dout.reshape(-1, dout.shape[-1]).shape != shape or not dout.is_contiguous():
+        return None
+    if delta.shape != (n_q, shape[0]):
+        return None
+    return delta
+
+
 # ----------------------------------------------------------------------------- input-gradient GEMM
 _DGRAD_MODE = os.environ.get("SFTAMD_DGRAD", "auto")  # auto | blas | hip
 
@@ -673,12 +744,15 @@ def rope_(qkv, cos, sin, n_q, n_kv, head_dim):
 # ----------------------------------------------------------------------------- attention
 class FlashAttnFn(Function):
     @staticmethod
-    def forward(ctx, qkv, cu_seqlens, max_seqlen, n_q, n_kv, head_dim, scale, causal):
+    def forward(ctx, qkv, cu_seqlens, max_seqlen, n_q, n_kv, head_dim, scale, causal, box=None):
         ctx.dims = (max_seqlen, n_q, n_kv, head_dim, scale, causal)
+        ctx.box = box
         if _ext.use_hip(qkv):
             out, lse = _ext.ops().flash_fwd(qkv, cu_seqlens, max_seqlen, n_q, n_kv, head_dim, scale, causal)
             ctx.save_for_backward(qkv, cu_seqlens, out, lse)
             ctx.hip = True
+            if box is not None and head_dim == 128:
+                box["armed"] = True
         else:
             out = ref.attention(qkv, n_q, n_kv, head_dim, cu_seqlens, scale, causal)
             ctx.save_for_backward(qkv, cu_seqlens)
@@ -690,7 +764,8 @@ class FlashAttnFn(Function):
         max_seqlen, n_q, n_kv, hd, scale, causal = ctx.dims
         if ctx.hip:
             qkv, cu, out, lse = ctx.saved_tensors
-            dqkv = _ext.ops().flash_bwd(dout.contiguous(), qkv, out, lse, cu, max_seqlen, n_q, n_kv, hd, scale, causal)
+            dqkv = _ext.ops().flash_bwd(dout.contiguous(), qkv, out, lse, cu, max_seqlen, n_q, n_kv, hd, scale, causal,
+                                        _take_delta(ctx.box, dout, n_q))
         else:
             qkv, cu = ctx.saved_tensors
             with torch.enable_grad():
@@ -698,12 +773,15 @@ class FlashAttnFn(Function):
                 o = ref.attention(q, n_q, n_kv, hd, cu, scale, causal)
                 (dq,) = torch.autograd.grad(o, q, dout.float())
             dqkv = dq.to(qkv.dtype)
-        return dqkv, None, None, None, None, None, None, None
+        return dqkv, None, None, None, None, None, None, None, None
 
 
-def flash_attention(qkv, cu_seqlens, max_seqlen, n_q, n_kv, head_dim, scale=None, causal=True):
+def flash_attention(qkv, cu_seqlens, max_seqlen, n_q, n_kv, head_dim, scale=None, causal=True, delta_box=None):
+    """delta_box: a fresh dict shared with attn_out_linear (the o_proj on this output): the o_proj backward computes
+    the attention backward's delta in its dgrad epilogue."""
     scale = scale if scale is not None else 1.0 / math.sqrt(head_dim)
-    return FlashAttnFn.apply(qkv, cu_seqlens, int(max_seqlen), n_q, n_kv, head_dim, float(scale), bool(causal))
+    return FlashAttnFn.apply(qkv, cu_seqlens, int(max_seqlen), n_q, n_kv, head_dim, float(scale), bool(causal),
+                             delta_box)
 
 
 class QKVRopeAttnFn(Function):
@@ -713,7 +791,10 @@ class QKVRopeAttnFn(Function):
     QKVRopeFn + FlashAttnFn (tests/test_model_gpu.py)."""
 
     @staticmethod
-    def forward(ctx, x, weight, cos, sin, cu_seqlens, max_seqlen, n_q, n_kv, head_dim, scale, causal):
+    def forward(ctx, x, weight, cos, sin, cu_seqlens, max_seqlen, n_q, n_kv, head_dim, scale, causal, box=None):
+        ctx.box = box
+        if box is not None:
+            box["armed"] = True
         x2d = x.reshape(-1, x.shape[-1])
         qkv = _ext.ops().gemm_tn_rope(x2d, weight, cos, sin, (n_q + n_kv) * head_dim,
                                       _tn_cfg(x2d.shape[0], weight.shape[0], x2d.shape[1]))
@@ -730,31 +811,32 @@ class QKVRopeAttnFn(Function):
         max_seqlen, n_q, n_kv, hd, scale, causal = ctx.dims
         w = ctx.weight
         dqkv = _ext.ops().flash_bwd_rope(dout.contiguous(), qkv, out, lse, cu, max_seqlen, n_q, n_kv, hd, scale, causal,
-                                         cos, sin)
+                                         cos, sin, _take_delta(ctx.box, dout, n_q))
         del qkv, out, lse
         dx = dw = None
         if ctx.needs_input_grad[0]:
             dx = dgrad_mm(dqkv, w).view(ctx.x_shape)
         if ctx.needs_input_grad[1]:
             dw = _accumulate_weight_grad(w, dqkv, x2d)
-        return dx, dw, None, None, None, None, None, None, None, None, None
+        return dx, dw, None, None, None, None, None, None, None, None, None, None
 
 
 _ROPE_ATTN_FUSED = True  # (a test seam: tests/test_model_gpu.py compares against the two separate nodes)
 
 
-def qkv_rope_attention(x, weight, cos, sin, cu_seqlens, max_seqlen, n_q, n_kv, head_dim, scale=None, causal=True):
+def qkv_rope_attention(x, weight, cos, sin, cu_seqlens, max_seqlen, n_q, n_kv, head_dim, scale=None, causal=True,
+                       delta_box=None):
     """flash_attention(linear_rope(x, W_qkv, cos, sin)) — one fused autograd node when the HIP paths apply
-    (the two separate nodes otherwise)."""
+    (the two separate nodes otherwise). delta_box: see flash_attention."""
     scale = scale if scale is not None else 1.0 / math.sqrt(head_dim)
     x2d = x.reshape(-1, x.shape[-1])
     if (_ROPE_ATTN_FUSED and _TN_MODE in ("1", "rope") and head_dim == 128 and _tn_ok(x2d, weight)
             and cos.dtype == torch.float32 and cos.is_contiguous() and sin.is_contiguous()
             and cos.shape == (x2d.shape[0], 64)):
         return QKVRopeAttnFn.apply(x, weight, cos, sin, cu_seqlens, int(max_seqlen), n_q, n_kv, head_dim,
-                                   float(scale), bool(causal))
+                                   float(scale), bool(causal), delta_box)
     qkv = linear_rope(x, weight, cos, sin, n_q, n_kv, head_dim)
-    return flash_attention(qkv, cu_seqlens, max_seqlen, n_q, n_kv, head_dim, scale, causal)
+    return flash_attention(qkv, cu_seqlens, max_seqlen, n_q, n_kv, head_dim, scale, causal, delta_box)
 
 
 # ----------------------------------------------------------------------------- LM head + CE

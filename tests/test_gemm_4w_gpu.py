@@ -177,3 +177,35 @@ def test_wgrad_4wave_padded_x_pitch(cfg, T, N, K):
     _ext.ops().wgrad_gemm(o1, dy, x, False, cfg, s1)
     _ext.ops().wgrad_gemm(o2, dy, buf[:, :K], False, cfg, s2)
     assert torch.equal(o1, o2) and torch.equal(s1, s2)
+
+
+@pytest.mark.parametrize("M,K,N", [(256, 256, 256), (1024, 2048, 2048), (8192, 2048, 2048), (512, 4096, 4096)])
+def test_dgrad_4wave_attention_delta(M, K, N):
+    """dgrad_gemm_delta (the o_proj input gradient with flash attention's delta in the epilogue): dO bitwise the plain
+    4-wave dgrad, delta [N / 128, M] == per-head rowsum(dO . a) in fp32, and exact on integer data (a head / row
+    mix-up cannot hide)."""
+    torch.manual_seed(7)
+    dy = torch.randn(M, K, device=DEV, dtype=torch.bfloat16)
+    w = (0.05 * torch.randn(K, N, device=DEV)).to(torch.bfloat16)
+    a = torch.randn(M, N, device=DEV, dtype=torch.bfloat16)
+    dx, delta = _ext.ops().dgrad_gemm_delta(dy, w, a)
+    assert torch.equal(dx, _ext.ops().dgrad_gemm(dy, w, None, 14))
+    assert delta.shape == (N // 128, M) and delta.dtype == torch.float32 and delta.is_contiguous()
+    want = (dx.float() * a.float()).view(M, N // 128, 128).sum(-1).t()
+    assert (delta - want).abs().max().item() <= 1e-5 * want.abs().max().item() + 1e-6
+    ramp = (torch.arange(M * K, device=DEV) % 7 - 3).float().view(M, K).to(torch.bfloat16)
+    eye = torch.zeros(K, N, device=DEV)
+    eye[torch.arange(min(K, N)), (torch.arange(min(K, N)) + 5) % N] = 1.0
+    ai = ((torch.arange(M * N, device=DEV) * 13) % 5 - 2).float().view(M, N).to(torch.bfloat16)
+    dxi, di = _ext.ops().dgrad_gemm_delta(ramp, eye.to(torch.bfloat16), ai)
+    exp = ramp.float() @ eye
+    assert torch.equal(dxi.float(), exp)
+    assert torch.equal(di, (exp * ai.float()).view(M, N // 128, 128).sum(-1).t())
+
+
+def test_dgrad_4wave_attention_delta_refuses_split_shapes():
+    """The delta epilogue runs on whole tiles only: a reduction long enough for the hybrid split-K is refused."""
+    dy = torch.randn(256, 8192, device=DEV, dtype=torch.bfloat16)
+    w = torch.randn(8192, 512, device=DEV, dtype=torch.bfloat16)
+    with pytest.raises(RuntimeError):
+        _ext.ops().dgrad_gemm_delta(dy, w, torch.randn(256, 512, device=DEV, dtype=torch.bfloat16))

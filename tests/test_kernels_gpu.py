@@ -266,6 +266,34 @@ def test_flash_attention_smollm3_shape():
     _attn_case([512] * 4, 16, 4, True)
 
 
+@pytest.mark.parametrize("path", ["default", "ds0"])
+def test_flash_bwd_precomputed_delta(path, monkeypatch):
+    """flash_bwd / flash_bwd_rope given delta (as dgrad_gemm_delta's epilogue computes it) skip the delta kernel and
+    match the self-computed backward; a wrongly shaped delta is refused."""
+    monkeypatch.setenv("SFTAMD_ATTN_DS_MB", "0" if path == "ds0" else "")
+    torch.manual_seed(9)
+    D, nq, nkv = 128, 8, 2
+    lens = [300, 17, 512, 129]
+    cu = torch.tensor([0] + list(torch.tensor(lens).cumsum(0)), dtype=torch.int32, device=DEV)
+    M = int(cu[-1])
+    qkv = torch.randn(M, (nq + 2 * nkv) * D, device=DEV, dtype=torch.bfloat16)
+    scale = 1 / math.sqrt(D)
+    out, lse = _ext.ops().flash_fwd(qkv, cu, max(lens), nq, nkv, D, scale, True)
+    dout = torch.randn_like(out)
+    delta = (dout.float() * out.float()).view(M, nq, D).sum(-1).t().contiguous()
+    want = _ext.ops().flash_bwd(dout, qkv, out, lse, cu, max(lens), nq, nkv, D, scale, True)
+    got = _ext.ops().flash_bwd(dout, qkv, out, lse, cu, max(lens), nq, nkv, D, scale, True, delta)
+    assert rel_err(got, want) < 1e-3
+    pos = torch.cat([torch.arange(l) for l in lens]).to(DEV).float()
+    ang = pos[:, None] / (10000 ** (torch.arange(0, 64, device=DEV).float() / 64))[None]
+    cos, sin = ang.cos().contiguous(), ang.sin().contiguous()
+    want_r = _ext.ops().flash_bwd_rope(dout, qkv, out, lse, cu, max(lens), nq, nkv, D, scale, True, cos, sin)
+    got_r = _ext.ops().flash_bwd_rope(dout, qkv, out, lse, cu, max(lens), nq, nkv, D, scale, True, cos, sin, delta)
+    assert rel_err(got_r, want_r) < 1e-3
+    with pytest.raises(RuntimeError):
+        _ext.ops().flash_bwd(dout, qkv, out, lse, cu, max(lens), nq, nkv, D, scale, True, delta.t())
+
+
 @pytest.mark.parametrize("path", ["default", "ds0", "mha"])
 def test_flash_bwd_rope(path, monkeypatch):
     """flash_bwd_rope == inverse-RoPE(flash_bwd): fused into the dq / dK epilogues on the default path (one bf16

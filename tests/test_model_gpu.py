@@ -130,6 +130,48 @@ def test_model_rope_attention_node(mt, monkeypatch):
         assert e < 5e-2, (k, e.item())
 
 
+@pytest.mark.parametrize("mt", ["smollm3", "llama"])
+def test_model_attention_delta_handoff(mt, monkeypatch):
+    """o_proj's backward computing the attention backward's delta in its dgrad epilogue (AttnOutLinearFn, handed to
+    QKVRopeAttnFn / FlashAttnFn through the layer's box) == the attention node's own delta kernel, on RoPE and NoPE
+    layers, and == the fp32 reference."""
+    import llm_fine_tune_distributed_amd.ops.fused as F
+    torch.manual_seed(0)
+    cfg = tiny(mt, hidden_size=512, num_attention_heads=8, num_key_value_heads=2, head_dim=128,
+               intermediate_size=1024, vocab_size=1024, num_hidden_layers=4)
+    m = build_model(cfg, device="cuda", dtype=torch.bfloat16, seed=1)
+    ids = torch.randint(0, 1024, (4, 256), device="cuda")
+    labels = ids.clone()
+    labels[:, 200:] = -100
+    n = {"delta": 0, "used": 0}
+    orig_op, orig_take = F.AttnOutLinearFn.apply, F._take_delta
+
+    def op(*a):
+        n["delta"] += 1
+        return orig_op(*a)
+
+    def take(*a):
+        d = orig_take(*a)
+        n["used"] += d is not None
+        return d
+
+    monkeypatch.setattr(F.AttnOutLinearFn, "apply", op)
+    monkeypatch.setattr(F, "_take_delta", take)
+    monkeypatch.setattr(F, "_DELTA_FUSED", True)
+    l_f, g_f = _run(m, ids, labels, True)
+    assert n["delta"] == 4 and n["used"] == 4, n  # every layer, NoPE layer 3 included
+    monkeypatch.setattr(F, "_DELTA_FUSED", False)
+    l_s, g_s = _run(m, ids, labels, True)
+    assert n["delta"] == 4 and n["used"] == 4, n
+    l_r, g_r = _run(m, ids, labels, False)
+    assert torch.equal(l_f, l_s)  # same forward kernels
+    for k in g_s:
+        e = (g_f[k] - g_s[k]).norm() / (g_s[k].norm() + 1e-12)
+        assert e < 1e-2, (k, e.item())
+        e = (g_f[k] - g_r[k]).norm() / (g_r[k].norm() + 1e-12)
+        assert e < 5e-2, (k, e.item())
+
+
 def test_lora_wide_gpu_matches_unfused():
     from llm_fine_tune_distributed_amd.models.lora import LoRAConfig, apply_lora
     import llm_fine_tune_distributed_amd.models.transformer as T

@@ -7,7 +7,7 @@ error against the first variant.
     python tools/bench_ab.py wgrad lm_head 10,1214 --rounds 5
 
 wgrad: dW[N, K] = dy[T, N]^T x[T, K] (sftamd.wgrad_gemm cfg); fwd: y[T, N] = x[T, K] W[N, K]^T (sftamd.gemm_tn cfg); dgrad: dX[T, N] = dy[T, K] W[K, N] (sftamd.dgrad_gemm cfg;
-'blas' = torch.mm on the TunableOp selection). SmolLM3-3B shapes at T = 8192 tokens.
+'blas' = torch.mm on the TunableOp selection; 'delta' = dgrad_gemm_delta). SmolLM3-3B shapes at T = 8192 tokens.
 """
 import argparse
 import json
@@ -81,8 +81,15 @@ def main():
             w = (0.02 * torch.randn(K, N, device="cuda")).to(torch.bfloat16)
             holder = [None]
 
-            def run(v):
-                holder[0] = torch.mm(dy, w) if v == "blas" else ops.dgrad_gemm(dy, w, None, int(v))
+            a_out = torch.randn(T, N, device="cuda", dtype=torch.bfloat16)
+
+            def run(v):  # 'delta': cfg 14 with flash attention's delta in the epilogue (dgrad_gemm_delta)
+                if v == "blas":
+                    holder[0] = torch.mm(dy, w)
+                elif v == "delta":
+                    holder[0] = ops.dgrad_gemm_delta(dy, w, a_out)[0]
+                else:
+                    holder[0] = ops.dgrad_gemm(dy, w, None, int(v))
                 return holder[0]
         ref = run(variants[0]).float().clone()
         errs = {}
