@@ -44,7 +44,8 @@ def timeit(fn, n=20):
     return statistics.median(ts)
 
 
-# "ds": the default backward (materialised dS^T + dq32); "dq3": the recompute path used past the dS^T budget
+# "ds": the default backward (materialised dS^T + dq32) incl. the delta kernel; "dsd": the same with delta given;
+# "dq3": the recompute path used past the dS^T budget
 CFGS = os.environ.get("CFGS", "ds,dq3").split(",")
 res = {}
 ref = None
@@ -60,7 +61,9 @@ for rnd in range(int(os.environ.get("ROUNDS", 3))):
             ed = ((dq.float() - ref[1]).norm() / ref[1].norm()).item()
             assert eo < 1e-2 and ed < 1e-2, (cfg, eo, ed)
         tf = timeit(lambda: ops.flash_fwd(qkv, cu, T, NQ, NKV, D, sc, True))
-        tb = timeit(lambda: ops.flash_bwd(dout, qkv, out, lse, cu, T, NQ, NKV, D, sc, True))
+        # "dsd": delta precomputed (the default training path: dgrad_gemm_delta's epilogue makes it), not timed here
+        dl = (dout.float() * out.float()).view(M, NQ, D).sum(-1).t().contiguous() if cfg == "dsd" else None
+        tb = timeit(lambda: ops.flash_bwd(dout, qkv, out, lse, cu, T, NQ, NKV, D, sc, True, dl))
         res.setdefault(cfg, []).append((tf, tb))
 for cfg, v in res.items():
     tf = statistics.median(x[0] for x in v)
