@@ -234,9 +234,21 @@ def run(a):
 
     from llm_fine_tune_distributed_amd.utils.faults import maybe_inject, nan_injection
     n_step = [0]
+    # diagnostic (not a benchmark setting): SFTAMD_BENCH_HOG_CUS=R holds R CUs on a side stream for the first
+    # SFTAMD_BENCH_HOG_US (default 100 ms) of every step — a one-GPU stand-in for the RCCL channel blocks that sit on
+    # CUs while collectives overlap compute at N > 1 (tools/bench_cu_contention.py, profiles/r6_cu_contention.md)
+    hog_cus = int(os.environ.get("SFTAMD_BENCH_HOG_CUS", "0")) if on_gpu else 0
+    if hog_cus > 0:
+        from llm_fine_tune_distributed_amd.ops import _ext as _hx
+        hog_stream = torch.cuda.Stream()
+        hog_sink = torch.zeros(256, device=st.device, dtype=torch.int32)
+        hog_us = float(os.environ.get("SFTAMD_BENCH_HOG_US", "100000"))
 
     def step():
         n_step[0] += 1
+        if hog_cus > 0:
+            with torch.cuda.stream(hog_stream):
+                _hx.ops().cu_hog(hog_sink, hog_cus, hog_us)
         maybe_inject(st.rank, n_step[0])  # SFTAMD_FAULT_INJECT=rank:step (launcher teardown test)
         if nan_injection(st.rank, n_step[0]):  # SFTAMD_FAULT_INJECT=rank:step:nan (the non-finite-loss exit test)
             with torch.no_grad():

@@ -28,6 +28,7 @@ void ddp_tracker_destroy(int64_t id);
 // csrc/dispatch_trace.cpp
 void dispatch_trace(bool on);
 std::string dispatch_trace_read();
+int64_t set_cu_budget(int64_t n);
 }
 
 TORCH_LIBRARY(sftamd, m) {
@@ -53,10 +54,12 @@ TORCH_LIBRARY(sftamd, m) {
   // runtime: dispatch trace of the kernel variants launched (tests assert the default paths)
   m.def("dispatch_trace(bool on) -> ()", &sftamd::dispatch_trace);
   m.def("dispatch_trace_read() -> str", &sftamd::dispatch_trace_read);
+  m.def("set_cu_budget(int n) -> int", &sftamd::set_cu_budget);
   // norms / elementwise
   m.def("rmsnorm_fwd(Tensor x, Tensor? residual, Tensor weight, float eps, int y_ld=0) -> (Tensor, Tensor, Tensor)");
   m.def("rmsnorm_bwd(Tensor dy, Tensor h, Tensor weight, Tensor rstd, Tensor? dres, Tensor(a!)? dw_out=None, bool accumulate=False) -> (Tensor, Tensor)");
   m.def("swiglu_fwd(Tensor gate_up) -> Tensor");
+  m.def("cu_hog(Tensor(a!) sink, int blocks, float usec) -> ()");
   m.def("swiglu_bwd(Tensor dy, Tensor gate_up) -> Tensor");
   m.def("rope_(Tensor(a!) qkv, Tensor cos, Tensor sin, int n_q, int n_kv, int head_dim, bool inverse) -> ()");
   m.def("embedding_fwd(Tensor ids, Tensor weight) -> Tensor");

@@ -9,6 +9,8 @@
 #include <hip/hip_runtime.h>
 #include <torch/library.h>
 
+#include "cu_budget.h"
+
 #include <cstdint>
 #include <string>
 
@@ -95,7 +97,7 @@ inline unsigned drop_thresh16(double p, float* scale) {
 
 inline hipStream_t cur_stream() { return c10::hip::getCurrentHIPStream().stream(); }
 
-inline int num_cus() { return 256; }  // MI355X: 8 XCDs x 32 CUs
+inline int num_cus() { return kNumCUs; }
 
 #define SFT_CHECK(cond, ...) TORCH_CHECK(cond, "sftamd: ", __VA_ARGS__)
 #define SFT_CHECK_CUDA(t) SFT_CHECK((t).is_cuda(), #t " must be a GPU tensor")

@@ -2,10 +2,14 @@
 // counted while enabled. Tests use it to assert that the SHIPPED default paths run (tests/test_default_path_gpu.py);
 // it costs one relaxed atomic load per launch when off.
 #include <atomic>
+#include <cstdint>
 #include <map>
 #include <mutex>
 #include <sstream>
+#include <stdexcept>
 #include <string>
+
+#include "cu_budget.h"
 
 namespace sftamd {
 
@@ -32,6 +36,13 @@ std::string dispatch_trace_read() {
   std::ostringstream os;
   for (const auto& kv : g_trace_counts) os << kv.first << '=' << kv.second << ';';
   return os.str();
+}
+
+// set_cu_budget(n): the CU count the split / hybrid GEMM grids assume (0 = all); returns the effective budget.
+int64_t set_cu_budget(int64_t n) {
+  if (n < 0 || n > kNumCUs) throw std::invalid_argument("sftamd: set_cu_budget: 0..256");
+  cu_budget_slot() = (int)n;
+  return cu_budget();
 }
 
 }  // namespace sftamd

@@ -388,7 +388,40 @@ std::tuple<at::Tensor, at::Tensor> lora_widen(const at::Tensor& x, int64_t R, do
   return {X, xd};
 }
 
+// ------------------------------------------------------------------------------ CU occupancy probe (tools only)
+// cu_hog(sink, blocks, usec): `blocks` workgroups that each hold one CU (81 KB of LDS: one per CU) and sleep until `usec`
+// of wall time (s_memrealtime, 100 MHz) have passed — a stand-in for the RCCL channel blocks that sit on CUs while a
+// collective overlaps the backward (tools/bench_cu_contention.py measures what the GEMM grids lose to them). Every wave
+// exits at the deadline (usec is capped at 2 s).
+__global__ __launch_bounds__(256) void cu_hog_kernel(unsigned long long ticks, int* __restrict__ sink) {
+  extern __shared__ int hog_lds[];
+  const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+  int n = 0;
+  while (__builtin_amdgcn_s_memrealtime() - t0 < ticks) {
+    __builtin_amdgcn_s_sleep(16);
+    ++n;
+  }
+  hog_lds[threadIdx.x] = n;
+  __syncthreads();
+  if (n < 0) sink[threadIdx.x] = hog_lds[255 - threadIdx.x];  // never taken: keeps the LDS allocation live
+}
+
+void cu_hog(at::Tensor sink, int64_t blocks, double usec) {
+  SFT_CHECK(blocks > 0 && blocks <= 4096 && usec > 0, "cu_hog: 1..4096 blocks, usec > 0");
+  SFT_CHECK(sink.is_cuda() && sink.scalar_type() == at::kInt && sink.numel() >= 256, "cu_hog: int32 sink of 256");
+  constexpr int LDS = 81 * 1024;
+  static bool attr = [] {
+    return hipFuncSetAttribute((const void*)cu_hog_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, LDS) ==
+           hipSuccess;
+  }();
+  SFT_CHECK(attr, "cu_hog: could not raise the dynamic LDS limit");
+  const double us = std::min(usec, 2.0e6);
+  cu_hog_kernel<<<(unsigned)blocks, 256, LDS, cur_stream()>>>((unsigned long long)(us * 100.0), sink.data_ptr<int>());
+  SFT_LAUNCH_CHECK();
+}
+
 TORCH_LIBRARY_IMPL(sftamd, CUDA, m) {
+  m.impl("cu_hog", &cu_hog);
   m.impl("dropout_add", &dropout_add);
   m.impl("lora_widen", &lora_widen);
   m.impl("swiglu_fwd", &swiglu_fwd);

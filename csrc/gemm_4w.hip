@@ -434,7 +434,8 @@ void g4_wgrad(const at::Tensor& dy, const at::Tensor& x, at::Tensor& out, bool a
   const int tiles = (N / 256) * (K / 256);
   if (splits < 1) splits = 1;
   splits = std::min(splits, T / 128);
-  const int ndp = splits <= 1 ? tiles : (hybrid ? tiles / 256 * 256 : 0);
+  const int B = cu_budget();  // one round = B workgroups (csrc/cu_budget.h)
+  const int ndp = splits <= 1 ? tiles : (hybrid ? tiles / B * B : 0);
   const int nsk = tiles - ndp;
   const long slots = (long)ndp * 8 + (long)nsk * 32;
   SFT_CHECK(nrm == nullptr || slots <= nrm_cap, "wgrad_gemm: norm slot buffer too small");
@@ -475,6 +476,7 @@ void g4_dgrad(const at::Tensor& dy, const at::Tensor& w, u16* out, long ldo, con
     SFT_CHECK(attn_out != nullptr && ld_attn % 8 == 0 && (uintptr_t)attn_out % 16 == 0,
               "dgrad 4-wave delta: 16-byte aligned attention output rows");
     SFT_CHECK(K < 8192 || (M / 256) * (N / 256) % 256 == 0, "dgrad 4-wave delta: whole tiles only (no split-K)");
+    // (and no budget split below: the delta epilogue needs whole tiles)
     ea.flags = 4;
     ea.O = attn_out;
     ea.Dl = delta;
@@ -483,9 +485,13 @@ void g4_dgrad(const at::Tensor& dy, const at::Tensor& w, u16* out, long ldo, con
   }
   const int nbm = M / 256, nbn = N / 256, tiles = nbm * nbn;
   int ndp = tiles, splits = 1;
-  if (tiles % 256 != 0 && K >= 8192) {  // short reductions: the fixup costs more
-    const int rest = tiles > 256 ? tiles % 256 : tiles;
-    const int s = std::min(std::min(256 / rest, 8), K / 128);
+  // one round = B workgroups (csrc/cu_budget.h). Short reductions split their leftover round only under a reduced
+  // budget (B < 256: the leftover tiles would otherwise wait a whole tile time on the CUs other work holds); with the
+  // whole chip the fixup costs more than the partial round
+  const int B = cu_budget();
+  if (delta == nullptr && tiles % B != 0 && (K >= 8192 || (B < num_cus() && tiles > B))) {
+    const int rest = tiles > B ? tiles % B : tiles;
+    const int s = std::min(std::min(B / rest, 8), K / 128);
     if (s >= 2) {
       ndp = tiles - rest;
       splits = s;

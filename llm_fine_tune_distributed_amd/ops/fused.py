@@ -45,6 +45,37 @@ def _weight_grad_done(param: torch.Tensor) -> None:
 _WGRAD_MODE = os.environ.get("SFTAMD_WGRAD", "auto")  # auto | blas | <cfg int> (kernel variant)
 
 
+_NUM_CUS = 256  # MI355X: 8 XCDs x 32 CUs
+
+
+def _budget_from_env() -> int:
+    try:
+        b = int(os.environ.get("SFTAMD_CU_BUDGET", "0") or 0)
+    except ValueError:
+        b = 0
+    return b if 0 < b < _NUM_CUS else _NUM_CUS
+
+
+_CU_BUDGET = _budget_from_env()  # the C++ side reads the same variable (csrc/cu_budget.h)
+
+
+def set_cu_budget(n: int) -> int:
+    """The CU count the one-round GEMM grids are sized for (0 = all 256). When collectives overlap compute at N > 1,
+    RCCL's channel blocks hold some CUs and a grid of exactly 256 one-per-CU workgroups waits a second round for
+    them (sftamd.cu_hog measurements, profiles/r6_cu_contention.md); with a budget the split / hybrid decisions of
+    the 4-wave GEMMs (here and in csrc/gemm_4w.hip) leave that many CUs free. Returns the effective budget."""
+    global _CU_BUDGET
+    b = int(n) if 0 < int(n) < _NUM_CUS else _NUM_CUS
+    if _ext.load():
+        b = int(_ext.ops().set_cu_budget(0 if b == _NUM_CUS else b))
+    _CU_BUDGET = b
+    return b
+
+
+def cu_budget() -> int:
+    return _CU_BUDGET
+
+
 def _wgrad_cfg(T: int, N: int, K: int) -> int:
     """Which wgrad GEMM runs dW[N,K] = dy[T,N]^T x[T,K]: 0 = hipBLASLt/rocBLAS, else a csrc/gemm_wgrad.hip cfg
     (1000 H + 100 S + c). From interleaved A/Bs on MI355X at T = 8192 (tools/bench_ab.py, profiles/r6_gemm_routing.md):
@@ -59,11 +90,12 @@ def _wgrad_cfg(T: int, N: int, K: int) -> int:
     if _WGRAD_MODE not in ("auto", ""):
         return int(_WGRAD_MODE)
     tiles = (N // 256) * (K // 256)
+    B = _CU_BUDGET  # one round of workgroups (256 unless collectives hold CUs: set_cu_budget)
     if N % 256 == 0 and K % 256 == 0 and T % 128 == 0:
-        if tiles < 256:
-            s = min(8, 256 // tiles, T // 128)
+        if tiles < B:
+            s = min(8, B // tiles, T // 128)
             return 100 * s + 14 if s >= 2 else 14
-        if (tiles < 512 or tiles >= 2048) and tiles % 256 and T // 128 >= 2:
+        if (tiles < 2 * B or tiles >= 8 * B) and tiles % B and T // 128 >= 2:
             return 1214
         return 14
     if N % 256 == 0 and K % 256 == 0 and tiles >= 512:
@@ -221,7 +253,11 @@ def _delta_ok(dy2d: torch.Tensor, w: torch.Tensor, a2d: torch.Tensor) -> bool:
     """Shapes dgrad_gemm_delta takes: the 4-wave dgrad (cfg 14) without split-K, a [M, N] attention output with
     16-byte aligned rows, head_dim 128 (N % 256)."""
     M, K = dy2d.shape
+    tiles = (M // 256) * (w.shape[1] // 256)
+    # (under a reduced CU budget a partial last round is split over K, which the delta epilogue cannot take: the
+    # attention node's own delta kernel is cheaper than a second round of whole tiles)
     return (_dgrad_ok(dy2d, w) and _dgrad_cfg(dy2d) == 14 and K < 8192 and a2d.dtype == torch.bfloat16
+            and (_CU_BUDGET >= _NUM_CUS or tiles % _CU_BUDGET == 0 or tiles < _CU_BUDGET)
             and a2d.shape == (M, w.shape[1]) and a2d.stride(1) == 1 and a2d.stride(0) % 8 == 0
             and a2d.data_ptr() % 16 == 0)
 

@@ -209,3 +209,37 @@ def test_dgrad_4wave_attention_delta_refuses_split_shapes():
     w = torch.randn(8192, 512, device=DEV, dtype=torch.bfloat16)
     with pytest.raises(RuntimeError):
         _ext.ops().dgrad_gemm_delta(dy, w, torch.randn(256, 512, device=DEV, dtype=torch.bfloat16))
+
+
+def test_4wave_grids_under_a_cu_budget():
+    """set_cu_budget(248) (collectives holding CUs at N > 1, profiles/r6_cu_contention.md): a 256-tile input gradient
+    with a short reduction splits its leftover 8 tiles over K, the hybrid weight gradient whole-rounds 248 tiles; both
+    == the fp32 reference and deterministic; the delta epilogue still runs on whole tiles (no split)."""
+    from llm_fine_tune_distributed_amd import ops
+    torch.manual_seed(11)
+    try:
+        assert ops.set_cu_budget(248) == 248
+        dy = torch.randn(4096, 2048, device=DEV, dtype=torch.bfloat16)
+        w = (0.05 * torch.randn(2048, 4096, device=DEV)).to(torch.bfloat16)
+        _ext.ops().dispatch_trace(True)
+        try:
+            out = _ext.ops().dgrad_gemm(dy, w, None, 14)
+        finally:
+            _ext.ops().dispatch_trace(False)
+        assert "dgrad.splitk" in _ext.ops().dispatch_trace_read()
+        assert rel_err(out, dy.float() @ w.float()) < 5e-3
+        assert torch.equal(out, _ext.ops().dgrad_gemm(dy, w, None, 14))
+        a = torch.randn(4096, 4096, device=DEV, dtype=torch.bfloat16)
+        dx, delta = _ext.ops().dgrad_gemm_delta(dy, w, a)
+        assert rel_err(dx, dy.float() @ w.float()) < 5e-3
+        want = (dx.float() * a.float()).view(4096, 32, 128).sum(-1).t()
+        assert (delta - want).abs().max().item() <= 1e-5 * want.abs().max().item() + 1e-6
+        T, N, K = 1024, 2048, 11008 // 256 * 256  # 8 x 43 = 344 tiles: 248 whole + 96 split 2 ways
+        dyw = torch.randn(T, N, device=DEV, dtype=torch.bfloat16)
+        x = torch.randn(T, K, device=DEV, dtype=torch.bfloat16)
+        o = torch.empty(N, K, device=DEV, dtype=torch.bfloat16)
+        _ext.ops().wgrad_gemm(o, dyw, x, False, 1214)
+        assert rel_err(o, dyw.float().t() @ x.float()) < 5e-3
+    finally:
+        ops.set_cu_budget(0)
+    assert ops.cu_budget() == 256

@@ -26,3 +26,18 @@ def test_shipped_selections_cover_the_headline_shapes():
     shapes = _tuned_tn(gemm_tuning._DEFAULT)
     assert os.path.exists(gemm_tuning._DEFAULT)
     assert all(len(s) == 3 for s in shapes)
+
+
+def test_wgrad_routing_under_a_cu_budget(monkeypatch):
+    """The split decisions of the 4-wave weight gradients follow the CU budget (ops.set_cu_budget): o_proj's 64 tiles
+    split 3 ways (192 workgroups) instead of 4 (256) when 8 CUs are reserved; the other SmolLM3 shapes keep theirs."""
+    import llm_fine_tune_distributed_amd.ops.fused as F
+    shapes = {"o": (2048, 2048), "qkv": (3072, 2048), "down": (2048, 11008), "lm_head": (128256, 2048),
+              "gate_up": (22016, 2048)}
+    monkeypatch.setattr(F, "_WGRAD_MODE", "auto")
+    monkeypatch.setattr(F, "_CU_BUDGET", 256)
+    assert {k: F._wgrad_cfg(8192, n, kk) for k, (n, kk) in shapes.items()} == {
+        "o": 414, "qkv": 214, "down": 1214, "lm_head": 1214, "gate_up": 14}
+    monkeypatch.setattr(F, "_CU_BUDGET", 248)
+    assert {k: F._wgrad_cfg(8192, n, kk) for k, (n, kk) in shapes.items()} == {
+        "o": 314, "qkv": 214, "down": 1214, "lm_head": 1214, "gate_up": 14}
