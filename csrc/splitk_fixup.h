@@ -65,62 +65,4 @@ __global__ void __launch_bounds__(256) splitk_fixup_kernel(const float* __restri
   }
 }
 
-// Stream-K fixup (gemm_4w.hip g4_kernel, splits < 0): tiles t = 0 .. ntiles - 1 past tile0, each nb K-tile pairs deep;
-// workgroup j of nsk owns pairs [j tot / nsk, (j + 1) tot / nsk) of the concatenated tiles (tot = ntiles nb) and wrote
-// slab 2 j for the first tile its range touches, 2 j + 1 for the second. C[tile0 + t] = bf16(sum over the workgroups
-// touching t, in workgroup order (+ C when accumulating)): deterministic. Norm slots and the parked whole-tile partials
-// as splitk_fixup_kernel (32 per tile, one per fixup block; the parked ones past the 2 nsk slabs).
-template <int BM, int BN>
-__global__ void __launch_bounds__(256) streamk_fixup_kernel(const float* __restrict__ P, u16* __restrict__ C, int tile0,
-                                                            int ntiles, int nb, int nsk, int nbk, int K, int accumulate,
-                                                            float* __restrict__ nrm, int nbm, int group) {
-  constexpr int E8 = BM * BN / 8;
-  static_assert((BM * BN / 8) % 256 == 0, "fixup blocks cover whole tiles");
-  if (nrm != nullptr && blockIdx.x == 0) {
-    const float* src = P + 2L * nsk * BM * BN;
-    for (int i = threadIdx.x; i < tile0 * 8; i += 256) nrm[i] = src[i];
-  }
-  const long idx = (long)blockIdx.x * 256 + threadIdx.x;
-  if (idx >= (long)ntiles * E8) return;  // never taken: the grid covers whole tiles
-  const int t = (int)(idx / E8), e = (int)(idx - (long)t * E8) * 8;
-  const int row = e / BN, col = e - row * BN;
-  const long tot = (long)ntiles * nb, lo = (long)t * nb, hi = lo + nb;
-  int j = (int)(lo * nsk / tot);  // the workgroup whose range holds pair lo: start(j) <= lo < start(j + 1)
-  while (j > 0 && (long)j * tot / nsk > lo) --j;
-  while ((long)(j + 1) * tot / nsk <= lo) ++j;
-  float v[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-  for (; j < nsk; ++j) {
-    const long sj = (long)j * tot / nsk;
-    if (sj >= hi) break;
-    const float* q = P + ((long)j * 2 + (sj < lo ? 1 : 0)) * BM * BN + e;
-    const float4 a = *(const float4*)q, b = *(const float4*)(q + 4);
-    v[0] += a.x; v[1] += a.y; v[2] += a.z; v[3] += a.w;
-    v[4] += b.x; v[5] += b.y; v[6] += b.z; v[7] += b.w;
-  }
-  const int tile = tile0 + t;
-  const int per_group = group * nbk, grp = tile / per_group, first = grp * group;
-  const int gsz = min(nbm - first, group), in = tile - grp * per_group;
-  const int bn = first + in % gsz, bk = in / gsz;
-  u16* out = C + (long)(bn * BM + row) * K + bk * BN + col;
-  if (accumulate) {
-    float o[8];
-    unpack8(*(const uint4*)out, o);
-#pragma unroll
-    for (int i = 0; i < 8; ++i) v[i] += o[i];
-  }
-  const uint4 pk = pack8(v);
-  *(uint4*)out = pk;
-  if (nrm != nullptr) {
-    float r[8], ss = 0.f;
-    unpack8(pk, r);
-#pragma unroll
-    for (int i = 0; i < 8; ++i) ss += r[i] * r[i];
-    ss = wave_sum(ss);
-    __shared__ float red[4];
-    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = ss;
-    __syncthreads();
-    if (threadIdx.x == 0) nrm[(long)tile0 * 8 + blockIdx.x] = red[0] + red[1] + red[2] + red[3];
-  }
-}
-
 }  // namespace sftamd

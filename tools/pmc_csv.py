@@ -1,7 +1,7 @@
 """Summarise rocprofv3 --pmc counter_collection.csv files: per kernel-name substring, the mean of every counter over
 its dispatches (the first warmup dispatches of pmc_tn.py are included; they are identical work).
 
-    python tools/pmc_csv.py <csv> [<csv> ...] --match tn4_kernel,Cijk
+    python tools/pmc_csv.py <csv> [<csv> ...] --match g4_kernel,Cijk
 """
 import argparse
 import csv
