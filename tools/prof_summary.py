@@ -11,11 +11,19 @@ import sqlite3
 from collections import defaultdict
 
 
-def load_db(path):
+def load_db(path, window=None):
+    """window = (regex, skip): keep only the kernels that start after the end of the skip-th kernel whose name
+    matches regex and end before the end of the last one (e.g. "adamw_kernel", 2 x warmup steps: the timed steps)."""
     c = sqlite3.connect(path)
     cols = [r[1] for r in c.execute("pragma table_info(kernels)")]
     name_col = "kernel_name" if "kernel_name" in cols else ("name" if "name" in cols else None)
-    rows = c.execute(f"select {name_col}, start, end from kernels").fetchall()
+    rows = c.execute(f"select {name_col}, start, end from kernels order by start").fetchall()
+    if window is not None:
+        rx, skip = re.compile(window[0]), window[1]
+        marks = [e for n, s, e in rows if rx.search(n)]
+        if len(marks) > skip:
+            lo, hi = marks[skip - 1] if skip > 0 else rows[0][1], marks[-1]
+            rows = [(n, s, e) for n, s, e in rows if s >= lo and e <= hi]
     return [(n, (e - s) / 1e3) for n, s, e in rows]  # us
 
 
@@ -39,8 +47,11 @@ def main():
     ap.add_argument("--top", type=int, default=40)
     ap.add_argument("--out")
     ap.add_argument("--title", default="rocprofv3 kernel summary")
+    ap.add_argument("--window", nargs=2, metavar=("REGEX", "SKIP"),
+                    help="only kernels between the end of the SKIP-th REGEX kernel and the end of the last one")
     a = ap.parse_args()
-    rows = load_db(a.path) if a.path.endswith(".db") else load_csv(a.path)
+    win = (a.window[0], int(a.window[1])) if a.window else None
+    rows = load_db(a.path, win) if a.path.endswith(".db") else load_csv(a.path)
     agg = defaultdict(lambda: [0, 0.0, 0.0])
     for n, us in rows:
         k = short(n)
