@@ -351,12 +351,25 @@ __device__ __forceinline__ void tile_origin(int tile, int nbm, int nbn, int grou
   n0 = (in / gsz) * 256;
 }
 
-// splits > 1: the tiles past ndp are split into `splits` equal ranges of 128-deep blocks (pieces -> fp32 slabs,
+// One GEMM of a launch: operands, tile grid (nbm x nbn tiles of 256 x 256, GROUP-blocked order), epilogue; park =
+// where this problem's whole tiles put their norm partials past P (a split launch's slabs), 0 = straight into P.
+struct Prob {
+  const u16* A;
+  const u16* B;
+  long lda, ldb;
+  int nbm, nbn, group;
+  long park;
+  Epi ea;
+};
+
+// A launch runs one problem or two with the same reduction length (tiles [0, tiles0) = p0, the rest = p1, e.g. the
+// MLP's down and gate_up weight gradients as ONE grid: 344 + 688 = 1032 tiles = 4.03 rounds of 256 CUs instead of
+// 1.34 + 2.69 — a partial last round costs most of a full one, profiles/r6_gemm_routing.md). splits > 1: the tiles
+// past ndp (all in the last problem) are split into `splits` equal ranges of 128-deep blocks (pieces -> fp32 slabs,
 // splitk_fixup_kernel).
 template <int LA, int LB>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1)))
-g4_kernel(const u16* __restrict__ A, const u16* __restrict__ B, long lda, long ldb, int kred, int nbm, int nbn,
-          int group, int ndp, int splits, Epi ea) {
+g4_kernel(Prob q0, Prob q1, int tiles0, int kred, int ndp, int splits) {
   __shared__ __attribute__((aligned(16))) char smem[4 * SLOT32];
   // Blocks [0, ndp) own whole tiles, XCD-aware bijective remap among them (consecutive ids on one XCD: shared L2 for
   // the GROUP-blocked tile order); blocks >= ndp are the split pieces. Classes by BLOCK index, not by remapped id:
@@ -377,8 +390,23 @@ g4_kernel(const u16* __restrict__ A, const u16* __restrict__ B, long lda, long l
     p0 = (int)((long)sk * nb_all / splits);
     p1 = (int)((long)(sk + 1) * nb_all / splits);
   }
+  // the problem this tile belongs to (wave-uniform selects of kernel arguments)
+  const bool sec = tile >= tiles0;
+  const int lt = sec ? tile - tiles0 : tile;
+  const u16* A = sec ? q1.A : q0.A;
+  const u16* B = sec ? q1.B : q0.B;
+  const long lda = sec ? q1.lda : q0.lda, ldb = sec ? q1.ldb : q0.ldb, park = sec ? q1.park : q0.park;
+  Epi ea;
+  ea.C = sec ? q1.ea.C : q0.ea.C;
+  ea.P = sec ? q1.ea.P : q0.ea.P;
+  ea.ldc = sec ? q1.ea.ldc : q0.ea.ldc;
+  ea.flags = sec ? q1.ea.flags : q0.ea.flags;
+  ea.O = sec ? q1.ea.O : q0.ea.O;
+  ea.Dl = sec ? q1.ea.Dl : q0.ea.Dl;
+  ea.ldO = sec ? q1.ea.ldO : q0.ea.ldO;
+  ea.dM = sec ? q1.ea.dM : q0.ea.dM;
   int m0, n0;
-  tile_origin(tile, nbm, nbn, group, m0, n0);
+  tile_origin(lt, sec ? q1.nbm : q0.nbm, sec ? q1.nbn : q0.nbn, sec ? q1.group : q0.group, m0, n0);
   const int tid = threadIdx.x, lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = w >> 1, wn = w & 1;
   const long k0 = (long)p0 * 4 * BK32;
@@ -403,21 +431,41 @@ g4_kernel(const u16* __restrict__ A, const u16* __restrict__ B, long lda, long l
     return;
   }
   float* nrm = nullptr;
-  if (ea.flags & 2)  // whole tiles of a split launch park theirs past the slabs
-    nrm = (splits <= 1 ? ea.P : ea.P + (long)(gridDim.x - ndp) * 65536) + tile * 8 + w;
+  if (ea.flags & 2)  // whole tiles of a split problem park theirs past the slabs (park > 0)
+    nrm = ea.P + park + lt * 8 + w;
   store_tile(acc, ea, m0 + 128 * wm, n0 + 128 * wn, lane, nrm);
 }
 
 static int group_m() { return 8; }  // GROUP_M tile order
 
+static Prob prob(const u16* A, long lda, const u16* B, long ldb, int M, int N, const Epi& ea, long park) {
+  Prob p;
+  p.A = A;
+  p.B = B;
+  p.lda = lda;
+  p.ldb = ldb;
+  p.nbm = M / 256;
+  p.nbn = N / 256;
+  p.group = std::min(group_m(), p.nbm);
+  p.park = park;
+  p.ea = ea;
+  return p;
+}
+
+template <int LA, int LB>
+static void launch2(const Prob& q0, const Prob& q1, int tiles0, int total, int kred, int ndp, int splits) {
+  const int grid = ndp + (total - ndp) * splits;
+  g4_kernel<LA, LB><<<grid, 256, 0, cur_stream()>>>(q0, q1, tiles0, kred, ndp, splits);
+  SFT_LAUNCH_CHECK();
+}
+
 template <int LA, int LB>
 static void launch(const u16* A, long lda, const u16* B, long ldb, int M, int N, int kred, int ndp, int splits,
                    const Epi& ea) {
-  const int nbm = M / 256, nbn = N / 256, tiles = nbm * nbn;
-  const int grid = ndp + (tiles - ndp) * splits;
-  g4_kernel<LA, LB><<<grid, 256, 0, cur_stream()>>>(A, B, lda, ldb, kred, nbm, nbn, std::min(group_m(), nbm), ndp,
-                                                     splits, ea);
-  SFT_LAUNCH_CHECK();
+  const int tiles = (M / 256) * (N / 256);
+  const long park = splits > 1 ? (long)(tiles - ndp) * splits * 65536 : 0;
+  const Prob q = prob(A, lda, B, ldb, M, N, ea, park);
+  launch2<LA, LB>(q, q, tiles, tiles, kred, ndp, splits);
 }
 
 }  // namespace g4
@@ -454,6 +502,58 @@ void g4_wgrad(const at::Tensor& dy, const at::Tensor& x, at::Tensor& out, bool a
     splitk_fixup_kernel<256, 256><<<(unsigned)((n8 + 255) / 256), 256, 0, cur_stream()>>>(
         part.data_ptr<float>(), (u16*)out.data_ptr(), ndp, nsk, splits, K / 256, K, accumulate ? 1 : 0, nrm, N / 256,
         std::min(g4::group_m(), N / 256));
+    SFT_LAUNCH_CHECK();
+  }
+}
+
+// Two weight gradients over the same tokens as ONE grid (g4_kernel with two problems): out0 (+)= dy0^T x0 and
+// out1 (+)= dy1^T x1. The whole rounds of 256 (cu_budget) tiles run across both; the partial last round must fall in
+// problem 1 and is split over the tokens (fp32 slabs + the ordered fixup), as the hybrid single-problem launch does.
+void g4_wgrad_pair(const at::Tensor& dy0, const at::Tensor& x0, at::Tensor& out0, bool acc0, float* nrm0, long cap0,
+                   const at::Tensor& dy1, const at::Tensor& x1, at::Tensor& out1, bool acc1, float* nrm1, long cap1) {
+  const int T = dy0.size(0);
+  const int N0 = dy0.size(1), K0 = x0.size(1), N1 = dy1.size(1), K1 = x1.size(1);
+  SFT_CHECK(dy1.size(0) == T && x0.size(0) == T && x1.size(0) == T, "wgrad pair: the same tokens");
+  SFT_CHECK(N0 % 256 == 0 && K0 % 256 == 0 && N1 % 256 == 0 && K1 % 256 == 0 && T % 128 == 0 && T > 0,
+            "wgrad pair: N, K % 256, T % 128");
+  for (const void* ptr : {dy0.data_ptr(), x0.data_ptr(), out0.data_ptr(), dy1.data_ptr(), x1.data_ptr(), out1.data_ptr()})
+    SFT_CHECK((uintptr_t)ptr % 16 == 0, "wgrad pair: 16-byte aligned operands");
+  const int tiles0 = (N0 / 256) * (K0 / 256), tiles1 = (N1 / 256) * (K1 / 256), total = tiles0 + tiles1;
+  const int B = cu_budget();
+  int ndp = total / B * B, splits = 1;
+  SFT_CHECK(total - ndp <= tiles1, "wgrad pair: the partial round must fall in the second problem");
+  if (total > ndp) {
+    splits = std::min(std::min(8, B / (total - ndp)), T / 128);
+    if (splits < 2) {
+      splits = 1;
+      ndp = total;
+    }
+  }
+  const int nsk = total - ndp, ndp1 = ndp - tiles0;
+  SFT_CHECK(nrm0 == nullptr || (long)tiles0 * 8 <= cap0, "wgrad pair: norm slot buffer 0 too small");
+  SFT_CHECK(nrm1 == nullptr || (long)ndp1 * 8 + (long)nsk * 32 <= cap1, "wgrad pair: norm slot buffer 1 too small");
+  at::Tensor part;
+  if (nsk > 0)
+    part = at::empty({(long)nsk * splits * 65536 + (nrm1 != nullptr ? (long)ndp1 * 8 : 0)},
+                     dy1.options().dtype(at::kFloat));
+  g4::Epi e0{}, e1{};
+  e0.C = (u16*)out0.data_ptr();
+  e0.ldc = K0;
+  e0.P = nrm0;
+  e0.flags = (acc0 ? 1 : 0) | (nrm0 != nullptr ? 2 : 0);
+  e1.C = (u16*)out1.data_ptr();
+  e1.ldc = K1;
+  e1.P = nsk > 0 ? part.data_ptr<float>() : nrm1;
+  e1.flags = (acc1 ? 1 : 0) | (nrm1 != nullptr ? 2 : 0);
+  const g4::Prob q0 = g4::prob((const u16*)dy0.data_ptr(), N0, (const u16*)x0.data_ptr(), x0.stride(0), N0, K0, e0, 0);
+  const g4::Prob q1 = g4::prob((const u16*)dy1.data_ptr(), N1, (const u16*)x1.data_ptr(), x1.stride(0), N1, K1, e1,
+                               nsk > 0 ? (long)nsk * splits * 65536 : 0);
+  g4::launch2<g4::TR, g4::TR>(q0, q1, tiles0, total, T, ndp, splits);
+  if (nsk > 0) {
+    const long n8 = (long)nsk * 65536 / 8;
+    splitk_fixup_kernel<256, 256><<<(unsigned)((n8 + 255) / 256), 256, 0, cur_stream()>>>(
+        part.data_ptr<float>(), (u16*)out1.data_ptr(), ndp1, nsk, splits, K1 / 256, K1, acc1 ? 1 : 0, nrm1, N1 / 256,
+        std::min(g4::group_m(), N1 / 256));
     SFT_LAUNCH_CHECK();
   }
 }

@@ -159,6 +159,53 @@ def _accumulate_weight_grad(param: torch.Tensor, dy2d: torch.Tensor, x2d: torch.
     return torch.mm(dy2d.t(), x2d).to(param.dtype)
 
 
+# The MLP's two weight gradients (down, gate_up) as ONE 4-wave grid: the down projection's backward defers its weight
+# gradient to the gate_up node (a per-call dict links the two), which then issues both in one launch —
+# 344 + 688 tiles = 4.03 rounds of 256 CUs instead of 1.34 + 2.69 with a partial last round each (a partial round
+# costs 0.75-1 of a full one: tools/debug/round_scaling.py, profiles/r6_gemm_routing.md). SFTAMD_WGRAD_PAIR=0: off.
+_WGRAD_PAIR = os.environ.get("SFTAMD_WGRAD_PAIR", "1") == "1"
+
+
+def _pair_ok(p0, dy0, x0, p1, dy1, x1) -> bool:
+    def one(p, dy, x):
+        mg = getattr(p, "main_grad", None)
+        return (mg is not None and mg.dtype == torch.bfloat16 and mg.is_contiguous() and dy.dtype == torch.bfloat16
+                and x.dtype == torch.bfloat16 and dy.shape[1] % 256 == 0 and x.shape[1] % 256 == 0
+                and x.stride(1) == 1 and x.stride(0) % 8 == 0 and x.data_ptr() % 16 == 0 and dy.data_ptr() % 16 == 0
+                and mg.data_ptr() % 16 == 0)
+    if not (_WGRAD_PAIR and _WGRAD_MODE in ("auto", "") and dy0.is_cuda and _ext.use_hip(dy0)):
+        return False
+    T = dy0.shape[0]
+    if not (T % 128 == 0 and T >= 1024 and dy1.shape[0] == T and x0.shape[0] == T and x1.shape[0] == T):
+        return False
+    if not (one(p0, dy0, x0) and one(p1, dy1, x1)):
+        return False
+    t0 = (dy0.shape[1] // 256) * (x0.shape[1] // 256)
+    t1 = (dy1.shape[1] // 256) * (x1.shape[1] // 256)
+    return (t0 + t1) % _CU_BUDGET <= t1
+
+
+def _accumulate_weight_grad_pair(p0, dy0, x0, p1, dy1, x1):
+    """_accumulate_weight_grad(p0, dy0, x0) and (p1, dy1, x1) — one wgrad_gemm_pair launch where it applies."""
+    if not _pair_ok(p0, dy0, x0, p1, dy1, x1):
+        _accumulate_weight_grad(p0, dy0, x0)
+        _accumulate_weight_grad(p1, dy1, x1)
+        return
+
+    def slots(p):
+        ns = getattr(p, "_sftamd_norm_slots", None)
+        return ns if (ns is not None and getattr(p, "_sftamd_remaining", 1) == 1) else None
+
+    n0, n1 = slots(p0), slots(p1)
+    _ext.ops().wgrad_gemm_pair(p0.main_grad, dy0.contiguous(), x0, not getattr(p0, "_sftamd_fresh", False), n0,
+                               p1.main_grad, dy1.contiguous(), x1, not getattr(p1, "_sftamd_fresh", False), n1)
+    for p, ns in ((p0, n0), (p1, n1)):
+        if ns is not None:
+            p._sftamd_norm_done = True
+        p._sftamd_fresh = False
+        _weight_grad_done(p)
+
+
 def _accumulate_small_grad(param: torch.Tensor, g: torch.Tensor):
     mg = getattr(param, "main_grad", None)
     if mg is not None:
@@ -246,6 +293,46 @@ class LinearFn(Function):
 
 
 def linear(x: torch.Tensor, weight: torch.Tensor) -> torch.Tensor:
+    return LinearFn.apply(x, weight)
+
+
+class MLPInLinearFn(Function):
+    """gate_up = x W^T (LinearFn) for an MLP whose down projection (SwiGLULinearFn with the same `box`) defers its
+    weight gradient here: the backward issues both weight gradients as one launch (_accumulate_weight_grad_pair)."""
+
+    @staticmethod
+    def forward(ctx, x, weight, box):
+        ctx.save_for_backward(x)
+        ctx.weight = weight
+        ctx.box = box
+        if weight.requires_grad:  # this node's backward will run: the down node may leave its weight gradient to it
+            box["armed"] = True
+        x2d = x.reshape(-1, x.shape[-1])
+        return _as_output(fwd_gemm(x2d, weight), x.shape[:-1])
+
+    @staticmethod
+    def backward(ctx, dy):
+        (x,) = ctx.saved_tensors
+        w = ctx.weight
+        dy2d = dy.reshape(-1, dy.shape[-1])
+        x2d = x.reshape(-1, x.shape[-1])
+        pending = ctx.box.pop("down", None)
+        dx = dw = None
+        if ctx.needs_input_grad[0]:
+            dx = dgrad_mm(dy2d, w).view(*dy.shape[:-1], w.shape[1])
+        if ctx.needs_input_grad[1]:
+            if pending is not None:
+                _accumulate_weight_grad_pair(*pending, w, dy2d, x2d)
+            else:
+                dw = _accumulate_weight_grad(w, dy2d, x2d)
+        elif pending is not None:
+            _accumulate_weight_grad(*pending)
+        return dx, dw, None
+
+
+def mlp_in_linear(x: torch.Tensor, weight: torch.Tensor, box: Optional[dict]) -> torch.Tensor:
+    if box is not None and _ext.use_hip(x):
+        return MLPInLinearFn.apply(x, weight, box)
     return LinearFn.apply(x, weight)
 
 
@@ -367,10 +454,11 @@ class SwiGLULinearFn(Function):
     written), plus the weight gradient from the saved activation."""
 
     @staticmethod
-    def forward(ctx, gu, weight):
+    def forward(ctx, gu, weight, box=None):
         act = _ext.ops().swiglu_fwd(gu)
         ctx.save_for_backward(gu, act)
         ctx.weight = weight
+        ctx.box = box
         a2d = act.reshape(-1, act.shape[-1])
         return _as_output(fwd_gemm(a2d, weight), gu.shape[:-1])
 
@@ -388,8 +476,13 @@ class SwiGLULinearFn(Function):
                 dgu = _ext.ops().swiglu_bwd(torch.mm(dy2d, w), gu2d)
             dgu = dgu.view(gu.shape)
         if ctx.needs_input_grad[1]:
-            dw = _accumulate_weight_grad(w, dy2d, act.reshape(-1, act.shape[-1]))
-        return dgu, dw
+            a2d = act.reshape(-1, act.shape[-1])
+            box = ctx.box
+            if box is not None and box.get("armed") and getattr(w, "main_grad", None) is not None:
+                box["down"] = (w, dy2d, a2d)  # issued together with gate_up's (MLPInLinearFn.backward)
+            else:
+                dw = _accumulate_weight_grad(w, dy2d, a2d)
+        return dgu, dw, None
 
 
 _SWIGLU_DOWN = True  # (a test seam: tests/test_model_gpu.py switches the MLP split off)
@@ -401,10 +494,11 @@ def fuse_swiglu_down() -> bool:
     return _SWIGLU_DOWN and _TN_MODE not in ("1", "swiglu")
 
 
-def swiglu_linear(gu: torch.Tensor, weight: torch.Tensor) -> torch.Tensor:
-    """linear(swiglu(gu), weight) with the fused backward where the HIP kernels apply."""
+def swiglu_linear(gu: torch.Tensor, weight: torch.Tensor, box: Optional[dict] = None) -> torch.Tensor:
+    """linear(swiglu(gu), weight) with the fused backward where the HIP kernels apply. box: shared with the
+    mlp_in_linear that produced gu (the two weight gradients then run as one launch)."""
     if _SWIGLU_DOWN and _ext.use_hip(gu) and gu.dtype == torch.bfloat16 and gu.is_contiguous():
-        return SwiGLULinearFn.apply(gu, weight)
+        return SwiGLULinearFn.apply(gu, weight, box)
     return linear(swiglu(gu), weight)
 
 
@@ -703,7 +797,8 @@ def swiglu_mlp(h: torch.Tensor, w_gate_up: torch.Tensor, w_down: torch.Tensor) -
         gu, act = GateUpActFn.apply(h, w_gate_up)
         return SwiGLUDownFn.apply(gu, act, w_down)
     if fuse_swiglu_down():
-        return swiglu_linear(linear(h, w_gate_up), w_down)
+        box = {} if _WGRAD_PAIR else None
+        return swiglu_linear(mlp_in_linear(h, w_gate_up, box), w_down, box)
     return linear(linear_swiglu(h, w_gate_up), w_down)
 
 

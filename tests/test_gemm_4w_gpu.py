@@ -243,3 +243,56 @@ def test_4wave_grids_under_a_cu_budget():
     finally:
         ops.set_cu_budget(0)
     assert ops.cu_budget() == 256
+
+
+@pytest.mark.parametrize("N0,K0,N1,K1,T", [(2048, 10752, 5632, 2048, 256),    # 336 + 176 = 512 tiles: 2 whole rounds
+                                           (2048, 11008, 22016, 2048, 256),   # the SmolLM3 MLP: 1032 = 4 rounds + 8
+                                           (2048, 11008, 22016, 2048, 1024)])
+@pytest.mark.parametrize("accumulate", [False, True])
+def test_wgrad_pair_one_launch(N0, K0, N1, K1, T, accumulate):
+    """wgrad_gemm_pair (the MLP's down + gate_up weight gradients as one grid) == two cfg-14 launches: whole tiles
+    bitwise, the split leftover tiles of problem 1 within fp32-order rounding, deterministic; the norm slots sum to
+    the squared norm of what was stored."""
+    torch.manual_seed(13)
+    dy0 = torch.randn(T, N0, device=DEV, dtype=torch.bfloat16)
+    x0 = torch.randn(T, K0, device=DEV, dtype=torch.bfloat16)
+    dy1 = torch.randn(T, N1, device=DEV, dtype=torch.bfloat16)
+    x1 = torch.randn(T, K1, device=DEV, dtype=torch.bfloat16)
+    base0 = torch.randn(N0, K0, device=DEV, dtype=torch.bfloat16)
+    base1 = torch.randn(N1, K1, device=DEV, dtype=torch.bfloat16)
+    w0, w1 = base0.clone(), base1.clone()
+    r0, r1 = base0.clone(), base1.clone()
+    cap0 = (N0 // 256) * (K0 // 128) * 32
+    cap1 = (N1 // 256) * (K1 // 128) * 32
+    n0 = torch.zeros(cap0, device=DEV)
+    n1 = torch.zeros(cap1, device=DEV)
+    _ext.ops().wgrad_gemm_pair(w0, dy0, x0, accumulate, n0, w1, dy1, x1, accumulate, n1)
+    _ext.ops().wgrad_gemm(r0, dy0, x0, accumulate, 14)
+    _ext.ops().wgrad_gemm(r1, dy1, x1, accumulate, 14)
+    assert torch.equal(w0, r0)
+    tiles = (N0 // 256) * (K0 // 256) + (N1 // 256) * (K1 // 256)
+    if tiles % 256 == 0:
+        assert torch.equal(w1, r1)
+    else:
+        assert rel_err(w1, r1) < 1e-2
+        assert (w1 != r1).float().mean().item() < 0.05  # only the split leftover tiles may differ
+    want = (dy1.float().t() @ x1.float()) + (base1.float() if accumulate else 0)
+    assert rel_err(w1, want) < 5e-3
+    assert abs(n0.sum().item() - w0.float().pow(2).sum().item()) < 1e-3 * w0.float().pow(2).sum().item()
+    assert abs(n1.sum().item() - w1.float().pow(2).sum().item()) < 1e-3 * w1.float().pow(2).sum().item()
+    v0, v1 = base0.clone(), base1.clone()
+    _ext.ops().wgrad_gemm_pair(v0, dy0, x0, accumulate, None, v1, dy1, x1, accumulate, None)
+    assert torch.equal(v0, w0) and torch.equal(v1, w1)
+
+
+def test_wgrad_pair_refuses_a_leftover_in_the_first_problem():
+    """The partial last round must fall in the second problem (its fixup); a pair whose leftover tiles would reach into
+    the first one is refused (ops.fused._pair_ok routes such pairs to two launches)."""
+    dy0 = torch.randn(256, 22016, device=DEV, dtype=torch.bfloat16)
+    x0 = torch.randn(256, 2048, device=DEV, dtype=torch.bfloat16)
+    dy1 = torch.randn(256, 256, device=DEV, dtype=torch.bfloat16)
+    x1 = torch.randn(256, 256, device=DEV, dtype=torch.bfloat16)
+    o0 = torch.empty(22016, 2048, device=DEV, dtype=torch.bfloat16)
+    o1 = torch.empty(256, 256, device=DEV, dtype=torch.bfloat16)
+    with pytest.raises(RuntimeError):
+        _ext.ops().wgrad_gemm_pair(o0, dy0, x0, False, None, o1, dy1, x1, False, None)
