@@ -365,8 +365,8 @@ struct Prob {
 // A launch runs one problem or two with the same reduction length (tiles [0, tiles0) = p0, the rest = p1, e.g. the
 // MLP's down and gate_up weight gradients as ONE grid: 344 + 688 = 1032 tiles = 4.03 rounds of 256 CUs instead of
 // 1.34 + 2.69 — a partial last round costs most of a full one, profiles/r6_gemm_routing.md). splits > 1: the tiles
-// past ndp (all in the last problem) are split into `splits` equal ranges of 128-deep blocks (pieces -> fp32 slabs,
-// splitk_fixup_kernel).
+// past ndp are split into `splits` equal ranges of 128-deep blocks (pieces -> fp32 slabs of their problem's P,
+// splitk_fixup_kernel per problem).
 template <int LA, int LB>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1)))
 g4_kernel(Prob q0, Prob q1, int tiles0, int kred, int ndp, int splits) {
@@ -427,7 +427,9 @@ g4_kernel(Prob q0, Prob q1, int tiles0, int kred, int ndp, int splits) {
   asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 3" ::: "memory");
   __builtin_amdgcn_sched_barrier(0);
   if (wgid >= ndp) {
-    store_partial(acc, ea.P + ((long)(tile - ndp) * splits + sk) * 65536, wm, wn, lane);
+    // slab of this problem's piece: its split tiles start at its first tile past ndp
+    const int ndpl = sec ? max(ndp - tiles0, 0) : min(ndp, tiles0);
+    store_partial(acc, ea.P + ((long)(lt - ndpl) * splits + sk) * 65536, wm, wn, lane);
     return;
   }
   float* nrm = nullptr;
@@ -509,8 +511,11 @@ void g4_wgrad(const at::Tensor& dy, const at::Tensor& x, at::Tensor& out, bool a
 // Two weight gradients over the same tokens as ONE grid (g4_kernel with two problems): out0 (+)= dy0^T x0 and
 // out1 (+)= dy1^T x1. The whole rounds of 256 (cu_budget) tiles run across both; the partial last round must fall in
 // problem 1 and is split over the tokens (fp32 slabs + the ordered fixup), as the hybrid single-problem launch does.
+// split_all > 1: every tile of both problems split that many ways (small pairs such as o_proj + qkv: 64 + 96 tiles x 3
+// = 480 pieces = 2 rounds of third-tiles, against one round of quarter-tiles + one of half-tiles apart).
 void g4_wgrad_pair(const at::Tensor& dy0, const at::Tensor& x0, at::Tensor& out0, bool acc0, float* nrm0, long cap0,
-                   const at::Tensor& dy1, const at::Tensor& x1, at::Tensor& out1, bool acc1, float* nrm1, long cap1) {
+                   const at::Tensor& dy1, const at::Tensor& x1, at::Tensor& out1, bool acc1, float* nrm1, long cap1,
+                   int split_all) {
   const int T = dy0.size(0);
   const int N0 = dy0.size(1), K0 = x0.size(1), N1 = dy1.size(1), K1 = x1.size(1);
   SFT_CHECK(dy1.size(0) == T && x0.size(0) == T && x1.size(0) == T, "wgrad pair: the same tokens");
@@ -521,41 +526,51 @@ void g4_wgrad_pair(const at::Tensor& dy0, const at::Tensor& x0, at::Tensor& out0
   const int tiles0 = (N0 / 256) * (K0 / 256), tiles1 = (N1 / 256) * (K1 / 256), total = tiles0 + tiles1;
   const int B = cu_budget();
   int ndp = total / B * B, splits = 1;
-  SFT_CHECK(total - ndp <= tiles1, "wgrad pair: the partial round must fall in the second problem");
-  if (total > ndp) {
-    splits = std::min(std::min(8, B / (total - ndp)), T / 128);
-    if (splits < 2) {
-      splits = 1;
-      ndp = total;
-    }
+  if (split_all > 1) {
+    ndp = 0;
+    splits = std::min(split_all, T / 128);
+  } else {
+    SFT_CHECK(total - ndp <= tiles1, "wgrad pair: the partial round must fall in the second problem");
+    if (total > ndp) splits = std::min(std::min(8, B / (total - ndp)), T / 128);
   }
-  const int nsk = total - ndp, ndp1 = ndp - tiles0;
-  SFT_CHECK(nrm0 == nullptr || (long)tiles0 * 8 <= cap0, "wgrad pair: norm slot buffer 0 too small");
-  SFT_CHECK(nrm1 == nullptr || (long)ndp1 * 8 + (long)nsk * 32 <= cap1, "wgrad pair: norm slot buffer 1 too small");
-  at::Tensor part;
-  if (nsk > 0)
-    part = at::empty({(long)nsk * splits * 65536 + (nrm1 != nullptr ? (long)ndp1 * 8 : 0)},
-                     dy1.options().dtype(at::kFloat));
-  g4::Epi e0{}, e1{};
-  e0.C = (u16*)out0.data_ptr();
-  e0.ldc = K0;
-  e0.P = nrm0;
-  e0.flags = (acc0 ? 1 : 0) | (nrm0 != nullptr ? 2 : 0);
-  e1.C = (u16*)out1.data_ptr();
-  e1.ldc = K1;
-  e1.P = nsk > 0 ? part.data_ptr<float>() : nrm1;
-  e1.flags = (acc1 ? 1 : 0) | (nrm1 != nullptr ? 2 : 0);
-  const g4::Prob q0 = g4::prob((const u16*)dy0.data_ptr(), N0, (const u16*)x0.data_ptr(), x0.stride(0), N0, K0, e0, 0);
-  const g4::Prob q1 = g4::prob((const u16*)dy1.data_ptr(), N1, (const u16*)x1.data_ptr(), x1.stride(0), N1, K1, e1,
-                               nsk > 0 ? (long)nsk * splits * 65536 : 0);
+  if (splits < 2) {
+    splits = 1;
+    ndp = total;
+  }
+  // per problem: whole tiles [0, w) and split tiles [w, tiles)
+  const int w0 = std::min(ndp, tiles0), w1 = std::max(ndp - tiles0, 0);
+  const int s0 = tiles0 - w0, s1 = tiles1 - w1;
+  SFT_CHECK(nrm0 == nullptr || (long)w0 * 8 + (long)s0 * 32 <= cap0, "wgrad pair: norm slot buffer 0 too small");
+  SFT_CHECK(nrm1 == nullptr || (long)w1 * 8 + (long)s1 * 32 <= cap1, "wgrad pair: norm slot buffer 1 too small");
+  auto slab = [&](int ns, int nw, float* nrm) {
+    return ns > 0 ? at::empty({(long)ns * splits * 65536 + (nrm != nullptr ? (long)nw * 8 : 0)},
+                              dy0.options().dtype(at::kFloat))
+                  : at::Tensor();
+  };
+  at::Tensor part0 = slab(s0, w0, nrm0), part1 = slab(s1, w1, nrm1);
+  auto epi = [&](const at::Tensor& out, int K, bool acc, float* nrm, int ns, const at::Tensor& part) {
+    g4::Epi e{};
+    e.C = (u16*)out.data_ptr();
+    e.ldc = K;
+    e.P = ns > 0 ? part.data_ptr<float>() : nrm;
+    e.flags = (acc ? 1 : 0) | (nrm != nullptr ? 2 : 0);
+    return e;
+  };
+  const g4::Prob q0 = g4::prob((const u16*)dy0.data_ptr(), N0, (const u16*)x0.data_ptr(), x0.stride(0), N0, K0,
+                               epi(out0, K0, acc0, nrm0, s0, part0), s0 > 0 ? (long)s0 * splits * 65536 : 0);
+  const g4::Prob q1 = g4::prob((const u16*)dy1.data_ptr(), N1, (const u16*)x1.data_ptr(), x1.stride(0), N1, K1,
+                               epi(out1, K1, acc1, nrm1, s1, part1), s1 > 0 ? (long)s1 * splits * 65536 : 0);
   g4::launch2<g4::TR, g4::TR>(q0, q1, tiles0, total, T, ndp, splits);
-  if (nsk > 0) {
-    const long n8 = (long)nsk * 65536 / 8;
+  auto fixup = [&](const at::Tensor& part, int ns, int nw, const at::Tensor& out, int N, int K, bool acc, float* nrm) {
+    if (ns <= 0) return;
+    const long n8 = (long)ns * 65536 / 8;
     splitk_fixup_kernel<256, 256><<<(unsigned)((n8 + 255) / 256), 256, 0, cur_stream()>>>(
-        part.data_ptr<float>(), (u16*)out1.data_ptr(), ndp1, nsk, splits, K1 / 256, K1, acc1 ? 1 : 0, nrm1, N1 / 256,
-        std::min(g4::group_m(), N1 / 256));
+        part.data_ptr<float>(), (u16*)out.data_ptr(), nw, ns, splits, K / 256, K, acc ? 1 : 0, nrm, N / 256,
+        std::min(g4::group_m(), N / 256));
     SFT_LAUNCH_CHECK();
-  }
+  };
+  fixup(part0, s0, w0, out0, N0, K0, acc0, nrm0);
+  fixup(part1, s1, w1, out1, N1, K1, acc1, nrm1);
 }
 
 // Input gradient dX[M, N] = dy[M, K] . w[K, N] into out (row stride ldo; w may be a column slice: row stride

@@ -418,13 +418,14 @@ void wgrad_gemm(at::Tensor out, at::Tensor dy, at::Tensor x, bool accumulate, in
 }
 
 void g4_wgrad_pair(const at::Tensor& dy0, const at::Tensor& x0, at::Tensor& out0, bool acc0, float* nrm0, long cap0,
-                   const at::Tensor& dy1, const at::Tensor& x1, at::Tensor& out1, bool acc1, float* nrm1, long cap1);
+                   const at::Tensor& dy1, const at::Tensor& x1, at::Tensor& out1, bool acc1, float* nrm1, long cap1,
+                   int split_all);
 
 // Two weight gradients over the same tokens in ONE 4-wave launch (e.g. the MLP's down and gate_up: 344 + 688 tiles =
 // 4.03 rounds instead of 1.34 + 2.69 with a partial last round each; csrc/gemm_4w.hip g4_wgrad_pair).
 void wgrad_gemm_pair(at::Tensor out0, at::Tensor dy0, at::Tensor x0, bool acc0, const c10::optional<at::Tensor>& norm0,
                      at::Tensor out1, at::Tensor dy1, at::Tensor x1, bool acc1,
-                     const c10::optional<at::Tensor>& norm1) {
+                     const c10::optional<at::Tensor>& norm1, int64_t split_all) {
   SFT_CHECK_CUDA(dy0);
   SFT_CHECK_BF16(out0);
   SFT_CHECK_BF16(dy0);
@@ -456,7 +457,8 @@ void wgrad_gemm_pair(at::Tensor out0, at::Tensor dy0, at::Tensor x0, bool acc0, 
   slots(norm1, n1, c1);
   SFT_TRACE("wgrad.pair");
   if (n0 != nullptr || n1 != nullptr) SFT_TRACE("wgrad.norm_slots");
-  g4_wgrad_pair(dy0, x0, out0, acc0, n0, c0, dy1, x1, out1, acc1, n1, c1);
+  SFT_CHECK(split_all >= 0 && split_all <= 8, "wgrad_gemm_pair: split_all 0..8");
+  g4_wgrad_pair(dy0, x0, out0, acc0, n0, c0, dy1, x1, out1, acc1, n1, c1, (int)split_all);
 }
 
 TORCH_LIBRARY_IMPL(sftamd, CUDA, m) {

@@ -159,10 +159,11 @@ def _accumulate_weight_grad(param: torch.Tensor, dy2d: torch.Tensor, x2d: torch.
     return torch.mm(dy2d.t(), x2d).to(param.dtype)
 
 
-# The MLP's two weight gradients (down, gate_up) as ONE 4-wave grid: the down projection's backward defers its weight
-# gradient to the gate_up node (a per-call dict links the two), which then issues both in one launch —
-# 344 + 688 tiles = 4.03 rounds of 256 CUs instead of 1.34 + 2.69 with a partial last round each (a partial round
-# costs 0.75-1 of a full one: tools/debug/round_scaling.py, profiles/r6_gemm_routing.md). SFTAMD_WGRAD_PAIR=0: off.
+# Weight gradients in pairs as ONE 4-wave grid: the MLP's down projection defers its weight gradient to the gate_up
+# node, the attention's o_proj to the qkv + RoPE + attention node (per-call dicts link them), which then issue both in
+# one launch — MLP: 344 + 688 tiles = 4.03 rounds of 256 CUs instead of 1.34 + 2.69 with a partial last round each (a
+# partial round costs 0.75-1 of a full one: tools/debug/round_scaling.py, profiles/r6_gemm_routing.md); attention:
+# 64 + 96 tiles split 3 ways = 2 rounds of third-tiles. SFTAMD_WGRAD_PAIR=0: off.
 _WGRAD_PAIR = os.environ.get("SFTAMD_WGRAD_PAIR", "1") == "1"
 
 
@@ -182,7 +183,23 @@ def _pair_ok(p0, dy0, x0, p1, dy1, x1) -> bool:
         return False
     t0 = (dy0.shape[1] // 256) * (x0.shape[1] // 256)
     t1 = (dy1.shape[1] // 256) * (x1.shape[1] // 256)
-    return (t0 + t1) % _CU_BUDGET <= t1
+    return _pair_split(t0, t1, T) > 1 or (t0 + t1) % _CU_BUDGET <= t1
+
+
+def _pair_split(t0: int, t1: int, T: int) -> int:
+    """Pairs smaller than one round (o_proj + qkv: 64 + 96 tiles) split every tile s ways, s minimising the rounds of
+    1/s-tiles plus the fp32 slab traffic of the fixup (~4e-4 of a tile's time per piece at T = 8192, from the o_proj /
+    qkv split launches: profiles/r6_gemm_routing.md) — 3 for o_proj + qkv (480 pieces = 2 rounds of third-tiles);
+    0 = whole rounds + the split leftover (hybrid)."""
+    n = t0 + t1
+    if n >= _CU_BUDGET:
+        return 0
+    best, cost = 0, None
+    for s in range(2, min(8, T // 128) + 1):
+        c = -(-n * s // _CU_BUDGET) / s + 4e-4 * n * s
+        if cost is None or c < cost - 1e-9:
+            best, cost = s, c
+    return best
 
 
 def _accumulate_weight_grad_pair(p0, dy0, x0, p1, dy1, x1):
@@ -191,6 +208,8 @@ def _accumulate_weight_grad_pair(p0, dy0, x0, p1, dy1, x1):
         _accumulate_weight_grad(p0, dy0, x0)
         _accumulate_weight_grad(p1, dy1, x1)
         return
+    split_all = _pair_split((dy0.shape[1] // 256) * (x0.shape[1] // 256), (dy1.shape[1] // 256) * (x1.shape[1] // 256),
+                            dy0.shape[0])
 
     def slots(p):
         ns = getattr(p, "_sftamd_norm_slots", None)
@@ -198,7 +217,8 @@ def _accumulate_weight_grad_pair(p0, dy0, x0, p1, dy1, x1):
 
     n0, n1 = slots(p0), slots(p1)
     _ext.ops().wgrad_gemm_pair(p0.main_grad, dy0.contiguous(), x0, not getattr(p0, "_sftamd_fresh", False), n0,
-                               p1.main_grad, dy1.contiguous(), x1, not getattr(p1, "_sftamd_fresh", False), n1)
+                               p1.main_grad, dy1.contiguous(), x1, not getattr(p1, "_sftamd_fresh", False), n1,
+                               split_all)
     for p, ns in ((p0, n0), (p1, n1)):
         if ns is not None:
             p._sftamd_norm_done = True
@@ -379,7 +399,10 @@ class AttnOutLinearFn(Function):
                 d2d = dgrad_mm(dy2d, w)
             dx = d2d.view(*dy.shape[:-1], w.shape[1])
         if ctx.needs_input_grad[1]:
-            dw = _accumulate_weight_grad(w, dy2d, x2d)
+            if ctx.box.get("wgrad_pair") and getattr(w, "main_grad", None) is not None:
+                ctx.box["o_wgrad"] = (w, dy2d, x2d)  # issued with qkv's (QKVRopeAttnFn.backward)
+            else:
+                dw = _accumulate_weight_grad(w, dy2d, x2d)
         return dx, dw, None
 
 
@@ -926,6 +949,8 @@ class QKVRopeAttnFn(Function):
         ctx.box = box
         if box is not None:
             box["armed"] = True
+            if _WGRAD_PAIR and weight.requires_grad:  # this node's backward runs: o_proj may leave its wgrad here
+                box["wgrad_pair"] = True
         x2d = x.reshape(-1, x.shape[-1])
         qkv = _ext.ops().gemm_tn_rope(x2d, weight, cos, sin, (n_q + n_kv) * head_dim,
                                       _tn_cfg(x2d.shape[0], weight.shape[0], x2d.shape[1]))
@@ -944,11 +969,17 @@ class QKVRopeAttnFn(Function):
         dqkv = _ext.ops().flash_bwd_rope(dout.contiguous(), qkv, out, lse, cu, max_seqlen, n_q, n_kv, hd, scale, causal,
                                          cos, sin, _take_delta(ctx.box, dout, n_q))
         del qkv, out, lse
+        pending = ctx.box.pop("o_wgrad", None) if ctx.box is not None else None
         dx = dw = None
         if ctx.needs_input_grad[0]:
             dx = dgrad_mm(dqkv, w).view(ctx.x_shape)
         if ctx.needs_input_grad[1]:
-            dw = _accumulate_weight_grad(w, dqkv, x2d)
+            if pending is not None:
+                _accumulate_weight_grad_pair(*pending, w, dqkv, x2d)
+            else:
+                dw = _accumulate_weight_grad(w, dqkv, x2d)
+        elif pending is not None:
+            _accumulate_weight_grad(*pending)
         return dx, dw, None, None, None, None, None, None, None, None, None, None
 
 

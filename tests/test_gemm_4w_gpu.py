@@ -296,3 +296,31 @@ def test_wgrad_pair_refuses_a_leftover_in_the_first_problem():
     o1 = torch.empty(256, 256, device=DEV, dtype=torch.bfloat16)
     with pytest.raises(RuntimeError):
         _ext.ops().wgrad_gemm_pair(o0, dy0, x0, False, None, o1, dy1, x1, False, None)
+
+
+@pytest.mark.parametrize("T", [1024, 8192])
+def test_wgrad_pair_split_all(T):
+    """o_proj + qkv weight gradients as one launch with every tile split 3 ways (split_all): == two cfg-14 launches
+    within fp32-order rounding, == the fp32 reference, deterministic, norm slots sum to the stored squared norm."""
+    torch.manual_seed(17)
+    dy0 = torch.randn(T, 2048, device=DEV, dtype=torch.bfloat16)
+    x0 = torch.randn(T, 2048, device=DEV, dtype=torch.bfloat16)
+    dy1 = torch.randn(T, 3072, device=DEV, dtype=torch.bfloat16)
+    x1 = torch.randn(T, 2048, device=DEV, dtype=torch.bfloat16)
+    w0 = torch.empty(2048, 2048, device=DEV, dtype=torch.bfloat16)
+    w1 = torch.empty(3072, 2048, device=DEV, dtype=torch.bfloat16)
+    n0 = torch.zeros(8 * 16 * 32, device=DEV)
+    n1 = torch.zeros(12 * 16 * 32, device=DEV)
+    _ext.ops().wgrad_gemm_pair(w0, dy0, x0, False, n0, w1, dy1, x1, False, n1, 3)
+    assert rel_err(w0, dy0.float().t() @ x0.float()) < 5e-3
+    assert rel_err(w1, dy1.float().t() @ x1.float()) < 5e-3
+    r0, r1 = torch.empty_like(w0), torch.empty_like(w1)
+    _ext.ops().wgrad_gemm(r0, dy0, x0, False, 14)
+    _ext.ops().wgrad_gemm(r1, dy1, x1, False, 14)
+    assert rel_err(w0, r0) < 1e-2 and rel_err(w1, r1) < 1e-2
+    for n, w in ((n0, w0), (n1, w1)):
+        ref = w.float().pow(2).sum().item()
+        assert abs(n.sum().item() - ref) < 1e-3 * ref
+    v0, v1 = torch.empty_like(w0), torch.empty_like(w1)
+    _ext.ops().wgrad_gemm_pair(v0, dy0, x0, False, None, v1, dy1, x1, False, None, 3)
+    assert torch.equal(v0, w0) and torch.equal(v1, w1)
