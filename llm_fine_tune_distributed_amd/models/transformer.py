@@ -73,12 +73,16 @@ class Attention(nn.Module):
             a = ops.lora_qkv_rope_attention(h, self.qkv_proj, self.lora["qkv"], rope_cs[0], rope_cs[1], cu_seqlens,
                                             max_seqlen, c.num_attention_heads, c.num_key_value_heads, c.head_dim)
             return ops.lora_linear(a, self.o_proj, self.lora["o"])
+        pair = None
         if self.lora is None and self.use_rope:
             # projection + RoPE in one HIP GEMM (epilogue rotation) where the shapes allow
             qkv = ops.linear_rope(h, self.qkv_proj, rope_cs[0], rope_cs[1], c.num_attention_heads,
                                   c.num_key_value_heads, c.head_dim)
         else:
-            qkv = ops.linear(h, self.qkv_proj) if self.lora is None else ops.lora_linear(h, self.qkv_proj, self.lora["qkv"])
+            # (a NoPE layer: the qkv node also issues o_proj's weight gradient, as one launch with its own)
+            pair = {} if (self.lora is None and not self.use_rope and self.cp_group is None) else None
+            qkv = (ops.qkv_in_linear(h, self.qkv_proj, pair) if self.lora is None
+                   else ops.lora_linear(h, self.qkv_proj, self.lora["qkv"]))
             if self.use_rope:
                 qkv = ops.rope_(qkv, rope_cs[0], rope_cs[1], c.num_attention_heads, c.num_key_value_heads, c.head_dim)
         if self.cp_group is not None:
@@ -86,7 +90,7 @@ class Attention(nn.Module):
             a = ring_attention(qkv, cu_seqlens, max_seqlen, c.num_attention_heads, c.num_key_value_heads, c.head_dim,
                                self.cp_group, layout=self.cp_layout)
         else:
-            box = {} if self.lora is None else None
+            box = (pair if pair is not None else {}) if self.lora is None else None
             a = ops.flash_attention(qkv, cu_seqlens, max_seqlen, c.num_attention_heads, c.num_key_value_heads,
                                     c.head_dim, delta_box=box)
             if box is not None:

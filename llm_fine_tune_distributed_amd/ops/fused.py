@@ -316,17 +316,20 @@ def linear(x: torch.Tensor, weight: torch.Tensor) -> torch.Tensor:
     return LinearFn.apply(x, weight)
 
 
-class MLPInLinearFn(Function):
-    """gate_up = x W^T (LinearFn) for an MLP whose down projection (SwiGLULinearFn with the same `box`) defers its
-    weight gradient here: the backward issues both weight gradients as one launch (_accumulate_weight_grad_pair)."""
+class PairedLinearFn(Function):
+    """y = x W^T (LinearFn) for a projection whose CONSUMER defers its own weight gradient here through `box[key]`:
+    the MLP's gate_up (the down projection, SwiGLULinearFn, leaves "down") and a NoPE layer's qkv (o_proj,
+    AttnOutLinearFn, leaves "o_wgrad"). The backward issues both weight gradients as one launch
+    (_accumulate_weight_grad_pair) after this node's input gradient."""
 
     @staticmethod
-    def forward(ctx, x, weight, box):
+    def forward(ctx, x, weight, box, key, arm):
         ctx.save_for_backward(x)
         ctx.weight = weight
         ctx.box = box
-        if weight.requires_grad:  # this node's backward will run: the down node may leave its weight gradient to it
-            box["armed"] = True
+        ctx.key = key
+        if weight.requires_grad:  # this node's backward will run: the consumer may leave its weight gradient to it
+            box[arm] = True
         x2d = x.reshape(-1, x.shape[-1])
         return _as_output(fwd_gemm(x2d, weight), x.shape[:-1])
 
@@ -336,7 +339,7 @@ class MLPInLinearFn(Function):
         w = ctx.weight
         dy2d = dy.reshape(-1, dy.shape[-1])
         x2d = x.reshape(-1, x.shape[-1])
-        pending = ctx.box.pop("down", None)
+        pending = ctx.box.pop(ctx.key, None)
         dx = dw = None
         if ctx.needs_input_grad[0]:
             dx = dgrad_mm(dy2d, w).view(*dy.shape[:-1], w.shape[1])
@@ -347,12 +350,20 @@ class MLPInLinearFn(Function):
                 dw = _accumulate_weight_grad(w, dy2d, x2d)
         elif pending is not None:
             _accumulate_weight_grad(*pending)
-        return dx, dw, None
+        return dx, dw, None, None, None
 
 
 def mlp_in_linear(x: torch.Tensor, weight: torch.Tensor, box: Optional[dict]) -> torch.Tensor:
+    """gate_up(x) whose backward also issues the down projection's weight gradient (swiglu_linear with `box`)."""
     if box is not None and _ext.use_hip(x):
-        return MLPInLinearFn.apply(x, weight, box)
+        return PairedLinearFn.apply(x, weight, box, "down", "armed")
+    return LinearFn.apply(x, weight)
+
+
+def qkv_in_linear(x: torch.Tensor, weight: torch.Tensor, box: Optional[dict]) -> torch.Tensor:
+    """qkv(x) of a NoPE layer whose backward also issues o_proj's weight gradient (attn_out_linear with `box`)."""
+    if box is not None and _WGRAD_PAIR and _ext.use_hip(x):
+        return PairedLinearFn.apply(x, weight, box, "o_wgrad", "wgrad_pair")
     return LinearFn.apply(x, weight)
 
 
