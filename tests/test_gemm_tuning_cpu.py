@@ -41,3 +41,17 @@ def test_wgrad_routing_under_a_cu_budget(monkeypatch):
     monkeypatch.setattr(F, "_CU_BUDGET", 248)
     assert {k: F._wgrad_cfg(8192, n, kk) for k, (n, kk) in shapes.items()} == {
         "o": 314, "qkv": 214, "down": 1214, "lm_head": 1214, "gate_up": 14}
+
+
+def test_weight_gradient_pair_planning():
+    """Pair planning (ops.fused): pairs smaller than one round split every tile s ways (o_proj + qkv: 64 + 96 tiles ->
+    3 ways, 2 rounds of third-tiles); larger pairs run whole rounds + the split leftover (0); CPU tensors never pair."""
+    import torch
+    import llm_fine_tune_distributed_amd.ops.fused as F
+    assert F._pair_split(64, 96, 8192) == 3
+    assert F._pair_split(344, 688, 8192) == 0 and F._pair_split(256, 384, 8192) == 0
+    assert F._pair_split(64, 96, 256) == 2  # at most T / 128 pieces per tile
+    p0 = torch.nn.Parameter(torch.zeros(256, 256))
+    p1 = torch.nn.Parameter(torch.zeros(256, 256))
+    x = torch.zeros(1024, 256, dtype=torch.bfloat16)
+    assert not F._pair_ok(p0, x, x, p1, x, x)
