@@ -59,6 +59,18 @@ __device__ __forceinline__ bf16x8 lds_tr(const char* base, int off) {
   return __builtin_bit_cast(bf16x8, v);
 }
 
+// cfg 7's transposed read in the natural k order: lane group g holds k = 8 g .. 8 g + 7 of a 32-deep sub-step (lo at
+// row 8 g + qq, hi 4 rows below), so the dY fragment is ONE 16-byte read (bank-conflict-free under swz_b2) instead of
+// two 8-byte halves of two chunks (2-way conflicted: 31 % of the LDS cycles, profiles/r6_gemm_routing.md)
+// (rows r and r + 4 carry different swz_a chunk swizzles: the hi half has its own offset)
+__device__ __forceinline__ bf16x8 lds_tr4(const char* base, int off, int offh) {
+  s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4*)(base + off));
+  s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4*)(base + offh));
+  typedef __attribute__((ext_vector_type(8))) short s16x8;
+  s16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+  return __builtin_bit_cast(bf16x8, v);
+}
+
 __device__ __forceinline__ bf16x8 lds_b2(const char* base, int off1, int off2) {
   const uint2 a = *(const uint2*)(base + off1), b = *(const uint2*)(base + off2);
   const uint4 v = make_uint4(a.x, a.y, b.x, b.y);
@@ -398,7 +410,7 @@ struct Stager2 {
 
 template <class G>
 __device__ __forceinline__ void ring2_loop(char* __restrict__ b0, char* __restrict__ b1, int nsteps, Stager2<G>& st,
-                                           const int (&offA)[G::FM], int ob00, int ob01, int ob10, int ob11,
+                                           const int (&offA)[G::FM], const int (&offH)[G::FM], int ob0, int ob1,
                                            f32x4 (&acc)[G::FM][G::FN]) {
   constexpr int PPW = G::PPW;
   bf16x8 fa[G::FM], fb[2][G::FN];
@@ -411,9 +423,9 @@ __device__ __forceinline__ void ring2_loop(char* __restrict__ b0, char* __restri
   __builtin_amdgcn_s_waitcnt(waitcnt_imm(PPW, 0));
   __builtin_amdgcn_s_barrier();
 #pragma unroll
-  for (int j = 0; j < G::FN; ++j) fb[0][j] = lds_b2(b0, ob00 + 2048 * j, ob01 + 2048 * j);
+  for (int j = 0; j < G::FN; ++j) fb[0][j] = *(const bf16x8*)(b0 + ob0 + 2048 * j);
 #pragma unroll
-  for (int i = 0; i < G::FM; ++i) fa[i] = lds_tr(b0, offA[i]);
+  for (int i = 0; i < G::FM; ++i) fa[i] = lds_tr4(b0, offA[i], offH[i]);
   for (int t0 = 0; t0 < nsteps; t0 += 2) {
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
@@ -422,28 +434,28 @@ __device__ __forceinline__ void ring2_loop(char* __restrict__ b0, char* __restri
         char* nxt = u == 0 ? b1 : b0;
         // sub-step 0: k 0..31 of stage t from registers; read k 32..63 of the same slot
 #pragma unroll
-        for (int j = 0; j < G::FN; ++j) fb[1][j] = lds_b2(cur, ob10 + 2048 * j, ob11 + 2048 * j);
+        for (int j = 0; j < G::FN; ++j) fb[1][j] = *(const bf16x8*)(cur + ob1 + 2048 * j);
         __builtin_amdgcn_s_setprio(1);
 #pragma unroll
         for (int i = 0; i < G::FM; ++i) {
 #pragma unroll
           for (int j = 0; j < G::FN; ++j)
             acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[0][j], acc[i][j], 0, 0, 0);
-          fa[i] = lds_tr(cur, offA[i] + 32 * AROWB);
+          fa[i] = lds_tr4(cur, offA[i] + 32 * AROWB, offH[i] + 32 * AROWB);
         }
         __builtin_amdgcn_s_setprio(0);
         // stage t + 1 landed (this wave's DMAs) and every wave is done reading slot t
         __builtin_amdgcn_s_waitcnt(waitcnt_imm(0, 0));
         __builtin_amdgcn_s_barrier();
 #pragma unroll
-        for (int j = 0; j < G::FN; ++j) fb[0][j] = lds_b2(nxt, ob00 + 2048 * j, ob01 + 2048 * j);
+        for (int j = 0; j < G::FN; ++j) fb[0][j] = *(const bf16x8*)(nxt + ob0 + 2048 * j);
         __builtin_amdgcn_s_setprio(1);
 #pragma unroll
         for (int i = 0; i < G::FM; ++i) {
 #pragma unroll
           for (int j = 0; j < G::FN; ++j)
             acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[1][j], acc[i][j], 0, 0, 0);
-          fa[i] = lds_tr(nxt, offA[i]);
+          fa[i] = lds_tr4(nxt, offA[i], offH[i]);
           if (2 * i < PPW) st.piece(cur, 2 * i);          // refill slot t with stage t + 2
           if (2 * i + 1 < PPW) st.piece(cur, 2 * i + 1);
         }
@@ -475,25 +487,24 @@ __global__ void __launch_bounds__(NT) dgrad2_kernel(const u16* __restrict__ dY, 
   Stager2<G> st;
   st.init(W, dY, ldw, ldd, n0, m0, w, lane, K / BK2);
   const int g = lane >> 4, ii = lane & 15, qq = ii >> 2, pp = ii & 3;
-  const int pg = ((g & 1) << 1) | (g >> 1);
-  const int r0 = 4 * pg + qq;
-  int offA[G::FM];
+  const int r0 = 8 * g + qq;  // natural k order (lds_tr4): lane group g holds k 8 g .. 8 g + 7 of each sub-step
+  int offA[G::FM], offH[G::FM];
 #pragma unroll
   for (int i = 0; i < G::FM; ++i) {
     const int nl = wm * G::TM + 16 * i;
     offA[i] = (nl >> 7) * AIMG2 + img_a(r0, 2 * ((nl & 127) >> 4) + (pp >> 1)) + 8 * (pp & 1);
+    offH[i] = (nl >> 7) * AIMG2 + img_a(r0 + 4, 2 * ((nl & 127) >> 4) + (pp >> 1)) + 8 * (pp & 1);
   }
-  // B fragment of sub-step s: bytes 64 s + 8 pg and 64 s + 32 + 8 pg of row wn*TN + 16 j + ii (swizzle of ii)
+  // B fragment of sub-step s: the 16-byte chunk 4 s + g of row wn*TN + 16 j + ii (swizzle of ii)
   const int rowb = wn * G::TN + ii;
-  const int bbase = G::STAGE_A + rowb * BROWB2 + 8 * (pg & 1);
-  const int ob00 = bbase + 16 * swz_b2(ii, (pg >> 1)), ob01 = bbase + 16 * swz_b2(ii, 2 + (pg >> 1));
-  const int ob10 = bbase + 16 * swz_b2(ii, 4 + (pg >> 1)), ob11 = bbase + 16 * swz_b2(ii, 6 + (pg >> 1));
+  const int bbase = G::STAGE_A + rowb * BROWB2;
+  const int ob0 = bbase + 16 * swz_b2(ii, g), ob1 = bbase + 16 * swz_b2(ii, 4 + g);
   f32x4 acc[G::FM][G::FN];
 #pragma unroll
   for (int i = 0; i < G::FM; ++i)
 #pragma unroll
     for (int j = 0; j < G::FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  ring2_loop<G>(smem, smem + G::STAGE, K / BK2, st, offA, ob00, ob01, ob10, ob11, acc);
+  ring2_loop<G>(smem, smem + G::STAGE, K / BK2, st, offA, offH, ob0, ob1, acc);
   __syncthreads();
   epilogue<Cfg<BM, BN, WM, WN, 2>, EPI>(smem, acc, ea, n0, m0, wm, wn, w, lane);
 }
