@@ -14,10 +14,10 @@
 // kernel reads its operands (gemm_wgrad.hip: [32 k][128 n] images, 256-B rows, chunk XOR swizzle applied on the
 // global source address because global_load_lds writes lane-linear), and the dY tile (K-contiguous rows m) is
 // the B operand read along its rows like the forward kernel's weight tile (gemm_tn.hip: [m][32 k] images,
-// 64-B rows). The transposed read hands lane group g the reduction indices
-//   phi(g, j) = 4 perm(g) + j (j < 4),  16 + 4 perm(g) + (j - 4) (j >= 4),  perm = {0, 2, 1, 3}
-// of each 32-deep step, so the B fragment is fetched in the same k order with two 8-byte reads per lane
-// (ds_read_b64 at bytes 8 perm(g) and 32 + 8 perm(g) of the row) instead of one 16-byte read.
+// 64-B rows). The transposed reads hand lane group g the reduction indices 8 g .. 8 g + 7 of each 32-deep step (rows
+// 8 g + qq and 8 g + 4 + qq, each with its own chunk swizzle), the natural order, so the B fragment is ONE 16-byte
+// read per lane (conflict-free under the B swizzle; the permuted order used before took two 8-byte reads, 2-way
+// bank-conflicted).
 //
 // Main loop = the ring of gemm_wgrad.hip: 256 x 256 tile (n x m) per 512-thread workgroup (8 waves 2 x 4),
 // BK = 32 per stage, NS stages of global_load_lds in flight, counted vmcnt + raw s_barrier once per stage,
@@ -51,17 +51,10 @@ __device__ __forceinline__ void glds16(const u16* src, char* dst) {
 
 typedef __attribute__((address_space(3))) s16x4 lds_s4;
 
-__device__ __forceinline__ bf16x8 lds_tr(const char* base, int off) {
-  s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4*)(base + off));
-  s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4*)(base + off + 16 * AROWB));
-  typedef __attribute__((ext_vector_type(8))) short s16x8;
-  s16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-  return __builtin_bit_cast(bf16x8, v);
-}
-
-// cfg 7's transposed read in the natural k order: lane group g holds k = 8 g .. 8 g + 7 of a 32-deep sub-step (lo at
-// row 8 g + qq, hi 4 rows below), so the dY fragment is ONE 16-byte read (bank-conflict-free under swz_b2) instead of
-// two 8-byte halves of two chunks (2-way conflicted: 31 % of the LDS cycles, profiles/r6_gemm_routing.md)
+// The transposed weight read in the natural k order: lane group g holds k = 8 g .. 8 g + 7 of a 32-deep step (lo at
+// row 8 g + qq, hi 4 rows below), so the dY fragment is ONE 16-byte read (bank-conflict-free under swz_b / swz_b2)
+// instead of two 8-byte halves of two chunks in a permuted k order (2-way conflicted: 31 % of cfg 7's LDS cycles,
+// profiles/r6_gemm_routing.md)
 // (rows r and r + 4 carry different swz_a chunk swizzles: the hi half has its own offset)
 __device__ __forceinline__ bf16x8 lds_tr4(const char* base, int off, int offh) {
   s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4*)(base + off));
@@ -71,11 +64,6 @@ __device__ __forceinline__ bf16x8 lds_tr4(const char* base, int off, int offh) {
   return __builtin_bit_cast(bf16x8, v);
 }
 
-__device__ __forceinline__ bf16x8 lds_b2(const char* base, int off1, int off2) {
-  const uint2 a = *(const uint2*)(base + off1), b = *(const uint2*)(base + off2);
-  const uint4 v = make_uint4(a.x, a.y, b.x, b.y);
-  return __builtin_bit_cast(bf16x8, v);
-}
 
 constexpr unsigned waitcnt_imm(int vm, int lgkm) {  // gfx9: vmcnt[3:0] expcnt[6:4] lgkmcnt[11:8] vmcnt[5:4]<<14
   return (unsigned)((vm & 15) | (7 << 4) | ((lgkm & 15) << 8) | ((vm >> 4) << 14));
@@ -153,7 +141,8 @@ __device__ __forceinline__ char* pick(int i, char* b0, char* b1, char* b2, char*
 template <class G, bool SCHED>
 __device__ __forceinline__ void ring_loop(char* __restrict__ b0, char* __restrict__ b1, char* __restrict__ b2,
                                           char* __restrict__ b3, char* __restrict__ b4, int nsteps, Stager<G>& st,
-                                          const int (&offA)[G::FM], int offB1, int offB2, f32x4 (&acc)[G::FM][G::FN]) {
+                                          const int (&offA)[G::FM], const int (&offH)[G::FM], int offB,
+                                          f32x4 (&acc)[G::FM][G::FN]) {
   constexpr int NS = G::NS, PPW = G::PPW;
   constexpr int U = (NS % 2) ? 2 * NS : NS;  // unroll: stage slot and B register set both compile-time
   bf16x8 fa[G::FM], fb[2][G::FN];
@@ -162,9 +151,9 @@ __device__ __forceinline__ void ring_loop(char* __restrict__ b0, char* __restric
   __builtin_amdgcn_s_waitcnt(waitcnt_imm((NS - 1) * PPW, 0));
   __builtin_amdgcn_s_barrier();
 #pragma unroll
-  for (int j = 0; j < G::FN; ++j) fb[0][j] = lds_b2(b0, offB1 + 1024 * j, offB2 + 1024 * j);
+  for (int j = 0; j < G::FN; ++j) fb[0][j] = *(const bf16x8*)(b0 + offB + 1024 * j);
 #pragma unroll
-  for (int i = 0; i < G::FM; ++i) fa[i] = lds_tr(b0, offA[i]);
+  for (int i = 0; i < G::FM; ++i) fa[i] = lds_tr4(b0, offA[i], offH[i]);
   for (int t0 = 0; t0 < nsteps; t0 += U) {
 #pragma unroll
     for (int u = 0; u < U; ++u) {
@@ -175,14 +164,14 @@ __device__ __forceinline__ void ring_loop(char* __restrict__ b0, char* __restric
         const char* nxt = pick((u + 1) % NS, b0, b1, b2, b3, b4);
         const int cb = u & 1;
 #pragma unroll
-        for (int j = 0; j < G::FN; ++j) fb[cb ^ 1][j] = lds_b2(nxt, offB1 + 1024 * j, offB2 + 1024 * j);
+        for (int j = 0; j < G::FN; ++j) fb[cb ^ 1][j] = *(const bf16x8*)(nxt + offB + 1024 * j);
         __builtin_amdgcn_s_setprio(1);
 #pragma unroll
         for (int i = 0; i < G::FM; ++i) {
 #pragma unroll
           for (int j = 0; j < G::FN; ++j)
             acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[cb][j], acc[i][j], 0, 0, 0);
-          fa[i] = lds_tr(nxt, offA[i]);
+          fa[i] = lds_tr4(nxt, offA[i], offH[i]);
           if (i < PPW) st.piece(dst, i);
           if (SCHED) {
             __builtin_amdgcn_sched_group_barrier(0x008, G::FN, 0);  // MFMA
@@ -320,18 +309,18 @@ __global__ void __launch_bounds__(WM * WN * 64, OCC) dgrad_kernel(const u16* __r
   Stager<G> st;
   st.init(W, dY, ldw, ldd, n0, m0, w, lane, K / BK);
   const int g = lane >> 4, ii = lane & 15, qq = ii >> 2, pp = ii & 3;
-  const int pg = ((g & 1) << 1) | (g >> 1);  // the block order of the transposed A reads (gemm_wgrad.hip)
-  const int r0 = 4 * pg + qq;
-  int offA[G::FM];
+  const int r0 = 8 * g + qq;  // natural k order (lds_tr4): lane group g holds k 8 g .. 8 g + 7
+  int offA[G::FM], offH[G::FM];
 #pragma unroll
   for (int i = 0; i < G::FM; ++i) {
     const int nl = wm * G::TM + 16 * i;
     offA[i] = (nl >> 7) * AIMG + img_a(r0, 2 * ((nl & 127) >> 4) + (pp >> 1)) + 8 * (pp & 1);
+    offH[i] = (nl >> 7) * AIMG + img_a(r0 + 4, 2 * ((nl & 127) >> 4) + (pp >> 1)) + 8 * (pp & 1);
   }
-  // B fragment rows wn*TN + 16 j + ii all share the swizzle of ii: fragment j is 1 KB after j - 1
+  // B fragment: the 16-byte chunk g of row wn*TN + 16 j + ii (rows share the swizzle of ii: fragment j is 1 KB
+  // after j - 1); conflict-free for ds_read_b128's 16-lane groups under swz_b
   const int rowb = wn * G::TN + ii;
-  const int offB1 = G::STAGE_A + rowb * BROWB + 16 * swz_b(ii, pg >> 1) + 8 * (pg & 1);
-  const int offB2 = G::STAGE_A + rowb * BROWB + 16 * swz_b(ii, 2 + (pg >> 1)) + 8 * (pg & 1);
+  const int offB = G::STAGE_A + rowb * BROWB + 16 * swz_b(ii, g);
   f32x4 acc[G::FM][G::FN];
 #pragma unroll
   for (int i = 0; i < G::FM; ++i)
@@ -341,7 +330,7 @@ __global__ void __launch_bounds__(WM * WN * 64, OCC) dgrad_kernel(const u16* __r
   char* b[5];
 #pragma unroll
   for (int i = 0; i < 5; ++i) b[i] = smem + (i < NS ? i : 0) * G::STAGE;
-  ring_loop<G, SCHED>(b[0], b[1], b[2], b[3], b[4], K / BK, st, offA, offB1, offB2, acc);
+  ring_loop<G, SCHED>(b[0], b[1], b[2], b[3], b[4], K / BK, st, offA, offH, offB, acc);
   __syncthreads();
   epilogue<G, EPI>(smem, acc, ea, n0, m0, wm, wn, w, lane);
 }
