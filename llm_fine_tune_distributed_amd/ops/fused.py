@@ -374,7 +374,7 @@ def _delta_ok(dy2d: torch.Tensor, w: torch.Tensor, a2d: torch.Tensor) -> bool:
     tiles = (M // 256) * (w.shape[1] // 256)
     # (under a reduced CU budget a partial last round is split over K, which the delta epilogue cannot take: the
     # attention node's own delta kernel is cheaper than a second round of whole tiles)
-    return (_dgrad_ok(dy2d, w) and _dgrad_cfg(dy2d) == 14 and K < 8192 and a2d.dtype == torch.bfloat16
+    return (_dgrad_ok(dy2d, w) and K % 128 == 0 and K < 8192 and a2d.dtype == torch.bfloat16
             and (_CU_BUDGET >= _NUM_CUS or tiles % _CU_BUDGET == 0 or tiles < _CU_BUDGET)
             and a2d.shape == (M, w.shape[1]) and a2d.stride(1) == 1 and a2d.stride(0) % 8 == 0
             and a2d.data_ptr() % 16 == 0)
@@ -459,25 +459,49 @@ def _dgrad_ok(dy2d: torch.Tensor, w: torch.Tensor) -> bool:
             and w.data_ptr() % 16 == 0)
 
 
-def _dgrad_cfg(dy2d: torch.Tensor, swiglu: bool = False) -> int:
-    """Kernel configuration (csrc/gemm_dgrad.hip): 14 = the 4-wave ring of csrc/gemm_4w.hip (one read / DMA piece per
-    MFMA gap) on every plain reduction length that is a multiple of 128 (M = 8192, profiles/r6_gemm_routing.md: o 0.0577
-    ms, qkv 0.0786, down 0.297 vs 0.315 for hipBLASLt, gate_up 0.543, lm_head 2.95 vs 3.09); 7 = 256 x 256 tiles with
-    64-deep stages for the fused SwiGLU-backward epilogue (0.425 vs 0.483 ms for the 4-wave kernel's register
-    epilogue) and K % 128 != 0; 5 = the 32-deep three-stage ring for K % 64 != 0."""
+# SFTAMD_DGRAD_RING8=0: plain dgrads stay on the 4-wave ring (cfg 14) whatever the grid; also the A/B seam
+_DGRAD_RING8 = os.environ.get("SFTAMD_DGRAD_RING8", "1") != "0"
+
+
+def _ring8_rounds(M: int, N: int) -> bool:
+    """The 8-wave rings run whole rounds of 256 x 256 tiles over the 256 CUs, or the wave-tail launch of
+    dgrad_gemm (csrc/gemm_dgrad.hip) turns the partial last round into one round of 256 x 128 half tiles."""
+    nbm, nbn = M // 256, N // 256
+    tiles = nbm * nbn
+    if tiles % _NUM_CUS == 0:
+        return True
+    if tiles < _NUM_CUS or _NUM_CUS % nbm:
+        return False
+    main_n = tiles // _NUM_CUS * (_NUM_CUS // nbm)
+    return (nbn - main_n) * (M // 128) <= _NUM_CUS
+
+
+def _dgrad_cfg(dy2d: torch.Tensor, swiglu: bool = False, N: Optional[int] = None) -> int:
+    """Kernel configuration (csrc/gemm_dgrad.hip). 5 = the 8-wave 32-deep three-stage ring, 7 = its 64-deep
+    two-stage sibling, both with conflict-free natural-order transposed reads; 14 = the 4-wave ring of
+    csrc/gemm_4w.hip (one read / DMA piece per MFMA gap, split-K for a partial last round).
+    M = 8192 (profiles/r6_gemm_routing.md, interleaved, ms): SwiGLU-fused down 0.400 (5) vs 0.409 (7) vs 0.483
+    (4-wave register epilogue); plain gate_up 0.535 (5) vs 0.546 (14), down 0.289 vs 0.297, qkv 0.0789 vs 0.0788,
+    o 0.058 vs 0.0597, lm_head 3.11 vs 3.04 -> cfg 5 when its grid is whole rounds (or the wave tail applies) and
+    the reduction is not vocabulary-long, cfg 14 otherwise (ragged token counts: its split-K tail)."""
     K = dy2d.shape[1]
-    if not swiglu and K % 128 == 0:
+    if swiglu:
+        return 5
+    if K % 128 == 0:
+        if (_DGRAD_RING8 and N is not None and K < 65536 and _ring8_rounds(dy2d.shape[0], N)):
+            return 5
         return 14
     return 7 if K % 64 == 0 else 5
 
 
 def dgrad_mm(dy2d: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
     """dX = dy @ W (W = the projection's [out, in] weight). The HIP kernel where it beats hipBLASLt: every
-    SmolLM3 shape with M % 256 == 0 on the 4-wave kernel (gate_up and lm_head included, _dgrad_cfg); reductions that
-    are not a multiple of 128 of at most 4096 output features into at most 4096 inputs on cfg 7 / 5."""
+    SmolLM3 / Llama shape with M % 256 == 0 and K % 128 == 0 (gate_up and lm_head included; cfg 5 or 14,
+    _dgrad_cfg); reductions that are not a multiple of 128 of at most 4096 output features into at most 4096 inputs
+    on cfg 7 / 5."""
     if _dgrad_ok(dy2d, w):
-        cfg = _dgrad_cfg(dy2d)
-        if cfg == 14 or _DGRAD_MODE == "hip" or (dy2d.shape[1] <= 4096 and w.shape[1] <= 4096):
+        cfg = _dgrad_cfg(dy2d, N=w.shape[1])
+        if dy2d.shape[1] % 128 == 0 or _DGRAD_MODE == "hip" or (dy2d.shape[1] <= 4096 and w.shape[1] <= 4096):
             return _ext.ops().dgrad_gemm(dy2d, w, None, cfg)
     return torch.mm(dy2d, w)
 

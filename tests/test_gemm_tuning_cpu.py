@@ -55,3 +55,28 @@ def test_weight_gradient_pair_planning():
     p1 = torch.nn.Parameter(torch.zeros(256, 256))
     x = torch.zeros(1024, 256, dtype=torch.bfloat16)
     assert not F._pair_ok(p0, x, x, p1, x, x)
+
+
+def test_dgrad_routing():
+    """Input-gradient configs (ops.fused._dgrad_cfg): the 8-wave 32-deep ring (5) for the SwiGLU-fused down dgrad and
+    for plain dgrads whose grid is whole rounds or takes the wave-tail launch; the 4-wave ring (14) for the
+    vocabulary-long lm_head reduction, ragged token counts and under SFTAMD_DGRAD_RING8=0."""
+    import torch
+    import llm_fine_tune_distributed_amd.ops.fused as F
+
+    def cfg(M, K, N, swiglu=False):
+        return F._dgrad_cfg(torch.empty(M, K, device="meta"), swiglu=swiglu, N=N)
+
+    assert cfg(8192, 2048, 11008, swiglu=True) == 5  # down + SwiGLU backward (1376 tiles, wave tail)
+    assert cfg(8192, 22016, 2048) == 5 and cfg(8192, 3072, 2048) == 5 and cfg(8192, 2048, 2048) == 5
+    assert cfg(8192, 2048, 11008) == 5  # 1376 tiles: 5 rounds + the half-tile round
+    assert cfg(8192, 128256, 2048) == 14  # lm_head
+    assert cfg(8192 + 512, 2048, 2048) == 14  # 34 x 8 = 272 tiles: 256 % 34 != 0, no wave tail
+    assert cfg(2048, 2048, 2048) == 14  # 64 tiles: less than one round
+    assert cfg(8192, 2016, 2048) == 5 and cfg(8192, 1984, 2048) == 7  # K % 128 != 0
+    F_ring8 = F._DGRAD_RING8
+    try:
+        F._DGRAD_RING8 = False
+        assert cfg(8192, 22016, 2048) == 14
+    finally:
+        F._DGRAD_RING8 = F_ring8
