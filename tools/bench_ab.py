@@ -7,7 +7,8 @@ error against the first variant.
     python tools/bench_ab.py wgrad lm_head 10,1214 --rounds 5
 
 wgrad: dW[N, K] = dy[T, N]^T x[T, K] (sftamd.wgrad_gemm cfg); fwd: y[T, N] = x[T, K] W[N, K]^T (sftamd.gemm_tn cfg); dgrad: dX[T, N] = dy[T, K] W[K, N] (sftamd.dgrad_gemm cfg;
-'blas' = torch.mm on the TunableOp selection; 'delta' = dgrad_gemm_delta). SmolLM3-3B shapes at T = 8192 tokens.
+'blas' = torch.mm on the TunableOp selection; 'delta' = dgrad_gemm_delta). SmolLM3-3B shapes at T = 8192 tokens;
+Llama-3-8B ones as l8b_qkv, l8b_o, l8b_gate_up, l8b_down, l8b_lm_head.
 """
 import argparse
 import json
@@ -25,6 +26,10 @@ WGRAD = {"qkv": (3072, 2048), "o": (2048, 2048), "gate_up": (22016, 2048), "down
          "lm_head": (128256, 2048)}
 DGRAD = {"qkv": (3072, 2048), "o": (2048, 2048), "gate_up": (22016, 2048), "down": (2048, 11008),
          "lm_head": (128256, 2048)}  # (K, N): dX[T, N] = dy[T, K] W[K, N]
+# Llama-3-8B widths (hidden 4096, 32 q / 8 kv heads x 128, intermediate 14336): the same layouts, "l8b_" names
+WGRAD.update({"l8b_qkv": (6144, 4096), "l8b_o": (4096, 4096), "l8b_gate_up": (28672, 4096),
+              "l8b_down": (4096, 14336), "l8b_lm_head": (128256, 4096)})
+DGRAD.update({k: v for k, v in WGRAD.items() if k.startswith("l8b_")})
 
 
 def timeit(fn, iters):
