@@ -87,6 +87,7 @@ TORCH_LIBRARY(sftamd, m) {
   m.def("sample_token(Tensor logits, Tensor(a!) presence, Tensor(b!) state, Tensor(c!)? tok_out, Tensor(d!)? pos_out, Tensor(e!)? len_out, Tensor(f!)? log, float temperature, int top_k, float top_p, float repetition_penalty, bool do_sample, int seed) -> ()");
   // weight-gradient GEMM: out[N,K] (+)= dy[T,N]^T x[T,K]
   m.def("wgrad_gemm(Tensor(a!) out, Tensor dy, Tensor x, bool accumulate, int cfg=14, Tensor(b!)? norm=None) -> ()");
+  m.def("wgrad_gemm_multi(Tensor(a!)[] outs, Tensor[] dys, Tensor[] xs, int[] accs, Tensor(b!)[] norms, int split_all=0, int split_left=0) -> ()");
   m.def("wgrad_gemm_pair(Tensor(a!) out0, Tensor dy0, Tensor x0, bool acc0, Tensor(b!)? norm0, Tensor(c!) out1, Tensor dy1, Tensor x1, bool acc1, Tensor(d!)? norm1, int split_all=0) -> ()");
   // input-gradient GEMM dX = dy w (w [K, N]), optional fused SwiGLU backward (csrc/gemm_dgrad.hip)
   m.def("dgrad_gemm(Tensor dy, Tensor w, Tensor? gate_up=None, int cfg=14) -> Tensor");

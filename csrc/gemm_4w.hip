@@ -43,7 +43,10 @@
 // per split) into fp32 slabs summed in a fixed order by splitk_fixup_kernel (deterministic); small grids (qkv 96
 // tiles, o_proj 64) split every tile. A stream-K partition of the last round (ranges crossing tile boundaries) was
 // measured and dropped: no faster on any SmolLM3 shape (profiles/r6_gemm_routing.md).
+#include <climits>
+
 #include "common.h"
+#include "g4_api.h"
 #include "splitk_fixup.h"
 
 namespace sftamd {
@@ -362,14 +365,20 @@ struct Prob {
   Epi ea;
 };
 
-// A launch runs one problem or two with the same reduction length (tiles [0, tiles0) = p0, the rest = p1, e.g. the
-// MLP's down and gate_up weight gradients as ONE grid: 344 + 688 = 1032 tiles = 4.03 rounds of 256 CUs instead of
-// 1.34 + 2.69 — a partial last round costs most of a full one, profiles/r6_gemm_routing.md). splits > 1: the tiles
-// past ndp are split into `splits` equal ranges of 128-deep blocks (pieces -> fp32 slabs of their problem's P,
-// splitk_fixup_kernel per problem).
+// Up to four problems of one launch: problem i owns tiles [s_i, s_{i+1}) (s_0 = 0; unused starts = INT_MAX).
+struct Probs {
+  Prob q0, q1, q2, q3;
+  int s1, s2, s3;
+};
+
+// A launch runs one to four problems with the same reduction length (e.g. the MLP's down and gate_up weight
+// gradients as ONE grid: 344 + 688 = 1032 tiles = 4.03 rounds of 256 CUs instead of 1.34 + 2.69 — a partial last round
+// costs most of a full one, profiles/r6_gemm_routing.md; with the next layer's o_proj + qkv: 1192 tiles = 4 rounds +
+// 168 split tiles). splits > 1: the tiles past ndp are split into `splits` equal ranges of 128-deep blocks (pieces ->
+// fp32 slabs of their problem's P, splitk_fixup_kernel per problem).
 template <int LA, int LB>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1)))
-g4_kernel(Prob q0, Prob q1, int tiles0, int kred, int ndp, int splits) {
+g4_kernel(Probs ps, int kred, int ndp, int splits) {
   __shared__ __attribute__((aligned(16))) char smem[4 * SLOT32];
   // Blocks [0, ndp) own whole tiles, XCD-aware bijective remap among them (consecutive ids on one XCD: shared L2 for
   // the GROUP-blocked tile order); blocks >= ndp are the split pieces. Classes by BLOCK index, not by remapped id:
@@ -390,23 +399,26 @@ g4_kernel(Prob q0, Prob q1, int tiles0, int kred, int ndp, int splits) {
     p0 = (int)((long)sk * nb_all / splits);
     p1 = (int)((long)(sk + 1) * nb_all / splits);
   }
-  // the problem this tile belongs to (wave-uniform selects of kernel arguments)
-  const bool sec = tile >= tiles0;
-  const int lt = sec ? tile - tiles0 : tile;
-  const u16* A = sec ? q1.A : q0.A;
-  const u16* B = sec ? q1.B : q0.B;
-  const long lda = sec ? q1.lda : q0.lda, ldb = sec ? q1.ldb : q0.ldb, park = sec ? q1.park : q0.park;
+  // the problem this tile belongs to (wave-uniform selects of kernel arguments, no indexed copy of the struct)
+  const int pi = (tile >= ps.s1) + (tile >= ps.s2) + (tile >= ps.s3);
+#define G4SEL(f) (pi == 0 ? ps.q0.f : pi == 1 ? ps.q1.f : pi == 2 ? ps.q2.f : ps.q3.f)
+  const int start = pi == 0 ? 0 : pi == 1 ? ps.s1 : pi == 2 ? ps.s2 : ps.s3;
+  const int lt = tile - start;
+  const u16* A = G4SEL(A);
+  const u16* B = G4SEL(B);
+  const long lda = G4SEL(lda), ldb = G4SEL(ldb), park = G4SEL(park);
   Epi ea;
-  ea.C = sec ? q1.ea.C : q0.ea.C;
-  ea.P = sec ? q1.ea.P : q0.ea.P;
-  ea.ldc = sec ? q1.ea.ldc : q0.ea.ldc;
-  ea.flags = sec ? q1.ea.flags : q0.ea.flags;
-  ea.O = sec ? q1.ea.O : q0.ea.O;
-  ea.Dl = sec ? q1.ea.Dl : q0.ea.Dl;
-  ea.ldO = sec ? q1.ea.ldO : q0.ea.ldO;
-  ea.dM = sec ? q1.ea.dM : q0.ea.dM;
+  ea.C = G4SEL(ea.C);
+  ea.P = G4SEL(ea.P);
+  ea.ldc = G4SEL(ea.ldc);
+  ea.flags = G4SEL(ea.flags);
+  ea.O = G4SEL(ea.O);
+  ea.Dl = G4SEL(ea.Dl);
+  ea.ldO = G4SEL(ea.ldO);
+  ea.dM = G4SEL(ea.dM);
   int m0, n0;
-  tile_origin(lt, sec ? q1.nbm : q0.nbm, sec ? q1.nbn : q0.nbn, sec ? q1.group : q0.group, m0, n0);
+  tile_origin(lt, G4SEL(nbm), G4SEL(nbn), G4SEL(group), m0, n0);
+#undef G4SEL
   const int tid = threadIdx.x, lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = w >> 1, wn = w & 1;
   const long k0 = (long)p0 * 4 * BK32;
@@ -428,7 +440,7 @@ g4_kernel(Prob q0, Prob q1, int tiles0, int kred, int ndp, int splits) {
   __builtin_amdgcn_sched_barrier(0);
   if (wgid >= ndp) {
     // slab of this problem's piece: its split tiles start at its first tile past ndp
-    const int ndpl = sec ? max(ndp - tiles0, 0) : min(ndp, tiles0);
+    const int ndpl = max(ndp - start, 0);
     store_partial(acc, ea.P + ((long)(lt - ndpl) * splits + sk) * 65536, wm, wn, lane);
     return;
   }
@@ -455,10 +467,15 @@ static Prob prob(const u16* A, long lda, const u16* B, long ldb, int M, int N, c
 }
 
 template <int LA, int LB>
-static void launch2(const Prob& q0, const Prob& q1, int tiles0, int total, int kred, int ndp, int splits) {
+static void launchn(const Probs& ps, int total, int kred, int ndp, int splits) {
   const int grid = ndp + (total - ndp) * splits;
-  g4_kernel<LA, LB><<<grid, 256, 0, cur_stream()>>>(q0, q1, tiles0, kred, ndp, splits);
+  g4_kernel<LA, LB><<<grid, 256, 0, cur_stream()>>>(ps, kred, ndp, splits);
   SFT_LAUNCH_CHECK();
+}
+
+template <int LA, int LB>
+static void launch2(const Prob& q0, const Prob& q1, int tiles0, int total, int kred, int ndp, int splits) {
+  launchn<LA, LB>(Probs{q0, q1, q1, q1, tiles0, INT_MAX, INT_MAX}, total, kred, ndp, splits);
 }
 
 template <int LA, int LB>
@@ -508,69 +525,87 @@ void g4_wgrad(const at::Tensor& dy, const at::Tensor& x, at::Tensor& out, bool a
   }
 }
 
-// Two weight gradients over the same tokens as ONE grid (g4_kernel with two problems): out0 (+)= dy0^T x0 and
-// out1 (+)= dy1^T x1. The whole rounds of 256 (cu_budget) tiles run across both; the partial last round must fall in
-// problem 1 and is split over the tokens (fp32 slabs + the ordered fixup), as the hybrid single-problem launch does.
-// split_all > 1: every tile of both problems split that many ways (small pairs such as o_proj + qkv: 64 + 96 tiles x 3
-// = 480 pieces = 2 rounds of third-tiles, against one round of quarter-tiles + one of half-tiles apart).
-void g4_wgrad_pair(const at::Tensor& dy0, const at::Tensor& x0, at::Tensor& out0, bool acc0, float* nrm0, long cap0,
-                   const at::Tensor& dy1, const at::Tensor& x1, at::Tensor& out1, bool acc1, float* nrm1, long cap1,
-                   int split_all) {
-  const int T = dy0.size(0);
-  const int N0 = dy0.size(1), K0 = x0.size(1), N1 = dy1.size(1), K1 = x1.size(1);
-  SFT_CHECK(dy1.size(0) == T && x0.size(0) == T && x1.size(0) == T, "wgrad pair: the same tokens");
-  SFT_CHECK(N0 % 256 == 0 && K0 % 256 == 0 && N1 % 256 == 0 && K1 % 256 == 0 && T % 128 == 0 && T > 0,
-            "wgrad pair: N, K % 256, T % 128");
-  for (const void* ptr : {dy0.data_ptr(), x0.data_ptr(), out0.data_ptr(), dy1.data_ptr(), x1.data_ptr(), out1.data_ptr()})
-    SFT_CHECK((uintptr_t)ptr % 16 == 0, "wgrad pair: 16-byte aligned operands");
-  const int tiles0 = (N0 / 256) * (K0 / 256), tiles1 = (N1 / 256) * (K1 / 256), total = tiles0 + tiles1;
+// Up to four weight gradients over the same tokens as ONE grid (g4_kernel with several problems): out_i (+)= dy_i^T
+// x_i. The whole rounds of B (cu_budget) tiles run across the problems in order; the partial last round (the tiles past
+// them, which may span several problems: put the small ones last) is split over the tokens into fp32 slabs + the
+// ordered fixup of each problem that has split tiles, split_left ways (0: min(8, B / leftover), the hybrid rule).
+// split_all > 1: every tile split that many ways (small groups such as o_proj + qkv: 64 + 96 tiles x 3 = 480 pieces =
+// 2 rounds of third-tiles, against one round of quarter-tiles + one of half-tiles apart).
+void g4_wgrad_multi(const std::vector<WgradJob>& jobs, int split_all, int split_left) {
+  const int np = (int)jobs.size();
+  SFT_CHECK(np >= 1 && np <= 4, "wgrad multi: 1..4 problems");
+  const int T = jobs[0].dy.size(0);
+  int tiles[4] = {0, 0, 0, 0}, start[5] = {0, 0, 0, 0, 0};
+  for (int i = 0; i < np; ++i) {
+    const WgradJob& j = jobs[i];
+    const int N = j.dy.size(1), K = j.x.size(1);
+    SFT_CHECK(j.dy.size(0) == T && j.x.size(0) == T, "wgrad multi: the same tokens");
+    SFT_CHECK(N % 256 == 0 && K % 256 == 0 && T % 128 == 0 && T > 0, "wgrad multi: N, K % 256, T % 128");
+    SFT_CHECK((uintptr_t)j.dy.data_ptr() % 16 == 0 && (uintptr_t)j.x.data_ptr() % 16 == 0 &&
+                  (uintptr_t)j.out.data_ptr() % 16 == 0,
+              "wgrad multi: 16-byte aligned operands");
+    tiles[i] = (N / 256) * (K / 256);
+    start[i + 1] = start[i] + tiles[i];
+  }
+  const int total = start[np];
   const int B = cu_budget();
   int ndp = total / B * B, splits = 1;
   if (split_all > 1) {
     ndp = 0;
     splits = std::min(split_all, T / 128);
-  } else {
-    SFT_CHECK(total - ndp <= tiles1, "wgrad pair: the partial round must fall in the second problem");
-    if (total > ndp) splits = std::min(std::min(8, B / (total - ndp)), T / 128);
+  } else if (total > ndp) {
+    splits = split_left > 0 ? split_left : std::min(8, B / (total - ndp));
+    splits = std::min(splits, T / 128);
   }
   if (splits < 2) {
     splits = 1;
     ndp = total;
   }
   // per problem: whole tiles [0, w) and split tiles [w, tiles)
-  const int w0 = std::min(ndp, tiles0), w1 = std::max(ndp - tiles0, 0);
-  const int s0 = tiles0 - w0, s1 = tiles1 - w1;
-  SFT_CHECK(nrm0 == nullptr || (long)w0 * 8 + (long)s0 * 32 <= cap0, "wgrad pair: norm slot buffer 0 too small");
-  SFT_CHECK(nrm1 == nullptr || (long)w1 * 8 + (long)s1 * 32 <= cap1, "wgrad pair: norm slot buffer 1 too small");
-  auto slab = [&](int ns, int nw, float* nrm) {
-    return ns > 0 ? at::empty({(long)ns * splits * 65536 + (nrm != nullptr ? (long)nw * 8 : 0)},
-                              dy0.options().dtype(at::kFloat))
-                  : at::Tensor();
-  };
-  at::Tensor part0 = slab(s0, w0, nrm0), part1 = slab(s1, w1, nrm1);
-  auto epi = [&](const at::Tensor& out, int K, bool acc, float* nrm, int ns, const at::Tensor& part) {
+  int w[4], sn[4];
+  at::Tensor part[4];
+  g4::Prob q[4];
+  for (int i = 0; i < np; ++i) {
+    const WgradJob& j = jobs[i];
+    w[i] = std::min(std::max(ndp - start[i], 0), tiles[i]);
+    sn[i] = tiles[i] - w[i];
+    SFT_CHECK(j.nrm == nullptr || (long)w[i] * 8 + (long)sn[i] * 32 <= j.cap, "wgrad multi: norm slot buffer too small");
+    if (sn[i] > 0)
+      part[i] = at::empty({(long)sn[i] * splits * 65536 + (j.nrm != nullptr ? (long)w[i] * 8 : 0)},
+                          j.dy.options().dtype(at::kFloat));
+    const int N = j.dy.size(1), K = j.x.size(1);
     g4::Epi e{};
-    e.C = (u16*)out.data_ptr();
+    e.C = (u16*)j.out.data_ptr();
     e.ldc = K;
-    e.P = ns > 0 ? part.data_ptr<float>() : nrm;
-    e.flags = (acc ? 1 : 0) | (nrm != nullptr ? 2 : 0);
-    return e;
-  };
-  const g4::Prob q0 = g4::prob((const u16*)dy0.data_ptr(), N0, (const u16*)x0.data_ptr(), x0.stride(0), N0, K0,
-                               epi(out0, K0, acc0, nrm0, s0, part0), s0 > 0 ? (long)s0 * splits * 65536 : 0);
-  const g4::Prob q1 = g4::prob((const u16*)dy1.data_ptr(), N1, (const u16*)x1.data_ptr(), x1.stride(0), N1, K1,
-                               epi(out1, K1, acc1, nrm1, s1, part1), s1 > 0 ? (long)s1 * splits * 65536 : 0);
-  g4::launch2<g4::TR, g4::TR>(q0, q1, tiles0, total, T, ndp, splits);
-  auto fixup = [&](const at::Tensor& part, int ns, int nw, const at::Tensor& out, int N, int K, bool acc, float* nrm) {
-    if (ns <= 0) return;
-    const long n8 = (long)ns * 65536 / 8;
+    e.P = sn[i] > 0 ? part[i].data_ptr<float>() : j.nrm;
+    e.flags = (j.acc ? 1 : 0) | (j.nrm != nullptr ? 2 : 0);
+    q[i] = g4::prob((const u16*)j.dy.data_ptr(), N, (const u16*)j.x.data_ptr(), j.x.stride(0), N, K, e,
+                sn[i] > 0 ? (long)sn[i] * splits * 65536 : 0);
+  }
+  for (int i = np; i < 4; ++i) q[i] = q[np - 1];
+  g4::launchn<g4::TR, g4::TR>(g4::Probs{q[0], q[1], q[2], q[3], np > 1 ? start[1] : INT_MAX, np > 2 ? start[2] : INT_MAX,
+                        np > 3 ? start[3] : INT_MAX},
+                  total, T, ndp, splits);
+  for (int i = 0; i < np; ++i) {
+    if (sn[i] <= 0) continue;
+    const WgradJob& j = jobs[i];
+    const int N = j.dy.size(1), K = j.x.size(1);
+    const long n8 = (long)sn[i] * 65536 / 8;
     splitk_fixup_kernel<256, 256><<<(unsigned)((n8 + 255) / 256), 256, 0, cur_stream()>>>(
-        part.data_ptr<float>(), (u16*)out.data_ptr(), nw, ns, splits, K / 256, K, acc ? 1 : 0, nrm, N / 256,
-        std::min(g4::group_m(), N / 256));
+        part[i].data_ptr<float>(), (u16*)j.out.data_ptr(), w[i], sn[i], splits, K / 256, K, j.acc ? 1 : 0, j.nrm,
+        N / 256, std::min(g4::group_m(), N / 256));
     SFT_LAUNCH_CHECK();
-  };
-  fixup(part0, s0, w0, out0, N0, K0, acc0, nrm0);
-  fixup(part1, s1, w1, out1, N1, K1, acc1, nrm1);
+  }
+}
+
+// Two weight gradients as one grid (g4_wgrad_multi); without split_all the partial round must fall in problem 1.
+void g4_wgrad_pair(const at::Tensor& dy0, const at::Tensor& x0, at::Tensor& out0, bool acc0, float* nrm0, long cap0,
+                   const at::Tensor& dy1, const at::Tensor& x1, at::Tensor& out1, bool acc1, float* nrm1, long cap1,
+                   int split_all) {
+  const int tiles0 = (dy0.size(1) / 256) * (x0.size(1) / 256), tiles1 = (dy1.size(1) / 256) * (x1.size(1) / 256);
+  const int B = cu_budget(), total = tiles0 + tiles1;
+  SFT_CHECK(split_all > 1 || total - total / B * B <= tiles1, "wgrad pair: the partial round must fall in the second problem");
+  g4_wgrad_multi({WgradJob{dy0, x0, out0, acc0, nrm0, cap0}, WgradJob{dy1, x1, out1, acc1, nrm1, cap1}}, split_all, 0);
 }
 
 // Input gradient dX[M, N] = dy[M, K] . w[K, N] into out (row stride ldo; w may be a column slice: row stride

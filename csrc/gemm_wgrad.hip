@@ -22,6 +22,7 @@
 // transposed reads bank-conflict free; v_mfma_f32_16x16x32_bf16; XCD-aware workgroup remap; epilogue through LDS
 // (fp32, padded rows) so the beta-accumulate read-modify-write of the bf16 gradient is 16-byte vectorised.
 #include "common.h"
+#include "g4_api.h"
 #include "splitk_fixup.h"
 
 #include <type_traits>
@@ -461,9 +462,48 @@ void wgrad_gemm_pair(at::Tensor out0, at::Tensor dy0, at::Tensor x0, bool acc0, 
   g4_wgrad_pair(dy0, x0, out0, acc0, n0, c0, dy1, x1, out1, acc1, n1, c1, (int)split_all);
 }
 
+// Up to four weight gradients over the same tokens in ONE 4-wave launch (csrc/gemm_4w.hip g4_wgrad_multi), e.g. a
+// layer's down + gate_up with the next layer's o_proj + qkv: 1192 tiles = 4 whole rounds + 168 tiles split
+// split_left ways (0: the hybrid rule), against 4 rounds + 8 split tiles and a separate 2-round grid of third-tiles.
+// norms[i] with numel 0 = no norm slots for problem i.
+void wgrad_gemm_multi(at::TensorList outs, at::TensorList dys, at::TensorList xs, at::IntArrayRef accs,
+                      at::TensorList norms, int64_t split_all, int64_t split_left) {
+  const size_t n = outs.size();
+  SFT_CHECK(n >= 1 && n <= 4 && dys.size() == n && xs.size() == n && accs.size() == n && norms.size() == n,
+            "wgrad_gemm_multi: 1..4 problems, one of each argument per problem");
+  SFT_CHECK(split_all >= 0 && split_all <= 8 && split_left >= 0 && split_left <= 8, "wgrad_gemm_multi: splits 0..8");
+  std::vector<WgradJob> jobs;
+  bool any_norm = false;
+  for (size_t i = 0; i < n; ++i) {
+    const at::Tensor &out = outs[i], &dy = dys[i], &x = xs[i], &nr = norms[i];
+    SFT_CHECK_CUDA(dy);
+    SFT_CHECK_BF16(out);
+    SFT_CHECK_BF16(dy);
+    SFT_CHECK_BF16(x);
+    SFT_CHECK_CONTIG(dy);
+    SFT_CHECK_CONTIG(out);
+    SFT_CHECK(x.dim() == 2 && x.stride(1) == 1 && x.stride(0) % 8 == 0 && x.stride(0) >= x.size(1),
+              "wgrad_gemm_multi: x rows contiguous");
+    SFT_CHECK(out.size(0) == dy.size(1) && out.size(1) == x.size(1), "wgrad_gemm_multi: shape mismatch");
+    float* np = nullptr;
+    long cap = 0;
+    if (nr.defined() && nr.numel() > 0) {
+      SFT_CHECK(nr.scalar_type() == at::kFloat && nr.is_contiguous() && nr.is_cuda(), "wgrad_gemm_multi: fp32 norm slots");
+      np = nr.data_ptr<float>();
+      cap = nr.numel();
+      any_norm = true;
+    }
+    jobs.push_back(WgradJob{dy, x, out, accs[i] != 0, np, cap});
+  }
+  SFT_TRACE(trace_name("wgrad.multi", (int)n));
+  if (any_norm) SFT_TRACE("wgrad.norm_slots");
+  g4_wgrad_multi(jobs, (int)split_all, (int)split_left);
+}
+
 TORCH_LIBRARY_IMPL(sftamd, CUDA, m) {
   m.impl("wgrad_gemm", &wgrad_gemm);
   m.impl("wgrad_gemm_pair", &wgrad_gemm_pair);
+  m.impl("wgrad_gemm_multi", &wgrad_gemm_multi);
 }
 
 }  // namespace sftamd

@@ -285,11 +285,14 @@ class CausalLM(nn.Module):
 
         x = ops.embedding(ids, self.model.embed_tokens)
         residual = None
-        for layer in self.model.layers:
-            if self.gradient_checkpointing and self.training and torch.is_grad_enabled():
-                x, residual = checkpoint(layer, x, residual, rope_cs, cu_seqlens, max_seqlen, use_reentrant=False)
-            else:
-                x, residual = layer(x, residual, rope_cs, cu_seqlens, max_seqlen)
+        ckpt = self.gradient_checkpointing and self.training and torch.is_grad_enabled()
+        # (a layer's o_proj + qkv weight gradients join the previous layer's MLP launch: ops.wgrad_carry_scope)
+        with ops.wgrad_carry_scope(enabled=not ckpt):
+            for layer in self.model.layers:
+                if ckpt:
+                    x, residual = checkpoint(layer, x, residual, rope_cs, cu_seqlens, max_seqlen, use_reentrant=False)
+                else:
+                    x, residual = layer(x, residual, rope_cs, cu_seqlens, max_seqlen)
         n = self.model.norm
         h, _ = ops.add_rms_norm(x, residual, n.weight, n.eps)
 

@@ -167,13 +167,17 @@ def _accumulate_weight_grad(param: torch.Tensor, dy2d: torch.Tensor, x2d: torch.
 _WGRAD_PAIR = os.environ.get("SFTAMD_WGRAD_PAIR", "1") == "1"
 
 
+def _job_ok(p, dy, x) -> bool:
+    """A weight gradient the 4-wave multi-problem launches take (bf16 main_grad, 256-multiple shapes, aligned rows)."""
+    mg = getattr(p, "main_grad", None)
+    return (mg is not None and mg.dtype == torch.bfloat16 and mg.is_contiguous() and dy.dtype == torch.bfloat16
+            and x.dtype == torch.bfloat16 and dy.shape[1] % 256 == 0 and x.shape[1] % 256 == 0
+            and x.stride(1) == 1 and x.stride(0) % 8 == 0 and x.data_ptr() % 16 == 0 and dy.data_ptr() % 16 == 0
+            and mg.data_ptr() % 16 == 0)
+
+
 def _pair_ok(p0, dy0, x0, p1, dy1, x1) -> bool:
-    def one(p, dy, x):
-        mg = getattr(p, "main_grad", None)
-        return (mg is not None and mg.dtype == torch.bfloat16 and mg.is_contiguous() and dy.dtype == torch.bfloat16
-                and x.dtype == torch.bfloat16 and dy.shape[1] % 256 == 0 and x.shape[1] % 256 == 0
-                and x.stride(1) == 1 and x.stride(0) % 8 == 0 and x.data_ptr() % 16 == 0 and dy.data_ptr() % 16 == 0
-                and mg.data_ptr() % 16 == 0)
+    one = _job_ok
     if not (_WGRAD_PAIR and _WGRAD_MODE in ("auto", "") and dy0.is_cuda and _ext.use_hip(dy0)):
         return False
     T = dy0.shape[0]
@@ -224,6 +228,119 @@ def _accumulate_weight_grad_pair(p0, dy0, x0, p1, dy1, x1):
             p._sftamd_norm_done = True
         p._sftamd_fresh = False
         _weight_grad_done(p)
+
+
+# SFTAMD_WGRAD_CARRY=0: a layer's o_proj + qkv weight gradients launch on their own (2 rounds of third-tiles)
+# instead of joining the previous layer's down + gate_up launch
+_WGRAD_CARRY = os.environ.get("SFTAMD_WGRAD_CARRY", "1") == "1"
+
+
+def _multi_split(total: int, T: int) -> int:
+    """Ways to split the partial last round of a multi-problem launch over the tokens: the count minimising the rounds
+    of 1/s-tiles plus the fp32 slab traffic (the cost model of _pair_split); 1 = no split."""
+    left = total % _CU_BUDGET
+    if left == 0:
+        return 1
+    best, cost = 1, 1.0
+    for s in range(2, min(8, T // 128) + 1):
+        c = -(-left * s // _CU_BUDGET) / s + 4e-4 * left * s
+        if c < cost - 1e-9:
+            best, cost = s, c
+    return best
+
+
+def _multi_ok(jobs) -> bool:
+    p0, dy0, x0 = jobs[0]
+    if not (_WGRAD_PAIR and _WGRAD_MODE in ("auto", "") and dy0.is_cuda and _ext.use_hip(dy0)):
+        return False
+    T = dy0.shape[0]
+    if not (T % 128 == 0 and T >= 1024 and all(dy.shape[0] == T and x.shape[0] == T for _, dy, x in jobs)):
+        return False
+    if not all(_job_ok(p, dy, x) for p, dy, x in jobs):
+        return False
+    return sum((dy.shape[1] // 256) * (x.shape[1] // 256) for _, dy, x in jobs) >= _CU_BUDGET
+
+
+def _accumulate_weight_grad_jobs(jobs):
+    """Weight gradients [(param, dy2d, x2d)] over the same tokens: ONE wgrad_gemm_multi launch for 3-4 of them (a
+    layer's down + gate_up with the next layer's o_proj + qkv: 1192 tiles = 4 whole rounds + 168 tiles split 3 ways,
+    against 4 rounds + 8 split tiles and a separate 2-round grid of third-tiles), pairs / single launches otherwise."""
+    if len(jobs) == 1:
+        _accumulate_weight_grad(*jobs[0])
+        return
+    if len(jobs) == 2:
+        _accumulate_weight_grad_pair(*jobs[0], *jobs[1])
+        return
+    if not _multi_ok(jobs):
+        _accumulate_weight_grad_jobs(jobs[:2])
+        _accumulate_weight_grad_jobs(jobs[2:])
+        return
+    T = jobs[0][1].shape[0]
+    total = sum((dy.shape[1] // 256) * (x.shape[1] // 256) for _, dy, x in jobs)
+    split_left = _multi_split(total, T)
+
+    def slots(p):
+        ns = getattr(p, "_sftamd_norm_slots", None)
+        return ns if (ns is not None and getattr(p, "_sftamd_remaining", 1) == 1) else None
+
+    ns = [slots(p) for p, _, _ in jobs]
+    empty = jobs[0][1].new_empty(0, dtype=torch.float32)
+    _ext.ops().wgrad_gemm_multi([p.main_grad for p, _, _ in jobs], [dy.contiguous() for _, dy, _ in jobs],
+                                [x for _, _, x in jobs], [0 if getattr(p, "_sftamd_fresh", False) else 1 for p, _, _ in jobs],
+                                [n if n is not None else empty for n in ns], 0, split_left)
+    for (p, _, _), n in zip(jobs, ns):
+        if n is not None:
+            p._sftamd_norm_done = True
+        p._sftamd_fresh = False
+        _weight_grad_done(p)
+
+
+# The hand-off of a layer's attention weight gradients to the previous layer's MLP launch: CausalLM.forward opens a
+# scope; swiglu_mlp leaves its (armed) dict in it and the next layer's attention node takes that dict, deposits its
+# o_proj + qkv weight-gradient jobs there in its backward (which always runs before the previous layer's gate_up
+# backward: that node's output feeds this layer), and the gate_up node launches all four at once.
+_CARRY = None
+
+
+class wgrad_carry_scope:
+    """`with wgrad_carry_scope(enabled):` around the decoder-layer loop of one forward (no activation checkpointing:
+    recomputed layers would arm dicts whose nodes never run)."""
+
+    def __init__(self, enabled: bool = True):
+        self.enabled = bool(enabled and _WGRAD_CARRY and _WGRAD_PAIR and torch.is_grad_enabled())
+
+    def __enter__(self):
+        global _CARRY
+        self.prev = _CARRY
+        _CARRY = {"mlp": None} if self.enabled else None
+        return self
+
+    def __exit__(self, *exc):
+        global _CARRY
+        _CARRY = self.prev
+        return False
+
+
+def _carry_put(box: Optional[dict]) -> None:
+    if _CARRY is not None:
+        _CARRY["mlp"] = box if (box is not None and box.get("armed")) else None
+
+
+def _carry_take() -> Optional[dict]:
+    if _CARRY is None:
+        return None
+    box, _CARRY["mlp"] = _CARRY["mlp"], None
+    return box
+
+
+def _carry_or_launch(carry: Optional[dict], jobs) -> None:
+    """The attention node's weight-gradient jobs: into the previous layer's MLP dict when it will launch them with its
+    own (armed, 4-problem launch eligible), else now."""
+    if (carry is not None and carry.get("armed") and "attn" not in carry and len(jobs) == 2
+            and all(getattr(p, "main_grad", None) is not None for p, _, _ in jobs)):
+        carry["attn"] = jobs
+        return
+    _accumulate_weight_grad_jobs(jobs)
 
 
 def _accumulate_small_grad(param: torch.Tensor, g: torch.Tensor):
@@ -323,11 +440,12 @@ class PairedLinearFn(Function):
     (_accumulate_weight_grad_pair) after this node's input gradient."""
 
     @staticmethod
-    def forward(ctx, x, weight, box, key, arm):
+    def forward(ctx, x, weight, box, key, arm, carry=None):
         ctx.save_for_backward(x)
         ctx.weight = weight
         ctx.box = box
         ctx.key = key
+        ctx.carry = carry
         if weight.requires_grad:  # this node's backward will run: the consumer may leave its weight gradient to it
             box[arm] = True
         x2d = x.reshape(-1, x.shape[-1])
@@ -340,17 +458,24 @@ class PairedLinearFn(Function):
         dy2d = dy.reshape(-1, dy.shape[-1])
         x2d = x.reshape(-1, x.shape[-1])
         pending = ctx.box.pop(ctx.key, None)
+        extra = ctx.box.pop("attn", None)  # the next layer's o_proj + qkv jobs (_carry_or_launch)
         dx = dw = None
         if ctx.needs_input_grad[0]:
             dx = dgrad_mm(dy2d, w).view(*dy.shape[:-1], w.shape[1])
-        if ctx.needs_input_grad[1]:
-            if pending is not None:
-                _accumulate_weight_grad_pair(*pending, w, dy2d, x2d)
-            else:
-                dw = _accumulate_weight_grad(w, dy2d, x2d)
-        elif pending is not None:
-            _accumulate_weight_grad(*pending)
-        return dx, dw, None, None, None
+        jobs = [pending] if pending is not None else []
+        if ctx.needs_input_grad[1] and getattr(w, "main_grad", None) is not None:
+            jobs.append((w, dy2d, x2d))
+        elif ctx.needs_input_grad[1]:
+            dw = _accumulate_weight_grad(w, dy2d, x2d)
+        if ctx.carry is not None and ctx.key == "o_wgrad":  # a NoPE layer's qkv: the previous layer's MLP may take them
+            if jobs:
+                _carry_or_launch(ctx.carry, jobs)
+        else:
+            if jobs:
+                _accumulate_weight_grad_jobs(jobs + (extra or []))
+            elif extra:
+                _accumulate_weight_grad_jobs(extra)
+        return dx, dw, None, None, None, None
 
 
 def mlp_in_linear(x: torch.Tensor, weight: torch.Tensor, box: Optional[dict]) -> torch.Tensor:
@@ -361,9 +486,10 @@ def mlp_in_linear(x: torch.Tensor, weight: torch.Tensor, box: Optional[dict]) ->
 
 
 def qkv_in_linear(x: torch.Tensor, weight: torch.Tensor, box: Optional[dict]) -> torch.Tensor:
-    """qkv(x) of a NoPE layer whose backward also issues o_proj's weight gradient (attn_out_linear with `box`)."""
+    """qkv(x) of a NoPE layer whose backward also issues o_proj's weight gradient (attn_out_linear with `box`) — or
+    hands both to the previous layer's MLP launch (wgrad_carry_scope)."""
     if box is not None and _WGRAD_PAIR and _ext.use_hip(x):
-        return PairedLinearFn.apply(x, weight, box, "o_wgrad", "wgrad_pair")
+        return PairedLinearFn.apply(x, weight, box, "o_wgrad", "wgrad_pair", _carry_take())
     return LinearFn.apply(x, weight)
 
 
@@ -847,6 +973,7 @@ def swiglu_mlp(h: torch.Tensor, w_gate_up: torch.Tensor, w_down: torch.Tensor) -
     (no separate SwiGLU kernel in either direction); default: gate_up GEMM (fwd_gemm) + SwiGLU kernel + the fused
     down dgrad; otherwise the unfused chain."""
     h2d = h.reshape(-1, h.shape[-1])
+    _carry_put(None)
     # (fusing it by default where gate_up has no TunableOp selection — the recipe's ragged batches — measured neutral:
     # 55.28 / 55.12 vs 55.01 / 55.04 HF, 82.84 / 82.68 vs 83.14 / 83.15 pure samples/s, r5_run22)
     fused_gu = _TN_MODE in ("1", "swiglu")
@@ -856,7 +983,9 @@ def swiglu_mlp(h: torch.Tensor, w_gate_up: torch.Tensor, w_down: torch.Tensor) -
         return SwiGLUDownFn.apply(gu, act, w_down)
     if fuse_swiglu_down():
         box = {} if _WGRAD_PAIR else None
-        return swiglu_linear(mlp_in_linear(h, w_gate_up, box), w_down, box)
+        y = swiglu_linear(mlp_in_linear(h, w_gate_up, box), w_down, box)
+        _carry_put(box)  # the next layer's attention may leave its weight gradients to this MLP's launch
+        return y
     return linear(linear_swiglu(h, w_gate_up), w_down)
 
 
@@ -980,8 +1109,10 @@ class QKVRopeAttnFn(Function):
     QKVRopeFn + FlashAttnFn (tests/test_model_gpu.py)."""
 
     @staticmethod
-    def forward(ctx, x, weight, cos, sin, cu_seqlens, max_seqlen, n_q, n_kv, head_dim, scale, causal, box=None):
+    def forward(ctx, x, weight, cos, sin, cu_seqlens, max_seqlen, n_q, n_kv, head_dim, scale, causal, box=None,
+                carry=None):
         ctx.box = box
+        ctx.carry = carry
         if box is not None:
             box["armed"] = True
             if _WGRAD_PAIR and weight.requires_grad:  # this node's backward runs: o_proj may leave its wgrad here
@@ -1008,14 +1139,14 @@ class QKVRopeAttnFn(Function):
         dx = dw = None
         if ctx.needs_input_grad[0]:
             dx = dgrad_mm(dqkv, w).view(ctx.x_shape)
-        if ctx.needs_input_grad[1]:
-            if pending is not None:
-                _accumulate_weight_grad_pair(*pending, w, dqkv, x2d)
-            else:
-                dw = _accumulate_weight_grad(w, dqkv, x2d)
-        elif pending is not None:
-            _accumulate_weight_grad(*pending)
-        return dx, dw, None, None, None, None, None, None, None, None, None, None
+        jobs = [pending] if pending is not None else []
+        if ctx.needs_input_grad[1] and getattr(w, "main_grad", None) is not None:
+            jobs.append((w, dqkv, x2d))
+        elif ctx.needs_input_grad[1]:
+            dw = _accumulate_weight_grad(w, dqkv, x2d)
+        if jobs:
+            _carry_or_launch(ctx.carry, jobs)
+        return dx, dw, None, None, None, None, None, None, None, None, None, None, None
 
 
 _ROPE_ATTN_FUSED = True  # (a test seam: tests/test_model_gpu.py compares against the two separate nodes)
@@ -1031,7 +1162,8 @@ def qkv_rope_attention(x, weight, cos, sin, cu_seqlens, max_seqlen, n_q, n_kv, h
             and cos.dtype == torch.float32 and cos.is_contiguous() and sin.is_contiguous()
             and cos.shape == (x2d.shape[0], 64)):
         return QKVRopeAttnFn.apply(x, weight, cos, sin, cu_seqlens, int(max_seqlen), n_q, n_kv, head_dim,
-                                   float(scale), bool(causal), delta_box)
+                                   float(scale), bool(causal), delta_box,
+                                   _carry_take() if delta_box is not None else None)
     qkv = linear_rope(x, weight, cos, sin, n_q, n_kv, head_dim)
     return flash_attention(qkv, cu_seqlens, max_seqlen, n_q, n_kv, head_dim, scale, causal, delta_box)
 
@@ -1564,6 +1696,7 @@ def lora_swiglu_mlp(h, w_gate_up, w_down, l_gate_up, l_down) -> torch.Tensor:
     """down(swiglu(gate_up(h))) with LoRA adapters on both projections: on the HIP wide path one node per projection,
     the SwiGLU formed inside the down projection's widening pass and its backward inside the adapter-dx pass (the
     node returns dgu); otherwise the plain composition of lora_linear and swiglu."""
+    _carry_put(None)
     gu_args, dn_args = _lora_wide_args(l_gate_up, w_gate_up), _lora_wide_args(l_down, w_down)
     h2d = h.reshape(-1, h.shape[-1])
     if (gu_args is not None and dn_args is not None and _ext.use_hip(h2d) and h2d.shape[0] % 256 == 0

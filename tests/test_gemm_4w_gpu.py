@@ -324,3 +324,50 @@ def test_wgrad_pair_split_all(T):
     v0, v1 = torch.empty_like(w0), torch.empty_like(w1)
     _ext.ops().wgrad_gemm_pair(v0, dy0, x0, False, None, v1, dy1, x1, False, None, 3)
     assert torch.equal(v0, w0) and torch.equal(v1, w1)
+
+
+@pytest.mark.parametrize("accumulate", [False, True])
+@pytest.mark.parametrize("split_left", [0, 3])
+def test_wgrad_multi_four_problems(accumulate, split_left):
+    """wgrad_gemm_multi: a layer's down + gate_up with the next layer's o_proj + qkv as ONE grid (SmolLM3 widths,
+    1192 tiles = 4 whole rounds + 168 tiles split over the tokens, spanning three problems): every gradient == the
+    fp32 reference, the whole tiles == separate cfg-14 launches bitwise, deterministic, norm slots sum to the stored
+    squared norm per problem."""
+    torch.manual_seed(19)
+    T = 8192
+    shapes = [(2048, 11008), (22016, 2048), (2048, 2048), (3072, 2048)]  # (N, K): down, gate_up, o, qkv
+    dys = [(0.05 * torch.randn(T, n, device=DEV)).to(torch.bfloat16) for n, _ in shapes]
+    xs = [(0.05 * torch.randn(T, k, device=DEV)).to(torch.bfloat16) for _, k in shapes]
+    bases = [torch.randn(n, k, device=DEV, dtype=torch.bfloat16) for n, k in shapes]
+    outs = [b.clone() for b in bases]
+    norms = [torch.zeros((n // 256) * (k // 128) * 32, device=DEV) for n, k in shapes]
+    acc = [1 if accumulate else 0] * 4
+    _ext.ops().wgrad_gemm_multi(outs, dys, xs, acc, norms, 0, split_left)
+    for o, dy, x, b, nr in zip(outs, dys, xs, bases, norms):
+        want = dy.float().t() @ x.float() + (b.float() if accumulate else 0)
+        assert rel_err(o, want) < 5e-3
+        ref = o.float().pow(2).sum().item()
+        assert abs(nr.sum().item() - ref) < 1e-3 * ref
+    # down (problem 0) lies wholly in the 4 whole rounds: bitwise the single cfg-14 launch
+    r0 = bases[0].clone()
+    _ext.ops().wgrad_gemm(r0, dys[0], xs[0], accumulate, 14)
+    assert torch.equal(outs[0], r0)
+    again = [b.clone() for b in bases]
+    empty = torch.empty(0, device=DEV)
+    _ext.ops().wgrad_gemm_multi(again, dys, xs, acc, [empty] * 4, 0, split_left)
+    assert all(torch.equal(a, o) for a, o in zip(again, outs))
+
+
+def test_wgrad_multi_three_problems_small():
+    """Three problems below one round with every tile split (split_all) and the hybrid rule on a ragged total."""
+    torch.manual_seed(23)
+    T = 1024
+    shapes = [(512, 256), (256, 512), (768, 256)]
+    dys = [torch.randn(T, n, device=DEV, dtype=torch.bfloat16) for n, _ in shapes]
+    xs = [torch.randn(T, k, device=DEV, dtype=torch.bfloat16) for _, k in shapes]
+    empty = torch.empty(0, device=DEV)
+    for split_all in (2, 4):
+        outs = [torch.empty(n, k, device=DEV, dtype=torch.bfloat16) for n, k in shapes]
+        _ext.ops().wgrad_gemm_multi(outs, dys, xs, [0, 0, 0], [empty] * 3, split_all, 0)
+        for o, dy, x in zip(outs, dys, xs):
+            assert rel_err(o, dy.float().t() @ x.float()) < 5e-3

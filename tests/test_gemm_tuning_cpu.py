@@ -80,3 +80,40 @@ def test_dgrad_routing():
         assert cfg(8192, 22016, 2048) == 14
     finally:
         F._DGRAD_RING8 = F_ring8
+
+
+def test_attention_wgrad_carry_into_the_previous_mlp_launch():
+    """The cross-layer hand-off (ops.fused wgrad_carry_scope): the leftover split of a four-problem launch (1192
+    SmolLM3 tiles -> 3 ways; Llama's 3328 tiles are whole rounds -> 1), a scope hands one MLP dict to the next
+    attention only, an armed dict takes the o_proj + qkv jobs and the MLP side then accumulates all four gradients
+    (CPU: the per-job fallback), and no carry outside a scope."""
+    import torch
+    import llm_fine_tune_distributed_amd.ops.fused as F
+    assert F._multi_split(344 + 688 + 64 + 96, 8192) == 3
+    assert F._multi_split(1792 + 896 + 384 + 256, 8192) == 1
+    assert F._carry_take() is None
+    with F.wgrad_carry_scope(True):
+        box = {"armed": True}
+        F._carry_put(box)
+        assert F._carry_take() is box and F._carry_take() is None
+        F._carry_put({})  # an MLP whose gate_up backward will not run (unarmed) is never offered
+        assert F._carry_take() is None
+    assert F._CARRY is None
+    torch.manual_seed(0)
+    T = 64
+
+    def job(n, k):
+        p = torch.nn.Parameter(torch.zeros(n, k))
+        p.main_grad = torch.zeros(n, k)
+        p._sftamd_fresh = True
+        return p, torch.randn(T, n), torch.randn(T, k)
+
+    o, qkv, down, gu = job(8, 16), job(24, 16), job(16, 32), job(64, 16)
+    carry = {"armed": True}
+    F._carry_or_launch(carry, [o, qkv])
+    assert carry["attn"] == [o, qkv] and o[0].main_grad.abs().sum() == 0  # deferred, nothing computed yet
+    F._accumulate_weight_grad_jobs([down, gu] + carry.pop("attn"))
+    for p, dy, x in (o, qkv, down, gu):
+        assert torch.allclose(p.main_grad, dy.t() @ x, atol=1e-4)
+    F._carry_or_launch(None, [o, qkv])  # no carry: launched at once (accumulating now)
+    assert torch.allclose(o[0].main_grad, 2 * (o[1].t() @ o[2]), atol=1e-4)
