@@ -586,16 +586,24 @@ void g4_wgrad_multi(const std::vector<WgradJob>& jobs, int split_all, int split_
   g4::launchn<g4::TR, g4::TR>(g4::Probs{q[0], q[1], q[2], q[3], np > 1 ? start[1] : INT_MAX, np > 2 ? start[2] : INT_MAX,
                         np > 3 ? start[3] : INT_MAX},
                   total, T, ndp, splits);
+  // the fixups of every problem with split tiles as one grid (32 blocks of 256 x 8 elements per tile)
+  FixArgs fa[4];
+  int nf = 0, bstart[4] = {0, 0, 0, 0}, nblocks = 0;
   for (int i = 0; i < np; ++i) {
     if (sn[i] <= 0) continue;
     const WgradJob& j = jobs[i];
     const int N = j.dy.size(1), K = j.x.size(1);
-    const long n8 = (long)sn[i] * 65536 / 8;
-    splitk_fixup_kernel<256, 256><<<(unsigned)((n8 + 255) / 256), 256, 0, cur_stream()>>>(
-        part[i].data_ptr<float>(), (u16*)j.out.data_ptr(), w[i], sn[i], splits, K / 256, K, j.acc ? 1 : 0, j.nrm,
-        N / 256, std::min(g4::group_m(), N / 256));
-    SFT_LAUNCH_CHECK();
+    fa[nf] = FixArgs{part[i].data_ptr<float>(), (u16*)j.out.data_ptr(), j.nrm, w[i], sn[i], K / 256, K,
+                     j.acc ? 1 : 0, N / 256, std::min(g4::group_m(), N / 256)};
+    bstart[nf++] = nblocks;
+    nblocks += sn[i] * 32;
   }
+  if (nf == 0) return;
+  for (int i = nf; i < 4; ++i) fa[i] = fa[nf - 1];
+  splitk_fixup_multi_kernel<256, 256><<<(unsigned)nblocks, 256, 0, cur_stream()>>>(
+      fa[0], fa[1], fa[2], fa[3], nf > 1 ? bstart[1] : INT_MAX, nf > 2 ? bstart[2] : INT_MAX,
+      nf > 3 ? bstart[3] : INT_MAX, splits);
+  SFT_LAUNCH_CHECK();
 }
 
 // Two weight gradients as one grid (g4_wgrad_multi); without split_all the partial round must fall in problem 1.

@@ -10,16 +10,16 @@ namespace sftamd {
 // 8 elements per thread, slabs summed in order s = 0..S-1. Tile numbering: row-major over [nbm][nbk] tiles, or
 // (group > 0) blocked by `group` row-tiles as the launching kernel walks them.
 template <int BM, int BN>
-__global__ void __launch_bounds__(256) splitk_fixup_kernel(const float* __restrict__ P, u16* __restrict__ C, int tile0,
-                                                           int ntiles, int splits, int nbk, int K, int accumulate,
-                                                           float* __restrict__ nrm, int nbm = 0, int group = 0) {
+__device__ __forceinline__ void splitk_fixup_body(const float* __restrict__ P, u16* __restrict__ C, int tile0,
+                                                  int ntiles, int splits, int nbk, int K, int accumulate,
+                                                  float* __restrict__ nrm, int nbm, int group, const int bid) {
   constexpr int E8 = BM * BN / 8;
-  if (nrm != nullptr && blockIdx.x == 0) {  // the whole tiles' partials, parked past the slabs by ring_kernel
+  if (nrm != nullptr && bid == 0) {  // the whole tiles' partials, parked past the slabs by ring_kernel
     const float* src = P + (long)ntiles * splits * BM * BN;
     for (int i = threadIdx.x; i < tile0 * 8; i += 256) nrm[i] = src[i];
   }
   static_assert((BM * BN / 8) % 256 == 0, "fixup blocks cover whole tiles");
-  const long idx = (long)blockIdx.x * 256 + threadIdx.x;
+  const long idx = (long)bid * 256 + threadIdx.x;
   if (idx >= (long)ntiles * E8) return;  // never taken: the grid covers whole tiles
   const int t = (int)(idx / E8), e = (int)(idx - (long)t * E8) * 8;
   const int row = e / BN, col = e - row * BN;
@@ -61,8 +61,36 @@ __global__ void __launch_bounds__(256) splitk_fixup_kernel(const float* __restri
     __shared__ float red[4];
     if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = ss;
     __syncthreads();
-    if (threadIdx.x == 0) nrm[(long)tile0 * 8 + blockIdx.x] = red[0] + red[1] + red[2] + red[3];
+    if (threadIdx.x == 0) nrm[(long)tile0 * 8 + bid] = red[0] + red[1] + red[2] + red[3];
   }
+}
+
+template <int BM, int BN>
+__global__ void __launch_bounds__(256) splitk_fixup_kernel(const float* __restrict__ P, u16* __restrict__ C, int tile0,
+                                                           int ntiles, int splits, int nbk, int K, int accumulate,
+                                                           float* __restrict__ nrm, int nbm = 0, int group = 0) {
+  splitk_fixup_body<BM, BN>(P, C, tile0, ntiles, splits, nbk, K, accumulate, nrm, nbm, group, blockIdx.x);
+}
+
+// The fixups of up to four problems of one multi-problem launch as ONE grid: problem i owns blocks [b_i, b_{i+1})
+// (b_0 = 0, unused = INT_MAX); per problem the arguments of splitk_fixup_kernel.
+struct FixArgs {
+  const float* P;
+  u16* C;
+  float* nrm;
+  int tile0, ntiles, nbk, K, accumulate, nbm, group;
+};
+
+template <int BM, int BN>
+__global__ void __launch_bounds__(256) splitk_fixup_multi_kernel(FixArgs f0, FixArgs f1, FixArgs f2, FixArgs f3,
+                                                                 int b1, int b2, int b3, int splits) {
+  const int b = blockIdx.x;
+  const int pi = (b >= b1) + (b >= b2) + (b >= b3);
+#define FXSEL(x) (pi == 0 ? f0.x : pi == 1 ? f1.x : pi == 2 ? f2.x : f3.x)
+  const int bid = b - (pi == 0 ? 0 : pi == 1 ? b1 : pi == 2 ? b2 : b3);
+  splitk_fixup_body<BM, BN>(FXSEL(P), FXSEL(C), FXSEL(tile0), FXSEL(ntiles), splits, FXSEL(nbk), FXSEL(K),
+                            FXSEL(accumulate), FXSEL(nrm), FXSEL(nbm), FXSEL(group), bid);
+#undef FXSEL
 }
 
 }  // namespace sftamd
