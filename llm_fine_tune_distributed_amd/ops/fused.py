@@ -237,11 +237,17 @@ _WGRAD_CARRY = os.environ.get("SFTAMD_WGRAD_CARRY", "1") == "1"
 
 def _multi_split(total: int, T: int) -> int:
     """Ways to split the partial last round of a multi-problem launch over the tokens: the count minimising the rounds
-    of 1/s-tiles plus the fp32 slab traffic (the cost model of _pair_split); 1 = no split."""
+    of 1/s-tiles plus the fp32 slab traffic (the cost model of _pair_split); 1 = no split. An unsplit partial round
+    costs at least 0.75 of a full one (tools/debug/round_scaling.py) — and no slabs: the SmolLM3 layer grid (1192
+    tiles, 168 left over) measured 0.9185 ms unsplit vs 0.9325 split 3 ways, 0.9466 / 0.9558 for 2 / 4
+    (tools/bench_pair.py --pair layer, profiles/r6_gemm_routing.md)."""
     left = total % _CU_BUDGET
     if left == 0:
         return 1
-    best, cost = 1, 1.0
+    forced = os.environ.get("SFTAMD_MULTI_SPLIT", "")
+    if forced:
+        return max(1, int(forced))
+    best, cost = 1, max(0.75, left / _CU_BUDGET)
     for s in range(2, min(8, T // 128) + 1):
         c = -(-left * s // _CU_BUDGET) / s + 4e-4 * left * s
         if c < cost - 1e-9:
@@ -263,8 +269,8 @@ def _multi_ok(jobs) -> bool:
 
 def _accumulate_weight_grad_jobs(jobs):
     """Weight gradients [(param, dy2d, x2d)] over the same tokens: ONE wgrad_gemm_multi launch for 3-4 of them (a
-    layer's down + gate_up with the next layer's o_proj + qkv: 1192 tiles = 4 whole rounds + 168 tiles split 3 ways,
-    against 4 rounds + 8 split tiles and a separate 2-round grid of third-tiles), pairs / single launches otherwise."""
+    layer's down + gate_up with the next layer's o_proj + qkv: 1192 tiles = 4 whole rounds + a partial round of 168
+    tiles, against 4 rounds + 8 split tiles and a separate 2-round grid of third-tiles), pairs / single launches otherwise."""
     if len(jobs) == 1:
         _accumulate_weight_grad(*jobs[0])
         return

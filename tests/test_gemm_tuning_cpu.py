@@ -84,12 +84,13 @@ def test_dgrad_routing():
 
 def test_attention_wgrad_carry_into_the_previous_mlp_launch():
     """The cross-layer hand-off (ops.fused wgrad_carry_scope): the leftover split of a four-problem launch (1192
-    SmolLM3 tiles -> 3 ways; Llama's 3328 tiles are whole rounds -> 1), a scope hands one MLP dict to the next
+    SmolLM3 tiles -> unsplit; Llama's 3328 tiles are whole rounds -> 1), a scope hands one MLP dict to the next
     attention only, an armed dict takes the o_proj + qkv jobs and the MLP side then accumulates all four gradients
     (CPU: the per-job fallback), and no carry outside a scope."""
     import torch
     import llm_fine_tune_distributed_amd.ops.fused as F
-    assert F._multi_split(344 + 688 + 64 + 96, 8192) == 3
+    assert F._multi_split(344 + 688 + 64 + 96, 8192) == 1  # 168 left over: an unsplit partial round is cheapest
+    assert F._multi_split(4 * 256 + 40, 8192) == 6  # a small leftover is split to fill the round
     assert F._multi_split(1792 + 896 + 384 + 256, 8192) == 1
     assert F._carry_take() is None
     with F.wgrad_carry_scope(True):

@@ -1,7 +1,9 @@
 """Paired weight-gradient launches (sftamd.wgrad_gemm_pair) at several split counts, interleaved rounds, medians (ms):
-the check of ops.fused._pair_split's cost model.
+the check of ops.fused._pair_split's cost model; --pair layer: the four-problem grid (wgrad_gemm_multi: down + gate_up
++ the next layer's o_proj + qkv) with its leftover split 1..8 ways (ops.fused._multi_split) and, as "pairs", the two
+separate pair launches it replaces.
 
-    python tools/bench_pair.py [--pair attn|mlp|l8b_attn] [--splits 0,2,3,4,6] [--rounds 7]
+    python tools/bench_pair.py [--pair attn|mlp|l8b_attn|layer] [--splits 0,2,3,4,6] [--rounds 7]
 
 attn = o_proj (2048 x 2048) + qkv (3072 x 2048) at SmolLM3 widths, mlp = down (2048 x 11008) + gate_up (22016 x 2048),
 l8b_attn = Llama-3-8B o_proj + qkv; T = 8192 tokens. split 0 = whole rounds + the split leftover (hybrid).
@@ -22,6 +24,7 @@ PAIRS = {  # ((N0, K0), (N1, K1)): out0 [N0, K0] = dy0[T, N0]^T x0[T, K0]
     "mlp": ((2048, 11008), (22016, 2048)),
     "l8b_attn": ((4096, 4096), (6144, 4096)),
 }
+LAYER = [(2048, 11008), (22016, 2048), (2048, 2048), (3072, 2048)]  # down, gate_up, o_proj, qkv
 
 
 def timeit(fn, iters):
@@ -38,7 +41,7 @@ def timeit(fn, iters):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--pair", default="attn", choices=sorted(PAIRS))
+    ap.add_argument("--pair", default="attn", choices=sorted(PAIRS) + ["layer"])
     ap.add_argument("--splits", default="0,2,3,4,6")
     ap.add_argument("--rounds", type=int, default=7)
     ap.add_argument("--iters", type=int, default=10)
@@ -47,6 +50,8 @@ def main():
     assert _ext.load(), _ext.load_error()
     ops = _ext.ops()
     T = a.tokens
+    if a.pair == "layer":
+        return layer(a, ops, T)
     (N0, K0), (N1, K1) = PAIRS[a.pair]
 
     def rnd(*s):
@@ -80,6 +85,31 @@ def main():
     for s in splits:
         rec[f"split{s}_ms"] = round(statistics.median(times[s]), 4)
         rec[f"split{s}_relerr"] = round(errs[s], 5)
+    print(json.dumps(rec), flush=True)
+
+
+def layer(a, ops, T):
+    dys = [(0.05 * torch.randn(T, n, device="cuda")).to(torch.bfloat16) for n, _ in LAYER]
+    xs = [(0.05 * torch.randn(T, k, device="cuda")).to(torch.bfloat16) for _, k in LAYER]
+    outs = [torch.empty(n, k, device="cuda", dtype=torch.bfloat16) for n, k in LAYER]
+    empty = torch.empty(0, device="cuda")
+    variants = ["pairs"] + [int(s) for s in a.splits.split(",")]
+
+    def run(v):
+        if v == "pairs":
+            ops.wgrad_gemm_pair(outs[0], dys[0], xs[0], False, None, outs[1], dys[1], xs[1], False, None, 0)
+            ops.wgrad_gemm_pair(outs[2], dys[2], xs[2], False, None, outs[3], dys[3], xs[3], False, None, 3)
+        else:
+            ops.wgrad_gemm_multi(outs, dys, xs, [0, 0, 0, 0], [empty] * 4, 0, v)
+
+    times = {v: [] for v in variants}
+    for r in range(a.rounds):
+        order = variants[r % len(variants):] + variants[:r % len(variants)]
+        for v in order:
+            times[v].append(timeit(lambda: run(v), a.iters))
+    rec = {"pair": "layer", "T": T, "tiles": sum((n // 256) * (k // 256) for n, k in LAYER)}
+    for v in variants:
+        rec[f"split{v}_ms"] = round(statistics.median(times[v]), 4)
     print(json.dumps(rec), flush=True)
 
 
